@@ -1,0 +1,120 @@
+"""ctypes binding of the C ABI in ``include/hmsc_amd.h`` (``hmsc_amd/libhmsc_amd.so``).
+
+This is the binding a maintainer would write on the R side as a ``.Call`` shim
+(INTEGRATION.md); here Python plays the role of the R wrapper.  There is no CPU
+fallback: if the HIP library is missing, importing the sampler raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+MAX_LEVELS = 8
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("HMSC_AMD_LIB", os.path.join(HERE, "libhmsc_amd.so"))
+
+UP = dict(Gamma2=1 << 0, GammaEta=1 << 1, BetaLambda=1 << 2, wRRR=1 << 3, BetaSel=1 << 4, GammaV=1 << 5,
+          Rho=1 << 6, LambdaPriors=1 << 7, wRRRPriors=1 << 8, Eta=1 << 9, Alpha=1 << 10, InvSigma=1 << 11,
+          Z=1 << 12)
+UP_ALL = 0x1FFF
+
+dp = C.POINTER(C.c_double)
+ip = C.POINTER(C.c_int32)
+
+
+class hmsc_model(C.Structure):
+    _fields_ = [("ny", C.c_int32), ("ns", C.c_int32), ("nc", C.c_int32), ("nt", C.c_int32), ("nr", C.c_int32),
+                ("Y", dp), ("Yraw", dp), ("X", dp), ("Tr", dp), ("Pi", ip), ("np", ip), ("distr", ip),
+                ("V0", dp), ("f0", C.c_double), ("mGamma", dp), ("UGamma", dp), ("aSigma", dp), ("bSigma", dp),
+                ("nu", dp), ("a1", dp), ("b1", dp), ("a2", dp), ("b2", dp), ("nfMin", ip), ("nfMax", ip),
+                ("sDim", ip), ("xDim", ip), ("C", dp)]
+
+
+class hmsc_params(C.Structure):
+    _fields_ = [("Gamma", dp), ("iV", dp), ("Beta", dp), ("iSigma", dp), ("Z", dp), ("rho", C.c_int32),
+                ("nf", C.c_int32 * MAX_LEVELS), ("Eta", dp * MAX_LEVELS), ("Lambda", dp * MAX_LEVELS),
+                ("Psi", dp * MAX_LEVELS), ("Delta", dp * MAX_LEVELS), ("Alpha", ip * MAX_LEVELS)]
+
+
+class hmsc_record(C.Structure):
+    _fields_ = [("Beta", dp), ("Gamma", dp), ("iV", dp), ("iSigma", dp), ("rho", ip),
+                ("Eta", dp * MAX_LEVELS), ("Lambda", dp * MAX_LEVELS), ("Psi", dp * MAX_LEVELS),
+                ("Delta", dp * MAX_LEVELS), ("Alpha", ip * MAX_LEVELS), ("rec_nf", ip)]
+
+
+class HmscNativeError(RuntimeError):
+    pass
+
+
+_lib = None
+
+# every symbol declared in include/hmsc_amd.h
+EXPORTS = ["hmsc_last_error", "hmsc_device_count", "hmsc_create", "hmsc_create_sharded", "hmsc_comm_unique_id",
+           "hmsc_destroy", "hmsc_init_state", "hmsc_set_state", "hmsc_get_state", "hmsc_get_nf", "hmsc_sweep",
+           "hmsc_update", "hmsc_set_noise_mode", "hmsc_run", "hmsc_run_verbose", "hmsc_sync", "hmsc_debug_get"]
+
+
+def lib():
+    """Load the HIP library (raises if it has not been built: no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise HmscNativeError(
+            f"{LIB_PATH} not found: build the gfx950 HIP library first (python -m hmsc_amd.build)")
+    L = C.CDLL(LIB_PATH)
+    L.hmsc_last_error.restype = C.c_char_p
+    L.hmsc_device_count.argtypes = [ip]
+    L.hmsc_create.argtypes = [C.POINTER(hmsc_model), C.c_uint64, C.c_int32, C.c_uint32, C.POINTER(C.c_void_p)]
+    L.hmsc_create_sharded.argtypes = [C.POINTER(hmsc_model), C.c_uint64, C.c_int32, C.c_uint32, C.c_int32,
+                                      C.c_int32, C.c_void_p, C.POINTER(C.c_void_p)]
+    L.hmsc_comm_unique_id.argtypes = [C.c_void_p]
+    L.hmsc_destroy.argtypes = [C.c_void_p]
+    L.hmsc_destroy.restype = None
+    L.hmsc_init_state.argtypes = [C.c_void_p, ip]
+    L.hmsc_set_state.argtypes = [C.c_void_p, C.POINTER(hmsc_params)]
+    L.hmsc_get_state.argtypes = [C.c_void_p, C.POINTER(hmsc_params)]
+    L.hmsc_get_nf.argtypes = [C.c_void_p, ip]
+    L.hmsc_sweep.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
+    L.hmsc_update.argtypes = [C.c_void_p, C.c_uint32, C.c_int32]
+    L.hmsc_set_noise_mode.argtypes = [C.c_void_p, C.c_int32]
+    L.hmsc_run.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, ip, C.c_int32, C.POINTER(hmsc_record)]
+    L.hmsc_run_verbose.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, ip, C.c_int32, C.c_int32,
+                                   C.c_int32, C.POINTER(hmsc_record)]
+    L.hmsc_sync.argtypes = [C.c_void_p]
+    L.hmsc_debug_get.argtypes = [C.c_void_p, C.c_char_p, dp, C.c_int64]
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        raise HmscNativeError(f"hmsc_amd error {rc}: {lib().hmsc_last_error().decode()}")
+
+
+def f64(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+
+
+def i32(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.int32))
+
+
+def fptr(a):
+    return None if a is None else a.ctypes.data_as(dp)
+
+
+def iptr(a):
+    return None if a is None else a.ctypes.data_as(ip)
+
+
+def fortran(a, dtype=np.float64):
+    """Column-major contiguous copy (R storage order)."""
+    return np.asfortranarray(np.asarray(a, dtype=dtype))
+
+
+def colmajor_ptr(a, keep, dtype=np.float64):
+    arr = np.asarray(a, dtype=dtype)
+    flat = np.ascontiguousarray(arr.reshape(-1, order="F")) if arr.ndim > 1 else np.ascontiguousarray(arr)
+    keep.append(flat)
+    return fptr(flat) if dtype == np.float64 else iptr(flat)

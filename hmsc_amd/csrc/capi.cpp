@@ -1,0 +1,875 @@
+// C ABI of hmsc_amd (include/hmsc_amd.h): chain state lifecycle, the sweep driver in
+// the reference block order (R/sampleMcmc.R:219-306), recording, updateNf, RCCL.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/hmsc_amd.h"
+#include "common.h"
+#include "rng.h"
+#include "state.h"
+
+struct hmsc_state {
+  hmsc::State s;
+};
+
+namespace hmsc {
+
+static thread_local std::string g_last_error;
+
+static int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+template <class F>
+static int guarded(F&& f) {
+  try {
+    f();
+    return 0;
+  } catch (const HmscError& e) {
+    return fail(e.code, e.what());
+  } catch (const std::exception& e) {
+    return fail(-3, e.what());
+  } catch (...) {
+    return fail(-4, "unknown error");
+  }
+}
+
+struct DeviceGuard {
+  int prev = 0;
+  explicit DeviceGuard(int d) {
+    HIP_OK(hipGetDevice(&prev));
+    if (prev != d) HIP_OK(hipSetDevice(d));
+  }
+  ~DeviceGuard() { (void)hipSetDevice(prev); }
+};
+
+// ---------------------------- host dense helpers ----------------------------
+using Mat = std::vector<double>;  // column-major
+
+static void host_chol(Mat& A, int n) {  // lower in place, upper zeroed
+  for (int c = 0; c < n; ++c) {
+    double d = A[c + n * c];
+    for (int k = 0; k < c; ++k) d -= A[c + n * k] * A[c + n * k];
+    HMSC_REQUIRE(d > 0.0, "matrix is not positive definite");
+    d = std::sqrt(d);
+    A[c + n * c] = d;
+    for (int i = c + 1; i < n; ++i) {
+      double v = A[i + n * c];
+      for (int k = 0; k < c; ++k) v -= A[i + n * k] * A[c + n * k];
+      A[i + n * c] = v / d;
+    }
+  }
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < j; ++i) A[i + n * j] = 0.0;
+}
+
+static Mat host_inv_spd(const Mat& A, int n) {
+  Mat L = A;
+  host_chol(L, n);
+  Mat Li(n * n, 0.0);
+  for (int c = 0; c < n; ++c)
+    for (int i = c; i < n; ++i) {
+      double s = (i == c) ? 1.0 : 0.0;
+      for (int k = c; k < i; ++k) s -= L[i + n * k] * Li[k + n * c];
+      Li[i + n * c] = s / L[i + n * i];
+    }
+  Mat R(n * n, 0.0);
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      double s = 0.0;
+      for (int k = std::max(i, j); k < n; ++k) s += Li[k + n * i] * Li[k + n * j];
+      R[i + n * j] = s;
+    }
+  return R;
+}
+
+static Mat host_mm(const Mat& A, const Mat& B, int m, int k, int n) {
+  Mat C(m * n, 0.0);
+  for (int j = 0; j < n; ++j)
+    for (int q = 0; q < k; ++q) {
+      const double b = B[q + k * j];
+      for (int i = 0; i < m; ++i) C[i + m * j] += A[i + m * q] * b;
+    }
+  return C;
+}
+
+// ---------------------------- device memory ----------------------------
+template <class T>
+static T* dalloc(size_t n) {
+  T* p = nullptr;
+  if (n == 0) n = 1;
+  HIP_OK(hipMalloc(&p, n * sizeof(T)));
+  HIP_OK(hipMemset(p, 0, n * sizeof(T)));
+  return p;
+}
+
+template <class T>
+static T* dupload(const T* h, size_t n) {
+  T* p = dalloc<T>(n);
+  if (h && n) HIP_OK(hipMemcpy(p, h, n * sizeof(T), hipMemcpyHostToDevice));
+  return p;
+}
+
+template <class T>
+static void h2d(T* d, const T* h, size_t n, hipStream_t st) {
+  if (n) HIP_OK(hipMemcpyAsync(d, h, n * sizeof(T), hipMemcpyHostToDevice, st));
+}
+
+template <class T>
+static void d2h(T* h, const T* d, size_t n, hipStream_t st) {
+  if (n) HIP_OK(hipMemcpyAsync(h, d, n * sizeof(T), hipMemcpyDeviceToHost, st));
+}
+
+void allreduce_sum(State& s, double* buf, size_t n) {
+  if (s.nranks <= 1) return;
+  const ncclResult_t r = ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, (ncclComm_t)s.comm, s.stream);
+  HMSC_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+}
+
+// ---------------------------- create ----------------------------
+static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device, uint32_t mask, int rank,
+                        int nranks, const void* comm_id) {
+  HMSC_REQUIRE(m != nullptr, "model is NULL");
+  HMSC_REQUIRE(m->ny > 0 && m->ns > 0 && m->nc >= 0 && m->nt > 0, "bad dimensions");
+  HMSC_REQUIRE(m->nr >= 0 && m->nr <= HMSC_MAX_LEVELS, "nr out of range");
+  HMSC_REQUIRE(m->C == nullptr, "phylogeny (C != NULL) is a 'next' row: not in this build");
+  s.ny = m->ny;
+  s.ns = m->ns;
+  s.nc = m->nc;
+  s.nt = m->nt;
+  s.nr = m->nr;
+  s.device = device;
+  s.mask = mask;
+  s.rank = rank;
+  s.nranks = nranks;
+  s.key = Key{(uint32_t)(seed & 0xFFFFFFFFu), (uint32_t)(seed >> 32)};
+  s.f0 = m->f0;
+  const int per = (m->ns + nranks - 1) / nranks;
+  s.sp0 = std::min(m->ns, rank * per);
+  s.nsl = std::min(m->ns, s.sp0 + per) - s.sp0;
+  HMSC_REQUIRE(s.nsl > 0, "species shard is empty (more ranks than species)");
+  DeviceGuard dg(device);
+  HIP_OK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  HIP_OK(hipStreamCreateWithFlags(&s.copy_stream, hipStreamNonBlocking));
+  if (nranks > 1) {
+    HMSC_REQUIRE(comm_id != nullptr, "sharded chain needs an RCCL unique id");
+    ncclUniqueId id;
+    std::memcpy(&id, comm_id, sizeof(id));
+    ncclComm_t comm;
+    const ncclResult_t r = ncclCommInitRank(&comm, nranks, id, rank);
+    HMSC_REQUIRE(r == ncclSuccess, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    s.comm = comm;
+  }
+  const int ny = s.ny, nc = s.nc, nt = s.nt, nsl = s.nsl, sp0 = s.sp0, N = nc * nt;
+  // levels
+  int sum_nfmax = 0;
+  for (int r = 0; r < s.nr; ++r) {
+    Level& L = s.lev[r];
+    HMSC_REQUIRE(m->sDim == nullptr || m->sDim[r] == 0, "spatial random levels are a 'next' row: not in this build");
+    HMSC_REQUIRE(m->xDim == nullptr || m->xDim[r] == 0,
+                 "covariate-dependent random levels are a 'next' row: not in this build");
+    L.np = m->np[r];
+    L.nfmin = m->nfMin[r];
+    L.nfmax = m->nfMax[r];
+    L.nf = L.nfmin;
+    L.nu = m->nu[r];
+    L.a1 = m->a1[r];
+    L.b1 = m->b1[r];
+    L.a2 = m->a2[r];
+    L.b2 = m->b2[r];
+    sum_nfmax += L.nfmax;
+  }
+  s.Kmax = std::min(nc + sum_nfmax, 64);
+  s.NFmax = s.Kmax - nc;
+  s.refresh_dims();
+  HMSC_REQUIRE(s.K <= s.Kmax, "nc + sum(nfMin) exceeds 64: not supported in this build");
+  for (int r = 0; r < s.nr; ++r) {
+    Level& L = s.lev[r];
+    const int nfcap = std::min(L.nfmax, s.NFmax);
+    L.Eta = dalloc<double>((size_t)L.np * nfcap);
+    std::vector<int> pi(ny), cnt(L.np + 1, 0), rows(ny);
+    for (int i = 0; i < ny; ++i) {
+      const int u = m->Pi[i + (size_t)ny * r] - 1;
+      HMSC_REQUIRE(u >= 0 && u < L.np, "Pi out of range");
+      pi[i] = u;
+      cnt[u + 1]++;
+    }
+    for (int q = 0; q < L.np; ++q) cnt[q + 1] += cnt[q];
+    std::vector<int> fill(cnt.begin(), cnt.end() - 1);
+    for (int i = 0; i < ny; ++i) rows[fill[pi[i]]++] = i;
+    for (int q = 0; q < L.np; ++q) HMSC_REQUIRE(cnt[q + 1] > cnt[q], "a random-level unit has no rows");
+    L.Pi = dupload(pi.data(), ny);
+    L.unit_ptr = dupload(cnt.data(), L.np + 1);
+    L.unit_rows = dupload(rows.data(), ny);
+    std::vector<int> alpha(std::max(1, L.nfmax > 0 ? std::min(L.nfmax, s.NFmax) : 1), 1);
+    L.Alpha = dupload(alpha.data(), alpha.size());
+  }
+  // local species slices
+  std::vector<int8_t> ycode((size_t)ny * nsl);
+  std::vector<double> yval((size_t)ny * nsl), yraw((size_t)ny * nsl), trl((size_t)nsl * nt);
+  std::vector<int> fam(nsl), var(nsl);
+  std::vector<double> as(nsl), bs(nsl);
+  std::vector<int> na_cols, na_index(nsl, -1);
+  std::vector<int8_t> row_na(ny, 0);
+  for (int j = 0; j < nsl; ++j) {
+    const int jg = sp0 + j;
+    fam[j] = m->distr[jg];
+    var[j] = m->distr[jg + (size_t)m->ns];
+    HMSC_REQUIRE(fam[j] == 1 || fam[j] == 2, "Poisson species (distr family 3) are a 'next' row: not in this build");
+    if (fam[j] != 2) s.all_probit = false;
+    if (fam[j] == 1) s.any_normal = true;
+    if (var[j] == 1) s.any_var = true;
+    as[j] = m->aSigma[jg];
+    bs[j] = m->bSigma[jg];
+    for (int q = 0; q < nt; ++q) trl[j + (size_t)nsl * q] = m->Tr[jg + (size_t)m->ns * q];
+    bool col_na = false;
+    for (int i = 0; i < ny; ++i) {
+      const double y = m->Y[i + (size_t)ny * jg];
+      const size_t c = i + (size_t)ny * j;
+      yval[c] = y;
+      yraw[c] = m->Yraw ? m->Yraw[i + (size_t)ny * jg] : y;
+      if (std::isnan(y)) {
+        ycode[c] = -1;
+        col_na = true;
+        row_na[i] = 1;
+      } else {
+        ycode[c] = (fam[j] == 2 && y != 0.0) ? 1 : 0;
+      }
+    }
+    if (col_na) {
+      na_index[j] = (int)na_cols.size();
+      na_cols.push_back(j);
+    }
+  }
+  s.has_na = !na_cols.empty();
+  s.Ycode = dupload(ycode.data(), ycode.size());
+  if (!s.all_probit) {
+    s.Yval = dupload(yval.data(), yval.size());
+    s.Yraw = dupload(yraw.data(), yraw.size());
+  }
+  s.fam = dupload(fam.data(), nsl);
+  s.varest = dupload(var.data(), nsl);
+  s.aSigma = dupload(as.data(), nsl);
+  s.bSigma = dupload(bs.data(), nsl);
+  s.Tr = dupload(trl.data(), trl.size());
+  s.X = dupload(m->X, (size_t)ny * nc);
+  s.n_na_cols = (int)na_cols.size();
+  s.h_na_cols = na_cols;
+  if (s.has_na) {
+    s.na_cols = dupload(na_cols.data(), na_cols.size());
+    s.na_index = dupload(na_index.data(), nsl);
+    std::vector<int> na_rows, slot(ny, -1);
+    for (int i = 0; i < ny; ++i)
+      if (row_na[i]) {
+        slot[i] = (int)na_rows.size();
+        na_rows.push_back(i);
+      }
+    s.n_na_rows = (int)na_rows.size();
+    s.na_rows = dupload(na_rows.data(), na_rows.size());
+    s.row_na = dupload(row_na.data(), ny);
+    s.row_slot = dupload(slot.data(), ny);
+    s.Gna = dalloc<double>((size_t)s.n_na_cols * s.Kmax * s.Kmax);
+    s.Msmall = dalloc<double>((size_t)s.n_na_rows * (s.NFmax * s.NFmax + s.NFmax));
+  }
+  // priors and constants (host precompute)
+  Mat X(m->X, m->X + (size_t)ny * nc), XX(nc * nc, 0.0), TT(nt * nt, 0.0);
+  for (int a = 0; a < nc; ++a)
+    for (int b = 0; b < nc; ++b) {
+      double v = 0.0;
+      for (int i = 0; i < ny; ++i) v += X[i + (size_t)ny * a] * X[i + (size_t)ny * b];
+      XX[a + nc * b] = v;
+    }
+  for (int a = 0; a < nt; ++a)
+    for (int b = 0; b < nt; ++b) {
+      double v = 0.0;
+      for (int j = 0; j < m->ns; ++j) v += m->Tr[j + (size_t)m->ns * a] * m->Tr[j + (size_t)m->ns * b];
+      TT[a + nt * b] = v;
+    }
+  Mat UG(m->UGamma, m->UGamma + (size_t)N * N);
+  Mat iUG = host_inv_spd(UG, N);
+  Mat UGL = UG;
+  host_chol(UGL, N);
+  Mat iV0(nc * nc);
+  for (int a = 0; a < nc; ++a)
+    for (int b = 0; b < nc; ++b) iV0[a + nc * b] = iUG[a + N * b];  // iUGamma[1:nc,1:nc] (R/updateGamma2.R:37)
+  Mat V0g = host_inv_spd(iV0, nc);
+  Mat V0gXXV0g = host_mm(host_mm(V0g, XX, nc, nc, nc), V0g, nc, nc, nc);
+  Mat V0(m->V0, m->V0 + (size_t)nc * nc);
+  Mat V0inv = host_inv_spd(V0, nc);
+  s.XX = dupload(XX.data(), XX.size());
+  s.TT = dupload(TT.data(), TT.size());
+  s.iUGamma = dupload(iUG.data(), iUG.size());
+  s.UGammaL = dupload(UGL.data(), UGL.size());
+  s.iV0 = dupload(iV0.data(), iV0.size());
+  s.V0g = dupload(V0g.data(), V0g.size());
+  s.V0gXXV0g = dupload(V0gXXV0g.data(), V0gXXV0g.size());
+  s.V0 = dupload(V0.data(), V0.size());
+  s.V0inv = dupload(V0inv.data(), V0inv.size());
+  s.mGamma = dupload(m->mGamma, (size_t)N);
+  // state
+  s.Z = dalloc<double>((size_t)ny * nsl);
+  s.BL = dalloc<double>((size_t)s.Kmax * nsl);
+  s.Psi = dalloc<double>((size_t)std::max(1, s.NFmax) * nsl);
+  s.Delta = dalloc<double>(std::max(1, s.NFmax));
+  s.Gamma = dalloc<double>(N);
+  s.iV = dalloc<double>((size_t)nc * nc);
+  s.iSigma = dalloc<double>(nsl);
+  s.rho = dalloc<int>(1);
+  // workspaces
+  const int n_tiles = (ny + 63) / 64;
+  s.ntile_j = (nsl + 63) / 64;
+  s.nchunk = std::max(1, std::min(n_tiles, 512 / std::max(1, s.ntile_j)));
+  const int n_sblk = (ny + 63) / 64;
+  s.zl_split = std::max(1, std::min(std::min(16, (nsl + 3) / 4), (640 + n_sblk - 1) / n_sblk));
+  s.XZ = dalloc<double>((size_t)s.Kmax * nsl);
+  s.G = dalloc<double>((size_t)s.Kmax * s.Kmax);
+  s.ZTr = dalloc<double>((size_t)ny * nt);
+  s.XZ_part = dalloc<double>((size_t)s.nchunk * s.Kmax * nsl);
+  s.G_part = dalloc<double>((size_t)s.nchunk * s.Kmax * s.Kmax);
+  s.ZTr_part = dalloc<double>((size_t)s.ntile_j * ny * nt);
+  const int nfm = std::max(1, s.NFmax);
+  s.ZL = dalloc<double>((size_t)ny * nfm);
+  s.ZL_part = dalloc<double>((size_t)s.zl_split * ny * nfm);
+  s.CR = dalloc<double>((size_t)s.Kmax * nfm);
+  s.scratch_doubles = 1 << 20;
+  s.scratch = dalloc<double>(s.scratch_doubles);
+  s.psi_rs = dalloc<double>((size_t)64 * nfm);
+  s.ABpart = dalloc<double>((size_t)32 * (nc * nc + N + nfm * nt));
+  s.allreduce_buf = dalloc<double>((size_t)nc * nc + 2 * N + nfm * nt + nfm + 64);
+  s.dev_flags = dalloc<int>(16);
+  HIP_OK(hipDeviceSynchronize());
+}
+
+static void free_state(State& s) {
+  DeviceGuard dg(s.device);
+  (void)hipDeviceSynchronize();
+  void* ptrs[] = {s.X, s.Tr, s.Yval, s.Yraw, s.Ycode, s.fam, s.varest, s.V0, s.iUGamma, s.mGamma, s.UGammaL,
+                  s.aSigma, s.bSigma, s.XX, s.TT, s.V0g, s.V0gXXV0g, s.iV0, s.V0inv, s.na_cols, s.na_index,
+                  s.na_rows, s.row_na, s.row_slot, s.dev_flags, s.Z, s.BL, s.Psi, s.Delta, s.Gamma, s.iV,
+                  s.iSigma, s.rho, s.XZ, s.G, s.ZTr, s.XZ_part, s.G_part, s.ZTr_part, s.Gna, s.ZL, s.ZL_part,
+                  s.CR, s.Msmall, s.scratch, s.psi_rs, s.ABpart, s.dbg_prec, s.ring, s.allreduce_buf};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  for (int r = 0; r < s.nr; ++r) {
+    Level& L = s.lev[r];
+    void* lp[] = {L.Eta, L.Pi, L.unit_ptr, L.unit_rows, L.Alpha};
+    for (void* p : lp)
+      if (p) (void)hipFree(p);
+  }
+  for (hipEvent_t e : s.ring_done) (void)hipEventDestroy(e);
+  if (s.host_rec) (void)hipHostFree(s.host_rec);
+  if (s.comm) ncclCommDestroy((ncclComm_t)s.comm);
+  if (s.stream) (void)hipStreamDestroy(s.stream);
+  if (s.copy_stream) (void)hipStreamDestroy(s.copy_stream);
+}
+
+// ---------------------------- state get / set ----------------------------
+static void get_state(State& s, hmsc_params* p) {
+  DeviceGuard dg(s.device);
+  HIP_OK(hipStreamSynchronize(s.stream));
+  const int K = s.K, nsl = s.nsl, nc = s.nc;
+  std::vector<double> BL((size_t)K * nsl), Psi((size_t)s.NF * nsl), Delta(std::max(1, s.NF));
+  d2h(BL.data(), s.BL, BL.size(), s.stream);
+  d2h(Psi.data(), s.Psi, Psi.size(), s.stream);
+  d2h(Delta.data(), s.Delta, s.NF, s.stream);
+  if (p->Gamma) d2h(p->Gamma, s.Gamma, (size_t)nc * s.nt, s.stream);
+  if (p->iV) d2h(p->iV, s.iV, (size_t)nc * nc, s.stream);
+  if (p->iSigma) d2h(p->iSigma, s.iSigma, nsl, s.stream);
+  if (p->Z) d2h(p->Z, s.Z, (size_t)s.ny * nsl, s.stream);
+  for (int r = 0; r < s.nr; ++r) {
+    p->nf[r] = s.lev[r].nf;
+    if (p->Eta[r]) d2h(p->Eta[r], s.lev[r].Eta, (size_t)s.lev[r].np * s.lev[r].nf, s.stream);
+  }
+  HIP_OK(hipStreamSynchronize(s.stream));
+  if (p->Beta)
+    for (int j = 0; j < nsl; ++j)
+      for (int c = 0; c < nc; ++c) p->Beta[c + (size_t)nc * j] = BL[c + (size_t)K * j];
+  for (int r = 0; r < s.nr; ++r) {
+    const int nf = s.lev[r].nf, lo = s.loff(r), fo = s.foff(r);
+    for (int j = 0; j < nsl; ++j)
+      for (int h = 0; h < nf; ++h) {
+        if (p->Lambda[r]) p->Lambda[r][h + (size_t)nf * j] = BL[lo + h + (size_t)K * j];
+        if (p->Psi[r]) p->Psi[r][h + (size_t)nf * j] = Psi[fo + h + (size_t)s.NF * j];
+      }
+    for (int h = 0; h < nf; ++h) {
+      if (p->Delta[r]) p->Delta[r][h] = Delta[fo + h];
+      if (p->Alpha[r]) p->Alpha[r][h] = 1;
+    }
+  }
+  p->rho = 1;
+}
+
+static void set_state(State& s, const hmsc_params* p) {
+  DeviceGuard dg(s.device);
+  HIP_OK(hipStreamSynchronize(s.stream));
+  for (int r = 0; r < s.nr; ++r) {
+    if (p->nf[r] > 0) {
+      HMSC_REQUIRE(p->nf[r] <= std::min(s.lev[r].nfmax, s.NFmax), "set_state: nf exceeds allocation");
+      s.lev[r].nf = p->nf[r];
+    }
+  }
+  s.refresh_dims();
+  HMSC_REQUIRE(s.K <= s.Kmax, "set_state: K exceeds 64");
+  const int K = s.K, nsl = s.nsl, nc = s.nc;
+  std::vector<double> BL((size_t)K * nsl), Psi((size_t)std::max(1, s.NF) * nsl), Delta(std::max(1, s.NF));
+  d2h(BL.data(), s.BL, BL.size(), s.stream);
+  d2h(Psi.data(), s.Psi, (size_t)s.NF * nsl, s.stream);
+  d2h(Delta.data(), s.Delta, s.NF, s.stream);
+  HIP_OK(hipStreamSynchronize(s.stream));
+  if (p->Beta)
+    for (int j = 0; j < nsl; ++j)
+      for (int c = 0; c < nc; ++c) BL[c + (size_t)K * j] = p->Beta[c + (size_t)nc * j];
+  for (int r = 0; r < s.nr; ++r) {
+    const int nf = s.lev[r].nf, lo = s.loff(r), fo = s.foff(r);
+    for (int j = 0; j < nsl; ++j)
+      for (int h = 0; h < nf; ++h) {
+        if (p->Lambda[r]) BL[lo + h + (size_t)K * j] = p->Lambda[r][h + (size_t)nf * j];
+        if (p->Psi[r]) Psi[fo + h + (size_t)s.NF * j] = p->Psi[r][h + (size_t)nf * j];
+      }
+    if (p->Delta[r])
+      for (int h = 0; h < nf; ++h) Delta[fo + h] = p->Delta[r][h];
+    if (p->Eta[r]) h2d(s.lev[r].Eta, p->Eta[r], (size_t)s.lev[r].np * nf, s.stream);
+  }
+  h2d(s.BL, BL.data(), BL.size(), s.stream);
+  h2d(s.Psi, Psi.data(), (size_t)s.NF * nsl, s.stream);
+  h2d(s.Delta, Delta.data(), s.NF, s.stream);
+  if (p->Gamma) h2d(s.Gamma, p->Gamma, (size_t)nc * s.nt, s.stream);
+  if (p->iV) h2d(s.iV, p->iV, (size_t)nc * nc, s.stream);
+  if (p->iSigma) h2d(s.iSigma, p->iSigma, nsl, s.stream);
+  if (p->Z) h2d(s.Z, p->Z, (size_t)s.ny * nsl, s.stream);
+  HIP_OK(hipStreamSynchronize(s.stream));
+  s.zt_valid = false;
+}
+
+// ---------------------------- updateNf (host decision) ----------------------------
+// R/updateNf.R:3-70: with probability exp(-(1 + 0.0005 iter)) add a factor (if none is
+// redundant) or drop (reference quirk: setdiff(1:nf, logical) drops factor 1).
+static void update_nf(State& s, int r, uint32_t iter) {
+  Level& L = s.lev[r];
+  const uint32_t st = LEVEL_STRIDE * r;
+  const double u = uniforms(s.key, 0, 0, S_NF + st, iter).a;
+  const double prob = 1.0 / std::exp(1.0 + 0.0005 * iter);
+  if (!(u < prob)) return;
+  HIP_OK(hipStreamSynchronize(s.stream));
+  const int K = s.K, nsl = s.nsl, nf = L.nf, lo = s.loff(r), fo = s.foff(r);
+  std::vector<double> BL((size_t)K * nsl);
+  d2h(BL.data(), s.BL, BL.size(), s.stream);
+  HIP_OK(hipStreamSynchronize(s.stream));
+  std::vector<double> small(nf, 0.0);
+  for (int j = 0; j < nsl; ++j)
+    for (int h = 0; h < nf; ++h) small[h] += std::fabs(BL[lo + h + (size_t)K * j]) < 1e-3 ? 1.0 : 0.0;
+  if (s.nranks > 1) {
+    h2d(s.allreduce_buf, small.data(), nf, s.stream);
+    allreduce_sum(s, s.allreduce_buf, nf);
+    d2h(small.data(), s.allreduce_buf, nf, s.stream);
+    HIP_OK(hipStreamSynchronize(s.stream));
+  }
+  int num_red = 0;
+  bool all_lt = true;
+  for (int h = 0; h < nf; ++h) {
+    const double prop = small[h] / s.ns;
+    if (prop >= 1.0) ++num_red;
+    if (!(prop < 0.995)) all_lt = false;
+  }
+  const int nfcap = std::min(L.nfmax, s.NFmax);
+  std::vector<double> Psi((size_t)s.NF * nsl), Delta(s.NF), Eta((size_t)L.np * nf);
+  d2h(Psi.data(), s.Psi, Psi.size(), s.stream);
+  d2h(Delta.data(), s.Delta, s.NF, s.stream);
+  d2h(Eta.data(), L.Eta, Eta.size(), s.stream);
+  HIP_OK(hipStreamSynchronize(s.stream));
+  if (nf < L.nfmax && iter > 20 && num_red == 0 && all_lt) {
+    HMSC_REQUIRE(nf + 1 <= nfcap && s.K + 1 <= 64, "updateNf: nf would exceed this build's limit (K <= 64)");
+    const int K2 = K + 1, NF2 = s.NF + 1;
+    std::vector<double> BL2((size_t)K2 * nsl), Psi2((size_t)NF2 * nsl), Delta2(NF2);
+    for (int j = 0; j < nsl; ++j) {
+      for (int k = 0, k2 = 0; k2 < K2; ++k2) {
+        if (k2 == lo + nf) {
+          BL2[k2 + (size_t)K2 * j] = 0.0;  // lambdaNew = rbind(lambda, 0)  (:33)
+        } else {
+          BL2[k2 + (size_t)K2 * j] = BL[k + (size_t)K * j];
+          ++k;
+        }
+      }
+      for (int f = 0, f2 = 0; f2 < NF2; ++f2) {
+        if (f2 == fo + nf) {
+          Psi2[f2 + (size_t)NF2 * j] =
+              gamma_std(s.key, (uint32_t)(s.sp0 + j), S_NF_PSI + st, iter, L.nu / 2) / (L.nu / 2);  // (:36)
+        } else {
+          Psi2[f2 + (size_t)NF2 * j] = Psi[f + (size_t)s.NF * j];
+          ++f;
+        }
+      }
+    }
+    for (int f = 0, f2 = 0; f2 < NF2; ++f2) {
+      if (f2 == fo + nf)
+        Delta2[f2] = gamma_std(s.key, 0, S_NF_DELTA + st, iter, L.a2) / L.b2;  // (:39)
+      else
+        Delta2[f2] = Delta[f++];
+    }
+    std::vector<double> col(L.np);
+    for (int q = 0; q < L.np; ++q) col[q] = normal(s.key, (uint32_t)q, 0, S_NF_ETA + st, iter);  // (:30)
+    h2d(s.BL, BL2.data(), BL2.size(), s.stream);
+    h2d(s.Psi, Psi2.data(), Psi2.size(), s.stream);
+    h2d(s.Delta, Delta2.data(), NF2, s.stream);
+    h2d(L.Eta + (size_t)L.np * nf, col.data(), L.np, s.stream);
+    HIP_OK(hipStreamSynchronize(s.stream));
+    L.nf = nf + 1;
+  } else if (num_red > 0 && nf > L.nfmin) {
+    // indNotRed = setdiff(1:nf, indRedundant): drops factor 1 (index 0)   (:56)
+    const int drop = 0;
+    const int K2 = K - 1, NF2 = s.NF - 1;
+    std::vector<double> BL2((size_t)K2 * nsl), Psi2((size_t)std::max(1, NF2) * nsl), Delta2(std::max(1, NF2));
+    for (int j = 0; j < nsl; ++j) {
+      for (int k = 0, k2 = 0; k < K; ++k)
+        if (k != lo + drop) BL2[k2++ + (size_t)K2 * j] = BL[k + (size_t)K * j];
+      for (int f = 0, f2 = 0; f < s.NF; ++f)
+        if (f != fo + drop) Psi2[f2++ + (size_t)NF2 * j] = Psi[f + (size_t)s.NF * j];
+    }
+    for (int f = 0, f2 = 0; f < s.NF; ++f)
+      if (f != fo + drop) Delta2[f2++] = Delta[f];
+    std::vector<double> Eta2((size_t)L.np * (nf - 1));
+    for (int h = 0, h2 = 0; h < nf; ++h)
+      if (h != drop) {
+        std::memcpy(&Eta2[(size_t)L.np * h2], &Eta[(size_t)L.np * h], L.np * sizeof(double));
+        ++h2;
+      }
+    h2d(s.BL, BL2.data(), BL2.size(), s.stream);
+    h2d(s.Psi, Psi2.data(), (size_t)NF2 * nsl, s.stream);
+    h2d(s.Delta, Delta2.data(), NF2, s.stream);
+    h2d(L.Eta, Eta2.data(), Eta2.size(), s.stream);
+    HIP_OK(hipStreamSynchronize(s.stream));
+    L.nf = nf - 1;
+  } else {
+    return;
+  }
+  s.refresh_dims();
+  s.zt_valid = false;
+}
+
+// ---------------------------- sweep ----------------------------
+static void run_updater(State& s, uint32_t which, uint32_t iter) {
+  switch (which) {
+    case HMSC_UP_GAMMA2:
+      launch_gamma2(s, iter);
+      break;
+    case HMSC_UP_GAMMAETA:
+      throw HmscError(-1, "updateGammaEta is a 'next' row: disable it with updater=list(GammaEta=FALSE)");
+    case HMSC_UP_BETALAMBDA:
+      launch_beta_lambda(s, iter);
+      break;
+    case HMSC_UP_GAMMAV:
+      launch_gamma_v(s, iter);
+      break;
+    case HMSC_UP_RHO:
+      break;  // C is NULL: updateRho is not called (R/sampleMcmc.R:263)
+    case HMSC_UP_LAMBDAPRIORS:
+      launch_lambda_priors(s, iter);
+      break;
+    case HMSC_UP_ETA:
+      launch_eta(s, iter);
+      break;
+    case HMSC_UP_ALPHA:
+      break;  // non-spatial levels: Alpha = rep(1, nf) (R/updateAlpha.R:81-82)
+    case HMSC_UP_INVSIGMA:
+      launch_inv_sigma(s, iter);
+      break;
+    case HMSC_UP_Z:
+      launch_update_z(s, iter, false);
+      break;
+    default:
+      throw HmscError(-1, "unknown or out-of-scope updater bit");
+  }
+}
+
+static void sweep(State& s, uint32_t iter, bool adapt) {
+  static const uint32_t order[] = {HMSC_UP_GAMMA2,       HMSC_UP_GAMMAETA, HMSC_UP_BETALAMBDA, HMSC_UP_GAMMAV,
+                                   HMSC_UP_RHO,          HMSC_UP_LAMBDAPRIORS, HMSC_UP_ETA,  HMSC_UP_ALPHA,
+                                   HMSC_UP_INVSIGMA,     HMSC_UP_Z};
+  for (uint32_t u : order)
+    if (s.mask & u) run_updater(s, u, iter);
+  if (adapt)
+    for (int r = 0; r < s.nr; ++r) update_nf(s, r, iter);
+}
+
+static void unpack_record(const State& s, const double* slot, int k, int samples, hmsc_record* rec) {
+  const int K = s.K, nsl = s.nsl, nc = s.nc, nt = s.nt, NF = s.NF;
+  const double* BL = slot;
+  const double* Psi = BL + (size_t)K * nsl;
+  const double* Delta = Psi + (size_t)NF * nsl;
+  const double* Gamma = Delta + NF;
+  const double* iV = Gamma + (size_t)nc * nt;
+  const double* iS = iV + (size_t)nc * nc;
+  const double* eta = iS + nsl;
+  if (rec->Beta)
+    for (int j = 0; j < nsl; ++j)
+      for (int c = 0; c < nc; ++c) rec->Beta[(size_t)k * nc * nsl + c + (size_t)nc * j] = BL[c + (size_t)K * j];
+  if (rec->Gamma) std::memcpy(rec->Gamma + (size_t)k * nc * nt, Gamma, sizeof(double) * nc * nt);
+  if (rec->iV) std::memcpy(rec->iV + (size_t)k * nc * nc, iV, sizeof(double) * nc * nc);
+  if (rec->iSigma) std::memcpy(rec->iSigma + (size_t)k * nsl, iS, sizeof(double) * nsl);
+  if (rec->rho) rec->rho[k] = 1;
+  for (int r = 0; r < s.nr; ++r) {
+    const Level& L = s.lev[r];
+    const int nf = L.nf, nfm = L.nfmax, lo = s.loff(r), fo = s.foff(r);
+    if (rec->rec_nf) rec->rec_nf[r * samples + k] = nf;
+    if (rec->Lambda[r] || rec->Psi[r])
+      for (int j = 0; j < nsl; ++j)
+        for (int h = 0; h < nfm; ++h) {
+          const size_t o = (size_t)k * nfm * nsl + h + (size_t)nfm * j;
+          if (rec->Lambda[r]) rec->Lambda[r][o] = h < nf ? BL[lo + h + (size_t)K * j] : 0.0;
+          if (rec->Psi[r]) rec->Psi[r][o] = h < nf ? Psi[fo + h + (size_t)NF * j] : 0.0;
+        }
+    for (int h = 0; h < nfm; ++h) {
+      if (rec->Delta[r]) rec->Delta[r][(size_t)k * nfm + h] = h < nf ? Delta[fo + h] : 1.0;
+      if (rec->Alpha[r]) rec->Alpha[r][(size_t)k * nfm + h] = 1;
+    }
+    if (rec->Eta[r])
+      for (int h = 0; h < nfm; ++h) {
+        double* dst = rec->Eta[r] + (size_t)k * L.np * nfm + (size_t)L.np * h;
+        if (h < nf)
+          std::memcpy(dst, eta + (size_t)L.np * h, sizeof(double) * L.np);
+        else
+          std::memset(dst, 0, sizeof(double) * L.np);
+      }
+    eta += (size_t)L.np * nf;
+  }
+}
+
+static void run(State& s, int transient, int samples, int thin, const int* adaptNf, int iter0, int verbose,
+                int chain, hmsc_record* rec) {
+  DeviceGuard dg(s.device);
+  HMSC_REQUIRE(thin >= 1 && samples >= 0 && transient >= 0, "bad transient/samples/thin");
+  for (int r = 0; r < s.nr; ++r)
+    HMSC_REQUIRE(adaptNf == nullptr || adaptNf[r] <= transient,
+                 "transient parameter should be no less than any element of adaptNf parameter");
+  const bool recording = rec != nullptr && samples > 0;
+  if (recording) {
+    s.slot_doubles = record_slot_doubles(s);
+    const int want_slots = std::min(samples, 32);
+    if (s.ring_slots < want_slots) {
+      if (s.ring) HIP_OK(hipFree(s.ring));
+      for (hipEvent_t e : s.ring_done) HIP_OK(hipEventDestroy(e));
+      s.ring_done.clear();
+      s.ring = dalloc<double>(s.slot_doubles * want_slots);
+      s.ring_slots = want_slots;
+      for (int i = 0; i < want_slots; ++i) {
+        hipEvent_t e;
+        HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        s.ring_done.push_back(e);
+      }
+    }
+    if (s.host_rec) HIP_OK(hipHostFree(s.host_rec));
+    HIP_OK(hipHostMalloc(&s.host_rec, sizeof(double) * s.slot_doubles * samples, hipHostMallocDefault));
+  }
+  const int total = transient + samples * thin;
+  std::vector<hipEvent_t> packed;
+  if (recording) {
+    packed.resize(s.ring_slots);
+    for (auto& e : packed) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  for (int it = 1; it <= total; ++it) {
+    const uint32_t iter = (uint32_t)(iter0 + it);
+    bool adapt = false;
+    if (adaptNf)
+      for (int r = 0; r < s.nr; ++r) adapt |= it <= adaptNf[r];
+    sweep(s, iter, adapt);
+    if (recording && it > transient && (it - transient) % thin == 0) {
+      const int k = (it - transient) / thin - 1;
+      const int slot = k % s.ring_slots;
+      if (k >= s.ring_slots) HIP_OK(hipStreamWaitEvent(s.stream, s.ring_done[slot], 0));
+      double* dslot = s.ring + s.slot_doubles * slot;
+      launch_record(s, dslot);
+      HIP_OK(hipEventRecord(packed[slot], s.stream));
+      HIP_OK(hipStreamWaitEvent(s.copy_stream, packed[slot], 0));
+      HIP_OK(hipMemcpyAsync(s.host_rec + s.slot_doubles * k, dslot, sizeof(double) * s.slot_doubles,
+                            hipMemcpyDeviceToHost, s.copy_stream));
+      HIP_OK(hipEventRecord(s.ring_done[slot], s.copy_stream));
+    }
+    if (verbose > 0 && it % verbose == 0) {
+      HIP_OK(hipStreamSynchronize(s.stream));
+      std::printf("[1] \"Chain %d, iteration %d of %d, (%s)\"\n", chain, it, total,
+                  it > transient ? "sampling" : "transient");
+      std::fflush(stdout);
+    }
+  }
+  HIP_OK(hipStreamSynchronize(s.stream));
+  HIP_OK(hipStreamSynchronize(s.copy_stream));
+  for (auto& e : packed) HIP_OK(hipEventDestroy(e));
+  int flag = 0;
+  HIP_OK(hipMemcpy(&flag, s.dev_flags, sizeof(int), hipMemcpyDeviceToHost));
+  HMSC_REQUIRE(flag == 0, "a Cholesky factorisation failed (matrix not positive definite)");
+  if (recording)
+    for (int k = 0; k < samples; ++k) unpack_record(s, s.host_rec + s.slot_doubles * k, k, samples, rec);
+}
+
+}  // namespace hmsc
+
+using namespace hmsc;
+
+extern "C" {
+
+const char* hmsc_last_error(void) { return g_last_error.c_str(); }
+
+int hmsc_device_count(int32_t* n) {
+  return guarded([&] {
+    int c = 0;
+    HIP_OK(hipGetDeviceCount(&c));
+    *n = c;
+  });
+}
+
+int hmsc_comm_unique_id(void* out128) {
+  return guarded([&] {
+    ncclUniqueId id;
+    const ncclResult_t r = ncclGetUniqueId(&id);
+    HMSC_REQUIRE(r == ncclSuccess, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    static_assert(sizeof(ncclUniqueId) == 128, "unexpected ncclUniqueId size");
+    std::memcpy(out128, &id, sizeof(id));
+  });
+}
+
+int hmsc_create_sharded(const hmsc_model* model, uint64_t seed, int32_t device, uint32_t updater_mask,
+                        int32_t rank, int32_t nranks, const void* comm_id, hmsc_state** out) {
+  return guarded([&] {
+    HMSC_REQUIRE(out != nullptr, "out is NULL");
+    HMSC_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank / nranks");
+    auto* h = new hmsc_state();
+    try {
+      build_state(h->s, model, seed, device, updater_mask, rank, nranks, comm_id);
+    } catch (...) {
+      free_state(h->s);
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+int hmsc_create(const hmsc_model* model, uint64_t seed, int32_t device, uint32_t updater_mask, hmsc_state** out) {
+  return hmsc_create_sharded(model, seed, device, updater_mask, 0, 1, nullptr, out);
+}
+
+void hmsc_destroy(hmsc_state* h) {
+  if (!h) return;
+  try {
+    free_state(h->s);
+  } catch (...) {
+  }
+  delete h;
+}
+
+int hmsc_init_state(hmsc_state* h, const int32_t* nf0) {
+  return guarded([&] {
+    State& s = h->s;
+    DeviceGuard dg(s.device);
+    if (nf0)
+      for (int r = 0; r < s.nr; ++r) {
+        HMSC_REQUIRE(nf0[r] >= 1 && nf0[r] <= std::min(s.lev[r].nfmax, s.NFmax), "init: bad nf0");
+        s.lev[r].nf = nf0[r];
+      }
+    s.refresh_dims();
+    HMSC_REQUIRE(s.K <= s.Kmax, "init: K exceeds 64");
+    launch_init(s);
+    launch_update_z(s, 0, true);  // Z = updateZ(Y=hM$Y, ...) (R/computeInitialParameters.R:254)
+    HIP_OK(hipStreamSynchronize(s.stream));
+  });
+}
+
+int hmsc_set_state(hmsc_state* h, const hmsc_params* p) {
+  return guarded([&] { set_state(h->s, p); });
+}
+
+int hmsc_get_state(hmsc_state* h, hmsc_params* p) {
+  return guarded([&] { get_state(h->s, p); });
+}
+
+int hmsc_get_nf(hmsc_state* h, int32_t* nf) {
+  return guarded([&] {
+    for (int r = 0; r < h->s.nr; ++r) nf[r] = h->s.lev[r].nf;
+  });
+}
+
+int hmsc_sweep(hmsc_state* h, int32_t iter, int32_t adapt_nf) {
+  return guarded([&] {
+    DeviceGuard dg(h->s.device);
+    sweep(h->s, (uint32_t)iter, adapt_nf != 0);
+  });
+}
+
+int hmsc_update(hmsc_state* h, uint32_t which, int32_t iter) {
+  return guarded([&] {
+    DeviceGuard dg(h->s.device);
+    run_updater(h->s, which, (uint32_t)iter);
+  });
+}
+
+int hmsc_set_noise_mode(hmsc_state* h, int32_t mode) {
+  return guarded([&] {
+    State& s = h->s;
+    DeviceGuard dg(s.device);
+    s.noise_mode = mode & 1;
+    if ((mode & 2) && !s.dbg_prec) s.dbg_prec = dalloc<double>((size_t)s.nsl * s.Kmax * s.Kmax);
+    if (!(mode & 2) && s.dbg_prec) {
+      HIP_OK(hipStreamSynchronize(s.stream));
+      HIP_OK(hipFree(s.dbg_prec));
+      s.dbg_prec = nullptr;
+    }
+  });
+}
+
+int hmsc_run(hmsc_state* h, int32_t transient, int32_t samples, int32_t thin, const int32_t* adaptNf,
+             int32_t iter0, hmsc_record* rec) {
+  return guarded([&] { run(h->s, transient, samples, thin, adaptNf, iter0, 0, 1, rec); });
+}
+
+int hmsc_run_verbose(hmsc_state* h, int32_t transient, int32_t samples, int32_t thin, const int32_t* adaptNf,
+                     int32_t iter0, int32_t verbose, int32_t chain, hmsc_record* rec) {
+  return guarded([&] { run(h->s, transient, samples, thin, adaptNf, iter0, verbose, chain, rec); });
+}
+
+int hmsc_sync(hmsc_state* h) {
+  return guarded([&] {
+    DeviceGuard dg(h->s.device);
+    HIP_OK(hipStreamSynchronize(h->s.stream));
+    HIP_OK(hipStreamSynchronize(h->s.copy_stream));
+  });
+}
+
+int hmsc_debug_get(hmsc_state* h, const char* name, double* out, int64_t n) {
+  return guarded([&] {
+    State& s = h->s;
+    DeviceGuard dg(s.device);
+    HIP_OK(hipStreamSynchronize(s.stream));
+    const std::string nm(name);
+    const double* src = nullptr;
+    int64_t avail = 0;
+    if (nm == "Z") src = s.Z, avail = (int64_t)s.ny * s.nsl;
+    else if (nm == "XZ") src = s.XZ, avail = (int64_t)s.K * s.nsl;
+    else if (nm == "G") src = s.G, avail = (int64_t)s.Kmax * s.Kmax;
+    else if (nm == "ZTr") src = s.ZTr, avail = (int64_t)s.ny * s.nt;
+    else if (nm == "BL") src = s.BL, avail = (int64_t)s.K * s.nsl;
+    else if (nm == "BL_prec") src = s.dbg_prec, avail = s.dbg_prec ? (int64_t)s.nsl * s.K * s.K : 0;
+    else if (nm == "CR") src = s.CR, avail = (int64_t)s.Kmax * s.NFmax;
+    else if (nm == "ZL") src = s.ZL_part, avail = (int64_t)s.zl_split * s.ny * s.NF;
+    else if (nm == "dims") {
+      HMSC_REQUIRE(n >= 8, "dims needs 8 slots");
+      const double d[8] = {(double)s.K, (double)s.NF, (double)s.Kmax, (double)s.NFmax, (double)s.nchunk,
+                           (double)s.ntile_j, (double)s.zl_split, (double)s.zt_valid};
+      std::memcpy(out, d, sizeof(d));
+      return;
+    } else
+      throw HmscError(-1, "debug_get: unknown buffer " + nm);
+    HMSC_REQUIRE(src != nullptr, "debug_get: buffer not allocated (enable with noise mode bit 2)");
+    HMSC_REQUIRE(n <= avail, "debug_get: n exceeds buffer size");
+    HIP_OK(hipMemcpy(out, src, sizeof(double) * n, hipMemcpyDeviceToHost));
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,1509 @@
+// HIP kernels for one Gibbs sweep of Hmsc's sampleMcmc (R/sampleMcmc.R:219-306) on gfx950.
+//
+// Dataflow (per sweep, synthetic config ny=10k ns=1k nc=20 nf=10):
+//   updateZ      z_fused_kernel   E = XEta*BL on the fly, truncated-normal draw, stores Z,
+//                                 and, while the Z tile is still on chip, the three linear
+//                                 contractions of Z the next sweep needs:
+//                                   XZ  = XEta^T (Yx o Z)   (updateBetaLambda, R/updateBetaLambda.R:66)
+//                                   G   = XEta^T XEta       (R/updateBetaLambda.R:65)
+//                                   ZTr = Z Tr              (updateGamma2, R/updateGamma2.R:46)
+//                                 so updateBetaLambda never re-reads Z from HBM.
+//   updateBetaLambda  beta_lambda_kernel  one wave per species: K x K precision in LDS,
+//                                 Cholesky, two triangular solves, draw.
+//   updateGammaV / updateGamma2 / updateLambdaPriors: species-parallel partial reductions
+//                                 + one single-workgroup kernel for the tiny dense algebra.
+//   updateEta    zl_kernel        the one HBM pass over Z: ZL = Z (Lambda diag(iSigma))^T
+//                eta_unit_kernel  one wave per unit: nf x nf precision, Cholesky, draw.
+//   updateInvSigma  inv_sigma_kernel (normal species only).
+// All randomness: counter-based Philox (rng.h), keyed by chain seed, counted by
+// (element, sub, stream, sweep), so draws do not depend on grid shape or sharding.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "common.h"
+#include "rng.h"
+#include "state.h"
+
+namespace hmsc {
+
+// ---------------------------------------------------------------------------
+// XEta row gather: XEta[i, k] = X[i, k] (k < nc) or Eta_r[Pi_r[i], h]
+// ---------------------------------------------------------------------------
+struct EtaView {
+  const double* X;
+  int ny, nc, nr;
+  const double* Eta[HMSC_MAX_LEVELS];
+  const int* Pi[HMSC_MAX_LEVELS];
+  int np[HMSC_MAX_LEVELS];
+  int nf[HMSC_MAX_LEVELS];
+};
+
+__device__ __forceinline__ double xeta_at(const EtaView& v, int i, int k) {
+  if (k < v.nc) return v.X[i + (size_t)v.ny * k];
+  int h = k - v.nc;
+  for (int r = 0; r < v.nr; ++r) {
+    if (h < v.nf[r]) return v.Eta[r][v.Pi[r][i] + (size_t)v.np[r] * h];
+    h -= v.nf[r];
+  }
+  return 0.0;
+}
+
+static EtaView make_view(const State& s) {
+  EtaView v{};
+  v.X = s.X;
+  v.ny = s.ny;
+  v.nc = s.nc;
+  v.nr = s.nr;
+  for (int r = 0; r < s.nr; ++r) {
+    v.Eta[r] = s.lev[r].Eta;
+    v.Pi[r] = s.lev[r].Pi;
+    v.np[r] = s.lev[r].np;
+    v.nf[r] = s.lev[r].nf;
+  }
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// updateZ (R/updateZ.R:4-94) fused with the Z contractions of the next sweep.
+// Grid: (site chunks, species tiles of 64); block 256 = 4 waves; each wave owns 16
+// species of the tile, each lane one site of the current 64-site tile.
+// ---------------------------------------------------------------------------
+struct ZArgs {
+  EtaView ev;
+  int K, ns_loc, sp0, nt, tiles_per_chunk;
+  const double* BL;
+  const double* iSigma;
+  const int8_t* Ycode;
+  const double* Yval;
+  const int* fam;
+  const double* Tr;  // local species rows, ld ns_loc
+  double* Z;
+  double* XZ_part;   // [chunk][K x ns_loc]
+  double* G_part;    // [chunk][Kmax x Kmax]
+  double* ZTr_part;  // [tile_j][ny x nt]
+  int Kmax;
+  Key key;
+  uint32_t iter;
+  int noise_zero;
+};
+
+constexpr int ZT_I = 64;   // sites per tile
+constexpr int ZT_J = 64;   // species per tile
+constexpr int ZT_LD = 65;  // padded LDS leading dimension (conflict-free column reads)
+constexpr int KMAX_Z = 64;
+
+template <bool DRAW, bool HAS_NA>
+__global__ __launch_bounds__(256) void z_fused_kernel(ZArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int K = a.K;
+  const int ny = a.ev.ny;
+  double* sXE = smem;                  // [k][ZT_LD]
+  double* sBL = sXE + K * ZT_LD;       // [k][64]
+  double* sZ = sBL + K * ZT_J;         // [jj][ZT_LD]   masked Z (XZ)
+  double* sZu = sZ + ZT_J * ZT_LD;     // [jj][ZT_LD]   unmasked Z (ZTr), HAS_NA only
+  double* sTr = (HAS_NA ? sZu + ZT_J * ZT_LD : sZu);  // [jj + 64 t]
+  double* sSd = sTr + ZT_J * a.nt;     // [jj]
+  int* sFam = (int*)(sSd + ZT_J);      // [jj]
+
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int j0 = blockIdx.y * ZT_J;
+  for (int p = t; p < K * ZT_J; p += 256) {
+    const int k = p >> 6, jj = p & 63, j = j0 + jj;
+    sBL[p] = (j < a.ns_loc) ? a.BL[k + (size_t)K * j] : 0.0;
+  }
+  for (int p = t; p < ZT_J * a.nt; p += 256) {
+    const int jj = p & 63, tt = p >> 6, j = j0 + jj;
+    sTr[p] = (j < a.ns_loc) ? a.Tr[j + (size_t)a.ns_loc * tt] : 0.0;
+  }
+  if (t < ZT_J) {
+    const int j = j0 + t;
+    sSd[t] = (j < a.ns_loc) ? 1.0 / sqrt(a.iSigma[j]) : 1.0;
+    sFam[t] = (j < a.ns_loc) ? a.fam[j] : 0;
+  }
+
+  double accXZ[KMAX_Z / 4];
+  double accG[KMAX_Z / 4];
+#pragma unroll
+  for (int q = 0; q < KMAX_Z / 4; ++q) accXZ[q] = accG[q] = 0.0;
+  const bool do_gram = (blockIdx.y == 0);
+
+  const int n_tiles = (ny + ZT_I - 1) / ZT_I;
+  const int tb = blockIdx.x * a.tiles_per_chunk;
+  const int te = min(n_tiles, tb + a.tiles_per_chunk);
+  for (int tile = tb; tile < te; ++tile) {
+    const int i0 = tile * ZT_I;
+    __syncthreads();
+    for (int p = t; p < K * ZT_I; p += 256) {
+      const int k = p >> 6, ii = p & 63, i = i0 + ii;
+      sXE[k * ZT_LD + ii] = (i < ny) ? xeta_at(a.ev, i, k) : 0.0;
+    }
+    __syncthreads();
+    const int i = i0 + lane;
+    double zq[16];
+    if (DRAW) {
+      double e[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) e[q] = 0.0;
+      for (int k = 0; k < K; ++k) {
+        const double x = sXE[k * ZT_LD + lane];
+        const double* b = sBL + k * ZT_J + w * 16;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) e[q] = fma(x, b[q], e[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int jj = w * 16 + q, j = j0 + jj;
+        double z = 0.0;
+        if (i < ny && j < a.ns_loc) {
+          const size_t cell = (size_t)i + (size_t)ny * j;
+          const uint32_t idx = (uint32_t)((size_t)i + (size_t)ny * (size_t)(a.sp0 + j));
+          const double sd = sSd[jj];
+          const int code = a.Ycode[cell];
+          const int fam = sFam[jj];
+          if (code < 0) {  // NA cell: Z ~ N(E, sd)   R/updateZ.R:92
+            const double nz = a.noise_zero ? 0.0 : normal(a.key, idx, 0, S_Z, a.iter);
+            z = e[q] + sd * nz;
+          } else if (fam == 2) {  // probit: truncated normal   R/updateZ.R:43-63
+            const double u = uniforms(a.key, idx, 0, S_Z, a.iter).a;
+            const double sg = code ? 1.0 : -1.0;
+            const double wdraw = trunc_normal_lower(-sg * e[q] / sd, u);
+            z = e[q] + sd * sg * wdraw;
+          } else {  // normal: Z = Y   R/updateZ.R:40-41
+            z = a.Yval[cell];
+          }
+          a.Z[cell] = z;
+        }
+        zq[q] = z;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int j = j0 + w * 16 + q;
+        zq[q] = (i < ny && j < a.ns_loc) ? a.Z[(size_t)i + (size_t)ny * j] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int jj = w * 16 + q, j = j0 + jj;
+      if (HAS_NA) {
+        const bool obs = (i < ny && j < a.ns_loc) ? (a.Ycode[(size_t)i + (size_t)ny * j] >= 0) : false;
+        sZ[jj * ZT_LD + lane] = obs ? zq[q] : 0.0;
+        sZu[jj * ZT_LD + lane] = zq[q];
+      } else {
+        sZ[jj * ZT_LD + lane] = zq[q];
+      }
+    }
+    __syncthreads();
+    // XZ partial: thread -> species lane, rows k = w + 4q
+    {
+      const double* zc = sZ + lane * ZT_LD;
+      for (int ii = 0; ii < ZT_I; ++ii) {
+        const double zv = zc[ii];
+#pragma unroll
+        for (int q = 0; q < KMAX_Z / 4; ++q) {
+          const int k = w + 4 * q;
+          if (k < K) accXZ[q] = fma(sXE[k * ZT_LD + ii], zv, accXZ[q]);
+        }
+      }
+    }
+    if (do_gram && lane < K) {
+      const double* xc = sXE + lane * ZT_LD;
+      for (int ii = 0; ii < ZT_I; ++ii) {
+        const double xv = xc[ii];
+#pragma unroll
+        for (int q = 0; q < KMAX_Z / 4; ++q) {
+          const int k = w + 4 * q;
+          if (k < K) accG[q] = fma(sXE[k * ZT_LD + ii], xv, accG[q]);
+        }
+      }
+    }
+    // ZTr partial for this (site tile, species tile)
+    if (i < ny) {
+      const double* zsrc = HAS_NA ? sZu : sZ;
+      for (int tt = w; tt < a.nt; tt += 4) {
+        double acc = 0.0;
+        for (int jj = 0; jj < ZT_J; ++jj) acc = fma(zsrc[jj * ZT_LD + lane], sTr[jj + ZT_J * tt], acc);
+        a.ZTr_part[(size_t)blockIdx.y * ny * a.nt + i + (size_t)ny * tt] = acc;
+      }
+    }
+  }
+  // write chunk partials
+  {
+    const int j = j0 + lane;
+    double* dst = a.XZ_part + (size_t)blockIdx.x * K * a.ns_loc;
+#pragma unroll
+    for (int q = 0; q < KMAX_Z / 4; ++q) {
+      const int k = w + 4 * q;
+      if (k < K && j < a.ns_loc) dst[k + (size_t)K * j] = accXZ[q];
+    }
+  }
+  if (do_gram && lane < K) {
+    double* dst = a.G_part + (size_t)blockIdx.x * a.Kmax * a.Kmax;
+#pragma unroll
+    for (int q = 0; q < KMAX_Z / 4; ++q) {
+      const int k = w + 4 * q;
+      if (k < K) dst[k + a.Kmax * lane] = accG[q];
+    }
+  }
+}
+
+// deterministic slab reduction: out[e] = sum_c part[c*stride + e]
+__global__ void slab_sum_kernel(const double* __restrict__ part, double* __restrict__ out, int64_t n,
+                                int nparts, int64_t stride) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    double s = 0.0;
+    for (int c = 0; c < nparts; ++c) s += part[c * stride + e];
+    out[e] = s;
+  }
+}
+
+static int grid_for(int64_t n, int block = 256, int cap = 2048) {
+  int64_t g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+static size_t z_smem_bytes(const State& s, bool has_na) {
+  size_t d = (size_t)s.K * ZT_LD + (size_t)s.K * ZT_J + (size_t)ZT_J * ZT_LD +
+             (has_na ? (size_t)ZT_J * ZT_LD : 0) + (size_t)ZT_J * s.nt + ZT_J;
+  return d * sizeof(double) + ZT_J * sizeof(int);
+}
+
+static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
+  HMSC_REQUIRE(s.K <= KMAX_Z, "updateZ: K = nc + sum(nf) must be <= 64 in this build");
+  ZArgs a{};
+  a.ev = make_view(s);
+  a.K = s.K;
+  a.Kmax = s.Kmax;
+  a.ns_loc = s.nsl;
+  a.sp0 = s.sp0;
+  a.nt = s.nt;
+  const int n_tiles = (s.ny + ZT_I - 1) / ZT_I;
+  a.tiles_per_chunk = (n_tiles + s.nchunk - 1) / s.nchunk;
+  const int nchunk = (n_tiles + a.tiles_per_chunk - 1) / a.tiles_per_chunk;
+  a.BL = s.BL;
+  a.iSigma = s.iSigma;
+  a.Ycode = s.Ycode;
+  a.Yval = use_raw_y ? s.Yraw : s.Yval;
+  a.fam = s.fam;
+  a.Tr = s.Tr;
+  a.Z = s.Z;
+  a.XZ_part = s.XZ_part;
+  a.G_part = s.G_part;
+  a.ZTr_part = s.ZTr_part;
+  a.key = s.key;
+  a.iter = iter;
+  a.noise_zero = s.noise_mode;
+  dim3 grid(nchunk, s.ntile_j);
+  const size_t smem = z_smem_bytes(s, s.has_na);
+  if (draw) {
+    if (s.has_na)
+      z_fused_kernel<true, true><<<grid, 256, smem, s.stream>>>(a);
+    else
+      z_fused_kernel<true, false><<<grid, 256, smem, s.stream>>>(a);
+  } else {
+    if (s.has_na)
+      z_fused_kernel<false, true><<<grid, 256, smem, s.stream>>>(a);
+    else
+      z_fused_kernel<false, false><<<grid, 256, smem, s.stream>>>(a);
+  }
+  HIP_OK(hipGetLastError());
+  const int64_t nXZ = (int64_t)s.K * s.nsl;
+  slab_sum_kernel<<<grid_for(nXZ), 256, 0, s.stream>>>(s.XZ_part, s.XZ, nXZ, nchunk, nXZ);
+  const int64_t nG = (int64_t)s.Kmax * s.Kmax;
+  slab_sum_kernel<<<grid_for(nG), 256, 0, s.stream>>>(s.G_part, s.G, nG, nchunk, nG);
+  const int64_t nZT = (int64_t)s.ny * s.nt;
+  slab_sum_kernel<<<grid_for(nZT), 256, 0, s.stream>>>(s.ZTr_part, s.ZTr, nZT, s.ntile_j, nZT);
+  HIP_OK(hipGetLastError());
+}
+
+// masked Gram XEta^T diag(Yx_j) XEta for species with NA (R/updateBetaLambda.R:103-112)
+__global__ __launch_bounds__(256) void gram_na_kernel(EtaView ev, int K, int Kmax, const int* na_cols,
+                                                      const int8_t* Ycode, double* Gna) {
+  const int c = blockIdx.x;
+  const int j = na_cols[c];
+  const int ny = ev.ny;
+  double* out = Gna + (size_t)c * Kmax * Kmax;
+  for (int p = threadIdx.x; p < K * K; p += blockDim.x) {
+    const int k1 = p % K, k2 = p / K;
+    if (k1 > k2) continue;
+    double s = 0.0;
+    for (int i = 0; i < ny; ++i)
+      if (Ycode[(size_t)i + (size_t)ny * j] >= 0) s += xeta_at(ev, i, k1) * xeta_at(ev, i, k2);
+    out[k1 + Kmax * k2] = s;
+    out[k2 + Kmax * k1] = s;
+  }
+}
+
+void launch_update_z(State& s, uint32_t iter, bool use_raw_y) {
+  run_z_fused(s, true, iter, use_raw_y);
+  s.zt_valid = true;
+}
+
+void launch_zt_refresh(State& s) {
+  run_z_fused(s, false, 0, false);
+  s.zt_valid = true;
+}
+
+// ---------------------------------------------------------------------------
+// updateBetaLambda, C = NULL branch (R/updateBetaLambda.R:76-123): one wave per
+// species, K x K precision iU = P + iSigma_j G in LDS, Cholesky, m = iU^-1 rhs,
+// draw m + R^-1 xi  computed as  L^-T (L^-1 rhs + xi).
+// ---------------------------------------------------------------------------
+struct BLArgs {
+  int K, Kmax, nc, nt, nr, NF, ns_loc, ns_glob, sp0;
+  const double* G;
+  const double* Gna;
+  const int* na_index;  // per local species: row in Gna or -1
+  const double* XZ;
+  const double* iV;
+  const double* Gamma;
+  const double* Tr;
+  const double* Psi;
+  const double* Delta;
+  const double* iSigma;
+  int lev_nf[HMSC_MAX_LEVELS];
+  double* BL;
+  double* dbg_prec;
+  Key key;
+  uint32_t iter;
+  int noise_zero;
+};
+
+__global__ __launch_bounds__(64) void beta_lambda_kernel(BLArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int K = a.K, nc = a.nc;
+  double* A = smem;               // K x K
+  double* rhs = A + K * K;        // K
+  double* tau = rhs + K;          // NF
+  double* mu = tau + a.NF + 1;    // nc
+  int* flag = (int*)(mu + nc + 1);
+  const int j = blockIdx.x, t = threadIdx.x;
+  if (t == 0) {  // tau = cumprod(delta) per level (R/updateBetaLambda.R:51)
+    int f = 0;
+    for (int r = 0; r < a.nr; ++r) {
+      double c = 1.0;
+      for (int h = 0; h < a.lev_nf[r]; ++h, ++f) {
+        c *= a.Delta[f];
+        tau[f] = c;
+      }
+    }
+  }
+  for (int c = t; c < nc; c += 64) {  // Mu_j = Gamma Tr_j^T   (:62)
+    double m = 0.0;
+    for (int q = 0; q < a.nt; ++q) m += a.Gamma[c + nc * q] * a.Tr[j + (size_t)a.ns_loc * q];
+    mu[c] = m;
+  }
+  __syncthreads();
+  const double isig = a.iSigma[j];
+  const int nai = a.na_index ? a.na_index[j] : -1;
+  const double* Gj = nai >= 0 ? a.Gna + (size_t)nai * a.Kmax * a.Kmax : a.G;
+  for (int p = t; p < K * K; p += 64) {  // iU = P + XEtaTXEta * iSigma[j]   (:83-92)
+    const int r = p % K, c = p / K;
+    double v = isig * Gj[r + a.Kmax * c];
+    if (r < nc && c < nc)
+      v += a.iV[r + nc * c];
+    else if (r == c)
+      v += a.Psi[(r - nc) + (size_t)a.NF * j] * tau[r - nc];
+    A[p] = v;
+  }
+  for (int r = t; r < K; r += 64) {  // rhs = P Mu + isXTS   (:66, :100)
+    double v = isig * a.XZ[r + (size_t)K * j];
+    if (r < nc) {
+      double pm = 0.0;
+      for (int c = 0; c < nc; ++c) pm += a.iV[r + nc * c] * mu[c];
+      v += pm;
+    }
+    rhs[r] = v;
+  }
+  __syncthreads();
+  if (a.dbg_prec)
+    for (int p = t; p < K * K; p += 64) a.dbg_prec[(size_t)j * K * K + p] = A[p];
+  wg_chol(A, K, K, flag);                 // RiU = chol(iU)  (:98)
+  wg_forward(A, K, K, rhs);               // y = L^-1 rhs
+  for (int r = t; r < K; r += 64) {
+    const double xi = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)(a.sp0 + j), (uint32_t)r, S_BETALAMBDA, a.iter);
+    rhs[r] += xi;
+  }
+  __syncthreads();
+  wg_backward_t(A, K, K, rhs);            // L^-T (y + xi) = m + backsolve(RiU, xi)  (:101)
+  for (int r = t; r < K; r += 64) a.BL[r + (size_t)K * j] = rhs[r];
+}
+
+void launch_beta_lambda(State& s, uint32_t iter) {
+  if (!s.zt_valid) launch_zt_refresh(s);
+  if (s.n_na_cols > 0) {
+    EtaView ev = make_view(s);
+    gram_na_kernel<<<s.n_na_cols, 256, 0, s.stream>>>(ev, s.K, s.Kmax, s.na_cols, s.Ycode, s.Gna);
+  }
+  BLArgs a{};
+  a.K = s.K;
+  a.Kmax = s.Kmax;
+  a.nc = s.nc;
+  a.nt = s.nt;
+  a.nr = s.nr;
+  a.NF = s.NF;
+  a.ns_loc = s.nsl;
+  a.ns_glob = s.ns;
+  a.sp0 = s.sp0;
+  a.G = s.G;
+  a.Gna = s.Gna;
+  a.na_index = s.n_na_cols > 0 ? s.na_index : nullptr;
+  a.XZ = s.XZ;
+  a.iV = s.iV;
+  a.Gamma = s.Gamma;
+  a.Tr = s.Tr;
+  a.Psi = s.Psi;
+  a.Delta = s.Delta;
+  a.iSigma = s.iSigma;
+  for (int r = 0; r < s.nr; ++r) a.lev_nf[r] = s.lev[r].nf;
+  a.BL = s.BL;
+  a.dbg_prec = s.dbg_prec;
+  a.key = s.key;
+  a.iter = iter;
+  a.noise_zero = s.noise_mode;
+  const size_t smem = ((size_t)s.K * s.K + s.K + s.NF + 1 + s.nc + 1) * sizeof(double) + 16;
+  beta_lambda_kernel<<<s.nsl, 64, smem, s.stream>>>(a);
+  HIP_OK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// Species-parallel partial sums for updateGammaV (R/updateGammaV.R:16-18,30):
+//   A = E E^T (E = Beta - Gamma Tr^T) and BTr = Beta Tr.
+// ---------------------------------------------------------------------------
+constexpr int GV_PARTS = 32;
+
+__global__ __launch_bounds__(256) void gammav_partial_kernel(const double* BL, int K, int nc, int nt, int ns_loc,
+                                                             const double* Gamma, const double* Tr,
+                                                             double* part) {
+  // part[b][0 : nc*nc] = A partial, part[b][nc*nc : nc*nc + nc*nt] = BTr partial
+  const int b = blockIdx.x;
+  const int per = (ns_loc + gridDim.x - 1) / gridDim.x;
+  const int ja = b * per, jb = min(ns_loc, ja + per);
+  const int nA = nc * nc, nB = nc * nt;
+  double* out = part + (size_t)b * (nA + nB);
+  for (int p = threadIdx.x; p < nA + nB; p += blockDim.x) {
+    double s = 0.0;
+    if (p < nA) {
+      const int c1 = p % nc, c2 = p / nc;
+      for (int j = ja; j < jb; ++j) {
+        double e1 = BL[c1 + (size_t)K * j], e2 = BL[c2 + (size_t)K * j];
+        for (int q = 0; q < nt; ++q) {
+          const double tr = Tr[j + (size_t)ns_loc * q];
+          e1 -= Gamma[c1 + nc * q] * tr;
+          e2 -= Gamma[c2 + nc * q] * tr;
+        }
+        s += e1 * e2;
+      }
+    } else {
+      const int pp = p - nA, c = pp % nc, q = pp / nc;
+      for (int j = ja; j < jb; ++j) s += BL[c + (size_t)K * j] * Tr[j + (size_t)ns_loc * q];
+    }
+    out[p] = s;
+  }
+}
+
+// Bartlett draw of MCMCpack::rwish(v, S): W = (Zb CC)^T (Zb CC), CC = chol(S) upper,
+// Zb upper-triangular, diag sqrt(chisq(v - i)), off-diagonal N(0,1).
+// Sl holds lower L = CC^T (n x n, ld n); result into W; T scratch n*n.
+__device__ void wg_rwish(const double* Sl, int n, double v, double* W, double* T, Key key, uint32_t s_diag,
+                         uint32_t s_off, uint32_t iter, int noise_zero) {
+  const int t = threadIdx.x;
+  // T = Zb * CC = Zb * L^T : T[i][c] = sum_{k>=i} Zb[i][k] * L[c][k]
+  for (int p = t; p < n * n; p += blockDim.x) {
+    const int i = p % n, c = p / n;
+    double s = 0.0;
+    for (int k = i; k < n; ++k) {
+      double z;
+      if (k == i)
+        z = sqrt(2.0 * gamma_std(key, (uint32_t)i, s_diag, iter, 0.5 * (v - i)));
+      else
+        z = noise_zero ? 0.0 : normal(key, (uint32_t)(i + n * k), 0, s_off, iter);
+      if (c >= k) s += z * Sl[c + n * k];
+    }
+    T[i + n * c] = s;
+  }
+  __syncthreads();
+  wg_gemm(n, n, n, 1.0, T, n, true, T, n, false, 0.0, W, n);
+}
+
+struct GVArgs {
+  int nc, nt, ns_glob, nparts;
+  const double* part;  // summed partials (already all-reduced in sharded mode)
+  const double* V0;
+  double f0;
+  const double* iUGamma;
+  const double* mGamma;
+  const double* TT;
+  double* iV;
+  double* Gamma;
+  double* scratch;
+  Key key;
+  uint32_t iter;
+  int noise_zero;
+  int* fail;
+};
+
+__global__ __launch_bounds__(256) void gammav_final_kernel(GVArgs a) {
+  const int nc = a.nc, nt = a.nt, N = nc * nt, t = threadIdx.x;
+  __shared__ int flag;
+  double* A = a.scratch;            // nc*nc
+  double* Vn = A + nc * nc;         // nc*nc
+  double* W = Vn + nc * nc;         // nc*nc scratch
+  double* T = W + nc * nc;          // nc*nc scratch
+  double* BTr = T + nc * nc;        // nc*nt
+  double* Pm = BTr + nc * nt;       // N*N
+  double* rhs = Pm + N * N;         // N
+  const int nA = nc * nc, nB = nc * nt;
+  for (int p = t; p < nA + nB; p += blockDim.x) {
+    double s = 0.0;
+    for (int b = 0; b < a.nparts; ++b) s += a.part[(size_t)b * (nA + nB) + p];
+    if (p < nA)
+      A[p] = s + a.V0[p];                        // A + V0   (:19)
+    else
+      BTr[p - nA] = s;
+  }
+  __syncthreads();
+  if (!wg_chol(A, nc, nc, &flag)) {
+    if (t == 0) *a.fail = 1;
+  }
+  wg_chol2inv(A, nc, nc, Vn, nc, W);             // Vn = chol2inv(chol(A+V0))  (:19)
+  wg_copy(A, Vn, nc * nc);
+  wg_chol(A, nc, nc, &flag);                      // CC = chol(Vn)
+  wg_lower_only(A, nc, nc);
+  wg_rwish(A, nc, a.f0 + a.ns_glob, a.iV, T, a.key, S_WISHART_DIAG, S_WISHART_OFF, a.iter, a.noise_zero);  // (:20)
+  // Gamma | iV: prec = iUGamma + kron(Tr'Tr, iV); rhs = iUGamma mGamma + vec(iV B Tr)   (:29-31)
+  for (int p = t; p < N * N; p += blockDim.x) {
+    const int r = p % N, c = p / N;
+    const int c1 = r % nc, t1 = r / nc, c2 = c % nc, t2 = c / nc;
+    Pm[p] = a.iUGamma[p] + a.TT[t1 + nt * t2] * a.iV[c1 + nc * c2];
+  }
+  for (int r = t; r < N; r += blockDim.x) {
+    const int c1 = r % nc, t1 = r / nc;
+    double v = 0.0;
+    for (int q = 0; q < N; ++q) v += a.iUGamma[r + N * q] * a.mGamma[q];
+    for (int c2 = 0; c2 < nc; ++c2) v += a.iV[c1 + nc * c2] * BTr[c2 + nc * t1];
+    rhs[r] = v;
+  }
+  __syncthreads();
+  wg_chol(Pm, N, N, &flag);
+  wg_forward(Pm, N, N, rhs);
+  for (int r = t; r < N; r += blockDim.x)
+    rhs[r] += a.noise_zero ? 0.0 : normal(a.key, (uint32_t)r, 0, S_GAMMAV, a.iter);
+  __syncthreads();
+  wg_backward_t(Pm, N, N, rhs);
+  for (int r = t; r < N; r += blockDim.x) a.Gamma[r] = rhs[r];
+}
+
+void allreduce_sum(State& s, double* buf, size_t n);  // capi.cpp
+
+void launch_gamma_v(State& s, uint32_t iter) {
+  const int nparts = std::min(GV_PARTS, std::max(1, s.nsl));
+  double* part = s.ABpart;
+  gammav_partial_kernel<<<nparts, 256, 0, s.stream>>>(s.BL, s.K, s.nc, s.nt, s.nsl, s.Gamma, s.Tr, part);
+  HIP_OK(hipGetLastError());
+  int np = nparts;
+  if (s.nranks > 1) {
+    const int64_t n = (int64_t)s.nc * s.nc + (int64_t)s.nc * s.nt;
+    slab_sum_kernel<<<grid_for(n), 256, 0, s.stream>>>(part, s.allreduce_buf, n, nparts, n);
+    allreduce_sum(s, s.allreduce_buf, n);
+    part = s.allreduce_buf;
+    np = 1;
+  }
+  GVArgs a{};
+  a.nc = s.nc;
+  a.nt = s.nt;
+  a.ns_glob = s.ns;
+  a.nparts = np;
+  a.part = part;
+  a.V0 = s.V0;
+  a.f0 = s.f0;
+  a.iUGamma = s.iUGamma;
+  a.mGamma = s.mGamma;
+  a.TT = s.TT;
+  a.iV = s.iV;
+  a.Gamma = s.Gamma;
+  a.scratch = s.scratch;
+  a.key = s.key;
+  a.iter = iter;
+  a.noise_zero = s.noise_mode;
+  a.fail = s.dev_flags;
+  gammav_final_kernel<<<1, 256, 0, s.stream>>>(a);
+  HIP_OK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// updateGamma2 (R/updateGamma2.R:6-60): Gamma with Beta integrated out.
+// Stage 1 (species-parallel): XZT = X^T S Tr with S = Z - sum_r LRan_r, via
+//   X^T Z Tr = XZ[0:nc,:] Tr (no NA)  and  X^T Eta_r[Pi] (Lambda_r Tr)  from G.
+// Stage 2: single-workgroup dense algebra.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void gamma2_partial_kernel(const double* XZ, const double* BL, int K, int nc,
+                                                             int NF, int nt, int ns_loc, const double* Tr,
+                                                             double* part) {
+  // part[b] = [ XZ[0:nc,:] Tr (nc*nt) | Lambda_all Tr (NF*nt) ]
+  const int b = blockIdx.x;
+  const int per = (ns_loc + gridDim.x - 1) / gridDim.x;
+  const int ja = b * per, jb = min(ns_loc, ja + per);
+  const int n1 = nc * nt, n2 = NF * nt;
+  double* out = part + (size_t)b * (n1 + n2);
+  for (int p = threadIdx.x; p < n1 + n2; p += blockDim.x) {
+    double s = 0.0;
+    if (p < n1) {
+      const int c = p % nc, q = p / nc;
+      for (int j = ja; j < jb; ++j) s += XZ[c + (size_t)K * j] * Tr[j + (size_t)ns_loc * q];
+    } else {
+      const int pp = p - n1, f = pp % NF, q = pp / NF;
+      for (int j = ja; j < jb; ++j) s += BL[nc + f + (size_t)K * j] * Tr[j + (size_t)ns_loc * q];
+    }
+    out[p] = s;
+  }
+}
+
+// X^T ZTr (nc x nt) for models with NA (where XZ is masked): reduction over sites
+__global__ __launch_bounds__(256) void xt_ztr_kernel(const double* X, const double* ZTr, int ny, int nc, int nt,
+                                                     double* out) {
+  __shared__ double red[256];
+  const int p = blockIdx.x, c = p % nc, q = p / nc;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < ny; i += 256) s += X[i + (size_t)ny * c] * ZTr[i + (size_t)ny * q];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[p] = red[0];
+}
+
+struct G2Args {
+  int nc, nt, K, Kmax, NF, nr, nparts, ns_loc, use_xtztr;
+  int lev_nf[HMSC_MAX_LEVELS];
+  const double* part;
+  const double* xtztr;
+  const double* G;
+  const double* iV;
+  const double* XX;
+  const double* TT;
+  const double* iV0;
+  const double* V0g;
+  const double* V0gXXV0g;
+  const double* iSigma;
+  double* Gamma;
+  double* scratch;
+  Key key;
+  uint32_t iter;
+  int noise_zero;
+  int check_isigma;
+};
+
+__global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
+  const int nc = a.nc, nt = a.nt, N = nc * nt, t = threadIdx.x;
+  __shared__ int flag;
+  __shared__ int all_one;
+  if (t == 0) all_one = 1;
+  __syncthreads();
+  if (a.check_isigma)
+    for (int j = t; j < a.ns_loc; j += blockDim.x)
+      if (a.iSigma[j] != 1.0) all_one = 0;  // acts only if all(iSigma == 1)  (:36)
+  __syncthreads();
+  if (!all_one) return;
+  double* S0 = a.scratch;             // XZT  nc*nt
+  double* LTr = S0 + nc * nt;         // NF*nt
+  double* iP = LTr + a.NF * nt;       // nc*nc
+  double* LiP = iP + nc * nc;         // nc*nc
+  double* W = LiP + nc * nc;          // nc*nc
+  double* T1 = W + nc * nc;           // nc*nc
+  double* M1 = T1 + nc * nc;          // nc*nc
+  double* Rm = M1 + nc * nc;          // N*N
+  double* WN = Rm + N * N;            // N*N
+  double* LR = WN + N * N;            // N*N
+  double* tmp = LR + N * N;           // N*N
+  double* Sg = tmp + N * N;           // N*N
+  double* iPXZT = Sg + N * N;         // nc*nt
+  double* v1 = iPXZT + nc * nt;       // N
+  double* v2 = v1 + N;                // N
+  double* muG = v2 + N;               // N
+  double* t2 = muG + N;               // nc*nc
+  double* W1 = t2 + nc * nc;          // nc*nc
+  const int n1 = nc * nt, n2 = a.NF * nt;
+  // reduce species partials
+  for (int p = t; p < n1 + n2; p += blockDim.x) {
+    double s = 0.0;
+    for (int b = 0; b < a.nparts; ++b) s += a.part[(size_t)b * (n1 + n2) + p];
+    if (p < n1)
+      S0[p] = a.use_xtztr ? a.xtztr[p] : s;
+    else
+      LTr[p - n1] = s;
+  }
+  __syncthreads();
+  // XZT -= sum_r (X^T Eta_r[Pi]) (Lambda_r Tr): X^T Eta block of G = rows [0,nc), cols [nc, K)
+  for (int p = t; p < nc * nt; p += blockDim.x) {
+    const int c = p % nc, q = p / nc;
+    double s = 0.0;
+    for (int f = 0; f < a.NF; ++f) s += a.G[c + a.Kmax * (nc + f)] * LTr[f + a.NF * q];
+    S0[p] -= s;
+  }
+  // iP = inv(iV + XX); LiP = chol(iP) lower
+  for (int p = t; p < nc * nc; p += blockDim.x) W[p] = a.iV[p] + a.XX[p];
+  __syncthreads();
+  wg_chol(W, nc, nc, &flag);
+  wg_chol2inv(W, nc, nc, iP, nc, T1);
+  wg_copy(LiP, iP, nc * nc);
+  wg_chol(LiP, nc, nc, &flag);
+  wg_lower_only(LiP, nc, nc);
+  // M1 = iV - (iV LiP)(iV LiP)^T
+  wg_gemm(nc, nc, nc, 1.0, a.iV, nc, false, LiP, nc, false, 0.0, T1, nc);
+  wg_gemm(nc, nc, nc, -1.0, T1, nc, false, T1, nc, true, 0.0, M1, nc);
+  for (int p = t; p < nc * nc; p += blockDim.x) M1[p] += a.iV[p];
+  __syncthreads();
+  // Rm = inv(kron(I_nt, iV0) + kron(TT, M1)); LR = chol(Rm) lower   (:44-45)
+  for (int p = t; p < N * N; p += blockDim.x) {
+    const int r = p % N, c = p / N, c1 = r % nc, q1 = r / nc, c2 = c % nc, q2 = c / nc;
+    WN[p] = (q1 == q2 ? a.iV0[c1 + nc * c2] : 0.0) + a.TT[q1 + nt * q2] * M1[c1 + nc * c2];
+  }
+  __syncthreads();
+  wg_chol(WN, N, N, &flag);
+  wg_chol2inv(WN, N, N, Rm, N, tmp);
+  wg_copy(LR, Rm, N * N);
+  wg_chol(LR, N, N, &flag);
+  wg_lower_only(LR, N, N);
+  // iPXZT = iP XZT
+  wg_gemm(nc, nt, nc, 1.0, iP, nc, false, S0, nc, false, 0.0, iPXZT, nc);
+  // W1 = V0g XX iP iV ; tmp = kron(TT, W1)
+  wg_gemm(nc, nc, nc, 1.0, a.V0g, nc, false, a.XX, nc, false, 0.0, T1, nc);
+  wg_gemm(nc, nc, nc, 1.0, T1, nc, false, iP, nc, false, 0.0, t2, nc);
+  wg_gemm(nc, nc, nc, 1.0, t2, nc, false, a.iV, nc, false, 0.0, W1, nc);
+  for (int p = t; p < N * N; p += blockDim.x) {
+    const int r = p % N, c = p / N, c1 = r % nc, q1 = r / nc, c2 = c % nc, q2 = c / nc;
+    tmp[p] = a.TT[q1 + nt * q2] * W1[c1 + nc * c2];
+  }
+  __syncthreads();
+  // muG = vec(V0g (XZT - XX iPXZT)) - tmp Rm vec(iV iPXZT)   (:49)
+  wg_gemm(nc, nt, nc, -1.0, a.XX, nc, false, iPXZT, nc, false, 0.0, v1, nc);
+  for (int p = t; p < nc * nt; p += blockDim.x) v1[p] += S0[p];
+  __syncthreads();
+  wg_gemm(nc, nt, nc, 1.0, a.V0g, nc, false, v1, nc, false, 0.0, muG, nc);
+  wg_gemm(nc, nt, nc, 1.0, a.iV, nc, false, iPXZT, nc, false, 0.0, v1, nc);
+  wg_gemm(N, 1, N, 1.0, Rm, N, false, v1, N, false, 0.0, v2, N);
+  wg_gemm(N, 1, N, -1.0, tmp, N, false, v2, N, false, 1.0, muG, N);
+  // SigmaG = kron(I, V0g) - kron(TT, V0g XX V0g - t2 t2^T) + (tmp LR)(tmp LR)^T, t2 = V0g XX LiP  (:50)
+  wg_gemm(nc, nc, nc, 1.0, a.V0g, nc, false, a.XX, nc, false, 0.0, T1, nc);
+  wg_gemm(nc, nc, nc, 1.0, T1, nc, false, LiP, nc, false, 0.0, t2, nc);
+  wg_gemm(nc, nc, nc, -1.0, t2, nc, false, t2, nc, true, 0.0, M1, nc);
+  for (int p = t; p < nc * nc; p += blockDim.x) M1[p] += a.V0gXXV0g[p];
+  __syncthreads();
+  wg_gemm(N, N, N, 1.0, tmp, N, false, LR, N, false, 0.0, WN, N);
+  wg_gemm(N, N, N, 1.0, WN, N, false, WN, N, true, 0.0, Sg, N);
+  for (int p = t; p < N * N; p += blockDim.x) {
+    const int r = p % N, c = p / N, c1 = r % nc, q1 = r / nc, c2 = c % nc, q2 = c / nc;
+    Sg[p] += (q1 == q2 ? a.V0g[c1 + nc * c2] : 0.0) - a.TT[q1 + nt * q2] * M1[c1 + nc * c2];
+  }
+  __syncthreads();
+  wg_chol(Sg, N, N, &flag);                // LSigmaG = t(chol(SigmaG))   (:52)
+  for (int r = t; r < N; r += blockDim.x) {
+    double v = muG[r];
+    if (!a.noise_zero)
+      for (int c = 0; c <= r; ++c) v += Sg[r + N * c] * normal(a.key, (uint32_t)c, 0, S_GAMMA2, a.iter);
+    a.Gamma[r] = v;                        // (:53-54)
+  }
+}
+
+void launch_gamma2(State& s, uint32_t iter) {
+  if (!s.zt_valid) launch_zt_refresh(s);
+  const int nparts = std::min(GV_PARTS, std::max(1, s.nsl));
+  gamma2_partial_kernel<<<nparts, 256, 0, s.stream>>>(s.XZ, s.BL, s.K, s.nc, s.NF, s.nt, s.nsl, s.Tr, s.ABpart);
+  HIP_OK(hipGetLastError());
+  const int n1 = s.nc * s.nt, n2 = s.NF * s.nt;
+  double* part = s.ABpart;
+  int np = nparts;
+  double* xtztr = s.allreduce_buf + (n1 + n2);
+  if (s.has_na) xt_ztr_kernel<<<n1, 256, 0, s.stream>>>(s.X, s.ZTr, s.ny, s.nc, s.nt, xtztr);
+  if (s.nranks > 1) {
+    slab_sum_kernel<<<grid_for(n1 + n2), 256, 0, s.stream>>>(part, s.allreduce_buf, n1 + n2, nparts, n1 + n2);
+    allreduce_sum(s, s.allreduce_buf, s.has_na ? 2 * n1 + n2 : n1 + n2);
+    part = s.allreduce_buf;
+    np = 1;
+  }
+  G2Args a{};
+  a.nc = s.nc;
+  a.nt = s.nt;
+  a.K = s.K;
+  a.Kmax = s.Kmax;
+  a.NF = s.NF;
+  a.nr = s.nr;
+  a.nparts = np;
+  a.ns_loc = s.nsl;
+  a.use_xtztr = s.has_na ? 1 : 0;
+  a.part = part;
+  a.xtztr = xtztr;
+  a.G = s.G;
+  a.iV = s.iV;
+  a.XX = s.XX;
+  a.TT = s.TT;
+  a.iV0 = s.iV0;
+  a.V0g = s.V0g;
+  a.V0gXXV0g = s.V0gXXV0g;
+  a.iSigma = s.iSigma;
+  a.Gamma = s.Gamma;
+  a.scratch = s.scratch;
+  a.key = s.key;
+  a.iter = iter;
+  a.noise_zero = s.noise_mode;
+  a.check_isigma = s.nranks == 1 ? 1 : 0;
+  gamma2_final_kernel<<<1, 256, 0, s.stream>>>(a);
+  HIP_OK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// updateLambdaPriors (R/updateLambdaPriors.R:3-53, matrix branch :21-33)
+// ---------------------------------------------------------------------------
+struct LPArgs {
+  int NF, K, nc, nr, ns_loc, sp0;
+  int lev_nf[HMSC_MAX_LEVELS];
+  double nu[HMSC_MAX_LEVELS], a1[HMSC_MAX_LEVELS], b1[HMSC_MAX_LEVELS], a2[HMSC_MAX_LEVELS],
+      b2[HMSC_MAX_LEVELS];
+  const double* BL;
+  double* Psi;
+  double* Delta;
+  double* rs_part;  // [block][NF]
+  int ns_glob;
+  Key key;
+  uint32_t iter;
+};
+
+__global__ __launch_bounds__(256) void psi_kernel(LPArgs a) {
+  // grid over species columns; each block handles a contiguous species range
+  __shared__ double sM[256];
+  __shared__ double sTau[64];
+  __shared__ int sLev[64], sH[64];
+  const int t = threadIdx.x;
+  if (t == 0) {
+    int f = 0;
+    for (int r = 0; r < a.nr; ++r) {
+      double c = 1.0;
+      for (int h = 0; h < a.lev_nf[r]; ++h, ++f) {
+        c *= a.Delta[f];
+        sTau[f] = c;       // tau = cumprod(delta)  (:17)
+        sLev[f] = r;
+        sH[f] = h;
+      }
+    }
+  }
+  __syncthreads();
+  const int NF = a.NF;
+  const int per = (a.ns_loc + gridDim.x - 1) / gridDim.x;
+  const int ja = blockIdx.x * per, jb = min(a.ns_loc, ja + per);
+  const int nelem = (jb > ja ? jb - ja : 0) * NF;
+  double* rs = a.rs_part + (size_t)blockIdx.x * NF;
+  double acc = 0.0;  // thread t < NF accumulates row t in fixed order
+  for (int base = 0; base < nelem; base += 256) {
+    const int p = base + t;
+    double m = 0.0;
+    if (p < nelem) {
+      const int f = p % NF, j = ja + p / NF;
+      const int r = sLev[f], h = sH[f];
+      const double lam = a.BL[a.nc + f + (size_t)a.K * j];
+      const double lam2 = lam * lam;
+      const double shape = a.nu[r] / 2 + 0.5;
+      const double rate = a.nu[r] / 2 + 0.5 * lam2 * sTau[f];            // (:22)
+      const uint32_t idx = (uint32_t)(h + a.lev_nf[r] * (a.sp0 + j));
+      const double psi = gamma_std(a.key, idx, S_PSI + LEVEL_STRIDE * r, a.iter, shape) / rate;  // (:23)
+      a.Psi[f + (size_t)NF * j] = psi;
+      m = psi * lam2;                                                     // M = psi*lambda^2 (:24)
+    }
+    sM[t] = m;
+    __syncthreads();
+    if (t < NF) {
+      const int q0 = (t - base % NF + NF) % NF;  // first q with (base + q) % NF == t
+      for (int q = q0; q < 256 && base + q < nelem; q += NF) acc += sM[q];
+    }
+    __syncthreads();
+  }
+  if (t < NF) rs[t] = acc;
+}
+
+__global__ void delta_kernel(LPArgs a, const double* rs_part, int nparts) {
+  // one thread per level: the sequential delta chain (:25-32)
+  const int r = threadIdx.x;
+  if (r >= a.nr) return;
+  const int nf = a.lev_nf[r];
+  int f0 = 0;
+  for (int q = 0; q < r; ++q) f0 += a.lev_nf[q];
+  double rs[64], delta[64];
+  for (int h = 0; h < nf; ++h) {
+    double s = 0.0;
+    for (int b = 0; b < nparts; ++b) s += rs_part[(size_t)b * a.NF + f0 + h];
+    rs[h] = s;
+    delta[h] = a.Delta[f0 + h];
+  }
+  const uint32_t stream = S_DELTA + LEVEL_STRIDE * r;
+  const double ns = (double)a.ns_glob;
+  double tau = 1.0, st = 0.0;
+  for (int h = 0; h < nf; ++h) {
+    tau *= delta[h];
+    st += tau * rs[h];
+  }
+  {
+    const double ad = a.a1[r] + 0.5 * ns * nf;
+    const double bd = a.b1[r] + 0.5 * st / delta[0];
+    delta[0] = gamma_std(a.key, 0, stream, a.iter, ad) / bd;
+  }
+  for (int h = 1; h < nf; ++h) {
+    double c = 1.0, s = 0.0;
+    for (int q = 0; q < nf; ++q) {
+      c *= delta[q];
+      if (q >= h) s += c * rs[q];
+    }
+    const double ad = a.a2[r] + 0.5 * ns * (nf - h);
+    const double bd = a.b2[r] + 0.5 * s / delta[h];
+    delta[h] = gamma_std(a.key, (uint32_t)h, stream, a.iter, ad) / bd;
+  }
+  for (int h = 0; h < nf; ++h) a.Delta[f0 + h] = delta[h];
+}
+
+constexpr int LP_PARTS = 64;
+
+void launch_lambda_priors(State& s, uint32_t iter) {
+  if (s.nr == 0) return;
+  HMSC_REQUIRE(s.NF <= 64, "updateLambdaPriors: sum(nf) must be <= 64 in this build");
+  LPArgs a{};
+  a.NF = s.NF;
+  a.K = s.K;
+  a.nc = s.nc;
+  a.nr = s.nr;
+  a.ns_loc = s.nsl;
+  a.sp0 = s.sp0;
+  a.ns_glob = s.ns;
+  for (int r = 0; r < s.nr; ++r) {
+    a.lev_nf[r] = s.lev[r].nf;
+    a.nu[r] = s.lev[r].nu;
+    a.a1[r] = s.lev[r].a1;
+    a.b1[r] = s.lev[r].b1;
+    a.a2[r] = s.lev[r].a2;
+    a.b2[r] = s.lev[r].b2;
+  }
+  a.BL = s.BL;
+  a.Psi = s.Psi;
+  a.Delta = s.Delta;
+  a.rs_part = s.psi_rs;
+  a.key = s.key;
+  a.iter = iter;
+  const int nparts = std::min(LP_PARTS, std::max(1, s.nsl));
+  psi_kernel<<<nparts, 256, 0, s.stream>>>(a);
+  HIP_OK(hipGetLastError());
+  const double* rs = s.psi_rs;
+  int np = nparts;
+  if (s.nranks > 1) {
+    slab_sum_kernel<<<1, 64, 0, s.stream>>>(s.psi_rs, s.allreduce_buf, s.NF, nparts, s.NF);
+    allreduce_sum(s, s.allreduce_buf, s.NF);
+    rs = s.allreduce_buf;
+    np = 1;
+  }
+  delta_kernel<<<1, 64, 0, s.stream>>>(a, rs, np);
+  HIP_OK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// updateEta, non-spatial levels (R/updateEta.R:42-92).
+//   ZL  = Z (Lambda_all diag(iSigma))^T      (ny x NF; the one HBM pass over Z)
+//   CR  = BL diag(iSigma) Lambda_all^T       (K x NF; small)
+//   per level r, per unit q:
+//     Q_q = I + n_q Lambda_r diag(iSigma) Lambda_r^T                         (:45,52,76)
+//     b_q = sum_{i in q} [ ZL_i,r - sum_{k not in level r} XEta_ik CR_k,r ]  (= S_i Lambda~^T, :55,79)
+//     eta_q = Q_q^-1 b_q + R_q^-1 xi                                          (:56,90)
+// ---------------------------------------------------------------------------
+template <int NFB>
+__global__ __launch_bounds__(256) void zl_kernel(const double* __restrict__ Z, const double* __restrict__ BL,
+                                                 const double* __restrict__ iSigma, int ny, int ns_loc, int K,
+                                                 int nc, int NF, int split, double* __restrict__ ZL_part) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int i = blockIdx.x * 64 + lane;
+  const int per = (ns_loc + split - 1) / split;
+  const int ja = blockIdx.y * per, jb = min(ns_loc, ja + per);
+  const int nj = jb > ja ? jb - ja : 0;
+  double* sL = smem;  // [jj][NF]
+  for (int p = t; p < nj * NF; p += 256) {
+    const int jj = p / NF, f = p % NF, j = ja + jj;
+    sL[p] = BL[nc + f + (size_t)K * j] * iSigma[j];
+  }
+  __syncthreads();
+  double acc[NFB];
+#pragma unroll
+  for (int f = 0; f < NFB; ++f) acc[f] = 0.0;
+  if (i < ny) {
+    int jj = w;
+    for (; jj + 12 < nj; jj += 16) {
+      const double z0 = Z[i + (size_t)ny * (ja + jj)];
+      const double z1 = Z[i + (size_t)ny * (ja + jj + 4)];
+      const double z2 = Z[i + (size_t)ny * (ja + jj + 8)];
+      const double z3 = Z[i + (size_t)ny * (ja + jj + 12)];
+      const double* l0 = sL + jj * NF;
+      const double* l1 = l0 + 4 * NF;
+      const double* l2 = l0 + 8 * NF;
+      const double* l3 = l0 + 12 * NF;
+#pragma unroll
+      for (int f = 0; f < NFB; ++f)
+        if (f < NF) acc[f] = fma(z3, l3[f], fma(z2, l2[f], fma(z1, l1[f], fma(z0, l0[f], acc[f]))));
+    }
+    for (; jj < nj; jj += 4) {
+      const double z0 = Z[i + (size_t)ny * (ja + jj)];
+      const double* l0 = sL + jj * NF;
+#pragma unroll
+      for (int f = 0; f < NFB; ++f)
+        if (f < NF) acc[f] = fma(z0, l0[f], acc[f]);
+    }
+  }
+  __syncthreads();
+  double* sR = smem;  // reuse: [w][f][lane]
+#pragma unroll
+  for (int f = 0; f < NFB; ++f)
+    if (f < NF) sR[(w * NF + f) * 64 + lane] = acc[f];
+  __syncthreads();
+  for (int p = t; p < NF * 64; p += 256) {
+    const int f = p / 64, l = p % 64, ii = blockIdx.x * 64 + l;
+    const double v = sR[(0 * NF + f) * 64 + l] + sR[(1 * NF + f) * 64 + l] + sR[(2 * NF + f) * 64 + l] +
+                     sR[(3 * NF + f) * 64 + l];
+    if (ii < ny) ZL_part[(size_t)blockIdx.y * ny * NF + (size_t)ii * NF + f] = v;
+  }
+}
+
+__global__ __launch_bounds__(64) void cr_kernel(const double* BL, const double* iSigma, int K, int nc, int NF,
+                                                int ns_loc, double* CR, int ldcr) {
+  // CR[k, f] = sum_j BL[k, j] iSigma[j] BL[nc+f, j]   one wave per (k, f)
+  const int k = blockIdx.x, f = blockIdx.y, t = threadIdx.x;
+  double s = 0.0;
+  for (int j = t; j < ns_loc; j += 64) s += BL[k + (size_t)K * j] * iSigma[j] * BL[nc + f + (size_t)K * j];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (t == 0) CR[k + (size_t)ldcr * f] = s;
+}
+
+struct EtaArgs {
+  EtaView ev;
+  int r, nf, np, K, nc, NF, foff, loff, ldcr, nzl;
+  const double* ZL;  // ny x NF (row-major per site), or partials [nzl][ny*NF]
+  const double* CR;  // K x NF (ld ldcr)
+  const int* unit_ptr;
+  const int* unit_rows;
+  const int8_t* row_na;   // ny (1 if any NA in row) or null
+  const double* Mrow;     // per-row masked precision (nf*nf) for NA rows, indexed by row_slot
+  const double* brow;     // per-row masked numerator (nf) for NA rows
+  const int* row_slot;    // ny -> slot or -1
+  double* Eta;            // np x nf
+  Key key;
+  uint32_t iter;
+  int noise_zero;
+};
+
+__global__ __launch_bounds__(64) void eta_unit_kernel(EtaArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int nf = a.nf, t = threadIdx.x, q = blockIdx.x;
+  double* Q = smem;        // nf x nf
+  double* b = Q + nf * nf; // nf
+  int* flag = (int*)(b + nf + 1);
+  const int rb = a.unit_ptr[q], re = a.unit_ptr[q + 1];
+  int n_full = 0;
+  for (int p = rb; p < re; ++p) n_full += (a.row_na && a.row_na[a.unit_rows[p]]) ? 0 : 1;
+  for (int p = t; p < nf * nf; p += 64) {
+    const int r1 = p % nf, c1 = p / nf;
+    double v = (r1 == c1 ? 1.0 : 0.0) + n_full * a.CR[a.loff + r1 + (size_t)a.ldcr * (a.foff + c1)];
+    if (a.row_na)
+      for (int pp = rb; pp < re; ++pp) {
+        const int slot = a.row_slot[a.unit_rows[pp]];
+        if (slot >= 0) v += a.Mrow[(size_t)slot * nf * nf + p];
+      }
+    Q[p] = v;
+  }
+  for (int h = t; h < nf; h += 64) {
+    double v = 0.0;
+    for (int pp = rb; pp < re; ++pp) {
+      const int i = a.unit_rows[pp];
+      const int slot = a.row_na ? a.row_slot[i] : -1;
+      if (slot >= 0) {
+        v += a.brow[(size_t)slot * nf + h];
+        continue;
+      }
+      double zl = 0.0;
+      for (int c = 0; c < a.nzl; ++c) zl += a.ZL[(size_t)c * a.ev.ny * a.NF + (size_t)i * a.NF + a.foff + h];
+      double corr = 0.0;
+      for (int k = 0; k < a.K; ++k) {
+        if (k >= a.loff && k < a.loff + nf) continue;
+        corr += xeta_at(a.ev, i, k) * a.CR[k + (size_t)a.ldcr * (a.foff + h)];
+      }
+      v += zl - corr;
+    }
+    b[h] = v;
+  }
+  __syncthreads();
+  wg_chol(Q, nf, nf, flag);                         // RiV = chol(iV)
+  wg_forward(Q, nf, nf, b);
+  for (int h = t; h < nf; h += 64)
+    b[h] += a.noise_zero ? 0.0 : normal(a.key, (uint32_t)q, (uint32_t)h, S_ETA + LEVEL_STRIDE * a.r, a.iter);
+  __syncthreads();
+  wg_backward_t(Q, nf, nf, b);                      // mu + t(backsolve(RiV, xi))
+  for (int h = t; h < nf; h += 64) a.Eta[q + (size_t)a.np * h] = b[h];
+}
+
+// NA rows (R/updateEta.R:59-70, :80-87): masked per-row precision and numerator
+// with the residual S computed on the fly.  One workgroup per NA row.
+__global__ __launch_bounds__(64) void eta_na_row_kernel(EtaView ev, int r, int nf, int K, int nc, int loff,
+                                                        const int* na_rows, const double* Z, const double* BL,
+                                                        const double* iSigma, const int8_t* Ycode, int ns_loc,
+                                                        double* Mrow, double* brow) {
+  const int slot = blockIdx.x, i = na_rows[slot], t = threadIdx.x, ny = ev.ny;
+  extern __shared__ __attribute__((aligned(16))) double sx[];  // XEta row (K)
+  for (int k = t; k < K; k += 64) sx[k] = xeta_at(ev, i, k);
+  __syncthreads();
+  for (int p = t; p < nf * nf + nf; p += 64) {
+    double s = 0.0;
+    if (p < nf * nf) {
+      const int h1 = p % nf, h2 = p / nf;
+      for (int j = 0; j < ns_loc; ++j)
+        if (Ycode[(size_t)i + (size_t)ny * j] >= 0)
+          s += BL[loff + h1 + (size_t)K * j] * iSigma[j] * BL[loff + h2 + (size_t)K * j];
+      Mrow[(size_t)slot * nf * nf + p] = s;
+    } else {
+      const int h = p - nf * nf;
+      for (int j = 0; j < ns_loc; ++j) {
+        if (Ycode[(size_t)i + (size_t)ny * j] < 0) continue;
+        double l = 0.0;  // L^{(-r)}_ij = XEta_i BL_j excluding level r
+        for (int k = 0; k < K; ++k)
+          if (k < loff || k >= loff + nf) l += sx[k] * BL[k + (size_t)K * j];
+        s += (Z[(size_t)i + (size_t)ny * j] - l) * iSigma[j] * BL[loff + h + (size_t)K * j];
+      }
+      brow[(size_t)slot * nf + h] = s;
+    }
+  }
+}
+
+void launch_eta(State& s, uint32_t iter) {
+  if (s.nr == 0) return;
+  HMSC_REQUIRE(s.NF <= 64, "updateEta: sum(nf) must be <= 64 in this build");
+  for (int r = 0; r < s.nr; ++r)
+    HMSC_REQUIRE(s.lev[r].nf >= 1, "updateEta: a level has zero factors");
+  // ZL over all levels in one pass over Z
+  {
+    dim3 grid((s.ny + 63) / 64, s.zl_split);
+    const int per = (s.nsl + s.zl_split - 1) / s.zl_split;
+    const size_t smem = std::max((size_t)per * s.NF, (size_t)4 * s.NF * 64) * sizeof(double);
+    if (s.NF <= 8)
+      zl_kernel<8><<<grid, 256, smem, s.stream>>>(s.Z, s.BL, s.iSigma, s.ny, s.nsl, s.K, s.nc, s.NF, s.zl_split, s.ZL_part);
+    else if (s.NF <= 16)
+      zl_kernel<16><<<grid, 256, smem, s.stream>>>(s.Z, s.BL, s.iSigma, s.ny, s.nsl, s.K, s.nc, s.NF, s.zl_split, s.ZL_part);
+    else if (s.NF <= 32)
+      zl_kernel<32><<<grid, 256, smem, s.stream>>>(s.Z, s.BL, s.iSigma, s.ny, s.nsl, s.K, s.nc, s.NF, s.zl_split, s.ZL_part);
+    else
+      zl_kernel<64><<<grid, 256, smem, s.stream>>>(s.Z, s.BL, s.iSigma, s.ny, s.nsl, s.K, s.nc, s.NF, s.zl_split, s.ZL_part);
+    HIP_OK(hipGetLastError());
+  }
+  dim3 gcr(s.K, s.NF);
+  cr_kernel<<<gcr, 64, 0, s.stream>>>(s.BL, s.iSigma, s.K, s.nc, s.NF, s.nsl, s.CR, s.Kmax);
+  HIP_OK(hipGetLastError());
+  const double* zl = s.ZL_part;
+  int nzl = s.zl_split;
+  if (s.nranks > 1) {
+    const int64_t nzle = (int64_t)s.ny * s.NF;
+    slab_sum_kernel<<<grid_for(nzle), 256, 0, s.stream>>>(s.ZL_part, s.ZL, nzle, s.zl_split, nzle);
+    allreduce_sum(s, s.ZL, nzle);
+    allreduce_sum(s, s.CR, (size_t)s.Kmax * s.NFmax);
+    zl = s.ZL;
+    nzl = 1;
+  }
+  for (int r = 0; r < s.nr; ++r) {
+    const Level& L = s.lev[r];
+    EtaArgs a{};
+    a.ev = make_view(s);
+    a.r = r;
+    a.nf = L.nf;
+    a.np = L.np;
+    a.K = s.K;
+    a.nc = s.nc;
+    a.NF = s.NF;
+    a.foff = s.foff(r);
+    a.loff = s.loff(r);
+    a.ldcr = s.Kmax;
+    a.nzl = nzl;
+    a.ZL = zl;
+    a.CR = s.CR;
+    a.unit_ptr = L.unit_ptr;
+    a.unit_rows = L.unit_rows;
+    a.Eta = L.Eta;
+    a.key = s.key;
+    a.iter = iter;
+    a.noise_zero = s.noise_mode;
+    if (s.n_na_rows > 0) {
+      HMSC_REQUIRE(s.nranks == 1, "updateEta: NA rows with species sharding not supported");
+      double* Mrow = s.Msmall;
+      double* brow = Mrow + (size_t)s.n_na_rows * L.nf * L.nf;
+      eta_na_row_kernel<<<s.n_na_rows, 64, s.K * sizeof(double), s.stream>>>(
+          a.ev, r, L.nf, s.K, s.nc, a.loff, s.na_rows, s.Z, s.BL, s.iSigma, s.Ycode, s.nsl, Mrow, brow);
+      HIP_OK(hipGetLastError());
+      a.row_na = s.row_na;
+      a.row_slot = s.row_slot;
+      a.Mrow = Mrow;
+      a.brow = brow;
+    }
+    const size_t smem = ((size_t)L.nf * L.nf + L.nf + 2) * sizeof(double);
+    eta_unit_kernel<<<L.np, 64, smem, s.stream>>>(a);
+    HIP_OK(hipGetLastError());
+  }
+  s.zt_valid = false;  // Eta changed: XZ / G are stale until the next updateZ
+}
+
+// ---------------------------------------------------------------------------
+// updateInvSigma (R/updateInvSigma.R:3-43): species with distr[,2] == 1 only.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void inv_sigma_kernel(EtaView ev, int K, const double* BL, const double* Z,
+                                                        const int8_t* Ycode, const int* varest,
+                                                        const double* aSigma, const double* bSigma, int sp0,
+                                                        double* iSigma, Key key, uint32_t iter) {
+  __shared__ double red[256];
+  __shared__ int cnt[256];
+  const int j = blockIdx.x, t = threadIdx.x, ny = ev.ny;
+  if (!varest[j]) return;
+  double ss = 0.0;
+  int n = 0;
+  for (int i = t; i < ny; i += 256) {
+    if (Ycode[(size_t)i + (size_t)ny * j] < 0) continue;
+    double e = 0.0;
+    for (int k = 0; k < K; ++k) e += xeta_at(ev, i, k) * BL[k + (size_t)K * j];
+    const double d = Z[(size_t)i + (size_t)ny * j] - e;
+    ss += d * d;
+    ++n;
+  }
+  red[t] = ss;
+  cnt[t] = n;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) {
+      red[t] += red[t + w];
+      cnt[t] += cnt[t + w];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    const double shape = aSigma[j] + cnt[0] / 2.0;   // (:37-38)
+    const double rate = bSigma[j] + red[0] / 2.0;    // (:39)
+    iSigma[j] = gamma_std(key, (uint32_t)(sp0 + j), S_INVSIGMA, iter, shape) / rate;  // (:40)
+  }
+}
+
+void launch_inv_sigma(State& s, uint32_t iter) {
+  if (!s.any_var) return;
+  inv_sigma_kernel<<<s.nsl, 256, 0, s.stream>>>(make_view(s), s.K, s.BL, s.Z, s.Ycode, s.varest, s.aSigma,
+                                                 s.bSigma, s.sp0, s.iSigma, s.key, iter);
+  HIP_OK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// computeInitialParameters (R/computeInitialParameters.R:17-273), initPar = NULL.
+// ---------------------------------------------------------------------------
+struct InitArgs {
+  int nc, nt, ns_loc, sp0, K, NF, nr;
+  int lev_nf[HMSC_MAX_LEVELS], lev_np[HMSC_MAX_LEVELS];
+  double nu[HMSC_MAX_LEVELS], a1[HMSC_MAX_LEVELS], b1[HMSC_MAX_LEVELS], a2[HMSC_MAX_LEVELS],
+      b2[HMSC_MAX_LEVELS];
+  double* Eta[HMSC_MAX_LEVELS];
+  const double* UGammaL;  // lower chol of UGamma
+  const double* mGamma;
+  const double* V0inv;    // V0^{-1}  (riwish(f0, V0) = solve(rwish(f0, solve(V0))))
+  double f0;
+  const double* Tr;
+  const int* fam;
+  const int* varest;
+  const double* aSigma;
+  const double* bSigma;
+  double* Gamma;
+  double* iV;
+  double* LV;             // lower chol of V (scratch)
+  double* BL;
+  double* Psi;
+  double* Delta;
+  double* iSigma;
+  double* scratch;
+  Key key;
+};
+
+__global__ __launch_bounds__(256) void init_small_kernel(InitArgs a) {
+  const int nc = a.nc, N = nc * a.nt, t = threadIdx.x;
+  __shared__ int flag;
+  double* S = a.scratch;        // nc*nc
+  double* T = S + nc * nc;      // nc*nc
+  double* W = T + nc * nc;      // nc*nc
+  for (int r = t; r < N; r += blockDim.x) {  // Gamma ~ N(mGamma, UGamma)   (:85)
+    double v = a.mGamma[r];
+    for (int c = 0; c <= r; ++c) v += a.UGammaL[r + N * c] * normal(a.key, (uint32_t)c, 0, S_INIT_GAMMA, 0);
+    a.Gamma[r] = v;
+  }
+  wg_copy(S, a.V0inv, nc * nc);
+  wg_chol(S, nc, nc, &flag);
+  wg_lower_only(S, nc, nc);
+  wg_rwish(S, nc, a.f0, a.iV, T, a.key, S_INIT_V_DIAG, S_INIT_V_OFF, 0, 0);   // iV = rwish(f0, V0^-1)  (:91)
+  wg_copy(S, a.iV, nc * nc);
+  wg_chol(S, nc, nc, &flag);
+  wg_chol2inv(S, nc, nc, T, nc, W);          // V = iV^-1
+  wg_copy(a.LV, T, nc * nc);
+  wg_chol(a.LV, nc, nc, &flag);
+  wg_lower_only(a.LV, nc, nc);
+  for (int j = t; j < a.ns_loc; j += blockDim.x) {  // sigma   (:111-126)
+    double sig = 1.0;
+    if (a.varest[j])
+      sig = gamma_std(a.key, (uint32_t)(a.sp0 + j), S_INIT_SIGMA, 0, a.aSigma[j]) / a.bSigma[j];
+    else if (a.fam[j] == 3)
+      sig = 1e-2;
+    a.iSigma[j] = 1.0 / sig;
+  }
+  if (t < a.nr) {  // Delta   (:175)
+    const int r = t;
+    int f0 = 0;
+    for (int q = 0; q < r; ++q) f0 += a.lev_nf[q];
+    const uint32_t st = S_INIT_DELTA + LEVEL_STRIDE * r;
+    for (int h = 0; h < a.lev_nf[r]; ++h) {
+      const double sh = h == 0 ? a.a1[r] : a.a2[r];
+      const double rt = h == 0 ? a.b1[r] : a.b2[r];
+      a.Delta[f0 + h] = gamma_std(a.key, (uint32_t)h, st, 0, sh) / rt;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void init_big_kernel(InitArgs a) {
+  const int nc = a.nc, K = a.K, NF = a.NF;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  // Beta_j ~ N(Gamma Tr_j^T, V)   (:97-101)
+  for (int64_t p = t0; p < (int64_t)nc * a.ns_loc; p += stride) {
+    const int c = (int)(p % nc), j = (int)(p / nc);
+    double mu = 0.0;
+    for (int q = 0; q < a.nt; ++q) mu += a.Gamma[c + nc * q] * a.Tr[j + (size_t)a.ns_loc * q];
+    double v = mu;
+    for (int c2 = 0; c2 <= c; ++c2)
+      v += a.LV[c + nc * c2] * normal(a.key, (uint32_t)(a.sp0 + j), (uint32_t)c2, S_INIT_BETA, 0);
+    a.BL[c + (size_t)K * j] = v;
+  }
+  // Psi, Lambda   (:183, :189-193)
+  for (int64_t p = t0; p < (int64_t)NF * a.ns_loc; p += stride) {
+    const int f = (int)(p % NF), j = (int)(p / NF);
+    int r = 0, h = f, f0 = 0;
+    while (h >= a.lev_nf[r]) {
+      h -= a.lev_nf[r];
+      f0 += a.lev_nf[r];
+      ++r;
+    }
+    double tau = 1.0;
+    for (int q = 0; q <= h; ++q) tau *= a.Delta[f0 + q];
+    const uint32_t idx = (uint32_t)(h + a.lev_nf[r] * (a.sp0 + j));
+    const double psi = gamma_std(a.key, idx, S_INIT_PSI + LEVEL_STRIDE * r, 0, a.nu[r] / 2) / (a.nu[r] / 2);
+    a.Psi[f + (size_t)NF * j] = psi;
+    a.BL[nc + f + (size_t)K * j] = normal(a.key, idx, 0, S_INIT_LAMBDA + LEVEL_STRIDE * r, 0) / sqrt(psi * tau);
+  }
+  // Eta ~ N(0,1)   (:207)
+  for (int r = 0; r < a.nr; ++r) {
+    const int64_t n = (int64_t)a.lev_np[r] * a.lev_nf[r];
+    for (int64_t p = t0; p < n; p += stride) {
+      const int q = (int)(p % a.lev_np[r]), h = (int)(p / a.lev_np[r]);
+      a.Eta[r][p] = normal(a.key, (uint32_t)q, (uint32_t)h, S_INIT_ETA + LEVEL_STRIDE * r, 0);
+    }
+  }
+}
+
+void launch_init(State& s) {
+  InitArgs a{};
+  a.nc = s.nc;
+  a.nt = s.nt;
+  a.ns_loc = s.nsl;
+  a.sp0 = s.sp0;
+  a.K = s.K;
+  a.NF = s.NF;
+  a.nr = s.nr;
+  for (int r = 0; r < s.nr; ++r) {
+    a.lev_nf[r] = s.lev[r].nf;
+    a.lev_np[r] = s.lev[r].np;
+    a.nu[r] = s.lev[r].nu;
+    a.a1[r] = s.lev[r].a1;
+    a.b1[r] = s.lev[r].b1;
+    a.a2[r] = s.lev[r].a2;
+    a.b2[r] = s.lev[r].b2;
+    a.Eta[r] = s.lev[r].Eta;
+  }
+  a.UGammaL = s.UGammaL;
+  a.mGamma = s.mGamma;
+  a.V0inv = s.V0inv;
+  a.f0 = s.f0;
+  a.Tr = s.Tr;
+  a.fam = s.fam;
+  a.varest = s.varest;
+  a.aSigma = s.aSigma;
+  a.bSigma = s.bSigma;
+  a.Gamma = s.Gamma;
+  a.iV = s.iV;
+  a.LV = s.scratch + 3 * (size_t)s.nc * s.nc;
+  a.BL = s.BL;
+  a.Psi = s.Psi;
+  a.Delta = s.Delta;
+  a.iSigma = s.iSigma;
+  a.scratch = s.scratch;
+  a.key = s.key;
+  init_small_kernel<<<1, 256, 0, s.stream>>>(a);
+  HIP_OK(hipGetLastError());
+  init_big_kernel<<<512, 256, 0, s.stream>>>(a);
+  HIP_OK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// record: pack the state into one contiguous ring slot (device), the D2H copy of
+// the slot then runs on the copy stream overlapped with the next sweeps.
+// ---------------------------------------------------------------------------
+struct PackPiece {
+  const double* src;
+  int64_t n;
+  int64_t dst;
+};
+constexpr int MAX_PIECES = 8 + 2 * HMSC_MAX_LEVELS;
+struct PackArgs {
+  PackPiece p[MAX_PIECES];
+  int npieces;
+  double* slot;
+};
+
+__global__ __launch_bounds__(256) void pack_kernel(PackArgs a) {
+  for (int k = 0; k < a.npieces; ++k) {
+    const PackPiece pc = a.p[k];
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < pc.n; e += (int64_t)gridDim.x * blockDim.x)
+      a.slot[pc.dst + e] = pc.src[e];
+  }
+}
+
+// slot layout: BL(K*nsl) | Psi(NF*nsl) | Delta(NF) | Gamma(nc*nt) | iV(nc*nc) | iSigma(nsl) | Eta_r ... | rho(1)
+size_t record_slot_doubles(const State& s) {
+  size_t n = (size_t)s.Kmax * s.nsl + (size_t)s.NFmax * s.nsl + s.NFmax + (size_t)s.nc * s.nt +
+             (size_t)s.nc * s.nc + s.nsl + 1;
+  for (int r = 0; r < s.nr; ++r) n += (size_t)s.lev[r].np * s.lev[r].nfmax;
+  return n;
+}
+
+void launch_record(State& s, double* slot) {
+  PackArgs a{};
+  int64_t off = 0;
+  int k = 0;
+  auto add = [&](const double* src, int64_t n) {
+    a.p[k++] = PackPiece{src, n, off};
+    off += n;
+  };
+  add(s.BL, (int64_t)s.K * s.nsl);
+  add(s.Psi, (int64_t)s.NF * s.nsl);
+  add(s.Delta, s.NF);
+  add(s.Gamma, (int64_t)s.nc * s.nt);
+  add(s.iV, (int64_t)s.nc * s.nc);
+  add(s.iSigma, s.nsl);
+  for (int r = 0; r < s.nr; ++r) add(s.lev[r].Eta, (int64_t)s.lev[r].np * s.lev[r].nf);
+  a.npieces = k;
+  a.slot = slot;
+  pack_kernel<<<512, 256, 0, s.stream>>>(a);
+  HIP_OK(hipGetLastError());
+}
+
+}  // namespace hmsc

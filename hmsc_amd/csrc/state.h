@@ -1,0 +1,146 @@
+// Device-resident state of one Hmsc chain (or one species shard of a chain).
+//
+// HBM layout (all fp64 column-major like R unless noted):
+//   Z        ny x ns_loc          latent responses (the only large mutable array)
+//   Ycode    ny x ns_loc  int8    0 / 1 / -1(NA)           (probit cells)
+//   Yval     ny x ns_loc          YScaled (only if non-probit species exist)
+//   X        ny x nc              XScaled
+//   BL       K x ns_loc           [Beta; Lambda_1; ...; Lambda_nr]   (K = nc + sum nf_r)
+//   Psi      NF x ns_loc          [Psi_1; ...; Psi_nr]               (NF = sum nf_r)
+//   Delta    NF                   [Delta_1; ...]
+//   Eta_r    np_r x nf_r          per level, column-major
+// Live K/NF change only through updateNf (transient), which repacks on the host;
+// buffers are allocated at nfMax so no reallocation ever happens.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "../../include/hmsc_amd.h"
+#include "rng.h"
+
+namespace hmsc {
+
+struct Level {
+  int np = 0, nf = 0, nfmax = 0, nfmin = 0;
+  double nu = 3, a1 = 50, b1 = 1, a2 = 50, b2 = 1;
+  double* Eta = nullptr;        // np x nfmax storage, live np x nf (ld = np)
+  int* Pi = nullptr;            // ny, 0-based unit of each row
+  int* unit_ptr = nullptr;      // np+1 CSR over rows of each unit
+  int* unit_rows = nullptr;     // ny
+  int* Alpha = nullptr;         // nfmax (host mirror in State::h_alpha)
+  bool all_units_single = true; // np == ny and Pi is a permutation
+};
+
+struct State {
+  // dims
+  int ny = 0, ns = 0, nc = 0, nt = 0, nr = 0;
+  int sp0 = 0, nsl = 0;          // species shard [sp0, sp0+nsl)
+  int rank = 0, nranks = 1;
+  int device = 0;
+  uint32_t mask = HMSC_UP_ALL;
+  Key key{0, 0};
+  int noise_mode = 0;
+  bool has_na = false;           // any NA in the local Y
+  bool any_normal = false;       // any family==1 species (local)
+  bool any_var = false;          // any species with estimated variance (distr[,2]==1)
+  bool any_poisson = false;
+  bool all_probit = true;
+  int K = 0, NF = 0, Kmax = 0, NFmax = 0;
+  double f0 = 0;
+  Level lev[HMSC_MAX_LEVELS];
+
+  hipStream_t stream = nullptr, copy_stream = nullptr;
+
+  // model (device)
+  double *X = nullptr, *Tr = nullptr, *Yval = nullptr, *Yraw = nullptr;
+  int8_t* Ycode = nullptr;
+  int* fam = nullptr;            // ns_loc family code
+  int* varest = nullptr;         // ns_loc distr[,2]
+  double *V0 = nullptr, *iUGamma = nullptr, *mGamma = nullptr, *UGammaL = nullptr;
+  double *aSigma = nullptr, *bSigma = nullptr;
+  double *XX = nullptr, *TT = nullptr, *V0g = nullptr, *V0gXXV0g = nullptr, *iV0 = nullptr;
+  double* V0inv = nullptr;       // V0^-1 (initial riwish draw)
+  int* na_cols = nullptr;        // local species with any NA
+  int* na_index = nullptr;       // nsl: row of species j in Gna, or -1
+  int n_na_cols = 0;
+  int* na_rows = nullptr;        // rows with any NA (local)
+  int8_t* row_na = nullptr;      // ny: 1 if the row has an NA
+  int* row_slot = nullptr;       // ny: index into na_rows, or -1
+  int n_na_rows = 0;
+  int* dev_flags = nullptr;      // device error flags (Cholesky failures)
+  std::vector<int> h_na_cols;
+
+  // chain state (device)
+  double *Z = nullptr, *BL = nullptr, *Psi = nullptr, *Delta = nullptr;
+  double *Gamma = nullptr, *iV = nullptr, *iSigma = nullptr;
+  int* rho = nullptr;
+
+  // per-sweep workspaces
+  double* XZ = nullptr;          // K x ns_loc   XEta^T (Yx o Z)
+  double* G = nullptr;           // Kmax x Kmax  XEta^T XEta
+  double* ZTr = nullptr;         // ny x nt      Z Tr (local species)
+  double* XZ_part = nullptr;     // nchunk x K x ns_loc
+  double* G_part = nullptr;      // nchunk x Kmax^2
+  double* ZTr_part = nullptr;    // ntile_j x ny x nt
+  double* Gna = nullptr;         // n_na_cols x Kmax^2 masked grams
+  double* ZL = nullptr;          // ny x NFP   Z * (Lambda diag(iSigma))^T, all levels
+  double* ZL_part = nullptr;     // zl_split x ny x NFP
+  double* CR = nullptr;          // Kmax x NFmax  BL diag(iSigma) Lambda_all^T
+  double* Msmall = nullptr;      // per-level masked row grams (NA rows)
+  double* scratch = nullptr;     // single-workgroup updaters
+  double* psi_rs = nullptr;      // psi-lambda^2 row-sum partials
+  double* ABpart = nullptr;      // GammaV species-partials
+  double* dbg_prec = nullptr;    // optional debug: per-species precisions
+  bool zt_valid = false;         // XZ/G/ZTr computed for the current Z and Eta
+  int nchunk = 0, ntile_j = 0, zl_split = 0, NFP = 0;
+  size_t scratch_doubles = 0;
+
+  // recording ring
+  double* ring = nullptr;
+  int ring_slots = 0;
+  size_t slot_doubles = 0;
+  std::vector<hipEvent_t> ring_done;
+  double* host_rec = nullptr;    // pinned
+
+  // RCCL (species-sharded chain)
+  void* comm = nullptr;
+  double* allreduce_buf = nullptr;
+
+  std::vector<int> h_nf() const {
+    std::vector<int> v(nr);
+    for (int r = 0; r < nr; ++r) v[r] = lev[r].nf;
+    return v;
+  }
+  int loff(int r) const {  // row offset of level r inside BL
+    int o = nc;
+    for (int q = 0; q < r; ++q) o += lev[q].nf;
+    return o;
+  }
+  int foff(int r) const {  // row offset of level r inside Psi / Delta
+    int o = 0;
+    for (int q = 0; q < r; ++q) o += lev[q].nf;
+    return o;
+  }
+  void refresh_dims() {
+    NF = 0;
+    for (int r = 0; r < nr; ++r) NF += lev[r].nf;
+    K = nc + NF;
+  }
+};
+
+// launchers implemented in kernels.hip
+void launch_init(State& s);
+void launch_update_z(State& s, uint32_t iter, bool use_raw_y);
+void launch_zt_refresh(State& s);
+void launch_beta_lambda(State& s, uint32_t iter);
+void launch_gamma_v(State& s, uint32_t iter);
+void launch_gamma2(State& s, uint32_t iter);
+void launch_lambda_priors(State& s, uint32_t iter);
+void launch_eta(State& s, uint32_t iter);
+void launch_inv_sigma(State& s, uint32_t iter);
+void launch_record(State& s, double* slot);
+size_t record_slot_doubles(const State& s);
+
+}  // namespace hmsc

@@ -1,0 +1,431 @@
+"""``sampleMcmc`` — host mirror of R/sampleMcmc.R:68-372 over the MI355X sampler.
+
+The R-side logic the reference keeps around its sweep loop stays here (argument
+checks, per-chain ``initSeed``, updater auto-disable, ``combineParameters``
+back-transform, ``alignPosterior`` x5, hM bookkeeping); the sweep loop itself
+(:219-325) runs on the GPU through the C ABI (``Chain``).  Independent chains
+run one per GPU, concurrently (threads; the C calls release the GIL), which is
+the MI355X form of the reference's PSOCK chain farm (:329-345).
+"""
+import ctypes as C
+import math
+import threading
+import warnings
+
+import numpy as np
+
+from . import _lib as L
+from .model import Hmsc
+
+
+def _r_bool_on(updater, name):
+    """R: ``!identical(updater$NAME, FALSE)`` (only a literal FALSE disables)."""
+    v = (updater or {}).get(name, None)
+    return not (v is False)
+
+
+def _finite_int(v, cap):
+    return int(min(cap, v)) if not (isinstance(v, float) and math.isinf(v)) else int(cap)
+
+
+class ModelBuffers:
+    """Column-major copies of the hM fields the sampler consumes (the marshalling the
+    R ``.Call`` shim would do), kept alive for the lifetime of the C struct."""
+
+    def __init__(self, hM):
+        if hM.C is not None:
+            raise NotImplementedError("phylogeny (C / phyloTree) is a 'next' row (SURVEY.md §8 f1): "
+                                      "the dense BetaLambda branch and updateRho are not on the device yet")
+        for rl in hM.rL or []:
+            if rl.sDim:
+                raise NotImplementedError("spatial random levels are a 'next' row (SURVEY.md §8 f2)")
+            if rl.xDim:
+                raise NotImplementedError("covariate-dependent random levels are a 'next' row")
+        if np.any(hM.distr[:, 0] == 3):
+            raise NotImplementedError("Poisson / lognormal-Poisson species are a 'next' row (SURVEY.md §8 f3)")
+        self.keep = []
+        k = self.keep
+        m = L.hmsc_model()
+        m.ny, m.ns, m.nc, m.nt, m.nr = hM.ny, hM.ns, hM.nc, hM.nt, hM.nr
+        m.Y = L.colmajor_ptr(hM.YScaled, k)
+        m.Yraw = L.colmajor_ptr(hM.Y, k)
+        m.X = L.colmajor_ptr(hM.XScaled, k)
+        m.Tr = L.colmajor_ptr(hM.TrScaled, k)
+        m.Pi = L.colmajor_ptr(hM.Pi if hM.nr else np.zeros((hM.ny, 1)), k, np.int32)
+        m.np = L.colmajor_ptr(hM.np if hM.nr else [0], k, np.int32)
+        m.distr = L.colmajor_ptr(hM.distr, k, np.int32)
+        m.V0 = L.colmajor_ptr(hM.V0, k)
+        m.f0 = float(hM.f0)
+        m.mGamma = L.colmajor_ptr(hM.mGamma, k)
+        m.UGamma = L.colmajor_ptr(hM.UGamma, k)
+        m.aSigma = L.colmajor_ptr(hM.aSigma, k)
+        m.bSigma = L.colmajor_ptr(hM.bSigma, k)
+        rl = hM.rL or []
+        vec = lambda name: L.colmajor_ptr([float(r[name]) for r in rl] or [0.0], k)  # noqa: E731
+        m.nu, m.a1, m.b1, m.a2, m.b2 = vec("nu"), vec("a1"), vec("b1"), vec("a2"), vec("b2")
+        self.nfMax = [_finite_int(r.nfMax, hM.ns) for r in rl]
+        self.nfMin = [int(r.nfMin) for r in rl]
+        m.nfMin = L.colmajor_ptr(self.nfMin or [0], k, np.int32)
+        m.nfMax = L.colmajor_ptr(self.nfMax or [0], k, np.int32)
+        m.sDim = L.colmajor_ptr([0] * max(1, hM.nr), k, np.int32)
+        m.xDim = L.colmajor_ptr([0] * max(1, hM.nr), k, np.int32)
+        m.C = None
+        self.struct = m
+
+
+def updater_mask(updater):
+    mask = 0
+    for name, bit in L.UP.items():
+        if _r_bool_on(updater, name):
+            mask |= bit
+    return mask
+
+
+class Chain:
+    """One chain's device-resident state (hmsc_create ... hmsc_destroy)."""
+
+    def __init__(self, hM, seed, device=0, updater=None, rank=0, nranks=1, comm_id=None, mask=None):
+        self.hM = hM
+        self.lib = L.lib()
+        self.buf = ModelBuffers(hM)
+        self.mask = updater_mask(updater) if mask is None else mask
+        h = C.c_void_p()
+        if nranks > 1:
+            cid = C.create_string_buffer(bytes(comm_id), 128)
+            L.check(self.lib.hmsc_create_sharded(C.byref(self.buf.struct), C.c_uint64(int(seed)), device,
+                                                 self.mask, rank, nranks, cid, C.byref(h)))
+        else:
+            L.check(self.lib.hmsc_create(C.byref(self.buf.struct), C.c_uint64(int(seed)), device, self.mask,
+                                         C.byref(h)))
+        self.h = h
+        self.rank, self.nranks = rank, nranks
+        per = -(-hM.ns // nranks)
+        self.sp0 = min(hM.ns, rank * per)
+        self.nsl = min(hM.ns, self.sp0 + per) - self.sp0
+
+    def close(self):
+        if self.h:
+            self.lib.hmsc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- state
+    def init(self, nf0=None):
+        arr = None if nf0 is None else L.i32(nf0)
+        L.check(self.lib.hmsc_init_state(self.h, L.iptr(arr)))
+
+    def nf(self):
+        out = np.zeros(L.MAX_LEVELS, dtype=np.int32)
+        L.check(self.lib.hmsc_get_nf(self.h, L.iptr(out)))
+        return out[: self.hM.nr].copy()
+
+    def get_state(self, with_z=True):
+        hM = self.hM
+        nf = self.nf()
+        ns = self.nsl
+        st = dict(Gamma=np.zeros(hM.nc * hM.nt), iV=np.zeros(hM.nc * hM.nc), Beta=np.zeros(hM.nc * ns),
+                  iSigma=np.zeros(ns))
+        if with_z:
+            st["Z"] = np.zeros(hM.ny * ns)
+        p = L.hmsc_params()
+        for key in st:
+            setattr(p, key, L.fptr(st[key]))
+        lv = {f: [] for f in ("Eta", "Lambda", "Psi", "Delta", "Alpha")}
+        for r in range(hM.nr):
+            lv["Eta"].append(np.zeros(int(hM.np[r]) * nf[r]))
+            lv["Lambda"].append(np.zeros(nf[r] * ns))
+            lv["Psi"].append(np.zeros(nf[r] * ns))
+            lv["Delta"].append(np.zeros(nf[r]))
+            lv["Alpha"].append(np.zeros(nf[r], dtype=np.int32))
+            p.Eta[r] = L.fptr(lv["Eta"][r])
+            p.Lambda[r] = L.fptr(lv["Lambda"][r])
+            p.Psi[r] = L.fptr(lv["Psi"][r])
+            p.Delta[r] = L.fptr(lv["Delta"][r])
+            p.Alpha[r] = L.iptr(lv["Alpha"][r])
+        L.check(self.lib.hmsc_get_state(self.h, C.byref(p)))
+        out = dict(Gamma=st["Gamma"].reshape(hM.nc, hM.nt, order="F"),
+                   iV=st["iV"].reshape(hM.nc, hM.nc, order="F"),
+                   Beta=st["Beta"].reshape(hM.nc, ns, order="F"), iSigma=st["iSigma"], rho=int(p.rho))
+        if with_z:
+            out["Z"] = st["Z"].reshape(hM.ny, ns, order="F")
+        out["Eta"] = [lv["Eta"][r].reshape(int(hM.np[r]), nf[r], order="F") for r in range(hM.nr)]
+        out["Lambda"] = [lv["Lambda"][r].reshape(nf[r], ns, order="F") for r in range(hM.nr)]
+        out["Psi"] = [lv["Psi"][r].reshape(nf[r], ns, order="F") for r in range(hM.nr)]
+        out["Delta"] = [lv["Delta"][r] for r in range(hM.nr)]
+        out["Alpha"] = [lv["Alpha"][r].astype(np.int64) for r in range(hM.nr)]
+        return out
+
+    def set_state(self, st):
+        """initPar-style override: any subset of Gamma, iV (or V), Beta, iSigma (or sigma),
+        Eta, Lambda, Psi, Delta, Z (R/computeInitialParameters.R:82-227)."""
+        hM = self.hM
+        keep = []
+        p = L.hmsc_params()
+        st = dict(st)
+        if "V" in st and "iV" not in st:
+            st["iV"] = np.linalg.inv(st["V"])
+        if "sigma" in st and "iSigma" not in st:
+            st["iSigma"] = 1.0 / np.asarray(st["sigma"], dtype=np.float64)
+        for key in ("Gamma", "iV", "Beta", "iSigma", "Z"):
+            if st.get(key) is not None:
+                setattr(p, key, L.colmajor_ptr(st[key], keep))
+        for r in range(hM.nr):
+            nf = 0
+            for key in ("Eta", "Lambda", "Psi", "Delta"):
+                v = st.get(key)
+                if v is not None and v[r] is not None:
+                    a = np.asarray(v[r], dtype=np.float64)
+                    nf = a.shape[1] if key == "Eta" else a.shape[0]
+                    getattr(p, key)[r] = L.colmajor_ptr(a, keep)
+            p.nf[r] = nf
+        L.check(self.lib.hmsc_set_state(self.h, C.byref(p)))
+
+    # ---- sweeps
+    def sweep(self, it, adapt=False):
+        L.check(self.lib.hmsc_sweep(self.h, int(it), 1 if adapt else 0))
+
+    def update(self, name, it):
+        L.check(self.lib.hmsc_update(self.h, L.UP[name], int(it)))
+
+    def set_noise_mode(self, mode):
+        L.check(self.lib.hmsc_set_noise_mode(self.h, int(mode)))
+
+    def sync(self):
+        L.check(self.lib.hmsc_sync(self.h))
+
+    def debug_get(self, name, n):
+        out = np.zeros(int(n))
+        L.check(self.lib.hmsc_debug_get(self.h, name.encode(), L.fptr(out), int(n)))
+        return out
+
+    def run(self, transient, samples, thin=1, adaptNf=None, iter0=0, verbose=0, chain=1, record=True):
+        """hmsc_run: the device sweep loop with recording; returns the raw record arrays."""
+        hM = self.hM
+        nr = hM.nr
+        ns = self.nsl
+        nfMax = self.buf.nfMax
+        adapt = L.i32(adaptNf if adaptNf is not None else [transient] * max(1, nr))
+        rec = None
+        arrays = None
+        if record and samples > 0:
+            S = samples
+            arrays = dict(Beta=np.zeros((S, ns, hM.nc)), Gamma=np.zeros((S, hM.nt, hM.nc)),
+                          iV=np.zeros((S, hM.nc, hM.nc)), iSigma=np.zeros((S, ns)),
+                          rho=np.zeros(S, dtype=np.int32), rec_nf=np.zeros((max(1, nr), S), dtype=np.int32))
+            rec = L.hmsc_record()
+            rec.Beta, rec.Gamma, rec.iV = L.fptr(arrays["Beta"]), L.fptr(arrays["Gamma"]), L.fptr(arrays["iV"])
+            rec.iSigma, rec.rho, rec.rec_nf = L.fptr(arrays["iSigma"]), L.iptr(arrays["rho"]), L.iptr(arrays["rec_nf"])
+            for r in range(nr):
+                nfm = nfMax[r]
+                arrays[f"Eta{r}"] = np.zeros((S, nfm, int(hM.np[r])))
+                arrays[f"Lambda{r}"] = np.zeros((S, ns, nfm))
+                arrays[f"Psi{r}"] = np.zeros((S, ns, nfm))
+                arrays[f"Delta{r}"] = np.zeros((S, nfm))
+                arrays[f"Alpha{r}"] = np.zeros((S, nfm), dtype=np.int32)
+                rec.Eta[r] = L.fptr(arrays[f"Eta{r}"])
+                rec.Lambda[r] = L.fptr(arrays[f"Lambda{r}"])
+                rec.Psi[r] = L.fptr(arrays[f"Psi{r}"])
+                rec.Delta[r] = L.fptr(arrays[f"Delta{r}"])
+                rec.Alpha[r] = L.iptr(arrays[f"Alpha{r}"])
+        L.check(self.lib.hmsc_run_verbose(self.h, int(transient), int(samples), int(thin), L.iptr(adapt),
+                                          int(iter0), int(verbose), int(chain),
+                                          C.byref(rec) if rec is not None else None))
+        if arrays is None:
+            return None
+        # C buffers were written column-major per sample: view them in R orientation
+        out = dict(Beta=arrays["Beta"].transpose(0, 2, 1), Gamma=arrays["Gamma"].transpose(0, 2, 1),
+                   iV=arrays["iV"].transpose(0, 2, 1), iSigma=arrays["iSigma"], rho=arrays["rho"],
+                   nf=arrays["rec_nf"][:nr])
+        for r in range(nr):
+            out[f"Eta{r}"] = arrays[f"Eta{r}"].transpose(0, 2, 1)
+            out[f"Lambda{r}"] = arrays[f"Lambda{r}"].transpose(0, 2, 1)
+            out[f"Psi{r}"] = arrays[f"Psi{r}"].transpose(0, 2, 1)
+            out[f"Delta{r}"] = arrays[f"Delta{r}"]
+            out[f"Alpha{r}"] = arrays[f"Alpha{r}"].astype(np.int64)
+        return out
+
+
+# ---------------------------------------------------------------------------
+# combineParameters — R/combineParameters.R:1-58, vectorised over samples
+# ---------------------------------------------------------------------------
+def combine_parameters(rec, hM):
+    Beta = rec["Beta"].copy()
+    Gamma = rec["Gamma"].copy()
+    iV = rec["iV"].copy()
+    TrI = None if hM.TrInterceptInd is None else hM.TrInterceptInd - 1
+    XI = None if hM.XInterceptInd is None else hM.XInterceptInd - 1
+    for p in range(hM.nt):                                           # :2-10
+        m, s = hM.TrScalePar[0, p], hM.TrScalePar[1, p]
+        if m != 0 or s != 1:
+            Gamma[:, :, p] = Gamma[:, :, p] / s
+            if TrI is not None:
+                Gamma[:, :, TrI] = Gamma[:, :, TrI] - m * Gamma[:, :, p]
+    for k in range(hM.ncNRRR):                                       # :12-26
+        m, s = hM.XScalePar[0, k], hM.XScalePar[1, k]
+        if m != 0 or s != 1:
+            Beta[:, k, :] = Beta[:, k, :] / s
+            Gamma[:, k, :] = Gamma[:, k, :] / s
+            if XI is not None:
+                Beta[:, XI, :] = Beta[:, XI, :] - m * Beta[:, k, :]
+                Gamma[:, XI, :] = Gamma[:, XI, :] - m * Gamma[:, k, :]
+            iV[:, k, :] = iV[:, k, :] * s
+            iV[:, :, k] = iV[:, :, k] * s
+    V = np.linalg.inv(iV)                                            # :53 chol2inv(chol(iV))
+    V = 0.5 * (V + V.transpose(0, 2, 1))
+    sigma = 1.0 / rec["iSigma"]
+    rho = hM.rhopw[rec["rho"] - 1, 0]
+    S = Beta.shape[0]
+    post = []
+    for k in range(S):
+        Eta, Lambda, Psi, Delta, Alpha = [], [], [], [], []
+        for r in range(hM.nr):
+            nf = int(rec["nf"][r][k])
+            Eta.append(rec[f"Eta{r}"][k, :, :nf])
+            Lambda.append(rec[f"Lambda{r}"][k, :nf, :])
+            Psi.append(rec[f"Psi{r}"][k, :nf, :])
+            Delta.append(rec[f"Delta{r}"][k, :nf].reshape(nf, 1))
+            Alpha.append(rec[f"Alpha{r}"][k, :nf])
+        post.append(dict(Beta=Beta[k], wRRR=None, Gamma=Gamma[k], V=V[k], rho=float(rho[k]), sigma=sigma[k],
+                         Eta=Eta, Lambda=Lambda, Alpha=Alpha, Psi=Psi, Delta=Delta, PsiRRR=None, DeltaRRR=None))
+    return post
+
+
+# ---------------------------------------------------------------------------
+# alignPosterior — R/alignPosterior.R:18-100 (sign alignment + nfMax padding)
+# ---------------------------------------------------------------------------
+def alignPosterior(hM):
+    for r in range(hM.nr):
+        nfVec = [pc[0]["Lambda"][r].shape[0] for pc in hM.postList]
+        nfMax = max(nfVec)
+        tmpl = hM.postList[int(np.argmax(nfVec))]
+        LamMean = np.mean(np.stack([s["Lambda"][r] for s in tmpl]), axis=0)          # :31-33
+        for cInd, cpL in enumerate(hM.postList):
+            lam = np.stack([s["Lambda"][r] for s in cpL])                           # (S, nf, ns)
+            nf = lam.shape[1]
+            if hM.ns > 1:
+                a = lam - lam.mean(axis=2, keepdims=True)
+                b = LamMean[:nf] - LamMean[:nf].mean(axis=1, keepdims=True)
+                num = np.einsum("skj,kj->sk", a, b)
+                den = np.sqrt((a ** 2).sum(axis=2) * (b ** 2).sum(axis=1)[None, :])
+                sd_ok = (lam.std(axis=2) > 0) & (LamMean[:nf].std(axis=1) > 0)[None, :]
+                with np.errstate(invalid="ignore", divide="ignore"):
+                    sgn = np.where(sd_ok, np.sign(num / den), 0.0)                # :41-46
+            else:
+                sgn = np.sign(LamMean[:nf, 0])[None, :] * np.sign(lam[:, :, 0])   # :48
+            for j, s in enumerate(cpL):
+                flip = sgn[j] < 0
+                if flip.any():                                                      # :50-56
+                    s["Lambda"][r] = np.where(flip[:, None], -s["Lambda"][r], s["Lambda"][r])
+                    s["Eta"][r] = np.where(flip[None, :], -s["Eta"][r], s["Eta"][r])
+                if nf < nfMax:                                                      # :57-68
+                    pad = nfMax - nf
+                    s["Lambda"][r] = np.vstack([s["Lambda"][r], np.zeros((pad, hM.ns))])
+                    s["Psi"][r] = np.vstack([s["Psi"][r], np.zeros((pad, hM.ns))])
+                    s["Delta"][r] = np.vstack([s["Delta"][r], np.ones((pad, 1))])
+                    s["Eta"][r] = np.hstack([s["Eta"][r], np.zeros((s["Eta"][r].shape[0], pad))])
+                    if hM.rL[r].sDim:
+                        s["Alpha"][r] = np.r_[s["Alpha"][r], np.ones(pad, dtype=np.int64)]
+    return hM
+
+
+# ---------------------------------------------------------------------------
+# sampleMcmc — R/sampleMcmc.R:68-372
+# ---------------------------------------------------------------------------
+def sampleMcmc(hM, samples, transient=0, thin=1, initPar=None, verbose=None, adaptNf=None, nChains=1,
+               nParallel=1, dataParList=None, updater=None, fromPrior=False, alignPost=True, seed=None,
+               devices=None):
+    if not isinstance(hM, Hmsc):
+        raise TypeError("sampleMcmc: hM must be an Hmsc object")
+    if verbose is None:
+        verbose = samples * thin / 100                                     # :69
+    if adaptNf is None:
+        adaptNf = [transient] * hM.nr
+    if fromPrior:
+        raise NotImplementedError("fromPrior=TRUE (samplePrior) is out of scope (SURVEY.md §2 row 10)")
+    if nParallel > nChains:                                                # :75-78
+        warnings.warn("Number of cores cannot be greater than the number of chains")
+        nParallel = nChains
+    if any(a > transient for a in adaptNf):                                # :79-80
+        raise ValueError("transient parameter should be no less than any element of adaptNf parameter")
+    updater = dict(updater or {})
+    rng = np.random.default_rng(seed)
+    initSeed = rng.integers(1, 2 ** 31 - 1, size=nChains)                 # :121 sample.int(.Machine$integer.max)
+    EPS = 1e-6                                                            # :123-152
+    nc, nt = hM.nc, hM.nt
+    iUGamma = np.linalg.inv(hM.UGamma)
+    if _r_bool_on(updater, "Gamma2") and np.any(np.abs(hM.mGamma) > EPS):
+        updater["Gamma2"] = False
+        print("Setting updater$Gamma2=FALSE due to non-zero mGamma")
+    if _r_bool_on(updater, "Gamma2") and np.any(np.abs(iUGamma - np.kron(iUGamma[:nc, :nc], np.eye(nt))) > EPS):
+        updater["Gamma2"] = False
+        print("Setting updater$Gamma2=FALSE due to non-kronecker structure of UGamma matrix")
+    if _r_bool_on(updater, "Gamma2") and hM.C is not None:
+        updater["Gamma2"] = False
+        print("Setting updater$Gamma2=FALSE due to specified phylogeny matrix")
+    if _r_bool_on(updater, "GammaEta") and np.any(np.abs(hM.mGamma) > EPS):
+        updater["GammaEta"] = False
+        print("Setting updater$GammaEta=FALSE due to non-zero mGamma")
+    if _r_bool_on(updater, "GammaEta") and hM.nr == 0:
+        updater["GammaEta"] = False
+        print("Setting updater$GammaEta=FALSE due to absence of random effects included to the model")
+    if _r_bool_on(updater, "GammaEta"):
+        raise NotImplementedError("updateGammaEta is a 'next' row (SURVEY.md §8 f1): pass "
+                                  "updater={'GammaEta': False} (as vignette_4 does)")
+    ndev = np.zeros(1, dtype=np.int32)
+    L.check(L.lib().hmsc_device_count(L.iptr(ndev)))
+    if ndev[0] < 1:
+        raise L.HmscNativeError("no MI355X device visible")
+    devices = list(range(int(ndev[0]))) if devices is None else list(devices)
+    nf0 = [int(rl.nfMin) for rl in hM.rL] if hM.nr else None
+    if initPar is not None and initPar != "fixed effects":
+        for r in range(hM.nr):
+            for key in ("Delta", "Psi", "Lambda", "Eta"):
+                v = initPar.get(key)
+                if v is not None and v[r] is not None:
+                    a = np.asarray(v[r])
+                    nf0[r] = a.shape[1] if key == "Eta" else a.shape[0]
+    elif initPar == "fixed effects":
+        raise NotImplementedError("initPar='fixed effects' (GLM initialisation) is not implemented")
+
+    results = [None] * nChains
+    errors = []
+
+    def sample_chain(c):                                                   # :155-327
+        try:
+            if nChains > 1:
+                print(f'[1] "Computing chain {c + 1}"')
+            ch = Chain(hM, int(initSeed[c]), device=devices[c % len(devices)], updater=updater)
+            ch.init(nf0)
+            if initPar is not None:
+                ch.set_state(initPar)
+            rec = ch.run(transient, samples, thin, adaptNf, verbose=int(verbose) if verbose else 0, chain=c + 1)
+            ch.close()
+            results[c] = combine_parameters(rec, hM)
+        except Exception as e:  # surface in the caller thread
+            errors.append(e)
+
+    if nParallel > 1:
+        for start in range(0, nChains, nParallel):
+            th = [threading.Thread(target=sample_chain, args=(c,)) for c in range(start, min(nChains, start + nParallel))]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+    else:
+        for c in range(nChains):
+            sample_chain(c)
+    if errors:
+        raise errors[0]
+    hM.postList = results
+    hM.repList = [None] * nChains
+    hM.samples, hM.transient, hM.thin, hM.verbose = samples, transient, thin, verbose   # :360-364
+    hM.adaptNf = list(adaptNf)
+    if alignPost:
+        for _ in range(5):                                                 # :365-369
+            hM = alignPosterior(hM)
+    return hM

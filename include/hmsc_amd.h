@@ -1,0 +1,183 @@
+/*
+ * hmsc_amd.h — C ABI of the MI355X-native Gibbs sampler behind Hmsc's sampleMcmc().
+ *
+ * The reference (taddallas/HMSC, R package Hmsc 3.0-4) has no native code and no
+ * FFI: its boundary is the R function sampleMcmc() (R/sampleMcmc.R:68-71) whose
+ * per-chain body sampleChain() (R/sampleMcmc.R:155-327) runs the sweep loop
+ * (:219-325) over R-level updaters.  Each entry point below names the reference
+ * interface it replaces.  A maintainer binds them from R with the .Call shim in
+ * INTEGRATION.md; this repository binds them with ctypes (hmsc_amd/_lib.py).
+ *
+ * Conventions
+ *   - every matrix is column-major fp64 exactly as R stores it (no transposes);
+ *   - Y carries R's NA as NaN; Pi is R's 1-based hM$Pi (stored as int32 here);
+ *   - caller owns every input buffer; hmsc_create copies them to the device;
+ *   - caller allocates every output buffer;
+ *   - return 0 on success, <0 on error; hmsc_last_error() gives the message
+ *     (thread-local); no C++ exception or longjmp crosses this boundary.
+ */
+#ifndef HMSC_AMD_H
+#define HMSC_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HMSC_MAX_LEVELS 8
+
+/* updater switches: R's updater=list(NAME=FALSE) (R/sampleMcmc.R:17,221-294) as a bitmask */
+enum hmsc_updater {
+  HMSC_UP_GAMMA2 = 1u << 0,       /* updateGamma2       R/updateGamma2.R:6      */
+  HMSC_UP_GAMMAETA = 1u << 1,     /* updateGammaEta     R/updateGammaEta.R:7    */
+  HMSC_UP_BETALAMBDA = 1u << 2,   /* updateBetaLambda   R/updateBetaLambda.R:8  */
+  HMSC_UP_WRRR = 1u << 3,         /* updatewRRR         (out of scope)          */
+  HMSC_UP_BETASEL = 1u << 4,      /* updateBetaSel      (out of scope)          */
+  HMSC_UP_GAMMAV = 1u << 5,       /* updateGammaV       R/updateGammaV.R:4      */
+  HMSC_UP_RHO = 1u << 6,          /* updateRho          R/updateRho.R:1         */
+  HMSC_UP_LAMBDAPRIORS = 1u << 7, /* updateLambdaPriors R/updateLambdaPriors.R:3 */
+  HMSC_UP_WRRRPRIORS = 1u << 8,   /* updatewRRRPriors   (out of scope)          */
+  HMSC_UP_ETA = 1u << 9,          /* updateEta          R/updateEta.R:4         */
+  HMSC_UP_ALPHA = 1u << 10,       /* updateAlpha        R/updateAlpha.R:3       */
+  HMSC_UP_INVSIGMA = 1u << 11,    /* updateInvSigma     R/updateInvSigma.R:3    */
+  HMSC_UP_Z = 1u << 12,           /* updateZ            R/updateZ.R:4           */
+  HMSC_UP_ALL = 0x1FFFu
+};
+
+/* The hM fields consumed by the sampler (R/Hmsc.R:118-167 after construction and
+ * setPriors defaults R/setPriors.Hmsc.R:28-77, R/setPriors.HmscRandomLevel.R:31-108). */
+typedef struct hmsc_model {
+  int32_t ny, ns, nc, nt, nr;
+  const double* Y;        /* ny*ns  hM$YScaled (NaN = NA)                      */
+  const double* Yraw;     /* ny*ns  hM$Y (initial Z, R/computeInitialParameters.R:254); may equal Y */
+  const double* X;        /* ny*nc  hM$XScaled                                 */
+  const double* Tr;       /* ns*nt  hM$TrScaled                                */
+  const int32_t* Pi;      /* ny*nr  hM$Pi, 1-based                             */
+  const int32_t* np;      /* nr     hM$np                                      */
+  const int32_t* distr;   /* ns*4   hM$distr (family, variance, link, -)       */
+  const double* V0;       /* nc*nc  */
+  double f0;
+  const double* mGamma;   /* nc*nt  */
+  const double* UGamma;   /* (nc*nt)^2 */
+  const double* aSigma;   /* ns */
+  const double* bSigma;   /* ns */
+  /* per random level r < nr (hM$rL[[r]]) */
+  const double* nu;
+  const double* a1;
+  const double* b1;
+  const double* a2;
+  const double* b2;
+  const int32_t* nfMin;
+  const int32_t* nfMax;
+  const int32_t* sDim;    /* spatial levels are a 'next' row: must be 0 */
+  const int32_t* xDim;    /* covariate-dependent levels: must be 0       */
+  /* phylogeny (C != NULL) is a 'next' row: must be NULL in this build */
+  const double* C;
+} hmsc_model;
+
+/* Sampler state = R's parList (R/computeInitialParameters.R:256-270) with iV in
+ * place of V and iSigma in place of sigma, as sampleChain keeps them
+ * (R/sampleMcmc.R:161-177).  Per-level arrays are indexed [r]; Eta[r] is
+ * np[r]*nf[r], Lambda/Psi[r] nf[r]*ns, Delta/Alpha[r] nf[r] (Alpha 1-based grid index). */
+typedef struct hmsc_params {
+  double* Gamma;          /* nc*nt */
+  double* iV;             /* nc*nc */
+  double* Beta;           /* nc*ns */
+  double* iSigma;         /* ns    */
+  double* Z;              /* ny*ns (may be NULL) */
+  int32_t rho;            /* 1-based */
+  int32_t nf[HMSC_MAX_LEVELS];
+  double* Eta[HMSC_MAX_LEVELS];
+  double* Lambda[HMSC_MAX_LEVELS];
+  double* Psi[HMSC_MAX_LEVELS];
+  double* Delta[HMSC_MAX_LEVELS];
+  int32_t* Alpha[HMSC_MAX_LEVELS];
+} hmsc_params;
+
+/* Recording buffers for hmsc_run: caller-allocated, `samples` slots each.  The
+ * fields are the raw (scaled-X) state; the host applies combineParameters
+ * (R/combineParameters.R:1-58) afterwards.  Eta/Lambda/Psi/Delta/Alpha slots are
+ * padded to nfMax[r]; rec_nf[r*samples+k] gives the live nf of sample k. */
+typedef struct hmsc_record {
+  double* Beta;           /* samples*nc*ns */
+  double* Gamma;          /* samples*nc*nt */
+  double* iV;             /* samples*nc*nc */
+  double* iSigma;         /* samples*ns    */
+  int32_t* rho;           /* samples       */
+  double* Eta[HMSC_MAX_LEVELS];     /* samples*np[r]*nfMax[r]  */
+  double* Lambda[HMSC_MAX_LEVELS];  /* samples*nfMax[r]*ns     */
+  double* Psi[HMSC_MAX_LEVELS];     /* samples*nfMax[r]*ns     */
+  double* Delta[HMSC_MAX_LEVELS];   /* samples*nfMax[r]        */
+  int32_t* Alpha[HMSC_MAX_LEVELS];  /* samples*nfMax[r]        */
+  int32_t* rec_nf;                  /* nr*samples              */
+} hmsc_record;
+
+typedef struct hmsc_state hmsc_state;
+
+/* Thread-local description of the last error. */
+const char* hmsc_last_error(void);
+
+/* Number of visible MI355X devices. */
+int hmsc_device_count(int32_t* n);
+
+/* Create one chain's device state: copies the model, allocates HBM for the state
+ * at nfMax, keys Philox by `seed` (R: set.seed(initSeed[chain]), R/sampleMcmc.R:158).
+ * Replaces the per-chain setup of sampleChain, R/sampleMcmc.R:155-216. */
+int hmsc_create(const hmsc_model* model, uint64_t seed, int32_t device, uint32_t updater_mask,
+                hmsc_state** out);
+
+/* Species-sharded single chain: this rank owns species
+ * [sp_begin, sp_end) of the model passed in full; `comm_id` is the 128-byte RCCL
+ * unique id from hmsc_comm_unique_id() broadcast by rank 0 (NULL when nranks==1). */
+int hmsc_create_sharded(const hmsc_model* model, uint64_t seed, int32_t device,
+                        uint32_t updater_mask, int32_t rank, int32_t nranks,
+                        const void* comm_id, hmsc_state** out);
+int hmsc_comm_unique_id(void* out128);
+
+void hmsc_destroy(hmsc_state* s);
+
+/* computeInitialParameters(hM, initPar=NULL) on the device, including the initial
+ * updateZ (R/computeInitialParameters.R:17-273). nf0[r] = starting nf (nfMin). */
+int hmsc_init_state(hmsc_state* s, const int32_t* nf0);
+
+/* initPar / resume: overwrite state (R/computeInitialParameters.R:82-227). */
+int hmsc_set_state(hmsc_state* s, const hmsc_params* p);
+int hmsc_get_state(hmsc_state* s, hmsc_params* p);
+int hmsc_get_nf(hmsc_state* s, int32_t* nf);
+
+/* One Gibbs sweep in the reference block order, R/sampleMcmc.R:219-306.
+ * `iter` is the 1-based sweep number (Philox counter word 3 and updateNf's iter). */
+int hmsc_sweep(hmsc_state* s, int32_t iter, int32_t adapt_nf);
+
+/* A single updater (per-updater tests; R's tests call updaters directly,
+ * tests/testthat/test-sampling.R). `which` is one hmsc_updater bit. */
+int hmsc_update(hmsc_state* s, uint32_t which, int32_t iter);
+
+/* noise_mode 1: every Gaussian innovation is zero, so Gaussian blocks return their
+ * conditional means (moment-parity tests); 0: normal sampling. */
+int hmsc_set_noise_mode(hmsc_state* s, int32_t mode);
+
+/* The sweep loop with recording: for iter in 1..transient+samples*thin, record when
+ * iter>transient and (iter-transient)%%thin==0 (R/sampleMcmc.R:219-315).
+ * adaptNf[r] = hM adaptNf.  `rec` may be NULL (no recording). */
+int hmsc_run(hmsc_state* s, int32_t transient, int32_t samples, int32_t thin,
+             const int32_t* adaptNf, int32_t iter0, hmsc_record* rec);
+
+/* hmsc_run with R's progress print every `verbose` sweeps
+ * ("Chain %d, iteration %d of %d, (%s)", R/sampleMcmc.R:317-324). */
+int hmsc_run_verbose(hmsc_state* s, int32_t transient, int32_t samples, int32_t thin,
+                     const int32_t* adaptNf, int32_t iter0, int32_t verbose, int32_t chain,
+                     hmsc_record* rec);
+
+/* Wait for all device work of this chain. */
+int hmsc_sync(hmsc_state* s);
+
+/* Copy a named internal device buffer (fp64) for tests / profiling:
+ * "Z", "E", "XEtaTZ", "Gram", "ZTr", "BL", "BL_prec" ... ; n = element count. */
+int hmsc_debug_get(hmsc_state* s, const char* name, double* out, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HMSC_AMD_H */

@@ -1,0 +1,550 @@
+"""ORACLE — test infrastructure only.
+
+CPU restatement (numpy, fp64) of the reference's Gibbs sweep for Hmsc 3.0-4
+(taddallas/HMSC).  Each function follows one R updater line by line and cites
+it; randomness follows the counter contract of ``oracle/rng.py`` (== the device
+``hmsc_amd/csrc/rng.h``), so given the same state and chain seed the HIP
+updaters must reproduce these draws to fp64 rounding.
+
+Imported only by ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg — never by the product path (``hmsc_amd``).
+
+Parity status: pinned by the reference's own deterministic known answers
+(computeDataParameters sums, WAIC, scaling, shapes — tests/test_oracle_golden.py)
+and statistically by the TD$m golden posterior; the reference's RNG-dependent
+``round(sum(.))`` test values depend on R's Mersenne-Twister + truncnorm /
+MCMCpack / BayesLogit bitstreams and are not reproducible.
+
+State dict keys (mirror R's parList, R/computeInitialParameters.R:256-270):
+  Gamma (nc,nt)  iV (nc,nc)  Beta (nc,ns)  iSigma (ns,)  rho (int, 1-based)
+  Eta [r] (np_r,nf_r)  Lambda [r] (nf_r,ns)  Psi [r] (nf_r,ns)  Delta [r] (nf_r,)
+  Alpha [r] (nf_r,) int 1-based   Z (ny,ns)
+Model dict keys (the hM fields the sampler consumes):
+  X (ny,nc)  Y (ny,ns) NaN=NA  Tr (ns,nt)  Pi (ny,nr) 1-based  distr (ns,4)
+  V0 f0 mGamma UGamma aSigma bSigma  rL [dict(nu,a1,b1,a2,b2,nfMin,nfMax,sDim,xDim)]
+  C (or None), iQg/RQg/detQg (from compute_data_parameters), rhopw
+"""
+import numpy as np
+from scipy.linalg import solve_triangular
+
+from . import rng as R
+
+
+def chol_upper(A):
+    """R's chol(): upper-triangular R with R'R = A."""
+    return np.linalg.cholesky(A).T
+
+
+def chol2inv(Rm):
+    """R's chol2inv(R) = (R'R)^-1."""
+    Ri = solve_triangular(Rm, np.eye(Rm.shape[0]), lower=False)
+    return Ri @ Ri.T
+
+
+def backsolve(Rm, b, transpose=False):
+    """R's backsolve(R, b[, transpose=TRUE])."""
+    return solve_triangular(Rm, b, lower=False, trans=1 if transpose else 0)
+
+
+# ---------------------------------------------------------------------------
+# data parameters — R/computeDataParameters.R:16-45 (phylogeny grid / identity)
+# ---------------------------------------------------------------------------
+def compute_data_parameters(model):
+    C = model.get("C")
+    ns = model["Y"].shape[1]
+    rhopw = model["rhopw"]
+    if C is not None:
+        nrho = rhopw.shape[0]
+        Qg = np.empty((nrho, ns, ns))
+        iQg = np.empty_like(Qg)
+        RQg = np.empty_like(Qg)
+        detQg = np.empty(nrho)
+        iC = chol2inv(chol_upper(C)) if np.any(rhopw[:, 0] < 0) else None
+        for g in range(nrho):                                  # :23-38
+            rho = rhopw[g, 0]
+            rhoC = rho * C if rho >= 0 else (-rho) * iC
+            Q = rhoC + (1 - abs(rho)) * np.eye(ns)
+            RQ = chol_upper(Q)
+            Qg[g], iQg[g], RQg[g] = Q, chol2inv(RQ), RQ
+            detQg[g] = 2 * np.sum(np.log(np.diag(RQ)))
+    else:                                                      # :40-45
+        Qg = np.eye(ns)[None]
+        iQg = np.eye(ns)[None]
+        RQg = np.eye(ns)[None]
+        detQg = np.zeros(1)
+    return dict(Qg=Qg, iQg=iQg, RQg=RQg, detQg=detQg)
+
+
+# ---------------------------------------------------------------------------
+# linear predictor — R/updateZ.R:11-34 (repeated in updateEta/InvSigma/Gamma2)
+# ---------------------------------------------------------------------------
+def eta_full(st, model, r):
+    return st["Eta"][r][model["Pi"][:, r] - 1, :]
+
+
+def l_ran(st, model, r):
+    return eta_full(st, model, r) @ st["Lambda"][r]
+
+
+def linear_predictor(st, model):
+    E = model["X"] @ st["Beta"]
+    for r in range(model["Pi"].shape[1]):
+        E = E + l_ran(st, model, r)
+    return E
+
+
+# ---------------------------------------------------------------------------
+# updateZ — R/updateZ.R:4-94 (normal :40-41, probit :43-63, NA :92)
+# ---------------------------------------------------------------------------
+def update_z(st, model, rng, it, Y=None):
+    Y = model["Y"] if Y is None else Y
+    ny, ns = Y.shape
+    E = linear_predictor(st, model)
+    sd = st["iSigma"] ** -0.5
+    idx = (np.arange(ny)[:, None] + ny * np.arange(ns)[None, :]).astype(np.uint64)
+    fam = model["distr"][:, 0]
+    if np.any(fam == 3):
+        raise NotImplementedError("Poisson updateZ (Polya-Gamma) is a 'next' row (SURVEY.md §8 f3)")
+    na = np.isnan(Y)
+    Z = np.empty((ny, ns))
+    normal_cols = fam == 1
+    Z[:, normal_cols] = Y[:, normal_cols]
+    u = rng.uniforms(idx, 0, R.S_Z, it)[0]
+    s = np.where(Y == 1, 1.0, -1.0)
+    alpha = -s * E / sd[None, :]
+    w = R.trunc_normal_lower(alpha, u)
+    zp = E + sd[None, :] * s * w
+    probit_cols = fam == 2
+    Z[:, probit_cols] = zp[:, probit_cols]
+    if na.any():
+        nz = E + sd[None, :] * rng.normal(idx, 0, R.S_Z, it)
+        Z[na] = nz[na]
+    return Z
+
+
+# ---------------------------------------------------------------------------
+# updateBetaLambda — R/updateBetaLambda.R:8-157
+# ---------------------------------------------------------------------------
+def _xeta_and_prior(st, model):
+    nr = model["Pi"].shape[1]
+    X = model["X"]
+    cols = [X] + [eta_full(st, model, r) for r in range(nr)]          # :21-41
+    XEta = np.concatenate(cols, axis=1)
+    ns = model["Y"].shape[1]
+    pl = []
+    for r in range(nr):                                               # :42-53
+        tau = np.cumprod(st["Delta"][r])
+        pl.append(st["Psi"][r] * tau[:, None])
+    priorLambda = np.concatenate(pl, axis=0) if pl else np.zeros((0, ns))
+    return XEta, priorLambda
+
+
+def beta_lambda_moments(st, model, data_par=None):
+    """Per-species precision iU_j and mean m_j of the C=NULL branch (:76-123)."""
+    Y, Z = model["Y"], st["Z"]
+    nc = model["X"].shape[1]
+    ns = Y.shape[1]
+    XEta, priorLambda = _xeta_and_prior(st, model)
+    K = XEta.shape[1]
+    Mu = np.concatenate([st["Gamma"] @ model["Tr"].T, np.zeros((K - nc, ns))])   # :62
+    iS = st["iSigma"]
+    Yx = ~np.isnan(Y)
+    precs = np.empty((ns, K, K))
+    means = np.empty((K, ns))
+    G = XEta.T @ XEta                                                  # :65
+    XS = XEta.T @ Z                                                    # :66
+    for j in range(ns):
+        P = np.zeros((K, K))
+        P[:nc, :nc] = st["iV"]                                         # :83-84
+        P[np.diag_indices(K)] = np.concatenate([np.diag(st["iV"]), priorLambda[:, j]])  # :89
+        if Yx[:, j].all():
+            iU = P + G * iS[j]                                         # :92
+            isXTS = XS[:, j] * iS[j]
+        else:                                                          # :103-117
+            o = Yx[:, j]
+            iU = P + (XEta[o].T @ XEta[o]) * iS[j]
+            isXTS = (XEta[o].T @ Z[o, j]) * iS[j]
+        precs[j] = iU
+        means[:, j] = np.linalg.solve(iU, P @ Mu[:, j] + isXTS)        # :98-100
+    return precs, means
+
+
+def update_beta_lambda(st, model, rng, it, data_par=None, zero_noise=False):
+    nc = model["X"].shape[1]
+    ns = model["Y"].shape[1]
+    nr = model["Pi"].shape[1]
+    if model.get("C") is not None:
+        BL = _beta_lambda_phylo(st, model, rng, it, data_par, zero_noise)
+    else:
+        precs, means = beta_lambda_moments(st, model)
+        K = means.shape[0]
+        BL = np.empty((K, ns))
+        for j in range(ns):
+            RiU = chol_upper(precs[j])                                 # :98
+            xi = np.zeros(K) if zero_noise else rng.normal(j, np.arange(K), R.S_BETALAMBDA, it)
+            BL[:, j] = means[:, j] + backsolve(RiU, xi)                # :101
+    Beta = BL[:nc].copy()                                              # :148
+    Lambda = []
+    off = nc
+    for r in range(nr):                                                # :149-155
+        nf = st["Lambda"][r].shape[0]
+        Lambda.append(BL[off:off + nf].copy())
+        off += nf
+    return Beta, Lambda
+
+
+def _beta_lambda_phylo(st, model, rng, it, data_par, zero_noise):
+    """Dense branch with phylogeny, R/updateBetaLambda.R:124-147 (species-fastest vec)."""
+    Z = st["Z"]
+    nc = model["X"].shape[1]
+    ns = Z.shape[1]
+    XEta, priorLambda = _xeta_and_prior(st, model)
+    K = XEta.shape[1]
+    iQ = data_par["iQg"][st["rho"] - 1]
+    Mu = np.concatenate([st["Gamma"] @ model["Tr"].T, np.zeros((K - nc, ns))])
+    iS = st["iSigma"]
+    G = XEta.T @ XEta
+    isXTS = (XEta.T @ Z) * iS[None, :]
+    P = np.zeros((K * ns, K * ns))
+    P[:nc * ns, :nc * ns] = np.kron(st["iV"], iQ)                      # :126
+    P[nc * ns:, nc * ns:] = np.diag(priorLambda.reshape(-1))           # Diagonal(x=t(priorLambda))
+    RiU = chol_upper(np.kron(G, np.diag(iS)) + P)                      # :129
+    m1 = backsolve(RiU, P @ Mu.reshape(-1) + isXTS.reshape(-1), transpose=True)   # :145
+    xi = np.zeros(K * ns) if zero_noise else \
+        rng.normal(np.tile(np.arange(ns), K), np.repeat(np.arange(K), ns), R.S_BETALAMBDA, it)
+    return backsolve(RiU, m1 + xi).reshape(K, ns)                      # :146 byrow=TRUE
+
+
+# ---------------------------------------------------------------------------
+# Wishart (MCMCpack::rwish restated) — Bartlett construction, upper Z
+# ---------------------------------------------------------------------------
+def rwish(v, S, rng, it, s_diag, s_off, zero_noise=False):
+    p = S.shape[0]
+    CC = chol_upper(S)
+    Zm = np.zeros((p, p))
+    df = v - np.arange(p)                                              # v:(v-p+1)
+    Zm[np.diag_indices(p)] = np.sqrt(2.0 * rng.gamma_std(np.arange(p), s_diag, it, df / 2.0))
+    iu = np.triu_indices(p, 1)
+    if p > 1 and not zero_noise:
+        Zm[iu] = rng.normal(iu[0] + p * iu[1], 0, s_off, it)
+    ZC = Zm @ CC
+    return ZC.T @ ZC
+
+
+# ---------------------------------------------------------------------------
+# updateGammaV — R/updateGammaV.R:4-34
+# ---------------------------------------------------------------------------
+def update_gamma_v(st, model, rng, it, data_par=None, zero_noise=False):
+    Beta, Gamma, Tr = st["Beta"], st["Gamma"], model["Tr"]
+    ns, nc, nt = Beta.shape[1], Beta.shape[0], Tr.shape[1]
+    if model.get("C") is None:                                         # :10-12
+        iQ = RQ = None
+    else:
+        iQ = data_par["iQg"][st["rho"] - 1]
+        RQ = data_par["RQg"][st["rho"] - 1]
+    E = Beta - Gamma @ Tr.T                                            # :16-17
+    A = E @ E.T if iQ is None else E @ (iQ @ E.T)                      # :18 (identity special-cased)
+    Vn = chol2inv(chol_upper(A + model["V0"]))                         # :19
+    iV = rwish(model["f0"] + ns, Vn, rng, it, R.S_WISHART_DIAG, R.S_WISHART_OFF)   # :20
+    iUGamma = np.linalg.inv(model["UGamma"])
+    TrQ = Tr if RQ is None else backsolve(RQ, Tr, transpose=True)
+    RG = chol_upper(iUGamma + np.kron(TrQ.T @ TrQ, iV))                # :29
+    QTr = Tr if iQ is None else iQ @ Tr
+    rhs = iUGamma @ model["mGamma"] + ((iV @ Beta) @ QTr).reshape(-1, order="F")
+    mg = chol2inv(RG) @ rhs                                            # :30
+    xi = np.zeros(nc * nt) if zero_noise else rng.normal(np.arange(nc * nt), 0, R.S_GAMMAV, it)
+    Gamma = (mg + backsolve(RG, xi)).reshape(nc, nt, order="F")        # :31
+    return Gamma, iV
+
+
+def gamma_v_moments(st, model, iV):
+    """Gamma conditional mean/precision given the new iV (C=NULL)."""
+    Beta, Tr = st["Beta"], model["Tr"]
+    iUGamma = np.linalg.inv(model["UGamma"])
+    prec = iUGamma + np.kron(Tr.T @ Tr, iV)
+    rhs = iUGamma @ model["mGamma"] + ((iV @ Beta) @ Tr).reshape(-1, order="F")
+    return prec, np.linalg.solve(prec, rhs)
+
+
+# ---------------------------------------------------------------------------
+# updateGamma2 — R/updateGamma2.R:6-60 (acts only if C is NULL and all iSigma==1)
+# ---------------------------------------------------------------------------
+def gamma2_moments(st, model):
+    X, Tr, iV = model["X"], model["Tr"], st["iV"]
+    nc, nt = X.shape[1], Tr.shape[1]
+    S = st["Z"].copy()
+    for r in range(model["Pi"].shape[1]):                              # :20-33
+        S -= l_ran(st, model, r)
+    inv = lambda A: chol2inv(chol_upper(A))                            # noqa: E731
+    cholL = lambda A: chol_upper(A).T                                  # noqa: E731
+    iUGamma = np.linalg.inv(model["UGamma"])
+    iV0 = iUGamma[:nc, :nc]                                            # :37
+    V0 = inv(iV0)
+    XX = X.T @ X
+    TT = Tr.T @ Tr
+    iP = inv(iV + XX)
+    LiP = cholL(iP)
+    t1 = iV @ LiP
+    Rm = inv(np.kron(np.eye(nt), iV0) + np.kron(TT, iV - t1 @ t1.T))   # :44
+    LR = cholL(Rm)
+    XZT = X.T @ (S @ Tr)                                               # :46
+    iPXZT = iP @ XZT
+    tmp = np.kron(TT, V0 @ XX @ iP @ iV)
+    muG = (V0 @ (XZT - XX @ iPXZT)).reshape(-1, order="F") - tmp @ Rm @ (iV @ iPXZT).reshape(-1, order="F")
+    V0Xt = V0 @ X.T
+    t2 = V0 @ XX @ LiP
+    t3 = tmp @ LR
+    SigmaG = np.kron(np.eye(nt), V0) - np.kron(TT, V0Xt @ V0Xt.T - t2 @ t2.T) + t3 @ t3.T   # :50
+    return muG, SigmaG
+
+
+def update_gamma2(st, model, rng, it, zero_noise=False):
+    if model.get("C") is not None or not np.all(st["iSigma"] == 1):  # :35-36
+        return st["Gamma"]
+    nc, nt = model["X"].shape[1], model["Tr"].shape[1]
+    muG, SigmaG = gamma2_moments(st, model)
+    LS = chol_upper(SigmaG).T
+    xi = np.zeros(nc * nt) if zero_noise else rng.normal(np.arange(nc * nt), 0, R.S_GAMMA2, it)
+    return (muG + LS @ xi).reshape(nc, nt, order="F")                 # :53-54
+
+
+# ---------------------------------------------------------------------------
+# updateLambdaPriors — R/updateLambdaPriors.R:3-53 (matrix branch :21-33)
+# ---------------------------------------------------------------------------
+def update_lambda_priors(st, model, rng, it):
+    Psi, Delta = [], []
+    ns = model["Y"].shape[1]
+    for r, rl in enumerate(model["rL"]):
+        nu, a1, b1, a2, b2 = rl["nu"], rl["a1"], rl["b1"], rl["a2"], rl["b2"]
+        delta = st["Delta"][r].astype(np.float64).copy()
+        lam = st["Lambda"][r]
+        nf = lam.shape[0]
+        tau = np.cumprod(delta)                                        # :17
+        lam2 = lam ** 2
+        aPsi = nu / 2 + 0.5
+        bPsi = nu / 2 + 0.5 * lam2 * tau[:, None]                      # :22
+        hh, jj = np.meshgrid(np.arange(nf), np.arange(ns), indexing="ij")
+        psi = rng.gamma(hh + nf * jj, R.S_PSI + R.LEVEL_STRIDE * r, it, aPsi, bPsi)   # :23
+        M = psi * lam2
+        rs = M.sum(axis=1)
+        ad = a1 + 0.5 * ns * nf                                        # :25
+        bd = b1 + 0.5 * np.sum(tau * rs) / delta[0]                    # :26
+        delta[0] = rng.gamma(0, R.S_DELTA + R.LEVEL_STRIDE * r, it, ad, bd)
+        for h in range(1, nf):                                         # :28-32
+            tau = np.cumprod(delta)
+            ad = a2 + 0.5 * ns * (nf - h)
+            bd = b2 + 0.5 * np.sum(tau[h:] * rs[h:]) / delta[h]
+            delta[h] = rng.gamma(h, R.S_DELTA + R.LEVEL_STRIDE * r, it, ad, bd)
+        Psi.append(psi)
+        Delta.append(delta)
+    return Psi, Delta
+
+
+# ---------------------------------------------------------------------------
+# updateEta — R/updateEta.R:4-212, non-spatial xDim=0 branch (:42-92)
+# ---------------------------------------------------------------------------
+def eta_unit_moments(st, model, r, S):
+    """Per-unit precision Q_q and mean mu_q for level r given residual S."""
+    Y = model["Y"]
+    lam = st["Lambda"][r]
+    nf = lam.shape[0]
+    iS = st["iSigma"]
+    Pi_r = model["Pi"][:, r] - 1
+    npr = st["Eta"][r].shape[0]
+    Yx = ~np.isnan(Y)
+    LamInvSigLam = (lam * iS[None, :]) @ lam.T                         # :45
+    precs = np.empty((npr, nf, nf))
+    means = np.empty((npr, nf))
+    lamT = (lam * iS[None, :]).T                                       # lambda*iSigma, transposed
+    for q in range(npr):
+        rows = np.nonzero(Pi_r == q)[0]
+        if Yx[rows].all():                                             # :46-57 and :75-79
+            Q = np.eye(nf) + LamInvSigLam * len(rows)
+            b = S[rows].sum(axis=0) @ lamT
+        else:                                                          # :59-70 and :80-87
+            Q = np.eye(nf)
+            b = np.zeros(nf)
+            for p in rows:
+                w = iS * Yx[p]
+                Q = Q + (lam * w[None, :]) @ lam.T
+                b = b + (np.where(Yx[p], S[p], 0.0) * iS) @ lam.T
+        precs[q] = Q
+        means[q] = np.linalg.solve(Q, b)
+    return precs, means
+
+
+def update_eta(st, model, rng, it, zero_noise=False):
+    nr = model["Pi"].shape[1]
+    st = dict(st)
+    Eta = list(st["Eta"])
+    LFix = model["X"] @ st["Beta"]                                     # :11-20
+    for r in range(nr):
+        if model["rL"][r].get("sDim", 0) > 0:
+            raise NotImplementedError("spatial updateEta is a 'next' row (SURVEY.md §8 f2)")
+        S = st["Z"] - LFix                                             # :31-37
+        for r2 in range(nr):
+            if r2 != r:
+                S = S - Eta[r2][model["Pi"][:, r2] - 1] @ st["Lambda"][r2]
+        st["Eta"] = Eta
+        precs, means = eta_unit_moments(st, model, r, S)
+        npr, nf = means.shape
+        eta = np.empty((npr, nf))
+        for q in range(npr):
+            RiV = chol_upper(precs[q])
+            xi = np.zeros(nf) if zero_noise else rng.normal(q, np.arange(nf), R.S_ETA + R.LEVEL_STRIDE * r, it)
+            eta[q] = means[q] + backsolve(RiV, xi)                     # :56,69,90
+        Eta[r] = eta
+    return Eta
+
+
+# ---------------------------------------------------------------------------
+# updateInvSigma — R/updateInvSigma.R:3-43
+# ---------------------------------------------------------------------------
+def update_inv_sigma(st, model, rng, it):
+    distr = model["distr"]
+    iS = st["iSigma"].copy()
+    ind = distr[:, 1] == 1                                             # :4
+    if ind.any():
+        Y = model["Y"]
+        Eps = st["Z"] - linear_predictor(st, model)                    # :31-34
+        Yx = ~np.isnan(Y)
+        shape = model["aSigma"] + Yx.sum(axis=0) / 2                   # :37-38
+        rate = model["bSigma"] + np.sum(np.where(Yx, Eps, 0.0) ** 2, axis=0) / 2   # :39
+        j = np.nonzero(ind)[0]
+        iS[j] = rng.gamma(j, R.S_INVSIGMA, it, shape[j], rate[j])      # :40
+    return iS
+
+
+# ---------------------------------------------------------------------------
+# updateNf — R/updateNf.R:3-70 (reproduces the setdiff(1:nf, logical) quirk, :56)
+# ---------------------------------------------------------------------------
+def update_nf(st, model, r, rng, it):
+    rl = model["rL"][r]
+    eta, lam, psi, delta, alpha = (st["Eta"][r], st["Lambda"][r], st["Psi"][r],
+                                   st["Delta"][r], st["Alpha"][r])
+    c0, c1, epsilon, prop = 1.0, 0.0005, 1e-3, 1.0                      # :10-13
+    prob = 1 / np.exp(c0 + c1 * it)
+    stream = R.LEVEL_STRIDE * r
+    u = rng.uniforms(0, 0, R.S_NF + stream, it)[0]
+    if u < prob:                                                       # :16
+        ns = lam.shape[1]
+        nf = lam.shape[0]
+        npr = eta.shape[0]
+        small = np.abs(lam) < epsilon
+        smallProp = small.mean(axis=1)
+        indRedundant = smallProp >= prop
+        numRedundant = int(indRedundant.sum())
+        if nf < rl["nfMax"] and it > 20 and numRedundant == 0 and np.all(smallProp < 0.995):
+            nf += 1                                                    # :26-54
+            eta = np.concatenate([eta, rng.normal(np.arange(npr), 0, R.S_NF_ETA + stream, it)[:, None]], axis=1)
+            alpha = np.concatenate([alpha, [1]])
+            lam = np.concatenate([lam, np.zeros((1, ns))], axis=0)
+            newpsi = rng.gamma(np.arange(ns), R.S_NF_PSI + stream, it, rl["nu"] / 2, rl["nu"] / 2)
+            psi = np.concatenate([psi, newpsi[None, :]], axis=0)
+            delta = np.concatenate([delta, [rng.gamma(0, R.S_NF_DELTA + stream, it, rl["a2"], rl["b2"])]])
+        elif numRedundant > 0 and nf > rl["nfMin"]:                    # :55-68
+            # setdiff(1:nf, indRedundant) with a logical vector: TRUE->1, FALSE->0,
+            # so factor 1 is dropped whenever any factor is redundant (quirk kept).
+            keep = [k for k in range(1, nf + 1) if k not in set(indRedundant.astype(int).tolist())]
+            keep = np.array(keep) - 1
+            eta, alpha, lam, psi, delta = eta[:, keep], alpha[keep], lam[keep], psi[keep], delta[keep]
+    return eta, lam, alpha, psi, delta
+
+
+# ---------------------------------------------------------------------------
+# computeInitialParameters — R/computeInitialParameters.R:17-273 (initPar=NULL)
+# ---------------------------------------------------------------------------
+def compute_initial_parameters(model, rng, nf=None):
+    it = 0
+    X, Tr, distr = model["X"], model["Tr"], model["distr"]
+    nc, nt, ns = X.shape[1], Tr.shape[1], Tr.shape[0]
+    LU = np.linalg.cholesky(model["UGamma"])
+    Gamma = (model["mGamma"] + LU @ rng.normal(np.arange(nc * nt), 0, R.S_INIT_GAMMA, it)).reshape(nc, nt, order="F")  # :85
+    iV0 = np.linalg.inv(model["V0"])
+    V = np.linalg.inv(rwish(model["f0"], iV0, rng, it, R.S_INIT_V_DIAG, R.S_INIT_V_OFF))   # :91 riwish
+    Mu = Gamma @ Tr.T
+    LV = np.linalg.cholesky(V)
+    jj, kk = np.meshgrid(np.arange(ns), np.arange(nc))
+    Beta = Mu + LV @ rng.normal(jj, kk, R.S_INIT_BETA, it)             # :97-101
+    sigma = np.ones(ns)                                                # :111-126
+    for j in range(ns):
+        if distr[j, 1] == 1:
+            sigma[j] = rng.gamma(j, R.S_INIT_SIGMA, it, model["aSigma"][j], model["bSigma"][j])
+        elif distr[j, 0] == 3:
+            sigma[j] = 1e-2
+    Eta, Lambda, Psi, Delta, Alpha = [], [], [], [], []
+    for r, rl in enumerate(model["rL"]):
+        nfr = int(rl["nfMin"]) if nf is None else int(nf[r])
+        s = R.LEVEL_STRIDE * r
+        d = np.empty(nfr)
+        d[0] = rng.gamma(0, R.S_INIT_DELTA + s, it, rl["a1"], rl["b1"])   # :175
+        if nfr > 1:
+            d[1:] = rng.gamma(np.arange(1, nfr), R.S_INIT_DELTA + s, it, rl["a2"], rl["b2"])
+        hh, jj2 = np.meshgrid(np.arange(nfr), np.arange(ns), indexing="ij")
+        psi = rng.gamma(hh + nfr * jj2, R.S_INIT_PSI + s, it, rl["nu"] / 2, rl["nu"] / 2)  # :183
+        tau = np.cumprod(d)
+        lam = rng.normal(hh + nfr * jj2, 0, R.S_INIT_LAMBDA + s, it) * np.sqrt(psi * tau[:, None]) ** -1  # :189-193
+        npr = int(model["np"][r])
+        qq, kk2 = np.meshgrid(np.arange(npr), np.arange(nfr), indexing="ij")
+        eta = rng.normal(qq, kk2, R.S_INIT_ETA + s, it)                # :207
+        Eta.append(eta), Lambda.append(lam), Psi.append(psi), Delta.append(d)
+        Alpha.append(np.ones(nfr, dtype=np.int64))
+    st = dict(Gamma=Gamma, iV=np.linalg.inv(V), V=V, Beta=Beta, iSigma=1.0 / sigma, Eta=Eta,
+              Lambda=Lambda, Psi=Psi, Delta=Delta, Alpha=Alpha, rho=1)
+    st["Z"] = update_z(st, model, rng, it, Y=model.get("Yraw", model["Y"]))   # :254 uses hM$Y
+    return st
+
+
+# ---------------------------------------------------------------------------
+# one sweep — R/sampleMcmc.R:219-306 (fixed block order)
+# ---------------------------------------------------------------------------
+def sweep(st, model, rng, it, updater=None, data_par=None, adapt_nf=None):
+    up = updater or {}
+    on = lambda name: up.get(name, True) is not False                  # noqa: E731  identical(x, FALSE)
+    st = dict(st)
+    nr = model["Pi"].shape[1]
+    if on("Gamma2"):
+        st["Gamma"] = update_gamma2(st, model, rng, it)
+    if on("GammaEta"):
+        raise NotImplementedError("updateGammaEta is a 'next' row (SURVEY.md §8 f1); pass updater GammaEta=False")
+    if on("BetaLambda"):
+        st["Beta"], st["Lambda"] = update_beta_lambda(st, model, rng, it, data_par)
+    if on("GammaV"):
+        st["Gamma"], st["iV"] = update_gamma_v(st, model, rng, it, data_par)
+    if model.get("C") is not None and on("Rho"):
+        st["rho"] = update_rho(st, model, rng, it, data_par)
+    if on("LambdaPriors"):
+        st["Psi"], st["Delta"] = update_lambda_priors(st, model, rng, it)
+    if on("Eta"):
+        st["Eta"] = update_eta(st, model, rng, it)
+    if on("InvSigma"):
+        st["iSigma"] = update_inv_sigma(st, model, rng, it)
+    if on("Z"):
+        st["Z"] = update_z(st, model, rng, it)
+    for r in range(nr):                                                # :296-306
+        if adapt_nf is not None and it <= adapt_nf[r]:
+            e, l, a, p, d = update_nf(st, model, r, rng, it)
+            st["Eta"] = list(st["Eta"]); st["Eta"][r] = e
+            st["Lambda"] = list(st["Lambda"]); st["Lambda"][r] = l
+            st["Alpha"] = list(st["Alpha"]); st["Alpha"][r] = a
+            st["Psi"] = list(st["Psi"]); st["Psi"][r] = p
+            st["Delta"] = list(st["Delta"]); st["Delta"][r] = d
+    return st
+
+
+# ---------------------------------------------------------------------------
+# updateRho — R/updateRho.R:1-25 (phylogeny grid; categorical by inverse CDF)
+# ---------------------------------------------------------------------------
+def update_rho(st, model, rng, it, data_par):
+    Beta, Gamma, iV, Tr = st["Beta"], st["Gamma"], st["iV"], model["Tr"]
+    rhopw = model["rhopw"]
+    nc = Beta.shape[0]
+    E = (Beta - Gamma @ Tr.T).T
+    RiV = chol_upper(iV)
+    E = E @ RiV.T                                                      # tcrossprod(E, RiV)
+    v = np.array([np.sum(backsolve(data_par["RQg"][g], E, transpose=True) ** 2)
+                  for g in range(rhopw.shape[0])])
+    logLike = np.log(rhopw[:, 1]) - 0.5 * nc * data_par["detQg"] - 0.5 * v
+    like = np.exp(logLike - logLike.max())
+    u = rng.uniforms(0, 0, R.S_RHO, it)[0]
+    return int(np.searchsorted(np.cumsum(like), u * like.sum(), side="right")) + 1

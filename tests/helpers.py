@@ -1,0 +1,70 @@
+"""Shared test helpers: synthetic Hmsc models and the hM -> oracle-model mapping."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+import hmsc_amd as H  # noqa: E402
+from oracle import hmsc_oracle as O  # noqa: E402
+
+
+def synthetic_model(ny=200, ns=30, nc=4, nf=3, seed=1, na_frac=0.0, n_normal=0, units=None, nr=1,
+                    nf_fit=None, nt=1, yscale=False):
+    """Probit (optionally mixed normal) JSDM generated like BASELINE.md's synthetic config."""
+    rng = np.random.default_rng(seed)
+    X = np.column_stack([np.ones(ny), rng.standard_normal((ny, nc - 1))])
+    Tr = np.column_stack([np.ones(ns)] + [rng.standard_normal(ns) for _ in range(nt - 1)]) if nt > 1 else None
+    G = rng.normal(0, 0.5, (nc, 1))
+    B = G + rng.normal(0, 0.3, (nc, ns))
+    L = X @ B
+    sd = {}
+    levels = {}
+    ranLevels = {}
+    for r in range(nr):
+        npr = ny if units is None else units[r]
+        pi = np.arange(ny) % npr if npr < ny else np.arange(ny)
+        rng.shuffle(pi) if npr < ny else None
+        eta = rng.standard_normal((npr, nf))
+        lam = rng.standard_normal((nf, ns)) / (np.arange(1, nf + 1)[:, None])
+        L = L + eta[pi] @ lam
+        name = f"lev{r}"
+        sd[name] = np.array([f"u{k}" for k in pi])
+        rl = H.HmscRandomLevel(units=sd[name])
+        nff = nf if nf_fit is None else nf_fit
+        H.setPriors(rl, nfMin=nff, nfMax=nff)
+        ranLevels[name] = rl
+        levels[name] = pi
+    Ylat = L + rng.standard_normal((ny, ns))
+    Y = (Ylat > 0).astype(float)
+    distr = ["probit"] * ns
+    for j in range(n_normal):
+        Y[:, j] = Ylat[:, j] * 2.0 + 1.0
+        distr[j] = "normal"
+    if na_frac > 0:
+        mask = rng.random((ny, ns)) < na_frac
+        Y[mask] = np.nan
+    import pandas as pd
+    studyDesign = pd.DataFrame(sd) if nr > 0 else None
+    covn = ["(Intercept)"] + [f"x{k}" for k in range(1, nc)]
+    hM = H.Hmsc(Y=Y, X=X, covNames=covn, XScale=True, YScale=yscale, Tr=Tr, distr=distr,
+                studyDesign=studyDesign, ranLevels=ranLevels if nr > 0 else None)
+    return hM
+
+
+def oracle_model(hM):
+    m = dict(X=hM.XScaled, Y=hM.YScaled, Yraw=hM.Y, Tr=hM.TrScaled, Pi=hM.Pi, np=hM.np, distr=hM.distr,
+             V0=hM.V0, f0=hM.f0, mGamma=hM.mGamma, UGamma=hM.UGamma, aSigma=hM.aSigma, bSigma=hM.bSigma,
+             rhopw=hM.rhopw, C=hM.C,
+             rL=[dict(nu=rl.nu, a1=rl.a1, b1=rl.b1, a2=rl.a2, b2=rl.b2, nfMin=rl.nfMin, nfMax=rl.nfMax,
+                      sDim=rl.sDim, xDim=rl.xDim) for rl in (hM.rL or [])])
+    return m
+
+
+def rel_err(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.max(np.abs(a - b)) / max(1e-300, np.max(np.abs(b))))
