@@ -1,0 +1,217 @@
+#!/usr/bin/env python
+"""bench.py — Gibbs sweeps/sec + Beta ESS/sec on the synthetic probit JSDM
+(BASELINE.json config 4: ny=10k sites, ns=1k species, nc=20, nf=10), MI355X.
+
+A "step" is one Gibbs sweep of Hmsc's sampleMcmc (R/sampleMcmc.R:219-315, all
+default updaters except GammaEta=FALSE as BASELINE.md §2 prescribes), including the
+per-sample record (the reference records every sweep at thin=1).
+
+    python bench.py [--gpus N --steps K --warmup W] [--mode chains|sharded]
+
+N>1 is launched by torch.distributed.run, one rank per GPU:
+  * chains  (default): one independent chain per GPU, no communication (the
+    reference's PSOCK chain farm, R/sampleMcmc.R:329-345) -> weak scaling;
+    value = total chain-sweeps/sec over all GPUs.
+  * sharded: ONE chain, species sharded over the GPUs, RCCL all-reduce of the
+    sufficient statistics inside the C library -> strong scaling.
+Rank 0 prints one JSON line.  The CPU baseline (rank 0, N=1 only) times the
+oracle restatement (oracle/, numpy fp64, 1 BLAS thread) on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import hmsc_amd as H  # noqa: E402
+from hmsc_amd.workloads import synthetic_probit  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=1000)
+    p.add_argument("--warmup", type=int, default=100)
+    p.add_argument("--mode", choices=["chains", "sharded"], default="chains")
+    p.add_argument("--ny", type=int, default=10000)
+    p.add_argument("--ns", type=int, default=1000)
+    p.add_argument("--nc", type=int, default=20)
+    p.add_argument("--nf", type=int, default=10)
+    p.add_argument("--cpu-seconds", type=float, default=20.0)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_r01.json"))
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    import torch
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    torch_cuda = torch.cuda.is_available()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def sync(ch):
+        ch.sync()
+        if torch_cuda:
+            torch.cuda.synchronize()
+
+    hM = synthetic_probit(ny=args.ny, ns=args.ns, nc=args.nc, nf=args.nf)
+    upd = {"GammaEta": False}
+    if args.mode == "sharded" and world > 1:
+        cid = None
+        if rank == 0:
+            buf = np.zeros(128, dtype=np.uint8)
+            H._lib.check(H._lib.lib().hmsc_comm_unique_id(buf.ctypes.data))
+            cid = bytes(buf)
+        obj = [cid]
+        dist.broadcast_object_list(obj, src=0)
+        ch = H.Chain(hM, 1234567, device=local, updater=upd, rank=rank, nranks=world, comm_id=obj[0])
+    else:
+        ch = H.Chain(hM, 1234567 + 7919 * rank, device=local, updater=upd)
+    ch.init([args.nf])
+    ch.run(transient=args.warmup, samples=0, adaptNf=[0], record=False)
+    ch.profile(True)
+    barrier()
+    sync(ch)
+    t0 = time.perf_counter()
+    rec = ch.run(transient=0, samples=args.steps, thin=1, adaptNf=[0], iter0=args.warmup, record=True)
+    sync(ch)
+    barrier()
+    t_run = time.perf_counter() - t0
+    kern = {}
+    for name in ("z", "zl", "betalambda", "eta_unit", "sweep"):
+        tot, n = ch.profile_get(name)
+        kern[name] = dict(total_ms=tot, launches=n, avg_us=1e3 * tot / max(1, n))
+    ch.profile(False)
+
+    # Beta ESS (coda::effectiveSize restated) over this rank's Beta entries
+    beta = rec["Beta"].reshape(args.steps, -1)
+    ess_local = H.effectiveSize(beta)
+    tmax = t_run
+    if dist is not None:
+        t = torch.tensor([t_run], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tmax = float(t.item())
+        gathered = [None] * world
+        dist.all_gather_object(gathered, ess_local)
+        if args.mode == "sharded":
+            ess_all = np.concatenate(gathered)       # disjoint species blocks of one chain
+        else:
+            ess_all = np.sum(np.stack(gathered), axis=0)  # sum over chains per Beta entry
+    else:
+        ess_all = ess_local
+    if rank != 0:
+        return
+    ny, ns = args.ny, args.ns
+    sweeps = args.steps * (world if args.mode == "chains" else 1)
+    value = sweeps / tmax
+    ess_rate_median = float(np.median(ess_all)) / tmax
+    ess_rate_min = float(np.min(ess_all)) / tmax
+
+    # roofline: the dominant kernel of the sweep, algorithmic bytes per launch
+    algo_bytes = {
+        # fused updateZ: writes Z (fp64) + reads the int8 Y code, ny*ns each (R/updateZ.R)
+        "z": ny * (ns // (world if args.mode == "sharded" else 1)) * (8 + 1),
+        # updateEta pass: reads Z once (R/updateEta.R:55)
+        "zl": ny * (ns // (world if args.mode == "sharded" else 1)) * 8,
+    }
+    dom = max(("z", "zl", "betalambda", "eta_unit"), key=lambda k: kern[k]["total_ms"])
+    roof_kernel = dom if dom in algo_bytes else max(algo_bytes, key=lambda k: kern[k]["total_ms"])
+    avg_s = kern[roof_kernel]["avg_us"] * 1e-6
+    achieved = algo_bytes[roof_kernel] / avg_s / 1e9
+    traffic = None
+    if os.path.exists(args.pmc_json):
+        try:
+            traffic = json.load(open(args.pmc_json)).get(roof_kernel, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(hM, args, float(np.median(ess_local)) / args.steps)
+
+    out = {
+        "metric": "Gibbs sweeps/sec + Beta ESS/sec at ny=10k, ns=1k, nf=10; 1/2/4/8 MI355X",
+        "value": round(value, 3),
+        "unit": "sweeps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * tmax / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak" if args.mode == "chains" else "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (BASELINE.md §2 generator, seed 20261015)",
+        "config": {"workload": f"synthetic probit JSDM ny={ny} ns={ns} nc={args.nc} nf={args.nf}, "
+                               f"1 sample-level random level, updater GammaEta=FALSE, record every sweep",
+                   "ny": ny, "ns": ns, "nc": args.nc, "nf": args.nf,
+                   "parallelism": (f"{world} independent chains, one per GPU" if args.mode == "chains"
+                                   else f"1 chain species-sharded over {world} GPUs (RCCL)")},
+        "beta_ess_per_s": {"median": round(ess_rate_median, 3), "min": round(ess_rate_min, 3),
+                           "n_beta": int(ess_all.size), "ess_median": float(np.median(ess_all))},
+        "roofline": {"kernel": roof_kernel, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "algorithmic_bytes_per_launch": algo_bytes[roof_kernel],
+                     "avg_launch_us": round(kern[roof_kernel]["avg_us"], 2)},
+        "kernels_us": {k: round(v["avg_us"], 2) for k, v in kern.items()},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+
+
+def cpu_baseline(hM, args, ess_per_sweep):
+    """Oracle restatement (numpy fp64) timed on this host on a bounded sample."""
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:  # pragma: no cover
+        threadpool_limits = None
+    from oracle import hmsc_oracle as O
+    from oracle.rng import Rng
+    ctx = threadpool_limits(limits=1) if threadpool_limits else None
+    try:
+        if ctx:
+            ctx.__enter__()
+        m = dict(X=hM.XScaled, Y=hM.YScaled, Yraw=hM.Y, Tr=hM.TrScaled, Pi=hM.Pi, np=hM.np, distr=hM.distr,
+                 V0=hM.V0, f0=hM.f0, mGamma=hM.mGamma, UGamma=hM.UGamma, aSigma=hM.aSigma, bSigma=hM.bSigma,
+                 rhopw=hM.rhopw, C=None,
+                 rL=[dict(nu=rl.nu, a1=rl.a1, b1=rl.b1, a2=rl.a2, b2=rl.b2, nfMin=rl.nfMin, nfMax=rl.nfMax,
+                          sDim=0, xDim=0) for rl in hM.rL])
+        rng = Rng(1234567)
+        st = O.compute_initial_parameters(m, rng)
+        n = 0
+        t0 = time.perf_counter()
+        while True:
+            st = O.sweep(st, m, rng, n + 1, updater={"GammaEta": False})
+            n += 1
+            el = time.perf_counter() - t0
+            if el > args.cpu_seconds or n >= 1000:
+                break
+        rate = n / el
+    finally:
+        if ctx:
+            ctx.__exit__(None, None, None)
+    return {"value": round(rate, 4), "unit": "sweeps/s", "cores": 1, "kind": "port",
+            "sample": f"{n} full sweeps of the numpy oracle at ny={args.ny} ns={args.ns} (1 BLAS thread), "
+                      f"{el:.1f} s",
+            "beta_ess_per_s_median_est": round(rate * ess_per_sweep, 5)}
+
+
+if __name__ == "__main__":
+    main()

@@ -590,6 +590,7 @@ static void run_updater(State& s, uint32_t which, uint32_t iter) {
 }
 
 static void sweep(State& s, uint32_t iter, bool adapt) {
+  ProfScope ps(s, PROF_SWEEP);
   static const uint32_t order[] = {HMSC_UP_GAMMA2,       HMSC_UP_GAMMAETA, HMSC_UP_BETALAMBDA, HMSC_UP_GAMMAV,
                                    HMSC_UP_RHO,          HMSC_UP_LAMBDAPRIORS, HMSC_UP_ETA,  HMSC_UP_ALPHA,
                                    HMSC_UP_INVSIGMA,     HMSC_UP_Z};
@@ -869,6 +870,46 @@ int hmsc_debug_get(hmsc_state* h, const char* name, double* out, int64_t n) {
     HMSC_REQUIRE(src != nullptr, "debug_get: buffer not allocated (enable with noise mode bit 2)");
     HMSC_REQUIRE(n <= avail, "debug_get: n exceeds buffer size");
     HIP_OK(hipMemcpy(out, src, sizeof(double) * n, hipMemcpyDeviceToHost));
+  });
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// Live per-kernel timing with HIP events on the chain's own stream (bench.py's
+// roofline numbers): id 0 updateZ fused kernel, 1 updateEta Z-pass, 2 batched
+// BetaLambda solve, 3 per-unit Eta solve, 4 whole sweep.
+int hmsc_profile(hmsc_state* h, int32_t enable) {
+  return guarded([&] {
+    State& s = h->s;
+    DeviceGuard dg(s.device);
+    HIP_OK(hipStreamSynchronize(s.stream));
+    for (auto& v : s.prof_ev) {
+      for (auto& e : v) {
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+      }
+      v.clear();
+    }
+    s.prof = enable != 0;
+  });
+}
+
+int hmsc_profile_get(hmsc_state* h, int32_t id, double* total_ms, int32_t* count) {
+  return guarded([&] {
+    State& s = h->s;
+    HMSC_REQUIRE(id >= 0 && id < PROF_N, "profile id out of range");
+    DeviceGuard dg(s.device);
+    HIP_OK(hipStreamSynchronize(s.stream));
+    double t = 0.0;
+    for (auto& e : s.prof_ev[id]) {
+      float ms = 0.f;
+      HIP_OK(hipEventElapsedTime(&ms, e.first, e.second));
+      t += ms;
+    }
+    *total_ms = t;
+    *count = (int32_t)s.prof_ev[id].size();
   });
 }
 

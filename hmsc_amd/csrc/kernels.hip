@@ -299,6 +299,8 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   a.noise_zero = s.noise_mode;
   dim3 grid(nchunk, s.ntile_j);
   const size_t smem = z_smem_bytes(s, s.has_na);
+  {
+  ProfScope ps(s, PROF_Z);
   if (draw) {
     if (s.has_na)
       z_fused_kernel<true, true><<<grid, 256, smem, s.stream>>>(a);
@@ -311,6 +313,8 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
       z_fused_kernel<false, false><<<grid, 256, smem, s.stream>>>(a);
   }
   HIP_OK(hipGetLastError());
+  }
+  {
   const int64_t nXZ = (int64_t)s.K * s.nsl;
   slab_sum_kernel<<<grid_for(nXZ), 256, 0, s.stream>>>(s.XZ_part, s.XZ, nXZ, nchunk, nXZ);
   const int64_t nG = (int64_t)s.Kmax * s.Kmax;
@@ -318,6 +322,7 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   const int64_t nZT = (int64_t)s.ny * s.nt;
   slab_sum_kernel<<<grid_for(nZT), 256, 0, s.stream>>>(s.ZTr_part, s.ZTr, nZT, s.ntile_j, nZT);
   HIP_OK(hipGetLastError());
+  }
 }
 
 // masked Gram XEta^T diag(Yx_j) XEta for species with NA (R/updateBetaLambda.R:103-112)
@@ -466,6 +471,7 @@ void launch_beta_lambda(State& s, uint32_t iter) {
   a.iter = iter;
   a.noise_zero = s.noise_mode;
   const size_t smem = ((size_t)s.K * s.K + s.K + s.NF + 1 + s.nc + 1) * sizeof(double) + 16;
+  ProfScope ps(s, PROF_BL);
   beta_lambda_kernel<<<s.nsl, 64, smem, s.stream>>>(a);
   HIP_OK(hipGetLastError());
 }
@@ -1190,6 +1196,7 @@ void launch_eta(State& s, uint32_t iter) {
     dim3 grid((s.ny + 63) / 64, s.zl_split);
     const int per = (s.nsl + s.zl_split - 1) / s.zl_split;
     const size_t smem = std::max((size_t)per * s.NF, (size_t)4 * s.NF * 64) * sizeof(double);
+    ProfScope ps(s, PROF_ZL);
     if (s.NF <= 8)
       zl_kernel<8><<<grid, 256, smem, s.stream>>>(s.Z, s.BL, s.iSigma, s.ny, s.nsl, s.K, s.nc, s.NF, s.zl_split, s.ZL_part);
     else if (s.NF <= 16)
@@ -1248,6 +1255,7 @@ void launch_eta(State& s, uint32_t iter) {
       a.brow = brow;
     }
     const size_t smem = ((size_t)L.nf * L.nf + L.nf + 2) * sizeof(double);
+    ProfScope ps(s, PROF_ETA_UNIT);
     eta_unit_kernel<<<L.np, 64, smem, s.stream>>>(a);
     HIP_OK(hipGetLastError());
   }

@@ -104,6 +104,10 @@ struct State {
   std::vector<hipEvent_t> ring_done;
   double* host_rec = nullptr;    // pinned
 
+  // live kernel timing (HIP events on this chain's stream), id -> launches
+  bool prof = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[8];
+
   // RCCL (species-sharded chain)
   void* comm = nullptr;
   double* allreduce_buf = nullptr;
@@ -127,6 +131,27 @@ struct State {
     NF = 0;
     for (int r = 0; r < nr; ++r) NF += lev[r].nf;
     K = nc + NF;
+  }
+};
+
+enum ProfId { PROF_Z = 0, PROF_ZL = 1, PROF_BL = 2, PROF_ETA_UNIT = 3, PROF_SWEEP = 4, PROF_N = 5 };
+
+struct ProfScope {  // records a start/stop event pair around one launch when profiling is on
+  State& s;
+  int id;
+  hipEvent_t a = nullptr, b = nullptr;
+  ProfScope(State& st, int i) : s(st), id(i) {
+    if (s.prof) {
+      (void)hipEventCreate(&a);
+      (void)hipEventCreate(&b);
+      (void)hipEventRecord(a, s.stream);
+    }
+  }
+  ~ProfScope() {
+    if (s.prof) {
+      (void)hipEventRecord(b, s.stream);
+      s.prof_ev[id].emplace_back(a, b);
+    }
   }
 };
 

@@ -198,6 +198,17 @@ class Chain:
     def sync(self):
         L.check(self.lib.hmsc_sync(self.h))
 
+    PROF_IDS = dict(z=0, zl=1, betalambda=2, eta_unit=3, sweep=4)
+
+    def profile(self, enable=True):
+        L.check(self.lib.hmsc_profile(self.h, 1 if enable else 0))
+
+    def profile_get(self, name):
+        t = np.zeros(1)
+        n = np.zeros(1, dtype=np.int32)
+        L.check(self.lib.hmsc_profile_get(self.h, self.PROF_IDS[name], L.fptr(t), L.iptr(n)))
+        return float(t[0]), int(n[0])
+
     def debug_get(self, name, n):
         out = np.zeros(int(n))
         L.check(self.lib.hmsc_debug_get(self.h, name.encode(), L.fptr(out), int(n)))

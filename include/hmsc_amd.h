@@ -170,6 +170,12 @@ int hmsc_run_verbose(hmsc_state* s, int32_t transient, int32_t samples, int32_t 
                      const int32_t* adaptNf, int32_t iter0, int32_t verbose, int32_t chain,
                      hmsc_record* rec);
 
+/* Live kernel timing with HIP events on the chain's stream (bench / roofline):
+ * id 0 = fused updateZ kernel, 1 = updateEta Z-pass, 2 = batched BetaLambda solve,
+ * 3 = per-unit Eta solve, 4 = whole sweep.  hmsc_profile(s,1) clears and enables. */
+int hmsc_profile(hmsc_state* s, int32_t enable);
+int hmsc_profile_get(hmsc_state* s, int32_t id, double* total_ms, int32_t* count);
+
 /* Wait for all device work of this chain. */
 int hmsc_sync(hmsc_state* s);
 
