@@ -206,6 +206,9 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
     std::vector<int> fill(cnt.begin(), cnt.end() - 1);
     for (int i = 0; i < ny; ++i) rows[fill[pi[i]]++] = i;
     for (int q = 0; q < L.np; ++q) HMSC_REQUIRE(cnt[q + 1] > cnt[q], "a random-level unit has no rows");
+    L.uniform_n = cnt[1] - cnt[0];
+    for (int q = 0; q < L.np; ++q)
+      if (cnt[q + 1] - cnt[q] != L.uniform_n) L.uniform_n = 0;
     L.Pi = dupload(pi.data(), ny);
     L.unit_ptr = dupload(cnt.data(), L.np + 1);
     L.unit_rows = dupload(rows.data(), ny);
@@ -325,15 +328,16 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.rho = dalloc<int>(1);
   // workspaces
   const int n_tiles = (ny + 63) / 64;
-  s.ntile_j = (nsl + 63) / 64;
-  s.nchunk = std::max(1, std::min(n_tiles, 512 / std::max(1, s.ntile_j)));
+  s.ntile_j = (nsl + 31) / 32;
+  s.nchunk = std::max(1, std::min(n_tiles, 1024 / std::max(1, s.ntile_j)));
   const int n_sblk = (ny + 63) / 64;
   s.zl_split = std::max(1, std::min(std::min(16, (nsl + 3) / 4), (640 + n_sblk - 1) / n_sblk));
   s.XZ = dalloc<double>((size_t)s.Kmax * nsl);
+  s.XEta = dalloc<double>((size_t)ny * s.Kmax);
   s.G = dalloc<double>((size_t)s.Kmax * s.Kmax);
   s.ZTr = dalloc<double>((size_t)ny * nt);
   s.XZ_part = dalloc<double>((size_t)s.nchunk * s.Kmax * nsl);
-  s.G_part = dalloc<double>((size_t)s.nchunk * s.Kmax * s.Kmax);
+  s.G_part = dalloc<double>((size_t)std::max(std::max(s.nchunk, 64), n_tiles) * s.Kmax * s.Kmax);
   s.ZTr_part = dalloc<double>((size_t)s.ntile_j * ny * nt);
   const int nfm = std::max(1, s.NFmax);
   s.ZL = dalloc<double>((size_t)ny * nfm);
@@ -353,7 +357,7 @@ static void free_state(State& s) {
   (void)hipDeviceSynchronize();
   void* ptrs[] = {s.X, s.Tr, s.Yval, s.Yraw, s.Ycode, s.fam, s.varest, s.V0, s.iUGamma, s.mGamma, s.UGammaL,
                   s.aSigma, s.bSigma, s.XX, s.TT, s.V0g, s.V0gXXV0g, s.iV0, s.V0inv, s.na_cols, s.na_index,
-                  s.na_rows, s.row_na, s.row_slot, s.dev_flags, s.Z, s.BL, s.Psi, s.Delta, s.Gamma, s.iV,
+                  s.na_rows, s.row_na, s.row_slot, s.dev_flags, s.Z, s.XEta, s.BL, s.Psi, s.Delta, s.Gamma, s.iV,
                   s.iSigma, s.rho, s.XZ, s.G, s.ZTr, s.XZ_part, s.G_part, s.ZTr_part, s.Gna, s.ZL, s.ZL_part,
                   s.CR, s.Msmall, s.scratch, s.psi_rs, s.ABpart, s.dbg_prec, s.ring, s.allreduce_buf};
   for (void* p : ptrs)
@@ -447,6 +451,7 @@ static void set_state(State& s, const hmsc_params* p) {
   if (p->Z) h2d(s.Z, p->Z, (size_t)s.ny * nsl, s.stream);
   HIP_OK(hipStreamSynchronize(s.stream));
   s.zt_valid = false;
+  s.xeta_valid = false;
 }
 
 // ---------------------------- updateNf (host decision) ----------------------------
@@ -552,6 +557,7 @@ static void update_nf(State& s, int r, uint32_t iter) {
   }
   s.refresh_dims();
   s.zt_valid = false;
+  s.xeta_valid = false;
 }
 
 // ---------------------------- sweep ----------------------------
@@ -778,6 +784,7 @@ int hmsc_init_state(hmsc_state* h, const int32_t* nf0) {
     s.refresh_dims();
     HMSC_REQUIRE(s.K <= s.Kmax, "init: K exceeds 64");
     launch_init(s);
+    s.xeta_valid = false;
     launch_update_z(s, 0, true);  // Z = updateZ(Y=hM$Y, ...) (R/computeInitialParameters.R:254)
     HIP_OK(hipStreamSynchronize(s.stream));
   });

@@ -72,6 +72,7 @@ static EtaView make_view(const State& s) {
 // ---------------------------------------------------------------------------
 struct ZArgs {
   EtaView ev;
+  const double* XEta;  // ny x K (ld ny)
   int K, ns_loc, sp0, nt, tiles_per_chunk;
   const double* BL;
   const double* iSigma;
@@ -89,32 +90,33 @@ struct ZArgs {
   int noise_zero;
 };
 
-constexpr int ZT_I = 64;   // sites per tile
-constexpr int ZT_J = 64;   // species per tile
+constexpr int ZT_I = 64;   // sites per tile (one per lane)
+constexpr int ZT_J = 32;   // species per tile (8 per wave)
 constexpr int ZT_LD = 65;  // padded LDS leading dimension (conflict-free column reads)
 constexpr int KMAX_Z = 64;
 
-template <bool DRAW, bool HAS_NA>
-__global__ __launch_bounds__(256) void z_fused_kernel(ZArgs a) {
+// KQ = accumulators per thread for the XZ contraction: rows k = kq + 8q, q < KQ  (K <= 8*KQ)
+template <bool DRAW, bool HAS_NA, int KQ>
+__global__ __launch_bounds__(256, 4) void z_fused_kernel(ZArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int K = a.K;
   const int ny = a.ev.ny;
   double* sXE = smem;                  // [k][ZT_LD]
-  double* sBL = sXE + K * ZT_LD;       // [k][64]
-  double* sZ = sBL + K * ZT_J;         // [jj][ZT_LD]   masked Z (XZ)
+  double* sBL = sXE + K * ZT_LD;       // [k][ZT_J]
+  double* sZ = sBL + K * ZT_J;         // [jj][ZT_LD]   E, then masked Z (XZ)
   double* sZu = sZ + ZT_J * ZT_LD;     // [jj][ZT_LD]   unmasked Z (ZTr), HAS_NA only
-  double* sTr = (HAS_NA ? sZu + ZT_J * ZT_LD : sZu);  // [jj + 64 t]
+  double* sTr = (HAS_NA ? sZu + ZT_J * ZT_LD : sZu);  // [jj + ZT_J t]
   double* sSd = sTr + ZT_J * a.nt;     // [jj]
   int* sFam = (int*)(sSd + ZT_J);      // [jj]
 
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int j0 = blockIdx.y * ZT_J;
   for (int p = t; p < K * ZT_J; p += 256) {
-    const int k = p >> 6, jj = p & 63, j = j0 + jj;
+    const int k = p / ZT_J, jj = p % ZT_J, j = j0 + jj;
     sBL[p] = (j < a.ns_loc) ? a.BL[k + (size_t)K * j] : 0.0;
   }
   for (int p = t; p < ZT_J * a.nt; p += 256) {
-    const int jj = p & 63, tt = p >> 6, j = j0 + jj;
+    const int jj = p % ZT_J, tt = p / ZT_J, j = j0 + jj;
     sTr[p] = (j < a.ns_loc) ? a.Tr[j + (size_t)a.ns_loc * tt] : 0.0;
   }
   if (t < ZT_J) {
@@ -123,11 +125,10 @@ __global__ __launch_bounds__(256) void z_fused_kernel(ZArgs a) {
     sFam[t] = (j < a.ns_loc) ? a.fam[j] : 0;
   }
 
-  double accXZ[KMAX_Z / 4];
-  double accG[KMAX_Z / 4];
+  const int xj = t & 31, xkq = t >> 5;  // XZ mapping: species xj, rows k = xkq + 8q
+  double accXZ[KQ];
 #pragma unroll
-  for (int q = 0; q < KMAX_Z / 4; ++q) accXZ[q] = accG[q] = 0.0;
-  const bool do_gram = (blockIdx.y == 0);
+  for (int q = 0; q < KQ; ++q) accXZ[q] = 0.0;
 
   const int n_tiles = (ny + ZT_I - 1) / ZT_I;
   const int tb = blockIdx.x * a.tiles_per_chunk;
@@ -137,115 +138,128 @@ __global__ __launch_bounds__(256) void z_fused_kernel(ZArgs a) {
     __syncthreads();
     for (int p = t; p < K * ZT_I; p += 256) {
       const int k = p >> 6, ii = p & 63, i = i0 + ii;
-      sXE[k * ZT_LD + ii] = (i < ny) ? xeta_at(a.ev, i, k) : 0.0;
+      sXE[k * ZT_LD + ii] = (i < ny) ? a.XEta[i + (size_t)ny * k] : 0.0;
     }
     __syncthreads();
     const int i = i0 + lane;
-    double zq[16];
     if (DRAW) {
-      double e[16];
+      // E = XEta BL for this lane's site and the wave's 8 species (R/updateZ.R:11-34)
+      double e[8];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) e[q] = 0.0;
+      for (int q = 0; q < 8; ++q) e[q] = 0.0;
       for (int k = 0; k < K; ++k) {
         const double x = sXE[k * ZT_LD + lane];
-        const double* b = sBL + k * ZT_J + w * 16;
+        const double* b = sBL + k * ZT_J + w * 8;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) e[q] = fma(x, b[q], e[q]);
+        for (int q = 0; q < 8; ++q) e[q] = fma(x, b[q], e[q]);
       }
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int jj = w * 16 + q, j = j0 + jj;
+      for (int q = 0; q < 8; ++q) sZ[(w * 8 + q) * ZT_LD + lane] = e[q];
+#pragma unroll 1
+      for (int q = 0; q < 8; ++q) {
+        const int jj = w * 8 + q, j = j0 + jj;
+        const double eq = sZ[jj * ZT_LD + lane];
         double z = 0.0;
+        bool obs = false;
         if (i < ny && j < a.ns_loc) {
           const size_t cell = (size_t)i + (size_t)ny * j;
           const uint32_t idx = (uint32_t)((size_t)i + (size_t)ny * (size_t)(a.sp0 + j));
           const double sd = sSd[jj];
           const int code = a.Ycode[cell];
-          const int fam = sFam[jj];
+          obs = code >= 0;
           if (code < 0) {  // NA cell: Z ~ N(E, sd)   R/updateZ.R:92
             const double nz = a.noise_zero ? 0.0 : normal(a.key, idx, 0, S_Z, a.iter);
-            z = e[q] + sd * nz;
-          } else if (fam == 2) {  // probit: truncated normal   R/updateZ.R:43-63
+            z = eq + sd * nz;
+          } else if (sFam[jj] == 2) {  // probit: truncated normal   R/updateZ.R:43-63
             const double u = uniforms(a.key, idx, 0, S_Z, a.iter).a;
             const double sg = code ? 1.0 : -1.0;
-            const double wdraw = trunc_normal_lower(-sg * e[q] / sd, u);
-            z = e[q] + sd * sg * wdraw;
+            z = eq + sd * sg * trunc_normal_lower(-sg * eq / sd, u);
           } else {  // normal: Z = Y   R/updateZ.R:40-41
             z = a.Yval[cell];
           }
           a.Z[cell] = z;
         }
-        zq[q] = z;
+        if (HAS_NA) {
+          sZ[jj * ZT_LD + lane] = obs ? z : 0.0;
+          sZu[jj * ZT_LD + lane] = z;
+        } else {
+          sZ[jj * ZT_LD + lane] = z;
+        }
       }
     } else {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int j = j0 + w * 16 + q;
-        zq[q] = (i < ny && j < a.ns_loc) ? a.Z[(size_t)i + (size_t)ny * j] : 0.0;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int jj = w * 16 + q, j = j0 + jj;
-      if (HAS_NA) {
-        const bool obs = (i < ny && j < a.ns_loc) ? (a.Ycode[(size_t)i + (size_t)ny * j] >= 0) : false;
-        sZ[jj * ZT_LD + lane] = obs ? zq[q] : 0.0;
-        sZu[jj * ZT_LD + lane] = zq[q];
-      } else {
-        sZ[jj * ZT_LD + lane] = zq[q];
+      for (int q = 0; q < 8; ++q) {
+        const int jj = w * 8 + q, j = j0 + jj;
+        const double z = (i < ny && j < a.ns_loc) ? a.Z[(size_t)i + (size_t)ny * j] : 0.0;
+        if (HAS_NA) {
+          const bool obs = (i < ny && j < a.ns_loc) ? (a.Ycode[(size_t)i + (size_t)ny * j] >= 0) : false;
+          sZ[jj * ZT_LD + lane] = obs ? z : 0.0;
+          sZu[jj * ZT_LD + lane] = z;
+        } else {
+          sZ[jj * ZT_LD + lane] = z;
+        }
       }
     }
     __syncthreads();
-    // XZ partial: thread -> species lane, rows k = w + 4q
+    // XZ partial (R/updateBetaLambda.R:66 for the next sweep): species xj, rows xkq + 8q
     {
-      const double* zc = sZ + lane * ZT_LD;
+      const double* zc = sZ + xj * ZT_LD;
       for (int ii = 0; ii < ZT_I; ++ii) {
         const double zv = zc[ii];
 #pragma unroll
-        for (int q = 0; q < KMAX_Z / 4; ++q) {
-          const int k = w + 4 * q;
+        for (int q = 0; q < KQ; ++q) {
+          const int k = xkq + 8 * q;
           if (k < K) accXZ[q] = fma(sXE[k * ZT_LD + ii], zv, accXZ[q]);
         }
       }
     }
-    if (do_gram && lane < K) {
-      const double* xc = sXE + lane * ZT_LD;
-      for (int ii = 0; ii < ZT_I; ++ii) {
-        const double xv = xc[ii];
-#pragma unroll
-        for (int q = 0; q < KMAX_Z / 4; ++q) {
-          const int k = w + 4 * q;
-          if (k < K) accG[q] = fma(sXE[k * ZT_LD + ii], xv, accG[q]);
-        }
-      }
-    }
-    // ZTr partial for this (site tile, species tile)
+    // ZTr partial for this (site tile, species tile)   (R/updateGamma2.R:46)
     if (i < ny) {
       const double* zsrc = HAS_NA ? sZu : sZ;
       for (int tt = w; tt < a.nt; tt += 4) {
         double acc = 0.0;
+#pragma unroll 8
         for (int jj = 0; jj < ZT_J; ++jj) acc = fma(zsrc[jj * ZT_LD + lane], sTr[jj + ZT_J * tt], acc);
         a.ZTr_part[(size_t)blockIdx.y * ny * a.nt + i + (size_t)ny * tt] = acc;
       }
     }
   }
-  // write chunk partials
   {
-    const int j = j0 + lane;
+    const int j = j0 + xj;
     double* dst = a.XZ_part + (size_t)blockIdx.x * K * a.ns_loc;
 #pragma unroll
-    for (int q = 0; q < KMAX_Z / 4; ++q) {
-      const int k = w + 4 * q;
+    for (int q = 0; q < KQ; ++q) {
+      const int k = xkq + 8 * q;
       if (k < K && j < a.ns_loc) dst[k + (size_t)K * j] = accXZ[q];
     }
   }
-  if (do_gram && lane < K) {
-    double* dst = a.G_part + (size_t)blockIdx.x * a.Kmax * a.Kmax;
-#pragma unroll
-    for (int q = 0; q < KMAX_Z / 4; ++q) {
-      const int k = w + 4 * q;
-      if (k < K) dst[k + a.Kmax * lane] = accG[q];
+}
+
+// Materialise XEta = [X, Eta_1[Pi_1,], ...] (R/updateBetaLambda.R:21-41) for one 64-site
+// tile and accumulate its Gram XEta^T XEta (:65) -> slab part[tile].
+__global__ __launch_bounds__(256) void xeta_gram_kernel(EtaView ev, int K, int Kmax, double* XEta, double* G_part) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* sXE = smem;  // [k][ZT_LD]
+  const int t = threadIdx.x, ny = ev.ny, i0 = blockIdx.x * 64;
+  for (int p = t; p < K * 64; p += 256) {
+    const int k = p >> 6, ii = p & 63, i = i0 + ii;
+    double v = 0.0;
+    if (i < ny) {
+      v = xeta_at(ev, i, k);
+      XEta[i + (size_t)ny * k] = v;
     }
+    sXE[k * ZT_LD + ii] = v;
+  }
+  __syncthreads();
+  double* dst = G_part + (size_t)blockIdx.x * Kmax * Kmax;
+  for (int p = t; p < K * K; p += 256) {
+    const int k1 = p % K, k2 = p / K;
+    const double* x1 = sXE + k1 * ZT_LD;
+    const double* x2 = sXE + k2 * ZT_LD;
+    double acc = 0.0;
+#pragma unroll 8
+    for (int ii = 0; ii < 64; ++ii) acc = fma(x1[ii], x2[ii], acc);
+    dst[k1 + Kmax * k2] = acc;
   }
 }
 
@@ -272,10 +286,31 @@ static size_t z_smem_bytes(const State& s, bool has_na) {
   return d * sizeof(double) + ZT_J * sizeof(int);
 }
 
+template <bool DRAW, bool HAS_NA>
+static void z_dispatch(const State& s, dim3 grid, size_t smem, const ZArgs& a) {
+  if (s.K <= 32)
+    z_fused_kernel<DRAW, HAS_NA, 4><<<grid, 256, smem, s.stream>>>(a);
+  else
+    z_fused_kernel<DRAW, HAS_NA, 8><<<grid, 256, smem, s.stream>>>(a);
+}
+
+void launch_xeta(State& s) {
+  const int n_tiles = (s.ny + 63) / 64;
+  xeta_gram_kernel<<<n_tiles, 256, (size_t)s.K * ZT_LD * sizeof(double), s.stream>>>(make_view(s), s.K, s.Kmax,
+                                                                                       s.XEta, s.G_part);
+  HIP_OK(hipGetLastError());
+  const int64_t nG = (int64_t)s.Kmax * s.Kmax;
+  slab_sum_kernel<<<grid_for(nG), 256, 0, s.stream>>>(s.G_part, s.G, nG, n_tiles, nG);
+  HIP_OK(hipGetLastError());
+  s.xeta_valid = true;
+}
+
 static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   HMSC_REQUIRE(s.K <= KMAX_Z, "updateZ: K = nc + sum(nf) must be <= 64 in this build");
+  if (!s.xeta_valid) launch_xeta(s);
   ZArgs a{};
   a.ev = make_view(s);
+  a.XEta = s.XEta;
   a.K = s.K;
   a.Kmax = s.Kmax;
   a.ns_loc = s.nsl;
@@ -300,33 +335,29 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   dim3 grid(nchunk, s.ntile_j);
   const size_t smem = z_smem_bytes(s, s.has_na);
   {
-  ProfScope ps(s, PROF_Z);
-  if (draw) {
-    if (s.has_na)
-      z_fused_kernel<true, true><<<grid, 256, smem, s.stream>>>(a);
-    else
-      z_fused_kernel<true, false><<<grid, 256, smem, s.stream>>>(a);
-  } else {
-    if (s.has_na)
-      z_fused_kernel<false, true><<<grid, 256, smem, s.stream>>>(a);
-    else
-      z_fused_kernel<false, false><<<grid, 256, smem, s.stream>>>(a);
+    ProfScope ps(s, PROF_Z);
+    if (draw) {
+      if (s.has_na)
+        z_dispatch<true, true>(s, grid, smem, a);
+      else
+        z_dispatch<true, false>(s, grid, smem, a);
+    } else {
+      if (s.has_na)
+        z_dispatch<false, true>(s, grid, smem, a);
+      else
+        z_dispatch<false, false>(s, grid, smem, a);
+    }
+    HIP_OK(hipGetLastError());
   }
-  HIP_OK(hipGetLastError());
-  }
-  {
   const int64_t nXZ = (int64_t)s.K * s.nsl;
   slab_sum_kernel<<<grid_for(nXZ), 256, 0, s.stream>>>(s.XZ_part, s.XZ, nXZ, nchunk, nXZ);
-  const int64_t nG = (int64_t)s.Kmax * s.Kmax;
-  slab_sum_kernel<<<grid_for(nG), 256, 0, s.stream>>>(s.G_part, s.G, nG, nchunk, nG);
   const int64_t nZT = (int64_t)s.ny * s.nt;
   slab_sum_kernel<<<grid_for(nZT), 256, 0, s.stream>>>(s.ZTr_part, s.ZTr, nZT, s.ntile_j, nZT);
   HIP_OK(hipGetLastError());
-  }
 }
 
 // masked Gram XEta^T diag(Yx_j) XEta for species with NA (R/updateBetaLambda.R:103-112)
-__global__ __launch_bounds__(256) void gram_na_kernel(EtaView ev, int K, int Kmax, const int* na_cols,
+__global__ __launch_bounds__(256) void gram_na_kernel(EtaView ev, const double* XEta, int K, int Kmax, const int* na_cols,
                                                       const int8_t* Ycode, double* Gna) {
   const int c = blockIdx.x;
   const int j = na_cols[c];
@@ -337,7 +368,7 @@ __global__ __launch_bounds__(256) void gram_na_kernel(EtaView ev, int K, int Kma
     if (k1 > k2) continue;
     double s = 0.0;
     for (int i = 0; i < ny; ++i)
-      if (Ycode[(size_t)i + (size_t)ny * j] >= 0) s += xeta_at(ev, i, k1) * xeta_at(ev, i, k2);
+      if (Ycode[(size_t)i + (size_t)ny * j] >= 0) s += XEta[i + (size_t)ny * k1] * XEta[i + (size_t)ny * k2];
     out[k1 + Kmax * k2] = s;
     out[k2 + Kmax * k1] = s;
   }
@@ -439,10 +470,11 @@ __global__ __launch_bounds__(64) void beta_lambda_kernel(BLArgs a) {
 }
 
 void launch_beta_lambda(State& s, uint32_t iter) {
+  if (!s.xeta_valid) launch_xeta(s);
   if (!s.zt_valid) launch_zt_refresh(s);
   if (s.n_na_cols > 0) {
     EtaView ev = make_view(s);
-    gram_na_kernel<<<s.n_na_cols, 256, 0, s.stream>>>(ev, s.K, s.Kmax, s.na_cols, s.Ycode, s.Gna);
+    gram_na_kernel<<<s.n_na_cols, 256, 0, s.stream>>>(ev, s.XEta, s.K, s.Kmax, s.na_cols, s.Ycode, s.Gna);
   }
   BLArgs a{};
   a.K = s.K;
@@ -514,25 +546,21 @@ __global__ __launch_bounds__(256) void gammav_partial_kernel(const double* BL, i
 
 // Bartlett draw of MCMCpack::rwish(v, S): W = (Zb CC)^T (Zb CC), CC = chol(S) upper,
 // Zb upper-triangular, diag sqrt(chisq(v - i)), off-diagonal N(0,1).
-// Sl holds lower L = CC^T (n x n, ld n); result into W; T scratch n*n.
-__device__ void wg_rwish(const double* Sl, int n, double v, double* W, double* T, Key key, uint32_t s_diag,
-                         uint32_t s_off, uint32_t iter, int noise_zero) {
-  const int t = threadIdx.x;
-  // T = Zb * CC = Zb * L^T : T[i][c] = sum_{k>=i} Zb[i][k] * L[c][k]
-  for (int p = t; p < n * n; p += blockDim.x) {
-    const int i = p % n, c = p / n;
-    double s = 0.0;
-    for (int k = i; k < n; ++k) {
-      double z;
-      if (k == i)
-        z = sqrt(2.0 * gamma_std(key, (uint32_t)i, s_diag, iter, 0.5 * (v - i)));
-      else
-        z = noise_zero ? 0.0 : normal(key, (uint32_t)(i + n * k), 0, s_off, iter);
-      if (c >= k) s += z * Sl[c + n * k];
-    }
-    T[i + n * c] = s;
+// Sl holds lower L = CC^T (n x n, ld n); result into W; T, Zb scratch n*n each.
+__device__ void wg_rwish(const double* Sl, int n, double v, double* W, double* T, double* Zb, Key key,
+                         uint32_t s_diag, uint32_t s_off, uint32_t iter, int noise_zero) {
+  for (int p = threadIdx.x; p < n * n; p += blockDim.x) {
+    const int i = p % n, k = p / n;
+    double z = 0.0;
+    if (k == i)
+      z = sqrt(2.0 * gamma_std(key, (uint32_t)i, s_diag, iter, 0.5 * (v - i)));
+    else if (k > i)
+      z = noise_zero ? 0.0 : normal(key, (uint32_t)(i + n * k), 0, s_off, iter);
+    Zb[p] = z;
   }
   __syncthreads();
+  // T = Zb * L^T
+  wg_gemm(n, n, n, 1.0, Zb, n, false, Sl, n, true, 0.0, T, n);
   wg_gemm(n, n, n, 1.0, T, n, true, T, n, false, 0.0, W, n);
 }
 
@@ -551,18 +579,21 @@ struct GVArgs {
   uint32_t iter;
   int noise_zero;
   int* fail;
+  int use_lds;
 };
 
 __global__ __launch_bounds__(256) void gammav_final_kernel(GVArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
   const int nc = a.nc, nt = a.nt, N = nc * nt, t = threadIdx.x;
   __shared__ int flag;
-  double* A = a.scratch;            // nc*nc
+  double* A = a.use_lds ? lds : a.scratch;  // nc*nc
   double* Vn = A + nc * nc;         // nc*nc
   double* W = Vn + nc * nc;         // nc*nc scratch
   double* T = W + nc * nc;          // nc*nc scratch
   double* BTr = T + nc * nc;        // nc*nt
   double* Pm = BTr + nc * nt;       // N*N
   double* rhs = Pm + N * N;         // N
+  double* Zb = rhs + N;             // nc*nc
   const int nA = nc * nc, nB = nc * nt;
   for (int p = t; p < nA + nB; p += blockDim.x) {
     double s = 0.0;
@@ -580,7 +611,7 @@ __global__ __launch_bounds__(256) void gammav_final_kernel(GVArgs a) {
   wg_copy(A, Vn, nc * nc);
   wg_chol(A, nc, nc, &flag);                      // CC = chol(Vn)
   wg_lower_only(A, nc, nc);
-  wg_rwish(A, nc, a.f0 + a.ns_glob, a.iV, T, a.key, S_WISHART_DIAG, S_WISHART_OFF, a.iter, a.noise_zero);  // (:20)
+  wg_rwish(A, nc, a.f0 + a.ns_glob, a.iV, T, Zb, a.key, S_WISHART_DIAG, S_WISHART_OFF, a.iter, a.noise_zero);  // (:20)
   // Gamma | iV: prec = iUGamma + kron(Tr'Tr, iV); rhs = iUGamma mGamma + vec(iV B Tr)   (:29-31)
   for (int p = t; p < N * N; p += blockDim.x) {
     const int r = p % N, c = p / N;
@@ -637,7 +668,10 @@ void launch_gamma_v(State& s, uint32_t iter) {
   a.iter = iter;
   a.noise_zero = s.noise_mode;
   a.fail = s.dev_flags;
-  gammav_final_kernel<<<1, 256, 0, s.stream>>>(a);
+  const size_t need = (5 * (size_t)s.nc * s.nc + (size_t)s.nc * s.nt + (size_t)s.nc * s.nt * s.nc * s.nt +
+                       (size_t)s.nc * s.nt) * sizeof(double);
+  a.use_lds = need <= 64 * 1024;
+  gammav_final_kernel<<<1, 256, a.use_lds ? need : 0, s.stream>>>(a);
   HIP_OK(hipGetLastError());
 }
 
@@ -704,6 +738,7 @@ struct G2Args {
   uint32_t iter;
   int noise_zero;
   int check_isigma;
+  int use_lds;
 };
 
 __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
@@ -717,7 +752,8 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
       if (a.iSigma[j] != 1.0) all_one = 0;  // acts only if all(iSigma == 1)  (:36)
   __syncthreads();
   if (!all_one) return;
-  double* S0 = a.scratch;             // XZT  nc*nt
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  double* S0 = a.use_lds ? lds : a.scratch;  // XZT  nc*nt
   double* LTr = S0 + nc * nt;         // NF*nt
   double* iP = LTr + a.NF * nt;       // nc*nc
   double* LiP = iP + nc * nc;         // nc*nc
@@ -735,6 +771,7 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
   double* muG = v2 + N;               // N
   double* t2 = muG + N;               // nc*nc
   double* W1 = t2 + nc * nc;          // nc*nc
+  double* xi = W1 + nc * nc;          // N
   const int n1 = nc * nt, n2 = a.NF * nt;
   // reduce species partials
   for (int p = t; p < n1 + n2; p += blockDim.x) {
@@ -810,15 +847,17 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
   }
   __syncthreads();
   wg_chol(Sg, N, N, &flag);                // LSigmaG = t(chol(SigmaG))   (:52)
+  for (int r = t; r < N; r += blockDim.x) xi[r] = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)r, 0, S_GAMMA2, a.iter);
+  __syncthreads();
   for (int r = t; r < N; r += blockDim.x) {
     double v = muG[r];
-    if (!a.noise_zero)
-      for (int c = 0; c <= r; ++c) v += Sg[r + N * c] * normal(a.key, (uint32_t)c, 0, S_GAMMA2, a.iter);
+    for (int c = 0; c <= r; ++c) v += Sg[r + N * c] * xi[c];
     a.Gamma[r] = v;                        // (:53-54)
   }
 }
 
 void launch_gamma2(State& s, uint32_t iter) {
+  if (!s.xeta_valid) launch_xeta(s);
   if (!s.zt_valid) launch_zt_refresh(s);
   const int nparts = std::min(GV_PARTS, std::max(1, s.nsl));
   gamma2_partial_kernel<<<nparts, 256, 0, s.stream>>>(s.XZ, s.BL, s.K, s.nc, s.NF, s.nt, s.nsl, s.Tr, s.ABpart);
@@ -860,7 +899,10 @@ void launch_gamma2(State& s, uint32_t iter) {
   a.iter = iter;
   a.noise_zero = s.noise_mode;
   a.check_isigma = s.nranks == 1 ? 1 : 0;
-  gamma2_final_kernel<<<1, 256, 0, s.stream>>>(a);
+  const size_t N = (size_t)s.nc * s.nt;
+  const size_t need = (9 * (size_t)s.nc * s.nc + 5 * N * N + 2 * N + (size_t)s.NF * s.nt + 4 * N) * sizeof(double);
+  a.use_lds = need <= 64 * 1024;
+  gamma2_final_kernel<<<1, 256, a.use_lds ? need : 0, s.stream>>>(a);
   HIP_OK(hipGetLastError());
 }
 
@@ -932,43 +974,61 @@ __global__ __launch_bounds__(256) void psi_kernel(LPArgs a) {
   if (t < NF) rs[t] = acc;
 }
 
-__global__ void delta_kernel(LPArgs a, const double* rs_part, int nparts) {
-  // one thread per level: the sequential delta chain (:25-32)
-  const int r = threadIdx.x;
-  if (r >= a.nr) return;
+// Marsaglia-Tsang with its first 64 trials evaluated in parallel by one wave; the
+// first accepted trial is taken, so the value equals the sequential gamma_std().
+__device__ double wave_gamma_std(Key key, uint32_t idx, uint32_t stream, uint32_t iter, double shape) {
+  const int lane = threadIdx.x & 63;
+  const double a = shape < 1.0 ? shape + 1.0 : shape;
+  const double d = a - 1.0 / 3.0;
+  const double c = 1.0 / sqrt(9.0 * d);
+  const double x = normal(key, idx, 2u * lane, stream, iter);
+  double v = 1.0 + c * x;
+  bool acc = false;
+  double val = d;
+  if (v > 0.0) {
+    v = v * v * v;
+    const double u = uniforms(key, idx, 2u * lane + 1u, stream, iter).a;
+    acc = log(u) < 0.5 * x * x + d - d * v + d * log(v);
+    val = d * v;
+  }
+  const unsigned long long m = __ballot(acc);
+  double out = d;
+  if (m) out = __shfl(val, __ffsll((long long)m) - 1);
+  if (shape < 1.0) out *= pow(uniforms(key, idx, GAMMA_BOOST_SUB, stream, iter).a, 1.0 / shape);
+  return out;
+}
+
+__global__ __launch_bounds__(64) void delta_kernel(LPArgs a, const double* rs_part, int nparts) {
+  // one wave per level: the sequential delta chain (R/updateLambdaPriors.R:25-32)
+  __shared__ double rs[64], delta[64];
+  const int r = blockIdx.x, t = threadIdx.x;
   const int nf = a.lev_nf[r];
   int f0 = 0;
   for (int q = 0; q < r; ++q) f0 += a.lev_nf[q];
-  double rs[64], delta[64];
-  for (int h = 0; h < nf; ++h) {
-    double s = 0.0;
-    for (int b = 0; b < nparts; ++b) s += rs_part[(size_t)b * a.NF + f0 + h];
-    rs[h] = s;
-    delta[h] = a.Delta[f0 + h];
+  if (t < nf) {
+    double sum = 0.0;
+    for (int b = 0; b < nparts; ++b) sum += rs_part[(size_t)b * a.NF + f0 + t];
+    rs[t] = sum;
+    delta[t] = a.Delta[f0 + t];
   }
+  __syncthreads();
   const uint32_t stream = S_DELTA + LEVEL_STRIDE * r;
   const double ns = (double)a.ns_glob;
-  double tau = 1.0, st = 0.0;
   for (int h = 0; h < nf; ++h) {
-    tau *= delta[h];
-    st += tau * rs[h];
-  }
-  {
-    const double ad = a.a1[r] + 0.5 * ns * nf;
-    const double bd = a.b1[r] + 0.5 * st / delta[0];
-    delta[0] = gamma_std(a.key, 0, stream, a.iter, ad) / bd;
-  }
-  for (int h = 1; h < nf; ++h) {
-    double c = 1.0, s = 0.0;
+    // sum_{h' >= h} tau_h' rs_h' / delta_h with tau = cumprod(current delta)
+    double c = 1.0, sum = 0.0;
     for (int q = 0; q < nf; ++q) {
       c *= delta[q];
-      if (q >= h) s += c * rs[q];
+      if (q >= h) sum += c * rs[q];
     }
-    const double ad = a.a2[r] + 0.5 * ns * (nf - h);
-    const double bd = a.b2[r] + 0.5 * s / delta[h];
-    delta[h] = gamma_std(a.key, (uint32_t)h, stream, a.iter, ad) / bd;
+    const double ad = (h == 0 ? a.a1[r] : a.a2[r]) + 0.5 * ns * (nf - h);
+    const double bd = (h == 0 ? a.b1[r] : a.b2[r]) + 0.5 * sum / delta[h];
+    const double g = wave_gamma_std(a.key, (uint32_t)h, stream, a.iter, ad) / bd;
+    __syncthreads();
+    if (t == 0) delta[h] = g;
+    __syncthreads();
   }
-  for (int h = 0; h < nf; ++h) a.Delta[f0 + h] = delta[h];
+  if (t < nf) a.Delta[f0 + t] = delta[t];
 }
 
 constexpr int LP_PARTS = 64;
@@ -1009,7 +1069,7 @@ void launch_lambda_priors(State& s, uint32_t iter) {
     rs = s.allreduce_buf;
     np = 1;
   }
-  delta_kernel<<<1, 64, 0, s.stream>>>(a, rs, np);
+  delta_kernel<<<s.nr, 64, 0, s.stream>>>(a, rs, np);
   HIP_OK(hipGetLastError());
 }
 
@@ -1154,6 +1214,77 @@ __global__ __launch_bounds__(64) void eta_unit_kernel(EtaArgs a) {
   for (int h = t; h < nf; h += 64) a.Eta[q + (size_t)a.np * h] = b[h];
 }
 
+// Fast path (no NA, every unit of level r has the same number n of rows, e.g. np == ny):
+// all units share Q = I + n Lambda_r diag(iSigma) Lambda_r^T, so each workgroup factors Q
+// once in LDS and every thread solves one unit with the shared factor (R/updateEta.R:52-56).
+template <int NFB>
+__global__ __launch_bounds__(256) void eta_shared_kernel(EtaArgs a, int nrow) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int nf = a.nf, K = a.K, t = threadIdx.x;
+  double* Q = smem;               // nf x nf -> lower L
+  double* sCR = Q + nf * nf;      // K x nf   (column h of level r)
+  int* flag = (int*)(sCR + K * nf + 1);
+  for (int p = t; p < K * nf; p += 256) {
+    const int k = p % K, h = p / K;
+    sCR[p] = a.CR[k + (size_t)a.ldcr * (a.foff + h)];
+  }
+  __syncthreads();
+  for (int p = t; p < nf * nf; p += 256) {
+    const int r1 = p % nf, c1 = p / nf;
+    Q[p] = (r1 == c1 ? 1.0 : 0.0) + nrow * sCR[a.loff + r1 + K * c1];
+  }
+  __syncthreads();
+  wg_chol(Q, nf, nf, flag);
+  const int q = blockIdx.x * 256 + t;
+  if (q >= a.np) return;
+  double b[NFB];
+#pragma unroll
+  for (int h = 0; h < NFB; ++h) b[h] = 0.0;
+  for (int pp = a.unit_ptr[q]; pp < a.unit_ptr[q + 1]; ++pp) {
+    const int i = a.unit_rows[pp];
+    for (int c = 0; c < a.nzl; ++c) {
+      const double* zl = a.ZL + (size_t)c * a.ev.ny * a.NF + (size_t)i * a.NF + a.foff;
+#pragma unroll
+      for (int h = 0; h < NFB; ++h)
+        if (h < nf) b[h] += zl[h];
+    }
+    for (int k = 0; k < K; ++k) {
+      if (k >= a.loff && k < a.loff + nf) continue;
+      const double x = xeta_at(a.ev, i, k);
+#pragma unroll
+      for (int h = 0; h < NFB; ++h)
+        if (h < nf) b[h] -= x * sCR[k + K * h];
+    }
+  }
+  // y = L^-1 b ; y += xi ; eta = L^-T y
+#pragma unroll
+  for (int h = 0; h < NFB; ++h) {
+    if (h < nf) {
+      double v = b[h];
+#pragma unroll
+      for (int k = 0; k < NFB; ++k)
+        if (k < h) v -= Q[h + nf * k] * b[k];
+      b[h] = v / Q[h + nf * h];
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < NFB; ++h)
+    if (h < nf && !a.noise_zero) b[h] += normal(a.key, (uint32_t)q, (uint32_t)h, S_ETA + LEVEL_STRIDE * a.r, a.iter);
+#pragma unroll
+  for (int h = NFB - 1; h >= 0; --h) {
+    if (h < nf) {
+      double v = b[h];
+#pragma unroll
+      for (int k = 0; k < NFB; ++k)
+        if (k > h && k < nf) v -= Q[k + nf * h] * b[k];
+      b[h] = v / Q[h + nf * h];
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < NFB; ++h)
+    if (h < nf) a.Eta[q + (size_t)a.np * h] = b[h];
+}
+
 // NA rows (R/updateEta.R:59-70, :80-87): masked per-row precision and numerator
 // with the residual S computed on the fly.  One workgroup per NA row.
 __global__ __launch_bounds__(64) void eta_na_row_kernel(EtaView ev, int r, int nf, int K, int nc, int loff,
@@ -1254,18 +1385,30 @@ void launch_eta(State& s, uint32_t iter) {
       a.Mrow = Mrow;
       a.brow = brow;
     }
-    const size_t smem = ((size_t)L.nf * L.nf + L.nf + 2) * sizeof(double);
     ProfScope ps(s, PROF_ETA_UNIT);
-    eta_unit_kernel<<<L.np, 64, smem, s.stream>>>(a);
+    if (s.n_na_rows == 0 && L.uniform_n > 0 && L.nf <= 32) {
+      const size_t smem = ((size_t)L.nf * L.nf + (size_t)s.K * L.nf + 2) * sizeof(double);
+      const int grid = (L.np + 255) / 256;
+      if (L.nf <= 8)
+        eta_shared_kernel<8><<<grid, 256, smem, s.stream>>>(a, L.uniform_n);
+      else if (L.nf <= 16)
+        eta_shared_kernel<16><<<grid, 256, smem, s.stream>>>(a, L.uniform_n);
+      else
+        eta_shared_kernel<32><<<grid, 256, smem, s.stream>>>(a, L.uniform_n);
+    } else {
+      const size_t smem = ((size_t)L.nf * L.nf + L.nf + 2) * sizeof(double);
+      eta_unit_kernel<<<L.np, 64, smem, s.stream>>>(a);
+    }
     HIP_OK(hipGetLastError());
   }
-  s.zt_valid = false;  // Eta changed: XZ / G are stale until the next updateZ
+  s.zt_valid = false;  // Eta changed: XZ is stale until the next updateZ
+  launch_xeta(s);      // XEta and G for the new Eta
 }
 
 // ---------------------------------------------------------------------------
 // updateInvSigma (R/updateInvSigma.R:3-43): species with distr[,2] == 1 only.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void inv_sigma_kernel(EtaView ev, int K, const double* BL, const double* Z,
+__global__ __launch_bounds__(256) void inv_sigma_kernel(EtaView ev, const double* XEta, int K, const double* BL, const double* Z,
                                                         const int8_t* Ycode, const int* varest,
                                                         const double* aSigma, const double* bSigma, int sp0,
                                                         double* iSigma, Key key, uint32_t iter) {
@@ -1278,7 +1421,7 @@ __global__ __launch_bounds__(256) void inv_sigma_kernel(EtaView ev, int K, const
   for (int i = t; i < ny; i += 256) {
     if (Ycode[(size_t)i + (size_t)ny * j] < 0) continue;
     double e = 0.0;
-    for (int k = 0; k < K; ++k) e += xeta_at(ev, i, k) * BL[k + (size_t)K * j];
+    for (int k = 0; k < K; ++k) e += XEta[i + (size_t)ny * k] * BL[k + (size_t)K * j];
     const double d = Z[(size_t)i + (size_t)ny * j] - e;
     ss += d * d;
     ++n;
@@ -1302,7 +1445,8 @@ __global__ __launch_bounds__(256) void inv_sigma_kernel(EtaView ev, int K, const
 
 void launch_inv_sigma(State& s, uint32_t iter) {
   if (!s.any_var) return;
-  inv_sigma_kernel<<<s.nsl, 256, 0, s.stream>>>(make_view(s), s.K, s.BL, s.Z, s.Ycode, s.varest, s.aSigma,
+  if (!s.xeta_valid) launch_xeta(s);
+  inv_sigma_kernel<<<s.nsl, 256, 0, s.stream>>>(make_view(s), s.XEta, s.K, s.BL, s.Z, s.Ycode, s.varest, s.aSigma,
                                                  s.bSigma, s.sp0, s.iSigma, s.key, iter);
   HIP_OK(hipGetLastError());
 }
@@ -1342,6 +1486,7 @@ __global__ __launch_bounds__(256) void init_small_kernel(InitArgs a) {
   double* S = a.scratch;        // nc*nc
   double* T = S + nc * nc;      // nc*nc
   double* W = T + nc * nc;      // nc*nc
+  double* Zb = W + nc * nc;     // nc*nc
   for (int r = t; r < N; r += blockDim.x) {  // Gamma ~ N(mGamma, UGamma)   (:85)
     double v = a.mGamma[r];
     for (int c = 0; c <= r; ++c) v += a.UGammaL[r + N * c] * normal(a.key, (uint32_t)c, 0, S_INIT_GAMMA, 0);
@@ -1350,7 +1495,7 @@ __global__ __launch_bounds__(256) void init_small_kernel(InitArgs a) {
   wg_copy(S, a.V0inv, nc * nc);
   wg_chol(S, nc, nc, &flag);
   wg_lower_only(S, nc, nc);
-  wg_rwish(S, nc, a.f0, a.iV, T, a.key, S_INIT_V_DIAG, S_INIT_V_OFF, 0, 0);   // iV = rwish(f0, V0^-1)  (:91)
+  wg_rwish(S, nc, a.f0, a.iV, T, Zb, a.key, S_INIT_V_DIAG, S_INIT_V_OFF, 0, 0);   // iV = rwish(f0, V0^-1)  (:91)
   wg_copy(S, a.iV, nc * nc);
   wg_chol(S, nc, nc, &flag);
   wg_chol2inv(S, nc, nc, T, nc, W);          // V = iV^-1
@@ -1448,7 +1593,7 @@ void launch_init(State& s) {
   a.bSigma = s.bSigma;
   a.Gamma = s.Gamma;
   a.iV = s.iV;
-  a.LV = s.scratch + 3 * (size_t)s.nc * s.nc;
+  a.LV = s.scratch + 4 * (size_t)s.nc * s.nc;
   a.BL = s.BL;
   a.Psi = s.Psi;
   a.Delta = s.Delta;

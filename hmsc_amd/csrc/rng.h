@@ -93,7 +93,12 @@ __host__ __device__ __forceinline__ Uniform2 uniforms(Key key, uint32_t idx, uin
 __host__ __device__ __forceinline__ double normal(Key key, uint32_t idx, uint32_t sub, uint32_t stream,
                                          uint32_t iter) {
   const Uniform2 u = uniforms(key, idx, sub, stream, iter);
+#if defined(__HIP_DEVICE_COMPILE__)
+  // cospi: exact argument reduction, no Payne-Hanek table (keeps kernels spill-free)
+  return sqrt(-2.0 * log(u.a)) * cospi(2.0 * u.b);
+#else
   return sqrt(-2.0 * log(u.a)) * cos(6.283185307179586 * u.b);
+#endif
 }
 
 // Gamma(shape, rate=1): Marsaglia & Tsang (2000); trial t uses sub-blocks 2t (normal)
@@ -122,13 +127,57 @@ __host__ __device__ __forceinline__ double gamma_std(Key key, uint32_t idx, uint
   return out;
 }
 
-// Standard normal truncated to [alpha, +inf) by inversion of the upper tail,
-//   x = sqrt(2) * erfcinv(u * erfc(alpha/sqrt(2))),
+// Phi^-1(p), Wichura (1988) AS241 PPND16 (the algorithm behind R's qnorm), |rel err| ~1e-16.
+__host__ __device__ __forceinline__ double qnorm_as241(double p) {
+  const double q = p - 0.5;
+  if (fabs(q) <= 0.425) {
+    const double r = 0.180625 - q * q;
+    const double num =
+        (((((((2.5090809287301226727e+3 * r + 3.3430575583588128105e+4) * r + 6.7265770927008700853e+4) * r +
+             4.5921953931549871457e+4) * r + 1.3731693765509461125e+4) * r + 1.9715909503065514427e+3) * r +
+          1.3314166789178437745e+2) * r + 3.3871328727963666080e0);
+    const double den =
+        (((((((5.2264952788528545610e+3 * r + 2.8729085735721942674e+4) * r + 3.9307895800092710610e+4) * r +
+             2.1213794301586595867e+4) * r + 5.3941960214247511077e+3) * r + 6.8718700749205790830e+2) * r +
+          4.2313330701600911252e+1) * r + 1.0);
+    return q * num / den;
+  }
+  double r = q < 0.0 ? p : 1.0 - p;
+  r = sqrt(-log(r));
+  double val;
+  if (r <= 5.0) {
+    r -= 1.6;
+    const double num =
+        (((((((7.74545014278341407640e-4 * r + 2.27238449892691845833e-2) * r + 2.41780725177450611770e-1) * r +
+             1.27045825245236838258e0) * r + 3.64784832476320460504e0) * r + 5.76949722146069140550e0) * r +
+          4.63033784615654529590e0) * r + 1.42343711074968357734e0);
+    const double den =
+        (((((((1.05075007164441684324e-9 * r + 5.47593808499534494600e-4) * r + 1.51986665636164571966e-2) * r +
+             1.48103976427480074590e-1) * r + 6.89767334985100004550e-1) * r + 1.67638483018380384940e0) * r +
+          2.05319162663775882187e0) * r + 1.0);
+    val = num / den;
+  } else {
+    r -= 5.0;
+    const double num =
+        (((((((2.01033439929228813265e-7 * r + 2.71155556874348757815e-5) * r + 1.24266094738807843860e-3) * r +
+             2.65321895265761230930e-2) * r + 2.96560571828504891230e-1) * r + 1.78482653991729133580e0) * r +
+          5.46378491116411436990e0) * r + 6.65790464350110377720e0);
+    const double den =
+        (((((((2.04426310338993978564e-15 * r + 1.42151175831644588870e-7) * r + 1.84631831751005468180e-5) * r +
+             7.86869131145613259100e-4) * r + 1.48753612908506148525e-2) * r + 1.36929880922735805310e-1) * r +
+          5.99832206555887937690e-1) * r + 1.0);
+    val = num / den;
+  }
+  return q < 0.0 ? -val : val;
+}
+
+// Standard normal truncated to [alpha, +inf) by inversion of the upper tail:
+//   x = Phic^-1(u * Phic(alpha)) = -qnorm(u * 0.5 erfc(alpha / sqrt 2)),
 // with the exponential tail expansion beyond alpha > 25 where erfc underflows.
 __device__ __forceinline__ double trunc_normal_lower(double alpha, double u) {
   if (alpha > 25.0) return alpha - log(u) / alpha;
-  const double t = u * erfc(alpha * 0.7071067811865476);
-  return 1.4142135623730951 * erfcinv(t);
+  const double p = u * (0.5 * erfc(alpha * 0.7071067811865476));
+  return -qnorm_as241(p);
 }
 
 }  // namespace hmsc

@@ -30,7 +30,7 @@ struct Level {
   int* unit_ptr = nullptr;      // np+1 CSR over rows of each unit
   int* unit_rows = nullptr;     // ny
   int* Alpha = nullptr;         // nfmax (host mirror in State::h_alpha)
-  bool all_units_single = true; // np == ny and Pi is a permutation
+  int uniform_n = 0;            // common row count of every unit (0 if they differ)
 };
 
 struct State {
@@ -78,6 +78,8 @@ struct State {
   int* rho = nullptr;
 
   // per-sweep workspaces
+  double* XEta = nullptr;        // ny x Kmax    [X, Eta_1[Pi_1], ...] materialised per Eta update
+  bool xeta_valid = false;
   double* XZ = nullptr;          // K x ns_loc   XEta^T (Yx o Z)
   double* G = nullptr;           // Kmax x Kmax  XEta^T XEta
   double* ZTr = nullptr;         // ny x nt      Z Tr (local species)
@@ -159,6 +161,7 @@ struct ProfScope {  // records a start/stop event pair around one launch when pr
 void launch_init(State& s);
 void launch_update_z(State& s, uint32_t iter, bool use_raw_y);
 void launch_zt_refresh(State& s);
+void launch_xeta(State& s);
 void launch_beta_lambda(State& s, uint32_t iter);
 void launch_gamma_v(State& s, uint32_t iter);
 void launch_gamma2(State& s, uint32_t iter);

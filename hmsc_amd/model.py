@@ -196,10 +196,10 @@ def _r_scale(A, center=True):
     """R's scale(): centre by column means, divide by column sd (n-1)."""
     A = np.asarray(A, dtype=np.float64)
     n = A.shape[0]
-    mu = A.mean(axis=0) if center else np.zeros(A.shape[1])
-    C = A - mu
-    sd = np.sqrt((C ** 2).sum(axis=0) / (n - 1))
     with np.errstate(divide="ignore", invalid="ignore"):
+        mu = A.mean(axis=0) if center else np.zeros(A.shape[1])
+        C = A - mu
+        sd = np.sqrt((C ** 2).sum(axis=0) / (n - 1))
         return C / sd, mu, sd
 
 

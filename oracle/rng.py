@@ -12,7 +12,7 @@ the published ones, and parity with the reference is pinned at the level of
 conditional moments and posterior distributions, not R's RNG bitstream.
 """
 import numpy as np
-from scipy.special import erfc, erfcinv
+from scipy.special import erfc
 
 M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
 W0, W1 = 0x9E3779B9, 0xBB67AE85
@@ -103,7 +103,8 @@ class Rng:
             x = self.normal(idx, 2 * t, stream, it)
             v = 1.0 + c * x
             ok = v > 0.0
-            v3 = np.where(ok, v, 1.0) ** 3
+            vv = np.where(ok, v, 1.0)
+            v3 = vv * vv * vv  # same rounding as rng.h (v*v*v)
             u = self.uniforms(idx, 2 * t + 1, stream, it)[0]
             with np.errstate(invalid="ignore", divide="ignore"):
                 acc = ok & (np.log(u) < 0.5 * x * x + d - d * v3 + d * np.log(v3))
@@ -120,11 +121,50 @@ class Rng:
         return self.gamma_std(idx, stream, it, shape) / np.asarray(rate, dtype=np.float64)
 
 
+def qnorm_as241(p):
+    """Phi^-1(p): Wichura (1988) AS241 PPND16, the algorithm of R's qnorm (rng.h mirror)."""
+    p = np.asarray(p, dtype=np.float64)
+    q = p - 0.5
+    out = np.empty_like(p)
+    c = np.abs(q) <= 0.425
+    r = 0.180625 - q[c] * q[c]
+    num = (((((((2.5090809287301226727e+3 * r + 3.3430575583588128105e+4) * r + 6.7265770927008700853e+4) * r
+                + 4.5921953931549871457e+4) * r + 1.3731693765509461125e+4) * r + 1.9715909503065514427e+3) * r
+            + 1.3314166789178437745e+2) * r + 3.3871328727963666080e0)
+    den = (((((((5.2264952788528545610e+3 * r + 2.8729085735721942674e+4) * r + 3.9307895800092710610e+4) * r
+                + 2.1213794301586595867e+4) * r + 5.3941960214247511077e+3) * r + 6.8718700749205790830e+2) * r
+            + 4.2313330701600911252e+1) * r + 1.0)
+    out[c] = q[c] * num / den
+    t = ~c
+    if t.any():
+        qt, pt = q[t], p[t]
+        rr = np.sqrt(-np.log(np.where(qt < 0, pt, 1.0 - pt)))
+        lo = rr <= 5.0
+        r1 = rr - 1.6
+        n1 = (((((((7.74545014278341407640e-4 * r1 + 2.27238449892691845833e-2) * r1 + 2.41780725177450611770e-1) * r1
+                  + 1.27045825245236838258e0) * r1 + 3.64784832476320460504e0) * r1 + 5.76949722146069140550e0) * r1
+               + 4.63033784615654529590e0) * r1 + 1.42343711074968357734e0)
+        d1 = (((((((1.05075007164441684324e-9 * r1 + 5.47593808499534494600e-4) * r1 + 1.51986665636164571966e-2) * r1
+                  + 1.48103976427480074590e-1) * r1 + 6.89767334985100004550e-1) * r1 + 1.67638483018380384940e0) * r1
+               + 2.05319162663775882187e0) * r1 + 1.0)
+        r2 = rr - 5.0
+        n2 = (((((((2.01033439929228813265e-7 * r2 + 2.71155556874348757815e-5) * r2 + 1.24266094738807843860e-3) * r2
+                  + 2.65321895265761230930e-2) * r2 + 2.96560571828504891230e-1) * r2 + 1.78482653991729133580e0) * r2
+               + 5.46378491116411436990e0) * r2 + 6.65790464350110377720e0)
+        d2 = (((((((2.04426310338993978564e-15 * r2 + 1.42151175831644588870e-7) * r2 + 1.84631831751005468180e-5) * r2
+                  + 7.86869131145613259100e-4) * r2 + 1.48753612908506148525e-2) * r2 + 1.36929880922735805310e-1) * r2
+               + 5.99832206555887937690e-1) * r2 + 1.0)
+        val = np.where(lo, n1 / d1, n2 / d2)
+        out[t] = np.where(qt < 0, -val, val)
+    return out
+
+
 def trunc_normal_lower(alpha, u):
-    """Standard normal truncated to [alpha, inf) by upper-tail inversion (rng.h)."""
-    alpha = np.asarray(alpha, dtype=np.float64)
+    """Standard normal truncated to [alpha, inf) by upper-tail inversion (rng.h):
+    x = -qnorm(u * Phic(alpha)), exponential tail beyond alpha > 25."""
+    alpha, u = np.broadcast_arrays(np.asarray(alpha, dtype=np.float64), np.asarray(u, dtype=np.float64))
     with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
-        t = u * erfc(alpha * 0.7071067811865476)
-        x = 1.4142135623730951 * erfcinv(t)
+        p = u * (0.5 * erfc(alpha * 0.7071067811865476))
+        x = -qnorm_as241(p.ravel()).reshape(p.shape)
         tail = alpha - np.log(u) / np.where(alpha == 0, 1.0, alpha)
     return np.where(alpha > 25.0, tail, x)

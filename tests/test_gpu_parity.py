@@ -37,7 +37,8 @@ MODELS = {
     "probit": dict(ny=300, ns=40, nc=4, nf=3),
     "probit_na": dict(ny=200, ns=30, nc=3, nf=2, na_frac=0.05, seed=3),
     "mixed_normal": dict(ny=150, ns=20, nc=3, nf=2, n_normal=5, seed=4),
-    "two_levels_units": dict(ny=240, ns=25, nc=3, nf=2, nr=2, units=[240, 30], seed=5),
+    "two_levels_units": dict(ny=240, ns=25, nc=3, nf=2, nr=2, units=[240, 37], seed=5),
+    "grouped_units": dict(ny=240, ns=20, nc=3, nf=3, nr=1, units=[40], seed=8),
     "traits": dict(ny=120, ns=35, nc=3, nf=2, nt=3, seed=6),
 }
 
