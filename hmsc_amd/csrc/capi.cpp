@@ -128,9 +128,10 @@ static void d2h(T* h, const T* d, size_t n, hipStream_t st) {
   if (n) HIP_OK(hipMemcpyAsync(h, d, n * sizeof(T), hipMemcpyDeviceToHost, st));
 }
 
-void allreduce_sum(State& s, double* buf, size_t n) {
+void allreduce_sum(State& s, double* buf, size_t n, hipStream_t st = nullptr);
+void allreduce_sum(State& s, double* buf, size_t n, hipStream_t st) {
   if (s.nranks <= 1) return;
-  const ncclResult_t r = ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, (ncclComm_t)s.comm, s.stream);
+  const ncclResult_t r = ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, (ncclComm_t)s.comm, st ? st : s.stream);
   HMSC_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
 }
 
@@ -159,6 +160,9 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   DeviceGuard dg(device);
   HIP_OK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&s.copy_stream, hipStreamNonBlocking));
+  HIP_OK(hipStreamCreateWithFlags(&s.side, hipStreamNonBlocking));
+  HIP_OK(hipEventCreateWithFlags(&s.ev_bl, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&s.ev_side, hipEventDisableTiming));
   if (nranks > 1) {
     HMSC_REQUIRE(comm_id != nullptr, "sharded chain needs an RCCL unique id");
     ncclUniqueId id;
@@ -304,7 +308,8 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   for (int a = 0; a < nc; ++a)
     for (int b = 0; b < nc; ++b) iV0[a + nc * b] = iUG[a + N * b];  // iUGamma[1:nc,1:nc] (R/updateGamma2.R:37)
   Mat V0g = host_inv_spd(iV0, nc);
-  Mat V0gXXV0g = host_mm(host_mm(V0g, XX, nc, nc, nc), V0g, nc, nc, nc);
+  Mat V0gXX = host_mm(V0g, XX, nc, nc, nc);
+  Mat V0gXXV0g = host_mm(V0gXX, V0g, nc, nc, nc);
   Mat V0(m->V0, m->V0 + (size_t)nc * nc);
   Mat V0inv = host_inv_spd(V0, nc);
   s.XX = dupload(XX.data(), XX.size());
@@ -314,9 +319,15 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.iV0 = dupload(iV0.data(), iV0.size());
   s.V0g = dupload(V0g.data(), V0g.size());
   s.V0gXXV0g = dupload(V0gXXV0g.data(), V0gXXV0g.size());
+  s.V0gXX = dupload(V0gXX.data(), V0gXX.size());
+  s.g2prep = dalloc<double>(2 * (size_t)nc * nc + 2 * (size_t)N * N);
   s.V0 = dupload(V0.data(), V0.size());
   s.V0inv = dupload(V0inv.data(), V0inv.size());
   s.mGamma = dupload(m->mGamma, (size_t)N);
+  Mat iUmG(N, 0.0);
+  for (int a = 0; a < N; ++a)
+    for (int b = 0; b < N; ++b) iUmG[a] += iUG[a + N * b] * m->mGamma[b];
+  s.iUmG = dupload(iUmG.data(), N);
   // state
   s.Z = dalloc<double>((size_t)ny * nsl);
   s.BL = dalloc<double>((size_t)s.Kmax * nsl);
@@ -343,10 +354,12 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.ZL = dalloc<double>((size_t)ny * nfm);
   s.ZL_part = dalloc<double>((size_t)s.zl_split * ny * nfm);
   s.CR = dalloc<double>((size_t)s.Kmax * nfm);
+  s.CR_part = dalloc<double>((size_t)((nsl + 31) / 32) * s.Kmax * nfm);
   s.scratch_doubles = 1 << 20;
   s.scratch = dalloc<double>(s.scratch_doubles);
+  s.scratch2 = dalloc<double>(s.scratch_doubles);
   s.psi_rs = dalloc<double>((size_t)64 * nfm);
-  s.ABpart = dalloc<double>((size_t)32 * (nc * nc + N + nfm * nt));
+  s.ABpart = dalloc<double>((size_t)((nsl + 31) / 32) * (nc * nc + 2 * N + nfm * nt + 8));
   s.allreduce_buf = dalloc<double>((size_t)nc * nc + 2 * N + nfm * nt + nfm + 64);
   s.dev_flags = dalloc<int>(16);
   HIP_OK(hipDeviceSynchronize());
@@ -356,10 +369,10 @@ static void free_state(State& s) {
   DeviceGuard dg(s.device);
   (void)hipDeviceSynchronize();
   void* ptrs[] = {s.X, s.Tr, s.Yval, s.Yraw, s.Ycode, s.fam, s.varest, s.V0, s.iUGamma, s.mGamma, s.UGammaL,
-                  s.aSigma, s.bSigma, s.XX, s.TT, s.V0g, s.V0gXXV0g, s.iV0, s.V0inv, s.na_cols, s.na_index,
+                  s.aSigma, s.bSigma, s.XX, s.TT, s.V0g, s.V0gXXV0g, s.iV0, s.V0inv, s.iUmG, s.V0gXX, s.g2prep, s.scratch2, s.na_cols, s.na_index,
                   s.na_rows, s.row_na, s.row_slot, s.dev_flags, s.Z, s.XEta, s.BL, s.Psi, s.Delta, s.Gamma, s.iV,
                   s.iSigma, s.rho, s.XZ, s.G, s.ZTr, s.XZ_part, s.G_part, s.ZTr_part, s.Gna, s.ZL, s.ZL_part,
-                  s.CR, s.Msmall, s.scratch, s.psi_rs, s.ABpart, s.dbg_prec, s.ring, s.allreduce_buf};
+                  s.CR, s.CR_part, s.Msmall, s.scratch, s.psi_rs, s.ABpart, s.dbg_prec, s.ring, s.allreduce_buf};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (int r = 0; r < s.nr; ++r) {
@@ -371,13 +384,26 @@ static void free_state(State& s) {
   for (hipEvent_t e : s.ring_done) (void)hipEventDestroy(e);
   if (s.host_rec) (void)hipHostFree(s.host_rec);
   if (s.comm) ncclCommDestroy((ncclComm_t)s.comm);
+  if (s.ev_bl) (void)hipEventDestroy(s.ev_bl);
+  if (s.ev_side) (void)hipEventDestroy(s.ev_side);
+  if (s.side) (void)hipStreamDestroy(s.side);
   if (s.stream) (void)hipStreamDestroy(s.stream);
   if (s.copy_stream) (void)hipStreamDestroy(s.copy_stream);
+}
+
+// Wait on the main stream for the side-stream work of the previous sweep (it writes Gamma,
+// iV, Psi, Delta and Gamma2's iV-only matrices).
+static void join_side(State& s) {
+  if (s.side_pending) {
+    HIP_OK(hipStreamWaitEvent(s.stream, s.ev_side, 0));
+    s.side_pending = false;
+  }
 }
 
 // ---------------------------- state get / set ----------------------------
 static void get_state(State& s, hmsc_params* p) {
   DeviceGuard dg(s.device);
+  join_side(s);
   HIP_OK(hipStreamSynchronize(s.stream));
   const int K = s.K, nsl = s.nsl, nc = s.nc;
   std::vector<double> BL((size_t)K * nsl), Psi((size_t)s.NF * nsl), Delta(std::max(1, s.NF));
@@ -413,6 +439,7 @@ static void get_state(State& s, hmsc_params* p) {
 
 static void set_state(State& s, const hmsc_params* p) {
   DeviceGuard dg(s.device);
+  join_side(s);
   HIP_OK(hipStreamSynchronize(s.stream));
   for (int r = 0; r < s.nr; ++r) {
     if (p->nf[r] > 0) {
@@ -452,6 +479,7 @@ static void set_state(State& s, const hmsc_params* p) {
   HIP_OK(hipStreamSynchronize(s.stream));
   s.zt_valid = false;
   s.xeta_valid = false;
+  s.g2prep_valid = false;
 }
 
 // ---------------------------- updateNf (host decision) ----------------------------
@@ -572,12 +600,12 @@ static void run_updater(State& s, uint32_t which, uint32_t iter) {
       launch_beta_lambda(s, iter);
       break;
     case HMSC_UP_GAMMAV:
-      launch_gamma_v(s, iter);
+      launch_gamma_v(s, iter, s.stream);
       break;
     case HMSC_UP_RHO:
       break;  // C is NULL: updateRho is not called (R/sampleMcmc.R:263)
     case HMSC_UP_LAMBDAPRIORS:
-      launch_lambda_priors(s, iter);
+      launch_lambda_priors(s, iter, s.stream);
       break;
     case HMSC_UP_ETA:
       launch_eta(s, iter);
@@ -595,15 +623,34 @@ static void run_updater(State& s, uint32_t which, uint32_t iter) {
   }
 }
 
+// One sweep in the reference order (R/sampleMcmc.R:219-306).  updateGammaV and
+// updateLambdaPriors of sweep t only feed sweep t+1 (Gamma2 / BetaLambda and the record),
+// so they run on the side stream after BetaLambda, overlapped with Eta / InvSigma / Z.
 static void sweep(State& s, uint32_t iter, bool adapt) {
   ProfScope ps(s, PROF_SWEEP);
-  static const uint32_t order[] = {HMSC_UP_GAMMA2,       HMSC_UP_GAMMAETA, HMSC_UP_BETALAMBDA, HMSC_UP_GAMMAV,
-                                   HMSC_UP_RHO,          HMSC_UP_LAMBDAPRIORS, HMSC_UP_ETA,  HMSC_UP_ALPHA,
-                                   HMSC_UP_INVSIGMA,     HMSC_UP_Z};
-  for (uint32_t u : order)
+  join_side(s);
+  if (s.mask & HMSC_UP_GAMMA2) run_updater(s, HMSC_UP_GAMMA2, iter);
+  if (s.mask & HMSC_UP_GAMMAETA) run_updater(s, HMSC_UP_GAMMAETA, iter);
+  if (s.mask & HMSC_UP_BETALAMBDA) run_updater(s, HMSC_UP_BETALAMBDA, iter);
+  // (sharded chains keep every RCCL collective on one stream: no side-stream overlap)
+  const bool side_work = s.nranks == 1 && (s.mask & (HMSC_UP_GAMMAV | HMSC_UP_LAMBDAPRIORS)) != 0;
+  if (side_work) {
+    HIP_OK(hipEventRecord(s.ev_bl, s.stream));
+    HIP_OK(hipStreamWaitEvent(s.side, s.ev_bl, 0));
+    if (s.mask & HMSC_UP_GAMMAV) launch_gamma_v(s, iter, s.side);
+    if (s.mask & HMSC_UP_LAMBDAPRIORS) launch_lambda_priors(s, iter, s.side);
+    HIP_OK(hipEventRecord(s.ev_side, s.side));
+    s.side_pending = true;
+  } else {
+    if (s.mask & HMSC_UP_GAMMAV) launch_gamma_v(s, iter, s.stream);
+    if (s.mask & HMSC_UP_LAMBDAPRIORS) launch_lambda_priors(s, iter, s.stream);
+  }
+  for (uint32_t u : {HMSC_UP_ETA, HMSC_UP_ALPHA, HMSC_UP_INVSIGMA, HMSC_UP_Z})
     if (s.mask & u) run_updater(s, u, iter);
-  if (adapt)
+  if (adapt) {
+    join_side(s);
     for (int r = 0; r < s.nr; ++r) update_nf(s, r, iter);
+  }
 }
 
 static void unpack_record(const State& s, const double* slot, int k, int samples, hmsc_record* rec) {
@@ -692,6 +739,7 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
       const int slot = k % s.ring_slots;
       if (k >= s.ring_slots) HIP_OK(hipStreamWaitEvent(s.stream, s.ring_done[slot], 0));
       double* dslot = s.ring + s.slot_doubles * slot;
+      join_side(s);
       launch_record(s, dslot);
       HIP_OK(hipEventRecord(packed[slot], s.stream));
       HIP_OK(hipStreamWaitEvent(s.copy_stream, packed[slot], 0));
@@ -706,12 +754,13 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
       std::fflush(stdout);
     }
   }
+  join_side(s);
   HIP_OK(hipStreamSynchronize(s.stream));
   HIP_OK(hipStreamSynchronize(s.copy_stream));
   for (auto& e : packed) HIP_OK(hipEventDestroy(e));
-  int flag = 0;
-  HIP_OK(hipMemcpy(&flag, s.dev_flags, sizeof(int), hipMemcpyDeviceToHost));
-  HMSC_REQUIRE(flag == 0, "a Cholesky factorisation failed (matrix not positive definite)");
+  int flag[2] = {0, 0};
+  HIP_OK(hipMemcpy(flag, s.dev_flags, sizeof(flag), hipMemcpyDeviceToHost));
+  HMSC_REQUIRE(flag[0] == 0 && flag[1] == 0, "a Cholesky factorisation failed (matrix not positive definite)");
   if (recording)
     for (int k = 0; k < samples; ++k) unpack_record(s, s.host_rec + s.slot_doubles * k, k, samples, rec);
 }
@@ -845,6 +894,7 @@ int hmsc_run_verbose(hmsc_state* h, int32_t transient, int32_t samples, int32_t 
 int hmsc_sync(hmsc_state* h) {
   return guarded([&] {
     DeviceGuard dg(h->s.device);
+    join_side(h->s);
     HIP_OK(hipStreamSynchronize(h->s.stream));
     HIP_OK(hipStreamSynchronize(h->s.copy_stream));
   });
@@ -854,6 +904,7 @@ int hmsc_debug_get(hmsc_state* h, const char* name, double* out, int64_t n) {
   return guarded([&] {
     State& s = h->s;
     DeviceGuard dg(s.device);
+    join_side(s);
     HIP_OK(hipStreamSynchronize(s.stream));
     const std::string nm(name);
     const double* src = nullptr;

@@ -37,25 +37,27 @@ constexpr int WAVE = 64;
 // ---------------------------------------------------------------------------
 
 // In-place lower Cholesky A = L L^T (lower triangle overwritten, upper untouched).
+// Right-looking, two barriers per column; the trailing update is distributed over a
+// 32 (rows) x (blockDim/32) (columns) thread grid so no integer division is needed.
 // Returns false (uniformly) if A is not positive definite.
 __device__ inline bool wg_chol(double* A, int n, int lda, int* flag) {
   const int t = threadIdx.x, nt = blockDim.x;
+  const int tr = t & 31, tc = t >> 5, ntc = nt >> 5;
   if (t == 0) *flag = 0;
   __syncthreads();
   for (int c = 0; c < n; ++c) {
-    if (t == 0) {
-      const double d = A[c + c * lda];
-      if (!(d > 0.0)) *flag = 1;
-      A[c + c * lda] = sqrt(d > 0.0 ? d : 1.0);
-    }
-    __syncthreads();
-    const double inv = 1.0 / A[c + c * lda];
+    const double d = A[c + c * lda];
+    const double sd = sqrt(d > 0.0 ? d : 1.0);
+    const double inv = 1.0 / sd;
     for (int i = c + 1 + t; i < n; i += nt) A[i + c * lda] *= inv;
     __syncthreads();
-    const int m = n - c - 1;
-    for (int p = t; p < m * m; p += nt) {
-      const int i = c + 1 + p % m, j = c + 1 + p / m;
-      if (i >= j) A[i + j * lda] -= A[i + c * lda] * A[j + c * lda];
+    if (t == 0) {
+      if (!(d > 0.0)) *flag = 1;
+      A[c + c * lda] = sd;
+    }
+    for (int i = c + 1 + tr; i < n; i += 32) {
+      const double lic = A[i + c * lda];
+      for (int j = c + 1 + tc; j <= i; j += ntc) A[i + j * lda] -= lic * A[j + c * lda];
     }
     __syncthreads();
   }
@@ -88,49 +90,57 @@ __device__ inline void t0_backward_t(const double* L, int n, int lda, double* x)
   __syncthreads();
 }
 
-// Wave-parallel triangular solves for one right-hand side (blockDim == 64 users):
-// column-oriented, one barrier per column.
+// Triangular solves for one right-hand side, column-oriented, one barrier per column:
+// the pivot x_c is final once column c-1 has been applied; every thread reads it.
 __device__ inline void wg_forward(const double* L, int n, int lda, double* x) {
   const int t = threadIdx.x, nt = blockDim.x;
   for (int c = 0; c < n; ++c) {
-    if (t == 0) x[c] /= L[c + c * lda];
-    __syncthreads();
-    const double xc = x[c];
+    const double xc = x[c] / L[c + c * lda];
     for (int i = c + 1 + t; i < n; i += nt) x[i] -= L[i + c * lda] * xc;
     __syncthreads();
+    if (t == 0) x[c] = xc;
   }
+  __syncthreads();
 }
 
 __device__ inline void wg_backward_t(const double* L, int n, int lda, double* x) {
   const int t = threadIdx.x, nt = blockDim.x;
   for (int c = n - 1; c >= 0; --c) {
-    if (t == 0) x[c] /= L[c + c * lda];
-    __syncthreads();
-    const double xc = x[c];
+    const double xc = x[c] / L[c + c * lda];
     for (int i = t; i < c; i += nt) x[i] -= L[c + i * lda] * xc;
     __syncthreads();
+    if (t == 0) x[c] = xc;
   }
+  __syncthreads();
 }
 
 // Inv <- (L L^T)^{-1} (R's chol2inv), Inv n x n with leading dim ldi; W scratch n*n.
+// W = L^{-1} by column-oriented forward elimination of all n right-hand sides at once
+// (one barrier per pivot), then Inv = W^T W.
 __device__ inline void wg_chol2inv(const double* L, int n, int lda, double* Inv, int ldi, double* W) {
   const int t = threadIdx.x, nt = blockDim.x;
-  // W = L^{-1}, column by column (each thread one column of the identity)
-  for (int c = t; c < n; c += nt) {
-    for (int i = 0; i < n; ++i) {
-      double s = (i == c) ? 1.0 : 0.0;
-      for (int k = c; k < i; ++k) s -= L[i + k * lda] * W[k + c * n];
-      W[i + c * n] = (i < c) ? 0.0 : s / L[i + i * lda];
-    }
-  }
+  const int tr = t & 31, tc = t >> 5, ntc = nt >> 5;
+  for (int i = tr; i < n; i += 32)
+    for (int j = tc; j < n; j += ntc) W[i + j * n] = (i == j) ? 1.0 : 0.0;
   __syncthreads();
-  // Inv = W^T W
-  for (int p = t; p < n * n; p += nt) {
-    const int i = p % n, j = p / n;
-    double s = 0.0;
-    for (int k = (i > j ? i : j); k < n; ++k) s += W[k + i * n] * W[k + j * n];
-    Inv[i + j * ldi] = s;
+  for (int c = 0; c < n; ++c) {
+    const double inv = 1.0 / L[c + c * lda];
+    // row c of W is final (columns j <= c); rows i > c get -L_ic * W_cj
+    for (int i = c + 1 + tr; i < n; i += 32) {
+      const double lic = L[i + c * lda] * inv;
+      for (int j = tc; j <= c; j += ntc) W[i + j * n] -= lic * W[c + j * n];
+    }
+    __syncthreads();
+    for (int j = t; j <= c; j += nt) W[c + j * n] *= inv;
+    __syncthreads();
   }
+  // Inv = W^T W (W lower triangular)
+  for (int i = tr; i < n; i += 32)
+    for (int j = tc; j < n; j += ntc) {
+      double s = 0.0;
+      for (int k = (i > j ? i : j); k < n; ++k) s += W[k + i * n] * W[k + j * n];
+      Inv[i + j * ldi] = s;
+    }
   __syncthreads();
 }
 
@@ -138,25 +148,26 @@ __device__ inline void wg_chol2inv(const double* L, int n, int lda, double* Inv,
 __device__ inline void wg_gemm(int m, int n, int k, double alpha, const double* A, int lda, bool ta,
                                const double* B, int ldb, bool tb, double beta, double* C, int ldc) {
   const int t = threadIdx.x, nt = blockDim.x;
-  for (int p = t; p < m * n; p += nt) {
-    const int i = p % m, j = p / m;
-    double s = 0.0;
-    for (int q = 0; q < k; ++q) {
-      const double a = ta ? A[q + i * lda] : A[i + q * lda];
-      const double b = tb ? B[j + q * ldb] : B[q + j * ldb];
-      s += a * b;
+  const int tr = t & 31, tc = t >> 5, ntc = nt >> 5;
+  const int sa_i = ta ? lda : 1, sa_q = ta ? 1 : lda;
+  const int sb_q = tb ? ldb : 1, sb_j = tb ? 1 : ldb;
+  for (int i = tr; i < m; i += 32)
+    for (int j = tc; j < n; j += ntc) {
+      double s = 0.0;
+      const double* a = A + i * sa_i;
+      const double* b = B + j * sb_j;
+      for (int q = 0; q < k; ++q) s = fma(a[q * sa_q], b[q * sb_q], s);
+      C[i + j * ldc] = alpha * s + (beta == 0.0 ? 0.0 : beta * C[i + j * ldc]);
     }
-    C[i + j * ldc] = alpha * s + (beta == 0.0 ? 0.0 : beta * C[i + j * ldc]);
-  }
   __syncthreads();
 }
 
 // zero the strict upper triangle (turn an in-place wg_chol result into a clean L)
 __device__ inline void wg_lower_only(double* A, int n, int lda) {
-  for (int p = threadIdx.x; p < n * n; p += blockDim.x) {
-    const int i = p % n, j = p / n;
-    if (i < j) A[i + j * lda] = 0.0;
-  }
+  const int t = threadIdx.x, tr = t & 31, tc = t >> 5, ntc = blockDim.x >> 5;
+  for (int i = tr; i < n; i += 32)
+    for (int j = tc; j < n; j += ntc)
+      if (i < j) A[i + j * lda] = 0.0;
   __syncthreads();
 }
 

@@ -50,6 +50,8 @@ __device__ __forceinline__ double xeta_at(const EtaView& v, int i, int k) {
   return 0.0;
 }
 
+static void launch_gamma2_prep(State& s, hipStream_t st);
+
 static EtaView make_view(const State& s) {
   EtaView v{};
   v.X = s.X;
@@ -90,33 +92,62 @@ struct ZArgs {
   int noise_zero;
 };
 
-constexpr int ZT_I = 64;   // sites per tile (one per lane)
-constexpr int ZT_J = 32;   // species per tile (8 per wave)
-constexpr int ZT_LD = 65;  // padded LDS leading dimension (conflict-free column reads)
+constexpr int ZT_I = 64;   // sites per tile (4 waves x 16)
+constexpr int ZT_J = 32;   // species per tile (2 MFMA column blocks of 16)
+constexpr int ZT_LD = 65;  // padded LDS leading dimension
 constexpr int KMAX_Z = 64;
 
-// KQ = accumulators per thread for the XZ contraction: rows k = kq + 8q, q < KQ  (K <= 8*KQ)
-template <bool DRAW, bool HAS_NA, int KQ>
-__global__ __launch_bounds__(256, 4) void z_fused_kernel(ZArgs a) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int K = a.K;
-  const int ny = a.ev.ny;
-  double* sXE = smem;                  // [k][ZT_LD]
-  double* sBL = sXE + K * ZT_LD;       // [k][ZT_J]
-  double* sZ = sBL + K * ZT_J;         // [jj][ZT_LD]   E, then masked Z (XZ)
-  double* sZu = sZ + ZT_J * ZT_LD;     // [jj][ZT_LD]   unmasked Z (ZTr), HAS_NA only
-  double* sTr = (HAS_NA ? sZu + ZT_J * ZT_LD : sZu);  // [jj + ZT_J t]
-  double* sSd = sTr + ZT_J * a.nt;     // [jj]
-  int* sFam = (int*)(sSd + ZT_J);      // [jj]
+typedef double d4 __attribute__((ext_vector_type(4)));
 
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+// v_mfma_f64_16x16x4_f64: D[16x16] += A[16x4] B[4x16]; lane l supplies A[l&15][l>>4] and
+// B[l>>4][l&15] and holds D[(l>>4) + 4r][l&15], r = 0..3 (checked by scripts/mfma_layout_check.hip).
+__device__ __forceinline__ d4 mfma_f64(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// one latent draw; kept out of line so the polynomial constants of erfc / AS241 are
+// materialised per call instead of being hoisted into the kernel's register file
+__device__ __noinline__ double z_draw(double e, double sd, int code, int fam, double yv, Key key, uint32_t idx,
+                                      uint32_t iter, int noise_zero) {
+  if (code < 0) {  // NA cell: Z ~ N(E, sd)   R/updateZ.R:92
+    const double nz = noise_zero ? 0.0 : normal(key, idx, 0, S_Z, iter);
+    return e + sd * nz;
+  }
+  if (fam == 2) {  // probit: truncated normal   R/updateZ.R:43-63
+    const double u = uniforms(key, idx, 0, S_Z, iter).a;
+    const double sg = code ? 1.0 : -1.0;
+    return e + sd * sg * trunc_normal_lower(-sg * e / sd, u);
+  }
+  return yv;  // normal: Z = Y   R/updateZ.R:40-41
+}
+
+// Fused updateZ.  Per 64-site x 32-species tile:
+//   E^T = BL^T XEta^T on the matrix cores (2 MFMA blocks per wave, K/4 steps),
+//   truncated-normal draws on the VALU (8 per lane), Z stored once,
+//   XZ += XEta^T (Yx o Z) on the matrix cores (accumulated over the chunk's tiles),
+//   ZTr += Z Tr (VALU, nt small).
+// NQ = XZ output tiles per wave (K <= 32: 1, K <= 64: 2).
+template <bool DRAW, bool HAS_NA, int NQ>
+__global__ __launch_bounds__(256) void z_fused_kernel(ZArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int K = a.K, K4 = (K + 3) & ~3, K16 = (K + 15) & ~15;
+  const int ny = a.ev.ny;
+  double* sXE = smem;                   // [K16][ZT_LD], rows >= K zero
+  double* sBL = sXE + K16 * ZT_LD;      // [K4][ZT_J],   rows >= K zero
+  double* sZ = sBL + K4 * ZT_J;         // [jj][ZT_LD]   masked Z (XZ)
+  double* sZu = sZ + ZT_J * ZT_LD;      // [jj][ZT_LD]   unmasked Z (ZTr), HAS_NA only
+  double* sTr = (HAS_NA ? sZu + ZT_J * ZT_LD : sZu);  // [jj + ZT_J t]
+  double* sSd = sTr + ZT_J * a.nt;      // [jj]
+  int* sFam = (int*)(sSd + ZT_J);       // [jj]
+
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, lm = lane & 15, lk = lane >> 4;
   const int j0 = blockIdx.y * ZT_J;
-  for (int p = t; p < K * ZT_J; p += 256) {
-    const int k = p / ZT_J, jj = p % ZT_J, j = j0 + jj;
-    sBL[p] = (j < a.ns_loc) ? a.BL[k + (size_t)K * j] : 0.0;
+  for (int p = t; p < K4 * ZT_J; p += 256) {
+    const int k = p >> 5, jj = p & 31, j = j0 + jj;
+    sBL[p] = (k < K && j < a.ns_loc) ? a.BL[k + (size_t)K * j] : 0.0;
   }
   for (int p = t; p < ZT_J * a.nt; p += 256) {
-    const int jj = p % ZT_J, tt = p / ZT_J, j = j0 + jj;
+    const int jj = p & 31, tt = p >> 5, j = j0 + jj;
     sTr[p] = (j < a.ns_loc) ? a.Tr[j + (size_t)a.ns_loc * tt] : 0.0;
   }
   if (t < ZT_J) {
@@ -124,11 +155,10 @@ __global__ __launch_bounds__(256, 4) void z_fused_kernel(ZArgs a) {
     sSd[t] = (j < a.ns_loc) ? 1.0 / sqrt(a.iSigma[j]) : 1.0;
     sFam[t] = (j < a.ns_loc) ? a.fam[j] : 0;
   }
-
-  const int xj = t & 31, xkq = t >> 5;  // XZ mapping: species xj, rows k = xkq + 8q
-  double accXZ[KQ];
+  d4 accXZ[NQ];
 #pragma unroll
-  for (int q = 0; q < KQ; ++q) accXZ[q] = 0.0;
+  for (int q = 0; q < NQ; ++q) accXZ[q] = d4{0.0, 0.0, 0.0, 0.0};
+  const int n_xz_tiles = 2 * (K16 >> 4);
 
   const int n_tiles = (ny + ZT_I - 1) / ZT_I;
   const int tb = blockIdx.x * a.tiles_per_chunk;
@@ -136,101 +166,91 @@ __global__ __launch_bounds__(256, 4) void z_fused_kernel(ZArgs a) {
   for (int tile = tb; tile < te; ++tile) {
     const int i0 = tile * ZT_I;
     __syncthreads();
-    for (int p = t; p < K * ZT_I; p += 256) {
+    for (int p = t; p < K16 * ZT_I; p += 256) {
       const int k = p >> 6, ii = p & 63, i = i0 + ii;
-      sXE[k * ZT_LD + ii] = (i < ny) ? a.XEta[i + (size_t)ny * k] : 0.0;
+      sXE[k * ZT_LD + ii] = (i < ny && k < K) ? a.XEta[i + (size_t)ny * k] : 0.0;
     }
     __syncthreads();
-    const int i = i0 + lane;
+    const int iloc = 16 * w + lm, i = i0 + iloc;
+    double zv[8];
     if (DRAW) {
-      // E = XEta BL for this lane's site and the wave's 8 species (R/updateZ.R:11-34)
-      double e[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) e[q] = 0.0;
-      for (int k = 0; k < K; ++k) {
-        const double x = sXE[k * ZT_LD + lane];
-        const double* b = sBL + k * ZT_J + w * 8;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) e[q] = fma(x, b[q], e[q]);
+      // E^T tile: rows = species (2 blocks of 16), cols = this wave's 16 sites   (R/updateZ.R:11-34)
+      d4 e0 = {0.0, 0.0, 0.0, 0.0}, e1 = {0.0, 0.0, 0.0, 0.0};
+      for (int k = lk; k < K4; k += 4) {
+        const double b = sXE[k * ZT_LD + iloc];
+        e0 = mfma_f64(sBL[k * ZT_J + lm], b, e0);
+        e1 = mfma_f64(sBL[k * ZT_J + 16 + lm], b, e1);
       }
 #pragma unroll
-      for (int q = 0; q < 8; ++q) sZ[(w * 8 + q) * ZT_LD + lane] = e[q];
-#pragma unroll 1
-      for (int q = 0; q < 8; ++q) {
-        const int jj = w * 8 + q, j = j0 + jj;
-        const double eq = sZ[jj * ZT_LD + lane];
+      for (int v = 0; v < 8; ++v) {
+        const int jj = 16 * (v >> 2) + lk + 4 * (v & 3), j = j0 + jj;
+        const double ev = (v < 4) ? e0[v & 3] : e1[v & 3];
         double z = 0.0;
-        bool obs = false;
         if (i < ny && j < a.ns_loc) {
           const size_t cell = (size_t)i + (size_t)ny * j;
           const uint32_t idx = (uint32_t)((size_t)i + (size_t)ny * (size_t)(a.sp0 + j));
-          const double sd = sSd[jj];
           const int code = a.Ycode[cell];
-          obs = code >= 0;
-          if (code < 0) {  // NA cell: Z ~ N(E, sd)   R/updateZ.R:92
-            const double nz = a.noise_zero ? 0.0 : normal(a.key, idx, 0, S_Z, a.iter);
-            z = eq + sd * nz;
-          } else if (sFam[jj] == 2) {  // probit: truncated normal   R/updateZ.R:43-63
-            const double u = uniforms(a.key, idx, 0, S_Z, a.iter).a;
-            const double sg = code ? 1.0 : -1.0;
-            z = eq + sd * sg * trunc_normal_lower(-sg * eq / sd, u);
-          } else {  // normal: Z = Y   R/updateZ.R:40-41
-            z = a.Yval[cell];
-          }
+          const int fam = sFam[jj];
+          z = z_draw(ev, sSd[jj], code, fam, fam == 1 ? a.Yval[cell] : 0.0, a.key, idx, a.iter, a.noise_zero);
           a.Z[cell] = z;
         }
-        if (HAS_NA) {
-          sZ[jj * ZT_LD + lane] = obs ? z : 0.0;
-          sZu[jj * ZT_LD + lane] = z;
-        } else {
-          sZ[jj * ZT_LD + lane] = z;
-        }
+        zv[v] = z;
       }
     } else {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int jj = w * 8 + q, j = j0 + jj;
-        const double z = (i < ny && j < a.ns_loc) ? a.Z[(size_t)i + (size_t)ny * j] : 0.0;
-        if (HAS_NA) {
-          const bool obs = (i < ny && j < a.ns_loc) ? (a.Ycode[(size_t)i + (size_t)ny * j] >= 0) : false;
-          sZ[jj * ZT_LD + lane] = obs ? z : 0.0;
-          sZu[jj * ZT_LD + lane] = z;
-        } else {
-          sZ[jj * ZT_LD + lane] = z;
-        }
+      for (int v = 0; v < 8; ++v) {
+        const int jj = 16 * (v >> 2) + lk + 4 * (v & 3), j = j0 + jj;
+        zv[v] = (i < ny && j < a.ns_loc) ? a.Z[(size_t)i + (size_t)ny * j] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      const int jj = 16 * (v >> 2) + lk + 4 * (v & 3), j = j0 + jj;
+      if (HAS_NA) {
+        const bool obs = (i < ny && j < a.ns_loc) ? (a.Ycode[(size_t)i + (size_t)ny * j] >= 0) : false;
+        sZ[jj * ZT_LD + iloc] = obs ? zv[v] : 0.0;
+        sZu[jj * ZT_LD + iloc] = zv[v];
+      } else {
+        sZ[jj * ZT_LD + iloc] = zv[v];
       }
     }
     __syncthreads();
-    // XZ partial (R/updateBetaLambda.R:66 for the next sweep): species xj, rows xkq + 8q
-    {
-      const double* zc = sZ + xj * ZT_LD;
-      for (int ii = 0; ii < ZT_I; ++ii) {
-        const double zv = zc[ii];
+    // XZ += XEta^T (Yx o Z) over the tile's 64 sites   (R/updateBetaLambda.R:66 of the next sweep)
 #pragma unroll
-        for (int q = 0; q < KQ; ++q) {
-          const int k = xkq + 8 * q;
-          if (k < K) accXZ[q] = fma(sXE[k * ZT_LD + ii], zv, accXZ[q]);
-        }
+    for (int q = 0; q < NQ; ++q) {
+      const int id = w + 4 * q;
+      if (id < n_xz_tiles) {
+        const int kb = id >> 1, sbb = id & 1;
+        const double* ar = sXE + (kb * 16 + lm) * ZT_LD;
+        const double* br = sZ + (16 * sbb + lm) * ZT_LD;
+        for (int st = lk; st < ZT_I; st += 4) accXZ[q] = mfma_f64(ar[st], br[st], accXZ[q]);
       }
     }
     // ZTr partial for this (site tile, species tile)   (R/updateGamma2.R:46)
-    if (i < ny) {
-      const double* zsrc = HAS_NA ? sZu : sZ;
-      for (int tt = w; tt < a.nt; tt += 4) {
-        double acc = 0.0;
+    {
+      const int ii = lane, is = i0 + lane;
+      if (is < ny) {
+        const double* zsrc = HAS_NA ? sZu : sZ;
+        for (int tt = w; tt < a.nt; tt += 4) {
+          double acc = 0.0;
 #pragma unroll 8
-        for (int jj = 0; jj < ZT_J; ++jj) acc = fma(zsrc[jj * ZT_LD + lane], sTr[jj + ZT_J * tt], acc);
-        a.ZTr_part[(size_t)blockIdx.y * ny * a.nt + i + (size_t)ny * tt] = acc;
+          for (int jj = 0; jj < ZT_J; ++jj) acc = fma(zsrc[jj * ZT_LD + ii], sTr[jj + ZT_J * tt], acc);
+          a.ZTr_part[(size_t)blockIdx.y * ny * a.nt + is + (size_t)ny * tt] = acc;
+        }
       }
     }
   }
-  {
-    const int j = j0 + xj;
-    double* dst = a.XZ_part + (size_t)blockIdx.x * K * a.ns_loc;
+  double* dst = a.XZ_part + (size_t)blockIdx.x * K * a.ns_loc;
 #pragma unroll
-    for (int q = 0; q < KQ; ++q) {
-      const int k = xkq + 8 * q;
-      if (k < K && j < a.ns_loc) dst[k + (size_t)K * j] = accXZ[q];
+  for (int q = 0; q < NQ; ++q) {
+    const int id = w + 4 * q;
+    if (id < n_xz_tiles) {
+      const int kb = id >> 1, sbb = id & 1, j = j0 + 16 * sbb + lm;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = kb * 16 + lk + 4 * r;
+        if (k < K && j < a.ns_loc) dst[k + (size_t)K * j] = accXZ[q][r];
+      }
     }
   }
 }
@@ -263,17 +283,27 @@ __global__ __launch_bounds__(256) void xeta_gram_kernel(EtaView ev, int K, int K
   }
 }
 
-// deterministic slab reduction: out[e] = sum_c part[c*stride + e]
-__global__ void slab_sum_kernel(const double* __restrict__ part, double* __restrict__ out, int64_t n,
-                                int nparts, int64_t stride) {
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+// deterministic slab reduction: out[e] = sum_c part[c*stride + e]; 64 outputs per block,
+// the four waves take every fourth partial (coalesced 512-B rows), fixed summation order.
+__global__ __launch_bounds__(256) void slab_sum_kernel(const double* __restrict__ part, double* __restrict__ out,
+                                                       int64_t n, int nparts, int64_t stride) {
+  __shared__ double red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += (int64_t)gridDim.x * 64) {
+    const int64_t e = base + lane;
     double s = 0.0;
-    for (int c = 0; c < nparts; ++c) s += part[c * stride + e];
-    out[e] = s;
+    if (e < n) {
+#pragma unroll 4
+      for (int c = w; c < nparts; c += 4) s += part[(int64_t)c * stride + e];
+    }
+    red[w][lane] = s;
+    __syncthreads();
+    if (w == 0 && e < n) out[e] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    __syncthreads();
   }
 }
 
-static int grid_for(int64_t n, int block = 256, int cap = 2048) {
+static int grid_for(int64_t n, int block = 64, int cap = 2048) {
   int64_t g = (n + block - 1) / block;
   if (g < 1) g = 1;
   if (g > cap) g = cap;
@@ -281,17 +311,18 @@ static int grid_for(int64_t n, int block = 256, int cap = 2048) {
 }
 
 static size_t z_smem_bytes(const State& s, bool has_na) {
-  size_t d = (size_t)s.K * ZT_LD + (size_t)s.K * ZT_J + (size_t)ZT_J * ZT_LD +
-             (has_na ? (size_t)ZT_J * ZT_LD : 0) + (size_t)ZT_J * s.nt + ZT_J;
+  const size_t K4 = (s.K + 3) & ~3, K16 = (s.K + 15) & ~15;
+  size_t d = K16 * ZT_LD + K4 * ZT_J + (size_t)ZT_J * ZT_LD + (has_na ? (size_t)ZT_J * ZT_LD : 0) +
+             (size_t)ZT_J * s.nt + ZT_J;
   return d * sizeof(double) + ZT_J * sizeof(int);
 }
 
 template <bool DRAW, bool HAS_NA>
 static void z_dispatch(const State& s, dim3 grid, size_t smem, const ZArgs& a) {
   if (s.K <= 32)
-    z_fused_kernel<DRAW, HAS_NA, 4><<<grid, 256, smem, s.stream>>>(a);
+    z_fused_kernel<DRAW, HAS_NA, 1><<<grid, 256, smem, s.stream>>>(a);
   else
-    z_fused_kernel<DRAW, HAS_NA, 8><<<grid, 256, smem, s.stream>>>(a);
+    z_fused_kernel<DRAW, HAS_NA, 2><<<grid, 256, smem, s.stream>>>(a);
 }
 
 void launch_xeta(State& s) {
@@ -512,35 +543,46 @@ void launch_beta_lambda(State& s, uint32_t iter) {
 // Species-parallel partial sums for updateGammaV (R/updateGammaV.R:16-18,30):
 //   A = E E^T (E = Beta - Gamma Tr^T) and BTr = Beta Tr.
 // ---------------------------------------------------------------------------
-constexpr int GV_PARTS = 32;
+constexpr int SB = 32;  // species per block of the species-sum reductions
 
+// Species-block partial sums for updateGammaV (R/updateGammaV.R:16-18,30):
+//   A = E E^T (E = Beta - Gamma Tr^T) and BTr = Beta Tr, staged through LDS.
 __global__ __launch_bounds__(256) void gammav_partial_kernel(const double* BL, int K, int nc, int nt, int ns_loc,
                                                              const double* Gamma, const double* Tr,
                                                              double* part) {
-  // part[b][0 : nc*nc] = A partial, part[b][nc*nc : nc*nc + nc*nt] = BTr partial
-  const int b = blockIdx.x;
-  const int per = (ns_loc + gridDim.x - 1) / gridDim.x;
-  const int ja = b * per, jb = min(ns_loc, ja + per);
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* sB = smem;             // nc x SB
+  double* sE = sB + nc * SB;     // nc x SB
+  double* sTr = sE + nc * SB;    // SB x nt
+  const int t = threadIdx.x, j0 = blockIdx.x * SB, nj = min(SB, ns_loc - j0);
+  for (int p = t; p < nc * nj; p += 256) {
+    const int c = p % nc, jj = p / nc;
+    sB[p] = BL[c + (size_t)K * (j0 + jj)];
+  }
+  for (int p = t; p < SB * nt; p += 256) {
+    const int jj = p % SB, q = p / SB;
+    sTr[p] = jj < nj ? Tr[j0 + jj + (size_t)ns_loc * q] : 0.0;
+  }
+  __syncthreads();
+  for (int p = t; p < nc * nj; p += 256) {
+    const int c = p % nc, jj = p / nc;
+    double e = sB[p];
+    for (int q = 0; q < nt; ++q) e -= Gamma[c + nc * q] * sTr[jj + SB * q];
+    sE[p] = e;
+  }
+  __syncthreads();
   const int nA = nc * nc, nB = nc * nt;
-  double* out = part + (size_t)b * (nA + nB);
-  for (int p = threadIdx.x; p < nA + nB; p += blockDim.x) {
-    double s = 0.0;
+  double* out = part + (size_t)blockIdx.x * (nA + nB);
+  for (int p = t; p < nA + nB; p += 256) {
+    double acc = 0.0;
     if (p < nA) {
       const int c1 = p % nc, c2 = p / nc;
-      for (int j = ja; j < jb; ++j) {
-        double e1 = BL[c1 + (size_t)K * j], e2 = BL[c2 + (size_t)K * j];
-        for (int q = 0; q < nt; ++q) {
-          const double tr = Tr[j + (size_t)ns_loc * q];
-          e1 -= Gamma[c1 + nc * q] * tr;
-          e2 -= Gamma[c2 + nc * q] * tr;
-        }
-        s += e1 * e2;
-      }
+      for (int jj = 0; jj < nj; ++jj) acc = fma(sE[c1 + nc * jj], sE[c2 + nc * jj], acc);
     } else {
       const int pp = p - nA, c = pp % nc, q = pp / nc;
-      for (int j = ja; j < jb; ++j) s += BL[c + (size_t)K * j] * Tr[j + (size_t)ns_loc * q];
+      for (int jj = 0; jj < nj; ++jj) acc = fma(sB[c + nc * jj], sTr[jj + SB * q], acc);
     }
-    out[p] = s;
+    out[p] = acc;
   }
 }
 
@@ -566,6 +608,7 @@ __device__ void wg_rwish(const double* Sl, int n, double v, double* W, double* T
 
 struct GVArgs {
   int nc, nt, ns_glob, nparts;
+  const double* iUmG;  // iUGamma %*% mGamma (constant, host precomputed)
   const double* part;  // summed partials (already all-reduced in sharded mode)
   const double* V0;
   double f0;
@@ -594,9 +637,11 @@ __global__ __launch_bounds__(256) void gammav_final_kernel(GVArgs a) {
   double* Pm = BTr + nc * nt;       // N*N
   double* rhs = Pm + N * N;         // N
   double* Zb = rhs + N;             // nc*nc
+  double* iVl = Zb + nc * nc;       // nc*nc (the new iV, kept on chip)
   const int nA = nc * nc, nB = nc * nt;
   for (int p = t; p < nA + nB; p += blockDim.x) {
     double s = 0.0;
+#pragma unroll 8
     for (int b = 0; b < a.nparts; ++b) s += a.part[(size_t)b * (nA + nB) + p];
     if (p < nA)
       A[p] = s + a.V0[p];                        // A + V0   (:19)
@@ -611,18 +656,18 @@ __global__ __launch_bounds__(256) void gammav_final_kernel(GVArgs a) {
   wg_copy(A, Vn, nc * nc);
   wg_chol(A, nc, nc, &flag);                      // CC = chol(Vn)
   wg_lower_only(A, nc, nc);
-  wg_rwish(A, nc, a.f0 + a.ns_glob, a.iV, T, Zb, a.key, S_WISHART_DIAG, S_WISHART_OFF, a.iter, a.noise_zero);  // (:20)
+  wg_rwish(A, nc, a.f0 + a.ns_glob, iVl, T, Zb, a.key, S_WISHART_DIAG, S_WISHART_OFF, a.iter, a.noise_zero);  // (:20)
+  for (int p = t; p < nc * nc; p += blockDim.x) a.iV[p] = iVl[p];
   // Gamma | iV: prec = iUGamma + kron(Tr'Tr, iV); rhs = iUGamma mGamma + vec(iV B Tr)   (:29-31)
   for (int p = t; p < N * N; p += blockDim.x) {
     const int r = p % N, c = p / N;
     const int c1 = r % nc, t1 = r / nc, c2 = c % nc, t2 = c / nc;
-    Pm[p] = a.iUGamma[p] + a.TT[t1 + nt * t2] * a.iV[c1 + nc * c2];
+    Pm[p] = a.iUGamma[p] + a.TT[t1 + nt * t2] * iVl[c1 + nc * c2];
   }
   for (int r = t; r < N; r += blockDim.x) {
     const int c1 = r % nc, t1 = r / nc;
-    double v = 0.0;
-    for (int q = 0; q < N; ++q) v += a.iUGamma[r + N * q] * a.mGamma[q];
-    for (int c2 = 0; c2 < nc; ++c2) v += a.iV[c1 + nc * c2] * BTr[c2 + nc * t1];
+    double v = a.iUmG[r];
+    for (int c2 = 0; c2 < nc; ++c2) v += iVl[c1 + nc * c2] * BTr[c2 + nc * t1];
     rhs[r] = v;
   }
   __syncthreads();
@@ -635,18 +680,19 @@ __global__ __launch_bounds__(256) void gammav_final_kernel(GVArgs a) {
   for (int r = t; r < N; r += blockDim.x) a.Gamma[r] = rhs[r];
 }
 
-void allreduce_sum(State& s, double* buf, size_t n);  // capi.cpp
+void allreduce_sum(State& s, double* buf, size_t n, hipStream_t st = nullptr);  // capi.cpp
 
-void launch_gamma_v(State& s, uint32_t iter) {
-  const int nparts = std::min(GV_PARTS, std::max(1, s.nsl));
+void launch_gamma_v(State& s, uint32_t iter, hipStream_t st) {
+  const int nparts = (s.nsl + SB - 1) / SB;
   double* part = s.ABpart;
-  gammav_partial_kernel<<<nparts, 256, 0, s.stream>>>(s.BL, s.K, s.nc, s.nt, s.nsl, s.Gamma, s.Tr, part);
+  gammav_partial_kernel<<<nparts, 256, (size_t)(2 * s.nc * SB + SB * s.nt) * sizeof(double), st>>>(
+      s.BL, s.K, s.nc, s.nt, s.nsl, s.Gamma, s.Tr, part);
   HIP_OK(hipGetLastError());
   int np = nparts;
   if (s.nranks > 1) {
     const int64_t n = (int64_t)s.nc * s.nc + (int64_t)s.nc * s.nt;
-    slab_sum_kernel<<<grid_for(n), 256, 0, s.stream>>>(part, s.allreduce_buf, n, nparts, n);
-    allreduce_sum(s, s.allreduce_buf, n);
+    slab_sum_kernel<<<grid_for(n), 256, 0, st>>>(part, s.allreduce_buf, n, nparts, n);
+    allreduce_sum(s, s.allreduce_buf, n, st);
     part = s.allreduce_buf;
     np = 1;
   }
@@ -660,6 +706,7 @@ void launch_gamma_v(State& s, uint32_t iter) {
   a.f0 = s.f0;
   a.iUGamma = s.iUGamma;
   a.mGamma = s.mGamma;
+  a.iUmG = s.iUmG;
   a.TT = s.TT;
   a.iV = s.iV;
   a.Gamma = s.Gamma;
@@ -668,11 +715,12 @@ void launch_gamma_v(State& s, uint32_t iter) {
   a.iter = iter;
   a.noise_zero = s.noise_mode;
   a.fail = s.dev_flags;
-  const size_t need = (5 * (size_t)s.nc * s.nc + (size_t)s.nc * s.nt + (size_t)s.nc * s.nt * s.nc * s.nt +
+  const size_t need = (6 * (size_t)s.nc * s.nc + (size_t)s.nc * s.nt + (size_t)s.nc * s.nt * s.nc * s.nt +
                        (size_t)s.nc * s.nt) * sizeof(double);
   a.use_lds = need <= 64 * 1024;
-  gammav_final_kernel<<<1, 256, a.use_lds ? need : 0, s.stream>>>(a);
+  gammav_final_kernel<<<1, 64, a.use_lds ? need : 0, st>>>(a);
   HIP_OK(hipGetLastError());
+  if (s.mask & HMSC_UP_GAMMA2) launch_gamma2_prep(s, st);  // Gamma2's iV-only algebra for the next sweep
 }
 
 // ---------------------------------------------------------------------------
@@ -684,22 +732,35 @@ void launch_gamma_v(State& s, uint32_t iter) {
 __global__ __launch_bounds__(256) void gamma2_partial_kernel(const double* XZ, const double* BL, int K, int nc,
                                                              int NF, int nt, int ns_loc, const double* Tr,
                                                              double* part) {
-  // part[b] = [ XZ[0:nc,:] Tr (nc*nt) | Lambda_all Tr (NF*nt) ]
-  const int b = blockIdx.x;
-  const int per = (ns_loc + gridDim.x - 1) / gridDim.x;
-  const int ja = b * per, jb = min(ns_loc, ja + per);
+  // part[b] = [ XZ[0:nc, block] Tr (nc*nt) | Lambda_all[:, block] Tr (NF*nt) ]
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* sX = smem;             // K x SB: rows < nc from XZ, rows >= nc from BL (Lambda)
+  double* sTr = sX + K * SB;     // SB x nt
+  const int t = threadIdx.x, j0 = blockIdx.x * SB, nj = min(SB, ns_loc - j0);
+  for (int p = t; p < K * nj; p += 256) {
+    const int k = p % K, jj = p / K;
+    const size_t g = k + (size_t)K * (j0 + jj);
+    sX[p] = k < nc ? XZ[g] : BL[g];
+  }
+  for (int p = t; p < SB * nt; p += 256) {
+    const int jj = p % SB, q = p / SB;
+    sTr[p] = jj < nj ? Tr[j0 + jj + (size_t)ns_loc * q] : 0.0;
+  }
+  __syncthreads();
   const int n1 = nc * nt, n2 = NF * nt;
-  double* out = part + (size_t)b * (n1 + n2);
-  for (int p = threadIdx.x; p < n1 + n2; p += blockDim.x) {
-    double s = 0.0;
+  double* out = part + (size_t)blockIdx.x * (n1 + n2);
+  for (int p = t; p < n1 + n2; p += 256) {
+    int k, q;
     if (p < n1) {
-      const int c = p % nc, q = p / nc;
-      for (int j = ja; j < jb; ++j) s += XZ[c + (size_t)K * j] * Tr[j + (size_t)ns_loc * q];
+      k = p % nc;
+      q = p / nc;
     } else {
-      const int pp = p - n1, f = pp % NF, q = pp / NF;
-      for (int j = ja; j < jb; ++j) s += BL[nc + f + (size_t)K * j] * Tr[j + (size_t)ns_loc * q];
+      k = nc + (p - n1) % NF;
+      q = (p - n1) / NF;
     }
-    out[p] = s;
+    double acc = 0.0;
+    for (int jj = 0; jj < nj; ++jj) acc = fma(sX[k + K * jj], sTr[jj + SB * q], acc);
+    out[p] = acc;
   }
 }
 
@@ -719,32 +780,119 @@ __global__ __launch_bounds__(256) void xt_ztr_kernel(const double* X, const doub
   if (threadIdx.x == 0) out[p] = red[0];
 }
 
-struct G2Args {
-  int nc, nt, K, Kmax, NF, nr, nparts, ns_loc, use_xtztr;
-  int lev_nf[HMSC_MAX_LEVELS];
-  const double* part;
-  const double* xtztr;
-  const double* G;
+// Gamma2 splits into the part that depends only on iV (prep; runs on the side stream right
+// after updateGammaV of the previous sweep, overlapped with updateEta / updateZ) and the part
+// that needs the new Z (final).  With iP = (iV + X'X)^-1 (R/updateGamma2.R:40-50):
+//   A1 = V0 - V0 X'X iP,  B1 = iV iP,  Rm = (I (x) iV0 + TT (x) (iV - iV iP iV))^-1,
+//   tmp = TT (x) (V0 X'X iP iV),  TR = tmp Rm,
+//   SigmaG = I (x) V0 - TT (x) (V0 X'X V0 - V0 X'X iP X'X V0) + TR tmp^T,   LS = chol(SigmaG)
+//   muG = vec(A1 XZT) - TR vec(B1 XZT);   Gamma = muG + LS xi.
+// (t2 t2^T = V0 X'X iP X'X V0 and (tmp LR)(tmp LR)^T = tmp Rm tmp^T: the reference's two
+// extra Cholesky factors LiP, LR are algebraically redundant.)
+struct G2PrepArgs {
+  int nc, nt;
   const double* iV;
   const double* XX;
   const double* TT;
   const double* iV0;
   const double* V0g;
+  const double* V0gXX;
   const double* V0gXXV0g;
+  double* prep;      // [A1 nc^2 | B1 nc^2 | TR N^2 | LS N^2]
+  double* scratch;
+  int use_lds;
+  int* fail;
+};
+
+__global__ __launch_bounds__(256) void gamma2_prep_kernel(G2PrepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int nc = a.nc, nt = a.nt, N = nc * nt, t = threadIdx.x, n2 = nc * nc;
+  __shared__ int flag;
+  double* iV = a.use_lds ? lds : a.scratch;  // nc^2
+  double* XX = iV + n2;
+  double* V0g = XX + n2;
+  double* V0gXX = V0g + n2;
+  double* W = V0gXX + n2;
+  double* iP = W + n2;
+  double* B1 = iP + n2;
+  double* M1 = B1 + n2;
+  double* T1 = M1 + n2;
+  double* W1 = T1 + n2;
+  double* WN = W1 + n2;      // N^2
+  double* Rm = WN + N * N;   // N^2
+  double* TM = Rm + N * N;   // N^2 (tmp)
+  double* TR = TM + N * N;   // N^2
+  double* Sg = TR + N * N;   // N^2
+  for (int p = t; p < n2; p += blockDim.x) {
+    iV[p] = a.iV[p];
+    XX[p] = a.XX[p];
+    V0g[p] = a.V0g[p];
+    V0gXX[p] = a.V0gXX[p];
+    W[p] = a.iV[p] + a.XX[p];
+  }
+  __syncthreads();
+  if (!wg_chol(W, nc, nc, &flag) && t == 0) *a.fail = 1;
+  wg_chol2inv(W, nc, nc, iP, nc, T1);                                      // iP = inv(iV + XX)
+  wg_gemm(nc, nc, nc, 1.0, iV, nc, false, iP, nc, false, 0.0, B1, nc);     // B1 = iV iP
+  wg_gemm(nc, nc, nc, -1.0, B1, nc, false, iV, nc, false, 0.0, M1, nc);    // M1 = iV - iV iP iV
+  for (int p = t; p < n2; p += blockDim.x) M1[p] += iV[p];
+  __syncthreads();
+  for (int p = t; p < N * N; p += blockDim.x) {
+    const int r = p % N, c = p / N, c1 = r % nc, q1 = r / nc, c2 = c % nc, q2 = c / nc;
+    WN[p] = (q1 == q2 ? a.iV0[c1 + nc * c2] : 0.0) + a.TT[q1 + nt * q2] * M1[c1 + nc * c2];
+  }
+  __syncthreads();
+  if (!wg_chol(WN, N, N, &flag) && t == 0) *a.fail = 1;
+  wg_chol2inv(WN, N, N, Rm, N, Sg);                                        // Rm   (:44)
+  wg_gemm(nc, nc, nc, 1.0, V0gXX, nc, false, iP, nc, false, 0.0, T1, nc);  // V0 XX iP
+  wg_gemm(nc, nc, nc, 1.0, T1, nc, false, iV, nc, false, 0.0, W1, nc);     // V0 XX iP iV
+  for (int p = t; p < N * N; p += blockDim.x) {
+    const int r = p % N, c = p / N, c1 = r % nc, q1 = r / nc, c2 = c % nc, q2 = c / nc;
+    TM[p] = a.TT[q1 + nt * q2] * W1[c1 + nc * c2];                        // tmp   (:48)
+  }
+  __syncthreads();
+  wg_gemm(N, N, N, 1.0, TM, N, false, Rm, N, false, 0.0, TR, N);           // TR = tmp Rm
+  wg_gemm(nc, nc, nc, -1.0, T1, nc, false, V0gXX, nc, true, 0.0, M1, nc);  // -V0 XX iP XX V0
+  for (int p = t; p < n2; p += blockDim.x) {
+    M1[p] += a.V0gXXV0g[p];
+    W[p] = V0g[p] - T1[p];                                                 // A1 = V0 - V0 XX iP
+  }
+  __syncthreads();
+  wg_gemm(N, N, N, 1.0, TR, N, false, TM, N, true, 0.0, Sg, N);            // tmp Rm tmp^T
+  for (int p = t; p < N * N; p += blockDim.x) {
+    const int r = p % N, c = p / N, c1 = r % nc, q1 = r / nc, c2 = c % nc, q2 = c / nc;
+    Sg[p] += (q1 == q2 ? V0g[c1 + nc * c2] : 0.0) - a.TT[q1 + nt * q2] * M1[c1 + nc * c2];   // (:50)
+  }
+  __syncthreads();
+  if (!wg_chol(Sg, N, N, &flag) && t == 0) *a.fail = 1;                    // LSigmaG   (:52)
+  double* out = a.prep;
+  for (int p = t; p < n2; p += blockDim.x) {
+    out[p] = W[p];
+    out[n2 + p] = B1[p];
+  }
+  for (int p = t; p < N * N; p += blockDim.x) {
+    out[2 * n2 + p] = TR[p];
+    out[2 * n2 + N * N + p] = (p % N >= p / N) ? Sg[p] : 0.0;
+  }
+}
+
+struct G2Args {
+  int nc, nt, Kmax, NF, nparts, ns_loc, use_xtztr, check_isigma;
+  const double* part;
+  const double* xtztr;
+  const double* G;
+  const double* prep;
   const double* iSigma;
   double* Gamma;
-  double* scratch;
   Key key;
   uint32_t iter;
   int noise_zero;
-  int check_isigma;
-  int use_lds;
 };
 
 __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
-  const int nc = a.nc, nt = a.nt, N = nc * nt, t = threadIdx.x;
-  __shared__ int flag;
   __shared__ int all_one;
+  __shared__ double S0[512], LTr[512], v1[256], v2[256], xi[256];
+  const int nc = a.nc, nt = a.nt, N = nc * nt, t = threadIdx.x, n2 = nc * nc;
   if (t == 0) all_one = 1;
   __syncthreads();
   if (a.check_isigma)
@@ -752,115 +900,80 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
       if (a.iSigma[j] != 1.0) all_one = 0;  // acts only if all(iSigma == 1)  (:36)
   __syncthreads();
   if (!all_one) return;
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  double* S0 = a.use_lds ? lds : a.scratch;  // XZT  nc*nt
-  double* LTr = S0 + nc * nt;         // NF*nt
-  double* iP = LTr + a.NF * nt;       // nc*nc
-  double* LiP = iP + nc * nc;         // nc*nc
-  double* W = LiP + nc * nc;          // nc*nc
-  double* T1 = W + nc * nc;           // nc*nc
-  double* M1 = T1 + nc * nc;          // nc*nc
-  double* Rm = M1 + nc * nc;          // N*N
-  double* WN = Rm + N * N;            // N*N
-  double* LR = WN + N * N;            // N*N
-  double* tmp = LR + N * N;           // N*N
-  double* Sg = tmp + N * N;           // N*N
-  double* iPXZT = Sg + N * N;         // nc*nt
-  double* v1 = iPXZT + nc * nt;       // N
-  double* v2 = v1 + N;                // N
-  double* muG = v2 + N;               // N
-  double* t2 = muG + N;               // nc*nc
-  double* W1 = t2 + nc * nc;          // nc*nc
-  double* xi = W1 + nc * nc;          // N
-  const int n1 = nc * nt, n2 = a.NF * nt;
-  // reduce species partials
-  for (int p = t; p < n1 + n2; p += blockDim.x) {
+  const int n1 = nc * nt, nL = a.NF * nt;
+  for (int p = t; p < n1 + nL; p += blockDim.x) {
     double s = 0.0;
-    for (int b = 0; b < a.nparts; ++b) s += a.part[(size_t)b * (n1 + n2) + p];
+#pragma unroll 8
+    for (int b = 0; b < a.nparts; ++b) s += a.part[(size_t)b * (n1 + nL) + p];
     if (p < n1)
       S0[p] = a.use_xtztr ? a.xtztr[p] : s;
     else
       LTr[p - n1] = s;
   }
+  for (int r = t; r < N; r += blockDim.x) xi[r] = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)r, 0, S_GAMMA2, a.iter);
   __syncthreads();
-  // XZT -= sum_r (X^T Eta_r[Pi]) (Lambda_r Tr): X^T Eta block of G = rows [0,nc), cols [nc, K)
-  for (int p = t; p < nc * nt; p += blockDim.x) {
+  // XZT = X^T Z Tr - sum_r (X^T Eta_r[Pi]) (Lambda_r Tr)   (:46 with S = Z - sum LRan)
+  for (int p = t; p < n1; p += blockDim.x) {
     const int c = p % nc, q = p / nc;
     double s = 0.0;
     for (int f = 0; f < a.NF; ++f) s += a.G[c + a.Kmax * (nc + f)] * LTr[f + a.NF * q];
     S0[p] -= s;
   }
-  // iP = inv(iV + XX); LiP = chol(iP) lower
-  for (int p = t; p < nc * nc; p += blockDim.x) W[p] = a.iV[p] + a.XX[p];
   __syncthreads();
-  wg_chol(W, nc, nc, &flag);
-  wg_chol2inv(W, nc, nc, iP, nc, T1);
-  wg_copy(LiP, iP, nc * nc);
-  wg_chol(LiP, nc, nc, &flag);
-  wg_lower_only(LiP, nc, nc);
-  // M1 = iV - (iV LiP)(iV LiP)^T
-  wg_gemm(nc, nc, nc, 1.0, a.iV, nc, false, LiP, nc, false, 0.0, T1, nc);
-  wg_gemm(nc, nc, nc, -1.0, T1, nc, false, T1, nc, true, 0.0, M1, nc);
-  for (int p = t; p < nc * nc; p += blockDim.x) M1[p] += a.iV[p];
-  __syncthreads();
-  // Rm = inv(kron(I_nt, iV0) + kron(TT, M1)); LR = chol(Rm) lower   (:44-45)
-  for (int p = t; p < N * N; p += blockDim.x) {
-    const int r = p % N, c = p / N, c1 = r % nc, q1 = r / nc, c2 = c % nc, q2 = c / nc;
-    WN[p] = (q1 == q2 ? a.iV0[c1 + nc * c2] : 0.0) + a.TT[q1 + nt * q2] * M1[c1 + nc * c2];
+  const double* A1 = a.prep;
+  const double* B1 = A1 + n2;
+  const double* TR = B1 + n2;
+  const double* LS = TR + N * N;
+  for (int p = t; p < N; p += blockDim.x) {
+    const int c = p % nc, q = p / nc;
+    double s1 = 0.0, s2 = 0.0;
+    for (int k = 0; k < nc; ++k) {
+      s1 += A1[c + nc * k] * S0[k + nc * q];
+      s2 += B1[c + nc * k] * S0[k + nc * q];
+    }
+    v1[p] = s1;
+    v2[p] = s2;
   }
-  __syncthreads();
-  wg_chol(WN, N, N, &flag);
-  wg_chol2inv(WN, N, N, Rm, N, tmp);
-  wg_copy(LR, Rm, N * N);
-  wg_chol(LR, N, N, &flag);
-  wg_lower_only(LR, N, N);
-  // iPXZT = iP XZT
-  wg_gemm(nc, nt, nc, 1.0, iP, nc, false, S0, nc, false, 0.0, iPXZT, nc);
-  // W1 = V0g XX iP iV ; tmp = kron(TT, W1)
-  wg_gemm(nc, nc, nc, 1.0, a.V0g, nc, false, a.XX, nc, false, 0.0, T1, nc);
-  wg_gemm(nc, nc, nc, 1.0, T1, nc, false, iP, nc, false, 0.0, t2, nc);
-  wg_gemm(nc, nc, nc, 1.0, t2, nc, false, a.iV, nc, false, 0.0, W1, nc);
-  for (int p = t; p < N * N; p += blockDim.x) {
-    const int r = p % N, c = p / N, c1 = r % nc, q1 = r / nc, c2 = c % nc, q2 = c / nc;
-    tmp[p] = a.TT[q1 + nt * q2] * W1[c1 + nc * c2];
-  }
-  __syncthreads();
-  // muG = vec(V0g (XZT - XX iPXZT)) - tmp Rm vec(iV iPXZT)   (:49)
-  wg_gemm(nc, nt, nc, -1.0, a.XX, nc, false, iPXZT, nc, false, 0.0, v1, nc);
-  for (int p = t; p < nc * nt; p += blockDim.x) v1[p] += S0[p];
-  __syncthreads();
-  wg_gemm(nc, nt, nc, 1.0, a.V0g, nc, false, v1, nc, false, 0.0, muG, nc);
-  wg_gemm(nc, nt, nc, 1.0, a.iV, nc, false, iPXZT, nc, false, 0.0, v1, nc);
-  wg_gemm(N, 1, N, 1.0, Rm, N, false, v1, N, false, 0.0, v2, N);
-  wg_gemm(N, 1, N, -1.0, tmp, N, false, v2, N, false, 1.0, muG, N);
-  // SigmaG = kron(I, V0g) - kron(TT, V0g XX V0g - t2 t2^T) + (tmp LR)(tmp LR)^T, t2 = V0g XX LiP  (:50)
-  wg_gemm(nc, nc, nc, 1.0, a.V0g, nc, false, a.XX, nc, false, 0.0, T1, nc);
-  wg_gemm(nc, nc, nc, 1.0, T1, nc, false, LiP, nc, false, 0.0, t2, nc);
-  wg_gemm(nc, nc, nc, -1.0, t2, nc, false, t2, nc, true, 0.0, M1, nc);
-  for (int p = t; p < nc * nc; p += blockDim.x) M1[p] += a.V0gXXV0g[p];
-  __syncthreads();
-  wg_gemm(N, N, N, 1.0, tmp, N, false, LR, N, false, 0.0, WN, N);
-  wg_gemm(N, N, N, 1.0, WN, N, false, WN, N, true, 0.0, Sg, N);
-  for (int p = t; p < N * N; p += blockDim.x) {
-    const int r = p % N, c = p / N, c1 = r % nc, q1 = r / nc, c2 = c % nc, q2 = c / nc;
-    Sg[p] += (q1 == q2 ? a.V0g[c1 + nc * c2] : 0.0) - a.TT[q1 + nt * q2] * M1[c1 + nc * c2];
-  }
-  __syncthreads();
-  wg_chol(Sg, N, N, &flag);                // LSigmaG = t(chol(SigmaG))   (:52)
-  for (int r = t; r < N; r += blockDim.x) xi[r] = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)r, 0, S_GAMMA2, a.iter);
   __syncthreads();
   for (int r = t; r < N; r += blockDim.x) {
-    double v = muG[r];
-    for (int c = 0; c <= r; ++c) v += Sg[r + N * c] * xi[c];
-    a.Gamma[r] = v;                        // (:53-54)
+    double m = v1[r];
+    for (int c = 0; c < N; ++c) m -= TR[r + N * c] * v2[c];
+    for (int c = 0; c <= r; ++c) m += LS[r + N * c] * xi[c];
+    a.Gamma[r] = m;                                                        // (:49, :53-54)
   }
 }
 
+static void launch_gamma2_prep(State& s, hipStream_t st) {
+  G2PrepArgs a{};
+  a.nc = s.nc;
+  a.nt = s.nt;
+  a.iV = s.iV;
+  a.XX = s.XX;
+  a.TT = s.TT;
+  a.iV0 = s.iV0;
+  a.V0g = s.V0g;
+  a.V0gXX = s.V0gXX;
+  a.V0gXXV0g = s.V0gXXV0g;
+  a.prep = s.g2prep;
+  a.scratch = s.scratch2;
+  a.fail = s.dev_flags + 1;
+  const size_t N = (size_t)s.nc * s.nt;
+  const size_t need = (10 * (size_t)s.nc * s.nc + 5 * N * N) * sizeof(double);
+  a.use_lds = need <= 64 * 1024;
+  gamma2_prep_kernel<<<1, 256, a.use_lds ? need : 0, st>>>(a);
+  HIP_OK(hipGetLastError());
+  s.g2prep_valid = true;
+}
+
 void launch_gamma2(State& s, uint32_t iter) {
+  HMSC_REQUIRE((size_t)s.nc * s.nt <= 256 && s.NF * s.nt + s.nc * s.nt <= 1024,
+               "updateGamma2: nc*nt must be <= 256 in this build");
   if (!s.xeta_valid) launch_xeta(s);
   if (!s.zt_valid) launch_zt_refresh(s);
-  const int nparts = std::min(GV_PARTS, std::max(1, s.nsl));
-  gamma2_partial_kernel<<<nparts, 256, 0, s.stream>>>(s.XZ, s.BL, s.K, s.nc, s.NF, s.nt, s.nsl, s.Tr, s.ABpart);
+  if (!s.g2prep_valid) launch_gamma2_prep(s, s.stream);
+  const int nparts = (s.nsl + SB - 1) / SB;
+  gamma2_partial_kernel<<<nparts, 256, (size_t)(s.K * SB + SB * s.nt) * sizeof(double), s.stream>>>(
+      s.XZ, s.BL, s.K, s.nc, s.NF, s.nt, s.nsl, s.Tr, s.ABpart);
   HIP_OK(hipGetLastError());
   const int n1 = s.nc * s.nt, n2 = s.NF * s.nt;
   double* part = s.ABpart;
@@ -876,33 +989,22 @@ void launch_gamma2(State& s, uint32_t iter) {
   G2Args a{};
   a.nc = s.nc;
   a.nt = s.nt;
-  a.K = s.K;
   a.Kmax = s.Kmax;
   a.NF = s.NF;
-  a.nr = s.nr;
   a.nparts = np;
   a.ns_loc = s.nsl;
   a.use_xtztr = s.has_na ? 1 : 0;
+  a.check_isigma = s.nranks == 1 ? 1 : 0;
   a.part = part;
   a.xtztr = xtztr;
   a.G = s.G;
-  a.iV = s.iV;
-  a.XX = s.XX;
-  a.TT = s.TT;
-  a.iV0 = s.iV0;
-  a.V0g = s.V0g;
-  a.V0gXXV0g = s.V0gXXV0g;
+  a.prep = s.g2prep;
   a.iSigma = s.iSigma;
   a.Gamma = s.Gamma;
-  a.scratch = s.scratch;
   a.key = s.key;
   a.iter = iter;
   a.noise_zero = s.noise_mode;
-  a.check_isigma = s.nranks == 1 ? 1 : 0;
-  const size_t N = (size_t)s.nc * s.nt;
-  const size_t need = (9 * (size_t)s.nc * s.nc + 5 * N * N + 2 * N + (size_t)s.NF * s.nt + 4 * N) * sizeof(double);
-  a.use_lds = need <= 64 * 1024;
-  gamma2_final_kernel<<<1, 256, a.use_lds ? need : 0, s.stream>>>(a);
+  gamma2_final_kernel<<<1, 256, 0, s.stream>>>(a);
   HIP_OK(hipGetLastError());
 }
 
@@ -1033,7 +1135,7 @@ __global__ __launch_bounds__(64) void delta_kernel(LPArgs a, const double* rs_pa
 
 constexpr int LP_PARTS = 64;
 
-void launch_lambda_priors(State& s, uint32_t iter) {
+void launch_lambda_priors(State& s, uint32_t iter, hipStream_t st) {
   if (s.nr == 0) return;
   HMSC_REQUIRE(s.NF <= 64, "updateLambdaPriors: sum(nf) must be <= 64 in this build");
   LPArgs a{};
@@ -1059,17 +1161,17 @@ void launch_lambda_priors(State& s, uint32_t iter) {
   a.key = s.key;
   a.iter = iter;
   const int nparts = std::min(LP_PARTS, std::max(1, s.nsl));
-  psi_kernel<<<nparts, 256, 0, s.stream>>>(a);
+  psi_kernel<<<nparts, 256, 0, st>>>(a);
   HIP_OK(hipGetLastError());
   const double* rs = s.psi_rs;
   int np = nparts;
   if (s.nranks > 1) {
-    slab_sum_kernel<<<1, 64, 0, s.stream>>>(s.psi_rs, s.allreduce_buf, s.NF, nparts, s.NF);
-    allreduce_sum(s, s.allreduce_buf, s.NF);
+    slab_sum_kernel<<<1, 256, 0, st>>>(s.psi_rs, s.allreduce_buf, s.NF, nparts, s.NF);
+    allreduce_sum(s, s.allreduce_buf, s.NF, st);
     rs = s.allreduce_buf;
     np = 1;
   }
-  delta_kernel<<<s.nr, 64, 0, s.stream>>>(a, rs, np);
+  delta_kernel<<<s.nr, 64, 0, st>>>(a, rs, np);
   HIP_OK(hipGetLastError());
 }
 
@@ -1138,14 +1240,25 @@ __global__ __launch_bounds__(256) void zl_kernel(const double* __restrict__ Z, c
   }
 }
 
-__global__ __launch_bounds__(64) void cr_kernel(const double* BL, const double* iSigma, int K, int nc, int NF,
-                                                int ns_loc, double* CR, int ldcr) {
-  // CR[k, f] = sum_j BL[k, j] iSigma[j] BL[nc+f, j]   one wave per (k, f)
-  const int k = blockIdx.x, f = blockIdx.y, t = threadIdx.x;
-  double s = 0.0;
-  for (int j = t; j < ns_loc; j += 64) s += BL[k + (size_t)K * j] * iSigma[j] * BL[nc + f + (size_t)K * j];
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  if (t == 0) CR[k + (size_t)ldcr * f] = s;
+// CR[k, f] = sum_j BL[k, j] iSigma[j] BL[nc + f, j] over a block of SB species -> slab
+__global__ __launch_bounds__(256) void cr_kernel(const double* BL, const double* iSigma, int K, int nc, int NF,
+                                                 int ns_loc, double* CR_part, int ldcr, int slab) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* sX = smem;   // K x SB
+  const int t = threadIdx.x, j0 = blockIdx.x * SB, nj = min(SB, ns_loc - j0);
+  for (int p = t; p < K * nj; p += 256) {
+    const int jj = p / K;
+    sX[p] = BL[(size_t)K * j0 + p];
+    (void)jj;
+  }
+  __syncthreads();
+  double* out = CR_part + (size_t)blockIdx.x * slab;
+  for (int p = t; p < K * NF; p += 256) {
+    const int k = p % K, f = p / K;
+    double acc = 0.0;
+    for (int jj = 0; jj < nj; ++jj) acc = fma(sX[k + K * jj] * iSigma[j0 + jj], sX[nc + f + K * jj], acc);
+    out[k + (size_t)ldcr * f] = acc;
+  }
 }
 
 struct EtaArgs {
@@ -1338,9 +1451,15 @@ void launch_eta(State& s, uint32_t iter) {
       zl_kernel<64><<<grid, 256, smem, s.stream>>>(s.Z, s.BL, s.iSigma, s.ny, s.nsl, s.K, s.nc, s.NF, s.zl_split, s.ZL_part);
     HIP_OK(hipGetLastError());
   }
-  dim3 gcr(s.K, s.NF);
-  cr_kernel<<<gcr, 64, 0, s.stream>>>(s.BL, s.iSigma, s.K, s.nc, s.NF, s.nsl, s.CR, s.Kmax);
-  HIP_OK(hipGetLastError());
+  {
+    const int ncr = (s.nsl + SB - 1) / SB;
+    const int64_t slab = (int64_t)s.Kmax * s.NFmax;
+    cr_kernel<<<ncr, 256, (size_t)s.K * SB * sizeof(double), s.stream>>>(s.BL, s.iSigma, s.K, s.nc, s.NF, s.nsl,
+                                                                           s.CR_part, s.Kmax, (int)slab);
+    HIP_OK(hipGetLastError());
+    slab_sum_kernel<<<grid_for(slab), 256, 0, s.stream>>>(s.CR_part, s.CR, slab, ncr, slab);
+    HIP_OK(hipGetLastError());
+  }
   const double* zl = s.ZL_part;
   int nzl = s.zl_split;
   if (s.nranks > 1) {

@@ -52,6 +52,11 @@ struct State {
   Level lev[HMSC_MAX_LEVELS];
 
   hipStream_t stream = nullptr, copy_stream = nullptr;
+  // side stream: updateGammaV, Gamma2's iV-only algebra and updateLambdaPriors of sweep t
+  // only feed sweep t+1, so they overlap updateEta / updateZ of sweep t
+  hipStream_t side = nullptr;
+  hipEvent_t ev_bl = nullptr, ev_side = nullptr;
+  bool side_pending = false;
 
   // model (device)
   double *X = nullptr, *Tr = nullptr, *Yval = nullptr, *Yraw = nullptr;
@@ -62,6 +67,11 @@ struct State {
   double *aSigma = nullptr, *bSigma = nullptr;
   double *XX = nullptr, *TT = nullptr, *V0g = nullptr, *V0gXXV0g = nullptr, *iV0 = nullptr;
   double* V0inv = nullptr;       // V0^-1 (initial riwish draw)
+  double* iUmG = nullptr;        // iUGamma %*% mGamma
+  double* V0gXX = nullptr;       // Gamma2 prior covariance times X'X
+  double* g2prep = nullptr;      // Gamma2 iV-only matrices [A1|B1|TR|LS]
+  double* scratch2 = nullptr;    // side-stream scratch
+  bool g2prep_valid = false;
   int* na_cols = nullptr;        // local species with any NA
   int* na_index = nullptr;       // nsl: row of species j in Gna, or -1
   int n_na_cols = 0;
@@ -90,6 +100,7 @@ struct State {
   double* ZL = nullptr;          // ny x NFP   Z * (Lambda diag(iSigma))^T, all levels
   double* ZL_part = nullptr;     // zl_split x ny x NFP
   double* CR = nullptr;          // Kmax x NFmax  BL diag(iSigma) Lambda_all^T
+  double* CR_part = nullptr;     // species-block partials of CR
   double* Msmall = nullptr;      // per-level masked row grams (NA rows)
   double* scratch = nullptr;     // single-workgroup updaters
   double* psi_rs = nullptr;      // psi-lambda^2 row-sum partials
@@ -163,9 +174,9 @@ void launch_update_z(State& s, uint32_t iter, bool use_raw_y);
 void launch_zt_refresh(State& s);
 void launch_xeta(State& s);
 void launch_beta_lambda(State& s, uint32_t iter);
-void launch_gamma_v(State& s, uint32_t iter);
+void launch_gamma_v(State& s, uint32_t iter, hipStream_t st);
 void launch_gamma2(State& s, uint32_t iter);
-void launch_lambda_priors(State& s, uint32_t iter);
+void launch_lambda_priors(State& s, uint32_t iter, hipStream_t st);
 void launch_eta(State& s, uint32_t iter);
 void launch_inv_sigma(State& s, uint32_t iter);
 void launch_record(State& s, double* slot);
