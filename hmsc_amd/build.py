@@ -14,10 +14,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libhmsc_amd.so")
 SOURCES = ["kernels.hip", "capi.cpp"]
-HEADERS = ["common.h", "rng.h", "state.h", os.path.join("..", "..", "include", "hmsc_amd.h")]
+HEADERS = ["common.h", "rng.h", "state.h", "wave_la.h", os.path.join("..", "..", "include", "hmsc_amd.h")]
 ARCH = os.environ.get("HMSC_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+FLAGS = ["-O3", "-fPIC", "-std=c++17", "-pthread", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
 
 
@@ -42,7 +42,7 @@ def build(force=False, verbose=True):
             subprocess.check_call(cmd)
     if force or _stale(LIB, objs):
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB] + objs + \
-              ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
+              ["-pthread", "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)

@@ -6,7 +6,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <atomic>
 #include <cstring>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -161,8 +163,10 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   HIP_OK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&s.copy_stream, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&s.side, hipStreamNonBlocking));
+  HIP_OK(hipStreamCreateWithFlags(&s.side2, hipStreamNonBlocking));
   HIP_OK(hipEventCreateWithFlags(&s.ev_bl, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&s.ev_side, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&s.ev_side2, hipEventDisableTiming));
   if (nranks > 1) {
     HMSC_REQUIRE(comm_id != nullptr, "sharded chain needs an RCCL unique id");
     ncclUniqueId id;
@@ -340,7 +344,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   // workspaces
   const int n_tiles = (ny + 63) / 64;
   s.ntile_j = (nsl + 31) / 32;
-  s.nchunk = std::max(1, std::min(n_tiles, 1024 / std::max(1, s.ntile_j)));
+  s.nchunk = std::max(1, std::min(n_tiles, z_resident_slots(s) / std::max(1, s.ntile_j)));
   const int n_sblk = (ny + 63) / 64;
   s.zl_split = std::max(1, std::min(std::min(16, (nsl + 3) / 4), (640 + n_sblk - 1) / n_sblk));
   s.XZ = dalloc<double>((size_t)s.Kmax * nsl);
@@ -386,7 +390,9 @@ static void free_state(State& s) {
   if (s.comm) ncclCommDestroy((ncclComm_t)s.comm);
   if (s.ev_bl) (void)hipEventDestroy(s.ev_bl);
   if (s.ev_side) (void)hipEventDestroy(s.ev_side);
+  if (s.ev_side2) (void)hipEventDestroy(s.ev_side2);
   if (s.side) (void)hipStreamDestroy(s.side);
+  if (s.side2) (void)hipStreamDestroy(s.side2);
   if (s.stream) (void)hipStreamDestroy(s.stream);
   if (s.copy_stream) (void)hipStreamDestroy(s.copy_stream);
 }
@@ -396,6 +402,7 @@ static void free_state(State& s) {
 static void join_side(State& s) {
   if (s.side_pending) {
     HIP_OK(hipStreamWaitEvent(s.stream, s.ev_side, 0));
+    HIP_OK(hipStreamWaitEvent(s.stream, s.ev_side2, 0));
     s.side_pending = false;
   }
 }
@@ -637,9 +644,11 @@ static void sweep(State& s, uint32_t iter, bool adapt) {
   if (side_work) {
     HIP_OK(hipEventRecord(s.ev_bl, s.stream));
     HIP_OK(hipStreamWaitEvent(s.side, s.ev_bl, 0));
+    HIP_OK(hipStreamWaitEvent(s.side2, s.ev_bl, 0));
     if (s.mask & HMSC_UP_GAMMAV) launch_gamma_v(s, iter, s.side);
-    if (s.mask & HMSC_UP_LAMBDAPRIORS) launch_lambda_priors(s, iter, s.side);
+    if (s.mask & HMSC_UP_LAMBDAPRIORS) launch_lambda_priors(s, iter, s.side2);
     HIP_OK(hipEventRecord(s.ev_side, s.side));
+    HIP_OK(hipEventRecord(s.ev_side2, s.side2));
     s.side_pending = true;
   } else {
     if (s.mask & HMSC_UP_GAMMAV) launch_gamma_v(s, iter, s.stream);
@@ -719,9 +728,46 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
         s.ring_done.push_back(e);
       }
     }
-    if (s.host_rec) HIP_OK(hipHostFree(s.host_rec));
-    HIP_OK(hipHostMalloc(&s.host_rec, sizeof(double) * s.slot_doubles * samples, hipHostMallocDefault));
+    if (s.host_rec_doubles < s.slot_doubles * s.ring_slots) {
+      if (s.host_rec) HIP_OK(hipHostFree(s.host_rec));
+      s.host_rec = nullptr;
+      HIP_OK(hipHostMalloc(&s.host_rec, sizeof(double) * s.slot_doubles * s.ring_slots, hipHostMallocDefault));
+      s.host_rec_doubles = s.slot_doubles * s.ring_slots;
+    }
   }
+  // Recorded samples are unpacked into the caller's arrays by a host worker thread as
+  // their device->host copies land, so the unpack overlaps the sweeps still being enqueued.
+  std::atomic<int> issued{0}, unpacked{0};
+  std::atomic<bool> stop{false}, worker_failed{false};
+  std::string worker_err;
+  std::thread worker;
+  struct Joiner {
+    std::thread& t;
+    std::atomic<bool>& stop;
+    ~Joiner() {
+      stop.store(true);
+      if (t.joinable()) t.join();
+    }
+  } joiner{worker, stop};
+  if (recording)
+    worker = std::thread([&] {
+      try {
+        HIP_OK(hipSetDevice(s.device));
+        for (int k = 0; k < samples; ++k) {
+          while (issued.load(std::memory_order_acquire) <= k) {
+            if (stop.load()) return;
+            std::this_thread::yield();
+          }
+          const int slot = k % s.ring_slots;
+          HIP_OK(hipEventSynchronize(s.ring_done[slot]));
+          unpack_record(s, s.host_rec + s.slot_doubles * slot, k, samples, rec);
+          unpacked.store(k + 1, std::memory_order_release);
+        }
+      } catch (const std::exception& e) {
+        worker_err = e.what();
+        worker_failed.store(true);
+      }
+    });
   const int total = transient + samples * thin;
   std::vector<hipEvent_t> packed;
   if (recording) {
@@ -737,15 +783,23 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
     if (recording && it > transient && (it - transient) % thin == 0) {
       const int k = (it - transient) / thin - 1;
       const int slot = k % s.ring_slots;
-      if (k >= s.ring_slots) HIP_OK(hipStreamWaitEvent(s.stream, s.ring_done[slot], 0));
+      if (k >= s.ring_slots) {
+        HIP_OK(hipStreamWaitEvent(s.stream, s.ring_done[slot], 0));
+        // the host slot is reused: the worker must have unpacked sample k - ring_slots
+        while (unpacked.load(std::memory_order_acquire) < k - s.ring_slots + 1) {
+          HMSC_REQUIRE(!worker_failed.load(), "record unpack: " + worker_err);
+          std::this_thread::yield();
+        }
+      }
       double* dslot = s.ring + s.slot_doubles * slot;
       join_side(s);
       launch_record(s, dslot);
       HIP_OK(hipEventRecord(packed[slot], s.stream));
       HIP_OK(hipStreamWaitEvent(s.copy_stream, packed[slot], 0));
-      HIP_OK(hipMemcpyAsync(s.host_rec + s.slot_doubles * k, dslot, sizeof(double) * s.slot_doubles,
+      HIP_OK(hipMemcpyAsync(s.host_rec + s.slot_doubles * slot, dslot, sizeof(double) * s.slot_doubles,
                             hipMemcpyDeviceToHost, s.copy_stream));
       HIP_OK(hipEventRecord(s.ring_done[slot], s.copy_stream));
+      issued.store(k + 1, std::memory_order_release);
     }
     if (verbose > 0 && it % verbose == 0) {
       HIP_OK(hipStreamSynchronize(s.stream));
@@ -761,8 +815,10 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
   int flag[2] = {0, 0};
   HIP_OK(hipMemcpy(flag, s.dev_flags, sizeof(flag), hipMemcpyDeviceToHost));
   HMSC_REQUIRE(flag[0] == 0 && flag[1] == 0, "a Cholesky factorisation failed (matrix not positive definite)");
-  if (recording)
-    for (int k = 0; k < samples; ++k) unpack_record(s, s.host_rec + s.slot_doubles * k, k, samples, rec);
+  if (recording) {
+    worker.join();
+    HMSC_REQUIRE(!worker_failed.load(), "record unpack: " + worker_err);
+  }
 }
 
 }  // namespace hmsc

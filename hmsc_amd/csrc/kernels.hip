@@ -25,6 +25,7 @@
 #include "common.h"
 #include "rng.h"
 #include "state.h"
+#include "wave_la.h"
 
 namespace hmsc {
 
@@ -310,10 +311,10 @@ static int grid_for(int64_t n, int block = 64, int cap = 2048) {
   return (int)g;
 }
 
-static size_t z_smem_bytes(const State& s, bool has_na) {
-  const size_t K4 = (s.K + 3) & ~3, K16 = (s.K + 15) & ~15;
+static size_t z_smem_bytes(int K, int nt, bool has_na) {
+  const size_t K4 = (K + 3) & ~3, K16 = (K + 15) & ~15;
   size_t d = K16 * ZT_LD + K4 * ZT_J + (size_t)ZT_J * ZT_LD + (has_na ? (size_t)ZT_J * ZT_LD : 0) +
-             (size_t)ZT_J * s.nt + ZT_J;
+             (size_t)ZT_J * nt + ZT_J;
   return d * sizeof(double) + ZT_J * sizeof(int);
 }
 
@@ -323,6 +324,21 @@ static void z_dispatch(const State& s, dim3 grid, size_t smem, const ZArgs& a) {
     z_fused_kernel<DRAW, HAS_NA, 1><<<grid, 256, smem, s.stream>>>(a);
   else
     z_fused_kernel<DRAW, HAS_NA, 2><<<grid, 256, smem, s.stream>>>(a);
+}
+
+// Workgroups of the drawing z kernel resident on the whole device at once (occupancy x CUs):
+// the site-chunk count is sized so the (chunk x species-tile) grid fills exactly one round.
+int z_resident_slots(const State& s) {
+  const size_t smem = z_smem_bytes(s.Kmax, s.nt, s.has_na);
+  int nb = 0, ncu = 0;
+  if (s.Kmax <= 32)
+    HIP_OK(s.has_na ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_fused_kernel<true, true, 1>, 256, smem)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_fused_kernel<true, false, 1>, 256, smem));
+  else
+    HIP_OK(s.has_na ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_fused_kernel<true, true, 2>, 256, smem)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_fused_kernel<true, false, 2>, 256, smem));
+  HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, s.device));
+  return std::max(1, nb) * std::max(1, ncu);
 }
 
 void launch_xeta(State& s) {
@@ -364,7 +380,7 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   a.iter = iter;
   a.noise_zero = s.noise_mode;
   dim3 grid(nchunk, s.ntile_j);
-  const size_t smem = z_smem_bytes(s, s.has_na);
+  const size_t smem = z_smem_bytes(s.K, s.nt, s.has_na);
   {
     ProfScope ps(s, PROF_Z);
     if (draw) {
@@ -500,6 +516,69 @@ __global__ __launch_bounds__(64) void beta_lambda_kernel(BLArgs a) {
   for (int r = t; r < K; r += 64) a.BL[r + (size_t)K * j] = rhs[r];
 }
 
+// Wave-resident variant for K <= 32: one species per wave, four per workgroup; the K x K
+// precision lives in registers (row r in lane r), Cholesky / solves via wave_la.h.
+template <int NM>
+__global__ __launch_bounds__(256) void beta_lambda_wave_kernel(BLArgs a) {
+  __shared__ __attribute__((aligned(16))) double tiles[4 * WV_TILE];
+  const int K = a.K, nc = a.nc, i = lane_id(), w = threadIdx.x >> 6;
+  const int j = blockIdx.x * 4 + w;
+  if (j >= a.ns_loc) return;
+  double* lds = tiles + w * WV_TILE;
+  // prior precision diagonal of Lambda rows: Psi_hj * tau_h, tau = cumprod(Delta) per level   (:51)
+  double pd = 0.0;
+  if (i >= nc && i < K) {
+    const int f = i - nc;
+    int base = 0;
+    for (int r = 0; r < a.nr; ++r) {
+      const int nf = a.lev_nf[r];
+      if (f < base + nf) {
+        double tau = 1.0;
+        for (int h = base; h <= f; ++h) tau *= a.Delta[h];
+        pd = a.Psi[f + (size_t)a.NF * j] * tau;
+        break;
+      }
+      base += nf;
+    }
+  }
+  double mu = 0.0;  // Mu_j = Gamma Tr_j^T   (:62)
+  if (i < nc)
+    for (int q = 0; q < a.nt; ++q) mu += a.Gamma[i + nc * q] * a.Tr[j + (size_t)a.ns_loc * q];
+  const double isig = a.iSigma[j];
+  const int nai = a.na_index ? a.na_index[j] : -1;
+  const double* Gj = nai >= 0 ? a.Gna + (size_t)nai * a.Kmax * a.Kmax : a.G;
+  // iU = P + XEtaTXEta * iSigma[j]   (:83-92)
+  double x[NM];
+  const int ir = i < K ? i : 0;
+#pragma unroll
+  for (int k = 0; k < NM; ++k) {
+    const int kc = k < K ? k : 0;
+    double v = isig * Gj[ir + a.Kmax * kc];
+    if (i < nc && k < nc) v += a.iV[ir + nc * kc];
+    if (i == k) v += pd;
+    x[k] = (i < K && k < K) ? v : (i == k ? 1.0 : 0.0);
+  }
+  // rhs = P Mu + isXTS   (:66, :100)
+  double r = i < K ? isig * a.XZ[ir + (size_t)K * j] : 0.0;
+  if (i < nc) {
+    double pm = 0.0;
+    for (int c = 0; c < nc; ++c) pm += a.iV[i + nc * c] * bcast(mu, c);
+    r += pm;
+  }
+  if (a.dbg_prec && i < K)
+#pragma unroll
+    for (int k = 0; k < NM; ++k)
+      if (k < K) a.dbg_prec[(size_t)j * K * K + i + (size_t)K * k] = x[k];
+  double dinv;
+  wv_chol<NM>(x, dinv);                    // RiU = chol(iU)  (:98)
+  wv_forward<NM>(x, dinv, r);              // y = L^-1 rhs
+  if (i < K && !a.noise_zero) r += normal(a.key, (uint32_t)(a.sp0 + j), (uint32_t)i, S_BETALAMBDA, a.iter);
+  double lt[NM];
+  wv_transpose<NM, true>(x, lt, lds);
+  wv_backward_t<NM>(lt, dinv, r);          // m + backsolve(RiU, xi)  (:101)
+  if (i < K) a.BL[i + (size_t)K * j] = r;
+}
+
 void launch_beta_lambda(State& s, uint32_t iter) {
   if (!s.xeta_valid) launch_xeta(s);
   if (!s.zt_valid) launch_zt_refresh(s);
@@ -533,8 +612,19 @@ void launch_beta_lambda(State& s, uint32_t iter) {
   a.key = s.key;
   a.iter = iter;
   a.noise_zero = s.noise_mode;
-  const size_t smem = ((size_t)s.K * s.K + s.K + s.NF + 1 + s.nc + 1) * sizeof(double) + 16;
   ProfScope ps(s, PROF_BL);
+  if (s.K <= 32) {
+    const int nb = (s.nsl + 3) / 4;
+    switch (wv_bucket(s.K)) {
+      case 8: beta_lambda_wave_kernel<8><<<nb, 256, 0, s.stream>>>(a); break;
+      case 16: beta_lambda_wave_kernel<16><<<nb, 256, 0, s.stream>>>(a); break;
+      case 24: beta_lambda_wave_kernel<24><<<nb, 256, 0, s.stream>>>(a); break;
+      default: beta_lambda_wave_kernel<32><<<nb, 256, 0, s.stream>>>(a); break;
+    }
+    HIP_OK(hipGetLastError());
+    return;
+  }
+  const size_t smem = ((size_t)s.K * s.K + s.K + s.NF + 1 + s.nc + 1) * sizeof(double) + 16;
   beta_lambda_kernel<<<s.nsl, 64, smem, s.stream>>>(a);
   HIP_OK(hipGetLastError());
 }
@@ -682,6 +772,175 @@ __global__ __launch_bounds__(256) void gammav_final_kernel(GVArgs a) {
 
 void allreduce_sum(State& s, double* buf, size_t n, hipStream_t st = nullptr);  // capi.cpp
 
+// ---------------------------------------------------------------------------
+// Wave-resident GammaV + Gamma2-prep for N = nc*nt <= 32 (the common case): one workgroup,
+// all four waves reduce the species partials into LDS, then wave 0 runs the whole chain
+// of small factorisations in registers (wave_la.h), products on the matrix cores.
+// Same algebra and the same Philox counters as gammav_final_kernel + gamma2_prep_kernel.
+// ---------------------------------------------------------------------------
+struct GVWArgs {
+  int nc, nt, ns_glob, nparts, do_prep;
+  const double* part;
+  const double* V0;
+  double f0;
+  const double* iUGamma;
+  const double* iUmG;
+  const double* TT;
+  double* iV;
+  double* Gamma;
+  // Gamma2 prep constants / output
+  const double* XX;
+  const double* iV0;
+  const double* V0g;
+  const double* V0gXX;
+  const double* V0gXXV0g;
+  double* prep;
+  Key key;
+  uint32_t iter;
+  int noise_zero;
+  int* fail;
+};
+
+// out(r, c) = alpha * (I_nt (x) Ablk)(r, c) + (TT (x) Bblk)(r, c) + C(r, c), padded with I.
+// Ablk / Bblk: nc x nc column-major with leading dims lda / ldb, C: N x N or null.
+template <int NM>
+__device__ inline void wv_kron(double (&o)[NM], int nc, int nt, const double* TT, double alpha, const double* Ablk,
+                               int lda, const double* Bblk, int ldb, const double* C) {
+  const int i = lane_id(), N = nc * nt;
+  const int ir = i < N ? i : 0;
+  const int c1 = ir % nc, t1 = ir / nc;
+  int c2 = 0, t2 = 0;
+#pragma unroll
+  for (int c = 0; c < NM; ++c) {
+    double v = (i == c) ? 1.0 : 0.0;
+    if (c < N) {
+      double e = TT[t1 + nt * t2] * Bblk[c1 + ldb * c2];
+      if (Ablk && t1 == t2) e += alpha * Ablk[c1 + lda * c2];
+      if (C) e += C[ir + (size_t)N * c];
+      if (i < N) v = e;
+      if (++c2 == nc) {
+        c2 = 0;
+        ++t2;
+      }
+    }
+    o[c] = v;
+  }
+}
+
+template <int NM>
+__global__ __launch_bounds__(256) void gammav_wave_kernel(GVWArgs a) {
+  // S: 3 scratch tiles for products; T0..T3: named tiles (sA aliases T0 during the reduction)
+  __shared__ __attribute__((aligned(16))) double S[3 * WV_TILE];
+  __shared__ __attribute__((aligned(16))) double T0[WV_TILE], T1[WV_TILE], T2[WV_TILE], T3[WV_TILE];
+  __shared__ double sBTr[32];
+  double* sA = T0;
+  const int nc = a.nc, nt = a.nt, N = nc * nt, t = threadIdx.x;
+  const int nA = nc * nc, nB = nc * nt;
+  for (int p = t; p < nA + nB; p += blockDim.x) {
+    double sum = 0.0;
+#pragma unroll 8
+    for (int b = 0; b < a.nparts; ++b) sum += a.part[(size_t)b * (nA + nB) + p];
+    if (p < nA)
+      sA[p] = sum + a.V0[p];  // E E^T + V0   (R/updateGammaV.R:18-19)
+    else
+      sBTr[p - nA] = sum;     // B Tr
+  }
+  __syncthreads();
+  if (t >= 64) return;
+  const int i = lane_id();
+  bool ok = true;
+  double x[NM], y[NM], z[NM], dinv;
+  // Vn = chol2inv(chol(A + V0)); LV = chol(Vn)   (:19-20)
+  wv_load<NM>(sA, nc, nc, x);
+  ok &= wv_chol<NM>(x, dinv);
+  wv_chol2inv<NM>(x, dinv, y, S);
+  ok &= wv_chol<NM>(y, dinv);  // y = LV
+  // iV = rwish(f0 + ns, Vn) by Bartlett: Zb upper, iV = (Zb LV^T)^T (Zb LV^T); Zb built in T3
+  const double v = a.f0 + a.ns_glob;
+  for (int k = 0; k < 32; ++k) {
+    double zz = (i == k && i < NM) ? 1.0 : 0.0;
+    if (i < nc && k < nc) {
+      if (k == i)
+        zz = sqrt(2.0 * gamma_std(a.key, (uint32_t)i, S_WISHART_DIAG, a.iter, 0.5 * (v - i)));
+      else if (k > i)
+        zz = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)(i + nc * k), 0, S_WISHART_OFF, a.iter);
+      else
+        zz = 0.0;
+    }
+    if (i < 32) T3[i + WV_LD * k] = zz;
+  }
+  wv_to_lds<NM, true, true>(y, S);                    // LV^T
+  wv_mm_lds<NM>(T3, S, x, S + WV_TILE);               // x = T = Zb LV^T
+  wv_gemm<NM, true, false>(x, x, z, S);               // z = iV = T^T T
+  wv_store<NM>(a.iV, nc, nc, z);
+  wv_to_lds<NM>(z, T1);                               // T1 = iV
+  wv_sync();
+  // Gamma | iV: prec = iUGamma + kron(TT, iV), rhs = iUGamma mGamma + vec(iV B Tr)   (:29-31)
+  wv_kron<NM>(x, nc, nt, a.TT, 0.0, nullptr, 0, T1, WV_LD, a.iUGamma);
+  double r = 0.0;
+  if (i < N) {
+    const int c1 = i % nc, t1 = i / nc;
+    r = a.iUmG[i];
+    for (int c2 = 0; c2 < nc; ++c2) r += T1[c1 + WV_LD * c2] * sBTr[c2 + nc * t1];
+  }
+  ok &= wv_chol<NM>(x, dinv);
+  wv_forward<NM>(x, dinv, r);
+  if (i < N && !a.noise_zero) r += normal(a.key, (uint32_t)i, 0, S_GAMMAV, a.iter);
+  wv_transpose<NM, true>(x, y, S);
+  wv_backward_t<NM>(y, dinv, r);
+  if (i < N) a.Gamma[i] = r;
+  if (!ok && i == 0) a.fail[0] = 1;
+  if (!a.do_prep) return;
+
+  // ---- Gamma2 prep (algebra as in gamma2_prep_kernel) ----
+  bool ok2 = true;
+  // iP = inv(iV + XX)                                           z = iV
+  wv_load<NM>(a.XX, nc, nc, x);
+#pragma unroll
+  for (int k = 0; k < NM; ++k) x[k] = (i < nc && k < nc) ? x[k] + z[k] : x[k];
+  ok2 &= wv_chol<NM>(x, dinv);
+  wv_chol2inv<NM>(x, dinv, y, S);                       // y = iP
+  wv_to_lds<NM>(y, T2);                                 // T2 = iP
+  wv_mm_rt<NM>(z, T2, x, S);                            // x = B1 = iV iP
+  wv_store<NM>(a.prep + nA, nc, nc, x);
+  wv_mm_rt<NM>(x, T1, y, S);                            // y = iV iP iV
+#pragma unroll
+  for (int k = 0; k < NM; ++k) y[k] = z[k] - y[k];      // M1 = iV - iV iP iV
+  wv_to_lds<NM>(y, T3);                                 // T3 = M1
+  wv_sync();
+  wv_kron<NM>(x, nc, nt, a.TT, 1.0, a.iV0, nc, T3, WV_LD, nullptr);  // WN = I (x) iV0 + TT (x) M1
+  ok2 &= wv_chol<NM>(x, dinv);
+  wv_chol2inv<NM>(x, dinv, y, S);                       // y = Rm   (:44)
+  wv_to_lds<NM>(y, T0);                                 // T0 = Rm
+  wv_load<NM>(a.V0gXX, nc, nc, x);
+  wv_mm_rt<NM>(x, T2, z, S);                            // z = T1m = V0 XX iP
+  wv_load<NM>(a.V0g, nc, nc, y);
+#pragma unroll
+  for (int k = 0; k < NM; ++k) y[k] -= z[k];            // A1 = V0 - V0 XX iP
+  wv_store<NM>(a.prep, nc, nc, y);
+  wv_mm_rt<NM>(z, T1, y, S);                            // y = W1 = T1m iV
+  wv_to_lds<NM>(y, T3);                                 // T3 = W1
+  wv_gemm<NM, false, true>(z, x, y, S);                 // y = T1m V0XX^T     (x = V0gXX)
+  wv_load<NM>(a.V0gXXV0g, nc, nc, x);
+#pragma unroll
+  for (int k = 0; k < NM; ++k) x[k] -= y[k];            // M1' = V0 XX V0 - V0 XX iP XX V0
+  wv_to_lds<NM>(x, T2);                                 // T2 = M1'
+  wv_sync();
+  wv_kron<NM>(z, nc, nt, a.TT, 0.0, nullptr, 0, T3, WV_LD, nullptr);  // z = tmp = TT (x) W1   (:48)
+  wv_mm_rt<NM>(z, T0, x, S);                            // x = TR = tmp Rm
+  wv_store<NM>(a.prep + 2 * nA, N, N, x);
+  wv_gemm<NM, false, true>(x, z, y, S);                 // y = tmp Rm tmp^T
+  wv_kron<NM>(x, nc, nt, a.TT, 1.0, a.V0g, nc, T2, WV_LD, nullptr);  // x = I (x) V0 + TT (x) M1'
+  wv_kron<NM>(z, nc, nt, a.TT, 0.0, nullptr, 0, T2, WV_LD, nullptr); // z = TT (x) M1'
+#pragma unroll
+  for (int k = 0; k < NM; ++k) x[k] = x[k] - 2.0 * z[k] + y[k];     // SigmaG   (:50)
+  wv_pad<NM>(x, N, 1.0);
+  ok2 &= wv_chol<NM>(x, dinv);                          // LSigmaG   (:52)
+  wv_store_lower<NM>(a.prep + 2 * nA + N * N, N, N, x);
+  if (!ok2 && i == 0) a.fail[1] = 1;
+}
+
+
 void launch_gamma_v(State& s, uint32_t iter, hipStream_t st) {
   const int nparts = (s.nsl + SB - 1) / SB;
   double* part = s.ABpart;
@@ -695,6 +954,42 @@ void launch_gamma_v(State& s, uint32_t iter, hipStream_t st) {
     allreduce_sum(s, s.allreduce_buf, n, st);
     part = s.allreduce_buf;
     np = 1;
+  }
+  const int Ng = s.nc * s.nt;
+  if (Ng <= 32) {
+    GVWArgs w{};
+    w.nc = s.nc;
+    w.nt = s.nt;
+    w.ns_glob = s.ns;
+    w.nparts = np;
+    w.do_prep = (s.mask & HMSC_UP_GAMMA2) ? 1 : 0;
+    w.part = part;
+    w.V0 = s.V0;
+    w.f0 = s.f0;
+    w.iUGamma = s.iUGamma;
+    w.iUmG = s.iUmG;
+    w.TT = s.TT;
+    w.iV = s.iV;
+    w.Gamma = s.Gamma;
+    w.XX = s.XX;
+    w.iV0 = s.iV0;
+    w.V0g = s.V0g;
+    w.V0gXX = s.V0gXX;
+    w.V0gXXV0g = s.V0gXXV0g;
+    w.prep = s.g2prep;
+    w.key = s.key;
+    w.iter = iter;
+    w.noise_zero = s.noise_mode;
+    w.fail = s.dev_flags;
+    switch (wv_bucket(Ng)) {
+      case 8: gammav_wave_kernel<8><<<1, 256, 0, st>>>(w); break;
+      case 16: gammav_wave_kernel<16><<<1, 256, 0, st>>>(w); break;
+      case 24: gammav_wave_kernel<24><<<1, 256, 0, st>>>(w); break;
+      default: gammav_wave_kernel<32><<<1, 256, 0, st>>>(w); break;
+    }
+    HIP_OK(hipGetLastError());
+    if (w.do_prep) s.g2prep_valid = true;
+    return;
   }
   GVArgs a{};
   a.nc = s.nc;

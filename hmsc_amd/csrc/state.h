@@ -54,8 +54,8 @@ struct State {
   hipStream_t stream = nullptr, copy_stream = nullptr;
   // side stream: updateGammaV, Gamma2's iV-only algebra and updateLambdaPriors of sweep t
   // only feed sweep t+1, so they overlap updateEta / updateZ of sweep t
-  hipStream_t side = nullptr;
-  hipEvent_t ev_bl = nullptr, ev_side = nullptr;
+  hipStream_t side = nullptr, side2 = nullptr;  // side: GammaV + Gamma2 prep; side2: LambdaPriors
+  hipEvent_t ev_bl = nullptr, ev_side = nullptr, ev_side2 = nullptr;
   bool side_pending = false;
 
   // model (device)
@@ -115,7 +115,8 @@ struct State {
   int ring_slots = 0;
   size_t slot_doubles = 0;
   std::vector<hipEvent_t> ring_done;
-  double* host_rec = nullptr;    // pinned
+  double* host_rec = nullptr;    // pinned host ring (ring_slots slots)
+  size_t host_rec_doubles = 0;
 
   // live kernel timing (HIP events on this chain's stream), id -> launches
   bool prof = false;
@@ -172,6 +173,7 @@ struct ProfScope {  // records a start/stop event pair around one launch when pr
 void launch_init(State& s);
 void launch_update_z(State& s, uint32_t iter, bool use_raw_y);
 void launch_zt_refresh(State& s);
+int z_resident_slots(const State& s);
 void launch_xeta(State& s);
 void launch_beta_lambda(State& s, uint32_t iter);
 void launch_gamma_v(State& s, uint32_t iter, hipStream_t st);

@@ -11,5 +11,5 @@ tail -2 gpurun_out/${TAG}_pytest.log
 timeout -k 10 600 python bench.py --steps $STEPS --warmup 30 --cpu-seconds 10 > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { echo "bench failed"; tail -20 gpurun_out/${TAG}_bench.err; exit 1; }
 cat gpurun_out/${TAG}_bench.json
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${TAG}_prof -o run -- python $R/bench.py --steps $STEPS --warmup 30 --no-cpu > $R/gpurun_out/${TAG}_prof_bench.json 2> $R/gpurun_out/${TAG}_prof.err || { echo "rocprof failed"; tail -20 $R/gpurun_out/${TAG}_prof.err; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_prof -o run -- python $R/bench.py --steps $STEPS --warmup 30 --no-cpu > $R/gpurun_out/${TAG}_prof_bench.json 2> $R/gpurun_out/${TAG}_prof.err || { echo "rocprof failed"; tail -20 $R/gpurun_out/${TAG}_prof.err; exit 1; }
 echo done

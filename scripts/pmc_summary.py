@@ -1,0 +1,39 @@
+"""Average rocprofv3 PMC counters per kernel over the passes of scripts/pmc_z.sh.
+
+FETCH_SIZE is reported in KB by rocprofv3 and, on gfx950, counts half the bytes of wide
+coalesced streaming reads (MI355X_MICROARCH.md, HBM section): the corrected read bytes are
+2 x FETCH_SIZE x 1024.  WRITE_SIZE (KB) is exact for 16-B streaming stores.
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+root = sys.argv[1]
+vals = defaultdict(lambda: defaultdict(list))
+dur = defaultdict(list)
+for f in sorted(glob.glob(os.path.join(root, "p*", "p_counter_collection.csv"))):
+    for r in csv.DictReader(open(f)):
+        k = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void ", "").replace("hmsc::", "")
+        vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        if r["Counter_Name"] in ("SQ_WAVES", "FETCH_SIZE"):
+            dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+out = {}
+for k, cs in vals.items():
+    d = {c: sum(v) / len(v) for c, v in cs.items()}
+    d["avg_us_profiled"] = sum(dur[k]) / max(1, len(dur[k]))
+    if "FETCH_SIZE" in d:
+        d["hbm_read_bytes_corrected"] = 2 * d["FETCH_SIZE"] * 1024
+    if "WRITE_SIZE" in d:
+        d["hbm_write_bytes"] = d["WRITE_SIZE"] * 1024
+    if "GRBM_GUI_ACTIVE" in d and d["avg_us_profiled"] > 0:
+        d["eff_clock_ghz"] = d["GRBM_GUI_ACTIVE"] / 8 / (d["avg_us_profiled"] * 1e3)
+    if "SQ_INSTS_VALU" in d and "SQ_WAVES" in d:
+        d["valu_insts_per_wave"] = d["SQ_INSTS_VALU"] / max(1, d["SQ_WAVES"])
+    if "SQ_WAVE_CYCLES" in d and "SQ_ACTIVE_INST_VALU" in d:
+        d["valu_active_frac_of_wave_cycles"] = d["SQ_ACTIVE_INST_VALU"] / max(1, d["SQ_WAVE_CYCLES"])
+    out[k] = d
+json.dump(out, sys.stdout, indent=1, sort_keys=True)

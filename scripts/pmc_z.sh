@@ -1,0 +1,17 @@
+#!/bin/bash
+# PMC passes (one counter group per rocprofv3 run, kernel-trace only) for the dominant kernels.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:-pmc}
+REGEX=${2:-z_fused|beta_lambda|eta_shared|gammav_wave|zl_kernel|xeta_gram}
+mkdir -p $R/gpurun_out/$TAG
+cd /tmp && export TMPDIR=/tmp
+i=0
+for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" \
+           "GRBM_GUI_ACTIVE SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_MFMA" \
+           "FETCH_SIZE" "WRITE_SIZE"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp --kernel-include-regex "$REGEX" --output-format csv \
+    -d $R/gpurun_out/$TAG/p$i -o p -- python $R/scripts/trace_sweeps.py > $R/gpurun_out/$TAG/p$i.log 2>&1 || { echo "pass $i failed"; tail -20 $R/gpurun_out/$TAG/p$i.log; exit 1; }
+done
+echo pmc done

@@ -40,6 +40,10 @@ MODELS = {
     "two_levels_units": dict(ny=240, ns=25, nc=3, nf=2, nr=2, units=[240, 37], seed=5),
     "grouped_units": dict(ny=240, ns=20, nc=3, nf=3, nr=1, units=[40], seed=8),
     "traits": dict(ny=120, ns=35, nc=3, nf=2, nt=3, seed=6),
+    # nc*nt = 36 > 32: GammaV / Gamma2 take the LDS workgroup path instead of the wave path
+    "wide_traits": dict(ny=150, ns=40, nc=12, nf=2, nt=3, seed=9),
+    # nc = 20 (wave bucket 24), K = 30: the bench's dimension class at small ny / ns
+    "bench_dims": dict(ny=300, ns=50, nc=20, nf=10, seed=10),
 }
 
 
