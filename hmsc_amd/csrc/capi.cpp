@@ -155,7 +155,9 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.nranks = nranks;
   s.key = Key{(uint32_t)(seed & 0xFFFFFFFFu), (uint32_t)(seed >> 32)};
   s.f0 = m->f0;
-  const int per = (m->ns + nranks - 1) / nranks;
+  // species shards start at even species: updateZ draws the species pair (2m, 2m+1) from one
+  // Philox call (kernels.hip, z_wave_kernel)
+  const int per = (((m->ns + nranks - 1) / nranks) + 1) & ~1;
   s.sp0 = std::min(m->ns, rank * per);
   s.nsl = std::min(m->ns, s.sp0 + per) - s.sp0;
   HMSC_REQUIRE(s.nsl > 0, "species shard is empty (more ranks than species)");

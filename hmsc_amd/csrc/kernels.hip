@@ -26,6 +26,7 @@
 #include "rng.h"
 #include "state.h"
 #include "wave_la.h"
+#include "z_kernel.h"
 
 namespace hmsc {
 
@@ -66,194 +67,6 @@ static EtaView make_view(const State& s) {
     v.nf[r] = s.lev[r].nf;
   }
   return v;
-}
-
-// ---------------------------------------------------------------------------
-// updateZ (R/updateZ.R:4-94) fused with the Z contractions of the next sweep.
-// Grid: (site chunks, species tiles of 64); block 256 = 4 waves; each wave owns 16
-// species of the tile, each lane one site of the current 64-site tile.
-// ---------------------------------------------------------------------------
-struct ZArgs {
-  EtaView ev;
-  const double* XEta;  // ny x K (ld ny)
-  int K, ns_loc, sp0, nt, tiles_per_chunk;
-  const double* BL;
-  const double* iSigma;
-  const int8_t* Ycode;
-  const double* Yval;
-  const int* fam;
-  const double* Tr;  // local species rows, ld ns_loc
-  double* Z;
-  double* XZ_part;   // [chunk][K x ns_loc]
-  double* G_part;    // [chunk][Kmax x Kmax]
-  double* ZTr_part;  // [tile_j][ny x nt]
-  int Kmax;
-  Key key;
-  uint32_t iter;
-  int noise_zero;
-};
-
-constexpr int ZT_I = 64;   // sites per tile (4 waves x 16)
-constexpr int ZT_J = 32;   // species per tile (2 MFMA column blocks of 16)
-constexpr int ZT_LD = 65;  // padded LDS leading dimension
-constexpr int KMAX_Z = 64;
-
-typedef double d4 __attribute__((ext_vector_type(4)));
-
-// v_mfma_f64_16x16x4_f64: D[16x16] += A[16x4] B[4x16]; lane l supplies A[l&15][l>>4] and
-// B[l>>4][l&15] and holds D[(l>>4) + 4r][l&15], r = 0..3 (checked by scripts/mfma_layout_check.hip).
-__device__ __forceinline__ d4 mfma_f64(double a, double b, d4 c) {
-  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-}
-
-// one latent draw; kept out of line so the polynomial constants of erfc / AS241 are
-// materialised per call instead of being hoisted into the kernel's register file
-__device__ __noinline__ double z_draw(double e, double sd, int code, int fam, double yv, Key key, uint32_t idx,
-                                      uint32_t iter, int noise_zero) {
-  if (code < 0) {  // NA cell: Z ~ N(E, sd)   R/updateZ.R:92
-    const double nz = noise_zero ? 0.0 : normal(key, idx, 0, S_Z, iter);
-    return e + sd * nz;
-  }
-  if (fam == 2) {  // probit: truncated normal   R/updateZ.R:43-63
-    const double u = uniforms(key, idx, 0, S_Z, iter).a;
-    const double sg = code ? 1.0 : -1.0;
-    return e + sd * sg * trunc_normal_lower(-sg * e / sd, u);
-  }
-  return yv;  // normal: Z = Y   R/updateZ.R:40-41
-}
-
-// Fused updateZ.  Per 64-site x 32-species tile:
-//   E^T = BL^T XEta^T on the matrix cores (2 MFMA blocks per wave, K/4 steps),
-//   truncated-normal draws on the VALU (8 per lane), Z stored once,
-//   XZ += XEta^T (Yx o Z) on the matrix cores (accumulated over the chunk's tiles),
-//   ZTr += Z Tr (VALU, nt small).
-// NQ = XZ output tiles per wave (K <= 32: 1, K <= 64: 2).
-template <bool DRAW, bool HAS_NA, int NQ>
-__global__ __launch_bounds__(256) void z_fused_kernel(ZArgs a) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int K = a.K, K4 = (K + 3) & ~3, K16 = (K + 15) & ~15;
-  const int ny = a.ev.ny;
-  double* sXE = smem;                   // [K16][ZT_LD], rows >= K zero
-  double* sBL = sXE + K16 * ZT_LD;      // [K4][ZT_J],   rows >= K zero
-  double* sZ = sBL + K4 * ZT_J;         // [jj][ZT_LD]   masked Z (XZ)
-  double* sZu = sZ + ZT_J * ZT_LD;      // [jj][ZT_LD]   unmasked Z (ZTr), HAS_NA only
-  double* sTr = (HAS_NA ? sZu + ZT_J * ZT_LD : sZu);  // [jj + ZT_J t]
-  double* sSd = sTr + ZT_J * a.nt;      // [jj]
-  int* sFam = (int*)(sSd + ZT_J);       // [jj]
-
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, lm = lane & 15, lk = lane >> 4;
-  const int j0 = blockIdx.y * ZT_J;
-  for (int p = t; p < K4 * ZT_J; p += 256) {
-    const int k = p >> 5, jj = p & 31, j = j0 + jj;
-    sBL[p] = (k < K && j < a.ns_loc) ? a.BL[k + (size_t)K * j] : 0.0;
-  }
-  for (int p = t; p < ZT_J * a.nt; p += 256) {
-    const int jj = p & 31, tt = p >> 5, j = j0 + jj;
-    sTr[p] = (j < a.ns_loc) ? a.Tr[j + (size_t)a.ns_loc * tt] : 0.0;
-  }
-  if (t < ZT_J) {
-    const int j = j0 + t;
-    sSd[t] = (j < a.ns_loc) ? 1.0 / sqrt(a.iSigma[j]) : 1.0;
-    sFam[t] = (j < a.ns_loc) ? a.fam[j] : 0;
-  }
-  d4 accXZ[NQ];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) accXZ[q] = d4{0.0, 0.0, 0.0, 0.0};
-  const int n_xz_tiles = 2 * (K16 >> 4);
-
-  const int n_tiles = (ny + ZT_I - 1) / ZT_I;
-  const int tb = blockIdx.x * a.tiles_per_chunk;
-  const int te = min(n_tiles, tb + a.tiles_per_chunk);
-  for (int tile = tb; tile < te; ++tile) {
-    const int i0 = tile * ZT_I;
-    __syncthreads();
-    for (int p = t; p < K16 * ZT_I; p += 256) {
-      const int k = p >> 6, ii = p & 63, i = i0 + ii;
-      sXE[k * ZT_LD + ii] = (i < ny && k < K) ? a.XEta[i + (size_t)ny * k] : 0.0;
-    }
-    __syncthreads();
-    const int iloc = 16 * w + lm, i = i0 + iloc;
-    double zv[8];
-    if (DRAW) {
-      // E^T tile: rows = species (2 blocks of 16), cols = this wave's 16 sites   (R/updateZ.R:11-34)
-      d4 e0 = {0.0, 0.0, 0.0, 0.0}, e1 = {0.0, 0.0, 0.0, 0.0};
-      for (int k = lk; k < K4; k += 4) {
-        const double b = sXE[k * ZT_LD + iloc];
-        e0 = mfma_f64(sBL[k * ZT_J + lm], b, e0);
-        e1 = mfma_f64(sBL[k * ZT_J + 16 + lm], b, e1);
-      }
-#pragma unroll
-      for (int v = 0; v < 8; ++v) {
-        const int jj = 16 * (v >> 2) + lk + 4 * (v & 3), j = j0 + jj;
-        const double ev = (v < 4) ? e0[v & 3] : e1[v & 3];
-        double z = 0.0;
-        if (i < ny && j < a.ns_loc) {
-          const size_t cell = (size_t)i + (size_t)ny * j;
-          const uint32_t idx = (uint32_t)((size_t)i + (size_t)ny * (size_t)(a.sp0 + j));
-          const int code = a.Ycode[cell];
-          const int fam = sFam[jj];
-          z = z_draw(ev, sSd[jj], code, fam, fam == 1 ? a.Yval[cell] : 0.0, a.key, idx, a.iter, a.noise_zero);
-          a.Z[cell] = z;
-        }
-        zv[v] = z;
-      }
-    } else {
-#pragma unroll
-      for (int v = 0; v < 8; ++v) {
-        const int jj = 16 * (v >> 2) + lk + 4 * (v & 3), j = j0 + jj;
-        zv[v] = (i < ny && j < a.ns_loc) ? a.Z[(size_t)i + (size_t)ny * j] : 0.0;
-      }
-    }
-#pragma unroll
-    for (int v = 0; v < 8; ++v) {
-      const int jj = 16 * (v >> 2) + lk + 4 * (v & 3), j = j0 + jj;
-      if (HAS_NA) {
-        const bool obs = (i < ny && j < a.ns_loc) ? (a.Ycode[(size_t)i + (size_t)ny * j] >= 0) : false;
-        sZ[jj * ZT_LD + iloc] = obs ? zv[v] : 0.0;
-        sZu[jj * ZT_LD + iloc] = zv[v];
-      } else {
-        sZ[jj * ZT_LD + iloc] = zv[v];
-      }
-    }
-    __syncthreads();
-    // XZ += XEta^T (Yx o Z) over the tile's 64 sites   (R/updateBetaLambda.R:66 of the next sweep)
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int id = w + 4 * q;
-      if (id < n_xz_tiles) {
-        const int kb = id >> 1, sbb = id & 1;
-        const double* ar = sXE + (kb * 16 + lm) * ZT_LD;
-        const double* br = sZ + (16 * sbb + lm) * ZT_LD;
-        for (int st = lk; st < ZT_I; st += 4) accXZ[q] = mfma_f64(ar[st], br[st], accXZ[q]);
-      }
-    }
-    // ZTr partial for this (site tile, species tile)   (R/updateGamma2.R:46)
-    {
-      const int ii = lane, is = i0 + lane;
-      if (is < ny) {
-        const double* zsrc = HAS_NA ? sZu : sZ;
-        for (int tt = w; tt < a.nt; tt += 4) {
-          double acc = 0.0;
-#pragma unroll 8
-          for (int jj = 0; jj < ZT_J; ++jj) acc = fma(zsrc[jj * ZT_LD + ii], sTr[jj + ZT_J * tt], acc);
-          a.ZTr_part[(size_t)blockIdx.y * ny * a.nt + is + (size_t)ny * tt] = acc;
-        }
-      }
-    }
-  }
-  double* dst = a.XZ_part + (size_t)blockIdx.x * K * a.ns_loc;
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    const int id = w + 4 * q;
-    if (id < n_xz_tiles) {
-      const int kb = id >> 1, sbb = id & 1, j = j0 + 16 * sbb + lm;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int k = kb * 16 + lk + 4 * r;
-        if (k < K && j < a.ns_loc) dst[k + (size_t)K * j] = accXZ[q][r];
-      }
-    }
-  }
 }
 
 // Materialise XEta = [X, Eta_1[Pi_1,], ...] (R/updateBetaLambda.R:21-41) for one 64-site
@@ -311,32 +124,35 @@ static int grid_for(int64_t n, int block = 64, int cap = 2048) {
   return (int)g;
 }
 
-static size_t z_smem_bytes(int K, int nt, bool has_na) {
-  const size_t K4 = (K + 3) & ~3, K16 = (K + 15) & ~15;
-  size_t d = K16 * ZT_LD + K4 * ZT_J + (size_t)ZT_J * ZT_LD + (has_na ? (size_t)ZT_J * ZT_LD : 0) +
-             (size_t)ZT_J * nt + ZT_J;
-  return d * sizeof(double) + ZT_J * sizeof(int);
-}
-
 template <bool DRAW, bool HAS_NA>
 static void z_dispatch(const State& s, dim3 grid, size_t smem, const ZArgs& a) {
-  if (s.K <= 32)
-    z_fused_kernel<DRAW, HAS_NA, 1><<<grid, 256, smem, s.stream>>>(a);
-  else
-    z_fused_kernel<DRAW, HAS_NA, 2><<<grid, 256, smem, s.stream>>>(a);
+  switch (z_nkb(s.K)) {
+    case 1: z_wave_kernel<DRAW, HAS_NA, 1><<<grid, 256, smem, s.stream>>>(a); break;
+    case 2: z_wave_kernel<DRAW, HAS_NA, 2><<<grid, 256, smem, s.stream>>>(a); break;
+    case 3: z_wave_kernel<DRAW, HAS_NA, 3><<<grid, 256, smem, s.stream>>>(a); break;
+    default: z_wave_kernel<DRAW, HAS_NA, 4><<<grid, 256, smem, s.stream>>>(a); break;
+  }
+}
+
+template <bool HAS_NA>
+static int z_occupancy(int nkb, size_t smem) {
+  int nb = 0;
+  switch (nkb) {
+    case 1: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 1>, 256, smem)); break;
+    case 2: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 2>, 256, smem)); break;
+    case 3: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 3>, 256, smem)); break;
+    default: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 4>, 256, smem)); break;
+  }
+  return nb;
 }
 
 // Workgroups of the drawing z kernel resident on the whole device at once (occupancy x CUs):
-// the site-chunk count is sized so the (chunk x species-tile) grid fills exactly one round.
+// the site-chunk count is sized so the (chunk x species-block) grid fills exactly one round.
 int z_resident_slots(const State& s) {
-  const size_t smem = z_smem_bytes(s.Kmax, s.nt, s.has_na);
-  int nb = 0, ncu = 0;
-  if (s.Kmax <= 32)
-    HIP_OK(s.has_na ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_fused_kernel<true, true, 1>, 256, smem)
-                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_fused_kernel<true, false, 1>, 256, smem));
-  else
-    HIP_OK(s.has_na ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_fused_kernel<true, true, 2>, 256, smem)
-                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_fused_kernel<true, false, 2>, 256, smem));
+  const size_t smem = z_smem_bytes(s.Kmax, s.nt);
+  const int nkb = z_nkb(s.Kmax);
+  int ncu = 0;
+  const int nb = s.has_na ? z_occupancy<true>(nkb, smem) : z_occupancy<false>(nkb, smem);
   HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, s.device));
   return std::max(1, nb) * std::max(1, ncu);
 }
@@ -354,12 +170,12 @@ void launch_xeta(State& s) {
 
 static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   HMSC_REQUIRE(s.K <= KMAX_Z, "updateZ: K = nc + sum(nf) must be <= 64 in this build");
+  HMSC_REQUIRE((s.sp0 & 1) == 0, "updateZ: species shards must start at an even species (Philox pairs)");
   if (!s.xeta_valid) launch_xeta(s);
   ZArgs a{};
-  a.ev = make_view(s);
   a.XEta = s.XEta;
+  a.ny = s.ny;
   a.K = s.K;
-  a.Kmax = s.Kmax;
   a.ns_loc = s.nsl;
   a.sp0 = s.sp0;
   a.nt = s.nt;
@@ -374,13 +190,12 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   a.Tr = s.Tr;
   a.Z = s.Z;
   a.XZ_part = s.XZ_part;
-  a.G_part = s.G_part;
   a.ZTr_part = s.ZTr_part;
   a.key = s.key;
   a.iter = iter;
   a.noise_zero = s.noise_mode;
   dim3 grid(nchunk, s.ntile_j);
-  const size_t smem = z_smem_bytes(s.K, s.nt, s.has_na);
+  const size_t smem = z_smem_bytes(s.K, s.nt);
   {
     ProfScope ps(s, PROF_Z);
     if (draw) {

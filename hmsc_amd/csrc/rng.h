@@ -171,43 +171,174 @@ __host__ __device__ __forceinline__ double qnorm_as241(double p) {
   return q < 0.0 ? -val : val;
 }
 
-// Standard normal truncated to [alpha, +inf) by inversion of the upper tail:
-//   x = Phic^-1(u * Phic(alpha)) = -qnorm(u * 0.5 erfc(alpha / sqrt 2)),
-// with the exponential tail expansion beyond alpha > 25 where erfc underflows.
-// Branch-free erfc for the truncated-normal transform: for z >= 0,
-// erfc(z) = t exp(-z^2 + g(t)), t = 2 / (2 + z), with g a degree-24 Chebyshev series in 2t - 1
-// (coefficients fitted by scripts/fit_erfc.py; max relative error 3.1e-14 on [0, 18], from
-// rounding of -z^2 at large z), and erfc(-z) = 2 - erfc(z).  One division, one exp and a
-// Clenshaw recurrence, the same instruction stream in every lane (the libm erfc branches on
-// five argument ranges, which diverges across a wave of cells).
-__device__ __forceinline__ double erfc_cheb(double z) {
-  constexpr double c[25] = {-0.6513268598908547, 0.6419697923564907, 0.019476473204185794, -0.009561514786808322,
-                            -0.0009465953444817606, 0.0003668394978524299, 4.252332480676113e-05,
-                            -2.0278578112090017e-05, -1.624290004616037e-06, 1.3036558354648522e-06,
-                            1.5626441965479678e-08, -8.523809553318847e-08, 6.5290545049341035e-09,
-                            5.059343126909536e-09, -9.913638910734626e-10, -2.2736555453727975e-10,
-                            9.646798632720434e-11, 2.393915069408435e-12, -6.886047244122345e-12,
-                            8.947117551256468e-13, 3.1297560583840907e-13, -1.1280057646648457e-13,
-                            8.695131613182434e-16, 6.889526006643458e-15, -1.856021631896973e-15};
-  const double a = fabs(z);
-  const double t = 2.0 / (2.0 + a);
-  const double x = 2.0 * t - 1.0, x2 = 2.0 * x;
-  double b1 = 0.0, b2 = 0.0;
-#pragma unroll
-  for (int k = 24; k >= 1; --k) {
-    const double tmp = b1;
-    b1 = fma(x2, b1, -b2) + c[k];
-    b2 = tmp;
+// ---------------------------------------------------------------------------
+// Truncated-normal draw of updateZ (probit, R/updateZ.R:43-63; NA cells :92).
+//
+// The device evaluates the same inversion as the oracle (oracle/rng.py,
+// trunc_normal_lower: x = -Phi^-1(u Phic(alpha)) with R's AS241 quantile and erfc)
+// through cheaper, equally accurate approximations of the two special functions:
+//   erfc_fast   t exp(-z^2 + g(t)), g a degree-24 polynomial (scripts/fit_erfc.py; 3.3e-15
+//               rel. on [0,18] with exact -z^2, ~5e-14 from rounding -z^2 + g near z = 18)
+//   qnorm_fast  Giles-form y F(w), w = -log(4p(1-p)) (degree-22 / 18 polynomials,
+//               1.2e-15 rel., scripts/fit_qnorm.py); no division, and one branch for
+//               p in (4.8e-4, 1 - 4.8e-4) so a wave rarely diverges; AS241's tail
+//               branch below p < 2.8e-8
+//   log_fast    2 atanh((m-1)/(m+1)) series; the libm f64 log is the single most
+//               expensive operation of the draw on gfx950
+// ---------------------------------------------------------------------------
+// Polynomial tables of the draw (fit scripts above).  Device code reads them from the
+// constant segment: scalar loads put each coefficient in an SGPR pair that v_fma_f64 takes
+// directly, instead of two v_mov_b32 per coefficient for an inline 64-bit constant (which
+// doubled the VALU cost of every Horner step).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define HMSC_TABLE __constant__ const
+#else
+#define HMSC_TABLE static constexpr
+#endif
+HMSC_TABLE double kErfcPoly[25] = {
+      -1.6096273515890176e-08, 2.8896766487768683e-08, 9.88621235162138e-08,   -2.844034573481913e-07,
+      -1.0193810001498908e-07, 1.2706984221004204e-06, -1.3111619454625253e-06, -2.9457683933017214e-06,
+      8.56105638070289e-06,    1.2449683704760738e-07, -3.016850594852468e-05,  3.175555345672128e-05,
+      7.138643642973066e-05,   -0.00017430723111562955, -9.37294005044714e-05,  0.0006736798283005599,
+      -0.00014624812013790348, -0.002345812641093767,  0.00175893371693428,     0.008824938566235015,
+      -0.009872689376767278,   -0.04689561023128137,   0.04734330684218011,     0.6726432239776464,
+      -0.6717940840566932};
+HMSC_TABLE double kQnormA[23] = {
+      -5.074424267359028e-21,  -2.3811955906043086e-19, 1.8144870687718696e-18, 1.5770660103399937e-17,
+      -1.8845358151887642e-16, 2.9846762245925465e-17,  9.386009135507089e-15,  -5.734239867658464e-14,
+      -1.152781205111968e-13,  3.7243600322751594e-12,  -1.834964551484408e-11, -7.658556077966893e-11,
+      1.486638762143385e-09,   -5.8161425593643965e-09, -4.111171165723433e-08, 5.988894312980168e-07,
+      -1.9310650615501303e-06, -1.9632852819320237e-05, 0.0002640820495606514,  -0.001047511569502178,
+      -0.008532899177271985,   0.33963495870114074,     2.3386207100265937};
+HMSC_TABLE double kQnormB[19] = {
+      3.0461394605911588e-09, 1.2830956896813974e-07,  -3.889559056501335e-07, 2.5883730570008207e-08,
+      2.1250018533444026e-06, -5.676547943250077e-06,  4.134476749930014e-06,  1.7642784745338954e-05,
+      -6.691811180311149e-05, 9.656935201727177e-05,   3.398512760254179e-05,  -0.0005020988747342482,
+      0.0013481547691666972,  -0.0023875821884917874,  0.0035234312022082047,  -0.005305009946688643,
+      0.007595620204033648,   1.421650865810257,       4.36127285516533};
+HMSC_TABLE double kLogSeries[10] = {2.0 / 21.0, 2.0 / 19.0, 2.0 / 17.0, 2.0 / 15.0, 2.0 / 13.0,
+                                    2.0 / 11.0, 2.0 / 9.0,  2.0 / 7.0,  2.0 / 5.0,  2.0 / 3.0};
+
+// Horner step a*b + c with c wave-uniform: forced into the VOP3 form whose third operand is
+// an SGPR pair (the compiler otherwise tends to copy c into VGPRs with two v_mov_b32 and use
+// v_fmac_f64, doubling the issue cost of each step).
+__host__ __device__ __forceinline__ double fma_sc(double a, double b, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+  return r;
+#else
+  return fma(a, b, c);
+#endif
+}
+
+// 1/d for d in [1, 1e3] (well conditioned): v_rcp_f64 + two Newton steps, ~1 ulp; the IEEE
+// division sequence (div_scale / div_fmas / div_fixup) costs twice as much
+__host__ __device__ __forceinline__ double rcp_pos(double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(r, fma(-d, r, 1.0), r);
+  r = fma(r, fma(-d, r, 1.0), r);
+  return r;
+#else
+  return 1.0 / d;
+#endif
+}
+
+__host__ __device__ __forceinline__ double log_fast(double x) {  // x positive, normal
+  uint64_t b;
+  __builtin_memcpy(&b, &x, 8);
+  int e = (int)(b >> 52) - 1023;
+  const uint64_t mb = (b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull;
+  double m;
+  __builtin_memcpy(&m, &mb, 8);
+  if (m > 1.4142135623730951) {
+    m *= 0.5;
+    e += 1;
   }
-  const double g = fma(x, b1, -b2) + c[0];
+  const double f = m - 1.0;
+  const double s = f * rcp_pos(2.0 + f);
+  const double z = s * s;
+  // P(z) = sum_{k=1..10} 2 z^(k-1) / (2k+1); truncation < 3e-17 relative for |s| <= 0.1716
+  double P = kLogSeries[0];
+#pragma unroll
+  for (int k = 1; k < 10; ++k) P = fma_sc(P, z, kLogSeries[k]);
+  const double lm = fma(s * z, P, 2.0 * s);
+  const double de = (double)e;
+  return fma(de, 0.6931471803691238, fma(de, 1.9082149292705877e-10, lm));  // ln2 = hi + lo, hi*e exact
+}
+
+__host__ __device__ __forceinline__ double erfc_fast(double z) {
+  const double a = fmin(fabs(z), 40.0);
+  const double t = 2.0 * rcp_pos(2.0 + a);
+  const double x = 2.0 * t - 1.0;
+  double g = kErfcPoly[0];
+#pragma unroll
+  for (int k = 1; k < 25; ++k) g = fma_sc(g, x, kErfcPoly[k]);
   const double r = t * exp(fma(-a, a, g));
   return z < 0.0 ? 2.0 - r : r;
 }
 
-__device__ __forceinline__ double trunc_normal_lower(double alpha, double u) {
-  if (alpha > 25.0) return alpha - log(u) / alpha;
-  const double p = u * (0.5 * erfc_cheb(alpha * 0.7071067811865476));
-  return -qnorm_as241(p);
+// AS241's |q| > 0.425 branch (R's qnorm), with log_fast
+__host__ __device__ __forceinline__ double qnorm_as241_tail(double p) {
+  const double q = p - 0.5;
+  double r = q < 0.0 ? p : 1.0 - p;
+  r = sqrt(-log_fast(r));
+  double val;
+  if (r <= 5.0) {
+    r -= 1.6;
+    const double num =
+        (((((((7.74545014278341407640e-4 * r + 2.27238449892691845833e-2) * r + 2.41780725177450611770e-1) * r +
+             1.27045825245236838258e0) * r + 3.64784832476320460504e0) * r + 5.76949722146069140550e0) * r +
+          4.63033784615654529590e0) * r + 1.42343711074968357734e0);
+    const double den =
+        (((((((1.05075007164441684324e-9 * r + 5.47593808499534494600e-4) * r + 1.51986665636164571966e-2) * r +
+             1.48103976427480074590e-1) * r + 6.89767334985100004550e-1) * r + 1.67638483018380384940e0) * r +
+          2.05319162663775882187e0) * r + 1.0);
+    val = num / den;
+  } else {
+    r -= 5.0;
+    const double num =
+        (((((((2.01033439929228813265e-7 * r + 2.71155556874348757815e-5) * r + 1.24266094738807843860e-3) * r +
+             2.65321895265761230930e-2) * r + 2.96560571828504891230e-1) * r + 1.78482653991729133580e0) * r +
+          5.46378491116411436990e0) * r + 6.65790464350110377720e0);
+    const double den =
+        (((((((2.04426310338993978564e-15 * r + 1.42151175831644588870e-7) * r + 1.84631831751005468180e-5) * r +
+             7.86869131145613259100e-4) * r + 1.48753612908506148525e-2) * r + 1.36929880922735805310e-1) * r +
+          5.99832206555887937690e-1) * r + 1.0);
+    val = num / den;
+  }
+  return q < 0.0 ? -val : val;
+}
+
+__host__ __device__ __forceinline__ double qnorm_fast(double p) {
+  const double y = 2.0 * p - 1.0;
+  const double w = -log_fast(4.0 * p * (1.0 - p));
+  if (w < 6.25) {
+    const double t = w - 3.125;
+    double f = kQnormA[0];
+#pragma unroll
+    for (int k = 1; k < 23; ++k) f = fma_sc(f, t, kQnormA[k]);
+    return y * f;
+  }
+  if (w < 16.0) {
+    const double t = sqrt(w) - 3.25;
+    double f = kQnormB[0];
+#pragma unroll
+    for (int k = 1; k < 19; ++k) f = fma_sc(f, t, kQnormB[k]);
+    return y * f;
+  }
+  return qnorm_as241_tail(p);
+}
+
+// Standard normal truncated to [alpha, +inf) by inversion of the upper tail:
+//   x = Phic^-1(u Phic(alpha)) = -Phi^-1(u * 0.5 erfc(alpha / sqrt 2)),
+// with the exponential tail expansion beyond alpha > 25 (u Phic(alpha) < 1e-138 there).
+// alpha = -inf (NA cells, R/updateZ.R:92) gives p = u: an untruncated normal.
+__host__ __device__ __forceinline__ double trunc_normal_lower(double alpha, double u) {
+  if (alpha > 25.0) return alpha - log_fast(u) / alpha;
+  const double p = u * (0.5 * erfc_fast(alpha * 0.7071067811865476));
+  return -qnorm_fast(p);
 }
 
 }  // namespace hmsc

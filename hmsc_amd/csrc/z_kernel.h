@@ -1,0 +1,277 @@
+// updateZ device kernel (R/updateZ.R:4-94), shared by kernels.hip and the microbenchmark
+// scripts/ubench_z.hip.  See kernels.hip for the launcher (run_z_fused).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rng.h"
+
+namespace hmsc {
+
+// ---------------------------------------------------------------------------
+// updateZ (R/updateZ.R:4-94) fused with the contractions of Z the next sweep needs.
+//
+// A workgroup (4 waves) owns 32 species (sBL in LDS) and a chunk of 64-site tiles;
+// wave w takes the 16-site sub-tile w of every tile, and the waves never synchronise
+// inside the site loop.  Per 16-site x 32-species wave tile, all in registers:
+//   E    = XEta BL          v_mfma_f64_16x16x4 (A = XEta rows, B = BL columns); the
+//                           accumulator leaves lane l holding sites lk+4r (r=0..3) of
+//                           species pair m = l&15, i.e. species j0+2m and j0+2m+1
+//   Z    truncated-normal draws (VALU); one Philox call feeds the species pair
+//   XZ  += XEta^T (Yx o Z)  the drawn Z already sits in the B-operand layout of this
+//                           MFMA (sites = reduction index), A = XEta^T from a wave-
+//                           private LDS copy of the site tile
+//   ZTr  = Z Tr             DPP row reductions over the 16 species pairs
+// so Z is written once and never re-read by updateBetaLambda or updateGamma2.
+// ---------------------------------------------------------------------------
+struct ZArgs {
+  const double* XEta;  // ny x K (ld ny)
+  int ny, K, ns_loc, sp0, nt, tiles_per_chunk;
+  const double* BL;
+  const double* iSigma;
+  const int8_t* Ycode;
+  const double* Yval;
+  const int* fam;
+  const double* Tr;  // local species rows, ld ns_loc
+  double* Z;
+  double* XZ_part;   // [chunk][K x ns_loc]
+  double* ZTr_part;  // [species block][ny x nt]
+  Key key;
+  uint32_t iter;
+  int noise_zero;
+};
+
+constexpr int ZT_I = 64;   // sites per workgroup tile (4 waves x 16)
+constexpr int ZT_J = 32;   // species per workgroup (16 pairs)
+constexpr int KMAX_Z = 64;
+constexpr int ZT_LD = 65;  // padded LDS leading dimension of the 64-site XEta tile (xeta_gram_kernel)
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// v_mfma_f64_16x16x4_f64: D[16x16] += A[16x4] B[4x16]; lane l supplies A[l&15][l>>4] and
+// B[l>>4][l&15] and holds D[(l>>4) + 4r][l&15], r = 0..3 (checked by scripts/mfma_layout_check.hip).
+__device__ __forceinline__ d4 mfma_f64(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// LDS written by one lane of a wave and read by another lane of the same wave
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// v rotated right by N lanes inside each row of 16 lanes (DPP row_ror)
+template <int N>
+__device__ __forceinline__ double row_ror(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x120 + N, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x120 + N, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double row_sum16(double v) {
+  v += row_ror<8>(v);
+  v += row_ror<4>(v);
+  v += row_ror<2>(v);
+  v += row_ror<1>(v);
+  return v;
+}
+
+// one latent draw, out of line: the ~100 polynomial constants of erfc / qnorm / log are
+// then materialised inside the call instead of being hoisted into the kernel's register
+// file (which would cut the z kernel to one wave per SIMD); called from a rolled loop so
+// only the loop state is live across the call.
+//   code 1 / 0: probit TN(E, sd) on [0, inf) / (-inf, 0]     R/updateZ.R:43-63
+//   code < 0 : NA cell, N(E, sd) = truncation at -inf           R/updateZ.R:92
+__device__ __noinline__ double z_probit_draw(double e, double sd, double isd, int code, double u, int noise_zero) {
+  const double sg = code == 0 ? -1.0 : 1.0;
+  if (code < 0 && noise_zero) return e;
+  const double alpha = code < 0 ? -INFINITY : -sg * e * isd;
+  return e + sd * sg * trunc_normal_lower(alpha, u);
+}
+
+// NKB = 16-row blocks of K (XZ output tiles per species block)
+// MODE bits (all set in the product; the microbenchmark clears them to cost each part):
+//   1 = E on the matrix cores, 2 = draws, 4 = XZ contraction, 8 = ZTr contraction
+constexpr int Z_ALL = 15;
+constexpr int ZT_TLD = 17;  // leading dimension of the wave's 16-site x 32-species tile T[jj][site]
+
+template <bool DRAW, bool HAS_NA, int NKB, int MODE = Z_ALL>
+__global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  constexpr int K16 = 16 * NKB;
+  const int K = a.K, K4 = (K + 3) & ~3;
+  const int ny = a.ny;
+  double* sBL = smem;                               // [K16][32], column jj = species j0 + jj
+  double* sTr = sBL + K16 * ZT_J;                   // [t][32]
+  double* sSd = sTr + ZT_J * a.nt;                  // [32] iSigma^-1/2
+  double* sIsd = sSd + ZT_J;                        // [32] iSigma^1/2
+  int* sFam = (int*)(sIsd + ZT_J);                  // [32]
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, lm = lane & 15, lk = lane >> 4;
+  double* sT = (double*)(sFam + ZT_J) + w * (ZT_J * ZT_TLD);  // this wave's tile: E, then Z
+  const int j0 = blockIdx.y * ZT_J;
+  for (int p = t; p < K16 * ZT_J; p += 256) {
+    const int k = p >> 5, jj = p & 31, j = j0 + jj;
+    sBL[p] = (k < K && j < a.ns_loc) ? a.BL[k + (size_t)K * j] : 0.0;
+  }
+  for (int p = t; p < ZT_J * a.nt; p += 256) {
+    const int jj = p & 31, tt = p >> 5, j = j0 + jj;
+    sTr[p] = (j < a.ns_loc) ? a.Tr[j + (size_t)a.ns_loc * tt] : 0.0;
+  }
+  if (t < ZT_J) {
+    const int j = j0 + t;
+    const double is = (j < a.ns_loc) ? a.iSigma[j] : 1.0;
+    sSd[t] = 1.0 / sqrt(is);
+    sIsd[t] = sqrt(is);
+    sFam[t] = (j < a.ns_loc) ? a.fam[j] : 0;
+  }
+  __syncthreads();
+
+  d4 acc[NKB][2];
+#pragma unroll
+  for (int q = 0; q < NKB; ++q) acc[q][0] = acc[q][1] = d4{0.0, 0.0, 0.0, 0.0};
+
+  const int n_tiles = (ny + ZT_I - 1) / ZT_I;
+  const int tb = blockIdx.x * a.tiles_per_chunk;
+  const int te = min(n_tiles, tb + a.tiles_per_chunk);
+  for (int tile = tb; tile < te; ++tile) {
+    const int i0 = tile * ZT_I + 16 * w;
+    if (i0 >= ny) break;
+    // ---- E = XEta BL for 16 sites x 32 species (R/updateZ.R:11-34); T[2m+b][lk+4r] <- E
+    if (DRAW) {
+      d4 e0 = {0.0, 0.0, 0.0, 0.0}, e1 = {0.0, 0.0, 0.0, 0.0};
+      const int i = i0 + lm;
+#pragma unroll
+      for (int s4 = 0; s4 < K16 / 4; ++s4)
+        if (s4 < K4 / 4) {
+          const int k = 4 * s4 + lk;
+          const double xa = (k < K && i < ny) ? a.XEta[i + (size_t)ny * k] : 0.0;
+          if (MODE & 1) {
+            e0 = mfma_f64(xa, sBL[k * ZT_J + 2 * lm], e0);
+            e1 = mfma_f64(xa, sBL[k * ZT_J + 2 * lm + 1], e1);
+          } else {
+            e0[s4 & 3] += xa;
+          }
+        }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sT[(2 * lm) * ZT_TLD + lk + 4 * r] = e0[r];
+        sT[(2 * lm + 1) * ZT_TLD + lk + 4 * r] = e1[r];
+      }
+      wave_lds_sync();
+    }
+    // ---- draws in coalesced order: lane = site s (16 consecutive) x species pair m = 4c + lk;
+    //      one Philox call per (site, pair); Z stores are 128-B site runs
+    {
+      const int s = lm, i = i0 + s;
+#pragma unroll 1
+      for (int c = 0; c < 4; ++c) {
+        const int m = 4 * c + lk, ja = j0 + 2 * m;
+        Uniform2 u{0.0, 0.0};
+        if (DRAW) u = uniforms(a.key, (uint32_t)((size_t)i + (size_t)ny * (uint32_t)((a.sp0 + ja) >> 1)), 0, S_Z, a.iter);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int jj = 2 * m + b, j = ja + b;
+          double z = 0.0;
+          if (i < ny && j < a.ns_loc) {
+            const size_t cell = (size_t)i + (size_t)ny * j;
+            if (DRAW) {
+              const int code = a.Ycode[cell];
+              const double e = sT[jj * ZT_TLD + s];
+              if (sFam[jj] == 1 && code >= 0)
+                z = a.Yval[cell];  // normal: Z = Y   R/updateZ.R:40-41
+              else if (MODE & 2)
+                z = z_probit_draw(e, sSd[jj], sIsd[jj], code, b ? u.b : u.a, a.noise_zero);
+              else
+                z = e + (b ? u.b : u.a);
+              a.Z[cell] = z;
+            } else {
+              z = a.Z[cell];
+            }
+          }
+          sT[jj * ZT_TLD + s] = z;
+        }
+      }
+    }
+    // ---- ZTr partial of this species block for the 16 sites   (R/updateGamma2.R:46)
+    if (MODE & 8) {
+      for (int tt = 0; tt < a.nt; ++tt) {
+        const double* tr = sTr + tt * ZT_J;
+        double v = 0.0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int m = 4 * c + lk;
+          v = fma(sT[(2 * m) * ZT_TLD + lm], tr[2 * m], v);
+          v = fma(sT[(2 * m + 1) * ZT_TLD + lm], tr[2 * m + 1], v);
+        }
+        v += __shfl_xor(v, 16);
+        v += __shfl_xor(v, 32);
+        const int i = i0 + lm;
+        if (lk == 0 && i < ny) a.ZTr_part[(size_t)blockIdx.y * ny * a.nt + i + (size_t)ny * tt] = v;
+      }
+    }
+    wave_lds_sync();
+    // ---- XZ += XEta^T (Yx o Z) over the 16 sites (R/updateBetaLambda.R:66 of the next sweep);
+    //      B operand = Z[site lk+4r][species 2lm+b] from the tile
+    if (MODE & 4) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ir = i0 + 4 * r + lk;
+        double z0 = sT[(2 * lm) * ZT_TLD + lk + 4 * r];
+        double z1 = sT[(2 * lm + 1) * ZT_TLD + lk + 4 * r];
+        if (HAS_NA && ir < ny) {
+          const int ja = j0 + 2 * lm;
+          if (ja < a.ns_loc && a.Ycode[(size_t)ir + (size_t)ny * ja] < 0) z0 = 0.0;
+          if (ja + 1 < a.ns_loc && a.Ycode[(size_t)ir + (size_t)ny * (ja + 1)] < 0) z1 = 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < NKB; ++q) {
+          const int k = 16 * q + lm;
+          const double xt = (k < K && ir < ny) ? a.XEta[ir + (size_t)ny * k] : 0.0;
+          acc[q][0] = mfma_f64(xt, z0, acc[q][0]);
+          acc[q][1] = mfma_f64(xt, z1, acc[q][1]);
+        }
+      }
+    }
+    wave_lds_sync();
+  }
+  // combine the 4 waves' XZ and write this chunk's partial
+  __syncthreads();
+  double* sR = smem;  // [w-1][K16][32] (reuses the whole workgroup's LDS)
+  if (w > 0) {
+#pragma unroll
+    for (int q = 0; q < NKB; ++q)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          sR[((w - 1) * K16 + 16 * q + lk + 4 * rr) * ZT_J + 2 * lm + b] = acc[q][b][rr];
+  }
+  __syncthreads();
+  if (w == 0) {
+    double* dst = a.XZ_part + (size_t)blockIdx.x * K * a.ns_loc;
+#pragma unroll
+    for (int q = 0; q < NKB; ++q)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int k = 16 * q + lk + 4 * rr, jj = 2 * lm + b, j = j0 + jj;
+          const double v = acc[q][b][rr] + sR[(0 * K16 + k) * ZT_J + jj] + sR[(1 * K16 + k) * ZT_J + jj] +
+                           sR[(2 * K16 + k) * ZT_J + jj];
+          if (k < K && j < a.ns_loc) dst[k + (size_t)K * j] = v;
+        }
+  }
+}
+
+// launch geometry shared by the launcher and the microbenchmark
+inline int z_nkb(int K) { return (K + 15) / 16; }
+
+inline size_t z_smem_bytes(int K, int nt) {
+  const size_t K16 = 16 * (size_t)z_nkb(K);
+  const size_t body = K16 * ZT_J + (size_t)ZT_J * nt + 2 * ZT_J + ZT_J / 2 + 4 * (size_t)ZT_J * ZT_TLD;  // doubles
+  const size_t red = 3 * K16 * ZT_J;                                                                   // wave combine
+  return (body > red ? body : red) * sizeof(double);
+}
+
+}  // namespace hmsc

@@ -99,7 +99,7 @@ class Chain:
                                          C.byref(h)))
         self.h = h
         self.rank, self.nranks = rank, nranks
-        per = -(-hM.ns // nranks)
+        per = ((-(-hM.ns // nranks)) + 1) & ~1   # even shard starts (capi.cpp: Philox species pairs)
         self.sp0 = min(hM.ns, rank * per)
         self.nsl = min(hM.ns, self.sp0 + per) - self.sp0
 

@@ -101,7 +101,10 @@ def update_z(st, model, rng, it, Y=None):
     ny, ns = Y.shape
     E = linear_predictor(st, model)
     sd = st["iSigma"] ** -0.5
-    idx = (np.arange(ny)[:, None] + ny * np.arange(ns)[None, :]).astype(np.uint64)
+    # one Philox block per (site, species pair (2m, 2m+1)); species 2m takes the first
+    # uniform, 2m+1 the second (rng.h contract, z_wave_kernel)
+    j = np.arange(ns)
+    idx = (np.arange(ny)[:, None] + ny * (j[None, :] >> 1)).astype(np.uint64)
     fam = model["distr"][:, 0]
     if np.any(fam == 3):
         raise NotImplementedError("Poisson updateZ (Polya-Gamma) is a 'next' row (SURVEY.md §8 f3)")
@@ -109,15 +112,16 @@ def update_z(st, model, rng, it, Y=None):
     Z = np.empty((ny, ns))
     normal_cols = fam == 1
     Z[:, normal_cols] = Y[:, normal_cols]
-    u = rng.uniforms(idx, 0, R.S_Z, it)[0]
+    ua, ub = rng.uniforms(idx, 0, R.S_Z, it)
+    u = np.where((j & 1)[None, :] == 1, ub, ua)
     s = np.where(Y == 1, 1.0, -1.0)
     alpha = -s * E / sd[None, :]
     w = R.trunc_normal_lower(alpha, u)
     zp = E + sd[None, :] * s * w
     probit_cols = fam == 2
     Z[:, probit_cols] = zp[:, probit_cols]
-    if na.any():
-        nz = E + sd[None, :] * rng.normal(idx, 0, R.S_Z, it)
+    if na.any():   # R/updateZ.R:92: N(E, sd), drawn by inversion of the same uniform
+        nz = E - sd[None, :] * R.qnorm_as241(u.ravel()).reshape(u.shape)
         Z[na] = nz[na]
     return Z
 

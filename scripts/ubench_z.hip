@@ -1,0 +1,86 @@
+// Microbenchmark of the fused updateZ kernel (hmsc_amd/csrc/z_kernel.h) at the synthetic
+// shape ny=10000, ns=1000, K=30, with parts switched off (MODE bits) to cost each of them.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+#include <algorithm>
+#include <cmath>
+#include "../hmsc_amd/csrc/z_kernel.h"
+using namespace hmsc;
+
+template <int MODE>
+float run(const ZArgs& a, dim3 grid, size_t smem, int reps) {
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  z_wave_kernel<true, false, 2, MODE><<<grid, 256, smem>>>(a);
+  (void)hipDeviceSynchronize();
+  (void)hipEventRecord(e0);
+  for (int i = 0; i < reps; ++i) z_wave_kernel<true, false, 2, MODE><<<grid, 256, smem>>>(a);
+  (void)hipEventRecord(e1);
+  (void)hipEventSynchronize(e1);
+  float ms;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  return 1e3f * ms / reps;
+}
+
+int main() {
+  const int ny = 10000, ns = 1000, K = 30, nt = 1;
+  std::vector<double> hX((size_t)ny * K), hBL((size_t)K * ns), hTr(ns, 1.0), hIs(ns, 1.0);
+  std::vector<int8_t> hY((size_t)ny * ns);
+  std::vector<int> hF(ns, 2);
+  unsigned s = 1;
+  auto rnd = [&] { s = s * 1664525u + 1013904223u; return ((s >> 8) * (1.0 / 16777216.0)) - 0.5; };
+  // like the synthetic probit chain: E = XEta BL with sd ~3, Y = 1[E + N(0,1) > 0]
+  auto nrm = [&] { double t = 0; for (int q = 0; q < 12; ++q) t += rnd(); return t; };
+  for (auto& v : hX) v = nrm();
+  for (auto& v : hBL) v = 0.55 * nrm();
+  for (int j = 0; j < ns; ++j)
+    for (int i = 0; i < ny; ++i) {
+      double e = 0;
+      for (int k = 0; k < K; ++k) e += hX[i + (size_t)ny * k] * hBL[k + (size_t)K * j];
+      hY[i + (size_t)ny * j] = (e + nrm() > 0) ? 1 : 0;
+    }
+  double *X, *BL, *Tr, *Is, *Z, *XZp, *ZTrp;
+  int8_t* Y;
+  int* F;
+  const int ntile_j = (ns + 31) / 32, n_tiles = (ny + 63) / 64;
+  (void)hipMalloc(&X, hX.size() * 8);
+  (void)hipMalloc(&BL, hBL.size() * 8);
+  (void)hipMalloc(&Tr, ns * 8);
+  (void)hipMalloc(&Is, ns * 8);
+  (void)hipMalloc(&Z, (size_t)ny * ns * 8);
+  (void)hipMalloc(&Y, (size_t)ny * ns);
+  (void)hipMalloc(&F, ns * 4);
+  (void)hipMalloc(&XZp, (size_t)n_tiles * K * ns * 8);
+  (void)hipMalloc(&ZTrp, (size_t)ntile_j * ny * 8);
+  (void)hipMemcpy(X, hX.data(), hX.size() * 8, hipMemcpyHostToDevice);
+  (void)hipMemcpy(BL, hBL.data(), hBL.size() * 8, hipMemcpyHostToDevice);
+  (void)hipMemcpy(Tr, hTr.data(), ns * 8, hipMemcpyHostToDevice);
+  (void)hipMemcpy(Is, hIs.data(), ns * 8, hipMemcpyHostToDevice);
+  (void)hipMemcpy(Y, hY.data(), hY.size(), hipMemcpyHostToDevice);
+  (void)hipMemcpy(F, hF.data(), ns * 4, hipMemcpyHostToDevice);
+  const size_t smem = z_smem_bytes(K, nt);
+  int nb = 0, ncu = 0;
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, false, 2, Z_ALL>, 256, smem);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
+  printf("occupancy %d blocks/CU, %d CUs, smem %zu B\n", nb, ncu, smem);
+  for (int nchunk_req : {nb * ncu / ntile_j, 2 * nb * ncu / ntile_j, n_tiles}) {
+    ZArgs a{};
+    a.XEta = X; a.ny = ny; a.K = K; a.ns_loc = ns; a.sp0 = 0; a.nt = nt;
+    a.tiles_per_chunk = (n_tiles + nchunk_req - 1) / nchunk_req;
+    const int nchunk = (n_tiles + a.tiles_per_chunk - 1) / a.tiles_per_chunk;
+    a.BL = BL; a.iSigma = Is; a.Ycode = Y; a.Yval = nullptr; a.fam = F; a.Tr = Tr; a.Z = Z;
+    a.XZ_part = XZp; a.ZTr_part = ZTrp; a.key = Key{7u, 9u}; a.iter = 3; a.noise_zero = 0;
+    dim3 grid(nchunk, ntile_j);
+    printf("grid %d x %d (tiles/chunk %d)\n", nchunk, ntile_j, a.tiles_per_chunk);
+    printf("  all                 %7.1f us\n", run<15>(a, grid, smem, 20));
+    printf("  no E mfma           %7.1f us\n", run<14>(a, grid, smem, 20));
+    printf("  no draw             %7.1f us\n", run<13>(a, grid, smem, 20));
+    printf("  no XZ               %7.1f us\n", run<11>(a, grid, smem, 20));
+    printf("  no ZTr              %7.1f us\n", run<7>(a, grid, smem, 20));
+    printf("  draw only (E VALU)  %7.1f us\n", run<2>(a, grid, smem, 20));
+    printf("  nothing             %7.1f us\n", run<0>(a, grid, smem, 20));
+  }
+  return 0;
+}

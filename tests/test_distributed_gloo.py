@@ -5,7 +5,7 @@ splits species into contiguous blocks and all-reduces, once per updater, the
 species-sums that couple the shards.  Here each rank computes its block's share of
 those sums with the oracle's formulas and a gloo all_reduce must reproduce the
 unsharded values — the same decomposition and block arithmetic the C library uses
-(capi.cpp build_state: per = ceil(ns / nranks)).  Chains mode needs no exchange;
+(capi.cpp build_state: per = ceil(ns / nranks) rounded up to even).  Chains mode needs no exchange;
 its timing reduction (max over ranks) is checked too.
 """
 import os
@@ -30,7 +30,7 @@ def _free_port():
 
 
 def species_block(ns, rank, nranks):
-    per = -(-ns // nranks)
+    per = ((-(-ns // nranks)) + 1) & ~1
     a = min(ns, rank * per)
     return a, min(ns, a + per)
 
