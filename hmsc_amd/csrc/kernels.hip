@@ -1,13 +1,13 @@
 // HIP kernels for one Gibbs sweep of Hmsc's sampleMcmc (R/sampleMcmc.R:219-306) on gfx950.
 //
 // Dataflow (per sweep, synthetic config ny=10k ns=1k nc=20 nf=10):
-//   updateZ      z_fused_kernel   E = XEta*BL on the fly, truncated-normal draw, stores Z,
-//                                 and, while the Z tile is still on chip, the three linear
-//                                 contractions of Z the next sweep needs:
+//   updateZ      z_wave_kernel    (z_kernel.h) E = XEta*BL on the matrix cores, truncated-
+//                                 normal draw, stores Z, and, while the Z tile is still on
+//                                 chip, the contractions of Z the next sweep needs:
 //                                   XZ  = XEta^T (Yx o Z)   (updateBetaLambda, R/updateBetaLambda.R:66)
-//                                   G   = XEta^T XEta       (R/updateBetaLambda.R:65)
 //                                   ZTr = Z Tr              (updateGamma2, R/updateGamma2.R:46)
-//                                 so updateBetaLambda never re-reads Z from HBM.
+//                                 so updateBetaLambda never re-reads Z from HBM
+//                xeta_gram_kernel G = XEta^T XEta (R/updateBetaLambda.R:65), once per Eta update.
 //   updateBetaLambda  beta_lambda_kernel  one wave per species: K x K precision in LDS,
 //                                 Cholesky, two triangular solves, draw.
 //   updateGammaV / updateGamma2 / updateLambdaPriors: species-parallel partial reductions
