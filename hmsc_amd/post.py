@@ -239,3 +239,72 @@ def computeWAIC(hM, ghN=11):
     Bl = -np.log(np.mean(np.exp(val), axis=0))
     Vv = val.var(axis=0, ddof=1)
     return float(np.mean(Bl + Vv))
+
+
+def computeVariancePartitioning(hM, group=None, groupnames=None, start=1):
+    """R/computeVariancePartitioning.R:37-204 (X a matrix, na.ignore=FALSE).
+
+    Reproduces the reference's loop ``for (i in 1:hM$samples)`` over the *pooled* list
+    (:125), i.e. with nChains > 1 only the first chain's samples enter (SURVEY.md
+    Appendix B quirk 4).  Returns dict(vals (ngroups+nr, ns), R2T=dict(Beta, Y), group,
+    groupnames, rownames).
+    """
+    ns, nc, nr = hM.ns, hM.nc, hM.nr
+    if group is None:                                                      # :42-51
+        if nc > 1:
+            group = np.r_[1, np.arange(1, nc)]
+            groupnames = list(hM.covNames[1:nc])
+        else:
+            group = np.array([1])
+            groupnames = [hM.covNames[0]]
+    group = np.asarray(group)
+    ngroups = int(group.max())
+    X, Tr = hM.X, hM.Tr
+    cM = np.cov(X, rowvar=False).reshape(nc, nc)                           # :66
+    post = poolMcmcChains(hM.postList, start=start)
+    S = hM.samples
+    fixed = np.zeros(ns)
+    fixedsplit = np.zeros((ns, ngroups))
+    random = np.zeros((ns, nr))
+    R2T_Y = 0.0
+    R2T_Beta = np.zeros(nc)
+    for i in range(S):                                                     # :125
+        s = post[i]
+        Beta = s["Beta"]
+        mu = (Tr @ s["Gamma"].T).T                                         # gemu :100-103
+        for k in range(nc):                                                # :126-128
+            R2T_Beta[k] += np.corrcoef(Beta[k], mu[k])[0, 1] ** 2
+        f = X @ Beta                                                       # getf :87-97
+        a = X @ mu                                                         # geta :75-84
+        a = a - a.mean(axis=1, keepdims=True)
+        f = f - f.mean(axis=1, keepdims=True)
+        res1 = np.sum((np.sum(a * f, axis=1) / (ns - 1)) ** 2)            # :139-141
+        res2 = np.sum((np.sum(a * a, axis=1) / (ns - 1)) * (np.sum(f * f, axis=1) / (ns - 1)))
+        R2T_Y += res1 / res2
+        fixed1 = np.einsum("kj,kl,lj->j", Beta, cM, Beta)                  # :142-146
+        fixedsplit1 = np.zeros((ns, ngroups))
+        for g in range(1, ngroups + 1):                                    # :147-151
+            sel = group == g
+            fixedsplit1[:, g - 1] = np.einsum("kj,kl,lj->j", Beta[sel], cM[np.ix_(sel, sel)], Beta[sel])
+        random1 = np.zeros((ns, nr))
+        for r in range(nr):                                                # :154-160
+            lam = s["Lambda"][r]
+            random1[:, r] = np.sum(lam * lam, axis=0)
+        if nr > 0:                                                         # :161-170
+            tot = fixed1 + random1.sum(axis=1)
+            fixed += fixed1 / tot
+            random += random1 / tot[:, None]
+        else:
+            fixed += 1.0
+        fixedsplit += fixedsplit1 / fixedsplit1.sum(axis=1, keepdims=True)  # :171-173
+    fixed /= S
+    random /= S
+    fixedsplit /= S
+    vals = np.zeros((ngroups + nr, ns))                                    # :180-187
+    for g in range(ngroups):
+        vals[g] = fixed * fixedsplit[:, g]
+    for r in range(nr):
+        vals[ngroups + r] = random[:, r]
+    rl = list(getattr(hM, "rLNames", None) or [f"level{r + 1}" for r in range(nr)])
+    return dict(vals=vals, R2T=dict(Beta=R2T_Beta / S, Y=R2T_Y / S), group=group, groupnames=groupnames,
+                rownames=list(groupnames) + [f"Random: {n}" for n in rl])

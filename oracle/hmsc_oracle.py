@@ -357,23 +357,25 @@ def eta_unit_moments(st, model, r, S):
     npr = st["Eta"][r].shape[0]
     Yx = ~np.isnan(Y)
     LamInvSigLam = (lam * iS[None, :]) @ lam.T                         # :45
-    precs = np.empty((npr, nf, nf))
-    means = np.empty((npr, nf))
     lamT = (lam * iS[None, :]).T                                       # lambda*iSigma, transposed
-    for q in range(npr):
-        rows = np.nonzero(Pi_r == q)[0]
-        if Yx[rows].all():                                             # :46-57 and :75-79
-            Q = np.eye(nf) + LamInvSigLam * len(rows)
-            b = S[rows].sum(axis=0) @ lamT
-        else:                                                          # :59-70 and :80-87
-            Q = np.eye(nf)
-            b = np.zeros(nf)
-            for p in rows:
-                w = iS * Yx[p]
-                Q = Q + (lam * w[None, :]) @ lam.T
-                b = b + (np.where(Yx[p], S[p], 0.0) * iS) @ lam.T
+    # units whose rows are all observed share Q = I + n_q LamInvSigLam   (:46-57, :75-79)
+    n_q = np.bincount(Pi_r, minlength=npr).astype(np.float64)
+    Ssum = np.zeros((npr, S.shape[1]))
+    np.add.at(Ssum, Pi_r, S)
+    precs = np.eye(nf)[None, :, :] + LamInvSigLam[None, :, :] * n_q[:, None, None]
+    bs = Ssum @ lamT
+    has_na = np.zeros(npr, dtype=bool)
+    np.logical_or.at(has_na, Pi_r, ~Yx.all(axis=1))
+    for q in np.nonzero(has_na)[0]:                                    # :59-70 and :80-87
+        Q = np.eye(nf)
+        b = np.zeros(nf)
+        for p in np.nonzero(Pi_r == q)[0]:
+            w = iS * Yx[p]
+            Q = Q + (lam * w[None, :]) @ lam.T
+            b = b + (np.where(Yx[p], S[p], 0.0) * iS) @ lam.T
         precs[q] = Q
-        means[q] = np.linalg.solve(Q, b)
+        bs[q] = b
+    means = np.linalg.solve(precs, bs[:, :, None])[:, :, 0]
     return precs, means
 
 
@@ -392,12 +394,12 @@ def update_eta(st, model, rng, it, zero_noise=False):
         st["Eta"] = Eta
         precs, means = eta_unit_moments(st, model, r, S)
         npr, nf = means.shape
-        eta = np.empty((npr, nf))
-        for q in range(npr):
-            RiV = chol_upper(precs[q])
-            xi = np.zeros(nf) if zero_noise else rng.normal(q, np.arange(nf), R.S_ETA + R.LEVEL_STRIDE * r, it)
-            eta[q] = means[q] + backsolve(RiV, xi)                     # :56,69,90
-        Eta[r] = eta
+        RiV = np.swapaxes(np.linalg.cholesky(precs), 1, 2)              # chol(): upper R, R'R = Q
+        if zero_noise:
+            xi = np.zeros((npr, nf))
+        else:
+            xi = rng.normal(np.arange(npr)[:, None], np.arange(nf)[None, :], R.S_ETA + R.LEVEL_STRIDE * r, it)
+        Eta[r] = means + np.linalg.solve(RiV, xi[:, :, None])[:, :, 0]  # backsolve(RiV, xi)  :56,69,90
     return Eta
 
 

@@ -156,3 +156,18 @@ def test_effective_size_ar1():
     assert np.all(np.abs(ess / expect - 1) < 0.1)
     point, upper = H.gelman_diag([x[:10000], x[10000:]])
     assert np.all(point < 1.05) and np.all(upper >= point)
+
+
+def test_variance_partitioning_td():
+    """computeVariancePartitioning(TD$m) (the reference's roxygen example,
+    tests/Examples/Hmsc-Ex.Rout.save:181, values not printed there: structure only).
+    Fixed groups + random levels partition each species' explained variance."""
+    hM = td_model()
+    hM.postList = td_postlist(hM)
+    hM.samples = M["n_samples"]
+    VP = H.computeVariancePartitioning(hM)
+    assert VP["vals"].shape == (hM.nc - 1 + hM.nr, hM.ns)
+    np.testing.assert_allclose(VP["vals"].sum(axis=0), 1.0, atol=1e-12)
+    assert np.all(VP["vals"] >= 0)
+    assert np.all((VP["R2T"]["Beta"] >= 0) & (VP["R2T"]["Beta"] <= 1)) and 0 <= VP["R2T"]["Y"] <= 1
+    assert VP["rownames"][-2:] == ["Random: sample", "Random: plot"]
