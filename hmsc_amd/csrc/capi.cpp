@@ -354,13 +354,14 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.G = dalloc<double>((size_t)s.Kmax * s.Kmax);
   s.ZTr = dalloc<double>((size_t)ny * nt);
   s.XZ_part = dalloc<double>((size_t)s.nchunk * s.Kmax * nsl);
-  s.G_part = dalloc<double>((size_t)std::max(std::max(s.nchunk, 64), n_tiles) * s.Kmax * s.Kmax);
+  s.G_part = dalloc<double>((size_t)std::max(std::max(s.nchunk, 64), (ny + 31) / 32) * s.Kmax * s.Kmax);
   s.ZTr_part = dalloc<double>((size_t)s.ntile_j * ny * nt);
   const int nfm = std::max(1, s.NFmax);
   s.ZL = dalloc<double>((size_t)ny * nfm);
   s.ZL_part = dalloc<double>((size_t)s.zl_split * ny * nfm);
   s.CR = dalloc<double>((size_t)s.Kmax * nfm);
   s.CR_part = dalloc<double>((size_t)((nsl + 31) / 32) * s.Kmax * nfm);
+  s.LS = dalloc<double>((size_t)nfm * nsl);
   s.scratch_doubles = 1 << 20;
   s.scratch = dalloc<double>(s.scratch_doubles);
   s.scratch2 = dalloc<double>(s.scratch_doubles);
@@ -378,7 +379,7 @@ static void free_state(State& s) {
                   s.aSigma, s.bSigma, s.XX, s.TT, s.V0g, s.V0gXXV0g, s.iV0, s.V0inv, s.iUmG, s.V0gXX, s.g2prep, s.scratch2, s.na_cols, s.na_index,
                   s.na_rows, s.row_na, s.row_slot, s.dev_flags, s.Z, s.XEta, s.BL, s.Psi, s.Delta, s.Gamma, s.iV,
                   s.iSigma, s.rho, s.XZ, s.G, s.ZTr, s.XZ_part, s.G_part, s.ZTr_part, s.Gna, s.ZL, s.ZL_part,
-                  s.CR, s.CR_part, s.Msmall, s.scratch, s.psi_rs, s.ABpart, s.dbg_prec, s.ring, s.allreduce_buf};
+                  s.CR, s.CR_part, s.LS, s.Msmall, s.scratch, s.psi_rs, s.ABpart, s.dbg_prec, s.ring, s.allreduce_buf};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (int r = 0; r < s.nr; ++r) {
@@ -975,7 +976,10 @@ int hmsc_debug_get(hmsc_state* h, const char* name, double* out, int64_t n) {
     else if (nm == "BL_prec") src = s.dbg_prec, avail = s.dbg_prec ? (int64_t)s.nsl * s.K * s.K : 0;
     else if (nm == "CR") src = s.CR, avail = (int64_t)s.Kmax * s.NFmax;
     else if (nm == "ZL") src = s.ZL_part, avail = (int64_t)s.zl_split * s.ny * s.NF;
-    else if (nm == "dims") {
+    else if (nm == "stamps") {
+      read_stamps(out, (int)n);
+      return;
+    } else if (nm == "dims") {
       HMSC_REQUIRE(n >= 8, "dims needs 8 slots");
       const double d[8] = {(double)s.K, (double)s.NF, (double)s.Kmax, (double)s.NFmax, (double)s.nchunk,
                            (double)s.ntile_j, (double)s.zl_split, (double)s.zt_valid};

@@ -28,6 +28,26 @@ struct HmscError : std::runtime_error {
 
 constexpr int WAVE = 64;
 
+// Diagnostic build only (python -m hmsc_amd.build --stamps -> libhmsc_amd_stamps.so):
+// HMSC_STAMP(i) records the shader clock (s_memtime) of lane 0 of the calling workgroup
+// into slot i of a device table read back with hmsc_debug_get(s, "stamps", ...).  The
+// product build compiles it away.
+#ifdef HMSC_STAMPS
+extern __device__ unsigned long long g_stamps[256];
+#define HMSC_STAMP(i)                                                              \
+  do {                                                                             \
+    unsigned long long t_;                                                         \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");    \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    if (threadIdx.x == 0) g_stamps[(i)] = t_;                                      \
+  } while (0)
+#else
+#define HMSC_STAMP(i) \
+  do {                \
+  } while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // Single-workgroup dense linear algebra on small column-major matrices
 // (n <= 64).  All threads of the workgroup call these together; the matrices

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "common.h"
@@ -29,6 +30,28 @@
 #include "z_kernel.h"
 
 namespace hmsc {
+
+#ifdef HMSC_STAMPS
+__device__ unsigned long long g_stamps[256];
+#endif
+
+static bool getenv_flag(const char* name) {
+  const char* v = getenv(name);
+  return v && v[0] && v[0] != '0';
+}
+
+void read_stamps(double* out, int n) {
+#ifdef HMSC_STAMPS
+  unsigned long long h[256];
+  HMSC_REQUIRE(n <= 256, "stamps: at most 256 slots");
+  HIP_OK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_stamps), sizeof(h)));
+  for (int i = 0; i < n; ++i) out[i] = (double)h[i];
+#else
+  (void)out;
+  (void)n;
+  throw HmscError(-1, "stamps: this library was built without --stamps");
+#endif
+}
 
 // ---------------------------------------------------------------------------
 // XEta row gather: XEta[i, k] = X[i, k] (k < nc) or Eta_r[Pi_r[i], h]
@@ -651,6 +674,7 @@ __global__ __launch_bounds__(256) void gammav_wave_kernel(GVWArgs a) {
   double* sA = T0;
   const int nc = a.nc, nt = a.nt, N = nc * nt, t = threadIdx.x;
   const int nA = nc * nc, nB = nc * nt;
+  HMSC_STAMP(0);
   for (int p = t; p < nA + nB; p += blockDim.x) {
     double sum = 0.0;
 #pragma unroll 8
@@ -660,7 +684,26 @@ __global__ __launch_bounds__(256) void gammav_wave_kernel(GVWArgs a) {
     else
       sBTr[p - nA] = sum;     // B Tr
   }
+  // Bartlett factor Zb of rwish (MCMCpack: diag sqrt(chisq(v - i)), upper N(0,1)), drawn by
+  // all 256 threads at once before wave 0 takes over: T3 = Zb padded with I to 32 x 32
+  {
+    const double v = a.f0 + a.ns_glob;
+    for (int p = t; p < 32 * 32; p += blockDim.x) {
+      const int ii = p & 31, k = p >> 5;
+      double zz = (ii == k && ii < NM) ? 1.0 : 0.0;
+      if (ii < nc && k < nc) {
+        if (k == ii)
+          zz = sqrt(2.0 * gamma_std(a.key, (uint32_t)ii, S_WISHART_DIAG, a.iter, 0.5 * (v - ii)));
+        else if (k > ii)
+          zz = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)(ii + nc * k), 0, S_WISHART_OFF, a.iter);
+        else
+          zz = 0.0;
+      }
+      T3[ii + WV_LD * k] = zz;
+    }
+  }
   __syncthreads();
+  HMSC_STAMP(1);
   if (t >= 64) return;
   const int i = lane_id();
   bool ok = true;
@@ -670,25 +713,15 @@ __global__ __launch_bounds__(256) void gammav_wave_kernel(GVWArgs a) {
   ok &= wv_chol<NM>(x, dinv);
   wv_chol2inv<NM>(x, dinv, y, S);
   ok &= wv_chol<NM>(y, dinv);  // y = LV
-  // iV = rwish(f0 + ns, Vn) by Bartlett: Zb upper, iV = (Zb LV^T)^T (Zb LV^T); Zb built in T3
-  const double v = a.f0 + a.ns_glob;
-  for (int k = 0; k < 32; ++k) {
-    double zz = (i == k && i < NM) ? 1.0 : 0.0;
-    if (i < nc && k < nc) {
-      if (k == i)
-        zz = sqrt(2.0 * gamma_std(a.key, (uint32_t)i, S_WISHART_DIAG, a.iter, 0.5 * (v - i)));
-      else if (k > i)
-        zz = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)(i + nc * k), 0, S_WISHART_OFF, a.iter);
-      else
-        zz = 0.0;
-    }
-    if (i < 32) T3[i + WV_LD * k] = zz;
-  }
+  HMSC_STAMP(2);
+  // iV = rwish(f0 + ns, Vn) by Bartlett: Zb upper (T3, drawn above), iV = (Zb LV^T)^T (Zb LV^T)
+  HMSC_STAMP(3);
   wv_to_lds<NM, true, true>(y, S);                    // LV^T
   wv_mm_lds<NM>(T3, S, x, S + WV_TILE);               // x = T = Zb LV^T
   wv_gemm<NM, true, false>(x, x, z, S);               // z = iV = T^T T
   wv_store<NM>(a.iV, nc, nc, z);
   wv_to_lds<NM>(z, T1);                               // T1 = iV
+  HMSC_STAMP(4);
   wv_sync();
   // Gamma | iV: prec = iUGamma + kron(TT, iV), rhs = iUGamma mGamma + vec(iV B Tr)   (:29-31)
   wv_kron<NM>(x, nc, nt, a.TT, 0.0, nullptr, 0, T1, WV_LD, a.iUGamma);
@@ -704,6 +737,7 @@ __global__ __launch_bounds__(256) void gammav_wave_kernel(GVWArgs a) {
   wv_transpose<NM, true>(x, y, S);
   wv_backward_t<NM>(y, dinv, r);
   if (i < N) a.Gamma[i] = r;
+  HMSC_STAMP(5);
   if (!ok && i == 0) a.fail[0] = 1;
   if (!a.do_prep) return;
 
@@ -716,6 +750,7 @@ __global__ __launch_bounds__(256) void gammav_wave_kernel(GVWArgs a) {
   ok2 &= wv_chol<NM>(x, dinv);
   wv_chol2inv<NM>(x, dinv, y, S);                       // y = iP
   wv_to_lds<NM>(y, T2);                                 // T2 = iP
+  HMSC_STAMP(6);
   wv_mm_rt<NM>(z, T2, x, S);                            // x = B1 = iV iP
   wv_store<NM>(a.prep + nA, nc, nc, x);
   wv_mm_rt<NM>(x, T1, y, S);                            // y = iV iP iV
@@ -727,6 +762,7 @@ __global__ __launch_bounds__(256) void gammav_wave_kernel(GVWArgs a) {
   ok2 &= wv_chol<NM>(x, dinv);
   wv_chol2inv<NM>(x, dinv, y, S);                       // y = Rm   (:44)
   wv_to_lds<NM>(y, T0);                                 // T0 = Rm
+  HMSC_STAMP(7);
   wv_load<NM>(a.V0gXX, nc, nc, x);
   wv_mm_rt<NM>(x, T2, z, S);                            // z = T1m = V0 XX iP
   wv_load<NM>(a.V0g, nc, nc, y);
@@ -744,6 +780,7 @@ __global__ __launch_bounds__(256) void gammav_wave_kernel(GVWArgs a) {
   wv_kron<NM>(z, nc, nt, a.TT, 0.0, nullptr, 0, T3, WV_LD, nullptr);  // z = tmp = TT (x) W1   (:48)
   wv_mm_rt<NM>(z, T0, x, S);                            // x = TR = tmp Rm
   wv_store<NM>(a.prep + 2 * nA, N, N, x);
+  HMSC_STAMP(8);
   wv_gemm<NM, false, true>(x, z, y, S);                 // y = tmp Rm tmp^T
   wv_kron<NM>(x, nc, nt, a.TT, 1.0, a.V0g, nc, T2, WV_LD, nullptr);  // x = I (x) V0 + TT (x) M1'
   wv_kron<NM>(z, nc, nt, a.TT, 0.0, nullptr, 0, T2, WV_LD, nullptr); // z = TT (x) M1'
@@ -753,6 +790,7 @@ __global__ __launch_bounds__(256) void gammav_wave_kernel(GVWArgs a) {
   ok2 &= wv_chol<NM>(x, dinv);                          // LSigmaG   (:52)
   wv_store_lower<NM>(a.prep + 2 * nA + N * N, N, N, x);
   if (!ok2 && i == 0) a.fail[1] = 1;
+  HMSC_STAMP(9);
 }
 
 
@@ -987,7 +1025,7 @@ __global__ __launch_bounds__(256) void gamma2_prep_kernel(G2PrepArgs a) {
 }
 
 struct G2Args {
-  int nc, nt, Kmax, NF, nparts, ns_loc, use_xtztr, check_isigma;
+  int nc, nt, Kmax, NF, nparts, ns_loc, use_xtztr, check_isigma, stage;
   const double* part;
   const double* xtztr;
   const double* G;
@@ -1000,8 +1038,12 @@ struct G2Args {
 };
 
 __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
+  // Every input is staged into LDS by all 256 threads first (coalesced, in parallel); the
+  // small products then run from LDS instead of as per-thread loops of dependent global loads.
   __shared__ int all_one;
-  __shared__ double S0[512], LTr[512], v1[256], v2[256], xi[256];
+  __shared__ double S0[512], LTr[512], v1[256], v2[256], xi[256], red[8][64];
+  extern __shared__ __attribute__((aligned(16))) double dyn[];  // A1 | B1 | TR | LS  when a.stage
+  HMSC_STAMP(30);
   const int nc = a.nc, nt = a.nt, N = nc * nt, t = threadIdx.x, n2 = nc * nc;
   if (t == 0) all_one = 1;
   __syncthreads();
@@ -1010,18 +1052,55 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
       if (a.iSigma[j] != 1.0) all_one = 0;  // acts only if all(iSigma == 1)  (:36)
   __syncthreads();
   if (!all_one) return;
-  const int n1 = nc * nt, nL = a.NF * nt;
-  for (int p = t; p < n1 + nL; p += blockDim.x) {
-    double s = 0.0;
+  const int n1 = nc * nt, nL = a.NF * nt, P = n1 + nL;
+  const double* A1g = a.prep;
+  const double* B1g = A1g + n2;
+  const double* TRg = B1g + n2;
+  const double* LSg = TRg + N * N;
+  const double *A1 = A1g, *B1 = B1g, *TR = TRg, *LS = LSg;
+  if (a.stage) {
+    double* d = dyn;
+    for (int p = t; p < 2 * n2 + 2 * N * N; p += blockDim.x) d[p] = a.prep[p];
+    A1 = d;
+    B1 = d + n2;
+    TR = B1 + n2;
+    LS = TR + N * N;
+  }
+  // species-block partials: 8 groups of 32 threads, each summing every 8th part
+  if (P <= 64 && a.nparts > 1) {
+    const int g = t >> 5, l = t & 31;
+    for (int p0 = 0; p0 < P; p0 += 32) {
+      const int p = p0 + l;
+      double s = 0.0;
+      if (p < P)
+        for (int b = g; b < a.nparts; b += 8) s += a.part[(size_t)b * P + p];
+      red[g][l + (p0 ? 32 : 0)] = s;
+    }
+    __syncthreads();
+    for (int p = t; p < P; p += blockDim.x) {
+      const int slot = p < 32 ? p : 32 + (p - 32);
+      double s = 0.0;
+#pragma unroll
+      for (int g2 = 0; g2 < 8; ++g2) s += red[g2][slot];
+      if (p < n1)
+        S0[p] = a.use_xtztr ? a.xtztr[p] : s;
+      else
+        LTr[p - n1] = s;
+    }
+  } else {
+    for (int p = t; p < P; p += blockDim.x) {
+      double s = 0.0;
 #pragma unroll 8
-    for (int b = 0; b < a.nparts; ++b) s += a.part[(size_t)b * (n1 + nL) + p];
-    if (p < n1)
-      S0[p] = a.use_xtztr ? a.xtztr[p] : s;
-    else
-      LTr[p - n1] = s;
+      for (int b = 0; b < a.nparts; ++b) s += a.part[(size_t)b * P + p];
+      if (p < n1)
+        S0[p] = a.use_xtztr ? a.xtztr[p] : s;
+      else
+        LTr[p - n1] = s;
+    }
   }
   for (int r = t; r < N; r += blockDim.x) xi[r] = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)r, 0, S_GAMMA2, a.iter);
   __syncthreads();
+  HMSC_STAMP(31);
   // XZT = X^T Z Tr - sum_r (X^T Eta_r[Pi]) (Lambda_r Tr)   (:46 with S = Z - sum LRan)
   for (int p = t; p < n1; p += blockDim.x) {
     const int c = p % nc, q = p / nc;
@@ -1030,10 +1109,6 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
     S0[p] -= s;
   }
   __syncthreads();
-  const double* A1 = a.prep;
-  const double* B1 = A1 + n2;
-  const double* TR = B1 + n2;
-  const double* LS = TR + N * N;
   for (int p = t; p < N; p += blockDim.x) {
     const int c = p % nc, q = p / nc;
     double s1 = 0.0, s2 = 0.0;
@@ -1051,6 +1126,7 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
     for (int c = 0; c <= r; ++c) m += LS[r + N * c] * xi[c];
     a.Gamma[r] = m;                                                        // (:49, :53-54)
   }
+  HMSC_STAMP(32);
 }
 
 static void launch_gamma2_prep(State& s, hipStream_t st) {
@@ -1114,7 +1190,9 @@ void launch_gamma2(State& s, uint32_t iter) {
   a.key = s.key;
   a.iter = iter;
   a.noise_zero = s.noise_mode;
-  gamma2_final_kernel<<<1, 256, 0, s.stream>>>(a);
+  const size_t N = (size_t)s.nc * s.nt, stage_bytes = (2 * (size_t)s.nc * s.nc + 2 * N * N) * sizeof(double);
+  a.stage = stage_bytes <= 48 * 1024;
+  gamma2_final_kernel<<<1, 256, a.stage ? stage_bytes : 0, s.stream>>>(a);
   HIP_OK(hipGetLastError());
 }
 
@@ -1200,7 +1278,7 @@ __device__ double wave_gamma_std(Key key, uint32_t idx, uint32_t stream, uint32_
   if (v > 0.0) {
     v = v * v * v;
     const double u = uniforms(key, idx, 2u * lane + 1u, stream, iter).a;
-    acc = log(u) < 0.5 * x * x + d - d * v + d * log(v);
+    acc = log_fast(u) < 0.5 * x * x + d - d * v + d * log_fast(v);
     val = d * v;
   }
   const unsigned long long m = __ballot(acc);
@@ -1224,6 +1302,7 @@ __global__ __launch_bounds__(64) void delta_kernel(LPArgs a, const double* rs_pa
     delta[t] = a.Delta[f0 + t];
   }
   __syncthreads();
+  if (r == 0) HMSC_STAMP(20);
   const uint32_t stream = S_DELTA + LEVEL_STRIDE * r;
   const double ns = (double)a.ns_glob;
   for (int h = 0; h < nf; ++h) {
@@ -1241,6 +1320,7 @@ __global__ __launch_bounds__(64) void delta_kernel(LPArgs a, const double* rs_pa
     __syncthreads();
   }
   if (t < nf) a.Delta[f0 + t] = delta[t];
+  if (r == 0) HMSC_STAMP(21);
 }
 
 constexpr int LP_PARTS = 64;
@@ -1351,8 +1431,9 @@ __global__ __launch_bounds__(256) void zl_kernel(const double* __restrict__ Z, c
 }
 
 // CR[k, f] = sum_j BL[k, j] iSigma[j] BL[nc + f, j] over a block of SB species -> slab
+// (and LS = Lambda_all diag(iSigma), NF x ns_loc, for the fused Eta kernel when LS != null)
 __global__ __launch_bounds__(256) void cr_kernel(const double* BL, const double* iSigma, int K, int nc, int NF,
-                                                 int ns_loc, double* CR_part, int ldcr, int slab) {
+                                                 int ns_loc, double* CR_part, int ldcr, int slab, double* LS) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double* sX = smem;   // K x SB
   const int t = threadIdx.x, j0 = blockIdx.x * SB, nj = min(SB, ns_loc - j0);
@@ -1362,6 +1443,11 @@ __global__ __launch_bounds__(256) void cr_kernel(const double* BL, const double*
     (void)jj;
   }
   __syncthreads();
+  if (LS)
+    for (int p = t; p < NF * nj; p += 256) {
+      const int f = p % NF, jj = p / NF;
+      LS[f + (size_t)NF * (j0 + jj)] = sX[nc + f + K * jj] * iSigma[j0 + jj];
+    }
   double* out = CR_part + (size_t)blockIdx.x * slab;
   for (int p = t; p < K * NF; p += 256) {
     const int k = p % K, f = p / K;
@@ -1373,6 +1459,7 @@ __global__ __launch_bounds__(256) void cr_kernel(const double* BL, const double*
 
 struct EtaArgs {
   EtaView ev;
+  const double* XEta;  // ny x K materialised [X, Eta_1[Pi_1,], ...] (before this update)
   int r, nf, np, K, nc, NF, foff, loff, ldcr, nzl;
   const double* ZL;  // ny x NF (row-major per site), or partials [nzl][ny*NF]
   const double* CR;  // K x NF (ld ldcr)
@@ -1438,27 +1525,31 @@ __global__ __launch_bounds__(64) void eta_unit_kernel(EtaArgs a) {
 }
 
 // Fast path (no NA, every unit of level r has the same number n of rows, e.g. np == ny):
-// all units share Q = I + n Lambda_r diag(iSigma) Lambda_r^T, so each workgroup factors Q
-// once in LDS and every thread solves one unit with the shared factor (R/updateEta.R:52-56).
+// all units share Q = I + n Lambda_r diag(iSigma) Lambda_r^T, so each workgroup (one wave)
+// factors Q once in LDS and every lane solves one unit with the shared factor
+// (R/updateEta.R:52-56).  The residual correction reads the materialised XEta (valid: Eta
+// has not changed since it was built), so a lane's loads are plain column reads.
 template <int NFB>
-__global__ __launch_bounds__(256) void eta_shared_kernel(EtaArgs a, int nrow) {
+__global__ __launch_bounds__(64) void eta_shared_kernel(EtaArgs a, int nrow) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int nf = a.nf, K = a.K, t = threadIdx.x;
+  const int nf = a.nf, K = a.K, t = threadIdx.x, ny = a.ev.ny;
   double* Q = smem;               // nf x nf -> lower L
   double* sCR = Q + nf * nf;      // K x nf   (column h of level r)
   int* flag = (int*)(sCR + K * nf + 1);
-  for (int p = t; p < K * nf; p += 256) {
+  if (blockIdx.x == 0) HMSC_STAMP(40);
+  for (int p = t; p < K * nf; p += 64) {
     const int k = p % K, h = p / K;
     sCR[p] = a.CR[k + (size_t)a.ldcr * (a.foff + h)];
   }
   __syncthreads();
-  for (int p = t; p < nf * nf; p += 256) {
+  for (int p = t; p < nf * nf; p += 64) {
     const int r1 = p % nf, c1 = p / nf;
     Q[p] = (r1 == c1 ? 1.0 : 0.0) + nrow * sCR[a.loff + r1 + K * c1];
   }
   __syncthreads();
   wg_chol(Q, nf, nf, flag);
-  const int q = blockIdx.x * 256 + t;
+  if (blockIdx.x == 0) HMSC_STAMP(41);
+  const int q = blockIdx.x * 64 + t;
   if (q >= a.np) return;
   double b[NFB];
 #pragma unroll
@@ -1466,19 +1557,21 @@ __global__ __launch_bounds__(256) void eta_shared_kernel(EtaArgs a, int nrow) {
   for (int pp = a.unit_ptr[q]; pp < a.unit_ptr[q + 1]; ++pp) {
     const int i = a.unit_rows[pp];
     for (int c = 0; c < a.nzl; ++c) {
-      const double* zl = a.ZL + (size_t)c * a.ev.ny * a.NF + (size_t)i * a.NF + a.foff;
+      const double* zl = a.ZL + (size_t)c * ny * a.NF + (size_t)i * a.NF + a.foff;
 #pragma unroll
       for (int h = 0; h < NFB; ++h)
         if (h < nf) b[h] += zl[h];
     }
+#pragma unroll 4
     for (int k = 0; k < K; ++k) {
       if (k >= a.loff && k < a.loff + nf) continue;
-      const double x = xeta_at(a.ev, i, k);
+      const double x = a.XEta[i + (size_t)ny * k];
 #pragma unroll
       for (int h = 0; h < NFB; ++h)
         if (h < nf) b[h] -= x * sCR[k + K * h];
     }
   }
+  if (blockIdx.x == 0) HMSC_STAMP(42);
   // y = L^-1 b ; y += xi ; eta = L^-T y
 #pragma unroll
   for (int h = 0; h < NFB; ++h) {
@@ -1493,6 +1586,7 @@ __global__ __launch_bounds__(256) void eta_shared_kernel(EtaArgs a, int nrow) {
 #pragma unroll
   for (int h = 0; h < NFB; ++h)
     if (h < nf && !a.noise_zero) b[h] += normal(a.key, (uint32_t)q, (uint32_t)h, S_ETA + LEVEL_STRIDE * a.r, a.iter);
+  if (blockIdx.x == 0) HMSC_STAMP(43);
 #pragma unroll
   for (int h = NFB - 1; h >= 0; --h) {
     if (h < nf) {
@@ -1506,6 +1600,7 @@ __global__ __launch_bounds__(256) void eta_shared_kernel(EtaArgs a, int nrow) {
 #pragma unroll
   for (int h = 0; h < NFB; ++h)
     if (h < nf) a.Eta[q + (size_t)a.np * h] = b[h];
+  if (blockIdx.x == 0) HMSC_STAMP(44);
 }
 
 // NA rows (R/updateEta.R:59-70, :80-87): masked per-row precision and numerator
@@ -1540,8 +1635,246 @@ __global__ __launch_bounds__(64) void eta_na_row_kernel(EtaView ev, int r, int n
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused updateEta for the common case -- one random level with np == ny (one row per
+// unit), no NA, one rank (R/updateEta.R:42-57).  One 1024-thread workgroup per 32-site tile:
+//   1. ZL_i = sum_j Z_ij LS_j, LS = Lambda diag(iSigma)  (:55): the 16 waves stream every
+//      32nd species pair (coalesced 256-B site runs), then an LDS tree reduction
+//   2. b_i = ZL_i - sum_{k < nc} XEta_ik CR_k  (the residual S of :31-37), and the noise
+//      xi_q for q = Pi_i (:56), one (site, factor) pair per thread
+//   3. eta_q = L^-T (L^-1 b_i + xi_q), L = chol(I + Lambda diag(iSigma) Lambda^T) (:45-56),
+//      factored once per tile by wave 0
+//   4. the tile's XEta rows get the new Eta (R/updateBetaLambda.R:21-41 of the next sweep)
+//      and the tile's Gram partial XEta^T XEta (:65) goes to G_part[tile]
+// This replaces zl_kernel + eta_shared_kernel + xeta_gram_kernel (and their Z / XEta
+// re-reads) with one pass over Z.
+// ---------------------------------------------------------------------------
+struct EtaFArgs {
+  const double* Z;
+  const double* LS;   // NF x ns_loc
+  const double* CR;   // Kmax x NF (ld ldcr): BL diag(iSigma) Lambda^T
+  double* XEta;       // ny x K (ld ny)
+  const int* Pi;      // ny: unit of each row (0-based)
+  double* Eta;        // np x nf
+  double* G_part;     // [tile][Kmax x Kmax]
+  int ny, ns_loc, K, Kmax, nc, nf, np, ldcr;
+  Key key;
+  uint32_t iter;
+  int noise_zero;
+};
+
+constexpr int EF_SITES = 32;
+
+template <int NFB>
+__global__ __launch_bounds__(512) void eta_fused_kernel(EtaFArgs a) {
+  __shared__ double red[8][NFB][64];
+  __shared__ double sL[NFB * NFB];           // lower factor of Q (column-major)
+  __shared__ double sB[NFB][EF_SITES], sXi[NFB][EF_SITES];
+  __shared__ double sX[64][EF_SITES + 1];     // XEta tile [k][site] (K <= 64)
+  __shared__ double sCR[64 * NFB];            // CR[k][h], k < K
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int ny = a.ny, nf = a.nf, K = a.K, nc = a.nc;
+  const int i0 = blockIdx.x * EF_SITES;
+  const int sl = lane & 31, hf = lane >> 5;
+  const int i = i0 + sl;
+  if (blockIdx.x == 0) HMSC_STAMP(50);
+  // ---- stage 1: ZL partials (every wave), Q factor (wave 0 first)
+  if (w == 0) {
+    double q[NFB], dinv;
+    const int r = lane < nf ? lane : 0;
+#pragma unroll
+    for (int c = 0; c < NFB; ++c) {
+      const double v = (r == c ? 1.0 : 0.0) + a.CR[nc + r + (size_t)a.ldcr * (c < nf ? c : 0)];
+      q[c] = (lane < nf && c < nf) ? v : (lane == c ? 1.0 : 0.0);
+    }
+    wv_chol<NFB>(q, dinv);
+    if (lane < nf)
+#pragma unroll
+      for (int c = 0; c < NFB; ++c)
+        if (c < nf) sL[lane + nf * c] = (c <= lane) ? q[c] : 0.0;
+  }
+  for (int p = t; p < K * nf; p += 512) {
+    const int k = p % K, h = p / K;
+    sCR[k * NFB + h] = a.CR[k + (size_t)a.ldcr * h];
+  }
+  double acc[NFB];
+#pragma unroll
+  for (int h = 0; h < NFB; ++h) acc[h] = 0.0;
+  // LS is staged through LDS in chunks of EF_CHUNK species (aliasing the reduction buffer,
+  // which is free until the end of stage 1); the waves read it back as broadcasts
+  constexpr int EF_CHUNK = 8 * 64;
+  double* sLS = &red[0][0][0];  // [jj][NFB]
+  const double* zc = a.Z + (i < ny ? i : 0);
+  for (int c0 = 0; c0 < a.ns_loc; c0 += EF_CHUNK) {
+    const int nj = min(EF_CHUNK, a.ns_loc - c0);
+    __syncthreads();
+    for (int p = t; p < nj * nf; p += 512) {
+      const int h = p % nf, jj = p / nf;
+      sLS[jj * NFB + h] = a.LS[(size_t)nf * (c0 + jj) + h];
+    }
+    __syncthreads();
+    if (i < ny) {
+      int jj = 2 * w + hf;
+      for (; jj + 48 < nj; jj += 64) {
+        const double z0 = zc[(size_t)ny * (c0 + jj)], z1 = zc[(size_t)ny * (c0 + jj + 16)];
+        const double z2 = zc[(size_t)ny * (c0 + jj + 32)], z3 = zc[(size_t)ny * (c0 + jj + 48)];
+        const double* l0 = sLS + jj * NFB;
+#pragma unroll
+        for (int h = 0; h < NFB; ++h)
+          if (h < nf)
+            acc[h] = fma(z3, l0[h + 48 * NFB],
+                         fma(z2, l0[h + 32 * NFB], fma(z1, l0[h + 16 * NFB], fma(z0, l0[h], acc[h]))));
+      }
+      for (; jj < nj; jj += 16) {
+        const double z0 = zc[(size_t)ny * (c0 + jj)];
+        const double* l0 = sLS + jj * NFB;
+#pragma unroll
+        for (int h = 0; h < NFB; ++h)
+          if (h < nf) acc[h] = fma(z0, l0[h], acc[h]);
+      }
+    }
+  }
+  __syncthreads();  // red is the reduction buffer again
+  if (blockIdx.x == 0) HMSC_STAMP(51);
+#pragma unroll
+  for (int h = 0; h < NFB; ++h) red[w][h][lane] = acc[h];
+  __syncthreads();
+  if (blockIdx.x == 0) HMSC_STAMP(52);
+  // ---- stage 2: b = ZL - X CR_x, and the noise, one (site, factor) per thread
+  if (t < EF_SITES * nf) {
+    const int s2 = t % EF_SITES, h = t / EF_SITES, ii = i0 + s2;
+    double zl = 0.0;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) zl += red[g][h][s2] + red[g][h][s2 + 32];
+    double corr = 0.0, xi = 0.0;
+    if (ii < ny) {
+      for (int k = 0; k < nc; ++k) corr = fma(a.XEta[ii + (size_t)ny * k], sCR[k * NFB + h], corr);
+      xi = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)a.Pi[ii], (uint32_t)h, S_ETA, a.iter);
+    }
+    sB[h][s2] = zl - corr;
+    sXi[h][s2] = xi;
+  }
+  // X columns of the tile into the Gram tile
+  for (int p = t; p < nc * EF_SITES; p += 512) {
+    const int s2 = p % EF_SITES, k = p / EF_SITES, ii = i0 + s2;
+    sX[k][s2] = ii < ny ? a.XEta[ii + (size_t)ny * k] : 0.0;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0) HMSC_STAMP(53);
+  // ---- stage 3: eta = L^-T (L^-1 b + xi), one site per thread of wave 0
+  if (t < EF_SITES) {
+    const int ii = i0 + t;
+    double y[NFB];
+#pragma unroll
+    for (int h = 0; h < NFB; ++h) {
+      if (h < nf) {
+        double v = sB[h][t];
+#pragma unroll
+        for (int k = 0; k < NFB; ++k)
+          if (k < h) v -= sL[h + nf * k] * y[k];
+        y[h] = v / sL[h + nf * h];
+      } else {
+        y[h] = 0.0;
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < NFB; ++h)
+      if (h < nf) y[h] += sXi[h][t];
+#pragma unroll
+    for (int h = NFB - 1; h >= 0; --h) {
+      if (h < nf) {
+        double v = y[h];
+#pragma unroll
+        for (int k = 0; k < NFB; ++k)
+          if (k > h && k < nf) v -= sL[k + nf * h] * y[k];
+        y[h] = v / sL[h + nf * h];
+      }
+    }
+    const int q = ii < ny ? a.Pi[ii] : 0;
+#pragma unroll
+    for (int h = 0; h < NFB; ++h)
+      if (h < nf) {
+        if (ii < ny) {
+          a.Eta[q + (size_t)a.np * h] = y[h];
+          a.XEta[ii + (size_t)ny * (nc + h)] = y[h];
+        }
+        sX[nc + h][t] = ii < ny ? y[h] : 0.0;
+      }
+  }
+  __syncthreads();
+  if (blockIdx.x == 0) HMSC_STAMP(54);
+  // ---- stage 4: Gram partial of the tile
+  double* dst = a.G_part + (size_t)blockIdx.x * a.Kmax * a.Kmax;
+  for (int p = t; p < K * K; p += 512) {
+    const int k1 = p % K, k2 = p / K;
+    double g = 0.0;
+#pragma unroll 8
+    for (int s2 = 0; s2 < EF_SITES; ++s2) g = fma(sX[k1][s2], sX[k2][s2], g);
+    dst[k1 + a.Kmax * k2] = g;
+  }
+  if (blockIdx.x == 0) HMSC_STAMP(55);
+}
+
+static bool eta_fused_ok(const State& s) {
+  return s.nranks == 1 && s.nr == 1 && s.n_na_rows == 0 && s.lev[0].np == s.ny && s.lev[0].uniform_n == 1 &&
+         s.lev[0].nf <= 16 && s.K <= 64 && s.LS != nullptr && !getenv_flag("HMSC_NO_ETA_FUSION");
+}
+
+static void launch_eta_fused(State& s, uint32_t iter) {
+  {
+    const int ncr = (s.nsl + SB - 1) / SB;
+    const int64_t slab = (int64_t)s.Kmax * s.NFmax;
+    cr_kernel<<<ncr, 256, (size_t)s.K * SB * sizeof(double), s.stream>>>(s.BL, s.iSigma, s.K, s.nc, s.NF, s.nsl,
+                                                                           s.CR_part, s.Kmax, (int)slab, s.LS);
+    HIP_OK(hipGetLastError());
+    slab_sum_kernel<<<grid_for(slab), 256, 0, s.stream>>>(s.CR_part, s.CR, slab, ncr, slab);
+    HIP_OK(hipGetLastError());
+  }
+  const Level& L = s.lev[0];
+  EtaFArgs a{};
+  a.Z = s.Z;
+  a.LS = s.LS;
+  a.CR = s.CR;
+  a.XEta = s.XEta;
+  a.Pi = L.Pi;
+  a.Eta = L.Eta;
+  a.G_part = s.G_part;
+  a.ny = s.ny;
+  a.ns_loc = s.nsl;
+  a.K = s.K;
+  a.Kmax = s.Kmax;
+  a.nc = s.nc;
+  a.nf = L.nf;
+  a.np = L.np;
+  a.ldcr = s.Kmax;
+  a.key = s.key;
+  a.iter = iter;
+  a.noise_zero = s.noise_mode;
+  const int ntile = (s.ny + EF_SITES - 1) / EF_SITES;
+  {
+    ProfScope ps(s, PROF_ETA_UNIT);
+    if (L.nf <= 8)
+      eta_fused_kernel<8><<<ntile, 512, 0, s.stream>>>(a);
+    else if (L.nf <= 12)  // 80 KB of LDS: two workgroups per CU
+      eta_fused_kernel<12><<<ntile, 512, 0, s.stream>>>(a);
+    else
+      eta_fused_kernel<16><<<ntile, 512, 0, s.stream>>>(a);
+    HIP_OK(hipGetLastError());
+  }
+  const int64_t nG = (int64_t)s.Kmax * s.Kmax;
+  slab_sum_kernel<<<grid_for(nG), 256, 0, s.stream>>>(s.G_part, s.G, nG, ntile, nG);
+  HIP_OK(hipGetLastError());
+  s.zt_valid = false;   // Eta changed: XZ is stale until the next updateZ
+  s.xeta_valid = true;  // XEta rows and G rewritten above
+}
+
 void launch_eta(State& s, uint32_t iter) {
   if (s.nr == 0) return;
+  if (!s.xeta_valid) launch_xeta(s);  // the Eta kernels read XEta of the current Eta
+  if (eta_fused_ok(s)) {
+    launch_eta_fused(s, iter);
+    return;
+  }
   HMSC_REQUIRE(s.NF <= 64, "updateEta: sum(nf) must be <= 64 in this build");
   for (int r = 0; r < s.nr; ++r)
     HMSC_REQUIRE(s.lev[r].nf >= 1, "updateEta: a level has zero factors");
@@ -1565,7 +1898,7 @@ void launch_eta(State& s, uint32_t iter) {
     const int ncr = (s.nsl + SB - 1) / SB;
     const int64_t slab = (int64_t)s.Kmax * s.NFmax;
     cr_kernel<<<ncr, 256, (size_t)s.K * SB * sizeof(double), s.stream>>>(s.BL, s.iSigma, s.K, s.nc, s.NF, s.nsl,
-                                                                           s.CR_part, s.Kmax, (int)slab);
+                                                                           s.CR_part, s.Kmax, (int)slab, nullptr);
     HIP_OK(hipGetLastError());
     slab_sum_kernel<<<grid_for(slab), 256, 0, s.stream>>>(s.CR_part, s.CR, slab, ncr, slab);
     HIP_OK(hipGetLastError());
@@ -1582,8 +1915,10 @@ void launch_eta(State& s, uint32_t iter) {
   }
   for (int r = 0; r < s.nr; ++r) {
     const Level& L = s.lev[r];
+    if (r > 0) launch_xeta(s);  // levels r' < r were just redrawn (R/updateEta.R:31-37 uses them)
     EtaArgs a{};
     a.ev = make_view(s);
+    a.XEta = s.XEta;
     a.r = r;
     a.nf = L.nf;
     a.np = L.np;
@@ -1617,13 +1952,13 @@ void launch_eta(State& s, uint32_t iter) {
     ProfScope ps(s, PROF_ETA_UNIT);
     if (s.n_na_rows == 0 && L.uniform_n > 0 && L.nf <= 32) {
       const size_t smem = ((size_t)L.nf * L.nf + (size_t)s.K * L.nf + 2) * sizeof(double);
-      const int grid = (L.np + 255) / 256;
+      const int grid = (L.np + 63) / 64;
       if (L.nf <= 8)
-        eta_shared_kernel<8><<<grid, 256, smem, s.stream>>>(a, L.uniform_n);
+        eta_shared_kernel<8><<<grid, 64, smem, s.stream>>>(a, L.uniform_n);
       else if (L.nf <= 16)
-        eta_shared_kernel<16><<<grid, 256, smem, s.stream>>>(a, L.uniform_n);
+        eta_shared_kernel<16><<<grid, 64, smem, s.stream>>>(a, L.uniform_n);
       else
-        eta_shared_kernel<32><<<grid, 256, smem, s.stream>>>(a, L.uniform_n);
+        eta_shared_kernel<32><<<grid, 64, smem, s.stream>>>(a, L.uniform_n);
     } else {
       const size_t smem = ((size_t)L.nf * L.nf + L.nf + 2) * sizeof(double);
       eta_unit_kernel<<<L.np, 64, smem, s.stream>>>(a);

@@ -89,44 +89,6 @@ __host__ __device__ __forceinline__ Uniform2 uniforms(Key key, uint32_t idx, uin
   return Uniform2{u53(r.x, r.y), u53(r.z, r.w)};
 }
 
-// standard normal: Box-Muller cosine branch of the (idx, sub) block
-__host__ __device__ __forceinline__ double normal(Key key, uint32_t idx, uint32_t sub, uint32_t stream,
-                                         uint32_t iter) {
-  const Uniform2 u = uniforms(key, idx, sub, stream, iter);
-#if defined(__HIP_DEVICE_COMPILE__)
-  // cospi: exact argument reduction, no Payne-Hanek table (keeps kernels spill-free)
-  return sqrt(-2.0 * log(u.a)) * cospi(2.0 * u.b);
-#else
-  return sqrt(-2.0 * log(u.a)) * cos(6.283185307179586 * u.b);
-#endif
-}
-
-// Gamma(shape, rate=1): Marsaglia & Tsang (2000); trial t uses sub-blocks 2t (normal)
-// and 2t+1 (acceptance uniform); shape<1 uses the boost x*U^(1/shape).
-__host__ __device__ __forceinline__ double gamma_std(Key key, uint32_t idx, uint32_t stream, uint32_t iter,
-                                            double shape) {
-  const double a = shape < 1.0 ? shape + 1.0 : shape;
-  const double d = a - 1.0 / 3.0;
-  const double c = 1.0 / sqrt(9.0 * d);
-  double out = d;  // fallback after GAMMA_MAX_TRIALS (probability < 1e-60)
-  for (int t = 0; t < GAMMA_MAX_TRIALS; ++t) {
-    const double x = normal(key, idx, 2u * t, stream, iter);
-    double v = 1.0 + c * x;
-    if (v <= 0.0) continue;
-    v = v * v * v;
-    const double u = uniforms(key, idx, 2u * t + 1u, stream, iter).a;
-    if (log(u) < 0.5 * x * x + d - d * v + d * log(v)) {
-      out = d * v;
-      break;
-    }
-  }
-  if (shape < 1.0) {
-    const double u = uniforms(key, idx, GAMMA_BOOST_SUB, stream, iter).a;
-    out *= pow(u, 1.0 / shape);
-  }
-  return out;
-}
-
 // Phi^-1(p), Wichura (1988) AS241 PPND16 (the algorithm behind R's qnorm), |rel err| ~1e-16.
 __host__ __device__ __forceinline__ double qnorm_as241(double p) {
   const double q = p - 0.5;
@@ -329,6 +291,39 @@ __host__ __device__ __forceinline__ double qnorm_fast(double p) {
     return y * f;
   }
   return qnorm_as241_tail(p);
+}
+
+// standard normal by inversion of the first uniform of the (idx, sub) block (R's default
+// rnorm method, INVERSION; the oracle uses AS241 itself, the device qnorm_fast)
+__host__ __device__ __forceinline__ double normal(Key key, uint32_t idx, uint32_t sub, uint32_t stream,
+                                                  uint32_t iter) {
+  return qnorm_fast(uniforms(key, idx, sub, stream, iter).a);
+}
+
+// Gamma(shape, rate=1): Marsaglia & Tsang (2000); trial t uses sub-blocks 2t (normal)
+// and 2t+1 (acceptance uniform); shape<1 uses the boost x*U^(1/shape).
+__host__ __device__ __forceinline__ double gamma_std(Key key, uint32_t idx, uint32_t stream, uint32_t iter,
+                                                     double shape) {
+  const double a = shape < 1.0 ? shape + 1.0 : shape;
+  const double d = a - 1.0 / 3.0;
+  const double c = 1.0 / sqrt(9.0 * d);
+  double out = d;  // fallback after GAMMA_MAX_TRIALS (probability < 1e-60)
+  for (int t = 0; t < GAMMA_MAX_TRIALS; ++t) {
+    const double x = normal(key, idx, 2u * t, stream, iter);
+    double v = 1.0 + c * x;
+    if (v <= 0.0) continue;
+    v = v * v * v;
+    const double u = uniforms(key, idx, 2u * t + 1u, stream, iter).a;
+    if (log_fast(u) < 0.5 * x * x + d - d * v + d * log_fast(v)) {
+      out = d * v;
+      break;
+    }
+  }
+  if (shape < 1.0) {
+    const double u = uniforms(key, idx, GAMMA_BOOST_SUB, stream, iter).a;
+    out *= pow(u, 1.0 / shape);
+  }
+  return out;
 }
 
 // Standard normal truncated to [alpha, +inf) by inversion of the upper tail:

@@ -101,6 +101,7 @@ struct State {
   double* ZL_part = nullptr;     // zl_split x ny x NFP
   double* CR = nullptr;          // Kmax x NFmax  BL diag(iSigma) Lambda_all^T
   double* CR_part = nullptr;     // species-block partials of CR
+  double* LS = nullptr;          // NFmax x ns_loc  Lambda_all diag(iSigma) (fused Eta kernel)
   double* Msmall = nullptr;      // per-level masked row grams (NA rows)
   double* scratch = nullptr;     // single-workgroup updaters
   double* psi_rs = nullptr;      // psi-lambda^2 row-sum partials
@@ -183,5 +184,6 @@ void launch_eta(State& s, uint32_t iter);
 void launch_inv_sigma(State& s, uint32_t iter);
 void launch_record(State& s, double* slot);
 size_t record_slot_doubles(const State& s);
+void read_stamps(double* out, int n);  // diagnostic build (HMSC_STAMPS)
 
 }  // namespace hmsc

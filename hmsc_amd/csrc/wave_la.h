@@ -88,6 +88,36 @@ __device__ inline bool wv_chol(double (&a)[NM], double& dinv) {
   return ok;
 }
 
+// The same factorisation with LDS broadcasts instead of v_readlane: per column every lane
+// stores its A[i][c] once and then reads the column back at uniform addresses (LDS
+// broadcast), so the NM - c - 1 trailing updates cost one ds_read each instead of two
+// readlanes plus the SGPR->VALU wait states.  col: wave-private LDS scratch of 128 doubles
+// (double-buffered by column parity; LDS executes one wave's instructions in order).
+template <int NM>
+__device__ inline bool wv_chol_s(double (&a)[NM], double& dinv, double* col) {
+  const int i = lane_id();
+  bool ok = true;
+  dinv = 1.0;
+#pragma unroll
+  for (int c = 0; c < NM; ++c) {
+    double* cb = col + 64 * (c & 1);
+    cb[i] = a[c];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const double d = cb[c];
+    ok = ok && d > 0.0;
+    const double l = sqrt(d > 0.0 ? d : 1.0);
+    const double inv = 1.0 / l;
+    const double sc = a[c] * inv * inv;  // L[i][c] L[j][c] = sc * A[j][c]
+#pragma unroll
+    for (int j = c + 1; j < NM; ++j) a[j] = fma(-sc, cb[j], a[j]);
+    if (i == c) dinv = inv;
+    a[c] = (i == c) ? l : a[c] * inv;
+  }
+  return ok;
+}
+
 // x <- L^{-1} x, x lane-distributed (lane i holds x_i)
 template <int NM>
 __device__ inline void wv_forward(const double (&l)[NM], double dinv, double& x) {
@@ -144,6 +174,34 @@ __device__ inline void wv_inv_lower(const double (&l)[NM], double dinv, double (
       w[k] = (i == m) ? wmk : (i > m ? fma(-l[m], wmk, w[k]) : w[k]);
     }
   }
+}
+
+// Columns of L^{-1}: lane i ends with column i of L^{-1} (w[r] = Linv[r][i]; zero for r < i).
+// L is staged once in LDS; every lane then forward-substitutes its own unit vector reading
+// L at uniform addresses (broadcasts) -- no cross-lane register traffic.  lds: scratch of
+// NM * (NM + 1) doubles (the staged diagonal holds 1 / L[i][i]).
+template <int NM>
+__device__ inline void wv_inv_lower_cols(const double (&l)[NM], double dinv, double (&w)[NM], double* lds) {
+  constexpr int LD = NM + 1;
+  const int i = lane_id();
+  if (i < NM) {
+#pragma unroll
+    for (int k = 0; k < NM; ++k) lds[i + LD * k] = (k < i) ? l[k] : (k == i ? dinv : 0.0);  // L[i][k]
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int r = 0; r < NM; ++r) w[r] = (r == i) ? 1.0 : 0.0;
+#pragma unroll
+  for (int c = 0; c < NM; ++c) {
+    w[c] *= lds[c + LD * c];
+#pragma unroll
+    for (int r = c + 1; r < NM; ++r) w[r] = fma(-lds[r + LD * c], w[c], w[r]);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // ---- products on the matrix cores -------------------------------------------------
@@ -240,12 +298,21 @@ __device__ inline void wv_syrk_tn_lower(const double (&w)[NM], double (&c)[NM], 
   wv_gemm<NM, true, false, true, true>(w, w, c, lds);
 }
 
-// chol2inv: c <- (L L^T)^{-1} from the factor of wv_chol
+// chol2inv: c <- (L L^T)^{-1} = L^{-T} L^{-1} from the factor of wv_chol; lds = 3 tiles.
 template <int NM>
 __device__ inline void wv_chol2inv(const double (&l)[NM], double dinv, double (&c)[NM], double* lds) {
   double w[NM];
   wv_inv_lower<NM>(l, dinv, w);
   wv_syrk_tn_lower<NM>(w, c, lds);
+}
+
+// the same through wv_inv_lower_cols (LDS broadcasts; measured slower on gfx950 at NM >= 24,
+// kept for scripts/ubench_wave.hip)
+template <int NM>
+__device__ inline void wv_chol2inv_cols(const double (&l)[NM], double dinv, double (&c)[NM], double* lds) {
+  double w[NM];
+  wv_inv_lower_cols<NM>(l, dinv, w, lds + 2 * WV_TILE);
+  wv_gemm<NM, false, true>(w, w, c, lds);
 }
 
 }  // namespace hmsc

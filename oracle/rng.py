@@ -3,7 +3,7 @@
 numpy restatement of the counter-based randomness contract of
 ``hmsc_amd/csrc/rng.h``: Philox4x32-10 (Salmon et al., SC'11; Random123 KAT
 vectors checked in tests/test_oracle_rng.py), 53-bit open-interval uniforms,
-Box-Muller normals, Marsaglia-Tsang gammas, inverse-CDF one-sided truncated
+inverse-CDF normals, Marsaglia-Tsang gammas, inverse-CDF one-sided truncated
 normals.  It stands in for the unvendored samplers the reference calls:
 stats::rnorm / rgamma (R/updateLambdaPriors.R:23-32, R/updateInvSigma.R:40),
 truncnorm::rtruncnorm (R/updateZ.R:59), MCMCpack::rwish (R/updateGammaV.R:21).
@@ -84,8 +84,10 @@ class Rng:
         return u53(x, y), u53(z, w)
 
     def normal(self, idx, sub, stream, it):
-        a, b = self.uniforms(idx, sub, stream, it)
-        return np.sqrt(-2.0 * np.log(a)) * np.cos(6.283185307179586 * b)
+        """Standard normal by inversion of the first uniform of the (idx, sub) block
+        (R's own default rnorm method, INVERSION)."""
+        a, _ = self.uniforms(idx, sub, stream, it)
+        return qnorm_as241(a)
 
     def gamma_std(self, idx, stream, it, shape):
         """Marsaglia-Tsang Gamma(shape, 1), elementwise over ``idx``/``shape``."""

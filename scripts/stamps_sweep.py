@@ -1,0 +1,25 @@
+"""Read the HMSC_STAMP clock stamps of one sweep at the synthetic config (diagnostic
+library: python -m hmsc_amd.build --stamps; run with HMSC_AMD_LIB=.../libhmsc_amd_stamps.so)."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("HMSC_AMD_LIB", os.path.join(ROOT, "hmsc_amd", "libhmsc_amd_stamps.so"))
+import hmsc_amd as H  # noqa: E402
+from hmsc_amd.workloads import synthetic_probit  # noqa: E402
+
+hM = synthetic_probit()
+ch = H.Chain(hM, 1234567, device=0, updater={"GammaEta": False})
+ch.init([10])
+for it in range(1, 6):
+    ch.sweep(it)
+ch.sync()
+st = ch.debug_get("stamps", 64)
+groups = {"gammav_wave": range(0, 10), "delta": range(20, 22), "gamma2_final": range(30, 33), "eta_shared(block0)": range(40, 45), "eta_fused(block0)": range(50, 56)}
+for name, idx in groups.items():
+    v = np.array([st[i] for i in idx])
+    d = np.diff(v)
+    print(name, "total cycles", v[-1] - v[0], "segments", d.astype(np.int64).tolist())

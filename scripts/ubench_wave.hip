@@ -24,6 +24,20 @@ __global__ __launch_bounds__(64) void k_chol(const double* A, int n, int reps, d
 }
 
 template <int NM>
+__global__ __launch_bounds__(64) void k_chol_s(const double* A, int n, int reps, double* out, long long* cyc) {
+  __shared__ double col[128];
+  double l[NM], dinv;
+  const long long t0 = clock64();
+  for (int r = 0; r < reps; ++r) {
+    wv_load<NM>(A, n, n, l);
+    wv_chol_s<NM>(l, dinv, col);
+  }
+  const long long t1 = clock64();
+  wv_store_lower<NM>(out, n, n, l);
+  if (threadIdx.x == 0) *cyc = (t1 - t0) / reps;
+}
+
+template <int NM>
 __global__ __launch_bounds__(64) void k_inv(const double* A, int n, int reps, double* out, long long* cyc) {
   __shared__ double lds[3 * WV_TILE];
   double l[NM], c[NM], dinv;
@@ -100,7 +114,7 @@ static void run(int n, double* dA, double* dB, double* dO, double* db, long long
   CK(hipMemcpy(dA, A.data(), n * n * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(dB, B.data(), n * n * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(db, b.data(), n * 8, hipMemcpyHostToDevice));
-  long long cy[4];
+  long long cy[5];
   std::vector<double> O(n * n);
   hipLaunchKernelGGL(k_chol<NM>, dim3(1), dim3(64), 0, 0, dA, n, reps, dO, dc);
   CK(hipMemcpy(&cy[0], dc, 8, hipMemcpyDeviceToHost));
@@ -110,6 +124,12 @@ static void run(int n, double* dA, double* dB, double* dO, double* db, long long
   double e_chol = 0;
   for (int j = 0; j < n; ++j)
     for (int i = j; i < n; ++i) e_chol = std::fmax(e_chol, std::fabs(O[i + n * j] - L[i + n * j]));
+  hipLaunchKernelGGL(k_chol_s<NM>, dim3(1), dim3(64), 0, 0, dA, n, reps, dO, dc);
+  CK(hipMemcpy(&cy[4], dc, 8, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(O.data(), dO, n * n * 8, hipMemcpyDeviceToHost));
+  double e_chol_s = 0;
+  for (int j = 0; j < n; ++j)
+    for (int i = j; i < n; ++i) e_chol_s = std::fmax(e_chol_s, std::fabs(O[i + n * j] - L[i + n * j]));
   hipLaunchKernelGGL(k_inv<NM>, dim3(1), dim3(64), 0, 0, dA, n, reps, dO, dc);
   CK(hipMemcpy(&cy[1], dc, 8, hipMemcpyDeviceToHost));
   CK(hipMemcpy(O.data(), dO, n * n * 8, hipMemcpyDeviceToHost));
@@ -139,9 +159,9 @@ static void run(int n, double* dA, double* dB, double* dO, double* db, long long
     for (int k = 0; k < n; ++k) s += A[i + n * k] * O[k];
     e_solve = std::fmax(e_solve, std::fabs(s - b[i]));
   }
-  printf("wave NM=%d n=%d  chol=%lld  chol2inv=%lld  gemm=%lld  fwd+bwd=%lld cycles | err chol=%.1e inv=%.1e "
-         "gemm=%.1e solve=%.1e\n",
-         NM, n, cy[0], cy[1], cy[2], cy[3], e_chol, e_inv, e_gemm, e_solve);
+  printf("wave NM=%d n=%d  chol=%lld chol_s=%lld  chol2inv=%lld  gemm=%lld  fwd+bwd=%lld cycles | err chol=%.1e "
+         "chol_s=%.1e inv=%.1e gemm=%.1e solve=%.1e\n",
+         NM, n, cy[0], cy[4], cy[1], cy[2], cy[3], e_chol, e_chol_s, e_inv, e_gemm, e_solve);
 }
 
 int main() {
