@@ -86,14 +86,20 @@ def main():
         ch = H.Chain(hM, 1234567 + 7919 * rank, device=local, updater=upd)
     ch.init([args.nf])
     ch.run(transient=args.warmup, samples=0, adaptNf=[0], record=False)
-    ch.profile(True)
     barrier()
     sync(ch)
     t0 = time.perf_counter()
+    # timed region: every sweep is a replay of the captured per-sweep hipGraph (capi.cpp)
     rec = ch.run(transient=0, samples=args.steps, thin=1, adaptNf=[0], iter0=args.warmup, record=True)
     sync(ch)
     barrier()
     t_run = time.perf_counter() - t0
+    # per-kernel durations: HIP events around the launches of a short eager (un-captured)
+    # run on the chain's own stream, after the timed region
+    n_prof = min(args.steps, 50)
+    ch.profile(True)
+    ch.run(transient=n_prof, samples=0, adaptNf=[0], iter0=args.warmup + args.steps, record=False)
+    sync(ch)
     kern = {}
     for name in ("z", "zl", "betalambda", "eta_unit", "sweep"):
         tot, n = ch.profile_get(name)

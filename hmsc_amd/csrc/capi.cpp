@@ -8,7 +8,12 @@
 #include <cstdio>
 #include <atomic>
 #include <cstring>
+#include <cstdlib>
 #include <thread>
+#include <memory>
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -24,6 +29,7 @@ struct hmsc_state {
 namespace hmsc {
 
 static thread_local std::string g_last_error;
+static constexpr int RING_SLOTS = 32;  // recorded samples in flight between device and host
 
 static int fail(int code, const std::string& msg) {
   g_last_error = msg;
@@ -369,6 +375,24 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.ABpart = dalloc<double>((size_t)((nsl + 31) / 32) * (nc * nc + 2 * N + nfm * nt + 8));
   s.allreduce_buf = dalloc<double>((size_t)nc * nc + 2 * N + nfm * nt + nfm + 64);
   s.dev_flags = dalloc<int>(16);
+  s.d_iter = dalloc<uint32_t>(1);
+  // recording ring: RING_SLOTS device slots, their pinned host mirror and the copied counter,
+  // allocated once here so no run pays for pinning
+  s.slot_doubles = record_slot_doubles(s);
+  s.ring_slots = RING_SLOTS;
+  s.ring = dalloc<double>(s.slot_doubles * s.ring_slots);
+  HIP_OK(hipHostMalloc(&s.host_rec, sizeof(double) * s.slot_doubles * s.ring_slots, hipHostMallocDefault));
+  HIP_OK(hipHostMalloc(&s.copied_host, 64, hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_OK(hipHostGetDevicePointer((void**)&s.copied_dev, s.copied_host, 0));
+  for (int i = 0; i < s.ring_slots; ++i) {
+    hipEvent_t e;
+    HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    s.ring_packed.push_back(e);
+  }
+  {
+    const char* g = getenv("HMSC_NO_GRAPH");
+    s.use_graph = !(g && g[0] && g[0] != '0');
+  }
   HIP_OK(hipDeviceSynchronize());
 }
 
@@ -388,8 +412,11 @@ static void free_state(State& s) {
     for (void* p : lp)
       if (p) (void)hipFree(p);
   }
-  for (hipEvent_t e : s.ring_done) (void)hipEventDestroy(e);
+  for (hipEvent_t e : s.ring_packed) (void)hipEventDestroy(e);
   if (s.host_rec) (void)hipHostFree(s.host_rec);
+  if (s.copied_host) (void)hipHostFree(s.copied_host);
+  if (s.gexec) (void)hipGraphExecDestroy(s.gexec);
+  if (s.d_iter) (void)hipFree(s.d_iter);
   if (s.comm) ncclCommDestroy((ncclComm_t)s.comm);
   if (s.ev_bl) (void)hipEventDestroy(s.ev_bl);
   if (s.ev_side) (void)hipEventDestroy(s.ev_side);
@@ -490,6 +517,7 @@ static void set_state(State& s, const hmsc_params* p) {
   s.zt_valid = false;
   s.xeta_valid = false;
   s.g2prep_valid = false;
+  s.graph_dirty = true;
 }
 
 // ---------------------------- updateNf (host decision) ----------------------------
@@ -596,6 +624,7 @@ static void update_nf(State& s, int r, uint32_t iter) {
   s.refresh_dims();
   s.zt_valid = false;
   s.xeta_valid = false;
+  s.graph_dirty = true;
 }
 
 // ---------------------------- sweep ----------------------------
@@ -665,6 +694,78 @@ static void sweep(State& s, uint32_t iter, bool adapt) {
   }
 }
 
+// ---------------------------- per-sweep hipGraph ----------------------------
+// A steady-state sweep (no updateNf, one rank) is captured once into a graph and replayed:
+// one launch per sweep instead of ~20 kernel launches + event records, so the GPU no longer
+// waits on the host between dependent kernels.  Kernels captured with s.capturing read the
+// Philox sweep counter from s.d_iter; the graph's first node advances it.
+__global__ void set_iter_kernel(uint32_t* p, uint32_t v) { *p = v; }
+__global__ void advance_iter_kernel(uint32_t* p) { *p += 1u; }
+
+static void destroy_graph(State& s) {
+  if (s.gexec) (void)hipGraphExecDestroy(s.gexec);
+  s.gexec = nullptr;
+}
+
+// Captures one sweep.  Returns false (and leaves no graph) when the sweep is not in a
+// steady state, i.e. the host-side validity flags it changes would differ on the next sweep.
+static bool build_sweep_graph(State& s, uint32_t iter) {
+  destroy_graph(s);
+  join_side(s);
+  const bool xv = s.xeta_valid, zv = s.zt_valid, gv = s.g2prep_valid;
+  hipGraph_t g = nullptr;
+  HIP_OK(hipStreamBeginCapture(s.stream, hipStreamCaptureModeThreadLocal));
+  s.capturing = true;
+  try {
+    advance_iter_kernel<<<1, 1, 0, s.stream>>>(s.d_iter);
+    sweep(s, iter, false);
+    join_side(s);
+  } catch (...) {
+    s.capturing = false;
+    (void)hipStreamEndCapture(s.stream, &g);
+    if (g) (void)hipGraphDestroy(g);
+    s.xeta_valid = xv, s.zt_valid = zv, s.g2prep_valid = gv;
+    throw;
+  }
+  s.capturing = false;
+  HIP_OK(hipStreamEndCapture(s.stream, &g));
+  const bool steady = xv == s.xeta_valid && zv == s.zt_valid && gv == s.g2prep_valid;
+  s.xeta_valid = xv, s.zt_valid = zv, s.g2prep_valid = gv;  // nothing ran yet
+  if (!steady) {
+    (void)hipGraphDestroy(g);
+    return false;
+  }
+  HIP_OK(hipGraphInstantiate(&s.gexec, g, nullptr, nullptr, 0));
+  HIP_OK(hipGraphDestroy(g));
+  s.graph_K = s.K;
+  s.graph_NF = s.NF;
+  s.graph_dirty = false;
+  return true;
+}
+
+// One sweep of the run loop: a graph replay when possible, else the eager launch sequence.
+static void run_sweep(State& s, uint32_t iter, bool adapt) {
+  const bool graphable = s.use_graph && s.nranks == 1 && !s.prof && !adapt;
+  if (!graphable) {
+    sweep(s, iter, adapt);
+    s.eager_streak = adapt ? 0 : s.eager_streak + 1;
+    return;
+  }
+  if (s.gexec && (s.graph_dirty || s.graph_K != s.K || s.graph_NF != s.NF)) destroy_graph(s);
+  if (s.graph_dirty) s.eager_streak = 0, s.graph_dirty = false;
+  if (!s.gexec) {
+    if (s.eager_streak < 1 || !build_sweep_graph(s, iter)) {  // reach a steady state first
+      sweep(s, iter, false);
+      ++s.eager_streak;
+      return;
+    }
+  }
+  join_side(s);
+  if (s.graph_next_iter != iter) set_iter_kernel<<<1, 1, 0, s.stream>>>(s.d_iter, iter - 1u);
+  HIP_OK(hipGraphLaunch(s.gexec, s.stream));
+  s.graph_next_iter = iter + 1u;
+}
+
 static void unpack_record(const State& s, const double* slot, int k, int samples, hmsc_record* rec) {
   const int K = s.K, nsl = s.nsl, nc = s.nc, nt = s.nt, NF = s.NF;
   const double* BL = slot;
@@ -716,93 +817,88 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
     HMSC_REQUIRE(adaptNf == nullptr || adaptNf[r] <= transient,
                  "transient parameter should be no less than any element of adaptNf parameter");
   const bool recording = rec != nullptr && samples > 0;
-  if (recording) {
-    s.slot_doubles = record_slot_doubles(s);
-    const int want_slots = std::min(samples, 32);
-    if (s.ring_slots < want_slots) {
-      if (s.ring) HIP_OK(hipFree(s.ring));
-      for (hipEvent_t e : s.ring_done) HIP_OK(hipEventDestroy(e));
-      s.ring_done.clear();
-      s.ring = dalloc<double>(s.slot_doubles * want_slots);
-      s.ring_slots = want_slots;
-      for (int i = 0; i < want_slots; ++i) {
-        hipEvent_t e;
-        HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        s.ring_done.push_back(e);
-      }
-    }
-    if (s.host_rec_doubles < s.slot_doubles * s.ring_slots) {
-      if (s.host_rec) HIP_OK(hipHostFree(s.host_rec));
-      s.host_rec = nullptr;
-      HIP_OK(hipHostMalloc(&s.host_rec, sizeof(double) * s.slot_doubles * s.ring_slots, hipHostMallocDefault));
-      s.host_rec_doubles = s.slot_doubles * s.ring_slots;
-    }
-  }
-  // Recorded samples are unpacked into the caller's arrays by a host worker thread as
-  // their device->host copies land, so the unpack overlaps the sweeps still being enqueued.
-  std::atomic<int> issued{0}, unpacked{0};
+  // Recording: sample k is packed into device slot k % ring_slots (main stream), copied to the
+  // pinned host slot (copy stream), after which a flag kernel bumps *copied_host to k + 1.
+  // Host unpack threads poll that counter -- no HIP call off the launching thread, so nothing
+  // contends with the sweep launches -- and unpack sample k into the caller's arrays (worker
+  // k % W).  The launcher reuses slot k % ring_slots only after sample k - ring_slots is
+  // unpacked, which also means its copy landed, so the device slot is free too.
   std::atomic<bool> stop{false}, worker_failed{false};
   std::string worker_err;
-  std::thread worker;
+  std::mutex mu;                        // worker_err + cv_done
+  std::condition_variable cv_done;
+  std::unique_ptr<std::atomic<uint8_t>[]> done(new std::atomic<uint8_t>[std::max(1, samples)]);
+  for (int k = 0; k < samples; ++k) done[k].store(0);
+  int low = 0;  // every sample < low is unpacked (main thread only)
+  volatile uint64_t* copied = s.copied_host;
+  if (recording) *copied = 0;           // no copy is in flight between runs
+  const char* w_env = getenv("HMSC_UNPACK_THREADS");
+  const int W = recording ? std::max(1, std::min(w_env ? atoi(w_env) : 2,
+                                                 std::max(1, (int)std::thread::hardware_concurrency() / 2)))
+                          : 0;
+  std::vector<std::thread> workers;
   struct Joiner {
-    std::thread& t;
+    std::vector<std::thread>& t;
     std::atomic<bool>& stop;
     ~Joiner() {
       stop.store(true);
-      if (t.joinable()) t.join();
+      for (auto& th : t)
+        if (th.joinable()) th.join();
     }
-  } joiner{worker, stop};
-  if (recording)
-    worker = std::thread([&] {
+  } joiner{workers, stop};
+  for (int w = 0; w < W; ++w)
+    workers.emplace_back([&, w] {
       try {
-        HIP_OK(hipSetDevice(s.device));
-        for (int k = 0; k < samples; ++k) {
-          while (issued.load(std::memory_order_acquire) <= k) {
-            if (stop.load()) return;
-            std::this_thread::yield();
+        for (int k = w; k < samples; k += W) {
+          for (int spin = 0; __atomic_load_n(copied, __ATOMIC_ACQUIRE) <= (uint64_t)k; ++spin) {
+            if (stop.load(std::memory_order_relaxed)) return;
+            if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+            else std::this_thread::yield();
           }
-          const int slot = k % s.ring_slots;
-          HIP_OK(hipEventSynchronize(s.ring_done[slot]));
-          unpack_record(s, s.host_rec + s.slot_doubles * slot, k, samples, rec);
-          unpacked.store(k + 1, std::memory_order_release);
+          unpack_record(s, s.host_rec + s.slot_doubles * (k % s.ring_slots), k, samples, rec);
+          done[k].store(1, std::memory_order_release);
+          {  // the launcher may be waiting for this host slot
+            std::lock_guard<std::mutex> lk(mu);
+          }
+          cv_done.notify_one();
         }
       } catch (const std::exception& e) {
+        std::lock_guard<std::mutex> lk(mu);
         worker_err = e.what();
         worker_failed.store(true);
+        cv_done.notify_all();
       }
     });
   const int total = transient + samples * thin;
-  std::vector<hipEvent_t> packed;
-  if (recording) {
-    packed.resize(s.ring_slots);
-    for (auto& e : packed) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  }
   for (int it = 1; it <= total; ++it) {
     const uint32_t iter = (uint32_t)(iter0 + it);
     bool adapt = false;
     if (adaptNf)
       for (int r = 0; r < s.nr; ++r) adapt |= it <= adaptNf[r];
-    sweep(s, iter, adapt);
+    run_sweep(s, iter, adapt);
     if (recording && it > transient && (it - transient) % thin == 0) {
       const int k = (it - transient) / thin - 1;
       const int slot = k % s.ring_slots;
-      if (k >= s.ring_slots) {
-        HIP_OK(hipStreamWaitEvent(s.stream, s.ring_done[slot], 0));
-        // the host slot is reused: the worker must have unpacked sample k - ring_slots
-        while (unpacked.load(std::memory_order_acquire) < k - s.ring_slots + 1) {
-          HMSC_REQUIRE(!worker_failed.load(), "record unpack: " + worker_err);
-          std::this_thread::yield();
+      if (k >= s.ring_slots) {  // slot reuse: sample k - ring_slots must be unpacked
+        const int need = k - s.ring_slots + 1;
+        while (low < need && done[low].load(std::memory_order_acquire)) ++low;
+        if (low < need) {
+          std::unique_lock<std::mutex> lk(mu);
+          cv_done.wait(lk, [&] {
+            while (low < need && done[low].load(std::memory_order_acquire)) ++low;
+            return worker_failed.load() || low >= need;
+          });
+          if (worker_failed.load()) throw HmscError(-1, "record unpack: " + worker_err);
         }
       }
       double* dslot = s.ring + s.slot_doubles * slot;
       join_side(s);
       launch_record(s, dslot);
-      HIP_OK(hipEventRecord(packed[slot], s.stream));
-      HIP_OK(hipStreamWaitEvent(s.copy_stream, packed[slot], 0));
+      HIP_OK(hipEventRecord(s.ring_packed[slot], s.stream));
+      HIP_OK(hipStreamWaitEvent(s.copy_stream, s.ring_packed[slot], 0));
       HIP_OK(hipMemcpyAsync(s.host_rec + s.slot_doubles * slot, dslot, sizeof(double) * s.slot_doubles,
                             hipMemcpyDeviceToHost, s.copy_stream));
-      HIP_OK(hipEventRecord(s.ring_done[slot], s.copy_stream));
-      issued.store(k + 1, std::memory_order_release);
+      launch_copied_flag(s, (uint64_t)k + 1);
     }
     if (verbose > 0 && it % verbose == 0) {
       HIP_OK(hipStreamSynchronize(s.stream));
@@ -814,12 +910,12 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
   join_side(s);
   HIP_OK(hipStreamSynchronize(s.stream));
   HIP_OK(hipStreamSynchronize(s.copy_stream));
-  for (auto& e : packed) HIP_OK(hipEventDestroy(e));
   int flag[2] = {0, 0};
   HIP_OK(hipMemcpy(flag, s.dev_flags, sizeof(flag), hipMemcpyDeviceToHost));
   HMSC_REQUIRE(flag[0] == 0 && flag[1] == 0, "a Cholesky factorisation failed (matrix not positive definite)");
   if (recording) {
-    worker.join();
+    for (auto& th : workers) th.join();
+    std::lock_guard<std::mutex> lk(mu);
     HMSC_REQUIRE(!worker_failed.load(), "record unpack: " + worker_err);
   }
 }
@@ -892,6 +988,7 @@ int hmsc_init_state(hmsc_state* h, const int32_t* nf0) {
     s.refresh_dims();
     HMSC_REQUIRE(s.K <= s.Kmax, "init: K exceeds 64");
     launch_init(s);
+    s.graph_dirty = true;
     s.xeta_valid = false;
     launch_update_z(s, 0, true);  // Z = updateZ(Y=hM$Y, ...) (R/computeInitialParameters.R:254)
     HIP_OK(hipStreamSynchronize(s.stream));
@@ -931,6 +1028,7 @@ int hmsc_set_noise_mode(hmsc_state* h, int32_t mode) {
     State& s = h->s;
     DeviceGuard dg(s.device);
     s.noise_mode = mode & 1;
+    s.graph_dirty = true;
     if ((mode & 2) && !s.dbg_prec) s.dbg_prec = dalloc<double>((size_t)s.nsl * s.Kmax * s.Kmax);
     if (!(mode & 2) && s.dbg_prec) {
       HIP_OK(hipStreamSynchronize(s.stream));

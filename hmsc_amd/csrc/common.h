@@ -28,6 +28,10 @@ struct HmscError : std::runtime_error {
 
 constexpr int WAVE = 64;
 
+// Philox sweep counter of a kernel-argument struct: the value passed at launch, or -- for
+// launches captured into the per-sweep hipGraph -- the device word the graph advances.
+#define SWEEP_ITER(a) ((a).iter_dev ? *(a).iter_dev : (a).iter)
+
 // Diagnostic build only (python -m hmsc_amd.build --stamps -> libhmsc_amd_stamps.so):
 // HMSC_STAMP(i) records the shader clock (s_memtime) of lane 0 of the calling workgroup
 // into slot i of a device table read back with hmsc_debug_get(s, "stamps", ...).  The

@@ -216,6 +216,7 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   a.ZTr_part = s.ZTr_part;
   a.key = s.key;
   a.iter = iter;
+  a.iter_dev = s.capturing ? s.d_iter : nullptr;
   a.noise_zero = s.noise_mode;
   dim3 grid(nchunk, s.ntile_j);
   const size_t smem = z_smem_bytes(s.K, s.nt);
@@ -291,6 +292,7 @@ struct BLArgs {
   double* dbg_prec;
   Key key;
   uint32_t iter;
+  const uint32_t* iter_dev;  // graph replay: the sweep counter is read from the device
   int noise_zero;
 };
 
@@ -346,7 +348,7 @@ __global__ __launch_bounds__(64) void beta_lambda_kernel(BLArgs a) {
   wg_chol(A, K, K, flag);                 // RiU = chol(iU)  (:98)
   wg_forward(A, K, K, rhs);               // y = L^-1 rhs
   for (int r = t; r < K; r += 64) {
-    const double xi = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)(a.sp0 + j), (uint32_t)r, S_BETALAMBDA, a.iter);
+    const double xi = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)(a.sp0 + j), (uint32_t)r, S_BETALAMBDA, SWEEP_ITER(a));
     rhs[r] += xi;
   }
   __syncthreads();
@@ -410,7 +412,7 @@ __global__ __launch_bounds__(256) void beta_lambda_wave_kernel(BLArgs a) {
   double dinv;
   wv_chol<NM>(x, dinv);                    // RiU = chol(iU)  (:98)
   wv_forward<NM>(x, dinv, r);              // y = L^-1 rhs
-  if (i < K && !a.noise_zero) r += normal(a.key, (uint32_t)(a.sp0 + j), (uint32_t)i, S_BETALAMBDA, a.iter);
+  if (i < K && !a.noise_zero) r += normal(a.key, (uint32_t)(a.sp0 + j), (uint32_t)i, S_BETALAMBDA, SWEEP_ITER(a));
   double lt[NM];
   wv_transpose<NM, true>(x, lt, lds);
   wv_backward_t<NM>(lt, dinv, r);          // m + backsolve(RiU, xi)  (:101)
@@ -449,6 +451,7 @@ void launch_beta_lambda(State& s, uint32_t iter) {
   a.dbg_prec = s.dbg_prec;
   a.key = s.key;
   a.iter = iter;
+  a.iter_dev = s.capturing ? s.d_iter : nullptr;
   a.noise_zero = s.noise_mode;
   ProfScope ps(s, PROF_BL);
   if (s.K <= 32) {
@@ -548,6 +551,7 @@ struct GVArgs {
   double* scratch;
   Key key;
   uint32_t iter;
+  const uint32_t* iter_dev;  // graph replay: the sweep counter is read from the device
   int noise_zero;
   int* fail;
   int use_lds;
@@ -584,7 +588,7 @@ __global__ __launch_bounds__(256) void gammav_final_kernel(GVArgs a) {
   wg_copy(A, Vn, nc * nc);
   wg_chol(A, nc, nc, &flag);                      // CC = chol(Vn)
   wg_lower_only(A, nc, nc);
-  wg_rwish(A, nc, a.f0 + a.ns_glob, iVl, T, Zb, a.key, S_WISHART_DIAG, S_WISHART_OFF, a.iter, a.noise_zero);  // (:20)
+  wg_rwish(A, nc, a.f0 + a.ns_glob, iVl, T, Zb, a.key, S_WISHART_DIAG, S_WISHART_OFF, SWEEP_ITER(a), a.noise_zero);  // (:20)
   for (int p = t; p < nc * nc; p += blockDim.x) a.iV[p] = iVl[p];
   // Gamma | iV: prec = iUGamma + kron(Tr'Tr, iV); rhs = iUGamma mGamma + vec(iV B Tr)   (:29-31)
   for (int p = t; p < N * N; p += blockDim.x) {
@@ -602,7 +606,7 @@ __global__ __launch_bounds__(256) void gammav_final_kernel(GVArgs a) {
   wg_chol(Pm, N, N, &flag);
   wg_forward(Pm, N, N, rhs);
   for (int r = t; r < N; r += blockDim.x)
-    rhs[r] += a.noise_zero ? 0.0 : normal(a.key, (uint32_t)r, 0, S_GAMMAV, a.iter);
+    rhs[r] += a.noise_zero ? 0.0 : normal(a.key, (uint32_t)r, 0, S_GAMMAV, SWEEP_ITER(a));
   __syncthreads();
   wg_backward_t(Pm, N, N, rhs);
   for (int r = t; r < N; r += blockDim.x) a.Gamma[r] = rhs[r];
@@ -635,6 +639,7 @@ struct GVWArgs {
   double* prep;
   Key key;
   uint32_t iter;
+  const uint32_t* iter_dev;  // graph replay: the sweep counter is read from the device
   int noise_zero;
   int* fail;
 };
@@ -693,9 +698,9 @@ __global__ __launch_bounds__(256) void gammav_wave_kernel(GVWArgs a) {
       double zz = (ii == k && ii < NM) ? 1.0 : 0.0;
       if (ii < nc && k < nc) {
         if (k == ii)
-          zz = sqrt(2.0 * gamma_std(a.key, (uint32_t)ii, S_WISHART_DIAG, a.iter, 0.5 * (v - ii)));
+          zz = sqrt(2.0 * gamma_std(a.key, (uint32_t)ii, S_WISHART_DIAG, SWEEP_ITER(a), 0.5 * (v - ii)));
         else if (k > ii)
-          zz = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)(ii + nc * k), 0, S_WISHART_OFF, a.iter);
+          zz = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)(ii + nc * k), 0, S_WISHART_OFF, SWEEP_ITER(a));
         else
           zz = 0.0;
       }
@@ -733,7 +738,7 @@ __global__ __launch_bounds__(256) void gammav_wave_kernel(GVWArgs a) {
   }
   ok &= wv_chol<NM>(x, dinv);
   wv_forward<NM>(x, dinv, r);
-  if (i < N && !a.noise_zero) r += normal(a.key, (uint32_t)i, 0, S_GAMMAV, a.iter);
+  if (i < N && !a.noise_zero) r += normal(a.key, (uint32_t)i, 0, S_GAMMAV, SWEEP_ITER(a));
   wv_transpose<NM, true>(x, y, S);
   wv_backward_t<NM>(y, dinv, r);
   if (i < N) a.Gamma[i] = r;
@@ -832,6 +837,7 @@ void launch_gamma_v(State& s, uint32_t iter, hipStream_t st) {
     w.prep = s.g2prep;
     w.key = s.key;
     w.iter = iter;
+    w.iter_dev = s.capturing ? s.d_iter : nullptr;
     w.noise_zero = s.noise_mode;
     w.fail = s.dev_flags;
     switch (wv_bucket(Ng)) {
@@ -861,6 +867,7 @@ void launch_gamma_v(State& s, uint32_t iter, hipStream_t st) {
   a.scratch = s.scratch;
   a.key = s.key;
   a.iter = iter;
+  a.iter_dev = s.capturing ? s.d_iter : nullptr;
   a.noise_zero = s.noise_mode;
   a.fail = s.dev_flags;
   const size_t need = (6 * (size_t)s.nc * s.nc + (size_t)s.nc * s.nt + (size_t)s.nc * s.nt * s.nc * s.nt +
@@ -1034,6 +1041,7 @@ struct G2Args {
   double* Gamma;
   Key key;
   uint32_t iter;
+  const uint32_t* iter_dev;  // graph replay: the sweep counter is read from the device
   int noise_zero;
 };
 
@@ -1098,7 +1106,7 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
         LTr[p - n1] = s;
     }
   }
-  for (int r = t; r < N; r += blockDim.x) xi[r] = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)r, 0, S_GAMMA2, a.iter);
+  for (int r = t; r < N; r += blockDim.x) xi[r] = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)r, 0, S_GAMMA2, SWEEP_ITER(a));
   __syncthreads();
   HMSC_STAMP(31);
   // XZT = X^T Z Tr - sum_r (X^T Eta_r[Pi]) (Lambda_r Tr)   (:46 with S = Z - sum LRan)
@@ -1189,6 +1197,7 @@ void launch_gamma2(State& s, uint32_t iter) {
   a.Gamma = s.Gamma;
   a.key = s.key;
   a.iter = iter;
+  a.iter_dev = s.capturing ? s.d_iter : nullptr;
   a.noise_zero = s.noise_mode;
   const size_t N = (size_t)s.nc * s.nt, stage_bytes = (2 * (size_t)s.nc * s.nc + 2 * N * N) * sizeof(double);
   a.stage = stage_bytes <= 48 * 1024;
@@ -1211,6 +1220,7 @@ struct LPArgs {
   int ns_glob;
   Key key;
   uint32_t iter;
+  const uint32_t* iter_dev;  // graph replay: the sweep counter is read from the device
 };
 
 __global__ __launch_bounds__(256) void psi_kernel(LPArgs a) {
@@ -1249,7 +1259,7 @@ __global__ __launch_bounds__(256) void psi_kernel(LPArgs a) {
       const double shape = a.nu[r] / 2 + 0.5;
       const double rate = a.nu[r] / 2 + 0.5 * lam2 * sTau[f];            // (:22)
       const uint32_t idx = (uint32_t)(h + a.lev_nf[r] * (a.sp0 + j));
-      const double psi = gamma_std(a.key, idx, S_PSI + LEVEL_STRIDE * r, a.iter, shape) / rate;  // (:23)
+      const double psi = gamma_std(a.key, idx, S_PSI + LEVEL_STRIDE * r, SWEEP_ITER(a), shape) / rate;  // (:23)
       a.Psi[f + (size_t)NF * j] = psi;
       m = psi * lam2;                                                     // M = psi*lambda^2 (:24)
     }
@@ -1314,7 +1324,7 @@ __global__ __launch_bounds__(64) void delta_kernel(LPArgs a, const double* rs_pa
     }
     const double ad = (h == 0 ? a.a1[r] : a.a2[r]) + 0.5 * ns * (nf - h);
     const double bd = (h == 0 ? a.b1[r] : a.b2[r]) + 0.5 * sum / delta[h];
-    const double g = wave_gamma_std(a.key, (uint32_t)h, stream, a.iter, ad) / bd;
+    const double g = wave_gamma_std(a.key, (uint32_t)h, stream, SWEEP_ITER(a), ad) / bd;
     __syncthreads();
     if (t == 0) delta[h] = g;
     __syncthreads();
@@ -1350,6 +1360,7 @@ void launch_lambda_priors(State& s, uint32_t iter, hipStream_t st) {
   a.rs_part = s.psi_rs;
   a.key = s.key;
   a.iter = iter;
+  a.iter_dev = s.capturing ? s.d_iter : nullptr;
   const int nparts = std::min(LP_PARTS, std::max(1, s.nsl));
   psi_kernel<<<nparts, 256, 0, st>>>(a);
   HIP_OK(hipGetLastError());
@@ -1472,6 +1483,7 @@ struct EtaArgs {
   double* Eta;            // np x nf
   Key key;
   uint32_t iter;
+  const uint32_t* iter_dev;  // graph replay: the sweep counter is read from the device
   int noise_zero;
 };
 
@@ -1518,7 +1530,7 @@ __global__ __launch_bounds__(64) void eta_unit_kernel(EtaArgs a) {
   wg_chol(Q, nf, nf, flag);                         // RiV = chol(iV)
   wg_forward(Q, nf, nf, b);
   for (int h = t; h < nf; h += 64)
-    b[h] += a.noise_zero ? 0.0 : normal(a.key, (uint32_t)q, (uint32_t)h, S_ETA + LEVEL_STRIDE * a.r, a.iter);
+    b[h] += a.noise_zero ? 0.0 : normal(a.key, (uint32_t)q, (uint32_t)h, S_ETA + LEVEL_STRIDE * a.r, SWEEP_ITER(a));
   __syncthreads();
   wg_backward_t(Q, nf, nf, b);                      // mu + t(backsolve(RiV, xi))
   for (int h = t; h < nf; h += 64) a.Eta[q + (size_t)a.np * h] = b[h];
@@ -1585,7 +1597,7 @@ __global__ __launch_bounds__(64) void eta_shared_kernel(EtaArgs a, int nrow) {
   }
 #pragma unroll
   for (int h = 0; h < NFB; ++h)
-    if (h < nf && !a.noise_zero) b[h] += normal(a.key, (uint32_t)q, (uint32_t)h, S_ETA + LEVEL_STRIDE * a.r, a.iter);
+    if (h < nf && !a.noise_zero) b[h] += normal(a.key, (uint32_t)q, (uint32_t)h, S_ETA + LEVEL_STRIDE * a.r, SWEEP_ITER(a));
   if (blockIdx.x == 0) HMSC_STAMP(43);
 #pragma unroll
   for (int h = NFB - 1; h >= 0; --h) {
@@ -1660,6 +1672,7 @@ struct EtaFArgs {
   int ny, ns_loc, K, Kmax, nc, nf, np, ldcr;
   Key key;
   uint32_t iter;
+  const uint32_t* iter_dev;  // graph replay: the sweep counter is read from the device
   int noise_zero;
 };
 
@@ -1749,7 +1762,7 @@ __global__ __launch_bounds__(512) void eta_fused_kernel(EtaFArgs a) {
     double corr = 0.0, xi = 0.0;
     if (ii < ny) {
       for (int k = 0; k < nc; ++k) corr = fma(a.XEta[ii + (size_t)ny * k], sCR[k * NFB + h], corr);
-      xi = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)a.Pi[ii], (uint32_t)h, S_ETA, a.iter);
+      xi = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)a.Pi[ii], (uint32_t)h, S_ETA, SWEEP_ITER(a));
     }
     sB[h][s2] = zl - corr;
     sXi[h][s2] = xi;
@@ -1849,6 +1862,7 @@ static void launch_eta_fused(State& s, uint32_t iter) {
   a.ldcr = s.Kmax;
   a.key = s.key;
   a.iter = iter;
+  a.iter_dev = s.capturing ? s.d_iter : nullptr;
   a.noise_zero = s.noise_mode;
   const int ntile = (s.ny + EF_SITES - 1) / EF_SITES;
   {
@@ -1936,6 +1950,7 @@ void launch_eta(State& s, uint32_t iter) {
     a.Eta = L.Eta;
     a.key = s.key;
     a.iter = iter;
+    a.iter_dev = s.capturing ? s.d_iter : nullptr;
     a.noise_zero = s.noise_mode;
     if (s.n_na_rows > 0) {
       HMSC_REQUIRE(s.nranks == 1, "updateEta: NA rows with species sharding not supported");
@@ -1975,7 +1990,9 @@ void launch_eta(State& s, uint32_t iter) {
 __global__ __launch_bounds__(256) void inv_sigma_kernel(EtaView ev, const double* XEta, int K, const double* BL, const double* Z,
                                                         const int8_t* Ycode, const int* varest,
                                                         const double* aSigma, const double* bSigma, int sp0,
-                                                        double* iSigma, Key key, uint32_t iter) {
+                                                        double* iSigma, Key key, uint32_t iter_h,
+                                                        const uint32_t* iter_dev) {
+  const uint32_t iter = iter_dev ? *iter_dev : iter_h;
   __shared__ double red[256];
   __shared__ int cnt[256];
   const int j = blockIdx.x, t = threadIdx.x, ny = ev.ny;
@@ -2011,7 +2028,8 @@ void launch_inv_sigma(State& s, uint32_t iter) {
   if (!s.any_var) return;
   if (!s.xeta_valid) launch_xeta(s);
   inv_sigma_kernel<<<s.nsl, 256, 0, s.stream>>>(make_view(s), s.XEta, s.K, s.BL, s.Z, s.Ycode, s.varest, s.aSigma,
-                                                 s.bSigma, s.sp0, s.iSigma, s.key, iter);
+                                                 s.bSigma, s.sp0, s.iSigma, s.key, iter,
+                                                 s.capturing ? s.d_iter : nullptr);
   HIP_OK(hipGetLastError());
 }
 
@@ -2192,6 +2210,18 @@ __global__ __launch_bounds__(256) void pack_kernel(PackArgs a) {
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < pc.n; e += (int64_t)gridDim.x * blockDim.x)
       a.slot[pc.dst + e] = pc.src[e];
   }
+}
+
+// Publishes "samples < value have landed in the host ring" to the host with a system-scope
+// release store into fine-grained pinned memory; enqueued on the copy stream after the
+// sample's D2H copy, so the unpack threads poll memory instead of calling into HIP.
+__global__ void copied_flag_kernel(uint64_t* flag, uint64_t value) {
+  __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void launch_copied_flag(State& s, uint64_t value) {
+  copied_flag_kernel<<<1, 1, 0, s.copy_stream>>>(s.copied_dev, value);
+  HIP_OK(hipGetLastError());
 }
 
 // slot layout: BL(K*nsl) | Psi(NF*nsl) | Delta(NF) | Gamma(nc*nt) | iV(nc*nc) | iSigma(nsl) | Eta_r ... | rho(1)

@@ -115,9 +115,21 @@ struct State {
   double* ring = nullptr;
   int ring_slots = 0;
   size_t slot_doubles = 0;
-  std::vector<hipEvent_t> ring_done;
+  std::vector<hipEvent_t> ring_packed;  // pack kernel of slot i done (copy stream waits on it)
   double* host_rec = nullptr;    // pinned host ring (ring_slots slots)
-  size_t host_rec_doubles = 0;
+  uint64_t* copied_host = nullptr;  // fine-grained pinned counter: samples whose D2H copy landed
+  uint64_t* copied_dev = nullptr;   // its device address
+
+  // per-sweep hipGraph (single rank, no updateNf): captured once, replayed every sweep; the
+  // kernels read the Philox sweep counter from d_iter, which the graph's first node advances
+  uint32_t* d_iter = nullptr;
+  bool capturing = false;
+  bool use_graph = true;
+  bool graph_dirty = true;
+  int graph_K = -1, graph_NF = -1;
+  hipGraphExec_t gexec = nullptr;
+  uint32_t graph_next_iter = 0;  // the iter the next replay will use (0: unknown, re-seed)
+  int eager_streak = 0;          // eager steady sweeps since the graph was invalidated
 
   // live kernel timing (HIP events on this chain's stream), id -> launches
   bool prof = false;
@@ -183,6 +195,7 @@ void launch_lambda_priors(State& s, uint32_t iter, hipStream_t st);
 void launch_eta(State& s, uint32_t iter);
 void launch_inv_sigma(State& s, uint32_t iter);
 void launch_record(State& s, double* slot);
+void launch_copied_flag(State& s, uint64_t value);
 size_t record_slot_doubles(const State& s);
 void read_stamps(double* out, int n);  // diagnostic build (HMSC_STAMPS)
 

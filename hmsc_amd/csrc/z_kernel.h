@@ -38,6 +38,7 @@ struct ZArgs {
   double* ZTr_part;  // [species block][ny x nt]
   Key key;
   uint32_t iter;
+  const uint32_t* iter_dev;  // graph replay: the sweep counter is read from the device
   int noise_zero;
 };
 
@@ -168,7 +169,7 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
       for (int c = 0; c < 4; ++c) {
         const int m = 4 * c + lk, ja = j0 + 2 * m;
         Uniform2 u{0.0, 0.0};
-        if (DRAW) u = uniforms(a.key, (uint32_t)((size_t)i + (size_t)ny * (uint32_t)((a.sp0 + ja) >> 1)), 0, S_Z, a.iter);
+        if (DRAW) u = uniforms(a.key, (uint32_t)((size_t)i + (size_t)ny * (uint32_t)((a.sp0 + ja) >> 1)), 0, S_Z, SWEEP_ITER(a));
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
           const int jj = 2 * m + b, j = ja + b;
