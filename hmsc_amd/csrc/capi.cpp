@@ -384,12 +384,17 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   HIP_OK(hipHostMalloc(&s.host_rec, sizeof(double) * s.slot_doubles * s.ring_slots, hipHostMallocDefault));
   HIP_OK(hipHostMalloc(&s.copied_host, 64, hipHostMallocMapped | hipHostMallocCoherent));
   HIP_OK(hipHostGetDevicePointer((void**)&s.copied_dev, s.copied_host, 0));
-  for (int i = 0; i < s.ring_slots; ++i) {
-    hipEvent_t e;
-    HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    s.ring_packed.push_back(e);
+  s.d_rec_desc = dalloc<int32_t>(4);
+  s.d_iter_side = dalloc<uint32_t>(1);
+  s.gv_part = dalloc<double>((size_t)((nsl + 31) / 32) * (nc * nc + nc * nt));
+  HIP_OK(hipEventCreateWithFlags(&s.ev_graph, hipEventDisableTiming));
+  {
+    const char* g = getenv("HMSC_GRAPH_SWEEPS");
+    s.graph_sweeps = g ? std::max(1, std::min(64, atoi(g))) : 4;
   }
   {
+    const char* g1 = getenv("HMSC_SINGLE_STREAM");
+    s.single_stream = g1 && g1[0] == '1';
     const char* g = getenv("HMSC_NO_GRAPH");
     s.use_graph = !(g && g[0] && g[0] != '0');
   }
@@ -412,7 +417,10 @@ static void free_state(State& s) {
     for (void* p : lp)
       if (p) (void)hipFree(p);
   }
-  for (hipEvent_t e : s.ring_packed) (void)hipEventDestroy(e);
+  if (s.ev_graph) (void)hipEventDestroy(s.ev_graph);
+  if (s.d_rec_desc) (void)hipFree(s.d_rec_desc);
+  if (s.d_iter_side) (void)hipFree(s.d_iter_side);
+  if (s.gv_part) (void)hipFree(s.gv_part);
   if (s.host_rec) (void)hipHostFree(s.host_rec);
   if (s.copied_host) (void)hipHostFree(s.copied_host);
   if (s.gexec) (void)hipGraphExecDestroy(s.gexec);
@@ -429,12 +437,17 @@ static void free_state(State& s) {
 
 // Wait on the main stream for the side-stream work of the previous sweep (it writes Gamma,
 // iV, Psi, Delta and Gamma2's iV-only matrices).
-static void join_side(State& s) {
-  if (s.side_pending) {
+// The main stream waits for everything enqueued on the side streams so far.
+void join_side(State& s) {
+  if (s.side_pending & 1) {
+    HIP_OK(hipEventRecord(s.ev_side, s.side));
     HIP_OK(hipStreamWaitEvent(s.stream, s.ev_side, 0));
-    HIP_OK(hipStreamWaitEvent(s.stream, s.ev_side2, 0));
-    s.side_pending = false;
   }
+  if (s.side_pending & 2) {
+    HIP_OK(hipEventRecord(s.ev_side2, s.side2));
+    HIP_OK(hipStreamWaitEvent(s.stream, s.ev_side2, 0));
+  }
+  s.side_pending = 0;
 }
 
 // ---------------------------- state get / set ----------------------------
@@ -667,58 +680,90 @@ static void run_updater(State& s, uint32_t which, uint32_t iter) {
 // so they run on the side stream after BetaLambda, overlapped with Eta / InvSigma / Z.
 static void sweep(State& s, uint32_t iter, bool adapt) {
   ProfScope ps(s, PROF_SWEEP);
-  join_side(s);
+  // co-launched side updaters (launch_side_fused): the GammaV algebra of the previous sweep
+  // may still run on the side stream; Gamma2 joins it before its final stage
+  const bool fused = s.nranks == 1 && side_fusion_ok(s);
+  if (!fused) join_side(s);
   if (s.mask & HMSC_UP_GAMMA2) run_updater(s, HMSC_UP_GAMMA2, iter);
   if (s.mask & HMSC_UP_GAMMAETA) run_updater(s, HMSC_UP_GAMMAETA, iter);
+  join_side(s);  // BetaLambda reads Gamma and iV
   if (s.mask & HMSC_UP_BETALAMBDA) run_updater(s, HMSC_UP_BETALAMBDA, iter);
-  // (sharded chains keep every RCCL collective on one stream: no side-stream overlap)
-  const bool side_work = s.nranks == 1 && (s.mask & (HMSC_UP_GAMMAV | HMSC_UP_LAMBDAPRIORS)) != 0;
-  if (side_work) {
-    HIP_OK(hipEventRecord(s.ev_bl, s.stream));
-    HIP_OK(hipStreamWaitEvent(s.side, s.ev_bl, 0));
-    HIP_OK(hipStreamWaitEvent(s.side2, s.ev_bl, 0));
-    if (s.mask & HMSC_UP_GAMMAV) launch_gamma_v(s, iter, s.side);
-    if (s.mask & HMSC_UP_LAMBDAPRIORS) launch_lambda_priors(s, iter, s.side2);
-    HIP_OK(hipEventRecord(s.ev_side, s.side));
-    HIP_OK(hipEventRecord(s.ev_side2, s.side2));
-    s.side_pending = true;
+  s.side_fused = fused;
+  if (fused) {
+    launch_side_fused(s, iter);
+    for (uint32_t u : {HMSC_UP_ALPHA, HMSC_UP_INVSIGMA, HMSC_UP_Z})
+      if (s.mask & u) run_updater(s, u, iter);
   } else {
-    if (s.mask & HMSC_UP_GAMMAV) launch_gamma_v(s, iter, s.stream);
-    if (s.mask & HMSC_UP_LAMBDAPRIORS) launch_lambda_priors(s, iter, s.stream);
+    // (sharded chains keep every RCCL collective on one stream: no side-stream overlap)
+    const bool side_work = s.nranks == 1 && !s.single_stream && (s.mask & (HMSC_UP_GAMMAV | HMSC_UP_LAMBDAPRIORS)) != 0;
+    if (side_work) {
+      HIP_OK(hipEventRecord(s.ev_bl, s.stream));
+      HIP_OK(hipStreamWaitEvent(s.side, s.ev_bl, 0));
+      HIP_OK(hipStreamWaitEvent(s.side2, s.ev_bl, 0));
+      if (s.mask & HMSC_UP_GAMMAV) launch_gamma_v(s, iter, s.side);
+      if (s.mask & HMSC_UP_LAMBDAPRIORS) launch_lambda_priors(s, iter, s.side2);
+      s.side_pending = 3;
+    } else {
+      if (s.mask & HMSC_UP_GAMMAV) launch_gamma_v(s, iter, s.stream);
+      if (s.mask & HMSC_UP_LAMBDAPRIORS) launch_lambda_priors(s, iter, s.stream);
+    }
+    for (uint32_t u : {HMSC_UP_ETA, HMSC_UP_ALPHA, HMSC_UP_INVSIGMA, HMSC_UP_Z})
+      if (s.mask & u) run_updater(s, u, iter);
   }
-  for (uint32_t u : {HMSC_UP_ETA, HMSC_UP_ALPHA, HMSC_UP_INVSIGMA, HMSC_UP_Z})
-    if (s.mask & u) run_updater(s, u, iter);
   if (adapt) {
     join_side(s);
     for (int r = 0; r < s.nr; ++r) update_nf(s, r, iter);
   }
 }
 
-// ---------------------------- per-sweep hipGraph ----------------------------
-// A steady-state sweep (no updateNf, one rank) is captured once into a graph and replayed:
-// one launch per sweep instead of ~20 kernel launches + event records, so the GPU no longer
-// waits on the host between dependent kernels.  Kernels captured with s.capturing read the
-// Philox sweep counter from s.d_iter; the graph's first node advances it.
+// ---------------------------- sweep hipGraphs ----------------------------
+// Steady-state sweeps (no updateNf, one rank) are captured once into graphs of
+// s.graph_sweeps consecutive sweeps and replayed: one launch per graph_sweeps sweeps instead
+// of ~20 kernel launches + event records per sweep, and the relaunch gap between replays is
+// paid once per replay.  Kernels captured with s.capturing read the Philox sweep counter
+// from s.d_iter; each captured sweep starts by advancing it.  gexec_rec is the same sequence
+// with the record pack after every sweep; the pack picks its ring slot (or returns, for a
+// sweep that is not recorded) from d_iter and the run descriptor d_rec_desc.
+// Pack the state after a sweep into a ring slot (nullptr: chosen on the device in a graph
+// replay).  With co-launched side updaters the side stream's outputs are packed on it, so
+// the main stream need not wait for the GammaV algebra.
+static void record_after_sweep(State& s, double* slot) {
+  if (s.side_fused && (s.side_pending & 1)) {
+    launch_record(s, slot, 1);
+    launch_record(s, slot, 2);
+  } else {
+    join_side(s);
+    launch_record(s, slot, 0);
+  }
+}
+
 __global__ void set_iter_kernel(uint32_t* p, uint32_t v) { *p = v; }
 __global__ void advance_iter_kernel(uint32_t* p) { *p += 1u; }
+__global__ void set_desc_kernel(int32_t* d, int32_t iter0, int32_t transient, int32_t thin, int32_t samples) {
+  d[0] = iter0, d[1] = transient, d[2] = thin, d[3] = samples;
+}
 
 static void destroy_graph(State& s) {
   if (s.gexec) (void)hipGraphExecDestroy(s.gexec);
-  s.gexec = nullptr;
+  if (s.gexec_rec) (void)hipGraphExecDestroy(s.gexec_rec);
+  s.gexec = s.gexec_rec = nullptr;
 }
 
-// Captures one sweep.  Returns false (and leaves no graph) when the sweep is not in a
-// steady state, i.e. the host-side validity flags it changes would differ on the next sweep.
-static bool build_sweep_graph(State& s, uint32_t iter) {
-  destroy_graph(s);
+// Captures graph_sweeps sweeps (with or without the record pack after each).  Returns
+// nullptr when the sweep is not in a steady state, i.e. the host-side validity flags it
+// changes would differ on the next sweep.
+static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record) {
   join_side(s);
   const bool xv = s.xeta_valid, zv = s.zt_valid, gv = s.g2prep_valid;
   hipGraph_t g = nullptr;
   HIP_OK(hipStreamBeginCapture(s.stream, hipStreamCaptureModeThreadLocal));
   s.capturing = true;
   try {
-    advance_iter_kernel<<<1, 1, 0, s.stream>>>(s.d_iter);
-    sweep(s, iter, false);
+    for (int i = 0; i < s.graph_sweeps; ++i) {
+      advance_iter_kernel<<<1, 1, 0, s.stream>>>(s.d_iter);
+      sweep(s, iter, false);
+      if (with_record) record_after_sweep(s, nullptr);
+    }
     join_side(s);
   } catch (...) {
     s.capturing = false;
@@ -731,39 +776,45 @@ static bool build_sweep_graph(State& s, uint32_t iter) {
   HIP_OK(hipStreamEndCapture(s.stream, &g));
   const bool steady = xv == s.xeta_valid && zv == s.zt_valid && gv == s.g2prep_valid;
   s.xeta_valid = xv, s.zt_valid = zv, s.g2prep_valid = gv;  // nothing ran yet
-  if (!steady) {
-    (void)hipGraphDestroy(g);
+  hipGraphExec_t ge = nullptr;
+  if (steady) HIP_OK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  HIP_OK(hipGraphDestroy(g));
+  return ge;
+}
+
+static bool build_sweep_graphs(State& s, uint32_t iter) {
+  destroy_graph(s);
+  s.gexec = capture_sweeps(s, iter, false);
+  if (!s.gexec) return false;
+  s.gexec_rec = capture_sweeps(s, iter, true);
+  if (!s.gexec_rec) {
+    destroy_graph(s);
     return false;
   }
-  HIP_OK(hipGraphInstantiate(&s.gexec, g, nullptr, nullptr, 0));
-  HIP_OK(hipGraphDestroy(g));
   s.graph_K = s.K;
   s.graph_NF = s.NF;
   s.graph_dirty = false;
   return true;
 }
 
-// One sweep of the run loop: a graph replay when possible, else the eager launch sequence.
-static void run_sweep(State& s, uint32_t iter, bool adapt) {
-  const bool graphable = s.use_graph && s.nranks == 1 && !s.prof && !adapt;
-  if (!graphable) {
-    sweep(s, iter, adapt);
-    s.eager_streak = adapt ? 0 : s.eager_streak + 1;
-    return;
-  }
+// Runs sweeps iter .. iter+n-1 (n == graph_sweeps) as one graph replay if the graphs exist
+// or can be built now; returns false (nothing launched) when the caller must run eagerly.
+static bool replay_sweeps(State& s, uint32_t iter, bool with_record) {
+  if (!s.use_graph || s.nranks != 1 || s.prof) return false;
   if (s.gexec && (s.graph_dirty || s.graph_K != s.K || s.graph_NF != s.NF)) destroy_graph(s);
   if (s.graph_dirty) s.eager_streak = 0, s.graph_dirty = false;
-  if (!s.gexec) {
-    if (s.eager_streak < 1 || !build_sweep_graph(s, iter)) {  // reach a steady state first
-      sweep(s, iter, false);
-      ++s.eager_streak;
-      return;
-    }
-  }
+  if (!s.gexec && (s.eager_streak < 1 || !build_sweep_graphs(s, iter))) return false;  // steady first
   join_side(s);
   if (s.graph_next_iter != iter) set_iter_kernel<<<1, 1, 0, s.stream>>>(s.d_iter, iter - 1u);
-  HIP_OK(hipGraphLaunch(s.gexec, s.stream));
-  s.graph_next_iter = iter + 1u;
+  HIP_OK(hipGraphLaunch(with_record ? s.gexec_rec : s.gexec, s.stream));
+  s.graph_next_iter = iter + (uint32_t)s.graph_sweeps;
+  return true;
+}
+
+static void eager_sweep(State& s, uint32_t iter, bool adapt) {
+  sweep(s, iter, adapt);
+  s.eager_streak = adapt ? 0 : s.eager_streak + 1;
+  s.graph_next_iter = 0;  // d_iter is stale
 }
 
 static void unpack_record(const State& s, const double* slot, int k, int samples, hmsc_record* rec) {
@@ -870,46 +921,89 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
       }
     });
   const int total = transient + samples * thin;
-  for (int it = 1; it <= total; ++it) {
-    const uint32_t iter = (uint32_t)(iter0 + it);
-    bool adapt = false;
-    if (adaptNf)
-      for (int r = 0; r < s.nr; ++r) adapt |= it <= adaptNf[r];
-    run_sweep(s, iter, adapt);
-    if (recording && it > transient && (it - transient) % thin == 0) {
-      const int k = (it - transient) / thin - 1;
-      const int slot = k % s.ring_slots;
-      if (k >= s.ring_slots) {  // slot reuse: sample k - ring_slots must be unpacked
-        const int need = k - s.ring_slots + 1;
+  auto recorded = [&](int it) { return recording && it > transient && (it - transient) % thin == 0; };
+  auto sample_of = [&](int it) { return (it - transient) / thin - 1; };
+  // slot reuse: before sample k is packed, sample k - ring_slots must be unpacked (which
+  // also means its copy landed, so the device slot is free as well)
+  auto wait_slot = [&](int k) {
+    const int need = k - s.ring_slots + 1;
+    if (need <= 0) return;
+    while (low < need && done[low].load(std::memory_order_acquire)) ++low;
+    if (low < need) {
+      std::unique_lock<std::mutex> lk(mu);
+      cv_done.wait(lk, [&] {
         while (low < need && done[low].load(std::memory_order_acquire)) ++low;
-        if (low < need) {
-          std::unique_lock<std::mutex> lk(mu);
-          cv_done.wait(lk, [&] {
-            while (low < need && done[low].load(std::memory_order_acquire)) ++low;
-            return worker_failed.load() || low >= need;
-          });
-          if (worker_failed.load()) throw HmscError(-1, "record unpack: " + worker_err);
+        return worker_failed.load() || low >= need;
+      });
+      if (worker_failed.load()) throw HmscError(-1, "record unpack: " + worker_err);
+    }
+  };
+  auto copy_out = [&](int k) {
+    const int slot = k % s.ring_slots;
+    HIP_OK(hipMemcpyAsync(s.host_rec + s.slot_doubles * slot, s.ring + s.slot_doubles * slot,
+                          sizeof(double) * s.slot_doubles, hipMemcpyDeviceToHost, s.copy_stream));
+  };
+  int max_adapt = 0;
+  if (adaptNf)
+    for (int r = 0; r < s.nr; ++r) max_adapt = std::max(max_adapt, adaptNf[r]);
+  if (recording) set_desc_kernel<<<1, 1, 0, s.stream>>>(s.d_rec_desc, iter0, transient, thin, samples);
+  const auto t_start = std::chrono::steady_clock::now();
+  for (int it = 1; it <= total;) {
+    const int G = s.graph_sweeps;
+    int n = 1;
+    bool replayed = false;
+    int kfirst = -1, klast = -1;
+    if (it > max_adapt && it + G - 1 <= total) {
+      for (int j = it; j < it + G; ++j)
+        if (recorded(j)) {
+          if (kfirst < 0) kfirst = sample_of(j);
+          klast = sample_of(j);
+        }
+      if (klast >= 0) wait_slot(klast);
+      if (replay_sweeps(s, (uint32_t)(iter0 + it), klast >= 0)) {
+        replayed = true;
+        n = G;
+        if (klast >= 0) {
+          HIP_OK(hipEventRecord(s.ev_graph, s.stream));
+          HIP_OK(hipStreamWaitEvent(s.copy_stream, s.ev_graph, 0));
+          for (int k = kfirst; k <= klast; ++k) copy_out(k);
+          launch_copied_flag(s, (uint64_t)klast + 1);
         }
       }
-      double* dslot = s.ring + s.slot_doubles * slot;
-      join_side(s);
-      launch_record(s, dslot);
-      HIP_OK(hipEventRecord(s.ring_packed[slot], s.stream));
-      HIP_OK(hipStreamWaitEvent(s.copy_stream, s.ring_packed[slot], 0));
-      HIP_OK(hipMemcpyAsync(s.host_rec + s.slot_doubles * slot, dslot, sizeof(double) * s.slot_doubles,
-                            hipMemcpyDeviceToHost, s.copy_stream));
-      launch_copied_flag(s, (uint64_t)k + 1);
     }
-    if (verbose > 0 && it % verbose == 0) {
+    if (!replayed) {
+      eager_sweep(s, (uint32_t)(iter0 + it), it <= max_adapt);
+      if (recorded(it)) {
+        const int k = sample_of(it);
+        wait_slot(k);
+        record_after_sweep(s, s.ring + s.slot_doubles * (k % s.ring_slots));
+        join_side(s);  // the copy below waits on the main stream only
+        HIP_OK(hipEventRecord(s.ev_graph, s.stream));
+        HIP_OK(hipStreamWaitEvent(s.copy_stream, s.ev_graph, 0));
+        copy_out(k);
+        launch_copied_flag(s, (uint64_t)k + 1);
+      }
+    }
+    if (verbose > 0 && (it + n - 1) / verbose > (it - 1) / verbose) {
       HIP_OK(hipStreamSynchronize(s.stream));
-      std::printf("[1] \"Chain %d, iteration %d of %d, (%s)\"\n", chain, it, total,
-                  it > transient ? "sampling" : "transient");
+      for (int j = it; j < it + n; ++j)
+        if (j % verbose == 0)
+          std::printf("[1] \"Chain %d, iteration %d of %d, (%s)\"\n", chain, j, total,
+                      j > transient ? "sampling" : "transient");
       std::fflush(stdout);
     }
+    it += n;
   }
   join_side(s);
+  const auto t_enq = std::chrono::steady_clock::now();
   HIP_OK(hipStreamSynchronize(s.stream));
   HIP_OK(hipStreamSynchronize(s.copy_stream));
+  if (getenv("HMSC_DIAG_TIMING")) {  // host run-ahead diagnostic: enqueue time vs total
+    const auto t_end = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[hmsc] run %d sweeps: enqueued in %.3f ms, done in %.3f ms\n", total,
+                 std::chrono::duration<double, std::milli>(t_enq - t_start).count(),
+                 std::chrono::duration<double, std::milli>(t_end - t_start).count());
+  }
   int flag[2] = {0, 0};
   HIP_OK(hipMemcpy(flag, s.dev_flags, sizeof(flag), hipMemcpyDeviceToHost));
   HMSC_REQUIRE(flag[0] == 0 && flag[1] == 0, "a Cholesky factorisation failed (matrix not positive definite)");
@@ -1012,7 +1106,7 @@ int hmsc_get_nf(hmsc_state* h, int32_t* nf) {
 int hmsc_sweep(hmsc_state* h, int32_t iter, int32_t adapt_nf) {
   return guarded([&] {
     DeviceGuard dg(h->s.device);
-    sweep(h->s, (uint32_t)iter, adapt_nf != 0);
+    eager_sweep(h->s, (uint32_t)iter, adapt_nf != 0);
   });
 }
 
@@ -1076,6 +1170,12 @@ int hmsc_debug_get(hmsc_state* h, const char* name, double* out, int64_t n) {
     else if (nm == "ZL") src = s.ZL_part, avail = (int64_t)s.zl_split * s.ny * s.NF;
     else if (nm == "stamps") {
       read_stamps(out, (int)n);
+      return;
+    } else if (nm == "graph") {
+      HMSC_REQUIRE(n >= 4, "graph needs 4 slots");
+      const double d[4] = {(double)(s.gexec != nullptr), (double)(s.gexec_rec != nullptr), (double)s.graph_sweeps,
+                           (double)s.eager_streak};
+      std::memcpy(out, d, sizeof(d));
       return;
     } else if (nm == "dims") {
       HMSC_REQUIRE(n >= 8, "dims needs 8 slots");

@@ -122,11 +122,13 @@ __global__ __launch_bounds__(256) void xeta_gram_kernel(EtaView ev, int K, int K
 
 // deterministic slab reduction: out[e] = sum_c part[c*stride + e]; 64 outputs per block,
 // the four waves take every fourth partial (coalesced 512-B rows), fixed summation order.
-__global__ __launch_bounds__(256) void slab_sum_kernel(const double* __restrict__ part, double* __restrict__ out,
-                                                       int64_t n, int nparts, int64_t stride) {
+// (bid, nb): this block's index among the nb blocks of the reduction (co-launched kernels
+// hand a slab reduction a sub-range of their grid).
+__device__ __forceinline__ void slab_sum_body(const double* __restrict__ part, double* __restrict__ out, int64_t n,
+                                              int nparts, int64_t stride, int bid, int nb) {
   __shared__ double red[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += (int64_t)gridDim.x * 64) {
+  for (int64_t base = (int64_t)bid * 64; base < n; base += (int64_t)nb * 64) {
     const int64_t e = base + lane;
     double s = 0.0;
     if (e < n) {
@@ -138,6 +140,26 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const double* __restrict_
     if (w == 0 && e < n) out[e] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
     __syncthreads();
   }
+}
+
+__global__ __launch_bounds__(256) void slab_sum_kernel(const double* __restrict__ part, double* __restrict__ out,
+                                                       int64_t n, int nparts, int64_t stride) {
+  slab_sum_body(part, out, n, nparts, stride, blockIdx.x, gridDim.x);
+}
+
+struct SlabJob {
+  const double* part;
+  double* out;
+  int64_t n, stride;
+  int nparts, nb;
+};
+
+// two independent slab reductions in one launch: blocks [0, j0.nb) reduce j0, the rest j1
+__global__ __launch_bounds__(256) void slab_sum2_kernel(SlabJob j0, SlabJob j1) {
+  if ((int)blockIdx.x < j0.nb)
+    slab_sum_body(j0.part, j0.out, j0.n, j0.nparts, j0.stride, blockIdx.x, j0.nb);
+  else
+    slab_sum_body(j1.part, j1.out, j1.n, j1.nparts, j1.stride, blockIdx.x - j0.nb, j1.nb);
 }
 
 static int grid_for(int64_t n, int block = 64, int cap = 2048) {
@@ -235,10 +257,11 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
     }
     HIP_OK(hipGetLastError());
   }
-  const int64_t nXZ = (int64_t)s.K * s.nsl;
-  slab_sum_kernel<<<grid_for(nXZ), 256, 0, s.stream>>>(s.XZ_part, s.XZ, nXZ, nchunk, nXZ);
-  const int64_t nZT = (int64_t)s.ny * s.nt;
-  slab_sum_kernel<<<grid_for(nZT), 256, 0, s.stream>>>(s.ZTr_part, s.ZTr, nZT, s.ntile_j, nZT);
+  // XZ and ZTr from their partials, one launch
+  const int64_t nXZ = (int64_t)s.K * s.nsl, nZT = (int64_t)s.ny * s.nt;
+  const SlabJob j0{s.XZ_part, s.XZ, nXZ, nXZ, nchunk, grid_for(nXZ)};
+  const SlabJob j1{s.ZTr_part, s.ZTr, nZT, nZT, s.ntile_j, grid_for(nZT)};
+  slab_sum2_kernel<<<j0.nb + j1.nb, 256, 0, s.stream>>>(j0, j1);
   HIP_OK(hipGetLastError());
 }
 
@@ -478,14 +501,13 @@ constexpr int SB = 32;  // species per block of the species-sum reductions
 
 // Species-block partial sums for updateGammaV (R/updateGammaV.R:16-18,30):
 //   A = E E^T (E = Beta - Gamma Tr^T) and BTr = Beta Tr, staged through LDS.
-__global__ __launch_bounds__(256) void gammav_partial_kernel(const double* BL, int K, int nc, int nt, int ns_loc,
-                                                             const double* Gamma, const double* Tr,
-                                                             double* part) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
+__device__ __forceinline__ void gammav_partial_body(const double* BL, int K, int nc, int nt, int ns_loc,
+                                                    const double* Gamma, const double* Tr, double* part,
+                                                    double* smem, int bid) {
   double* sB = smem;             // nc x SB
   double* sE = sB + nc * SB;     // nc x SB
   double* sTr = sE + nc * SB;    // SB x nt
-  const int t = threadIdx.x, j0 = blockIdx.x * SB, nj = min(SB, ns_loc - j0);
+  const int t = threadIdx.x, j0 = bid * SB, nj = min(SB, ns_loc - j0);
   for (int p = t; p < nc * nj; p += 256) {
     const int c = p % nc, jj = p / nc;
     sB[p] = BL[c + (size_t)K * (j0 + jj)];
@@ -503,7 +525,7 @@ __global__ __launch_bounds__(256) void gammav_partial_kernel(const double* BL, i
   }
   __syncthreads();
   const int nA = nc * nc, nB = nc * nt;
-  double* out = part + (size_t)blockIdx.x * (nA + nB);
+  double* out = part + (size_t)bid * (nA + nB);
   for (int p = t; p < nA + nB; p += 256) {
     double acc = 0.0;
     if (p < nA) {
@@ -515,6 +537,13 @@ __global__ __launch_bounds__(256) void gammav_partial_kernel(const double* BL, i
     }
     out[p] = acc;
   }
+}
+
+__global__ __launch_bounds__(256) void gammav_partial_kernel(const double* BL, int K, int nc, int nt, int ns_loc,
+                                                             const double* Gamma, const double* Tr,
+                                                             double* part) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  gammav_partial_body(BL, K, nc, nt, ns_loc, Gamma, Tr, part, smem, blockIdx.x);
 }
 
 // Bartlett draw of MCMCpack::rwish(v, S): W = (Zb CC)^T (Zb CC), CC = chol(S) upper,
@@ -799,22 +828,10 @@ __global__ __launch_bounds__(256) void gammav_wave_kernel(GVWArgs a) {
 }
 
 
-void launch_gamma_v(State& s, uint32_t iter, hipStream_t st) {
-  const int nparts = (s.nsl + SB - 1) / SB;
-  double* part = s.ABpart;
-  gammav_partial_kernel<<<nparts, 256, (size_t)(2 * s.nc * SB + SB * s.nt) * sizeof(double), st>>>(
-      s.BL, s.K, s.nc, s.nt, s.nsl, s.Gamma, s.Tr, part);
-  HIP_OK(hipGetLastError());
-  int np = nparts;
-  if (s.nranks > 1) {
-    const int64_t n = (int64_t)s.nc * s.nc + (int64_t)s.nc * s.nt;
-    slab_sum_kernel<<<grid_for(n), 256, 0, st>>>(part, s.allreduce_buf, n, nparts, n);
-    allreduce_sum(s, s.allreduce_buf, n, st);
-    part = s.allreduce_buf;
-    np = 1;
-  }
+static void launch_gammav_wave(State& s, uint32_t iter, hipStream_t st, const double* part, int np,
+                               const uint32_t* iter_dev) {
   const int Ng = s.nc * s.nt;
-  if (Ng <= 32) {
+  {
     GVWArgs w{};
     w.nc = s.nc;
     w.nt = s.nt;
@@ -837,7 +854,7 @@ void launch_gamma_v(State& s, uint32_t iter, hipStream_t st) {
     w.prep = s.g2prep;
     w.key = s.key;
     w.iter = iter;
-    w.iter_dev = s.capturing ? s.d_iter : nullptr;
+    w.iter_dev = iter_dev;
     w.noise_zero = s.noise_mode;
     w.fail = s.dev_flags;
     switch (wv_bucket(Ng)) {
@@ -848,6 +865,27 @@ void launch_gamma_v(State& s, uint32_t iter, hipStream_t st) {
     }
     HIP_OK(hipGetLastError());
     if (w.do_prep) s.g2prep_valid = true;
+  }
+}
+
+
+void launch_gamma_v(State& s, uint32_t iter, hipStream_t st) {
+  const int nparts = (s.nsl + SB - 1) / SB;
+  double* part = s.ABpart;
+  gammav_partial_kernel<<<nparts, 256, (size_t)(2 * s.nc * SB + SB * s.nt) * sizeof(double), st>>>(
+      s.BL, s.K, s.nc, s.nt, s.nsl, s.Gamma, s.Tr, part);
+  HIP_OK(hipGetLastError());
+  int np = nparts;
+  if (s.nranks > 1) {
+    const int64_t n = (int64_t)s.nc * s.nc + (int64_t)s.nc * s.nt;
+    slab_sum_kernel<<<grid_for(n), 256, 0, st>>>(part, s.allreduce_buf, n, nparts, n);
+    allreduce_sum(s, s.allreduce_buf, n, st);
+    part = s.allreduce_buf;
+    np = 1;
+  }
+  const int Ng = s.nc * s.nt;
+  if (Ng <= 32) {
+    launch_gammav_wave(s, iter, st, part, np, s.capturing ? s.d_iter : nullptr);
     return;
   }
   GVArgs a{};
@@ -1164,7 +1202,10 @@ void launch_gamma2(State& s, uint32_t iter) {
                "updateGamma2: nc*nt must be <= 256 in this build");
   if (!s.xeta_valid) launch_xeta(s);
   if (!s.zt_valid) launch_zt_refresh(s);
-  if (!s.g2prep_valid) launch_gamma2_prep(s, s.stream);
+  if (!s.g2prep_valid) {
+    join_side(s);
+    launch_gamma2_prep(s, s.stream);
+  }
   const int nparts = (s.nsl + SB - 1) / SB;
   gamma2_partial_kernel<<<nparts, 256, (size_t)(s.K * SB + SB * s.nt) * sizeof(double), s.stream>>>(
       s.XZ, s.BL, s.K, s.nc, s.NF, s.nt, s.nsl, s.Tr, s.ABpart);
@@ -1201,6 +1242,7 @@ void launch_gamma2(State& s, uint32_t iter) {
   a.noise_zero = s.noise_mode;
   const size_t N = (size_t)s.nc * s.nt, stage_bytes = (2 * (size_t)s.nc * s.nc + 2 * N * N) * sizeof(double);
   a.stage = stage_bytes <= 48 * 1024;
+  join_side(s);  // iV and the prep matrices come from the previous sweep's GammaV (side stream)
   gamma2_final_kernel<<<1, 256, a.stage ? stage_bytes : 0, s.stream>>>(a);
   HIP_OK(hipGetLastError());
 }
@@ -1223,7 +1265,7 @@ struct LPArgs {
   const uint32_t* iter_dev;  // graph replay: the sweep counter is read from the device
 };
 
-__global__ __launch_bounds__(256) void psi_kernel(LPArgs a) {
+__device__ __forceinline__ void psi_body(const LPArgs& a, int bid, int nb) {
   // grid over species columns; each block handles a contiguous species range
   __shared__ double sM[256];
   __shared__ double sTau[64];
@@ -1243,10 +1285,10 @@ __global__ __launch_bounds__(256) void psi_kernel(LPArgs a) {
   }
   __syncthreads();
   const int NF = a.NF;
-  const int per = (a.ns_loc + gridDim.x - 1) / gridDim.x;
-  const int ja = blockIdx.x * per, jb = min(a.ns_loc, ja + per);
+  const int per = (a.ns_loc + nb - 1) / nb;
+  const int ja = bid * per, jb = min(a.ns_loc, ja + per);
   const int nelem = (jb > ja ? jb - ja : 0) * NF;
-  double* rs = a.rs_part + (size_t)blockIdx.x * NF;
+  double* rs = a.rs_part + (size_t)bid * NF;
   double acc = 0.0;  // thread t < NF accumulates row t in fixed order
   for (int base = 0; base < nelem; base += 256) {
     const int p = base + t;
@@ -1274,6 +1316,8 @@ __global__ __launch_bounds__(256) void psi_kernel(LPArgs a) {
   if (t < NF) rs[t] = acc;
 }
 
+__global__ __launch_bounds__(256) void psi_kernel(LPArgs a) { psi_body(a, blockIdx.x, gridDim.x); }
+
 // Marsaglia-Tsang with its first 64 trials evaluated in parallel by one wave; the
 // first accepted trial is taken, so the value equals the sequential gamma_std().
 __device__ double wave_gamma_std(Key key, uint32_t idx, uint32_t stream, uint32_t iter, double shape) {
@@ -1298,10 +1342,12 @@ __device__ double wave_gamma_std(Key key, uint32_t idx, uint32_t stream, uint32_
   return out;
 }
 
-__global__ __launch_bounds__(64) void delta_kernel(LPArgs a, const double* rs_part, int nparts) {
+// any block size that is a multiple of 64: waves beyond the first repeat wave 0's gamma
+// trials (same values) and only thread 0 / threads t < nf write
+__device__ __forceinline__ void delta_body(const LPArgs& a, const double* rs_part, int nparts, int r) {
   // one wave per level: the sequential delta chain (R/updateLambdaPriors.R:25-32)
   __shared__ double rs[64], delta[64];
-  const int r = blockIdx.x, t = threadIdx.x;
+  const int t = threadIdx.x;
   const int nf = a.lev_nf[r];
   int f0 = 0;
   for (int q = 0; q < r; ++q) f0 += a.lev_nf[q];
@@ -1333,11 +1379,13 @@ __global__ __launch_bounds__(64) void delta_kernel(LPArgs a, const double* rs_pa
   if (r == 0) HMSC_STAMP(21);
 }
 
+__global__ __launch_bounds__(64) void delta_kernel(LPArgs a, const double* rs_part, int nparts) {
+  delta_body(a, rs_part, nparts, blockIdx.x);
+}
+
 constexpr int LP_PARTS = 64;
 
-void launch_lambda_priors(State& s, uint32_t iter, hipStream_t st) {
-  if (s.nr == 0) return;
-  HMSC_REQUIRE(s.NF <= 64, "updateLambdaPriors: sum(nf) must be <= 64 in this build");
+static LPArgs make_lp_args(State& s, uint32_t iter) {
   LPArgs a{};
   a.NF = s.NF;
   a.K = s.K;
@@ -1361,6 +1409,13 @@ void launch_lambda_priors(State& s, uint32_t iter, hipStream_t st) {
   a.key = s.key;
   a.iter = iter;
   a.iter_dev = s.capturing ? s.d_iter : nullptr;
+  return a;
+}
+
+void launch_lambda_priors(State& s, uint32_t iter, hipStream_t st) {
+  if (s.nr == 0) return;
+  HMSC_REQUIRE(s.NF <= 64, "updateLambdaPriors: sum(nf) must be <= 64 in this build");
+  const LPArgs a = make_lp_args(s, iter);
   const int nparts = std::min(LP_PARTS, std::max(1, s.nsl));
   psi_kernel<<<nparts, 256, 0, st>>>(a);
   HIP_OK(hipGetLastError());
@@ -1443,11 +1498,10 @@ __global__ __launch_bounds__(256) void zl_kernel(const double* __restrict__ Z, c
 
 // CR[k, f] = sum_j BL[k, j] iSigma[j] BL[nc + f, j] over a block of SB species -> slab
 // (and LS = Lambda_all diag(iSigma), NF x ns_loc, for the fused Eta kernel when LS != null)
-__global__ __launch_bounds__(256) void cr_kernel(const double* BL, const double* iSigma, int K, int nc, int NF,
-                                                 int ns_loc, double* CR_part, int ldcr, int slab, double* LS) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
+__device__ __forceinline__ void cr_body(const double* BL, const double* iSigma, int K, int nc, int NF, int ns_loc,
+                                        double* CR_part, int ldcr, int slab, double* LS, double* smem, int bid) {
   double* sX = smem;   // K x SB
-  const int t = threadIdx.x, j0 = blockIdx.x * SB, nj = min(SB, ns_loc - j0);
+  const int t = threadIdx.x, j0 = bid * SB, nj = min(SB, ns_loc - j0);
   for (int p = t; p < K * nj; p += 256) {
     const int jj = p / K;
     sX[p] = BL[(size_t)K * j0 + p];
@@ -1459,13 +1513,19 @@ __global__ __launch_bounds__(256) void cr_kernel(const double* BL, const double*
       const int f = p % NF, jj = p / NF;
       LS[f + (size_t)NF * (j0 + jj)] = sX[nc + f + K * jj] * iSigma[j0 + jj];
     }
-  double* out = CR_part + (size_t)blockIdx.x * slab;
+  double* out = CR_part + (size_t)bid * slab;
   for (int p = t; p < K * NF; p += 256) {
     const int k = p % K, f = p / K;
     double acc = 0.0;
     for (int jj = 0; jj < nj; ++jj) acc = fma(sX[k + K * jj] * iSigma[j0 + jj], sX[nc + f + K * jj], acc);
     out[k + (size_t)ldcr * f] = acc;
   }
+}
+
+__global__ __launch_bounds__(256) void cr_kernel(const double* BL, const double* iSigma, int K, int nc, int NF,
+                                                 int ns_loc, double* CR_part, int ldcr, int slab, double* LS) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  cr_body(BL, iSigma, K, nc, NF, ns_loc, CR_part, ldcr, slab, LS, smem, blockIdx.x);
 }
 
 struct EtaArgs {
@@ -1828,13 +1888,111 @@ __global__ __launch_bounds__(512) void eta_fused_kernel(EtaFArgs a) {
   if (blockIdx.x == 0) HMSC_STAMP(55);
 }
 
+// ---------------------------------------------------------------------------
+// Co-launched side updaters (one queue).  After BetaLambda a sweep has three independent
+// species-parallel passes -- CR for updateEta, the GammaV partials (R/updateGammaV.R:17-19)
+// and the psi draws of updateLambdaPriors (:22-24) -- and two small serial tails, the delta
+// chain (:25-32) and the GammaV algebra.  An event wait between queues leaves the GPU idle
+// for ~10-20 us on this stack, so instead of two side streams the three passes share one
+// launch (post_bl_kernel), and only the two serial tails -- the GammaV algebra and the
+// delta chain, one workgroup each -- run on the side stream, which is joined just before
+// the next sweep's Gamma2 final stage.
+// ---------------------------------------------------------------------------
+struct PostBLArgs {
+  const double* BL;
+  const double* iSigma;
+  int K, nc, NF, ns_loc, ldcr, slab, n_cr;
+  double* CR_part;
+  double* LS;
+  int nt, n_gv;
+  const double* Gamma;
+  const double* Tr;
+  double* gv_part;
+  LPArgs lp;
+  int n_psi;
+  const uint32_t* iter_src;  // graph replay: d_iter, snapshotted into iter_side for the side stream
+  uint32_t* iter_side;
+};
+
+__global__ __launch_bounds__(256) void post_bl_kernel(PostBLArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  int b = blockIdx.x;
+  if (b == 0 && threadIdx.x == 0 && a.iter_src) *a.iter_side = *a.iter_src;
+  if (b < a.n_cr) {
+    cr_body(a.BL, a.iSigma, a.K, a.nc, a.NF, a.ns_loc, a.CR_part, a.ldcr, a.slab, a.LS, smem, b);
+    return;
+  }
+  b -= a.n_cr;
+  if (b < a.n_gv) {
+    gammav_partial_body(a.BL, a.K, a.nc, a.nt, a.ns_loc, a.Gamma, a.Tr, a.gv_part, smem, b);
+    return;
+  }
+  psi_body(a.lp, b - a.n_gv, a.n_psi);
+}
+
+static bool eta_fused_ok(const State& s);
+static void launch_eta_fused(State& s, uint32_t iter, bool cr_done);
+
+bool side_fusion_ok(const State& s) {
+  const uint32_t need = HMSC_UP_GAMMAV | HMSC_UP_LAMBDAPRIORS | HMSC_UP_ETA;
+  return (s.mask & need) == need && !s.single_stream && s.nc * s.nt <= 32 && s.NF <= 64 && eta_fused_ok(s) &&
+         !getenv_flag("HMSC_NO_SIDE_FUSION");
+}
+
+// GammaV + LambdaPriors + Eta of one sweep (BetaLambda done), main stream + one side launch
+void launch_side_fused(State& s, uint32_t iter) {
+  if (!s.xeta_valid) launch_xeta(s);
+  const int ncr = (s.nsl + SB - 1) / SB, ngv = (s.nsl + SB - 1) / SB;
+  const int npsi = std::min(LP_PARTS, std::max(1, s.nsl));
+  const int64_t slab = (int64_t)s.Kmax * s.NFmax;
+  PostBLArgs a{};
+  a.BL = s.BL;
+  a.iSigma = s.iSigma;
+  a.K = s.K;
+  a.nc = s.nc;
+  a.NF = s.NF;
+  a.ns_loc = s.nsl;
+  a.ldcr = s.Kmax;
+  a.slab = (int)slab;
+  a.n_cr = ncr;
+  a.CR_part = s.CR_part;
+  a.LS = s.LS;
+  a.nt = s.nt;
+  a.n_gv = ngv;
+  a.Gamma = s.Gamma;
+  a.Tr = s.Tr;
+  a.gv_part = s.gv_part;
+  a.lp = make_lp_args(s, iter);
+  a.n_psi = npsi;
+  a.iter_src = s.capturing ? s.d_iter : nullptr;
+  a.iter_side = s.d_iter_side;
+  const size_t smem = std::max((size_t)s.K * SB, (size_t)(2 * s.nc * SB + SB * s.nt)) * sizeof(double);
+  post_bl_kernel<<<ncr + ngv + npsi, 256, smem, s.stream>>>(a);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(s.ev_bl, s.stream));
+  // the main continuation is captured before the side branch: the graph executor keeps the
+  // first-created child of a node on its parent's queue, so the critical path stays on one
+  slab_sum_kernel<<<grid_for(slab), 256, 0, s.stream>>>(s.CR_part, s.CR, slab, ncr, slab);
+  HIP_OK(hipGetLastError());
+  // GammaV algebra on the side stream (reads gv_part; writes Gamma, iV and Gamma2's prep)
+  HIP_OK(hipStreamWaitEvent(s.side, s.ev_bl, 0));
+  launch_gammav_wave(s, iter, s.side, s.gv_part, ngv, s.capturing ? s.d_iter_side : nullptr);
+  // the delta chain (reads the psi partials) follows it there
+  LPArgs lps = a.lp;
+  lps.iter_dev = s.capturing ? s.d_iter_side : nullptr;
+  delta_kernel<<<s.nr, 64, 0, s.side>>>(lps, s.psi_rs, npsi);
+  HIP_OK(hipGetLastError());
+  s.side_pending |= 1;  // joined (ev_side recorded) by the next join_side
+  launch_eta_fused(s, iter, true);
+}
+
 static bool eta_fused_ok(const State& s) {
   return s.nranks == 1 && s.nr == 1 && s.n_na_rows == 0 && s.lev[0].np == s.ny && s.lev[0].uniform_n == 1 &&
          s.lev[0].nf <= 16 && s.K <= 64 && s.LS != nullptr && !getenv_flag("HMSC_NO_ETA_FUSION");
 }
 
-static void launch_eta_fused(State& s, uint32_t iter) {
-  {
+static void launch_eta_fused(State& s, uint32_t iter, bool cr_done = false) {
+  if (!cr_done) {
     const int ncr = (s.nsl + SB - 1) / SB;
     const int64_t slab = (int64_t)s.Kmax * s.NFmax;
     cr_kernel<<<ncr, 256, (size_t)s.K * SB * sizeof(double), s.stream>>>(s.BL, s.iSigma, s.K, s.nc, s.NF, s.nsl,
@@ -2202,13 +2360,28 @@ struct PackArgs {
   PackPiece p[MAX_PIECES];
   int npieces;
   double* slot;
+  // graph replays: the slot follows from the device sweep counter and the run descriptor
+  // {iter0, transient, thin, samples}; sweeps that are not recorded return at once
+  const uint32_t* iter_dev;
+  const int32_t* desc;
+  int64_t slot_stride;
+  int ring_slots;
 };
 
 __global__ __launch_bounds__(256) void pack_kernel(PackArgs a) {
+  double* slot = a.slot;
+  if (a.iter_dev) {
+    const int it = (int)(*a.iter_dev - (uint32_t)a.desc[0]);
+    const int transient = a.desc[1], thin = a.desc[2], samples = a.desc[3];
+    if (it <= transient || (it - transient) % thin != 0) return;
+    const int k = (it - transient) / thin - 1;
+    if (k >= samples) return;
+    slot += (int64_t)(k % a.ring_slots) * a.slot_stride;
+  }
   for (int k = 0; k < a.npieces; ++k) {
     const PackPiece pc = a.p[k];
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < pc.n; e += (int64_t)gridDim.x * blockDim.x)
-      a.slot[pc.dst + e] = pc.src[e];
+      slot[pc.dst + e] = pc.src[e];
   }
 }
 
@@ -2232,24 +2405,36 @@ size_t record_slot_doubles(const State& s) {
   return n;
 }
 
-void launch_record(State& s, double* slot) {
+void launch_record(State& s, double* slot, int part) {
   PackArgs a{};
   int64_t off = 0;
   int k = 0;
-  auto add = [&](const double* src, int64_t n) {
-    a.p[k++] = PackPiece{src, n, off};
+  // side pieces (Gamma, iV, Delta) are written by the GammaV algebra and the delta chain,
+  // which may still run on the side stream: part 2 packs them there, part 1 the rest
+  auto add = [&](const double* src, int64_t n, bool side) {
+    if (part == 0 || (part == 2) == side) a.p[k++] = PackPiece{src, n, off};
     off += n;
   };
-  add(s.BL, (int64_t)s.K * s.nsl);
-  add(s.Psi, (int64_t)s.NF * s.nsl);
-  add(s.Delta, s.NF);
-  add(s.Gamma, (int64_t)s.nc * s.nt);
-  add(s.iV, (int64_t)s.nc * s.nc);
-  add(s.iSigma, s.nsl);
-  for (int r = 0; r < s.nr; ++r) add(s.lev[r].Eta, (int64_t)s.lev[r].np * s.lev[r].nf);
+  add(s.BL, (int64_t)s.K * s.nsl, false);
+  add(s.Psi, (int64_t)s.NF * s.nsl, false);
+  add(s.Delta, s.NF, true);
+  add(s.Gamma, (int64_t)s.nc * s.nt, true);
+  add(s.iV, (int64_t)s.nc * s.nc, true);
+  add(s.iSigma, s.nsl, false);
+  for (int r = 0; r < s.nr; ++r) add(s.lev[r].Eta, (int64_t)s.lev[r].np * s.lev[r].nf, false);
   a.npieces = k;
   a.slot = slot;
-  pack_kernel<<<512, 256, 0, s.stream>>>(a);
+  if (slot == nullptr) {  // captured into a graph replay: slot chosen on the device
+    a.slot = s.ring;
+    a.iter_dev = part == 2 ? s.d_iter_side : s.d_iter;
+    a.desc = s.d_rec_desc;
+    a.slot_stride = (int64_t)s.slot_doubles;
+    a.ring_slots = s.ring_slots;
+  }
+  if (part == 2)
+    pack_kernel<<<1, 256, 0, s.side>>>(a);
+  else
+    pack_kernel<<<512, 256, 0, s.stream>>>(a);
   HIP_OK(hipGetLastError());
 }
 

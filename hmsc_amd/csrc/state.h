@@ -56,7 +56,13 @@ struct State {
   // only feed sweep t+1, so they overlap updateEta / updateZ of sweep t
   hipStream_t side = nullptr, side2 = nullptr;  // side: GammaV + Gamma2 prep; side2: LambdaPriors
   hipEvent_t ev_bl = nullptr, ev_side = nullptr, ev_side2 = nullptr;
-  bool side_pending = false;
+  int side_pending = 0;          // bit 0: side has unjoined work (ev_side), bit 1: side2 (ev_side2)
+  // co-launched sweep (see launch_side_fused): only the GammaV algebra stays on `side`; its
+  // Philox sweep counter is snapshotted into d_iter_side by the launch that forks it, so the
+  // main stream may advance d_iter for the next sweep while it runs
+  bool side_fused = false;
+  uint32_t* d_iter_side = nullptr;
+  double* gv_part = nullptr;     // GammaV species partials (not shared with Gamma2's ABpart)
 
   // model (device)
   double *X = nullptr, *Tr = nullptr, *Yval = nullptr, *Yraw = nullptr;
@@ -115,7 +121,6 @@ struct State {
   double* ring = nullptr;
   int ring_slots = 0;
   size_t slot_doubles = 0;
-  std::vector<hipEvent_t> ring_packed;  // pack kernel of slot i done (copy stream waits on it)
   double* host_rec = nullptr;    // pinned host ring (ring_slots slots)
   uint64_t* copied_host = nullptr;  // fine-grained pinned counter: samples whose D2H copy landed
   uint64_t* copied_dev = nullptr;   // its device address
@@ -128,6 +133,11 @@ struct State {
   bool graph_dirty = true;
   int graph_K = -1, graph_NF = -1;
   hipGraphExec_t gexec = nullptr;
+  hipGraphExec_t gexec_rec = nullptr;  // the same sweeps, each followed by the record pack
+  bool single_stream = false;          // HMSC_SINGLE_STREAM: no side-stream overlap (diagnostic)
+  int graph_sweeps = 4;                 // sweeps per replay (HMSC_GRAPH_SWEEPS)
+  int32_t* d_rec_desc = nullptr;        // {iter0, transient, thin, samples} of the current run
+  hipEvent_t ev_graph = nullptr;        // after a recording replay: the copy stream waits on it
   uint32_t graph_next_iter = 0;  // the iter the next replay will use (0: unknown, re-seed)
   int eager_streak = 0;          // eager steady sweeps since the graph was invalidated
 
@@ -194,7 +204,12 @@ void launch_gamma2(State& s, uint32_t iter);
 void launch_lambda_priors(State& s, uint32_t iter, hipStream_t st);
 void launch_eta(State& s, uint32_t iter);
 void launch_inv_sigma(State& s, uint32_t iter);
-void launch_record(State& s, double* slot);
+// record pack; slot == nullptr: device-chosen (graph replay).  part: 0 all, 1 the main-stream
+// quantities (BL, Psi, iSigma, Eta), 2 the side-stream ones (Gamma, iV, Delta) on `side`
+void launch_record(State& s, double* slot, int part = 0);
+bool side_fusion_ok(const State& s);
+void launch_side_fused(State& s, uint32_t iter);  // GammaV + LambdaPriors + Eta, co-launched
+void join_side(State& s);
 void launch_copied_flag(State& s, uint64_t value);
 size_t record_slot_doubles(const State& s);
 void read_stamps(double* out, int n);  // diagnostic build (HMSC_STAMPS)

@@ -198,17 +198,24 @@ def test_sample_mcmc_layout():
     assert mp["Beta"][0].shape == (20, 36) and cols["Beta"][0].startswith("B[(Intercept) (C1), sp01 (S1)]")
 
 
-def test_graph_replay_matches_eager(monkeypatch):
-    """hmsc_run replays a captured per-sweep hipGraph; the recorded chain must equal the
-    eager launch sequence bit for bit (same kernels, same order, same Philox counters)."""
+@pytest.mark.parametrize("thin", [1, 2])
+def test_graph_replay_matches_eager(monkeypatch, thin):
+    """hmsc_run replays captured graphs of several sweeps (the record pack inside, its ring
+    slot chosen on the device); the recorded chain must equal the eager launch sequence bit
+    for bit (same kernels, same order, same Philox counters), also when the run length is
+    not a multiple of the sweeps per replay."""
     hM = synthetic_model(ny=200, ns=30, nc=4, nf=3, nt=2, seed=12)
     out = []
-    for no_graph in ("0", "1"):
+    for no_graph, per in (("1", "4"), ("0", "4"), ("0", "3"), ("0", "1")):
         monkeypatch.setenv("HMSC_NO_GRAPH", no_graph)
+        monkeypatch.setenv("HMSC_GRAPH_SWEEPS", per)
         ch = H.Chain(hM, 77, device=0, updater={"GammaEta": False})
         ch.init()
-        rec = ch.run(transient=5, samples=12, thin=2, adaptNf=[0])
-        out.append(rec)
+        rec = ch.run(transient=5, samples=41, thin=thin, adaptNf=[0])
+        rec2 = ch.run(transient=2, samples=7, thin=thin, adaptNf=[0], iter0=5 + 41 * thin)
+        out.append((rec, rec2))
         ch.close()
-    for k in ("Beta", "Gamma", "iV", "iSigma", "Lambda0", "Eta0", "Delta0"):
-        np.testing.assert_array_equal(out[0][k], out[1][k], err_msg=k)
+    for o in out[1:]:
+        for i in range(2):
+            for k in ("Beta", "Gamma", "iV", "iSigma", "Lambda0", "Eta0", "Delta0", "Psi0"):
+                np.testing.assert_array_equal(out[0][i][k], o[i][k], err_msg=k)
