@@ -56,20 +56,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # Load the HIP library before torch: torch bundles its own libamdhip64 with the same
+    # soname, and whichever is loaded first serves the whole process.  The sampler is built
+    # against /opt/rocm's runtime, whose graph launches are several times cheaper on the host.
+    H._lib.lib()
     import torch
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
-    torch_cuda = torch.cuda.is_available()
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
     def sync(ch):
-        ch.sync()
-        if torch_cuda:
-            torch.cuda.synchronize()
+        ch.sync()  # every stream of the chain (torch runs nothing on the GPU here)
 
     hM = synthetic_probit(ny=args.ny, ns=args.ns, nc=args.nc, nf=args.nf)
     upd = {"GammaEta": False}
@@ -85,7 +86,9 @@ def main():
     else:
         ch = H.Chain(hM, 1234567 + 7919 * rank, device=local, updater=upd)
     ch.init([args.nf])
-    ch.run(transient=args.warmup, samples=0, adaptNf=[0], record=False)
+    # warm-up: the same recorded replay path as the timed region (graph instantiation and
+    # first launches, host ring and unpack threads), output discarded
+    ch.run(transient=0, samples=args.warmup, thin=1, adaptNf=[0], record=True)
     barrier()
     sync(ch)
     t0 = time.perf_counter()

@@ -881,6 +881,8 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
   std::unique_ptr<std::atomic<uint8_t>[]> done(new std::atomic<uint8_t>[std::max(1, samples)]);
   for (int k = 0; k < samples; ++k) done[k].store(0);
   int low = 0;  // every sample < low is unpacked (main thread only)
+  std::atomic<int64_t> diag_unpack_ns{0};  // HMSC_DIAG_TIMING: time in unpack (all workers)
+  int64_t diag_wait_ns = 0;                 // and the launcher's waits for a free ring slot
   volatile uint64_t* copied = s.copied_host;
   if (recording) *copied = 0;           // no copy is in flight between runs
   const char* w_env = getenv("HMSC_UNPACK_THREADS");
@@ -906,7 +908,9 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
             if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
             else std::this_thread::yield();
           }
+          const auto tu0 = std::chrono::steady_clock::now();
           unpack_record(s, s.host_rec + s.slot_doubles * (k % s.ring_slots), k, samples, rec);
+          diag_unpack_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tu0).count();
           done[k].store(1, std::memory_order_release);
           {  // the launcher may be waiting for this host slot
             std::lock_guard<std::mutex> lk(mu);
@@ -930,6 +934,12 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
     if (need <= 0) return;
     while (low < need && done[low].load(std::memory_order_acquire)) ++low;
     if (low < need) {
+      const auto tw0 = std::chrono::steady_clock::now();
+      struct Acc {
+        std::chrono::steady_clock::time_point t0;
+        int64_t& acc;
+        ~Acc() { acc += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count(); }
+      } acc{tw0, diag_wait_ns};
       std::unique_lock<std::mutex> lk(mu);
       cv_done.wait(lk, [&] {
         while (low < need && done[low].load(std::memory_order_acquire)) ++low;
@@ -1000,9 +1010,10 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
   HIP_OK(hipStreamSynchronize(s.copy_stream));
   if (getenv("HMSC_DIAG_TIMING")) {  // host run-ahead diagnostic: enqueue time vs total
     const auto t_end = std::chrono::steady_clock::now();
-    std::fprintf(stderr, "[hmsc] run %d sweeps: enqueued in %.3f ms, done in %.3f ms\n", total,
-                 std::chrono::duration<double, std::milli>(t_enq - t_start).count(),
-                 std::chrono::duration<double, std::milli>(t_end - t_start).count());
+    std::fprintf(stderr, "[hmsc] run %d sweeps: enqueued in %.3f ms, done in %.3f ms; unpack %.3f ms, slot waits %.3f ms\n",
+                 total, std::chrono::duration<double, std::milli>(t_enq - t_start).count(),
+                 std::chrono::duration<double, std::milli>(t_end - t_start).count(), 1e-6 * diag_unpack_ns.load(),
+                 1e-6 * diag_wait_ns);
   }
   int flag[2] = {0, 0};
   HIP_OK(hipMemcpy(flag, s.dev_flags, sizeof(flag), hipMemcpyDeviceToHost));
