@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--nf", type=int, default=10)
     p.add_argument("--cpu-seconds", type=float, default=20.0)
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_r01.json"))
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc.json"))
     return p.parse_args()
 
 
@@ -86,17 +86,26 @@ def main():
     else:
         ch = H.Chain(hM, 1234567 + 7919 * rank, device=local, updater=upd)
     ch.init([args.nf])
+    # in-kernel launch timer (wall clock at every workgroup's start/finish, per sweep slot):
+    # on before the graph is captured so the replays of the timed region carry it
+    ch.kernel_timing(True)
     # warm-up: the same recorded replay path as the timed region (graph instantiation and
     # first launches, host ring and unpack threads), output discarded
     ch.run(transient=0, samples=args.warmup, thin=1, adaptNf=[0], record=True)
     barrier()
     sync(ch)
+    ch.kernel_timing(True)  # clear: keep only the timed region's launches
     t0 = time.perf_counter()
     # timed region: every sweep is a replay of the captured per-sweep hipGraph (capi.cpp)
     rec = ch.run(transient=0, samples=args.steps, thin=1, adaptNf=[0], iter0=args.warmup, record=True)
     sync(ch)
     barrier()
     t_run = time.perf_counter() - t0
+    live = {}
+    for name in ("z", "eta", "betalambda"):
+        tot_us, n = ch.kernel_timing_get(name)
+        live[name] = dict(total_us=tot_us, launches=n, avg_us=tot_us / max(1, n))
+    ch.kernel_timing(False)
     # per-kernel durations: HIP events around the launches of a short eager (un-captured)
     # run on the chain's own stream, after the timed region
     n_prof = min(args.steps, 50)
@@ -104,7 +113,7 @@ def main():
     ch.run(transient=n_prof, samples=0, adaptNf=[0], iter0=args.warmup + args.steps, record=False)
     sync(ch)
     kern = {}
-    for name in ("z", "zl", "betalambda", "eta_unit", "sweep"):
+    for name in ("z", "betalambda", "eta_unit", "sweep"):
         tot, n = ch.profile_get(name)
         kern[name] = dict(total_ms=tot, launches=n, avg_us=1e3 * tot / max(1, n))
     ch.profile(False)
@@ -137,17 +146,23 @@ def main():
     algo_bytes = {
         # fused updateZ: writes Z (fp64) + reads the int8 Y code, ny*ns each (R/updateZ.R)
         "z": ny * (ns // (world if args.mode == "sharded" else 1)) * (8 + 1),
-        # updateEta pass: reads Z once (R/updateEta.R:55)
-        "zl": ny * (ns // (world if args.mode == "sharded" else 1)) * 8,
+        # fused updateEta: reads Z once for S*diag(iSigma)*Lambda^T (R/updateEta.R:33-55)
+        "eta": ny * (ns // (world if args.mode == "sharded" else 1)) * 8,
+        # BetaLambda: XEta^T Z arrives precomputed from the z kernel; reads XZ + writes BL
+        "betalambda": (ns // (world if args.mode == "sharded" else 1)) * (args.nc + args.nf) * 8 * 2,
     }
-    dom = max(("z", "zl", "betalambda", "eta_unit"), key=lambda k: kern[k]["total_ms"])
-    roof_kernel = dom if dom in algo_bytes else max(algo_bytes, key=lambda k: kern[k]["total_ms"])
-    avg_s = kern[roof_kernel]["avg_us"] * 1e-6
+    # roofline: the dominant kernel, its average duration measured live on the timed
+    # region's graph replays by the in-kernel wall-clock timer (hmsc_kernel_timing)
+    roof_kernel = max(live, key=lambda k: live[k]["total_us"])
+    avg_s = live[roof_kernel]["avg_us"] * 1e-6
     achieved = algo_bytes[roof_kernel] / avg_s / 1e9
     traffic = None
     if os.path.exists(args.pmc_json):
         try:
-            traffic = json.load(open(args.pmc_json)).get(roof_kernel, {}).get("hbm_bytes_per_launch")
+            pmc = json.load(open(args.pmc_json))
+            pref = {"z": "z_wave_kernel", "eta": "eta_fused_kernel", "betalambda": "beta_lambda_wave_kernel"}
+            hit = [v for k, v in pmc.items() if k.startswith(pref[roof_kernel])]
+            traffic = round(hit[0]["hbm_bytes_per_launch"]) if hit else None
         except Exception:
             traffic = None
 
@@ -178,8 +193,11 @@ def main():
         "roofline": {"kernel": roof_kernel, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "algorithmic_bytes_per_launch": algo_bytes[roof_kernel],
-                     "avg_launch_us": round(kern[roof_kernel]["avg_us"], 2)},
-        "kernels_us": {k: round(v["avg_us"], 2) for k, v in kern.items()},
+                     "avg_launch_us": round(live[roof_kernel]["avg_us"], 3),
+                     "timed_launches": live[roof_kernel]["launches"],
+                     "timer": "in-kernel wall clock (s_memrealtime, 100 MHz) over the timed region's graph replays"},
+        "kernels_live_us": {k: round(v["avg_us"], 3) for k, v in live.items()},
+        "kernels_eager_events_us": {k: round(v["avg_us"], 2) for k, v in kern.items()},
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)

@@ -52,7 +52,7 @@ _lib = None
 EXPORTS = ["hmsc_last_error", "hmsc_device_count", "hmsc_create", "hmsc_create_sharded", "hmsc_comm_unique_id",
            "hmsc_destroy", "hmsc_init_state", "hmsc_set_state", "hmsc_get_state", "hmsc_get_nf", "hmsc_sweep",
            "hmsc_update", "hmsc_set_noise_mode", "hmsc_run", "hmsc_run_verbose", "hmsc_sync", "hmsc_debug_get",
-           "hmsc_profile", "hmsc_profile_get"]
+           "hmsc_profile", "hmsc_profile_get", "hmsc_kernel_timing", "hmsc_kernel_timing_get"]
 
 
 def lib():
@@ -86,6 +86,8 @@ def lib():
     L.hmsc_debug_get.argtypes = [C.c_void_p, C.c_char_p, dp, C.c_int64]
     L.hmsc_profile.argtypes = [C.c_void_p, C.c_int32]
     L.hmsc_profile_get.argtypes = [C.c_void_p, C.c_int32, dp, ip]
+    L.hmsc_kernel_timing.argtypes = [C.c_void_p, C.c_int32]
+    L.hmsc_kernel_timing_get.argtypes = [C.c_void_p, C.c_int32, dp, ip]
     _lib = L
     return L
 

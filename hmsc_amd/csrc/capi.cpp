@@ -425,6 +425,7 @@ static void free_state(State& s) {
   if (s.copied_host) (void)hipHostFree(s.copied_host);
   if (s.gexec) (void)hipGraphExecDestroy(s.gexec);
   if (s.d_iter) (void)hipFree(s.d_iter);
+  if (s.d_kt) (void)hipFree(s.d_kt);
   if (s.comm) ncclCommDestroy((ncclComm_t)s.comm);
   if (s.ev_bl) (void)hipEventDestroy(s.ev_bl);
   if (s.ev_side) (void)hipEventDestroy(s.ev_side);
@@ -1222,6 +1223,52 @@ int hmsc_profile(hmsc_state* h, int32_t enable) {
       v.clear();
     }
     s.prof = enable != 0;
+  });
+}
+
+// Launch timing from inside the kernels (common.h kt_record), graph replays included.
+int hmsc_kernel_timing(hmsc_state* h, int32_t enable) {
+  return guarded([&] {
+    State& s = h->s;
+    DeviceGuard dg(s.device);
+    join_side(s);
+    HIP_OK(hipStreamSynchronize(s.stream));
+    if (enable && !s.d_kt) s.d_kt = dalloc<unsigned long long>((size_t)KT_N * 2 * KT_SLOTS);
+    if (enable)
+      for (int id = 0; id < KT_N; ++id) {
+        unsigned long long* b = s.d_kt + (size_t)id * 2 * KT_SLOTS;
+        HIP_OK(hipMemsetAsync(b, 0xff, sizeof(unsigned long long) * KT_SLOTS, s.stream));  // starts: max
+        HIP_OK(hipMemsetAsync(b + KT_SLOTS, 0, sizeof(unsigned long long) * KT_SLOTS, s.stream));
+      }
+    HIP_OK(hipStreamSynchronize(s.stream));
+    if (s.kt_on != (enable != 0)) s.graph_dirty = true;  // the kernels' kt pointer changes
+    s.kt_on = enable != 0;
+  });
+}
+
+int hmsc_kernel_timing_get(hmsc_state* h, int32_t id, double* total_us, int32_t* count) {
+  return guarded([&] {
+    State& s = h->s;
+    HMSC_REQUIRE(id >= 0 && id < KT_N, "kernel timing id out of range");
+    *total_us = 0.0;
+    *count = 0;
+    if (!s.d_kt) return;
+    DeviceGuard dg(s.device);
+    join_side(s);
+    HIP_OK(hipStreamSynchronize(s.stream));
+    std::vector<unsigned long long> v((size_t)2 * KT_SLOTS);
+    HIP_OK(hipMemcpy(v.data(), s.d_kt + (size_t)id * 2 * KT_SLOTS, sizeof(unsigned long long) * v.size(),
+                     hipMemcpyDeviceToHost));
+    int khz = 0;
+    HIP_OK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, s.device));
+    HMSC_REQUIRE(khz > 0, "wall clock rate unavailable");
+    double ticks = 0.0;
+    for (int i = 0; i < KT_SLOTS; ++i)
+      if (v[KT_SLOTS + i] != 0 && v[i] != ~0ull && v[KT_SLOTS + i] >= v[i]) {
+        ticks += (double)(v[KT_SLOTS + i] - v[i]);
+        ++*count;
+      }
+    *total_us = ticks * 1e3 / khz;
   });
 }
 

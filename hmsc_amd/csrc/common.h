@@ -32,6 +32,21 @@ constexpr int WAVE = 64;
 // launches captured into the per-sweep hipGraph -- the device word the graph advances.
 #define SWEEP_ITER(a) ((a).iter_dev ? *(a).iter_dev : (a).iter)
 
+// Live launch timing (hmsc_kernel_timing): each workgroup reads the constant-rate wall
+// clock (s_memrealtime) when it starts and when it finishes, and the launch's first start /
+// last finish are kept per sweep slot by device-scope atomic min / max -- the duration of
+// every launch of the timed region, graph replays included, with no event in the stream.
+// Layout per timed kernel: KT_SLOTS starts, then KT_SLOTS ends.
+constexpr int KT_SLOTS = 8192;
+enum KtId { KT_Z = 0, KT_ETA = 1, KT_BL = 2, KT_N = 3 };
+__device__ inline unsigned long long kt_now() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ inline void kt_record(unsigned long long* kt, uint32_t iter, unsigned long long t0) {
+  const unsigned long long t1 = kt_now();
+  const uint32_t slot = iter & (KT_SLOTS - 1);
+  __hip_atomic_fetch_min(kt + slot, t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_max(kt + KT_SLOTS + slot, t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Diagnostic build only (python -m hmsc_amd.build --stamps -> libhmsc_amd_stamps.so):
 // HMSC_STAMP(i) records the shader clock (s_memtime) of lane 0 of the calling workgroup
 // into slot i of a device table read back with hmsc_debug_get(s, "stamps", ...).  The

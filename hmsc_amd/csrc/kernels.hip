@@ -240,6 +240,7 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   a.iter = iter;
   a.iter_dev = s.capturing ? s.d_iter : nullptr;
   a.noise_zero = s.noise_mode;
+  a.kt = s.kt_on ? s.d_kt + (size_t)KT_Z * 2 * KT_SLOTS : nullptr;
   dim3 grid(nchunk, s.ntile_j);
   const size_t smem = z_smem_bytes(s.K, s.nt);
   {
@@ -316,6 +317,7 @@ struct BLArgs {
   Key key;
   uint32_t iter;
   const uint32_t* iter_dev;  // graph replay: the sweep counter is read from the device
+  unsigned long long* kt;    // live launch timing (KT_BL block) or null
   int noise_zero;
 };
 
@@ -384,6 +386,7 @@ __global__ __launch_bounds__(64) void beta_lambda_kernel(BLArgs a) {
 template <int NM>
 __global__ __launch_bounds__(256) void beta_lambda_wave_kernel(BLArgs a) {
   __shared__ __attribute__((aligned(16))) double tiles[4 * WV_TILE];
+  const unsigned long long kt0 = a.kt ? kt_now() : 0ull;
   const int K = a.K, nc = a.nc, i = lane_id(), w = threadIdx.x >> 6;
   const int j = blockIdx.x * 4 + w;
   if (j >= a.ns_loc) return;
@@ -440,6 +443,7 @@ __global__ __launch_bounds__(256) void beta_lambda_wave_kernel(BLArgs a) {
   wv_transpose<NM, true>(x, lt, lds);
   wv_backward_t<NM>(lt, dinv, r);          // m + backsolve(RiU, xi)  (:101)
   if (i < K) a.BL[i + (size_t)K * j] = r;
+  if (a.kt && i == 0) kt_record(a.kt, SWEEP_ITER(a), kt0);
 }
 
 void launch_beta_lambda(State& s, uint32_t iter) {
@@ -476,6 +480,7 @@ void launch_beta_lambda(State& s, uint32_t iter) {
   a.iter = iter;
   a.iter_dev = s.capturing ? s.d_iter : nullptr;
   a.noise_zero = s.noise_mode;
+  a.kt = s.kt_on ? s.d_kt + (size_t)KT_BL * 2 * KT_SLOTS : nullptr;
   ProfScope ps(s, PROF_BL);
   if (s.K <= 32) {
     const int nb = (s.nsl + 3) / 4;
@@ -1734,6 +1739,7 @@ struct EtaFArgs {
   uint32_t iter;
   const uint32_t* iter_dev;  // graph replay: the sweep counter is read from the device
   int noise_zero;
+  unsigned long long* kt;    // live launch timing (KT_ETA block) or null
 };
 
 constexpr int EF_SITES = 32;
@@ -1745,6 +1751,7 @@ __global__ __launch_bounds__(512) void eta_fused_kernel(EtaFArgs a) {
   __shared__ double sB[NFB][EF_SITES], sXi[NFB][EF_SITES];
   __shared__ double sX[64][EF_SITES + 1];     // XEta tile [k][site] (K <= 64)
   __shared__ double sCR[64 * NFB];            // CR[k][h], k < K
+  const unsigned long long kt0 = a.kt ? kt_now() : 0ull;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int ny = a.ny, nf = a.nf, K = a.K, nc = a.nc;
   const int i0 = blockIdx.x * EF_SITES;
@@ -1886,6 +1893,10 @@ __global__ __launch_bounds__(512) void eta_fused_kernel(EtaFArgs a) {
     dst[k1 + a.Kmax * k2] = g;
   }
   if (blockIdx.x == 0) HMSC_STAMP(55);
+  if (a.kt) {
+    __syncthreads();
+    if (t == 0) kt_record(a.kt, SWEEP_ITER(a), kt0);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2022,6 +2033,7 @@ static void launch_eta_fused(State& s, uint32_t iter, bool cr_done = false) {
   a.iter = iter;
   a.iter_dev = s.capturing ? s.d_iter : nullptr;
   a.noise_zero = s.noise_mode;
+  a.kt = s.kt_on ? s.d_kt + (size_t)KT_ETA * 2 * KT_SLOTS : nullptr;
   const int ntile = (s.ny + EF_SITES - 1) / EF_SITES;
   {
     ProfScope ps(s, PROF_ETA_UNIT);

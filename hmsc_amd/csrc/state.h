@@ -141,6 +141,11 @@ struct State {
   uint32_t graph_next_iter = 0;  // the iter the next replay will use (0: unknown, re-seed)
   int eager_streak = 0;          // eager steady sweeps since the graph was invalidated
 
+  // live launch timing of the timed kernels (common.h kt_record): per-sweep-slot first
+  // start / last finish wall-clock ticks, KT_N blocks of 2 * KT_SLOTS
+  unsigned long long* d_kt = nullptr;
+  bool kt_on = false;
+
   // live kernel timing (HIP events on this chain's stream), id -> launches
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[8];

@@ -40,6 +40,7 @@ struct ZArgs {
   uint32_t iter;
   const uint32_t* iter_dev;  // graph replay: the sweep counter is read from the device
   int noise_zero;
+  unsigned long long* kt;    // live launch timing (KT_Z block) or null
 };
 
 constexpr int ZT_I = 64;   // sites per workgroup tile (4 waves x 16)
@@ -100,6 +101,7 @@ constexpr int ZT_TLD = 17;  // leading dimension of the wave's 16-site x 32-spec
 template <bool DRAW, bool HAS_NA, int NKB, int MODE = Z_ALL>
 __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  const unsigned long long kt0 = a.kt ? kt_now() : 0ull;
   constexpr int K16 = 16 * NKB;
   const int K = a.K, K4 = (K + 3) & ~3;
   const int ny = a.ny;
@@ -262,6 +264,7 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
                            sR[(2 * K16 + k) * ZT_J + jj];
           if (k < K && j < a.ns_loc) dst[k + (size_t)K * j] = v;
         }
+    if (a.kt && t == 0) kt_record(a.kt, SWEEP_ITER(a), kt0);
   }
 }
 

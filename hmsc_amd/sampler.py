@@ -209,6 +209,19 @@ class Chain:
         L.check(self.lib.hmsc_profile_get(self.h, self.PROF_IDS[name], L.fptr(t), L.iptr(n)))
         return float(t[0]), int(n[0])
 
+    KT_IDS = dict(z=0, eta=1, betalambda=2)
+
+    def kernel_timing(self, enable=True):
+        """Clear and enable (or disable) the in-kernel launch timer (hmsc_kernel_timing)."""
+        L.check(self.lib.hmsc_kernel_timing(self.h, 1 if enable else 0))
+
+    def kernel_timing_get(self, name):
+        """(total microseconds, launches) of one timed kernel since kernel_timing(True)."""
+        t = np.zeros(1)
+        n = np.zeros(1, dtype=np.int32)
+        L.check(self.lib.hmsc_kernel_timing_get(self.h, self.KT_IDS[name], L.fptr(t), L.iptr(n)))
+        return float(t[0]), int(n[0])
+
     def debug_get(self, name, n):
         out = np.zeros(int(n))
         L.check(self.lib.hmsc_debug_get(self.h, name.encode(), L.fptr(out), int(n)))

@@ -176,6 +176,16 @@ int hmsc_run_verbose(hmsc_state* s, int32_t transient, int32_t samples, int32_t 
 int hmsc_profile(hmsc_state* s, int32_t enable);
 int hmsc_profile_get(hmsc_state* s, int32_t id, double* total_ms, int32_t* count);
 
+/* Live launch timing measured inside the kernels (bench.py's roofline figure): every
+ * workgroup reads the constant-rate wall clock when it starts and finishes; a launch's
+ * duration is its last finish minus its first start, kept per sweep (graph replays
+ * included; up to 8192 sweeps per window).  id 0 = updateZ kernel, 1 = fused updateEta
+ * kernel, 2 = BetaLambda wave kernel.  hmsc_kernel_timing(s,1) clears and enables (0
+ * disables); _get returns the summed duration (us) and the number of timed launches.
+ * No reference counterpart: instrumentation of this port. */
+int hmsc_kernel_timing(hmsc_state* s, int32_t enable);
+int hmsc_kernel_timing_get(hmsc_state* s, int32_t id, double* total_us, int32_t* count);
+
 /* Wait for all device work of this chain. */
 int hmsc_sync(hmsc_state* s);
 
