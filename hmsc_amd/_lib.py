@@ -27,7 +27,8 @@ class hmsc_model(C.Structure):
                 ("Y", dp), ("Yraw", dp), ("X", dp), ("Tr", dp), ("Pi", ip), ("np", ip), ("distr", ip),
                 ("V0", dp), ("f0", C.c_double), ("mGamma", dp), ("UGamma", dp), ("aSigma", dp), ("bSigma", dp),
                 ("nu", dp), ("a1", dp), ("b1", dp), ("a2", dp), ("b2", dp), ("nfMin", ip), ("nfMax", ip),
-                ("sDim", ip), ("xDim", ip), ("C", dp)]
+                ("sDim", ip), ("xDim", ip), ("C", dp), ("nrho", C.c_int32), ("rhopw", dp),
+                ("C_vectors", dp), ("C_values", dp)]
 
 
 class hmsc_params(C.Structure):

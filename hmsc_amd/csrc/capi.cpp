@@ -143,13 +143,59 @@ void allreduce_sum(State& s, double* buf, size_t n, hipStream_t st) {
   HMSC_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
 }
 
+// ---------------------------- phylogeny ----------------------------
+// computeDataParameters' rho grid (R/computeDataParameters.R:19-39) in spectral form: with
+// C = U diag(d) U^T every Q_g = U diag(q_g) U^T (phylo.hip), so the device keeps U, the table
+// 1 / q_g,i and log(rhopw[g,2]) - nc/2 logdet Q_g instead of nrho dense ns x ns matrices.
+static void setup_phylo(State& s, const hmsc_model* m) {
+  const int ns = s.ns, nt = s.nt, nc = s.nc;
+  HMSC_REQUIRE(m->C_vectors != nullptr && m->C_values != nullptr,
+               "phylogeny: pass the eigendecomposition of C (C_vectors, C_values)");
+  HMSC_REQUIRE(m->nrho > 0 && m->rhopw != nullptr, "phylogeny: rhopw grid missing");
+  HMSC_REQUIRE(s.nranks == 1, "phylogeny couples all species: species-sharded chains are not supported");
+  HMSC_REQUIRE(!s.has_na, "phylogeny with NA in Y is not supported in this build");
+  s.phylo = true;
+  s.nrho = m->nrho;
+  std::vector<double> winv((size_t)s.nrho * ns), rbase(s.nrho);
+  for (int i = 0; i < ns; ++i) HMSC_REQUIRE(m->C_values[i] > 0.0, "phylogeny: C must be positive definite");
+  for (int g = 0; g < s.nrho; ++g) {
+    const double rho = m->rhopw[g], pw = m->rhopw[g + s.nrho];
+    double ld = 0.0;
+    for (int i = 0; i < ns; ++i) {
+      const double d = m->C_values[i];
+      const double q = rho >= 0.0 ? rho * d + (1.0 - rho) : (-rho) / d + (1.0 + rho);
+      HMSC_REQUIRE(q > 0.0, "phylogeny: Q_g not positive definite");
+      winv[(size_t)ns * g + i] = 1.0 / q;
+      ld += std::log(q);
+    }
+    rbase[g] = std::log(pw) - 0.5 * nc * ld;  // R/updateRho.R:19-20
+  }
+  std::vector<double> tt((size_t)ns * nt, 0.0);  // U^T Tr
+  for (int q = 0; q < nt; ++q)
+    for (int i = 0; i < ns; ++i) {
+      double v = 0.0;
+      for (int j = 0; j < ns; ++j) v += m->C_vectors[j + (size_t)ns * i] * m->Tr[j + (size_t)ns * q];
+      tt[i + (size_t)ns * q] = v;
+    }
+  s.phU = dupload(m->C_vectors, (size_t)ns * ns);
+  s.phWinv = dupload(winv.data(), winv.size());
+  s.phRbase = dupload(rbase.data(), rbase.size());
+  s.phTt = dupload(tt.data(), tt.size());
+  s.phBt = dalloc<double>((size_t)nc * ns + 1);
+  s.phEt = dalloc<double>((size_t)nc * ns + 1);
+  s.phTTw = dalloc<double>((size_t)nt * nt);
+  s.phNmax = s.Kmax * ns;
+  HMSC_REQUIRE(s.phNmax <= 8192, "phylogeny: (nc + nfMax) * ns must be <= 8192 for the dense BetaLambda branch");
+  s.phWork = dalloc<double>(phylo_work_doubles(ns, s.Kmax, nc, s.nrho));
+  s.mask &= ~(uint32_t)HMSC_UP_GAMMA2;  // updateGamma2 returns Gamma unchanged when C is given (R/updateGamma2.R:35-36)
+}
+
 // ---------------------------- create ----------------------------
 static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device, uint32_t mask, int rank,
                         int nranks, const void* comm_id) {
   HMSC_REQUIRE(m != nullptr, "model is NULL");
   HMSC_REQUIRE(m->ny > 0 && m->ns > 0 && m->nc >= 0 && m->nt > 0, "bad dimensions");
   HMSC_REQUIRE(m->nr >= 0 && m->nr <= HMSC_MAX_LEVELS, "nr out of range");
-  HMSC_REQUIRE(m->C == nullptr, "phylogeny (C != NULL) is a 'next' row: not in this build");
   s.ny = m->ny;
   s.ns = m->ns;
   s.nc = m->nc;
@@ -348,7 +394,12 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.Gamma = dalloc<double>(N);
   s.iV = dalloc<double>((size_t)nc * nc);
   s.iSigma = dalloc<double>(nsl);
-  s.rho = dalloc<int>(1);
+  s.rho = dalloc<double>(1);
+  {
+    const double one = 1.0;  // rho = 1 (R/computeInitialParameters.R:226)
+    HIP_OK(hipMemcpy(s.rho, &one, sizeof(double), hipMemcpyHostToDevice));
+  }
+  if (m->C != nullptr) setup_phylo(s, m);
   // workspaces
   const int n_tiles = (ny + 63) / 64;
   s.ntile_j = (nsl + 31) / 32;
@@ -408,7 +459,8 @@ static void free_state(State& s) {
                   s.aSigma, s.bSigma, s.XX, s.TT, s.V0g, s.V0gXXV0g, s.iV0, s.V0inv, s.iUmG, s.V0gXX, s.g2prep, s.scratch2, s.na_cols, s.na_index,
                   s.na_rows, s.row_na, s.row_slot, s.dev_flags, s.Z, s.XEta, s.BL, s.Psi, s.Delta, s.Gamma, s.iV,
                   s.iSigma, s.rho, s.XZ, s.G, s.ZTr, s.XZ_part, s.G_part, s.ZTr_part, s.Gna, s.ZL, s.ZL_part,
-                  s.CR, s.CR_part, s.LS, s.Msmall, s.scratch, s.psi_rs, s.ABpart, s.dbg_prec, s.ring, s.allreduce_buf};
+                  s.CR, s.CR_part, s.LS, s.Msmall, s.scratch, s.psi_rs, s.ABpart, s.dbg_prec, s.ring, s.allreduce_buf,
+                  s.phU, s.phWinv, s.phRbase, s.phTt, s.phBt, s.phEt, s.phTTw, s.phWork};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (int r = 0; r < s.nr; ++r) {
@@ -485,7 +537,9 @@ static void get_state(State& s, hmsc_params* p) {
       if (p->Alpha[r]) p->Alpha[r][h] = 1;
     }
   }
-  p->rho = 1;
+  double rho = 1.0;
+  HIP_OK(hipMemcpy(&rho, s.rho, sizeof(double), hipMemcpyDeviceToHost));
+  p->rho = (int32_t)rho;
 }
 
 static void set_state(State& s, const hmsc_params* p) {
@@ -527,6 +581,11 @@ static void set_state(State& s, const hmsc_params* p) {
   if (p->iV) h2d(s.iV, p->iV, (size_t)nc * nc, s.stream);
   if (p->iSigma) h2d(s.iSigma, p->iSigma, nsl, s.stream);
   if (p->Z) h2d(s.Z, p->Z, (size_t)s.ny * nsl, s.stream);
+  if (p->rho > 0) {  // initPar$rho as a grid index (R/computeInitialParameters.R:223-224)
+    HMSC_REQUIRE(!s.phylo || p->rho <= s.nrho, "set_state: rho index out of range");
+    const double rho = p->rho;
+    HIP_OK(hipMemcpy(s.rho, &rho, sizeof(double), hipMemcpyHostToDevice));
+  }
   HIP_OK(hipStreamSynchronize(s.stream));
   s.zt_valid = false;
   s.xeta_valid = false;
@@ -656,7 +715,8 @@ static void run_updater(State& s, uint32_t which, uint32_t iter) {
       launch_gamma_v(s, iter, s.stream);
       break;
     case HMSC_UP_RHO:
-      break;  // C is NULL: updateRho is not called (R/sampleMcmc.R:263)
+      if (s.phylo) launch_rho(s, iter, s.stream);  // only with C (R/sampleMcmc.R:263)
+      break;
     case HMSC_UP_LAMBDAPRIORS:
       launch_lambda_priors(s, iter, s.stream);
       break;
@@ -696,7 +756,7 @@ static void sweep(State& s, uint32_t iter, bool adapt) {
       if (s.mask & u) run_updater(s, u, iter);
   } else {
     // (sharded chains keep every RCCL collective on one stream: no side-stream overlap)
-    const bool side_work = s.nranks == 1 && !s.single_stream && (s.mask & (HMSC_UP_GAMMAV | HMSC_UP_LAMBDAPRIORS)) != 0;
+    const bool side_work = s.nranks == 1 && !s.single_stream && !s.phylo && (s.mask & (HMSC_UP_GAMMAV | HMSC_UP_LAMBDAPRIORS)) != 0;
     if (side_work) {
       HIP_OK(hipEventRecord(s.ev_bl, s.stream));
       HIP_OK(hipStreamWaitEvent(s.side, s.ev_bl, 0));
@@ -706,6 +766,7 @@ static void sweep(State& s, uint32_t iter, bool adapt) {
       s.side_pending = 3;
     } else {
       if (s.mask & HMSC_UP_GAMMAV) launch_gamma_v(s, iter, s.stream);
+      if ((s.mask & HMSC_UP_RHO) && s.phylo) launch_rho(s, iter, s.stream);  // R/sampleMcmc.R:263-266
       if (s.mask & HMSC_UP_LAMBDAPRIORS) launch_lambda_priors(s, iter, s.stream);
     }
     for (uint32_t u : {HMSC_UP_ETA, HMSC_UP_ALPHA, HMSC_UP_INVSIGMA, HMSC_UP_Z})
@@ -833,7 +894,6 @@ static void unpack_record(const State& s, const double* slot, int k, int samples
   if (rec->Gamma) std::memcpy(rec->Gamma + (size_t)k * nc * nt, Gamma, sizeof(double) * nc * nt);
   if (rec->iV) std::memcpy(rec->iV + (size_t)k * nc * nc, iV, sizeof(double) * nc * nc);
   if (rec->iSigma) std::memcpy(rec->iSigma + (size_t)k * nsl, iS, sizeof(double) * nsl);
-  if (rec->rho) rec->rho[k] = 1;
   for (int r = 0; r < s.nr; ++r) {
     const Level& L = s.lev[r];
     const int nf = L.nf, nfm = L.nfmax, lo = s.loff(r), fo = s.foff(r);
@@ -859,6 +919,7 @@ static void unpack_record(const State& s, const double* slot, int k, int samples
       }
     eta += (size_t)L.np * nf;
   }
+  if (rec->rho) rec->rho[k] = (int32_t)eta[0];  // packed after the Eta blocks (launch_record)
 }
 
 static void run(State& s, int transient, int samples, int thin, const int* adaptNf, int iter0, int verbose,
@@ -1094,6 +1155,8 @@ int hmsc_init_state(hmsc_state* h, const int32_t* nf0) {
     s.refresh_dims();
     HMSC_REQUIRE(s.K <= s.Kmax, "init: K exceeds 64");
     launch_init(s);
+    const double one = 1.0;  // rho = 1 (R/computeInitialParameters.R:226)
+    HIP_OK(hipMemcpyAsync(s.rho, &one, sizeof(double), hipMemcpyHostToDevice, s.stream));
     s.graph_dirty = true;
     s.xeta_valid = false;
     launch_update_z(s, 0, true);  // Z = updateZ(Y=hM$Y, ...) (R/computeInitialParameters.R:254)

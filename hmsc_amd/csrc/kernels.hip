@@ -449,6 +449,10 @@ __global__ __launch_bounds__(256) void beta_lambda_wave_kernel(BLArgs a) {
 void launch_beta_lambda(State& s, uint32_t iter) {
   if (!s.xeta_valid) launch_xeta(s);
   if (!s.zt_valid) launch_zt_refresh(s);
+  if (s.phylo) {  // dense branch with phylogeny (R/updateBetaLambda.R:124-147), phylo.hip
+    launch_beta_lambda_phylo(s, iter);
+    return;
+  }
   if (s.n_na_cols > 0) {
     EtaView ev = make_view(s);
     gram_na_kernel<<<s.n_na_cols, 256, 0, s.stream>>>(ev, s.XEta, s.K, s.Kmax, s.na_cols, s.Ycode, s.Gna);
@@ -848,7 +852,7 @@ static void launch_gammav_wave(State& s, uint32_t iter, hipStream_t st, const do
     w.f0 = s.f0;
     w.iUGamma = s.iUGamma;
     w.iUmG = s.iUmG;
-    w.TT = s.TT;
+    w.TT = s.phylo ? s.phTTw : s.TT;  // Tr^T iQ Tr with phylogeny (R/updateGammaV.R:29)
     w.iV = s.iV;
     w.Gamma = s.Gamma;
     w.XX = s.XX;
@@ -877,10 +881,15 @@ static void launch_gammav_wave(State& s, uint32_t iter, hipStream_t st, const do
 void launch_gamma_v(State& s, uint32_t iter, hipStream_t st) {
   const int nparts = (s.nsl + SB - 1) / SB;
   double* part = s.ABpart;
-  gammav_partial_kernel<<<nparts, 256, (size_t)(2 * s.nc * SB + SB * s.nt) * sizeof(double), st>>>(
-      s.BL, s.K, s.nc, s.nt, s.nsl, s.Gamma, s.Tr, part);
-  HIP_OK(hipGetLastError());
   int np = nparts;
+  if (s.phylo) {  // E iQ E^T, B iQ Tr, Tr^T iQ Tr in the eigenbasis of C (phylo.hip)
+    launch_phylo_gv_sums(s, iter, st);
+    np = 1;
+  } else {
+    gammav_partial_kernel<<<nparts, 256, (size_t)(2 * s.nc * SB + SB * s.nt) * sizeof(double), st>>>(
+        s.BL, s.K, s.nc, s.nt, s.nsl, s.Gamma, s.Tr, part);
+    HIP_OK(hipGetLastError());
+  }
   if (s.nranks > 1) {
     const int64_t n = (int64_t)s.nc * s.nc + (int64_t)s.nc * s.nt;
     slab_sum_kernel<<<grid_for(n), 256, 0, st>>>(part, s.allreduce_buf, n, nparts, n);
@@ -904,7 +913,7 @@ void launch_gamma_v(State& s, uint32_t iter, hipStream_t st) {
   a.iUGamma = s.iUGamma;
   a.mGamma = s.mGamma;
   a.iUmG = s.iUmG;
-  a.TT = s.TT;
+  a.TT = s.phylo ? s.phTTw : s.TT;
   a.iV = s.iV;
   a.Gamma = s.Gamma;
   a.scratch = s.scratch;
@@ -1946,7 +1955,7 @@ static void launch_eta_fused(State& s, uint32_t iter, bool cr_done);
 
 bool side_fusion_ok(const State& s) {
   const uint32_t need = HMSC_UP_GAMMAV | HMSC_UP_LAMBDAPRIORS | HMSC_UP_ETA;
-  return (s.mask & need) == need && !s.single_stream && s.nc * s.nt <= 32 && s.NF <= 64 && eta_fused_ok(s) &&
+  return (s.mask & need) == need && !s.single_stream && !s.phylo && s.nc * s.nt <= 32 && s.NF <= 64 && eta_fused_ok(s) &&
          !getenv_flag("HMSC_NO_SIDE_FUSION");
 }
 
@@ -2412,7 +2421,7 @@ void launch_copied_flag(State& s, uint64_t value) {
 // slot layout: BL(K*nsl) | Psi(NF*nsl) | Delta(NF) | Gamma(nc*nt) | iV(nc*nc) | iSigma(nsl) | Eta_r ... | rho(1)
 size_t record_slot_doubles(const State& s) {
   size_t n = (size_t)s.Kmax * s.nsl + (size_t)s.NFmax * s.nsl + s.NFmax + (size_t)s.nc * s.nt +
-             (size_t)s.nc * s.nc + s.nsl + 1;
+             (size_t)s.nc * s.nc + s.nsl + 2;
   for (int r = 0; r < s.nr; ++r) n += (size_t)s.lev[r].np * s.lev[r].nfmax;
   return n;
 }
@@ -2434,6 +2443,7 @@ void launch_record(State& s, double* slot, int part) {
   add(s.iV, (int64_t)s.nc * s.nc, true);
   add(s.iSigma, s.nsl, false);
   for (int r = 0; r < s.nr; ++r) add(s.lev[r].Eta, (int64_t)s.lev[r].np * s.lev[r].nf, false);
+  add(s.rho, 1, true);  // updateRho's grid index (written with GammaV's outputs)
   a.npieces = k;
   a.slot = slot;
   if (slot == nullptr) {  // captured into a graph replay: slot chosen on the device

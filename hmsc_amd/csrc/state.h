@@ -91,7 +91,20 @@ struct State {
   // chain state (device)
   double *Z = nullptr, *BL = nullptr, *Psi = nullptr, *Delta = nullptr;
   double *Gamma = nullptr, *iV = nullptr, *iSigma = nullptr;
-  int* rho = nullptr;
+  double* rho = nullptr;          // updateRho grid index, 1-based (R's rho), as a double
+
+  // phylogeny (hM$C != NULL, phylo.hip): spectral form of computeDataParameters' Qg grid
+  bool phylo = false;
+  int nrho = 0;
+  int phNmax = 0;                // K * ns the dense BetaLambda workspace holds
+  double* phU = nullptr;         // ns x ns eigenvectors of C
+  double* phWinv = nullptr;      // nrho x ns  1 / q_g,i
+  double* phRbase = nullptr;     // nrho  log(rhopw[,2]) - nc/2 logdet Q_g
+  double* phTt = nullptr;        // ns x nt  U^T Tr
+  double* phBt = nullptr;        // nc x ns  Beta U
+  double* phEt = nullptr;        // nc x ns  Beta U - Gamma Tt^T
+  double* phTTw = nullptr;       // nt x nt  Tr^T iQ Tr
+  double* phWork = nullptr;      // dense BetaLambda / Rho workspace
 
   // per-sweep workspaces
   double* XEta = nullptr;        // ny x Kmax    [X, Eta_1[Pi_1], ...] materialised per Eta update
@@ -213,6 +226,11 @@ void launch_inv_sigma(State& s, uint32_t iter);
 // quantities (BL, Psi, iSigma, Eta), 2 the side-stream ones (Gamma, iV, Delta) on `side`
 void launch_record(State& s, double* slot, int part = 0);
 bool side_fusion_ok(const State& s);
+// phylogeny branch (phylo.hip)
+size_t phylo_work_doubles(int ns, int Kmax, int nc, int nrho);
+void launch_phylo_gv_sums(State& s, uint32_t iter, hipStream_t st);
+void launch_rho(State& s, uint32_t iter, hipStream_t st);
+void launch_beta_lambda_phylo(State& s, uint32_t iter);
 void launch_side_fused(State& s, uint32_t iter);  // GammaV + LambdaPriors + Eta, co-launched
 void join_side(State& s);
 void launch_copied_flag(State& s, uint64_t value);

@@ -33,9 +33,6 @@ class ModelBuffers:
     R ``.Call`` shim would do), kept alive for the lifetime of the C struct."""
 
     def __init__(self, hM):
-        if hM.C is not None:
-            raise NotImplementedError("phylogeny (C / phyloTree) is a 'next' row (SURVEY.md §8 f1): "
-                                      "the dense BetaLambda branch and updateRho are not on the device yet")
         for rl in hM.rL or []:
             if rl.sDim:
                 raise NotImplementedError("spatial random levels are a 'next' row (SURVEY.md §8 f2)")
@@ -70,6 +67,17 @@ class ModelBuffers:
         m.sDim = L.colmajor_ptr([0] * max(1, hM.nr), k, np.int32)
         m.xDim = L.colmajor_ptr([0] * max(1, hM.nr), k, np.int32)
         m.C = None
+        if hM.C is not None:
+            # computeDataParameters' rho grid in spectral form (include/hmsc_amd.h): the
+            # R shim would pass eigen(hM$C, symmetric=TRUE)
+            Cm = np.asarray(hM.C, dtype=np.float64)
+            d, U = np.linalg.eigh(Cm)
+            rhopw = np.asarray(hM.rhopw, dtype=np.float64)
+            m.C = L.colmajor_ptr(Cm, k)
+            m.nrho = rhopw.shape[0]
+            m.rhopw = L.colmajor_ptr(rhopw, k)
+            m.C_vectors = L.colmajor_ptr(U, k)
+            m.C_values = L.colmajor_ptr(d, k)
         self.struct = m
 
 
@@ -174,6 +182,8 @@ class Chain:
         for key in ("Gamma", "iV", "Beta", "iSigma", "Z"):
             if st.get(key) is not None:
                 setattr(p, key, L.colmajor_ptr(st[key], keep))
+        if st.get("rho") is not None:
+            p.rho = int(st["rho"])   # 1-based grid index, as parList$rho
         for r in range(hM.nr):
             nf = 0
             for key in ("Eta", "Lambda", "Psi", "Delta"):

@@ -72,8 +72,15 @@ typedef struct hmsc_model {
   const int32_t* nfMax;
   const int32_t* sDim;    /* spatial levels are a 'next' row: must be 0 */
   const int32_t* xDim;    /* covariate-dependent levels: must be 0       */
-  /* phylogeny (C != NULL) is a 'next' row: must be NULL in this build */
-  const double* C;
+  /* Phylogeny (hM$C; NULL = none).  The grid of R/computeDataParameters.R:19-39
+   * (iQg/RQg/detQg over hM$rhopw) is taken in spectral form: the caller passes the
+   * eigendecomposition of C (R: e <- eigen(hM$C, symmetric=TRUE); numpy: eigh), from which
+   * every Q_g = rho_g C + (1-rho_g) I (or -rho_g iC + (1+rho_g) I for rho_g < 0) follows. */
+  const double* C;        /* ns*ns (only tested for != NULL)                  */
+  int32_t nrho;           /* nrow(hM$rhopw)                                    */
+  const double* rhopw;    /* nrho*2 column-major: grid value, prior weight     */
+  const double* C_vectors;/* ns*ns eigenvectors of C, column-major             */
+  const double* C_values; /* ns    eigenvalues of C (> 0)                      */
 } hmsc_model;
 
 /* Sampler state = R's parList (R/computeInitialParameters.R:256-270) with iV in

@@ -13,7 +13,7 @@ from oracle import hmsc_oracle as O  # noqa: E402
 
 
 def synthetic_model(ny=200, ns=30, nc=4, nf=3, seed=1, na_frac=0.0, n_normal=0, units=None, nr=1,
-                    nf_fit=None, nt=1, yscale=False):
+                    nf_fit=None, nt=1, yscale=False, C=None):
     """Probit (optionally mixed normal) JSDM generated like BASELINE.md's synthetic config."""
     rng = np.random.default_rng(seed)
     X = np.column_stack([np.ones(ny), rng.standard_normal((ny, nc - 1))])
@@ -50,9 +50,17 @@ def synthetic_model(ny=200, ns=30, nc=4, nf=3, seed=1, na_frac=0.0, n_normal=0, 
     import pandas as pd
     studyDesign = pd.DataFrame(sd) if nr > 0 else None
     covn = ["(Intercept)"] + [f"x{k}" for k in range(1, nc)]
-    hM = H.Hmsc(Y=Y, X=X, covNames=covn, XScale=True, YScale=yscale, Tr=Tr, distr=distr,
+    hM = H.Hmsc(Y=Y, X=X, covNames=covn, XScale=True, YScale=yscale, Tr=Tr, distr=distr, C=C,
                 studyDesign=studyDesign, ranLevels=ranLevels if nr > 0 else None)
     return hM
+
+
+def phylo_corr(ns, seed=0, scale=0.6):
+    """Positive-definite phylogenetic correlation matrix: exp(-distance / scale) between random
+    points on a line (an exponential / Ornstein-Uhlenbeck kernel), unit diagonal like vcv(tree, corr=TRUE)."""
+    rng = np.random.default_rng(seed)
+    x = np.sort(rng.random(ns))
+    return np.exp(-np.abs(x[:, None] - x[None, :]) / scale)
 
 
 def oracle_model(hM):
