@@ -288,7 +288,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
     const int jg = sp0 + j;
     fam[j] = m->distr[jg];
     var[j] = m->distr[jg + (size_t)m->ns];
-    HMSC_REQUIRE(fam[j] == 1 || fam[j] == 2, "Poisson species (distr family 3) are a 'next' row: not in this build");
+    HMSC_REQUIRE(fam[j] >= 1 && fam[j] <= 3, "distr family must be 1 (normal), 2 (probit) or 3 (Poisson)");
     if (fam[j] != 2) s.all_probit = false;
     if (fam[j] == 1) s.any_normal = true;
     if (var[j] == 1) s.any_var = true;

@@ -26,8 +26,12 @@ enum Stream : uint32_t {
   S_WISHART_OFF = 5,
   S_GAMMAV = 6,
   S_RHO = 7,
+  S_GE_BETA = 8,   // updateGammaEta (+ LEVEL_STRIDE * r)
+  S_GE_GAMMA = 9,
+  S_GE_ETA = 10,
   S_INVSIGMA = 11,
   S_Z = 12,
+  S_ZPOIS = 13,
   S_PSI = 20,
   S_DELTA = 21,
   S_ETA = 22,
@@ -324,6 +328,31 @@ __host__ __device__ __forceinline__ double gamma_std(Key key, uint32_t idx, uint
     out *= pow(u, 1.0 / shape);
   }
   return out;
+}
+
+// Mean and variance of the Polya-Gamma PG(b, c) (Polson, Scott & Windle 2013):
+//   E = b tanh(c/2) / (2c),   Var = b (sinh c - c) sech^2(c/2) / (4 c^3)
+// written as b (2 tanh(x/2) - x sech^2(x/2)) / (4 x^3) for x = |c| >= 1 (no overflow) and
+// as the Taylor series (sinh x - x) / x^3 = sum_k x^2k / (2k+3)! below 1 (no cancellation).
+// oracle/hmsc_oracle.py pg_moments is the same formula.
+__host__ __device__ inline void pg_moments(double b, double c, double* mean, double* var) {
+  const double x = fabs(c), x2 = x * x;
+  const double th = tanh(0.5 * x);
+  *mean = b * (x < 1e-4 ? 0.25 - x2 / 48.0 : th / (2.0 * x));
+  const double ch = cosh(0.5 * x);
+  const double sech2 = 1.0 / (ch * ch);
+  if (x < 1.0) {
+    double q = 1.0 + x2 / 272.0;
+    q = 1.0 + x2 / 210.0 * q;
+    q = 1.0 + x2 / 156.0 * q;
+    q = 1.0 + x2 / 110.0 * q;
+    q = 1.0 + x2 / 72.0 * q;
+    q = 1.0 + x2 / 42.0 * q;
+    q = 1.0 + x2 / 20.0 * q;
+    *var = b * (q / 6.0) * sech2 / 4.0;
+  } else {
+    *var = b * (2.0 * th - x * sech2) / (4.0 * x2 * x);
+  }
 }
 
 // Standard normal truncated to [alpha, +inf) by inversion of the upper tail:

@@ -40,6 +40,7 @@ struct ZArgs {
   uint32_t iter;
   const uint32_t* iter_dev;  // graph replay: the sweep counter is read from the device
   int noise_zero;
+  int zprev_is_e;            // chain init: ZPrev = LFix + LRan (R/computeInitialParameters.R:250-254)
   unsigned long long* kt;    // live launch timing (KT_Z block) or null
 };
 
@@ -90,6 +91,22 @@ __device__ __noinline__ double z_probit_draw(double e, double sd, double isd, in
   if (code < 0 && noise_zero) return e;
   const double alpha = code < 0 ? -INFINITY : -sg * e * isd;
   return e + sd * sg * trunc_normal_lower(alpha, u);
+}
+
+// Poisson cell (R/updateZ.R:65-90): omega ~ PG(y + r, zPrev - log r) with r = 1000, then
+// Z ~ N(sigmaZ ((y - r)/2 + prec (E - log r)) + log r, sigmaZ), sigmaZ = 1 / (prec + omega).
+// BayesLogit's rpg takes its normal-approximation branch for h > 170 (always: h >= 1000), so
+// omega = PG mean + PG sd * N(0,1); both normals invert the cell's own Philox block (S_ZPOIS).
+__device__ __noinline__ double z_poisson_draw(double e, double sd, double y, double zprev, Uniform2 u,
+                                              int noise_zero) {
+  constexpr double R_NB = 1000.0, LOG_R = 6.907755278982137;
+  double m, v;
+  pg_moments(y + R_NB, zprev - LOG_R, &m, &v);
+  const double omega = noise_zero ? m : fma(sqrt(v), qnorm_fast(u.a), m);
+  const double prec = 1.0 / (sd * sd);
+  const double sigz = 1.0 / (prec + omega);
+  const double muz = fma(sigz, fma(prec, e - LOG_R, 0.5 * (y - R_NB)), LOG_R);
+  return noise_zero ? muz : fma(sqrt(sigz), qnorm_fast(u.b), muz);
 }
 
 // NKB = 16-row blocks of K (XZ output tiles per species block)
@@ -183,6 +200,11 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
               const double e = sT[jj * ZT_TLD + s];
               if (sFam[jj] == 1 && code >= 0)
                 z = a.Yval[cell];  // normal: Z = Y   R/updateZ.R:40-41
+              else if (sFam[jj] == 3 && code >= 0)
+                z = z_poisson_draw(e, sSd[jj], a.Yval[cell], a.zprev_is_e ? e : a.Z[cell],
+                                   uniforms(a.key, (uint32_t)((size_t)i + (size_t)ny * (uint32_t)(a.sp0 + j)), 0,
+                                            S_ZPOIS, SWEEP_ITER(a)),
+                                   a.noise_zero);
               else if (MODE & 2)
                 z = z_probit_draw(e, sSd[jj], sIsd[jj], code, b ? u.b : u.a, a.noise_zero);
               else

@@ -208,13 +208,19 @@ def getPostEstimate(hM, parName, r=1, x=None, q=(), chainIndex=None, start=1):
 
 
 def computeWAIC(hM, ghN=11):
-    """R/computeWAIC.R:25-131 for normal and probit columns."""
+    """R/computeWAIC.R:25-131.  Poisson columns integrate the lognormal intensity with
+    ghN-point Gauss-Hermite quadrature (:108-118); ``dpois(Y, exp(gX))`` there recycles the
+    whole ny x ns Y column-major against the ny x cN x ghN node array, which is reproduced
+    as written (it only equals the per-cell likelihood when every species is Poisson)."""
     post = poolMcmcChains(hM.postList)
     Y, X, Pi = hM.Y, hM.X, hM.Pi
     fam = hM.distr[:, 0]
-    if np.any(fam == 3):
-        raise NotImplementedError("computeWAIC for Poisson columns needs the Poisson path (SURVEY.md §8 f3)")
-    normal, probit = fam == 1, fam == 2
+    normal, probit, pois = fam == 1, fam == 2, fam == 3
+    if pois.any():
+        gx, gw = np.polynomial.hermite.hermgauss(ghN)   # statmod::gauss.quad(kind="hermite")
+        cN = int(pois.sum())
+        ii, cc, gg = np.meshgrid(np.arange(hM.ny), np.arange(cN), np.arange(ghN), indexing="ij")
+        Yrec = Y.ravel(order="F")[(ii + hM.ny * cc + hM.ny * cN * gg) % Y.size]
     na = np.isnan(Y)
     vals = []
     for s in post:
@@ -233,6 +239,12 @@ def computeWAIC(hM, ghN=11):
             Yp = Y[:, probit]
             t = pz1 * Yp + pz0 * (1 - Yp)
             t[na[:, probit]] = 0
+            Lr += t.sum(axis=1)
+        if pois.any():
+            gX = E[:, pois][:, :, None] + np.sqrt(2.0) * gx[None, None, :] * std[pois][None, :, None]
+            like = stats.poisson.pmf(Yrec, np.exp(gX))
+            t = np.log(np.sum(like * gw[None, None, :], axis=2) / np.sqrt(np.pi))
+            t[na[:, pois]] = 0
             Lr += t.sum(axis=1)
         vals.append(Lr)
     val = np.stack(vals)

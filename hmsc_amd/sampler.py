@@ -38,8 +38,6 @@ class ModelBuffers:
                 raise NotImplementedError("spatial random levels are a 'next' row (SURVEY.md §8 f2)")
             if rl.xDim:
                 raise NotImplementedError("covariate-dependent random levels are a 'next' row")
-        if np.any(hM.distr[:, 0] == 3):
-            raise NotImplementedError("Poisson / lognormal-Poisson species are a 'next' row (SURVEY.md §8 f3)")
         self.keep = []
         k = self.keep
         m = L.hmsc_model()

@@ -96,7 +96,49 @@ def linear_predictor(st, model):
 # ---------------------------------------------------------------------------
 # updateZ — R/updateZ.R:4-94 (normal :40-41, probit :43-63, NA :92)
 # ---------------------------------------------------------------------------
-def update_z(st, model, rng, it, Y=None):
+POIS_R = 1e3   # Poisson as the limit of the negative binomial, R/updateZ.R:68
+
+
+def pg_moments(b, c):
+    """Mean and variance of the Polya-Gamma PG(b, c) (Polson, Scott & Windle 2013, eqs. in
+    section 2.2): E = b tanh(c/2) / (2c), Var = b (sinh c - c) sech^2(c/2) / (4 c^3), written
+    as b (2 tanh(x/2) - x sech^2(x/2)) / (4 x^3) for x = |c| >= 1 and as its Taylor series
+    below 1 (no cancellation, no overflow).  Same formulas as rng.h pg_moments."""
+    x = np.abs(np.asarray(c, dtype=np.float64))
+    x2 = x * x
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+        m = np.where(x < 1e-4, 0.25 - x2 / 48.0, np.tanh(0.5 * x) / (2.0 * x))
+        # (sinh x - x) / x^3 = sum_k x^(2k) / (2k+3)!
+        q = 1.0 + x2 / 272.0
+        for d in (210.0, 156.0, 110.0, 72.0, 42.0, 20.0):
+            q = 1.0 + x2 / d * q
+        q = q / 6.0
+        ch = np.cosh(0.5 * x)
+        sech2 = 1.0 / (ch * ch)
+        v_small = q * sech2 / 4.0
+        v_big = (2.0 * np.tanh(0.5 * x) - x * sech2) / (4.0 * x2 * x)
+        v = np.where(x < 1.0, v_small, v_big)
+    return b * m, b * v
+
+
+def poisson_z_draw(y, e, sd, zprev, u1, u2, zero_noise=False):
+    """Poisson Z (R/updateZ.R:65-90): omega ~ PG(y + r, zPrev - log r), r = 1000; then
+    Z ~ N(sigmaZ ((y - r)/2 + prec (E - log r)) + log r, sigmaZ), sigmaZ = 1/(prec + omega).
+    BayesLogit's rpg draws PG(h, z) for h > 170 -- always here, h >= 1000 -- as the normal
+    with the PG mean and variance (PolyaGammaHybrid::draw, BayesLogit 2.x; the package is
+    unvendored and unpinned, DESCRIPTION:33), so omega = m + sqrt(v) Phi^-1(u1)."""
+    lr = np.log(POIS_R)
+    m, v = pg_moments(y + POIS_R, zprev - lr)
+    omega = m if zero_noise else m + np.sqrt(v) * R.qnorm_as241(u1.ravel()).reshape(u1.shape)
+    prec = sd ** -2.0
+    sigz = 1.0 / (prec + omega)
+    muz = sigz * ((y - POIS_R) / 2.0 + prec * (e - lr)) + lr
+    if zero_noise:
+        return muz
+    return muz + np.sqrt(sigz) * R.qnorm_as241(u2.ravel()).reshape(u2.shape)
+
+
+def update_z(st, model, rng, it, Y=None, zero_noise=False):
     Y = model["Y"] if Y is None else Y
     ny, ns = Y.shape
     E = linear_predictor(st, model)
@@ -106,8 +148,6 @@ def update_z(st, model, rng, it, Y=None):
     j = np.arange(ns)
     idx = (np.arange(ny)[:, None] + ny * (j[None, :] >> 1)).astype(np.uint64)
     fam = model["distr"][:, 0]
-    if np.any(fam == 3):
-        raise NotImplementedError("Poisson updateZ (Polya-Gamma) is a 'next' row (SURVEY.md §8 f3)")
     na = np.isnan(Y)
     Z = np.empty((ny, ns))
     normal_cols = fam == 1
@@ -120,6 +160,14 @@ def update_z(st, model, rng, it, Y=None):
     zp = E + sd[None, :] * s * w
     probit_cols = fam == 2
     Z[:, probit_cols] = zp[:, probit_cols]
+    pois_cols = fam == 3
+    if pois_cols.any():   # R/updateZ.R:65-90
+        jp = np.nonzero(pois_cols)[0]
+        Zprev = st["Z"][:, jp] if "Z" in st else E[:, jp]   # init: Z = LFix + LRan (computeInitialParameters.R:250-254)
+        cell = (np.arange(ny)[:, None] + ny * jp[None, :]).astype(np.uint64)
+        u1, u2 = rng.uniforms(cell, 0, R.S_ZPOIS, it)
+        Z[:, jp] = poisson_z_draw(Y[:, jp], E[:, jp], sd[jp][None, :], Zprev, u1, u2,
+                                  zero_noise)
     if na.any():   # R/updateZ.R:92: N(E, sd), drawn by inversion of the same uniform
         nz = E - sd[None, :] * R.qnorm_as241(u.ravel()).reshape(u.shape)
         Z[na] = nz[na]
@@ -512,7 +560,7 @@ def sweep(st, model, rng, it, updater=None, data_par=None, adapt_nf=None):
     if on("Gamma2"):
         st["Gamma"] = update_gamma2(st, model, rng, it)
     if on("GammaEta"):
-        raise NotImplementedError("updateGammaEta is a 'next' row (SURVEY.md §8 f1); pass updater GammaEta=False")
+        st["Gamma"], st["Eta"] = update_gamma_eta(st, model, rng, it, data_par)
     if on("BetaLambda"):
         st["Beta"], st["Lambda"] = update_beta_lambda(st, model, rng, it, data_par)
     if on("GammaV"):
@@ -536,6 +584,129 @@ def sweep(st, model, rng, it, updater=None, data_par=None, adapt_nf=None):
             st["Psi"] = list(st["Psi"]); st["Psi"][r] = p
             st["Delta"] = list(st["Delta"]); st["Delta"][r] = d
     return st
+
+
+# ---------------------------------------------------------------------------
+# updateGammaEta — R/updateGammaEta.R:7-206 (non-spatial levels, xDim = 0)
+# Gamma and Eta_r given Z with Beta integrated out, level by level; Beta is drawn as an
+# auxiliary and discarded (the function returns only Gamma and Eta).  Randomness: Beta's
+# rnorm(nc*ns) is normal(c + nc*j, 0, S_GE_BETA), Gamma's normal(c + nc*t, 0, S_GE_GAMMA),
+# Eta's rnorm(ny*nf) / rnorm(np*nf) normal(row i (np == ny) or unit p, h, S_GE_ETA), each
+# plus LEVEL_STRIDE * r.
+# ---------------------------------------------------------------------------
+def update_gamma_eta(st, model, rng, it, data_par=None, zero_noise=False):
+    X, Tr, Pi, Z = model["X"], model["Tr"], model["Pi"], st["Z"]
+    ny, ns = Z.shape
+    nc, nt, nr = X.shape[1], Tr.shape[1], Pi.shape[1]
+    dp = data_par if data_par is not None else compute_data_parameters(model)
+    g = st.get("rho", 1) - 1 if model.get("C") is not None else 0
+    Q, iQ, RQ = dp["Qg"][g], dp["iQg"][g], dp["RQg"][g]
+    iV = st["iV"]
+    V = chol2inv(chol_upper(iV))
+    U = model["UGamma"]
+    iU = chol2inv(chol_upper(U))
+    idv = st["iSigma"]
+    lam_all = st["Lambda"]
+    LRan = [eta_full(st, model, r) @ lam_all[r] for r in range(nr)]          # :15-26
+    Eta = [e.copy() for e in st["Eta"]]
+    Gamma = st["Gamma"]
+    XtX = X.T @ X
+    KT = np.kron(Tr, np.eye(nc))
+    A = KT @ U @ KT.T + np.kron(Q, V)                                         # :32
+    iA = chol2inv(chol_upper(A))                                              # :33
+
+    def nrm(idx, sub, stream, shape):
+        if zero_noise:
+            return np.zeros(shape)
+        return rng.normal(idx, sub, stream, it).reshape(shape, order="F")
+
+    for r in range(nr):
+        rl = model["rL"][r]
+        if rl.get("sDim", 0) or rl.get("xDim", 0):
+            raise NotImplementedError("updateGammaEta: spatial / covariate-dependent levels (SURVEY.md §8 f2)")
+        s = R.LEVEL_STRIDE * r
+        S = Z - sum(LRan[q] for q in range(nr) if q != r) if nr > 1 else Z  # :37-42
+        lam = lam_all[r]
+        nf = lam.shape[0]
+        lPi = Pi[:, r] - 1
+        npr = int(model["np"][r])
+        LamiD = lam * idv[None, :]
+        LamiDLam = (lam * np.sqrt(idv)[None, :]) @ (lam * np.sqrt(idv)[None, :]).T
+        XtS = X.T @ S
+        mb10 = (XtS * idv[None, :]).ravel(order="F")
+        jj, cc = np.meshgrid(np.arange(ns), np.arange(nc))
+        xi_b = nrm((cc + nc * jj).ravel(order="F"), 0, R.S_GE_BETA + s, nc * ns)
+        if npr == ny:                                                         # :51-75
+            W0 = LamiDLam + np.eye(nf)
+            RW0 = chol_upper(W0)
+            iW0 = chol2inv(RW0)
+            iLW0LamiD = backsolve(RW0, LamiD, transpose=True)
+            tmp1 = np.diag(idv) - iLW0LamiD.T @ iLW0LamiD
+            K1 = np.kron(tmp1, XtX)
+            M = iA + K1
+            RM = chol_upper(M)
+            mb20 = ((XtS @ LamiD.T) @ iW0 @ LamiD).ravel(order="F")
+            mb31 = backsolve(RM, backsolve(RM, mb10 - mb20, transpose=True))
+            mb30 = K1 @ mb31
+            mb = A @ (mb10 - mb20 - mb30)
+            Beta = (mb + backsolve(RM, xi_b)).reshape((nc, ns), order="F")
+        else:                                                                 # :76-150
+            P = np.zeros((ny, npr))
+            P[np.arange(ny), lPi] = 1.0
+            PtX = P.T @ X
+            colSumP = P.sum(axis=0)
+            iWs, LiWs = [], []
+            for q in range(npr):
+                Wp = np.eye(nf) + colSumP[q] * LamiDLam
+                RWp = chol_upper(Wp)
+                iWs.append(chol2inv(RWp))
+                LiWs.append(np.linalg.solve(RWp, np.eye(nf)))
+            # W, iW, LiW are block-diagonal in the (p + np h) ordering of vec(np x nf)
+            LiW = np.zeros((nf * npr, nf * npr))
+            iW = np.zeros((nf * npr, nf * npr))
+            for q in range(npr):
+                ix = q + npr * np.arange(nf)
+                LiW[np.ix_(ix, ix)] = LiWs[q]
+                iW[np.ix_(ix, ix)] = iWs[q]
+            LamiD_PtX = np.kron(LamiD, PtX)
+            iLW = LiW.T @ LamiD_PtX
+            tmp1 = np.kron(np.diag(idv), XtX) - iLW.T @ iLW
+            M = iA + tmp1
+            RM = chol_upper(M)
+            mb21 = ((P.T @ S) @ LamiD.T).ravel(order="F")
+            mb22 = iW @ mb21
+            mb20 = (PtX.T @ mb22.reshape((npr, nf), order="F") @ LamiD).ravel(order="F")
+            mb31 = backsolve(RM, backsolve(RM, mb10 - mb20, transpose=True))
+            mb30 = tmp1 @ mb31
+            mb = A @ (mb10 - mb20 - mb30)
+            Beta = (mb + backsolve(RM, xi_b)).reshape((nc, ns), order="F")
+        # Gamma | Beta  (:66-69 / :130-133)
+        TQT = backsolve(RQ, Tr, transpose=True)
+        RG = chol_upper(iU + np.kron(TQT.T @ TQT, iV))
+        mg = chol2inv(RG) @ ((iV @ Beta) @ (iQ @ Tr)).ravel(order="F")
+        tt, cg = np.meshgrid(np.arange(nt), np.arange(nc))
+        xi_g = nrm((cg + nc * tt).ravel(order="F"), 0, R.S_GE_GAMMA + s, nc * nt)
+        Gamma = (mg + backsolve(RG, xi_g)).reshape((nc, nt), order="F")
+        # Eta | Beta, S
+        S1 = S - X @ Beta
+        if npr == ny:                                                         # :71-74
+            me = S1 @ LamiD.T @ iW0
+            hh, ii = np.meshgrid(np.arange(nf), np.arange(ny))
+            xi = nrm(ii.ravel(order="F"), hh.ravel(order="F"), R.S_GE_ETA + s, (ny, nf))
+            E = np.empty((ny, nf))
+            E[lPi, :] = me + backsolve(RW0, xi.T).T
+            Eta[r] = E
+        else:                                                                 # :136-146
+            PtS1 = P.T @ S1
+            me10 = (PtS1 @ LamiD.T).ravel(order="F")
+            me21 = iW @ me10
+            me20 = (np.diag(colSumP) @ me21.reshape((npr, nf), order="F") @ LamiDLam).ravel(order="F")
+            me = me10 - me20
+            hh, qq = np.meshgrid(np.arange(nf), np.arange(npr))
+            xi = nrm(qq.ravel(order="F"), hh.ravel(order="F"), R.S_GE_ETA + s, nf * npr)
+            Eta[r] = (me + LiW @ xi).reshape((npr, nf), order="F")
+        LRan[r] = Eta[r][lPi, :] @ lam                                        # :201
+    return Gamma, Eta
 
 
 # ---------------------------------------------------------------------------

@@ -25,8 +25,12 @@ S_WISHART_DIAG = 4
 S_WISHART_OFF = 5
 S_GAMMAV = 6
 S_RHO = 7
+S_GE_BETA = 8
+S_GE_GAMMA = 9
+S_GE_ETA = 10
 S_INVSIGMA = 11
 S_Z = 12
+S_ZPOIS = 13
 S_PSI = 20
 S_DELTA = 21
 S_ETA = 22

@@ -13,8 +13,10 @@ from oracle import hmsc_oracle as O  # noqa: E402
 
 
 def synthetic_model(ny=200, ns=30, nc=4, nf=3, seed=1, na_frac=0.0, n_normal=0, units=None, nr=1,
-                    nf_fit=None, nt=1, yscale=False, C=None):
-    """Probit (optionally mixed normal) JSDM generated like BASELINE.md's synthetic config."""
+                    nf_fit=None, nt=1, yscale=False, C=None, n_poisson=0, n_lognormal=0):
+    """Probit JSDM generated like BASELINE.md's synthetic config; optionally the first
+    n_normal species normal, the next n_poisson Poisson and n_lognormal lognormal Poisson
+    (counts ~ Poisson(exp(L / 2)), vignette_2's mixed-distribution model)."""
     rng = np.random.default_rng(seed)
     X = np.column_stack([np.ones(ny), rng.standard_normal((ny, nc - 1))])
     Tr = np.column_stack([np.ones(ns)] + [rng.standard_normal(ns) for _ in range(nt - 1)]) if nt > 1 else None
@@ -44,6 +46,10 @@ def synthetic_model(ny=200, ns=30, nc=4, nf=3, seed=1, na_frac=0.0, n_normal=0, 
     for j in range(n_normal):
         Y[:, j] = Ylat[:, j] * 2.0 + 1.0
         distr[j] = "normal"
+    for k in range(n_poisson + n_lognormal):
+        j = n_normal + k
+        Y[:, j] = rng.poisson(np.exp(np.clip(0.5 * Ylat[:, j], -20, 3))).astype(float)
+        distr[j] = "poisson" if k < n_poisson else "lognormal poisson"
     if na_frac > 0:
         mask = rng.random((ny, ns)) < na_frac
         Y[mask] = np.nan

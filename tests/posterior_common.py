@@ -11,6 +11,8 @@ MODELS = {
     "probit_traits": dict(ny=150, ns=12, nc=3, nf=2, nt=2, seed=21),
     # normal + probit species with NA cells: InvSigma acts, Gamma from GammaV only
     "mixed_na": dict(ny=120, ns=10, nc=3, nf=2, n_normal=3, na_frac=0.04, seed=22),
+    # Poisson + lognormal Poisson + probit (Polya-Gamma updateZ, InvSigma on the lognormal ones)
+    "poisson_mixed": dict(ny=120, ns=10, nc=3, nf=2, n_poisson=4, n_lognormal=3, seed=23),
 }
 N_CHAINS = 4
 TRANSIENT = 200

@@ -44,6 +44,10 @@ MODELS = {
     "wide_traits": dict(ny=150, ns=40, nc=12, nf=2, nt=3, seed=9),
     # nc = 20 (wave bucket 24), K = 30: the bench's dimension class at small ny / ns
     "bench_dims": dict(ny=300, ns=50, nc=20, nf=10, seed=10),
+    # vignette_2's mixed families: normal, Poisson and lognormal Poisson (Polya-Gamma Z), with NA
+    "mixed_poisson": dict(ny=160, ns=24, nc=3, nf=2, n_normal=3, n_poisson=6, n_lognormal=4,
+                          na_frac=0.03, seed=11),
+    "poisson_only": dict(ny=200, ns=20, nc=3, nf=2, n_poisson=20, seed=12),
 }
 
 
