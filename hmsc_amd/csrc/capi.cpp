@@ -374,6 +374,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.TT = dupload(TT.data(), TT.size());
   s.iUGamma = dupload(iUG.data(), iUG.size());
   s.UGammaL = dupload(UGL.data(), UGL.size());
+  s.UGamma = dupload(UG.data(), UG.size());
   s.iV0 = dupload(iV0.data(), iV0.size());
   s.V0g = dupload(V0g.data(), V0g.size());
   s.V0gXXV0g = dupload(V0gXXV0g.data(), V0gXXV0g.size());
@@ -427,6 +428,13 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.allreduce_buf = dalloc<double>((size_t)nc * nc + 2 * N + nfm * nt + nfm + 64);
   s.dev_flags = dalloc<int>(16);
   s.d_iter = dalloc<uint32_t>(1);
+  if (s.mask & HMSC_UP_GAMMAETA) {  // updateGammaEta: dense (nc ns)^2 systems, one workgroup per level
+    HMSC_REQUIRE(s.nranks == 1, "updateGammaEta cannot run on a species-sharded chain: pass updater GammaEta=FALSE");
+    HMSC_REQUIRE((size_t)nc * s.ns <= 4096, "updateGammaEta: nc * ns must be <= 4096 (dense (nc ns)^2 system)");
+    for (int r = 0; r < s.nr; ++r)
+      HMSC_REQUIRE(s.lev[r].nfmax <= 16, "updateGammaEta: nfMax must be <= 16 in this build");
+    s.geWork = dalloc<double>(gamma_eta_work_doubles(s));
+  }
   // recording ring: RING_SLOTS device slots, their pinned host mirror and the copied counter,
   // allocated once here so no run pays for pinning
   s.slot_doubles = record_slot_doubles(s);
@@ -460,7 +468,7 @@ static void free_state(State& s) {
                   s.na_rows, s.row_na, s.row_slot, s.dev_flags, s.Z, s.XEta, s.BL, s.Psi, s.Delta, s.Gamma, s.iV,
                   s.iSigma, s.rho, s.XZ, s.G, s.ZTr, s.XZ_part, s.G_part, s.ZTr_part, s.Gna, s.ZL, s.ZL_part,
                   s.CR, s.CR_part, s.LS, s.Msmall, s.scratch, s.psi_rs, s.ABpart, s.dbg_prec, s.ring, s.allreduce_buf,
-                  s.phU, s.phWinv, s.phRbase, s.phTt, s.phBt, s.phEt, s.phTTw, s.phWork};
+                  s.phU, s.phWinv, s.phRbase, s.phTt, s.phBt, s.phEt, s.phTTw, s.phWork, s.UGamma, s.geWork};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (int r = 0; r < s.nr; ++r) {
@@ -707,7 +715,9 @@ static void run_updater(State& s, uint32_t which, uint32_t iter) {
       launch_gamma2(s, iter);
       break;
     case HMSC_UP_GAMMAETA:
-      throw HmscError(-1, "updateGammaEta is a 'next' row: disable it with updater=list(GammaEta=FALSE)");
+      join_side(s);  // reads iV (GammaV) and Eta of the previous sweep
+      launch_gamma_eta(s, iter);
+      break;
     case HMSC_UP_BETALAMBDA:
       launch_beta_lambda(s, iter);
       break;

@@ -1,0 +1,522 @@
+// updateGammaEta on the device (R/updateGammaEta.R:7-206), non-spatial levels (xDim = 0).
+//
+// Per random level r (sequentially, each level sees the new Eta of the levels before it):
+//   S    = Z - sum_{q != r} Eta_q[Pi_q,] Lambda_q                                  (:37-42)
+//   A    = (Tr x I) U (Tr x I)^T + Q x V,  iA = A^-1                               (:32-33)
+//   Beta ~ N(A (mb10 - mb20 - mb30), M^-1),  M = iA + T1                            (:57-66 / :101-126)
+//          with T1 = kron(diag(id) - LamiD' iW0 LamiD, X'X)       (np = ny, one W0 = I + Lam D Lam')
+//          or   T1 = kron(diag(id), X'X) - sum_p (P'X)_p (P'X)_p' x LamiD' iW_p LamiD  (np < ny)
+//   Gamma ~ N(Pg^-1 vec(iV Beta iQ Tr), Pg^-1),  Pg = iU + (Tr' iQ Tr) x iV          (:66-69)
+//   Eta_r | Beta, S: per row (np = ny) or per unit (np < ny) nf x nf solves          (:71-74 / :136-146)
+// Beta is an auxiliary draw and is discarded, as in the reference.
+//
+// The whole update is one workgroup (1024 threads) per level on an L2-resident workspace:
+// the dense systems are (nc ns)^2 -- tiny at the configs that run this updater (TD: 12,
+// vignette_3: a few hundred) -- and every step is a chain of dependent factorizations,
+// so a single workgroup with barrier-separated stages is the latency-optimal shape.
+// Randomness (oracle/hmsc_oracle.py update_gamma_eta): Beta normal(c + nc j, 0, S_GE_BETA),
+// Gamma normal(c + nc t, 0, S_GE_GAMMA), Eta normal(row i | unit p, h, S_GE_ETA), each
+// + LEVEL_STRIDE r.
+#include "common.h"
+#include "state.h"
+
+namespace hmsc {
+
+constexpr int GE_NF_MAX = 16;
+
+struct GEArgs {
+  int ny, ns, nc, nt, K, r, nr, nf, np, loff;
+  int lev_np[HMSC_MAX_LEVELS], lev_nf[HMSC_MAX_LEVELS], lev_loff[HMSC_MAX_LEVELS];
+  const double* lev_eta[HMSC_MAX_LEVELS];
+  const int* lev_pi[HMSC_MAX_LEVELS];
+  double* Eta;            // level r, np x nf (ld np), written
+  const int* unit_ptr;    // level r CSR over rows
+  const int* unit_rows;
+  const double* Z;        // ny x ns
+  const double* X;        // ny x nc
+  const double* Tr;       // ns x nt
+  const double* BL;       // K x ns   [Beta; Lambda_1; ...]
+  const double* iSigma;   // ns
+  const double* UGamma;   // (nc nt)^2
+  const double* iUGamma;  // (nc nt)^2
+  const double* iV;       // nc x nc
+  double* Gamma;          // nc x nt, written
+  // phylogeny: iQ = U diag(w) U^T, Q = U diag(1/w) U^T (w = Winv row rho); null: identity
+  const double* phU;
+  const double* phWinv;
+  const double* rho;
+  double* work;
+  int* fail;
+  Key key;
+  uint32_t iter;
+  const uint32_t* iter_dev;
+  int noise_zero;
+};
+
+// workspace carve-up (doubles), shared by the launcher's size computation
+struct GELayout {
+  size_t A, L, M, T, S, XtX, V, Wv, XtS, LamiD, LDL, W0, iW0, L0i, tmp1, Qm, iQm, iQTr, vec, Beta, Pg, rg, PtX, PtS,
+      iWp, Lip, Ltp, m21, tot;
+};
+
+__host__ __device__ inline GELayout ge_layout(int ny, int ns, int nc, int nt, int nf, int np) {
+  GELayout o{};
+  const size_t N = (size_t)nc * ns, G = (size_t)nc * nt;
+  size_t p = 0;
+  auto take = [&](size_t n) {
+    const size_t at = p;
+    p += (n + 7) & ~(size_t)7;
+    return at;
+  };
+  o.A = take(N * N);
+  o.L = take(N * N);
+  o.M = take(N * N);
+  o.T = take(N * N);
+  o.S = take((size_t)ny * ns);
+  o.XtX = take((size_t)nc * nc);
+  o.V = take((size_t)nc * nc);
+  o.Wv = take((size_t)nc * nc);
+  o.XtS = take(N);
+  o.LamiD = take((size_t)nf * ns);
+  o.LDL = take((size_t)nf * nf);
+  o.W0 = take((size_t)nf * nf);
+  o.iW0 = take((size_t)nf * nf);
+  o.L0i = take((size_t)nf * nf);
+  o.tmp1 = take((size_t)ns * ns);
+  o.Qm = take((size_t)ns * ns);
+  o.iQm = take((size_t)ns * ns);
+  o.iQTr = take((size_t)ns * nt);
+  o.vec = take(6 * N);
+  o.Beta = take(N);
+  o.Pg = take(G * G);
+  o.rg = take(G);
+  o.PtX = take((size_t)np * nc);
+  o.PtS = take((size_t)np * ns);
+  o.iWp = take((size_t)np * nf * nf);
+  o.Lip = take((size_t)np * nf * nf);
+  o.Ltp = take((size_t)np * nf * ns);
+  o.m21 = take((size_t)np * nf);
+  o.tot = p;
+  return o;
+}
+
+// serial lower Cholesky of an n x n (ld n) block and the inverse of its factor, one thread
+__device__ inline bool t_chol_inv(double* A, double* Li, int n) {
+  bool ok = true;
+  for (int c = 0; c < n; ++c) {
+    double d = A[c + n * c];
+    for (int k = 0; k < c; ++k) d -= A[c + n * k] * A[c + n * k];
+    if (!(d > 0.0)) ok = false;
+    d = sqrt(d > 0.0 ? d : 1.0);
+    A[c + n * c] = d;
+    for (int i = c + 1; i < n; ++i) {
+      double s = A[i + n * c];
+      for (int k = 0; k < c; ++k) s -= A[i + n * k] * A[c + n * k];
+      A[i + n * c] = s / d;
+    }
+  }
+  for (int j = 0; j < n; ++j)  // Li = L^-1 (lower), column by column
+    for (int i = 0; i < n; ++i) {
+      if (i < j) {
+        Li[i + n * j] = 0.0;
+        continue;
+      }
+      double s = (i == j) ? 1.0 : 0.0;
+      for (int k = j; k < i; ++k) s -= A[i + n * k] * Li[k + n * j];
+      Li[i + n * j] = s / A[i + n * i];
+    }
+  return ok;
+}
+
+__global__ __launch_bounds__(1024) void gamma_eta_kernel(GEArgs a) {
+  __shared__ int flag;
+  const int t = threadIdx.x, nthr = blockDim.x;
+  const int ny = a.ny, ns = a.ns, nc = a.nc, nt = a.nt, nf = a.nf, np = a.np, K = a.K;
+  const int N = nc * ns, G = nc * nt;
+  const bool obs = (np == ny);
+  const GELayout o = ge_layout(ny, ns, nc, nt, nf, obs ? 0 : np);
+  double* w = a.work;
+  double *A = w + o.A, *L = w + o.L, *M = w + o.M, *T = w + o.T, *S = w + o.S;
+  double *XtX = w + o.XtX, *V = w + o.V, *Wv = w + o.Wv, *XtS = w + o.XtS, *LamiD = w + o.LamiD, *LDL = w + o.LDL;
+  double *W0 = w + o.W0, *iW0 = w + o.iW0, *L0i = w + o.L0i, *tmp1 = w + o.tmp1, *Qm = w + o.Qm, *iQm = w + o.iQm;
+  double *iQTr = w + o.iQTr, *mb10 = w + o.vec, *mb20 = mb10 + N, *v = mb20 + N, *wv = v + N, *mb = wv + N,
+         *xi = mb + N;
+  double *Beta = w + o.Beta, *Pg = w + o.Pg, *rg = w + o.rg;
+  double *PtX = w + o.PtX, *PtS = w + o.PtS, *iWp = w + o.iWp, *Lip = w + o.Lip, *Ltp = w + o.Ltp, *m21 = w + o.m21;
+  const uint32_t it = SWEEP_ITER(a);
+  const uint32_t str = LEVEL_STRIDE * (uint32_t)a.r;
+  const double* lam = a.BL + a.loff;  // Lambda_r[h, j] = lam[h + K j]
+
+  // ---- stage 1: S, X'X, V = iV^-1, LamiD, Lam D Lam', Q / iQ
+  for (size_t p = t; p < (size_t)ny * ns; p += nthr) {
+    const int i = (int)(p % ny), j = (int)(p / ny);
+    double sv = a.Z[p];
+    for (int q = 0; q < a.nr; ++q) {
+      if (q == a.r) continue;
+      const double* eq = a.lev_eta[q];
+      const int u = a.lev_pi[q][i], npq = a.lev_np[q];
+      const double* lq = a.BL + a.lev_loff[q] + (size_t)K * j;
+      for (int h = 0; h < a.lev_nf[q]; ++h) sv -= eq[u + (size_t)npq * h] * lq[h];
+    }
+    S[p] = sv;
+  }
+  for (int p = t; p < nc * nc; p += nthr) {
+    const int c1 = p % nc, c2 = p / nc;
+    double s = 0.0;
+    for (int i = 0; i < ny; ++i) s = fma(a.X[i + (size_t)ny * c1], a.X[i + (size_t)ny * c2], s);
+    XtX[p] = s;
+    Wv[p] = a.iV[p];
+  }
+  for (int p = t; p < nf * ns; p += nthr) {
+    const int h = p % nf, j = p / nf;
+    LamiD[p] = lam[h + (size_t)K * j] * a.iSigma[j];
+  }
+  for (int p = t; p < nf * nf; p += nthr) {
+    const int h1 = p % nf, h2 = p / nf;
+    double s = 0.0;
+    for (int j = 0; j < ns; ++j) s = fma(lam[h1 + (size_t)K * j] * a.iSigma[j], lam[h2 + (size_t)K * j], s);
+    LDL[p] = s;
+  }
+  if (a.phU) {
+    const double* wq = a.phWinv + (size_t)ns * ((int)(*a.rho) - 1);
+    for (int p = t; p < ns * ns; p += nthr) {
+      const int j1 = p % ns, j2 = p / ns;
+      double s = 0.0, si = 0.0;
+      for (int i = 0; i < ns; ++i) {
+        const double uu = a.phU[j1 + (size_t)ns * i] * a.phU[j2 + (size_t)ns * i];
+        si = fma(uu, wq[i], si);
+        s = fma(uu, 1.0 / wq[i], s);
+      }
+      iQm[p] = si;
+      Qm[p] = s;
+    }
+  } else {
+    for (int p = t; p < ns * ns; p += nthr) iQm[p] = Qm[p] = (p % ns == p / ns) ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  // V = chol2inv(chol(iV))
+  if (!wg_chol(Wv, nc, nc, &flag) && t == 0) a.fail[0] = 1;
+  wg_chol2inv(Wv, nc, nc, V, nc, T /* scratch: nc^2 <= N^2 */);
+  // X'S, iQ Tr
+  for (int p = t; p < N; p += nthr) {
+    const int c = p % nc, j = p / nc;
+    double s = 0.0;
+    for (int i = 0; i < ny; ++i) s = fma(a.X[i + (size_t)ny * c], S[i + (size_t)ny * j], s);
+    XtS[p] = s;
+  }
+  for (int p = t; p < ns * nt; p += nthr) {
+    const int j = p % ns, q = p / ns;
+    double s = 0.0;
+    for (int j2 = 0; j2 < ns; ++j2) s = fma(iQm[j + (size_t)ns * j2], a.Tr[j2 + (size_t)ns * q], s);
+    iQTr[p] = s;
+  }
+  // ---- stage 2: A = (Tr x I) U (Tr x I)^T + Q x V   (:32)
+  for (size_t p = t; p < (size_t)N * N; p += nthr) {
+    const int r1 = (int)(p % N), r2 = (int)(p / N);
+    const int c1 = r1 % nc, j1 = r1 / nc, c2 = r2 % nc, j2 = r2 / nc;
+    double s = Qm[j1 + (size_t)ns * j2] * V[c1 + nc * c2];
+    for (int t1 = 0; t1 < nt; ++t1) {
+      const double a1 = a.Tr[j1 + (size_t)ns * t1];
+      for (int t2 = 0; t2 < nt; ++t2)
+        s = fma(a1 * a.UGamma[(c1 + nc * t1) + (size_t)G * (c2 + nc * t2)], a.Tr[j2 + (size_t)ns * t2], s);
+    }
+    A[p] = s;
+    L[p] = s;
+  }
+  __syncthreads();
+  // iA = chol2inv(chol(A)) into M (scratch T)
+  if (!wg_chol(L, N, N, &flag) && t == 0) a.fail[0] = 1;
+  wg_chol2inv(L, N, N, M, N, T);
+
+  // ---- stage 3: the level's Eta-integrated precision term T1 and the mean pieces
+  if (obs) {
+    // W0 = Lam D Lam' + I, RW0 = chol(W0), iW0 = chol2inv(RW0)      (:53-55)
+    if (t == 0) {
+      for (int p = 0; p < nf * nf; ++p) W0[p] = LDL[p] + ((p % nf == p / nf) ? 1.0 : 0.0);
+      if (!t_chol_inv(W0, L0i, nf)) a.fail[0] = 1;
+      for (int h1 = 0; h1 < nf; ++h1)
+        for (int h2 = 0; h2 < nf; ++h2) {
+          double s = 0.0;
+          for (int k = 0; k < nf; ++k) s += L0i[k + nf * h1] * L0i[k + nf * h2];
+          iW0[h1 + nf * h2] = s;
+        }
+    }
+    __syncthreads();
+    // tmp1 = diag(id) - LamiD' iW0 LamiD   (:57)
+    for (int p = t; p < ns * ns; p += nthr) {
+      const int j1 = p % ns, j2 = p / ns;
+      double s = 0.0;
+      for (int h1 = 0; h1 < nf; ++h1) {
+        double u = 0.0;
+        for (int h2 = 0; h2 < nf; ++h2) u = fma(iW0[h1 + nf * h2], LamiD[h2 + nf * j2], u);
+        s = fma(LamiD[h1 + nf * j1], u, s);
+      }
+      tmp1[p] = (j1 == j2 ? a.iSigma[j1] : 0.0) - s;
+    }
+    __syncthreads();
+    // M = iA + kron(tmp1, X'X)   (:58)
+    for (size_t p = t; p < (size_t)N * N; p += nthr) {
+      const int r1 = (int)(p % N), r2 = (int)(p / N);
+      M[p] += tmp1[(r1 / nc) + (size_t)ns * (r2 / nc)] * XtX[(r1 % nc) + nc * (r2 % nc)];
+    }
+    // mb20 = vec((X'S LamiD') iW0 LamiD)   (:62)
+    for (int p = t; p < N; p += nthr) {
+      const int c = p % nc, j = p / nc;
+      double s = 0.0;
+      for (int h2 = 0; h2 < nf; ++h2) {
+        double u = 0.0;
+        for (int h1 = 0; h1 < nf; ++h1) {
+          double x1 = 0.0;
+          for (int j2 = 0; j2 < ns; ++j2) x1 = fma(XtS[c + nc * j2], LamiD[h1 + nf * j2], x1);
+          u = fma(x1, iW0[h1 + nf * h2], u);
+        }
+        s = fma(u, LamiD[h2 + nf * j], s);
+      }
+      mb20[p] = s;
+    }
+  } else {
+    // per unit p: P'X, P'S, W_p = I + n_p Lam D Lam', iW_p, LiW_p^T LamiD   (:78-107)
+    for (int q = t; q < np; q += nthr) {
+      const int b = a.unit_ptr[q], e = a.unit_ptr[q + 1];
+      for (int c = 0; c < nc; ++c) {
+        double s = 0.0;
+        for (int k = b; k < e; ++k) s += a.X[a.unit_rows[k] + (size_t)ny * c];
+        PtX[q + (size_t)np * c] = s;
+      }
+      for (int j = 0; j < ns; ++j) {
+        double s = 0.0;
+        for (int k = b; k < e; ++k) s += S[a.unit_rows[k] + (size_t)ny * j];
+        PtS[q + (size_t)np * j] = s;
+      }
+      double* Wq = iWp + (size_t)q * nf * nf;  // W_p factorised in place, then replaced by iW_p
+      double* Li = Lip + (size_t)q * nf * nf;
+      const double cnt = (double)(e - b);
+      for (int p = 0; p < nf * nf; ++p) Wq[p] = ((p % nf == p / nf) ? 1.0 : 0.0) + cnt * LDL[p];
+      if (!t_chol_inv(Wq, Li, nf)) a.fail[0] = 1;
+      for (int h1 = 0; h1 < nf; ++h1)
+        for (int h2 = 0; h2 < nf; ++h2) {
+          double s = 0.0;
+          for (int k = 0; k < nf; ++k) s += Li[k + nf * h1] * Li[k + nf * h2];
+          Wq[h1 + nf * h2] = s;
+        }
+      // Lt_p = L_p^-1 LamiD  (nf x ns): rows of LiW_p^T LamiD  (:104)
+      double* Lt = Ltp + (size_t)q * nf * ns;
+      for (int j = 0; j < ns; ++j)
+        for (int h = 0; h < nf; ++h) {
+          double s = 0.0;
+          for (int k = 0; k <= h; ++k) s += Li[h + nf * k] * LamiD[k + nf * j];
+          Lt[h + (size_t)nf * j] = s;
+        }
+      // mb22_p = iW_p (P'S LamiD')_p    (:115-117)
+      for (int h = 0; h < nf; ++h) {
+        double s = 0.0;
+        for (int h2 = 0; h2 < nf; ++h2) {
+          double u = 0.0;
+          for (int j = 0; j < ns; ++j) u = fma(PtS[q + (size_t)np * j], LamiD[h2 + nf * j], u);
+          s = fma(Wq[h + nf * h2], u, s);
+        }
+        m21[q + (size_t)np * h] = s;
+      }
+    }
+    __syncthreads();
+    // T = kron(diag(id), X'X) - sum_p (P'X)_p (P'X)_p' x Lt_p' Lt_p ;  M = iA + T   (:105-108)
+    for (size_t p = t; p < (size_t)N * N; p += nthr) {
+      const int r1 = (int)(p % N), r2 = (int)(p / N);
+      const int c1 = r1 % nc, j1 = r1 / nc, c2 = r2 % nc, j2 = r2 / nc;
+      double s = 0.0;
+      for (int q = 0; q < np; ++q) {
+        const double* Lt = Ltp + (size_t)q * nf * ns;
+        double u = 0.0;
+        for (int h = 0; h < nf; ++h) u = fma(Lt[h + (size_t)nf * j1], Lt[h + (size_t)nf * j2], u);
+        s = fma(PtX[q + (size_t)np * c1] * PtX[q + (size_t)np * c2], u, s);
+      }
+      const double tv = (j1 == j2 ? a.iSigma[j1] * XtX[c1 + nc * c2] : 0.0) - s;
+      T[p] = tv;
+      M[p] += tv;
+    }
+    // mb20 = vec(P'X' mb22 LamiD)   (:118)
+    for (int p = t; p < N; p += nthr) {
+      const int c = p % nc, j = p / nc;
+      double s = 0.0;
+      for (int h = 0; h < nf; ++h) {
+        double u = 0.0;
+        for (int q = 0; q < np; ++q) u = fma(PtX[q + (size_t)np * c], m21[q + (size_t)np * h], u);
+        s = fma(u, LamiD[h + nf * j], s);
+      }
+      mb20[p] = s;
+    }
+  }
+  // mb10 = vec(X'S o id)  (:61 / :113)
+  for (int p = t; p < N; p += nthr) {
+    mb10[p] = XtS[p] * a.iSigma[p / nc];
+    v[p] = mb10[p] - mb20[p];
+  }
+  __syncthreads();
+  // ---- stage 4: RM = chol(M); mb31 = M^-1 (mb10 - mb20); mb30 = T1 mb31; mb = A (mb10 - mb20 - mb30)
+  if (!wg_chol(M, N, N, &flag) && t == 0) a.fail[0] = 1;
+  wg_forward(M, N, N, v);
+  wg_backward_t(M, N, N, v);
+  for (int p = t; p < N; p += nthr) {
+    const int c = p % nc, j = p / nc;
+    double s = 0.0;
+    if (obs) {
+      for (int j2 = 0; j2 < ns; ++j2) {
+        const double tj = tmp1[j + (size_t)ns * j2];
+        if (tj == 0.0) continue;
+        double u = 0.0;
+        for (int c2 = 0; c2 < nc; ++c2) u = fma(XtX[c + nc * c2], v[c2 + nc * j2], u);
+        s = fma(tj, u, s);
+      }
+    } else {
+      for (int p2 = 0; p2 < N; ++p2) s = fma(T[p + (size_t)N * p2], v[p2], s);
+    }
+    wv[p] = mb10[p] - mb20[p] - s;
+    xi[p] = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)p, 0, S_GE_BETA + str, it);
+  }
+  __syncthreads();
+  for (int p = t; p < N; p += nthr) {
+    double s = 0.0;
+    for (int p2 = 0; p2 < N; ++p2) s = fma(A[p + (size_t)N * p2], wv[p2], s);
+    mb[p] = s;
+  }
+  __syncthreads();
+  wg_backward_t(M, N, N, xi);  // backsolve(RM, rnorm(nc ns))  (:66)
+  for (int p = t; p < N; p += nthr) Beta[p] = mb[p] + xi[p];
+  __syncthreads();
+
+  // ---- stage 5: Gamma | Beta   (:69-71)
+  for (size_t p = t; p < (size_t)G * G; p += nthr) {
+    const int r1 = (int)(p % G), r2 = (int)(p / G);
+    const int c1 = r1 % nc, t1 = r1 / nc, c2 = r2 % nc, t2 = r2 / nc;
+    double tq = 0.0;
+    for (int j = 0; j < ns; ++j) tq = fma(a.Tr[j + (size_t)ns * t1], iQTr[j + (size_t)ns * t2], tq);
+    Pg[p] = a.iUGamma[p] + tq * a.iV[c1 + nc * c2];
+  }
+  for (int p = t; p < G; p += nthr) {
+    const int c = p % nc, q = p / nc;
+    double s = 0.0;
+    for (int j = 0; j < ns; ++j) {
+      double ib = 0.0;
+      for (int c2 = 0; c2 < nc; ++c2) ib = fma(a.iV[c + nc * c2], Beta[c2 + nc * j], ib);
+      s = fma(ib, iQTr[j + (size_t)ns * q], s);
+    }
+    rg[p] = s;
+  }
+  __syncthreads();
+  if (!wg_chol(Pg, G, G, &flag) && t == 0) a.fail[0] = 1;
+  wg_forward(Pg, G, G, rg);
+  for (int p = t; p < G; p += nthr)
+    if (!a.noise_zero) rg[p] += normal(a.key, (uint32_t)p, 0, S_GE_GAMMA + str, it);
+  __syncthreads();
+  wg_backward_t(Pg, G, G, rg);
+  for (int p = t; p < G; p += nthr) a.Gamma[p] = rg[p];
+
+  // ---- stage 6: Eta | Beta, S   (:71-74 / :136-146); S1 = S - X Beta
+  if (obs) {
+    for (int i = t; i < ny; i += nthr) {
+      double tv[GE_NF_MAX];
+      for (int h = 0; h < nf; ++h) tv[h] = 0.0;
+      for (int j = 0; j < ns; ++j) {
+        double s1 = S[i + (size_t)ny * j];
+        for (int c = 0; c < nc; ++c) s1 -= a.X[i + (size_t)ny * c] * Beta[c + nc * j];
+        for (int h = 0; h < nf; ++h) tv[h] = fma(s1, LamiD[h + nf * j], tv[h]);
+      }
+      const int u = a.lev_pi[a.r][i];
+      for (int h = 0; h < nf; ++h) {
+        double me = 0.0, nz = 0.0;
+        for (int h2 = 0; h2 < nf; ++h2) me = fma(tv[h2], iW0[h2 + nf * h], me);
+        if (!a.noise_zero)
+          for (int h2 = h; h2 < nf; ++h2)  // (RW0^-1 xi)_h = sum_h2 L0i[h2, h] xi_h2
+            nz = fma(L0i[h2 + nf * h], normal(a.key, (uint32_t)i, (uint32_t)h2, S_GE_ETA + str, it), nz);
+        a.Eta[u + (size_t)np * h] = me + nz;
+      }
+    }
+  } else {
+    for (int q = t; q < np; q += nthr) {
+      const int b = a.unit_ptr[q], e = a.unit_ptr[q + 1];
+      double tv[GE_NF_MAX];
+      for (int h = 0; h < nf; ++h) tv[h] = 0.0;
+      for (int j = 0; j < ns; ++j) {
+        double s1 = PtS[q + (size_t)np * j];
+        for (int c = 0; c < nc; ++c) s1 -= PtX[q + (size_t)np * c] * Beta[c + nc * j];
+        for (int h = 0; h < nf; ++h) tv[h] = fma(s1, LamiD[h + nf * j], tv[h]);
+      }
+      (void)b;
+      (void)e;
+      const double* iW = iWp + (size_t)q * nf * nf;
+      const double* Li = Lip + (size_t)q * nf * nf;
+      for (int h = 0; h < nf; ++h) {
+        double me = 0.0, nz = 0.0;
+        for (int h2 = 0; h2 < nf; ++h2) me = fma(iW[h + nf * h2], tv[h2], me);
+        if (!a.noise_zero)
+          for (int h2 = h; h2 < nf; ++h2)  // (LiW_p xi)_h = sum_h2 Li[h2, h] xi_h2
+            nz = fma(Li[h2 + nf * h], normal(a.key, (uint32_t)q, (uint32_t)h2, S_GE_ETA + str, it), nz);
+        a.Eta[q + (size_t)np * h] = me + nz;
+      }
+    }
+  }
+}
+
+size_t gamma_eta_work_doubles(const State& s) {
+  size_t m = 0;
+  for (int r = 0; r < s.nr; ++r) {
+    const int nf = std::max(1, s.lev[r].nfmax);
+    const int np = s.lev[r].np == s.ny ? 0 : s.lev[r].np;
+    m = std::max(m, ge_layout(s.ny, s.ns, s.nc, s.nt, nf, np).tot);
+  }
+  return m + 64;
+}
+
+void launch_gamma_eta(State& s, uint32_t iter) {
+  HMSC_REQUIRE(s.nranks == 1, "updateGammaEta: species-sharded chains are not supported (dense (nc ns)^2 system)");
+  HMSC_REQUIRE(s.geWork != nullptr, "updateGammaEta: workspace not allocated");
+  for (int r = 0; r < s.nr; ++r) {
+    GEArgs a{};
+    a.ny = s.ny;
+    a.ns = s.ns;
+    a.nc = s.nc;
+    a.nt = s.nt;
+    a.K = s.K;
+    a.r = r;
+    a.nr = s.nr;
+    a.nf = s.lev[r].nf;
+    a.np = s.lev[r].np;
+    a.loff = s.loff(r);
+    HMSC_REQUIRE(a.nf <= GE_NF_MAX, "updateGammaEta: nf must be <= 16 in this build");
+    for (int q = 0; q < s.nr; ++q) {
+      a.lev_np[q] = s.lev[q].np;
+      a.lev_nf[q] = s.lev[q].nf;
+      a.lev_loff[q] = s.loff(q);
+      a.lev_eta[q] = s.lev[q].Eta;
+      a.lev_pi[q] = s.lev[q].Pi;
+    }
+    a.Eta = s.lev[r].Eta;
+    a.unit_ptr = s.lev[r].unit_ptr;
+    a.unit_rows = s.lev[r].unit_rows;
+    a.Z = s.Z;
+    a.X = s.X;
+    a.Tr = s.Tr;
+    a.BL = s.BL;
+    a.iSigma = s.iSigma;
+    a.UGamma = s.UGamma;
+    a.iUGamma = s.iUGamma;
+    a.iV = s.iV;
+    a.Gamma = s.Gamma;
+    a.phU = s.phylo ? s.phU : nullptr;
+    a.phWinv = s.phWinv;
+    a.rho = s.rho;
+    a.work = s.geWork;
+    a.fail = s.dev_flags;
+    a.key = s.key;
+    a.iter = iter;
+    a.iter_dev = s.capturing ? s.d_iter : nullptr;
+    a.noise_zero = s.noise_mode;
+    gamma_eta_kernel<<<1, 1024, 0, s.stream>>>(a);
+    HIP_OK(hipGetLastError());
+  }
+  // Eta changed: XEta, its Gram and X'Eta Z of the next BetaLambda are stale
+  s.xeta_valid = false;
+  s.zt_valid = false;
+}
+
+}  // namespace hmsc

@@ -69,7 +69,8 @@ struct State {
   int8_t* Ycode = nullptr;
   int* fam = nullptr;            // ns_loc family code
   int* varest = nullptr;         // ns_loc distr[,2]
-  double *V0 = nullptr, *iUGamma = nullptr, *mGamma = nullptr, *UGammaL = nullptr;
+  double *V0 = nullptr, *iUGamma = nullptr, *mGamma = nullptr, *UGammaL = nullptr, *UGamma = nullptr;
+  double* geWork = nullptr;      // updateGammaEta workspace (gamma_eta.hip), only if that updater is on
   double *aSigma = nullptr, *bSigma = nullptr;
   double *XX = nullptr, *TT = nullptr, *V0g = nullptr, *V0gXXV0g = nullptr, *iV0 = nullptr;
   double* V0inv = nullptr;       // V0^-1 (initial riwish draw)
@@ -231,7 +232,10 @@ size_t phylo_work_doubles(int ns, int Kmax, int nc, int nrho);
 void launch_phylo_gv_sums(State& s, uint32_t iter, hipStream_t st);
 void launch_rho(State& s, uint32_t iter, hipStream_t st);
 void launch_beta_lambda_phylo(State& s, uint32_t iter);
-void launch_side_fused(State& s, uint32_t iter);  // GammaV + LambdaPriors + Eta, co-launched
+void launch_side_fused(State& s, uint32_t iter);
+// updateGammaEta (gamma_eta.hip)
+size_t gamma_eta_work_doubles(const State& s);
+void launch_gamma_eta(State& s, uint32_t iter);  // GammaV + LambdaPriors + Eta, co-launched
 void join_side(State& s);
 void launch_copied_flag(State& s, uint64_t value);
 size_t record_slot_doubles(const State& s);

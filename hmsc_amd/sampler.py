@@ -405,9 +405,6 @@ def sampleMcmc(hM, samples, transient=0, thin=1, initPar=None, verbose=None, ada
     if _r_bool_on(updater, "GammaEta") and hM.nr == 0:
         updater["GammaEta"] = False
         print("Setting updater$GammaEta=FALSE due to absence of random effects included to the model")
-    if _r_bool_on(updater, "GammaEta"):
-        raise NotImplementedError("updateGammaEta is a 'next' row (SURVEY.md §8 f1): pass "
-                                  "updater={'GammaEta': False} (as vignette_4 does)")
     ndev = np.zeros(1, dtype=np.int32)
     L.check(L.lib().hmsc_device_count(L.iptr(ndev)))
     if ndev[0] < 1:
