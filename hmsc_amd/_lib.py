@@ -28,7 +28,9 @@ class hmsc_model(C.Structure):
                 ("V0", dp), ("f0", C.c_double), ("mGamma", dp), ("UGamma", dp), ("aSigma", dp), ("bSigma", dp),
                 ("nu", dp), ("a1", dp), ("b1", dp), ("a2", dp), ("b2", dp), ("nfMin", ip), ("nfMax", ip),
                 ("sDim", ip), ("xDim", ip), ("C", dp), ("nrho", C.c_int32), ("rhopw", dp),
-                ("C_vectors", dp), ("C_values", dp)]
+                ("C_vectors", dp), ("C_values", dp),
+                ("spatialMethod", ip), ("nalpha", ip), ("alphapw", dp * MAX_LEVELS), ("iWg", dp * MAX_LEVELS),
+                ("RiWg", dp * MAX_LEVELS), ("detWg", dp * MAX_LEVELS)]
 
 
 class hmsc_params(C.Structure):

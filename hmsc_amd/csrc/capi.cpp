@@ -235,7 +235,15 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   int sum_nfmax = 0;
   for (int r = 0; r < s.nr; ++r) {
     Level& L = s.lev[r];
-    HMSC_REQUIRE(m->sDim == nullptr || m->sDim[r] == 0, "spatial random levels are a 'next' row: not in this build");
+    L.spatial = m->sDim != nullptr && m->sDim[r] != 0;
+    if (L.spatial) {
+      HMSC_REQUIRE(m->spatialMethod != nullptr && m->spatialMethod[r] == 1,
+                   "spatial levels: only spatialMethod 'Full' is in this build (NNGP / GPP are a 'next' row)");
+      HMSC_REQUIRE(m->nalpha != nullptr && m->nalpha[r] > 0 && m->alphapw[r] && m->iWg[r] && m->RiWg[r] && m->detWg[r],
+                   "spatial level: alphapw / iWg / RiWg / detWg (computeDataParameters' rLPar) must be given");
+      HMSC_REQUIRE(!(mask & HMSC_UP_GAMMAETA),
+                   "updateGammaEta's spatial branch is a 'next' row: pass updater GammaEta=FALSE with spatial levels");
+    }
     HMSC_REQUIRE(m->xDim == nullptr || m->xDim[r] == 0,
                  "covariate-dependent random levels are a 'next' row: not in this build");
     L.np = m->np[r];
@@ -276,6 +284,17 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
     L.unit_rows = dupload(rows.data(), ny);
     std::vector<int> alpha(std::max(1, L.nfmax > 0 ? std::min(L.nfmax, s.NFmax) : 1), 1);
     L.Alpha = dupload(alpha.data(), alpha.size());
+    std::vector<double> alphad(alpha.size(), 1.0);  // Alpha = rep(1, nf) (R/computeInitialParameters.R:216-221)
+    L.AlphaD = dupload(alphad.data(), alphad.size());
+    if (L.spatial) {
+      const size_t G = m->nalpha[r], np2 = (size_t)L.np * L.np;
+      L.nalpha = (int)G;
+      L.alphapw = dupload(m->alphapw[r], 2 * G);
+      L.iWg = dupload(m->iWg[r], np2 * G);
+      L.RiWg = dupload(m->RiWg[r], np2 * G);
+      L.detWg = dupload(m->detWg[r], G);
+      L.spWork = dalloc<double>(spatial_work_doubles(s, r));
+    }
   }
   // local species slices
   std::vector<int8_t> ycode((size_t)ny * nsl);
@@ -473,7 +492,7 @@ static void free_state(State& s) {
     if (p) (void)hipFree(p);
   for (int r = 0; r < s.nr; ++r) {
     Level& L = s.lev[r];
-    void* lp[] = {L.Eta, L.Pi, L.unit_ptr, L.unit_rows, L.Alpha};
+    void* lp[] = {L.Eta, L.Pi, L.unit_ptr, L.unit_rows, L.Alpha, L.AlphaD, L.alphapw, L.iWg, L.RiWg, L.detWg, L.spWork};
     for (void* p : lp)
       if (p) (void)hipFree(p);
   }
@@ -540,9 +559,11 @@ static void get_state(State& s, hmsc_params* p) {
         if (p->Lambda[r]) p->Lambda[r][h + (size_t)nf * j] = BL[lo + h + (size_t)K * j];
         if (p->Psi[r]) p->Psi[r][h + (size_t)nf * j] = Psi[fo + h + (size_t)s.NF * j];
       }
+    std::vector<double> ad(std::max(1, nf), 1.0);
+    if (nf > 0) HIP_OK(hipMemcpy(ad.data(), s.lev[r].AlphaD, sizeof(double) * nf, hipMemcpyDeviceToHost));
     for (int h = 0; h < nf; ++h) {
       if (p->Delta[r]) p->Delta[r][h] = Delta[fo + h];
-      if (p->Alpha[r]) p->Alpha[r][h] = 1;
+      if (p->Alpha[r]) p->Alpha[r][h] = (int32_t)ad[h];
     }
   }
   double rho = 1.0;
@@ -581,6 +602,15 @@ static void set_state(State& s, const hmsc_params* p) {
     if (p->Delta[r])
       for (int h = 0; h < nf; ++h) Delta[fo + h] = p->Delta[r][h];
     if (p->Eta[r]) h2d(s.lev[r].Eta, p->Eta[r], (size_t)s.lev[r].np * nf, s.stream);
+    if (p->Alpha[r] && nf > 0) {  // initPar$Alpha (R/computeInitialParameters.R:212-221)
+      std::vector<double> ad(nf);
+      for (int h = 0; h < nf; ++h) {
+        HMSC_REQUIRE(p->Alpha[r][h] >= 1 && (!s.lev[r].spatial || p->Alpha[r][h] <= s.lev[r].nalpha),
+                     "set_state: Alpha index out of the alphapw grid");
+        ad[h] = s.lev[r].spatial ? p->Alpha[r][h] : 1.0;
+      }
+      HIP_OK(hipMemcpy(s.lev[r].AlphaD, ad.data(), sizeof(double) * nf, hipMemcpyHostToDevice));
+    }
   }
   h2d(s.BL, BL.data(), BL.size(), s.stream);
   h2d(s.Psi, Psi.data(), (size_t)s.NF * nsl, s.stream);
@@ -672,6 +702,8 @@ static void update_nf(State& s, int r, uint32_t iter) {
     h2d(s.Psi, Psi2.data(), Psi2.size(), s.stream);
     h2d(s.Delta, Delta2.data(), NF2, s.stream);
     h2d(L.Eta + (size_t)L.np * nf, col.data(), L.np, s.stream);
+    const double one = 1.0;  // alphaNew = c(alpha, 1)  (:31)
+    h2d(L.AlphaD + nf, &one, 1, s.stream);
     HIP_OK(hipStreamSynchronize(s.stream));
     L.nf = nf + 1;
   } else if (num_red > 0 && nf > L.nfmin) {
@@ -697,6 +729,10 @@ static void update_nf(State& s, int r, uint32_t iter) {
     h2d(s.Psi, Psi2.data(), (size_t)NF2 * nsl, s.stream);
     h2d(s.Delta, Delta2.data(), NF2, s.stream);
     h2d(L.Eta, Eta2.data(), Eta2.size(), s.stream);
+    std::vector<double> ad(nf);  // alpha = alpha[indNotRed]  (:59)
+    d2h(ad.data(), L.AlphaD, nf, s.stream);
+    HIP_OK(hipStreamSynchronize(s.stream));
+    if (nf > 1) h2d(L.AlphaD, ad.data() + 1, nf - 1, s.stream);
     HIP_OK(hipStreamSynchronize(s.stream));
     L.nf = nf - 1;
   } else {
@@ -734,7 +770,8 @@ static void run_updater(State& s, uint32_t which, uint32_t iter) {
       launch_eta(s, iter);
       break;
     case HMSC_UP_ALPHA:
-      break;  // non-spatial levels: Alpha = rep(1, nf) (R/updateAlpha.R:81-82)
+      launch_alpha(s, iter);  // spatial 'Full' levels; rep(1, nf) otherwise (R/updateAlpha.R:81-82)
+      break;
     case HMSC_UP_INVSIGMA:
       launch_inv_sigma(s, iter);
       break;
@@ -917,7 +954,7 @@ static void unpack_record(const State& s, const double* slot, int k, int samples
         }
     for (int h = 0; h < nfm; ++h) {
       if (rec->Delta[r]) rec->Delta[r][(size_t)k * nfm + h] = h < nf ? Delta[fo + h] : 1.0;
-      if (rec->Alpha[r]) rec->Alpha[r][(size_t)k * nfm + h] = 1;
+      if (rec->Alpha[r] && !L.spatial) rec->Alpha[r][(size_t)k * nfm + h] = 1;
     }
     if (rec->Eta[r])
       for (int h = 0; h < nfm; ++h) {
@@ -930,6 +967,14 @@ static void unpack_record(const State& s, const double* slot, int k, int samples
     eta += (size_t)L.np * nf;
   }
   if (rec->rho) rec->rho[k] = (int32_t)eta[0];  // packed after the Eta blocks (launch_record)
+  const double* al = eta + 1;                   // then AlphaD of every spatial level
+  for (int r = 0; r < s.nr; ++r) {
+    const Level& L = s.lev[r];
+    if (!L.spatial) continue;
+    for (int h = 0; h < L.nfmax; ++h)
+      if (rec->Alpha[r]) rec->Alpha[r][(size_t)k * L.nfmax + h] = h < L.nf ? (int32_t)al[h] : 1;
+    al += L.nf;
+  }
 }
 
 static void run(State& s, int transient, int samples, int thin, const int* adaptNf, int iter0, int verbose,

@@ -2008,7 +2008,7 @@ void launch_side_fused(State& s, uint32_t iter) {
 }
 
 static bool eta_fused_ok(const State& s) {
-  return s.nranks == 1 && s.nr == 1 && s.n_na_rows == 0 && s.lev[0].np == s.ny && s.lev[0].uniform_n == 1 &&
+  return s.nranks == 1 && s.nr == 1 && !s.lev[0].spatial && s.n_na_rows == 0 && s.lev[0].np == s.ny && s.lev[0].uniform_n == 1 &&
          s.lev[0].nf <= 16 && s.K <= 64 && s.LS != nullptr && !getenv_flag("HMSC_NO_ETA_FUSION");
 }
 
@@ -2110,6 +2110,10 @@ void launch_eta(State& s, uint32_t iter) {
   for (int r = 0; r < s.nr; ++r) {
     const Level& L = s.lev[r];
     if (r > 0) launch_xeta(s);  // levels r' < r were just redrawn (R/updateEta.R:31-37 uses them)
+    if (L.spatial) {            // R/updateEta.R:111-140 (spatial.hip)
+      launch_eta_spatial(s, r, iter);
+      continue;
+    }
     EtaArgs a{};
     a.ev = make_view(s);
     a.XEta = s.XEta;
@@ -2423,7 +2427,7 @@ void launch_copied_flag(State& s, uint64_t value) {
 size_t record_slot_doubles(const State& s) {
   size_t n = (size_t)s.Kmax * s.nsl + (size_t)s.NFmax * s.nsl + s.NFmax + (size_t)s.nc * s.nt +
              (size_t)s.nc * s.nc + s.nsl + 2;
-  for (int r = 0; r < s.nr; ++r) n += (size_t)s.lev[r].np * s.lev[r].nfmax;
+  for (int r = 0; r < s.nr; ++r) n += (size_t)s.lev[r].np * s.lev[r].nfmax + (s.lev[r].spatial ? s.lev[r].nfmax : 0);
   return n;
 }
 
@@ -2445,6 +2449,8 @@ void launch_record(State& s, double* slot, int part) {
   add(s.iSigma, s.nsl, false);
   for (int r = 0; r < s.nr; ++r) add(s.lev[r].Eta, (int64_t)s.lev[r].np * s.lev[r].nf, false);
   add(s.rho, 1, true);  // updateRho's grid index (written with GammaV's outputs)
+  for (int r = 0; r < s.nr; ++r)
+    if (s.lev[r].spatial) add(s.lev[r].AlphaD, s.lev[r].nf, false);  // updateAlpha's grid indices
   a.npieces = k;
   a.slot = slot;
   if (slot == nullptr) {  // captured into a graph replay: slot chosen on the device

@@ -1,0 +1,216 @@
+// Spatial latent factors, method "Full" (SURVEY.md §8 f2), on the device.
+//
+// updateEta, spatial branch (R/updateEta.R:111-140): for a level with np units and nf
+// factors, one dense system in the vec(np x nf) ordering (unit fastest)
+//   iUEta = bdiag(iWg[,,alpha_1], ..., iWg[,,alpha_nf]) + kron(Lam D Lam', diag(n_p))
+//   fS    = P'S (Lam diag(iSigma))',  S = Z - X Beta - other levels' Eta Lambda
+//   eta   = R^-1 (R^-T vec(fS) + xi),  R = chol(iUEta)
+// np = ny (observation-level, P a permutation) and np < ny are the same formula.
+// updateAlpha (R/updateAlpha.R:20-79, 'Full'): v_gh = |RiWg[,,g] eta_h|^2 for every grid
+// point g, log-likelihood log(alphapw[g,2]) - detWg[g]/2 - v_gh/2, categorical draw.
+//
+// Layout in HBM: the alphapw grid arrays iWg / RiWg (np^2 x nalpha each, column-major as R
+// holds them) stay resident for the whole chain -- at np = 5000 and 101 grid points that is
+// 20 GB per array, which 288 GB of HBM holds -- so no sweep ever recomputes a grid matrix.
+// The Eta system is one workgroup with the shared wg_* Cholesky on an L2-resident (np nf)^2
+// workspace; updateAlpha's nalpha x nf quadratic forms are one workgroup per grid point
+// streaming that grid matrix once (the HBM-bound step at large np).
+// Randomness (oracle/hmsc_oracle.py _eta_spatial_full / update_alpha): Eta normal(p, h,
+// S_ETA + LEVEL_STRIDE r) -- the same counters as the non-spatial branch --, Alpha the first
+// uniform of (h, 0, S_ALPHA + LEVEL_STRIDE r).
+#include "common.h"
+#include "state.h"
+
+namespace hmsc {
+
+struct SpArgs {
+  int ny, ns, K, nf, np, loff, nalpha, r;
+  const double* Z;        // ny x ns
+  const double* XEta;     // ny x Kmax (ld ny): [X, Eta_1[Pi_1,], ...]
+  const double* BL;       // K x ns
+  const double* iSigma;
+  const int* unit_ptr;
+  const int* unit_rows;
+  const double* iWg;      // np x np x nalpha
+  const double* RiWg;
+  const double* detWg;
+  const double* alphapw;  // nalpha x 2
+  double* AlphaD;         // nf (1-based grid index as double)
+  double* Eta;            // np x nf (ld np)
+  double* work;
+  int* fail;
+  Key key;
+  uint32_t iter;
+  const uint32_t* iter_dev;
+  int noise_zero;
+};
+
+__global__ __launch_bounds__(1024) void eta_spatial_full_kernel(SpArgs a) {
+  __shared__ int flag;
+  const int t = threadIdx.x, nthr = blockDim.x;
+  const int np = a.np, nf = a.nf, ns = a.ns, ny = a.ny, K = a.K, N = np * nf;
+  double* U = a.work;                       // N x N
+  double* rhs = U + (size_t)N * N;          // N
+  double* LDL = rhs + N;                    // nf x nf
+  const double* lam = a.BL + a.loff;        // Lambda_r[h, j] = lam[h + K j]
+  for (int p = t; p < nf * nf; p += nthr) {
+    const int h1 = p % nf, h2 = p / nf;
+    double s = 0.0;
+    for (int j = 0; j < ns; ++j) s = fma(lam[h1 + (size_t)K * j] * a.iSigma[j], lam[h2 + (size_t)K * j], s);
+    LDL[p] = s;
+  }
+  // fS[p, h] = sum_{rows i of unit p} sum_j S[i, j] Lam[h, j] iSigma[j], where S excludes this
+  // level's own columns of XEta (R/updateEta.R:31-37, :119-127)
+  for (int e = t; e < N; e += nthr) {
+    const int q = e % np, h = e / np;
+    double acc = 0.0;
+    for (int k = a.unit_ptr[q]; k < a.unit_ptr[q + 1]; ++k) {
+      const int i = a.unit_rows[k];
+      for (int j = 0; j < ns; ++j) {
+        double sv = a.Z[i + (size_t)ny * j];
+        for (int c = 0; c < K; ++c) {
+          if (c >= a.loff && c < a.loff + nf) continue;
+          sv = fma(-a.XEta[i + (size_t)ny * c], a.BL[c + (size_t)K * j], sv);
+        }
+        acc = fma(sv, lam[h + (size_t)K * j] * a.iSigma[j], acc);
+      }
+    }
+    rhs[e] = acc;
+  }
+  __syncthreads();
+  // iUEta (upper triangle is all wg_chol reads; fill the whole matrix for simplicity)
+  for (size_t e = t; e < (size_t)N * N; e += nthr) {
+    const int r1 = (int)(e % N), r2 = (int)(e / N);
+    const int q1 = r1 % np, h1 = r1 / np, q2 = r2 % np, h2 = r2 / np;
+    double v = 0.0;
+    if (h1 == h2) {
+      const int g = (int)a.AlphaD[h1] - 1;
+      v = a.iWg[q1 + (size_t)np * q2 + (size_t)np * np * g];
+    }
+    if (q1 == q2) v = fma(LDL[h1 + nf * h2], (double)(a.unit_ptr[q1 + 1] - a.unit_ptr[q1]), v);
+    U[e] = v;
+  }
+  __syncthreads();
+  if (!wg_chol(U, N, N, &flag) && t == 0) a.fail[0] = 1;
+  wg_forward(U, N, N, rhs);  // backsolve(R, fS, transpose=TRUE)
+  for (int e = t; e < N; e += nthr)
+    if (!a.noise_zero) rhs[e] += normal(a.key, (uint32_t)(e % np), (uint32_t)(e / np), S_ETA + LEVEL_STRIDE * a.r, SWEEP_ITER(a));
+  __syncthreads();
+  wg_backward_t(U, N, N, rhs);  // backsolve(R, tmp2)
+  for (int e = t; e < N; e += nthr) a.Eta[e] = rhs[e];
+}
+
+// v[g * nf + h] = |RiWg[,,g] eta_h|^2 ; RiWg upper triangular (chol(iW)), one workgroup per g
+__global__ __launch_bounds__(256) void alpha_quad_kernel(SpArgs a) {
+  const int g = blockIdx.x, np = a.np, nf = a.nf;
+  const double* Rg = a.RiWg + (size_t)np * np * g;
+  double* v = a.work;
+  __shared__ double red[256];
+  for (int h = 0; h < nf; ++h) {
+    const double* eh = a.Eta + (size_t)np * h;
+    double s = 0.0;
+    for (int p = threadIdx.x; p < np; p += blockDim.x) {
+      double x = 0.0;
+      for (int p2 = p; p2 < np; ++p2) x = fma(Rg[p + (size_t)np * p2], eh[p2], x);
+      s = fma(x, x, s);
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+      if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) v[(size_t)g * nf + h] = red[0];
+    __syncthreads();
+  }
+}
+
+// one thread per factor: likelihood over the grid, inverse-CDF categorical draw (R's
+// sample.int(gN, 1, prob=like), R/updateAlpha.R:76-78)
+__global__ __launch_bounds__(64) void alpha_draw_kernel(SpArgs a) {
+  const int h = threadIdx.x;
+  if (h >= a.nf) return;
+  const double* v = a.work;
+  const int G = a.nalpha;
+  double mx = -INFINITY;
+  for (int g = 0; g < G; ++g) {
+    const double l = log(a.alphapw[G + g]) - 0.5 * a.detWg[g] - 0.5 * v[(size_t)g * a.nf + h];
+    mx = fmax(mx, l);
+  }
+  double tot = 0.0;
+  for (int g = 0; g < G; ++g) tot += exp(log(a.alphapw[G + g]) - 0.5 * a.detWg[g] - 0.5 * v[(size_t)g * a.nf + h] - mx);
+  const double u = uniforms(a.key, (uint32_t)h, 0, S_ALPHA + LEVEL_STRIDE * a.r, SWEEP_ITER(a)).a * tot;
+  double c = 0.0;
+  int pick = G;
+  for (int g = 0; g < G; ++g) {
+    c += exp(log(a.alphapw[G + g]) - 0.5 * a.detWg[g] - 0.5 * v[(size_t)g * a.nf + h] - mx);
+    if (c > u) {
+      pick = g + 1;
+      break;
+    }
+  }
+  a.AlphaD[h] = (double)(pick > G ? G : pick);
+}
+
+static SpArgs sp_args(State& s, int r, uint32_t iter) {
+  const Level& L = s.lev[r];
+  SpArgs a{};
+  a.ny = s.ny;
+  a.ns = s.nsl;
+  a.K = s.K;
+  a.nf = L.nf;
+  a.np = L.np;
+  a.loff = s.loff(r);
+  a.nalpha = L.nalpha;
+  a.r = r;
+  a.Z = s.Z;
+  a.XEta = s.XEta;
+  a.BL = s.BL;
+  a.iSigma = s.iSigma;
+  a.unit_ptr = L.unit_ptr;
+  a.unit_rows = L.unit_rows;
+  a.iWg = L.iWg;
+  a.RiWg = L.RiWg;
+  a.detWg = L.detWg;
+  a.alphapw = L.alphapw;
+  a.AlphaD = L.AlphaD;
+  a.Eta = L.Eta;
+  a.work = L.spWork;
+  a.fail = s.dev_flags;
+  a.key = s.key;
+  a.iter = iter;
+  a.iter_dev = s.capturing ? s.d_iter : nullptr;
+  a.noise_zero = s.noise_mode;
+  return a;
+}
+
+size_t spatial_work_doubles(const State& s, int r) {
+  const Level& L = s.lev[r];
+  const size_t N = std::min<size_t>((size_t)L.np * std::max(1, std::min(L.nfmax, s.NFmax)), 8192);
+  const size_t eta = N * N + N + 64 * 64;
+  const size_t alpha = (size_t)L.nalpha * std::max(1, std::min(L.nfmax, s.NFmax));
+  return std::max(eta, alpha) + 64;
+}
+
+void launch_eta_spatial(State& s, int r, uint32_t iter) {
+  const Level& L = s.lev[r];
+  HMSC_REQUIRE(s.nranks == 1, "spatial levels: species-sharded chains are not supported");
+  HMSC_REQUIRE((size_t)L.np * L.nf <= 8192, "spatial 'Full' level: np * nf must be <= 8192 in this build");
+  if (!s.xeta_valid) launch_xeta(s);
+  eta_spatial_full_kernel<<<1, 1024, 0, s.stream>>>(sp_args(s, r, iter));
+  HIP_OK(hipGetLastError());
+}
+
+void launch_alpha(State& s, uint32_t iter) {
+  for (int r = 0; r < s.nr; ++r) {
+    const Level& L = s.lev[r];
+    if (!L.spatial || L.nf == 0) continue;  // rep(1, nf) otherwise (R/updateAlpha.R:81-82)
+    const SpArgs a = sp_args(s, r, iter);
+    alpha_quad_kernel<<<L.nalpha, 256, 0, s.stream>>>(a);
+    HIP_OK(hipGetLastError());
+    alpha_draw_kernel<<<1, 64, 0, s.stream>>>(a);
+    HIP_OK(hipGetLastError());
+  }
+}
+
+}  // namespace hmsc

@@ -31,6 +31,15 @@ struct Level {
   int* unit_rows = nullptr;     // ny
   int* Alpha = nullptr;         // nfmax (host mirror in State::h_alpha)
   int uniform_n = 0;            // common row count of every unit (0 if they differ)
+  // spatial "Full" level (spatial.hip): alphapw grid of R/computeDataParameters.R:53-81
+  bool spatial = false;
+  int nalpha = 0;
+  double* alphapw = nullptr;    // nalpha x 2
+  double* iWg = nullptr;        // np x np x nalpha
+  double* RiWg = nullptr;       // np x np x nalpha (upper triangular)
+  double* detWg = nullptr;      // nalpha
+  double* AlphaD = nullptr;     // nfmax: 1-based grid index of each factor (recorded)
+  double* spWork = nullptr;     // dense (np nf)^2 Eta system + Alpha likelihoods
 };
 
 struct State {
@@ -233,6 +242,10 @@ void launch_phylo_gv_sums(State& s, uint32_t iter, hipStream_t st);
 void launch_rho(State& s, uint32_t iter, hipStream_t st);
 void launch_beta_lambda_phylo(State& s, uint32_t iter);
 void launch_side_fused(State& s, uint32_t iter);
+// spatial "Full" levels (spatial.hip)
+size_t spatial_work_doubles(const State& s, int r);
+void launch_eta_spatial(State& s, int r, uint32_t iter);
+void launch_alpha(State& s, uint32_t iter);
 // updateGammaEta (gamma_eta.hip)
 size_t gamma_eta_work_doubles(const State& s);
 void launch_gamma_eta(State& s, uint32_t iter);  // GammaV + LambdaPriors + Eta, co-launched

@@ -42,6 +42,12 @@ def computeDataParameters(hM):
         RQg = np.eye(ns)[:, :, None]
         detQg = np.array([0.0])
     par.update(Qg=Qg, iQg=iQg, RQg=RQg, detQg=detQg)
+    par["rLPar"] = spatialDataParameters(hM)
+    return par
+
+
+def spatialDataParameters(hM):
+    """rLPar of R/computeDataParameters.R:47-81 (spatial 'Full' levels; {} for the others)."""
     rLPar = []
     for r, rl in enumerate(hM.rL or []):
         if not rl.sDim:
@@ -71,8 +77,7 @@ def computeDataParameters(hM):
             Wg[:, :, k], iWg[:, :, k], RiWg[:, :, k] = W, iW, _chol_upper(iW)
             detWg[k] = 2 * np.sum(np.log(np.diag(RW)))
         rLPar.append(dict(Wg=Wg, iWg=iWg, RiWg=RiWg, detWg=detWg))
-    par["rLPar"] = rLPar
-    return par
+    return rLPar
 
 
 def _level_order(hM, r, rl):

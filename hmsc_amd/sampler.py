@@ -34,8 +34,8 @@ class ModelBuffers:
 
     def __init__(self, hM):
         for rl in hM.rL or []:
-            if rl.sDim:
-                raise NotImplementedError("spatial random levels are a 'next' row (SURVEY.md §8 f2)")
+            if rl.sDim and rl.spatialMethod != "Full":
+                raise NotImplementedError("NNGP / GPP spatial levels are a 'next' row (SURVEY.md §8 f2)")
             if rl.xDim:
                 raise NotImplementedError("covariate-dependent random levels are a 'next' row")
         self.keep = []
@@ -62,7 +62,21 @@ class ModelBuffers:
         self.nfMin = [int(r.nfMin) for r in rl]
         m.nfMin = L.colmajor_ptr(self.nfMin or [0], k, np.int32)
         m.nfMax = L.colmajor_ptr(self.nfMax or [0], k, np.int32)
-        m.sDim = L.colmajor_ptr([0] * max(1, hM.nr), k, np.int32)
+        sdim = [1 if r.sDim else 0 for r in rl]
+        m.sDim = L.colmajor_ptr(sdim or [0], k, np.int32)
+        m.spatialMethod = L.colmajor_ptr(sdim or [0], k, np.int32)     # 1 = Full
+        if any(sdim):
+            # computeDataParameters' alphapw grid (R/computeDataParameters.R:53-81); the R shim
+            # would pass dataParList$rLPar[[r]]$iWg / RiWg / detWg
+            from .dataparams import spatialDataParameters
+            rlp = spatialDataParameters(hM)
+            m.nalpha = L.colmajor_ptr([r.alphapw.shape[0] if r.sDim else 0 for r in rl], k, np.int32)
+            for r, lv in enumerate(rl):
+                if lv.sDim:
+                    m.alphapw[r] = L.colmajor_ptr(np.asarray(lv.alphapw, dtype=np.float64), k)
+                    m.iWg[r] = L.colmajor_ptr(rlp[r]["iWg"], k)
+                    m.RiWg[r] = L.colmajor_ptr(rlp[r]["RiWg"], k)
+                    m.detWg[r] = L.colmajor_ptr(rlp[r]["detWg"], k)
         m.xDim = L.colmajor_ptr([0] * max(1, hM.nr), k, np.int32)
         m.C = None
         if hM.C is not None:
@@ -191,6 +205,9 @@ class Chain:
                     nf = a.shape[1] if key == "Eta" else a.shape[0]
                     getattr(p, key)[r] = L.colmajor_ptr(a, keep)
             p.nf[r] = nf
+            al = st.get("Alpha")
+            if al is not None and al[r] is not None:   # initPar$Alpha: 1-based grid indices
+                p.Alpha[r] = L.colmajor_ptr(np.asarray(al[r]), keep, np.int32)
         L.check(self.lib.hmsc_set_state(self.h, C.byref(p)))
 
     # ---- sweeps

@@ -70,7 +70,7 @@ typedef struct hmsc_model {
   const double* b2;
   const int32_t* nfMin;
   const int32_t* nfMax;
-  const int32_t* sDim;    /* spatial levels are a 'next' row: must be 0 */
+  const int32_t* sDim;    /* > 0: spatial level (see spatialMethod below)     */
   const int32_t* xDim;    /* covariate-dependent levels: must be 0       */
   /* Phylogeny (hM$C; NULL = none).  The grid of R/computeDataParameters.R:19-39
    * (iQg/RQg/detQg over hM$rhopw) is taken in spectral form: the caller passes the
@@ -81,6 +81,16 @@ typedef struct hmsc_model {
   const double* rhopw;    /* nrho*2 column-major: grid value, prior weight     */
   const double* C_vectors;/* ns*ns eigenvectors of C, column-major             */
   const double* C_values; /* ns    eigenvalues of C (> 0)                      */
+  /* Spatial levels (rL$sDim > 0), spatialMethod "Full" only: the alphapw grid of
+   * R/computeDataParameters.R:53-81 as computeDataParameters (or dataParList$rLPar) holds it,
+   * per level r (entries of non-spatial levels ignored / NULL).  iWg, RiWg are
+   * np*np*nalpha column-major (R's [np, np, alphaN] arrays), detWg nalpha. */
+  const int32_t* spatialMethod;              /* nr: 0 none, 1 Full (NNGP / GPP: not in this build) */
+  const int32_t* nalpha;                     /* nr: nrow(rL$alphapw)                     */
+  const double* alphapw[HMSC_MAX_LEVELS];    /* nalpha*2: grid value, prior weight      */
+  const double* iWg[HMSC_MAX_LEVELS];
+  const double* RiWg[HMSC_MAX_LEVELS];
+  const double* detWg[HMSC_MAX_LEVELS];
 } hmsc_model;
 
 /* Sampler state = R's parList (R/computeInitialParameters.R:256-270) with iV in

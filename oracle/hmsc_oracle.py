@@ -72,7 +72,25 @@ def compute_data_parameters(model):
         iQg = np.eye(ns)[None]
         RQg = np.eye(ns)[None]
         detQg = np.zeros(1)
-    return dict(Qg=Qg, iQg=iQg, RQg=RQg, detQg=detQg)
+    rLPar = []
+    for rl in model.get("rL", []):                             # :47-81 spatial "Full" grid
+        if not rl.get("sDim", 0):
+            rLPar.append({})
+            continue
+        if rl.get("spatialMethod", "Full") != "Full":
+            raise NotImplementedError("NNGP / GPP spatial levels (SURVEY.md §8 f2)")
+        d = rl["dist"]                                         # np x np, levels(dfPi) order
+        alphapw = rl["alphapw"]
+        npr, G = d.shape[0], alphapw.shape[0]
+        iWg, RiWg, detWg = np.empty((G, npr, npr)), np.empty((G, npr, npr)), np.empty(G)
+        for g in range(G):
+            a = alphapw[g, 0]
+            W = np.eye(npr) if a == 0 else np.exp(-d / a)
+            RW = chol_upper(W)
+            iW = chol2inv(RW)
+            iWg[g], RiWg[g], detWg[g] = iW, chol_upper(iW), 2 * np.sum(np.log(np.diag(RW)))
+        rLPar.append(dict(iWg=iWg, RiWg=RiWg, detWg=detWg))
+    return dict(Qg=Qg, iQg=iQg, RQg=RQg, detQg=detQg, rLPar=rLPar)
 
 
 # ---------------------------------------------------------------------------
@@ -427,19 +445,71 @@ def eta_unit_moments(st, model, r, S):
     return precs, means
 
 
-def update_eta(st, model, rng, it, zero_noise=False):
+def _eta_spatial_full(st, model, r, S, dp, rng, it, zero_noise):
+    """Spatial 'Full' level, R/updateEta.R:115-140: one dense (np nf)^2 system
+    iUEta = bdiag(iWg[,,alpha_h]) + kron(Lam iSigma Lam', diag(colSums P)),
+    fS = P'S (Lam diag(iSigma))', eta = R^-1 (R^-T vec(fS) + xi), R = chol(iUEta)."""
+    lam, iS = st["Lambda"][r], st["iSigma"]
+    nf = lam.shape[0]
+    npr = int(model["np"][r])
+    lPi = model["Pi"][:, r] - 1
+    iWg = dp["rLPar"][r]["iWg"]
+    alpha = np.asarray(st["Alpha"][r], dtype=np.int64)
+    P = np.zeros((S.shape[0], npr))
+    P[np.arange(S.shape[0]), lPi] = 1.0
+    LamInvSigLam = (lam * np.sqrt(iS)[None, :]) @ (lam * np.sqrt(iS)[None, :]).T
+    iU = np.kron(LamInvSigLam, np.diag(P.sum(axis=0)))
+    for h in range(nf):
+        iU[h * npr:(h + 1) * npr, h * npr:(h + 1) * npr] += iWg[alpha[h] - 1]
+    fS = (P.T @ S) @ (lam * iS[None, :]).T
+    Rm = chol_upper(iU)
+    tmp2 = backsolve(Rm, fS.ravel(order="F"), transpose=True)
+    if not zero_noise:
+        xi = rng.normal(np.arange(npr)[:, None], np.arange(nf)[None, :], R.S_ETA + R.LEVEL_STRIDE * r, it)
+        tmp2 = tmp2 + xi.ravel(order="F")
+    return backsolve(Rm, tmp2).reshape((npr, nf), order="F")
+
+
+def update_alpha(st, model, rng, it, data_par=None):
+    """R/updateAlpha.R:3-86, 'Full' levels: v_gh = |RiWg[,,g] eta_h|^2, log-likelihood
+    log(alphapw[g,2]) - detWg[g]/2 - v_gh/2, categorical draw by inverse CDF of the uniform
+    (idx h, S_ALPHA + LEVEL_STRIDE r); rep(1, nf) for non-spatial levels (:81-82)."""
+    out = []
+    for r, rl in enumerate(model["rL"]):
+        eta = st["Eta"][r]
+        nf = eta.shape[1]
+        if not rl.get("sDim", 0):
+            out.append(np.ones(nf, dtype=np.int64))
+            continue
+        dp = data_par if data_par is not None else compute_data_parameters(model)
+        par = dp["rLPar"][r]
+        alphapw = rl["alphapw"]
+        v = np.stack([np.sum((par["RiWg"][g] @ eta) ** 2, axis=0) for g in range(alphapw.shape[0])])
+        a = np.empty(nf, dtype=np.int64)
+        for h in range(nf):
+            like = np.log(alphapw[:, 1]) - 0.5 * par["detWg"] - 0.5 * v[:, h]
+            like = np.exp(like - like.max())
+            u = rng.uniforms(h, 0, R.S_ALPHA + R.LEVEL_STRIDE * r, it)[0]
+            a[h] = int(np.searchsorted(np.cumsum(like), u * like.sum(), side="right")) + 1
+        out.append(a)
+    return out
+
+
+def update_eta(st, model, rng, it, zero_noise=False, data_par=None):
     nr = model["Pi"].shape[1]
     st = dict(st)
     Eta = list(st["Eta"])
     LFix = model["X"] @ st["Beta"]                                     # :11-20
     for r in range(nr):
-        if model["rL"][r].get("sDim", 0) > 0:
-            raise NotImplementedError("spatial updateEta is a 'next' row (SURVEY.md §8 f2)")
         S = st["Z"] - LFix                                             # :31-37
         for r2 in range(nr):
             if r2 != r:
                 S = S - Eta[r2][model["Pi"][:, r2] - 1] @ st["Lambda"][r2]
         st["Eta"] = Eta
+        if model["rL"][r].get("sDim", 0) > 0:                          # :111-197
+            dp = data_par if data_par is not None else compute_data_parameters(model)
+            Eta[r] = _eta_spatial_full(st, model, r, S, dp, rng, it, zero_noise)
+            continue
         precs, means = eta_unit_moments(st, model, r, S)
         npr, nf = means.shape
         RiV = np.swapaxes(np.linalg.cholesky(precs), 1, 2)              # chol(): upper R, R'R = Q
@@ -570,7 +640,9 @@ def sweep(st, model, rng, it, updater=None, data_par=None, adapt_nf=None):
     if on("LambdaPriors"):
         st["Psi"], st["Delta"] = update_lambda_priors(st, model, rng, it)
     if on("Eta"):
-        st["Eta"] = update_eta(st, model, rng, it)
+        st["Eta"] = update_eta(st, model, rng, it, data_par=data_par)
+    if on("Alpha") and any(rl.get("sDim", 0) for rl in model["rL"]):
+        st["Alpha"] = update_alpha(st, model, rng, it, data_par)
     if on("InvSigma"):
         st["iSigma"] = update_inv_sigma(st, model, rng, it)
     if on("Z"):

@@ -13,7 +13,8 @@ from oracle import hmsc_oracle as O  # noqa: E402
 
 
 def synthetic_model(ny=200, ns=30, nc=4, nf=3, seed=1, na_frac=0.0, n_normal=0, units=None, nr=1,
-                    nf_fit=None, nt=1, yscale=False, C=None, n_poisson=0, n_lognormal=0):
+                    nf_fit=None, nt=1, yscale=False, C=None, n_poisson=0, n_lognormal=0, spatial=None,
+                    alpha_n=None):
     """Probit JSDM generated like BASELINE.md's synthetic config; optionally the first
     n_normal species normal, the next n_poisson Poisson and n_lognormal lognormal Poisson
     (counts ~ Poisson(exp(L / 2)), vignette_2's mixed-distribution model)."""
@@ -34,8 +35,18 @@ def synthetic_model(ny=200, ns=30, nc=4, nf=3, seed=1, na_frac=0.0, n_normal=0, 
         lam = rng.standard_normal((nf, ns)) / (np.arange(1, nf + 1)[:, None])
         L = L + eta[pi] @ lam
         name = f"lev{r}"
-        sd[name] = np.array([f"u{k}" for k in pi])
-        rl = H.HmscRandomLevel(units=sd[name])
+        if spatial is not None and r in spatial:
+            # spatial 'Full' level: unit coordinates on the unit square, zero-padded unit
+            # names so levels(dfPi) order is the coordinate row order
+            sd[name] = np.array([f"s{k:05d}" for k in pi])
+            rl = H.HmscRandomLevel(sData=rng.random((npr, 2)))
+            if alpha_n is not None:
+                diag = np.sqrt(2.0)
+                H.setPriors(rl, alphapw=np.column_stack([diag * np.arange(alpha_n + 1) / alpha_n,
+                                                          np.r_[0.5, np.full(alpha_n, 0.5 / alpha_n)]]))
+        else:
+            sd[name] = np.array([f"u{k}" for k in pi])
+            rl = H.HmscRandomLevel(units=sd[name])
         nff = nf if nf_fit is None else nf_fit
         H.setPriors(rl, nfMin=nff, nfMax=nff)
         ranLevels[name] = rl
@@ -75,6 +86,11 @@ def oracle_model(hM):
              rhopw=hM.rhopw, C=hM.C,
              rL=[dict(nu=rl.nu, a1=rl.a1, b1=rl.b1, a2=rl.a2, b2=rl.b2, nfMin=rl.nfMin, nfMax=rl.nfMax,
                       sDim=rl.sDim, xDim=rl.xDim) for rl in (hM.rL or [])])
+    for d, rl in zip(m["rL"], hM.rL or []):
+        if rl.sDim:   # spatial 'Full': the distance matrix of the unit coordinates, alphapw grid
+            xy = np.asarray(rl.s, dtype=np.float64)
+            d.update(spatialMethod=rl.spatialMethod, alphapw=np.asarray(rl.alphapw, dtype=np.float64),
+                     dist=np.sqrt(((xy[:, None, :] - xy[None, :, :]) ** 2).sum(-1)))
     return m
 
 

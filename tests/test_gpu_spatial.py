@@ -1,0 +1,126 @@
+"""GPU parity of spatial 'Full' latent factors against the oracle:
+updateEta's spatial branch (R/updateEta.R:111-140: one dense (np nf)^2 system over the
+alphapw grid matrices iWg[,,alpha_h]) and updateAlpha (R/updateAlpha.R:20-79: grid
+posterior from |RiWg eta_h|^2 and detWg).  The grids are computeDataParameters' (host,
+R/computeDataParameters.R:53-81; the oracle recomputes them itself from the distances).
+Both sides share the Philox counters: moments to 1e-10, draws to fp64 rounding, the drawn
+grid indices exactly, and full sweeps (GammaEta off: its spatial branch is not built)."""
+import numpy as np
+import pytest
+
+from helpers import H, O, oracle_model, rel_err, synthetic_model
+from oracle.rng import Rng
+
+pytestmark = pytest.mark.gpu
+
+TOL_MOMENT = 1e-10
+TOL_DRAW = 1e-9
+TOL_SWEEP = 1e-7
+UPD = {"GammaEta": False}
+
+MODELS = {
+    # TD's plot level: 10 spatial units over 50 sampling units, plus the sample level
+    "td_like": dict(ny=50, ns=4, nc=3, nf=2, nr=2, units=[50, 10], spatial=[1], seed=51, alpha_n=30),
+    # observation-level spatial factors (np = ny), the default 101-point grid
+    "obs_level": dict(ny=40, ns=6, nc=2, nf=2, nr=1, spatial=[0], seed=52),
+}
+
+
+@pytest.fixture(scope="module", params=list(MODELS))
+def setup(request):
+    hM = synthetic_model(**MODELS[request.param])
+    m = oracle_model(hM)
+    dp = O.compute_data_parameters(m)
+    seed = 777
+    rng = Rng(seed)
+    st = O.compute_initial_parameters(m, rng)
+    for it in range(1, 3):
+        st = O.sweep(st, m, rng, it, updater=UPD, data_par=dp)
+    r = [k for k, rl in enumerate(m["rL"]) if rl["sDim"]][0]
+    # a smooth spatial field in Eta_r and an interior alpha: exercises both the grid
+    # likelihood of updateAlpha and iWg[,,alpha] != I in updateEta
+    xy = np.asarray(hM.rL[r].s)
+    st["Eta"] = list(st["Eta"])
+    st["Eta"][r] = np.column_stack([np.sin(3 * xy[:, 0]) + xy[:, 1], np.cos(2 * xy[:, 1])])[:, :st["Eta"][r].shape[1]]
+    st["Alpha"] = list(st["Alpha"])
+    st["Alpha"][r] = np.array([7, 12])[:st["Eta"][r].shape[1]]
+    return request.param, hM, m, dp, seed, st, r
+
+
+def _chain(hM, seed, st):
+    ch = H.Chain(hM, seed, device=0, updater=UPD)
+    ch.init()
+    ch.set_state(st)
+    return ch
+
+
+def test_state_roundtrip_alpha(setup):
+    name, hM, m, dp, seed, st, r = setup
+    ch = _chain(hM, seed, st)
+    g = ch.get_state()
+    assert np.array_equal(g["Alpha"][r], st["Alpha"][r])
+    ch.close()
+
+
+def test_spatial_eta_moments(setup):
+    name, hM, m, dp, seed, st, r = setup
+    ch = _chain(hM, seed, st)
+    ch.set_noise_mode(1)
+    ch.update("Eta", 4)
+    g = ch.get_state()
+    Eta = O.update_eta(st, m, Rng(seed), 4, zero_noise=True, data_par=dp)
+    for q in range(hM.nr):
+        assert rel_err(g["Eta"][q], Eta[q]) < TOL_MOMENT, (name, q, rel_err(g["Eta"][q], Eta[q]))
+    ch.close()
+
+
+def test_spatial_eta_draws(setup):
+    name, hM, m, dp, seed, st, r = setup
+    ch = _chain(hM, seed, st)
+    ch.update("Eta", 5)
+    g = ch.get_state()
+    Eta = O.update_eta(st, m, Rng(seed), 5, data_par=dp)
+    for q in range(hM.nr):
+        assert rel_err(g["Eta"][q], Eta[q]) < TOL_DRAW, (name, q)
+    ch.close()
+
+
+def test_alpha_draws(setup):
+    name, hM, m, dp, seed, st, r = setup
+    ch = _chain(hM, seed, st)
+    picks = []
+    for it in (6, 7, 8, 9):
+        ch.update("Alpha", it)
+        g = ch.get_state()
+        a = O.update_alpha(st, m, Rng(seed), it, dp)
+        assert np.array_equal(g["Alpha"][r], a[r]), (name, it, g["Alpha"][r], a[r])
+        picks.append(a[r])
+    assert np.any(np.concatenate(picks) > 1), picks   # the smooth field moves alpha off 0
+    ch.close()
+
+
+def test_spatial_sweeps(setup):
+    name, hM, m, dp, seed, st, r = setup
+    ch = _chain(hM, seed, st)
+    rng = Rng(seed)
+    o = dict(st)
+    for it in range(3, 6):
+        ch.sweep(it)
+        o = O.sweep(o, m, rng, it, updater=UPD, data_par=dp)
+    g = ch.get_state()
+    for k in ("Beta", "Gamma", "iV", "Z"):
+        assert rel_err(g[k], o[k]) < TOL_SWEEP, (name, k, rel_err(g[k], o[k]))
+    for q in range(hM.nr):
+        assert rel_err(g["Eta"][q], o["Eta"][q]) < TOL_SWEEP, (name, q)
+        assert np.array_equal(g["Alpha"][q], o["Alpha"][q])
+    ch.close()
+
+
+def test_spatial_recorded_run(setup):
+    name, hM, m, dp, seed, st, r = setup
+    ch = _chain(hM, seed, st)
+    rec = ch.run(transient=10, samples=20, thin=1, iter0=5)
+    a = rec[f"Alpha{r}"]
+    assert a.shape[0] == 20 and np.all(a >= 1) and np.all(a <= hM.rL[r].alphapw.shape[0])
+    assert np.all(np.isfinite(rec["Beta"]))
+    ch.close()
