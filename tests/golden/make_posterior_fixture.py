@@ -26,7 +26,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
-from posterior_common import (MODELS, N_CHAINS, SAMPLES, START_SEED, START_SWEEPS, TRANSIENT, pack_state,  # noqa: E402
+from posterior_common import (MODELS, N_CHAINS, SAMPLES, START_SEED, START_SWEEPS, THIN, TRANSIENT, pack_state,  # noqa: E402
                               summarise)
 
 
@@ -52,9 +52,10 @@ def oracle_chain(args):
     m = helpers.oracle_model(hM)
     rng = Rng(1000 + c)
     rec = {k: [] for k in ("Beta", "Gamma", "iV", "iSigma", "Lambda0")}
-    for it in range(1, TRANSIENT + SAMPLES + 1):
+    thin = THIN.get(name, 1)
+    for it in range(1, TRANSIENT + SAMPLES * thin + 1):
         st = O.sweep(st, m, rng, it, updater={"GammaEta": False})
-        if it > TRANSIENT:
+        if it > TRANSIENT and (it - TRANSIENT) % thin == 0:
             rec["Beta"].append(st["Beta"].copy())
             rec["Gamma"].append(st["Gamma"].copy())
             rec["iV"].append(st["iV"].copy())

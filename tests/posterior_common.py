@@ -14,6 +14,10 @@ MODELS = {
     # Poisson + lognormal Poisson + probit (Polya-Gamma updateZ, InvSigma on the lognormal ones)
     "poisson_mixed": dict(ny=120, ns=10, nc=3, nf=2, n_poisson=4, n_lognormal=3, seed=23),
 }
+# models that mix slowly record every THIN-th sweep (same number of recorded samples): with
+# iSigma = 100 fixed for Poisson species (R/computeInitialParameters.R:122) Z moves little per
+# sweep, so Beta's autocorrelation is long on both sides alike
+THIN = {"poisson_mixed": 4}
 N_CHAINS = 4
 TRANSIENT = 200
 SAMPLES = 1500

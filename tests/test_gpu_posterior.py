@@ -24,7 +24,7 @@ from scipy import stats
 
 import hmsc_amd as H
 from helpers import synthetic_model
-from posterior_common import MODELS, SAMPLES, TRANSIENT, summarise, unpack_state
+from posterior_common import MODELS, SAMPLES, THIN, TRANSIENT, summarise, unpack_state
 
 pytestmark = pytest.mark.gpu
 
@@ -34,13 +34,13 @@ FIX = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
 N_GPU_CHAINS = 8
 
 
-def gpu_chains(hM, start, n=N_GPU_CHAINS):
+def gpu_chains(hM, start, n=N_GPU_CHAINS, thin=1):
     out = []
     for c in range(n):
         ch = H.Chain(hM, 1 + c, device=0, updater={"GammaEta": False})
         ch.init()
         ch.set_state(start)
-        rec = ch.run(transient=TRANSIENT, samples=SAMPLES, thin=1, adaptNf=[0] * hM.nr)
+        rec = ch.run(transient=TRANSIENT, samples=SAMPLES, thin=thin, adaptNf=[0] * hM.nr)
         ch.close()
         out.append(dict(Beta=rec["Beta"], Gamma=rec["Gamma"], iV=rec["iV"], iSigma=rec["iSigma"],
                         Lambda0=rec["Lambda0"][:, :int(rec["nf"][0][0]), :]))
@@ -51,7 +51,7 @@ def gpu_chains(hM, start, n=N_GPU_CHAINS):
 def both(request):
     name = request.param
     hM = synthetic_model(**MODELS[name])
-    g = summarise(hM, gpu_chains(hM, unpack_state(FIX, f"{name}/start", hM.nr)))
+    g = summarise(hM, gpu_chains(hM, unpack_state(FIX, f"{name}/start", hM.nr), thin=THIN.get(name, 1)))
     c = {k: FIX[f"{name}/{k}"] for k in ("draws", "mean", "sd", "ess", "vp")}
     return name, g, c
 
