@@ -45,6 +45,13 @@ class hmsc_record(C.Structure):
                 ("Delta", dp * MAX_LEVELS), ("Alpha", ip * MAX_LEVELS), ("rec_nf", ip)]
 
 
+class hmsc_predict_args(C.Structure):
+    _fields_ = [("ny", C.c_int32), ("ns", C.c_int32), ("nc", C.c_int32), ("nr", C.c_int32),
+                ("nsamples", C.c_int32), ("expected", C.c_int32), ("seed", C.c_uint64), ("device", C.c_int32),
+                ("X", dp), ("Beta", dp), ("sigma", dp), ("family", ip), ("YScalePar", dp), ("Pi", ip),
+                ("np", ip), ("nf", ip), ("Eta", dp * MAX_LEVELS), ("Lambda", dp * MAX_LEVELS)]
+
+
 class HmscNativeError(RuntimeError):
     pass
 
@@ -55,7 +62,7 @@ _lib = None
 EXPORTS = ["hmsc_last_error", "hmsc_device_count", "hmsc_create", "hmsc_create_sharded", "hmsc_comm_unique_id",
            "hmsc_destroy", "hmsc_init_state", "hmsc_set_state", "hmsc_get_state", "hmsc_get_nf", "hmsc_sweep",
            "hmsc_update", "hmsc_set_noise_mode", "hmsc_run", "hmsc_run_verbose", "hmsc_sync", "hmsc_debug_get",
-           "hmsc_profile", "hmsc_profile_get", "hmsc_kernel_timing", "hmsc_kernel_timing_get"]
+           "hmsc_profile", "hmsc_profile_get", "hmsc_kernel_timing", "hmsc_kernel_timing_get", "hmsc_predict"]
 
 
 def lib():
@@ -91,6 +98,7 @@ def lib():
     L.hmsc_profile_get.argtypes = [C.c_void_p, C.c_int32, dp, ip]
     L.hmsc_kernel_timing.argtypes = [C.c_void_p, C.c_int32]
     L.hmsc_kernel_timing_get.argtypes = [C.c_void_p, C.c_int32, dp, ip]
+    L.hmsc_predict.argtypes = [C.POINTER(hmsc_predict_args), dp]
     _lib = L
     return L
 

@@ -1146,9 +1146,20 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
 
 using namespace hmsc;
 
+namespace hmsc {
+void run_predict(const hmsc_predict_args* p, double* out);  // predict.hip
+}
+
 extern "C" {
 
 const char* hmsc_last_error(void) { return g_last_error.c_str(); }
+
+int hmsc_predict(const hmsc_predict_args* args, double* out) {
+  return guarded([&] {
+    HMSC_REQUIRE(args != nullptr && out != nullptr, "hmsc_predict: NULL argument");
+    run_predict(args, out);
+  });
+}
 
 int hmsc_device_count(int32_t* n) {
   return guarded([&] {

@@ -1,0 +1,214 @@
+"""Post-sampling callers of the hot path, host side of the R wrapper.
+
+predict (R/predict.R:1-231) keeps R's host logic -- argument checks, predictLatentFactor for
+the prediction units (R/predictLatentFactor.R), the Pi of the new study design -- and hands
+the per-sample loop (linear predictor, expected values or draws, Y back-scaling) to the HIP
+kernel behind ``hmsc_predict`` (hmsc_amd/csrc/predict.hip).  computePredictedValues
+(R/computePredictedValues.R:66-142) and evaluateModelFit (R/evaluateModelFit.R) sit on top.
+There is no CPU fallback: without the HIP library predict raises HmscNativeError.
+"""
+import ctypes as C
+
+import numpy as np
+from scipy import stats
+
+from . import _lib as L
+from .model import _factor_levels
+from .post import poolMcmcChains
+
+
+def _levels(values):
+    """levels(as.factor(x)) by the same rule hM$Pi was built with (model._as_factor_codes)."""
+    return [str(v) for v in _factor_levels(values)]
+
+
+def predictLatentFactor(unitsPred, units, postEta, rL, predictMean=False, rng=None):
+    """R/predictLatentFactor.R:1-211 for non-spatial levels: known units keep their
+    posterior Eta rows; new units get N(0, 1) draws (or 0 with predictMean)."""
+    units = [str(u) for u in units]
+    pos = {u: k for k, u in enumerate(units)}
+    old = np.array([u in pos for u in unitsPred], dtype=bool)
+    if (~old).any() and rL.sDim:
+        raise NotImplementedError("predictLatentFactor: new units of a spatial level (SURVEY.md §8 f2)")
+    rng = rng or np.random.default_rng()
+    out = []
+    for eta in postEta:
+        nf = eta.shape[1]
+        e = np.empty((len(unitsPred), nf))
+        if old.any():
+            e[old] = eta[[pos[u] for u, o in zip(unitsPred, old) if o]]
+        if (~old).any():
+            e[~old] = 0.0 if predictMean else rng.standard_normal(((~old).sum(), nf))
+        out.append(e)
+    return out
+
+
+def predict(hM, post=None, X=None, studyDesign=None, expected=False, predictEtaMean=False, seed=None,
+            device=0):
+    """predict.Hmsc (R/predict.R): a list of ny x ns arrays, one per posterior sample."""
+    post = poolMcmcChains(hM.postList) if post is None else post
+    X = np.asarray(hM.X if X is None else X, dtype=np.float64)
+    nyN = X.shape[0]
+    studyDesign = hM.studyDesign if studyDesign is None else studyDesign
+    rng = np.random.default_rng(seed)
+    S = len(post)
+    keep = []
+    a = L.hmsc_predict_args()
+    a.ny, a.ns, a.nc, a.nr, a.nsamples = nyN, hM.ns, X.shape[1], hM.nr, S
+    a.expected = 1 if expected else 0
+    a.seed = int(rng.integers(1, 2 ** 62)) if seed is None else int(seed)
+    a.device = device
+    a.X = L.colmajor_ptr(X, keep)
+    a.Beta = L.fptr(_stack(keep, [np.asarray(s["Beta"]).reshape(-1, order="F") for s in post]))
+    a.sigma = L.fptr(_stack(keep, [np.asarray(s["sigma"], dtype=np.float64) for s in post]))
+    a.family = L.colmajor_ptr(hM.distr[:, 0], keep, np.int32)
+    a.YScalePar = L.colmajor_ptr(hM.YScalePar, keep)
+    if hM.nr:
+        PiNew = np.zeros((nyN, hM.nr), dtype=np.int32)
+        nps, nfs = [], []
+        for r, name in enumerate(hM.rLNames):
+            raw = studyDesign[name]
+            col = np.asarray(raw).astype(str)
+            unitsPred = _levels(raw)
+            units = _levels(hM.dfPi[name])
+            etas = predictLatentFactor(unitsPred, units, [s["Eta"][r] for s in post], hM.rL[r],
+                                       predictMean=predictEtaMean, rng=rng)
+            nf = max(e.shape[1] for e in etas)
+            lams = [np.asarray(s["Lambda"][r]) for s in post]
+            etas = [np.pad(e, ((0, 0), (0, nf - e.shape[1]))) for e in etas]      # nf may vary (updateNf)
+            lams = [np.pad(lm, ((0, nf - lm.shape[0]), (0, 0))) for lm in lams]
+            idx = {u: k for k, u in enumerate(unitsPred)}
+            PiNew[:, r] = [idx[v] + 1 for v in col]
+            a.Eta[r] = L.fptr(_stack(keep, [e.reshape(-1, order="F") for e in etas]))
+            a.Lambda[r] = L.fptr(_stack(keep, [lm.reshape(-1, order="F") for lm in lams]))
+            nps.append(len(unitsPred))
+            nfs.append(nf)
+        a.Pi = L.colmajor_ptr(PiNew, keep, np.int32)
+        a.np = L.colmajor_ptr(nps, keep, np.int32)
+        a.nf = L.colmajor_ptr(nfs, keep, np.int32)
+    out = np.empty(S * nyN * hM.ns)
+    L.check(L.lib().hmsc_predict(C.byref(a), L.fptr(out)))
+    out = out.reshape(S, hM.ns, nyN).transpose(0, 2, 1)
+    return [out[k] for k in range(S)]
+
+
+def _stack(keep, arrays):
+    flat = np.ascontiguousarray(np.concatenate(arrays).astype(np.float64)) if arrays else np.zeros(1)
+    keep.append(flat)
+    return flat
+
+
+def computePredictedValues(hM, partition=None, start=1, thin=1, Yc=None, mcmcStep=1, expected=True,
+                           initPar=None, nParallel=1, nChains=None, updater=None, verbose=None, seed=None):
+    """R/computePredictedValues.R:66-142: ny x ns x predN.  Without a partition, the fitted
+    model's own predictions; with one, K-fold cross-validation refits (sampleMcmc on the
+    training rows with the fitted run's samples / transient / thin, predictions for the
+    held-out rows)."""
+    if Yc is not None:
+        raise NotImplementedError("computePredictedValues: conditional prediction (Yc) is a 'next' row")
+    if partition is None:
+        post = poolMcmcChains(hM.postList, start=start, thin=thin)
+        pred = predict(hM, post=post, expected=expected, seed=seed)
+        return np.stack(pred, axis=2)
+    from .model import Hmsc
+    from .sampler import sampleMcmc
+    partition = np.asarray(partition)
+    nfolds = len(np.unique(partition))
+    nChains = len(hM.postList) if nChains is None else nChains
+    postN = hM.samples * nChains
+    out = np.full((hM.ny, hM.ns, postN), np.nan)
+    for k in np.unique(partition):
+        train, val = partition != k, partition == k
+        sd = None if hM.studyDesign is None else hM.studyDesign.loc[train].reset_index(drop=True)
+        rl = {name: hM.ranLevels[name] for name in hM.rLNames} if hM.nr else None
+        yscaled = bool(np.any(np.asarray(hM.YScalePar) != np.array([[0.0], [1.0]])))
+        hM1 = Hmsc(Y=hM.Y[train], X=hM.X[train], XScale=True, YScale=yscaled, Tr=hM.Tr, distr=hM.distr, C=hM.C,
+                   studyDesign=sd, ranLevels=rl, covNames=list(hM.covNames), spNames=list(hM.spNames))
+        hM1.V0, hM1.f0, hM1.mGamma, hM1.UGamma = hM.V0, hM.f0, hM.mGamma, hM.UGamma
+        hM1 = sampleMcmc(hM1, samples=hM.samples, thin=hM.thin, transient=hM.transient, nChains=nChains,
+                         updater=updater, initPar=initPar, verbose=0)
+        post = poolMcmcChains(hM1.postList, start=start)
+        sdv = None if hM.studyDesign is None else hM.studyDesign.loc[val].reset_index(drop=True)
+        pred = predict(hM1, post=post, X=hM.X[val], studyDesign=sdv, expected=expected, seed=seed)
+        out[val] = np.stack(pred, axis=2)
+    del nfolds
+    return out
+
+
+def _auc(y, p):
+    """pROC::auc(levels=c(0,1), direction="<"): Mann-Whitney with average ranks for ties."""
+    r = stats.rankdata(p)
+    n1 = np.sum(y == 1)
+    n0 = np.sum(y == 0)
+    return (np.sum(r[y == 1]) - n1 * (n1 + 1) / 2) / (n1 * n0)
+
+
+def evaluateModelFit(hM, predY):
+    """R/evaluateModelFit.R: RMSE for all species; R2 (normal); AUC and TjurR2 (probit);
+    SR2, O.AUC, O.TjurR2, O.RMSE, C.SR2, C.RMSE (Poisson)."""
+    Y = np.asarray(hM.Y, dtype=np.float64)
+    fam = hM.distr[:, 0]
+    m = np.full((hM.ny, hM.ns), np.nan)
+    with np.errstate(all="ignore"):
+        pois = fam == 3
+        if pois.any():
+            m[:, pois] = np.nanmedian(predY[:, pois, :], axis=2)
+        if (~pois).any():
+            m[:, ~pois] = np.nanmean(predY[:, ~pois, :], axis=2)
+
+    def rmse(Yc, P):
+        return np.sqrt(np.nanmean((Yc - P) ** 2, axis=0))
+
+    def r2(Yc, P, method="pearson"):
+        out = np.full(Yc.shape[1], np.nan)
+        for j in range(Yc.shape[1]):
+            ok = ~np.isnan(Yc[:, j]) & ~np.isnan(P[:, j])
+            if ok.sum() > 1:
+                if method == "spearman":
+                    co = stats.spearmanr(Yc[ok, j], P[ok, j])[0]
+                else:
+                    co = np.corrcoef(Yc[ok, j], P[ok, j])[0, 1]
+                out[j] = np.sign(co) * co ** 2
+        return out
+
+    def auc(Yc, P):
+        Yb = np.where(np.isnan(Yc), np.nan, (Yc > 0).astype(float))
+        out = np.full(Yc.shape[1], np.nan)
+        for j in range(Yc.shape[1]):
+            sel = ~np.isnan(Yb[:, j])
+            if len(np.unique(Yb[sel, j])) == 2:
+                out[j] = _auc(Yb[sel, j], P[sel, j])
+        return out
+
+    def tjur(Yc, P):
+        return np.array([np.mean(P[Yc[:, j] == 1, j]) - np.mean(P[Yc[:, j] == 0, j]) for j in range(Yc.shape[1])])
+
+    res = dict(RMSE=rmse(Y, m))
+    sel = fam == 1
+    if sel.any():
+        res["R2"] = np.full(hM.ns, np.nan)
+        res["R2"][sel] = r2(Y[:, sel], m[:, sel])
+    sel = fam == 2
+    if sel.any():
+        res["AUC"] = np.full(hM.ns, np.nan)
+        res["TjurR2"] = np.full(hM.ns, np.nan)
+        res["AUC"][sel] = auc(Y[:, sel], m[:, sel])
+        res["TjurR2"][sel] = tjur(Y[:, sel], m[:, sel])
+    sel = fam == 3
+    if sel.any():
+        Ys, ms = Y[:, sel], m[:, sel]
+        res["SR2"] = np.full(hM.ns, np.nan)
+        res["SR2"][sel] = r2(Ys, ms, method="spearman")
+        Yo = np.where(np.isnan(Ys), np.nan, (Ys > 0).astype(float))
+        pO = np.nanmean((predY[:, sel, :] > 0).astype(float), axis=2)
+        for key, val in (("O.AUC", auc(Yo, pO)), ("O.TjurR2", tjur(Yo, pO)), ("O.RMSE", rmse(Yo, pO))):
+            res[key] = np.full(hM.ns, np.nan)
+            res[key][sel] = val
+        with np.errstate(all="ignore"):
+            mc = ms / pO                                    # mPredCY = mPredY / mPredO  (:150)
+        Yc = np.where(Ys == 0, np.nan, Ys)                  # CY[CY == 0] = NA  (:151-152)
+        res["C.SR2"] = np.full(hM.ns, np.nan)
+        res["C.RMSE"] = np.full(hM.ns, np.nan)
+        res["C.SR2"][sel] = r2(Yc, mc, method="spearman")
+        res["C.RMSE"][sel] = rmse(Yc, mc)
+    return res

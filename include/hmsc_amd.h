@@ -210,6 +210,32 @@ int hmsc_sync(hmsc_state* s);
  * "Z", "E", "XEtaTZ", "Gram", "ZTr", "BL", "BL_prec" ... ; n = element count. */
 int hmsc_debug_get(hmsc_state* s, const char* name, double* out, int64_t n);
 
+/* predict.Hmsc (R/predict.R:1-231) for a pooled posterior: every sample's
+ * L = X Beta + sum_r Eta_r[Pi_r,] Lambda_r, then expected values (pnorm / exp(L + sigma/2) / L)
+ * or draws (1[L + sqrt(sigma) e > 0] / rpois / L + sqrt(sigma) e), then the YScalePar
+ * back-transform.  Replaces the per-sample loop of R/predict.R:143-229; the caller (the R
+ * wrapper) keeps predictLatentFactor (R/predict.R:120-129) and passes the per-sample Eta rows
+ * of the prediction units.  Arrays are sample-major stacks of R's column-major matrices. */
+typedef struct hmsc_predict_args {
+  int32_t ny, ns, nc, nr, nsamples;
+  int32_t expected;       /* R's `expected` */
+  uint64_t seed;          /* Philox key of the draws (expected = 0) */
+  int32_t device;
+  const double* X;        /* ny*nc  (unscaled X, as post holds un-scaled Beta) */
+  const double* Beta;     /* nsamples*nc*ns */
+  const double* sigma;    /* nsamples*ns */
+  const int32_t* family;  /* ns: hM$distr[,1] */
+  const double* YScalePar;/* 2*ns */
+  const int32_t* Pi;      /* ny*nr, 1-based rows of the per-level Eta */
+  const int32_t* np;      /* nr */
+  const int32_t* nf;      /* nr */
+  const double* Eta[HMSC_MAX_LEVELS];     /* nsamples*np[r]*nf[r] */
+  const double* Lambda[HMSC_MAX_LEVELS];  /* nsamples*nf[r]*ns */
+} hmsc_predict_args;
+
+/* out: nsamples*ny*ns (pred[[s]] column-major, sample-major stack) */
+int hmsc_predict(const hmsc_predict_args* args, double* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -797,3 +797,72 @@ def update_rho(st, model, rng, it, data_par):
     like = np.exp(logLike - logLike.max())
     u = rng.uniforms(0, 0, R.S_RHO, it)[0]
     return int(np.searchsorted(np.cumsum(like), u * like.sum(), side="right")) + 1
+
+
+# ---------------------------------------------------------------------------
+# predict.Hmsc per-sample loop — R/predict.R:143-229 (device: hmsc_amd/csrc/predict.hip)
+# ---------------------------------------------------------------------------
+S_PREDICT = 30
+
+
+def _rpois_ptrs(lam, rng, cell, s):
+    """numpy's PTRS (Hormann 1993) for lam >= 10, sequential inversion below; trial t uses
+    the uniforms of (cell, 1 + t, S_PREDICT, s) -- the rpois of R/predict.R:216 restated with
+    the Philox counter contract."""
+    if not lam > 0:
+        return 0.0
+    if lam < 10:
+        u = rng.uniforms(cell, 1, S_PREDICT, s)[0]
+        p = c = np.exp(-lam)
+        k = 0
+        while u > c and k < 1000:
+            k += 1
+            p *= lam / k
+            c += p
+        return float(k)
+    from math import floor, lgamma, log, sqrt
+    slam, loglam = sqrt(lam), log(lam)
+    b = 0.931 + 2.53 * slam
+    a = -0.059 + 0.02483 * b
+    invalpha = 1.1239 + 1.1328 / (b - 3.4)
+    vr = 0.9277 - 3.6224 / (b - 2.0)
+    for t in range(256):
+        ua, ub = rng.uniforms(cell, 1 + t, S_PREDICT, s)
+        U, V = float(ua) - 0.5, float(ub)
+        us = 0.5 - abs(U)
+        k = floor((2 * a / us + b) * U + lam + 0.43)
+        if us >= 0.07 and V <= vr:
+            return float(k)
+        if k < 0 or (us < 0.013 and V > us):
+            continue
+        if log(V) + log(invalpha) - log(a / (us * us) + b) <= -lam + k * loglam - lgamma(k + 1.0):
+            return float(k)
+    return float(floor(lam))
+
+
+def predict_samples(X, post, PiNew, family, YScalePar, expected, rng):
+    """post: list of dict(Beta nc x ns, sigma ns, Eta [np_r x nf_r] (prediction units),
+    Lambda [nf_r x ns]); PiNew ny x nr (1-based).  Returns the list of ny x ns predictions."""
+    from scipy.special import ndtr
+    ny, ns = X.shape[0], post[0]["Beta"].shape[1]
+    out = []
+    cells = (np.arange(ny)[:, None] + ny * np.arange(ns)[None, :]).astype(np.uint64)
+    for s, sam in enumerate(post):
+        L = X @ sam["Beta"]
+        for r in range(PiNew.shape[1]):
+            L = L + sam["Eta"][r][PiNew[:, r] - 1] @ sam["Lambda"][r]
+        sg = np.asarray(sam["sigma"], dtype=np.float64)
+        if expected:
+            Z = L.copy()
+            Z[:, family == 2] = ndtr(L[:, family == 2])
+            Z[:, family == 3] = np.exp(L[:, family == 3] + sg[family == 3] / 2)
+        else:
+            Z = L + np.sqrt(sg)[None, :] * rng.normal(cells, 0, S_PREDICT, s)
+            Z[:, family == 2] = (Z[:, family == 2] > 0).astype(float)
+            for j in np.nonzero(family == 3)[0]:
+                Z[:, j] = [_rpois_ptrs(float(np.exp(Z[i, j])), rng, int(cells[i, j]), s) for i in range(ny)]
+        m, sd = YScalePar[0], YScalePar[1]
+        tr = (m != 0) | (sd != 1)
+        Z[:, tr] = Z[:, tr] * sd[tr] + m[tr]
+        out.append(Z)
+    return out

@@ -1,0 +1,61 @@
+"""GPU parity of predict.Hmsc (R/predict.R:143-229, hmsc_amd/csrc/predict.hip) against the
+oracle's restatement of the per-sample loop (oracle.hmsc_oracle.predict_samples) on the same
+pooled posterior and Philox key: expected values to 1e-12 (pnorm via erfc_fast to 1e-13),
+normal / probit draws exactly up to fp64 rounding, Poisson draws identical counts (PTRS on
+the same uniforms; log / lgamma rounding can flip a boundary acceptance, so <= 0.1 %).
+Then computePredictedValues (no partition and 2-fold CV) and evaluateModelFit end to end."""
+import numpy as np
+import pytest
+
+from helpers import H, O, synthetic_model
+from oracle.rng import Rng
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def fitted():
+    hM = synthetic_model(ny=90, ns=9, nc=3, nf=2, nr=2, units=[90, 15], n_normal=2, n_poisson=3, seed=61,
+                         yscale=True)
+    hM = H.sampleMcmc(hM, samples=12, transient=20, thin=2, nChains=2, updater={"GammaEta": False}, seed=5,
+                      verbose=0)
+    return hM
+
+
+def _oracle_inputs(hM):
+    post = H.poolMcmcChains(hM.postList)
+    return post, hM.Pi.astype(np.int32), hM.distr[:, 0].astype(int), np.asarray(hM.YScalePar)
+
+
+@pytest.mark.parametrize("expected", [True, False])
+def test_predict_matches_oracle(fitted, expected):
+    hM = fitted
+    post, Pi, fam, ysp = _oracle_inputs(hM)
+    seed = 4321
+    g = H.predict(hM, post=post, expected=expected, seed=seed)
+    o = O.predict_samples(np.asarray(hM.X, dtype=np.float64), post, Pi, fam, ysp, expected, Rng(seed))
+    assert len(g) == len(post)
+    for gs, os_ in zip(g, o):
+        cont = fam != 3 if not expected else np.ones(hM.ns, dtype=bool)
+        assert np.max(np.abs(gs[:, cont] - os_[:, cont])) < 1e-9 * max(1.0, np.max(np.abs(os_[:, cont])))
+        if not expected:
+            pois = fam == 3
+            assert np.mean(gs[:, pois] != os_[:, pois]) <= 1e-3
+            assert np.all(gs[:, pois] >= 0) and np.all(gs[:, pois] == np.round(gs[:, pois]))
+
+
+def test_computed_predicted_values_and_fit(fitted):
+    hM = fitted
+    predY = H.computePredictedValues(hM, expected=True, seed=3)
+    assert predY.shape == (hM.ny, hM.ns, len(H.poolMcmcChains(hM.postList)))
+    mf = H.evaluateModelFit(hM, predY)
+    probit = hM.distr[:, 0] == 2
+    assert np.all(mf["AUC"][probit] > 0.6)       # the model fits its own data
+    assert np.all(np.isfinite(mf["RMSE"]))
+
+
+def test_cross_validated_predictions(fitted):
+    hM = fitted
+    part = np.arange(hM.ny) % 2 + 1
+    predY = H.computePredictedValues(hM, partition=part, expected=True, seed=9)
+    assert predY.shape[:2] == (hM.ny, hM.ns) and np.all(np.isfinite(predY))

@@ -1,0 +1,58 @@
+"""Host logic of the post-sampling path: evaluateModelFit's measures
+(R/evaluateModelFit.R) against independent implementations, and predictLatentFactor's unit
+bookkeeping (R/predictLatentFactor.R:1-30).  No GPU: predict itself is tested in
+tests/test_gpu_predict.py."""
+import numpy as np
+from sklearn.metrics import roc_auc_score
+
+from helpers import H, synthetic_model
+from hmsc_amd.predict import _auc, evaluateModelFit, predictLatentFactor
+
+
+def test_auc_matches_sklearn_with_ties():
+    rng = np.random.default_rng(0)
+    y = (rng.random(300) < 0.4).astype(float)
+    p = np.round(rng.random(300) + 0.3 * y, 2)   # ties on purpose
+    assert abs(_auc(y, p) - roc_auc_score(y, p)) < 1e-12
+
+
+def test_evaluate_model_fit_probit_and_normal():
+    hM = synthetic_model(ny=80, ns=6, nc=2, nf=1, n_normal=2, seed=3)
+    rng = np.random.default_rng(1)
+    predY = np.clip(np.nan_to_num(hM.Y)[:, :, None] * 0.6 + 0.2 * rng.random((80, 6, 5)), 0, None)
+    mf = evaluateModelFit(hM, predY)
+    m = predY.mean(axis=2)
+    Y = hM.Y
+    assert np.allclose(mf["RMSE"], np.sqrt(np.mean((Y - m) ** 2, axis=0)))
+    for j in range(2):
+        co = np.corrcoef(Y[:, j], m[:, j])[0, 1]
+        assert abs(mf["R2"][j] - np.sign(co) * co ** 2) < 1e-12
+    for j in range(2, 6):
+        assert abs(mf["AUC"][j] - roc_auc_score(Y[:, j], m[:, j])) < 1e-12
+        assert abs(mf["TjurR2"][j] - (m[Y[:, j] == 1, j].mean() - m[Y[:, j] == 0, j].mean())) < 1e-12
+    assert np.isnan(mf["AUC"][0]) and np.isnan(mf["R2"][3])
+
+
+def test_evaluate_model_fit_poisson_measures():
+    hM = synthetic_model(ny=60, ns=3, nc=2, nf=1, n_poisson=3, seed=4)
+    rng = np.random.default_rng(2)
+    predY = rng.poisson(np.nan_to_num(hM.Y)[:, :, None] + 0.5, size=(60, 3, 7)).astype(float)
+    mf = evaluateModelFit(hM, predY)
+    med = np.median(predY, axis=2)
+    assert np.allclose(mf["RMSE"], np.sqrt(np.mean((hM.Y - med) ** 2, axis=0)))
+    pO = (predY > 0).mean(axis=2)
+    Yo = (hM.Y > 0).astype(float)
+    for j in range(3):
+        assert abs(mf["O.AUC"][j] - roc_auc_score(Yo[:, j], pO[:, j])) < 1e-12
+        assert abs(mf["O.RMSE"][j] - np.sqrt(np.mean((Yo[:, j] - pO[:, j]) ** 2))) < 1e-12
+    assert set(mf) >= {"SR2", "O.TjurR2", "C.SR2", "C.RMSE"}
+
+
+def test_predict_latent_factor_units():
+    post = [np.arange(6.0).reshape(3, 2), 10 + np.arange(6.0).reshape(3, 2)]
+    rl = H.HmscRandomLevel(units=["a", "b", "c"])
+    out = predictLatentFactor(["b", "z", "a"], ["a", "b", "c"], post, rl, predictMean=True)
+    assert np.array_equal(out[0], np.array([[2.0, 3.0], [0.0, 0.0], [0.0, 1.0]]))
+    assert np.array_equal(out[1][0], [12.0, 13.0])
+    draws = predictLatentFactor(["z", "y"], ["a"], post[:1], rl, rng=np.random.default_rng(0))
+    assert draws[0].shape == (2, 2) and np.all(draws[0] != 0)
