@@ -310,6 +310,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
     HMSC_REQUIRE(fam[j] >= 1 && fam[j] <= 3, "distr family must be 1 (normal), 2 (probit) or 3 (Poisson)");
     if (fam[j] != 2) s.all_probit = false;
     if (fam[j] == 1) s.any_normal = true;
+    if (fam[j] == 3) s.any_poisson = true;
     if (var[j] == 1) s.any_var = true;
     as[j] = m->aSigma[jg];
     bs[j] = m->bSigma[jg];

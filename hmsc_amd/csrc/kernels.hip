@@ -169,13 +169,13 @@ static int grid_for(int64_t n, int block = 64, int cap = 2048) {
   return (int)g;
 }
 
-template <bool DRAW, bool HAS_NA>
+template <bool DRAW, bool HAS_NA, bool POIS = false>
 static void z_dispatch(const State& s, dim3 grid, size_t smem, const ZArgs& a) {
   switch (z_nkb(s.K)) {
-    case 1: z_wave_kernel<DRAW, HAS_NA, 1><<<grid, 256, smem, s.stream>>>(a); break;
-    case 2: z_wave_kernel<DRAW, HAS_NA, 2><<<grid, 256, smem, s.stream>>>(a); break;
-    case 3: z_wave_kernel<DRAW, HAS_NA, 3><<<grid, 256, smem, s.stream>>>(a); break;
-    default: z_wave_kernel<DRAW, HAS_NA, 4><<<grid, 256, smem, s.stream>>>(a); break;
+    case 1: z_wave_kernel<DRAW, HAS_NA, 1, Z_ALL, POIS><<<grid, 256, smem, s.stream>>>(a); break;
+    case 2: z_wave_kernel<DRAW, HAS_NA, 2, Z_ALL, POIS><<<grid, 256, smem, s.stream>>>(a); break;
+    case 3: z_wave_kernel<DRAW, HAS_NA, 3, Z_ALL, POIS><<<grid, 256, smem, s.stream>>>(a); break;
+    default: z_wave_kernel<DRAW, HAS_NA, 4, Z_ALL, POIS><<<grid, 256, smem, s.stream>>>(a); break;
   }
 }
 
@@ -246,7 +246,12 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   const size_t smem = z_smem_bytes(s.K, s.nt);
   {
     ProfScope ps(s, PROF_Z);
-    if (draw) {
+    if (draw && s.any_poisson) {
+      if (s.has_na)
+        z_dispatch<true, true, true>(s, grid, smem, a);
+      else
+        z_dispatch<true, false, true>(s, grid, smem, a);
+    } else if (draw) {
       if (s.has_na)
         z_dispatch<true, true>(s, grid, smem, a);
       else

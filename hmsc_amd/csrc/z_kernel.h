@@ -115,7 +115,9 @@ __device__ __noinline__ double z_poisson_draw(double e, double sd, double y, dou
 constexpr int Z_ALL = 15;
 constexpr int ZT_TLD = 17;  // leading dimension of the wave's 16-site x 32-species tile T[jj][site]
 
-template <bool DRAW, bool HAS_NA, int NKB, int MODE = Z_ALL>
+// POIS: instantiated only for chains with Poisson species, so the probit kernel carries no
+// Poisson call site (its call-saved registers and code size cost the probit path ~5 %)
+template <bool DRAW, bool HAS_NA, int NKB, int MODE = Z_ALL, bool POIS = false>
 __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const unsigned long long kt0 = a.kt ? kt_now() : 0ull;
@@ -200,7 +202,7 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
               const double e = sT[jj * ZT_TLD + s];
               if (sFam[jj] == 1 && code >= 0)
                 z = a.Yval[cell];  // normal: Z = Y   R/updateZ.R:40-41
-              else if (sFam[jj] == 3 && code >= 0)
+              else if (POIS && sFam[jj] == 3 && code >= 0)
                 z = z_poisson_draw(e, sSd[jj], a.Yval[cell], a.zprev_is_e ? e : a.Z[cell],
                                    uniforms(a.key, (uint32_t)((size_t)i + (size_t)ny * (uint32_t)(a.sp0 + j)), 0,
                                             S_ZPOIS, SWEEP_ITER(a)),
