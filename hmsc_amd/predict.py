@@ -43,13 +43,21 @@ def predictLatentFactor(unitsPred, units, postEta, rL, predictMean=False, rng=No
     return out
 
 
-def predict(hM, post=None, X=None, studyDesign=None, expected=False, predictEtaMean=False, seed=None,
-            device=0):
-    """predict.Hmsc (R/predict.R): a list of ny x ns arrays, one per posterior sample."""
+def predict(hM, post=None, X=None, studyDesign=None, Yc=None, mcmcStep=1, expected=False, predictEtaMean=False,
+            seed=None, device=0):
+    """predict.Hmsc (R/predict.R): a list of ny x ns arrays, one per posterior sample.  With Yc
+    (conditional prediction, :191-202) each sample's latent factors are first updated given the
+    observed part of Yc by updateZ / (updateEta, updateZ) x mcmcStep on the device."""
     post = poolMcmcChains(hM.postList) if post is None else post
     X = np.asarray(hM.X if X is None else X, dtype=np.float64)
     nyN = X.shape[0]
     studyDesign = hM.studyDesign if studyDesign is None else studyDesign
+    if Yc is not None:
+        Yc = np.asarray(Yc, dtype=np.float64)
+        if Yc.shape[1] != hM.ns:
+            raise ValueError("hMsc.predict: number of columns in Yc must be equal to ns")
+        if Yc.shape[0] != nyN:
+            raise ValueError("hMsc.predict: number of rows in Yc and X must be equal")
     rng = np.random.default_rng(seed)
     S = len(post)
     keep = []
@@ -73,6 +81,10 @@ def predict(hM, post=None, X=None, studyDesign=None, expected=False, predictEtaM
             units = _levels(hM.dfPi[name])
             etas = predictLatentFactor(unitsPred, units, [s["Eta"][r] for s in post], hM.rL[r],
                                        predictMean=predictEtaMean, rng=rng)
+            if Yc is not None and np.any(~np.isnan(Yc)):
+                if r == 0:
+                    cond = _conditional_etas(hM, post, X, studyDesign, Yc, mcmcStep, rng, device)
+                etas = [c[r] for c in cond]
             nf = max(e.shape[1] for e in etas)
             lams = [np.asarray(s["Lambda"][r]) for s in post]
             etas = [np.pad(e, ((0, 0), (0, nf - e.shape[1]))) for e in etas]      # nf may vary (updateNf)
@@ -92,6 +104,41 @@ def predict(hM, post=None, X=None, studyDesign=None, expected=False, predictEtaM
     return [out[k] for k in range(S)]
 
 
+def _conditional_etas(hM, post, X, studyDesign, Yc, mcmcStep, rng, device):
+    """R/predict.R:191-202: per sample, Z = L; Z = updateZ(Yc); then mcmcStep x (updateEta,
+    updateZ), all with the sample's Beta, sigma, Lambda fixed -- the device updaters of a chain
+    built on (Yc, X) in R's unscaled space (X and Beta as `post` holds them)."""
+    from .model import Hmsc
+    from .sampler import Chain
+    rl = {name: hM.rL[r] for r, name in enumerate(hM.rLNames)}
+    sd = studyDesign.reset_index(drop=True) if hasattr(studyDesign, "reset_index") else studyDesign
+    hMc = Hmsc(Y=Yc, X=X, XScale=False, YScale=False, distr=hM.distr, studyDesign=sd, ranLevels=rl,
+               covNames=list(hM.covNames), spNames=list(hM.spNames))
+    ch = Chain(hMc, int(rng.integers(1, 2 ** 62)), device=device, updater={"GammaEta": False})
+    out = []
+    try:
+        ch.init()
+        units = [_levels(hM.dfPi[name]) for name in hM.rLNames]
+        for k, sam in enumerate(post):
+            etas = []
+            for r, name in enumerate(hM.rLNames):
+                etas.append(predictLatentFactor(_levels(sd[name]), units[r], [sam["Eta"][r]], hM.rL[r], rng=rng)[0])
+            L = X @ sam["Beta"]
+            for r in range(hM.nr):
+                L = L + etas[r][hMc.Pi[:, r] - 1] @ sam["Lambda"][r]
+            ch.set_state(dict(Beta=sam["Beta"], sigma=np.asarray(sam["sigma"]), Eta=etas,
+                              Lambda=[np.asarray(lm) for lm in sam["Lambda"]], Z=L))
+            it = 1 + k * (2 * mcmcStep + 1)
+            ch.update("Z", it)
+            for m in range(mcmcStep):
+                ch.update("Eta", it + 1 + 2 * m)
+                ch.update("Z", it + 2 + 2 * m)
+            out.append(ch.get_state(with_z=False)["Eta"])
+    finally:
+        ch.close()
+    return out
+
+
 def _stack(keep, arrays):
     flat = np.ascontiguousarray(np.concatenate(arrays).astype(np.float64)) if arrays else np.zeros(1)
     keep.append(flat)
@@ -104,11 +151,9 @@ def computePredictedValues(hM, partition=None, start=1, thin=1, Yc=None, mcmcSte
     model's own predictions; with one, K-fold cross-validation refits (sampleMcmc on the
     training rows with the fitted run's samples / transient / thin, predictions for the
     held-out rows)."""
-    if Yc is not None:
-        raise NotImplementedError("computePredictedValues: conditional prediction (Yc) is a 'next' row")
     if partition is None:
         post = poolMcmcChains(hM.postList, start=start, thin=thin)
-        pred = predict(hM, post=post, expected=expected, seed=seed)
+        pred = predict(hM, post=post, Yc=Yc, mcmcStep=mcmcStep, expected=expected, seed=seed)
         return np.stack(pred, axis=2)
     from .model import Hmsc
     from .sampler import sampleMcmc
@@ -129,7 +174,8 @@ def computePredictedValues(hM, partition=None, start=1, thin=1, Yc=None, mcmcSte
                          updater=updater, initPar=initPar, verbose=0)
         post = poolMcmcChains(hM1.postList, start=start)
         sdv = None if hM.studyDesign is None else hM.studyDesign.loc[val].reset_index(drop=True)
-        pred = predict(hM1, post=post, X=hM.X[val], studyDesign=sdv, expected=expected, seed=seed)
+        pred = predict(hM1, post=post, X=hM.X[val], studyDesign=sdv, Yc=None if Yc is None else np.asarray(Yc)[val],
+                       mcmcStep=mcmcStep, expected=expected, seed=seed)
         out[val] = np.stack(pred, axis=2)
     del nfolds
     return out

@@ -59,3 +59,21 @@ def test_cross_validated_predictions(fitted):
     part = np.arange(hM.ny) % 2 + 1
     predY = H.computePredictedValues(hM, partition=part, expected=True, seed=9)
     assert predY.shape[:2] == (hM.ny, hM.ns) and np.all(np.isfinite(predY))
+
+
+def test_conditional_prediction(fitted):
+    """predict(Yc=...) (R/predict.R:191-202): Eta updated on the device given the observed
+    part of Yc.  Conditioning on the probit species' own data must sharpen their predictions
+    (AUC up), and an all-NA Yc must reproduce the unconditional predictions exactly."""
+    hM = fitted
+    post = H.poolMcmcChains(hM.postList)[:6]
+    probit = np.nonzero(hM.distr[:, 0] == 2)[0]
+    Yc = np.full((hM.ny, hM.ns), np.nan)
+    Yc[:, probit] = hM.Y[:, probit]
+    base = np.stack(H.predict(hM, post=post, expected=True, seed=11), axis=2)
+    cond = np.stack(H.predict(hM, post=post, Yc=Yc, mcmcStep=3, expected=True, seed=11), axis=2)
+    fb = H.evaluateModelFit(hM, base)["AUC"][probit]
+    fc = H.evaluateModelFit(hM, cond)["AUC"][probit]
+    assert np.all(np.isfinite(cond)) and np.mean(fc) > np.mean(fb), (fb, fc)
+    same = np.stack(H.predict(hM, post=post, Yc=np.full((hM.ny, hM.ns), np.nan), expected=True, seed=11), axis=2)
+    assert np.array_equal(same, base)
