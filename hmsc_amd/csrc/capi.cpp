@@ -237,8 +237,10 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
     Level& L = s.lev[r];
     L.spatial = m->sDim != nullptr && m->sDim[r] != 0;
     if (L.spatial) {
-      HMSC_REQUIRE(m->spatialMethod != nullptr && m->spatialMethod[r] == 1,
-                   "spatial levels: only spatialMethod 'Full' is in this build (NNGP / GPP are a 'next' row)");
+      HMSC_REQUIRE(m->spatialMethod != nullptr && m->spatialMethod[r] >= 1 && m->spatialMethod[r] <= 3,
+                   "spatial level: spatialMethod must be 1 (Full), 2 (NNGP) or 3 (GPP)");
+      HMSC_REQUIRE(m->spatialMethod[r] == 1 || m->np[r] == ny,
+                   "spatial level: NNGP / GPP levels need np == ny (R/updateEta.R:140,165)");
       HMSC_REQUIRE(m->nalpha != nullptr && m->nalpha[r] > 0 && m->alphapw[r] && m->iWg[r] && m->RiWg[r] && m->detWg[r],
                    "spatial level: alphapw / iWg / RiWg / detWg (computeDataParameters' rLPar) must be given");
       HMSC_REQUIRE(!(mask & HMSC_UP_GAMMAETA),
@@ -292,6 +294,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
       L.alphapw = dupload(m->alphapw[r], 2 * G);
       L.iWg = dupload(m->iWg[r], np2 * G);
       L.RiWg = dupload(m->RiWg[r], np2 * G);
+      L.riw_lower = m->spatialMethod[r] == 2;
       L.detWg = dupload(m->detWg[r], G);
       L.spWork = dalloc<double>(spatial_work_doubles(s, r));
     }

@@ -33,6 +33,7 @@ struct SpArgs {
   const int* unit_rows;
   const double* iWg;      // np x np x nalpha
   const double* RiWg;
+  int riw_lower;          // RiWg lower triangular (NNGP's Vecchia factor), else upper (chol)
   const double* detWg;
   const double* alphapw;  // nalpha x 2
   double* AlphaD;         // nf (1-based grid index as double)
@@ -100,7 +101,8 @@ __global__ __launch_bounds__(1024) void eta_spatial_full_kernel(SpArgs a) {
   for (int e = t; e < N; e += nthr) a.Eta[e] = rhs[e];
 }
 
-// v[g * nf + h] = |RiWg[,,g] eta_h|^2 ; RiWg upper triangular (chol(iW)), one workgroup per g
+// v[g * nf + h] = |RiWg[,,g] eta_h|^2 ; RiWg upper triangular (chol(iW), Full / GPP) or lower
+// triangular (the NNGP factor D^-1/2 (I - A), R/computeDataParameters.R:127), one workgroup per g
 __global__ __launch_bounds__(256) void alpha_quad_kernel(SpArgs a) {
   const int g = blockIdx.x, np = a.np, nf = a.nf;
   const double* Rg = a.RiWg + (size_t)np * np * g;
@@ -111,7 +113,8 @@ __global__ __launch_bounds__(256) void alpha_quad_kernel(SpArgs a) {
     double s = 0.0;
     for (int p = threadIdx.x; p < np; p += blockDim.x) {
       double x = 0.0;
-      for (int p2 = p; p2 < np; ++p2) x = fma(Rg[p + (size_t)np * p2], eh[p2], x);
+      const int lo = a.riw_lower ? 0 : p, hi = a.riw_lower ? p + 1 : np;
+      for (int p2 = lo; p2 < hi; ++p2) x = fma(Rg[p + (size_t)np * p2], eh[p2], x);
       s = fma(x, x, s);
     }
     red[threadIdx.x] = s;
@@ -171,6 +174,7 @@ static SpArgs sp_args(State& s, int r, uint32_t iter) {
   a.unit_rows = L.unit_rows;
   a.iWg = L.iWg;
   a.RiWg = L.RiWg;
+  a.riw_lower = L.riw_lower;
   a.detWg = L.detWg;
   a.alphapw = L.alphapw;
   a.AlphaD = L.AlphaD;

@@ -28,14 +28,19 @@ def _finite_int(v, cap):
     return int(min(cap, v)) if not (isinstance(v, float) and math.isinf(v)) else int(cap)
 
 
+# include/hmsc_amd.h spatialMethod codes; every method reaches the device as the dense
+# prior precision of its alphapw grid (hmsc_amd/dataparams.py)
+SPATIAL_CODE = {"Full": 1, "NNGP": 2, "GPP": 3}
+
+
 class ModelBuffers:
     """Column-major copies of the hM fields the sampler consumes (the marshalling the
     R ``.Call`` shim would do), kept alive for the lifetime of the C struct."""
 
     def __init__(self, hM):
         for rl in hM.rL or []:
-            if rl.sDim and rl.spatialMethod != "Full":
-                raise NotImplementedError("NNGP / GPP spatial levels are a 'next' row (SURVEY.md §8 f2)")
+            if rl.sDim and rl.spatialMethod not in SPATIAL_CODE:
+                raise ValueError(f"unknown spatialMethod {rl.spatialMethod!r}")
             if rl.xDim:
                 raise NotImplementedError("covariate-dependent random levels are a 'next' row")
         self.keep = []
@@ -64,7 +69,8 @@ class ModelBuffers:
         m.nfMax = L.colmajor_ptr(self.nfMax or [0], k, np.int32)
         sdim = [1 if r.sDim else 0 for r in rl]
         m.sDim = L.colmajor_ptr(sdim or [0], k, np.int32)
-        m.spatialMethod = L.colmajor_ptr(sdim or [0], k, np.int32)     # 1 = Full
+        m.spatialMethod = L.colmajor_ptr([SPATIAL_CODE[r.spatialMethod] if r.sDim else 0 for r in rl] or [0],
+                                         k, np.int32)
         if any(sdim):
             # computeDataParameters' alphapw grid (R/computeDataParameters.R:53-81); the R shim
             # would pass dataParList$rLPar[[r]]$iWg / RiWg / detWg

@@ -81,11 +81,17 @@ typedef struct hmsc_model {
   const double* rhopw;    /* nrho*2 column-major: grid value, prior weight     */
   const double* C_vectors;/* ns*ns eigenvectors of C, column-major             */
   const double* C_values; /* ns    eigenvalues of C (> 0)                      */
-  /* Spatial levels (rL$sDim > 0), spatialMethod "Full" only: the alphapw grid of
-   * R/computeDataParameters.R:53-81 as computeDataParameters (or dataParList$rLPar) holds it,
-   * per level r (entries of non-spatial levels ignored / NULL).  iWg, RiWg are
-   * np*np*nalpha column-major (R's [np, np, alphaN] arrays), detWg nalpha. */
-  const int32_t* spatialMethod;              /* nr: 0 none, 1 Full (NNGP / GPP: not in this build) */
+  /* Spatial levels (rL$sDim > 0): the alphapw grid of R/computeDataParameters.R:47-196,
+   * per level r (entries of non-spatial levels ignored / NULL), as the dense prior
+   * precision of each grid point.  iWg, RiWg are np*np*nalpha column-major (R's
+   * [np, np, alphaN] arrays) with RiWg' RiWg = iWg, detWg nalpha = log det W.  RiWg is
+   * upper triangular, except for NNGP where it is R's lower-triangular factor.
+   *   Full: computeDataParameters' iWg / RiWg / detWg as they are (:53-81).
+   *   NNGP: as.matrix(iWg[[g]]), as.matrix(RiWg[[g]]) (the Vecchia factor), detWg (:82-136).
+   *   GPP:  iWg = diag(idDg[,g]) - idDW12g[,,g] iFg[,,g] t(idDW12g[,,g]), RiWg = chol(iWg),
+   *         detWg = detDg (:138-194; the precision R/updateEta.R:148-196 samples from).
+   * NNGP and GPP levels need np == ny (R/updateEta.R:140,165 build Diagonal(ny)). */
+  const int32_t* spatialMethod;              /* nr: 0 none, 1 Full, 2 NNGP, 3 GPP        */
   const int32_t* nalpha;                     /* nr: nrow(rL$alphapw)                     */
   const double* alphapw[HMSC_MAX_LEVELS];    /* nalpha*2: grid value, prior weight      */
   const double* iWg[HMSC_MAX_LEVELS];

@@ -73,12 +73,17 @@ def compute_data_parameters(model):
         RQg = np.eye(ns)[None]
         detQg = np.zeros(1)
     rLPar = []
-    for rl in model.get("rL", []):                             # :47-81 spatial "Full" grid
+    for rl in model.get("rL", []):                             # :47-196 spatial grids
         if not rl.get("sDim", 0):
             rLPar.append({})
             continue
-        if rl.get("spatialMethod", "Full") != "Full":
-            raise NotImplementedError("NNGP / GPP spatial levels (SURVEY.md §8 f2)")
+        method = rl.get("spatialMethod", "Full")
+        if method == "NNGP":
+            rLPar.append(_nngp_data_parameters(rl))
+            continue
+        if method == "GPP":
+            rLPar.append(_gpp_data_parameters(rl))
+            continue
         d = rl["dist"]                                         # np x np, levels(dfPi) order
         alphapw = rl["alphapw"]
         npr, G = d.shape[0], alphapw.shape[0]
@@ -91,6 +96,115 @@ def compute_data_parameters(model):
             iWg[g], RiWg[g], detWg[g] = iW, chol_upper(iW), 2 * np.sum(np.log(np.diag(RW)))
         rLPar.append(dict(iWg=iWg, RiWg=RiWg, detWg=detWg))
     return dict(Qg=Qg, iQg=iQg, RQg=RQg, detQg=detQg, rLPar=rLPar)
+
+
+def _nngp_data_parameters(rl):
+    """R/computeDataParameters.R:82-136.  Neighbours: FNN::get.knn(s, k) (FNN 1.1.x, exact
+    Euclidean kNN without the point itself; not vendored in the reference) restated by brute
+    force, sorted ascending, only earlier units kept (:93-104).  Per grid point: A[i, nb] =
+    K11^-1 k12, D[i] = 1 - k21 K11^-1 k12 (D = 1 for units without earlier neighbours),
+    RiW = D^-1/2 (I - A), iW = RiW' RiW, detW = sum(log D); identity for alpha = 0."""
+    s = np.asarray(rl["s"], dtype=np.float64)
+    k = int(rl.get("nNeighbours") or 10)
+    n = s.shape[0]
+    nb = []
+    for i in range(n):
+        dist = [(float(np.sum((s[i] - s[j]) ** 2)), j) for j in range(n) if j != i]
+        near = sorted(j for _, j in sorted(dist)[:k])
+        nb.append([j for j in near if j < i])
+    alphapw = rl["alphapw"]
+    G = alphapw.shape[0]
+    iWg, RiWg, detWg = np.empty((G, n, n)), np.empty((G, n, n)), np.zeros(G)
+    for g in range(G):
+        a = alphapw[g, 0]
+        RiW = np.eye(n)
+        if a != 0:
+            for i in range(n):
+                if not nb[i]:
+                    continue
+                pts = s[nb[i] + [i]]
+                Kp = np.exp(-np.sqrt(((pts[:, None] - pts[None, :]) ** 2).sum(-1)) / a)
+                v = np.linalg.solve(Kp[:-1, :-1], Kp[:-1, -1])
+                Di = Kp[-1, -1] - Kp[-1, :-1] @ v
+                RiW[i, :] = 0.0
+                RiW[i, i] = 1.0
+                RiW[i, nb[i]] = -v
+                RiW[i, :] /= np.sqrt(Di)
+                detWg[g] += np.log(Di)
+        iWg[g], RiWg[g] = RiW.T @ RiW, RiW
+    return dict(iWg=iWg, RiWg=RiWg, detWg=detWg)
+
+
+def _gpp_data_parameters(rl):
+    """R/computeDataParameters.R:138-194 literally (idDg, idDW12g, Fg, iFg, detDg), plus the
+    dense prior precision iW = diag(idD) - idDW12 iF idDW12' (Woodbury on W = D + W12 iW22
+    W12') with RiW = chol(iW) and detW = detD, which the sweep's updateEta uses
+    (_eta_spatial_full); gpp_eta_literal() restates R's own GPP updateEta and
+    tests/test_oracle_spatial.py pins the two to the same posterior."""
+    s = np.asarray(rl["s"], dtype=np.float64)
+    sK = np.asarray(rl["sKnot"], dtype=np.float64)
+    di12 = np.sqrt(((s[:, None] - sK[None, :]) ** 2).sum(-1))
+    di22 = np.sqrt(((sK[:, None] - sK[None, :]) ** 2).sum(-1))
+    alphapw = rl["alphapw"]
+    G, n, nK = alphapw.shape[0], s.shape[0], sK.shape[0]
+    out = dict(idDg=np.empty((G, n)), idDW12g=np.empty((G, n, nK)), Fg=np.empty((G, nK, nK)),
+               iFg=np.empty((G, nK, nK)), detDg=np.empty(G), iWg=np.empty((G, n, n)), RiWg=np.empty((G, n, n)))
+    for g in range(G):
+        a = alphapw[g, 0]
+        W22 = np.eye(nK) if a == 0 else np.exp(-di22 / a)
+        W12 = np.zeros((n, nK)) if a == 0 else np.exp(-di12 / a)
+        iW22 = np.linalg.solve(W22, np.eye(nK))
+        dD = 1 - np.diag(W12 @ iW22 @ W12.T)
+        liW22 = np.linalg.cholesky(iW22)
+        idD = 1 / dD
+        idDW12 = idD[:, None] * W12
+        F = W22 + W12.T @ idDW12
+        tmp2 = W12 @ liW22
+        DS = tmp2.T @ (idD[:, None] * tmp2) + np.eye(nK)
+        out["idDg"][g], out["idDW12g"][g], out["Fg"][g] = idD, idDW12, F
+        out["iFg"][g] = np.linalg.solve(F, np.eye(nK))
+        out["detDg"][g] = np.sum(np.log(dD)) + 2 * np.sum(np.log(np.diag(np.linalg.cholesky(DS))))
+        iW = np.diag(idD) - idDW12 @ out["iFg"][g] @ idDW12.T
+        out["iWg"][g] = 0.5 * (iW + iW.T)
+        out["RiWg"][g] = chol_upper(out["iWg"][g])
+    out["detWg"] = out["detDg"]
+    return out
+
+
+def gpp_eta_literal(st, model, r, S, dp, xi1=None, xi2=None):
+    """R/updateEta.R:148-196 as written: per-unit nf x nf blocks B0_i = Lam iSigma Lam' +
+    diag(idD[i, alpha]), iA = blockdiag(B0_i^-1), H = Fmat - idD1W12' iA idD1W12, and
+    eta = iA fS + iA W iRH iRH' W' iA fS + LiA xi1 + iA W iRH xi2 (xi1: np nf, xi2: nK nf
+    normals; zero -> the posterior mean).  Returns (eta, posterior covariance)."""
+    lam, iS = st["Lambda"][r], st["iSigma"]
+    nf = lam.shape[0]
+    par = dp["rLPar"][r]
+    alpha = np.asarray(st["Alpha"][r], dtype=np.int64) - 1
+    n = int(model["np"][r])
+    nK = par["Fg"].shape[1]
+    order = np.argsort(model["Pi"][:, r] - 1, kind="stable")
+    fS = (S[order] @ (iS[:, None] * lam.T)).ravel(order="F")
+    LSL = lam @ (iS[:, None] * lam.T)
+    iA = np.zeros((n * nf, n * nf))
+    LiA = np.zeros_like(iA)
+    for i in range(n):
+        idx = i + n * np.arange(nf)
+        B1 = np.linalg.inv(LSL + np.diag(par["idDg"][alpha, i]))
+        iA[np.ix_(idx, idx)] = B1
+        LiA[np.ix_(idx, idx)] = np.linalg.cholesky(B1)
+    Fmat = np.zeros((nK * nf, nK * nf))
+    W = np.zeros((n * nf, nK * nf))
+    for h in range(nf):
+        Fmat[h * nK:(h + 1) * nK, h * nK:(h + 1) * nK] = par["Fg"][alpha[h]]
+        W[h * n:(h + 1) * n, h * nK:(h + 1) * nK] = par["idDW12g"][alpha[h]]
+    iAW = iA @ W
+    H = Fmat - W.T @ iAW
+    iRH = np.linalg.inv(chol_upper(H))
+    tmp1 = iAW @ iRH
+    eta = iA @ fS + tmp1 @ (tmp1.T @ fS)
+    if xi1 is not None:
+        eta = eta + LiA @ xi1 + tmp1 @ xi2
+    return eta.reshape((n, nf), order="F"), iA + tmp1 @ tmp1.T
 
 
 # ---------------------------------------------------------------------------
@@ -446,7 +560,8 @@ def eta_unit_moments(st, model, r, S):
 
 
 def _eta_spatial_full(st, model, r, S, dp, rng, it, zero_noise):
-    """Spatial 'Full' level, R/updateEta.R:115-140: one dense (np nf)^2 system
+    """Spatial level, R/updateEta.R:115-147 ('Full'; 'NNGP' is the same code on a sparse
+    iWg; 'GPP' on the dense precision of _gpp_data_parameters): one dense (np nf)^2 system
     iUEta = bdiag(iWg[,,alpha_h]) + kron(Lam iSigma Lam', diag(colSums P)),
     fS = P'S (Lam diag(iSigma))', eta = R^-1 (R^-T vec(fS) + xi), R = chol(iUEta)."""
     lam, iS = st["Lambda"][r], st["iSigma"]
@@ -471,8 +586,9 @@ def _eta_spatial_full(st, model, r, S, dp, rng, it, zero_noise):
 
 
 def update_alpha(st, model, rng, it, data_par=None):
-    """R/updateAlpha.R:3-86, 'Full' levels: v_gh = |RiWg[,,g] eta_h|^2, log-likelihood
-    log(alphapw[g,2]) - detWg[g]/2 - v_gh/2, categorical draw by inverse CDF of the uniform
+    """R/updateAlpha.R:3-86: v_gh = |RiWg[,,g] eta_h|^2 ('Full', 'NNGP'), or for 'GPP'
+    eta_h' diag(idDg[,g]) eta_h - (eta' idDW12g iFg idDW12g' eta)_hh; log-likelihood
+    log(alphapw[g,2]) - detWg[g]/2 - v_gh/2 (detDg for GPP), categorical draw by inverse CDF of the uniform
     (idx h, S_ALPHA + LEVEL_STRIDE r); rep(1, nf) for non-spatial levels (:81-82)."""
     out = []
     for r, rl in enumerate(model["rL"]):
@@ -484,10 +600,22 @@ def update_alpha(st, model, rng, it, data_par=None):
         dp = data_par if data_par is not None else compute_data_parameters(model)
         par = dp["rLPar"][r]
         alphapw = rl["alphapw"]
-        v = np.stack([np.sum((par["RiWg"][g] @ eta) ** 2, axis=0) for g in range(alphapw.shape[0])])
+        if rl.get("spatialMethod", "Full") == "GPP":                   # :35-49, :64-75
+            G = alphapw.shape[0]
+            v = np.empty((G, nf))
+            det = par["detDg"]
+            for g in range(G):
+                t2 = eta.T @ par["idDW12g"][g]
+                t4 = (t2 @ par["iFg"][g]) @ t2.T
+                for h in range(nf):
+                    v[g, h] = eta[:, h] @ eta[:, h] if alphapw[g, 0] == 0 else \
+                        eta[:, h] @ (par["idDg"][g] * eta[:, h]) - t4[h, h]
+        else:                                                          # :21-34, :56-63
+            v = np.stack([np.sum((par["RiWg"][g] @ eta) ** 2, axis=0) for g in range(alphapw.shape[0])])
+            det = par["detWg"]
         a = np.empty(nf, dtype=np.int64)
         for h in range(nf):
-            like = np.log(alphapw[:, 1]) - 0.5 * par["detWg"] - 0.5 * v[:, h]
+            like = np.log(alphapw[:, 1]) - 0.5 * det - 0.5 * v[:, h]
             like = np.exp(like - like.max())
             u = rng.uniforms(h, 0, R.S_ALPHA + R.LEVEL_STRIDE * r, it)[0]
             a[h] = int(np.searchsorted(np.cumsum(like), u * like.sum(), side="right")) + 1

@@ -14,7 +14,7 @@ from oracle import hmsc_oracle as O  # noqa: E402
 
 def synthetic_model(ny=200, ns=30, nc=4, nf=3, seed=1, na_frac=0.0, n_normal=0, units=None, nr=1,
                     nf_fit=None, nt=1, yscale=False, C=None, n_poisson=0, n_lognormal=0, spatial=None,
-                    alpha_n=None):
+                    alpha_n=None, spatial_method="Full", n_neighbours=None, n_knots=None):
     """Probit JSDM generated like BASELINE.md's synthetic config; optionally the first
     n_normal species normal, the next n_poisson Poisson and n_lognormal lognormal Poisson
     (counts ~ Poisson(exp(L / 2)), vignette_2's mixed-distribution model)."""
@@ -39,7 +39,12 @@ def synthetic_model(ny=200, ns=30, nc=4, nf=3, seed=1, na_frac=0.0, n_normal=0, 
             # spatial 'Full' level: unit coordinates on the unit square, zero-padded unit
             # names so levels(dfPi) order is the coordinate row order
             sd[name] = np.array([f"s{k:05d}" for k in pi])
-            rl = H.HmscRandomLevel(sData=rng.random((npr, 2)))
+            xy = rng.random((npr, 2))
+            sKnot = None
+            if spatial_method == "GPP":
+                from hmsc_amd.dataparams import constructKnots
+                sKnot = constructKnots(xy, nKnots=n_knots or 4)
+            rl = H.HmscRandomLevel(sData=xy, sMethod=spatial_method, nNeighbours=n_neighbours, sKnot=sKnot)
             if alpha_n is not None:
                 diag = np.sqrt(2.0)
                 H.setPriors(rl, alphapw=np.column_stack([diag * np.arange(alpha_n + 1) / alpha_n,
@@ -90,7 +95,9 @@ def oracle_model(hM):
         if rl.sDim:   # spatial 'Full': the distance matrix of the unit coordinates, alphapw grid
             xy = np.asarray(rl.s, dtype=np.float64)
             d.update(spatialMethod=rl.spatialMethod, alphapw=np.asarray(rl.alphapw, dtype=np.float64),
-                     dist=np.sqrt(((xy[:, None, :] - xy[None, :, :]) ** 2).sum(-1)))
+                     dist=np.sqrt(((xy[:, None, :] - xy[None, :, :]) ** 2).sum(-1)),
+                     s=xy, nNeighbours=rl.nNeighbours,
+                     sKnot=rl["sKnot"] if "sKnot" in rl.names() else None)
     return m
 
 

@@ -1,4 +1,4 @@
-"""GPU parity of spatial 'Full' latent factors against the oracle:
+"""GPU parity of spatial latent factors ('Full', 'NNGP', 'GPP') against the oracle:
 updateEta's spatial branch (R/updateEta.R:111-140: one dense (np nf)^2 system over the
 alphapw grid matrices iWg[,,alpha_h]) and updateAlpha (R/updateAlpha.R:20-79: grid
 posterior from |RiWg eta_h|^2 and detWg).  The grids are computeDataParameters' (host,
@@ -23,6 +23,13 @@ MODELS = {
     "td_like": dict(ny=50, ns=4, nc=3, nf=2, nr=2, units=[50, 10], spatial=[1], seed=51, alpha_n=30),
     # observation-level spatial factors (np = ny), the default 101-point grid
     "obs_level": dict(ny=40, ns=6, nc=2, nf=2, nr=1, spatial=[0], seed=52),
+    # NNGP (R/computeDataParameters.R:82-136) and GPP (:138-194) levels reach the device as
+    # the dense prior precision of their grid (hmsc_amd/dataparams.py); the oracle's GPP
+    # updateAlpha is R's literal knot formula (R/updateAlpha.R:35-75)
+    "nngp": dict(ny=40, ns=6, nc=2, nf=2, nr=1, spatial=[0], seed=53, spatial_method="NNGP", n_neighbours=6),
+    "gpp": dict(ny=40, ns=6, nc=2, nf=2, nr=1, spatial=[0], seed=54, spatial_method="GPP", n_knots=4),
+    "nngp_two_levels": dict(ny=40, ns=5, nc=2, nf=2, nr=2, units=[40, 8], spatial=[0], seed=55,
+                            spatial_method="NNGP", alpha_n=20),
 }
 
 
