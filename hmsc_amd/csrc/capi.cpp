@@ -243,8 +243,9 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
                    "spatial level: NNGP / GPP levels need np == ny (R/updateEta.R:140,165)");
       HMSC_REQUIRE(m->nalpha != nullptr && m->nalpha[r] > 0 && m->alphapw[r] && m->iWg[r] && m->RiWg[r] && m->detWg[r],
                    "spatial level: alphapw / iWg / RiWg / detWg (computeDataParameters' rLPar) must be given");
-      HMSC_REQUIRE(!(mask & HMSC_UP_GAMMAETA),
-                   "updateGammaEta's spatial branch is a 'next' row: pass updater GammaEta=FALSE with spatial levels");
+      HMSC_REQUIRE(!(mask & HMSC_UP_GAMMAETA) || m->spatialMethod[r] == 1,
+                   "updataGammaEta: no method implemented yet for NNGP / GPP with GammaEta updater "
+                   "(R/updateGammaEta.R:153-158): pass updater GammaEta=FALSE");
     }
     HMSC_REQUIRE(m->xDim == nullptr || m->xDim[r] == 0,
                  "covariate-dependent random levels are a 'next' row: not in this build");
@@ -455,7 +456,11 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
     HMSC_REQUIRE(s.nranks == 1, "updateGammaEta cannot run on a species-sharded chain: pass updater GammaEta=FALSE");
     HMSC_REQUIRE((size_t)nc * s.ns <= 4096, "updateGammaEta: nc * ns must be <= 4096 (dense (nc ns)^2 system)");
     for (int r = 0; r < s.nr; ++r)
+    {
       HMSC_REQUIRE(s.lev[r].nfmax <= 16, "updateGammaEta: nfMax must be <= 16 in this build");
+      HMSC_REQUIRE(!s.lev[r].spatial || (size_t)nc * s.nt + (size_t)s.lev[r].np * s.lev[r].nfmax <= 8192,
+                   "updateGammaEta, spatial level: nc nt + np nfMax must be <= 8192 (dense joint system)");
+    }
     s.geWork = dalloc<double>(gamma_eta_work_doubles(s));
   }
   // recording ring: RING_SLOTS device slots, their pinned host mirror and the copied counter,

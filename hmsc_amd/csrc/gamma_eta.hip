@@ -1,4 +1,5 @@
-// updateGammaEta on the device (R/updateGammaEta.R:7-206), non-spatial levels (xDim = 0).
+// updateGammaEta on the device (R/updateGammaEta.R:7-206), levels with xDim = 0: non-spatial
+// levels below, spatial 'Full' levels in gamma_eta_spatial_kernel further down.
 //
 // Per random level r (sequentially, each level sees the new Eta of the levels before it):
 //   S    = Z - sum_{q != r} Eta_q[Pi_q,] Lambda_q                                  (:37-42)
@@ -457,12 +458,233 @@ __global__ __launch_bounds__(1024) void gamma_eta_kernel(GEArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Spatial 'Full' level (R/updateGammaEta.R:139-198): (vec Gamma, vec Eta_r) drawn jointly
+// with Beta integrated out, from the precision
+//   iG = bdiag(iU, iK) + Gm'Gm - tmp'tmp,  Gm = [kron(iD^.5 Tr, X), kron(iD^.5 Lam', P)],
+//   tmp = L_H^-1 C,  H = kron(iQ, iV) + kron(iD, X'X) = L_H L_H',
+//   C = [kron(iD Tr, X'X), t(kron(Lam iD, P'X))],  iK = bdiag(iWg[,,alpha_h]),
+// and mean iG^-1 (c0 - tmp' L_H^-1 vec(X'S iD)), c0 = [vec(X'S iD Tr); vec(P'S iD Lam')]:
+// the natural form of R's mg / me chain (the oracle pins the two equal,
+// tests/test_oracle_spatial.py).  Draw: m + chol(iG)^-1 xi, xi = normal(p, 0, S_GE_GAMMA).
+// One workgroup: every step is a dependent dense factorization of (nc ns)^2 or
+// (nc nt + np nf)^2, small at the configs that run this updater (TD's plot level).
+struct GESLayout {
+  size_t S, XtX, XtS, LamiD, LDL, iQm, PtX, PtS, cnt, TdT, TdL, H, C, y, iG, b, tot;
+};
+
+__host__ __device__ inline GESLayout ges_layout(int ny, int ns, int nc, int nt, int nf, int np) {
+  GESLayout o{};
+  const size_t N = (size_t)nc * ns, D2 = (size_t)nc * nt + (size_t)np * nf;
+  size_t p = 0;
+  auto take = [&](size_t n) {
+    const size_t at = p;
+    p += (n + 7) & ~(size_t)7;
+    return at;
+  };
+  o.S = take((size_t)ny * ns);
+  o.XtX = take((size_t)nc * nc);
+  o.XtS = take(N);
+  o.LamiD = take((size_t)nf * ns);
+  o.LDL = take((size_t)nf * nf);
+  o.iQm = take((size_t)ns * ns);
+  o.PtX = take((size_t)np * nc);
+  o.PtS = take((size_t)np * ns);
+  o.cnt = take(np);
+  o.TdT = take((size_t)nt * nt);
+  o.TdL = take((size_t)nt * nf);
+  o.H = take(N * N);
+  o.C = take(N * D2);
+  o.y = take(N);
+  o.iG = take(D2 * D2);
+  o.b = take(D2);
+  o.tot = p;
+  return o;
+}
+
+struct GESArgs {
+  GEArgs g;
+  const double* iWg;      // np x np x nalpha
+  const double* AlphaD;   // nf, 1-based grid index
+};
+
+__global__ __launch_bounds__(1024) void gamma_eta_spatial_kernel(GESArgs sa) {
+  const GEArgs& a = sa.g;
+  __shared__ int flag;
+  const int t = threadIdx.x, nthr = blockDim.x;
+  const int ny = a.ny, ns = a.ns, nc = a.nc, nt = a.nt, nf = a.nf, np = a.np, K = a.K;
+  const int N = nc * ns, G = nc * nt, D2 = G + np * nf;
+  const GESLayout o = ges_layout(ny, ns, nc, nt, nf, np);
+  double* w = a.work;
+  double *S = w + o.S, *XtX = w + o.XtX, *XtS = w + o.XtS, *LamiD = w + o.LamiD, *LDL = w + o.LDL;
+  double *iQm = w + o.iQm, *PtX = w + o.PtX, *PtS = w + o.PtS, *cnt = w + o.cnt, *TdT = w + o.TdT;
+  double *TdL = w + o.TdL, *H = w + o.H, *C = w + o.C, *y = w + o.y, *iG = w + o.iG, *b = w + o.b;
+  const uint32_t it = SWEEP_ITER(a);
+  const uint32_t str = LEVEL_STRIDE * (uint32_t)a.r;
+  const double* lam = a.BL + a.loff;  // Lambda_r[h, j] = lam[h + K j]
+  const double* id = a.iSigma;
+  const int* pi = a.lev_pi[a.r];
+
+  // ---- stage 1: S (:37-42), X'X, Lam iD, Lam iD Lam', iQ, P'X, unit counts, Tr'iD Tr, Tr'iD Lam'
+  for (size_t p = t; p < (size_t)ny * ns; p += nthr) {
+    const int i = (int)(p % ny), j = (int)(p / ny);
+    double sv = a.Z[p];
+    for (int q = 0; q < a.nr; ++q) {
+      if (q == a.r) continue;
+      const double* eq = a.lev_eta[q];
+      const int u = a.lev_pi[q][i], npq = a.lev_np[q];
+      const double* lq = a.BL + a.lev_loff[q] + (size_t)K * j;
+      for (int h = 0; h < a.lev_nf[q]; ++h) sv -= eq[u + (size_t)npq * h] * lq[h];
+    }
+    S[p] = sv;
+  }
+  for (int p = t; p < nc * nc; p += nthr) {
+    const int c1 = p % nc, c2 = p / nc;
+    double s = 0.0;
+    for (int i = 0; i < ny; ++i) s = fma(a.X[i + (size_t)ny * c1], a.X[i + (size_t)ny * c2], s);
+    XtX[p] = s;
+  }
+  for (int p = t; p < nf * ns; p += nthr) {
+    const int h = p % nf, j = p / nf;
+    LamiD[p] = lam[h + (size_t)K * j] * id[j];
+  }
+  for (int p = t; p < nf * nf; p += nthr) {
+    const int h1 = p % nf, h2 = p / nf;
+    double s = 0.0;
+    for (int j = 0; j < ns; ++j) s = fma(lam[h1 + (size_t)K * j] * id[j], lam[h2 + (size_t)K * j], s);
+    LDL[p] = s;
+  }
+  if (a.phU) {
+    const double* wq = a.phWinv + (size_t)ns * ((int)(*a.rho) - 1);
+    for (int p = t; p < ns * ns; p += nthr) {
+      const int j1 = p % ns, j2 = p / ns;
+      double si = 0.0;
+      for (int i = 0; i < ns; ++i) si = fma(a.phU[j1 + (size_t)ns * i] * a.phU[j2 + (size_t)ns * i], wq[i], si);
+      iQm[p] = si;
+    }
+  } else {
+    for (int p = t; p < ns * ns; p += nthr) iQm[p] = (p % ns == p / ns) ? 1.0 : 0.0;
+  }
+  for (int p = t; p < np * (nc + 1); p += nthr) {
+    const int u = p % np, c = p / np;
+    double s = 0.0;
+    for (int i = 0; i < ny; ++i)
+      if (pi[i] == u) s += (c < nc) ? a.X[i + (size_t)ny * c] : 1.0;
+    if (c < nc) PtX[p] = s; else cnt[u] = s;
+  }
+  for (int p = t; p < nt * (nt + nf); p += nthr) {
+    const int t1 = p % nt, k = p / nt;
+    double s = 0.0;
+    for (int j = 0; j < ns; ++j)
+      s = fma(id[j] * a.Tr[j + (size_t)ns * t1], k < nt ? a.Tr[j + (size_t)ns * k] : lam[(k - nt) + (size_t)K * j], s);
+    if (k < nt) TdT[t1 + nt * k] = s; else TdL[t1 + nt * (k - nt)] = s;
+  }
+  __syncthreads();
+  // ---- stage 2: X'S, P'S, H = kron(iQ, iV) + kron(iD, X'X)  (:183)
+  for (int p = t; p < N; p += nthr) {
+    const int c = p % nc, j = p / nc;
+    double s = 0.0;
+    for (int i = 0; i < ny; ++i) s = fma(a.X[i + (size_t)ny * c], S[i + (size_t)ny * j], s);
+    XtS[p] = s;
+  }
+  for (int p = t; p < np * ns; p += nthr) {
+    const int u = p % np, j = p / np;
+    double s = 0.0;
+    for (int i = 0; i < ny; ++i)
+      if (pi[i] == u) s += S[i + (size_t)ny * j];
+    PtS[p] = s;
+  }
+  for (size_t p = t; p < (size_t)N * N; p += nthr) {
+    const int r1 = (int)(p % N), r2 = (int)(p / N);
+    const int c1 = r1 % nc, j1 = r1 / nc, c2 = r2 % nc, j2 = r2 / nc;
+    H[p] = iQm[j1 + (size_t)ns * j2] * a.iV[c1 + nc * c2] + (j1 == j2 ? id[j1] * XtX[c1 + nc * c2] : 0.0);
+  }
+  __syncthreads();
+  // ---- stage 3: C, then L_H and tmp = L_H^-1 C (one column per thread), y = L_H^-1 vec(X'S iD)
+  for (size_t p = t; p < (size_t)N * D2; p += nthr) {
+    const int r1 = (int)(p % N), col = (int)(p / N);
+    const int c1 = r1 % nc, j = r1 / nc;
+    double v;
+    if (col < G) {
+      const int c2 = col % nc, q = col / nc;
+      v = id[j] * a.Tr[j + (size_t)ns * q] * XtX[c1 + nc * c2];
+    } else {
+      const int e = col - G, u = e % np, h = e / np;
+      v = LamiD[h + nf * j] * PtX[u + (size_t)np * c1];
+    }
+    C[p] = v;
+  }
+  for (int p = t; p < N; p += nthr) y[p] = XtS[p] * id[p / nc];
+  __syncthreads();
+  if (!wg_chol(H, N, N, &flag) && t == 0) a.fail[0] = 1;
+  for (int col = t; col < D2 + 1; col += nthr) {
+    double* x = col < D2 ? C + (size_t)N * col : y;
+    for (int i = 0; i < N; ++i) {
+      double s = x[i];
+      for (int k = 0; k < i; ++k) s -= H[i + (size_t)N * k] * x[k];
+      x[i] = s / H[i + (size_t)N * i];
+    }
+  }
+  __syncthreads();
+  // ---- stage 4: iG = bdiag(iU, iK) + Gm'Gm - tmp'tmp (:184-191), b = c0 - tmp'y
+  for (size_t p = t; p < (size_t)D2 * D2; p += nthr) {
+    const int p1 = (int)(p % D2), p2 = (int)(p / D2);
+    double v;
+    if (p1 < G && p2 < G) {
+      const int c1 = p1 % nc, t1 = p1 / nc, c2 = p2 % nc, t2 = p2 / nc;
+      v = TdT[t1 + nt * t2] * XtX[c1 + nc * c2] + a.iUGamma[p1 + (size_t)G * p2];
+    } else if (p1 >= G && p2 >= G) {
+      const int e1 = p1 - G, e2 = p2 - G, u1 = e1 % np, h1 = e1 / np, u2 = e2 % np, h2 = e2 / np;
+      v = (u1 == u2) ? cnt[u1] * LDL[h1 + nf * h2] : 0.0;
+      if (h1 == h2) {
+        const int g = (int)sa.AlphaD[h1] - 1;
+        v += sa.iWg[(size_t)np * np * g + u1 + (size_t)np * u2];
+      }
+    } else {
+      const int pg = p1 < G ? p1 : p2, pe = (p1 < G ? p2 : p1) - G;
+      const int c = pg % nc, q = pg / nc, u = pe % np, h = pe / np;
+      v = TdL[q + nt * h] * PtX[u + (size_t)np * c];
+    }
+    const double* c1 = C + (size_t)N * p1;
+    const double* c2 = C + (size_t)N * p2;
+    double s = 0.0;
+    for (int k = 0; k < N; ++k) s = fma(c1[k], c2[k], s);
+    iG[p] = v - s;
+  }
+  for (int p = t; p < D2; p += nthr) {
+    double c0 = 0.0;
+    if (p < G) {
+      const int c = p % nc, q = p / nc;
+      for (int j = 0; j < ns; ++j) c0 = fma(XtS[c + nc * j] * id[j], a.Tr[j + (size_t)ns * q], c0);
+    } else {
+      const int e = p - G, u = e % np, h = e / np;
+      for (int j = 0; j < ns; ++j) c0 = fma(PtS[u + (size_t)np * j], LamiD[h + nf * j], c0);
+    }
+    const double* cp = C + (size_t)N * p;
+    double s = 0.0;
+    for (int k = 0; k < N; ++k) s = fma(cp[k], y[k], s);
+    b[p] = c0 - s;
+  }
+  __syncthreads();
+  // ---- stage 5: m + chol(iG)^-1 xi = L^-T (L^-1 b + xi)   (:193-194)
+  if (!wg_chol(iG, D2, D2, &flag) && t == 0) a.fail[0] = 1;
+  wg_forward(iG, D2, D2, b);
+  for (int p = t; p < D2; p += nthr)
+    if (!a.noise_zero) b[p] += normal(a.key, (uint32_t)p, 0, S_GE_GAMMA + str, it);
+  __syncthreads();
+  wg_backward_t(iG, D2, D2, b);
+  for (int p = t; p < G; p += nthr) a.Gamma[p] = b[p];
+  for (int p = t; p < np * nf; p += nthr) a.Eta[p] = b[G + p];
+}
+
 size_t gamma_eta_work_doubles(const State& s) {
   size_t m = 0;
   for (int r = 0; r < s.nr; ++r) {
     const int nf = std::max(1, s.lev[r].nfmax);
     const int np = s.lev[r].np == s.ny ? 0 : s.lev[r].np;
     m = std::max(m, ge_layout(s.ny, s.ns, s.nc, s.nt, nf, np).tot);
+    if (s.lev[r].spatial) m = std::max(m, ges_layout(s.ny, s.ns, s.nc, s.nt, nf, s.lev[r].np).tot);
   }
   return m + 64;
 }
@@ -511,7 +733,15 @@ void launch_gamma_eta(State& s, uint32_t iter) {
     a.iter = iter;
     a.iter_dev = s.capturing ? s.d_iter : nullptr;
     a.noise_zero = s.noise_mode;
-    gamma_eta_kernel<<<1, 1024, 0, s.stream>>>(a);
+    if (s.lev[r].spatial) {
+      GESArgs sa{};
+      sa.g = a;
+      sa.iWg = s.lev[r].iWg;
+      sa.AlphaD = s.lev[r].AlphaD;
+      gamma_eta_spatial_kernel<<<1, 1024, 0, s.stream>>>(sa);
+    } else {
+      gamma_eta_kernel<<<1, 1024, 0, s.stream>>>(a);
+    }
     HIP_OK(hipGetLastError());
   }
   // Eta changed: XEta, its Gram and X'Eta Z of the next BetaLambda are stale

@@ -794,6 +794,87 @@ def sweep(st, model, rng, it, updater=None, data_par=None, adapt_nf=None):
 # Eta's rnorm(ny*nf) / rnorm(np*nf) normal(row i (np == ny) or unit p, h, S_GE_ETA), each
 # plus LEVEL_STRIDE * r.
 # ---------------------------------------------------------------------------
+def _spatial_pieces(st, model, r, S, dp):
+    X, Tr = model["X"], model["Tr"]
+    lam, idv = st["Lambda"][r], st["iSigma"]
+    ny = X.shape[0]
+    npr = int(model["np"][r])
+    P = np.zeros((ny, npr))
+    P[np.arange(ny), model["Pi"][:, r] - 1] = 1.0
+    alpha = np.asarray(st["Alpha"][r], dtype=np.int64) - 1
+    iWg = dp["rLPar"][r]["iWg"]
+    iK = np.zeros((npr * lam.shape[0],) * 2)
+    for h, a in enumerate(alpha):
+        iK[h * npr:(h + 1) * npr, h * npr:(h + 1) * npr] = iWg[a]
+    return X, Tr, lam, idv, P, iK
+
+
+def gamma_eta_spatial_literal(st, model, r, S, dp, iQ, iV, U, iU, iA):
+    """R/updateGammaEta.R:139-194 ('Full' spatial level) as written: the mean (mg, me)
+    through W = iK + kron(Lam iD Lam', P'P), M = iA + kron(iD, X'X) - ..., and the joint
+    precision iG = bdiag(iU, iK) + iG2 - iG3 of (vec Gamma, vec Eta).  K = bdiag(Wg) is
+    applied as a solve with iK (K = iK^-1).  Returns (m, iG)."""
+    X, Tr, lam, idv, P, iK = _spatial_pieces(st, model, r, S, dp)
+    nc, nt, ns = X.shape[1], Tr.shape[1], S.shape[1]
+    XtX, XtS = X.T @ X, X.T @ S
+    LamiD = lam * idv[None, :]
+    LamiDLam = (lam * np.sqrt(idv)[None, :]) @ (lam * np.sqrt(idv)[None, :]).T
+    iDT = idv[:, None] * Tr
+    iD05T = np.sqrt(idv)[:, None] * Tr
+    iD05Lamt = np.sqrt(idv)[:, None] * lam.T
+    PtX = P.T @ X
+    PtP = np.diag(P.sum(axis=0))
+    LamiDLam_PtP = np.kron(LamiDLam, PtP)                                    # :145
+    LamiD_PtX = np.kron(LamiD, PtX)
+    LamiDT_PtX = np.kron(LamiD @ Tr, PtX)
+    iDT_XtX = np.kron(iDT, XtX)
+    RW = chol_upper(iK + LamiDLam_PtP)                                       # :160-161
+    iLW = backsolve(RW, LamiD_PtX, transpose=True)                           # :163
+    iDL = iLW.T @ iLW
+    RM = chol_upper(iA + np.kron(np.diag(idv), XtX) - iDL)                  # :165-166
+    mg10 = (XtS @ iDT).ravel(order="F")                                      # :168
+    mg21 = ((P.T @ S) @ LamiD.T).ravel(order="F")
+    mg22 = backsolve(RW, backsolve(RW, mg21, transpose=True))
+    mg20 = LamiDT_PtX.T @ mg22
+    mg31 = (XtS * idv[None, :]).ravel(order="F") - LamiD_PtX.T @ mg22
+    mg32 = backsolve(RM, backsolve(RM, mg31, transpose=True))
+    tmp1 = iDT_XtX - iDL @ np.kron(Tr, np.eye(nc))                           # :174
+    mg = U @ (mg10 - mg20 - tmp1.T @ mg32)                                   # :175-176
+    me20 = LamiDLam_PtP @ mg22                                               # :178-181
+    me30 = LamiD_PtX @ mg32 - LamiDLam_PtP @ backsolve(RW, iLW @ mg32)
+    me = np.linalg.solve(iK, mg21 - me20 - me30)
+    H = np.kron(iQ, iV) + np.kron(np.diag(idv), XtX)                         # :183
+    nE = iK.shape[0]
+    iG1 = np.zeros((nc * nt + nE,) * 2)
+    iG1[:nc * nt, :nc * nt] = iU
+    iG1[nc * nt:, nc * nt:] = iK
+    Gm = np.hstack([np.kron(iD05T, X), np.kron(iD05Lamt, P)])                # :185
+    tmp = backsolve(chol_upper(H), np.hstack([iDT_XtX, LamiD_PtX.T]), transpose=True)
+    return np.r_[mg, me], iG1 + Gm.T @ Gm - tmp.T @ tmp
+
+
+def gamma_eta_spatial_natural(st, model, r, S, dp, iQ, iV, iU):
+    """The same joint conditional in natural form, as the device computes it
+    (hmsc_amd/csrc/gamma_eta.hip gamma_eta_spatial_kernel): with H = kron(iQ, iV) +
+    kron(iD, X'X) and C = [kron(iD Tr, X'X), t(kron(Lam iD, P'X))] (the Woodbury factors of
+    the B-integrated likelihood), mean = iG^-1 (c0 - C' H^-1 vec(X'S iD)),
+    c0 = [vec(X'S iD Tr); vec(P'S iD Lam')].  Returns (m, iG)."""
+    X, Tr, lam, idv, P, iK = _spatial_pieces(st, model, r, S, dp)
+    nc, nt = X.shape[1], Tr.shape[1]
+    XtX, XtS = X.T @ X, X.T @ S
+    LamiD = lam * idv[None, :]
+    LH = np.linalg.cholesky(np.kron(iQ, iV) + np.kron(np.diag(idv), XtX))
+    C = np.hstack([np.kron(idv[:, None] * Tr, XtX), np.kron(LamiD, P.T @ X).T])
+    tmp = solve_triangular(LH, C, lower=True)
+    y = solve_triangular(LH, (XtS * idv[None, :]).ravel(order="F"), lower=True)
+    c0 = np.r_[(XtS @ (idv[:, None] * Tr)).ravel(order="F"), ((P.T @ S) @ LamiD.T).ravel(order="F")]
+    Gm = np.hstack([np.kron(np.sqrt(idv)[:, None] * Tr, X), np.kron(np.sqrt(idv)[:, None] * lam.T, P)])
+    iG = Gm.T @ Gm - tmp.T @ tmp
+    iG[:nc * nt, :nc * nt] += iU
+    iG[nc * nt:, nc * nt:] += iK
+    return np.linalg.solve(iG, c0 - tmp.T @ y), iG
+
+
 def update_gamma_eta(st, model, rng, it, data_par=None, zero_noise=False):
     X, Tr, Pi, Z = model["X"], model["Tr"], model["Pi"], st["Z"]
     ny, ns = Z.shape
@@ -822,10 +903,21 @@ def update_gamma_eta(st, model, rng, it, data_par=None, zero_noise=False):
 
     for r in range(nr):
         rl = model["rL"][r]
-        if rl.get("sDim", 0) or rl.get("xDim", 0):
-            raise NotImplementedError("updateGammaEta: spatial / covariate-dependent levels (SURVEY.md §8 f2)")
+        if rl.get("xDim", 0):
+            raise NotImplementedError("updateGammaEta: covariate-dependent levels (SURVEY.md §8 f2)")
         s = R.LEVEL_STRIDE * r
         S = Z - sum(LRan[q] for q in range(nr) if q != r) if nr > 1 else Z  # :37-42
+        if rl.get("sDim", 0):                                                 # :139-198
+            if rl.get("spatialMethod", "Full") != "Full":
+                raise ValueError("updataGammaEta: no method implemented yet for NNGP / GPP with GammaEta updater")
+            mvec, iG = gamma_eta_spatial_literal(st, model, r, S, dp, iQ, iV, U, iU, iA)
+            D2 = iG.shape[0]
+            RG = chol_upper(iG)
+            ge = mvec + backsolve(RG, nrm(np.arange(D2), 0, R.S_GE_GAMMA + s, D2))   # :193-194
+            Gamma = ge[:nc * nt].reshape((nc, nt), order="F")
+            Eta[r] = ge[nc * nt:].reshape((int(model["np"][r]), -1), order="F")
+            LRan[r] = Eta[r][Pi[:, r] - 1] @ lam_all[r]
+            continue
         lam = lam_all[r]
         nf = lam.shape[0]
         lPi = Pi[:, r] - 1

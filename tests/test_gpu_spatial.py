@@ -131,3 +131,81 @@ def test_spatial_recorded_run(setup):
     assert a.shape[0] == 20 and np.all(a >= 1) and np.all(a <= hM.rL[r].alphapw.shape[0])
     assert np.all(np.isfinite(rec["Beta"]))
     ch.close()
+
+
+# updateGammaEta's spatial 'Full' branch (R/updateGammaEta.R:139-198): the joint (Gamma, Eta_r)
+# draw with Beta integrated out, default updater set (GammaEta on, as TD$m runs it)
+GE_MODELS = [k for k in MODELS if "nngp" not in k and "gpp" not in k]
+
+
+@pytest.fixture(scope="module", params=GE_MODELS)
+def ge_setup(request):
+    hM = synthetic_model(**MODELS[request.param])
+    m = oracle_model(hM)
+    dp = O.compute_data_parameters(m)
+    seed = 778
+    rng = Rng(seed)
+    st = O.compute_initial_parameters(m, rng)
+    for it in range(1, 3):
+        st = O.sweep(st, m, rng, it, data_par=dp)
+    r = [k for k, rl in enumerate(m["rL"]) if rl["sDim"]][0]
+    st["Alpha"] = list(st["Alpha"])
+    st["Alpha"][r] = np.array([7, 12])[:st["Eta"][r].shape[1]]
+    return request.param, hM, m, dp, seed, st
+
+
+def _ge_chain(hM, seed, st):
+    ch = H.Chain(hM, seed, device=0, updater={})
+    ch.init()
+    ch.set_state(st)
+    return ch
+
+
+def test_spatial_gamma_eta_moments(ge_setup):
+    name, hM, m, dp, seed, st = ge_setup
+    ch = _ge_chain(hM, seed, st)
+    ch.set_noise_mode(1)
+    ch.update("GammaEta", 5)
+    g = ch.get_state()
+    Gm, Eta = O.update_gamma_eta(st, m, Rng(seed), 5, data_par=dp, zero_noise=True)
+    assert rel_err(g["Gamma"], Gm) < TOL_MOMENT, (name, rel_err(g["Gamma"], Gm))
+    for q in range(hM.nr):
+        assert rel_err(g["Eta"][q], Eta[q]) < TOL_MOMENT, (name, q, rel_err(g["Eta"][q], Eta[q]))
+    ch.close()
+
+
+def test_spatial_gamma_eta_draws(ge_setup):
+    name, hM, m, dp, seed, st = ge_setup
+    ch = _ge_chain(hM, seed, st)
+    ch.update("GammaEta", 6)
+    g = ch.get_state()
+    Gm, Eta = O.update_gamma_eta(st, m, Rng(seed), 6, data_par=dp)
+    assert rel_err(g["Gamma"], Gm) < TOL_DRAW, (name, rel_err(g["Gamma"], Gm))
+    for q in range(hM.nr):
+        assert rel_err(g["Eta"][q], Eta[q]) < TOL_DRAW, (name, q)
+    ch.close()
+
+
+def test_spatial_default_updater_sweeps(ge_setup):
+    name, hM, m, dp, seed, st = ge_setup
+    ch = _ge_chain(hM, seed, st)
+    rng = Rng(seed)
+    o = dict(st)
+    for it in range(3, 6):
+        ch.sweep(it)
+        o = O.sweep(o, m, rng, it, data_par=dp)
+    g = ch.get_state()
+    for k in ("Beta", "Gamma", "iV", "Z"):
+        assert rel_err(g[k], o[k]) < TOL_SWEEP, (name, k, rel_err(g[k], o[k]))
+    for q in range(hM.nr):
+        assert rel_err(g["Eta"][q], o["Eta"][q]) < TOL_SWEEP, (name, q)
+        assert np.array_equal(g["Alpha"][q], o["Alpha"][q])
+    ch.close()
+
+
+def test_spatial_recorded_run_default_updaters(ge_setup):
+    name, hM, m, dp, seed, st = ge_setup
+    ch = _ge_chain(hM, seed, st)
+    rec = ch.run(transient=10, samples=20, thin=1, iter0=5)
+    assert np.all(np.isfinite(rec["Beta"])) and np.all(np.isfinite(rec["Gamma"]))
+    ch.close()

@@ -148,3 +148,31 @@ def test_model_buffers_accept_nngp_gpp():
     for meth in ("NNGP", "GPP"):
         b = ModelBuffers(_model(meth))
         assert b.struct.spatialMethod[0] == SPATIAL_CODE[meth]
+
+
+@pytest.mark.parametrize("kw", [
+    dict(ny=50, ns=4, nc=3, nf=2, nr=2, units=[50, 10], spatial=[1], seed=51, alpha_n=30, nt=2),
+    dict(ny=30, ns=5, nc=2, nf=2, nr=1, spatial=[0], seed=52)])
+def test_spatial_gamma_eta_natural_form_equals_literal(kw):
+    """R/updateGammaEta.R:139-194's mean chain (mg, me) equals iG^-1 (c0 - C'H^-1 s), the
+    natural form the device kernel evaluates; both use the same iG."""
+    from oracle.rng import Rng
+    hM = synthetic_model(**kw)
+    m = oracle_model(hM)
+    dp = O.compute_data_parameters(m)
+    st = O.compute_initial_parameters(m, Rng(5))
+    r = [k for k, rl in enumerate(m["rL"]) if rl["sDim"]][0]
+    st["Alpha"] = list(st["Alpha"])
+    st["Alpha"][r] = np.array([7, 12])
+    S = st["Z"] - sum(O.l_ran(st, m, q) for q in range(len(m["rL"])) if q != r)
+    iQ, Q = dp["iQg"][0], dp["Qg"][0]
+    iV = st["iV"]
+    V = O.chol2inv(O.chol_upper(iV))
+    U = m["UGamma"]
+    iU = O.chol2inv(O.chol_upper(U))
+    KT = np.kron(m["Tr"], np.eye(m["X"].shape[1]))
+    iA = O.chol2inv(O.chol_upper(KT @ U @ KT.T + np.kron(Q, V)))
+    m1, g1 = O.gamma_eta_spatial_literal(st, m, r, S, dp, iQ, iV, U, iU, iA)
+    m2, g2 = O.gamma_eta_spatial_natural(st, m, r, S, dp, iQ, iV, iU)
+    assert rel_err(g1, g2) < 1e-12
+    assert rel_err(m1, m2) < 1e-10
