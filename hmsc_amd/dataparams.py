@@ -213,10 +213,15 @@ def constructKnots(sData, nKnots=None, knotDist=None, minKnotDist=None):
 
 
 def _level_order(hM, r, rl):
-    """Rows of rl$s in levels(dfPi[,r]) order (R indexes s by unit names)."""
-    names = rl["sNames"] if "sNames" in rl.names() and rl["sNames"] is not None else None
-    levels = hM["dfPiLevels"][r] if "dfPiLevels" in hM.names() and hM["dfPiLevels"] is not None else None
-    if names is None or levels is None:
+    """Rows of rl$s in levels(dfPi[,r]) order (R indexes s by unit names,
+    R/computeDataParameters.R:56,92,142); unnamed coordinates are taken in that order."""
+    names = rl["sNames"] if "sNames" in rl.names() else None
+    if names is None:
         return np.arange(rl.s.shape[0] if rl.s is not None else rl.distMat.shape[0])
+    from .model import _factor_levels
+    levels = _factor_levels(hM.dfPi[hM.rLNames[r]])
     pos = {str(n): k for k, n in enumerate(names)}
+    missing = [lv for lv in levels if str(lv) not in pos]
+    if missing:
+        raise ValueError(f"spatial level {hM.rLNames[r]}: no coordinates for units {missing[:5]}")
     return np.array([pos[str(lv)] for lv in levels])

@@ -80,6 +80,8 @@ class HmscRandomLevel(_RList):
         if sData is not None:
             s = np.asarray(sData, dtype=np.float64)
             self.s = s
+            # rownames(sData): R indexes rL$s by unit name (computeDataParameters, predictLatentFactor)
+            self["sNames"] = [str(i) for i in sData.index] if hasattr(sData, "index") else None
             self.N = s.shape[0]
             self.sDim = s.shape[1]
             self.spatialMethod = sMethod

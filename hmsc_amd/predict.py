@@ -22,29 +22,138 @@ def _levels(values):
     return [str(v) for v in _factor_levels(values)]
 
 
-def predictLatentFactor(unitsPred, units, postEta, rL, predictMean=False, rng=None):
-    """R/predictLatentFactor.R:1-211 for non-spatial levels: known units keep their
-    posterior Eta rows; new units get N(0, 1) draws (or 0 with predictMean)."""
+def _coords(rL, names, units):
+    """Rows of rL$s for the given unit names (R indexes rL$s by rownames)."""
+    sn = rL["sNames"] if "sNames" in rL.names() else None
+    s = np.asarray(rL.s, dtype=np.float64)
+    if sn is None:            # unnamed coordinates: row k is the k-th level of the fitted units
+        pos = {u: k for k, u in enumerate(units)}
+        if any(n not in pos for n in names) or s.shape[0] != len(units):
+            raise ValueError("predictLatentFactor: coordinates of new spatial units are needed: give sData "
+                             "as a DataFrame whose index names every unit (rownames of rL$s)")
+    else:
+        pos = {str(u): k for k, u in enumerate(sn)}
+    return s[[pos[str(n)] for n in names]]
+
+
+def _pdist(a, b):
+    return np.sqrt(((a[:, None, :] - b[None, :, :]) ** 2).sum(-1))
+
+
+def predictLatentFactor(unitsPred, units, postEta, rL, predictMean=False, rng=None, postAlpha=None,
+                        predictMeanField=False):
+    """R/predictLatentFactor.R:35-210 (host side of predict, as in R): known units keep their
+    posterior Eta rows; new units of a non-spatial level get N(0, 1) draws (0 with
+    predictMean); new units of a spatial level are kriged from the sample's Eta with its
+    alphapw grid scale alpha_h (:59-204): predictMean / predictMeanField (:62-92), or the
+    method's joint conditional -- Full (:95-117), NNGP over the nNeighbours nearest fitted
+    units (:118-160), GPP through the knots (:161-203; R uses alpha[nf] for every factor
+    there, and so does this restatement)."""
+    if predictMean and predictMeanField:
+        raise ValueError("Hmsc.predictLatentFactor: predictMean and predictMeanField arguments cannot be simultaneously TRUE")
     units = [str(u) for u in units]
+    unitsPred = [str(u) for u in unitsPred]
     pos = {u: k for k, u in enumerate(units)}
     old = np.array([u in pos for u in unitsPred], dtype=bool)
-    if (~old).any() and rL.sDim:
-        raise NotImplementedError("predictLatentFactor: new units of a spatial level (SURVEY.md §8 f2)")
+    new = ~old
+    nn = int(new.sum())
     rng = rng or np.random.default_rng()
+    spatial = bool(rL.sDim) and nn > 0
+    if spatial:
+        if postAlpha is None:
+            raise ValueError("predictLatentFactor: postAlpha is needed for new units of a spatial level")
+        if rL.distMat is not None:
+            raise NotImplementedError("predictLatentFactor: spatial levels given by distMat")
+        s1 = _coords(rL, units, units)
+        s2 = _coords(rL, [u for u, o in zip(unitsPred, old) if not o], units)
+        alphapw = np.asarray(rL.alphapw, dtype=np.float64)
     out = []
-    for eta in postEta:
+    for k, eta in enumerate(postEta):
         nf = eta.shape[1]
         e = np.empty((len(unitsPred), nf))
         if old.any():
             e[old] = eta[[pos[u] for u, o in zip(unitsPred, old) if o]]
-        if (~old).any():
-            e[~old] = 0.0 if predictMean else rng.standard_normal(((~old).sum(), nf))
+        if nn and not spatial:
+            e[new] = 0.0 if predictMean else rng.standard_normal((nn, nf))
+        elif nn:
+            e[new] = _krige(rL, eta, np.asarray(postAlpha[k]), alphapw, s1, s2, predictMean, predictMeanField, rng)
         out.append(e)
     return out
 
 
+def _krige(rL, eta, alpha, alphapw, s1, s2, predictMean, predictMeanField, rng):
+    npo, nf, nn = s1.shape[0], eta.shape[1], s2.shape[0]
+    res = np.empty((nn, nf))
+    if predictMean or predictMeanField:                                       # :62-92
+        D11, D12 = _pdist(s1, s1), _pdist(s1, s2)
+        for h in range(nf):
+            a = alphapw[alpha[h] - 1, 0]
+            if a > 0:
+                K11, K12 = np.exp(-D11 / a), np.exp(-D12 / a)
+                m = K12.T @ np.linalg.solve(K11, eta[:, h])
+                if predictMean:
+                    res[:, h] = m
+                else:
+                    iLK = np.linalg.solve(np.linalg.cholesky(K11), K12)
+                    res[:, h] = m + rng.standard_normal(nn) * np.sqrt(1 - (iLK ** 2).sum(axis=0))
+            else:
+                res[:, h] = 0.0 if predictMean else rng.standard_normal(nn)
+        return res
+    method = rL.spatialMethod
+    if method == "Full":                                                      # :95-117
+        D = _pdist(np.vstack([s1, s2]), np.vstack([s1, s2]))
+        for h in range(nf):
+            a = alphapw[alpha[h] - 1, 0]
+            if a > 0:
+                K = np.exp(-D / a)
+                K11, K12, K22 = K[:npo, :npo], K[:npo, npo:], K[npo:, npo:]
+                m = K12.T @ np.linalg.solve(K11, eta[:, h])
+                W = K22 - K12.T @ np.linalg.solve(K11, K12)
+                res[:, h] = m + np.linalg.cholesky(W) @ rng.standard_normal(nn)
+            else:
+                res[:, h] = rng.standard_normal(nn)
+    elif method == "NNGP":                                                    # :118-160
+        k = int(rL.nNeighbours) if rL.nNeighbours is not None else 10
+        d = _pdist(s2, s1)
+        ind = np.argsort(d, axis=1, kind="stable")[:, :k]                     # FNN::knnx.index
+        for h in range(nf):
+            a = alphapw[alpha[h] - 1, 0]
+            if a > 0:
+                m = np.empty(nn)
+                F = np.empty(nn)
+                for i in range(nn):
+                    K11 = np.exp(-_pdist(s1[ind[i]], s1[ind[i]]) / a)
+                    K12 = np.exp(-d[i, ind[i]] / a)
+                    w = np.linalg.solve(K11, K12)
+                    m[i] = w @ eta[ind[i], h]
+                    F[i] = 1 - w @ K12
+                res[:, h] = m + np.sqrt(F) * rng.standard_normal(nn)
+            else:
+                res[:, h] = rng.standard_normal(nn)
+    elif method == "GPP":                                                     # :161-203
+        sK = np.asarray(rL["sKnot"], dtype=np.float64)
+        dss, dns, dnsOld = _pdist(sK, sK), _pdist(s2, sK), _pdist(s1, sK)
+        for h in range(nf):
+            a = alphapw[alpha[nf - 1] - 1, 0]                                  # R: ag = alpha[nf]
+            if a > 0:
+                Wns, W12, Wss = np.exp(-dns / a), np.exp(-dnsOld / a), np.exp(-dss / a)
+                iWss = np.linalg.inv(Wss)
+                dDn = 1 - ((Wns @ iWss) * Wns).sum(axis=1)
+                idD = 1 / (1 - np.einsum("ik,kl,il->i", W12, iWss, W12))
+                idDW12 = idD[:, None] * W12
+                iF = np.linalg.inv(Wss + W12.T @ idDW12)
+                LiF = np.linalg.cholesky(iF).T                                 # chol(): upper
+                mu = iF @ idDW12.T @ eta[:, h] + LiF @ rng.standard_normal(sK.shape[0])
+                res[:, h] = Wns @ mu + np.sqrt(dDn) * rng.standard_normal(nn)
+            else:
+                res[:, h] = rng.standard_normal(nn)
+    else:
+        raise ValueError(f"unknown spatialMethod {method!r}")
+    return res
+
+
 def predict(hM, post=None, X=None, studyDesign=None, Yc=None, mcmcStep=1, expected=False, predictEtaMean=False,
-            seed=None, device=0):
+            seed=None, device=0, predictEtaMeanField=False):
     """predict.Hmsc (R/predict.R): a list of ny x ns arrays, one per posterior sample.  With Yc
     (conditional prediction, :191-202) each sample's latent factors are first updated given the
     observed part of Yc by updateZ / (updateEta, updateZ) x mcmcStep on the device."""
@@ -80,7 +189,9 @@ def predict(hM, post=None, X=None, studyDesign=None, Yc=None, mcmcStep=1, expect
             unitsPred = _levels(raw)
             units = _levels(hM.dfPi[name])
             etas = predictLatentFactor(unitsPred, units, [s["Eta"][r] for s in post], hM.rL[r],
-                                       predictMean=predictEtaMean, rng=rng)
+                                       predictMean=predictEtaMean, rng=rng,
+                                       postAlpha=[s["Alpha"][r] for s in post] if hM.rL[r].sDim else None,
+                                       predictMeanField=predictEtaMeanField)
             if Yc is not None and np.any(~np.isnan(Yc)):
                 if r == 0:
                     cond = _conditional_etas(hM, post, X, studyDesign, Yc, mcmcStep, rng, device)
@@ -122,7 +233,8 @@ def _conditional_etas(hM, post, X, studyDesign, Yc, mcmcStep, rng, device):
         for k, sam in enumerate(post):
             etas = []
             for r, name in enumerate(hM.rLNames):
-                etas.append(predictLatentFactor(_levels(sd[name]), units[r], [sam["Eta"][r]], hM.rL[r], rng=rng)[0])
+                etas.append(predictLatentFactor(_levels(sd[name]), units[r], [sam["Eta"][r]], hM.rL[r], rng=rng,
+                                                postAlpha=[sam["Alpha"][r]] if hM.rL[r].sDim else None)[0])
             L = X @ sam["Beta"]
             for r in range(hM.nr):
                 L = L + etas[r][hMc.Pi[:, r] - 1] @ sam["Lambda"][r]

@@ -3,6 +3,7 @@
 bookkeeping (R/predictLatentFactor.R:1-30).  No GPU: predict itself is tested in
 tests/test_gpu_predict.py."""
 import numpy as np
+import pytest
 from sklearn.metrics import roc_auc_score
 
 from helpers import H, synthetic_model
@@ -56,3 +57,42 @@ def test_predict_latent_factor_units():
     assert np.array_equal(out[1][0], [12.0, 13.0])
     draws = predictLatentFactor(["z", "y"], ["a"], post[:1], rl, rng=np.random.default_rng(0))
     assert draws[0].shape == (2, 2) and np.all(draws[0] != 0)
+
+
+def _spatial_rl(method, s_df, **kw):
+    rl = H.HmscRandomLevel(sData=s_df, sMethod=method, **kw)
+    H.setPriors(rl, nfMin=2, nfMax=2)
+    return rl
+
+
+@pytest.mark.parametrize("method", ["Full", "NNGP", "GPP"])
+def test_predict_latent_factor_spatial(method):
+    """R/predictLatentFactor.R:59-204: new units of a spatial level are kriged; a new unit at
+    (almost) the location of a fitted one inherits its Eta under a smooth kernel."""
+    import pandas as pd
+    from hmsc_amd.dataparams import constructKnots
+    rng = np.random.default_rng(1)
+    xy = rng.random((30, 2))
+    names = [f"p{k:02d}" for k in range(30)]
+    xy_new = xy[:3] + 1e-6
+    df = pd.DataFrame(np.vstack([xy, xy_new]), index=names + ["n0", "n1", "n2"])
+    kw = dict(nNeighbours=5) if method == "NNGP" else dict(sKnot=constructKnots(xy, nKnots=6)) if method == "GPP" else {}
+    rl = _spatial_rl(method, df, **kw)
+    eta = np.column_stack([np.sin(4 * xy[:, 0]), np.cos(3 * xy[:, 1])])
+    alpha = np.array([60, 80])                   # long range: W ~ smooth, kriging ~ interpolation
+    unitsPred = ["n0", "p05", "n1", "n2"]
+    mean = predictLatentFactor(unitsPred, names, [eta], rl, predictMean=True, postAlpha=[alpha])[0]
+    assert np.allclose(mean[1], eta[5])
+    assert np.allclose(mean[[0, 2, 3]], eta[:3], atol=1e-3)
+    draws = predictLatentFactor(unitsPred, names, [eta] * 200, rl, postAlpha=[alpha] * 200,
+                                rng=np.random.default_rng(2))
+    d = np.stack(draws)
+    assert np.allclose(d[:, 1], eta[5])
+    if method != "GPP":                          # GPP's knot approximation leaves a nugget
+        assert np.abs(d[:, [0, 2, 3]].mean(0) - eta[:3]).max() < 1e-2
+    assert np.all(np.isfinite(d))
+    mf = predictLatentFactor(unitsPred, names, [eta], rl, predictMeanField=True, postAlpha=[alpha],
+                             rng=np.random.default_rng(3))[0]
+    assert np.allclose(mf[[0, 2, 3]], eta[:3], atol=1e-2)
+    with pytest.raises(ValueError):
+        predictLatentFactor(unitsPred, names, [eta], rl, predictMean=True, predictMeanField=True, postAlpha=[alpha])
