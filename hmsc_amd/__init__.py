@@ -10,10 +10,10 @@ from .model import Hmsc, HmscRandomLevel, setPriors, model_matrix  # noqa: F401
 from .post import (computeVariancePartitioning, convertToCodaObject, computeWAIC, effectiveSize,  # noqa: F401
                    gelman_diag, getPostEstimate, poolMcmcChains, spectrum0_ar)
 from .sampler import Chain, alignPosterior, combine_parameters, sampleMcmc, updater_mask  # noqa: F401
-from .dataparams import computeDataParameters  # noqa: F401
+from .dataparams import computeDataParameters, constructKnots  # noqa: F401
 from .predict import computePredictedValues, evaluateModelFit, predict, predictLatentFactor  # noqa: F401
 
 __all__ = ["Hmsc", "HmscRandomLevel", "setPriors", "sampleMcmc", "convertToCodaObject", "computeWAIC",
            "effectiveSize", "gelman_diag", "getPostEstimate", "poolMcmcChains", "alignPosterior",
-           "computeDataParameters", "Chain", "computeVariancePartitioning", "predict", "predictLatentFactor",
+           "computeDataParameters", "constructKnots", "Chain", "computeVariancePartitioning", "predict", "predictLatentFactor",
            "computePredictedValues", "evaluateModelFit"]

@@ -188,7 +188,11 @@ def _gpp_grid(hM, r, rl):
         iW = np.diag(idD) - idDW12 @ iF @ idDW12.T
         iW = 0.5 * (iW + iW.T)
         iWg[:, :, g] = iW
-        RiWg[:, :, g] = _chol_upper(iW)
+        try:
+            RiWg[:, :, g] = _chol_upper(iW)
+        except np.linalg.LinAlgError:
+            raise ValueError(f"computeDataParameters, GPP: precision at alphapw[{g + 1}] is not positive definite "
+                             f"(min dD = {dD.min():.3g}: is a knot on a sampling unit?)") from None
     return dict(idDg=idDg, idDW12g=idDW12g, Fg=Fg, iFg=iFg, detDg=detDg,
                 iWg=iWg, RiWg=RiWg, detWg=detDg.copy())
 
