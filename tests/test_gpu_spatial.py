@@ -8,7 +8,7 @@ grid indices exactly, and full sweeps (GammaEta off: its spatial branch is not b
 import numpy as np
 import pytest
 
-from helpers import H, O, oracle_model, rel_err, synthetic_model
+from helpers import H, O, oracle_model, phylo_corr, rel_err, synthetic_model
 from oracle.rng import Rng
 
 pytestmark = pytest.mark.gpu
@@ -28,6 +28,9 @@ MODELS = {
     # updateAlpha is R's literal knot formula (R/updateAlpha.R:35-75)
     "nngp": dict(ny=40, ns=6, nc=2, nf=2, nr=1, spatial=[0], seed=53, spatial_method="NNGP", n_neighbours=6),
     "gpp": dict(ny=40, ns=6, nc=2, nf=2, nr=1, spatial=[0], seed=54, spatial_method="GPP", n_knots=4),
+    # TD's shape with a phylogeny: updateGammaEta's spatial branch with iQ != I
+    "td_like_phylo": dict(ny=50, ns=4, nc=3, nf=2, nr=2, units=[50, 10], spatial=[1], seed=56, alpha_n=30,
+                          C=phylo_corr(4, seed=3)),
     "nngp_two_levels": dict(ny=40, ns=5, nc=2, nf=2, nr=2, units=[40, 8], spatial=[0], seed=55,
                             spatial_method="NNGP", alpha_n=20),
 }
