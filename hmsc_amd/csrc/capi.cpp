@@ -295,7 +295,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
       L.alphapw = dupload(m->alphapw[r], 2 * G);
       L.iWg = dupload(m->iWg[r], np2 * G);
       L.RiWg = dupload(m->RiWg[r], np2 * G);
-      L.riw_lower = m->spatialMethod[r] == 2;
+      L.riw_lower = m->spatialMethod[r] == 2 || m->spatialMethod[r] == 3;
       L.detWg = dupload(m->detWg[r], G);
       L.spWork = dalloc<double>(spatial_work_doubles(s, r));
     }

@@ -101,8 +101,9 @@ __global__ __launch_bounds__(1024) void eta_spatial_full_kernel(SpArgs a) {
   for (int e = t; e < N; e += nthr) a.Eta[e] = rhs[e];
 }
 
-// v[g * nf + h] = |RiWg[,,g] eta_h|^2 ; RiWg upper triangular (chol(iW), Full / GPP) or lower
-// triangular (the NNGP factor D^-1/2 (I - A), R/computeDataParameters.R:127), one workgroup per g
+// v[g * nf + h] = |RiWg[,,g] eta_h|^2 ; RiWg upper triangular (chol(iW), Full) or lower
+// triangular (NNGP's D^-1/2 (I - A), R/computeDataParameters.R:127; GPP's chol(W)^-1), one
+// workgroup per g
 __global__ __launch_bounds__(256) void alpha_quad_kernel(SpArgs a) {
   const int g = blockIdx.x, np = a.np, nf = a.nf;
   const double* Rg = a.RiWg + (size_t)np * np * g;

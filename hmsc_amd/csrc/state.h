@@ -36,8 +36,8 @@ struct Level {
   int nalpha = 0;
   double* alphapw = nullptr;    // nalpha x 2
   double* iWg = nullptr;        // np x np x nalpha
-  double* RiWg = nullptr;       // np x np x nalpha (upper triangular; lower for NNGP)
-  int riw_lower = 0;            // spatialMethod 2 (NNGP): RiWg is the lower Vecchia factor
+  double* RiWg = nullptr;       // np x np x nalpha (upper triangular; lower for NNGP / GPP)
+  int riw_lower = 0;            // spatialMethod 2 / 3: RiWg is lower (Vecchia factor / chol(W)^-1)
   double* detWg = nullptr;      // nalpha
   double* AlphaD = nullptr;     // nfmax: 1-based grid index of each factor (recorded)
   double* spWork = nullptr;     // dense (np nf)^2 Eta system + Alpha likelihoods

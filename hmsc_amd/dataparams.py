@@ -9,8 +9,10 @@ own fields as iWg / RiWg / detWg (RiWg' RiWg = iWg): the device runs every spati
 through the one dense (np nf)^2 updateEta / updateAlpha path (DESIGN.md §4 "Spatial
 levels"), and for GPP
 
-    iW = diag(idD) - idDW12 iF idDW12'      (Woodbury on W = D + W12 iW22 W12'),
+    iW = diag(idD) - idDW12 iF idDW12' = W^-1  (Woodbury on W = D + W12 iW22 W12'),
     det W = detD,
+
+computed as iW = RiW' RiW with RiW = chol(W)^-1 (lower triangular, like NNGP's factor),
 
 which is exactly the prior R/updateEta.R:148-196 and R/updateAlpha.R:35-75 condition on.
 """
@@ -185,14 +187,19 @@ def _gpp_grid(hM, r, rl):
         DS = tmp2.T @ (idD[:, None] * tmp2) + np.eye(nK)            # :184
         detD = float(np.sum(np.log(dD)) + 2 * np.sum(np.log(np.diag(np.linalg.cholesky(DS)))))
         idDg[:, g], idDW12g[:, :, g], Fg[:, :, g], iFg[:, :, g], detDg[g] = idD, idDW12, F, iF, detD
-        iW = np.diag(idD) - idDW12 @ iF @ idDW12.T
-        iW = 0.5 * (iW + iW.T)
-        iWg[:, :, g] = iW
+        # dense precision through W itself (unit diagonal): W = L L', RiW = L^-1 (lower),
+        # iW = RiW' RiW.  Equal to diag(idD) - idDW12 iF idDW12' but without its cancellation
+        # when a unit sits on a knot (dD -> 0, idD -> inf while W stays well conditioned)
+        W = W12 @ iW22 @ W12.T
+        W = 0.5 * (W + W.T)
+        W[np.diag_indices(npr)] = 1.0
         try:
-            RiWg[:, :, g] = _chol_upper(iW)
+            LW = np.linalg.cholesky(W)
         except np.linalg.LinAlgError:
-            raise ValueError(f"computeDataParameters, GPP: precision at alphapw[{g + 1}] is not positive definite "
-                             f"(min dD = {dD.min():.3g}: is a knot on a sampling unit?)") from None
+            raise ValueError(f"computeDataParameters, GPP: W at alphapw[{g + 1}] is not positive definite") from None
+        RiW = solve_triangular(LW, np.eye(npr), lower=True)
+        RiWg[:, :, g] = RiW
+        iWg[:, :, g] = RiW.T @ RiW
     return dict(idDg=idDg, idDW12g=idDW12g, Fg=Fg, iFg=iFg, detDg=detDg,
                 iWg=iWg, RiWg=RiWg, detWg=detDg.copy())
 

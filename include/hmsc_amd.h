@@ -85,10 +85,11 @@ typedef struct hmsc_model {
    * per level r (entries of non-spatial levels ignored / NULL), as the dense prior
    * precision of each grid point.  iWg, RiWg are np*np*nalpha column-major (R's
    * [np, np, alphaN] arrays) with RiWg' RiWg = iWg, detWg nalpha = log det W.  RiWg is
-   * upper triangular, except for NNGP where it is R's lower-triangular factor.
+   * upper triangular, except for NNGP (R's lower-triangular factor) and GPP (lower).
    *   Full: computeDataParameters' iWg / RiWg / detWg as they are (:53-81).
    *   NNGP: as.matrix(iWg[[g]]), as.matrix(RiWg[[g]]) (the Vecchia factor), detWg (:82-136).
-   *   GPP:  iWg = diag(idDg[,g]) - idDW12g[,,g] iFg[,,g] t(idDW12g[,,g]), RiWg = chol(iWg),
+   *   GPP:  iWg = diag(idDg[,g]) - idDW12g[,,g] iFg[,,g] t(idDW12g[,,g]) = W^-1, passed as
+   *         RiWg = solve(t(chol(W))) (lower) with W = D + W12 iW22 t(W12), iWg = t(RiWg) RiWg,
    *         detWg = detDg (:138-194; the precision R/updateEta.R:148-196 samples from).
    * NNGP and GPP levels need np == ny (R/updateEta.R:140,165 build Diagonal(ny)). */
   const int32_t* spatialMethod;              /* nr: 0 none, 1 Full, 2 NNGP, 3 GPP        */

@@ -137,8 +137,9 @@ def _nngp_data_parameters(rl):
 
 def _gpp_data_parameters(rl):
     """R/computeDataParameters.R:138-194 literally (idDg, idDW12g, Fg, iFg, detDg), plus the
-    dense prior precision iW = diag(idD) - idDW12 iF idDW12' (Woodbury on W = D + W12 iW22
-    W12') with RiW = chol(iW) and detW = detD, which the sweep's updateEta uses
+    dense prior precision iW = W^-1 = diag(idD) - idDW12 iF idDW12' (Woodbury on W = D + W12
+    iW22 W12'), as RiW' RiW with the lower factor RiW = chol(W)^-1, and detW = detD, which the
+    sweep's updateEta uses
     (_eta_spatial_full); gpp_eta_literal() restates R's own GPP updateEta and
     tests/test_oracle_spatial.py pins the two to the same posterior."""
     s = np.asarray(rl["s"], dtype=np.float64)
@@ -164,9 +165,10 @@ def _gpp_data_parameters(rl):
         out["idDg"][g], out["idDW12g"][g], out["Fg"][g] = idD, idDW12, F
         out["iFg"][g] = np.linalg.solve(F, np.eye(nK))
         out["detDg"][g] = np.sum(np.log(dD)) + 2 * np.sum(np.log(np.diag(np.linalg.cholesky(DS))))
-        iW = np.diag(idD) - idDW12 @ out["iFg"][g] @ idDW12.T
-        out["iWg"][g] = 0.5 * (iW + iW.T)
-        out["RiWg"][g] = chol_upper(out["iWg"][g])
+        W = W12 @ iW22 @ W12.T + np.diag(dD)                  # = D + W12 iW22 W12' (unit diagonal)
+        RiW = np.linalg.inv(np.linalg.cholesky(0.5 * (W + W.T)))
+        out["RiWg"][g] = np.tril(RiW)
+        out["iWg"][g] = out["RiWg"][g].T @ out["RiWg"][g]
     out["detWg"] = out["detDg"]
     return out
 

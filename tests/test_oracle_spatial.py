@@ -176,3 +176,24 @@ def test_spatial_gamma_eta_natural_form_equals_literal(kw):
     m2, g2 = O.gamma_eta_spatial_natural(st, m, r, S, dp, iQ, iV, iU)
     assert rel_err(g1, g2) < 1e-12
     assert rel_err(m1, m2) < 1e-10
+
+
+def test_gpp_knot_on_a_site():
+    """A knot (almost) on a sampling unit makes dD ~ 0 there (idD huge in R's form, where
+    diag(idD) - idDW12 iF idDW12' loses digits to cancellation); the dense precision, built from
+    W = D + W12 iW22 W12' itself, stays accurate.  (Exactly on a site, R's own DS / F are
+    infinite and R fails too.)"""
+    hM = _model("GPP")
+    rl = hM.rL[0]
+    s = np.asarray(rl.s)
+    rl["sKnot"] = np.vstack([np.asarray(rl["sKnot"]), s[7] + 1e-6])
+    prod = DPm.spatialDataParameters(hM)[0]
+    sK = np.asarray(rl["sKnot"])
+    d12 = np.sqrt(((s[:, None] - sK[None]) ** 2).sum(-1))
+    d22 = np.sqrt(((sK[:, None] - sK[None]) ** 2).sum(-1))
+    for g in (10, 60):
+        a = rl.alphapw[g, 0]
+        Q = np.exp(-d12 / a) @ np.linalg.solve(np.exp(-d22 / a), np.exp(-d12 / a).T)
+        W = Q + np.diag(1 - np.diag(Q))
+        assert np.all(np.isfinite(prod["iWg"][:, :, g]))
+        assert rel_err(prod["iWg"][:, :, g] @ W, np.eye(s.shape[0])) < 1e-6, g
