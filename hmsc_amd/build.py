@@ -5,51 +5,96 @@
 hipcc compiles the HIP kernels and the C ABI for --offload-arch=gfx950 and links
 RCCL (species-sharded chains).  No CPU fallback is built: the product path needs
 this library and fails loudly without it.
+
+Staleness is decided by content, not by mtime: every object records a hash of its
+source, the headers, the compiler flags and the hipcc version next to it
+(``*.o.sha``), so a tree copied to another machine (whose mtimes say nothing) is
+recompiled exactly when something that goes into the object differs.
 """
+import hashlib
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libhmsc_amd.so")
-SOURCES = ["kernels.hip", "phylo.hip", "gamma_eta.hip", "spatial.hip", "predict.hip", "capi.cpp"]
+SOURCES = ["kernels.hip", "zdraw.hip", "phylo.hip", "gamma_eta.hip", "spatial.hip", "predict.hip", "capi.cpp"]
 HEADERS = ["common.h", "rng.h", "state.h", "wave_la.h", "z_kernel.h", os.path.join("..", "..", "include", "hmsc_amd.h")]
 ARCH = os.environ.get("HMSC_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-fPIC", "-std=c++17", "-pthread", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
+# per-source extra flags: the z kernel's inlined draw keeps its polynomial constants at their
+# uses (MachineLICM would hoist ~60 f64 constants out of the site loop and spill them)
+EXTRA = {"zdraw.hip": ["-mllvm", "-disable-machine-licm"]}
 
 
-def _stale(target, deps):
-    if not os.path.exists(target):
-        return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(d) > t for d in deps)
+def _hipcc_version():
+    try:
+        return subprocess.run([HIPCC, "--version"], capture_output=True, text=True, timeout=60).stdout
+    except Exception:  # pragma: no cover
+        return "unknown"
 
 
-def build(force=False, verbose=True, stamps=False):
+def _digest(paths, extra):
+    h = hashlib.sha256()
+    for p in paths:
+        with open(p, "rb") as f:
+            h.update(p.encode() + b"\0" + f.read())
+    h.update("\0".join(extra).encode())
+    return h.hexdigest()
+
+
+def _fresh(target, digest):
+    stamp = target + ".sha"
+    if not (os.path.exists(target) and os.path.exists(stamp)):
+        return False
+    with open(stamp) as f:
+        return f.read().strip() == digest
+
+
+def _stamp(target, digest):
+    with open(target + ".sha", "w") as f:
+        f.write(digest + "\n")
+
+
+def build(force=False, verbose=True, stamps=False, jobs=None):
     """stamps=True builds the diagnostic library libhmsc_amd_stamps.so (HMSC_STAMP clock
     stamps in the kernels; select it with HMSC_AMD_LIB=...)."""
     lib = LIB.replace(".so", "_stamps.so") if stamps else LIB
     flags = FLAGS + (["-DHMSC_STAMPS"] if stamps else [])
-    objs = []
     hdrs = [os.path.join(CSRC, h) for h in HEADERS]
+    ver = _hipcc_version()
+    todo, objs, digests = [], [], []
     for src in SOURCES:
         path = os.path.join(CSRC, src)
         obj = os.path.join(CSRC, os.path.splitext(src)[0] + ("_stamps.o" if stamps else ".o"))
+        cmd = [HIPCC] + flags + EXTRA.get(src, []) + ["-x", "hip", "-c", path, "-o", obj]
+        dg = _digest([path] + hdrs, cmd + [ver])
         objs.append(obj)
-        if force or _stale(obj, [path] + hdrs):
-            cmd = [HIPCC] + flags + ["-x", "hip", "-c", path, "-o", obj]
-            if verbose:
-                print(" ".join(cmd), flush=True)
-            subprocess.check_call(cmd)
-    if force or _stale(lib, objs):
-        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", lib] + objs + \
-              ["-pthread", "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
+        digests.append(dg)
+        if force or not _fresh(obj, dg):
+            todo.append((cmd, obj, dg))
+
+    def compile_one(job):
+        cmd, obj, dg = job
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
+        _stamp(obj, dg)
+
+    with ThreadPoolExecutor(max_workers=jobs or min(8, max(1, len(todo)))) as ex:
+        list(ex.map(compile_one, todo))
+    link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", lib] + objs + \
+           ["-pthread", "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
+    ldg = hashlib.sha256(("\0".join(digests + link)).encode()).hexdigest()
+    if force or todo or not _fresh(lib, ldg):
+        if verbose:
+            print(" ".join(link), flush=True)
+        subprocess.check_call(link)
+        _stamp(lib, ldg)
     return lib
 
 

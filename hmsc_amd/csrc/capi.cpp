@@ -339,6 +339,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
     }
   }
   s.has_na = !na_cols.empty();
+  ycode.resize((size_t)ny * (nsl + 32) + 64, 0);  // z kernel loads past the last species (z_kernel.h ZArgs)
   s.Ycode = dupload(ycode.data(), ycode.size());
   if (!s.all_probit) {
     s.Yval = dupload(yval.data(), yval.size());
@@ -432,7 +433,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   const int n_sblk = (ny + 63) / 64;
   s.zl_split = std::max(1, std::min(std::min(16, (nsl + 3) / 4), (640 + n_sblk - 1) / n_sblk));
   s.XZ = dalloc<double>((size_t)s.Kmax * nsl);
-  s.XEta = dalloc<double>((size_t)ny * s.Kmax);
+  s.XEta = dalloc<double>((size_t)ny * 16 * ((s.Kmax + 15) / 16) + 64);  // padded (z_kernel.h ZArgs)
   s.G = dalloc<double>((size_t)s.Kmax * s.Kmax);
   s.ZTr = dalloc<double>((size_t)ny * nt);
   s.XZ_part = dalloc<double>((size_t)s.nchunk * s.Kmax * nsl);

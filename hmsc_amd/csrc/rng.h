@@ -156,11 +156,7 @@ __host__ __device__ __forceinline__ double qnorm_as241(double p) {
 // constant segment: scalar loads put each coefficient in an SGPR pair that v_fma_f64 takes
 // directly, instead of two v_mov_b32 per coefficient for an inline 64-bit constant (which
 // doubled the VALU cost of every Horner step).
-#if defined(__HIP_DEVICE_COMPILE__)
-#define HMSC_TABLE __constant__ const
-#else
 #define HMSC_TABLE static constexpr
-#endif
 HMSC_TABLE double kErfcPoly[25] = {
       -1.6096273515890176e-08, 2.8896766487768683e-08, 9.88621235162138e-08,   -2.844034573481913e-07,
       -1.0193810001498908e-07, 1.2706984221004204e-06, -1.3111619454625253e-06, -2.9457683933017214e-06,
@@ -211,7 +207,9 @@ __host__ __device__ __forceinline__ double rcp_pos(double d) {
 #endif
 }
 
-__host__ __device__ __forceinline__ double log_fast(double x) {  // x positive, normal
+// The *_t forms take their coefficient tables as pointers (device kernels pass pointers the
+// compiler cannot hoist, z_kernel.h opaque_table); the plain forms use the global tables.
+__host__ __device__ __forceinline__ double log_fast_t(double x, const double* ls) {  // x positive, normal
   uint64_t b;
   __builtin_memcpy(&b, &x, 8);
   int e = (int)(b >> 52) - 1023;
@@ -226,30 +224,34 @@ __host__ __device__ __forceinline__ double log_fast(double x) {  // x positive, 
   const double s = f * rcp_pos(2.0 + f);
   const double z = s * s;
   // P(z) = sum_{k=1..10} 2 z^(k-1) / (2k+1); truncation < 3e-17 relative for |s| <= 0.1716
-  double P = kLogSeries[0];
+  double P = ls[0];
 #pragma unroll
-  for (int k = 1; k < 10; ++k) P = fma_sc(P, z, kLogSeries[k]);
+  for (int k = 1; k < 10; ++k) P = fma_sc(P, z, ls[k]);
   const double lm = fma(s * z, P, 2.0 * s);
   const double de = (double)e;
   return fma(de, 0.6931471803691238, fma(de, 1.9082149292705877e-10, lm));  // ln2 = hi + lo, hi*e exact
 }
 
-__host__ __device__ __forceinline__ double erfc_fast(double z) {
+__host__ __device__ __forceinline__ double log_fast(double x) { return log_fast_t(x, kLogSeries); }
+
+__host__ __device__ __forceinline__ double erfc_fast_t(double z, const double* ep) {
   const double a = fmin(fabs(z), 40.0);
   const double t = 2.0 * rcp_pos(2.0 + a);
   const double x = 2.0 * t - 1.0;
-  double g = kErfcPoly[0];
+  double g = ep[0];
 #pragma unroll
-  for (int k = 1; k < 25; ++k) g = fma_sc(g, x, kErfcPoly[k]);
+  for (int k = 1; k < 25; ++k) g = fma_sc(g, x, ep[k]);
   const double r = t * exp(fma(-a, a, g));
   return z < 0.0 ? 2.0 - r : r;
 }
 
+__host__ __device__ __forceinline__ double erfc_fast(double z) { return erfc_fast_t(z, kErfcPoly); }
+
 // AS241's |q| > 0.425 branch (R's qnorm), with log_fast
-__host__ __device__ __forceinline__ double qnorm_as241_tail(double p) {
+__host__ __device__ __forceinline__ double qnorm_as241_tail_t(double p, const double* ls) {
   const double q = p - 0.5;
   double r = q < 0.0 ? p : 1.0 - p;
-  r = sqrt(-log_fast(r));
+  r = sqrt(-log_fast_t(r, ls));
   double val;
   if (r <= 5.0) {
     r -= 1.6;
@@ -277,25 +279,28 @@ __host__ __device__ __forceinline__ double qnorm_as241_tail(double p) {
   return q < 0.0 ? -val : val;
 }
 
-__host__ __device__ __forceinline__ double qnorm_fast(double p) {
+__host__ __device__ __forceinline__ double qnorm_fast_t(double p, const double* qa, const double* qb,
+                                                        const double* ls) {
   const double y = 2.0 * p - 1.0;
-  const double w = -log_fast(4.0 * p * (1.0 - p));
+  const double w = -log_fast_t(4.0 * p * (1.0 - p), ls);
   if (w < 6.25) {
     const double t = w - 3.125;
-    double f = kQnormA[0];
+    double f = qa[0];
 #pragma unroll
-    for (int k = 1; k < 23; ++k) f = fma_sc(f, t, kQnormA[k]);
+    for (int k = 1; k < 23; ++k) f = fma_sc(f, t, qa[k]);
     return y * f;
   }
   if (w < 16.0) {
     const double t = sqrt(w) - 3.25;
-    double f = kQnormB[0];
+    double f = qb[0];
 #pragma unroll
-    for (int k = 1; k < 19; ++k) f = fma_sc(f, t, kQnormB[k]);
+    for (int k = 1; k < 19; ++k) f = fma_sc(f, t, qb[k]);
     return y * f;
   }
-  return qnorm_as241_tail(p);
+  return qnorm_as241_tail_t(p, ls);
 }
+
+__host__ __device__ __forceinline__ double qnorm_fast(double p) { return qnorm_fast_t(p, kQnormA, kQnormB, kLogSeries); }
 
 // standard normal by inversion of the first uniform of the (idx, sub) block (R's default
 // rnorm method, INVERSION; the oracle uses AS241 itself, the device qnorm_fast)
@@ -359,10 +364,16 @@ __host__ __device__ inline void pg_moments(double b, double c, double* mean, dou
 //   x = Phic^-1(u Phic(alpha)) = -Phi^-1(u * 0.5 erfc(alpha / sqrt 2)),
 // with the exponential tail expansion beyond alpha > 25 (u Phic(alpha) < 1e-138 there).
 // alpha = -inf (NA cells, R/updateZ.R:92) gives p = u: an untruncated normal.
+__host__ __device__ __forceinline__ double trunc_normal_lower_t(double alpha, double u, const double* ep,
+                                                                const double* qa, const double* qb,
+                                                                const double* ls) {
+  if (alpha > 25.0) return alpha - log_fast_t(u, ls) / alpha;
+  const double p = u * (0.5 * erfc_fast_t(alpha * 0.7071067811865476, ep));
+  return -qnorm_fast_t(p, qa, qb, ls);
+}
+
 __host__ __device__ __forceinline__ double trunc_normal_lower(double alpha, double u) {
-  if (alpha > 25.0) return alpha - log_fast(u) / alpha;
-  const double p = u * (0.5 * erfc_fast(alpha * 0.7071067811865476));
-  return -qnorm_fast(p);
+  return trunc_normal_lower_t(alpha, u, kErfcPoly, kQnormA, kQnormB, kLogSeries);
 }
 
 }  // namespace hmsc

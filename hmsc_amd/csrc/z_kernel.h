@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "common.h"
 #include "rng.h"
 
 namespace hmsc {
@@ -24,6 +25,10 @@ namespace hmsc {
 //   ZTr  = Z Tr             DPP row reductions over the 16 species pairs
 // so Z is written once and never re-read by updateBetaLambda or updateGamma2.
 // ---------------------------------------------------------------------------
+// XEta and Ycode are allocated with padding (capi.cpp build_state) so the kernel loads them
+// unguarded: XEta holds ny * 16 ceil(Kmax / 16) + 64 doubles (finite; columns >= K and the
+// rows past ny of the last tile only ever meet zero BL rows / zeroed Z), Ycode ny (nsl + 32) + 64
+// bytes (zero past the last species).
 struct ZArgs {
   const double* XEta;  // ny x K (ld ny)
   int ny, K, ns_loc, sp0, nt, tiles_per_chunk;
@@ -80,10 +85,7 @@ __device__ __forceinline__ double row_sum16(double v) {
   return v;
 }
 
-// one latent draw, out of line: the ~100 polynomial constants of erfc / qnorm / log are
-// then materialised inside the call instead of being hoisted into the kernel's register
-// file (which would cut the z kernel to one wave per SIMD); called from a rolled loop so
-// only the loop state is live across the call.
+// one latent draw (rare paths: Poisson-chain kernels, the tails of the paired draw below)
 //   code 1 / 0: probit TN(E, sd) on [0, inf) / (-inf, 0]     R/updateZ.R:43-63
 //   code < 0 : NA cell, N(E, sd) = truncation at -inf           R/updateZ.R:92
 __device__ __noinline__ double z_probit_draw(double e, double sd, double isd, int code, double u, int noise_zero) {
@@ -91,6 +93,86 @@ __device__ __noinline__ double z_probit_draw(double e, double sd, double isd, in
   if (code < 0 && noise_zero) return e;
   const double alpha = code < 0 ? -INFINITY : -sg * e * isd;
   return e + sd * sg * trunc_normal_lower(alpha, u);
+}
+
+// Two truncated-normal draws of one Philox block (species 2m and 2m+1 of a site), out of
+// line (the ~60 polynomial coefficients then live in SGPRs only inside the call, instead of
+// being hoisted into the kernel's register file), with their Horner chains interleaved: the
+// same arithmetic as trunc_normal_lower (rng.h) on each cell, two independent dependency
+// chains per lane.  Tails (alpha > 25, or a quantile outside qnorm_fast's central branch,
+// w >= 6.25) take the scalar path.
+struct ZPair {
+  double z0, z1;
+};
+__device__ __forceinline__ ZPair z_probit_pair(double e0, double e1, double sd0, double sd1, double isd0, double isd1,
+                                            int c0, int c1, double u0, double u1, int noise_zero) {
+  const double sg0 = c0 == 0 ? -1.0 : 1.0, sg1 = c1 == 0 ? -1.0 : 1.0;
+  const double al0 = c0 < 0 ? -INFINITY : -sg0 * e0 * isd0;
+  const double al1 = c1 < 0 ? -INFINITY : -sg1 * e1 * isd1;
+  double q0, q1;  // -Phic^-1 (u Phic(alpha)) = qnorm(p), z = e - sd sg q
+  if (al0 > 25.0 || al1 > 25.0) {  // deep tail of either cell: each cell by the scalar inversion
+    q0 = -trunc_normal_lower(al0, u0);
+    q1 = -trunc_normal_lower(al1, u1);
+  } else {
+    // erfc_fast(alpha / sqrt 2) for both cells
+    const double h0 = al0 * 0.7071067811865476, h1 = al1 * 0.7071067811865476;
+    const double a0 = fmin(fabs(h0), 40.0), a1 = fmin(fabs(h1), 40.0);
+    const double t0 = 2.0 * rcp_pos(2.0 + a0), t1 = 2.0 * rcp_pos(2.0 + a1);
+    const double x0 = 2.0 * t0 - 1.0, x1 = 2.0 * t1 - 1.0;
+    double g0 = kErfcPoly[0], g1 = kErfcPoly[0];
+#pragma unroll
+    for (int k = 1; k < 25; ++k) {
+      g0 = fma_sc(g0, x0, kErfcPoly[k]);
+      g1 = fma_sc(g1, x1, kErfcPoly[k]);
+    }
+    const double r0 = t0 * exp(fma(-a0, a0, g0)), r1 = t1 * exp(fma(-a1, a1, g1));
+    const double p0 = u0 * (0.5 * (h0 < 0.0 ? 2.0 - r0 : r0));
+    const double p1 = u1 * (0.5 * (h1 < 0.0 ? 2.0 - r1 : r1));
+    // w = -log_fast(4 p (1 - p)) for both cells, interleaved
+    const double m0 = 4.0 * p0 * (1.0 - p0), m1 = 4.0 * p1 * (1.0 - p1);
+    uint64_t b0, b1;
+    __builtin_memcpy(&b0, &m0, 8);
+    __builtin_memcpy(&b1, &m1, 8);
+    int ex0 = (int)(b0 >> 52) - 1023, ex1 = (int)(b1 >> 52) - 1023;
+    const uint64_t mb0 = (b0 & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull;
+    const uint64_t mb1 = (b1 & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull;
+    double mm0, mm1;
+    __builtin_memcpy(&mm0, &mb0, 8);
+    __builtin_memcpy(&mm1, &mb1, 8);
+    if (mm0 > 1.4142135623730951) mm0 *= 0.5, ex0 += 1;
+    if (mm1 > 1.4142135623730951) mm1 *= 0.5, ex1 += 1;
+    const double f0 = mm0 - 1.0, f1 = mm1 - 1.0;
+    const double s0 = f0 * rcp_pos(2.0 + f0), s1 = f1 * rcp_pos(2.0 + f1);
+    const double v0 = s0 * s0, v1 = s1 * s1;
+    double P0 = kLogSeries[0], P1 = kLogSeries[0];
+#pragma unroll
+    for (int k = 1; k < 10; ++k) {
+      P0 = fma_sc(P0, v0, kLogSeries[k]);
+      P1 = fma_sc(P1, v1, kLogSeries[k]);
+    }
+    const double l0 = fma(s0 * v0, P0, 2.0 * s0), l1 = fma(s1 * v1, P1, 2.0 * s1);
+    const double d0 = (double)ex0, d1 = (double)ex1;
+    const double w0 = -fma(d0, 0.6931471803691238, fma(d0, 1.9082149292705877e-10, l0));
+    const double w1 = -fma(d1, 0.6931471803691238, fma(d1, 1.9082149292705877e-10, l1));
+    if (w0 < 6.25 && w1 < 6.25) {  // qnorm_fast's central branch for both cells
+      const double y0 = w0 - 3.125, y1 = w1 - 3.125;
+      double F0 = kQnormA[0], F1 = kQnormA[0];
+#pragma unroll
+      for (int k = 1; k < 23; ++k) {
+        F0 = fma_sc(F0, y0, kQnormA[k]);
+        F1 = fma_sc(F1, y1, kQnormA[k]);
+      }
+      q0 = (2.0 * p0 - 1.0) * F0;
+      q1 = (2.0 * p1 - 1.0) * F1;
+    } else {
+      q0 = qnorm_fast(p0);
+      q1 = qnorm_fast(p1);
+    }
+  }
+  ZPair z;
+  z.z0 = (c0 < 0 && noise_zero) ? e0 : e0 - sd0 * sg0 * q0;
+  z.z1 = (c1 < 0 && noise_zero) ? e1 : e1 - sd1 * sg1 * q1;
+  return z;
 }
 
 // Poisson cell (R/updateZ.R:65-90): omega ~ PG(y + r, zPrev - log r) with r = 1000, then
@@ -117,7 +199,10 @@ constexpr int ZT_TLD = 17;  // leading dimension of the wave's 16-site x 32-spec
 
 // POIS: instantiated only for chains with Poisson species, so the probit kernel carries no
 // Poisson call site (its call-saved registers and code size cost the probit path ~5 %)
-template <bool DRAW, bool HAS_NA, int NKB, int MODE = Z_ALL, bool POIS = false>
+// NORMAL: the chain has normal species (their cells copy Yval, R/updateZ.R:40-41); a probit-
+// only chain's kernel then issues no load inside the draw loop (a load there would make each
+// use wait, vmcnt being in order, behind every Z store still in flight).
+template <bool DRAW, bool HAS_NA, int NKB, int MODE = Z_ALL, bool POIS = false, bool NORMAL = true>
 __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const unsigned long long kt0 = a.kt ? kt_now() : 0ull;
@@ -130,6 +215,9 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
   double* sIsd = sSd + ZT_J;                        // [32] iSigma^1/2
   int* sFam = (int*)(sIsd + ZT_J);                  // [32]
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, lm = lane & 15, lk = lane >> 4;
+  // the Philox sweep counter, read once (a load inside the site loop would wait, vmcnt(0),
+  // behind every Z store in flight)
+  const uint32_t iter = SWEEP_ITER(a);
   double* sT = (double*)(sFam + ZT_J) + w * (ZT_J * ZT_TLD);  // this wave's tile: E, then Z
   const int j0 = blockIdx.y * ZT_J;
   for (int p = t; p < K16 * ZT_J; p += 256) {
@@ -159,22 +247,39 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
   for (int tile = tb; tile < te; ++tile) {
     const int i0 = tile * ZT_I + 16 * w;
     if (i0 >= ny) break;
+    // ---- this lane's 8 Y codes (site i0 + lm, species j0 + 2(4c + lk) + b), loaded before
+    //      the E contraction so their latency overlaps it; 4 bits each, code + 1
+    uint32_t ycodes = 0;
+    if (DRAW) {
+      const int i = i0 + lm;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int j = j0 + 2 * (4 * c + lk) + b;
+          const int code = a.Ycode[(size_t)i + (size_t)ny * j];  // padded buffer (ZArgs)
+          ycodes |= (uint32_t)(code + 1) << (8 * c + 4 * b);
+        }
+    }
     // ---- E = XEta BL for 16 sites x 32 species (R/updateZ.R:11-34); T[2m+b][lk+4r] <- E
     if (DRAW) {
       d4 e0 = {0.0, 0.0, 0.0, 0.0}, e1 = {0.0, 0.0, 0.0, 0.0};
-      const int i = i0 + lm;
+      // all K16 operand rows, loaded before the first MFMA (padded buffer, ZArgs: rows k >= K
+      // meet zero BL rows), so their latency is paid once per tile
+      const double* xp = a.XEta + (i0 + lm) + (size_t)ny * lk;
+      double xa[K16 / 4];
 #pragma unroll
-      for (int s4 = 0; s4 < K16 / 4; ++s4)
-        if (s4 < K4 / 4) {
-          const int k = 4 * s4 + lk;
-          const double xa = (k < K && i < ny) ? a.XEta[i + (size_t)ny * k] : 0.0;
-          if (MODE & 1) {
-            e0 = mfma_f64(xa, sBL[k * ZT_J + 2 * lm], e0);
-            e1 = mfma_f64(xa, sBL[k * ZT_J + 2 * lm + 1], e1);
-          } else {
-            e0[s4 & 3] += xa;
-          }
+      for (int s4 = 0; s4 < K16 / 4; ++s4) xa[s4] = xp[(size_t)ny * 4 * s4];
+#pragma unroll
+      for (int s4 = 0; s4 < K16 / 4; ++s4) {
+        const int k = 4 * s4 + lk;
+        if (MODE & 1) {
+          e0 = mfma_f64(xa[s4], sBL[k * ZT_J + 2 * lm], e0);
+          e1 = mfma_f64(xa[s4], sBL[k * ZT_J + 2 * lm + 1], e1);
+        } else {
+          e0[s4 & 3] += xa[s4];
         }
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         sT[(2 * lm) * ZT_TLD + lk + 4 * r] = e0[r];
@@ -186,11 +291,33 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
     //      one Philox call per (site, pair); Z stores are 128-B site runs
     {
       const int s = lm, i = i0 + s;
-#pragma unroll 1
+#ifndef Z_CUNROLL
+#define Z_CUNROLL 1
+#endif
+#pragma unroll Z_CUNROLL
       for (int c = 0; c < 4; ++c) {
         const int m = 4 * c + lk, ja = j0 + 2 * m;
         Uniform2 u{0.0, 0.0};
-        if (DRAW) u = uniforms(a.key, (uint32_t)((size_t)i + (size_t)ny * (uint32_t)((a.sp0 + ja) >> 1)), 0, S_Z, SWEEP_ITER(a));
+        if (DRAW) u = uniforms(a.key, (uint32_t)((size_t)i + (size_t)ny * (uint32_t)((a.sp0 + ja) >> 1)), 0, S_Z, iter);
+        if (DRAW && !POIS && (MODE & 2)) {
+          // probit / NA pair (the whole chain is probit, or the pair's species are):
+          // both draws inline with interleaved chains; normal species keep Z = Y
+          const int cd0 = (int)((ycodes >> (8 * c)) & 15u) - 1, cd1 = (int)((ycodes >> (8 * c + 4)) & 15u) - 1;
+          const int jj0 = 2 * m, jj1 = 2 * m + 1;
+          const bool in0 = i < ny && ja < a.ns_loc, in1 = i < ny && ja + 1 < a.ns_loc;
+          const double e0 = sT[jj0 * ZT_TLD + s], e1 = sT[jj1 * ZT_TLD + s];
+          const ZPair zp = z_probit_pair(e0, e1, sSd[jj0], sSd[jj1], sIsd[jj0], sIsd[jj1], cd0, cd1, u.a, u.b, a.noise_zero);
+          double z0 = zp.z0, z1 = zp.z1;
+          if (NORMAL) {  // R/updateZ.R:40-41
+            if (sFam[jj0] == 1 && cd0 >= 0 && in0) z0 = a.Yval[(size_t)i + (size_t)ny * ja];
+            if (sFam[jj1] == 1 && cd1 >= 0 && in1) z1 = a.Yval[(size_t)i + (size_t)ny * (ja + 1)];
+          }
+          if (in0) a.Z[(size_t)i + (size_t)ny * ja] = z0;
+          if (in1) a.Z[(size_t)i + (size_t)ny * (ja + 1)] = z1;
+          sT[jj0 * ZT_TLD + s] = in0 ? z0 : 0.0;
+          sT[jj1 * ZT_TLD + s] = in1 ? z1 : 0.0;
+          continue;
+        }
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
           const int jj = 2 * m + b, j = ja + b;
@@ -205,7 +332,7 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
               else if (POIS && sFam[jj] == 3 && code >= 0)
                 z = z_poisson_draw(e, sSd[jj], a.Yval[cell], a.zprev_is_e ? e : a.Z[cell],
                                    uniforms(a.key, (uint32_t)((size_t)i + (size_t)ny * (uint32_t)(a.sp0 + j)), 0,
-                                            S_ZPOIS, SWEEP_ITER(a)),
+                                            S_ZPOIS, iter),
                                    a.noise_zero);
               else if (MODE & 2)
                 z = z_probit_draw(e, sSd[jj], sIsd[jj], code, b ? u.b : u.a, a.noise_zero);
@@ -241,6 +368,13 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
     // ---- XZ += XEta^T (Yx o Z) over the 16 sites (R/updateBetaLambda.R:66 of the next sweep);
     //      B operand = Z[site lk+4r][species 2lm+b] from the tile
     if (MODE & 4) {
+      // A operands (XEta^T rows) of all 4 x NKB MFMAs loaded first: one latency per tile
+      double xt[4][NKB];
+      const double* xq = a.XEta + (i0 + lk) + (size_t)ny * lm;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < NKB; ++q) xt[r][q] = xq[4 * r + (size_t)ny * 16 * q];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int ir = i0 + 4 * r + lk;
@@ -252,11 +386,9 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
           if (ja + 1 < a.ns_loc && a.Ycode[(size_t)ir + (size_t)ny * (ja + 1)] < 0) z1 = 0.0;
         }
 #pragma unroll
-        for (int q = 0; q < NKB; ++q) {
-          const int k = 16 * q + lm;
-          const double xt = (k < K && ir < ny) ? a.XEta[ir + (size_t)ny * k] : 0.0;
-          acc[q][0] = mfma_f64(xt, z0, acc[q][0]);
-          acc[q][1] = mfma_f64(xt, z1, acc[q][1]);
+        for (int q = 0; q < NKB; ++q) {  // rows >= K are discarded, sites >= ny have Z = 0
+          acc[q][0] = mfma_f64(xt[r][q], z0, acc[q][0]);
+          acc[q][1] = mfma_f64(xt[r][q], z1, acc[q][1]);
         }
       }
     }
@@ -288,7 +420,7 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
                            sR[(2 * K16 + k) * ZT_J + jj];
           if (k < K && j < a.ns_loc) dst[k + (size_t)K * j] = v;
         }
-    if (a.kt && t == 0) kt_record(a.kt, SWEEP_ITER(a), kt0);
+    if (a.kt && t == 0) kt_record(a.kt, iter, kt0);
   }
 }
 

@@ -1,0 +1,124 @@
+// updateZ launcher (R/updateZ.R:4-94): the fused z kernel of z_kernel.h and its slab
+// reductions.  Its own translation unit: it is compiled with MachineLICM off (build.py), so
+// the ~60 polynomial constants of the inlined truncated-normal draws are materialised where
+// they are used inside the site loop instead of being hoisted into (and spilled from) the
+// register file.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "common.h"
+#include "rng.h"
+#include "state.h"
+#include "z_kernel.h"
+
+namespace hmsc {
+
+template <bool DRAW, bool HAS_NA, bool POIS, bool NORMAL>
+static void z_dispatch_k(const State& s, dim3 grid, size_t smem, const ZArgs& a) {
+  switch (z_nkb(s.K)) {
+    case 1: z_wave_kernel<DRAW, HAS_NA, 1, Z_ALL, POIS, NORMAL><<<grid, 256, smem, s.stream>>>(a); break;
+    case 2: z_wave_kernel<DRAW, HAS_NA, 2, Z_ALL, POIS, NORMAL><<<grid, 256, smem, s.stream>>>(a); break;
+    case 3: z_wave_kernel<DRAW, HAS_NA, 3, Z_ALL, POIS, NORMAL><<<grid, 256, smem, s.stream>>>(a); break;
+    default: z_wave_kernel<DRAW, HAS_NA, 4, Z_ALL, POIS, NORMAL><<<grid, 256, smem, s.stream>>>(a); break;
+  }
+}
+
+template <bool DRAW, bool HAS_NA, bool POIS = false>
+static void z_dispatch(const State& s, dim3 grid, size_t smem, const ZArgs& a) {
+  if (!DRAW || POIS || s.any_normal)
+    z_dispatch_k<DRAW, HAS_NA, POIS, true>(s, grid, smem, a);
+  else
+    z_dispatch_k<DRAW, HAS_NA, POIS, false>(s, grid, smem, a);
+}
+
+template <bool HAS_NA>
+static int z_occupancy(int nkb, size_t smem) {
+  int nb = 0;
+  switch (nkb) {
+    case 1: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 1>, 256, smem)); break;
+    case 2: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 2>, 256, smem)); break;
+    case 3: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 3>, 256, smem)); break;
+    default: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 4>, 256, smem)); break;
+  }
+  return nb;
+}
+
+// Workgroups of the drawing z kernel resident on the whole device at once (occupancy x CUs):
+// the site-chunk count is sized so the (chunk x species-block) grid fills exactly one round.
+int z_resident_slots(const State& s) {
+  const size_t smem = z_smem_bytes(s.Kmax, s.nt);
+  const int nkb = z_nkb(s.Kmax);
+  int ncu = 0;
+  const int nb = s.has_na ? z_occupancy<true>(nkb, smem) : z_occupancy<false>(nkb, smem);
+  HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, s.device));
+  return std::max(1, nb) * std::max(1, ncu);
+}
+
+static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
+  HMSC_REQUIRE(s.K <= KMAX_Z, "updateZ: K = nc + sum(nf) must be <= 64 in this build");
+  HMSC_REQUIRE((s.sp0 & 1) == 0, "updateZ: species shards must start at an even species (Philox pairs)");
+  if (!s.xeta_valid) launch_xeta(s);
+  ZArgs a{};
+  a.XEta = s.XEta;
+  a.ny = s.ny;
+  a.K = s.K;
+  a.ns_loc = s.nsl;
+  a.sp0 = s.sp0;
+  a.nt = s.nt;
+  const int n_tiles = (s.ny + ZT_I - 1) / ZT_I;
+  a.tiles_per_chunk = (n_tiles + s.nchunk - 1) / s.nchunk;
+  const int nchunk = (n_tiles + a.tiles_per_chunk - 1) / a.tiles_per_chunk;
+  a.BL = s.BL;
+  a.iSigma = s.iSigma;
+  a.Ycode = s.Ycode;
+  a.Yval = use_raw_y ? s.Yraw : s.Yval;
+  a.fam = s.fam;
+  a.Tr = s.Tr;
+  a.Z = s.Z;
+  a.XZ_part = s.XZ_part;
+  a.ZTr_part = s.ZTr_part;
+  a.key = s.key;
+  a.iter = iter;
+  a.iter_dev = s.capturing ? s.d_iter : nullptr;
+  a.noise_zero = s.noise_mode;
+  a.zprev_is_e = use_raw_y;  // only the init draw reads hM$Y (R/computeInitialParameters.R:254)
+  a.kt = s.kt_on ? s.d_kt + (size_t)KT_Z * 2 * KT_SLOTS : nullptr;
+  dim3 grid(nchunk, s.ntile_j);
+  const size_t smem = z_smem_bytes(s.K, s.nt);
+  {
+    ProfScope ps(s, PROF_Z);
+    if (draw && s.any_poisson) {
+      if (s.has_na)
+        z_dispatch<true, true, true>(s, grid, smem, a);
+      else
+        z_dispatch<true, false, true>(s, grid, smem, a);
+    } else if (draw) {
+      if (s.has_na)
+        z_dispatch<true, true>(s, grid, smem, a);
+      else
+        z_dispatch<true, false>(s, grid, smem, a);
+    } else {
+      if (s.has_na)
+        z_dispatch<false, true>(s, grid, smem, a);
+      else
+        z_dispatch<false, false>(s, grid, smem, a);
+    }
+    HIP_OK(hipGetLastError());
+  }
+  // XZ and ZTr from their partials, one launch
+  const int64_t nXZ = (int64_t)s.K * s.nsl, nZT = (int64_t)s.ny * s.nt;
+  launch_slab_sum2(s.XZ_part, s.XZ, nXZ, nchunk, s.ZTr_part, s.ZTr, nZT, s.ntile_j, s.stream);
+}
+
+void launch_update_z(State& s, uint32_t iter, bool use_raw_y) {
+  run_z_fused(s, true, iter, use_raw_y);
+  s.zt_valid = true;
+}
+
+void launch_zt_refresh(State& s) {
+  run_z_fused(s, false, 0, false);
+  s.zt_valid = true;
+}
+
+}  // namespace hmsc

@@ -13,10 +13,10 @@ float run(const ZArgs& a, dim3 grid, size_t smem, int reps) {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
-  z_wave_kernel<true, false, 2, MODE><<<grid, 256, smem>>>(a);
+  z_wave_kernel<true, false, 2, MODE, false, false><<<grid, 256, smem>>>(a);
   (void)hipDeviceSynchronize();
   (void)hipEventRecord(e0);
-  for (int i = 0; i < reps; ++i) z_wave_kernel<true, false, 2, MODE><<<grid, 256, smem>>>(a);
+  for (int i = 0; i < reps; ++i) z_wave_kernel<true, false, 2, MODE, false, false><<<grid, 256, smem>>>(a);
   (void)hipEventRecord(e1);
   (void)hipEventSynchronize(e1);
   float ms;
@@ -24,7 +24,8 @@ float run(const ZArgs& a, dim3 grid, size_t smem, int reps) {
   return 1e3f * ms / reps;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const bool prof_only = argc > 1;
   const int ny = 10000, ns = 1000, K = 30, nt = 1;
   std::vector<double> hX((size_t)ny * K), hBL((size_t)K * ns), hTr(ns, 1.0), hIs(ns, 1.0);
   std::vector<int8_t> hY((size_t)ny * ns);
@@ -60,9 +61,12 @@ int main() {
   (void)hipMemcpy(Is, hIs.data(), ns * 8, hipMemcpyHostToDevice);
   (void)hipMemcpy(Y, hY.data(), hY.size(), hipMemcpyHostToDevice);
   (void)hipMemcpy(F, hF.data(), ns * 4, hipMemcpyHostToDevice);
+  uint32_t* dIter;
+  (void)hipMalloc(&dIter, 4);
+  { const uint32_t three = 3; (void)hipMemcpy(dIter, &three, 4, hipMemcpyHostToDevice); }
   const size_t smem = z_smem_bytes(K, nt);
   int nb = 0, ncu = 0;
-  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, false, 2, Z_ALL>, 256, smem);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, false, 2, Z_ALL, false, false>, 256, smem);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
   printf("occupancy %d blocks/CU, %d CUs, smem %zu B\n", nb, ncu, smem);
   for (int nchunk_req : {nb * ncu / ntile_j, 2 * nb * ncu / ntile_j, n_tiles}) {
@@ -72,8 +76,13 @@ int main() {
     const int nchunk = (n_tiles + a.tiles_per_chunk - 1) / a.tiles_per_chunk;
     a.BL = BL; a.iSigma = Is; a.Ycode = Y; a.Yval = nullptr; a.fam = F; a.Tr = Tr; a.Z = Z;
     a.XZ_part = XZp; a.ZTr_part = ZTrp; a.key = Key{7u, 9u}; a.iter = 3; a.noise_zero = 0;
+    a.iter_dev = dIter;  // as in the product's graph replays
     dim3 grid(nchunk, ntile_j);
     printf("grid %d x %d (tiles/chunk %d)\n", nchunk, ntile_j, a.tiles_per_chunk);
+    if (prof_only) {
+      printf("  all                 %7.1f us\n", run<15>(a, grid, smem, 20));
+      return 0;
+    }
     printf("  all                 %7.1f us\n", run<15>(a, grid, smem, 20));
     printf("  no E mfma           %7.1f us\n", run<14>(a, grid, smem, 20));
     printf("  no draw             %7.1f us\n", run<13>(a, grid, smem, 20));
@@ -81,6 +90,12 @@ int main() {
     printf("  no ZTr              %7.1f us\n", run<7>(a, grid, smem, 20));
     printf("  draw only (E VALU)  %7.1f us\n", run<2>(a, grid, smem, 20));
     printf("  nothing             %7.1f us\n", run<0>(a, grid, smem, 20));
+    run<15>(a, grid, smem, 1);
+    std::vector<double> hz((size_t)ny * ns);
+    (void)hipMemcpy(hz.data(), Z, hz.size() * 8, hipMemcpyDeviceToHost);
+    double cs = 0, ca = 0;
+    for (size_t q = 0; q < hz.size(); ++q) cs += hz[q], ca += std::fabs(hz[q]) * (1 + (q % 7));
+    printf("  checksum Z %.15e %.15e  z[12345] %.17g\n", cs, ca, hz[12345]);
   }
   return 0;
 }
