@@ -105,3 +105,13 @@ def rel_err(a, b):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
     return float(np.max(np.abs(a - b)) / max(1e-300, np.max(np.abs(b))))
+
+
+def rel_err_elem(a, b, floor=1e-3):
+    """Elementwise relative error max_i |a_i - b_i| / max(|b_i|, floor * max|b|): unlike the
+    normwise rel_err, a small entry cannot hide a large relative error (entries below
+    floor * max|b| are measured against that floor)."""
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    scale = np.maximum(np.abs(b), floor * max(1e-300, float(np.max(np.abs(b)))))
+    return float(np.max(np.abs(a - b) / scale))

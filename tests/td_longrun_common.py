@@ -68,3 +68,44 @@ def pooled(means, variances, ess):
     n = means.shape[0]
     se = np.sqrt(np.sum(variances / np.maximum(ess, 1.0), axis=0)) / n
     return means.mean(0), se
+
+
+def reference_rows(hM, postList):
+    """The reference's stored TD$m$postList (combineParameters output: original X / Tr
+    scale, R/combineParameters.R:1-58) mapped back to the sampler's scaled parameterisation,
+    one (S, P) row block per chain: the inverse of combineParameters' un-scaling."""
+    XS, TS = hM.XScalePar, hM.TrScalePar
+    XI, TI = hM.XInterceptInd - 1, hM.TrInterceptInd - 1
+    out = []
+    for ch in postList:
+        Bs, Gs, iVs = [], [], []
+        for s in ch:
+            B, G, V = (np.array(s[k], dtype=np.float64) for k in ("Beta", "Gamma", "V"))
+            for k in range(hM.nc):                       # undo :12-26 (X scaling)
+                m, sd = XS[0, k], XS[1, k]
+                if m != 0 or sd != 1:
+                    B[XI] += m * B[k]
+                    G[XI] += m * G[k]
+                    B[k] *= sd
+                    G[k] *= sd
+                    V[k, :] *= sd
+                    V[:, k] *= sd
+            for p in range(hM.nt):                       # undo :2-10 (Tr scaling)
+                m, sd = TS[0, p], TS[1, p]
+                if m != 0 or sd != 1:
+                    G[:, TI] += m * G[:, p]
+                    G[:, p] *= sd
+            Bs.append(B), Gs.append(G), iVs.append(np.linalg.inv(V))
+        rho_idx = np.array([int(np.argmin(np.abs(np.asarray(hM.rhopw)[:, 0] - s["rho"]))) + 1 for s in ch])
+        lams = [np.stack([np.asarray(s["Lambda"][r]) for s in ch]) for r in range(hM.nr)]
+        alphas = [np.stack([np.asarray(s["Alpha"][r]).ravel() for s in ch]).astype(np.int64) for r in range(hM.nr)]
+        out.append(param_rows(hM, np.stack(Bs), np.stack(Gs), np.stack(iVs), rho_idx, lams, alphas))
+    return out
+
+
+def between_chain_t(means_a, means_b):
+    """Welch t of two sets of independent chain means (per statistic): the standard error
+    comes from the spread of the chain means themselves, which needs no ESS estimate."""
+    na, nb = means_a.shape[0], means_b.shape[0]
+    se = np.sqrt(means_a.var(0, ddof=1) / na + means_b.var(0, ddof=1) / nb)
+    return (means_a.mean(0) - means_b.mean(0)) / np.maximum(se, 1e-300)
