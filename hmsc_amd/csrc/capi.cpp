@@ -29,6 +29,11 @@ struct hmsc_state {
 namespace hmsc {
 
 static thread_local std::string g_last_error;
+// Chains may live on concurrent host threads (sampleMcmc nParallel, one stream each).  A
+// stream capture must not overlap another thread's device-wide synchronising calls
+// (hipMalloc / hipFree / hipDeviceSynchronize): those would invalidate it.  Captures,
+// chain construction / destruction and every other allocation take this lock.
+static std::recursive_mutex g_dev_mu;
 static constexpr int RING_SLOTS = 32;  // recorded samples in flight between device and host
 
 static int fail(int code, const std::string& msg) {
@@ -139,7 +144,18 @@ static void d2h(T* h, const T* d, size_t n, hipStream_t st) {
 void allreduce_sum(State& s, double* buf, size_t n, hipStream_t st = nullptr);
 void allreduce_sum(State& s, double* buf, size_t n, hipStream_t st) {
   if (s.nranks <= 1) return;
-  const ncclResult_t r = ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, (ncclComm_t)s.comm, st ? st : s.stream);
+  hipStream_t q = st ? st : s.stream;
+  if (s.host_allreduce) {  // host transport: device -> host, caller's sum over ranks, back
+    s.host_ar_buf.resize(n);
+    HIP_OK(hipMemcpyAsync(s.host_ar_buf.data(), buf, n * sizeof(double), hipMemcpyDeviceToHost, q));
+    HIP_OK(hipStreamSynchronize(q));
+    HMSC_REQUIRE(s.host_allreduce(s.host_ar_buf.data(), (int64_t)n, s.host_allreduce_ctx) == 0,
+                 "host all-reduce callback failed");
+    HIP_OK(hipMemcpyAsync(buf, s.host_ar_buf.data(), n * sizeof(double), hipMemcpyHostToDevice, q));
+    HIP_OK(hipStreamSynchronize(q));
+    return;
+  }
+  const ncclResult_t r = ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, (ncclComm_t)s.comm, q);
   HMSC_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
 }
 
@@ -191,8 +207,21 @@ static void setup_phylo(State& s, const hmsc_model* m) {
 }
 
 // ---------------------------- create ----------------------------
+// Species shard of `rank`: blocks of an even number of species (updateZ draws species pairs
+// 2m, 2m+1 from one Philox block), per = 2 ceil(ceil(ns / 2) / nranks); the last shard takes
+// the remainder.  Returns -1 if this rank's shard is empty.
+static int shard_range(int ns, int rank, int nranks, int* sp0, int* nsl) {
+  const int pairs = (ns + 1) / 2;
+  const int per = 2 * ((pairs + nranks - 1) / nranks);
+  *sp0 = std::min(ns, rank * per);
+  *nsl = std::min(ns, *sp0 + per) - *sp0;
+  return *nsl > 0 ? 0 : -1;
+}
+
 static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device, uint32_t mask, int rank,
-                        int nranks, const void* comm_id) {
+                        int nranks, const void* comm_id, hmsc_allreduce_fn host_fn = nullptr,
+                        void* host_ctx = nullptr) {
+  std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
   HMSC_REQUIRE(m != nullptr, "model is NULL");
   HMSC_REQUIRE(m->ny > 0 && m->ns > 0 && m->nc >= 0 && m->nt > 0, "bad dimensions");
   HMSC_REQUIRE(m->nr >= 0 && m->nr <= HMSC_MAX_LEVELS, "nr out of range");
@@ -209,10 +238,8 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.f0 = m->f0;
   // species shards start at even species: updateZ draws the species pair (2m, 2m+1) from one
   // Philox call (kernels.hip, z_wave_kernel)
-  const int per = (((m->ns + nranks - 1) / nranks) + 1) & ~1;
-  s.sp0 = std::min(m->ns, rank * per);
-  s.nsl = std::min(m->ns, s.sp0 + per) - s.sp0;
-  HMSC_REQUIRE(s.nsl > 0, "species shard is empty (more ranks than species)");
+  HMSC_REQUIRE(shard_range(m->ns, rank, nranks, &s.sp0, &s.nsl) == 0,
+               "species shard is empty: a sharded chain needs at least 2 species per rank (shards start at even species)");
   DeviceGuard dg(device);
   HIP_OK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&s.copy_stream, hipStreamNonBlocking));
@@ -221,7 +248,9 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   HIP_OK(hipEventCreateWithFlags(&s.ev_bl, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&s.ev_side, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&s.ev_side2, hipEventDisableTiming));
-  if (nranks > 1) {
+  s.host_allreduce = host_fn;
+  s.host_allreduce_ctx = host_ctx;
+  if (nranks > 1 && host_fn == nullptr) {
     HMSC_REQUIRE(comm_id != nullptr, "sharded chain needs an RCCL unique id");
     ncclUniqueId id;
     std::memcpy(&id, comm_id, sizeof(id));
@@ -490,6 +519,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
 }
 
 static void free_state(State& s) {
+  std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
   DeviceGuard dg(s.device);
   (void)hipDeviceSynchronize();
   void* ptrs[] = {s.X, s.Tr, s.Yval, s.Yraw, s.Ycode, s.fam, s.varest, s.V0, s.iUGamma, s.mGamma, s.UGammaL,
@@ -585,6 +615,17 @@ static void set_state(State& s, const hmsc_params* p) {
   DeviceGuard dg(s.device);
   join_side(s);
   HIP_OK(hipStreamSynchronize(s.stream));
+  // the device holds BL / Psi / Delta in the current layout (K, NF and the per-level row
+  // offsets); read them in that layout, then remap every level's rows to the new nf (rows a
+  // level gains: Lambda 0, Psi 1, Delta 1) before the supplied fields are applied
+  const int K0 = s.K, NF0 = s.NF, nsl = s.nsl, nc = s.nc;
+  std::vector<int> lo0(s.nr), fo0(s.nr), nf0(s.nr);
+  for (int r = 0; r < s.nr; ++r) lo0[r] = s.loff(r), fo0[r] = s.foff(r), nf0[r] = s.lev[r].nf;
+  std::vector<double> BL0((size_t)K0 * nsl), Psi0((size_t)std::max(1, NF0) * nsl), Delta0(std::max(1, NF0));
+  d2h(BL0.data(), s.BL, BL0.size(), s.stream);
+  d2h(Psi0.data(), s.Psi, (size_t)NF0 * nsl, s.stream);
+  d2h(Delta0.data(), s.Delta, NF0, s.stream);
+  HIP_OK(hipStreamSynchronize(s.stream));
   for (int r = 0; r < s.nr; ++r) {
     if (p->nf[r] > 0) {
       HMSC_REQUIRE(p->nf[r] <= std::min(s.lev[r].nfmax, s.NFmax), "set_state: nf exceeds allocation");
@@ -593,12 +634,20 @@ static void set_state(State& s, const hmsc_params* p) {
   }
   s.refresh_dims();
   HMSC_REQUIRE(s.K <= s.Kmax, "set_state: K exceeds 64");
-  const int K = s.K, nsl = s.nsl, nc = s.nc;
-  std::vector<double> BL((size_t)K * nsl), Psi((size_t)std::max(1, s.NF) * nsl), Delta(std::max(1, s.NF));
-  d2h(BL.data(), s.BL, BL.size(), s.stream);
-  d2h(Psi.data(), s.Psi, (size_t)s.NF * nsl, s.stream);
-  d2h(Delta.data(), s.Delta, s.NF, s.stream);
-  HIP_OK(hipStreamSynchronize(s.stream));
+  const int K = s.K;
+  std::vector<double> BL((size_t)K * nsl, 0.0), Psi((size_t)std::max(1, s.NF) * nsl, 1.0), Delta(std::max(1, s.NF), 1.0);
+  for (int j = 0; j < nsl; ++j)
+    for (int c = 0; c < nc; ++c) BL[c + (size_t)K * j] = BL0[c + (size_t)K0 * j];
+  for (int r = 0; r < s.nr; ++r) {
+    const int keep = std::min(nf0[r], s.lev[r].nf), lo = s.loff(r), fo = s.foff(r);
+    for (int h = 0; h < keep; ++h) {
+      for (int j = 0; j < nsl; ++j) {
+        BL[lo + h + (size_t)K * j] = BL0[lo0[r] + h + (size_t)K0 * j];
+        Psi[fo + h + (size_t)s.NF * j] = Psi0[fo0[r] + h + (size_t)NF0 * j];
+      }
+      Delta[fo + h] = Delta0[fo0[r] + h];
+    }
+  }
   if (p->Beta)
     for (int j = 0; j < nsl; ++j)
       for (int c = 0; c < nc; ++c) BL[c + (size_t)K * j] = p->Beta[c + (size_t)nc * j];
@@ -872,6 +921,7 @@ static void destroy_graph(State& s) {
 // nullptr when the sweep is not in a steady state, i.e. the host-side validity flags it
 // changes would differ on the next sweep.
 static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record) {
+  std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
   join_side(s);
   const bool xv = s.xeta_valid, zv = s.zt_valid, gv = s.g2prep_valid;
   hipGraph_t g = nullptr;
@@ -1167,7 +1217,18 @@ const char* hmsc_last_error(void) { return g_last_error.c_str(); }
 int hmsc_predict(const hmsc_predict_args* args, double* out) {
   return guarded([&] {
     HMSC_REQUIRE(args != nullptr && out != nullptr, "hmsc_predict: NULL argument");
+    std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);  // it allocates (predict.hip)
     run_predict(args, out);
+  });
+}
+
+int hmsc_shard_range(int32_t ns, int32_t rank, int32_t nranks, int32_t* sp0, int32_t* nsl) {
+  return guarded([&] {
+    HMSC_REQUIRE(ns > 0 && nranks >= 1 && rank >= 0 && rank < nranks, "bad ns / rank / nranks");
+    int a = 0, b = 0;
+    HMSC_REQUIRE(shard_range(ns, rank, nranks, &a, &b) == 0, "species shard is empty: fewer than 2 species per rank");
+    *sp0 = a;
+    *nsl = b;
   });
 }
 
@@ -1197,6 +1258,23 @@ int hmsc_create_sharded(const hmsc_model* model, uint64_t seed, int32_t device, 
     auto* h = new hmsc_state();
     try {
       build_state(h->s, model, seed, device, updater_mask, rank, nranks, comm_id);
+    } catch (...) {
+      free_state(h->s);
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+int hmsc_create_sharded_host(const hmsc_model* model, uint64_t seed, int32_t device, uint32_t updater_mask,
+                             int32_t rank, int32_t nranks, hmsc_allreduce_fn fn, void* ctx, hmsc_state** out) {
+  return guarded([&] {
+    HMSC_REQUIRE(out != nullptr && fn != nullptr, "out / fn is NULL");
+    HMSC_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank / nranks");
+    auto* h = new hmsc_state();
+    try {
+      build_state(h->s, model, seed, device, updater_mask, rank, nranks, nullptr, fn, ctx);
     } catch (...) {
       free_state(h->s);
       delete h;
@@ -1240,6 +1318,17 @@ int hmsc_init_state(hmsc_state* h, const int32_t* nf0) {
   });
 }
 
+int hmsc_init_z(hmsc_state* h) {
+  return guarded([&] {
+    State& s = h->s;
+    DeviceGuard dg(s.device);
+    join_side(s);
+    s.graph_dirty = true;
+    launch_update_z(s, 0, true);  // R/computeInitialParameters.R:254 (iter 0: the init stream)
+    HIP_OK(hipStreamSynchronize(s.stream));
+  });
+}
+
 int hmsc_set_state(hmsc_state* h, const hmsc_params* p) {
   return guarded([&] { set_state(h->s, p); });
 }
@@ -1274,6 +1363,7 @@ int hmsc_set_noise_mode(hmsc_state* h, int32_t mode) {
     DeviceGuard dg(s.device);
     s.noise_mode = mode & 1;
     s.graph_dirty = true;
+    std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
     if ((mode & 2) && !s.dbg_prec) s.dbg_prec = dalloc<double>((size_t)s.nsl * s.Kmax * s.Kmax);
     if (!(mode & 2) && s.dbg_prec) {
       HIP_OK(hipStreamSynchronize(s.stream));
@@ -1372,7 +1462,10 @@ int hmsc_kernel_timing(hmsc_state* h, int32_t enable) {
     DeviceGuard dg(s.device);
     join_side(s);
     HIP_OK(hipStreamSynchronize(s.stream));
-    if (enable && !s.d_kt) s.d_kt = dalloc<unsigned long long>((size_t)KT_N * 2 * KT_SLOTS);
+    if (enable && !s.d_kt) {
+      std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
+      s.d_kt = dalloc<unsigned long long>((size_t)KT_N * 2 * KT_SLOTS);
+    }
     if (enable)
       for (int id = 0; id < KT_N; ++id) {
         unsigned long long* b = s.d_kt + (size_t)id * 2 * KT_SLOTS;

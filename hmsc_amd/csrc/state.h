@@ -174,9 +174,12 @@ struct State {
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[8];
 
-  // RCCL (species-sharded chain)
+  // RCCL (species-sharded chain), or a host transport (hmsc_create_sharded_host)
   void* comm = nullptr;
   double* allreduce_buf = nullptr;
+  hmsc_allreduce_fn host_allreduce = nullptr;
+  void* host_allreduce_ctx = nullptr;
+  std::vector<double> host_ar_buf;
 
   std::vector<int> h_nf() const {
     std::vector<int> v(nr);

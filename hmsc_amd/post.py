@@ -23,20 +23,20 @@ def poolMcmcChains(postList, start=1, thin=1):
     return out
 
 
-def convertToCodaObject(hM, start=1, spNamesNumbers=(True, False), covNamesNumbers=(True, False),
-                        trNamesNumbers=(True, False), Beta=True, Gamma=True, V=True, Sigma=True, Rho=True,
-                        Eta=True, Lambda=True, Omega=True, Psi=True, Delta=True):
-    def nm(names, numbers, prefix):
+def convertToCodaObject(hM, start=1, spNamesNumbers=(True, True), covNamesNumbers=(True, True),
+                        trNamesNumbers=(True, True), Beta=True, Gamma=True, V=True, Sigma=True, Rho=True,
+                        Eta=True, Lambda=True, Alpha=True, Omega=True, Psi=True, Delta=True):
+    """R/convertToCodaObject.r:36-290: per chain, one (samples, P) matrix per parameter and
+    its column names (the coda mcmc.list layout)."""
+    def nm(names, numbers, prefix):                                        # :54-92
         res = []
         for k, n in enumerate(names):
-            if numbers[0] and numbers[1]:
-                res.append(f"{n} ({prefix}{k + 1})")
-            elif numbers[0]:
-                res.append(f"{n} ({prefix}{k + 1})")
-            elif numbers[1]:
-                res.append(f"{prefix}{k + 1}")
-            else:
-                res.append(n)
+            parts = []
+            if numbers[0]:
+                parts.append(str(n))
+            if numbers[1]:
+                parts.append(f"({prefix}{k + 1})")
+            res.append(" ".join(parts))
         return res
 
     sp = nm(hM.spNames, spNamesNumbers, "S")
@@ -60,28 +60,49 @@ def convertToCodaObject(hM, start=1, spNamesNumbers=(True, False), covNamesNumbe
         out["Rho"] = [np.array([[s["rho"]] for s in c]) for c in chains]
         cols["Rho"] = ["Rho"]
     for r in range(hM.nr):
-        lvl = hM.rLNames[r]
         nfMax = max(c[0]["Lambda"][r].shape[0] for c in chains)
-        if Lambda:                                                          # :174-178 as.vector(t(Lambda))
+        if Eta:                                                             # :171-176
+            units = list(_levels(hM.dfPi[hM.rLNames[r]])) if hM.dfPi is not None else \
+                [str(q + 1) for q in range(int(hM.np[r]))]
+            out.setdefault("Eta", []).append(
+                [np.stack([_pad_cols(s["Eta"][r], nfMax).reshape(-1, order="F") for s in c]) for c in chains])
+            cols.setdefault("Eta", []).append(
+                [f"Eta{r + 1}[{u}, factor{h + 1}]" for h in range(nfMax) for u in units])
+        if Lambda:                                                          # :178-183 as.vector(t(Lambda))
             out.setdefault("Lambda", []).append(
                 [np.stack([_pad_rows(s["Lambda"][r], nfMax).T.reshape(-1, order="F") for s in c]) for c in chains])
             cols.setdefault("Lambda", []).append(
                 [f"Lambda{r + 1}[{s}, factor{h + 1}]" for h in range(nfMax) for s in sp])
-        if Omega:                                                           # :186-190 crossprod(Lambda)
+        if Omega:                                                           # :184-188 crossprod(Lambda)
             out.setdefault("Omega", []).append(
                 [np.stack([(s["Lambda"][r].T @ s["Lambda"][r]).reshape(-1, order="F") for s in c]) for c in chains])
             cols.setdefault("Omega", []).append([f"Omega{r + 1}[{a}, {b}]" for b in sp for a in sp])
-        if Eta:
-            out.setdefault("Eta", []).append(
-                [np.stack([_pad_cols(s["Eta"][r], nfMax).reshape(-1, order="F") for s in c]) for c in chains])
-        if Psi:
+        if Alpha:                                                           # :189-195 alphapw[Alpha, 1], 0-padded
+            apw = np.asarray(hM.rL[r].alphapw)[:, 0] if hM.rL[r].sDim else None
+            rows = []
+            for c in chains:
+                m = np.zeros((len(c), nfMax))
+                for k, smp in enumerate(c):
+                    a = np.asarray(smp["Alpha"][r], dtype=np.int64).ravel()
+                    m[k, :len(a)] = apw[a - 1] if apw is not None else 0.0
+                rows.append(m)
+            out.setdefault("Alpha", []).append(rows)
+            cols.setdefault("Alpha", []).append([f"Alpha{r + 1}[factor{h + 1}]" for h in range(nfMax)])
+        if Psi:                                                             # :197-203
             out.setdefault("Psi", []).append(
                 [np.stack([_pad_rows(s["Psi"][r], nfMax).T.reshape(-1, order="F") for s in c]) for c in chains])
-        if Delta:
+            cols.setdefault("Psi", []).append([f"Psi{r + 1}[{s}, factor{h + 1}]" for h in range(nfMax) for s in sp])
+        if Delta:                                                           # :205-210 0-padded
             out.setdefault("Delta", []).append(
-                [np.stack([_pad_rows(s["Delta"][r], nfMax, fill=1.0).reshape(-1) for s in c]) for c in chains])
-        _ = lvl
+                [np.stack([_pad_rows(s["Delta"][r], nfMax, fill=0.0).reshape(-1) for s in c]) for c in chains])
+            cols.setdefault("Delta", []).append([f"Delta{r + 1}[factor{h + 1}]" for h in range(nfMax)])
     return out, cols
+
+
+def _levels(col):
+    """levels(hM$dfPi[, r]): the rule hM$Pi was built with (model._factor_levels)."""
+    from .model import _factor_levels
+    return [str(v) for v in _factor_levels(col)]
 
 
 def _pad_rows(a, n, fill=0.0):

@@ -238,8 +238,11 @@ def _conditional_etas(hM, post, X, studyDesign, Yc, mcmcStep, rng, device):
             L = X @ sam["Beta"]
             for r in range(hM.nr):
                 L = L + etas[r][hMc.Pi[:, r] - 1] @ sam["Lambda"][r]
+            # the sample's spatial scales condition the spatial levels' updateEta prior
+            # (R/predict.R:185 passes Alpha = sam$Alpha)
             ch.set_state(dict(Beta=sam["Beta"], sigma=np.asarray(sam["sigma"]), Eta=etas,
-                              Lambda=[np.asarray(lm) for lm in sam["Lambda"]], Z=L))
+                              Lambda=[np.asarray(lm) for lm in sam["Lambda"]], Z=L,
+                              Alpha=[np.asarray(a, dtype=np.int64).ravel() for a in sam["Alpha"]]))
             it = 1 + k * (2 * mcmcStep + 1)
             ch.update("Z", it)
             for m in range(mcmcStep):
@@ -278,12 +281,22 @@ def computePredictedValues(hM, partition=None, start=1, thin=1, Yc=None, mcmcSte
         train, val = partition != k, partition == k
         sd = None if hM.studyDesign is None else hM.studyDesign.loc[train].reset_index(drop=True)
         rl = {name: hM.ranLevels[name] for name in hM.rLNames} if hM.nr else None
-        yscaled = bool(np.any(np.asarray(hM.YScalePar) != np.array([[0.0], [1.0]])))
-        hM1 = Hmsc(Y=hM.Y[train], X=hM.X[train], XScale=True, YScale=yscaled, Tr=hM.Tr, distr=hM.distr, C=hM.C,
+        hM1 = Hmsc(Y=hM.Y[train], X=hM.X[train], Tr=hM.Tr, distr=hM.distr, C=hM.C,               # :92
                    studyDesign=sd, ranLevels=rl, covNames=list(hM.covNames), spNames=list(hM.spNames))
-        hM1.V0, hM1.f0, hM1.mGamma, hM1.UGamma = hM.V0, hM.f0, hM.mGamma, hM.UGamma
-        hM1 = sampleMcmc(hM1, samples=hM.samples, thin=hM.thin, transient=hM.transient, nChains=nChains,
-                         updater=updater, initPar=initPar, verbose=0)
+        # :93-94 calls setPriors(hM1, V0 = hM$V0, ...) without assigning its result, so the
+        # refit keeps Hmsc()'s default priors (the random levels' priors travel with ranLevels);
+        # the scalings are the full model's (:95-116)
+        hM1.YScalePar = hM.YScalePar
+        hM1.YScaled = (hM1.Y - hM1.YScalePar[0][None, :]) / hM1.YScalePar[1][None, :]
+        hM1.XInterceptInd = hM.XInterceptInd
+        hM1.XScalePar = hM.XScalePar
+        hM1.XScaled = (np.asarray(hM1.X, dtype=np.float64) - hM1.XScalePar[0][None, :]) / hM1.XScalePar[1][None, :]
+        hM1.TrInterceptInd = hM.TrInterceptInd
+        hM1.TrScalePar = hM.TrScalePar
+        hM1.TrScaled = (np.asarray(hM1.Tr, dtype=np.float64) - hM1.TrScalePar[0][None, :]) / hM1.TrScalePar[1][None, :]
+        hM1 = sampleMcmc(hM1, samples=hM.samples, thin=hM.thin, transient=hM.transient, nChains=nChains,      # :117
+                         adaptNf=getattr(hM, "adaptNf", None), updater=updater, initPar=initPar, verbose=0,
+                         nParallel=nParallel)
         post = poolMcmcChains(hM1.postList, start=start)
         sdv = None if hM.studyDesign is None else hM.studyDesign.loc[val].reset_index(drop=True)
         pred = predict(hM1, post=post, X=hM.X[val], studyDesign=sdv, Yc=None if Yc is None else np.asarray(Yc)[val],

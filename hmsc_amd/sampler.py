@@ -107,16 +107,38 @@ def updater_mask(updater):
     return mask
 
 
+def shard_range(ns, rank, nranks):
+    """(sp0, nsl): the species block of `rank` in a species-sharded chain (hmsc_shard_range,
+    the one formula the C library also uses)."""
+    a = np.zeros(1, dtype=np.int32)
+    b = np.zeros(1, dtype=np.int32)
+    L.check(L.lib().hmsc_shard_range(int(ns), int(rank), int(nranks), L.iptr(a), L.iptr(b)))
+    return int(a[0]), int(b[0])
+
+
 class Chain:
     """One chain's device-resident state (hmsc_create ... hmsc_destroy)."""
 
-    def __init__(self, hM, seed, device=0, updater=None, rank=0, nranks=1, comm_id=None, mask=None):
+    def __init__(self, hM, seed, device=0, updater=None, rank=0, nranks=1, comm_id=None, mask=None,
+                 host_allreduce=None):
+        """host_allreduce: for a species-sharded chain without RCCL, a callable f(x) that
+        replaces the float64 array x by its sum over all ranks, in place (hmsc_create_sharded_host)."""
         self.hM = hM
         self.lib = L.lib()
         self.buf = ModelBuffers(hM)
         self.mask = updater_mask(updater) if mask is None else mask
         h = C.c_void_p()
-        if nranks > 1:
+        if nranks > 1 and host_allreduce is not None:
+            def _cb(ptr, n, ctx):
+                try:
+                    host_allreduce(np.ctypeslib.as_array(ptr, shape=(int(n),)))
+                    return 0
+                except Exception:  # reported by the library as a failed callback
+                    return -1
+            self._ar_cb = L.ALLREDUCE_FN(_cb)
+            L.check(self.lib.hmsc_create_sharded_host(C.byref(self.buf.struct), C.c_uint64(int(seed)), device,
+                                                      self.mask, rank, nranks, self._ar_cb, None, C.byref(h)))
+        elif nranks > 1:
             cid = C.create_string_buffer(bytes(comm_id), 128)
             L.check(self.lib.hmsc_create_sharded(C.byref(self.buf.struct), C.c_uint64(int(seed)), device,
                                                  self.mask, rank, nranks, cid, C.byref(h)))
@@ -125,9 +147,7 @@ class Chain:
                                          C.byref(h)))
         self.h = h
         self.rank, self.nranks = rank, nranks
-        per = ((-(-hM.ns // nranks)) + 1) & ~1   # even shard starts (capi.cpp: Philox species pairs)
-        self.sp0 = min(hM.ns, rank * per)
-        self.nsl = min(hM.ns, self.sp0 + per) - self.sp0
+        self.sp0, self.nsl = shard_range(hM.ns, rank, nranks)
 
     def close(self):
         if self.h:
@@ -144,6 +164,10 @@ class Chain:
     def init(self, nf0=None):
         arr = None if nf0 is None else L.i32(nf0)
         L.check(self.lib.hmsc_init_state(self.h, L.iptr(arr)))
+
+    def init_z(self):
+        """Z = updateZ(Y = hM$Y, ...) at the current state (R/computeInitialParameters.R:254)."""
+        L.check(self.lib.hmsc_init_z(self.h))
 
     def nf(self):
         out = np.zeros(L.MAX_LEVELS, dtype=np.int32)
@@ -441,36 +465,50 @@ def sampleMcmc(hM, samples, transient=0, thin=1, initPar=None, verbose=None, ada
                 if v is not None and v[r] is not None:
                     a = np.asarray(v[r])
                     nf0[r] = a.shape[1] if key == "Eta" else a.shape[0]
-    elif initPar == "fixed effects":
-        raise NotImplementedError("initPar='fixed effects' (GLM initialisation) is not implemented")
+    elif initPar == "fixed effects":                                  # R/computeInitialParameters.R:52-79
+        print("Hmsc::computeInitialParameter - initializing fixed effects with SSDM estimates")
+        from .initpar import fixed_effects_init
+        initPar = fixed_effects_init(hM)
 
     results = [None] * nChains
     errors = []
 
-    def sample_chain(c):                                                   # :155-327
+    def make_chain(c):
+        if nChains > 1:
+            print(f'[1] "Computing chain {c + 1}"')
+        ch = Chain(hM, int(initSeed[c]), device=devices[c % len(devices)], updater=updater)
+        ch.init(nf0)
+        if initPar is not None:
+            ch.set_state(initPar)
+            ch.init_z()        # the reference draws Z last, from the initPar state (:229-254)
+        return ch
+
+    def run_chain(c, ch):                                                  # :155-327
         try:
-            if nChains > 1:
-                print(f'[1] "Computing chain {c + 1}"')
-            ch = Chain(hM, int(initSeed[c]), device=devices[c % len(devices)], updater=updater)
-            ch.init(nf0)
-            if initPar is not None:
-                ch.set_state(initPar)
             rec = ch.run(transient, samples, thin, adaptNf, verbose=int(verbose) if verbose else 0, chain=c + 1)
-            ch.close()
             results[c] = combine_parameters(rec, hM)
         except Exception as e:  # surface in the caller thread
             errors.append(e)
 
-    if nParallel > 1:
-        for start in range(0, nChains, nParallel):
-            th = [threading.Thread(target=sample_chain, args=(c,)) for c in range(start, min(nChains, start + nParallel))]
-            for t in th:
-                t.start()
-            for t in th:
-                t.join()
-    else:
-        for c in range(nChains):
-            sample_chain(c)
+    # Chains are created, initialised and destroyed on this thread (device allocation and
+    # synchronisation), and only their sweep loops run concurrently, nParallel at a time.
+    for start in range(0, nChains, max(1, nParallel)):
+        idx = list(range(start, min(nChains, start + max(1, nParallel))))
+        chains = [make_chain(c) for c in idx]
+        try:
+            if len(idx) > 1:
+                th = [threading.Thread(target=run_chain, args=(c, ch)) for c, ch in zip(idx, chains)]
+                for t in th:
+                    t.start()
+                for t in th:
+                    t.join()
+            else:
+                run_chain(idx[0], chains[0])
+        finally:
+            for ch in chains:
+                ch.close()
+        if errors:
+            break
     if errors:
         raise errors[0]
     hM.postList = results

@@ -159,6 +159,19 @@ int hmsc_create_sharded(const hmsc_model* model, uint64_t seed, int32_t device,
                         const void* comm_id, hmsc_state** out);
 int hmsc_comm_unique_id(void* out128);
 
+/* The same species-sharded chain with a host transport in place of RCCL: every cross-shard
+ * fp64 sum calls fn(buf, n, ctx), which must replace the n doubles at buf (host memory) by
+ * their sum over all ranks and return 0.  For hosts without a device-to-device fabric, and
+ * for exercising the sharded path on one GPU (several ranks, one device). */
+typedef int (*hmsc_allreduce_fn)(double* buf, int64_t n, void* ctx);
+int hmsc_create_sharded_host(const hmsc_model* model, uint64_t seed, int32_t device,
+                             uint32_t updater_mask, int32_t rank, int32_t nranks,
+                             hmsc_allreduce_fn fn, void* ctx, hmsc_state** out);
+/* The species block [sp0, sp0 + nsl) rank `rank` of `nranks` owns in hmsc_create_sharded:
+ * even-sized blocks of 2 ceil(ceil(ns/2)/nranks) species (updateZ's Philox species pairs);
+ * an error if that block is empty.  No reference counterpart (species sharding is new). */
+int hmsc_shard_range(int32_t ns, int32_t rank, int32_t nranks, int32_t* sp0, int32_t* nsl);
+
 void hmsc_destroy(hmsc_state* s);
 
 /* computeInitialParameters(hM, initPar=NULL) on the device, including the initial
@@ -169,6 +182,11 @@ int hmsc_init_state(hmsc_state* s, const int32_t* nf0);
 int hmsc_set_state(hmsc_state* s, const hmsc_params* p);
 int hmsc_get_state(hmsc_state* s, hmsc_params* p);
 int hmsc_get_nf(hmsc_state* s, int32_t* nf);
+
+/* The closing step of computeInitialParameters: Z = updateZ(Y = hM$Y, Z = LFix + LRan, ...)
+ * at the CURRENT state (R/computeInitialParameters.R:229-254) -- after hmsc_set_state has
+ * applied an initPar (or initPar = "fixed effects", :52-79), as the reference draws Z last. */
+int hmsc_init_z(hmsc_state* s);
 
 /* One Gibbs sweep in the reference block order, R/sampleMcmc.R:219-306.
  * `iter` is the 1-based sweep number (Philox counter word 3 and updateNf's iter). */

@@ -5,7 +5,7 @@ splits species into contiguous blocks and all-reduces, once per updater, the
 species-sums that couple the shards.  Here each rank computes its block's share of
 those sums with the oracle's formulas and a gloo all_reduce must reproduce the
 unsharded values — the same decomposition and block arithmetic the C library uses
-(capi.cpp build_state: per = ceil(ns / nranks) rounded up to even).  Chains mode needs no exchange;
+(capi.cpp shard_range: per = 2 ceil(ceil(ns / 2) / nranks)).  Chains mode needs no exchange;
 its timing reduction (max over ranks) is checked too.
 """
 import os
@@ -30,7 +30,8 @@ def _free_port():
 
 
 def species_block(ns, rank, nranks):
-    per = ((-(-ns // nranks)) + 1) & ~1
+    """capi.cpp shard_range (hmsc_shard_range): even blocks of 2 ceil(ceil(ns/2)/nranks)."""
+    per = 2 * (-(-((ns + 1) // 2) // nranks))
     a = min(ns, rank * per)
     return a, min(ns, a + per)
 
@@ -98,8 +99,9 @@ def test_species_sharded_statistics_allreduce_gloo():
 def test_species_blocks_partition():
     for ns in (1, 7, 1000, 1003):
         for n in (1, 2, 4, 8):
-            if n > ns:
+            if 2 * n > ns + 1:
                 continue
             blocks = [species_block(ns, r, n) for r in range(n)]
+            assert all(b > a for a, b in blocks)
             assert blocks[0][0] == 0 and blocks[-1][1] == ns
             assert all(blocks[i][1] == blocks[i + 1][0] for i in range(n - 1))

@@ -171,3 +171,21 @@ def test_variance_partitioning_td():
     assert np.all(VP["vals"] >= 0)
     assert np.all((VP["R2T"]["Beta"] >= 0) & (VP["R2T"]["Beta"] <= 1)) and 0 <= VP["R2T"]["Y"] <= 1
     assert VP["rownames"][-2:] == ["Random: sample", "Random: plot"]
+
+
+def test_coda_name_flags_follow_r():
+    """convertToCodaObject's *NamesNumbers flags (R/convertToCodaObject.r:54-92): [1] adds
+    the name, [2] adds '(S%d)', joined by a space; Delta / Alpha are 0-padded; Eta columns
+    are named by unit."""
+    hM = td_model()
+    hM.postList = td_postlist(hM)
+    sp = M["spNames"]
+    _, c = H.convertToCodaObject(hM, spNamesNumbers=(True, False), covNamesNumbers=(False, True))
+    assert c["Beta"][0] == f"B[(C1), {sp[0]}]"
+    _, c = H.convertToCodaObject(hM, spNamesNumbers=(False, True), covNamesNumbers=(True, False))
+    assert c["Beta"][1] == "B[x1, (S1)]"
+    mp, c = H.convertToCodaObject(hM)
+    assert c["Beta"][0] == f"B[(Intercept) (C1), {sp[0]} (S1)]"
+    assert c["Eta"][1][0] == "Eta2[1, factor1]" and c["Alpha"][1] == ["Alpha2[factor1]", "Alpha2[factor2]"]
+    a = mp["Alpha"][1][0]
+    assert a.shape == (100, 2) and np.all(np.isin(a, hM.rL[1].alphapw[:, 0]))

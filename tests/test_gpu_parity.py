@@ -223,3 +223,28 @@ def test_graph_replay_matches_eager(monkeypatch, thin):
         for i in range(2):
             for k in ("Beta", "Gamma", "iV", "iSigma", "Lambda0", "Eta0", "Delta0", "Psi0"):
                 np.testing.assert_array_equal(out[0][i][k], o[i][k], err_msg=k)
+
+
+def test_init_par_fixed_effects_chain_start():
+    """initPar = "fixed effects": the chain starts from the GLM Beta / Gamma / V (host,
+    hmsc_amd/initpar.py) and its Z is then drawn by the initial updateZ from that state
+    (R/computeInitialParameters.R:229-254, hmsc_init_z), equal to the oracle's draw."""
+    from hmsc_amd.initpar import fixed_effects_init
+    hM = synthetic_model(ny=150, ns=12, nc=3, nf=2, n_normal=2, n_poisson=2, seed=21)
+    m = oracle_model(hM)
+    seed = 2468
+    fe = fixed_effects_init(hM)
+    ch = H.Chain(hM, seed, device=0, updater={"GammaEta": False})
+    ch.init()
+    ch.set_state(fe)
+    ch.init_z()
+    g = ch.get_state()
+    ch.close()
+    assert rel_err(g["Beta"], fe["Beta"]) < 1e-14 and rel_err(g["Gamma"], fe["Gamma"]) < 1e-14
+    assert rel_err(np.linalg.inv(g["iV"]), fe["V"]) < 1e-12
+    st = dict(g)
+    Z = O.update_z(st, m, Rng(seed), 0, Y=m["Yraw"])
+    assert rel_err(g["Z"], Z) < TOL_DRAW
+    out = H.sampleMcmc(hM, samples=5, transient=3, initPar="fixed effects", updater={"GammaEta": False},
+                       seed=5, verbose=0)
+    assert len(out.postList[0]) == 5 and np.all(np.isfinite(out.postList[0][-1]["Beta"]))

@@ -30,31 +30,38 @@ FIX = os.path.join(HERE, "golden", "td_longrun.npz")
 DEV_TRANSIENT, DEV_SAMPLES, DEV_CHAINS = 500, 8000, 8
 
 
-def _device_chain_rows(hM, seeds, updater, transient, samples):
-    """Run one device chain per seed, concurrently (one stream each; the C calls release
-    the GIL), and return each chain's (S, P) statistic rows."""
+def _device_chain_rows(hM, seeds, updater, transient, samples, batch=8):
+    """One device chain per seed: created and initialised on this thread, then run `batch`
+    at a time concurrently (one stream each; the C calls release the GIL); returns each
+    chain's (S, P) statistic rows."""
     out = [None] * len(seeds)
     err = []
 
-    def work(c):
+    def work(c, ch):
         try:
-            ch = H.Chain(hM, int(seeds[c]), device=0, updater=updater)
-            ch.init([int(rl.nfMin) for rl in hM.rL])
             rec = ch.run(transient=transient, samples=samples, thin=1)
-            ch.close()
             lams = [rec[f"Lambda{r}"] for r in range(hM.nr)]
             alphas = [rec[f"Alpha{r}"] for r in range(hM.nr)]
             out[c] = param_rows(hM, rec["Beta"], rec["Gamma"], rec["iV"], rec["rho"], lams, alphas)
         except Exception as e:  # surfaced below
             err.append(e)
 
-    th = [threading.Thread(target=work, args=(c,)) for c in range(len(seeds))]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
-    if err:
-        raise err[0]
+    for b0 in range(0, len(seeds), batch):
+        idx = list(range(b0, min(len(seeds), b0 + batch)))
+        chains = []
+        for c in idx:
+            ch = H.Chain(hM, int(seeds[c]), device=0, updater=updater)
+            ch.init([int(rl.nfMin) for rl in hM.rL])
+            chains.append(ch)
+        th = [threading.Thread(target=work, args=(c, ch)) for c, ch in zip(idx, chains)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        for ch in chains:
+            ch.close()
+        if err:
+            raise err[0]
     return out
 
 
