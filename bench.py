@@ -14,8 +14,11 @@ N>1 is launched by torch.distributed.run, one rank per GPU:
     value = total chain-sweeps/sec over all GPUs.
   * sharded: ONE chain, species sharded over the GPUs, RCCL all-reduce of the
     sufficient statistics inside the C library -> strong scaling.
-Rank 0 prints one JSON line.  The CPU baseline (rank 0, N=1 only) times the
-oracle restatement (oracle/, numpy fp64, 1 BLAS thread) on a bounded sample.
+Rank 0 prints one JSON line.  Beta ESS/sec = (coda ESS per sweep of a separate recorded run
+of >= 1000 samples after the timed region) x the timed sweeps/sec.  The CPU baseline (rank 0,
+N=1 only) times the compiled C++ restatement of the same sweep (oracle/cpu/hmsc_cpu.cpp,
+validated against the numpy oracle) with chains = host cores, one thread per chain, on a
+bounded sample (R is absent, so the reference itself cannot be timed: kind "port").
 """
 import argparse
 import json
@@ -44,9 +47,10 @@ def parse():
     p.add_argument("--ns", type=int, default=1000)
     p.add_argument("--nc", type=int, default=20)
     p.add_argument("--nf", type=int, default=10)
-    p.add_argument("--cpu-seconds", type=float, default=20.0)
+    p.add_argument("--cpu-sweeps", type=int, default=3, help="sweeps per CPU chain in the baseline sample")
+    p.add_argument("--ess-samples", type=int, default=2000, help="recorded sweeps of the separate ESS run")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc.json"))
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02_pmc.json"))
     return p.parse_args()
 
 
@@ -118,9 +122,15 @@ def main():
         kern[name] = dict(total_ms=tot, launches=n, avg_us=1e3 * tot / max(1, n))
     ch.profile(False)
 
-    # Beta ESS (coda::effectiveSize restated) over this rank's Beta entries
-    beta = rec["Beta"].reshape(args.steps, -1)
-    ess_local = H.effectiveSize(beta)
+    # Beta ESS (coda::effectiveSize restated) from a separate recorded run of >= 1000 sweeps
+    # of the same chain after the timed region (Beta only), per sweep; x the timed rate below
+    n_ess = max(1000, args.ess_samples)
+    rec_ess = ch.run(transient=0, samples=n_ess, thin=1, adaptNf=[0], iter0=args.warmup + args.steps + n_prof,
+                     record=True, fields=("Beta",))
+    sync(ch)
+    beta = rec_ess["Beta"].reshape(n_ess, -1)
+    ess_local = H.effectiveSize(beta) / n_ess                   # ESS per sweep, per Beta entry
+    del rec
     tmax = t_run
     if dist is not None:
         t = torch.tensor([t_run], dtype=torch.float64)
@@ -131,7 +141,7 @@ def main():
         if args.mode == "sharded":
             ess_all = np.concatenate(gathered)       # disjoint species blocks of one chain
         else:
-            ess_all = np.sum(np.stack(gathered), axis=0)  # sum over chains per Beta entry
+            ess_all = np.sum(np.stack(gathered), axis=0)  # chains: per-sweep ESS adds over chains
     else:
         ess_all = ess_local
     if rank != 0:
@@ -139,8 +149,9 @@ def main():
     ny, ns = args.ny, args.ns
     sweeps = args.steps * (world if args.mode == "chains" else 1)
     value = sweeps / tmax
-    ess_rate_median = float(np.median(ess_all)) / tmax
-    ess_rate_min = float(np.min(ess_all)) / tmax
+    per_chain_rate = args.steps / tmax                         # sweeps/s of each chain
+    ess_rate_median = float(np.median(ess_all)) * per_chain_rate
+    ess_rate_min = float(np.min(ess_all)) * per_chain_rate
 
     # roofline: the dominant kernel of the sweep, algorithmic bytes per launch
     algo_bytes = {
@@ -156,19 +167,29 @@ def main():
     roof_kernel = max(live, key=lambda k: live[k]["total_us"])
     avg_s = live[roof_kernel]["avg_us"] * 1e-6
     achieved = algo_bytes[roof_kernel] / avg_s / 1e9
-    traffic = None
+    traffic, valu = None, None
     if os.path.exists(args.pmc_json):
         try:
             pmc = json.load(open(args.pmc_json))
             pref = {"z": "z_wave_kernel", "eta": "eta_fused_kernel", "betalambda": "beta_lambda_wave_kernel"}
             hit = [v for k, v in pmc.items() if k.startswith(pref[roof_kernel])]
-            traffic = round(hit[0]["hbm_bytes_per_launch"]) if hit else None
+            if hit:
+                traffic = round(hit[0]["hbm_bytes_per_launch"])
+                # VALU issue floor: every VALU instruction of the launch at the fp64 issue cost
+                # (4 cycles per wave instruction on a SIMD-32, MI355X_MICROARCH.md) over the
+                # 1024 SIMDs at 2.4 GHz; frac = floor / the measured launch duration
+                ni = hit[0].get("SQ_INSTS_VALU")
+                if ni:
+                    floor_us = ni * 4.0 / 1024 / 2.4e9 * 1e6
+                    valu = {"bound": "valu", "valu_insts_per_launch": round(ni), "issue_floor_us": round(floor_us, 2),
+                            "frac": round(floor_us / live[roof_kernel]["avg_us"], 4),
+                            "source": os.path.relpath(args.pmc_json, ROOT)}
         except Exception:
-            traffic = None
+            traffic, valu = None, None
 
     cpu = None
     if world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(hM, args, float(np.median(ess_local)) / args.steps)
+        cpu = cpu_baseline(hM, args, float(np.median(ess_local)))
 
     out = {
         "metric": "Gibbs sweeps/sec + Beta ESS/sec at ny=10k, ns=1k, nf=10; 1/2/4/8 MI355X",
@@ -189,13 +210,20 @@ def main():
                    "parallelism": (f"{world} independent chains, one per GPU" if args.mode == "chains"
                                    else f"1 chain species-sharded over {world} GPUs (RCCL)")},
         "beta_ess_per_s": {"median": round(ess_rate_median, 3), "min": round(ess_rate_min, 3),
-                           "n_beta": int(ess_all.size), "ess_median": float(np.median(ess_all))},
+                           "n_beta": int(ess_all.size), "ess_per_sweep_median": float(np.median(ess_all)),
+                           "ess_run": f"separate recorded run of {n_ess} sweeps after the timed region (coda "
+                                      f"effectiveSize restated); ESS/s = ESS per sweep x timed sweeps/s"},
         "roofline": {"kernel": roof_kernel, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "algorithmic_bytes_per_launch": algo_bytes[roof_kernel],
                      "avg_launch_us": round(live[roof_kernel]["avg_us"], 3),
                      "timed_launches": live[roof_kernel]["launches"],
-                     "timer": "in-kernel wall clock (s_memrealtime, 100 MHz) over the timed region's graph replays"},
+                     "timer": "in-kernel wall clock (s_memrealtime, 100 MHz) over the timed region's graph replays",
+                     "valu": valu,
+                     "sweep_level": {"algorithmic_bytes_per_sweep": ny * ns * 25,
+                                     "achieved": round(ny * ns * 25 * per_chain_rate / 1e9, 1),
+                                     "frac": round(ny * ns * 25 * per_chain_rate / 1e9 / HBM_PEAK_GBS, 4),
+                                     "note": "SURVEY 8(d): 3 fp64 Z touches + 1 B Y per cell per sweep"}},
         "kernels_live_us": {k: round(v["avg_us"], 3) for k, v in live.items()},
         "kernels_eager_events_us": {k: round(v["avg_us"], 2) for k, v in kern.items()},
         "cpu_baseline": cpu,
@@ -204,39 +232,33 @@ def main():
 
 
 def cpu_baseline(hM, args, ess_per_sweep):
-    """Oracle restatement (numpy fp64) timed on this host on a bounded sample."""
+    """The compiled C++ restatement of the same sweep (oracle/cpu/hmsc_cpu.cpp; equal to the
+    numpy oracle to fp64 rounding, tests/test_oracle_cpu_port.py), chains = host cores, one
+    thread per chain, timed on a bounded sample: args.cpu_sweeps sweeps of every chain after
+    its initialisation (R is absent, so this stands in for sampleMcmc with
+    nChains = nParallel = cores, labelled "port")."""
+    import platform
+    from oracle import cpu_port
+    m = dict(X=hM.XScaled, Y=hM.YScaled, Yraw=hM.Y, Tr=hM.TrScaled, Pi=hM.Pi, np=hM.np, distr=hM.distr,
+             V0=hM.V0, f0=hM.f0, mGamma=hM.mGamma, UGamma=hM.UGamma, aSigma=hM.aSigma, bSigma=hM.bSigma,
+             rL=[dict(nu=rl.nu, a1=rl.a1, b1=rl.b1, a2=rl.a2, b2=rl.b2, nfMin=rl.nfMin, nfMax=rl.nfMax)
+                 for rl in hM.rL])
+    cores = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count() or 1, 64)
+    _, sec = cpu_port.run(m, 1234567, n_sweeps=args.cpu_sweeps, nchains=cores, iter0=0, gamma2=True)
+    rate = cores * args.cpu_sweeps / sec
+    model = platform.processor() or platform.machine()
     try:
-        from threadpoolctl import threadpool_limits
-    except Exception:  # pragma: no cover
-        threadpool_limits = None
-    from oracle import hmsc_oracle as O
-    from oracle.rng import Rng
-    ctx = threadpool_limits(limits=1) if threadpool_limits else None
-    try:
-        if ctx:
-            ctx.__enter__()
-        m = dict(X=hM.XScaled, Y=hM.YScaled, Yraw=hM.Y, Tr=hM.TrScaled, Pi=hM.Pi, np=hM.np, distr=hM.distr,
-                 V0=hM.V0, f0=hM.f0, mGamma=hM.mGamma, UGamma=hM.UGamma, aSigma=hM.aSigma, bSigma=hM.bSigma,
-                 rhopw=hM.rhopw, C=None,
-                 rL=[dict(nu=rl.nu, a1=rl.a1, b1=rl.b1, a2=rl.a2, b2=rl.b2, nfMin=rl.nfMin, nfMax=rl.nfMax,
-                          sDim=0, xDim=0) for rl in hM.rL])
-        rng = Rng(1234567)
-        st = O.compute_initial_parameters(m, rng)
-        n = 0
-        t0 = time.perf_counter()
-        while True:
-            st = O.sweep(st, m, rng, n + 1, updater={"GammaEta": False})
-            n += 1
-            el = time.perf_counter() - t0
-            if el > args.cpu_seconds or n >= 1000:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
                 break
-        rate = n / el
-    finally:
-        if ctx:
-            ctx.__exit__(None, None, None)
-    return {"value": round(rate, 4), "unit": "sweeps/s", "cores": 1, "kind": "port",
-            "sample": f"{n} full sweeps of the numpy oracle at ny={args.ny} ns={args.ns} (1 BLAS thread), "
-                      f"{el:.1f} s",
+    except OSError:
+        pass
+    return {"value": round(rate, 4), "unit": "sweeps/s", "cores": cores, "kind": "port",
+            "sample": f"{cores} chains x {args.cpu_sweeps} full sweeps of the C++ restatement (oracle/cpu/hmsc_cpu.cpp, "
+                      f"one thread per chain) at ny={args.ny} ns={args.ns} nc={args.nc} nf={args.nf}, "
+                      f"{sec:.1f} s wall; {model}",
+            "per_chain_sweeps_per_s": round(args.cpu_sweeps / sec, 4),
             "beta_ess_per_s_median_est": round(rate * ess_per_sweep, 5)}
 
 

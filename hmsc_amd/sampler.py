@@ -282,8 +282,9 @@ class Chain:
         L.check(self.lib.hmsc_debug_get(self.h, name.encode(), L.fptr(out), int(n)))
         return out
 
-    def run(self, transient, samples, thin=1, adaptNf=None, iter0=0, verbose=0, chain=1, record=True):
-        """hmsc_run: the device sweep loop with recording; returns the raw record arrays."""
+    def run(self, transient, samples, thin=1, adaptNf=None, iter0=0, verbose=0, chain=1, record=True, fields=None):
+        """hmsc_run: the device sweep loop with recording; returns the raw record arrays.
+        fields: record only these (e.g. ("Beta",)); None records everything."""
         hM = self.hM
         nr = hM.nr
         ns = self.nsl
@@ -296,21 +297,20 @@ class Chain:
             arrays = dict(Beta=np.zeros((S, ns, hM.nc)), Gamma=np.zeros((S, hM.nt, hM.nc)),
                           iV=np.zeros((S, hM.nc, hM.nc)), iSigma=np.zeros((S, ns)),
                           rho=np.zeros(S, dtype=np.int32), rec_nf=np.zeros((max(1, nr), S), dtype=np.int32))
+            want = (lambda k: True) if fields is None else (lambda k: k in fields)  # noqa: E731
             rec = L.hmsc_record()
-            rec.Beta, rec.Gamma, rec.iV = L.fptr(arrays["Beta"]), L.fptr(arrays["Gamma"]), L.fptr(arrays["iV"])
-            rec.iSigma, rec.rho, rec.rec_nf = L.fptr(arrays["iSigma"]), L.iptr(arrays["rho"]), L.iptr(arrays["rec_nf"])
+            for k, fp in (("Beta", L.fptr), ("Gamma", L.fptr), ("iV", L.fptr), ("iSigma", L.fptr), ("rho", L.iptr)):
+                if want(k):
+                    setattr(rec, k, fp(arrays[k]))
+            rec.rec_nf = L.iptr(arrays["rec_nf"])
             for r in range(nr):
                 nfm = nfMax[r]
-                arrays[f"Eta{r}"] = np.zeros((S, nfm, int(hM.np[r])))
-                arrays[f"Lambda{r}"] = np.zeros((S, ns, nfm))
-                arrays[f"Psi{r}"] = np.zeros((S, ns, nfm))
-                arrays[f"Delta{r}"] = np.zeros((S, nfm))
-                arrays[f"Alpha{r}"] = np.zeros((S, nfm), dtype=np.int32)
-                rec.Eta[r] = L.fptr(arrays[f"Eta{r}"])
-                rec.Lambda[r] = L.fptr(arrays[f"Lambda{r}"])
-                rec.Psi[r] = L.fptr(arrays[f"Psi{r}"])
-                rec.Delta[r] = L.fptr(arrays[f"Delta{r}"])
-                rec.Alpha[r] = L.iptr(arrays[f"Alpha{r}"])
+                for k, shape, dt in (("Eta", (S, nfm, int(hM.np[r])), np.float64), ("Lambda", (S, ns, nfm), np.float64),
+                                     ("Psi", (S, ns, nfm), np.float64), ("Delta", (S, nfm), np.float64),
+                                     ("Alpha", (S, nfm), np.int32)):
+                    if want(k):
+                        arrays[f"{k}{r}"] = np.zeros(shape, dtype=dt)
+                        getattr(rec, k)[r] = (L.iptr if dt == np.int32 else L.fptr)(arrays[f"{k}{r}"])
         L.check(self.lib.hmsc_run_verbose(self.h, int(transient), int(samples), int(thin), L.iptr(adapt),
                                           int(iter0), int(verbose), int(chain),
                                           C.byref(rec) if rec is not None else None))
@@ -321,11 +321,13 @@ class Chain:
                    iV=arrays["iV"].transpose(0, 2, 1), iSigma=arrays["iSigma"], rho=arrays["rho"],
                    nf=arrays["rec_nf"][:nr])
         for r in range(nr):
-            out[f"Eta{r}"] = arrays[f"Eta{r}"].transpose(0, 2, 1)
-            out[f"Lambda{r}"] = arrays[f"Lambda{r}"].transpose(0, 2, 1)
-            out[f"Psi{r}"] = arrays[f"Psi{r}"].transpose(0, 2, 1)
-            out[f"Delta{r}"] = arrays[f"Delta{r}"]
-            out[f"Alpha{r}"] = arrays[f"Alpha{r}"].astype(np.int64)
+            for k in ("Eta", "Lambda", "Psi"):
+                if f"{k}{r}" in arrays:
+                    out[f"{k}{r}"] = arrays[f"{k}{r}"].transpose(0, 2, 1)
+            if f"Delta{r}" in arrays:
+                out[f"Delta{r}"] = arrays[f"Delta{r}"]
+            if f"Alpha{r}" in arrays:
+                out[f"Alpha{r}"] = arrays[f"Alpha{r}"].astype(np.int64)
         return out
 
 
