@@ -207,14 +207,15 @@ static void setup_phylo(State& s, const hmsc_model* m) {
 }
 
 // ---------------------------- create ----------------------------
-// Species shard of `rank`: blocks of an even number of species (updateZ draws species pairs
-// 2m, 2m+1 from one Philox block), per = 2 ceil(ceil(ns / 2) / nranks); the last shard takes
-// the remainder.  Returns -1 if this rank's shard is empty.
+// Species shard of `rank`: whole species pairs (updateZ draws species 2m, 2m+1 from one Philox
+// block), the ceil(ns / 2) pairs spread as evenly as possible over the ranks: rank r owns pairs
+// [floor(r P / n), floor((r + 1) P / n)).  Every rank gets a pair when P >= n; returns -1 if
+// this rank's shard is empty.
 static int shard_range(int ns, int rank, int nranks, int* sp0, int* nsl) {
-  const int pairs = (ns + 1) / 2;
-  const int per = 2 * ((pairs + nranks - 1) / nranks);
-  *sp0 = std::min(ns, rank * per);
-  *nsl = std::min(ns, *sp0 + per) - *sp0;
+  const long pairs = (ns + 1) / 2;
+  const long p0 = pairs * rank / nranks, p1 = pairs * (rank + 1) / nranks;
+  *sp0 = (int)std::min<long>(ns, 2 * p0);
+  *nsl = (int)std::min<long>(ns, 2 * p1) - *sp0;
   return *nsl > 0 ? 0 : -1;
 }
 

@@ -998,6 +998,7 @@ __global__ __launch_bounds__(256) void gamma2_prep_kernel(G2PrepArgs a) {
 
 struct G2Args {
   int nc, nt, Kmax, NF, nparts, ns_loc, use_xtztr, check_isigma, stage;
+  const double* isig_count;  // sharded chain: all-reduced count of species with iSigma != 1
   const double* part;
   const double* xtztr;
   const double* G;
@@ -1023,6 +1024,7 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
   if (a.check_isigma)
     for (int j = t; j < a.ns_loc; j += blockDim.x)
       if (a.iSigma[j] != 1.0) all_one = 0;  // acts only if all(iSigma == 1)  (:36)
+  if (t == 0 && a.isig_count && *a.isig_count != 0.0) all_one = 0;  // ... over every rank's species
   __syncthreads();
   if (!all_one) return;
   const int n1 = nc * nt, nL = a.NF * nt, P = n1 + nL;
@@ -1124,6 +1126,19 @@ static void launch_gamma2_prep(State& s, hipStream_t st) {
   s.g2prep_valid = true;
 }
 
+// number of local species with iSigma != 1 (updateGamma2 acts only if there is none in the
+// whole chain, R/updateGamma2.R:35-36): one slot of a sharded chain's all-reduce
+__global__ __launch_bounds__(256) void isigma_ne1_count_kernel(const double* iSigma, int n, double* out) {
+  __shared__ int c;
+  if (threadIdx.x == 0) c = 0;
+  __syncthreads();
+  int k = 0;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) k += iSigma[j] != 1.0;
+  if (k) atomicAdd(&c, k);
+  __syncthreads();
+  if (threadIdx.x == 0) *out = (double)c;
+}
+
 void launch_gamma2(State& s, uint32_t iter) {
   HMSC_REQUIRE((size_t)s.nc * s.nt <= 256 && s.NF * s.nt + s.nc * s.nt <= 1024,
                "updateGamma2: nc*nt must be <= 256 in this build");
@@ -1142,9 +1157,13 @@ void launch_gamma2(State& s, uint32_t iter) {
   int np = nparts;
   double* xtztr = s.allreduce_buf + (n1 + n2);
   if (s.has_na) xt_ztr_kernel<<<n1, 256, 0, s.stream>>>(s.X, s.ZTr, s.ny, s.nc, s.nt, xtztr);
+  double* isig_count = nullptr;
   if (s.nranks > 1) {
     slab_sum_kernel<<<grid_for(n1 + n2), 256, 0, s.stream>>>(part, s.allreduce_buf, n1 + n2, nparts, n1 + n2);
-    allreduce_sum(s, s.allreduce_buf, s.has_na ? 2 * n1 + n2 : n1 + n2);
+    isig_count = s.allreduce_buf + 2 * n1 + n2;  // after the X'ZTr slot (used with NA only)
+    if (!s.has_na) HIP_OK(hipMemsetAsync(xtztr, 0, sizeof(double) * n1, s.stream));
+    isigma_ne1_count_kernel<<<1, 256, 0, s.stream>>>(s.iSigma, s.nsl, isig_count);
+    allreduce_sum(s, s.allreduce_buf, 2 * n1 + n2 + 1);
     part = s.allreduce_buf;
     np = 1;
   }
@@ -1156,7 +1175,8 @@ void launch_gamma2(State& s, uint32_t iter) {
   a.nparts = np;
   a.ns_loc = s.nsl;
   a.use_xtztr = s.has_na ? 1 : 0;
-  a.check_isigma = s.nranks == 1 ? 1 : 0;
+  a.check_isigma = 1;
+  a.isig_count = isig_count;
   a.part = part;
   a.xtztr = xtztr;
   a.G = s.G;

@@ -5,7 +5,7 @@ splits species into contiguous blocks and all-reduces, once per updater, the
 species-sums that couple the shards.  Here each rank computes its block's share of
 those sums with the oracle's formulas and a gloo all_reduce must reproduce the
 unsharded values — the same decomposition and block arithmetic the C library uses
-(capi.cpp shard_range: per = 2 ceil(ceil(ns / 2) / nranks)).  Chains mode needs no exchange;
+(capi.cpp shard_range: whole species pairs spread evenly over the ranks).  Chains mode needs no exchange;
 its timing reduction (max over ranks) is checked too.
 """
 import os
@@ -30,10 +30,9 @@ def _free_port():
 
 
 def species_block(ns, rank, nranks):
-    """capi.cpp shard_range (hmsc_shard_range): even blocks of 2 ceil(ceil(ns/2)/nranks)."""
-    per = 2 * (-(-((ns + 1) // 2) // nranks))
-    a = min(ns, rank * per)
-    return a, min(ns, a + per)
+    """capi.cpp shard_range (hmsc_shard_range): whole species pairs, spread evenly."""
+    pairs = (ns + 1) // 2
+    return min(ns, 2 * (pairs * rank // nranks)), min(ns, 2 * (pairs * (rank + 1) // nranks))
 
 
 def sufficient_stats(st, m, sl):

@@ -242,7 +242,7 @@ def test_init_par_fixed_effects_chain_start():
     ch.close()
     assert rel_err(g["Beta"], fe["Beta"]) < 1e-14 and rel_err(g["Gamma"], fe["Gamma"]) < 1e-14
     assert rel_err(np.linalg.inv(g["iV"]), fe["V"]) < 1e-12
-    st = dict(g)
+    st = {k: v for k, v in g.items() if k != "Z"}   # init: Poisson ZPrev = LFix + LRan (:250-254)
     Z = O.update_z(st, m, Rng(seed), 0, Y=m["Yraw"])
     assert rel_err(g["Z"], Z) < TOL_DRAW
     out = H.sampleMcmc(hM, samples=5, transient=3, initPar="fixed effects", updater={"GammaEta": False},

@@ -88,7 +88,7 @@ def test_sharded_chain_follows_unsharded(kw):
 def test_shard_range_blocks():
     for ns in (2, 7, 41, 1000, 1003):
         for n in (1, 2, 4, 8):
-            if 2 * n > ns + 1:
+            if n > (ns + 1) // 2:
                 continue
             bl = [shard_range(ns, r, n) for r in range(n)]
             assert bl[0][0] == 0 and sum(b for _, b in bl) == ns
