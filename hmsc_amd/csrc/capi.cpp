@@ -1233,6 +1233,37 @@ int hmsc_shard_range(int32_t ns, int32_t rank, int32_t nranks, int32_t* sp0, int
   });
 }
 
+int hmsc_dense_chol_solve(int32_t device, double* A, int32_t n, double* b, int32_t* info) {
+  return guarded([&] {
+    HMSC_REQUIRE(A != nullptr && n > 0 && info != nullptr, "hmsc_dense_chol_solve: bad arguments");
+    std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
+    DeviceGuard dg(device);
+    hipStream_t st;
+    HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    const size_t nn = (size_t)n * n;
+    double *dA = nullptr, *db = nullptr, *ws = nullptr;
+    int* dinfo = nullptr;
+    HIP_OK(hipMalloc(&dA, nn * sizeof(double)));
+    HIP_OK(hipMalloc(&db, (size_t)n * sizeof(double)));
+    HIP_OK(hipMalloc(&ws, 64 * 64 * sizeof(double)));
+    HIP_OK(hipMalloc(&dinfo, sizeof(int)));
+    HIP_OK(hipMemsetAsync(dinfo, 0, sizeof(int), st));
+    HIP_OK(hipMemcpyAsync(dA, A, nn * sizeof(double), hipMemcpyHostToDevice, st));
+    if (b) HIP_OK(hipMemcpyAsync(db, b, (size_t)n * sizeof(double), hipMemcpyHostToDevice, st));
+    dense_potrf_lower(st, dA, n, n, ws, dinfo);
+    if (b) {
+      dense_trsv_lower(st, dA, n, n, db, 0);
+      dense_trsv_lower(st, dA, n, n, db, 1);
+      HIP_OK(hipMemcpyAsync(b, db, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, st));
+    }
+    HIP_OK(hipMemcpyAsync(A, dA, nn * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(info, dinfo, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    (void)hipFree(dA), (void)hipFree(db), (void)hipFree(ws), (void)hipFree(dinfo);
+    (void)hipStreamDestroy(st);
+  });
+}
+
 int hmsc_device_count(int32_t* n) {
   return guarded([&] {
     int c = 0;

@@ -101,6 +101,64 @@ __global__ __launch_bounds__(1024) void eta_spatial_full_kernel(SpArgs a) {
   for (int e = t; e < N; e += nthr) a.Eta[e] = rhs[e];
 }
 
+// ---- blocked path for large np * nf (dense.hip): the same system, assembled and factorised
+// by many workgroups (one-workgroup wg_chol above is the latency-optimal shape only while
+// the (np nf)^2 matrix is small)
+// LDL = Lam diag(iSigma) Lam' (block 0) and rhs = vec(fS) (every thread one (p, h))
+__global__ __launch_bounds__(256) void sp_rhs_kernel(SpArgs a, double* rhs, double* LDL) {
+  const int np = a.np, nf = a.nf, ns = a.ns, ny = a.ny, K = a.K, N = np * nf;
+  const double* lam = a.BL + a.loff;
+  if (blockIdx.x == 0)
+    for (int p = threadIdx.x; p < nf * nf; p += blockDim.x) {
+      const int h1 = p % nf, h2 = p / nf;
+      double s = 0.0;
+      for (int j = 0; j < ns; ++j) s = fma(lam[h1 + (size_t)K * j] * a.iSigma[j], lam[h2 + (size_t)K * j], s);
+      LDL[p] = s;
+    }
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= N) return;
+  const int q = e % np, h = e / np;
+  double acc = 0.0;
+  for (int k = a.unit_ptr[q]; k < a.unit_ptr[q + 1]; ++k) {
+    const int i = a.unit_rows[k];
+    for (int j = 0; j < ns; ++j) {
+      double sv = a.Z[i + (size_t)ny * j];
+      for (int c = 0; c < K; ++c) {
+        if (c >= a.loff && c < a.loff + nf) continue;
+        sv = fma(-a.XEta[i + (size_t)ny * c], a.BL[c + (size_t)K * j], sv);
+      }
+      acc = fma(sv, lam[h + (size_t)K * j] * a.iSigma[j], acc);
+    }
+  }
+  rhs[e] = acc;
+}
+
+// lower triangle of iUEta = bdiag(iWg[,,alpha_h]) + kron(LDL, diag(n_p)); grid (N / 256, N)
+__global__ __launch_bounds__(256) void sp_assemble_kernel(SpArgs a, double* U, const double* LDL) {
+  const int np = a.np, nf = a.nf, N = np * nf;
+  const int r2 = blockIdx.y, r1 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r1 >= N || r1 < r2) return;
+  const int q1 = r1 % np, h1 = r1 / np, q2 = r2 % np, h2 = r2 / np;
+  double v = 0.0;
+  if (h1 == h2) {
+    const int g = (int)a.AlphaD[h1] - 1;
+    v = a.iWg[q1 + (size_t)np * q2 + (size_t)np * np * g];
+  }
+  if (q1 == q2) v = fma(LDL[h1 + nf * h2], (double)(a.unit_ptr[q1 + 1] - a.unit_ptr[q1]), v);
+  U[r1 + (size_t)N * r2] = v;
+}
+
+__global__ __launch_bounds__(256) void sp_noise_kernel(SpArgs a, double* rhs) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x, np = a.np;
+  if (e >= np * a.nf || a.noise_zero) return;
+  rhs[e] += normal(a.key, (uint32_t)(e % np), (uint32_t)(e / np), S_ETA + LEVEL_STRIDE * a.r, SWEEP_ITER(a));
+}
+
+__global__ __launch_bounds__(256) void sp_store_kernel(SpArgs a, const double* rhs) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < a.np * a.nf) a.Eta[e] = rhs[e];
+}
+
 // v[g * nf + h] = |RiWg[,,g] eta_h|^2 ; RiWg upper triangular (chol(iW), Full) or lower
 // triangular (NNGP's D^-1/2 (I - A), R/computeDataParameters.R:127; GPP's chol(W)^-1), one
 // workgroup per g
@@ -189,10 +247,14 @@ static SpArgs sp_args(State& s, int r, uint32_t iter) {
   return a;
 }
 
+// np * nf above which updateEta's dense system goes to the multi-workgroup blocked path
+constexpr int SP_BLOCKED_N = 1024;
+
 size_t spatial_work_doubles(const State& s, int r) {
   const Level& L = s.lev[r];
-  const size_t N = std::min<size_t>((size_t)L.np * std::max(1, std::min(L.nfmax, s.NFmax)), 8192);
-  const size_t eta = N * N + N + 64 * 64;
+  const size_t nfc = std::max(1, std::min(L.nfmax, s.NFmax));
+  const size_t N = (size_t)L.np * nfc;
+  const size_t eta = N * N + N + 64 * 64 + nfc * nfc + 64;
   const size_t alpha = (size_t)L.nalpha * std::max(1, std::min(L.nfmax, s.NFmax));
   return std::max(eta, alpha) + 64;
 }
@@ -200,9 +262,28 @@ size_t spatial_work_doubles(const State& s, int r) {
 void launch_eta_spatial(State& s, int r, uint32_t iter) {
   const Level& L = s.lev[r];
   HMSC_REQUIRE(s.nranks == 1, "spatial levels: species-sharded chains are not supported");
-  HMSC_REQUIRE((size_t)L.np * L.nf <= 8192, "spatial 'Full' level: np * nf must be <= 8192 in this build");
   if (!s.xeta_valid) launch_xeta(s);
-  eta_spatial_full_kernel<<<1, 1024, 0, s.stream>>>(sp_args(s, r, iter));
+  const SpArgs a = sp_args(s, r, iter);
+  const int N = L.np * L.nf;
+  if (N <= SP_BLOCKED_N) {
+    eta_spatial_full_kernel<<<1, 1024, 0, s.stream>>>(a);
+    HIP_OK(hipGetLastError());
+    return;
+  }
+  // blocked: R = chol(iUEta) as the lower factor L = R^T; eta = L^-T (L^-1 fS + xi)
+  double* U = L.spWork;
+  double* rhs = U + (size_t)N * N;
+  double* ws = rhs + N;
+  double* LDL = ws + 64 * 64;
+  const int g1 = (N + 255) / 256;
+  sp_rhs_kernel<<<g1, 256, 0, s.stream>>>(a, rhs, LDL);
+  sp_assemble_kernel<<<dim3(g1, N), 256, 0, s.stream>>>(a, U, LDL);
+  HIP_OK(hipGetLastError());
+  dense_potrf_lower(s.stream, U, N, N, ws, s.dev_flags);
+  dense_trsv_lower(s.stream, U, N, N, rhs, 0);   // backsolve(R, fS, transpose = TRUE)
+  sp_noise_kernel<<<g1, 256, 0, s.stream>>>(a, rhs);
+  dense_trsv_lower(s.stream, U, N, N, rhs, 1);   // backsolve(R, tmp2)
+  sp_store_kernel<<<g1, 256, 0, s.stream>>>(a, rhs);
   HIP_OK(hipGetLastError());
 }
 

@@ -248,6 +248,9 @@ void launch_phylo_gv_sums(State& s, uint32_t iter, hipStream_t st);
 void launch_rho(State& s, uint32_t iter, hipStream_t st);
 void launch_beta_lambda_phylo(State& s, uint32_t iter);
 void launch_side_fused(State& s, uint32_t iter);
+// blocked dense fp64 factorisation / solves (dense.hip)
+void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, int* info);
+void dense_trsv_lower(hipStream_t st, const double* L, int n, int lda, double* x, int trans);
 // spatial "Full" levels (spatial.hip)
 size_t spatial_work_doubles(const State& s, int r);
 void launch_eta_spatial(State& s, int r, uint32_t iter);

@@ -232,6 +232,12 @@ int hmsc_kernel_timing_get(hmsc_state* s, int32_t id, double* total_us, int32_t*
 /* Wait for all device work of this chain. */
 int hmsc_sync(hmsc_state* s);
 
+/* The blocked device Cholesky (dense.hip) on one host matrix, for tests: A (n x n,
+ * column-major, lower triangle read) is overwritten by L (A = L L^T; the strict upper
+ * triangle is scratch), b (may be NULL) by A^-1 b through L^-T L^-1; *info = 1 if A is not
+ * positive definite.  Instrumentation of this port, no reference counterpart. */
+int hmsc_dense_chol_solve(int32_t device, double* A, int32_t n, double* b, int32_t* info);
+
 /* Copy a named internal device buffer (fp64) for tests / profiling:
  * "Z", "E", "XEtaTZ", "Gram", "ZTr", "BL", "BL_prec" ... ; n = element count. */
 int hmsc_debug_get(hmsc_state* s, const char* name, double* out, int64_t n);

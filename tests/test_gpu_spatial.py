@@ -33,6 +33,10 @@ MODELS = {
                           C=phylo_corr(4, seed=3)),
     "nngp_two_levels": dict(ny=40, ns=5, nc=2, nf=2, nr=2, units=[40, 8], spatial=[0], seed=55,
                             spatial_method="NNGP", alpha_n=20),
+    # np nf > 1024: updateEta's system on the multi-workgroup blocked path (dense.hip)
+    "large_full": dict(ny=700, ns=6, nc=2, nf=2, nr=1, spatial=[0], seed=57, alpha_n=20),
+    "large_nngp": dict(ny=600, ns=5, nc=2, nf=2, nr=1, spatial=[0], seed=58, alpha_n=20,
+                       spatial_method="NNGP", n_neighbours=8),
 }
 
 
