@@ -43,6 +43,8 @@ def parse():
     p.add_argument("--steps", type=int, default=1000)
     p.add_argument("--warmup", type=int, default=100)
     p.add_argument("--mode", choices=["chains", "sharded"], default="chains")
+    p.add_argument("--workload", choices=["synthetic", "spatial"], default="synthetic",
+                   help="synthetic: config 4 (the metric); spatial: config 5, vignette_4 'Full' at --ny")
     p.add_argument("--ny", type=int, default=10000)
     p.add_argument("--ns", type=int, default=1000)
     p.add_argument("--nc", type=int, default=20)
@@ -56,6 +58,8 @@ def parse():
 
 def main():
     args = parse()
+    if args.workload == "spatial":
+        return main_spatial(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -227,6 +231,92 @@ def main():
         "kernels_live_us": {k: round(v["avg_us"], 3) for k, v in live.items()},
         "kernels_eager_events_us": {k: round(v["avg_us"], 2) for k, v in kern.items()},
         "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+
+
+def main_spatial(args):
+    """BASELINE.json config 5 (vignette_4 spatial, 'Full' GP latent factor) at ny = --ny
+    (default 5000 when --ny is left at the config-4 value): ns=5, nc=2, nf=1, probit,
+    updater GammaEta=FALSE (vignettes/vignette_4_spatial.Rmd:124).  One chain per GPU.  The
+    alphapw grid (101 x ny^2 iW and RiW, 2 x 20 GB at ny=5k) is built on the device at chain
+    creation (setup_s, outside the timed region).  Each sweep solves the (ny nf)^2 Eta system
+    with the blocked Cholesky on the matrix cores and streams the grid once for updateAlpha;
+    the roofline object prices the Cholesky (n^3 / 3 fp64 flops) against the fp64 matrix peak."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    H._lib.lib()
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    from hmsc_amd.workloads import spatial_vignette4
+    ny = 5000 if args.ny == 10000 else args.ny
+    hM = spatial_vignette4(ny=ny, method="Full")
+    t0 = time.perf_counter()
+    ch = H.Chain(hM, 4242 + 7919 * rank, device=local, updater={"GammaEta": False})
+    ch.init([1])
+    ch.sync()
+    setup = time.perf_counter() - t0
+    ch.run(transient=0, samples=args.warmup, thin=1, adaptNf=[0], record=True)
+    ch.sync()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    rec = ch.run(transient=0, samples=args.steps, thin=1, adaptNf=[0], iter0=args.warmup, record=True)
+    ch.sync()
+    if dist is not None:
+        dist.barrier()
+    t_run = time.perf_counter() - t0
+    alpha_mean = float(np.mean(rec["Alpha0"]))
+    del rec
+    n_prof = min(args.steps, 20)
+    ch.profile(True)
+    ch.run(transient=n_prof, samples=0, adaptNf=[0], iter0=args.warmup + args.steps, record=False)
+    ch.sync()
+    kern = {}
+    for name in ("eta_spatial", "chol", "alpha", "z", "betalambda", "sweep"):
+        tot, n = ch.profile_get(name)
+        kern[name] = dict(total_ms=tot, launches=n, avg_us=1e3 * tot / max(1, n))
+    ch.profile(False)
+    ch.close()
+    tmax = t_run
+    if dist is not None:
+        t = torch.tensor([t_run], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tmax = float(t.item())
+    if rank != 0:
+        return
+    N = ny  # np * nf
+    chol_flops = N ** 3 / 3.0
+    chol_s = kern["chol"]["avg_us"] * 1e-6
+    peak_tf = 78.6
+    achieved = chol_flops / max(chol_s, 1e-12) / 1e12
+    grid_bytes = 101 * ny * ny * 8 / 2  # lower-triangular RiW_g streamed once per sweep
+    alpha_s = kern["alpha"]["avg_us"] * 1e-6
+    out = {
+        "metric": "Gibbs sweeps/sec, config 5 (vignette_4 spatial Full) at ny=%d" % ny,
+        "value": round(world * args.steps / tmax, 3), "unit": "sweeps/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1e3 * tmax / args.steps, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (vignette_4 generator scaled to ny, seed 20261015)",
+        "config": {"workload": f"vignette_4 spatial 'Full' ny={ny} ns=5 nc=2 nf=1, 101-point alphapw grid, "
+                               f"updater GammaEta=FALSE, record every sweep",
+                   "ny": ny, "ns": 5, "nc": 2, "nf": 1, "parallelism": f"{world} independent chains, one per GPU"},
+        "setup_s": round(setup, 2),
+        "roofline": {"kernel": "blocked Cholesky of the (np nf)^2 Eta precision (chol_diag/panel/update)",
+                     "bound": "mfma", "achieved": round(achieved, 2), "peak": peak_tf, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak_tf, 4), "traffic": None,
+                     "algorithmic_flops_per_launch": chol_flops, "avg_launch_us": round(kern["chol"]["avg_us"], 1),
+                     "timer": "HIP events on the chain stream around each factorization (eager sweeps)",
+                     "alpha_grid": {"bytes_per_sweep": grid_bytes, "avg_us": round(kern["alpha"]["avg_us"], 1),
+                                    "achieved_GBs": round(grid_bytes / max(alpha_s, 1e-12) / 1e9, 1),
+                                    "peak_GBs": HBM_PEAK_GBS}},
+        "kernels_eager_events_us": {k: round(v["avg_us"], 1) for k, v in kern.items()},
+        "alpha_posterior_mean_index": round(alpha_mean, 2),
+        "cpu_baseline": None,
     }
     print(json.dumps(out), flush=True)
 

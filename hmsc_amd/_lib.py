@@ -30,7 +30,8 @@ class hmsc_model(C.Structure):
                 ("sDim", ip), ("xDim", ip), ("C", dp), ("nrho", C.c_int32), ("rhopw", dp),
                 ("C_vectors", dp), ("C_values", dp),
                 ("spatialMethod", ip), ("nalpha", ip), ("alphapw", dp * MAX_LEVELS), ("iWg", dp * MAX_LEVELS),
-                ("RiWg", dp * MAX_LEVELS), ("detWg", dp * MAX_LEVELS)]
+                ("RiWg", dp * MAX_LEVELS), ("detWg", dp * MAX_LEVELS),
+                ("sCoord", dp * MAX_LEVELS), ("distMat", dp * MAX_LEVELS)]
 
 
 class hmsc_params(C.Structure):
@@ -63,7 +64,7 @@ _lib = None
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int64, C.c_void_p)
 
 EXPORTS = ["hmsc_last_error", "hmsc_device_count", "hmsc_create", "hmsc_create_sharded", "hmsc_comm_unique_id",
-           "hmsc_shard_range", "hmsc_create_sharded_host", "hmsc_dense_chol_solve",
+           "hmsc_shard_range", "hmsc_create_sharded_host", "hmsc_dense_chol_solve", "hmsc_spatial_full_grid",
            "hmsc_destroy", "hmsc_init_state", "hmsc_init_z", "hmsc_set_state", "hmsc_get_state", "hmsc_get_nf", "hmsc_sweep",
            "hmsc_update", "hmsc_set_noise_mode", "hmsc_run", "hmsc_run_verbose", "hmsc_sync", "hmsc_debug_get",
            "hmsc_profile", "hmsc_profile_get", "hmsc_kernel_timing", "hmsc_kernel_timing_get", "hmsc_predict"]
@@ -89,6 +90,7 @@ def lib():
     L.hmsc_init_state.argtypes = [C.c_void_p, ip]
     L.hmsc_init_z.argtypes = [C.c_void_p]
     L.hmsc_dense_chol_solve.argtypes = [C.c_int32, dp, C.c_int32, dp, ip]
+    L.hmsc_spatial_full_grid.argtypes = [C.c_int32, C.c_int32, C.c_int32, dp, dp, C.c_int32, dp, dp, dp, dp]
     L.hmsc_shard_range.argtypes = [C.c_int32, C.c_int32, C.c_int32, ip, ip]
     L.hmsc_create_sharded_host.argtypes = [C.POINTER(hmsc_model), C.c_uint64, C.c_int32, C.c_uint32, C.c_int32,
                                            C.c_int32, ALLREDUCE_FN, C.c_void_p, C.POINTER(C.c_void_p)]

@@ -201,7 +201,8 @@ static void setup_phylo(State& s, const hmsc_model* m) {
   s.phEt = dalloc<double>((size_t)nc * ns + 1);
   s.phTTw = dalloc<double>((size_t)nt * nt);
   s.phNmax = s.Kmax * ns;
-  HMSC_REQUIRE(s.phNmax <= 8192, "phylogeny: (nc + nfMax) * ns must be <= 8192 for the dense BetaLambda branch");
+  HMSC_REQUIRE(s.phNmax <= 65536, "phylogeny: (nc + nfMax) * ns must be <= 65536 for the dense BetaLambda branch "
+                                   "(a 34 GB system)");
   s.phWork = dalloc<double>(phylo_work_doubles(ns, s.Kmax, nc, s.nrho));
   s.mask &= ~(uint32_t)HMSC_UP_GAMMA2;  // updateGamma2 returns Gamma unchanged when C is given (R/updateGamma2.R:35-36)
 }
@@ -271,8 +272,11 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
                    "spatial level: spatialMethod must be 1 (Full), 2 (NNGP) or 3 (GPP)");
       HMSC_REQUIRE(m->spatialMethod[r] == 1 || m->np[r] == ny,
                    "spatial level: NNGP / GPP levels need np == ny (R/updateEta.R:140,165)");
-      HMSC_REQUIRE(m->nalpha != nullptr && m->nalpha[r] > 0 && m->alphapw[r] && m->iWg[r] && m->RiWg[r] && m->detWg[r],
-                   "spatial level: alphapw / iWg / RiWg / detWg (computeDataParameters' rLPar) must be given");
+      const bool geom = m->spatialMethod[r] == 1 && !m->iWg[r] && (m->sCoord[r] || m->distMat[r]);
+      HMSC_REQUIRE(m->nalpha != nullptr && m->nalpha[r] > 0 && m->alphapw[r] &&
+                       (geom || (m->iWg[r] && m->RiWg[r] && m->detWg[r])),
+                   "spatial level: alphapw and either iWg / RiWg / detWg (computeDataParameters' rLPar) "
+                   "or, for 'Full', sCoord / distMat must be given");
       HMSC_REQUIRE(!(mask & HMSC_UP_GAMMAETA) || m->spatialMethod[r] == 1,
                    "updataGammaEta: no method implemented yet for NNGP / GPP with GammaEta updater "
                    "(R/updateGammaEta.R:153-158): pass updater GammaEta=FALSE");
@@ -323,10 +327,31 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
       const size_t G = m->nalpha[r], np2 = (size_t)L.np * L.np;
       L.nalpha = (int)G;
       L.alphapw = dupload(m->alphapw[r], 2 * G);
-      L.iWg = dupload(m->iWg[r], np2 * G);
-      L.RiWg = dupload(m->RiWg[r], np2 * G);
-      L.riw_lower = m->spatialMethod[r] == 2 || m->spatialMethod[r] == 3;
-      L.detWg = dupload(m->detWg[r], G);
+      if (m->iWg[r]) {
+        L.iWg = dupload(m->iWg[r], np2 * G);
+        L.RiWg = dupload(m->RiWg[r], np2 * G);
+        L.riw_lower = m->spatialMethod[r] == 2 || m->spatialMethod[r] == 3;
+        L.detWg = dupload(m->detWg[r], G);
+      } else {  // 'Full' grid from the level's geometry, on the device
+        L.iWg = dalloc<double>(np2 * G);
+        L.RiWg = dalloc<double>(np2 * G);
+        L.detWg = dalloc<double>(G);
+        L.riw_lower = 1;
+        const bool crd = m->sCoord[r] != nullptr;
+        HMSC_REQUIRE(!crd || m->sDim[r] > 0, "spatial level: sDim must give the coordinate columns");
+        int* flag = dalloc<int>(1);
+        double* geo = crd ? dupload(m->sCoord[r], (size_t)L.np * m->sDim[r]) : dupload(m->distMat[r], np2);
+        std::vector<double> alphas(m->alphapw[r], m->alphapw[r] + G);
+        spatial_full_grid(s.stream, L.np, crd ? m->sDim[r] : 0, crd ? geo : nullptr, crd ? nullptr : geo,
+                          alphas.data(), (int)G, L.iWg, L.RiWg, L.detWg, flag);
+        HIP_OK(hipStreamSynchronize(s.stream));
+        HIP_OK(hipFree(geo));
+        int bad = 0;
+        HIP_OK(hipMemcpy(&bad, flag, sizeof(int), hipMemcpyDeviceToHost));
+        HIP_OK(hipFree(flag));
+        HMSC_REQUIRE(bad == 0, "spatial level: a grid matrix W_g = exp(-d / alpha_g) is not positive definite "
+                               "(duplicated coordinates?)");
+      }
       L.spWork = dalloc<double>(spatial_work_doubles(s, r));
     }
   }
@@ -1261,6 +1286,34 @@ int hmsc_dense_chol_solve(int32_t device, double* A, int32_t n, double* b, int32
     HIP_OK(hipStreamSynchronize(st));
     (void)hipFree(dA), (void)hipFree(db), (void)hipFree(ws), (void)hipFree(dinfo);
     (void)hipStreamDestroy(st);
+  });
+}
+
+int hmsc_spatial_full_grid(int32_t device, int32_t np, int32_t sdim, const double* coords, const double* dist,
+                           int32_t G, const double* alphas, double* iWg, double* RiWg, double* detWg) {
+  return guarded([&] {
+    HMSC_REQUIRE(np > 0 && G > 0 && alphas && iWg && RiWg && detWg && ((coords && sdim > 0) || dist),
+                 "hmsc_spatial_full_grid: bad arguments");
+    std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
+    DeviceGuard dg(device);
+    hipStream_t st;
+    HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    const size_t n2 = (size_t)np * np;
+    double* geo = coords ? dupload(coords, (size_t)np * sdim) : dupload(dist, n2);
+    double* dI = dalloc<double>(n2 * G);
+    double* dR = dalloc<double>(n2 * G);
+    double* dd = dalloc<double>(G);
+    int* flag = dalloc<int>(1);
+    spatial_full_grid(st, np, coords ? sdim : 0, coords ? geo : nullptr, coords ? nullptr : geo, alphas, G, dI, dR,
+                      dd, flag);
+    int bad = 0;
+    HIP_OK(hipMemcpy(&bad, flag, sizeof(int), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(iWg, dI, n2 * G * sizeof(double), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(RiWg, dR, n2 * G * sizeof(double), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(detWg, dd, G * sizeof(double), hipMemcpyDeviceToHost));
+    (void)hipFree(geo), (void)hipFree(dI), (void)hipFree(dR), (void)hipFree(dd), (void)hipFree(flag);
+    (void)hipStreamDestroy(st);
+    HMSC_REQUIRE(bad == 0, "hmsc_spatial_full_grid: a grid matrix is not positive definite");
   });
 }
 

@@ -232,8 +232,180 @@ __global__ __launch_bounds__(256) void trsv_bwd_update_kernel(const double* L, i
 }
 
 // ---------------------------------------------------------------------------------------
+// inverse of a lower factor (trtri) and M^T M (lauum): the spatial grid precompute
+// (R/computeDataParameters.R:53-81 evaluates iW = chol2inv(chol(W)) for every grid point)
+// ---------------------------------------------------------------------------------------
+// LDS staging of a 64 x 64 tile, zero padded: S[r][k] at r + DLD k
+//   stage_n: S[r][k] = M[R0 + r, C0 + k]         (r < rows, k < cols)
+//   stage_t: S[c][k] = M[R0 + k, C0 + c]         (k < rows, c < cols)
+__device__ inline void stage_n(double* S, const double* M, int ld, int R0, int C0, int rows, int cols) {
+  for (int p = threadIdx.x; p < DB * DB; p += 256) {
+    const int r = p & 63, k = p >> 6;
+    S[r + DLD * k] = (r < rows && k < cols) ? M[(size_t)(R0 + r) + (size_t)ld * (C0 + k)] : 0.0;
+  }
+}
+__device__ inline void stage_t(double* S, const double* M, int ld, int R0, int C0, int rows, int cols) {
+  for (int p = threadIdx.x; p < DB * DB; p += 256) {
+    const int k = p & 63, c = p >> 6;
+    S[c + DLD * k] = (k < rows && c < cols) ? M[(size_t)(R0 + k) + (size_t)ld * (C0 + c)] : 0.0;
+  }
+}
+
+// out[r][c] += sum_k SA[r][k] SB[c][k] over the wave's 32 x 32 quadrant (as chol_update_kernel):
+// acc[a][b][q] holds out[qr + 16 b + lm][qc + 16 a + lk + 4 q]
+__device__ inline void tile_mma(d4 (&acc)[2][2], const double* SA, const double* SB) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lm = lane & 15, lk = lane >> 4;
+  const int qr = 32 * (w & 1), qc = 32 * (w >> 1);
+#pragma unroll 4
+  for (int s = 0; s < DB / 4; ++s) {
+    const int k = 4 * s + lk;
+    const double b0 = SA[qr + lm + DLD * k], b1 = SA[qr + 16 + lm + DLD * k];
+    const double a0 = SB[qc + lm + DLD * k], a1 = SB[qc + 16 + lm + DLD * k];
+    acc[0][0] = mfma_f64(a0, b0, acc[0][0]);
+    acc[0][1] = mfma_f64(a0, b1, acc[0][1]);
+    acc[1][0] = mfma_f64(a1, b0, acc[1][0]);
+    acc[1][1] = mfma_f64(a1, b1, acc[1][1]);
+  }
+}
+
+__device__ inline void zero_acc(d4 (&acc)[2][2]) {
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+}
+
+// visit the quadrant's entries: f(r, c, value)
+template <class F>
+__device__ inline void acc_each(const d4 (&acc)[2][2], F f) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lm = lane & 15, lk = lane >> 4;
+  const int qr = 32 * (w & 1), qc = 32 * (w >> 1);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) f(qr + 16 * b + lm, qc + 16 * a + lk + 4 * q, acc[a][b][q]);
+}
+
+// every diagonal block inverse of a lower-triangular L: Dinv[b] = L_bb^-1 (64 x 64, ld 64,
+// zero above, identity-padded past n); one workgroup per block
+__global__ __launch_bounds__(64) void trtri_diag_kernel(const double* L, int ld, int n, double* Dinv) {
+  __shared__ double T[DB * DLD];
+  __shared__ double I[DB * DLD];
+  const int k0 = DB * blockIdx.x, nb = min(DB, n - k0), t = threadIdx.x;
+  for (int c = 0; c < DB; ++c)
+    T[t + DLD * c] = (t < nb && c < nb && t >= c) ? L[(size_t)(k0 + t) + (size_t)ld * (k0 + c)] : (t == c ? 1.0 : 0.0);
+  __syncthreads();
+  for (int i = 0; i < DB; ++i) {  // column t of T X = I by forward substitution
+    double x = (i == t) ? 1.0 : 0.0;
+    if (i >= t)
+      for (int k = t; k < i; ++k) x -= T[i + DLD * k] * I[k + DLD * t];
+    I[i + DLD * t] = i >= t ? x / T[i + DLD * i] : 0.0;
+  }
+  __syncthreads();
+  double* D = Dinv + (size_t)DB * DB * blockIdx.x;
+  for (int c = 0; c < DB; ++c) D[t + DB * c] = I[t + DLD * c];
+}
+
+// right-looking block forward substitution for X = L^-1, in M (zeroed beforehand):
+//   row step k:    X_kj = Dinv_k B_kj (j < k), X_kk = Dinv_k       -- grid k + 1
+//   update step k: B_ij -= L_ik X_kj   (i > k, j <= k)             -- grid (nbk-k-1)(k+1)
+__global__ __launch_bounds__(256) void trtri_row_kernel(double* M, int ldm, int n, int k, const double* Dinv) {
+  __shared__ double SA[DB * DLD];
+  __shared__ double SB[DB * DLD];
+  const int j = blockIdx.x, K0 = DB * k, J0 = DB * j, rowsK = min(DB, n - K0), colsJ = min(DB, n - J0);
+  const double* D = Dinv + (size_t)DB * DB * k;
+  if (j == k) {
+    for (int p = threadIdx.x; p < DB * DB; p += 256) {
+      const int r = p & 63, c = p >> 6;
+      if (r < rowsK && c < rowsK) M[(size_t)(K0 + r) + (size_t)ldm * (K0 + c)] = D[r + DB * c];
+    }
+    return;
+  }
+  stage_n(SA, D, DB, 0, 0, DB, DB);
+  stage_t(SB, M, ldm, K0, J0, rowsK, colsJ);
+  __syncthreads();
+  d4 acc[2][2];
+  zero_acc(acc);
+  tile_mma(acc, SA, SB);
+  acc_each(acc, [&](int r, int c, double v) {
+    if (r < rowsK && c < colsJ) M[(size_t)(K0 + r) + (size_t)ldm * (J0 + c)] = v;
+  });
+}
+
+__global__ __launch_bounds__(256) void trtri_update_kernel(double* M, int ldm, const double* L, int ldl, int n, int k) {
+  __shared__ double SA[DB * DLD];
+  __shared__ double SB[DB * DLD];
+  const int nbk = (n + DB - 1) / DB, ni = nbk - k - 1;
+  const int i = k + 1 + (int)blockIdx.x % ni, j = (int)blockIdx.x / ni;
+  const int I0 = DB * i, J0 = DB * j, K0 = DB * k;
+  const int rowsI = min(DB, n - I0), rowsK = min(DB, n - K0), colsJ = min(DB, n - J0);
+  stage_n(SA, L, ldl, I0, K0, rowsI, rowsK);
+  stage_t(SB, M, ldm, K0, J0, rowsK, colsJ);
+  __syncthreads();
+  d4 acc[2][2];
+  zero_acc(acc);
+  tile_mma(acc, SA, SB);
+  acc_each(acc, [&](int r, int c, double v) {
+    if (r < rowsI && c < colsJ) M[(size_t)(I0 + r) + (size_t)ldm * (J0 + c)] -= v;
+  });
+}
+
+// out = M^T M for lower-triangular M (full symmetric result): lower tile (i, j), i >= j, is
+// sum_{k >= i} M_ki^T M_kj, mirrored into the upper triangle (diagonal tiles mirror their
+// lower half, so the result is exactly symmetric)
+__global__ __launch_bounds__(256) void lauum_kernel(const double* M, int ldm, int n, double* out, int ldo) {
+  __shared__ double SA[DB * DLD];
+  __shared__ double SB[DB * DLD];
+  int ti = (int)((sqrt(8.0 * blockIdx.x + 1.0) - 1.0) * 0.5);
+  int tj = (int)blockIdx.x - ti * (ti + 1) / 2;
+  if (tj > ti) ++ti, tj = (int)blockIdx.x - ti * (ti + 1) / 2;
+  if (tj < 0) --ti, tj = (int)blockIdx.x - ti * (ti + 1) / 2;
+  const int nbk = (n + DB - 1) / DB, I0 = DB * ti, J0 = DB * tj;
+  const int rowsI = min(DB, n - I0), rowsJ = min(DB, n - J0);
+  d4 acc[2][2];
+  zero_acc(acc);
+  for (int k = ti; k < nbk; ++k) {
+    const int K0 = DB * k, rowsK = min(DB, n - K0);
+    stage_t(SA, M, ldm, K0, I0, rowsK, rowsI);
+    stage_t(SB, M, ldm, K0, J0, rowsK, rowsJ);
+    __syncthreads();
+    tile_mma(acc, SA, SB);
+    __syncthreads();
+  }
+  acc_each(acc, [&](int r, int c, double v) {
+    if (r < rowsI && c < rowsJ && (ti != tj || r >= c)) {
+      out[(size_t)(I0 + r) + (size_t)ldo * (J0 + c)] = v;
+      out[(size_t)(J0 + c) + (size_t)ldo * (I0 + r)] = v;
+    }
+  });
+}
+
+// ---------------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------------
+// M <- L^-1 (lower, zero above; n x n, ld ldm) of the lower-triangular L; `dinv` holds
+// ceil(n / 64) * 64 * 64 doubles
+void dense_trtri_lower(hipStream_t st, const double* L, int ldl, int n, double* M, int ldm, double* dinv) {
+  const int nbk = (n + DB - 1) / DB;
+  HIP_OK(hipMemset2DAsync(M, sizeof(double) * ldm, 0, sizeof(double) * n, n, st));
+  trtri_diag_kernel<<<nbk, 64, 0, st>>>(L, ldl, n, dinv);
+  for (int k = 0; k < nbk; ++k) {
+    trtri_row_kernel<<<k + 1, 256, 0, st>>>(M, ldm, n, k, dinv);
+    const int ni = nbk - k - 1;
+    if (ni > 0) trtri_update_kernel<<<ni * (k + 1), 256, 0, st>>>(M, ldm, L, ldl, n, k);
+  }
+  HIP_OK(hipGetLastError());
+}
+
+// out <- M^T M (full symmetric, n x n, ld ldo) of the lower-triangular M
+void dense_lauum_lower(hipStream_t st, const double* M, int ldm, int n, double* out, int ldo) {
+  const int nbk = (n + DB - 1) / DB;
+  lauum_kernel<<<nbk * (nbk + 1) / 2, 256, 0, st>>>(M, ldm, n, out, ldo);
+  HIP_OK(hipGetLastError());
+}
+
 // In-place lower Cholesky of the n x n matrix at A (column-major, ld lda; lower triangle
 // read); `ws` >= 64 * 64 doubles; *info (device) is set to 1 if A is not positive definite.
 void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, int* info) {

@@ -221,6 +221,94 @@ __global__ __launch_bounds__(1024) void phylo_beta_lambda_kernel(PhyloArgs a) {
   }
 }
 
+// ---- the same system above one workgroup's reach: multi-workgroup assembly, the blocked
+// ---- Cholesky / triangular solves of dense.hip (MFMA trailing updates), elementwise noise
+// iQ = U diag(w) U^T  (ns^2 outputs), Y = iV Mu and tau (thread 0 of workgroup 0)
+__global__ __launch_bounds__(256) void ph_prep_kernel(PhyloArgs a) {
+  const int ns = a.ns, nc = a.nc;
+  double* iQ = a.work + (size_t)a.K * ns * (size_t)a.K * ns;
+  double* rhs = iQ + (size_t)ns * ns;
+  double* Y = rhs + (size_t)a.K * ns;
+  double* tau = Y + (size_t)nc * ns;
+  const double* w = a.Winv + (size_t)ns * rho_index(a.rho);
+  const size_t p = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (p < (size_t)ns * ns) {
+    const int j1 = (int)(p % ns), j2 = (int)(p / ns);
+    double s = 0.0;
+    for (int i = 0; i < ns; ++i) s = fma(a.U[j1 + (size_t)ns * i] * w[i], a.U[j2 + (size_t)ns * i], s);
+    iQ[p] = s;
+  } else if (p < (size_t)ns * ns + (size_t)nc * ns) {
+    const int q = (int)(p - (size_t)ns * ns), c = q % nc, j = q / nc;
+    double s = 0.0;
+    for (int c2 = 0; c2 < nc; ++c2) {
+      double mu = 0.0;
+      for (int t = 0; t < a.nt; ++t) mu = fma(a.Gamma[c2 + nc * t], a.Tr[j + (size_t)ns * t], mu);
+      s = fma(a.iV[c + nc * c2], mu, s);
+    }
+    Y[q] = s;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    int f = 0;
+    for (int r = 0; r < a.nr; ++r) {
+      double c = 1.0;
+      for (int h = 0; h < a.lev_nf[r]; ++h, ++f) {
+        c *= a.Delta[f];
+        tau[f] = c;
+      }
+    }
+  }
+}
+
+// lower triangle of iU (grid (N / 256, N)) and the right-hand side (column 0 row of blocks)
+__global__ __launch_bounds__(256) void ph_assemble_kernel(PhyloArgs a) {
+  const int ns = a.ns, nc = a.nc, N = a.K * ns;
+  double* M = a.work;
+  const double* iQ = M + (size_t)N * N;
+  const double* tau = iQ + (size_t)ns * ns + N + (size_t)nc * ns;
+  const int c = blockIdx.y, r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= N || r < c) return;
+  const int k1 = r / ns, j1 = r % ns, k2 = c / ns, j2 = c % ns;
+  double v = (j1 == j2) ? a.G[k1 + a.Kmax * k2] * a.iSigma[j1] : 0.0;
+  if (k1 < nc && k2 < nc)
+    v = fma(a.iV[k1 + nc * k2], iQ[j1 + (size_t)ns * j2], v);
+  else if (k1 == k2 && j1 == j2)
+    v += a.Psi[(k1 - nc) + (size_t)a.NF * j1] * tau[k1 - nc];
+  M[r + (size_t)N * c] = v;
+}
+
+__global__ __launch_bounds__(256) void ph_rhs_kernel(PhyloArgs a) {
+  const int ns = a.ns, nc = a.nc, K = a.K, N = K * ns;
+  const double* iQ = a.work + (size_t)N * N;
+  double* rhs = (double*)iQ + (size_t)ns * ns;
+  const double* Y = rhs + N;
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= N) return;
+  const int k = r / ns, j = r % ns;
+  double v = a.iSigma[j] * a.XZ[k + (size_t)K * j];
+  if (k < nc)
+    for (int j2 = 0; j2 < ns; ++j2) v = fma(Y[k + nc * j2], iQ[j2 + (size_t)ns * j], v);
+  rhs[r] = v;
+}
+
+__global__ __launch_bounds__(256) void ph_noise_kernel(PhyloArgs a) {
+  const int ns = a.ns, N = a.K * ns;
+  double* rhs = a.work + (size_t)N * N + (size_t)ns * ns;
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= N || a.noise_zero) return;
+  rhs[r] += normal(a.key, (uint32_t)(r % ns), (uint32_t)(r / ns), S_BETALAMBDA, SWEEP_ITER(a));
+}
+
+__global__ __launch_bounds__(256) void ph_store_kernel(PhyloArgs a) {
+  const int ns = a.ns, N = a.K * ns;
+  const double* rhs = a.work + (size_t)N * N + (size_t)ns * ns;
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= N) return;
+  a.BLout[r / ns + (size_t)a.K * (r % ns)] = rhs[r];
+}
+
+// K * ns above which the dense BetaLambda system goes to the multi-workgroup blocked path
+constexpr int PH_BLOCKED_N = 1024;
+
 static PhyloArgs phylo_args(State& s, uint32_t iter) {
   PhyloArgs a{};
   a.ns = s.ns;
@@ -262,7 +350,7 @@ static PhyloArgs phylo_args(State& s, uint32_t iter) {
 
 size_t phylo_work_doubles(int ns, int Kmax, int nc, int nrho) {
   const size_t N = (size_t)Kmax * ns;
-  const size_t bl = N * N + (size_t)ns * ns + N + (size_t)nc * ns + 64;
+  const size_t bl = N * N + (size_t)ns * ns + N + (size_t)nc * ns + (size_t)Kmax + 64 * 64 + 64;
   const size_t rho = (size_t)ns + nrho + 64;
   return bl > rho ? bl : rho;
 }
@@ -286,7 +374,27 @@ void launch_rho(State& s, uint32_t iter, hipStream_t st) {
 void launch_beta_lambda_phylo(State& s, uint32_t iter) {
   HMSC_REQUIRE((size_t)s.K * s.ns <= (size_t)s.phNmax, "phylogeny BetaLambda: K * ns exceeds the allocation");
   PhyloArgs a = phylo_args(s, iter);
-  phylo_beta_lambda_kernel<<<1, 1024, 0, s.stream>>>(a);
+  const int N = s.K * s.ns;
+  if (N <= PH_BLOCKED_N) {
+    phylo_beta_lambda_kernel<<<1, 1024, 0, s.stream>>>(a);
+    HIP_OK(hipGetLastError());
+    return;
+  }
+  // blocked: RiU = chol(iU) as the lower factor L = RiU^T; BL = L^-T (L^-1 rhs + xi)
+  const size_t ns2 = (size_t)s.ns * s.ns;
+  double* M = s.phWork;
+  double* rhs = M + (size_t)N * N + ns2;
+  double* ws = rhs + N + (size_t)s.nc * s.ns + s.Kmax;
+  const int g1 = (N + 255) / 256;
+  ph_prep_kernel<<<(unsigned)((ns2 + (size_t)s.nc * s.ns + 255) / 256), 256, 0, s.stream>>>(a);
+  ph_assemble_kernel<<<dim3(g1, N), 256, 0, s.stream>>>(a);
+  ph_rhs_kernel<<<g1, 256, 0, s.stream>>>(a);
+  HIP_OK(hipGetLastError());
+  dense_potrf_lower(s.stream, M, N, N, ws, s.dev_flags + 2);
+  dense_trsv_lower(s.stream, M, N, N, rhs, 0);   // m1 = backsolve(RiU, ., transpose=TRUE)  (:145)
+  ph_noise_kernel<<<g1, 256, 0, s.stream>>>(a);
+  dense_trsv_lower(s.stream, M, N, N, rhs, 1);   // backsolve(RiU, m1 + rnorm)  (:146)
+  ph_store_kernel<<<g1, 256, 0, s.stream>>>(a);
   HIP_OK(hipGetLastError());
 }
 

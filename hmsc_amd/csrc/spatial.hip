@@ -12,9 +12,12 @@
 // Layout in HBM: the alphapw grid arrays iWg / RiWg (np^2 x nalpha each, column-major as R
 // holds them) stay resident for the whole chain -- at np = 5000 and 101 grid points that is
 // 20 GB per array, which 288 GB of HBM holds -- so no sweep ever recomputes a grid matrix.
-// The Eta system is one workgroup with the shared wg_* Cholesky on an L2-resident (np nf)^2
-// workspace; updateAlpha's nalpha x nf quadratic forms are one workgroup per grid point
-// streaming that grid matrix once (the HBM-bound step at large np).
+// The grid is either uploaded (computeDataParameters' arrays) or, for 'Full' levels given
+// by coordinates / distances, built in place by spatial_full_grid (chol, trtri, lauum on
+// the matrix cores, dense.hip).  The Eta system is one workgroup with the shared wg_*
+// Cholesky up to np nf = 1024 and the blocked multi-workgroup Cholesky above;
+// updateAlpha's nalpha x nf quadratic forms stream each grid matrix once over
+// nalpha x ceil(np / 256) workgroups (the HBM-bound step at large np).
 // Randomness (oracle/hmsc_oracle.py _eta_spatial_full / update_alpha): Eta normal(p, h,
 // S_ETA + LEVEL_STRIDE r) -- the same counters as the non-spatial branch --, Alpha the first
 // uniform of (h, 0, S_ALPHA + LEVEL_STRIDE r).
@@ -159,32 +162,48 @@ __global__ __launch_bounds__(256) void sp_store_kernel(SpArgs a, const double* r
   if (e < a.np * a.nf) a.Eta[e] = rhs[e];
 }
 
-// v[g * nf + h] = |RiWg[,,g] eta_h|^2 ; RiWg upper triangular (chol(iW), Full) or lower
-// triangular (NNGP's D^-1/2 (I - A), R/computeDataParameters.R:127; GPP's chol(W)^-1), one
-// workgroup per g
+// v[g, h] = |RiWg[,,g] eta_h|^2 ; RiWg upper triangular (chol(iW), Full from the host) or lower
+// triangular (NNGP's D^-1/2 (I - A), R/computeDataParameters.R:127; GPP's and the device-built
+// Full grid's chol(W)^-1).  Grid (nalpha, ceil(np / 256)): a workgroup takes 256 rows p of one
+// grid matrix (coalesced down the columns), four factors per pass, and leaves its partial
+// sums at work[(g * nch + chunk) * nf + h]; alpha_draw_kernel adds the chunks in order.
 __global__ __launch_bounds__(256) void alpha_quad_kernel(SpArgs a) {
-  const int g = blockIdx.x, np = a.np, nf = a.nf;
+  const int g = blockIdx.x, chunk = blockIdx.y, nch = gridDim.y, np = a.np, nf = a.nf;
   const double* Rg = a.RiWg + (size_t)np * np * g;
-  double* v = a.work;
-  __shared__ double red[256];
-  for (int h = 0; h < nf; ++h) {
-    const double* eh = a.Eta + (size_t)np * h;
-    double s = 0.0;
-    for (int p = threadIdx.x; p < np; p += blockDim.x) {
-      double x = 0.0;
+  const int p = chunk * 256 + threadIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __shared__ double red[4][4];
+  for (int h0 = 0; h0 < nf; h0 += 4) {
+    const int nh = min(4, nf - h0);
+    double x[4] = {0.0, 0.0, 0.0, 0.0};
+    if (p < np) {
       const int lo = a.riw_lower ? 0 : p, hi = a.riw_lower ? p + 1 : np;
-      for (int p2 = lo; p2 < hi; ++p2) x = fma(Rg[p + (size_t)np * p2], eh[p2], x);
-      s = fma(x, x, s);
+      const double* e = a.Eta + (size_t)np * h0;
+      for (int p2 = lo; p2 < hi; ++p2) {
+        const double rv = Rg[p + (size_t)np * p2];
+#pragma unroll
+        for (int hh = 0; hh < 4; ++hh)
+          if (hh < nh) x[hh] = fma(rv, e[p2 + (size_t)np * hh], x[hh]);
+      }
     }
-    red[threadIdx.x] = s;
+#pragma unroll
+    for (int hh = 0; hh < 4; ++hh) {
+      double s = x[hh] * x[hh];
+      for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+      if (lane == 0) red[w][hh] = s;
+    }
     __syncthreads();
-    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
-      if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) v[(size_t)g * nf + h] = red[0];
+    if (threadIdx.x < nh)
+      a.work[((size_t)g * nch + chunk) * nf + h0 + threadIdx.x] =
+          (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
     __syncthreads();
   }
+}
+
+__device__ inline double alpha_quad_sum(const SpArgs& a, int g, int h) {
+  const int nch = (a.np + 255) / 256;
+  double v = 0.0;
+  for (int c = 0; c < nch; ++c) v += a.work[((size_t)g * nch + c) * a.nf + h];
+  return v;
 }
 
 // one thread per factor: likelihood over the grid, inverse-CDF categorical draw (R's
@@ -192,20 +211,19 @@ __global__ __launch_bounds__(256) void alpha_quad_kernel(SpArgs a) {
 __global__ __launch_bounds__(64) void alpha_draw_kernel(SpArgs a) {
   const int h = threadIdx.x;
   if (h >= a.nf) return;
-  const double* v = a.work;
   const int G = a.nalpha;
   double mx = -INFINITY;
   for (int g = 0; g < G; ++g) {
-    const double l = log(a.alphapw[G + g]) - 0.5 * a.detWg[g] - 0.5 * v[(size_t)g * a.nf + h];
+    const double l = log(a.alphapw[G + g]) - 0.5 * a.detWg[g] - 0.5 * alpha_quad_sum(a, g, h);
     mx = fmax(mx, l);
   }
   double tot = 0.0;
-  for (int g = 0; g < G; ++g) tot += exp(log(a.alphapw[G + g]) - 0.5 * a.detWg[g] - 0.5 * v[(size_t)g * a.nf + h] - mx);
+  for (int g = 0; g < G; ++g) tot += exp(log(a.alphapw[G + g]) - 0.5 * a.detWg[g] - 0.5 * alpha_quad_sum(a, g, h) - mx);
   const double u = uniforms(a.key, (uint32_t)h, 0, S_ALPHA + LEVEL_STRIDE * a.r, SWEEP_ITER(a)).a * tot;
   double c = 0.0;
   int pick = G;
   for (int g = 0; g < G; ++g) {
-    c += exp(log(a.alphapw[G + g]) - 0.5 * a.detWg[g] - 0.5 * v[(size_t)g * a.nf + h] - mx);
+    c += exp(log(a.alphapw[G + g]) - 0.5 * a.detWg[g] - 0.5 * alpha_quad_sum(a, g, h) - mx);
     if (c > u) {
       pick = g + 1;
       break;
@@ -255,7 +273,7 @@ size_t spatial_work_doubles(const State& s, int r) {
   const size_t nfc = std::max(1, std::min(L.nfmax, s.NFmax));
   const size_t N = (size_t)L.np * nfc;
   const size_t eta = N * N + N + 64 * 64 + nfc * nfc + 64;
-  const size_t alpha = (size_t)L.nalpha * std::max(1, std::min(L.nfmax, s.NFmax));
+  const size_t alpha = (size_t)L.nalpha * ((L.np + 255) / 256) * std::max(1, std::min(L.nfmax, s.NFmax));
   return std::max(eta, alpha) + 64;
 }
 
@@ -265,6 +283,7 @@ void launch_eta_spatial(State& s, int r, uint32_t iter) {
   if (!s.xeta_valid) launch_xeta(s);
   const SpArgs a = sp_args(s, r, iter);
   const int N = L.np * L.nf;
+  ProfScope ps(s, PROF_ETA_SP);
   if (N <= SP_BLOCKED_N) {
     eta_spatial_full_kernel<<<1, 1024, 0, s.stream>>>(a);
     HIP_OK(hipGetLastError());
@@ -279,7 +298,10 @@ void launch_eta_spatial(State& s, int r, uint32_t iter) {
   sp_rhs_kernel<<<g1, 256, 0, s.stream>>>(a, rhs, LDL);
   sp_assemble_kernel<<<dim3(g1, N), 256, 0, s.stream>>>(a, U, LDL);
   HIP_OK(hipGetLastError());
-  dense_potrf_lower(s.stream, U, N, N, ws, s.dev_flags);
+  {
+    ProfScope pc(s, PROF_CHOL);
+    dense_potrf_lower(s.stream, U, N, N, ws, s.dev_flags);
+  }
   dense_trsv_lower(s.stream, U, N, N, rhs, 0);   // backsolve(R, fS, transpose = TRUE)
   sp_noise_kernel<<<g1, 256, 0, s.stream>>>(a, rhs);
   dense_trsv_lower(s.stream, U, N, N, rhs, 1);   // backsolve(R, tmp2)
@@ -292,11 +314,84 @@ void launch_alpha(State& s, uint32_t iter) {
     const Level& L = s.lev[r];
     if (!L.spatial || L.nf == 0) continue;  // rep(1, nf) otherwise (R/updateAlpha.R:81-82)
     const SpArgs a = sp_args(s, r, iter);
-    alpha_quad_kernel<<<L.nalpha, 256, 0, s.stream>>>(a);
+    ProfScope ps(s, PROF_ALPHA);
+    alpha_quad_kernel<<<dim3(L.nalpha, (L.np + 255) / 256), 256, 0, s.stream>>>(a);
     HIP_OK(hipGetLastError());
     alpha_draw_kernel<<<1, 64, 0, s.stream>>>(a);
     HIP_OK(hipGetLastError());
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// the 'Full' alphapw grid on the device (R/computeDataParameters.R:53-81): for every grid
+// point W = exp(-d / alpha) (W = I for alpha = 0), RW = chol(W), detW = 2 sum log diag(RW),
+// iW = chol2inv(RW).  R keeps RiW = chol(iW) (upper); here RiW = RW^-1 with RW the lower
+// factor, which has the same RiW' RiW = iW and quadratic forms, so updateAlpha reads it
+// through riw_lower.  Costs per grid point: chol + trtri + lauum = np^3 flops on MFMA.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sp_w_kernel(double* W, int np, int sdim, const double* crd, const double* dist,
+                                                   double alpha) {
+  const int q = blockIdx.y, p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= np || p < q) return;
+  double d;
+  if (dist) {
+    d = dist[p + (size_t)np * q];
+  } else {  // dist(s): sqrt of the summed squared coordinate differences
+    double s = 0.0;
+    for (int k = 0; k < sdim; ++k) {
+      const double e = crd[p + (size_t)np * k] - crd[q + (size_t)np * k];
+      s += e * e;
+    }
+    d = sqrt(s);
+  }
+  W[p + (size_t)np * q] = exp(-d / alpha);
+}
+
+__global__ __launch_bounds__(256) void sp_logdet_kernel(const double* L, int n, double* out) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) s += log(L[i + (size_t)n * i]);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = 2.0 * red[0];
+}
+
+__global__ __launch_bounds__(256) void sp_identity_kernel(double* A, double* B, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) A[i + (size_t)n * i] = B[i + (size_t)n * i] = 1.0;
+}
+
+void spatial_full_grid(hipStream_t st, int np, int sdim, const double* coords, const double* dist,
+                       const double* alphas, int G, double* iWg, double* RiWg, double* detWg, int* info) {
+  const size_t n2 = (size_t)np * np;
+  const int nbk = (np + 63) / 64;
+  double *W = nullptr, *dinv = nullptr;
+  HIP_OK(hipMalloc(&W, n2 * sizeof(double)));
+  HIP_OK(hipMalloc(&dinv, (size_t)std::max(1, nbk) * 64 * 64 * sizeof(double)));
+  for (int g = 0; g < G; ++g) {
+    double* iW = iWg + n2 * g;
+    double* RiW = RiWg + n2 * g;
+    if (alphas[g] == 0.0) {
+      HIP_OK(hipMemsetAsync(iW, 0, n2 * sizeof(double), st));
+      HIP_OK(hipMemsetAsync(RiW, 0, n2 * sizeof(double), st));
+      HIP_OK(hipMemsetAsync(detWg + g, 0, sizeof(double), st));
+      sp_identity_kernel<<<(np + 255) / 256, 256, 0, st>>>(iW, RiW, np);
+      continue;
+    }
+    sp_w_kernel<<<dim3((np + 255) / 256, np), 256, 0, st>>>(W, np, sdim, coords, dist, alphas[g]);
+    dense_potrf_lower(st, W, np, np, dinv, info);
+    sp_logdet_kernel<<<1, 256, 0, st>>>(W, np, detWg + g);
+    dense_trtri_lower(st, W, np, np, RiW, np, dinv);
+    dense_lauum_lower(st, RiW, np, np, iW, np);
+  }
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipStreamSynchronize(st));
+  HIP_OK(hipFree(W));
+  HIP_OK(hipFree(dinv));
 }
 
 }  // namespace hmsc

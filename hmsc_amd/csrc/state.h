@@ -37,7 +37,7 @@ struct Level {
   double* alphapw = nullptr;    // nalpha x 2
   double* iWg = nullptr;        // np x np x nalpha
   double* RiWg = nullptr;       // np x np x nalpha (upper triangular; lower for NNGP / GPP)
-  int riw_lower = 0;            // spatialMethod 2 / 3: RiWg is lower (Vecchia factor / chol(W)^-1)
+  int riw_lower = 0;            // RiWg lower: NNGP's Vecchia factor, GPP's / the device-built Full grid's chol(W)^-1
   double* detWg = nullptr;      // nalpha
   double* AlphaD = nullptr;     // nfmax: 1-based grid index of each factor (recorded)
   double* spWork = nullptr;     // dense (np nf)^2 Eta system + Alpha likelihoods
@@ -203,7 +203,13 @@ struct State {
   }
 };
 
-enum ProfId { PROF_Z = 0, PROF_ZL = 1, PROF_BL = 2, PROF_ETA_UNIT = 3, PROF_SWEEP = 4, PROF_N = 5 };
+enum ProfId {
+  PROF_Z = 0, PROF_ZL = 1, PROF_BL = 2, PROF_ETA_UNIT = 3, PROF_SWEEP = 4,
+  PROF_ETA_SP = 5,  // spatial updateEta (assembly + blocked Cholesky + solves)
+  PROF_CHOL = 6,    // the blocked Cholesky inside it
+  PROF_ALPHA = 7,   // updateAlpha (grid quadratic forms + draw)
+  PROF_N = 8
+};
 
 struct ProfScope {  // records a start/stop event pair around one launch when profiling is on
   State& s;
@@ -251,6 +257,13 @@ void launch_side_fused(State& s, uint32_t iter);
 // blocked dense fp64 factorisation / solves (dense.hip)
 void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, int* info);
 void dense_trsv_lower(hipStream_t st, const double* L, int n, int lda, double* x, int trans);
+void dense_trtri_lower(hipStream_t st, const double* L, int ldl, int n, double* M, int ldm, double* dinv);
+void dense_lauum_lower(hipStream_t st, const double* M, int ldm, int n, double* out, int ldo);
+// the 'Full' alphapw grid on the device (R/computeDataParameters.R:53-81) from coordinates
+// (np x sdim, column-major) or a distance matrix (np x np): RiWg = chol(W_g)^-1 (lower),
+// iWg = RiWg^T RiWg, detWg = log det W_g
+void spatial_full_grid(hipStream_t st, int np, int sdim, const double* coords, const double* dist,
+                       const double* alphas, int G, double* iWg, double* RiWg, double* detWg, int* info);
 // spatial "Full" levels (spatial.hip)
 size_t spatial_work_doubles(const State& s, int r);
 void launch_eta_spatial(State& s, int r, uint32_t iter);

@@ -57,11 +57,12 @@ def computeDataParameters(hM):
     return par
 
 
-def spatialDataParameters(hM):
-    """rLPar of R/computeDataParameters.R:47-196 ({} for non-spatial levels)."""
+def spatialDataParameters(hM, skip=None):
+    """rLPar of R/computeDataParameters.R:47-196 ({} for non-spatial levels and for levels
+    with skip[r] true)."""
     rLPar = []
     for r, rl in enumerate(hM.rL or []):
-        if not rl.sDim:
+        if not rl.sDim or (skip is not None and skip[r]):
             rLPar.append({})
             continue
         method = rl.spatialMethod

@@ -37,7 +37,12 @@ class ModelBuffers:
     """Column-major copies of the hM fields the sampler consumes (the marshalling the
     R ``.Call`` shim would do), kept alive for the lifetime of the C struct."""
 
-    def __init__(self, hM):
+    def __init__(self, hM, spatial_grid="device"):
+        """spatial_grid: "device" hands 'Full' levels' coordinates / distances to the library,
+        which builds the alphapw grid on the GPU; "host" passes computeDataParameters'
+        arrays (hmsc_amd/dataparams.py) as R's shim could."""
+        if spatial_grid not in ("device", "host"):
+            raise ValueError("spatial_grid must be 'device' or 'host'")
         for rl in hM.rL or []:
             if rl.sDim and rl.spatialMethod not in SPATIAL_CODE:
                 raise ValueError(f"unknown spatialMethod {rl.spatialMethod!r}")
@@ -67,19 +72,28 @@ class ModelBuffers:
         self.nfMin = [int(r.nfMin) for r in rl]
         m.nfMin = L.colmajor_ptr(self.nfMin or [0], k, np.int32)
         m.nfMax = L.colmajor_ptr(self.nfMax or [0], k, np.int32)
-        sdim = [1 if r.sDim else 0 for r in rl]
+        sdim = [(r.s.shape[1] if r.s is not None else 1) if r.sDim else 0 for r in rl]
         m.sDim = L.colmajor_ptr(sdim or [0], k, np.int32)
         m.spatialMethod = L.colmajor_ptr([SPATIAL_CODE[r.spatialMethod] if r.sDim else 0 for r in rl] or [0],
                                          k, np.int32)
         if any(sdim):
             # computeDataParameters' alphapw grid (R/computeDataParameters.R:53-81); the R shim
             # would pass dataParList$rLPar[[r]]$iWg / RiWg / detWg
-            from .dataparams import spatialDataParameters
-            rlp = spatialDataParameters(hM)
+            from .dataparams import _level_order, spatialDataParameters
+            on_device = [bool(lv.sDim) and spatial_grid == "device" and lv.spatialMethod == "Full" for lv in rl]
+            rlp = spatialDataParameters(hM, skip=on_device)
             m.nalpha = L.colmajor_ptr([r.alphapw.shape[0] if r.sDim else 0 for r in rl], k, np.int32)
             for r, lv in enumerate(rl):
-                if lv.sDim:
-                    m.alphapw[r] = L.colmajor_ptr(np.asarray(lv.alphapw, dtype=np.float64), k)
+                if not lv.sDim:
+                    continue
+                m.alphapw[r] = L.colmajor_ptr(np.asarray(lv.alphapw, dtype=np.float64), k)
+                if on_device[r]:
+                    idx = _level_order(hM, r, lv)
+                    if lv.distMat is None:
+                        m.sCoord[r] = L.colmajor_ptr(np.asarray(lv.s, dtype=np.float64)[idx], k)
+                    else:
+                        m.distMat[r] = L.colmajor_ptr(lv.distMat[np.ix_(idx, idx)], k)
+                else:
                     m.iWg[r] = L.colmajor_ptr(rlp[r]["iWg"], k)
                     m.RiWg[r] = L.colmajor_ptr(rlp[r]["RiWg"], k)
                     m.detWg[r] = L.colmajor_ptr(rlp[r]["detWg"], k)
@@ -120,12 +134,13 @@ class Chain:
     """One chain's device-resident state (hmsc_create ... hmsc_destroy)."""
 
     def __init__(self, hM, seed, device=0, updater=None, rank=0, nranks=1, comm_id=None, mask=None,
-                 host_allreduce=None):
+                 host_allreduce=None, spatial_grid="device"):
         """host_allreduce: for a species-sharded chain without RCCL, a callable f(x) that
-        replaces the float64 array x by its sum over all ranks, in place (hmsc_create_sharded_host)."""
+        replaces the float64 array x by its sum over all ranks, in place (hmsc_create_sharded_host).
+        spatial_grid: where a 'Full' level's alphapw grid is evaluated (ModelBuffers)."""
         self.hM = hM
         self.lib = L.lib()
-        self.buf = ModelBuffers(hM)
+        self.buf = ModelBuffers(hM, spatial_grid=spatial_grid)
         self.mask = updater_mask(updater) if mask is None else mask
         h = C.c_void_p()
         if nranks > 1 and host_allreduce is not None:
@@ -253,7 +268,7 @@ class Chain:
     def sync(self):
         L.check(self.lib.hmsc_sync(self.h))
 
-    PROF_IDS = dict(z=0, zl=1, betalambda=2, eta_unit=3, sweep=4)
+    PROF_IDS = dict(z=0, zl=1, betalambda=2, eta_unit=3, sweep=4, eta_spatial=5, chol=6, alpha=7)
 
     def profile(self, enable=True):
         L.check(self.lib.hmsc_profile(self.h, 1 if enable else 0))

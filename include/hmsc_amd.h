@@ -70,7 +70,8 @@ typedef struct hmsc_model {
   const double* b2;
   const int32_t* nfMin;
   const int32_t* nfMax;
-  const int32_t* sDim;    /* > 0: spatial level (see spatialMethod below)     */
+  const int32_t* sDim;    /* > 0: spatial level (see spatialMethod below); the number of
+                           * coordinate columns when sCoord[r] is given             */
   const int32_t* xDim;    /* covariate-dependent levels: must be 0       */
   /* Phylogeny (hM$C; NULL = none).  The grid of R/computeDataParameters.R:19-39
    * (iQg/RQg/detQg over hM$rhopw) is taken in spectral form: the caller passes the
@@ -98,6 +99,14 @@ typedef struct hmsc_model {
   const double* iWg[HMSC_MAX_LEVELS];
   const double* RiWg[HMSC_MAX_LEVELS];
   const double* detWg[HMSC_MAX_LEVELS];
+  /* 'Full' levels may leave iWg / RiWg / detWg NULL and hand over the level's geometry
+   * instead -- the coordinates hM$rL[[r]]$s of its units in unit order (np x sDim[r],
+   * column-major) or their distance matrix (np x np) --: the device then evaluates the grid
+   * itself (dist(), exp(-d/alpha), chol, inverse on the matrix cores), storing
+   * RiWg = chol(W_g)^-1 (lower; RiWg' RiWg = iWg as before).  At np = 5000 this is the
+   * path that fits: two 20 GB grids are built in HBM without a host copy. */
+  const double* sCoord[HMSC_MAX_LEVELS];
+  const double* distMat[HMSC_MAX_LEVELS];
 } hmsc_model;
 
 /* Sampler state = R's parList (R/computeInitialParameters.R:256-270) with iV in
@@ -237,6 +246,14 @@ int hmsc_sync(hmsc_state* s);
  * triangle is scratch), b (may be NULL) by A^-1 b through L^-T L^-1; *info = 1 if A is not
  * positive definite.  Instrumentation of this port, no reference counterpart. */
 int hmsc_dense_chol_solve(int32_t device, double* A, int32_t n, double* b, int32_t* info);
+
+/* computeDataParameters' 'Full' grid (R/computeDataParameters.R:53-81) on the device, for
+ * np units given by coordinates (np x sdim, column-major) or a distance matrix (np x np;
+ * coords NULL) over the G grid values alphas: iWg, RiWg (np*np*G) and detWg (G) exactly as
+ * hmsc_model takes them, RiWg = chol(W_g)^-1 lower triangular.  This is what hmsc_create
+ * runs for a 'Full' level passed by sCoord / distMat. */
+int hmsc_spatial_full_grid(int32_t device, int32_t np, int32_t sdim, const double* coords, const double* dist,
+                           int32_t G, const double* alphas, double* iWg, double* RiWg, double* detWg);
 
 /* Copy a named internal device buffer (fp64) for tests / profiling:
  * "Z", "E", "XEtaTZ", "Gram", "ZTr", "BL", "BL_prec" ... ; n = element count. */

@@ -24,6 +24,10 @@ MODELS = {
     "phylo_td_dims": dict(ny=50, ns=4, nc=3, nf=2, nt=3, seed=21),
     "phylo_mid": dict(ny=120, ns=24, nc=3, nf=2, nt=2, seed=22),
     "phylo_two_levels": dict(ny=90, ns=10, nc=2, nf=2, nr=2, units=[90, 15], seed=23),
+    # (nc + nf) ns above 1024: the multi-workgroup blocked Cholesky path (dense.hip)
+    "phylo_blocked": dict(ny=150, ns=300, nc=3, nf=2, nt=2, seed=25),
+    # config-3 class (vignette_3 scaled to hundreds of species): ns = 300, nf = 15, N = 5400
+    "phylo_cfg3": dict(ny=200, ns=300, nc=3, nf=15, nt=2, seed=26),
 }
 
 

@@ -197,3 +197,20 @@ def test_gpp_knot_on_a_site():
         W = Q + np.diag(1 - np.diag(Q))
         assert np.all(np.isfinite(prod["iWg"][:, :, g]))
         assert rel_err(prod["iWg"][:, :, g] @ W, np.eye(s.shape[0])) < 1e-6, g
+
+
+def test_model_buffers_full_grid_routing():
+    """'Full' levels hand their coordinates (unit order) to the device by default and
+    computeDataParameters' arrays with spatial_grid='host'; NNGP / GPP always pass arrays."""
+    from hmsc_amd.sampler import ModelBuffers
+    hM = _model("Full")
+    b = ModelBuffers(hM)
+    m = b.struct
+    assert bool(m.sCoord[0]) and not bool(m.iWg[0]) and not bool(m.distMat[0])
+    assert m.sDim[0] == hM.rL[0].s.shape[1]
+    h = ModelBuffers(hM, spatial_grid="host").struct
+    assert bool(h.iWg[0]) and bool(h.RiWg[0]) and not bool(h.sCoord[0])
+    g = ModelBuffers(_model("GPP")).struct
+    assert bool(g.iWg[0]) and not bool(g.sCoord[0])
+    with pytest.raises(ValueError):
+        ModelBuffers(hM, spatial_grid="cpu")
