@@ -1270,15 +1270,15 @@ int hmsc_dense_chol_solve(int32_t device, double* A, int32_t n, double* b, int32
     int* dinfo = nullptr;
     HIP_OK(hipMalloc(&dA, nn * sizeof(double)));
     HIP_OK(hipMalloc(&db, (size_t)n * sizeof(double)));
-    HIP_OK(hipMalloc(&ws, 64 * 64 * sizeof(double)));
+    HIP_OK(hipMalloc(&ws, dense_ws_doubles(n) * sizeof(double)));
     HIP_OK(hipMalloc(&dinfo, sizeof(int)));
     HIP_OK(hipMemsetAsync(dinfo, 0, sizeof(int), st));
     HIP_OK(hipMemcpyAsync(dA, A, nn * sizeof(double), hipMemcpyHostToDevice, st));
     if (b) HIP_OK(hipMemcpyAsync(db, b, (size_t)n * sizeof(double), hipMemcpyHostToDevice, st));
     dense_potrf_lower(st, dA, n, n, ws, dinfo);
     if (b) {
-      dense_trsv_lower(st, dA, n, n, db, 0);
-      dense_trsv_lower(st, dA, n, n, db, 1);
+      dense_trsv_lower(st, dA, n, n, db, 0, ws);
+      dense_trsv_lower(st, dA, n, n, db, 1, ws);
       HIP_OK(hipMemcpyAsync(b, db, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, st));
     }
     HIP_OK(hipMemcpyAsync(A, dA, nn * sizeof(double), hipMemcpyDeviceToHost, st));

@@ -29,44 +29,130 @@ constexpr int DB = 64;       // panel / tile size
 constexpr int DLD = DB + 1;  // padded LDS leading dimension
 
 // ---------------------------------------------------------------------------------------
-// 1. diagonal block: L_kk (in place) and Linv = L_kk^-1 (64 x 64, ld 64, zero above)
+// 1. diagonal block: L_kk (in place) and Linv_k = L_kk^-1 (64 x 64, ld 64, zero above)
 // ---------------------------------------------------------------------------------------
+// The block sits in LDS and is factored in four 16-column steps (the serial pivot chain is
+// only ever 16 long inside one wave):
+//   a. wave 0 factors the 16 x 16 diagonal sub-block with one row per lane in registers,
+//      pivots and column entries broadcast by v_readlane (no LDS round trip per pivot), and
+//      inverts it the same way;
+//   b. all 256 threads apply that inverse to the rows below (P = A L16^-T);
+//   c. all 256 threads update the trailing lower triangle (A -= P P^T).
+// L^-1's off-diagonal 16-blocks then follow by diagonal distance,
+//   I_ib,jb = -I_ib,ib sum_{k = jb}^{ib - 1} L_ib,k I_k,jb.
+// Rows / columns past n are identity padding.
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 __global__ __launch_bounds__(256) void chol_diag_kernel(double* A, int lda, int n, int k0, double* Linv, int* info) {
-  __shared__ double T[DB * DLD];
-  __shared__ double I[DB * DLD];
+  __shared__ double T[DB * DLD];  // the block; its lower triangle becomes L
+  __shared__ double I[DB * DLD];  // L^-1 (lower)
+  __shared__ double S[DB * DLD];  // scratch of the L^-1 off-diagonal blocks
   __shared__ int bad;
-  const int nb = min(DB, n - k0), t = threadIdx.x;
+  const int nb = min(DB, n - k0), t = threadIdx.x, lane = t & 63, w = t >> 6;
   if (t == 0) bad = 0;
   for (int p = t; p < DB * DB; p += 256) {
     const int r = p & 63, c = p >> 6;
-    T[r + DLD * c] = (r < nb && c < nb && r >= c) ? A[(size_t)(k0 + r) + (size_t)lda * (k0 + c)] : (r == c ? 1.0 : 0.0);
+    T[r + DLD * c] = (r < nb && c < nb) ? (r >= c ? A[(size_t)(k0 + r) + (size_t)lda * (k0 + c)] : 0.0)
+                                        : (r == c ? 1.0 : 0.0);
+    I[r + DLD * c] = 0.0;
   }
   __syncthreads();
-  for (int c = 0; c < nb; ++c) {  // unblocked right-looking Cholesky in LDS
-    const double d = T[c + DLD * c];
-    if (t == 0 && !(d > 0.0)) bad = 1;
-    const double s = sqrt(d > 0.0 ? d : 1.0), inv = 1.0 / s;
+  for (int kb = 0; kb < 4; ++kb) {
+    const int K0 = 16 * kb;
+    if (w == 0) {  // a. 16 x 16 Cholesky + inverse, row (lane & 15) per lane
+      const int rl = lane & 15;
+      double b[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) b[j] = T[(K0 + rl) + DLD * (K0 + j)];
+      bool nonpd = false;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const double d = readlane_d(b[c], c);
+        nonpd |= !(d > 0.0);
+        const double sq = sqrt(d > 0.0 ? d : 1.0);
+        const double l = b[c] / sq;
+        b[c] = (rl == c) ? sq : l;
+        const double m = (rl > c) ? l : 0.0;
+#pragma unroll
+        for (int j = c + 1; j < 16; ++j) b[j] = fma(-m, readlane_d(m, j), b[j]);
+      }
+      if (nonpd && lane == 0) bad = 1;
+      double dl = 1.0;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) dl = (rl == c) ? b[c] : dl;
+      double x[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) x[j] = (j == rl) ? 1.0 / dl : 0.0;
+#pragma unroll
+      for (int j = 14; j >= 0; --j) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = j + 1; k < 16; ++k) s = fma(x[k], readlane_d(b[j], k), s);
+        const double v = -s / readlane_d(b[j], j);
+        x[j] = (j < rl) ? v : x[j];
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          T[(K0 + rl) + DLD * (K0 + j)] = j <= rl ? b[j] : 0.0;
+          I[(K0 + rl) + DLD * (K0 + j)] = x[j];
+        }
+      }
+    }
     __syncthreads();
-    if (t == 0) T[c + DLD * c] = s;
-    for (int r = c + 1 + t; r < nb; r += 256) T[r + DLD * c] *= inv;
+    const int R0 = K0 + 16, rows = DB - R0;
+    if (rows > 0) {  // b. P[r][j] = sum_{k <= j} A[r][K0 + k] Linv16[j][k]
+      double pv[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int p = t + 256 * q, r = R0 + (p >> 4), j = p & 15;
+        double s = 0.0;
+        if (p < rows * 16)
+          for (int k = 0; k <= j; ++k) s = fma(T[r + DLD * (K0 + k)], I[(K0 + j) + DLD * (K0 + k)], s);
+        pv[q] = s;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int p = t + 256 * q;
+        if (p < rows * 16) T[(R0 + (p >> 4)) + DLD * (K0 + (p & 15))] = pv[q];
+      }
+      __syncthreads();
+      // c. trailing lower triangle: A[r][c] -= sum_k P[r][k] P[c][k]
+      for (int p = t; p < DB * DB; p += 256) {
+        const int r = p & 63, c = p >> 6;
+        if (c >= R0 && r >= c) {
+          double s = 0.0;
+#pragma unroll
+          for (int k = 0; k < 16; ++k) s = fma(T[r + DLD * (K0 + k)], T[c + DLD * (K0 + k)], s);
+          T[r + DLD * c] -= s;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // off-diagonal 16-blocks of L^-1 by diagonal distance
+  for (int dd = 1; dd < 4; ++dd) {
+    const int nblk = 4 - dd;
+    for (int p = t; p < nblk * 256; p += 256) {  // S = sum_{k} L_ib,k I_k,jb
+      const int jb = p >> 8, ib = jb + dd, r = 16 * ib + (p & 15), c = 16 * jb + ((p >> 4) & 15);
+      double s = 0.0;
+      for (int kk = 16 * jb; kk < 16 * ib; ++kk) s = fma(T[r + DLD * kk], I[kk + DLD * c], s);
+      S[r + DLD * c] = s;
+    }
     __syncthreads();
-    const int m = nb - c - 1;  // trailing lower update, (m x m) lower triangle
-    for (int p = t; p < m * m; p += 256) {
-      const int r = c + 1 + p % m, cc = c + 1 + p / m;
-      if (r >= cc) T[r + DLD * cc] -= T[r + DLD * c] * T[cc + DLD * c];
+    for (int p = t; p < nblk * 256; p += 256) {  // I_ib,jb = -I_ib,ib S
+      const int jb = p >> 8, ib = jb + dd, r = 16 * ib + (p & 15), c = 16 * jb + ((p >> 4) & 15);
+      double s = 0.0;
+      for (int kk = 16 * ib; kk <= r; ++kk) s = fma(I[r + DLD * kk], S[kk + DLD * c], s);
+      I[r + DLD * c] = -s;
     }
     __syncthreads();
   }
-  // Linv: thread t < 64 solves column t of L X = I by forward substitution
-  if (t < DB) {
-    for (int i = 0; i < DB; ++i) {
-      double x = (i == t) ? 1.0 : 0.0;
-      if (i >= t)
-        for (int k = t; k < i; ++k) x -= T[i + DLD * k] * I[k + DLD * t];
-      I[i + DLD * t] = i >= t ? x / T[i + DLD * i] : 0.0;
-    }
-  }
-  __syncthreads();
   for (int p = t; p < DB * DB; p += 256) {
     const int r = p & 63, c = p >> 6;
     if (r < nb && c < nb && r >= c) A[(size_t)(k0 + r) + (size_t)lda * (k0 + c)] = T[r + DLD * c];
@@ -120,8 +206,8 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* A, int lda, in
   __shared__ double PI[DB * DLD];
   __shared__ double PJ[DB * DLD];
   const int nb = min(DB, n - k0), base = k0 + nb;
-  const int tI = (int)((sqrt(8.0 * blockIdx.x + 1.0) - 1.0) * 0.5);
-  int ti = tI, tj = (int)blockIdx.x - ti * (ti + 1) / 2;
+  int ti = (int)((sqrt(8.0 * blockIdx.x + 1.0) - 1.0) * 0.5);
+  int tj = (int)blockIdx.x - ti * (ti + 1) / 2;
   if (tj > ti) ++ti, tj = (int)blockIdx.x - ti * (ti + 1) / 2;  // guard sqrt rounding
   if (tj < 0) --ti, tj = (int)blockIdx.x - ti * (ti + 1) / 2;
   const int I0 = base + DB * ti, J0 = base + DB * tj;
@@ -167,68 +253,69 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* A, int lda, in
 }
 
 // ---------------------------------------------------------------------------------------
-// triangular solves with one right-hand side, in place on x (length n)
+// triangular solves with one right-hand side, from the factorization's diagonal-block
+// inverses: one launch per 64-block, every workgroup forming z = Linv_k x_k (or Linv_k^T x_k)
+// -- a 64 x 64 matrix-vector product, no serial substitution -- and then applying its share
+// of the block's update.  The solved block goes to y; the updates go to x -- a block of x is
+// only written by launches of earlier blocks, so no workgroup reads a value another
+// workgroup of its launch writes.
 // ---------------------------------------------------------------------------------------
-// diagonal block: forward L_kk y = x_k, or backward L_kk^T y = x_k (one workgroup)
-__global__ __launch_bounds__(64) void trsv_diag_kernel(const double* L, int lda, int n, int k0, double* x, int trans) {
-  __shared__ double T[DB * DLD];
-  __shared__ double v[DB];
-  const int nb = min(DB, n - k0), t = threadIdx.x;
-  for (int c = 0; c < nb; ++c) T[t + DLD * c] = t < nb ? L[(size_t)(k0 + t) + (size_t)lda * (k0 + c)] : 0.0;
-  v[t] = t < nb ? x[k0 + t] : 0.0;
+__device__ inline void block_solve(const double* Linv, const double* x, int k0, int nb, int trans, double* T,
+                                   double* z, double* part) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  for (int p = t; p < DB * DB; p += 256) T[(p & 63) + DLD * (p >> 6)] = Linv[p];
+  if (t < DB) z[t] = t < nb ? x[k0 + t] : 0.0;
   __syncthreads();
-  if (!trans) {
-    for (int c = 0; c < nb; ++c) {
-      const double xc = v[c] / T[c + DLD * c];
-      __syncthreads();
-      if (t > c && t < nb) v[t] -= T[t + DLD * c] * xc;
-      if (t == c) v[c] = xc;
-      __syncthreads();
-    }
-  } else {
-    for (int c = nb - 1; c >= 0; --c) {
-      const double xc = v[c] / T[c + DLD * c];
-      __syncthreads();
-      if (t < c) v[t] -= T[c + DLD * t] * xc;
-      if (t == c) v[c] = xc;
-      __syncthreads();
-    }
-  }
-  if (t < nb) x[k0 + t] = v[t];
-}
-
-// forward update: x[i] -= sum_{c in block k} L[i, c] x_c for rows i below the block
-__global__ __launch_bounds__(256) void trsv_fwd_update_kernel(const double* L, int lda, int n, int k0, double* x) {
-  __shared__ double xc[DB];
-  const int nb = min(DB, n - k0), t = threadIdx.x;
-  if (t < DB) xc[t] = t < nb ? x[k0 + t] : 0.0;
-  __syncthreads();
-  const int i = k0 + nb + blockIdx.x * 256 + t;
-  if (i >= n) return;
   double s = 0.0;
-  for (int c = 0; c < nb; ++c) s = fma(L[(size_t)i + (size_t)lda * (k0 + c)], xc[c], s);
-  x[i] -= s;
+  for (int c = 16 * w; c < 16 * w + 16; ++c) s = fma(trans ? T[c + DLD * lane] : T[lane + DLD * c], z[c], s);
+  part[w * DB + lane] = s;
+  __syncthreads();
+  if (t < DB) z[t] = (part[t] + part[DB + t]) + (part[2 * DB + t] + part[3 * DB + t]);
+  __syncthreads();
 }
 
-// backward update: x[j] -= sum_{c in block k} L[c, j] x_c for columns j above the block;
-// a workgroup takes 64 columns and reads the 64 x 64 tile L[block k, its columns] coalesced
-__global__ __launch_bounds__(256) void trsv_bwd_update_kernel(const double* L, int lda, int n, int k0, double* x) {
+// forward, block k: z = Linv_k x_k -> y_k; x[i] -= sum_c L[i, k0 + c] z_c for the rows
+// below, 64 rows per workgroup (4 waves x 16 columns, reduced in LDS)
+__global__ __launch_bounds__(256) void trsv_fwd_kernel(const double* L, int lda, int n, int k0, const double* Linv,
+                                                       double* x, double* y) {
   __shared__ double T[DB * DLD];
-  __shared__ double xc[DB];
-  __shared__ double part[4][DB];
-  const int nb = min(DB, n - k0), t = threadIdx.x, j0 = blockIdx.x * DB, cols = min(DB, k0 - j0);
-  if (t < DB) xc[t] = t < nb ? x[k0 + t] : 0.0;
+  __shared__ double z[DB];
+  __shared__ double part[4 * DB];
+  const int nb = min(DB, n - k0), t = threadIdx.x, lane = t & 63, w = t >> 6;
+  block_solve(Linv + (size_t)(k0 / DB) * DB * DB, x, k0, nb, 0, T, z, part);
+  if (blockIdx.x == 0 && t < nb) y[k0 + t] = z[t];
+  const int i = k0 + nb + blockIdx.x * DB + lane;
+  double s = 0.0;
+  if (i < n)
+#pragma unroll 4
+    for (int c = 16 * w; c < min(16 * w + 16, nb); ++c) s = fma(L[(size_t)i + (size_t)lda * (k0 + c)], z[c], s);
+  part[w * DB + lane] = s;
+  __syncthreads();
+  if (w == 0 && i < n) x[i] -= (part[lane] + part[DB + lane]) + (part[2 * DB + lane] + part[3 * DB + lane]);
+}
+
+// backward, block k: z = Linv_k^T x_k -> y_k; x[j] -= sum_c L[k0 + c, j] z_c for the
+// columns j < k0, 64 columns per workgroup read as a coalesced 64 x 64 tile
+__global__ __launch_bounds__(256) void trsv_bwd_kernel(const double* L, int lda, int n, int k0, const double* Linv,
+                                                       double* x, double* y) {
+  __shared__ double T[DB * DLD];
+  __shared__ double z[DB];
+  __shared__ double part[4 * DB];
+  const int nb = min(DB, n - k0), t = threadIdx.x, lane = t & 63, w = t >> 6;
+  block_solve(Linv + (size_t)(k0 / DB) * DB * DB, x, k0, nb, 1, T, z, part);
+  if (blockIdx.x == 0 && t < nb) y[k0 + t] = z[t];
+  const int j0 = blockIdx.x * DB, cols = min(DB, k0 - j0);
+  if (cols <= 0) return;
   for (int p = t; p < DB * DB; p += 256) {
     const int r = p & 63, c = p >> 6;
     T[r + DLD * c] = (r < nb && c < cols) ? L[(size_t)(k0 + r) + (size_t)lda * (j0 + c)] : 0.0;
   }
   __syncthreads();
-  const int c = t & 63, g = t >> 6;
   double s = 0.0;
-  for (int r = g; r < DB; r += 4) s = fma(T[r + DLD * c], xc[r], s);
-  part[g][c] = s;
+  for (int r = w; r < DB; r += 4) s = fma(T[r + DLD * lane], z[r], s);
+  part[w * DB + lane] = s;
   __syncthreads();
-  if (t < cols) x[j0 + t] -= (part[0][t] + part[1][t]) + (part[2][t] + part[3][t]);
+  if (w == 0 && lane < cols) x[j0 + lane] -= (part[lane] + part[DB + lane]) + (part[2 * DB + lane] + part[3 * DB + lane]);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -386,11 +473,13 @@ __global__ __launch_bounds__(256) void lauum_kernel(const double* M, int ldm, in
 // host launchers
 // ---------------------------------------------------------------------------------------
 // M <- L^-1 (lower, zero above; n x n, ld ldm) of the lower-triangular L; `dinv` holds
-// ceil(n / 64) * 64 * 64 doubles
-void dense_trtri_lower(hipStream_t st, const double* L, int ldl, int n, double* M, int ldm, double* dinv) {
+// ceil(n / 64) * 64 * 64 doubles: the diagonal-block inverses, computed here unless
+// have_dinv (dense_potrf_lower's workspace already holds them)
+void dense_trtri_lower(hipStream_t st, const double* L, int ldl, int n, double* M, int ldm, double* dinv,
+                       bool have_dinv) {
   const int nbk = (n + DB - 1) / DB;
   HIP_OK(hipMemset2DAsync(M, sizeof(double) * ldm, 0, sizeof(double) * n, n, st));
-  trtri_diag_kernel<<<nbk, 64, 0, st>>>(L, ldl, n, dinv);
+  if (!have_dinv) trtri_diag_kernel<<<nbk, 64, 0, st>>>(L, ldl, n, dinv);
   for (int k = 0; k < nbk; ++k) {
     trtri_row_kernel<<<k + 1, 256, 0, st>>>(M, ldm, n, k, dinv);
     const int ni = nbk - k - 1;
@@ -407,37 +496,43 @@ void dense_lauum_lower(hipStream_t st, const double* M, int ldm, int n, double* 
 }
 
 // In-place lower Cholesky of the n x n matrix at A (column-major, ld lda; lower triangle
-// read); `ws` >= 64 * 64 doubles; *info (device) is set to 1 if A is not positive definite.
+// read); `ws` holds dense_ws_doubles(n) doubles and keeps the diagonal-block inverses for
+// dense_trsv_lower; *info (device) is set to 1 if A is not positive definite.  (A one-panel
+// look-ahead on a second stream was measured slower: the co-running trailing update more
+// than doubles the one-workgroup diagonal factorization, and the cross-stream joins add
+// ~10 us per panel.)
 void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, int* info) {
   for (int k0 = 0; k0 < n; k0 += DB) {
-    chol_diag_kernel<<<1, 256, 0, st>>>(A, lda, n, k0, ws, info);
+    double* Linv = ws + (size_t)(k0 / DB) * DB * DB;
+    chol_diag_kernel<<<1, 256, 0, st>>>(A, lda, n, k0, Linv, info);
     const int rem = n - (k0 + DB);
     if (rem > 0) {
       const int nt = (rem + DB - 1) / DB;
-      chol_panel_kernel<<<nt, 256, 0, st>>>(A, lda, n, k0, ws);
+      chol_panel_kernel<<<nt, 256, 0, st>>>(A, lda, n, k0, Linv);
       chol_update_kernel<<<nt * (nt + 1) / 2, 256, 0, st>>>(A, lda, n, k0);
     }
   }
   HIP_OK(hipGetLastError());
 }
 
-// x <- L^-1 x  (trans = 0)  or  x <- L^-T x  (trans = 1), L lower (n x n, ld lda)
-void dense_trsv_lower(hipStream_t st, const double* L, int n, int lda, double* x, int trans) {
+// x <- L^-1 x  (trans = 0)  or  x <- L^-T x  (trans = 1), L lower (n x n, ld lda) as left by
+// dense_potrf_lower together with its workspace `ws` (diagonal-block inverses, then n doubles
+// in which the solution is assembled before it is copied back to x)
+void dense_trsv_lower(hipStream_t st, const double* L, int n, int lda, double* x, int trans, double* ws) {
   const int nbk = (n + DB - 1) / DB;
+  double* y = ws + (size_t)nbk * DB * DB;
   if (!trans) {
     for (int b = 0; b < nbk; ++b) {
-      const int k0 = b * DB;
-      trsv_diag_kernel<<<1, 64, 0, st>>>(L, lda, n, k0, x, 0);
-      const int rem = n - (k0 + DB);
-      if (rem > 0) trsv_fwd_update_kernel<<<(rem + 255) / 256, 256, 0, st>>>(L, lda, n, k0, x);
+      const int k0 = b * DB, rem = n - (k0 + DB);
+      trsv_fwd_kernel<<<rem > 0 ? (rem + DB - 1) / DB : 1, 256, 0, st>>>(L, lda, n, k0, ws, x, y);
     }
   } else {
     for (int b = nbk - 1; b >= 0; --b) {
       const int k0 = b * DB;
-      trsv_diag_kernel<<<1, 64, 0, st>>>(L, lda, n, k0, x, 1);
-      if (k0 > 0) trsv_bwd_update_kernel<<<(k0 + DB - 1) / DB, 256, 0, st>>>(L, lda, n, k0, x);
+      trsv_bwd_kernel<<<k0 > 0 ? (k0 + DB - 1) / DB : 1, 256, 0, st>>>(L, lda, n, k0, ws, x, y);
     }
   }
+  HIP_OK(hipMemcpyAsync(x, y, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, st));
   HIP_OK(hipGetLastError());
 }
 

@@ -350,7 +350,7 @@ static PhyloArgs phylo_args(State& s, uint32_t iter) {
 
 size_t phylo_work_doubles(int ns, int Kmax, int nc, int nrho) {
   const size_t N = (size_t)Kmax * ns;
-  const size_t bl = N * N + (size_t)ns * ns + N + (size_t)nc * ns + (size_t)Kmax + 64 * 64 + 64;
+  const size_t bl = N * N + (size_t)ns * ns + N + (size_t)nc * ns + (size_t)Kmax + dense_ws_doubles((int)N) + 64;
   const size_t rho = (size_t)ns + nrho + 64;
   return bl > rho ? bl : rho;
 }
@@ -391,9 +391,9 @@ void launch_beta_lambda_phylo(State& s, uint32_t iter) {
   ph_rhs_kernel<<<g1, 256, 0, s.stream>>>(a);
   HIP_OK(hipGetLastError());
   dense_potrf_lower(s.stream, M, N, N, ws, s.dev_flags + 2);
-  dense_trsv_lower(s.stream, M, N, N, rhs, 0);   // m1 = backsolve(RiU, ., transpose=TRUE)  (:145)
+  dense_trsv_lower(s.stream, M, N, N, rhs, 0, ws);   // m1 = backsolve(RiU, ., transpose=TRUE)  (:145)
   ph_noise_kernel<<<g1, 256, 0, s.stream>>>(a);
-  dense_trsv_lower(s.stream, M, N, N, rhs, 1);   // backsolve(RiU, m1 + rnorm)  (:146)
+  dense_trsv_lower(s.stream, M, N, N, rhs, 1, ws);   // backsolve(RiU, m1 + rnorm)  (:146)
   ph_store_kernel<<<g1, 256, 0, s.stream>>>(a);
   HIP_OK(hipGetLastError());
 }

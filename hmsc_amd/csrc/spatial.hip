@@ -272,7 +272,7 @@ size_t spatial_work_doubles(const State& s, int r) {
   const Level& L = s.lev[r];
   const size_t nfc = std::max(1, std::min(L.nfmax, s.NFmax));
   const size_t N = (size_t)L.np * nfc;
-  const size_t eta = N * N + N + 64 * 64 + nfc * nfc + 64;
+  const size_t eta = N * N + N + dense_ws_doubles((int)N) + nfc * nfc + 64;
   const size_t alpha = (size_t)L.nalpha * ((L.np + 255) / 256) * std::max(1, std::min(L.nfmax, s.NFmax));
   return std::max(eta, alpha) + 64;
 }
@@ -293,7 +293,7 @@ void launch_eta_spatial(State& s, int r, uint32_t iter) {
   double* U = L.spWork;
   double* rhs = U + (size_t)N * N;
   double* ws = rhs + N;
-  double* LDL = ws + 64 * 64;
+  double* LDL = ws + dense_ws_doubles(N);
   const int g1 = (N + 255) / 256;
   sp_rhs_kernel<<<g1, 256, 0, s.stream>>>(a, rhs, LDL);
   sp_assemble_kernel<<<dim3(g1, N), 256, 0, s.stream>>>(a, U, LDL);
@@ -302,9 +302,9 @@ void launch_eta_spatial(State& s, int r, uint32_t iter) {
     ProfScope pc(s, PROF_CHOL);
     dense_potrf_lower(s.stream, U, N, N, ws, s.dev_flags);
   }
-  dense_trsv_lower(s.stream, U, N, N, rhs, 0);   // backsolve(R, fS, transpose = TRUE)
+  dense_trsv_lower(s.stream, U, N, N, rhs, 0, ws);   // backsolve(R, fS, transpose = TRUE)
   sp_noise_kernel<<<g1, 256, 0, s.stream>>>(a, rhs);
-  dense_trsv_lower(s.stream, U, N, N, rhs, 1);   // backsolve(R, tmp2)
+  dense_trsv_lower(s.stream, U, N, N, rhs, 1, ws);   // backsolve(R, tmp2)
   sp_store_kernel<<<g1, 256, 0, s.stream>>>(a, rhs);
   HIP_OK(hipGetLastError());
 }
@@ -368,10 +368,9 @@ __global__ __launch_bounds__(256) void sp_identity_kernel(double* A, double* B, 
 void spatial_full_grid(hipStream_t st, int np, int sdim, const double* coords, const double* dist,
                        const double* alphas, int G, double* iWg, double* RiWg, double* detWg, int* info) {
   const size_t n2 = (size_t)np * np;
-  const int nbk = (np + 63) / 64;
   double *W = nullptr, *dinv = nullptr;
   HIP_OK(hipMalloc(&W, n2 * sizeof(double)));
-  HIP_OK(hipMalloc(&dinv, (size_t)std::max(1, nbk) * 64 * 64 * sizeof(double)));
+  HIP_OK(hipMalloc(&dinv, dense_ws_doubles(np) * sizeof(double)));
   for (int g = 0; g < G; ++g) {
     double* iW = iWg + n2 * g;
     double* RiW = RiWg + n2 * g;
@@ -385,7 +384,7 @@ void spatial_full_grid(hipStream_t st, int np, int sdim, const double* coords, c
     sp_w_kernel<<<dim3((np + 255) / 256, np), 256, 0, st>>>(W, np, sdim, coords, dist, alphas[g]);
     dense_potrf_lower(st, W, np, np, dinv, info);
     sp_logdet_kernel<<<1, 256, 0, st>>>(W, np, detWg + g);
-    dense_trtri_lower(st, W, np, np, RiW, np, dinv);
+    dense_trtri_lower(st, W, np, np, RiW, np, dinv, true);
     dense_lauum_lower(st, RiW, np, np, iW, np);
   }
   HIP_OK(hipGetLastError());

@@ -256,8 +256,11 @@ void launch_beta_lambda_phylo(State& s, uint32_t iter);
 void launch_side_fused(State& s, uint32_t iter);
 // blocked dense fp64 factorisation / solves (dense.hip)
 void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, int* info);
-void dense_trsv_lower(hipStream_t st, const double* L, int n, int lda, double* x, int trans);
-void dense_trtri_lower(hipStream_t st, const double* L, int ldl, int n, double* M, int ldm, double* dinv);
+void dense_trsv_lower(hipStream_t st, const double* L, int n, int lda, double* x, int trans, double* ws);
+void dense_trtri_lower(hipStream_t st, const double* L, int ldl, int n, double* M, int ldm, double* dinv,
+                       bool have_dinv);
+// workspace of dense_potrf_lower + dense_trsv_lower: the 64 x 64 diagonal-block inverses, then n
+inline size_t dense_ws_doubles(int n) { return (size_t)((n + 63) / 64) * 64 * 64 + (size_t)n + 64; }
 void dense_lauum_lower(hipStream_t st, const double* M, int ldm, int n, double* out, int ldo);
 // the 'Full' alphapw grid on the device (R/computeDataParameters.R:53-81) from coordinates
 // (np x sdim, column-major) or a distance matrix (np x np): RiWg = chol(W_g)^-1 (lower),
