@@ -484,7 +484,12 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   // workspaces
   const int n_tiles = (ny + 63) / 64;
   s.ntile_j = (nsl + 31) / 32;
-  s.nchunk = std::max(1, std::min(n_tiles, z_resident_slots(s) / std::max(1, s.ntile_j)));
+  // three rounds of the resident z workgroups: a grid of exactly one round leaves every
+  // workgroup displaced by a concurrent side-stream kernel to run after the round (measured
+  // 142 us vs 104 us per launch at the config-4 size, scripts/z_chunk_sweep.sh)
+  s.nchunk = std::max(1, std::min(n_tiles, 3 * z_resident_slots(s) / std::max(1, s.ntile_j)));
+  if (const char* e = std::getenv("HMSC_Z_CHUNKS"))  // tuning knob: site chunks of the z grid
+    if (std::atoi(e) > 0) s.nchunk = std::max(1, std::min(n_tiles, std::atoi(e)));
   const int n_sblk = (ny + 63) / 64;
   s.zl_split = std::max(1, std::min(std::min(16, (nsl + 3) / 4), (640 + n_sblk - 1) / n_sblk));
   s.XZ = dalloc<double>((size_t)s.Kmax * nsl);

@@ -621,16 +621,28 @@ __device__ inline void wv_kron(double (&o)[NM], int nc, int nt, const double* TT
   }
 }
 
+// Phases (one workgroup of 4 waves; block-wide barriers only between phases):
+//   A  all waves: reduce the species partials, draw the Bartlett factor;
+//   B  wave 0: Vn and iV.  R_S = chol(Vn) (upper) comes from one factorization: with J the
+//      exchange matrix, chol(J (A + V0) J) = M M^T gives A + V0 = (J M J)(J M J)^T and hence
+//      R_S = J M^-1 J -- the same matrix R's chol(chol2inv(chol(A + V0))) forms, up to
+//      rounding, with one factorization and one triangular inverse instead of two and a
+//      product;
+//   C  wave 0: Gamma | iV;  wave 1 (concurrently): Gamma2's iV-only prep.
 template <int NM>
-__global__ __launch_bounds__(256) void gammav_wave_kernel(GVWArgs a) {
-  // S: 3 scratch tiles for products; T0..T3: named tiles (sA aliases T0 during the reduction)
+__device__ __forceinline__ void gammav_body(const GVWArgs& a) {
+  // S: 3 scratch tiles for products (wave 1 in phase C); SG: wave 0's scratch in phase C;
+  // T0..T3: named tiles (sA aliases T0 during the reduction)
   __shared__ __attribute__((aligned(16))) double S[3 * WV_TILE];
+  __shared__ __attribute__((aligned(16))) double SG[WV_TILE];
   __shared__ __attribute__((aligned(16))) double T0[WV_TILE], T1[WV_TILE], T2[WV_TILE], T3[WV_TILE];
   __shared__ double sBTr[32];
+  __shared__ int sok;
   double* sA = T0;
-  const int nc = a.nc, nt = a.nt, N = nc * nt, t = threadIdx.x;
+  const int nc = a.nc, nt = a.nt, N = nc * nt, t = threadIdx.x, w = t >> 6;
   const int nA = nc * nc, nB = nc * nt;
   HMSC_STAMP(0);
+  if (t == 0) sok = 1;
   for (int p = t; p < nA + nB; p += blockDim.x) {
     double sum = 0.0;
 #pragma unroll 8
@@ -641,7 +653,7 @@ __global__ __launch_bounds__(256) void gammav_wave_kernel(GVWArgs a) {
       sBTr[p - nA] = sum;     // B Tr
   }
   // Bartlett factor Zb of rwish (MCMCpack: diag sqrt(chisq(v - i)), upper N(0,1)), drawn by
-  // all 256 threads at once before wave 0 takes over: T3 = Zb padded with I to 32 x 32
+  // all 256 threads at once: T3 = Zb padded with I to 32 x 32
   {
     const double v = a.f0 + a.ns_glob;
     for (int p = t; p < 32 * 32; p += blockDim.x) {
@@ -660,53 +672,58 @@ __global__ __launch_bounds__(256) void gammav_wave_kernel(GVWArgs a) {
   }
   __syncthreads();
   HMSC_STAMP(1);
-  if (t >= 64) return;
+  if (w >= 2 || (w == 1 && !a.do_prep)) return;
   const int i = lane_id();
-  bool ok = true;
   double x[NM], y[NM], z[NM], dinv;
-  // Vn = chol2inv(chol(A + V0)); LV = chol(Vn)   (:19-20)
-  wv_load<NM>(sA, nc, nc, x);
-  ok &= wv_chol<NM>(x, dinv);
-  wv_chol2inv<NM>(x, dinv, y, S);
-  ok &= wv_chol<NM>(y, dinv);  // y = LV
-  HMSC_STAMP(2);
-  // iV = rwish(f0 + ns, Vn) by Bartlett: Zb upper (T3, drawn above), iV = (Zb LV^T)^T (Zb LV^T)
-  HMSC_STAMP(3);
-  wv_to_lds<NM, true, true>(y, S);                    // LV^T
-  wv_mm_lds<NM>(T3, S, x, S + WV_TILE);               // x = T = Zb LV^T
-  wv_gemm<NM, true, false>(x, x, z, S);               // z = iV = T^T T
-  wv_store<NM>(a.iV, nc, nc, z);
-  wv_to_lds<NM>(z, T1);                               // T1 = iV
-  HMSC_STAMP(4);
-  wv_sync();
-  // Gamma | iV: prec = iUGamma + kron(TT, iV), rhs = iUGamma mGamma + vec(iV B Tr)   (:29-31)
-  wv_kron<NM>(x, nc, nt, a.TT, 0.0, nullptr, 0, T1, WV_LD, a.iUGamma);
-  double r = 0.0;
-  if (i < N) {
-    const int c1 = i % nc, t1 = i / nc;
-    r = a.iUmG[i];
-    for (int c2 = 0; c2 < nc; ++c2) r += T1[c1 + WV_LD * c2] * sBTr[c2 + nc * t1];
+  if (w == 0) {
+    bool ok = true;
+    wv_load_rev<NM>(sA, nc, nc, x);                     // J (A + V0) J
+    ok &= wv_chol<NM>(x, dinv);                         // = M M^T
+    wv_inv_lower<NM>(x, dinv, y);                       // M^-1
+    HMSC_STAMP(2);
+    wv_to_lds_rev<NM>(y, nc, S);                        // R_S = J M^-1 J = chol(Vn)
+    // iV = rwish(f0 + ns, Vn) by Bartlett: iV = (Zb R_S)^T (Zb R_S)
+    wv_mm_lds<NM>(T3, S, x, S + WV_TILE);               // x = T = Zb R_S
+    wv_gemm<NM, true, false>(x, x, z, S);               // z = iV = T^T T
+    wv_store<NM>(a.iV, nc, nc, z);
+    wv_to_lds<NM>(z, T1);                               // T1 = iV
+    if (!ok && i == 0) sok = 0;
+    HMSC_STAMP(3);
   }
-  ok &= wv_chol<NM>(x, dinv);
-  wv_forward<NM>(x, dinv, r);
-  if (i < N && !a.noise_zero) r += normal(a.key, (uint32_t)i, 0, S_GAMMAV, SWEEP_ITER(a));
-  wv_transpose<NM, true>(x, y, S);
-  wv_backward_t<NM>(y, dinv, r);
-  if (i < N) a.Gamma[i] = r;
-  HMSC_STAMP(5);
-  if (!ok && i == 0) a.fail[0] = 1;
-  if (!a.do_prep) return;
+  __syncthreads();
+  if (w == 0) {
+    // Gamma | iV: prec = iUGamma + kron(TT, iV), rhs = iUGamma mGamma + vec(iV B Tr)   (:29-31)
+    bool ok = sok != 0;
+    wv_kron<NM>(x, nc, nt, a.TT, 0.0, nullptr, 0, T1, WV_LD, a.iUGamma);
+    double r = 0.0;
+    if (i < N) {
+      const int c1 = i % nc, t1 = i / nc;
+      r = a.iUmG[i];
+      for (int c2 = 0; c2 < nc; ++c2) r += T1[c1 + WV_LD * c2] * sBTr[c2 + nc * t1];
+    }
+    ok &= wv_chol<NM>(x, dinv);
+    wv_forward<NM>(x, dinv, r);
+    if (i < N && !a.noise_zero) r += normal(a.key, (uint32_t)i, 0, S_GAMMAV, SWEEP_ITER(a));
+    wv_transpose<NM, true>(x, y, SG);
+    wv_backward_t<NM>(y, dinv, r);
+    if (i < N) a.Gamma[i] = r;
+    HMSC_STAMP(4);
+    if (!ok && i == 0) a.fail[0] = 1;
+    return;
+  }
 
-  // ---- Gamma2 prep (algebra as in gamma2_prep_kernel) ----
+  // ---- wave 1: Gamma2 prep (algebra as in gamma2_prep_kernel) ----
+  HMSC_STAMP_W(10);
+  wv_from_lds<NM>(T1, z);                               // z = iV
   bool ok2 = true;
-  // iP = inv(iV + XX)                                           z = iV
+  // iP = inv(iV + XX)
   wv_load<NM>(a.XX, nc, nc, x);
 #pragma unroll
   for (int k = 0; k < NM; ++k) x[k] = (i < nc && k < nc) ? x[k] + z[k] : x[k];
   ok2 &= wv_chol<NM>(x, dinv);
   wv_chol2inv<NM>(x, dinv, y, S);                       // y = iP
   wv_to_lds<NM>(y, T2);                                 // T2 = iP
-  HMSC_STAMP(6);
+  HMSC_STAMP_W(11);
   wv_mm_rt<NM>(z, T2, x, S);                            // x = B1 = iV iP
   wv_store<NM>(a.prep + nA, nc, nc, x);
   wv_mm_rt<NM>(x, T1, y, S);                            // y = iV iP iV
@@ -718,7 +735,7 @@ __global__ __launch_bounds__(256) void gammav_wave_kernel(GVWArgs a) {
   ok2 &= wv_chol<NM>(x, dinv);
   wv_chol2inv<NM>(x, dinv, y, S);                       // y = Rm   (:44)
   wv_to_lds<NM>(y, T0);                                 // T0 = Rm
-  HMSC_STAMP(7);
+  HMSC_STAMP_W(12);
   wv_load<NM>(a.V0gXX, nc, nc, x);
   wv_mm_rt<NM>(x, T2, z, S);                            // z = T1m = V0 XX iP
   wv_load<NM>(a.V0g, nc, nc, y);
@@ -736,7 +753,7 @@ __global__ __launch_bounds__(256) void gammav_wave_kernel(GVWArgs a) {
   wv_kron<NM>(z, nc, nt, a.TT, 0.0, nullptr, 0, T3, WV_LD, nullptr);  // z = tmp = TT (x) W1   (:48)
   wv_mm_rt<NM>(z, T0, x, S);                            // x = TR = tmp Rm
   wv_store<NM>(a.prep + 2 * nA, N, N, x);
-  HMSC_STAMP(8);
+  HMSC_STAMP_W(13);
   wv_gemm<NM, false, true>(x, z, y, S);                 // y = tmp Rm tmp^T
   wv_kron<NM>(x, nc, nt, a.TT, 1.0, a.V0g, nc, T2, WV_LD, nullptr);  // x = I (x) V0 + TT (x) M1'
   wv_kron<NM>(z, nc, nt, a.TT, 0.0, nullptr, 0, T2, WV_LD, nullptr); // z = TT (x) M1'
@@ -746,48 +763,54 @@ __global__ __launch_bounds__(256) void gammav_wave_kernel(GVWArgs a) {
   ok2 &= wv_chol<NM>(x, dinv);                          // LSigmaG   (:52)
   wv_store_lower<NM>(a.prep + 2 * nA + N * N, N, N, x);
   if (!ok2 && i == 0) a.fail[1] = 1;
-  HMSC_STAMP(9);
+  HMSC_STAMP_W(14);
 }
 
+template <int NM>
+__global__ __launch_bounds__(256) void gammav_wave_kernel(GVWArgs a) {
+  gammav_body<NM>(a);
+}
+
+static GVWArgs make_gvw_args(State& s, uint32_t iter, const double* part, int np, const uint32_t* iter_dev) {
+  GVWArgs w{};
+  w.nc = s.nc;
+  w.nt = s.nt;
+  w.ns_glob = s.ns;
+  w.nparts = np;
+  w.do_prep = (s.mask & HMSC_UP_GAMMA2) ? 1 : 0;
+  w.part = part;
+  w.V0 = s.V0;
+  w.f0 = s.f0;
+  w.iUGamma = s.iUGamma;
+  w.iUmG = s.iUmG;
+  w.TT = s.phylo ? s.phTTw : s.TT;  // Tr^T iQ Tr with phylogeny (R/updateGammaV.R:29)
+  w.iV = s.iV;
+  w.Gamma = s.Gamma;
+  w.XX = s.XX;
+  w.iV0 = s.iV0;
+  w.V0g = s.V0g;
+  w.V0gXX = s.V0gXX;
+  w.V0gXXV0g = s.V0gXXV0g;
+  w.prep = s.g2prep;
+  w.key = s.key;
+  w.iter = iter;
+  w.iter_dev = iter_dev;
+  w.noise_zero = s.noise_mode;
+  w.fail = s.dev_flags;
+  return w;
+}
 
 static void launch_gammav_wave(State& s, uint32_t iter, hipStream_t st, const double* part, int np,
                                const uint32_t* iter_dev) {
-  const int Ng = s.nc * s.nt;
-  {
-    GVWArgs w{};
-    w.nc = s.nc;
-    w.nt = s.nt;
-    w.ns_glob = s.ns;
-    w.nparts = np;
-    w.do_prep = (s.mask & HMSC_UP_GAMMA2) ? 1 : 0;
-    w.part = part;
-    w.V0 = s.V0;
-    w.f0 = s.f0;
-    w.iUGamma = s.iUGamma;
-    w.iUmG = s.iUmG;
-    w.TT = s.phylo ? s.phTTw : s.TT;  // Tr^T iQ Tr with phylogeny (R/updateGammaV.R:29)
-    w.iV = s.iV;
-    w.Gamma = s.Gamma;
-    w.XX = s.XX;
-    w.iV0 = s.iV0;
-    w.V0g = s.V0g;
-    w.V0gXX = s.V0gXX;
-    w.V0gXXV0g = s.V0gXXV0g;
-    w.prep = s.g2prep;
-    w.key = s.key;
-    w.iter = iter;
-    w.iter_dev = iter_dev;
-    w.noise_zero = s.noise_mode;
-    w.fail = s.dev_flags;
-    switch (wv_bucket(Ng)) {
-      case 8: gammav_wave_kernel<8><<<1, 256, 0, st>>>(w); break;
-      case 16: gammav_wave_kernel<16><<<1, 256, 0, st>>>(w); break;
-      case 24: gammav_wave_kernel<24><<<1, 256, 0, st>>>(w); break;
-      default: gammav_wave_kernel<32><<<1, 256, 0, st>>>(w); break;
-    }
-    HIP_OK(hipGetLastError());
-    if (w.do_prep) s.g2prep_valid = true;
+  const GVWArgs w = make_gvw_args(s, iter, part, np, iter_dev);
+  switch (wv_bucket(s.nc * s.nt)) {
+    case 8: gammav_wave_kernel<8><<<1, 256, 0, st>>>(w); break;
+    case 16: gammav_wave_kernel<16><<<1, 256, 0, st>>>(w); break;
+    case 24: gammav_wave_kernel<24><<<1, 256, 0, st>>>(w); break;
+    default: gammav_wave_kernel<32><<<1, 256, 0, st>>>(w); break;
   }
+  HIP_OK(hipGetLastError());
+  if (w.do_prep) s.g2prep_valid = true;
 }
 
 
@@ -1328,6 +1351,17 @@ __device__ __forceinline__ void delta_body(const LPArgs& a, const double* rs_par
 
 __global__ __launch_bounds__(64) void delta_kernel(LPArgs a, const double* rs_part, int nparts) {
   delta_body(a, rs_part, nparts, blockIdx.x);
+}
+
+// The side stream's whole chain in one launch: workgroup 0 runs updateGammaV (+ Gamma2's
+// prep), workgroups 1..nr the delta chains of updateLambdaPriors -- independent updaters, so
+// neither waits behind the other.
+template <int NM>
+__global__ __launch_bounds__(256) void side_chain_kernel(GVWArgs g, LPArgs lp, const double* rs_part, int nparts) {
+  if (blockIdx.x == 0)
+    gammav_body<NM>(g);
+  else
+    delta_body(lp, rs_part, nparts, blockIdx.x - 1);
 }
 
 constexpr int LP_PARTS = 64;
@@ -1929,12 +1963,19 @@ void launch_side_fused(State& s, uint32_t iter) {
   HIP_OK(hipGetLastError());
   // GammaV algebra on the side stream (reads gv_part; writes Gamma, iV and Gamma2's prep)
   HIP_OK(hipStreamWaitEvent(s.side, s.ev_bl, 0));
-  launch_gammav_wave(s, iter, s.side, s.gv_part, ngv, s.capturing ? s.d_iter_side : nullptr);
-  // the delta chain (reads the psi partials) follows it there
+  // with the delta chains (reading the psi partials) as extra workgroups of the same launch
+  const uint32_t* itd = s.capturing ? s.d_iter_side : nullptr;
+  const GVWArgs gw = make_gvw_args(s, iter, s.gv_part, ngv, itd);
   LPArgs lps = a.lp;
-  lps.iter_dev = s.capturing ? s.d_iter_side : nullptr;
-  delta_kernel<<<s.nr, 64, 0, s.side>>>(lps, s.psi_rs, npsi);
+  lps.iter_dev = itd;
+  switch (wv_bucket(s.nc * s.nt)) {
+    case 8: side_chain_kernel<8><<<1 + s.nr, 256, 0, s.side>>>(gw, lps, s.psi_rs, npsi); break;
+    case 16: side_chain_kernel<16><<<1 + s.nr, 256, 0, s.side>>>(gw, lps, s.psi_rs, npsi); break;
+    case 24: side_chain_kernel<24><<<1 + s.nr, 256, 0, s.side>>>(gw, lps, s.psi_rs, npsi); break;
+    default: side_chain_kernel<32><<<1 + s.nr, 256, 0, s.side>>>(gw, lps, s.psi_rs, npsi); break;
+  }
   HIP_OK(hipGetLastError());
+  if (gw.do_prep) s.g2prep_valid = true;
   s.side_pending |= 1;  // joined (ev_side recorded) by the next join_side
   launch_eta_fused(s, iter, true);
 }

@@ -48,6 +48,18 @@ __device__ inline void wv_load(const double* A, int lda, int n, double (&a)[NM])
   }
 }
 
+// lane i <- row i of J A J (J the exchange matrix of order n), padded with the identity
+template <int NM>
+__device__ inline void wv_load_rev(const double* A, int lda, int n, double (&a)[NM]) {
+  const int i = lane_id();
+  const int ic = i < n ? n - 1 - i : 0;
+#pragma unroll
+  for (int k = 0; k < NM; ++k) {
+    const double v = A[ic + (size_t)lda * (k < n ? n - 1 - k : 0)];
+    a[k] = (i < n && k < n) ? v : (i == k ? 1.0 : 0.0);
+  }
+}
+
 template <int NM>
 __device__ inline void wv_store(double* A, int lda, int n, const double (&a)[NM]) {
   const int i = lane_id();
@@ -67,8 +79,21 @@ __device__ inline void wv_store_lower(double* A, int lda, int n, const double (&
       if (k < n) A[i + (size_t)lda * k] = (k <= i) ? a[k] : 0.0;
 }
 
+// 1 / sqrt(d) for d > 0 to full double precision: the hardware estimate refined by one
+// Newton step (shorter dependency chain than sqrt followed by a division)
+__device__ __forceinline__ double rsqrt_nr(double d) {
+  const double y = __builtin_amdgcn_rsq(d);
+  const double h = 0.5 * d * y;
+  const double r = fma(-h, y, 0.5);  // 0.5 (1 - d y^2)
+  return fma(y, r, y);
+}
+
 // In-place lower Cholesky: lane i ends with L[i][0..i] in a[0..i] and dinv = 1/L[i][i].
-// Returns false (wave-uniformly) when a pivot is not positive.
+// Returns false (wave-uniformly) when a pivot is not positive.  The pivot chain is kept
+// short: the column's entries are broadcast before the pivot's square root is known (the
+// trailing update uses A[i][c] A[j][c] / d), and 1 / L[c][c] comes from a refined
+// reciprocal square root (scripts/ubench_wave.hip: 5.7k vs 10.5k cycles at NM = 24 for the
+// sqrt-then-divide form).
 template <int NM>
 __device__ inline bool wv_chol(double (&a)[NM], double& dinv) {
   const int i = lane_id();
@@ -76,16 +101,39 @@ __device__ inline bool wv_chol(double (&a)[NM], double& dinv) {
   dinv = 1.0;
 #pragma unroll
   for (int c = 0; c < NM; ++c) {
-    const double d = bcast(a[c], c);
-    ok = ok && d > 0.0;
-    const double l = sqrt(d > 0.0 ? d : 1.0);
-    const double inv = 1.0 / l;
-    if (i == c) dinv = inv;
-    a[c] = (i == c) ? l : a[c] * inv;
+    double col[NM];
 #pragma unroll
-    for (int j = c + 1; j < NM; ++j) a[j] = fma(-a[c], bcast(a[c], j), a[j]);
+    for (int j = c; j < NM; ++j) col[j] = bcast(a[c], j);
+    const double d = col[c];
+    ok = ok && d > 0.0;
+    const double inv = rsqrt_nr(d > 0.0 ? d : 1.0);
+    const double sc = a[c] * inv * inv;
+#pragma unroll
+    for (int j = c + 1; j < NM; ++j) a[j] = fma(-sc, col[j], a[j]);
+    if (i == c) dinv = inv;
+    a[c] = (i == c) ? d * inv : a[c] * inv;
   }
   return ok;
+}
+
+// L^{-1} by rows with the L entries broadcast by v_readlane (independent of the unknowns, so
+// they issue ahead of the substitution chain): lane i, X_ij = -(sum_{k > j} X_ik L_kj) / L_jj
+template <int NM>
+__device__ inline void wv_inv_lower_rl(const double (&l)[NM], double dinv, double (&w)[NM]) {
+  const int i = lane_id();
+#pragma unroll
+  for (int k = 0; k < NM; ++k) w[k] = (k == i) ? dinv : 0.0;
+#pragma unroll
+  for (int j = NM - 2; j >= 0; --j) {
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int k = j + 1; k < NM; k += 2) {
+      s0 = fma(w[k], bcast(l[j], k), s0);
+      if (k + 1 < NM) s1 = fma(w[k + 1], bcast(l[j], k + 1), s1);
+    }
+    const double v = -(s0 + s1) * bcast(dinv, j);
+    w[j] = (j < i) ? v : w[j];
+  }
 }
 
 // The same factorisation with LDS broadcasts instead of v_readlane: per column every lane
@@ -176,6 +224,40 @@ __device__ inline void wv_inv_lower(const double (&l)[NM], double dinv, double (
   }
 }
 
+// w <- L^{-1} by rows (lane i: row i), L staged once in wave-private LDS (column-major,
+// ld NM + 1, the diagonal slot holding 1 / L[i][i]); row i by substitution along the row,
+// X_ij = -(sum_{k > j} X_ik L_kj) / L_jj, every L entry read at a uniform address (an LDS
+// broadcast, no cross-lane register traffic), two partial sums per dot product.
+// lds: NM * (NM + 1) doubles.
+template <int NM>
+__device__ inline void wv_inv_lower_rows(const double (&l)[NM], double dinv, double (&w)[NM], double* lds) {
+  constexpr int LD = NM + 1;
+  const int i = lane_id();
+  if (i < NM) {
+#pragma unroll
+    for (int k = 0; k < NM; ++k) lds[i + LD * k] = (k < i) ? l[k] : (k == i ? dinv : 0.0);  // L[i][k]
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int k = 0; k < NM; ++k) w[k] = (k == i) ? dinv : 0.0;
+#pragma unroll
+  for (int j = NM - 2; j >= 0; --j) {
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int k = j + 1; k < NM; k += 2) {
+      s0 = fma(w[k], lds[k + LD * j], s0);
+      if (k + 1 < NM) s1 = fma(w[k + 1], lds[k + 1 + LD * j], s1);
+    }
+    const double v = -(s0 + s1) * lds[j + LD * j];
+    w[j] = (j < i) ? v : w[j];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Columns of L^{-1}: lane i ends with column i of L^{-1} (w[r] = Linv[r][i]; zero for r < i).
 // L is staged once in LDS; every lane then forward-substitutes its own unit vector reading
 // L at uniform addresses (broadcasts) -- no cross-lane register traffic.  lds: scratch of
@@ -233,6 +315,21 @@ __device__ inline void wv_to_lds(const double (&a)[NM], double* lds) {
         lds[k + WV_LD * i] = v;  // element (k, i) of a^T
       else
         lds[i + WV_LD * k] = v;  // element (i, k)
+    }
+}
+
+// lds <- blockdiag(J w_n J, I) zero-padded to 32 x 32, w an embedded blockdiag(w_n, I)
+// by rows (J the exchange matrix of order n)
+template <int NM>
+__device__ inline void wv_to_lds_rev(const double (&w)[NM], int n, double* lds) {
+  const int i = lane_id();
+  if (i < 32)
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      if (i < n && k < n)
+        lds[(n - 1 - i) + WV_LD * (n - 1 - k)] = w[k < NM ? k : 0];
+      else
+        lds[i + WV_LD * k] = (i == k && i < NM) ? 1.0 : 0.0;
     }
 }
 
@@ -303,6 +400,21 @@ template <int NM>
 __device__ inline void wv_chol2inv(const double (&l)[NM], double dinv, double (&c)[NM], double* lds) {
   double w[NM];
   wv_inv_lower<NM>(l, dinv, w);
+  wv_syrk_tn_lower<NM>(w, c, lds);
+}
+
+template <int NM>
+__device__ inline void wv_chol2inv_rl(const double (&l)[NM], double dinv, double (&c)[NM], double* lds) {
+  double w[NM];
+  wv_inv_lower_rl<NM>(l, dinv, w);
+  wv_syrk_tn_lower<NM>(w, c, lds);
+}
+
+// chol2inv through wv_inv_lower_rows (L staged in the third scratch tile)
+template <int NM>
+__device__ inline void wv_chol2inv_rows(const double (&l)[NM], double dinv, double (&c)[NM], double* lds) {
+  double w[NM];
+  wv_inv_lower_rows<NM>(l, dinv, w, lds + 2 * WV_TILE);
   wv_syrk_tn_lower<NM>(w, c, lds);
 }
 

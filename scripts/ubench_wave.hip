@@ -51,6 +51,45 @@ __global__ __launch_bounds__(64) void k_inv(const double* A, int n, int reps, do
 }
 
 template <int NM>
+__global__ __launch_bounds__(64) void k_inv2(const double* A, int n, int reps, double* out, long long* cyc) {
+  __shared__ double lds[3 * WV_TILE];
+  double l[NM], c[NM], dinv;
+  wv_load<NM>(A, n, n, l);
+  wv_chol<NM>(l, dinv);
+  const long long t0 = clock64();
+  for (int r = 0; r < reps; ++r) wv_chol2inv_rows<NM>(l, dinv, c, lds);
+  const long long t1 = clock64();
+  wv_store<NM>(out, n, n, c);
+  if (threadIdx.x == 0) *cyc = (t1 - t0) / reps;
+}
+
+template <int NM>
+__global__ __launch_bounds__(64) void k_inv3(const double* A, int n, int reps, double* out, long long* cyc) {
+  __shared__ double lds[3 * WV_TILE];
+  double l[NM], c[NM], dinv;
+  wv_load<NM>(A, n, n, l);
+  wv_chol<NM>(l, dinv);
+  const long long t0 = clock64();
+  for (int r = 0; r < reps; ++r) wv_chol2inv_rl<NM>(l, dinv, c, lds);
+  const long long t1 = clock64();
+  wv_store<NM>(out, n, n, c);
+  if (threadIdx.x == 0) *cyc = (t1 - t0) / reps;
+}
+
+template <int NM>
+__global__ __launch_bounds__(64) void k_chol_f(const double* A, int n, int reps, double* out, long long* cyc) {
+  double l[NM], dinv;
+  const long long t0 = clock64();
+  for (int r = 0; r < reps; ++r) {
+    wv_load<NM>(A, n, n, l);
+    wv_chol<NM>(l, dinv);
+  }
+  const long long t1 = clock64();
+  wv_store_lower<NM>(out, n, n, l);
+  if (threadIdx.x == 0) *cyc = (t1 - t0) / reps;
+}
+
+template <int NM>
 __global__ __launch_bounds__(64) void k_gemm(const double* A, const double* B, int n, int reps, double* out,
                                              long long* cyc) {
   __shared__ double lds[3 * WV_TILE];
@@ -140,6 +179,36 @@ static void run(int n, double* dA, double* dB, double* dO, double* db, long long
       for (int k = 0; k < n; ++k) s += A[i + n * k] * O[k + n * j];
       e_inv = std::fmax(e_inv, std::fabs(s - (i == j)));
     }
+  long long cy_inv2 = 0;
+  hipLaunchKernelGGL(k_inv2<NM>, dim3(1), dim3(64), 0, 0, dA, n, reps, dO, dc);
+  CK(hipMemcpy(&cy_inv2, dc, 8, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(O.data(), dO, n * n * 8, hipMemcpyDeviceToHost));
+  double e_inv2 = 0;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      double s = 0;
+      for (int k = 0; k < n; ++k) s += A[i + n * k] * O[k + n * j];
+      e_inv2 = std::fmax(e_inv2, std::fabs(s - (i == j)));
+    }
+  printf("  chol2inv_rows=%lld cycles err=%.1e\n", cy_inv2, e_inv2);
+  hipLaunchKernelGGL(k_inv3<NM>, dim3(1), dim3(64), 0, 0, dA, n, reps, dO, dc);
+  CK(hipMemcpy(&cy_inv2, dc, 8, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(O.data(), dO, n * n * 8, hipMemcpyDeviceToHost));
+  e_inv2 = 0;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      double s = 0;
+      for (int k = 0; k < n; ++k) s += A[i + n * k] * O[k + n * j];
+      e_inv2 = std::fmax(e_inv2, std::fabs(s - (i == j)));
+    }
+  printf("  chol2inv_rl=%lld cycles err=%.1e\n", cy_inv2, e_inv2);
+  hipLaunchKernelGGL(k_chol_f<NM>, dim3(1), dim3(64), 0, 0, dA, n, reps, dO, dc);
+  CK(hipMemcpy(&cy_inv2, dc, 8, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(O.data(), dO, n * n * 8, hipMemcpyDeviceToHost));
+  e_inv2 = 0;
+  for (int j = 0; j < n; ++j)
+    for (int i = j; i < n; ++i) e_inv2 = std::fmax(e_inv2, std::fabs(O[i + n * j] - L[i + n * j]));
+  printf("  chol_fast=%lld cycles err=%.1e\n", cy_inv2, e_inv2);
   hipLaunchKernelGGL(k_gemm<NM>, dim3(1), dim3(64), 0, 0, dA, dB, n, reps, dO, dc);
   CK(hipMemcpy(&cy[2], dc, 8, hipMemcpyDeviceToHost));
   CK(hipMemcpy(O.data(), dO, n * n * 8, hipMemcpyDeviceToHost));
