@@ -95,7 +95,28 @@ def build(force=False, verbose=True, stamps=False, jobs=None):
             print(" ".join(link), flush=True)
         subprocess.check_call(link)
         _stamp(lib, ldg)
+    if not stamps:
+        build_shim(force=force, verbose=verbose)
     return lib
+
+
+def build_shim(force=False, verbose=True):
+    """tests/capi/shim_run: the INTEGRATION.md .Call shim as a plain C program, gcc against
+    include/hmsc_amd.h, linked to the in-tree library (tests/test_gpu_capi_c.py)."""
+    root = os.path.dirname(HERE)
+    src = os.path.join(root, "tests", "capi", "shim_run.c")
+    out = os.path.join(root, "tests", "capi", "shim_run")
+    if not os.path.exists(src):
+        return None
+    cmd = ["gcc", "-std=c99", "-O2", "-Wall", "-Wextra", "-I", os.path.join(root, "include"), src, "-L", HERE,
+           "-lhmsc_amd", "-Wl,-rpath,$ORIGIN/../../hmsc_amd", "-o", out]
+    dg = _digest([src, os.path.join(root, "include", "hmsc_amd.h")], cmd)
+    if force or not _fresh(out, dg):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+        _stamp(out, dg)
+    return out
 
 
 if __name__ == "__main__":

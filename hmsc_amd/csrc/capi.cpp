@@ -497,14 +497,15 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.G = dalloc<double>((size_t)s.Kmax * s.Kmax);
   s.ZTr = dalloc<double>((size_t)ny * nt);
   s.XZ_part = dalloc<double>((size_t)s.nchunk * s.Kmax * nsl);
-  s.G_part = dalloc<double>((size_t)std::max(std::max(s.nchunk, 64), (ny + 31) / 32) * s.Kmax * s.Kmax);
+  s.G_part = dalloc<double>(std::max((size_t)std::max(std::max(s.nchunk, 64), (ny + 31) / 32) * s.Kmax * s.Kmax,
+                                      (size_t)((ny + 15) / 16) * s.Kmax * std::max(1, s.NFmax)));
   s.ZTr_part = dalloc<double>((size_t)s.ntile_j * ny * nt);
   const int nfm = std::max(1, s.NFmax);
   s.ZL = dalloc<double>((size_t)ny * nfm);
   s.ZL_part = dalloc<double>((size_t)s.zl_split * ny * nfm);
   s.CR = dalloc<double>((size_t)s.Kmax * nfm);
   s.CR_part = dalloc<double>((size_t)((nsl + 31) / 32) * s.Kmax * nfm);
-  s.LS = dalloc<double>((size_t)nfm * nsl);
+  s.LS = dalloc<double>((size_t)std::max(nfm, 16) * nsl);  // [species][16] (cr_body)
   s.scratch_doubles = 1 << 20;
   s.scratch = dalloc<double>(s.scratch_doubles);
   s.scratch2 = dalloc<double>(s.scratch_doubles);

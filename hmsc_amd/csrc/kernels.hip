@@ -1489,10 +1489,10 @@ __device__ __forceinline__ void cr_body(const double* BL, const double* iSigma, 
     (void)jj;
   }
   __syncthreads();
-  if (LS)
-    for (int p = t; p < NF * nj; p += 256) {
-      const int f = p % NF, jj = p / NF;
-      LS[f + (size_t)NF * (j0 + jj)] = sX[nc + f + K * jj] * iSigma[j0 + jj];
+  if (LS)  // [species][16], zero past NF (<= 16): the fused Eta kernel's MFMA B operand
+    for (int p = t; p < 16 * nj; p += 256) {
+      const int f = p & 15, jj = p >> 4;
+      LS[f + (size_t)16 * (j0 + jj)] = f < NF ? sX[nc + f + K * jj] * iSigma[j0 + jj] : 0.0;
     }
   double* out = CR_part + (size_t)bid * slab;
   for (int p = t; p < K * NF; p += 256) {
@@ -1690,26 +1690,28 @@ __global__ __launch_bounds__(64) void eta_na_row_kernel(EtaView ev, int r, int n
 
 // ---------------------------------------------------------------------------
 // Fused updateEta for the common case -- one random level with np == ny (one row per
-// unit), no NA, one rank (R/updateEta.R:42-57).  One 1024-thread workgroup per 32-site tile:
-//   1. ZL_i = sum_j Z_ij LS_j, LS = Lambda diag(iSigma)  (:55): the 16 waves stream every
-//      32nd species pair (coalesced 256-B site runs), then an LDS tree reduction
+// unit), no NA, one rank (R/updateEta.R:42-57).  One 256-thread workgroup per 16-site tile:
+//   1. ZL_i = sum_j Z_ij LS_j, LS = Lambda diag(iSigma)  (:55), on the matrix cores: wave w
+//      takes every 4th group of 4 species, A = Z (16 sites x 4 species, loaded straight from
+//      HBM as 128-B site runs), B = LS (4 species x 16 factors, from L2); the 4 waves'
+//      partials meet in LDS
 //   2. b_i = ZL_i - sum_{k < nc} XEta_ik CR_k  (the residual S of :31-37), and the noise
 //      xi_q for q = Pi_i (:56), one (site, factor) pair per thread
 //   3. eta_q = L^-T (L^-1 b_i + xi_q), L = chol(I + Lambda diag(iSigma) Lambda^T) (:45-56),
 //      factored once per tile by wave 0
 //   4. the tile's XEta rows get the new Eta (R/updateBetaLambda.R:21-41 of the next sweep)
-//      and the tile's Gram partial XEta^T XEta (:65) goes to G_part[tile]
+//      and the tile's Gram partial Eta^T XEta (nf x K; X^T X is constant) goes to G_part[tile]
 // This replaces zl_kernel + eta_shared_kernel + xeta_gram_kernel (and their Z / XEta
 // re-reads) with one pass over Z.
 // ---------------------------------------------------------------------------
 struct EtaFArgs {
   const double* Z;
-  const double* LS;   // NF x ns_loc
+  const double* LS;   // ns_loc x 16: Lambda diag(iSigma), zero past nf (cr_body)
   const double* CR;   // Kmax x NF (ld ldcr): BL diag(iSigma) Lambda^T
   double* XEta;       // ny x K (ld ny)
   const int* Pi;      // ny: unit of each row (0-based)
   double* Eta;        // np x nf
-  double* G_part;     // [tile][Kmax x Kmax]
+  double* G_part;     // [tile][K x nf]  (Eta^T XEta partial, ld Kmax)
   int ny, ns_loc, K, Kmax, nc, nf, np, ldcr;
   Key key;
   uint32_t iter;
@@ -1718,23 +1720,21 @@ struct EtaFArgs {
   unsigned long long* kt;    // live launch timing (KT_ETA block) or null
 };
 
-constexpr int EF_SITES = 32;
+constexpr int EF_SITES = 16;
 
 template <int NFB>
-__global__ __launch_bounds__(512) void eta_fused_kernel(EtaFArgs a) {
-  __shared__ double red[8][NFB][64];
-  __shared__ double sL[NFB * NFB];           // lower factor of Q (column-major)
+__global__ __launch_bounds__(256) void eta_fused_kernel(EtaFArgs a) {
+  __shared__ double sPart[4][16][EF_SITES + 1];  // [wave][factor][site] ZL partials
+  __shared__ double sL[NFB * NFB];            // lower factor of Q (column-major, ld nf)
   __shared__ double sB[NFB][EF_SITES], sXi[NFB][EF_SITES];
   __shared__ double sX[64][EF_SITES + 1];     // XEta tile [k][site] (K <= 64)
   __shared__ double sCR[64 * NFB];            // CR[k][h], k < K
   const unsigned long long kt0 = a.kt ? kt_now() : 0ull;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int ny = a.ny, nf = a.nf, K = a.K, nc = a.nc;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, lm = lane & 15, lk = lane >> 4;
+  const int ny = a.ny, nf = a.nf, K = a.K, nc = a.nc, ns = a.ns_loc;
   const int i0 = blockIdx.x * EF_SITES;
-  const int sl = lane & 31, hf = lane >> 5;
-  const int i = i0 + sl;
   if (blockIdx.x == 0) HMSC_STAMP(50);
-  // ---- stage 1: ZL partials (every wave), Q factor (wave 0 first)
+  // ---- stage 1: Q factor (wave 0 first), ZL on the matrix cores (every wave)
   if (w == 0) {
     double q[NFB], dinv;
     const int r = lane < nf ? lane : 0;
@@ -1749,59 +1749,42 @@ __global__ __launch_bounds__(512) void eta_fused_kernel(EtaFArgs a) {
       for (int c = 0; c < NFB; ++c)
         if (c < nf) sL[lane + nf * c] = (c <= lane) ? q[c] : 0.0;
   }
-  for (int p = t; p < K * nf; p += 512) {
+  for (int p = t; p < K * nf; p += 256) {
     const int k = p % K, h = p / K;
     sCR[k * NFB + h] = a.CR[k + (size_t)a.ldcr * h];
   }
-  double acc[NFB];
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  const double* zc = a.Z + min(i0 + lm, ny - 1);  // sites past ny: any finite row, unused
+  // species j = 16 s + 4 w + lk; B = LS[j][lm] straight from L2 (128 KB, shared by every
+  // workgroup); eight steps' loads issued before their MFMAs
+  const int nsteps = (ns + 15) >> 4;
+  int s = 0;
+  for (; s + 8 <= nsteps; s += 8) {
+    double zv[8], lv[8];
 #pragma unroll
-  for (int h = 0; h < NFB; ++h) acc[h] = 0.0;
-  // LS is staged through LDS in chunks of EF_CHUNK species (aliasing the reduction buffer,
-  // which is free until the end of stage 1); the waves read it back as broadcasts
-  constexpr int EF_CHUNK = 8 * 64;
-  double* sLS = &red[0][0][0];  // [jj][NFB]
-  const double* zc = a.Z + (i < ny ? i : 0);
-  for (int c0 = 0; c0 < a.ns_loc; c0 += EF_CHUNK) {
-    const int nj = min(EF_CHUNK, a.ns_loc - c0);
-    __syncthreads();
-    for (int p = t; p < nj * nf; p += 512) {
-      const int h = p % nf, jj = p / nf;
-      sLS[jj * NFB + h] = a.LS[(size_t)nf * (c0 + jj) + h];
+    for (int u = 0; u < 8; ++u) {
+      const int j = 16 * (s + u) + 4 * w + lk;
+      zv[u] = j < ns ? zc[(size_t)ny * j] : 0.0;
+      lv[u] = j < ns ? a.LS[(size_t)16 * j + lm] : 0.0;
     }
-    __syncthreads();
-    if (i < ny) {
-      int jj = 2 * w + hf;
-      for (; jj + 48 < nj; jj += 64) {
-        const double z0 = zc[(size_t)ny * (c0 + jj)], z1 = zc[(size_t)ny * (c0 + jj + 16)];
-        const double z2 = zc[(size_t)ny * (c0 + jj + 32)], z3 = zc[(size_t)ny * (c0 + jj + 48)];
-        const double* l0 = sLS + jj * NFB;
 #pragma unroll
-        for (int h = 0; h < NFB; ++h)
-          if (h < nf)
-            acc[h] = fma(z3, l0[h + 48 * NFB],
-                         fma(z2, l0[h + 32 * NFB], fma(z1, l0[h + 16 * NFB], fma(z0, l0[h], acc[h]))));
-      }
-      for (; jj < nj; jj += 16) {
-        const double z0 = zc[(size_t)ny * (c0 + jj)];
-        const double* l0 = sLS + jj * NFB;
-#pragma unroll
-        for (int h = 0; h < NFB; ++h)
-          if (h < nf) acc[h] = fma(z0, l0[h], acc[h]);
-      }
-    }
+    for (int u = 0; u < 8; ++u) acc = mfma_f64(zv[u], lv[u], acc);
   }
-  __syncthreads();  // red is the reduction buffer again
-  if (blockIdx.x == 0) HMSC_STAMP(51);
+  for (; s < nsteps; ++s) {
+    const int j = 16 * s + 4 * w + lk;
+    const double zv = j < ns ? zc[(size_t)ny * j] : 0.0;
+    const double lv = j < ns ? a.LS[(size_t)16 * j + lm] : 0.0;
+    acc = mfma_f64(zv, lv, acc);
+  }
+  // acc[r] = partial ZL[site lk + 4 r][factor lm]
 #pragma unroll
-  for (int h = 0; h < NFB; ++h) red[w][h][lane] = acc[h];
+  for (int r = 0; r < 4; ++r) sPart[w][lm][lk + 4 * r] = acc[r];
   __syncthreads();
-  if (blockIdx.x == 0) HMSC_STAMP(52);
+  if (blockIdx.x == 0) HMSC_STAMP(51);
   // ---- stage 2: b = ZL - X CR_x, and the noise, one (site, factor) per thread
   if (t < EF_SITES * nf) {
     const int s2 = t % EF_SITES, h = t / EF_SITES, ii = i0 + s2;
-    double zl = 0.0;
-#pragma unroll
-    for (int g = 0; g < 8; ++g) zl += red[g][h][s2] + red[g][h][s2 + 32];
+    const double zl = (sPart[0][h][s2] + sPart[1][h][s2]) + (sPart[2][h][s2] + sPart[3][h][s2]);
     double corr = 0.0, xi = 0.0;
     if (ii < ny) {
       for (int k = 0; k < nc; ++k) corr = fma(a.XEta[ii + (size_t)ny * k], sCR[k * NFB + h], corr);
@@ -1811,7 +1794,7 @@ __global__ __launch_bounds__(512) void eta_fused_kernel(EtaFArgs a) {
     sXi[h][s2] = xi;
   }
   // X columns of the tile into the Gram tile
-  for (int p = t; p < nc * EF_SITES; p += 512) {
+  for (int p = t; p < nc * EF_SITES; p += 256) {
     const int s2 = p % EF_SITES, k = p / EF_SITES, ii = i0 + s2;
     sX[k][s2] = ii < ny ? a.XEta[ii + (size_t)ny * k] : 0.0;
   }
@@ -1859,14 +1842,14 @@ __global__ __launch_bounds__(512) void eta_fused_kernel(EtaFArgs a) {
   }
   __syncthreads();
   if (blockIdx.x == 0) HMSC_STAMP(54);
-  // ---- stage 4: Gram partial of the tile
-  double* dst = a.G_part + (size_t)blockIdx.x * a.Kmax * a.Kmax;
-  for (int p = t; p < K * K; p += 512) {
-    const int k1 = p % K, k2 = p / K;
+  // ---- stage 4: Gram partial of the tile's Eta rows, Eta^T XEta (nf x K, ld Kmax)
+  double* dst = a.G_part + (size_t)blockIdx.x * a.Kmax * nf;
+  for (int p = t; p < K * nf; p += 256) {
+    const int k = p % K, h = p / K;
     double g = 0.0;
-#pragma unroll 8
-    for (int s2 = 0; s2 < EF_SITES; ++s2) g = fma(sX[k1][s2], sX[k2][s2], g);
-    dst[k1 + a.Kmax * k2] = g;
+#pragma unroll
+    for (int s2 = 0; s2 < EF_SITES; ++s2) g = fma(sX[nc + h][s2], sX[k][s2], g);
+    dst[k + a.Kmax * h] = g;
   }
   if (blockIdx.x == 0) HMSC_STAMP(55);
   if (a.kt) {
@@ -1980,6 +1963,33 @@ void launch_side_fused(State& s, uint32_t iter) {
   launch_eta_fused(s, iter, true);
 }
 
+// G = XEta^T XEta after the fused Eta pass: the X^T X block is the constant s.XX, the Eta
+// rows the sum of the tiles' partials G_part[tile][k + Kmax h] in tile order (deterministic).
+// Workgroup b: outputs 64 b .. 64 b + 63 of the K x nf slab (lane = output), the 4 waves
+// taking every 4th tile, combined in LDS; written to both (k, nc + h) and (nc + h, k).
+__global__ __launch_bounds__(256) void g_eta_reduce_kernel(const double* part, int ntile, int K, int Kmax, int nc,
+                                                           int nf, const double* XX, double* G) {
+  __shared__ double red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, o = blockIdx.x * 64 + lane;
+  const int k = o % K, h = o / K;
+  const size_t stride = (size_t)Kmax * nf;
+  double s = 0.0;
+  if (o < K * nf) {
+    const double* p = part + k + (size_t)Kmax * h;
+#pragma unroll 8
+    for (int b = w; b < ntile; b += 4) s += p[stride * b];
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && o < K * nf) {
+    const double v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    G[k + (size_t)Kmax * (nc + h)] = v;
+    G[(nc + h) + (size_t)Kmax * k] = v;
+  }
+  if (blockIdx.x == 0)
+    for (int p = threadIdx.x; p < nc * nc; p += 256) G[p % nc + (size_t)Kmax * (p / nc)] = XX[p];
+}
+
 static bool eta_fused_ok(const State& s) {
   return s.nranks == 1 && s.nr == 1 && !s.lev[0].spatial && s.n_na_rows == 0 && s.lev[0].np == s.ny && s.lev[0].uniform_n == 1 &&
          s.lev[0].nf <= 16 && s.K <= 64 && s.LS != nullptr && !getenv_flag("HMSC_NO_ETA_FUSION");
@@ -2021,15 +2031,14 @@ static void launch_eta_fused(State& s, uint32_t iter, bool cr_done = false) {
   {
     ProfScope ps(s, PROF_ETA_UNIT);
     if (L.nf <= 8)
-      eta_fused_kernel<8><<<ntile, 512, 0, s.stream>>>(a);
-    else if (L.nf <= 12)  // 80 KB of LDS: two workgroups per CU
-      eta_fused_kernel<12><<<ntile, 512, 0, s.stream>>>(a);
+      eta_fused_kernel<8><<<ntile, 256, 0, s.stream>>>(a);
+    else if (L.nf <= 12)
+      eta_fused_kernel<12><<<ntile, 256, 0, s.stream>>>(a);
     else
-      eta_fused_kernel<16><<<ntile, 512, 0, s.stream>>>(a);
+      eta_fused_kernel<16><<<ntile, 256, 0, s.stream>>>(a);
     HIP_OK(hipGetLastError());
   }
-  const int64_t nG = (int64_t)s.Kmax * s.Kmax;
-  slab_sum_kernel<<<grid_for(nG), 256, 0, s.stream>>>(s.G_part, s.G, nG, ntile, nG);
+  g_eta_reduce_kernel<<<(s.K * L.nf + 63) / 64, 256, 0, s.stream>>>(s.G_part, ntile, s.K, s.Kmax, s.nc, L.nf, s.XX, s.G);
   HIP_OK(hipGetLastError());
   s.zt_valid = false;   // Eta changed: XZ is stale until the next updateZ
   s.xeta_valid = true;  // XEta rows and G rewritten above
