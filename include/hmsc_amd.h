@@ -224,7 +224,8 @@ int hmsc_run_verbose(hmsc_state* s, int32_t transient, int32_t samples, int32_t 
 
 /* Live kernel timing with HIP events on the chain's stream (bench / roofline):
  * id 0 = fused updateZ kernel, 1 = updateEta Z-pass, 2 = batched BetaLambda solve,
- * 3 = per-unit Eta solve, 4 = whole sweep.  hmsc_profile(s,1) clears and enables. */
+ * 3 = per-unit Eta solve, 4 = whole sweep, 5 = spatial updateEta (dense system), 6 = its
+ * blocked Cholesky, 7 = updateAlpha.  hmsc_profile(s,1) clears and enables. */
 int hmsc_profile(hmsc_state* s, int32_t enable);
 int hmsc_profile_get(hmsc_state* s, int32_t id, double* total_ms, int32_t* count);
 
