@@ -513,7 +513,8 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.ABpart = dalloc<double>((size_t)((nsl + 31) / 32) * (nc * nc + 2 * N + nfm * nt + 8));
   s.allreduce_buf = dalloc<double>((size_t)nc * nc + 2 * N + nfm * nt + nfm + 64);
   s.dev_flags = dalloc<int>(16);
-  s.d_iter = dalloc<uint32_t>(1);
+  s.d_iters = dalloc<uint32_t>(64);  // graph_sweeps <= 64
+  s.d_iter = s.d_iters;
   if (s.mask & HMSC_UP_GAMMAETA) {  // updateGammaEta: dense (nc ns)^2 systems, one workgroup per level
     HMSC_REQUIRE(s.nranks == 1, "updateGammaEta cannot run on a species-sharded chain: pass updater GammaEta=FALSE");
     HMSC_REQUIRE((size_t)nc * s.ns <= 4096, "updateGammaEta: nc * ns must be <= 4096 (dense (nc ns)^2 system)");
@@ -575,7 +576,7 @@ static void free_state(State& s) {
   if (s.host_rec) (void)hipHostFree(s.host_rec);
   if (s.copied_host) (void)hipHostFree(s.copied_host);
   if (s.gexec) (void)hipGraphExecDestroy(s.gexec);
-  if (s.d_iter) (void)hipFree(s.d_iter);
+  if (s.d_iters) (void)hipFree(s.d_iters);
   if (s.d_kt) (void)hipFree(s.d_kt);
   if (s.comm) ncclCommDestroy((ncclComm_t)s.comm);
   if (s.ev_bl) (void)hipEventDestroy(s.ev_bl);
@@ -921,7 +922,8 @@ static void sweep(State& s, uint32_t iter, bool adapt) {
 // s.graph_sweeps consecutive sweeps and replayed: one launch per graph_sweeps sweeps instead
 // of ~20 kernel launches + event records per sweep, and the relaunch gap between replays is
 // paid once per replay.  Kernels captured with s.capturing read the Philox sweep counter
-// from s.d_iter; each captured sweep starts by advancing it.  gexec_rec is the same sequence
+// from s.d_iter, which for the i-th captured sweep is slot i of s.d_iters; one small kernel
+// writes iter .. iter + graph_sweeps - 1 into the slots before each replay.  gexec_rec is the same sequence
 // with the record pack after every sweep; the pack picks its ring slot (or returns, for a
 // sweep that is not recorded) from d_iter and the run descriptor d_rec_desc.
 // Pack the state after a sweep into a ring slot (nullptr: chosen on the device in a graph
@@ -937,8 +939,9 @@ static void record_after_sweep(State& s, double* slot) {
   }
 }
 
-__global__ void set_iter_kernel(uint32_t* p, uint32_t v) { *p = v; }
-__global__ void advance_iter_kernel(uint32_t* p) { *p += 1u; }
+__global__ void set_iters_kernel(uint32_t* p, uint32_t v, int n) {
+  if ((int)threadIdx.x < n) p[threadIdx.x] = v + threadIdx.x;
+}
 __global__ void set_desc_kernel(int32_t* d, int32_t iter0, int32_t transient, int32_t thin, int32_t samples) {
   d[0] = iter0, d[1] = transient, d[2] = thin, d[3] = samples;
 }
@@ -961,12 +964,14 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record) 
   s.capturing = true;
   try {
     for (int i = 0; i < s.graph_sweeps; ++i) {
-      advance_iter_kernel<<<1, 1, 0, s.stream>>>(s.d_iter);
+      s.d_iter = s.d_iters + i;
       sweep(s, iter, false);
       if (with_record) record_after_sweep(s, nullptr);
     }
+    s.d_iter = s.d_iters;
     join_side(s);
   } catch (...) {
+    s.d_iter = s.d_iters;
     s.capturing = false;
     (void)hipStreamEndCapture(s.stream, &g);
     if (g) (void)hipGraphDestroy(g);
@@ -1006,16 +1011,14 @@ static bool replay_sweeps(State& s, uint32_t iter, bool with_record) {
   if (s.graph_dirty) s.eager_streak = 0, s.graph_dirty = false;
   if (!s.gexec && (s.eager_streak < 1 || !build_sweep_graphs(s, iter))) return false;  // steady first
   join_side(s);
-  if (s.graph_next_iter != iter) set_iter_kernel<<<1, 1, 0, s.stream>>>(s.d_iter, iter - 1u);
+  set_iters_kernel<<<1, 64, 0, s.stream>>>(s.d_iters, iter, s.graph_sweeps);
   HIP_OK(hipGraphLaunch(with_record ? s.gexec_rec : s.gexec, s.stream));
-  s.graph_next_iter = iter + (uint32_t)s.graph_sweeps;
   return true;
 }
 
 static void eager_sweep(State& s, uint32_t iter, bool adapt) {
   sweep(s, iter, adapt);
   s.eager_streak = adapt ? 0 : s.eager_streak + 1;
-  s.graph_next_iter = 0;  // d_iter is stale
 }
 
 static void unpack_record(const State& s, const double* slot, int k, int samples, hmsc_record* rec) {

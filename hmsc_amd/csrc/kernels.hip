@@ -1707,7 +1707,9 @@ __global__ __launch_bounds__(64) void eta_na_row_kernel(EtaView ev, int r, int n
 struct EtaFArgs {
   const double* Z;
   const double* LS;   // ns_loc x 16: Lambda diag(iSigma), zero past nf (cr_body)
-  const double* CR;   // Kmax x NF (ld ldcr): BL diag(iSigma) Lambda^T
+  const double* CR_part;  // [ncr][slab] species-block partials of CR = BL diag(iSigma) Lambda^T
+  double* CR;         // Kmax x NF (ld ldcr): the reduced CR, written by workgroup 0 (debug / other paths)
+  int ncr, slab;
   double* XEta;       // ny x K (ld ny)
   const int* Pi;      // ny: unit of each row (0-based)
   double* Eta;        // np x nf
@@ -1735,12 +1737,31 @@ __global__ __launch_bounds__(256) void eta_fused_kernel(EtaFArgs a) {
   const int i0 = blockIdx.x * EF_SITES;
   if (blockIdx.x == 0) HMSC_STAMP(50);
   // ---- stage 1: Q factor (wave 0 first), ZL on the matrix cores (every wave)
+  // CR from its species-block partials, in block order; eight partials' loads in flight
+  // per thread before they are added (a plain loop would pay one L2 round trip per block)
+  for (int p = t; p < K * nf; p += 256) {
+    const int k = p % K, h = p / K;
+    const double* src = a.CR_part + k + (size_t)a.ldcr * h;
+    double v = 0.0;
+    int b = 0;
+    for (; b + 8 <= a.ncr; b += 8) {
+      double x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = src[(size_t)a.slab * (b + u)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v += x[u];
+    }
+    for (; b < a.ncr; ++b) v += src[(size_t)a.slab * b];
+    sCR[k * NFB + h] = v;
+    if (blockIdx.x == 0) a.CR[k + (size_t)a.ldcr * h] = v;
+  }
+  __syncthreads();
   if (w == 0) {
     double q[NFB], dinv;
     const int r = lane < nf ? lane : 0;
 #pragma unroll
     for (int c = 0; c < NFB; ++c) {
-      const double v = (r == c ? 1.0 : 0.0) + a.CR[nc + r + (size_t)a.ldcr * (c < nf ? c : 0)];
+      const double v = (r == c ? 1.0 : 0.0) + sCR[(nc + r) * NFB + (c < nf ? c : 0)];
       q[c] = (lane < nf && c < nf) ? v : (lane == c ? 1.0 : 0.0);
     }
     wv_chol<NFB>(q, dinv);
@@ -1748,10 +1769,6 @@ __global__ __launch_bounds__(256) void eta_fused_kernel(EtaFArgs a) {
 #pragma unroll
       for (int c = 0; c < NFB; ++c)
         if (c < nf) sL[lane + nf * c] = (c <= lane) ? q[c] : 0.0;
-  }
-  for (int p = t; p < K * nf; p += 256) {
-    const int k = p % K, h = p / K;
-    sCR[k * NFB + h] = a.CR[k + (size_t)a.ldcr * h];
   }
   d4 acc = {0.0, 0.0, 0.0, 0.0};
   const double* zc = a.Z + min(i0 + lm, ny - 1);  // sites past ny: any finite row, unused
@@ -1940,10 +1957,10 @@ void launch_side_fused(State& s, uint32_t iter) {
   post_bl_kernel<<<ncr + ngv + npsi, 256, smem, s.stream>>>(a);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(s.ev_bl, s.stream));
-  // the main continuation is captured before the side branch: the graph executor keeps the
+  // the main continuation is captured before the side branch (the graph executor keeps the
   // first-created child of a node on its parent's queue, so the critical path stays on one
-  slab_sum_kernel<<<grid_for(slab), 256, 0, s.stream>>>(s.CR_part, s.CR, slab, ncr, slab);
-  HIP_OK(hipGetLastError());
+  // queue); the CR partials are reduced inside the fused Eta kernel
+  launch_eta_fused(s, iter, true);
   // GammaV algebra on the side stream (reads gv_part; writes Gamma, iV and Gamma2's prep)
   HIP_OK(hipStreamWaitEvent(s.side, s.ev_bl, 0));
   // with the delta chains (reading the psi partials) as extra workgroups of the same launch
@@ -1960,16 +1977,16 @@ void launch_side_fused(State& s, uint32_t iter) {
   HIP_OK(hipGetLastError());
   if (gw.do_prep) s.g2prep_valid = true;
   s.side_pending |= 1;  // joined (ev_side recorded) by the next join_side
-  launch_eta_fused(s, iter, true);
 }
 
 // G = XEta^T XEta after the fused Eta pass: the X^T X block is the constant s.XX, the Eta
-// rows the sum of the tiles' partials G_part[tile][k + Kmax h] in tile order (deterministic).
-// Workgroup b: outputs 64 b .. 64 b + 63 of the K x nf slab (lane = output), the 4 waves
-// taking every 4th tile, combined in LDS; written to both (k, nc + h) and (nc + h, k).
-__global__ __launch_bounds__(256) void g_eta_reduce_kernel(const double* part, int ntile, int K, int Kmax, int nc,
-                                                           int nf, const double* XX, double* G) {
-  __shared__ double red[4][64];
+// rows the sum of the tiles' partials G_part[tile][k + Kmax h] in a fixed order
+// (deterministic).  Workgroup b: outputs 64 b .. 64 b + 63 of the K x nf slab (lane =
+// output), its 16 waves taking every 16th tile, combined in LDS; written to both (k, nc + h)
+// and (nc + h, k).
+__global__ __launch_bounds__(1024) void g_eta_reduce_kernel(const double* part, int ntile, int K, int Kmax, int nc,
+                                                            int nf, const double* XX, double* G) {
+  __shared__ double red[16][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, o = blockIdx.x * 64 + lane;
   const int k = o % K, h = o / K;
   const size_t stride = (size_t)Kmax * nf;
@@ -1977,17 +1994,19 @@ __global__ __launch_bounds__(256) void g_eta_reduce_kernel(const double* part, i
   if (o < K * nf) {
     const double* p = part + k + (size_t)Kmax * h;
 #pragma unroll 8
-    for (int b = w; b < ntile; b += 4) s += p[stride * b];
+    for (int b = w; b < ntile; b += 16) s += p[stride * b];
   }
   red[w][lane] = s;
   __syncthreads();
   if (w == 0 && o < K * nf) {
-    const double v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    double v = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v += red[q][lane];
     G[k + (size_t)Kmax * (nc + h)] = v;
     G[(nc + h) + (size_t)Kmax * k] = v;
   }
   if (blockIdx.x == 0)
-    for (int p = threadIdx.x; p < nc * nc; p += 256) G[p % nc + (size_t)Kmax * (p / nc)] = XX[p];
+    for (int p = threadIdx.x; p < nc * nc; p += 1024) G[p % nc + (size_t)Kmax * (p / nc)] = XX[p];
 }
 
 static bool eta_fused_ok(const State& s) {
@@ -1996,20 +2015,21 @@ static bool eta_fused_ok(const State& s) {
 }
 
 static void launch_eta_fused(State& s, uint32_t iter, bool cr_done = false) {
-  if (!cr_done) {
-    const int ncr = (s.nsl + SB - 1) / SB;
-    const int64_t slab = (int64_t)s.Kmax * s.NFmax;
+  const int ncr = (s.nsl + SB - 1) / SB;
+  const int64_t slab = (int64_t)s.Kmax * s.NFmax;
+  if (!cr_done) {  // the CR partials (post_bl_kernel computes them in the co-launched path)
     cr_kernel<<<ncr, 256, (size_t)s.K * SB * sizeof(double), s.stream>>>(s.BL, s.iSigma, s.K, s.nc, s.NF, s.nsl,
                                                                            s.CR_part, s.Kmax, (int)slab, s.LS);
-    HIP_OK(hipGetLastError());
-    slab_sum_kernel<<<grid_for(slab), 256, 0, s.stream>>>(s.CR_part, s.CR, slab, ncr, slab);
     HIP_OK(hipGetLastError());
   }
   const Level& L = s.lev[0];
   EtaFArgs a{};
   a.Z = s.Z;
   a.LS = s.LS;
+  a.CR_part = s.CR_part;
   a.CR = s.CR;
+  a.ncr = ncr;
+  a.slab = (int)slab;
   a.XEta = s.XEta;
   a.Pi = L.Pi;
   a.Eta = L.Eta;
@@ -2038,7 +2058,7 @@ static void launch_eta_fused(State& s, uint32_t iter, bool cr_done = false) {
       eta_fused_kernel<16><<<ntile, 256, 0, s.stream>>>(a);
     HIP_OK(hipGetLastError());
   }
-  g_eta_reduce_kernel<<<(s.K * L.nf + 63) / 64, 256, 0, s.stream>>>(s.G_part, ntile, s.K, s.Kmax, s.nc, L.nf, s.XX, s.G);
+  g_eta_reduce_kernel<<<(s.K * L.nf + 63) / 64, 1024, 0, s.stream>>>(s.G_part, ntile, s.K, s.Kmax, s.nc, L.nf, s.XX, s.G);
   HIP_OK(hipGetLastError());
   s.zt_valid = false;   // Eta changed: XZ is stale until the next updateZ
   s.xeta_valid = true;  // XEta rows and G rewritten above

@@ -151,7 +151,8 @@ struct State {
 
   // per-sweep hipGraph (single rank, no updateNf): captured once, replayed every sweep; the
   // kernels read the Philox sweep counter from d_iter, which the graph's first node advances
-  uint32_t* d_iter = nullptr;
+  uint32_t* d_iter = nullptr;          // the Philox sweep counter captured kernels read (a slot of d_iters)
+  uint32_t* d_iters = nullptr;         // one counter per captured sweep, set once per replay
   bool capturing = false;
   bool use_graph = true;
   bool graph_dirty = true;
@@ -162,7 +163,6 @@ struct State {
   int graph_sweeps = 4;                 // sweeps per replay (HMSC_GRAPH_SWEEPS)
   int32_t* d_rec_desc = nullptr;        // {iter0, transient, thin, samples} of the current run
   hipEvent_t ev_graph = nullptr;        // after a recording replay: the copy stream waits on it
-  uint32_t graph_next_iter = 0;  // the iter the next replay will use (0: unknown, re-seed)
   int eager_streak = 0;          // eager steady sweeps since the graph was invalidated
 
   // live launch timing of the timed kernels (common.h kt_record): per-sweep-slot first
