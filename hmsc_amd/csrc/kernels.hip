@@ -303,6 +303,7 @@ __global__ __launch_bounds__(256) void beta_lambda_wave_kernel(BLArgs a) {
   const int K = a.K, nc = a.nc, i = lane_id(), w = threadIdx.x >> 6;
   const int j = blockIdx.x * 4 + w;
   if (j >= a.ns_loc) return;
+  if (blockIdx.x == 0) HMSC_STAMP(60);
   double* lds = tiles + w * WV_TILE;
   // prior precision diagonal of Lambda rows: Psi_hj * tau_h, tau = cumprod(Delta) per level   (:51)
   double pd = 0.0;
@@ -349,13 +350,17 @@ __global__ __launch_bounds__(256) void beta_lambda_wave_kernel(BLArgs a) {
     for (int k = 0; k < NM; ++k)
       if (k < K) a.dbg_prec[(size_t)j * K * K + i + (size_t)K * k] = x[k];
   double dinv;
+  if (blockIdx.x == 0) HMSC_STAMP(61);
   wv_chol<NM>(x, dinv);                    // RiU = chol(iU)  (:98)
+  if (blockIdx.x == 0) HMSC_STAMP(62);
   wv_forward<NM>(x, dinv, r);              // y = L^-1 rhs
   if (i < K && !a.noise_zero) r += normal(a.key, (uint32_t)(a.sp0 + j), (uint32_t)i, S_BETALAMBDA, SWEEP_ITER(a));
+  if (blockIdx.x == 0) HMSC_STAMP(63);
   double lt[NM];
   wv_transpose<NM, true>(x, lt, lds);
   wv_backward_t<NM>(lt, dinv, r);          // m + backsolve(RiU, xi)  (:101)
   if (i < K) a.BL[i + (size_t)K * j] = r;
+  if (blockIdx.x == 0) HMSC_STAMP(64);
   if (a.kt && i == 0) kt_record(a.kt, SWEEP_ITER(a), kt0);
 }
 

@@ -14,13 +14,19 @@
 
 namespace hmsc {
 
+// Z Tr is only consumed with NA (updateGamma2 forms X^T Z Tr from XZ otherwise, and a
+// sharded chain all-reduces that), so the no-NA kernels skip the ZTr contraction
+template <bool HAS_NA>
+constexpr int z_mode() { return HAS_NA ? Z_ALL : (Z_ALL & ~8); }
+
 template <bool DRAW, bool HAS_NA, bool POIS, bool NORMAL>
 static void z_dispatch_k(const State& s, dim3 grid, size_t smem, const ZArgs& a) {
+  constexpr int M = z_mode<HAS_NA>();
   switch (z_nkb(s.K)) {
-    case 1: z_wave_kernel<DRAW, HAS_NA, 1, Z_ALL, POIS, NORMAL><<<grid, 256, smem, s.stream>>>(a); break;
-    case 2: z_wave_kernel<DRAW, HAS_NA, 2, Z_ALL, POIS, NORMAL><<<grid, 256, smem, s.stream>>>(a); break;
-    case 3: z_wave_kernel<DRAW, HAS_NA, 3, Z_ALL, POIS, NORMAL><<<grid, 256, smem, s.stream>>>(a); break;
-    default: z_wave_kernel<DRAW, HAS_NA, 4, Z_ALL, POIS, NORMAL><<<grid, 256, smem, s.stream>>>(a); break;
+    case 1: z_wave_kernel<DRAW, HAS_NA, 1, M, POIS, NORMAL><<<grid, 256, smem, s.stream>>>(a); break;
+    case 2: z_wave_kernel<DRAW, HAS_NA, 2, M, POIS, NORMAL><<<grid, 256, smem, s.stream>>>(a); break;
+    case 3: z_wave_kernel<DRAW, HAS_NA, 3, M, POIS, NORMAL><<<grid, 256, smem, s.stream>>>(a); break;
+    default: z_wave_kernel<DRAW, HAS_NA, 4, M, POIS, NORMAL><<<grid, 256, smem, s.stream>>>(a); break;
   }
 }
 
@@ -36,10 +42,10 @@ template <bool HAS_NA>
 static int z_occupancy(int nkb, size_t smem) {
   int nb = 0;
   switch (nkb) {
-    case 1: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 1>, 256, smem)); break;
-    case 2: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 2>, 256, smem)); break;
-    case 3: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 3>, 256, smem)); break;
-    default: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 4>, 256, smem)); break;
+    case 1: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 1, z_mode<HAS_NA>()>, 256, smem)); break;
+    case 2: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 2, z_mode<HAS_NA>()>, 256, smem)); break;
+    case 3: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 3, z_mode<HAS_NA>()>, 256, smem)); break;
+    default: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 4, z_mode<HAS_NA>()>, 256, smem)); break;
   }
   return nb;
 }
@@ -107,7 +113,7 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
     HIP_OK(hipGetLastError());
   }
   // XZ and ZTr from their partials, one launch
-  const int64_t nXZ = (int64_t)s.K * s.nsl, nZT = (int64_t)s.ny * s.nt;
+  const int64_t nXZ = (int64_t)s.K * s.nsl, nZT = s.has_na ? (int64_t)s.ny * s.nt : 0;
   launch_slab_sum2(s.XZ_part, s.XZ, nXZ, nchunk, s.ZTr_part, s.ZTr, nZT, s.ntile_j, s.stream);
 }
 

@@ -17,8 +17,9 @@ ch.init([10])
 for it in range(1, 6):
     ch.sweep(it)
 ch.sync()
-st = ch.debug_get("stamps", 64)
-groups = {"gammav_wave": range(0, 10), "delta": range(20, 22), "gamma2_final": range(30, 33), "eta_shared(block0)": range(40, 45), "eta_fused(block0)": range(50, 56)}
+st = ch.debug_get("stamps", 128)
+groups = {"gammav_wave": range(0, 10), "delta": range(20, 22), "gamma2_final": range(30, 33), "eta_shared(block0)": range(40, 45), "eta_fused(block0)": range(50, 56),
+          "beta_lambda(block0)": range(60, 65), "gammav_wave1": range(10, 15)}
 for name, idx in groups.items():
     v = np.array([st[i] for i in idx])
     d = np.diff(v)
