@@ -295,54 +295,77 @@ __global__ __launch_bounds__(64) void beta_lambda_kernel(BLArgs a) {
 }
 
 // Wave-resident variant for K <= 32: one species per wave, four per workgroup; the K x K
-// precision lives in registers (row r in lane r), Cholesky / solves via wave_la.h.
+// precision lives in registers (row r in lane r), Cholesky / solves via wave_la.h.  The
+// inputs every species shares (G = XEta^T XEta, iV, Gamma, tau = cumprod(Delta)) are staged
+// into LDS once per workgroup by all 256 threads, so each wave's prologue is LDS reads plus
+// its own species' column loads, all issued before the first use.
 template <int NM>
 __global__ __launch_bounds__(256) void beta_lambda_wave_kernel(BLArgs a) {
   __shared__ __attribute__((aligned(16))) double tiles[4 * WV_TILE];
+  __shared__ double sG[32 * 33], sIV[32 * 32], sGam[32 * 8], sTau[64];
   const unsigned long long kt0 = a.kt ? kt_now() : 0ull;
-  const int K = a.K, nc = a.nc, i = lane_id(), w = threadIdx.x >> 6;
+  const int K = a.K, nc = a.nc, nt = a.nt, i = lane_id(), w = threadIdx.x >> 6, t = threadIdx.x;
   const int j = blockIdx.x * 4 + w;
-  if (j >= a.ns_loc) return;
   if (blockIdx.x == 0) HMSC_STAMP(60);
-  double* lds = tiles + w * WV_TILE;
-  // prior precision diagonal of Lambda rows: Psi_hj * tau_h, tau = cumprod(Delta) per level   (:51)
-  double pd = 0.0;
-  if (i >= nc && i < K) {
-    const int f = i - nc;
-    int base = 0;
-    for (int r = 0; r < a.nr; ++r) {
-      const int nf = a.lev_nf[r];
-      if (f < base + nf) {
-        double tau = 1.0;
-        for (int h = base; h <= f; ++h) tau *= a.Delta[h];
-        pd = a.Psi[f + (size_t)a.NF * j] * tau;
-        break;
-      }
-      base += nf;
+  for (int p = t; p < K * K; p += 256) sG[p % K + 33 * (p / K)] = a.G[p % K + (size_t)a.Kmax * (p / K)];
+  for (int p = t; p < nc * nc; p += 256) sIV[p] = a.iV[p];
+  for (int p = t; p < nc * nt && p < 32 * 8; p += 256) sGam[p] = a.Gamma[p];
+  if (t < a.nr) {  // tau = cumprod(Delta) per level   (:51)
+    int f0 = 0;
+    for (int r = 0; r < t; ++r) f0 += a.lev_nf[r];
+    double c = 1.0;
+    for (int h = 0; h < a.lev_nf[t]; ++h) {
+      c *= a.Delta[f0 + h];
+      sTau[f0 + h] = c;
     }
   }
+  // this species' own inputs, loaded before the barrier so their latency overlaps it
+  const int jj = j < a.ns_loc ? j : a.ns_loc - 1;
+  const double isig = a.iSigma[jj];
+  const double xz = i < K ? a.XZ[(i < K ? i : 0) + (size_t)K * jj] : 0.0;
+  const double psi = (i >= nc && i < K) ? a.Psi[(i - nc) + (size_t)a.NF * jj] : 0.0;
+  double trj[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) trj[q] = q < nt ? a.Tr[jj + (size_t)a.ns_loc * q] : 0.0;
+  const int nai = a.na_index ? a.na_index[jj] : -1;
+  __syncthreads();
+  if (j >= a.ns_loc) return;
+  double* lds = tiles + w * WV_TILE;
+  // prior precision diagonal of Lambda rows: Psi_hj * tau_h
+  const double pd = (i >= nc && i < K) ? psi * sTau[i - nc] : 0.0;
   double mu = 0.0;  // Mu_j = Gamma Tr_j^T   (:62)
   if (i < nc)
-    for (int q = 0; q < a.nt; ++q) mu += a.Gamma[i + nc * q] * a.Tr[j + (size_t)a.ns_loc * q];
-  const double isig = a.iSigma[j];
-  const int nai = a.na_index ? a.na_index[j] : -1;
-  const double* Gj = nai >= 0 ? a.Gna + (size_t)nai * a.Kmax * a.Kmax : a.G;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (q < nt) mu += sGam[i + nc * q] * trj[q];
   // iU = P + XEtaTXEta * iSigma[j]   (:83-92)
   double x[NM];
   const int ir = i < K ? i : 0;
+  if (nai >= 0) {  // species with NA: its own masked Gram
+    const double* Gj = a.Gna + (size_t)nai * a.Kmax * a.Kmax;
 #pragma unroll
-  for (int k = 0; k < NM; ++k) {
-    const int kc = k < K ? k : 0;
-    double v = isig * Gj[ir + a.Kmax * kc];
-    if (i < nc && k < nc) v += a.iV[ir + nc * kc];
-    if (i == k) v += pd;
-    x[k] = (i < K && k < K) ? v : (i == k ? 1.0 : 0.0);
+    for (int k = 0; k < NM; ++k) {
+      const int kc = k < K ? k : 0;
+      double v = isig * Gj[ir + a.Kmax * kc];
+      if (i < nc && k < nc) v += sIV[ir + nc * kc];
+      if (i == k) v += pd;
+      x[k] = (i < K && k < K) ? v : (i == k ? 1.0 : 0.0);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < NM; ++k) {
+      const int kc = k < K ? k : 0;
+      double v = isig * sG[ir + 33 * kc];
+      if (i < nc && k < nc) v += sIV[ir + nc * kc];
+      if (i == k) v += pd;
+      x[k] = (i < K && k < K) ? v : (i == k ? 1.0 : 0.0);
+    }
   }
   // rhs = P Mu + isXTS   (:66, :100)
-  double r = i < K ? isig * a.XZ[ir + (size_t)K * j] : 0.0;
+  double r = isig * xz;
   if (i < nc) {
     double pm = 0.0;
-    for (int c = 0; c < nc; ++c) pm += a.iV[i + nc * c] * bcast(mu, c);
+    for (int c = 0; c < nc; ++c) pm += sIV[i + nc * c] * bcast(mu, c);
     r += pm;
   }
   if (a.dbg_prec && i < K)
@@ -404,7 +427,7 @@ void launch_beta_lambda(State& s, uint32_t iter) {
   a.noise_zero = s.noise_mode;
   a.kt = s.kt_on ? s.d_kt + (size_t)KT_BL * 2 * KT_SLOTS : nullptr;
   ProfScope ps(s, PROF_BL);
-  if (s.K <= 32) {
+  if (s.K <= 32 && s.nt <= 8 && s.nc * s.nt <= 256 && s.NF <= 64) {
     const int nb = (s.nsl + 3) / 4;
     switch (wv_bucket(s.K)) {
       case 8: beta_lambda_wave_kernel<8><<<nb, 256, 0, s.stream>>>(a); break;
