@@ -931,12 +931,13 @@ static void sweep(State& s, uint32_t iter, bool adapt) {
 // the main stream need not wait for the GammaV algebra.
 static void record_after_sweep(State& s, double* slot) {
   if (s.side_fused && (s.side_pending & 1)) {
-    launch_record(s, slot, 1);
+    if (!s.pack_done) launch_record(s, slot, 1);  // else updateZ's slab-sum launch packed it
     launch_record(s, slot, 2);
   } else {
     join_side(s);
     launch_record(s, slot, 0);
   }
+  s.pack_req = s.pack_done = false;
 }
 
 __global__ void set_iters_kernel(uint32_t* p, uint32_t v, int n) {
@@ -965,6 +966,8 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record) 
   try {
     for (int i = 0; i < s.graph_sweeps; ++i) {
       s.d_iter = s.d_iters + i;
+      s.pack_req = with_record;
+      s.pack_done = false;
       sweep(s, iter, false);
       if (with_record) record_after_sweep(s, nullptr);
     }
@@ -972,6 +975,7 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record) 
     join_side(s);
   } catch (...) {
     s.d_iter = s.d_iters;
+    s.pack_req = s.pack_done = false;
     s.capturing = false;
     (void)hipStreamEndCapture(s.stream, &g);
     if (g) (void)hipGraphDestroy(g);

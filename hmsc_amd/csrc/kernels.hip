@@ -2021,8 +2021,17 @@ __global__ __launch_bounds__(1024) void g_eta_reduce_kernel(const double* part, 
   double s = 0.0;
   if (o < K * nf) {
     const double* p = part + k + (size_t)Kmax * h;
-#pragma unroll 8
-    for (int b = w; b < ntile; b += 16) s += p[stride * b];
+    // twenty tiles' loads in flight per lane before they are added (the partials were
+    // written by workgroups on every XCD: each round trip goes past the local L2)
+    int b = w;
+    for (; b + 16 * 19 < ntile; b += 16 * 20) {
+      double x[20];
+#pragma unroll
+      for (int u = 0; u < 20; ++u) x[u] = p[stride * (b + 16 * u)];
+#pragma unroll
+      for (int u = 0; u < 20; ++u) s += x[u];
+    }
+    for (; b < ntile; b += 16) s += p[stride * b];
   }
   red[w][lane] = s;
   __syncthreads();
@@ -2424,7 +2433,7 @@ struct PackArgs {
   int ring_slots;
 };
 
-__global__ __launch_bounds__(256) void pack_kernel(PackArgs a) {
+__device__ __forceinline__ void pack_body(const PackArgs& a, int bid, int nb) {
   double* slot = a.slot;
   if (a.iter_dev) {
     const int it = (int)(*a.iter_dev - (uint32_t)a.desc[0]);
@@ -2436,9 +2445,24 @@ __global__ __launch_bounds__(256) void pack_kernel(PackArgs a) {
   }
   for (int k = 0; k < a.npieces; ++k) {
     const PackPiece pc = a.p[k];
-    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < pc.n; e += (int64_t)gridDim.x * blockDim.x)
+    for (int64_t e = bid * (int64_t)blockDim.x + threadIdx.x; e < pc.n; e += (int64_t)nb * blockDim.x)
       slot[pc.dst + e] = pc.src[e];
   }
+}
+
+__global__ __launch_bounds__(256) void pack_kernel(PackArgs a) { pack_body(a, blockIdx.x, gridDim.x); }
+
+// updateZ's two slab reductions and the record pack of the sweep's main-stream outputs in one
+// launch (graph replays of recorded sweeps): the pack reads none of what the slab sums or
+// updateZ write (Z is not recorded), so it need not wait for them
+__global__ __launch_bounds__(256) void slab_pack_kernel(SlabJob j0, SlabJob j1, PackArgs pk, int npack) {
+  const int b = blockIdx.x;
+  if (b < j0.nb)
+    slab_sum_body(j0.part, j0.out, j0.n, j0.nparts, j0.stride, b, j0.nb);
+  else if (b < j0.nb + j1.nb)
+    slab_sum_body(j1.part, j1.out, j1.n, j1.nparts, j1.stride, b - j0.nb, j1.nb);
+  else
+    pack_body(pk, b - j0.nb - j1.nb, npack);
 }
 
 // Publishes "samples < value have landed in the host ring" to the host with a system-scope
@@ -2461,7 +2485,7 @@ size_t record_slot_doubles(const State& s) {
   return n;
 }
 
-void launch_record(State& s, double* slot, int part) {
+static PackArgs make_pack_args(State& s, double* slot, int part) {
   PackArgs a{};
   int64_t off = 0;
   int k = 0;
@@ -2490,10 +2514,25 @@ void launch_record(State& s, double* slot, int part) {
     a.slot_stride = (int64_t)s.slot_doubles;
     a.ring_slots = s.ring_slots;
   }
+  return a;
+}
+
+void launch_record(State& s, double* slot, int part) {
+  const PackArgs a = make_pack_args(s, slot, part);
   if (part == 2)
     pack_kernel<<<1, 256, 0, s.side>>>(a);
   else
     pack_kernel<<<512, 256, 0, s.stream>>>(a);
+  HIP_OK(hipGetLastError());
+}
+
+void launch_slab_sum2_pack(State& s, const double* p0, double* o0, int64_t n0, int np0, const double* p1, double* o1,
+                           int64_t n1, int np1) {
+  const SlabJob j0{p0, o0, n0, n0, np0, grid_for(n0)};
+  const SlabJob j1{p1, o1, n1, n1, np1, grid_for(n1)};
+  const PackArgs pk = make_pack_args(s, nullptr, 1);
+  constexpr int NPACK = 256;
+  slab_pack_kernel<<<j0.nb + j1.nb + NPACK, 256, 0, s.stream>>>(j0, j1, pk, NPACK);
   HIP_OK(hipGetLastError());
 }
 

@@ -65,6 +65,8 @@ struct State {
   // side stream: updateGammaV, Gamma2's iV-only algebra and updateLambdaPriors of sweep t
   // only feed sweep t+1, so they overlap updateEta / updateZ of sweep t
   hipStream_t side = nullptr, side2 = nullptr;  // side: GammaV + Gamma2 prep; side2: LambdaPriors
+  // a captured recorded sweep asks updateZ's slab-sum launch to carry the record pack (part 1)
+  bool pack_req = false, pack_done = false;
   hipEvent_t ev_bl = nullptr, ev_side = nullptr, ev_side2 = nullptr;
   int side_pending = 0;          // bit 0: side has unjoined work (ev_side), bit 1: side2 (ev_side2)
   // co-launched sweep (see launch_side_fused): only the GammaV algebra stays on `side`; its
@@ -238,6 +240,9 @@ int z_resident_slots(const State& s);
 void launch_xeta(State& s);
 void launch_slab_sum2(const double* p0, double* o0, int64_t n0, int np0, const double* p1, double* o1, int64_t n1,
                       int np1, hipStream_t st);
+// the same with the main-stream record pack (part 1) of a captured recorded sweep appended
+void launch_slab_sum2_pack(State& s, const double* p0, double* o0, int64_t n0, int np0, const double* p1, double* o1,
+                           int64_t n1, int np1);
 void launch_beta_lambda(State& s, uint32_t iter);
 void launch_gamma_v(State& s, uint32_t iter, hipStream_t st);
 void launch_gamma2(State& s, uint32_t iter);

@@ -114,7 +114,13 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   }
   // XZ and ZTr from their partials, one launch
   const int64_t nXZ = (int64_t)s.K * s.nsl, nZT = s.has_na ? (int64_t)s.ny * s.nt : 0;
-  launch_slab_sum2(s.XZ_part, s.XZ, nXZ, nchunk, s.ZTr_part, s.ZTr, nZT, s.ntile_j, s.stream);
+  if (draw && s.pack_req && s.side_fused && s.capturing) {
+    launch_slab_sum2_pack(s, s.XZ_part, s.XZ, nXZ, nchunk, s.ZTr_part, s.ZTr, nZT, s.ntile_j);
+    s.pack_req = false;
+    s.pack_done = true;
+  } else {
+    launch_slab_sum2(s.XZ_part, s.XZ, nXZ, nchunk, s.ZTr_part, s.ZTr, nZT, s.ntile_j, s.stream);
+  }
 }
 
 void launch_update_z(State& s, uint32_t iter, bool use_raw_y) {
