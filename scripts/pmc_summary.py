@@ -31,6 +31,9 @@ for k, cs in vals.items():
         d["hbm_write_bytes"] = d["WRITE_SIZE"] * 1024
     if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
         d["hbm_bytes_per_launch"] = d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"]
+        # the 2x correction is established for 16-B/lane streaming reads; kernels whose reads
+        # are 8-B or 1-B per lane may be over-corrected, so the raw figure is kept beside it
+        d["hbm_bytes_per_launch_uncorrected"] = d["FETCH_SIZE"] * 1024 + d["hbm_write_bytes"]
     if "GRBM_GUI_ACTIVE" in d and d["avg_us_profiled"] > 0:
         d["eff_clock_ghz"] = d["GRBM_GUI_ACTIVE"] / 8 / (d["avg_us_profiled"] * 1e3)
     if "SQ_INSTS_VALU" in d and "SQ_WAVES" in d:

@@ -3,7 +3,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-pmc}
-REGEX=${2:-z_fused|beta_lambda|eta_shared|gammav_wave|zl_kernel|xeta_gram}
+REGEX=${2:-z_wave|eta_fused|beta_lambda_wave|side_chain|g_eta_reduce|slab_pack}
 mkdir -p $R/gpurun_out/$TAG
 cd /tmp && export TMPDIR=/tmp
 i=0
