@@ -517,7 +517,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.d_iter = s.d_iters;
   if (s.mask & HMSC_UP_GAMMAETA) {  // updateGammaEta: dense (nc ns)^2 systems, one workgroup per level
     HMSC_REQUIRE(s.nranks == 1, "updateGammaEta cannot run on a species-sharded chain: pass updater GammaEta=FALSE");
-    HMSC_REQUIRE((size_t)nc * s.ns <= 4096, "updateGammaEta: nc * ns must be <= 4096 (dense (nc ns)^2 system)");
+    HMSC_REQUIRE((size_t)nc * s.ns <= 32768, "updateGammaEta: nc * ns must be <= 32768 (dense (nc ns)^2 systems, 4 x 8.6 GB)");
     for (int r = 0; r < s.nr; ++r)
     {
       HMSC_REQUIRE(s.lev[r].nfmax <= 16, "updateGammaEta: nfMax must be <= 16 in this build");

@@ -129,27 +129,40 @@ __device__ inline bool t_chol_inv(double* A, double* Li, int n) {
   return ok;
 }
 
-__global__ __launch_bounds__(1024) void gamma_eta_kernel(GEArgs a) {
-  __shared__ int flag;
-  const int t = threadIdx.x, nthr = blockDim.x;
-  const int ny = a.ny, ns = a.ns, nc = a.nc, nt = a.nt, nf = a.nf, np = a.np, K = a.K;
-  const int N = nc * ns, G = nc * nt;
-  const bool obs = (np == ny);
-  const GELayout o = ge_layout(ny, ns, nc, nt, nf, obs ? 0 : np);
-  double* w = a.work;
-  double *A = w + o.A, *L = w + o.L, *M = w + o.M, *T = w + o.T, *S = w + o.S;
-  double *XtX = w + o.XtX, *V = w + o.V, *Wv = w + o.Wv, *XtS = w + o.XtS, *LamiD = w + o.LamiD, *LDL = w + o.LDL;
-  double *W0 = w + o.W0, *iW0 = w + o.iW0, *L0i = w + o.L0i, *tmp1 = w + o.tmp1, *Qm = w + o.Qm, *iQm = w + o.iQm;
-  double *iQTr = w + o.iQTr, *mb10 = w + o.vec, *mb20 = mb10 + N, *v = mb20 + N, *wv = v + N, *mb = wv + N,
-         *xi = mb + N;
-  double *Beta = w + o.Beta, *Pg = w + o.Pg, *rg = w + o.rg;
-  double *PtX = w + o.PtX, *PtS = w + o.PtS, *iWp = w + o.iWp, *Lip = w + o.Lip, *Ltp = w + o.Ltp, *m21 = w + o.m21;
-  const uint32_t it = SWEEP_ITER(a);
-  const uint32_t str = LEVEL_STRIDE * (uint32_t)a.r;
-  const double* lam = a.BL + a.loff;  // Lambda_r[h, j] = lam[h + K j]
+// Workspace pointers of one level's update (ge_layout)
+struct GEPtrs {
+  double *A, *L, *M, *T, *S, *XtX, *V, *Wv, *XtS, *LamiD, *LDL, *W0, *iW0, *L0i, *tmp1, *Qm, *iQm, *iQTr;
+  double *mb10, *mb20, *v, *wv, *mb, *xi, *Beta, *Pg, *rg, *PtX, *PtS, *iWp, *Lip, *Ltp, *m21;
+  bool obs;
+  int N, G;
+};
 
-  // ---- stage 1: S, X'X, V = iV^-1, LamiD, Lam D Lam', Q / iQ
-  for (size_t p = t; p < (size_t)ny * ns; p += nthr) {
+__device__ inline GEPtrs ge_ptrs(const GEArgs& a) {
+  GEPtrs P;
+  P.obs = (a.np == a.ny);
+  P.N = a.nc * a.ns;
+  P.G = a.nc * a.nt;
+  const GELayout o = ge_layout(a.ny, a.ns, a.nc, a.nt, a.nf, P.obs ? 0 : a.np);
+  double* w = a.work;
+  P.A = w + o.A, P.L = w + o.L, P.M = w + o.M, P.T = w + o.T, P.S = w + o.S, P.XtX = w + o.XtX, P.V = w + o.V;
+  P.Wv = w + o.Wv, P.XtS = w + o.XtS, P.LamiD = w + o.LamiD, P.LDL = w + o.LDL, P.W0 = w + o.W0, P.iW0 = w + o.iW0;
+  P.L0i = w + o.L0i, P.tmp1 = w + o.tmp1, P.Qm = w + o.Qm, P.iQm = w + o.iQm, P.iQTr = w + o.iQTr;
+  P.mb10 = w + o.vec, P.mb20 = P.mb10 + P.N, P.v = P.mb20 + P.N, P.wv = P.v + P.N, P.mb = P.wv + P.N,
+  P.xi = P.mb + P.N;
+  P.Beta = w + o.Beta, P.Pg = w + o.Pg, P.rg = w + o.rg, P.PtX = w + o.PtX, P.PtS = w + o.PtS, P.iWp = w + o.iWp;
+  P.Lip = w + o.Lip, P.Ltp = w + o.Ltp, P.m21 = w + o.m21;
+  return P;
+}
+
+// The update's element-parallel segments.  Each loops p = g0, g0 + gs, ...: the one-workgroup
+// kernel calls them with (threadIdx.x, blockDim.x) between its barriers, the blocked path
+// (large nc ns) with the global thread index and grid size from one launch per segment.
+
+// S, X'X (+ a copy of iV), LamiD, Lam D Lam', Q / iQ   (:37-42, :27-31)
+__device__ inline void ge_seg_prep(const GEArgs& a, const GEPtrs& P, int g0, int gs) {
+  const int ny = a.ny, ns = a.ns, nc = a.nc, nf = a.nf, K = a.K;
+  const double* lam = a.BL + a.loff;  // Lambda_r[h, j] = lam[h + K j]
+  for (size_t p = g0; p < (size_t)ny * ns; p += gs) {
     const int i = (int)(p % ny), j = (int)(p / ny);
     double sv = a.Z[p];
     for (int q = 0; q < a.nr; ++q) {
@@ -159,28 +172,28 @@ __global__ __launch_bounds__(1024) void gamma_eta_kernel(GEArgs a) {
       const double* lq = a.BL + a.lev_loff[q] + (size_t)K * j;
       for (int h = 0; h < a.lev_nf[q]; ++h) sv -= eq[u + (size_t)npq * h] * lq[h];
     }
-    S[p] = sv;
+    P.S[p] = sv;
   }
-  for (int p = t; p < nc * nc; p += nthr) {
+  for (int p = g0; p < nc * nc; p += gs) {
     const int c1 = p % nc, c2 = p / nc;
     double s = 0.0;
     for (int i = 0; i < ny; ++i) s = fma(a.X[i + (size_t)ny * c1], a.X[i + (size_t)ny * c2], s);
-    XtX[p] = s;
-    Wv[p] = a.iV[p];
+    P.XtX[p] = s;
+    P.Wv[p] = a.iV[p];
   }
-  for (int p = t; p < nf * ns; p += nthr) {
+  for (int p = g0; p < nf * ns; p += gs) {
     const int h = p % nf, j = p / nf;
-    LamiD[p] = lam[h + (size_t)K * j] * a.iSigma[j];
+    P.LamiD[p] = lam[h + (size_t)K * j] * a.iSigma[j];
   }
-  for (int p = t; p < nf * nf; p += nthr) {
+  for (int p = g0; p < nf * nf; p += gs) {
     const int h1 = p % nf, h2 = p / nf;
     double s = 0.0;
     for (int j = 0; j < ns; ++j) s = fma(lam[h1 + (size_t)K * j] * a.iSigma[j], lam[h2 + (size_t)K * j], s);
-    LDL[p] = s;
+    P.LDL[p] = s;
   }
   if (a.phU) {
     const double* wq = a.phWinv + (size_t)ns * ((int)(*a.rho) - 1);
-    for (int p = t; p < ns * ns; p += nthr) {
+    for (int p = g0; p < ns * ns; p += gs) {
       const int j1 = p % ns, j2 = p / ns;
       double s = 0.0, si = 0.0;
       for (int i = 0; i < ns; ++i) {
@@ -188,264 +201,288 @@ __global__ __launch_bounds__(1024) void gamma_eta_kernel(GEArgs a) {
         si = fma(uu, wq[i], si);
         s = fma(uu, 1.0 / wq[i], s);
       }
-      iQm[p] = si;
-      Qm[p] = s;
+      P.iQm[p] = si;
+      P.Qm[p] = s;
     }
   } else {
-    for (int p = t; p < ns * ns; p += nthr) iQm[p] = Qm[p] = (p % ns == p / ns) ? 1.0 : 0.0;
+    for (int p = g0; p < ns * ns; p += gs) P.iQm[p] = P.Qm[p] = (p % ns == p / ns) ? 1.0 : 0.0;
   }
-  __syncthreads();
-  // V = chol2inv(chol(iV))
-  if (!wg_chol(Wv, nc, nc, &flag) && t == 0) a.fail[0] = 1;
-  wg_chol2inv(Wv, nc, nc, V, nc, T /* scratch: nc^2 <= N^2 */);
-  // X'S, iQ Tr
-  for (int p = t; p < N; p += nthr) {
+}
+
+// X'S, iQ Tr
+__device__ inline void ge_seg_xts(const GEArgs& a, const GEPtrs& P, int g0, int gs) {
+  const int ny = a.ny, ns = a.ns, nc = a.nc, nt = a.nt;
+  for (int p = g0; p < P.N; p += gs) {
     const int c = p % nc, j = p / nc;
     double s = 0.0;
-    for (int i = 0; i < ny; ++i) s = fma(a.X[i + (size_t)ny * c], S[i + (size_t)ny * j], s);
-    XtS[p] = s;
+    for (int i = 0; i < ny; ++i) s = fma(a.X[i + (size_t)ny * c], P.S[i + (size_t)ny * j], s);
+    P.XtS[p] = s;
   }
-  for (int p = t; p < ns * nt; p += nthr) {
+  for (int p = g0; p < ns * nt; p += gs) {
     const int j = p % ns, q = p / ns;
     double s = 0.0;
-    for (int j2 = 0; j2 < ns; ++j2) s = fma(iQm[j + (size_t)ns * j2], a.Tr[j2 + (size_t)ns * q], s);
-    iQTr[p] = s;
+    for (int j2 = 0; j2 < ns; ++j2) s = fma(P.iQm[j + (size_t)ns * j2], a.Tr[j2 + (size_t)ns * q], s);
+    P.iQTr[p] = s;
   }
-  // ---- stage 2: A = (Tr x I) U (Tr x I)^T + Q x V   (:32)
-  for (size_t p = t; p < (size_t)N * N; p += nthr) {
+}
+
+// A = (Tr x I) U (Tr x I)^T + Q x V   (:32), and its copy L to be factorised
+__device__ inline void ge_seg_a(const GEArgs& a, const GEPtrs& P, int g0, int gs) {
+  const int ns = a.ns, nc = a.nc, nt = a.nt, N = P.N, G = P.G;
+  for (size_t p = g0; p < (size_t)N * N; p += gs) {
     const int r1 = (int)(p % N), r2 = (int)(p / N);
     const int c1 = r1 % nc, j1 = r1 / nc, c2 = r2 % nc, j2 = r2 / nc;
-    double s = Qm[j1 + (size_t)ns * j2] * V[c1 + nc * c2];
+    double s = P.Qm[j1 + (size_t)ns * j2] * P.V[c1 + nc * c2];
     for (int t1 = 0; t1 < nt; ++t1) {
       const double a1 = a.Tr[j1 + (size_t)ns * t1];
       for (int t2 = 0; t2 < nt; ++t2)
         s = fma(a1 * a.UGamma[(c1 + nc * t1) + (size_t)G * (c2 + nc * t2)], a.Tr[j2 + (size_t)ns * t2], s);
     }
-    A[p] = s;
-    L[p] = s;
+    P.A[p] = s;
+    P.L[p] = s;
   }
-  __syncthreads();
-  // iA = chol2inv(chol(A)) into M (scratch T)
-  if (!wg_chol(L, N, N, &flag) && t == 0) a.fail[0] = 1;
-  wg_chol2inv(L, N, N, M, N, T);
+}
 
-  // ---- stage 3: the level's Eta-integrated precision term T1 and the mean pieces
-  if (obs) {
-    // W0 = Lam D Lam' + I, RW0 = chol(W0), iW0 = chol2inv(RW0)      (:53-55)
-    if (t == 0) {
-      for (int p = 0; p < nf * nf; ++p) W0[p] = LDL[p] + ((p % nf == p / nf) ? 1.0 : 0.0);
-      if (!t_chol_inv(W0, L0i, nf)) a.fail[0] = 1;
-      for (int h1 = 0; h1 < nf; ++h1)
-        for (int h2 = 0; h2 < nf; ++h2) {
-          double s = 0.0;
-          for (int k = 0; k < nf; ++k) s += L0i[k + nf * h1] * L0i[k + nf * h2];
-          iW0[h1 + nf * h2] = s;
-        }
-    }
-    __syncthreads();
-    // tmp1 = diag(id) - LamiD' iW0 LamiD   (:57)
-    for (int p = t; p < ns * ns; p += nthr) {
-      const int j1 = p % ns, j2 = p / ns;
+// np = ny: W0 = Lam D Lam' + I, RW0 = chol(W0), iW0 = chol2inv(RW0)  (:53-55); one thread
+__device__ inline bool ge_w0(const GEArgs& a, const GEPtrs& P) {
+  const int nf = a.nf;
+  for (int p = 0; p < nf * nf; ++p) P.W0[p] = P.LDL[p] + ((p % nf == p / nf) ? 1.0 : 0.0);
+  const bool ok = t_chol_inv(P.W0, P.L0i, nf);
+  for (int h1 = 0; h1 < nf; ++h1)
+    for (int h2 = 0; h2 < nf; ++h2) {
       double s = 0.0;
+      for (int k = 0; k < nf; ++k) s += P.L0i[k + nf * h1] * P.L0i[k + nf * h2];
+      P.iW0[h1 + nf * h2] = s;
+    }
+  return ok;
+}
+
+// np = ny: tmp1 = diag(id) - LamiD' iW0 LamiD   (:57)
+__device__ inline void ge_seg_tmp1(const GEArgs& a, const GEPtrs& P, int g0, int gs) {
+  const int ns = a.ns, nf = a.nf;
+  for (int p = g0; p < ns * ns; p += gs) {
+    const int j1 = p % ns, j2 = p / ns;
+    double s = 0.0;
+    for (int h1 = 0; h1 < nf; ++h1) {
+      double u = 0.0;
+      for (int h2 = 0; h2 < nf; ++h2) u = fma(P.iW0[h1 + nf * h2], P.LamiD[h2 + nf * j2], u);
+      s = fma(P.LamiD[h1 + nf * j1], u, s);
+    }
+    P.tmp1[p] = (j1 == j2 ? a.iSigma[j1] : 0.0) - s;
+  }
+}
+
+// np = ny: M = iA + kron(tmp1, X'X) (:58), mb20 = vec((X'S LamiD') iW0 LamiD) (:62)
+__device__ inline void ge_seg_m_obs(const GEArgs& a, const GEPtrs& P, int g0, int gs) {
+  const int ns = a.ns, nc = a.nc, nf = a.nf, N = P.N;
+  for (size_t p = g0; p < (size_t)N * N; p += gs) {
+    const int r1 = (int)(p % N), r2 = (int)(p / N);
+    P.M[p] += P.tmp1[(r1 / nc) + (size_t)ns * (r2 / nc)] * P.XtX[(r1 % nc) + nc * (r2 % nc)];
+  }
+  for (int p = g0; p < N; p += gs) {
+    const int c = p % nc, j = p / nc;
+    double s = 0.0;
+    for (int h2 = 0; h2 < nf; ++h2) {
+      double u = 0.0;
       for (int h1 = 0; h1 < nf; ++h1) {
-        double u = 0.0;
-        for (int h2 = 0; h2 < nf; ++h2) u = fma(iW0[h1 + nf * h2], LamiD[h2 + nf * j2], u);
-        s = fma(LamiD[h1 + nf * j1], u, s);
+        double x1 = 0.0;
+        for (int j2 = 0; j2 < ns; ++j2) x1 = fma(P.XtS[c + nc * j2], P.LamiD[h1 + nf * j2], x1);
+        u = fma(x1, P.iW0[h1 + nf * h2], u);
       }
-      tmp1[p] = (j1 == j2 ? a.iSigma[j1] : 0.0) - s;
+      s = fma(u, P.LamiD[h2 + nf * j], s);
     }
-    __syncthreads();
-    // M = iA + kron(tmp1, X'X)   (:58)
-    for (size_t p = t; p < (size_t)N * N; p += nthr) {
-      const int r1 = (int)(p % N), r2 = (int)(p / N);
-      M[p] += tmp1[(r1 / nc) + (size_t)ns * (r2 / nc)] * XtX[(r1 % nc) + nc * (r2 % nc)];
+    P.mb20[p] = s;
+  }
+}
+
+// np < ny, per unit q: P'X, P'S, W_p = I + n_p Lam D Lam', iW_p, LiW_p^T LamiD, mb22_p (:78-117)
+__device__ inline bool ge_seg_units(const GEArgs& a, const GEPtrs& P, int g0, int gs) {
+  const int ny = a.ny, ns = a.ns, nc = a.nc, nf = a.nf, np = a.np;
+  bool ok = true;
+  for (int q = g0; q < np; q += gs) {
+    const int b = a.unit_ptr[q], e = a.unit_ptr[q + 1];
+    for (int c = 0; c < nc; ++c) {
+      double s = 0.0;
+      for (int k = b; k < e; ++k) s += a.X[a.unit_rows[k] + (size_t)ny * c];
+      P.PtX[q + (size_t)np * c] = s;
     }
-    // mb20 = vec((X'S LamiD') iW0 LamiD)   (:62)
-    for (int p = t; p < N; p += nthr) {
-      const int c = p % nc, j = p / nc;
+    for (int j = 0; j < ns; ++j) {
+      double s = 0.0;
+      for (int k = b; k < e; ++k) s += P.S[a.unit_rows[k] + (size_t)ny * j];
+      P.PtS[q + (size_t)np * j] = s;
+    }
+    double* Wq = P.iWp + (size_t)q * nf * nf;  // W_p factorised in place, then replaced by iW_p
+    double* Li = P.Lip + (size_t)q * nf * nf;
+    const double cnt = (double)(e - b);
+    for (int p = 0; p < nf * nf; ++p) Wq[p] = ((p % nf == p / nf) ? 1.0 : 0.0) + cnt * P.LDL[p];
+    if (!t_chol_inv(Wq, Li, nf)) ok = false;
+    for (int h1 = 0; h1 < nf; ++h1)
+      for (int h2 = 0; h2 < nf; ++h2) {
+        double s = 0.0;
+        for (int k = 0; k < nf; ++k) s += Li[k + nf * h1] * Li[k + nf * h2];
+        Wq[h1 + nf * h2] = s;
+      }
+    // Lt_p = L_p^-1 LamiD  (nf x ns): rows of LiW_p^T LamiD  (:104)
+    double* Lt = P.Ltp + (size_t)q * nf * ns;
+    for (int j = 0; j < ns; ++j)
+      for (int h = 0; h < nf; ++h) {
+        double s = 0.0;
+        for (int k = 0; k <= h; ++k) s += Li[h + nf * k] * P.LamiD[k + nf * j];
+        Lt[h + (size_t)nf * j] = s;
+      }
+    // mb22_p = iW_p (P'S LamiD')_p    (:115-117)
+    for (int h = 0; h < nf; ++h) {
       double s = 0.0;
       for (int h2 = 0; h2 < nf; ++h2) {
         double u = 0.0;
-        for (int h1 = 0; h1 < nf; ++h1) {
-          double x1 = 0.0;
-          for (int j2 = 0; j2 < ns; ++j2) x1 = fma(XtS[c + nc * j2], LamiD[h1 + nf * j2], x1);
-          u = fma(x1, iW0[h1 + nf * h2], u);
-        }
-        s = fma(u, LamiD[h2 + nf * j], s);
+        for (int j = 0; j < ns; ++j) u = fma(P.PtS[q + (size_t)np * j], P.LamiD[h2 + nf * j], u);
+        s = fma(Wq[h + nf * h2], u, s);
       }
-      mb20[p] = s;
-    }
-  } else {
-    // per unit p: P'X, P'S, W_p = I + n_p Lam D Lam', iW_p, LiW_p^T LamiD   (:78-107)
-    for (int q = t; q < np; q += nthr) {
-      const int b = a.unit_ptr[q], e = a.unit_ptr[q + 1];
-      for (int c = 0; c < nc; ++c) {
-        double s = 0.0;
-        for (int k = b; k < e; ++k) s += a.X[a.unit_rows[k] + (size_t)ny * c];
-        PtX[q + (size_t)np * c] = s;
-      }
-      for (int j = 0; j < ns; ++j) {
-        double s = 0.0;
-        for (int k = b; k < e; ++k) s += S[a.unit_rows[k] + (size_t)ny * j];
-        PtS[q + (size_t)np * j] = s;
-      }
-      double* Wq = iWp + (size_t)q * nf * nf;  // W_p factorised in place, then replaced by iW_p
-      double* Li = Lip + (size_t)q * nf * nf;
-      const double cnt = (double)(e - b);
-      for (int p = 0; p < nf * nf; ++p) Wq[p] = ((p % nf == p / nf) ? 1.0 : 0.0) + cnt * LDL[p];
-      if (!t_chol_inv(Wq, Li, nf)) a.fail[0] = 1;
-      for (int h1 = 0; h1 < nf; ++h1)
-        for (int h2 = 0; h2 < nf; ++h2) {
-          double s = 0.0;
-          for (int k = 0; k < nf; ++k) s += Li[k + nf * h1] * Li[k + nf * h2];
-          Wq[h1 + nf * h2] = s;
-        }
-      // Lt_p = L_p^-1 LamiD  (nf x ns): rows of LiW_p^T LamiD  (:104)
-      double* Lt = Ltp + (size_t)q * nf * ns;
-      for (int j = 0; j < ns; ++j)
-        for (int h = 0; h < nf; ++h) {
-          double s = 0.0;
-          for (int k = 0; k <= h; ++k) s += Li[h + nf * k] * LamiD[k + nf * j];
-          Lt[h + (size_t)nf * j] = s;
-        }
-      // mb22_p = iW_p (P'S LamiD')_p    (:115-117)
-      for (int h = 0; h < nf; ++h) {
-        double s = 0.0;
-        for (int h2 = 0; h2 < nf; ++h2) {
-          double u = 0.0;
-          for (int j = 0; j < ns; ++j) u = fma(PtS[q + (size_t)np * j], LamiD[h2 + nf * j], u);
-          s = fma(Wq[h + nf * h2], u, s);
-        }
-        m21[q + (size_t)np * h] = s;
-      }
-    }
-    __syncthreads();
-    // T = kron(diag(id), X'X) - sum_p (P'X)_p (P'X)_p' x Lt_p' Lt_p ;  M = iA + T   (:105-108)
-    for (size_t p = t; p < (size_t)N * N; p += nthr) {
-      const int r1 = (int)(p % N), r2 = (int)(p / N);
-      const int c1 = r1 % nc, j1 = r1 / nc, c2 = r2 % nc, j2 = r2 / nc;
-      double s = 0.0;
-      for (int q = 0; q < np; ++q) {
-        const double* Lt = Ltp + (size_t)q * nf * ns;
-        double u = 0.0;
-        for (int h = 0; h < nf; ++h) u = fma(Lt[h + (size_t)nf * j1], Lt[h + (size_t)nf * j2], u);
-        s = fma(PtX[q + (size_t)np * c1] * PtX[q + (size_t)np * c2], u, s);
-      }
-      const double tv = (j1 == j2 ? a.iSigma[j1] * XtX[c1 + nc * c2] : 0.0) - s;
-      T[p] = tv;
-      M[p] += tv;
-    }
-    // mb20 = vec(P'X' mb22 LamiD)   (:118)
-    for (int p = t; p < N; p += nthr) {
-      const int c = p % nc, j = p / nc;
-      double s = 0.0;
-      for (int h = 0; h < nf; ++h) {
-        double u = 0.0;
-        for (int q = 0; q < np; ++q) u = fma(PtX[q + (size_t)np * c], m21[q + (size_t)np * h], u);
-        s = fma(u, LamiD[h + nf * j], s);
-      }
-      mb20[p] = s;
+      P.m21[q + (size_t)np * h] = s;
     }
   }
-  // mb10 = vec(X'S o id)  (:61 / :113)
-  for (int p = t; p < N; p += nthr) {
-    mb10[p] = XtS[p] * a.iSigma[p / nc];
-    v[p] = mb10[p] - mb20[p];
+  return ok;
+}
+
+// np < ny: T = kron(diag(id), X'X) - sum_p (P'X)_p (P'X)_p' x Lt_p' Lt_p ; M = iA + T (:105-108),
+// mb20 = vec(P'X' mb22 LamiD) (:118)
+__device__ inline void ge_seg_m_units(const GEArgs& a, const GEPtrs& P, int g0, int gs) {
+  const int ns = a.ns, nc = a.nc, nf = a.nf, np = a.np, N = P.N;
+  for (size_t p = g0; p < (size_t)N * N; p += gs) {
+    const int r1 = (int)(p % N), r2 = (int)(p / N);
+    const int c1 = r1 % nc, j1 = r1 / nc, c2 = r2 % nc, j2 = r2 / nc;
+    double s = 0.0;
+    for (int q = 0; q < np; ++q) {
+      const double* Lt = P.Ltp + (size_t)q * nf * ns;
+      double u = 0.0;
+      for (int h = 0; h < nf; ++h) u = fma(Lt[h + (size_t)nf * j1], Lt[h + (size_t)nf * j2], u);
+      s = fma(P.PtX[q + (size_t)np * c1] * P.PtX[q + (size_t)np * c2], u, s);
+    }
+    const double tv = (j1 == j2 ? a.iSigma[j1] * P.XtX[c1 + nc * c2] : 0.0) - s;
+    P.T[p] = tv;
+    P.M[p] += tv;
   }
-  __syncthreads();
-  // ---- stage 4: RM = chol(M); mb31 = M^-1 (mb10 - mb20); mb30 = T1 mb31; mb = A (mb10 - mb20 - mb30)
-  if (!wg_chol(M, N, N, &flag) && t == 0) a.fail[0] = 1;
-  wg_forward(M, N, N, v);
-  wg_backward_t(M, N, N, v);
-  for (int p = t; p < N; p += nthr) {
+  for (int p = g0; p < N; p += gs) {
     const int c = p % nc, j = p / nc;
     double s = 0.0;
-    if (obs) {
+    for (int h = 0; h < nf; ++h) {
+      double u = 0.0;
+      for (int q = 0; q < np; ++q) u = fma(P.PtX[q + (size_t)np * c], P.m21[q + (size_t)np * h], u);
+      s = fma(u, P.LamiD[h + nf * j], s);
+    }
+    P.mb20[p] = s;
+  }
+}
+
+// mb10 = vec(X'S o id) (:61 / :113), v = mb10 - mb20 (same index set as mb20's loop)
+__device__ inline void ge_seg_mb10(const GEArgs& a, const GEPtrs& P, int g0, int gs) {
+  for (int p = g0; p < P.N; p += gs) {
+    P.mb10[p] = P.XtS[p] * a.iSigma[p / a.nc];
+    P.v[p] = P.mb10[p] - P.mb20[p];
+  }
+}
+
+// with v = M^-1 (mb10 - mb20): wv = mb10 - mb20 - T1 v (mb30, :63-64), xi ~ N(0, I)
+__device__ inline void ge_seg_wv(const GEArgs& a, const GEPtrs& P, int g0, int gs, uint32_t it) {
+  const int ns = a.ns, nc = a.nc, N = P.N;
+  const uint32_t str = LEVEL_STRIDE * (uint32_t)a.r;
+  for (int p = g0; p < N; p += gs) {
+    const int c = p % nc, j = p / nc;
+    double s = 0.0;
+    if (P.obs) {
       for (int j2 = 0; j2 < ns; ++j2) {
-        const double tj = tmp1[j + (size_t)ns * j2];
+        const double tj = P.tmp1[j + (size_t)ns * j2];
         if (tj == 0.0) continue;
         double u = 0.0;
-        for (int c2 = 0; c2 < nc; ++c2) u = fma(XtX[c + nc * c2], v[c2 + nc * j2], u);
+        for (int c2 = 0; c2 < nc; ++c2) u = fma(P.XtX[c + nc * c2], P.v[c2 + nc * j2], u);
         s = fma(tj, u, s);
       }
     } else {
-      for (int p2 = 0; p2 < N; ++p2) s = fma(T[p + (size_t)N * p2], v[p2], s);
+      for (int p2 = 0; p2 < N; ++p2) s = fma(P.T[p + (size_t)N * p2], P.v[p2], s);
     }
-    wv[p] = mb10[p] - mb20[p] - s;
-    xi[p] = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)p, 0, S_GE_BETA + str, it);
+    P.wv[p] = P.mb10[p] - P.mb20[p] - s;
+    P.xi[p] = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)p, 0, S_GE_BETA + str, it);
   }
-  __syncthreads();
-  for (int p = t; p < N; p += nthr) {
-    double s = 0.0;
-    for (int p2 = 0; p2 < N; ++p2) s = fma(A[p + (size_t)N * p2], wv[p2], s);
-    mb[p] = s;
-  }
-  __syncthreads();
-  wg_backward_t(M, N, N, xi);  // backsolve(RM, rnorm(nc ns))  (:66)
-  for (int p = t; p < N; p += nthr) Beta[p] = mb[p] + xi[p];
-  __syncthreads();
+}
 
-  // ---- stage 5: Gamma | Beta   (:69-71)
+// mb = A wv   (:65)
+__device__ inline void ge_seg_mb(const GEPtrs& P, int g0, int gs) {
+  const int N = P.N;
+  for (int p = g0; p < N; p += gs) {
+    double s = 0.0;
+    for (int p2 = 0; p2 < N; ++p2) s = fma(P.A[p + (size_t)N * p2], P.wv[p2], s);
+    P.mb[p] = s;
+  }
+}
+
+// Beta = mb + RM^-1 xi (xi already back-solved); then Gamma | Beta (:66-71) -- one workgroup
+__device__ inline void ge_wg_gamma(const GEArgs& a, const GEPtrs& P, int* flag, uint32_t it) {
+  const int t = threadIdx.x, nthr = blockDim.x;
+  const int ns = a.ns, nc = a.nc, G = P.G, N = P.N;
+  const uint32_t str = LEVEL_STRIDE * (uint32_t)a.r;
+  for (int p = t; p < N; p += nthr) P.Beta[p] = P.mb[p] + P.xi[p];
+  __syncthreads();
   for (size_t p = t; p < (size_t)G * G; p += nthr) {
     const int r1 = (int)(p % G), r2 = (int)(p / G);
     const int c1 = r1 % nc, t1 = r1 / nc, c2 = r2 % nc, t2 = r2 / nc;
     double tq = 0.0;
-    for (int j = 0; j < ns; ++j) tq = fma(a.Tr[j + (size_t)ns * t1], iQTr[j + (size_t)ns * t2], tq);
-    Pg[p] = a.iUGamma[p] + tq * a.iV[c1 + nc * c2];
+    for (int j = 0; j < ns; ++j) tq = fma(a.Tr[j + (size_t)ns * t1], P.iQTr[j + (size_t)ns * t2], tq);
+    P.Pg[p] = a.iUGamma[p] + tq * a.iV[c1 + nc * c2];
   }
   for (int p = t; p < G; p += nthr) {
     const int c = p % nc, q = p / nc;
     double s = 0.0;
     for (int j = 0; j < ns; ++j) {
       double ib = 0.0;
-      for (int c2 = 0; c2 < nc; ++c2) ib = fma(a.iV[c + nc * c2], Beta[c2 + nc * j], ib);
-      s = fma(ib, iQTr[j + (size_t)ns * q], s);
+      for (int c2 = 0; c2 < nc; ++c2) ib = fma(a.iV[c + nc * c2], P.Beta[c2 + nc * j], ib);
+      s = fma(ib, P.iQTr[j + (size_t)ns * q], s);
     }
-    rg[p] = s;
+    P.rg[p] = s;
   }
   __syncthreads();
-  if (!wg_chol(Pg, G, G, &flag) && t == 0) a.fail[0] = 1;
-  wg_forward(Pg, G, G, rg);
+  if (!wg_chol(P.Pg, G, G, flag) && t == 0) a.fail[0] = 1;
+  wg_forward(P.Pg, G, G, P.rg);
   for (int p = t; p < G; p += nthr)
-    if (!a.noise_zero) rg[p] += normal(a.key, (uint32_t)p, 0, S_GE_GAMMA + str, it);
+    if (!a.noise_zero) P.rg[p] += normal(a.key, (uint32_t)p, 0, S_GE_GAMMA + str, it);
   __syncthreads();
-  wg_backward_t(Pg, G, G, rg);
-  for (int p = t; p < G; p += nthr) a.Gamma[p] = rg[p];
+  wg_backward_t(P.Pg, G, G, P.rg);
+  for (int p = t; p < G; p += nthr) a.Gamma[p] = P.rg[p];
+}
 
-  // ---- stage 6: Eta | Beta, S   (:71-74 / :136-146); S1 = S - X Beta
-  if (obs) {
-    for (int i = t; i < ny; i += nthr) {
+// Eta | Beta, S   (:71-74 / :136-146); S1 = S - X Beta, per row (np = ny) or per unit
+__device__ inline void ge_seg_eta(const GEArgs& a, const GEPtrs& P, int g0, int gs, uint32_t it) {
+  const int ny = a.ny, ns = a.ns, nc = a.nc, nf = a.nf, np = a.np;
+  const uint32_t str = LEVEL_STRIDE * (uint32_t)a.r;
+  if (P.obs) {
+    for (int i = g0; i < ny; i += gs) {
       double tv[GE_NF_MAX];
       for (int h = 0; h < nf; ++h) tv[h] = 0.0;
       for (int j = 0; j < ns; ++j) {
-        double s1 = S[i + (size_t)ny * j];
-        for (int c = 0; c < nc; ++c) s1 -= a.X[i + (size_t)ny * c] * Beta[c + nc * j];
-        for (int h = 0; h < nf; ++h) tv[h] = fma(s1, LamiD[h + nf * j], tv[h]);
+        double s1 = P.S[i + (size_t)ny * j];
+        for (int c = 0; c < nc; ++c) s1 -= a.X[i + (size_t)ny * c] * P.Beta[c + nc * j];
+        for (int h = 0; h < nf; ++h) tv[h] = fma(s1, P.LamiD[h + nf * j], tv[h]);
       }
       const int u = a.lev_pi[a.r][i];
       for (int h = 0; h < nf; ++h) {
         double me = 0.0, nz = 0.0;
-        for (int h2 = 0; h2 < nf; ++h2) me = fma(tv[h2], iW0[h2 + nf * h], me);
+        for (int h2 = 0; h2 < nf; ++h2) me = fma(tv[h2], P.iW0[h2 + nf * h], me);
         if (!a.noise_zero)
           for (int h2 = h; h2 < nf; ++h2)  // (RW0^-1 xi)_h = sum_h2 L0i[h2, h] xi_h2
-            nz = fma(L0i[h2 + nf * h], normal(a.key, (uint32_t)i, (uint32_t)h2, S_GE_ETA + str, it), nz);
+            nz = fma(P.L0i[h2 + nf * h], normal(a.key, (uint32_t)i, (uint32_t)h2, S_GE_ETA + str, it), nz);
         a.Eta[u + (size_t)np * h] = me + nz;
       }
     }
   } else {
-    for (int q = t; q < np; q += nthr) {
-      const int b = a.unit_ptr[q], e = a.unit_ptr[q + 1];
+    for (int q = g0; q < np; q += gs) {
       double tv[GE_NF_MAX];
       for (int h = 0; h < nf; ++h) tv[h] = 0.0;
       for (int j = 0; j < ns; ++j) {
-        double s1 = PtS[q + (size_t)np * j];
-        for (int c = 0; c < nc; ++c) s1 -= PtX[q + (size_t)np * c] * Beta[c + nc * j];
-        for (int h = 0; h < nf; ++h) tv[h] = fma(s1, LamiD[h + nf * j], tv[h]);
+        double s1 = P.PtS[q + (size_t)np * j];
+        for (int c = 0; c < nc; ++c) s1 -= P.PtX[q + (size_t)np * c] * P.Beta[c + nc * j];
+        for (int h = 0; h < nf; ++h) tv[h] = fma(s1, P.LamiD[h + nf * j], tv[h]);
       }
-      (void)b;
-      (void)e;
-      const double* iW = iWp + (size_t)q * nf * nf;
-      const double* Li = Lip + (size_t)q * nf * nf;
+      const double* iW = P.iWp + (size_t)q * nf * nf;
+      const double* Li = P.Lip + (size_t)q * nf * nf;
       for (int h = 0; h < nf; ++h) {
         double me = 0.0, nz = 0.0;
         for (int h2 = 0; h2 < nf; ++h2) me = fma(iW[h + nf * h2], tv[h2], me);
@@ -458,6 +495,154 @@ __global__ __launch_bounds__(1024) void gamma_eta_kernel(GEArgs a) {
   }
 }
 
+// One workgroup per level (small nc ns): the segments between barriers, the factorizations
+// by wg_chol / wg_chol2inv on the L2-resident workspace.
+__global__ __launch_bounds__(1024) void gamma_eta_kernel(GEArgs a) {
+  __shared__ int flag;
+  const int t = threadIdx.x, nthr = blockDim.x;
+  const GEPtrs P = ge_ptrs(a);
+  const int N = P.N, nc = a.nc;
+  const uint32_t it = SWEEP_ITER(a);
+  ge_seg_prep(a, P, t, nthr);
+  __syncthreads();
+  // V = chol2inv(chol(iV))
+  if (!wg_chol(P.Wv, nc, nc, &flag) && t == 0) a.fail[0] = 1;
+  wg_chol2inv(P.Wv, nc, nc, P.V, nc, P.T /* scratch: nc^2 <= N^2 */);
+  ge_seg_xts(a, P, t, nthr);
+  ge_seg_a(a, P, t, nthr);
+  __syncthreads();
+  // iA = chol2inv(chol(A)) into M (scratch T)
+  if (!wg_chol(P.L, N, N, &flag) && t == 0) a.fail[0] = 1;
+  wg_chol2inv(P.L, N, N, P.M, N, P.T);
+  if (P.obs) {
+    if (t == 0 && !ge_w0(a, P)) a.fail[0] = 1;
+    __syncthreads();
+    ge_seg_tmp1(a, P, t, nthr);
+    __syncthreads();
+    ge_seg_m_obs(a, P, t, nthr);
+  } else {
+    if (!ge_seg_units(a, P, t, nthr)) a.fail[0] = 1;
+    __syncthreads();
+    ge_seg_m_units(a, P, t, nthr);
+  }
+  ge_seg_mb10(a, P, t, nthr);
+  __syncthreads();
+  // RM = chol(M); v = M^-1 (mb10 - mb20)
+  if (!wg_chol(P.M, N, N, &flag) && t == 0) a.fail[0] = 1;
+  wg_forward(P.M, N, N, P.v);
+  wg_backward_t(P.M, N, N, P.v);
+  ge_seg_wv(a, P, t, nthr, it);
+  __syncthreads();
+  ge_seg_mb(P, t, nthr);
+  __syncthreads();
+  wg_backward_t(P.M, N, N, P.xi);  // backsolve(RM, rnorm(nc ns))  (:66)
+  ge_wg_gamma(a, P, &flag, it);
+  __syncthreads();
+  ge_seg_eta(a, P, t, nthr, it);
+}
+
+// ---- the blocked path (nc ns > GE_WG_MAX): one launch per segment, the three (nc ns)^2
+// factorizations (chol(A) and its inverse, chol(M)) and the solves on dense.hip's
+// multi-workgroup MFMA kernels
+constexpr int GE_WG_MAX = 512;
+
+#define GE_GRID_IDX                                        \
+  const GEPtrs P = ge_ptrs(a);                             \
+  const int g0 = blockIdx.x * blockDim.x + threadIdx.x;    \
+  const int gs = gridDim.x * blockDim.x;                   \
+  (void)P, (void)g0, (void)gs;
+
+__global__ __launch_bounds__(256) void ge_b_prep_kernel(GEArgs a) {
+  GE_GRID_IDX
+  ge_seg_prep(a, P, g0, gs);
+}
+// X'S, iQ Tr; V = iV^-1 and (np = ny) W0 by single threads; (np < ny) the per-unit blocks
+__global__ __launch_bounds__(256) void ge_b_xts_kernel(GEArgs a) {
+  GE_GRID_IDX
+  ge_seg_xts(a, P, g0, gs);
+  const int nc = a.nc;
+  if (g0 == 0) {  // V = chol2inv(chol(iV)) = L^-T L^-1, L^-1 in the (not yet used) T block
+    if (!t_chol_inv(P.Wv, P.T, nc)) a.fail[0] = 1;
+    for (int c1 = 0; c1 < nc; ++c1)
+      for (int c2 = 0; c2 < nc; ++c2) {
+        double s = 0.0;
+        for (int k = 0; k < nc; ++k) s += P.T[k + nc * c1] * P.T[k + nc * c2];
+        P.V[c1 + nc * c2] = s;
+      }
+  }
+  if (P.obs) {
+    if (g0 == 64 && !ge_w0(a, P)) a.fail[0] = 1;
+  } else if (!ge_seg_units(a, P, g0, gs)) {
+    a.fail[0] = 1;
+  }
+}
+__global__ __launch_bounds__(256) void ge_b_a_kernel(GEArgs a) {
+  GE_GRID_IDX
+  ge_seg_a(a, P, g0, gs);
+  if (P.obs) ge_seg_tmp1(a, P, g0, gs);
+}
+__global__ __launch_bounds__(256) void ge_b_m_kernel(GEArgs a) {
+  GE_GRID_IDX
+  if (P.obs)
+    ge_seg_m_obs(a, P, g0, gs);
+  else
+    ge_seg_m_units(a, P, g0, gs);
+  ge_seg_mb10(a, P, g0, gs);
+}
+__global__ __launch_bounds__(256) void ge_b_wv_kernel(GEArgs a) {
+  GE_GRID_IDX
+  ge_seg_wv(a, P, g0, gs, SWEEP_ITER(a));
+}
+__global__ __launch_bounds__(256) void ge_b_mb_kernel(GEArgs a) {
+  GE_GRID_IDX
+  ge_seg_mb(P, g0, gs);
+}
+__global__ __launch_bounds__(1024) void ge_b_gamma_kernel(GEArgs a) {
+  __shared__ int flag;
+  const GEPtrs P = ge_ptrs(a);
+  ge_wg_gamma(a, P, &flag, SWEEP_ITER(a));
+}
+__global__ __launch_bounds__(256) void ge_b_eta_kernel(GEArgs a) {
+  GE_GRID_IDX
+  ge_seg_eta(a, P, g0, gs, SWEEP_ITER(a));
+}
+#undef GE_GRID_IDX
+
+static int ge_blocks(size_t elems) { return (int)std::max<size_t>(1, std::min<size_t>(4096, (elems + 255) / 256)); }
+
+// workspace of the blocked path past ge_layout: the two dense_potrf_lower workspaces
+static size_t ge_blocked_extra(int N) { return N > GE_WG_MAX ? 2 * dense_ws_doubles(N) + 16 : 0; }
+
+static void launch_gamma_eta_blocked(State& s, const GEArgs& a, hipStream_t st) {
+  const bool obs = a.np == a.ny;
+  const int N = a.nc * a.ns;
+  const GELayout o = ge_layout(a.ny, a.ns, a.nc, a.nt, a.nf, obs ? 0 : a.np);
+  double* w = a.work;
+  double *L = w + o.L, *M = w + o.M, *T = w + o.T;
+  double *v = w + o.vec + 2 * (size_t)N, *xi = w + o.vec + 5 * (size_t)N;
+  double* ws1 = w + o.tot;
+  double* ws2 = ws1 + dense_ws_doubles(N);
+  const size_t NN = (size_t)N * N;
+  const size_t big = std::max<size_t>((size_t)a.ny * a.ns, (size_t)a.ns * a.ns);
+  ge_b_prep_kernel<<<ge_blocks(big), 256, 0, st>>>(a);
+  ge_b_xts_kernel<<<ge_blocks(std::max<size_t>(std::max(N, a.ns * a.nt), obs ? 128 : a.np)), 256, 0, st>>>(a);
+  ge_b_a_kernel<<<ge_blocks(NN), 256, 0, st>>>(a);
+  // iA = chol2inv(chol(A)) = L^-T L^-1   (:33)
+  dense_potrf_lower(st, L, N, N, ws1, a.fail);
+  dense_trtri_lower(st, L, N, N, T, N, ws1, true);
+  dense_lauum_lower(st, T, N, N, M, N);
+  ge_b_m_kernel<<<ge_blocks(NN), 256, 0, st>>>(a);
+  // RM = chol(M); v = M^-1 (mb10 - mb20)
+  dense_potrf_lower(st, M, N, N, ws2, a.fail);
+  dense_trsv_lower(st, M, N, N, v, 0, ws2);
+  dense_trsv_lower(st, M, N, N, v, 1, ws2);
+  ge_b_wv_kernel<<<ge_blocks(N), 256, 0, st>>>(a);
+  ge_b_mb_kernel<<<ge_blocks(N), 256, 0, st>>>(a);
+  dense_trsv_lower(st, M, N, N, xi, 1, ws2);  // backsolve(RM, rnorm(nc ns))  (:66)
+  ge_b_gamma_kernel<<<1, 1024, 0, st>>>(a);
+  ge_b_eta_kernel<<<ge_blocks(obs ? a.ny : a.np), 256, 0, st>>>(a);
+  HIP_OK(hipGetLastError());
+}
 
 // ---------------------------------------------------------------------------------------
 // Spatial 'Full' level (R/updateGammaEta.R:139-198): (vec Gamma, vec Eta_r) drawn jointly
@@ -683,7 +868,7 @@ size_t gamma_eta_work_doubles(const State& s) {
   for (int r = 0; r < s.nr; ++r) {
     const int nf = std::max(1, s.lev[r].nfmax);
     const int np = s.lev[r].np == s.ny ? 0 : s.lev[r].np;
-    m = std::max(m, ge_layout(s.ny, s.ns, s.nc, s.nt, nf, np).tot);
+    m = std::max(m, ge_layout(s.ny, s.ns, s.nc, s.nt, nf, np).tot + ge_blocked_extra(s.nc * s.ns));
     if (s.lev[r].spatial) m = std::max(m, ges_layout(s.ny, s.ns, s.nc, s.nt, nf, s.lev[r].np).tot);
   }
   return m + 64;
@@ -739,6 +924,8 @@ void launch_gamma_eta(State& s, uint32_t iter) {
       sa.iWg = s.lev[r].iWg;
       sa.AlphaD = s.lev[r].AlphaD;
       gamma_eta_spatial_kernel<<<1, 1024, 0, s.stream>>>(sa);
+    } else if (a.nc * a.ns > GE_WG_MAX) {
+      launch_gamma_eta_blocked(s, a, s.stream);
     } else {
       gamma_eta_kernel<<<1, 1024, 0, s.stream>>>(a);
     }

@@ -23,6 +23,11 @@ MODELS = {
     "phylo_td_dims": dict(ny=50, ns=4, nc=3, nf=2, nt=3, seed=44, phylo=True),
     # vignette_3 class: 50 species, nc = 3 -> a 150 x 150 dense system
     "vignette3_class": dict(ny=100, ns=50, nc=3, nf=3, seed=45, phylo=True),
+    # nc ns > 512: the blocked path (one launch per segment, dense.hip factorizations)
+    "blocked_obs": dict(ny=120, ns=200, nc=3, nf=3, seed=46, phylo=True),
+    "blocked_grouped": dict(ny=90, ns=180, nc=3, nf=2, units=[15], seed=47),
+    # config 3 (vignette_3: nc = 4, two traits + intercept, phylogeny) at 300 species
+    "blocked_cfg3": dict(ny=200, ns=300, nc=4, nt=3, nf=5, seed=48, phylo=True),
 }
 
 
