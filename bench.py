@@ -43,8 +43,9 @@ def parse():
     p.add_argument("--steps", type=int, default=1000)
     p.add_argument("--warmup", type=int, default=100)
     p.add_argument("--mode", choices=["chains", "sharded"], default="chains")
-    p.add_argument("--workload", choices=["synthetic", "spatial"], default="synthetic",
-                   help="synthetic: config 4 (the metric); spatial: config 5, vignette_4 'Full' at --ny")
+    p.add_argument("--workload", choices=["synthetic", "spatial", "phylo"], default="synthetic",
+                   help="synthetic: config 4 (the metric); spatial: config 5, vignette_4 'Full' at --ny; "
+                        "phylo: config 3, vignette_3 (phylogeny, traits, GammaEta) at --ns species")
     p.add_argument("--ny", type=int, default=10000)
     p.add_argument("--ns", type=int, default=1000)
     p.add_argument("--nc", type=int, default=20)
@@ -60,6 +61,8 @@ def main():
     args = parse()
     if args.workload == "spatial":
         return main_spatial(args)
+    if args.workload == "phylo":
+        return main_phylo(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -316,6 +319,91 @@ def main_spatial(args):
                                     "peak_GBs": HBM_PEAK_GBS}},
         "kernels_eager_events_us": {k: round(v["avg_us"], 1) for k, v in kern.items()},
         "alpha_posterior_mean_index": round(alpha_mean, 2),
+        "cpu_baseline": None,
+    }
+    print(json.dumps(out), flush=True)
+
+
+def main_phylo(args):
+    """BASELINE.json config 3: vignette_3 (vignettes/vignette_3_multivariate_high.Rmd:42-128)
+    scaled to --ns species (default 300 when --ns is left at the config-4 value): ny=200, nc=4,
+    nt=3, coalescent phylogeny, normal species, one sample-level level with nfMax=15, the
+    reference's default updater set (GammaEta and Rho on; R/sampleMcmc.R:124-152 keeps both).
+    One chain per GPU (the vignette's nChains).  Warm-up = transient with updateNf adaptation
+    (adaptNf = transient, R's default), then the timed sweeps with recording.  Per sweep the
+    dense phylogeny BetaLambda ((nc+nf) ns)^2 system and updateGammaEta's (nc ns)^2 systems run
+    on the blocked fp64 Cholesky (dense.hip); the roofline prices BetaLambda's factorization
+    ((nc+nf) ns)^3 / 3 flops against the fp64 matrix peak."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    H._lib.lib()
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    from hmsc_amd.workloads import vignette3_phylo
+    ns = 300 if args.ns == 1000 else args.ns
+    hM = vignette3_phylo(ns=ns)
+    t0 = time.perf_counter()
+    ch = H.Chain(hM, 4242 + 7919 * rank, device=local, updater={})
+    ch.init([int(hM.rL[0].nfMin)])
+    ch.sync()
+    setup = time.perf_counter() - t0
+    ch.run(transient=args.warmup, samples=0, thin=1, adaptNf=[args.warmup], record=False)
+    ch.sync()
+    nf = int(ch.nf()[0])
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    rec = ch.run(transient=0, samples=args.steps, thin=1, adaptNf=[0], iter0=args.warmup, record=True)
+    ch.sync()
+    if dist is not None:
+        dist.barrier()
+    t_run = time.perf_counter() - t0
+    rho_mean = float(np.mean(rec["rho"]))
+    del rec
+    n_prof = min(args.steps, 20)
+    ch.profile(True)
+    ch.run(transient=n_prof, samples=0, adaptNf=[0], iter0=args.warmup + args.steps, record=False)
+    ch.sync()
+    kern = {}
+    for name in ("betalambda", "gamma_eta", "rho", "eta_unit", "z", "sweep"):
+        tot, n = ch.profile_get(name)
+        kern[name] = dict(total_ms=tot, launches=n, avg_us=1e3 * tot / max(1, n))
+    ch.profile(False)
+    ch.close()
+    tmax = t_run
+    if dist is not None:
+        t = torch.tensor([t_run], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tmax = float(t.item())
+    if rank != 0:
+        return
+    N = (hM.nc + nf) * ns
+    flops = N ** 3 / 3.0
+    bl_s = kern["betalambda"]["avg_us"] * 1e-6
+    peak_tf = 78.6
+    achieved = flops / max(bl_s, 1e-12) / 1e12
+    out = {
+        "metric": "Gibbs sweeps/sec, config 3 (vignette_3 phylogeny + traits, default updaters) at ns=%d" % ns,
+        "value": round(world * args.steps / tmax, 3), "unit": "sweeps/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1e3 * tmax / args.steps, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (vignette_3 generator scaled to ns, coalescent phylogeny, seed 20261015)",
+        "config": {"workload": f"vignette_3 ny=200 ns={ns} nc=4 nt=3 normal, phylogeny C, sample level nfMax=15 "
+                               f"(nf={nf} after adaptation), default updaters incl. GammaEta and Rho, record every sweep",
+                   "ny": 200, "ns": ns, "nc": 4, "nt": 3, "nf": int(nf),
+                   "parallelism": f"{world} independent chains, one per GPU"},
+        "setup_s": round(setup, 2),
+        "roofline": {"kernel": "phylogeny BetaLambda: blocked Cholesky of the ((nc+nf) ns)^2 precision + solves",
+                     "bound": "mfma", "achieved": round(achieved, 2), "peak": peak_tf, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak_tf, 4), "traffic": None,
+                     "algorithmic_flops_per_launch": flops, "avg_launch_us": round(kern["betalambda"]["avg_us"], 1),
+                     "timer": "HIP events on the chain stream around the updater (eager sweeps)"},
+        "kernels_eager_events_us": {k: round(v["avg_us"], 1) for k, v in kern.items()},
+        "rho_posterior_mean_index": round(rho_mean, 2),
         "cpu_baseline": None,
     }
     print(json.dumps(out), flush=True)

@@ -959,7 +959,7 @@ static void destroy_graph(State& s) {
 static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record) {
   std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
   join_side(s);
-  const bool xv = s.xeta_valid, zv = s.zt_valid, gv = s.g2prep_valid;
+  const bool xv = s.xeta_valid, zv = s.zt_valid, gv = s.g2prep_valid, gp = s.g_pending;
   hipGraph_t g = nullptr;
   HIP_OK(hipStreamBeginCapture(s.stream, hipStreamCaptureModeThreadLocal));
   s.capturing = true;
@@ -979,13 +979,13 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record) 
     s.capturing = false;
     (void)hipStreamEndCapture(s.stream, &g);
     if (g) (void)hipGraphDestroy(g);
-    s.xeta_valid = xv, s.zt_valid = zv, s.g2prep_valid = gv;
+    s.xeta_valid = xv, s.zt_valid = zv, s.g2prep_valid = gv, s.g_pending = gp;
     throw;
   }
   s.capturing = false;
   HIP_OK(hipStreamEndCapture(s.stream, &g));
-  const bool steady = xv == s.xeta_valid && zv == s.zt_valid && gv == s.g2prep_valid;
-  s.xeta_valid = xv, s.zt_valid = zv, s.g2prep_valid = gv;  // nothing ran yet
+  const bool steady = xv == s.xeta_valid && zv == s.zt_valid && gv == s.g2prep_valid && gp == s.g_pending;
+  s.xeta_valid = xv, s.zt_valid = zv, s.g2prep_valid = gv, s.g_pending = gp;  // nothing ran yet
   hipGraphExec_t ge = nullptr;
   if (steady) HIP_OK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
   HIP_OK(hipGraphDestroy(g));
@@ -1501,7 +1501,7 @@ int hmsc_debug_get(hmsc_state* h, const char* name, double* out, int64_t n) {
     int64_t avail = 0;
     if (nm == "Z") src = s.Z, avail = (int64_t)s.ny * s.nsl;
     else if (nm == "XZ") src = s.XZ, avail = (int64_t)s.K * s.nsl;
-    else if (nm == "G") src = s.G, avail = (int64_t)s.Kmax * s.Kmax;
+    else if (nm == "G") flush_g(s), src = s.G, avail = (int64_t)s.Kmax * s.Kmax;
     else if (nm == "ZTr") src = s.ZTr, avail = (int64_t)s.ny * s.nt;
     else if (nm == "BL") src = s.BL, avail = (int64_t)s.K * s.nsl;
     else if (nm == "BL_prec") src = s.dbg_prec, avail = s.dbg_prec ? (int64_t)s.nsl * s.K * s.K : 0;

@@ -877,6 +877,7 @@ size_t gamma_eta_work_doubles(const State& s) {
 void launch_gamma_eta(State& s, uint32_t iter) {
   HMSC_REQUIRE(s.nranks == 1, "updateGammaEta: species-sharded chains are not supported (dense (nc ns)^2 system)");
   HMSC_REQUIRE(s.geWork != nullptr, "updateGammaEta: workspace not allocated");
+  ProfScope ps(s, PROF_GE);
   for (int r = 0; r < s.nr; ++r) {
     GEArgs a{};
     a.ny = s.ny;

@@ -170,6 +170,7 @@ static int grid_for(int64_t n, int block = 64, int cap = 2048) {
 }
 
 void launch_xeta(State& s) {
+  s.g_pending = false;  // G rebuilt below
   const int n_tiles = (s.ny + 63) / 64;
   xeta_gram_kernel<<<n_tiles, 256, (size_t)s.K * ZT_LD * sizeof(double), s.stream>>>(make_view(s), s.K, s.Kmax,
                                                                                        s.XEta, s.G_part);
@@ -389,8 +390,10 @@ __global__ __launch_bounds__(256) void beta_lambda_wave_kernel(BLArgs a) {
 
 void launch_beta_lambda(State& s, uint32_t iter) {
   if (!s.xeta_valid) launch_xeta(s);
+  flush_g(s);
   if (!s.zt_valid) launch_zt_refresh(s);
   if (s.phylo) {  // dense branch with phylogeny (R/updateBetaLambda.R:124-147), phylo.hip
+    ProfScope ps(s, PROF_BL);
     launch_beta_lambda_phylo(s, iter);
     return;
   }
@@ -612,10 +615,7 @@ struct GVWArgs {
   // Gamma2 prep constants / output
   const double* XX;
   const double* iV0;
-  const double* V0g;
-  const double* V0gXX;
-  const double* V0gXXV0g;
-  double* prep;
+  double* prep;      // Gamma2 prep [B1 nc^2 | LS N^2]
   Key key;
   uint32_t iter;
   const uint32_t* iter_dev;  // graph replay: the sweep counter is read from the device
@@ -664,6 +664,7 @@ __device__ __forceinline__ void gammav_body(const GVWArgs& a) {
   __shared__ __attribute__((aligned(16))) double S[3 * WV_TILE];
   __shared__ __attribute__((aligned(16))) double SG[WV_TILE];
   __shared__ __attribute__((aligned(16))) double T0[WV_TILE], T1[WV_TILE], T2[WV_TILE], T3[WV_TILE];
+  __shared__ __attribute__((aligned(16))) double sXX[WV_TILE];  // X'X for wave 1 (ld WV_LD)
   __shared__ double sBTr[32];
   __shared__ int sok;
   double* sA = T0;
@@ -671,10 +672,28 @@ __device__ __forceinline__ void gammav_body(const GVWArgs& a) {
   const int nA = nc * nc, nB = nc * nt;
   HMSC_STAMP(0);
   if (t == 0) sok = 1;
+  for (int p = t; p < nA; p += blockDim.x) sXX[p % nc + WV_LD * (p / nc)] = a.XX[p];
   for (int p = t; p < nA + nB; p += blockDim.x) {
+    // species-block partials in block order, 32 loads in flight (one L2 round trip per 32)
+    const double* src = a.part + p;
+    const size_t st = (size_t)(nA + nB);
     double sum = 0.0;
-#pragma unroll 8
-    for (int b = 0; b < a.nparts; ++b) sum += a.part[(size_t)b * (nA + nB) + p];
+    int b = 0;
+    for (; b + 32 <= a.nparts; b += 32) {
+      double x[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) x[u] = src[st * (b + u)];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) sum += x[u];
+    }
+    for (; b + 8 <= a.nparts; b += 8) {
+      double x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = src[st * (b + u)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sum += x[u];
+    }
+    for (; b < a.nparts; ++b) sum += src[st * b];
     if (p < nA)
       sA[p] = sum + a.V0[p];  // E E^T + V0   (R/updateGammaV.R:18-19)
     else
@@ -745,7 +764,7 @@ __device__ __forceinline__ void gammav_body(const GVWArgs& a) {
   wv_from_lds<NM>(T1, z);                               // z = iV
   bool ok2 = true;
   // iP = inv(iV + XX)
-  wv_load<NM>(a.XX, nc, nc, x);
+  wv_load<NM>(sXX, WV_LD, nc, x);
 #pragma unroll
   for (int k = 0; k < NM; ++k) x[k] = (i < nc && k < nc) ? x[k] + z[k] : x[k];
   ok2 &= wv_chol<NM>(x, dinv);
@@ -753,43 +772,26 @@ __device__ __forceinline__ void gammav_body(const GVWArgs& a) {
   wv_to_lds<NM>(y, T2);                                 // T2 = iP
   HMSC_STAMP_W(11);
   wv_mm_rt<NM>(z, T2, x, S);                            // x = B1 = iV iP
-  wv_store<NM>(a.prep + nA, nc, nc, x);
-  wv_mm_rt<NM>(x, T1, y, S);                            // y = iV iP iV
-#pragma unroll
-  for (int k = 0; k < NM; ++k) y[k] = z[k] - y[k];      // M1 = iV - iV iP iV
-  wv_to_lds<NM>(y, T3);                                 // T3 = M1
+  wv_store<NM>(a.prep, nc, nc, x);
+  wv_load<NM>(sXX, WV_LD, nc, y);
+  wv_gemm<NM, false, true>(y, x, z, S);                 // z = M = XX iP iV = XX B1^T
+  wv_to_lds<NM>(z, T3);                                 // T3 = M
   wv_sync();
-  wv_kron<NM>(x, nc, nt, a.TT, 1.0, a.iV0, nc, T3, WV_LD, nullptr);  // WN = I (x) iV0 + TT (x) M1
-  ok2 &= wv_chol<NM>(x, dinv);
-  wv_chol2inv<NM>(x, dinv, y, S);                       // y = Rm   (:44)
-  wv_to_lds<NM>(y, T0);                                 // T0 = Rm
-  HMSC_STAMP_W(12);
-  wv_load<NM>(a.V0gXX, nc, nc, x);
-  wv_mm_rt<NM>(x, T2, z, S);                            // z = T1m = V0 XX iP
-  wv_load<NM>(a.V0g, nc, nc, y);
-#pragma unroll
-  for (int k = 0; k < NM; ++k) y[k] -= z[k];            // A1 = V0 - V0 XX iP
-  wv_store<NM>(a.prep, nc, nc, y);
-  wv_mm_rt<NM>(z, T1, y, S);                            // y = W1 = T1m iV
-  wv_to_lds<NM>(y, T3);                                 // T3 = W1
-  wv_gemm<NM, false, true>(z, x, y, S);                 // y = T1m V0XX^T     (x = V0gXX)
-  wv_load<NM>(a.V0gXXV0g, nc, nc, x);
-#pragma unroll
-  for (int k = 0; k < NM; ++k) x[k] -= y[k];            // M1' = V0 XX V0 - V0 XX iP XX V0
-  wv_to_lds<NM>(x, T2);                                 // T2 = M1'
-  wv_sync();
-  wv_kron<NM>(z, nc, nt, a.TT, 0.0, nullptr, 0, T3, WV_LD, nullptr);  // z = tmp = TT (x) W1   (:48)
-  wv_mm_rt<NM>(z, T0, x, S);                            // x = TR = tmp Rm
-  wv_store<NM>(a.prep + 2 * nA, N, N, x);
-  HMSC_STAMP_W(13);
-  wv_gemm<NM, false, true>(x, z, y, S);                 // y = tmp Rm tmp^T
-  wv_kron<NM>(x, nc, nt, a.TT, 1.0, a.V0g, nc, T2, WV_LD, nullptr);  // x = I (x) V0 + TT (x) M1'
-  wv_kron<NM>(z, nc, nt, a.TT, 0.0, nullptr, 0, T2, WV_LD, nullptr); // z = TT (x) M1'
-#pragma unroll
-  for (int k = 0; k < NM; ++k) x[k] = x[k] - 2.0 * z[k] + y[k];     // SigmaG   (:50)
+  wv_kron<NM>(x, nc, nt, a.TT, 1.0, a.iV0, nc, T3, WV_LD, nullptr);  // Pg = I (x) iV0 + TT (x) M
   wv_pad<NM>(x, N, 1.0);
-  ok2 &= wv_chol<NM>(x, dinv);                          // LSigmaG   (:52)
-  wv_store_lower<NM>(a.prep + 2 * nA + N * N, N, N, x);
+  wv_to_lds<NM>(x, T0);
+  wv_sync();
+  HMSC_STAMP_W(12);
+  wv_load_rev<NM>(T0, WV_LD, N, x);                     // J Pg J
+  ok2 &= wv_chol<NM>(x, dinv);                          // = Mc Mc^T
+  wv_inv_lower<NM>(x, dinv, y);                         // Mc^-1 by rows
+  HMSC_STAMP_W(13);
+  // LS = J Mc^-T J: element (i, k) of Mc^-1 (lane i, k <= i) is LS[N-1-k][N-1-i]
+  double* LS = a.prep + nA;
+  if (i < N)
+#pragma unroll
+    for (int k = 0; k < NM; ++k)
+      if (k < N) LS[(N - 1 - k) + (size_t)N * (N - 1 - i)] = (k <= i) ? y[k] : 0.0;
   if (!ok2 && i == 0) a.fail[1] = 1;
   HMSC_STAMP_W(14);
 }
@@ -816,9 +818,6 @@ static GVWArgs make_gvw_args(State& s, uint32_t iter, const double* part, int np
   w.Gamma = s.Gamma;
   w.XX = s.XX;
   w.iV0 = s.iV0;
-  w.V0g = s.V0g;
-  w.V0gXX = s.V0gXX;
-  w.V0gXXV0g = s.V0gXXV0g;
   w.prep = s.g2prep;
   w.key = s.key;
   w.iter = iter;
@@ -953,23 +952,23 @@ __global__ __launch_bounds__(256) void xt_ztr_kernel(const double* X, const doub
 
 // Gamma2 splits into the part that depends only on iV (prep; runs on the side stream right
 // after updateGammaV of the previous sweep, overlapped with updateEta / updateZ) and the part
-// that needs the new Z (final).  With iP = (iV + X'X)^-1 (R/updateGamma2.R:40-50):
-//   A1 = V0 - V0 X'X iP,  B1 = iV iP,  Rm = (I (x) iV0 + TT (x) (iV - iV iP iV))^-1,
-//   tmp = TT (x) (V0 X'X iP iV),  TR = tmp Rm,
-//   SigmaG = I (x) V0 - TT (x) (V0 X'X V0 - V0 X'X iP X'X V0) + TR tmp^T,   LS = chol(SigmaG)
-//   muG = vec(A1 XZT) - TR vec(B1 XZT);   Gamma = muG + LS xi.
-// (t2 t2^T = V0 X'X iP X'X V0 and (tmp LR)(tmp LR)^T = tmp Rm tmp^T: the reference's two
-// extra Cholesky factors LiP, LR are algebraically redundant.)
+// that needs the new Z (final).  R (R/updateGamma2.R:40-54) forms the posterior covariance
+// SigmaG of Gamma (B integrated out) and its mean muG through Rm = (I (x) iV0 + TT (x) (iV -
+// iV iP iV))^-1, iP = (iV + X'X)^-1.  With M = X'X iP iV (= iV - iV iP iV, symmetric) and
+// B1 = iV iP the same two quantities are
+//   SigmaG = Pg^-1,  Pg = I (x) iV0 + TT (x) M   (Woodbury on R's expression),
+//   muG    = Pg^-1 vec(B1 XZT)                    (XZT - X'X iP XZT = B1 XZT),
+// so the prep keeps B1 and LS = chol(SigmaG) (lower; unique, hence R's LSigmaG), and the final
+// stage draws Gamma = muG + LS xi = LS (LS^T vec(B1 XZT) + xi) -- two triangular products.
+// LS without forming SigmaG: chol(J Pg J) = Mc Mc^T (J the exchange matrix) gives
+// Pg = (J Mc J)(J Mc J)^T and LS = J Mc^-T J.
 struct G2PrepArgs {
   int nc, nt;
   const double* iV;
   const double* XX;
   const double* TT;
   const double* iV0;
-  const double* V0g;
-  const double* V0gXX;
-  const double* V0gXXV0g;
-  double* prep;      // [A1 nc^2 | B1 nc^2 | TR N^2 | LS N^2]
+  double* prep;      // [B1 nc^2 | LS N^2]
   double* scratch;
   int use_lds;
   int* fail;
@@ -981,70 +980,35 @@ __global__ __launch_bounds__(256) void gamma2_prep_kernel(G2PrepArgs a) {
   __shared__ int flag;
   double* iV = a.use_lds ? lds : a.scratch;  // nc^2
   double* XX = iV + n2;
-  double* V0g = XX + n2;
-  double* V0gXX = V0g + n2;
-  double* W = V0gXX + n2;
+  double* W = XX + n2;
   double* iP = W + n2;
   double* B1 = iP + n2;
-  double* M1 = B1 + n2;
-  double* T1 = M1 + n2;
-  double* W1 = T1 + n2;
-  double* WN = W1 + n2;      // N^2
-  double* Rm = WN + N * N;   // N^2
-  double* TM = Rm + N * N;   // N^2 (tmp)
-  double* TR = TM + N * N;   // N^2
-  double* Sg = TR + N * N;   // N^2
+  double* M = B1 + n2;
+  double* T1 = M + n2;
+  double* Pg = T1 + n2;      // N^2
+  double* Sg = Pg + N * N;   // N^2
+  double* Tn = Sg + N * N;   // N^2 scratch
   for (int p = t; p < n2; p += blockDim.x) {
     iV[p] = a.iV[p];
     XX[p] = a.XX[p];
-    V0g[p] = a.V0g[p];
-    V0gXX[p] = a.V0gXX[p];
     W[p] = a.iV[p] + a.XX[p];
   }
   __syncthreads();
   if (!wg_chol(W, nc, nc, &flag) && t == 0) *a.fail = 1;
   wg_chol2inv(W, nc, nc, iP, nc, T1);                                      // iP = inv(iV + XX)
   wg_gemm(nc, nc, nc, 1.0, iV, nc, false, iP, nc, false, 0.0, B1, nc);     // B1 = iV iP
-  wg_gemm(nc, nc, nc, -1.0, B1, nc, false, iV, nc, false, 0.0, M1, nc);    // M1 = iV - iV iP iV
-  for (int p = t; p < n2; p += blockDim.x) M1[p] += iV[p];
-  __syncthreads();
+  wg_gemm(nc, nc, nc, 1.0, XX, nc, false, B1, nc, true, 0.0, M, nc);       // M = XX iP iV
   for (int p = t; p < N * N; p += blockDim.x) {
     const int r = p % N, c = p / N, c1 = r % nc, q1 = r / nc, c2 = c % nc, q2 = c / nc;
-    WN[p] = (q1 == q2 ? a.iV0[c1 + nc * c2] : 0.0) + a.TT[q1 + nt * q2] * M1[c1 + nc * c2];
+    Pg[p] = (q1 == q2 ? a.iV0[c1 + nc * c2] : 0.0) + a.TT[q1 + nt * q2] * M[c1 + nc * c2];
   }
   __syncthreads();
-  if (!wg_chol(WN, N, N, &flag) && t == 0) *a.fail = 1;
-  wg_chol2inv(WN, N, N, Rm, N, Sg);                                        // Rm   (:44)
-  wg_gemm(nc, nc, nc, 1.0, V0gXX, nc, false, iP, nc, false, 0.0, T1, nc);  // V0 XX iP
-  wg_gemm(nc, nc, nc, 1.0, T1, nc, false, iV, nc, false, 0.0, W1, nc);     // V0 XX iP iV
-  for (int p = t; p < N * N; p += blockDim.x) {
-    const int r = p % N, c = p / N, c1 = r % nc, q1 = r / nc, c2 = c % nc, q2 = c / nc;
-    TM[p] = a.TT[q1 + nt * q2] * W1[c1 + nc * c2];                        // tmp   (:48)
-  }
-  __syncthreads();
-  wg_gemm(N, N, N, 1.0, TM, N, false, Rm, N, false, 0.0, TR, N);           // TR = tmp Rm
-  wg_gemm(nc, nc, nc, -1.0, T1, nc, false, V0gXX, nc, true, 0.0, M1, nc);  // -V0 XX iP XX V0
-  for (int p = t; p < n2; p += blockDim.x) {
-    M1[p] += a.V0gXXV0g[p];
-    W[p] = V0g[p] - T1[p];                                                 // A1 = V0 - V0 XX iP
-  }
-  __syncthreads();
-  wg_gemm(N, N, N, 1.0, TR, N, false, TM, N, true, 0.0, Sg, N);            // tmp Rm tmp^T
-  for (int p = t; p < N * N; p += blockDim.x) {
-    const int r = p % N, c = p / N, c1 = r % nc, q1 = r / nc, c2 = c % nc, q2 = c / nc;
-    Sg[p] += (q1 == q2 ? V0g[c1 + nc * c2] : 0.0) - a.TT[q1 + nt * q2] * M1[c1 + nc * c2];   // (:50)
-  }
-  __syncthreads();
+  if (!wg_chol(Pg, N, N, &flag) && t == 0) *a.fail = 1;
+  wg_chol2inv(Pg, N, N, Sg, N, Tn);                                        // SigmaG = Pg^-1
   if (!wg_chol(Sg, N, N, &flag) && t == 0) *a.fail = 1;                    // LSigmaG   (:52)
   double* out = a.prep;
-  for (int p = t; p < n2; p += blockDim.x) {
-    out[p] = W[p];
-    out[n2 + p] = B1[p];
-  }
-  for (int p = t; p < N * N; p += blockDim.x) {
-    out[2 * n2 + p] = TR[p];
-    out[2 * n2 + N * N + p] = (p % N >= p / N) ? Sg[p] : 0.0;
-  }
+  for (int p = t; p < n2; p += blockDim.x) out[p] = B1[p];
+  for (int p = t; p < N * N; p += blockDim.x) out[n2 + p] = (p % N >= p / N) ? Sg[p] : 0.0;
 }
 
 struct G2Args {
@@ -1067,7 +1031,7 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
   // small products then run from LDS instead of as per-thread loops of dependent global loads.
   __shared__ int all_one;
   __shared__ double S0[512], LTr[512], v1[256], v2[256], xi[256], red[8][64];
-  extern __shared__ __attribute__((aligned(16))) double dyn[];  // A1 | B1 | TR | LS  when a.stage
+  extern __shared__ __attribute__((aligned(16))) double dyn[];  // B1 | LS  when a.stage
   HMSC_STAMP(30);
   const int nc = a.nc, nt = a.nt, N = nc * nt, t = threadIdx.x, n2 = nc * nc;
   if (t == 0) all_one = 1;
@@ -1079,18 +1043,12 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
   __syncthreads();
   if (!all_one) return;
   const int n1 = nc * nt, nL = a.NF * nt, P = n1 + nL;
-  const double* A1g = a.prep;
-  const double* B1g = A1g + n2;
-  const double* TRg = B1g + n2;
-  const double* LSg = TRg + N * N;
-  const double *A1 = A1g, *B1 = B1g, *TR = TRg, *LS = LSg;
+  const double *B1 = a.prep, *LS = a.prep + n2;
   if (a.stage) {
     double* d = dyn;
-    for (int p = t; p < 2 * n2 + 2 * N * N; p += blockDim.x) d[p] = a.prep[p];
-    A1 = d;
-    B1 = d + n2;
-    TR = B1 + n2;
-    LS = TR + N * N;
+    for (int p = t; p < n2 + N * N; p += blockDim.x) d[p] = a.prep[p];
+    B1 = d;
+    LS = d + n2;
   }
   // species-block partials: 8 groups of 32 threads, each summing every 8th part
   if (P <= 64 && a.nparts > 1) {
@@ -1135,22 +1093,24 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
     S0[p] -= s;
   }
   __syncthreads();
+  // r = vec(B1 XZT); u = LS^T r + xi; Gamma = LS u = muG + LS xi   (:49, :53-54)
   for (int p = t; p < N; p += blockDim.x) {
     const int c = p % nc, q = p / nc;
-    double s1 = 0.0, s2 = 0.0;
-    for (int k = 0; k < nc; ++k) {
-      s1 += A1[c + nc * k] * S0[k + nc * q];
-      s2 += B1[c + nc * k] * S0[k + nc * q];
-    }
-    v1[p] = s1;
+    double s2 = 0.0;
+    for (int k = 0; k < nc; ++k) s2 += B1[c + nc * k] * S0[k + nc * q];
     v2[p] = s2;
   }
   __syncthreads();
   for (int r = t; r < N; r += blockDim.x) {
-    double m = v1[r];
-    for (int c = 0; c < N; ++c) m -= TR[r + N * c] * v2[c];
-    for (int c = 0; c <= r; ++c) m += LS[r + N * c] * xi[c];
-    a.Gamma[r] = m;                                                        // (:49, :53-54)
+    double u = xi[r];
+    for (int c = r; c < N; ++c) u = fma(LS[c + N * r], v2[c], u);
+    v1[r] = u;
+  }
+  __syncthreads();
+  for (int r = t; r < N; r += blockDim.x) {
+    double g = 0.0;
+    for (int c = 0; c <= r; ++c) g = fma(LS[r + N * c], v1[c], g);
+    a.Gamma[r] = g;
   }
   HMSC_STAMP(32);
 }
@@ -1163,14 +1123,11 @@ static void launch_gamma2_prep(State& s, hipStream_t st) {
   a.XX = s.XX;
   a.TT = s.TT;
   a.iV0 = s.iV0;
-  a.V0g = s.V0g;
-  a.V0gXX = s.V0gXX;
-  a.V0gXXV0g = s.V0gXXV0g;
   a.prep = s.g2prep;
   a.scratch = s.scratch2;
   a.fail = s.dev_flags + 1;
   const size_t N = (size_t)s.nc * s.nt;
-  const size_t need = (10 * (size_t)s.nc * s.nc + 5 * N * N) * sizeof(double);
+  const size_t need = (7 * (size_t)s.nc * s.nc + 3 * N * N) * sizeof(double);
   a.use_lds = need <= 64 * 1024;
   gamma2_prep_kernel<<<1, 256, a.use_lds ? need : 0, st>>>(a);
   HIP_OK(hipGetLastError());
@@ -1194,6 +1151,7 @@ void launch_gamma2(State& s, uint32_t iter) {
   HMSC_REQUIRE((size_t)s.nc * s.nt <= 256 && s.NF * s.nt + s.nc * s.nt <= 1024,
                "updateGamma2: nc*nt must be <= 256 in this build");
   if (!s.xeta_valid) launch_xeta(s);
+  flush_g(s);
   if (!s.zt_valid) launch_zt_refresh(s);
   if (!s.g2prep_valid) {
     join_side(s);
@@ -1238,7 +1196,7 @@ void launch_gamma2(State& s, uint32_t iter) {
   a.iter = iter;
   a.iter_dev = s.capturing ? s.d_iter : nullptr;
   a.noise_zero = s.noise_mode;
-  const size_t N = (size_t)s.nc * s.nt, stage_bytes = (2 * (size_t)s.nc * s.nc + 2 * N * N) * sizeof(double);
+  const size_t N = (size_t)s.nc * s.nt, stage_bytes = ((size_t)s.nc * s.nc + N * N) * sizeof(double);
   a.stage = stage_bytes <= 48 * 1024;
   join_side(s);  // iV and the prep matrices come from the previous sweep's GammaV (side stream)
   gamma2_final_kernel<<<1, 256, a.stage ? stage_bytes : 0, s.stream>>>(a);
@@ -1755,8 +1713,9 @@ constexpr int EF_SITES = 16;
 template <int NFB>
 __global__ __launch_bounds__(256) void eta_fused_kernel(EtaFArgs a) {
   __shared__ double sPart[4][16][EF_SITES + 1];  // [wave][factor][site] ZL partials
-  __shared__ double sL[NFB * NFB];            // lower factor of Q (column-major, ld nf)
-  __shared__ double sB[NFB][EF_SITES], sXi[NFB][EF_SITES];
+  __shared__ double sW[NFB * NFB];            // W = L^-1, L the lower factor of Q (row m at m NFB)
+  __shared__ double sWs[NFB * (NFB + 1)];     // wv_inv_lower_rows scratch
+  __shared__ double sB[NFB][EF_SITES], sXi[NFB][EF_SITES], sU[NFB][EF_SITES];
   __shared__ double sX[64][EF_SITES + 1];     // XEta tile [k][site] (K <= 64)
   __shared__ double sCR[64 * NFB];            // CR[k][h], k < K
   const unsigned long long kt0 = a.kt ? kt_now() : 0ull;
@@ -1764,14 +1723,54 @@ __global__ __launch_bounds__(256) void eta_fused_kernel(EtaFArgs a) {
   const int ny = a.ny, nf = a.nf, K = a.K, nc = a.nc, ns = a.ns_loc;
   const int i0 = blockIdx.x * EF_SITES;
   if (blockIdx.x == 0) HMSC_STAMP(50);
-  // ---- stage 1: Q factor (wave 0 first), ZL on the matrix cores (every wave)
-  // CR from its species-block partials, in block order; eight partials' loads in flight
-  // per thread before they are added (a plain loop would pay one L2 round trip per block)
+  // ---- stage 1: ZL = Z (Lambda diag(iSigma))^T on the matrix cores, the HBM stream of the
+  // launch, issued first: species j = 16 s + 4 w + lk, B = LS[j][lm] straight from L2 (128 KB,
+  // shared by every workgroup); sixteen steps' loads in flight before their MFMAs, so a wave's
+  // 63 steps (ns = 1000) cost four memory round trips
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  const double* zc = a.Z + min(i0 + lm, ny - 1);  // sites past ny: any finite row, unused
+  const int nsteps = (ns + 15) >> 4;
+  int s = 0;
+  for (; s + 16 <= nsteps; s += 16) {
+    double zv[16], lv[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int j = 16 * (s + u) + 4 * w + lk;
+      zv[u] = j < ns ? zc[(size_t)ny * j] : 0.0;
+      lv[u] = j < ns ? a.LS[(size_t)16 * j + lm] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc = mfma_f64(zv[u], lv[u], acc);
+  }
+  if (s < nsteps) {  // the tail: all its loads at once
+    double zv[16], lv[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int j = 16 * (s + u) + 4 * w + lk;
+      const bool in = s + u < nsteps && j < ns;
+      zv[u] = in ? zc[(size_t)ny * j] : 0.0;
+      lv[u] = in ? a.LS[(size_t)16 * j + lm] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc = mfma_f64(zv[u], lv[u], acc);
+  }
+  // acc[r] = partial ZL[site lk + 4 r][factor lm]
+#pragma unroll
+  for (int r = 0; r < 4; ++r) sPart[w][lm][lk + 4 * r] = acc[r];
+  // CR from its species-block partials, in block order (L2; every partial's load in flight
+  // before the adds)
   for (int p = t; p < K * nf; p += 256) {
     const int k = p % K, h = p / K;
     const double* src = a.CR_part + k + (size_t)a.ldcr * h;
     double v = 0.0;
     int b = 0;
+    for (; b + 32 <= a.ncr; b += 32) {
+      double x[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) x[u] = src[(size_t)a.slab * (b + u)];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) v += x[u];
+    }
     for (; b + 8 <= a.ncr; b += 8) {
       double x[8];
 #pragma unroll
@@ -1784,7 +1783,8 @@ __global__ __launch_bounds__(256) void eta_fused_kernel(EtaFArgs a) {
     if (blockIdx.x == 0) a.CR[k + (size_t)a.ldcr * h] = v;
   }
   __syncthreads();
-  if (w == 0) {
+  if (blockIdx.x == 0) HMSC_STAMP(51);
+  if (w == 0) {  // Q = I + Lambda D Lambda^T factor, while waves 1-3 form the right-hand sides
     double q[NFB], dinv;
     const int r = lane < nf ? lane : 0;
 #pragma unroll
@@ -1793,97 +1793,50 @@ __global__ __launch_bounds__(256) void eta_fused_kernel(EtaFArgs a) {
       q[c] = (lane < nf && c < nf) ? v : (lane == c ? 1.0 : 0.0);
     }
     wv_chol<NFB>(q, dinv);
-    if (lane < nf)
+    double wr[NFB];
+    wv_inv_lower_rows<NFB>(q, dinv, wr, sWs);  // lane m: row m of L^-1
+    if (lane < NFB)
 #pragma unroll
-      for (int c = 0; c < NFB; ++c)
-        if (c < nf) sL[lane + nf * c] = (c <= lane) ? q[c] : 0.0;
-  }
-  d4 acc = {0.0, 0.0, 0.0, 0.0};
-  const double* zc = a.Z + min(i0 + lm, ny - 1);  // sites past ny: any finite row, unused
-  // species j = 16 s + 4 w + lk; B = LS[j][lm] straight from L2 (128 KB, shared by every
-  // workgroup); eight steps' loads issued before their MFMAs
-  const int nsteps = (ns + 15) >> 4;
-  int s = 0;
-  for (; s + 8 <= nsteps; s += 8) {
-    double zv[8], lv[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int j = 16 * (s + u) + 4 * w + lk;
-      zv[u] = j < ns ? zc[(size_t)ny * j] : 0.0;
-      lv[u] = j < ns ? a.LS[(size_t)16 * j + lm] : 0.0;
+      for (int c = 0; c < NFB; ++c) sW[lane * NFB + c] = (lane < nf && c < nf && c <= lane) ? wr[c] : 0.0;
+  } else {
+    // ---- stage 2: b = ZL - X CR_x, and the noise, one (site, factor) per thread
+    for (int p = t - 64; p < EF_SITES * nf; p += 192) {
+      const int s2 = p % EF_SITES, h = p / EF_SITES, ii = i0 + s2;
+      const double zl = (sPart[0][h][s2] + sPart[1][h][s2]) + (sPart[2][h][s2] + sPart[3][h][s2]);
+      double corr = 0.0, xi = 0.0;
+      if (ii < ny) {
+        for (int k = 0; k < nc; ++k) corr = fma(a.XEta[ii + (size_t)ny * k], sCR[k * NFB + h], corr);
+        xi = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)a.Pi[ii], (uint32_t)h, S_ETA, SWEEP_ITER(a));
+      }
+      sB[h][s2] = zl - corr;
+      sXi[h][s2] = xi;
     }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) acc = mfma_f64(zv[u], lv[u], acc);
-  }
-  for (; s < nsteps; ++s) {
-    const int j = 16 * s + 4 * w + lk;
-    const double zv = j < ns ? zc[(size_t)ny * j] : 0.0;
-    const double lv = j < ns ? a.LS[(size_t)16 * j + lm] : 0.0;
-    acc = mfma_f64(zv, lv, acc);
-  }
-  // acc[r] = partial ZL[site lk + 4 r][factor lm]
-#pragma unroll
-  for (int r = 0; r < 4; ++r) sPart[w][lm][lk + 4 * r] = acc[r];
-  __syncthreads();
-  if (blockIdx.x == 0) HMSC_STAMP(51);
-  // ---- stage 2: b = ZL - X CR_x, and the noise, one (site, factor) per thread
-  if (t < EF_SITES * nf) {
-    const int s2 = t % EF_SITES, h = t / EF_SITES, ii = i0 + s2;
-    const double zl = (sPart[0][h][s2] + sPart[1][h][s2]) + (sPart[2][h][s2] + sPart[3][h][s2]);
-    double corr = 0.0, xi = 0.0;
-    if (ii < ny) {
-      for (int k = 0; k < nc; ++k) corr = fma(a.XEta[ii + (size_t)ny * k], sCR[k * NFB + h], corr);
-      xi = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)a.Pi[ii], (uint32_t)h, S_ETA, SWEEP_ITER(a));
+    // X columns of the tile into the Gram tile
+    for (int p = t - 64; p < nc * EF_SITES; p += 192) {
+      const int s2 = p % EF_SITES, k = p / EF_SITES, ii = i0 + s2;
+      sX[k][s2] = ii < ny ? a.XEta[ii + (size_t)ny * k] : 0.0;
     }
-    sB[h][s2] = zl - corr;
-    sXi[h][s2] = xi;
-  }
-  // X columns of the tile into the Gram tile
-  for (int p = t; p < nc * EF_SITES; p += 256) {
-    const int s2 = p % EF_SITES, k = p / EF_SITES, ii = i0 + s2;
-    sX[k][s2] = ii < ny ? a.XEta[ii + (size_t)ny * k] : 0.0;
   }
   __syncthreads();
   if (blockIdx.x == 0) HMSC_STAMP(53);
-  // ---- stage 3: eta = L^-T (L^-1 b + xi), one site per thread of wave 0
-  if (t < EF_SITES) {
-    const int ii = i0 + t;
-    double y[NFB];
-#pragma unroll
-    for (int h = 0; h < NFB; ++h) {
-      if (h < nf) {
-        double v = sB[h][t];
-#pragma unroll
-        for (int k = 0; k < NFB; ++k)
-          if (k < h) v -= sL[h + nf * k] * y[k];
-        y[h] = v / sL[h + nf * h];
-      } else {
-        y[h] = 0.0;
-      }
+  // ---- stage 3: eta = L^-T (L^-1 b + xi) = W^T (W b + xi), two matrix-vector phases over
+  // the (factor, site) pairs (no serial substitution chain)
+  for (int p = t; p < EF_SITES * nf; p += 256) {
+    const int s2 = p % EF_SITES, m = p / EF_SITES;
+    double u = sXi[m][s2];
+    for (int k = 0; k <= m; ++k) u = fma(sW[m * NFB + k], sB[k][s2], u);
+    sU[m][s2] = u;
+  }
+  __syncthreads();
+  for (int p = t; p < EF_SITES * nf; p += 256) {
+    const int s2 = p % EF_SITES, h = p / EF_SITES, ii = i0 + s2;
+    double e = 0.0;
+    for (int m = h; m < nf; ++m) e = fma(sW[m * NFB + h], sU[m][s2], e);
+    if (ii < ny) {
+      a.Eta[a.Pi[ii] + (size_t)a.np * h] = e;
+      a.XEta[ii + (size_t)ny * (nc + h)] = e;
     }
-#pragma unroll
-    for (int h = 0; h < NFB; ++h)
-      if (h < nf) y[h] += sXi[h][t];
-#pragma unroll
-    for (int h = NFB - 1; h >= 0; --h) {
-      if (h < nf) {
-        double v = y[h];
-#pragma unroll
-        for (int k = 0; k < NFB; ++k)
-          if (k > h && k < nf) v -= sL[k + nf * h] * y[k];
-        y[h] = v / sL[h + nf * h];
-      }
-    }
-    const int q = ii < ny ? a.Pi[ii] : 0;
-#pragma unroll
-    for (int h = 0; h < NFB; ++h)
-      if (h < nf) {
-        if (ii < ny) {
-          a.Eta[q + (size_t)a.np * h] = y[h];
-          a.XEta[ii + (size_t)ny * (nc + h)] = y[h];
-        }
-        sX[nc + h][t] = ii < ny ? y[h] : 0.0;
-      }
+    sX[nc + h][s2] = ii < ny ? e : 0.0;
   }
   __syncthreads();
   if (blockIdx.x == 0) HMSC_STAMP(54);
@@ -2046,6 +1999,14 @@ __global__ __launch_bounds__(1024) void g_eta_reduce_kernel(const double* part, 
     for (int p = threadIdx.x; p < nc * nc; p += 1024) G[p % nc + (size_t)Kmax * (p / nc)] = XX[p];
 }
 
+void flush_g(State& s) {
+  if (!s.g_pending) return;
+  g_eta_reduce_kernel<<<(s.K * s.g_nf + 63) / 64, 1024, 0, s.stream>>>(s.G_part, s.g_ntile, s.K, s.Kmax, s.nc, s.g_nf,
+                                                                       s.XX, s.G);
+  HIP_OK(hipGetLastError());
+  s.g_pending = false;
+}
+
 static bool eta_fused_ok(const State& s) {
   return s.nranks == 1 && s.nr == 1 && !s.lev[0].spatial && s.n_na_rows == 0 && s.lev[0].np == s.ny && s.lev[0].uniform_n == 1 &&
          s.lev[0].nf <= 16 && s.K <= 64 && s.LS != nullptr && !getenv_flag("HMSC_NO_ETA_FUSION");
@@ -2095,10 +2056,12 @@ static void launch_eta_fused(State& s, uint32_t iter, bool cr_done = false) {
       eta_fused_kernel<16><<<ntile, 256, 0, s.stream>>>(a);
     HIP_OK(hipGetLastError());
   }
-  g_eta_reduce_kernel<<<(s.K * L.nf + 63) / 64, 1024, 0, s.stream>>>(s.G_part, ntile, s.K, s.Kmax, s.nc, L.nf, s.XX, s.G);
-  HIP_OK(hipGetLastError());
+  // G's Eta rows: reduced from G_part by the next updateZ launch (or flush_g)
+  s.g_pending = true;
+  s.g_ntile = ntile;
+  s.g_nf = L.nf;
   s.zt_valid = false;   // Eta changed: XZ is stale until the next updateZ
-  s.xeta_valid = true;  // XEta rows and G rewritten above
+  s.xeta_valid = true;  // XEta rows rewritten above, G pending
 }
 
 void launch_eta(State& s, uint32_t iter) {

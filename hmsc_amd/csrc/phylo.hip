@@ -364,6 +364,7 @@ void launch_phylo_gv_sums(State& s, uint32_t iter, hipStream_t st) {
 }
 
 void launch_rho(State& s, uint32_t iter, hipStream_t st) {
+  ProfScope ps(s, PROF_RHO);
   PhyloArgs a = phylo_args(s, iter);
   phylo_bt_kernel<<<(s.nc * s.ns + 255) / 256, 256, 0, st>>>(a);  // Beta may have changed since GammaV
   HIP_OK(hipGetLastError());

@@ -122,6 +122,11 @@ struct State {
   // per-sweep workspaces
   double* XEta = nullptr;        // ny x Kmax    [X, Eta_1[Pi_1], ...] materialised per Eta update
   bool xeta_valid = false;
+  // G's Eta rows from the fused Eta pass' tile partials not reduced yet: the next updateZ
+  // launch reduces them on extra workgroups (z_kernel.h), any other reader of G first calls
+  // flush_g (kernels.hip)
+  bool g_pending = false;
+  int g_ntile = 0, g_nf = 0;
   double* XZ = nullptr;          // K x ns_loc   XEta^T (Yx o Z)
   double* G = nullptr;           // Kmax x Kmax  XEta^T XEta
   double* ZTr = nullptr;         // ny x nt      Z Tr (local species)
@@ -174,7 +179,7 @@ struct State {
 
   // live kernel timing (HIP events on this chain's stream), id -> launches
   bool prof = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[8];
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[10];
 
   // RCCL (species-sharded chain), or a host transport (hmsc_create_sharded_host)
   void* comm = nullptr;
@@ -210,8 +215,11 @@ enum ProfId {
   PROF_ETA_SP = 5,  // spatial updateEta (assembly + blocked Cholesky + solves)
   PROF_CHOL = 6,    // the blocked Cholesky inside it
   PROF_ALPHA = 7,   // updateAlpha (grid quadratic forms + draw)
-  PROF_N = 8
+  PROF_GE = 8,      // updateGammaEta (all levels)
+  PROF_RHO = 9,     // updateRho
+  PROF_N = 10
 };
+static_assert(PROF_N <= 10, "State::prof_ev holds 10 profile ids");
 
 struct ProfScope {  // records a start/stop event pair around one launch when profiling is on
   State& s;
@@ -238,6 +246,7 @@ void launch_update_z(State& s, uint32_t iter, bool use_raw_y);
 void launch_zt_refresh(State& s);
 int z_resident_slots(const State& s);
 void launch_xeta(State& s);
+void flush_g(State& s);
 void launch_slab_sum2(const double* p0, double* o0, int64_t n0, int np0, const double* p1, double* o1, int64_t n1,
                       int np1, hipStream_t st);
 // the same with the main-stream record pack (part 1) of a captured recorded sweep appended

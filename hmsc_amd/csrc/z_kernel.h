@@ -47,6 +47,12 @@ struct ZArgs {
   int noise_zero;
   int zprev_is_e;            // chain init: ZPrev = LFix + LRan (R/computeInitialParameters.R:250-254)
   unsigned long long* kt;    // live launch timing (KT_Z block) or null
+  // G = XEta^T XEta's Eta rows from the fused Eta pass' tile partials, reduced by the first
+  // grid row's workgroups while the others draw (gred_y0 = 1; see g_reduce_body)
+  int gred_y0, gred_groups, gred_ntile, gred_nf, gred_Kmax;
+  const double* gred_part;
+  const double* gred_XX;
+  double* gred_G;
 };
 
 constexpr int ZT_I = 64;   // sites per workgroup tile (4 waves x 16)
@@ -191,6 +197,42 @@ __device__ __noinline__ double z_poisson_draw(double e, double sd, double y, dou
   return noise_zero ? muz : fma(sqrt(sigz), qnorm_fast(u.b), muz);
 }
 
+// G's Eta rows (R/updateBetaLambda.R:21-41 of the next sweep: XEta^T XEta), deterministic:
+// output group g (64 outputs of the K x nf slab, lane = output), the 4 waves taking every 4th
+// tile, combined in LDS in wave order; written to (k, nc + h) and (nc + h, k).  The X^T X block
+// is the constant XX.  Runs on the z launch's first grid row, off updateZ's critical path.
+__device__ inline void g_reduce_body(const ZArgs& a, double* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int K = a.K, Kmax = a.gred_Kmax, nf = a.gred_nf, nc = K - nf;
+  const size_t stride = (size_t)Kmax * nf;
+  for (int g = blockIdx.x; g < a.gred_groups; g += gridDim.x) {
+    const int o = g * 64 + lane, k = o % K, h = o / K;
+    double s = 0.0;
+    if (o < K * nf) {
+      const double* p = a.gred_part + k + (size_t)Kmax * h;
+      int b = w;
+      for (; b + 4 * 19 < a.gred_ntile; b += 4 * 20) {
+        double x[20];
+#pragma unroll
+        for (int u = 0; u < 20; ++u) x[u] = p[stride * (b + 4 * u)];
+#pragma unroll
+        for (int u = 0; u < 20; ++u) s += x[u];
+      }
+      for (; b < a.gred_ntile; b += 4) s += p[stride * b];
+    }
+    __syncthreads();
+    red[w * 64 + lane] = s;
+    __syncthreads();
+    if (w == 0 && o < K * nf) {
+      const double v = (red[lane] + red[64 + lane]) + (red[128 + lane] + red[192 + lane]);
+      a.gred_G[k + (size_t)Kmax * (nc + h)] = v;
+      a.gred_G[(nc + h) + (size_t)Kmax * k] = v;
+    }
+    if (g == 0)
+      for (int p = threadIdx.x; p < nc * nc; p += blockDim.x) a.gred_G[p % nc + (size_t)Kmax * (p / nc)] = a.gred_XX[p];
+  }
+}
+
 // NKB = 16-row blocks of K (XZ output tiles per species block)
 // MODE bits (all set in the product; the microbenchmark clears them to cost each part):
 //   1 = E on the matrix cores, 2 = draws, 4 = XZ contraction, 8 = ZTr contraction
@@ -205,6 +247,11 @@ constexpr int ZT_TLD = 17;  // leading dimension of the wave's 16-site x 32-spec
 template <bool DRAW, bool HAS_NA, int NKB, int MODE = Z_ALL, bool POIS = false, bool NORMAL = true>
 __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  if (a.gred_y0 && blockIdx.y == 0) {  // the co-launched G reduction row
+    g_reduce_body(a, smem);
+    return;
+  }
+  const int by = (int)blockIdx.y - a.gred_y0;  // species block
   const unsigned long long kt0 = a.kt ? kt_now() : 0ull;
   constexpr int K16 = 16 * NKB;
   const int K = a.K, K4 = (K + 3) & ~3;
@@ -219,7 +266,7 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
   // behind every Z store in flight)
   const uint32_t iter = SWEEP_ITER(a);
   double* sT = (double*)(sFam + ZT_J) + w * (ZT_J * ZT_TLD);  // this wave's tile: E, then Z
-  const int j0 = blockIdx.y * ZT_J;
+  const int j0 = by * ZT_J;
   for (int p = t; p < K16 * ZT_J; p += 256) {
     const int k = p >> 5, jj = p & 31, j = j0 + jj;
     sBL[p] = (k < K && j < a.ns_loc) ? a.BL[k + (size_t)K * j] : 0.0;
@@ -361,7 +408,7 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
         v += __shfl_xor(v, 16);
         v += __shfl_xor(v, 32);
         const int i = i0 + lm;
-        if (lk == 0 && i < ny) a.ZTr_part[(size_t)blockIdx.y * ny * a.nt + i + (size_t)ny * tt] = v;
+        if (lk == 0 && i < ny) a.ZTr_part[(size_t)by * ny * a.nt + i + (size_t)ny * tt] = v;
       }
     }
     wave_lds_sync();

@@ -91,7 +91,20 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   a.zprev_is_e = use_raw_y;  // only the init draw reads hM$Y (R/computeInitialParameters.R:254)
   a.kt = s.kt_on ? s.d_kt + (size_t)KT_Z * 2 * KT_SLOTS : nullptr;
   dim3 grid(nchunk, s.ntile_j);
-  const size_t smem = z_smem_bytes(s.K, s.nt);
+  size_t smem = z_smem_bytes(s.K, s.nt);
+  if (draw && s.g_pending) {  // G's Eta rows reduced on an extra first grid row
+    a.gred_y0 = 1;
+    a.gred_ntile = s.g_ntile;
+    a.gred_nf = s.g_nf;
+    a.gred_Kmax = s.Kmax;
+    a.gred_groups = (s.K * s.g_nf + 63) / 64;
+    a.gred_part = s.G_part;
+    a.gred_XX = s.XX;
+    a.gred_G = s.G;
+    grid.y += 1;
+    smem = std::max(smem, (size_t)256 * sizeof(double));
+    s.g_pending = false;
+  }
   {
     ProfScope ps(s, PROF_Z);
     if (draw && s.any_poisson) {

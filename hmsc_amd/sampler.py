@@ -268,7 +268,7 @@ class Chain:
     def sync(self):
         L.check(self.lib.hmsc_sync(self.h))
 
-    PROF_IDS = dict(z=0, zl=1, betalambda=2, eta_unit=3, sweep=4, eta_spatial=5, chol=6, alpha=7)
+    PROF_IDS = dict(z=0, zl=1, betalambda=2, eta_unit=3, sweep=4, eta_spatial=5, chol=6, alpha=7, gamma_eta=8, rho=9)
 
     def profile(self, enable=True):
         L.check(self.lib.hmsc_profile(self.h, 1 if enable else 0))

@@ -78,3 +78,55 @@ def spatial_vignette4(ny=5000, method="Full", seed=SYNTHETIC_SEED, nNeighbours=1
     setPriors(rl, nfMin=1, nfMax=1)
     return Hmsc(Y=Y, X=x, covNames=["(Intercept)", "x1"], XScale=True, distr="probit", studyDesign=study,
                 ranLevels={"sample": rl})
+
+
+def coalescent_corr(ns, rng):
+    """vcv(ape::rcoal(ns), corr=TRUE): correlation matrix of a random Kingman coalescent tree
+    (ultrametric; C_ij = 1 - t_ij / T, t_ij the coalescence time of tips i and j, T the root's)."""
+    groups = [[i] for i in range(ns)]
+    t = 0.0
+    tij = np.zeros((ns, ns))
+    while len(groups) > 1:
+        k = len(groups)
+        t += rng.exponential(1.0 / (k * (k - 1) / 2.0))
+        a, b = rng.choice(k, size=2, replace=False)
+        ga, gb = groups[a], groups[b]
+        tij[np.ix_(ga, gb)] = t
+        tij[np.ix_(gb, ga)] = t
+        groups = [g for q, g in enumerate(groups) if q not in (a, b)] + [ga + gb]
+    return 1.0 - tij / t
+
+
+def vignette3_phylo(ns=300, ny=200, seed=SYNTHETIC_SEED):
+    """BASELINE.json config 3: vignettes/vignette_3_multivariate_high.Rmd:42-128 with ns species
+    ("hundreds of species"): a coalescent phylogeny C, two traits (habitat use, thermal optimum)
+    drawn N(0, C), habitat (forest/open) and climate covariates, X = [1, forest, climate,
+    climate^2] (nc = 4), TrFormula ~habitat.use + thermal.optimum (nt = 3), species niches
+    mu + 0.25 N(0, 1), normal Y = X beta + N(0, 1), one sample-level random level with
+    nfMax = 15 (nfMin default 2), default updaters (GammaEta, Rho on)."""
+    rng = np.random.default_rng(seed)
+    C = coalescent_corr(ns, rng)
+    Lc = np.linalg.cholesky(C + 1e-12 * np.eye(ns))
+    traits = np.column_stack([Lc @ rng.standard_normal(ns) for _ in range(2)])
+    habitat = rng.random(ny) < 0.5
+    climate = rng.standard_normal(ny)
+    nc = 4
+    mu = np.zeros((nc, ns))
+    mu[0] = -traits[:, 1] ** 2 / 4 - traits[:, 0]
+    mu[1] = 2 * traits[:, 0]
+    mu[2] = traits[:, 1] / 2
+    mu[3] = -0.25
+    beta = mu + 0.25 * rng.standard_normal((nc, ns))
+    X = np.column_stack([np.ones(ny), habitat.astype(float), climate, climate ** 2])
+    Y = X @ beta + rng.standard_normal((ny, ns))
+    Tr = np.column_stack([np.ones(ns), traits])
+    units = np.array([f"sample_{i:03d}" for i in range(1, ny + 1)])
+    rl = HmscRandomLevel(units=units)
+    setPriors(rl, nfMax=15)
+    try:
+        import pandas as pd
+        study = pd.DataFrame({"sample": units})
+    except Exception:  # pragma: no cover
+        study = {"sample": units}
+    return Hmsc(Y=Y, X=X, covNames=["(Intercept)", "habitatforest", "climate", "climate2"], XScale=True,
+                Tr=Tr, C=C, distr="normal", studyDesign=study, ranLevels={"sample": rl})
