@@ -1710,8 +1710,11 @@ struct EtaFArgs {
 
 constexpr int EF_SITES = 16;
 
+// __launch_bounds__(256, 3): <= 168 VGPRs, three waves per SIMD, so the 625 workgroups of the
+// synthetic config (2500 waves) are resident in one round (at 196 VGPRs they took two: 33 ->
+// 29 us).  A fifth wave doing the Z-independent work during the stream measured slower (49 us).
 template <int NFB>
-__global__ __launch_bounds__(256) void eta_fused_kernel(EtaFArgs a) {
+__global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
   __shared__ double sPart[4][16][EF_SITES + 1];  // [wave][factor][site] ZL partials
   __shared__ double sW[NFB * NFB];            // W = L^-1, L the lower factor of Q (row m at m NFB)
   __shared__ double sWs[NFB * (NFB + 1)];     // wv_inv_lower_rows scratch
@@ -1725,34 +1728,33 @@ __global__ __launch_bounds__(256) void eta_fused_kernel(EtaFArgs a) {
   if (blockIdx.x == 0) HMSC_STAMP(50);
   // ---- stage 1: ZL = Z (Lambda diag(iSigma))^T on the matrix cores, the HBM stream of the
   // launch, issued first: species j = 16 s + 4 w + lk, B = LS[j][lm] straight from L2 (128 KB,
-  // shared by every workgroup); sixteen steps' loads in flight before their MFMAs, so a wave's
-  // 63 steps (ns = 1000) cost four memory round trips
+  // shared by every workgroup); eight steps' loads in flight before their MFMAs
   d4 acc = {0.0, 0.0, 0.0, 0.0};
   const double* zc = a.Z + min(i0 + lm, ny - 1);  // sites past ny: any finite row, unused
   const int nsteps = (ns + 15) >> 4;
   int s = 0;
-  for (; s + 16 <= nsteps; s += 16) {
-    double zv[16], lv[16];
+  for (; s + 8 <= nsteps; s += 8) {
+    double zv[8], lv[8];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < 8; ++u) {
       const int j = 16 * (s + u) + 4 * w + lk;
       zv[u] = j < ns ? zc[(size_t)ny * j] : 0.0;
       lv[u] = j < ns ? a.LS[(size_t)16 * j + lm] : 0.0;
     }
 #pragma unroll
-    for (int u = 0; u < 16; ++u) acc = mfma_f64(zv[u], lv[u], acc);
+    for (int u = 0; u < 8; ++u) acc = mfma_f64(zv[u], lv[u], acc);
   }
   if (s < nsteps) {  // the tail: all its loads at once
-    double zv[16], lv[16];
+    double zv[8], lv[8];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < 8; ++u) {
       const int j = 16 * (s + u) + 4 * w + lk;
       const bool in = s + u < nsteps && j < ns;
       zv[u] = in ? zc[(size_t)ny * j] : 0.0;
       lv[u] = in ? a.LS[(size_t)16 * j + lm] : 0.0;
     }
 #pragma unroll
-    for (int u = 0; u < 16; ++u) acc = mfma_f64(zv[u], lv[u], acc);
+    for (int u = 0; u < 8; ++u) acc = mfma_f64(zv[u], lv[u], acc);
   }
   // acc[r] = partial ZL[site lk + 4 r][factor lm]
 #pragma unroll
