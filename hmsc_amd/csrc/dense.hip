@@ -6,7 +6,9 @@
 //
 // Cholesky A = L L^T, right-looking in 64-column panels, three launches per panel:
 //   1. chol_diag_kernel    one workgroup factors the 64 x 64 diagonal block in LDS and
-//                          writes L_kk and its inverse L_kk^-1 (a 64 x 64 workspace)
+//                          writes L_kk and its inverse L_kk^-1 (a 64 x 64 workspace).  (Fusing
+//                          it into workgroup 0 of the previous trailing update was measured: its
+//                          register demand halves the update's occupancy, no net gain.)
 //   2. chol_panel_kernel   every 64-row block below: A_ik <- A_ik L_kk^-T, a 64x64x64 GEMM
 //                          on v_mfma_f64_16x16x4 (L_kk^-1 from the workspace, in LDS)
 //   3. chol_update_kernel  every lower tile (i >= j) of the trailing matrix:
@@ -34,11 +36,13 @@ constexpr int DLD = DB + 1;  // padded LDS leading dimension
 // The block sits in LDS and is factored in four 16-column steps (the serial pivot chain is
 // only ever 16 long inside one wave):
 //   a. wave 0 factors the 16 x 16 diagonal sub-block with one row per lane in registers,
-//      pivots and column entries broadcast by v_readlane (no LDS round trip per pivot), and
-//      inverts it the same way;
-//   b. all 256 threads apply that inverse to the rows below (P = A L16^-T);
-//   c. all 256 threads update the trailing lower triangle (A -= P P^T).
-// L^-1's off-diagonal 16-blocks then follow by diagonal distance,
+//      pivots and column entries broadcast by v_readlane (no LDS round trip per pivot); the
+//      rows of its inverse then follow by substitution along each row with the factor read
+//      back from LDS at wave-uniform addresses (broadcast reads, no cross-lane traffic);
+//   b. the panel below, P = A L16^-T, as 16 x 16 MFMA tiles (one wave per 16-row tile);
+//   c. the trailing lower 16 x 16 tiles, A_IJ -= P_I P_J^T, on the matrix cores, the tiles
+//      spread over the four waves.
+// L^-1's off-diagonal 16-blocks then follow by diagonal distance (one wave per block, MFMA),
 //   I_ib,jb = -I_ib,ib sum_{k = jb}^{ib - 1} L_ib,k I_k,jb.
 // Rows / columns past n are identity padding.
 __device__ __forceinline__ double readlane_d(double v, int l) {
@@ -47,23 +51,27 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-__global__ __launch_bounds__(256) void chol_diag_kernel(double* A, int lda, int n, int k0, double* Linv, int* info) {
-  __shared__ double T[DB * DLD];  // the block; its lower triangle becomes L
-  __shared__ double I[DB * DLD];  // L^-1 (lower)
-  __shared__ double S[DB * DLD];  // scratch of the L^-1 off-diagonal blocks
+// D[i][j] (+)= sum_{k < 16} X[xr + i][xc + k] Y[yr + j][yc + k] for LDS tiles (ld DLD); lane
+// holds D[lk + 4 r][lm]
+__device__ __forceinline__ d4 mma16_nt(const double* X, int xr, int xc, const double* Y, int yr, int yc, d4 acc) {
+  const int lane = threadIdx.x & 63, lm = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4)
+    acc = mfma_f64(X[(xr + lm) + DLD * (xc + 4 * s4 + lk)], Y[(yr + lm) + DLD * (yc + 4 * s4 + lk)], acc);
+  return acc;
+}
+
+// The factorization of the block staged in T (lower triangle, zeros above, identity past nb);
+// I zeroed; S: 4 x 16 x 17 doubles.  All 256 threads.
+__device__ inline void diag_body(double* T, double* I, double (*S)[16 * 17], double* A, int lda, int n, int k0,
+                          double* Linv, int* info) {
   __shared__ int bad;
-  const int nb = min(DB, n - k0), t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int nb = min(DB, n - k0), t = threadIdx.x, lane = t & 63, w = t >> 6, lm = lane & 15, lk = lane >> 4;
   if (t == 0) bad = 0;
-  for (int p = t; p < DB * DB; p += 256) {
-    const int r = p & 63, c = p >> 6;
-    T[r + DLD * c] = (r < nb && c < nb) ? (r >= c ? A[(size_t)(k0 + r) + (size_t)lda * (k0 + c)] : 0.0)
-                                        : (r == c ? 1.0 : 0.0);
-    I[r + DLD * c] = 0.0;
-  }
   __syncthreads();
   for (int kb = 0; kb < 4; ++kb) {
     const int K0 = 16 * kb;
-    if (w == 0) {  // a. 16 x 16 Cholesky + inverse, row (lane & 15) per lane
+    if (w == 0) {  // a. 16 x 16 Cholesky, row (lane & 15) per lane
       const int rl = lane & 15;
       double b[16];
 #pragma unroll
@@ -81,75 +89,79 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(double* A, int lda, int 
         for (int j = c + 1; j < 16; ++j) b[j] = fma(-m, readlane_d(m, j), b[j]);
       }
       if (nonpd && lane == 0) bad = 1;
+      if (lane < 16) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) T[(K0 + rl) + DLD * (K0 + j)] = j <= rl ? b[j] : 0.0;
+      }
+      wave_lds_sync();
+      // row rl of L16^-1: x_rl = 1 / L_rl,rl, x_j = -(sum_{k = j+1}^{rl} x_k L_kj) / L_jj
+      double x[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) x[j] = 0.0;
       double dl = 1.0;
 #pragma unroll
       for (int c = 0; c < 16; ++c) dl = (rl == c) ? b[c] : dl;
-      double x[16];
+      const double xr = 1.0 / dl;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) x[j] = (j == rl) ? 1.0 / dl : 0.0;
-#pragma unroll
-      for (int j = 14; j >= 0; --j) {
+      for (int j = 15; j >= 0; --j) {
         double s = 0.0;
 #pragma unroll
-        for (int k = j + 1; k < 16; ++k) s = fma(x[k], readlane_d(b[j], k), s);
-        const double v = -s / readlane_d(b[j], j);
-        x[j] = (j < rl) ? v : x[j];
+        for (int k = j + 1; k < 16; ++k) s = fma(x[k], T[(K0 + k) + DLD * (K0 + j)], s);
+        const double v = -s / T[(K0 + j) + DLD * (K0 + j)];
+        x[j] = (j == rl) ? xr : ((j < rl) ? v : 0.0);
       }
       if (lane < 16) {
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          T[(K0 + rl) + DLD * (K0 + j)] = j <= rl ? b[j] : 0.0;
-          I[(K0 + rl) + DLD * (K0 + j)] = x[j];
-        }
+        for (int j = 0; j < 16; ++j) I[(K0 + rl) + DLD * (K0 + j)] = x[j];
       }
     }
     __syncthreads();
-    const int R0 = K0 + 16, rows = DB - R0;
-    if (rows > 0) {  // b. P[r][j] = sum_{k <= j} A[r][K0 + k] Linv16[j][k]
-      double pv[3];
+    const int nrt = 3 - kb;  // 16-row tiles below this diagonal block
+    if (nrt > 0) {
+      // b. P_I = A_I,kb L16^-T for tiles I = kb + 1 + w (w < nrt)
+      if (w < nrt) {
+        const int R = K0 + 16 + 16 * w;
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        acc = mma16_nt(T, R, K0, I, K0, K0, acc);
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const int p = t + 256 * q, r = R0 + (p >> 4), j = p & 15;
-        double s = 0.0;
-        if (p < rows * 16)
-          for (int k = 0; k <= j; ++k) s = fma(T[r + DLD * (K0 + k)], I[(K0 + j) + DLD * (K0 + k)], s);
-        pv[q] = s;
+        for (int r = 0; r < 4; ++r) T[(R + lk + 4 * r) + DLD * (K0 + lm)] = acc[r];
       }
       __syncthreads();
+      // c. A_IJ -= P_I P_J^T for kb < J <= I (nrt (nrt + 1) / 2 <= 6 tiles over the 4 waves)
+      const int ntile = nrt * (nrt + 1) / 2;
+      for (int q = w; q < ntile; q += 4) {
+        int ti = 0;
+        while ((ti + 1) * (ti + 2) / 2 <= q) ++ti;
+        const int tj = q - ti * (ti + 1) / 2;
+        const int R = K0 + 16 + 16 * ti, C = K0 + 16 + 16 * tj;
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        acc = mma16_nt(T, R, K0, T, C, K0, acc);
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const int p = t + 256 * q;
-        if (p < rows * 16) T[(R0 + (p >> 4)) + DLD * (K0 + (p & 15))] = pv[q];
-      }
-      __syncthreads();
-      // c. trailing lower triangle: A[r][c] -= sum_k P[r][k] P[c][k]
-      for (int p = t; p < DB * DB; p += 256) {
-        const int r = p & 63, c = p >> 6;
-        if (c >= R0 && r >= c) {
-          double s = 0.0;
-#pragma unroll
-          for (int k = 0; k < 16; ++k) s = fma(T[r + DLD * (K0 + k)], T[c + DLD * (K0 + k)], s);
-          T[r + DLD * c] -= s;
-        }
+        for (int r = 0; r < 4; ++r) T[(R + lk + 4 * r) + DLD * (C + lm)] -= acc[r];
       }
       __syncthreads();
     }
   }
-  // off-diagonal 16-blocks of L^-1 by diagonal distance
+  // off-diagonal 16-blocks of L^-1 by diagonal distance, one wave per block
   for (int dd = 1; dd < 4; ++dd) {
     const int nblk = 4 - dd;
-    for (int p = t; p < nblk * 256; p += 256) {  // S = sum_{k} L_ib,k I_k,jb
-      const int jb = p >> 8, ib = jb + dd, r = 16 * ib + (p & 15), c = 16 * jb + ((p >> 4) & 15);
-      double s = 0.0;
-      for (int kk = 16 * jb; kk < 16 * ib; ++kk) s = fma(T[r + DLD * kk], I[kk + DLD * c], s);
-      S[r + DLD * c] = s;
-    }
-    __syncthreads();
-    for (int p = t; p < nblk * 256; p += 256) {  // I_ib,jb = -I_ib,ib S
-      const int jb = p >> 8, ib = jb + dd, r = 16 * ib + (p & 15), c = 16 * jb + ((p >> 4) & 15);
-      double s = 0.0;
-      for (int kk = 16 * ib; kk <= r; ++kk) s = fma(I[r + DLD * kk], S[kk + DLD * c], s);
-      I[r + DLD * c] = -s;
+    if (w < nblk) {
+      const int jb = w, ib = jb + dd;
+      double* Sw = S[w];
+      // S = sum_{k = jb}^{ib - 1} L_ib,k I_k,jb   (B operand B[k][j] = I[16 k' + k][16 jb + j])
+      d4 acc = {0.0, 0.0, 0.0, 0.0};
+      for (int kk = 16 * jb; kk < 16 * ib; kk += 4)
+        acc = mfma_f64(T[(16 * ib + lm) + DLD * (kk + lk)], I[(kk + lk) + DLD * (16 * jb + lm)], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Sw[(lk + 4 * r) + 17 * lm] = acc[r];
+      wave_lds_sync();
+      // I_ib,jb = -I_ib,ib S
+      d4 acc2 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+        acc2 = mfma_f64(I[(16 * ib + lm) + DLD * (16 * ib + 4 * s4 + lk)], Sw[(4 * s4 + lk) + 17 * lm], acc2);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) I[(16 * ib + lk + 4 * r) + DLD * (16 * jb + lm)] = -acc2[r];
     }
     __syncthreads();
   }
@@ -159,6 +171,21 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(double* A, int lda, int 
     Linv[r + DB * c] = I[r + DLD * c];
   }
   if (t == 0 && bad) atomicExch(info, 1);
+}
+
+__global__ __launch_bounds__(256) void chol_diag_kernel(double* A, int lda, int n, int k0, double* Linv, int* info) {
+  __shared__ double T[DB * DLD];  // the block; its lower triangle becomes L
+  __shared__ double I[DB * DLD];  // L^-1 (lower)
+  __shared__ double S[4][16 * 17];  // per-wave 16 x 16 scratch (ld 17)
+  const int nb = min(DB, n - k0), t = threadIdx.x;
+  for (int p = t; p < DB * DB; p += 256) {
+    const int r = p & 63, c = p >> 6;
+    T[r + DLD * c] = (r < nb && c < nb) ? (r >= c ? A[(size_t)(k0 + r) + (size_t)lda * (k0 + c)] : 0.0)
+                                        : (r == c ? 1.0 : 0.0);
+    I[r + DLD * c] = 0.0;
+  }
+  __syncthreads();
+  diag_body(T, I, S, A, lda, n, k0, Linv, info);
 }
 
 // ---------------------------------------------------------------------------------------
