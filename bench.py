@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--workload", choices=["synthetic", "spatial", "phylo"], default="synthetic",
                    help="synthetic: config 4 (the metric); spatial: config 5, vignette_4 'Full' at --ny; "
                         "phylo: config 3, vignette_3 (phylogeny, traits, GammaEta) at --ns species")
+    p.add_argument("--method", choices=["Full", "GPP"], default="Full",
+                   help="config 5's spatial method (vignettes/vignette_4_spatial.Rmd:95-245)")
     p.add_argument("--ny", type=int, default=10000)
     p.add_argument("--ns", type=int, default=1000)
     p.add_argument("--nc", type=int, default=20)
@@ -245,7 +247,10 @@ def main_spatial(args):
     alphapw grid (101 x ny^2 iW and RiW, 2 x 20 GB at ny=5k) is built on the device at chain
     creation (setup_s, outside the timed region).  Each sweep solves the (ny nf)^2 Eta system
     with the blocked Cholesky on the matrix cores and streams the grid once for updateAlpha;
-    the roofline object prices the Cholesky (n^3 / 3 fp64 flops) against the fp64 matrix peak."""
+    the roofline object prices the Cholesky (n^3 / 3 fp64 flops) against the fp64 matrix peak.
+    --method GPP: the same model on the constructKnots(knotDist=0.2, minKnotDist=0.4) knots
+    (:177-228), sampled in R's low-rank form (no np^2 array); the roofline prices updateAlpha's
+    stream of the predictive-process grid (idDW12g + idDg, np (nK + 1) nalpha doubles) against HBM."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -257,7 +262,7 @@ def main_spatial(args):
         dist.init_process_group("gloo")
     from hmsc_amd.workloads import spatial_vignette4
     ny = 5000 if args.ny == 10000 else args.ny
-    hM = spatial_vignette4(ny=ny, method="Full")
+    hM = spatial_vignette4(ny=ny, method=args.method)
     t0 = time.perf_counter()
     ch = H.Chain(hM, 4242 + 7919 * rank, device=local, updater={"GammaEta": False})
     ch.init([1])
@@ -299,24 +304,38 @@ def main_spatial(args):
     achieved = chol_flops / max(chol_s, 1e-12) / 1e12
     grid_bytes = 101 * ny * ny * 8 / 2  # lower-triangular RiW_g streamed once per sweep
     alpha_s = kern["alpha"]["avg_us"] * 1e-6
+    if args.method == "GPP":
+        nK = int(hM.rL[0]["sKnot"].shape[0])
+        gpp_bytes = 101 * ny * (nK + 1) * 8
+        roof = {"kernel": "updateAlpha's GPP statistic (gpp_alpha_kernel): idDW12g and idDg streamed once per sweep",
+                "bound": "hbm", "achieved": round(gpp_bytes / max(alpha_s, 1e-12) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(gpp_bytes / max(alpha_s, 1e-12) / 1e9 / HBM_PEAK_GBS, 4),
+                "traffic": None, "algorithmic_bytes_per_launch": gpp_bytes,
+                "avg_launch_us": round(kern["alpha"]["avg_us"], 1), "n_knots": nK,
+                "timer": "HIP events on the chain stream around the updater (eager sweeps)"}
+        workload = (f"vignette_4 spatial 'GPP' ny={ny} ns=5 nc=2 nf=1, {nK} knots (knotDist 0.2), "
+                    f"101-point alphapw grid, R's low-rank updateEta, updater GammaEta=FALSE, record every sweep")
+    else:
+        roof = {"kernel": "blocked Cholesky of the (np nf)^2 Eta precision (chol_diag/panel/update)",
+                "bound": "mfma", "achieved": round(achieved, 2), "peak": peak_tf, "unit": "TFLOP/s",
+                "frac": round(achieved / peak_tf, 4), "traffic": None,
+                "algorithmic_flops_per_launch": chol_flops, "avg_launch_us": round(kern["chol"]["avg_us"], 1),
+                "timer": "HIP events on the chain stream around each factorization (eager sweeps)",
+                "alpha_grid": {"bytes_per_sweep": grid_bytes, "avg_us": round(kern["alpha"]["avg_us"], 1),
+                               "achieved_GBs": round(grid_bytes / max(alpha_s, 1e-12) / 1e9, 1),
+                               "peak_GBs": HBM_PEAK_GBS}}
+        workload = (f"vignette_4 spatial 'Full' ny={ny} ns=5 nc=2 nf=1, 101-point alphapw grid, "
+                    f"updater GammaEta=FALSE, record every sweep")
     out = {
-        "metric": "Gibbs sweeps/sec, config 5 (vignette_4 spatial Full) at ny=%d" % ny,
+        "metric": "Gibbs sweeps/sec, config 5 (vignette_4 spatial %s) at ny=%d" % (args.method, ny),
         "value": round(world * args.steps / tmax, 3), "unit": "sweeps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1e3 * tmax / args.steps, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (vignette_4 generator scaled to ny, seed 20261015)",
-        "config": {"workload": f"vignette_4 spatial 'Full' ny={ny} ns=5 nc=2 nf=1, 101-point alphapw grid, "
-                               f"updater GammaEta=FALSE, record every sweep",
+        "config": {"workload": workload,
                    "ny": ny, "ns": 5, "nc": 2, "nf": 1, "parallelism": f"{world} independent chains, one per GPU"},
         "setup_s": round(setup, 2),
-        "roofline": {"kernel": "blocked Cholesky of the (np nf)^2 Eta precision (chol_diag/panel/update)",
-                     "bound": "mfma", "achieved": round(achieved, 2), "peak": peak_tf, "unit": "TFLOP/s",
-                     "frac": round(achieved / peak_tf, 4), "traffic": None,
-                     "algorithmic_flops_per_launch": chol_flops, "avg_launch_us": round(kern["chol"]["avg_us"], 1),
-                     "timer": "HIP events on the chain stream around each factorization (eager sweeps)",
-                     "alpha_grid": {"bytes_per_sweep": grid_bytes, "avg_us": round(kern["alpha"]["avg_us"], 1),
-                                    "achieved_GBs": round(grid_bytes / max(alpha_s, 1e-12) / 1e9, 1),
-                                    "peak_GBs": HBM_PEAK_GBS}},
+        "roofline": roof,
         "kernels_eager_events_us": {k: round(v["avg_us"], 1) for k, v in kern.items()},
         "alpha_posterior_mean_index": round(alpha_mean, 2),
         "cpu_baseline": None,

@@ -31,7 +31,9 @@ class hmsc_model(C.Structure):
                 ("C_vectors", dp), ("C_values", dp),
                 ("spatialMethod", ip), ("nalpha", ip), ("alphapw", dp * MAX_LEVELS), ("iWg", dp * MAX_LEVELS),
                 ("RiWg", dp * MAX_LEVELS), ("detWg", dp * MAX_LEVELS),
-                ("sCoord", dp * MAX_LEVELS), ("distMat", dp * MAX_LEVELS)]
+                ("sCoord", dp * MAX_LEVELS), ("distMat", dp * MAX_LEVELS),
+                ("nKnots", ip), ("idDg", dp * MAX_LEVELS), ("idDW12g", dp * MAX_LEVELS), ("Fg", dp * MAX_LEVELS),
+                ("iFg", dp * MAX_LEVELS), ("detDg", dp * MAX_LEVELS)]
 
 
 class hmsc_params(C.Structure):

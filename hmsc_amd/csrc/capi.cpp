@@ -273,10 +273,12 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
       HMSC_REQUIRE(m->spatialMethod[r] == 1 || m->np[r] == ny,
                    "spatial level: NNGP / GPP levels need np == ny (R/updateEta.R:140,165)");
       const bool geom = m->spatialMethod[r] == 1 && !m->iWg[r] && (m->sCoord[r] || m->distMat[r]);
+      const bool gpp = m->spatialMethod[r] == 3 && !m->iWg[r] && m->nKnots && m->nKnots[r] > 0 && m->idDg[r] &&
+                       m->idDW12g[r] && m->Fg[r] && m->iFg[r] && m->detDg[r];
       HMSC_REQUIRE(m->nalpha != nullptr && m->nalpha[r] > 0 && m->alphapw[r] &&
-                       (geom || (m->iWg[r] && m->RiWg[r] && m->detWg[r])),
-                   "spatial level: alphapw and either iWg / RiWg / detWg (computeDataParameters' rLPar) "
-                   "or, for 'Full', sCoord / distMat must be given");
+                       (geom || gpp || (m->iWg[r] && m->RiWg[r] && m->detWg[r])),
+                   "spatial level: alphapw and either iWg / RiWg / detWg (computeDataParameters' rLPar), "
+                   "for 'Full' sCoord / distMat, or for 'GPP' nKnots / idDg / idDW12g / Fg / iFg / detDg must be given");
       HMSC_REQUIRE(!(mask & HMSC_UP_GAMMAETA) || m->spatialMethod[r] == 1,
                    "updataGammaEta: no method implemented yet for NNGP / GPP with GammaEta updater "
                    "(R/updateGammaEta.R:153-158): pass updater GammaEta=FALSE");
@@ -327,7 +329,16 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
       const size_t G = m->nalpha[r], np2 = (size_t)L.np * L.np;
       L.nalpha = (int)G;
       L.alphapw = dupload(m->alphapw[r], 2 * G);
-      if (m->iWg[r]) {
+      if (m->spatialMethod[r] == 3 && !m->iWg[r]) {  // GPP in R's low-rank form
+        const size_t nK = (size_t)m->nKnots[r];
+        L.gpp = true;
+        L.nK = (int)nK;
+        L.idDg = dupload(m->idDg[r], (size_t)L.np * G);
+        L.idDW12g = dupload(m->idDW12g[r], (size_t)L.np * nK * G);
+        L.Fg = dupload(m->Fg[r], nK * nK * G);
+        L.iFg = dupload(m->iFg[r], nK * nK * G);
+        L.detWg = dupload(m->detDg[r], G);
+      } else if (m->iWg[r]) {
         L.iWg = dupload(m->iWg[r], np2 * G);
         L.RiWg = dupload(m->RiWg[r], np2 * G);
         L.riw_lower = m->spatialMethod[r] == 2 || m->spatialMethod[r] == 3;
@@ -565,7 +576,8 @@ static void free_state(State& s) {
     if (p) (void)hipFree(p);
   for (int r = 0; r < s.nr; ++r) {
     Level& L = s.lev[r];
-    void* lp[] = {L.Eta, L.Pi, L.unit_ptr, L.unit_rows, L.Alpha, L.AlphaD, L.alphapw, L.iWg, L.RiWg, L.detWg, L.spWork};
+    void* lp[] = {L.Eta, L.Pi, L.unit_ptr, L.unit_rows, L.Alpha, L.AlphaD, L.alphapw, L.iWg, L.RiWg, L.detWg, L.spWork,
+                  L.idDg, L.idDW12g, L.Fg, L.iFg};
     for (void* p : lp)
       if (p) (void)hipFree(p);
   }

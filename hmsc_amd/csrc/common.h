@@ -213,6 +213,34 @@ __device__ inline void wg_gemm(int m, int n, int k, double alpha, const double* 
   __syncthreads();
 }
 
+// serial lower Cholesky of an n x n (ld n) block and the inverse of its factor, one thread
+__device__ inline bool t_chol_inv(double* A, double* Li, int n) {
+  bool ok = true;
+  for (int c = 0; c < n; ++c) {
+    double d = A[c + n * c];
+    for (int k = 0; k < c; ++k) d -= A[c + n * k] * A[c + n * k];
+    if (!(d > 0.0)) ok = false;
+    d = sqrt(d > 0.0 ? d : 1.0);
+    A[c + n * c] = d;
+    for (int i = c + 1; i < n; ++i) {
+      double s = A[i + n * c];
+      for (int k = 0; k < c; ++k) s -= A[i + n * k] * A[c + n * k];
+      A[i + n * c] = s / d;
+    }
+  }
+  for (int j = 0; j < n; ++j)  // Li = L^-1 (lower), column by column
+    for (int i = 0; i < n; ++i) {
+      if (i < j) {
+        Li[i + n * j] = 0.0;
+        continue;
+      }
+      double s = (i == j) ? 1.0 : 0.0;
+      for (int k = j; k < i; ++k) s -= A[i + n * k] * Li[k + n * j];
+      Li[i + n * j] = s / A[i + n * i];
+    }
+  return ok;
+}
+
 // zero the strict upper triangle (turn an in-place wg_chol result into a clean L)
 __device__ inline void wg_lower_only(double* A, int n, int lda) {
   const int t = threadIdx.x, tr = t & 31, tc = t >> 5, ntc = blockDim.x >> 5;

@@ -101,34 +101,6 @@ __host__ __device__ inline GELayout ge_layout(int ny, int ns, int nc, int nt, in
   return o;
 }
 
-// serial lower Cholesky of an n x n (ld n) block and the inverse of its factor, one thread
-__device__ inline bool t_chol_inv(double* A, double* Li, int n) {
-  bool ok = true;
-  for (int c = 0; c < n; ++c) {
-    double d = A[c + n * c];
-    for (int k = 0; k < c; ++k) d -= A[c + n * k] * A[c + n * k];
-    if (!(d > 0.0)) ok = false;
-    d = sqrt(d > 0.0 ? d : 1.0);
-    A[c + n * c] = d;
-    for (int i = c + 1; i < n; ++i) {
-      double s = A[i + n * c];
-      for (int k = 0; k < c; ++k) s -= A[i + n * k] * A[c + n * k];
-      A[i + n * c] = s / d;
-    }
-  }
-  for (int j = 0; j < n; ++j)  // Li = L^-1 (lower), column by column
-    for (int i = 0; i < n; ++i) {
-      if (i < j) {
-        Li[i + n * j] = 0.0;
-        continue;
-      }
-      double s = (i == j) ? 1.0 : 0.0;
-      for (int k = j; k < i; ++k) s -= A[i + n * k] * Li[k + n * j];
-      Li[i + n * j] = s / A[i + n * i];
-    }
-  return ok;
-}
-
 // Workspace pointers of one level's update (ge_layout)
 struct GEPtrs {
   double *A, *L, *M, *T, *S, *XtX, *V, *Wv, *XtS, *LamiD, *LDL, *W0, *iW0, *L0i, *tmp1, *Qm, *iQm, *iQTr;

@@ -39,6 +39,12 @@ struct SpArgs {
   int riw_lower;          // RiWg lower triangular (NNGP's Vecchia factor), else upper (chol)
   const double* detWg;
   const double* alphapw;  // nalpha x 2
+  // GPP in R's low-rank form (Level::gpp)
+  int nK;
+  const double* idDg;     // np x nalpha
+  const double* idDW12g;  // np x nK x nalpha
+  const double* Fg;       // nK x nK x nalpha
+  const double* iFg;      // nK x nK x nalpha
   double* AlphaD;         // nf (1-based grid index as double)
   double* Eta;            // np x nf (ld np)
   double* work;
@@ -254,6 +260,11 @@ static SpArgs sp_args(State& s, int r, uint32_t iter) {
   a.riw_lower = L.riw_lower;
   a.detWg = L.detWg;
   a.alphapw = L.alphapw;
+  a.nK = L.nK;
+  a.idDg = L.idDg;
+  a.idDW12g = L.idDW12g;
+  a.Fg = L.Fg;
+  a.iFg = L.iFg;
   a.AlphaD = L.AlphaD;
   a.Eta = L.Eta;
   a.work = L.spWork;
@@ -265,12 +276,221 @@ static SpArgs sp_args(State& s, int r, uint32_t iter) {
   return a;
 }
 
+// ---------------------------------------------------------------------------------------
+// 'GPP' levels in R's low-rank form (R/updateEta.R:148-196; np == ny, units in unit order).
+// With B0_i = Lam iSigma Lam' + diag(idD[i, alpha_h]) (nf x nf per unit), iA = bdiag(B0_i^-1),
+// W = bdiag_h(idDW12g[,,alpha_h]) ((np nf) x (nK nf)), H = bdiag_h(Fg[,,alpha_h]) - W' iA W:
+//   eta = iA fS + T (T' fS + xi2) + LiA xi1,   T = iA W RH^-1,  RH = chol(H),
+// LiA = bdiag(chol(B0_i^-1)) (lower) -- O(np (nK nf)^2) work, nothing np^2.  Normals: xi1 of
+// unit i, factor h = normal(i, h, S_ETA + LEVEL_STRIDE r) (the counters of the other
+// branches), xi2 of knot k, factor h = normal(k, GPP_XI2_SUB + h, same stream).
+// updateAlpha (R/updateAlpha.R:35-75): v_gh = eta_h' diag(idDg[,g]) eta_h - t_h iFg[,,g] t_h'
+// with t_h = eta_h' idDW12g[,,g] (eta_h' eta_h at alpha_g = 0), likelihood with detDg.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t GPP_XI2_SUB = 1024;
+
+struct GppLayout {
+  size_t rhs, LDL, B1, LB1, iAW, H, M, ws, T, v, alpha, tot;
+};
+
+// nfc: factor capacity (nfmax), nch: updateAlpha's partial-sum chunks
+inline GppLayout gpp_layout(int np, int nfc, int nK, int nalpha) {
+  GppLayout o{};
+  const size_t NP = (size_t)np * nfc, KF = (size_t)nK * nfc;
+  size_t p = 0;
+  auto take = [&](size_t n) {
+    const size_t at = p;
+    p += (n + 7) & ~(size_t)7;
+    return at;
+  };
+  o.rhs = take(NP);
+  o.LDL = take((size_t)nfc * nfc);
+  o.B1 = take((size_t)np * nfc * nfc);
+  o.LB1 = take((size_t)np * nfc * nfc);
+  o.iAW = take(NP * KF);
+  o.H = take(KF * KF);
+  o.M = take(KF * KF);
+  o.ws = take(dense_ws_doubles((int)KF));
+  o.T = take(NP * KF);
+  o.v = take(KF);
+  o.alpha = take((size_t)nalpha * ((np + 255) / 256) * nfc);
+  o.tot = p;
+  return o;
+}
+
+// per unit i: B1_i = B0_i^-1 and LB1_i = chol(B1_i) (lower), nf x nf column-major at i nf^2
+__global__ __launch_bounds__(256) void gpp_unit_kernel(SpArgs a, const double* LDL, double* B1, double* LB1) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x, nf = a.nf, np = a.np;
+  if (i >= np) return;
+  double A[16 * 16], Li[16 * 16];
+  for (int c = 0; c < nf; ++c)
+    for (int r = 0; r < nf; ++r)
+      A[r + nf * c] = LDL[r + nf * c] + (r == c ? a.idDg[i + (size_t)np * ((int)a.AlphaD[r] - 1)] : 0.0);
+  bool ok = t_chol_inv(A, Li, nf);  // A <- L0 (lower), Li = L0^-1
+  double* b1 = B1 + (size_t)i * nf * nf;
+  double* lb = LB1 + (size_t)i * nf * nf;
+  for (int c = 0; c < nf; ++c)
+    for (int r = 0; r < nf; ++r) {  // B1 = L0^-T L0^-1
+      double s = 0.0;
+      for (int k = (r > c ? r : c); k < nf; ++k) s += Li[k + nf * r] * Li[k + nf * c];
+      b1[r + nf * c] = s;
+      A[r + nf * c] = s;
+    }
+  ok = t_chol_inv(A, Li, nf) && ok;  // A <- chol(B1)
+  for (int c = 0; c < nf; ++c)
+    for (int r = 0; r < nf; ++r) lb[r + nf * c] = r >= c ? A[r + nf * c] : 0.0;
+  if (!ok) a.fail[0] = 1;
+}
+
+// iAW[e, c] = B1_i[h, h'] idDW12g[i, k, alpha_h'],  e = i + np h, c = k + nK h'
+__global__ __launch_bounds__(256) void gpp_iaw_kernel(SpArgs a, const double* B1, double* iAW) {
+  const int np = a.np, nf = a.nf, nK = a.nK, NP = np * nf;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x, c = blockIdx.y;
+  if (e >= NP) return;
+  const int i = e % np, h = e / np, k = c % nK, h2 = c / nK;
+  const double w = a.idDW12g[i + (size_t)np * k + (size_t)np * nK * ((int)a.AlphaD[h2] - 1)];
+  iAW[e + (size_t)NP * c] = B1[(size_t)i * nf * nf + h + nf * h2] * w;
+}
+
+// H = bdiag_h(Fg[,,alpha_h]) - W' iAW, one workgroup per entry (reduction over the np units)
+__global__ __launch_bounds__(256) void gpp_h_kernel(SpArgs a, const double* iAW, double* H) {
+  const int np = a.np, nf = a.nf, nK = a.nK, NP = np * nf, KF = nK * nf;
+  const int c1 = blockIdx.x, c2 = blockIdx.y, k = c1 % nK, h = c1 / nK;
+  const double* w = a.idDW12g + (size_t)np * k + (size_t)np * nK * ((int)a.AlphaD[h] - 1);
+  const double* x = iAW + (size_t)np * h + (size_t)NP * c2;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < np; i += 256) s = fma(w[i], x[i], s);
+  __shared__ double red[4];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int k2 = c2 % nK, h2 = c2 / nK;
+    const double f = h == h2 ? a.Fg[k + (size_t)nK * k2 + (size_t)nK * nK * ((int)a.AlphaD[h] - 1)] : 0.0;
+    H[c1 + (size_t)KF * c2] = f - ((red[0] + red[1]) + (red[2] + red[3]));
+  }
+}
+
+// T = iAW RH^-1 = iAW M^T with M = L_H^-1 (lower): T[e, c] = sum_{c' <= c} iAW[e, c'] M[c, c']
+__global__ __launch_bounds__(256) void gpp_t_kernel(SpArgs a, const double* iAW, const double* M, double* T) {
+  const int NP = a.np * a.nf, KF = a.nK * a.nf;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x, c = blockIdx.y;
+  if (e >= NP) return;
+  double s = 0.0;
+  for (int c2 = 0; c2 <= c; ++c2) s = fma(iAW[e + (size_t)NP * c2], M[c + (size_t)KF * c2], s);
+  T[e + (size_t)NP * c] = s;
+}
+
+// v[c] = T[, c]' fS + xi2[c], one workgroup per c
+__global__ __launch_bounds__(256) void gpp_v_kernel(SpArgs a, const double* T, const double* rhs, double* v) {
+  const int NP = a.np * a.nf, c = blockIdx.x;
+  double s = 0.0;
+  for (int e = threadIdx.x; e < NP; e += 256) s = fma(T[e + (size_t)NP * c], rhs[e], s);
+  __shared__ double red[4];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int k = c % a.nK, h = c / a.nK;
+    const double xi2 = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)k, GPP_XI2_SUB + (uint32_t)h, S_ETA + LEVEL_STRIDE * a.r,
+                                                    SWEEP_ITER(a));
+    v[c] = (red[0] + red[1]) + (red[2] + red[3]) + xi2;
+  }
+}
+
+// eta[e] = (B1_i fS_i)_h + (LB1_i xi1_i)_h + T[e, ] v
+__global__ __launch_bounds__(256) void gpp_eta_kernel(SpArgs a, const double* B1, const double* LB1, const double* T,
+                                                      const double* rhs, const double* v) {
+  const int np = a.np, nf = a.nf, NP = np * nf, KF = a.nK * nf;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= NP) return;
+  const int i = e % np, h = e / np;
+  const double* b1 = B1 + (size_t)i * nf * nf;
+  const double* lb = LB1 + (size_t)i * nf * nf;
+  double s = 0.0;
+  for (int h2 = 0; h2 < nf; ++h2) s = fma(b1[h + nf * h2], rhs[i + (size_t)np * h2], s);
+  if (!a.noise_zero)
+    for (int h2 = 0; h2 <= h; ++h2)
+      s = fma(lb[h + nf * h2], normal(a.key, (uint32_t)i, (uint32_t)h2, S_ETA + LEVEL_STRIDE * a.r, SWEEP_ITER(a)), s);
+  for (int c = 0; c < KF; ++c) s = fma(T[e + (size_t)NP * c], v[c], s);
+  a.Eta[e] = s;
+}
+
+// updateAlpha's GPP statistic, one workgroup per grid point; v_gh goes to chunk 0 of the
+// partial-sum slots alpha_draw_kernel adds (the other chunks zero)
+__global__ __launch_bounds__(256) void gpp_alpha_kernel(SpArgs a, double* out) {
+  const int g = blockIdx.x, np = a.np, nf = a.nf, nK = a.nK, nch = (np + 255) / 256;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  __shared__ double red[4], t2[1024];
+  const bool zero = a.alphapw[g] == 0.0;
+  const double* idD = a.idDg + (size_t)np * g;
+  const double* W = a.idDW12g + (size_t)np * nK * g;
+  const double* iF = a.iFg + (size_t)nK * nK * g;
+  auto block_sum = [&](double s) {
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    __syncthreads();
+    if (lane == 0) red[w] = s;
+    __syncthreads();
+    return (red[0] + red[1]) + (red[2] + red[3]);
+  };
+  for (int h = 0; h < nf; ++h) {
+    const double* eta = a.Eta + (size_t)np * h;
+    double s = 0.0;
+    for (int i = t; i < np; i += 256) s = fma(eta[i] * (zero ? 1.0 : idD[i]), eta[i], s);
+    double v = block_sum(s);
+    if (!zero) {
+      for (int k = 0; k < nK; ++k) {  // t_h = eta_h' idDW12g[,,g]
+        double q = 0.0;
+        for (int i = t; i < np; i += 256) q = fma(eta[i], W[i + (size_t)np * k], q);
+        const double tk = block_sum(q);
+        if (t == 0) t2[k] = tk;
+      }
+      __syncthreads();
+      double q = 0.0;  // t_h iF t_h'
+      for (int p = t; p < nK * nK; p += 256) q = fma(t2[p % nK] * iF[p], t2[p / nK], q);
+      v -= block_sum(q);
+    }
+    if (t == 0) {
+      double* o = out + (size_t)g * nch * nf;
+      for (int c = 0; c < nch; ++c) o[(size_t)c * nf + h] = c == 0 ? v : 0.0;
+    }
+    __syncthreads();
+  }
+}
+
+static void launch_eta_gpp(State& s, int r, uint32_t iter) {
+  const Level& L = s.lev[r];
+  HMSC_REQUIRE(L.nK <= 1024, "GPP level: at most 1024 knots in this build");
+  const SpArgs a = sp_args(s, r, iter);
+  const int np = L.np, nf = L.nf, NP = np * nf, KF = L.nK * nf;
+  const GppLayout o = gpp_layout(np, std::max(1, std::min(L.nfmax, s.NFmax)), L.nK, L.nalpha);
+  double* w = L.spWork;
+  double *rhs = w + o.rhs, *LDL = w + o.LDL, *B1 = w + o.B1, *LB1 = w + o.LB1, *iAW = w + o.iAW, *H = w + o.H;
+  double *M = w + o.M, *ws = w + o.ws, *T = w + o.T, *v = w + o.v;
+  const int g1 = (NP + 255) / 256;
+  sp_rhs_kernel<<<g1, 256, 0, s.stream>>>(a, rhs, LDL);
+  gpp_unit_kernel<<<(np + 255) / 256, 256, 0, s.stream>>>(a, LDL, B1, LB1);
+  gpp_iaw_kernel<<<dim3(g1, KF), 256, 0, s.stream>>>(a, B1, iAW);
+  gpp_h_kernel<<<dim3(KF, KF), 256, 0, s.stream>>>(a, iAW, H);
+  HIP_OK(hipGetLastError());
+  {
+    ProfScope pc(s, PROF_CHOL);
+    dense_potrf_lower(s.stream, H, KF, KF, ws, s.dev_flags);  // RH = chol(H) = L_H^T
+  }
+  dense_trtri_lower(s.stream, H, KF, KF, M, KF, ws, true);     // M = L_H^-1, RH^-1 = M^T
+  gpp_t_kernel<<<dim3(g1, KF), 256, 0, s.stream>>>(a, iAW, M, T);
+  gpp_v_kernel<<<KF, 256, 0, s.stream>>>(a, T, rhs, v);
+  gpp_eta_kernel<<<g1, 256, 0, s.stream>>>(a, B1, LB1, T, rhs, v);
+  HIP_OK(hipGetLastError());
+}
+
 // np * nf above which updateEta's dense system goes to the multi-workgroup blocked path
 constexpr int SP_BLOCKED_N = 1024;
 
 size_t spatial_work_doubles(const State& s, int r) {
   const Level& L = s.lev[r];
   const size_t nfc = std::max(1, std::min(L.nfmax, s.NFmax));
+  if (L.gpp) return gpp_layout(L.np, (int)nfc, L.nK, L.nalpha).tot + 64;
   const size_t N = (size_t)L.np * nfc;
   const size_t eta = N * N + N + dense_ws_doubles((int)N) + nfc * nfc + 64;
   const size_t alpha = (size_t)L.nalpha * ((L.np + 255) / 256) * std::max(1, std::min(L.nfmax, s.NFmax));
@@ -281,9 +501,13 @@ void launch_eta_spatial(State& s, int r, uint32_t iter) {
   const Level& L = s.lev[r];
   HMSC_REQUIRE(s.nranks == 1, "spatial levels: species-sharded chains are not supported");
   if (!s.xeta_valid) launch_xeta(s);
+  ProfScope ps(s, PROF_ETA_SP);
+  if (L.gpp) {
+    launch_eta_gpp(s, r, iter);
+    return;
+  }
   const SpArgs a = sp_args(s, r, iter);
   const int N = L.np * L.nf;
-  ProfScope ps(s, PROF_ETA_SP);
   if (N <= SP_BLOCKED_N) {
     eta_spatial_full_kernel<<<1, 1024, 0, s.stream>>>(a);
     HIP_OK(hipGetLastError());
@@ -315,6 +539,16 @@ void launch_alpha(State& s, uint32_t iter) {
     if (!L.spatial || L.nf == 0) continue;  // rep(1, nf) otherwise (R/updateAlpha.R:81-82)
     const SpArgs a = sp_args(s, r, iter);
     ProfScope ps(s, PROF_ALPHA);
+    if (L.gpp) {
+      const GppLayout o = gpp_layout(L.np, std::max(1, std::min(L.nfmax, s.NFmax)), L.nK, L.nalpha);
+      SpArgs b = a;
+      b.work = L.spWork + o.alpha;
+      gpp_alpha_kernel<<<L.nalpha, 256, 0, s.stream>>>(b, b.work);
+      HIP_OK(hipGetLastError());
+      alpha_draw_kernel<<<1, 64, 0, s.stream>>>(b);
+      HIP_OK(hipGetLastError());
+      continue;
+    }
     alpha_quad_kernel<<<dim3(L.nalpha, (L.np + 255) / 256), 256, 0, s.stream>>>(a);
     HIP_OK(hipGetLastError());
     alpha_draw_kernel<<<1, 64, 0, s.stream>>>(a);

@@ -41,6 +41,13 @@ struct Level {
   double* detWg = nullptr;      // nalpha
   double* AlphaD = nullptr;     // nfmax: 1-based grid index of each factor (recorded)
   double* spWork = nullptr;     // dense (np nf)^2 Eta system + Alpha likelihoods
+  // 'GPP' level in R's low-rank form (spatial.hip, R/computeDataParameters.R:138-194)
+  bool gpp = false;
+  int nK = 0;
+  double* idDg = nullptr;       // np x nalpha
+  double* idDW12g = nullptr;    // np x nK x nalpha
+  double* Fg = nullptr;         // nK x nK x nalpha
+  double* iFg = nullptr;        // nK x nK x nalpha
 };
 
 struct State {

@@ -57,9 +57,10 @@ def computeDataParameters(hM):
     return par
 
 
-def spatialDataParameters(hM, skip=None):
+def spatialDataParameters(hM, skip=None, gpp_dense=True):
     """rLPar of R/computeDataParameters.R:47-196 ({} for non-spatial levels and for levels
-    with skip[r] true)."""
+    with skip[r] true).  gpp_dense=False leaves out the dense np^2 iWg / RiWg of GPP levels
+    (the device samples them in R's low-rank form from idDg / idDW12g / Fg / iFg)."""
     rLPar = []
     for r, rl in enumerate(hM.rL or []):
         if not rl.sDim or (skip is not None and skip[r]):
@@ -70,7 +71,7 @@ def spatialDataParameters(hM, skip=None):
             rLPar.append(_nngp_grid(hM, r, rl))
             continue
         if method == "GPP":
-            rLPar.append(_gpp_grid(hM, r, rl))
+            rLPar.append(_gpp_grid(hM, r, rl, dense=gpp_dense))
             continue
         if method != "Full":
             raise ValueError(f"computeDataParameters: unknown spatialMethod {method!r}")
@@ -149,9 +150,10 @@ def _nngp_grid(hM, r, rl):
     return dict(iWg=iWg, RiWg=RiWg, detWg=detWg)
 
 
-def _gpp_grid(hM, r, rl):
+def _gpp_grid(hM, r, rl, dense=True):
     """R/computeDataParameters.R:138-194 (predictive process over the knots sKnot), plus
-    the dense precision iWg / RiWg / detWg the device path consumes (module docstring)."""
+    (dense=True) the dense precision iWg / RiWg / detWg of the same prior (module docstring;
+    the device samples GPP levels from the low-rank arrays and needs none of it)."""
     if rl.distMat is not None:
         raise ValueError("computeDataParameters: predictive gaussian process not available for distance matrices")
     sKnot = rl["sKnot"] if "sKnot" in rl.names() else None
@@ -169,8 +171,8 @@ def _gpp_grid(hM, r, rl):
     Fg = np.empty((nK, nK, G))
     iFg = np.empty((nK, nK, G))
     detDg = np.empty(G)
-    iWg = np.empty((npr, npr, G))
-    RiWg = np.empty_like(iWg)
+    iWg = np.empty((npr, npr, G)) if dense else None
+    RiWg = np.empty_like(iWg) if dense else None
     for g in range(G):
         a = alphapw[g, 0]
         if a == 0:
@@ -188,6 +190,8 @@ def _gpp_grid(hM, r, rl):
         DS = tmp2.T @ (idD[:, None] * tmp2) + np.eye(nK)            # :184
         detD = float(np.sum(np.log(dD)) + 2 * np.sum(np.log(np.diag(np.linalg.cholesky(DS)))))
         idDg[:, g], idDW12g[:, :, g], Fg[:, :, g], iFg[:, :, g], detDg[g] = idD, idDW12, F, iF, detD
+        if not dense:
+            continue
         # dense precision through W itself (unit diagonal): W = L L', RiW = L^-1 (lower),
         # iW = RiW' RiW.  Equal to diag(idD) - idDW12 iF idDW12' but without its cancellation
         # when a unit sits on a knot (dD -> 0, idD -> inf while W stays well conditioned)

@@ -28,8 +28,9 @@ def _finite_int(v, cap):
     return int(min(cap, v)) if not (isinstance(v, float) and math.isinf(v)) else int(cap)
 
 
-# include/hmsc_amd.h spatialMethod codes; every method reaches the device as the dense
-# prior precision of its alphapw grid (hmsc_amd/dataparams.py)
+# include/hmsc_amd.h spatialMethod codes; Full and NNGP reach the device as the dense prior
+# precision of their alphapw grid (Full built on the device from the coordinates), GPP as
+# R's low-rank predictive-process arrays (hmsc_amd/dataparams.py)
 SPATIAL_CODE = {"Full": 1, "NNGP": 2, "GPP": 3}
 
 
@@ -81,8 +82,10 @@ class ModelBuffers:
             # would pass dataParList$rLPar[[r]]$iWg / RiWg / detWg
             from .dataparams import _level_order, spatialDataParameters
             on_device = [bool(lv.sDim) and spatial_grid == "device" and lv.spatialMethod == "Full" for lv in rl]
-            rlp = spatialDataParameters(hM, skip=on_device)
+            rlp = spatialDataParameters(hM, skip=on_device, gpp_dense=False)
             m.nalpha = L.colmajor_ptr([r.alphapw.shape[0] if r.sDim else 0 for r in rl], k, np.int32)
+            m.nKnots = L.colmajor_ptr([rlp[r]["Fg"].shape[0] if lv.sDim and lv.spatialMethod == "GPP" else 0
+                                       for r, lv in enumerate(rl)], k, np.int32)
             for r, lv in enumerate(rl):
                 if not lv.sDim:
                     continue
@@ -93,6 +96,9 @@ class ModelBuffers:
                         m.sCoord[r] = L.colmajor_ptr(np.asarray(lv.s, dtype=np.float64)[idx], k)
                     else:
                         m.distMat[r] = L.colmajor_ptr(lv.distMat[np.ix_(idx, idx)], k)
+                elif lv.spatialMethod == "GPP":  # R's low-rank arrays (include/hmsc_amd.h)
+                    for f in ("idDg", "idDW12g", "Fg", "iFg", "detDg"):
+                        getattr(m, f)[r] = L.colmajor_ptr(rlp[r][f], k)
                 else:
                     m.iWg[r] = L.colmajor_ptr(rlp[r]["iWg"], k)
                     m.RiWg[r] = L.colmajor_ptr(rlp[r]["RiWg"], k)

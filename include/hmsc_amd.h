@@ -107,6 +107,18 @@ typedef struct hmsc_model {
    * path that fits: two 20 GB grids are built in HBM without a host copy. */
   const double* sCoord[HMSC_MAX_LEVELS];
   const double* distMat[HMSC_MAX_LEVELS];
+  /* 'GPP' levels may instead (iWg / RiWg / detWg NULL) hand over computeDataParameters'
+   * predictive-process grid as R keeps it (R/computeDataParameters.R:138-194): nKnots[r]
+   * knots, idDg (np x nalpha), idDW12g (np x nK x nalpha), Fg and iFg (nK x nK x nalpha),
+   * detDg (nalpha), all column-major.  updateEta then samples R's low-rank form
+   * (R/updateEta.R:148-196: per-unit nf x nf blocks and one (nK nf)^2 factorization, no
+   * np^2 array anywhere) and updateAlpha evaluates R's GPP statistic (R/updateAlpha.R:35-75). */
+  const int32_t* nKnots;                     /* nr (entries of non-GPP levels ignored)  */
+  const double* idDg[HMSC_MAX_LEVELS];
+  const double* idDW12g[HMSC_MAX_LEVELS];
+  const double* Fg[HMSC_MAX_LEVELS];
+  const double* iFg[HMSC_MAX_LEVELS];
+  const double* detDg[HMSC_MAX_LEVELS];
 } hmsc_model;
 
 /* Sampler state = R's parList (R/computeInitialParameters.R:256-270) with iV in

@@ -563,7 +563,7 @@ def eta_unit_moments(st, model, r, S):
 
 def _eta_spatial_full(st, model, r, S, dp, rng, it, zero_noise):
     """Spatial level, R/updateEta.R:115-147 ('Full'; 'NNGP' is the same code on a sparse
-    iWg; 'GPP' on the dense precision of _gpp_data_parameters): one dense (np nf)^2 system
+    iWg; 'GPP' goes to _eta_spatial_gpp, R's low-rank form): one dense (np nf)^2 system
     iUEta = bdiag(iWg[,,alpha_h]) + kron(Lam iSigma Lam', diag(colSums P)),
     fS = P'S (Lam diag(iSigma))', eta = R^-1 (R^-T vec(fS) + xi), R = chol(iUEta)."""
     lam, iS = st["Lambda"][r], st["iSigma"]
@@ -585,6 +585,25 @@ def _eta_spatial_full(st, model, r, S, dp, rng, it, zero_noise):
         xi = rng.normal(np.arange(npr)[:, None], np.arange(nf)[None, :], R.S_ETA + R.LEVEL_STRIDE * r, it)
         tmp2 = tmp2 + xi.ravel(order="F")
     return backsolve(Rm, tmp2).reshape((npr, nf), order="F")
+
+
+GPP_XI2_SUB = 1024  # hmsc_amd/csrc/spatial.hip
+
+
+def _eta_spatial_gpp(st, model, r, S, dp, rng, it, zero_noise):
+    """'GPP' level (np == ny), R/updateEta.R:148-196 in R's own low-rank form
+    (gpp_eta_literal): eta = iA fS + T (T' fS + xi2) + LiA xi1 with xi1 of unit i, factor h =
+    normal(i, h, S_ETA + LEVEL_STRIDE r) and xi2 of knot k, factor h = normal(k,
+    GPP_XI2_SUB + h, same stream), as the device draws them."""
+    nf = st["Lambda"][r].shape[0]
+    n = int(model["np"][r])
+    nK = dp["rLPar"][r]["Fg"].shape[1]
+    if zero_noise:
+        return gpp_eta_literal(st, model, r, S, dp)[0]
+    stream = R.S_ETA + R.LEVEL_STRIDE * r
+    xi1 = rng.normal(np.arange(n)[:, None], np.arange(nf)[None, :], stream, it).ravel(order="F")
+    xi2 = rng.normal(np.arange(nK)[:, None], GPP_XI2_SUB + np.arange(nf)[None, :], stream, it).ravel(order="F")
+    return gpp_eta_literal(st, model, r, S, dp, xi1, xi2)[0]
 
 
 def update_alpha(st, model, rng, it, data_par=None):
@@ -638,7 +657,10 @@ def update_eta(st, model, rng, it, zero_noise=False, data_par=None):
         st["Eta"] = Eta
         if model["rL"][r].get("sDim", 0) > 0:                          # :111-197
             dp = data_par if data_par is not None else compute_data_parameters(model)
-            Eta[r] = _eta_spatial_full(st, model, r, S, dp, rng, it, zero_noise)
+            if model["rL"][r].get("spatialMethod", "Full") == "GPP":
+                Eta[r] = _eta_spatial_gpp(st, model, r, S, dp, rng, it, zero_noise)
+            else:
+                Eta[r] = _eta_spatial_full(st, model, r, S, dp, rng, it, zero_noise)
             continue
         precs, means = eta_unit_moments(st, model, r, S)
         npr, nf = means.shape

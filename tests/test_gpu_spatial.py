@@ -23,8 +23,9 @@ MODELS = {
     "td_like": dict(ny=50, ns=4, nc=3, nf=2, nr=2, units=[50, 10], spatial=[1], seed=51, alpha_n=30),
     # observation-level spatial factors (np = ny), the default 101-point grid
     "obs_level": dict(ny=40, ns=6, nc=2, nf=2, nr=1, spatial=[0], seed=52),
-    # NNGP (R/computeDataParameters.R:82-136) and GPP (:138-194) levels reach the device as
-    # the dense prior precision of their grid (hmsc_amd/dataparams.py); the oracle's GPP
+    # NNGP (R/computeDataParameters.R:82-136) reaches the device as the dense prior precision
+    # of its grid, GPP (:138-194) as R's low-rank arrays, sampled in R's form on both sides
+    # (R/updateEta.R:148-196: oracle gpp_eta_literal, spatial.hip gpp_*); the oracle's GPP
     # updateAlpha is R's literal knot formula (R/updateAlpha.R:35-75)
     "nngp": dict(ny=40, ns=6, nc=2, nf=2, nr=1, spatial=[0], seed=53, spatial_method="NNGP", n_neighbours=6),
     "gpp": dict(ny=40, ns=6, nc=2, nf=2, nr=1, spatial=[0], seed=54, spatial_method="GPP", n_knots=4),
@@ -37,6 +38,9 @@ MODELS = {
     "large_full": dict(ny=700, ns=6, nc=2, nf=2, nr=1, spatial=[0], seed=57, alpha_n=20),
     "large_nngp": dict(ny=600, ns=5, nc=2, nf=2, nr=1, spatial=[0], seed=58, alpha_n=20,
                        spatial_method="NNGP", n_neighbours=8),
+    # GPP in R's low-rank form at a size the dense path would not take cheaply: 25 knots, 3 factors
+    "large_gpp": dict(ny=800, ns=5, nc=2, nf=3, nr=1, spatial=[0], seed=59, alpha_n=20,
+                      spatial_method="GPP", n_knots=5),
 }
 
 
@@ -55,9 +59,10 @@ def setup(request):
     # likelihood of updateAlpha and iWg[,,alpha] != I in updateEta
     xy = np.asarray(hM.rL[r].s)
     st["Eta"] = list(st["Eta"])
-    st["Eta"][r] = np.column_stack([np.sin(3 * xy[:, 0]) + xy[:, 1], np.cos(2 * xy[:, 1])])[:, :st["Eta"][r].shape[1]]
+    st["Eta"][r] = np.column_stack([np.sin(3 * xy[:, 0]) + xy[:, 1], np.cos(2 * xy[:, 1]),
+                                    xy[:, 0] * xy[:, 1] - 0.25])[:, :st["Eta"][r].shape[1]]
     st["Alpha"] = list(st["Alpha"])
-    st["Alpha"][r] = np.array([7, 12])[:st["Eta"][r].shape[1]]
+    st["Alpha"][r] = np.array([7, 12, 4])[:st["Eta"][r].shape[1]]
     return request.param, hM, m, dp, seed, st, r
 
 

@@ -201,7 +201,8 @@ def test_gpp_knot_on_a_site():
 
 def test_model_buffers_full_grid_routing():
     """'Full' levels hand their coordinates (unit order) to the device by default and
-    computeDataParameters' arrays with spatial_grid='host'; NNGP / GPP always pass arrays."""
+    computeDataParameters' arrays with spatial_grid='host'; NNGP passes its dense arrays, GPP
+    R's low-rank arrays (nKnots, idDg, idDW12g, Fg, iFg, detDg) and no np^2 array."""
     from hmsc_amd.sampler import ModelBuffers
     hM = _model("Full")
     b = ModelBuffers(hM)
@@ -211,6 +212,9 @@ def test_model_buffers_full_grid_routing():
     h = ModelBuffers(hM, spatial_grid="host").struct
     assert bool(h.iWg[0]) and bool(h.RiWg[0]) and not bool(h.sCoord[0])
     g = ModelBuffers(_model("GPP")).struct
-    assert bool(g.iWg[0]) and not bool(g.sCoord[0])
+    assert not bool(g.iWg[0]) and not bool(g.RiWg[0]) and not bool(g.sCoord[0])
+    assert g.nKnots[0] > 0 and all(bool(getattr(g, f)[0]) for f in ("idDg", "idDW12g", "Fg", "iFg", "detDg"))
+    n = ModelBuffers(_model("NNGP")).struct
+    assert bool(n.iWg[0]) and bool(n.RiWg[0])
     with pytest.raises(ValueError):
         ModelBuffers(hM, spatial_grid="cpu")
