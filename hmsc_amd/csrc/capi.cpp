@@ -275,6 +275,8 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
       const bool geom = m->spatialMethod[r] == 1 && !m->iWg[r] && (m->sCoord[r] || m->distMat[r]);
       const bool gpp = m->spatialMethod[r] == 3 && !m->iWg[r] && m->nKnots && m->nKnots[r] > 0 && m->idDg[r] &&
                        m->idDW12g[r] && m->Fg[r] && m->iFg[r] && m->detDg[r];
+      HMSC_REQUIRE(m->nalpha == nullptr || m->nalpha[r] <= HMSC_MAX_ALPHA,
+                   "spatial level: the alphapw grid may have at most 2048 rows in this build");
       HMSC_REQUIRE(m->nalpha != nullptr && m->nalpha[r] > 0 && m->alphapw[r] &&
                        (geom || gpp || (m->iWg[r] && m->RiWg[r] && m->detWg[r])),
                    "spatial level: alphapw and either iWg / RiWg / detWg (computeDataParameters' rLPar), "

@@ -8,6 +8,9 @@
 
 namespace hmsc {
 
+// largest alphapw grid (nrow(rL$alphapw); R's default has 101 points) the device takes
+constexpr int HMSC_MAX_ALPHA = 2048;
+
 struct HmscError : std::runtime_error {
   int code;
   HmscError(int c, const std::string& m) : std::runtime_error(m), code(c) {}

@@ -212,30 +212,43 @@ __device__ inline double alpha_quad_sum(const SpArgs& a, int g, int h) {
   return v;
 }
 
-// one thread per factor: likelihood over the grid, inverse-CDF categorical draw (R's
-// sample.int(gN, 1, prob=like), R/updateAlpha.R:76-78)
-__global__ __launch_bounds__(64) void alpha_draw_kernel(SpArgs a) {
-  const int h = threadIdx.x;
-  if (h >= a.nf) return;
-  const int G = a.nalpha;
-  double mx = -INFINITY;
-  for (int g = 0; g < G; ++g) {
-    const double l = log(a.alphapw[G + g]) - 0.5 * a.detWg[g] - 0.5 * alpha_quad_sum(a, g, h);
-    mx = fmax(mx, l);
-  }
-  double tot = 0.0;
-  for (int g = 0; g < G; ++g) tot += exp(log(a.alphapw[G + g]) - 0.5 * a.detWg[g] - 0.5 * alpha_quad_sum(a, g, h) - mx);
-  const double u = uniforms(a.key, (uint32_t)h, 0, S_ALPHA + LEVEL_STRIDE * a.r, SWEEP_ITER(a)).a * tot;
-  double c = 0.0;
-  int pick = G;
-  for (int g = 0; g < G; ++g) {
-    c += exp(log(a.alphapw[G + g]) - 0.5 * a.detWg[g] - 0.5 * alpha_quad_sum(a, g, h) - mx);
-    if (c > u) {
-      pick = g + 1;
-      break;
+// likelihood over the grid and inverse-CDF categorical draw (R's sample.int(gN, 1,
+// prob=like), R/updateAlpha.R:76-78), one workgroup: the grid points' log-likelihoods (their
+// chunk sums) in parallel, then one thread per factor runs the max / total / cumulative sum
+// over them in grid order (sequential sums, as the oracle's)
+__global__ __launch_bounds__(256) void alpha_draw_kernel(SpArgs a) {
+  __shared__ double like[HMSC_MAX_ALPHA];
+  __shared__ double mx_s;
+  const int G = a.nalpha, t = threadIdx.x;
+  for (int h = 0; h < a.nf; ++h) {
+    for (int g = t; g < G; g += blockDim.x)
+      like[g] = log(a.alphapw[G + g]) - 0.5 * a.detWg[g] - 0.5 * alpha_quad_sum(a, g, h);
+    __syncthreads();
+    if (t == 0) {
+      double mx = -INFINITY;
+      for (int g = 0; g < G; ++g) mx = fmax(mx, like[g]);
+      mx_s = mx;
     }
+    __syncthreads();
+    for (int g = t; g < G; g += blockDim.x) like[g] = exp(like[g] - mx_s);
+    __syncthreads();
+    if (t == 0) {
+      double tot = 0.0;
+      for (int g = 0; g < G; ++g) tot += like[g];
+      const double u = uniforms(a.key, (uint32_t)h, 0, S_ALPHA + LEVEL_STRIDE * a.r, SWEEP_ITER(a)).a * tot;
+      double c = 0.0;
+      int pick = G;
+      for (int g = 0; g < G; ++g) {
+        c += like[g];
+        if (c > u) {
+          pick = g + 1;
+          break;
+        }
+      }
+      a.AlphaD[h] = (double)(pick > G ? G : pick);
+    }
+    __syncthreads();
   }
-  a.AlphaD[h] = (double)(pick > G ? G : pick);
 }
 
 static SpArgs sp_args(State& s, int r, uint32_t iter) {
@@ -417,7 +430,10 @@ __global__ __launch_bounds__(256) void gpp_eta_kernel(SpArgs a, const double* B1
 }
 
 // updateAlpha's GPP statistic, one workgroup per grid point; v_gh goes to chunk 0 of the
-// partial-sum slots alpha_draw_kernel adds (the other chunks zero)
+// partial-sum slots alpha_draw_kernel adds (the other chunks zero).  t_h = eta_h' idDW12g[,,g]:
+// wave w takes the knots k = w, w + 4, ..., its 64 lanes stride down the units (coalesced
+// column reads of idDW12g, the HBM stream of this updater) and reduce by shuffles -- no
+// workgroup barrier per knot.
 __global__ __launch_bounds__(256) void gpp_alpha_kernel(SpArgs a, double* out) {
   const int g = blockIdx.x, np = a.np, nf = a.nf, nK = a.nK, nch = (np + 255) / 256;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -426,29 +442,39 @@ __global__ __launch_bounds__(256) void gpp_alpha_kernel(SpArgs a, double* out) {
   const double* idD = a.idDg + (size_t)np * g;
   const double* W = a.idDW12g + (size_t)np * nK * g;
   const double* iF = a.iFg + (size_t)nK * nK * g;
-  auto block_sum = [&](double s) {
+  auto wave_sum = [&](double s) {
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    __syncthreads();
-    if (lane == 0) red[w] = s;
-    __syncthreads();
-    return (red[0] + red[1]) + (red[2] + red[3]);
+    return s;
   };
   for (int h = 0; h < nf; ++h) {
     const double* eta = a.Eta + (size_t)np * h;
     double s = 0.0;
     for (int i = t; i < np; i += 256) s = fma(eta[i] * (zero ? 1.0 : idD[i]), eta[i], s);
-    double v = block_sum(s);
-    if (!zero) {
-      for (int k = 0; k < nK; ++k) {  // t_h = eta_h' idDW12g[,,g]
-        double q = 0.0;
-        for (int i = t; i < np; i += 256) q = fma(eta[i], W[i + (size_t)np * k], q);
-        const double tk = block_sum(q);
-        if (t == 0) t2[k] = tk;
+    s = wave_sum(s);
+    if (lane == 0) red[w] = s;
+    if (!zero)
+      for (int k = w; k < nK; k += 4) {  // t_h = eta_h' idDW12g[,,g]
+        const double* col = W + (size_t)np * k;
+        double q0 = 0.0, q1 = 0.0;
+        int i = lane;
+        for (; i + 64 < np; i += 128) {
+          q0 = fma(eta[i], col[i], q0);
+          q1 = fma(eta[i + 64], col[i + 64], q1);
+        }
+        if (i < np) q0 = fma(eta[i], col[i], q0);
+        const double tk = wave_sum(q0 + q1);
+        if (lane == 0) t2[k] = tk;
       }
-      __syncthreads();
+    __syncthreads();
+    double v = (red[0] + red[1]) + (red[2] + red[3]);
+    if (!zero) {
       double q = 0.0;  // t_h iF t_h'
       for (int p = t; p < nK * nK; p += 256) q = fma(t2[p % nK] * iF[p], t2[p / nK], q);
-      v -= block_sum(q);
+      q = wave_sum(q);
+      __syncthreads();
+      if (lane == 0) red[w] = q;
+      __syncthreads();
+      v -= (red[0] + red[1]) + (red[2] + red[3]);
     }
     if (t == 0) {
       double* o = out + (size_t)g * nch * nf;
@@ -545,13 +571,13 @@ void launch_alpha(State& s, uint32_t iter) {
       b.work = L.spWork + o.alpha;
       gpp_alpha_kernel<<<L.nalpha, 256, 0, s.stream>>>(b, b.work);
       HIP_OK(hipGetLastError());
-      alpha_draw_kernel<<<1, 64, 0, s.stream>>>(b);
+      alpha_draw_kernel<<<1, 256, 0, s.stream>>>(b);
       HIP_OK(hipGetLastError());
       continue;
     }
     alpha_quad_kernel<<<dim3(L.nalpha, (L.np + 255) / 256), 256, 0, s.stream>>>(a);
     HIP_OK(hipGetLastError());
-    alpha_draw_kernel<<<1, 64, 0, s.stream>>>(a);
+    alpha_draw_kernel<<<1, 256, 0, s.stream>>>(a);
     HIP_OK(hipGetLastError());
   }
 }
