@@ -553,7 +553,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   HIP_OK(hipEventCreateWithFlags(&s.ev_graph, hipEventDisableTiming));
   {
     const char* g = getenv("HMSC_GRAPH_SWEEPS");
-    s.graph_sweeps = g ? std::max(1, std::min(64, atoi(g))) : 4;
+    s.graph_sweeps = g ? std::max(1, std::min(64, atoi(g))) : 8;  // 8: +1.8 % over 4 (one replay launch per 8 sweeps)
   }
   {
     const char* g1 = getenv("HMSC_SINGLE_STREAM");

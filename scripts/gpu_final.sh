@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round-end evidence on one GPU: the full GPU parity suite (test names in the log), smoke(),
+# PMC passes of the dominant kernels, the headline bench reading that PMC summary, a
+# rocprofv3 kernel-trace --stats pass of the same bench, and the config-3 / config-5 lines.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:-final}
+mkdir -p $R/gpurun_out
+cd $R
+timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/${TAG}_pytest.log; exit 1; }
+tail -2 gpurun_out/${TAG}_pytest.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/${TAG}_smoke.log; exit 1; }
+tail -1 gpurun_out/${TAG}_smoke.log
+bash scripts/pmc_z.sh ${TAG}_pmc "z_wave|eta_fused|beta_lambda|side_chain" || exit 1
+python scripts/pmc_summary.py gpurun_out/${TAG}_pmc > gpurun_out/${TAG}_pmc.json || exit 1
+timeout -k 10 600 python bench.py --steps 1000 --warmup 100 --pmc-json gpurun_out/${TAG}_pmc.json > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { echo "bench failed"; tail -20 gpurun_out/${TAG}_bench.err; exit 1; }
+cat gpurun_out/${TAG}_bench.json
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_prof -o run -- python $R/bench.py --steps 1000 --warmup 100 --no-cpu --pmc-json $R/gpurun_out/${TAG}_pmc.json > $R/gpurun_out/${TAG}_prof_bench.json 2> $R/gpurun_out/${TAG}_prof.err || { echo "rocprof failed"; tail -20 $R/gpurun_out/${TAG}_prof.err; exit 1; }
+cd $R
+timeout -k 10 300 python bench.py --workload phylo --steps 200 --warmup 200 > gpurun_out/${TAG}_config3.json 2>/dev/null || exit 1
+timeout -k 10 300 python bench.py --workload spatial --method GPP --steps 500 --warmup 50 > gpurun_out/${TAG}_config5_gpp.json 2>/dev/null || exit 1
+timeout -k 10 300 python bench.py --workload spatial --steps 20 --warmup 5 > gpurun_out/${TAG}_config5_full.json 2>/dev/null || exit 1
+cat gpurun_out/${TAG}_config3.json gpurun_out/${TAG}_config5_gpp.json gpurun_out/${TAG}_config5_full.json
+echo done
