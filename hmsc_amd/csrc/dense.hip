@@ -499,13 +499,24 @@ __global__ __launch_bounds__(256) void lauum_kernel(const double* M, int ldm, in
 // ---------------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------------
+// (kernels instead of hipMemset2DAsync / hipMemcpyAsync: one more kernel node in a captured
+// sweep graph rather than a runtime blit)
+__global__ __launch_bounds__(256) void zero_cols_kernel(double* M, int ldm, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
+  if (i < n) M[(size_t)i + (size_t)ldm * c] = 0.0;
+}
+__global__ __launch_bounds__(256) void copy_vec_kernel(double* x, const double* y, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) x[i] = y[i];
+}
+
 // M <- L^-1 (lower, zero above; n x n, ld ldm) of the lower-triangular L; `dinv` holds
 // ceil(n / 64) * 64 * 64 doubles: the diagonal-block inverses, computed here unless
 // have_dinv (dense_potrf_lower's workspace already holds them)
 void dense_trtri_lower(hipStream_t st, const double* L, int ldl, int n, double* M, int ldm, double* dinv,
                        bool have_dinv) {
   const int nbk = (n + DB - 1) / DB;
-  HIP_OK(hipMemset2DAsync(M, sizeof(double) * ldm, 0, sizeof(double) * n, n, st));
+  zero_cols_kernel<<<dim3((n + 255) / 256, n), 256, 0, st>>>(M, ldm, n);
   if (!have_dinv) trtri_diag_kernel<<<nbk, 64, 0, st>>>(L, ldl, n, dinv);
   for (int k = 0; k < nbk; ++k) {
     trtri_row_kernel<<<k + 1, 256, 0, st>>>(M, ldm, n, k, dinv);
@@ -559,7 +570,7 @@ void dense_trsv_lower(hipStream_t st, const double* L, int n, int lda, double* x
       trsv_bwd_kernel<<<k0 > 0 ? (k0 + DB - 1) / DB : 1, 256, 0, st>>>(L, lda, n, k0, ws, x, y);
     }
   }
-  HIP_OK(hipMemcpyAsync(x, y, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, st));
+  copy_vec_kernel<<<(n + 255) / 256, 256, 0, st>>>(x, y, n);
   HIP_OK(hipGetLastError());
 }
 
