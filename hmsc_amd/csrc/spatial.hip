@@ -184,7 +184,18 @@ __global__ __launch_bounds__(256) void alpha_quad_kernel(SpArgs a) {
     if (p < np) {
       const int lo = a.riw_lower ? 0 : p, hi = a.riw_lower ? p + 1 : np;
       const double* e = a.Eta + (size_t)np * h0;
-      for (int p2 = lo; p2 < hi; ++p2) {
+      int p2 = lo;
+      for (; p2 + 8 <= hi; p2 += 8) {  // eight column loads in flight per lane
+        double rv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) rv[u] = Rg[p + (size_t)np * (p2 + u)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+          for (int hh = 0; hh < 4; ++hh)
+            if (hh < nh) x[hh] = fma(rv[u], e[p2 + u + (size_t)np * hh], x[hh]);
+      }
+      for (; p2 < hi; ++p2) {
         const double rv = Rg[p + (size_t)np * p2];
 #pragma unroll
         for (int hh = 0; hh < 4; ++hh)
