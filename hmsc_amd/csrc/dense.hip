@@ -45,6 +45,29 @@ constexpr int DLD = DB + 1;  // padded LDS leading dimension
 // L^-1's off-diagonal 16-blocks then follow by diagonal distance (one wave per block, MFMA),
 //   I_ib,jb = -I_ib,ib sum_{k = jb}^{ib - 1} L_ib,k I_k,jb.
 // Rows / columns past n are identity padding.
+// Panel staging and the output read-modify-write are latency-bound, not bandwidth-bound (a
+// 64 x 64 tile is 96 KB of traffic): every global load of a thread is issued before the first
+// LDS store or use, at clamped (always valid) addresses, and the output tile is read into
+// registers before the MFMA loop, so one memory latency covers the whole tile.
+template <int ROWS>
+__device__ __forceinline__ void panel_load(const double* A, int lda, int R0, int rows, int k0, int nb,
+                                           double (&v)[ROWS * DB / 256]) {
+#pragma unroll
+  for (int u = 0; u < ROWS * DB / 256; ++u) {
+    const int p = threadIdx.x + 256 * u, r = p % ROWS, c = p / ROWS;
+    v[u] = A[(size_t)(R0 + min(r, rows - 1)) + (size_t)lda * (k0 + min(c, nb - 1))];
+  }
+}
+
+template <int ROWS, int LD>
+__device__ __forceinline__ void panel_store(double* P, int rows, int nb, const double (&v)[ROWS * DB / 256]) {
+#pragma unroll
+  for (int u = 0; u < ROWS * DB / 256; ++u) {
+    const int p = threadIdx.x + 256 * u, r = p % ROWS, c = p / ROWS;
+    P[r + LD * c] = (r < rows && c < nb) ? v[u] : 0.0;
+  }
+}
+
 __device__ __forceinline__ double readlane_d(double v, int l) {
   const long long b = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
@@ -178,10 +201,12 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(double* A, int lda, int 
   __shared__ double I[DB * DLD];  // L^-1 (lower)
   __shared__ double S[4][16 * 17];  // per-wave 16 x 16 scratch (ld 17)
   const int nb = min(DB, n - k0), t = threadIdx.x;
-  for (int p = t; p < DB * DB; p += 256) {
-    const int r = p & 63, c = p >> 6;
-    T[r + DLD * c] = (r < nb && c < nb) ? (r >= c ? A[(size_t)(k0 + r) + (size_t)lda * (k0 + c)] : 0.0)
-                                        : (r == c ? 1.0 : 0.0);
+  double v[DB * DB / 256];
+  panel_load<DB>(A, lda, k0, nb, k0, nb, v);  // all 16 loads in flight (see panel_load)
+#pragma unroll
+  for (int u = 0; u < DB * DB / 256; ++u) {
+    const int p = t + 256 * u, r = p & 63, c = p >> 6;
+    T[r + DLD * c] = (r < nb && c < nb) ? (r >= c ? v[u] : 0.0) : (r == c ? 1.0 : 0.0);
     I[r + DLD * c] = 0.0;
   }
   __syncthreads();
@@ -196,10 +221,14 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(double* A, int lda, int
   __shared__ double Li[DB * DLD];  // Linv[c][k] at c + DLD k
   const int nb = min(DB, n - k0), i0 = k0 + nb + blockIdx.x * DB, rows = min(DB, n - i0);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, lm = lane & 15, lk = lane >> 4;
-  for (int p = t; p < DB * DB; p += 256) {
-    const int r = p & 63, c = p >> 6;
-    P[r + DLD * c] = (r < rows && c < nb) ? A[(size_t)(i0 + r) + (size_t)lda * (k0 + c)] : 0.0;
-    Li[r + DLD * c] = Linv[r + DB * c];
+  {
+    double v[DB * DB / 256], li[DB * DB / 256];
+    panel_load<DB>(A, lda, i0, rows, k0, nb, v);
+#pragma unroll
+    for (int u = 0; u < DB * DB / 256; ++u) li[u] = Linv[t + 256 * u];
+    panel_store<DB, DLD>(P, rows, nb, v);
+#pragma unroll
+    for (int u = 0; u < DB * DB / 256; ++u) Li[((t + 256 * u) & 63) + DLD * ((t + 256 * u) >> 6)] = li[u];
   }
   __syncthreads();
   // out^T[c][r] = sum_k Linv[c][k] P[r][k]: A operand rows = c (column of the output),
@@ -240,15 +269,30 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* A, int lda, in
   const int I0 = base + DB * ti, J0 = base + DB * tj;
   const int rowsI = min(DB, n - I0), rowsJ = min(DB, n - J0);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, lm = lane & 15, lk = lane >> 4;
-  for (int p = t; p < DB * DB; p += 256) {
-    const int r = p & 63, c = p >> 6;
-    PI[r + DLD * c] = (r < rowsI && c < nb) ? A[(size_t)(I0 + r) + (size_t)lda * (k0 + c)] : 0.0;
-    PJ[r + DLD * c] = (r < rowsJ && c < nb) ? A[(size_t)(J0 + r) + (size_t)lda * (k0 + c)] : 0.0;
-  }
-  __syncthreads();
   // wave w: output quadrant rows 32 (w & 1) + [0, 32), columns 32 (w >> 1) + [0, 32); computed
-  // transposed (A operand = PJ rows = output columns, B operand = PI rows = output rows)
+  // transposed (A operand = PJ rows = output columns, B operand = PI rows = output rows);
+  // acc[a][b][q] is column qc + 16 a + lk + 4 q, row qr + 16 b + lm
   const int qr = 32 * (w & 1), qc = 32 * (w >> 1);
+  const bool live = !(ti == tj && qc > qr);  // strictly upper quadrant of a diagonal tile: idle
+  {
+    double vI[DB * DB / 256], vJ[DB * DB / 256];
+    panel_load<DB>(A, lda, I0, rowsI, k0, nb, vI);
+    panel_load<DB>(A, lda, J0, rowsJ, k0, nb, vJ);
+    panel_store<DB, DLD>(PI, rowsI, nb, vI);
+    panel_store<DB, DLD>(PJ, rowsJ, nb, vJ);
+  }
+  double cv[2][2][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = min(qc + 16 * a + lk + 4 * q, rowsJ - 1), r = min(qr + 16 * b + lm, rowsI - 1);
+        cv[a][b][q] = live ? A[(size_t)(I0 + r) + (size_t)lda * (J0 + c)] : 0.0;
+      }
+  __syncthreads();
+  if (!live) return;
   d4 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -264,7 +308,6 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* A, int lda, in
     acc[1][0] = mfma_f64(aJ1, bI0, acc[1][0]);
     acc[1][1] = mfma_f64(aJ1, bI1, acc[1][1]);
   }
-  // acc[a][b][q]: column qc + 16 a + lk + 4 q, row qr + 16 b + lm
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -272,10 +315,7 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* A, int lda, in
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int c = qc + 16 * a + lk + 4 * q, r = qr + 16 * b + lm;
-        if (r < rowsI && c < rowsJ) {
-          double* dst = A + (size_t)(I0 + r) + (size_t)lda * (J0 + c);
-          *dst -= acc[a][b][q];
-        }
+        if (r < rowsI && c < rowsJ) A[(size_t)(I0 + r) + (size_t)lda * (J0 + c)] = cv[a][b][q] - acc[a][b][q];
       }
 }
 
@@ -287,11 +327,39 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* A, int lda, in
 // only written by launches of earlier blocks, so no workgroup reads a value another
 // workgroup of its launch writes.
 // ---------------------------------------------------------------------------------------
+template <bool TR>
+__device__ inline void stage(double* S, const double* M, int ld, int R0, int C0, int rows, int cols) {
+  double v[DB * DB / 256];  // all loads in flight before the first LDS store (see panel_load)
+#pragma unroll
+  for (int u = 0; u < DB * DB / 256; ++u) {
+    const int p = threadIdx.x + 256 * u, a = p & 63, b = p >> 6;
+    v[u] = M[(size_t)(R0 + min(a, rows - 1)) + (size_t)ld * (C0 + min(b, cols - 1))];
+  }
+#pragma unroll
+  for (int u = 0; u < DB * DB / 256; ++u) {
+    const int p = threadIdx.x + 256 * u, a = p & 63, b = p >> 6;
+    S[TR ? b + DLD * a : a + DLD * b] = (a < rows && b < cols) ? v[u] : 0.0;
+  }
+}
+__device__ inline void stage_n(double* S, const double* M, int ld, int R0, int C0, int rows, int cols) {
+  stage<false>(S, M, ld, R0, C0, rows, cols);
+}
+__device__ inline void stage_t(double* S, const double* M, int ld, int R0, int C0, int rows, int cols) {
+  stage<true>(S, M, ld, R0, C0, rows, cols);
+}
+
 __device__ inline void block_solve(const double* Linv, const double* x, int k0, int nb, int trans, double* T,
                                    double* z, double* part) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  for (int p = t; p < DB * DB; p += 256) T[(p & 63) + DLD * (p >> 6)] = Linv[p];
-  if (t < DB) z[t] = t < nb ? x[k0 + t] : 0.0;
+  {
+    double v[DB * DB / 256];
+#pragma unroll
+    for (int u = 0; u < DB * DB / 256; ++u) v[u] = Linv[t + 256 * u];
+    const double xv = x[k0 + min(t & 63, nb - 1)];
+#pragma unroll
+    for (int u = 0; u < DB * DB / 256; ++u) T[((t + 256 * u) & 63) + DLD * ((t + 256 * u) >> 6)] = v[u];
+    if (t < DB) z[t] = t < nb ? xv : 0.0;
+  }
   __syncthreads();
   double s = 0.0;
   for (int c = 16 * w; c < 16 * w + 16; ++c) s = fma(trans ? T[c + DLD * lane] : T[lane + DLD * c], z[c], s);
@@ -312,10 +380,12 @@ __global__ __launch_bounds__(256) void trsv_fwd_kernel(const double* L, int lda,
   block_solve(Linv + (size_t)(k0 / DB) * DB * DB, x, k0, nb, 0, T, z, part);
   if (blockIdx.x == 0 && t < nb) y[k0 + t] = z[t];
   const int i = k0 + nb + blockIdx.x * DB + lane;
+  double lv[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) lv[u] = L[(size_t)min(i, n - 1) + (size_t)lda * (k0 + min(16 * w + u, nb - 1))];
   double s = 0.0;
-  if (i < n)
-#pragma unroll 4
-    for (int c = 16 * w; c < min(16 * w + 16, nb); ++c) s = fma(L[(size_t)i + (size_t)lda * (k0 + c)], z[c], s);
+#pragma unroll
+  for (int u = 0; u < 16; ++u) s = fma(16 * w + u < nb ? lv[u] : 0.0, z[16 * w + u], s);
   part[w * DB + lane] = s;
   __syncthreads();
   if (w == 0 && i < n) x[i] -= (part[lane] + part[DB + lane]) + (part[2 * DB + lane] + part[3 * DB + lane]);
@@ -333,10 +403,7 @@ __global__ __launch_bounds__(256) void trsv_bwd_kernel(const double* L, int lda,
   if (blockIdx.x == 0 && t < nb) y[k0 + t] = z[t];
   const int j0 = blockIdx.x * DB, cols = min(DB, k0 - j0);
   if (cols <= 0) return;
-  for (int p = t; p < DB * DB; p += 256) {
-    const int r = p & 63, c = p >> 6;
-    T[r + DLD * c] = (r < nb && c < cols) ? L[(size_t)(k0 + r) + (size_t)lda * (j0 + c)] : 0.0;
-  }
+  stage_n(T, L, lda, k0, j0, nb, cols);
   __syncthreads();
   double s = 0.0;
   for (int r = w; r < DB; r += 4) s = fma(T[r + DLD * lane], z[r], s);
@@ -352,19 +419,6 @@ __global__ __launch_bounds__(256) void trsv_bwd_kernel(const double* L, int lda,
 // LDS staging of a 64 x 64 tile, zero padded: S[r][k] at r + DLD k
 //   stage_n: S[r][k] = M[R0 + r, C0 + k]         (r < rows, k < cols)
 //   stage_t: S[c][k] = M[R0 + k, C0 + c]         (k < rows, c < cols)
-__device__ inline void stage_n(double* S, const double* M, int ld, int R0, int C0, int rows, int cols) {
-  for (int p = threadIdx.x; p < DB * DB; p += 256) {
-    const int r = p & 63, k = p >> 6;
-    S[r + DLD * k] = (r < rows && k < cols) ? M[(size_t)(R0 + r) + (size_t)ld * (C0 + k)] : 0.0;
-  }
-}
-__device__ inline void stage_t(double* S, const double* M, int ld, int R0, int C0, int rows, int cols) {
-  for (int p = threadIdx.x; p < DB * DB; p += 256) {
-    const int k = p & 63, c = p >> 6;
-    S[c + DLD * k] = (k < rows && c < cols) ? M[(size_t)(R0 + k) + (size_t)ld * (C0 + c)] : 0.0;
-  }
-}
-
 // out[r][c] += sum_k SA[r][k] SB[c][k] over the wave's 32 x 32 quadrant (as chol_update_kernel):
 // acc[a][b][q] holds out[qr + 16 b + lm][qc + 16 a + lk + 4 q]
 __device__ inline void tile_mma(d4 (&acc)[2][2], const double* SA, const double* SB) {
@@ -400,6 +454,19 @@ __device__ inline void acc_each(const d4 (&acc)[2][2], F f) {
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int q = 0; q < 4; ++q) f(qr + 16 * b + lm, qc + 16 * a + lk + 4 * q, acc[a][b][q]);
+}
+
+// the same visit order without values: f(r, c)
+template <class F>
+__device__ inline void acc_each_index(F f) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lm = lane & 15, lk = lane >> 4;
+  const int qr = 32 * (w & 1), qc = 32 * (w >> 1);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) f(qr + 16 * b + lm, qc + 16 * a + lk + 4 * q);
 }
 
 // every diagonal block inverse of a lower-triangular L: Dinv[b] = L_bb^-1 (64 x 64, ld 64,
@@ -457,12 +524,17 @@ __global__ __launch_bounds__(256) void trtri_update_kernel(double* M, int ldm, c
   const int rowsI = min(DB, n - I0), rowsK = min(DB, n - K0), colsJ = min(DB, n - J0);
   stage_n(SA, L, ldl, I0, K0, rowsI, rowsK);
   stage_t(SB, M, ldm, K0, J0, rowsK, colsJ);
+  double cv[16];  // the output tile, read before the MFMA loop
+  int e = 0;
+  acc_each_index([&](int r, int c) { cv[e++] = M[(size_t)(I0 + min(r, rowsI - 1)) + (size_t)ldm * (J0 + min(c, colsJ - 1))]; });
   __syncthreads();
   d4 acc[2][2];
   zero_acc(acc);
   tile_mma(acc, SA, SB);
+  e = 0;
   acc_each(acc, [&](int r, int c, double v) {
-    if (r < rowsI && c < colsJ) M[(size_t)(I0 + r) + (size_t)ldm * (J0 + c)] -= v;
+    const double o = cv[e++];
+    if (r < rowsI && c < colsJ) M[(size_t)(I0 + r) + (size_t)ldm * (J0 + c)] = o - v;
   });
 }
 
@@ -539,6 +611,7 @@ void dense_lauum_lower(hipStream_t st, const double* M, int ldm, int n, double* 
 // look-ahead on a second stream was measured slower: the co-running trailing update more
 // than doubles the one-workgroup diagonal factorization, and the cross-stream joins add
 // ~10 us per panel.)
+
 void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, int* info) {
   for (int k0 = 0; k0 < n; k0 += DB) {
     double* Linv = ws + (size_t)(k0 / DB) * DB * DB;
