@@ -24,6 +24,7 @@
 #include "common.h"
 #include "state.h"
 #include "z_kernel.h"  // d4, mfma_f64
+#include "wave_la.h"
 
 namespace hmsc {
 
@@ -84,6 +85,91 @@ __device__ __forceinline__ d4 mma16_nt(const double* X, int xr, int xc, const do
   return acc;
 }
 
+// 16 x 16 lower Cholesky L and L^-1 by one wave, in 4-column steps on the matrix cores.
+// The block is held in the MFMA accumulator layout, d[r] = A[lk + 4 r][lm] (the full
+// symmetric matrix, read from the lower triangle at Tb, ld DLD).  Step s:
+//   - the 4 x 4 pivot block (register s, lanes (4 s + j) + 16 i) is gathered by v_readlane
+//     and factored uniformly: L4 and Li4 = L4^-1 (refined rsqrt pivots, no divisions);
+//   - the column panel P = A[:, 4s:4s+4] L4^-T = (Li4 A[4s:4s+4, :])^T is one MFMA whose B
+//     operand is register s itself (by symmetry), and lands in the A-operand layout
+//     (lane (lm = i, lk = j) holds P[i][j]); rows above the block are masked to zero;
+//   - the Schur complement update A -= P P^T is one MFMA with P as both operands.
+// L^-1 then follows by block forward substitution on R = I - L X: X_t = Li4_t R_t and
+// R -= P_t X_t, two MFMAs per block row.  Writes L (zeros above) to Tb and L^-1 to Ib.
+// 8 MFMAs and 80 readlanes in place of ~500 readlanes of the row-per-lane form.
+__device__ inline bool chol16_mfma(double* Tb, double* Ib) {
+  const int lane = threadIdx.x & 63, lm = lane & 15, lk = lane >> 4;
+  d4 d;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = lk + 4 * r;
+    d[r] = row >= lm ? Tb[row + DLD * lm] : Tb[lm + DLD * row];
+  }
+  const d4 zero = {0.0, 0.0, 0.0, 0.0};
+  double pc[4], li_op[4];
+  bool ok = true;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    double a[4][4], l[4][4], li[4][4], rinv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j <= i; ++j) a[i][j] = readlane_d(d[s], (4 * s + j) + 16 * i);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      double piv = a[j][j];
+#pragma unroll
+      for (int m = 0; m < j; ++m) piv = fma(-l[j][m], l[j][m], piv);
+      ok = ok && piv > 0.0;
+      rinv[j] = rsqrt_nr(piv > 0.0 ? piv : 1.0);
+      l[j][j] = piv * rinv[j];
+#pragma unroll
+      for (int i = j + 1; i < 4; ++i) {
+        double v = a[i][j];
+#pragma unroll
+        for (int m = 0; m < j; ++m) v = fma(-l[i][m], l[j][m], v);
+        l[i][j] = v * rinv[j];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      li[i][i] = rinv[i];
+#pragma unroll
+      for (int j = i - 1; j >= 0; --j) {
+        double v = 0.0;
+#pragma unroll
+        for (int m = j; m < i; ++m) v = fma(l[i][m], li[m][j], v);
+        li[i][j] = -rinv[i] * v;
+      }
+    }
+    // Li4 as an A operand: lane (lm = k, lk = m) -> Li4[k][m]
+    double op = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int m = 0; m <= k; ++m) op = (lm == k && lk == m) ? li[k][m] : op;
+    li_op[s] = op;
+    double p = mfma_f64(op, d[s], zero)[0];  // P[lm][lk]
+    const int rel = lm - 4 * s;
+    p = (rel < 0 || (rel < 4 && lk > rel)) ? 0.0 : p;
+    pc[s] = p;
+    d = mfma_f64(-p, p, d);
+  }
+  // L: column block s at lane (lm = i, lk = j) = L[i][4 s + j]
+#pragma unroll
+  for (int s = 0; s < 4; ++s) Tb[lm + DLD * (4 * s + lk)] = pc[s];
+  d4 R;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) R[r] = (lk + 4 * r == lm) ? 1.0 : 0.0;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const double x = mfma_f64(li_op[t], R[t], zero)[0];  // X_t[lk][lm] = Linv[4 t + lk][lm]
+    Ib[(4 * t + lk) + DLD * lm] = x;
+    R = mfma_f64(-pc[t], x, R);
+  }
+  return ok;
+}
+
 // The factorization of the block staged in T (lower triangle, zeros above, identity past nb);
 // I zeroed; S: 4 x 16 x 17 doubles.  All 256 threads.
 __device__ inline void diag_body(double* T, double* I, double (*S)[16 * 17], double* A, int lda, int n, int k0,
@@ -94,51 +180,11 @@ __device__ inline void diag_body(double* T, double* I, double (*S)[16 * 17], dou
   __syncthreads();
   for (int kb = 0; kb < 4; ++kb) {
     const int K0 = 16 * kb;
-    if (w == 0) {  // a. 16 x 16 Cholesky, row (lane & 15) per lane
-      const int rl = lane & 15;
-      double b[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) b[j] = T[(K0 + rl) + DLD * (K0 + j)];
-      bool nonpd = false;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const double d = readlane_d(b[c], c);
-        nonpd |= !(d > 0.0);
-        const double sq = sqrt(d > 0.0 ? d : 1.0);
-        const double l = b[c] / sq;
-        b[c] = (rl == c) ? sq : l;
-        const double m = (rl > c) ? l : 0.0;
-#pragma unroll
-        for (int j = c + 1; j < 16; ++j) b[j] = fma(-m, readlane_d(m, j), b[j]);
-      }
-      if (nonpd && lane == 0) bad = 1;
-      if (lane < 16) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) T[(K0 + rl) + DLD * (K0 + j)] = j <= rl ? b[j] : 0.0;
-      }
-      wave_lds_sync();
-      // row rl of L16^-1: x_rl = 1 / L_rl,rl, x_j = -(sum_{k = j+1}^{rl} x_k L_kj) / L_jj
-      double x[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) x[j] = 0.0;
-      double dl = 1.0;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) dl = (rl == c) ? b[c] : dl;
-      const double xr = 1.0 / dl;
-#pragma unroll
-      for (int j = 15; j >= 0; --j) {
-        double s = 0.0;
-#pragma unroll
-        for (int k = j + 1; k < 16; ++k) s = fma(x[k], T[(K0 + k) + DLD * (K0 + j)], s);
-        const double v = -s / T[(K0 + j) + DLD * (K0 + j)];
-        x[j] = (j == rl) ? xr : ((j < rl) ? v : 0.0);
-      }
-      if (lane < 16) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) I[(K0 + rl) + DLD * (K0 + j)] = x[j];
-      }
+    if (w == 0) {  // a. 16 x 16 Cholesky and inverse on the matrix cores (chol16_mfma)
+      if (!chol16_mfma(T + K0 + DLD * K0, I + K0 + DLD * K0) && lane == 0) bad = 1;
     }
     __syncthreads();
+    HMSC_STAMP(102 + 2 * kb);
     const int nrt = 3 - kb;  // 16-row tiles below this diagonal block
     if (nrt > 0) {
       // b. P_I = A_I,kb L16^-T for tiles I = kb + 1 + w (w < nrt)
@@ -164,6 +210,7 @@ __device__ inline void diag_body(double* T, double* I, double (*S)[16 * 17], dou
       }
       __syncthreads();
     }
+    HMSC_STAMP(103 + 2 * kb);
   }
   // off-diagonal 16-blocks of L^-1 by diagonal distance, one wave per block
   for (int dd = 1; dd < 4; ++dd) {
@@ -188,18 +235,31 @@ __device__ inline void diag_body(double* T, double* I, double (*S)[16 * 17], dou
     }
     __syncthreads();
   }
-  for (int p = t; p < DB * DB; p += 256) {
-    const int r = p & 63, c = p >> 6;
-    if (r < nb && c < nb && r >= c) A[(size_t)(k0 + r) + (size_t)lda * (k0 + c)] = T[r + DLD * c];
-    Linv[r + DB * c] = I[r + DLD * c];
+  HMSC_STAMP(110);
+  {
+    double tv[DB * DB / 256], iv[DB * DB / 256];  // every LDS read before the first store
+#pragma unroll
+    for (int u = 0; u < DB * DB / 256; ++u) {
+      const int p = t + 256 * u, r = p & 63, c = p >> 6;
+      tv[u] = T[r + DLD * c];
+      iv[u] = I[r + DLD * c];
+    }
+#pragma unroll
+    for (int u = 0; u < DB * DB / 256; ++u) {
+      const int p = t + 256 * u, r = p & 63, c = p >> 6;
+      if (r < nb && c < nb && r >= c) A[(size_t)(k0 + r) + (size_t)lda * (k0 + c)] = tv[u];
+      Linv[p] = iv[u];
+    }
   }
   if (t == 0 && bad) atomicExch(info, 1);
+  HMSC_STAMP(111);
 }
 
 __global__ __launch_bounds__(256) void chol_diag_kernel(double* A, int lda, int n, int k0, double* Linv, int* info) {
   __shared__ double T[DB * DLD];  // the block; its lower triangle becomes L
   __shared__ double I[DB * DLD];  // L^-1 (lower)
   __shared__ double S[4][16 * 17];  // per-wave 16 x 16 scratch (ld 17)
+  HMSC_STAMP(100);
   const int nb = min(DB, n - k0), t = threadIdx.x;
   double v[DB * DB / 256];
   panel_load<DB>(A, lda, k0, nb, k0, nb, v);  // all 16 loads in flight (see panel_load)
@@ -210,6 +270,7 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(double* A, int lda, int 
     I[r + DLD * c] = 0.0;
   }
   __syncthreads();
+  HMSC_STAMP(101);
   diag_body(T, I, S, A, lda, n, k0, Linv, info);
 }
 
