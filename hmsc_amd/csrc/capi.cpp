@@ -10,6 +10,7 @@
 #include <cstring>
 #include <cstdlib>
 #include <thread>
+#include <map>
 #include <memory>
 #include <chrono>
 #include <condition_variable>
@@ -115,19 +116,39 @@ static Mat host_mm(const Mat& A, const Mat& B, int m, int k, int n) {
 }
 
 // ---------------------------- device memory ----------------------------
+// Host <-> device copies and fills go through non-blocking streams, never the legacy null
+// stream: a legacy-stream operation in one thread while another thread's chain is capturing
+// its sweep graph fails with "operation would make the legacy stream depend on a capturing
+// blocking stream" (several chains driven from host threads of one process).
+static hipStream_t thread_stream() {
+  thread_local std::map<int, hipStream_t> streams;
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  hipStream_t& st = streams[dev];
+  if (!st) HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  return st;
+}
+static void copy_sync(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t st = nullptr) {
+  if (!st) st = thread_stream();
+  HIP_OK(hipMemcpyAsync(dst, src, bytes, kind, st));
+  HIP_OK(hipStreamSynchronize(st));
+}
+
 template <class T>
 static T* dalloc(size_t n) {
   T* p = nullptr;
   if (n == 0) n = 1;
   HIP_OK(hipMalloc(&p, n * sizeof(T)));
-  HIP_OK(hipMemset(p, 0, n * sizeof(T)));
+  const hipStream_t st = thread_stream();
+  HIP_OK(hipMemsetAsync(p, 0, n * sizeof(T), st));
+  HIP_OK(hipStreamSynchronize(st));
   return p;
 }
 
 template <class T>
 static T* dupload(const T* h, size_t n) {
   T* p = dalloc<T>(n);
-  if (h && n) HIP_OK(hipMemcpy(p, h, n * sizeof(T), hipMemcpyHostToDevice));
+  if (h && n) copy_sync(p, h, n * sizeof(T), hipMemcpyHostToDevice);
   return p;
 }
 
@@ -360,7 +381,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
         HIP_OK(hipStreamSynchronize(s.stream));
         HIP_OK(hipFree(geo));
         int bad = 0;
-        HIP_OK(hipMemcpy(&bad, flag, sizeof(int), hipMemcpyDeviceToHost));
+        copy_sync(&bad, flag, sizeof(int), hipMemcpyDeviceToHost);
         HIP_OK(hipFree(flag));
         HMSC_REQUIRE(bad == 0, "spatial level: a grid matrix W_g = exp(-d / alpha_g) is not positive definite "
                                "(duplicated coordinates?)");
@@ -491,7 +512,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.rho = dalloc<double>(1);
   {
     const double one = 1.0;  // rho = 1 (R/computeInitialParameters.R:226)
-    HIP_OK(hipMemcpy(s.rho, &one, sizeof(double), hipMemcpyHostToDevice));
+    copy_sync(s.rho, &one, sizeof(double), hipMemcpyHostToDevice, s.stream);
   }
   if (m->C != nullptr) setup_phylo(s, m);
   // workspaces
@@ -647,14 +668,14 @@ static void get_state(State& s, hmsc_params* p) {
         if (p->Psi[r]) p->Psi[r][h + (size_t)nf * j] = Psi[fo + h + (size_t)s.NF * j];
       }
     std::vector<double> ad(std::max(1, nf), 1.0);
-    if (nf > 0) HIP_OK(hipMemcpy(ad.data(), s.lev[r].AlphaD, sizeof(double) * nf, hipMemcpyDeviceToHost));
+    if (nf > 0) copy_sync(ad.data(), s.lev[r].AlphaD, sizeof(double) * nf, hipMemcpyDeviceToHost, s.stream);
     for (int h = 0; h < nf; ++h) {
       if (p->Delta[r]) p->Delta[r][h] = Delta[fo + h];
       if (p->Alpha[r]) p->Alpha[r][h] = (int32_t)ad[h];
     }
   }
   double rho = 1.0;
-  HIP_OK(hipMemcpy(&rho, s.rho, sizeof(double), hipMemcpyDeviceToHost));
+  copy_sync(&rho, s.rho, sizeof(double), hipMemcpyDeviceToHost, s.stream);
   p->rho = (int32_t)rho;
 }
 
@@ -715,7 +736,7 @@ static void set_state(State& s, const hmsc_params* p) {
                      "set_state: Alpha index out of the alphapw grid");
         ad[h] = s.lev[r].spatial ? p->Alpha[r][h] : 1.0;
       }
-      HIP_OK(hipMemcpy(s.lev[r].AlphaD, ad.data(), sizeof(double) * nf, hipMemcpyHostToDevice));
+      copy_sync(s.lev[r].AlphaD, ad.data(), sizeof(double) * nf, hipMemcpyHostToDevice, s.stream);
     }
   }
   h2d(s.BL, BL.data(), BL.size(), s.stream);
@@ -728,7 +749,7 @@ static void set_state(State& s, const hmsc_params* p) {
   if (p->rho > 0) {  // initPar$rho as a grid index (R/computeInitialParameters.R:223-224)
     HMSC_REQUIRE(!s.phylo || p->rho <= s.nrho, "set_state: rho index out of range");
     const double rho = p->rho;
-    HIP_OK(hipMemcpy(s.rho, &rho, sizeof(double), hipMemcpyHostToDevice));
+    copy_sync(s.rho, &rho, sizeof(double), hipMemcpyHostToDevice, s.stream);
   }
   HIP_OK(hipStreamSynchronize(s.stream));
   s.zt_valid = false;
@@ -1246,7 +1267,7 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
                  1e-6 * diag_wait_ns);
   }
   int flag[2] = {0, 0};
-  HIP_OK(hipMemcpy(flag, s.dev_flags, sizeof(flag), hipMemcpyDeviceToHost));
+  copy_sync(flag, s.dev_flags, sizeof(flag), hipMemcpyDeviceToHost, s.stream);
   HMSC_REQUIRE(flag[0] == 0 && flag[1] == 0, "a Cholesky factorisation failed (matrix not positive definite)");
   if (recording) {
     for (auto& th : workers) th.join();
@@ -1334,10 +1355,10 @@ int hmsc_spatial_full_grid(int32_t device, int32_t np, int32_t sdim, const doubl
     spatial_full_grid(st, np, coords ? sdim : 0, coords ? geo : nullptr, coords ? nullptr : geo, alphas, G, dI, dR,
                       dd, flag);
     int bad = 0;
-    HIP_OK(hipMemcpy(&bad, flag, sizeof(int), hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(iWg, dI, n2 * G * sizeof(double), hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(RiWg, dR, n2 * G * sizeof(double), hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(detWg, dd, G * sizeof(double), hipMemcpyDeviceToHost));
+    copy_sync(&bad, flag, sizeof(int), hipMemcpyDeviceToHost);
+    copy_sync(iWg, dI, n2 * G * sizeof(double), hipMemcpyDeviceToHost);
+    copy_sync(RiWg, dR, n2 * G * sizeof(double), hipMemcpyDeviceToHost);
+    copy_sync(detWg, dd, G * sizeof(double), hipMemcpyDeviceToHost);
     (void)hipFree(geo), (void)hipFree(dI), (void)hipFree(dR), (void)hipFree(dd), (void)hipFree(flag);
     (void)hipStreamDestroy(st);
     HMSC_REQUIRE(bad == 0, "hmsc_spatial_full_grid: a grid matrix is not positive definite");
@@ -1540,7 +1561,7 @@ int hmsc_debug_get(hmsc_state* h, const char* name, double* out, int64_t n) {
       throw HmscError(-1, "debug_get: unknown buffer " + nm);
     HMSC_REQUIRE(src != nullptr, "debug_get: buffer not allocated (enable with noise mode bit 2)");
     HMSC_REQUIRE(n <= avail, "debug_get: n exceeds buffer size");
-    HIP_OK(hipMemcpy(out, src, sizeof(double) * n, hipMemcpyDeviceToHost));
+    copy_sync(out, src, sizeof(double) * n, hipMemcpyDeviceToHost, s.stream);
   });
 }
 
@@ -1601,8 +1622,8 @@ int hmsc_kernel_timing_get(hmsc_state* h, int32_t id, double* total_us, int32_t*
     join_side(s);
     HIP_OK(hipStreamSynchronize(s.stream));
     std::vector<unsigned long long> v((size_t)2 * KT_SLOTS);
-    HIP_OK(hipMemcpy(v.data(), s.d_kt + (size_t)id * 2 * KT_SLOTS, sizeof(unsigned long long) * v.size(),
-                     hipMemcpyDeviceToHost));
+    copy_sync(v.data(), s.d_kt + (size_t)id * 2 * KT_SLOTS, sizeof(unsigned long long) * v.size(),
+                     hipMemcpyDeviceToHost);
     int khz = 0;
     HIP_OK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, s.device));
     HMSC_REQUIRE(khz > 0, "wall clock rate unavailable");

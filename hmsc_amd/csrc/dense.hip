@@ -28,6 +28,16 @@
 
 namespace hmsc {
 
+// phase clock stamps of chol_diag_kernel for scripts/tmp-style microbenchmarks that define
+// g_stamps in their own translation unit (-DHMSC_STAMPS -DHMSC_DENSE_STAMPS)
+#ifdef HMSC_DENSE_STAMPS
+#define DENSE_STAMP(i) HMSC_STAMP(i)
+#else
+#define DENSE_STAMP(i) \
+  do {                 \
+  } while (0)
+#endif
+
 constexpr int DB = 64;       // panel / tile size
 constexpr int DLD = DB + 1;  // padded LDS leading dimension
 
@@ -184,7 +194,7 @@ __device__ inline void diag_body(double* T, double* I, double (*S)[16 * 17], dou
       if (!chol16_mfma(T + K0 + DLD * K0, I + K0 + DLD * K0) && lane == 0) bad = 1;
     }
     __syncthreads();
-    HMSC_STAMP(102 + 2 * kb);
+    DENSE_STAMP(102 + 2 * kb);
     const int nrt = 3 - kb;  // 16-row tiles below this diagonal block
     if (nrt > 0) {
       // b. P_I = A_I,kb L16^-T for tiles I = kb + 1 + w (w < nrt)
@@ -210,7 +220,7 @@ __device__ inline void diag_body(double* T, double* I, double (*S)[16 * 17], dou
       }
       __syncthreads();
     }
-    HMSC_STAMP(103 + 2 * kb);
+    DENSE_STAMP(103 + 2 * kb);
   }
   // off-diagonal 16-blocks of L^-1 by diagonal distance, one wave per block
   for (int dd = 1; dd < 4; ++dd) {
@@ -235,7 +245,7 @@ __device__ inline void diag_body(double* T, double* I, double (*S)[16 * 17], dou
     }
     __syncthreads();
   }
-  HMSC_STAMP(110);
+  DENSE_STAMP(110);
   {
     double tv[DB * DB / 256], iv[DB * DB / 256];  // every LDS read before the first store
 #pragma unroll
@@ -252,14 +262,14 @@ __device__ inline void diag_body(double* T, double* I, double (*S)[16 * 17], dou
     }
   }
   if (t == 0 && bad) atomicExch(info, 1);
-  HMSC_STAMP(111);
+  DENSE_STAMP(111);
 }
 
 __global__ __launch_bounds__(256) void chol_diag_kernel(double* A, int lda, int n, int k0, double* Linv, int* info) {
   __shared__ double T[DB * DLD];  // the block; its lower triangle becomes L
   __shared__ double I[DB * DLD];  // L^-1 (lower)
   __shared__ double S[4][16 * 17];  // per-wave 16 x 16 scratch (ld 17)
-  HMSC_STAMP(100);
+  DENSE_STAMP(100);
   const int nb = min(DB, n - k0), t = threadIdx.x;
   double v[DB * DB / 256];
   panel_load<DB>(A, lda, k0, nb, k0, nb, v);  // all 16 loads in flight (see panel_load)
@@ -270,7 +280,7 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(double* A, int lda, int 
     I[r + DLD * c] = 0.0;
   }
   __syncthreads();
-  HMSC_STAMP(101);
+  DENSE_STAMP(101);
   diag_body(T, I, S, A, lda, n, k0, Linv, info);
 }
 

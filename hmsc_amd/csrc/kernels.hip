@@ -308,18 +308,17 @@ __global__ __launch_bounds__(256) void beta_lambda_wave_kernel(BLArgs a) {
   const int K = a.K, nc = a.nc, nt = a.nt, i = lane_id(), w = threadIdx.x >> 6, t = threadIdx.x;
   const int j = blockIdx.x * 4 + w;
   if (blockIdx.x == 0) HMSC_STAMP(60);
-  for (int p = t; p < K * K; p += 256) sG[p % K + 33 * (p / K)] = a.G[p % K + (size_t)a.Kmax * (p / K)];
-  for (int p = t; p < nc * nc; p += 256) sIV[p] = a.iV[p];
-  for (int p = t; p < nc * nt && p < 32 * 8; p += 256) sGam[p] = a.Gamma[p];
-  if (t < a.nr) {  // tau = cumprod(Delta) per level   (:51)
-    int f0 = 0;
-    for (int r = 0; r < t; ++r) f0 += a.lev_nf[r];
-    double c = 1.0;
-    for (int h = 0; h < a.lev_nf[t]; ++h) {
-      c *= a.Delta[f0 + h];
-      sTau[f0 + h] = c;
-    }
+  // every global load of the prologue is issued before the first LDS store (a staging loop
+  // with a store per iteration waits out one memory latency per iteration)
+  double gv[4], ivv[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int p = t + 256 * u, pc = p < K * K ? p : 0;
+    gv[u] = a.G[pc % K + (size_t)a.Kmax * (pc / K)];
+    ivv[u] = a.iV[p < nc * nc ? p : 0];
   }
+  const double gam = a.Gamma[t < nc * nt ? t : 0];
+  const double del = a.NF > 0 ? a.Delta[t < a.NF ? t : 0] : 1.0;
   // this species' own inputs, loaded before the barrier so their latency overlaps it
   const int jj = j < a.ns_loc ? j : a.ns_loc - 1;
   const double isig = a.iSigma[jj];
@@ -329,11 +328,26 @@ __global__ __launch_bounds__(256) void beta_lambda_wave_kernel(BLArgs a) {
 #pragma unroll
   for (int q = 0; q < 8; ++q) trj[q] = q < nt ? a.Tr[jj + (size_t)a.ns_loc * q] : 0.0;
   const int nai = a.na_index ? a.na_index[jj] : -1;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int p = t + 256 * u;
+    if (p < K * K) sG[p % K + 33 * (p / K)] = gv[u];
+    if (p < nc * nc) sIV[p] = ivv[u];
+  }
+  if (t < nc * nt && t < 32 * 8) sGam[t] = gam;
+  if (t < a.NF) sTau[t] = del;  // Delta here; each lane forms its own cumprod below
   __syncthreads();
   if (j >= a.ns_loc) return;
   double* lds = tiles + w * WV_TILE;
+  // tau = cumprod(Delta) within the level of factor i - nc   (:51)
+  double tau = 1.0;
+  if (i >= nc && i < K) {
+    int f0 = 0, r = 0;
+    while (r < a.nr && f0 + a.lev_nf[r] <= i - nc) f0 += a.lev_nf[r++];
+    for (int h = f0; h <= i - nc; ++h) tau *= sTau[h];
+  }
   // prior precision diagonal of Lambda rows: Psi_hj * tau_h
-  const double pd = (i >= nc && i < K) ? psi * sTau[i - nc] : 0.0;
+  const double pd = (i >= nc && i < K) ? psi * tau : 0.0;
   double mu = 0.0;  // Mu_j = Gamma Tr_j^T   (:62)
   if (i < nc)
 #pragma unroll
@@ -1026,19 +1040,35 @@ struct G2Args {
   int noise_zero;
 };
 
+// for (p = threadIdx.x; p < n; p += blockDim.x) store(p, load(p)) with U loads of a thread in
+// flight before its stores (a loop with a store per iteration waits one latency per iteration)
+template <int U, class Load, class Store>
+__device__ __forceinline__ void batched_for(int n, Load load, Store store) {
+  const int nt = blockDim.x;
+  for (int p0 = threadIdx.x; p0 < n; p0 += U * nt) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = p0 + u * nt < n ? load(p0 + u * nt) : 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (p0 + u * nt < n) store(p0 + u * nt, v[u]);
+  }
+}
+
 __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
   // Every input is staged into LDS by all 256 threads first (coalesced, in parallel); the
   // small products then run from LDS instead of as per-thread loops of dependent global loads.
   __shared__ int all_one;
-  __shared__ double S0[512], LTr[512], v1[256], v2[256], xi[256], red[8][64];
+  __shared__ double S0[512], LTr[512], v1[256], v2[256], xi[256], red[8][64], sGL[2048];
   extern __shared__ __attribute__((aligned(16))) double dyn[];  // B1 | LS  when a.stage
   HMSC_STAMP(30);
   const int nc = a.nc, nt = a.nt, N = nc * nt, t = threadIdx.x, n2 = nc * nc;
   if (t == 0) all_one = 1;
   __syncthreads();
-  if (a.check_isigma)
-    for (int j = t; j < a.ns_loc; j += blockDim.x)
-      if (a.iSigma[j] != 1.0) all_one = 0;  // acts only if all(iSigma == 1)  (:36)
+  if (a.check_isigma)  // acts only if all(iSigma == 1)  (:36)
+    batched_for<8>(a.ns_loc, [&](int j) { return a.iSigma[j]; }, [&](int, double v) {
+      if (v != 1.0) all_one = 0;
+    });
   if (t == 0 && a.isig_count && *a.isig_count != 0.0) all_one = 0;  // ... over every rank's species
   __syncthreads();
   if (!all_one) return;
@@ -1046,7 +1076,7 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
   const double *B1 = a.prep, *LS = a.prep + n2;
   if (a.stage) {
     double* d = dyn;
-    for (int p = t; p < n2 + N * N; p += blockDim.x) d[p] = a.prep[p];
+    batched_for<8>(n2 + N * N, [&](int p) { return a.prep[p]; }, [&](int p, double v) { d[p] = v; });
     B1 = d;
     LS = d + n2;
   }
@@ -1056,8 +1086,17 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
     for (int p0 = 0; p0 < P; p0 += 32) {
       const int p = p0 + l;
       double s = 0.0;
-      if (p < P)
-        for (int b = g; b < a.nparts; b += 8) s += a.part[(size_t)b * P + p];
+      if (p < P) {  // every 8th part, eight loads in flight per step, summed in order
+        int b = g;
+        for (; b + 56 < a.nparts; b += 64) {
+          double x[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) x[u] = a.part[(size_t)(b + 8 * u) * P + p];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) s += x[u];
+        }
+        for (; b < a.nparts; b += 8) s += a.part[(size_t)b * P + p];
+      }
       red[g][l + (p0 ? 32 : 0)] = s;
     }
     __syncthreads();
@@ -1082,6 +1121,10 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
         LTr[p - n1] = s;
     }
   }
+  const bool stage_g = nc * a.NF <= 2048;
+  if (stage_g)  // X^T Eta block of G, read by the XZT products below
+    batched_for<8>(nc * a.NF, [&](int p) { return a.G[p % nc + (size_t)a.Kmax * (nc + p / nc)]; },
+                   [&](int p, double v) { sGL[p] = v; });
   for (int r = t; r < N; r += blockDim.x) xi[r] = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)r, 0, S_GAMMA2, SWEEP_ITER(a));
   __syncthreads();
   HMSC_STAMP(31);
@@ -1089,7 +1132,8 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
   for (int p = t; p < n1; p += blockDim.x) {
     const int c = p % nc, q = p / nc;
     double s = 0.0;
-    for (int f = 0; f < a.NF; ++f) s += a.G[c + a.Kmax * (nc + f)] * LTr[f + a.NF * q];
+    for (int f = 0; f < a.NF; ++f)
+      s += (stage_g ? sGL[c + nc * f] : a.G[c + a.Kmax * (nc + f)]) * LTr[f + a.NF * q];
     S0[p] -= s;
   }
   __syncthreads();
@@ -1197,7 +1241,7 @@ void launch_gamma2(State& s, uint32_t iter) {
   a.iter_dev = s.capturing ? s.d_iter : nullptr;
   a.noise_zero = s.noise_mode;
   const size_t N = (size_t)s.nc * s.nt, stage_bytes = ((size_t)s.nc * s.nc + N * N) * sizeof(double);
-  a.stage = stage_bytes <= 48 * 1024;
+  a.stage = stage_bytes <= 28 * 1024;  // + 35 KB static: within 64 KB per workgroup
   join_side(s);  // iV and the prep matrices come from the previous sweep's GammaV (side stream)
   gamma2_final_kernel<<<1, 256, a.stage ? stage_bytes : 0, s.stream>>>(a);
   HIP_OK(hipGetLastError());
