@@ -173,35 +173,68 @@ __global__ __launch_bounds__(256) void sp_store_kernel(SpArgs a, const double* r
 // Full grid's chol(W)^-1).  Grid (nalpha, ceil(np / 256)): a workgroup takes 256 rows p of one
 // grid matrix (coalesced down the columns), four factors per pass, and leaves its partial
 // sums at work[(g * nch + chunk) * nf + h]; alpha_draw_kernel adds the chunks in order.
+constexpr int AQ_LDS = 6144;  // Eta values (np x 4-factor block) staged per workgroup: 48 KB
+
 __global__ __launch_bounds__(256) void alpha_quad_kernel(SpArgs a) {
   const int g = blockIdx.x, chunk = blockIdx.y, nch = gridDim.y, np = a.np, nf = a.nf;
   const double* Rg = a.RiWg + (size_t)np * np * g;
   const int p = chunk * 256 + threadIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   __shared__ double red[4][4];
+  __shared__ double sE[AQ_LDS];
+  // The column range is the workgroup's (uniform): the Eta block is staged in LDS and read
+  // back at uniform addresses (broadcast), so the vector memory path carries only the R
+  // stream; the triangle's edge inside the workgroup's 256 x 256 diagonal block is an exec
+  // mask on the loads (masked columns add exact zeros: the per-row sums are unchanged).
+  const int p0 = chunk * 256, lower = a.riw_lower;
+  const int c_lo = lower ? 0 : p0, c_hi = lower ? min(np, p0 + 256) : np;
+  const int pr = min(p, np - 1);
   for (int h0 = 0; h0 < nf; h0 += 4) {
     const int nh = min(4, nf - h0);
-    double x[4] = {0.0, 0.0, 0.0, 0.0};
-    if (p < np) {
-      const int lo = a.riw_lower ? 0 : p, hi = a.riw_lower ? p + 1 : np;
-      const double* e = a.Eta + (size_t)np * h0;
-      int p2 = lo;
-      for (; p2 + 8 <= hi; p2 += 8) {  // eight column loads in flight per lane
-        double rv[8];
+    const int ncol = c_hi - c_lo;
+    const bool staged = ncol * nh <= AQ_LDS;
+    const double* e = a.Eta + (size_t)np * h0;
+    if (staged) {  // sE[(c - c_lo) nh + hh] = Eta[c, h0 + hh]
+      const int n = ncol * nh;
+      for (int q0 = threadIdx.x; q0 < n; q0 += 8 * 256) {
+        double v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) rv[u] = Rg[p + (size_t)np * (p2 + u)];
+        for (int u = 0; u < 8; ++u) {
+          const int q = min(q0 + 256 * u, n - 1), c = q / nh, hh = q - c * nh;
+          v[u] = e[c_lo + c + (size_t)np * hh];
+        }
 #pragma unroll
         for (int u = 0; u < 8; ++u)
+          if (q0 + 256 * u < n) sE[q0 + 256 * u] = v[u];
+      }
+      __syncthreads();
+    }
+    double x[4] = {0.0, 0.0, 0.0, 0.0};
+    auto rows = [&](auto ev) {  // ev(c, hh) = Eta[c, h0 + hh]
+      int p2 = c_lo;
+      for (; p2 + 16 <= c_hi; p2 += 16) {  // sixteen column loads in flight per lane
+        double rv[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int c = p2 + u;
+          rv[u] = (p < np && (lower ? c <= p : c >= p)) ? Rg[pr + (size_t)np * c] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
 #pragma unroll
           for (int hh = 0; hh < 4; ++hh)
-            if (hh < nh) x[hh] = fma(rv[u], e[p2 + u + (size_t)np * hh], x[hh]);
+            if (hh < nh) x[hh] = fma(rv[u], ev(p2 + u, hh), x[hh]);
       }
-      for (; p2 < hi; ++p2) {
-        const double rv = Rg[p + (size_t)np * p2];
+      for (; p2 < c_hi; ++p2) {
+        const double rv = (p < np && (lower ? p2 <= p : p2 >= p)) ? Rg[pr + (size_t)np * p2] : 0.0;
 #pragma unroll
         for (int hh = 0; hh < 4; ++hh)
-          if (hh < nh) x[hh] = fma(rv, e[p2 + (size_t)np * hh], x[hh]);
+          if (hh < nh) x[hh] = fma(rv, ev(p2, hh), x[hh]);
       }
-    }
+    };
+    if (staged)
+      rows([&](int c, int hh) { return sE[(c - c_lo) * nh + hh]; });
+    else
+      rows([&](int c, int hh) { return e[c + (size_t)np * hh]; });
 #pragma unroll
     for (int hh = 0; hh < 4; ++hh) {
       double s = x[hh] * x[hh];
