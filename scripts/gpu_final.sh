@@ -17,6 +17,7 @@ timeout -k 10 600 python bench.py --steps 1000 --warmup 100 --pmc-json gpurun_ou
 cat gpurun_out/${TAG}_bench.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_prof -o run -- python $R/bench.py --steps 1000 --warmup 100 --no-cpu --pmc-json $R/gpurun_out/${TAG}_pmc.json > $R/gpurun_out/${TAG}_prof_bench.json 2> $R/gpurun_out/${TAG}_prof.err || { echo "rocprof failed"; tail -20 $R/gpurun_out/${TAG}_prof.err; exit 1; }
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_chol -o run -- python $R/scripts/chol_bench.py 5000 3 > $R/gpurun_out/${TAG}_chol.log 2>&1 || { echo "chol profile failed"; exit 1; }
 cd $R
 timeout -k 10 300 python bench.py --workload phylo --steps 200 --warmup 200 > gpurun_out/${TAG}_config3.json 2>/dev/null || exit 1
 timeout -k 10 300 python bench.py --workload spatial --method GPP --steps 500 --warmup 50 > gpurun_out/${TAG}_config5_gpp.json 2>/dev/null || exit 1
