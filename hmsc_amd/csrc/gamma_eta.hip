@@ -253,14 +253,16 @@ __device__ inline void ge_seg_m_obs(const GEArgs& a, const GEPtrs& P, int g0, in
   }
   for (int p = g0; p < N; p += gs) {
     const int c = p % nc, j = p / nc;
+    double x1[GE_NF_MAX];  // (X'S LamiD')[c, h1]: the same for every j, formed once
+    for (int h1 = 0; h1 < nf; ++h1) {
+      double x = 0.0;
+      for (int j2 = 0; j2 < ns; ++j2) x = fma(P.XtS[c + nc * j2], P.LamiD[h1 + nf * j2], x);
+      x1[h1] = x;
+    }
     double s = 0.0;
     for (int h2 = 0; h2 < nf; ++h2) {
       double u = 0.0;
-      for (int h1 = 0; h1 < nf; ++h1) {
-        double x1 = 0.0;
-        for (int j2 = 0; j2 < ns; ++j2) x1 = fma(P.XtS[c + nc * j2], P.LamiD[h1 + nf * j2], x1);
-        u = fma(x1, P.iW0[h1 + nf * h2], u);
-      }
+      for (int h1 = 0; h1 < nf; ++h1) u = fma(x1[h1], P.iW0[h1 + nf * h2], u);
       s = fma(u, P.LamiD[h2 + nf * j], s);
     }
     P.mb20[p] = s;
@@ -561,23 +563,144 @@ __global__ __launch_bounds__(256) void ge_b_m_kernel(GEArgs a) {
     ge_seg_m_units(a, P, g0, gs);
   ge_seg_mb10(a, P, g0, gs);
 }
+// The blocked path's reductions: one wave per output, lanes over the summation index
+// (coalesced where the operand is a column), U terms' loads in flight per lane, a
+// cross-lane sum at the end.  (A thread per output with a serial loop over ns or nc ns
+// terms waited out one L2 round trip per few terms: 0.1-0.3 ms per segment at nc ns = 1200.)
+template <int U, class F>
+__device__ inline double wave_sum(int n, F f) {
+  const int lane = threadIdx.x & 63;
+  double s = 0.0;
+  for (int k0 = lane; k0 < n; k0 += 64 * U) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = k0 + 64 * u < n ? f(k0 + 64 * u) : 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) s += v[u];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  return s;
+}
+
+#define GE_WAVE_IDX                                                      \
+  const GEPtrs P = ge_ptrs(a);                                           \
+  const int lane = threadIdx.x & 63;                                     \
+  const int w0 = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);    \
+  const int ws = (int)((gridDim.x * blockDim.x) >> 6);                   \
+  (void)P, (void)lane;
+
+// with v = M^-1 (mb10 - mb20): wv = mb10 - mb20 - T1 v (mb30, :63-64), xi ~ N(0, I); T1 is
+// symmetric (kron(tmp1, X'X) for np = ny, T otherwise), read by columns
 __global__ __launch_bounds__(256) void ge_b_wv_kernel(GEArgs a) {
-  GE_GRID_IDX
-  ge_seg_wv(a, P, g0, gs, SWEEP_ITER(a));
+  GE_WAVE_IDX
+  const int ns = a.ns, nc = a.nc, N = P.N;
+  const uint32_t str = LEVEL_STRIDE * (uint32_t)a.r, it = SWEEP_ITER(a);
+  for (int p = w0; p < N; p += ws) {
+    const int c = p % nc, j = p / nc;
+    double s;
+    if (P.obs)
+      s = wave_sum<8>(ns, [&](int j2) {
+        double u = 0.0;
+        for (int c2 = 0; c2 < nc; ++c2) u = fma(P.XtX[c + nc * c2], P.v[c2 + nc * j2], u);
+        return P.tmp1[j2 + (size_t)ns * j] * u;
+      });
+    else
+      s = wave_sum<8>(N, [&](int p2) { return P.T[p2 + (size_t)N * p] * P.v[p2]; });
+    if (lane == 0) {
+      P.wv[p] = P.mb10[p] - P.mb20[p] - s;
+      P.xi[p] = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)p, 0, S_GE_BETA + str, it);
+    }
+  }
 }
+// mb = A wv   (:65); A symmetric, read by columns
 __global__ __launch_bounds__(256) void ge_b_mb_kernel(GEArgs a) {
-  GE_GRID_IDX
-  ge_seg_mb(P, g0, gs);
+  GE_WAVE_IDX
+  const int N = P.N;
+  for (int p = w0; p < N; p += ws) {
+    const double s = wave_sum<8>(N, [&](int p2) { return P.A[p2 + (size_t)N * p] * P.wv[p2]; });
+    if (lane == 0) P.mb[p] = s;
+  }
 }
+// Beta = mb + RM^-1 xi; Gamma | Beta (:66-71): one 1024-thread workgroup, the Pg entries and
+// the right-hand side one wave each
 __global__ __launch_bounds__(1024) void ge_b_gamma_kernel(GEArgs a) {
   __shared__ int flag;
   const GEPtrs P = ge_ptrs(a);
-  ge_wg_gamma(a, P, &flag, SWEEP_ITER(a));
+  const int t = threadIdx.x, nthr = blockDim.x, lane = t & 63, w = t >> 6, nw = nthr >> 6;
+  const int ns = a.ns, nc = a.nc, G = P.G, N = P.N;
+  const uint32_t str = LEVEL_STRIDE * (uint32_t)a.r, it = SWEEP_ITER(a);
+  for (int p = t; p < N; p += nthr) P.Beta[p] = P.mb[p] + P.xi[p];
+  __syncthreads();
+  for (int p = w; p < G * G + G; p += nw) {
+    if (p < G * G) {
+      const int r1 = p % G, r2 = p / G;
+      const int c1 = r1 % nc, t1 = r1 / nc, c2 = r2 % nc, t2 = r2 / nc;
+      const double tq = wave_sum<8>(ns, [&](int j) { return a.Tr[j + (size_t)ns * t1] * P.iQTr[j + (size_t)ns * t2]; });
+      if (lane == 0) P.Pg[p] = a.iUGamma[p] + tq * a.iV[c1 + nc * c2];
+    } else {
+      const int q0 = p - G * G, c = q0 % nc, q = q0 / nc;
+      const double sv = wave_sum<8>(ns, [&](int j) {
+        double ib = 0.0;
+        for (int c2 = 0; c2 < nc; ++c2) ib = fma(a.iV[c + nc * c2], P.Beta[c2 + nc * j], ib);
+        return ib * P.iQTr[j + (size_t)ns * q];
+      });
+      if (lane == 0) P.rg[q0] = sv;
+    }
+  }
+  __syncthreads();
+  if (!wg_chol(P.Pg, G, G, &flag) && t == 0) a.fail[0] = 1;
+  wg_forward(P.Pg, G, G, P.rg);
+  for (int p = t; p < G; p += nthr)
+    if (!a.noise_zero) P.rg[p] += normal(a.key, (uint32_t)p, 0, S_GE_GAMMA + str, it);
+  __syncthreads();
+  wg_backward_t(P.Pg, G, G, P.rg);
+  for (int p = t; p < G; p += nthr) a.Gamma[p] = P.rg[p];
 }
+// Eta | Beta, S (:71-74 / :136-146): one wave per row (np = ny) or unit, lanes over species
 __global__ __launch_bounds__(256) void ge_b_eta_kernel(GEArgs a) {
-  GE_GRID_IDX
-  ge_seg_eta(a, P, g0, gs, SWEEP_ITER(a));
+  GE_WAVE_IDX
+  const int ny = a.ny, ns = a.ns, nc = a.nc, nf = a.nf, np = a.np;
+  const uint32_t str = LEVEL_STRIDE * (uint32_t)a.r, it = SWEEP_ITER(a);
+  const int nrow = P.obs ? ny : np;
+  for (int i = w0; i < nrow; i += ws) {
+    double tv[GE_NF_MAX];
+    for (int h = 0; h < nf; ++h) tv[h] = 0.0;
+    for (int j = lane; j < ns; j += 64) {
+      double s1;
+      if (P.obs) {
+        s1 = P.S[i + (size_t)ny * j];
+        for (int c = 0; c < nc; ++c) s1 -= a.X[i + (size_t)ny * c] * P.Beta[c + nc * j];
+      } else {
+        s1 = P.PtS[i + (size_t)np * j];
+        for (int c = 0; c < nc; ++c) s1 -= P.PtX[i + (size_t)np * c] * P.Beta[c + nc * j];
+      }
+      for (int h = 0; h < nf; ++h) tv[h] = fma(s1, P.LamiD[h + nf * j], tv[h]);
+    }
+    for (int h = 0; h < nf; ++h)
+      for (int o = 32; o > 0; o >>= 1) tv[h] += __shfl_xor(tv[h], o);
+    const int h = lane;
+    if (h < nf) {
+      double me = 0.0, nz = 0.0;
+      if (P.obs) {
+        for (int h2 = 0; h2 < nf; ++h2) me = fma(tv[h2], P.iW0[h2 + nf * h], me);
+        if (!a.noise_zero)
+          for (int h2 = h; h2 < nf; ++h2)  // (RW0^-1 xi)_h = sum_h2 L0i[h2, h] xi_h2
+            nz = fma(P.L0i[h2 + nf * h], normal(a.key, (uint32_t)i, (uint32_t)h2, S_GE_ETA + str, it), nz);
+        a.Eta[a.lev_pi[a.r][i] + (size_t)np * h] = me + nz;
+      } else {
+        const double* iW = P.iWp + (size_t)i * nf * nf;
+        const double* Li = P.Lip + (size_t)i * nf * nf;
+        for (int h2 = 0; h2 < nf; ++h2) me = fma(iW[h + nf * h2], tv[h2], me);
+        if (!a.noise_zero)
+          for (int h2 = h; h2 < nf; ++h2)  // (LiW_p xi)_h = sum_h2 Li[h2, h] xi_h2
+            nz = fma(Li[h2 + nf * h], normal(a.key, (uint32_t)i, (uint32_t)h2, S_GE_ETA + str, it), nz);
+        a.Eta[i + (size_t)np * h] = me + nz;
+      }
+    }
+  }
 }
+#undef GE_WAVE_IDX
 #undef GE_GRID_IDX
 
 static int ge_blocks(size_t elems) { return (int)std::max<size_t>(1, std::min<size_t>(4096, (elems + 255) / 256)); }
@@ -608,11 +731,11 @@ static void launch_gamma_eta_blocked(State& s, const GEArgs& a, hipStream_t st) 
   dense_potrf_lower(st, M, N, N, ws2, a.fail);
   dense_trsv_lower(st, M, N, N, v, 0, ws2);
   dense_trsv_lower(st, M, N, N, v, 1, ws2);
-  ge_b_wv_kernel<<<ge_blocks(N), 256, 0, st>>>(a);
-  ge_b_mb_kernel<<<ge_blocks(N), 256, 0, st>>>(a);
+  ge_b_wv_kernel<<<ge_blocks(64 * (size_t)N), 256, 0, st>>>(a);  // one wave per output
+  ge_b_mb_kernel<<<ge_blocks(64 * (size_t)N), 256, 0, st>>>(a);
   dense_trsv_lower(st, M, N, N, xi, 1, ws2);  // backsolve(RM, rnorm(nc ns))  (:66)
   ge_b_gamma_kernel<<<1, 1024, 0, st>>>(a);
-  ge_b_eta_kernel<<<ge_blocks(obs ? a.ny : a.np), 256, 0, st>>>(a);
+  ge_b_eta_kernel<<<ge_blocks(64 * (size_t)(obs ? a.ny : a.np)), 256, 0, st>>>(a);
   HIP_OK(hipGetLastError());
 }
 
