@@ -639,6 +639,59 @@ __global__ __launch_bounds__(256) void lauum_kernel(const double* M, int ldm, in
   });
 }
 
+// out = U diag(d) U^T (n x n, full symmetric, ld ldo) for U n x n (ld ldu) with
+// d = dbase + n * (*rho - 1) (the phylogeny's spectral grid at the current rho index), or its
+// reciprocal when `recip`: iQ = U diag(1/w) U^T and Q = U diag(w) U^T.  One lower 64 x 64
+// tile per workgroup, MFMA tile products over 64-column chunks of U.
+__global__ __launch_bounds__(256) void gram_diag_kernel(const double* U, int ldu, int n, const double* dbase,
+                                                        const double* rho, int recip, double* out, int ldo) {
+  __shared__ double SA[DB * DLD];
+  __shared__ double SB[DB * DLD];
+  int ti = (int)((sqrt(8.0 * blockIdx.x + 1.0) - 1.0) * 0.5);
+  int tj = (int)blockIdx.x - ti * (ti + 1) / 2;
+  if (tj > ti) ++ti, tj = (int)blockIdx.x - ti * (ti + 1) / 2;
+  if (tj < 0) --ti, tj = (int)blockIdx.x - ti * (ti + 1) / 2;
+  const int I0 = DB * ti, J0 = DB * tj, rowsI = min(DB, n - I0), rowsJ = min(DB, n - J0);
+  const double* d = dbase + (size_t)n * ((int)(*rho) - 1);
+  const int t = threadIdx.x;
+  d4 acc[2][2];
+  zero_acc(acc);
+  for (int K0 = 0; K0 < n; K0 += DB) {
+    const int cols = min(DB, n - K0);
+    double va[DB * DB / 256], vb[DB * DB / 256], dv[DB * DB / 256];
+#pragma unroll
+    for (int u = 0; u < DB * DB / 256; ++u) {
+      const int p = t + 256 * u, r = p & 63, k = p >> 6, kc = min(k, cols - 1);
+      va[u] = U[(size_t)(I0 + min(r, rowsI - 1)) + (size_t)ldu * (K0 + kc)];
+      vb[u] = U[(size_t)(J0 + min(r, rowsJ - 1)) + (size_t)ldu * (K0 + kc)];
+      dv[u] = d[K0 + kc];
+    }
+    if (K0 > 0) __syncthreads();  // the previous chunk's products are done with SA / SB
+#pragma unroll
+    for (int u = 0; u < DB * DB / 256; ++u) {
+      const int p = t + 256 * u, r = p & 63, k = p >> 6;
+      const double dk = recip ? 1.0 / dv[u] : dv[u];
+      SA[r + DLD * k] = (r < rowsI && k < cols) ? va[u] * dk : 0.0;
+      SB[r + DLD * k] = (r < rowsJ && k < cols) ? vb[u] : 0.0;
+    }
+    __syncthreads();
+    tile_mma(acc, SA, SB);
+  }
+  acc_each(acc, [&](int r, int c, double v) {
+    if (r < rowsI && c < rowsJ && (ti != tj || r >= c)) {
+      out[(size_t)(I0 + r) + (size_t)ldo * (J0 + c)] = v;
+      out[(size_t)(J0 + c) + (size_t)ldo * (I0 + r)] = v;
+    }
+  });
+}
+
+void dense_gram_diag(hipStream_t st, const double* U, int ldu, int n, const double* dbase, const double* rho,
+                     bool recip, double* out, int ldo) {
+  const int nbk = (n + DB - 1) / DB;
+  gram_diag_kernel<<<nbk * (nbk + 1) / 2, 256, 0, st>>>(U, ldu, n, dbase, rho, recip ? 1 : 0, out, ldo);
+  HIP_OK(hipGetLastError());
+}
+
 // ---------------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------------

@@ -109,7 +109,7 @@ struct GEPtrs {
   int N, G;
 };
 
-__device__ inline GEPtrs ge_ptrs(const GEArgs& a) {
+__host__ __device__ inline GEPtrs ge_ptrs(const GEArgs& a) {
   GEPtrs P;
   P.obs = (a.np == a.ny);
   P.N = a.nc * a.ns;
@@ -131,7 +131,7 @@ __device__ inline GEPtrs ge_ptrs(const GEArgs& a) {
 // (large nc ns) with the global thread index and grid size from one launch per segment.
 
 // S, X'X (+ a copy of iV), LamiD, Lam D Lam', Q / iQ   (:37-42, :27-31)
-__device__ inline void ge_seg_prep(const GEArgs& a, const GEPtrs& P, int g0, int gs) {
+__device__ inline void ge_seg_prep(const GEArgs& a, const GEPtrs& P, int g0, int gs, bool with_q = true) {
   const int ny = a.ny, ns = a.ns, nc = a.nc, nf = a.nf, K = a.K;
   const double* lam = a.BL + a.loff;  // Lambda_r[h, j] = lam[h + K j]
   for (size_t p = g0; p < (size_t)ny * ns; p += gs) {
@@ -163,6 +163,7 @@ __device__ inline void ge_seg_prep(const GEArgs& a, const GEPtrs& P, int g0, int
     for (int j = 0; j < ns; ++j) s = fma(lam[h1 + (size_t)K * j] * a.iSigma[j], lam[h2 + (size_t)K * j], s);
     P.LDL[p] = s;
   }
+  if (!with_q) return;  // (blocked path: Q / iQ by dense_gram_diag)
   if (a.phU) {
     const double* wq = a.phWinv + (size_t)ns * ((int)(*a.rho) - 1);
     for (int p = g0; p < ns * ns; p += gs) {
@@ -526,14 +527,55 @@ constexpr int GE_WG_MAX = 512;
   const int gs = gridDim.x * blockDim.x;                   \
   (void)P, (void)g0, (void)gs;
 
+// The blocked path's reductions: one wave per output, lanes over the summation index
+// (coalesced where the operand is a column), U terms' loads in flight per lane, a
+// cross-lane sum at the end.  (A thread per output with a serial loop over ns or nc ns
+// terms waited out one L2 round trip per few terms: 0.1-0.3 ms per segment at nc ns = 1200.)
+template <int U, class F>
+__device__ inline double wave_sum(int n, F f) {
+  const int lane = threadIdx.x & 63;
+  double s = 0.0;
+  for (int k0 = lane; k0 < n; k0 += 64 * U) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = k0 + 64 * u < n ? f(k0 + 64 * u) : 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) s += v[u];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  return s;
+}
+
+#define GE_WAVE_IDX                                                      \
+  const GEPtrs P = ge_ptrs(a);                                           \
+  const int lane = threadIdx.x & 63;                                     \
+  const int w0 = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);    \
+  const int ws = (int)((gridDim.x * blockDim.x) >> 6);                   \
+  (void)P, (void)lane;
+
 __global__ __launch_bounds__(256) void ge_b_prep_kernel(GEArgs a) {
   GE_GRID_IDX
-  ge_seg_prep(a, P, g0, gs);
+  ge_seg_prep(a, P, g0, gs, a.phU == nullptr);
 }
 // X'S, iQ Tr; V = iV^-1 and (np = ny) W0 by single threads; (np < ny) the per-unit blocks
 __global__ __launch_bounds__(256) void ge_b_xts_kernel(GEArgs a) {
   GE_GRID_IDX
-  ge_seg_xts(a, P, g0, gs);
+  {  // X'S and iQ Tr, one wave per output (iQ symmetric: read by columns)
+    const int lane = threadIdx.x & 63, w0 = g0 >> 6, ws = gs >> 6;
+    const int ny = a.ny, ns = a.ns, nc = a.nc, N = P.N;
+    for (int p = w0; p < N + ns * a.nt; p += ws) {
+      if (p < N) {
+        const int c = p % nc, j = p / nc;
+        const double s = wave_sum<8>(ny, [&](int i) { return a.X[i + (size_t)ny * c] * P.S[i + (size_t)ny * j]; });
+        if (lane == 0) P.XtS[p] = s;
+      } else {
+        const int q0 = p - N, j = q0 % ns, q = q0 / ns;
+        const double s = wave_sum<8>(ns, [&](int j2) { return P.iQm[j2 + (size_t)ns * j] * a.Tr[j2 + (size_t)ns * q]; });
+        if (lane == 0) P.iQTr[q0] = s;
+      }
+    }
+  }
   const int nc = a.nc;
   if (g0 == 0) {  // V = chol2inv(chol(iV)) = L^-T L^-1, L^-1 in the (not yet used) T block
     if (!t_chol_inv(P.Wv, P.T, nc)) a.fail[0] = 1;
@@ -563,33 +605,6 @@ __global__ __launch_bounds__(256) void ge_b_m_kernel(GEArgs a) {
     ge_seg_m_units(a, P, g0, gs);
   ge_seg_mb10(a, P, g0, gs);
 }
-// The blocked path's reductions: one wave per output, lanes over the summation index
-// (coalesced where the operand is a column), U terms' loads in flight per lane, a
-// cross-lane sum at the end.  (A thread per output with a serial loop over ns or nc ns
-// terms waited out one L2 round trip per few terms: 0.1-0.3 ms per segment at nc ns = 1200.)
-template <int U, class F>
-__device__ inline double wave_sum(int n, F f) {
-  const int lane = threadIdx.x & 63;
-  double s = 0.0;
-  for (int k0 = lane; k0 < n; k0 += 64 * U) {
-    double v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = k0 + 64 * u < n ? f(k0 + 64 * u) : 0.0;
-#pragma unroll
-    for (int u = 0; u < U; ++u) s += v[u];
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  return s;
-}
-
-#define GE_WAVE_IDX                                                      \
-  const GEPtrs P = ge_ptrs(a);                                           \
-  const int lane = threadIdx.x & 63;                                     \
-  const int w0 = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);    \
-  const int ws = (int)((gridDim.x * blockDim.x) >> 6);                   \
-  (void)P, (void)lane;
-
 // with v = M^-1 (mb10 - mb20): wv = mb10 - mb20 - T1 v (mb30, :63-64), xi ~ N(0, I); T1 is
 // symmetric (kron(tmp1, X'X) for np = ny, T otherwise), read by columns
 __global__ __launch_bounds__(256) void ge_b_wv_kernel(GEArgs a) {
@@ -720,7 +735,12 @@ static void launch_gamma_eta_blocked(State& s, const GEArgs& a, hipStream_t st) 
   const size_t NN = (size_t)N * N;
   const size_t big = std::max<size_t>((size_t)a.ny * a.ns, (size_t)a.ns * a.ns);
   ge_b_prep_kernel<<<ge_blocks(big), 256, 0, st>>>(a);
-  ge_b_xts_kernel<<<ge_blocks(std::max<size_t>(std::max(N, a.ns * a.nt), obs ? 128 : a.np)), 256, 0, st>>>(a);
+  if (a.phU) {  // Q = U diag(w) U^T, iQ = U diag(1/w) U^T on the matrix cores
+    const GEPtrs hp = ge_ptrs(a);
+    dense_gram_diag(st, a.phU, a.ns, a.ns, a.phWinv, a.rho, true, hp.Qm, a.ns);
+    dense_gram_diag(st, a.phU, a.ns, a.ns, a.phWinv, a.rho, false, hp.iQm, a.ns);
+  }
+  ge_b_xts_kernel<<<ge_blocks(std::max<size_t>(64 * ((size_t)N + a.ns * a.nt), obs ? 128 : a.np)), 256, 0, st>>>(a);
   ge_b_a_kernel<<<ge_blocks(NN), 256, 0, st>>>(a);
   // iA = chol2inv(chol(A)) = L^-T L^-1   (:33)
   dense_potrf_lower(st, L, N, N, ws1, a.fail);

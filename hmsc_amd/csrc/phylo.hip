@@ -231,14 +231,10 @@ __global__ __launch_bounds__(256) void ph_prep_kernel(PhyloArgs a) {
   double* Y = rhs + (size_t)a.K * ns;
   double* tau = Y + (size_t)nc * ns;
   const double* w = a.Winv + (size_t)ns * rho_index(a.rho);
+  (void)iQ, (void)w;  // iQ = U diag(w) U^T: dense_gram_diag (MFMA tiles)
   const size_t p = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (p < (size_t)ns * ns) {
-    const int j1 = (int)(p % ns), j2 = (int)(p / ns);
-    double s = 0.0;
-    for (int i = 0; i < ns; ++i) s = fma(a.U[j1 + (size_t)ns * i] * w[i], a.U[j2 + (size_t)ns * i], s);
-    iQ[p] = s;
-  } else if (p < (size_t)ns * ns + (size_t)nc * ns) {
-    const int q = (int)(p - (size_t)ns * ns), c = q % nc, j = q / nc;
+  if (p < (size_t)nc * ns) {
+    const int q = (int)p, c = q % nc, j = q / nc;
     double s = 0.0;
     for (int c2 = 0; c2 < nc; ++c2) {
       double mu = 0.0;
@@ -387,7 +383,8 @@ void launch_beta_lambda_phylo(State& s, uint32_t iter) {
   double* rhs = M + (size_t)N * N + ns2;
   double* ws = rhs + N + (size_t)s.nc * s.ns + s.Kmax;
   const int g1 = (N + 255) / 256;
-  ph_prep_kernel<<<(unsigned)((ns2 + (size_t)s.nc * s.ns + 255) / 256), 256, 0, s.stream>>>(a);
+  dense_gram_diag(s.stream, s.phU, s.ns, s.ns, s.phWinv, s.rho, false, M + (size_t)N * N, s.ns);  // iQ
+  ph_prep_kernel<<<(unsigned)(((size_t)s.nc * s.ns + 255) / 256), 256, 0, s.stream>>>(a);
   ph_assemble_kernel<<<dim3(g1, N), 256, 0, s.stream>>>(a);
   ph_rhs_kernel<<<g1, 256, 0, s.stream>>>(a);
   HIP_OK(hipGetLastError());

@@ -283,6 +283,9 @@ void dense_trtri_lower(hipStream_t st, const double* L, int ldl, int n, double* 
 // workspace of dense_potrf_lower + dense_trsv_lower: the 64 x 64 diagonal-block inverses, then n
 inline size_t dense_ws_doubles(int n) { return (size_t)((n + 63) / 64) * 64 * 64 + (size_t)n + 64; }
 void dense_lauum_lower(hipStream_t st, const double* M, int ldm, int n, double* out, int ldo);
+// out = U diag(d) U^T (full symmetric), d = dbase + n (*rho - 1) or its reciprocal
+void dense_gram_diag(hipStream_t st, const double* U, int ldu, int n, const double* dbase, const double* rho,
+                     bool recip, double* out, int ldo);
 // the 'Full' alphapw grid on the device (R/computeDataParameters.R:53-81) from coordinates
 // (np x sdim, column-major) or a distance matrix (np x np): RiWg = chol(W_g)^-1 (lower),
 // iWg = RiWg^T RiWg, detWg = log det W_g
