@@ -623,11 +623,28 @@ __global__ __launch_bounds__(256) void lauum_kernel(const double* M, int ldm, in
   const int rowsI = min(DB, n - I0), rowsJ = min(DB, n - J0);
   d4 acc[2][2];
   zero_acc(acc);
-  for (int k = ti; k < nbk; ++k) {
+  // chunk k's loads are issued during chunk k - 1's MFMAs (registers), stored after its barrier
+  double va[DB * DB / 256], vb[DB * DB / 256];
+  auto load = [&](int k) {
     const int K0 = DB * k, rowsK = min(DB, n - K0);
-    stage_t(SA, M, ldm, K0, I0, rowsK, rowsI);
-    stage_t(SB, M, ldm, K0, J0, rowsK, rowsJ);
+#pragma unroll
+    for (int u = 0; u < DB * DB / 256; ++u) {
+      const int p = threadIdx.x + 256 * u, kk = p & 63, c = p >> 6;
+      va[u] = M[(size_t)(K0 + min(kk, rowsK - 1)) + (size_t)ldm * (I0 + min(c, rowsI - 1))];
+      vb[u] = M[(size_t)(K0 + min(kk, rowsK - 1)) + (size_t)ldm * (J0 + min(c, rowsJ - 1))];
+    }
+  };
+  load(ti);
+  for (int k = ti; k < nbk; ++k) {
+    const int rowsK = min(DB, n - DB * k);
+#pragma unroll
+    for (int u = 0; u < DB * DB / 256; ++u) {  // stage_t layout: S[c][k] = M[K0 + k, C0 + c]
+      const int p = threadIdx.x + 256 * u, kk = p & 63, c = p >> 6;
+      SA[c + DLD * kk] = (kk < rowsK && c < rowsI) ? va[u] : 0.0;
+      SB[c + DLD * kk] = (kk < rowsK && c < rowsJ) ? vb[u] : 0.0;
+    }
     __syncthreads();
+    if (k + 1 < nbk) load(k + 1);
     tile_mma(acc, SA, SB);
     __syncthreads();
   }
@@ -656,9 +673,9 @@ __global__ __launch_bounds__(256) void gram_diag_kernel(const double* U, int ldu
   const int t = threadIdx.x;
   d4 acc[2][2];
   zero_acc(acc);
-  for (int K0 = 0; K0 < n; K0 += DB) {
+  double va[DB * DB / 256], vb[DB * DB / 256], dv[DB * DB / 256];
+  auto load = [&](int K0) {  // chunk K0's loads, issued during the previous chunk's MFMAs
     const int cols = min(DB, n - K0);
-    double va[DB * DB / 256], vb[DB * DB / 256], dv[DB * DB / 256];
 #pragma unroll
     for (int u = 0; u < DB * DB / 256; ++u) {
       const int p = t + 256 * u, r = p & 63, k = p >> 6, kc = min(k, cols - 1);
@@ -666,6 +683,10 @@ __global__ __launch_bounds__(256) void gram_diag_kernel(const double* U, int ldu
       vb[u] = U[(size_t)(J0 + min(r, rowsJ - 1)) + (size_t)ldu * (K0 + kc)];
       dv[u] = d[K0 + kc];
     }
+  };
+  load(0);
+  for (int K0 = 0; K0 < n; K0 += DB) {
+    const int cols = min(DB, n - K0);
     if (K0 > 0) __syncthreads();  // the previous chunk's products are done with SA / SB
 #pragma unroll
     for (int u = 0; u < DB * DB / 256; ++u) {
@@ -675,6 +696,7 @@ __global__ __launch_bounds__(256) void gram_diag_kernel(const double* U, int ldu
       SB[r + DLD * k] = (r < rowsJ && k < cols) ? vb[u] : 0.0;
     }
     __syncthreads();
+    if (K0 + DB < n) load(K0 + DB);
     tile_mma(acc, SA, SB);
   }
   acc_each(acc, [&](int r, int c, double v) {

@@ -17,6 +17,8 @@
 //   |RQ_g^-T E RiV^T|^2 = sum_i w_g,i Et_i^T iV Et_i          (updateRho's v_g)
 // with w = 1 / q_rho: the 101 backsolves become one weighted sum per grid point.  Only the
 // dense BetaLambda system needs iQ itself, assembled from U and w inside that kernel.
+#include <algorithm>
+
 #include "common.h"
 #include "state.h"
 
@@ -272,18 +274,24 @@ __global__ __launch_bounds__(256) void ph_assemble_kernel(PhyloArgs a) {
   M[r + (size_t)N * c] = v;
 }
 
+// rhs = vec(iSigma XZ) + (P Mu) rows: one wave per output (the nc ns P Mu entries are
+// ns-term sums over iQ's column j, lanes over j2)
 __global__ __launch_bounds__(256) void ph_rhs_kernel(PhyloArgs a) {
   const int ns = a.ns, nc = a.nc, K = a.K, N = K * ns;
   const double* iQ = a.work + (size_t)N * N;
   double* rhs = (double*)iQ + (size_t)ns * ns;
   const double* Y = rhs + N;
-  const int r = blockIdx.x * 256 + threadIdx.x;
-  if (r >= N) return;
-  const int k = r / ns, j = r % ns;
-  double v = a.iSigma[j] * a.XZ[k + (size_t)K * j];
-  if (k < nc)
-    for (int j2 = 0; j2 < ns; ++j2) v = fma(Y[k + nc * j2], iQ[j2 + (size_t)ns * j], v);
-  rhs[r] = v;
+  const int lane = threadIdx.x & 63;
+  const int w0 = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6), ws = (int)((gridDim.x * blockDim.x) >> 6);
+  for (int r = w0; r < N; r += ws) {
+    const int k = r / ns, j = r % ns;
+    double pm = 0.0;
+    if (k < nc) {
+      for (int j2 = lane; j2 < ns; j2 += 64) pm = fma(Y[k + nc * j2], iQ[j2 + (size_t)ns * j], pm);
+      for (int o = 32; o > 0; o >>= 1) pm += __shfl_xor(pm, o);
+    }
+    if (lane == 0) rhs[r] = a.iSigma[j] * a.XZ[k + (size_t)K * j] + pm;
+  }
 }
 
 __global__ __launch_bounds__(256) void ph_noise_kernel(PhyloArgs a) {
@@ -386,7 +394,7 @@ void launch_beta_lambda_phylo(State& s, uint32_t iter) {
   dense_gram_diag(s.stream, s.phU, s.ns, s.ns, s.phWinv, s.rho, false, M + (size_t)N * N, s.ns);  // iQ
   ph_prep_kernel<<<(unsigned)(((size_t)s.nc * s.ns + 255) / 256), 256, 0, s.stream>>>(a);
   ph_assemble_kernel<<<dim3(g1, N), 256, 0, s.stream>>>(a);
-  ph_rhs_kernel<<<g1, 256, 0, s.stream>>>(a);
+  ph_rhs_kernel<<<(unsigned)std::min<size_t>(4096, ((size_t)N * 64 + 255) / 256), 256, 0, s.stream>>>(a);
   HIP_OK(hipGetLastError());
   dense_potrf_lower(s.stream, M, N, N, ws, s.dev_flags + 2);
   dense_trsv_lower(s.stream, M, N, N, rhs, 0, ws);   // m1 = backsolve(RiU, ., transpose=TRUE)  (:145)
