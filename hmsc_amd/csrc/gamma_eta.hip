@@ -131,7 +131,8 @@ __host__ __device__ inline GEPtrs ge_ptrs(const GEArgs& a) {
 // (large nc ns) with the global thread index and grid size from one launch per segment.
 
 // S, X'X (+ a copy of iV), LamiD, Lam D Lam', Q / iQ   (:37-42, :27-31)
-__device__ inline void ge_seg_prep(const GEArgs& a, const GEPtrs& P, int g0, int gs, bool with_q = true) {
+__device__ inline void ge_seg_prep(const GEArgs& a, const GEPtrs& P, int g0, int gs, bool with_q = true,
+                                   bool with_sums = true) {
   const int ny = a.ny, ns = a.ns, nc = a.nc, nf = a.nf, K = a.K;
   const double* lam = a.BL + a.loff;  // Lambda_r[h, j] = lam[h + K j]
   for (size_t p = g0; p < (size_t)ny * ns; p += gs) {
@@ -148,21 +149,24 @@ __device__ inline void ge_seg_prep(const GEArgs& a, const GEPtrs& P, int g0, int
   }
   for (int p = g0; p < nc * nc; p += gs) {
     const int c1 = p % nc, c2 = p / nc;
-    double s = 0.0;
-    for (int i = 0; i < ny; ++i) s = fma(a.X[i + (size_t)ny * c1], a.X[i + (size_t)ny * c2], s);
-    P.XtX[p] = s;
+    if (with_sums) {
+      double s = 0.0;
+      for (int i = 0; i < ny; ++i) s = fma(a.X[i + (size_t)ny * c1], a.X[i + (size_t)ny * c2], s);
+      P.XtX[p] = s;
+    }
     P.Wv[p] = a.iV[p];
   }
   for (int p = g0; p < nf * ns; p += gs) {
     const int h = p % nf, j = p / nf;
     P.LamiD[p] = lam[h + (size_t)K * j] * a.iSigma[j];
   }
-  for (int p = g0; p < nf * nf; p += gs) {
-    const int h1 = p % nf, h2 = p / nf;
-    double s = 0.0;
-    for (int j = 0; j < ns; ++j) s = fma(lam[h1 + (size_t)K * j] * a.iSigma[j], lam[h2 + (size_t)K * j], s);
-    P.LDL[p] = s;
-  }
+  if (with_sums)
+    for (int p = g0; p < nf * nf; p += gs) {
+      const int h1 = p % nf, h2 = p / nf;
+      double s = 0.0;
+      for (int j = 0; j < ns; ++j) s = fma(lam[h1 + (size_t)K * j] * a.iSigma[j], lam[h2 + (size_t)K * j], s);
+      P.LDL[p] = s;
+    }
   if (!with_q) return;  // (blocked path: Q / iQ by dense_gram_diag)
   if (a.phU) {
     const double* wq = a.phWinv + (size_t)ns * ((int)(*a.rho) - 1);
@@ -556,7 +560,22 @@ __device__ inline double wave_sum(int n, F f) {
 
 __global__ __launch_bounds__(256) void ge_b_prep_kernel(GEArgs a) {
   GE_GRID_IDX
-  ge_seg_prep(a, P, g0, gs, a.phU == nullptr);
+  ge_seg_prep(a, P, g0, gs, a.phU == nullptr, false);
+  // X'X and Lam D Lam', one wave per entry
+  const int lane = threadIdx.x & 63, w0 = g0 >> 6, ws = gs >> 6;
+  const int ny = a.ny, ns = a.ns, nc = a.nc, nf = a.nf, K = a.K;
+  const double* lam = a.BL + a.loff;
+  for (int p = w0; p < nc * nc + nf * nf; p += ws) {
+    if (p < nc * nc) {
+      const int c1 = p % nc, c2 = p / nc;
+      const double s = wave_sum<8>(ny, [&](int i) { return a.X[i + (size_t)ny * c1] * a.X[i + (size_t)ny * c2]; });
+      if (lane == 0) P.XtX[p] = s;
+    } else {
+      const int q = p - nc * nc, h1 = q % nf, h2 = q / nf;
+      const double s = wave_sum<8>(ns, [&](int j) { return lam[h1 + (size_t)K * j] * a.iSigma[j] * lam[h2 + (size_t)K * j]; });
+      if (lane == 0) P.LDL[q] = s;
+    }
+  }
 }
 // X'S, iQ Tr; V = iV^-1 and (np = ny) W0 by single threads; (np < ny) the per-unit blocks
 __global__ __launch_bounds__(256) void ge_b_xts_kernel(GEArgs a) {
@@ -599,11 +618,35 @@ __global__ __launch_bounds__(256) void ge_b_a_kernel(GEArgs a) {
 }
 __global__ __launch_bounds__(256) void ge_b_m_kernel(GEArgs a) {
   GE_GRID_IDX
-  if (P.obs)
-    ge_seg_m_obs(a, P, g0, gs);
-  else
+  if (!P.obs) {
     ge_seg_m_units(a, P, g0, gs);
-  ge_seg_mb10(a, P, g0, gs);
+    ge_seg_mb10(a, P, g0, gs);
+    return;
+  }
+  // np = ny: M += kron(tmp1, X'X) elementwise; mb20, mb10 and v one wave per entry   (:58-62)
+  const int ns = a.ns, nc = a.nc, nf = a.nf, N = P.N;
+  for (size_t p = g0; p < (size_t)N * N; p += gs) {
+    const int r1 = (int)(p % N), r2 = (int)(p / N);
+    P.M[p] += P.tmp1[(r1 / nc) + (size_t)ns * (r2 / nc)] * P.XtX[(r1 % nc) + nc * (r2 % nc)];
+  }
+  const int lane = threadIdx.x & 63, w0 = g0 >> 6, ws = gs >> 6;
+  for (int p = w0; p < N; p += ws) {
+    const int c = p % nc, j = p / nc;
+    double x1[GE_NF_MAX];
+    for (int h1 = 0; h1 < nf; ++h1)
+      x1[h1] = wave_sum<8>(ns, [&](int j2) { return P.XtS[c + nc * j2] * P.LamiD[h1 + nf * j2]; });
+    if (lane == 0) {
+      double s = 0.0;
+      for (int h2 = 0; h2 < nf; ++h2) {
+        double u = 0.0;
+        for (int h1 = 0; h1 < nf; ++h1) u = fma(x1[h1], P.iW0[h1 + nf * h2], u);
+        s = fma(u, P.LamiD[h2 + nf * j], s);
+      }
+      P.mb20[p] = s;
+      P.mb10[p] = P.XtS[p] * a.iSigma[j];
+      P.v[p] = P.mb10[p] - s;
+    }
+  }
 }
 // with v = M^-1 (mb10 - mb20): wv = mb10 - mb20 - T1 v (mb30, :63-64), xi ~ N(0, I); T1 is
 // symmetric (kron(tmp1, X'X) for np = ny, T otherwise), read by columns
