@@ -80,31 +80,38 @@ __device__ inline void phylo_et(const PhyloArgs& a) {
 
 // updateGammaV's iQ-weighted sums (R/updateGammaV.R:16-18,29-30) in the eigenbasis; the
 // Wishart / Gamma algebra that follows is the shared gammav kernel with nparts = 1, TT = TTw.
-__global__ __launch_bounds__(256) void phylo_gv_kernel(PhyloArgs a) {
+__global__ __launch_bounds__(1024) void phylo_gv_kernel(PhyloArgs a) {
   phylo_et(a);
   const double* w = a.Winv + (size_t)a.ns * rho_index(a.rho);
   const int nc = a.nc, nt = a.nt, ns = a.ns, nA = nc * nc, nB = nc * nt;
-  for (int p = threadIdx.x; p < nA + nB + nt * nt; p += blockDim.x) {
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  // one wave per output, lanes over species (a thread per output waited out ns dependent
+  // L2 round trips)
+  for (int p = threadIdx.x >> 6; p < nA + nB + nt * nt; p += nw) {
     double s = 0.0;
     if (p < nA) {  // A = E iQ E^T
       const int c1 = p % nc, c2 = p / nc;
-      for (int i = 0; i < ns; ++i) s = fma(w[i] * a.Et[c1 + nc * i], a.Et[c2 + nc * i], s);
-      a.part[p] = s;
+      for (int i = lane; i < ns; i += 64) s = fma(w[i] * a.Et[c1 + nc * i], a.Et[c2 + nc * i], s);
     } else if (p < nA + nB) {  // B iQ Tr
       const int q = p - nA, c = q % nc, t = q / nc;
-      for (int i = 0; i < ns; ++i) s = fma(w[i] * a.Bt[c + nc * i], a.Tt[i + (size_t)ns * t], s);
-      a.part[p] = s;
+      for (int i = lane; i < ns; i += 64) s = fma(w[i] * a.Bt[c + nc * i], a.Tt[i + (size_t)ns * t], s);
     } else {  // Tr^T iQ Tr = crossprod(backsolve(RQ, Tr, transpose=TRUE))
       const int q = p - nA - nB, t1 = q % nt, t2 = q / nt;
-      for (int i = 0; i < ns; ++i) s = fma(w[i] * a.Tt[i + (size_t)ns * t1], a.Tt[i + (size_t)ns * t2], s);
-      a.TTw[q] = s;
+      for (int i = lane; i < ns; i += 64) s = fma(w[i] * a.Tt[i + (size_t)ns * t1], a.Tt[i + (size_t)ns * t2], s);
+    }
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) {
+      if (p < nA + nB)
+        a.part[p] = s;
+      else
+        a.TTw[p - nA - nB] = s;
     }
   }
 }
 
 // updateRho (R/updateRho.R:1-25) given the new Gamma and iV: v_g = sum_i w_g,i Et_i^T iV Et_i,
 // logLike_g = log(rhopw[g,2]) - nc/2 logdet Q_g - v_g/2, one categorical draw by inversion.
-__global__ __launch_bounds__(256) void phylo_rho_kernel(PhyloArgs a) {
+__global__ __launch_bounds__(1024) void phylo_rho_kernel(PhyloArgs a) {
   phylo_et(a);
   const int nc = a.nc, ns = a.ns;
   double* sq = a.work;  // ns quadratic forms
@@ -119,12 +126,16 @@ __global__ __launch_bounds__(256) void phylo_rho_kernel(PhyloArgs a) {
     sq[i] = s;
   }
   __syncthreads();
-  double* ll = a.work + ns;  // nrho log-likelihoods
-  for (int g = threadIdx.x; g < a.nrho; g += blockDim.x) {
-    const double* w = a.Winv + (size_t)ns * g;
-    double v = 0.0;
-    for (int i = 0; i < ns; ++i) v = fma(w[i], sq[i], v);
-    ll[g] = a.rbase[g] - 0.5 * v;
+  double* ll = a.work + ns;  // nrho log-likelihoods: one wave per grid point, lanes over species
+  {
+    const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    for (int g = threadIdx.x >> 6; g < a.nrho; g += nw) {
+      const double* w = a.Winv + (size_t)ns * g;
+      double v = 0.0;
+      for (int i = lane; i < ns; i += 64) v = fma(w[i], sq[i], v);
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      if (lane == 0) ll[g] = a.rbase[g] - 0.5 * v;
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -363,7 +374,7 @@ void launch_phylo_gv_sums(State& s, uint32_t iter, hipStream_t st) {
   PhyloArgs a = phylo_args(s, iter);
   phylo_bt_kernel<<<(s.nc * s.ns + 255) / 256, 256, 0, st>>>(a);
   HIP_OK(hipGetLastError());
-  phylo_gv_kernel<<<1, 256, 0, st>>>(a);
+  phylo_gv_kernel<<<1, 1024, 0, st>>>(a);
   HIP_OK(hipGetLastError());
 }
 
@@ -372,7 +383,7 @@ void launch_rho(State& s, uint32_t iter, hipStream_t st) {
   PhyloArgs a = phylo_args(s, iter);
   phylo_bt_kernel<<<(s.nc * s.ns + 255) / 256, 256, 0, st>>>(a);  // Beta may have changed since GammaV
   HIP_OK(hipGetLastError());
-  phylo_rho_kernel<<<1, 256, 0, st>>>(a);
+  phylo_rho_kernel<<<1, 1024, 0, st>>>(a);
   HIP_OK(hipGetLastError());
 }
 
