@@ -20,6 +20,7 @@
 // + LEVEL_STRIDE r.
 #include "common.h"
 #include "state.h"
+#include "wave_la.h"
 
 namespace hmsc {
 
@@ -707,6 +708,22 @@ __global__ __launch_bounds__(1024) void ge_b_gamma_kernel(GEArgs a) {
     }
   }
   __syncthreads();
+  if (G <= 16) {  // the G x G solve in one wave's registers (wave_la.h) instead of wg_chol's
+    __shared__ __attribute__((aligned(16))) double tile[WV_TILE];  // per-column barriers
+    if (w == 0) {
+      double x[16], y[16], dinv;
+      wv_load<16>(P.Pg, G, G, x);
+      double r = lane < G ? P.rg[lane] : 0.0;
+      const bool ok = wv_chol<16>(x, dinv);
+      wv_forward<16>(x, dinv, r);
+      if (lane < G && !a.noise_zero) r += normal(a.key, (uint32_t)lane, 0, S_GE_GAMMA + str, it);
+      wv_transpose<16, true>(x, y, tile);
+      wv_backward_t<16>(y, dinv, r);
+      if (lane < G) a.Gamma[lane] = r;
+      if (!ok && lane == 0) a.fail[0] = 1;
+    }
+    return;
+  }
   if (!wg_chol(P.Pg, G, G, &flag) && t == 0) a.fail[0] = 1;
   wg_forward(P.Pg, G, G, P.rg);
   for (int p = t; p < G; p += nthr)
