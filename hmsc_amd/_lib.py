@@ -69,7 +69,8 @@ EXPORTS = ["hmsc_last_error", "hmsc_device_count", "hmsc_create", "hmsc_create_s
            "hmsc_shard_range", "hmsc_create_sharded_host", "hmsc_dense_chol_solve", "hmsc_spatial_full_grid",
            "hmsc_destroy", "hmsc_init_state", "hmsc_init_z", "hmsc_set_state", "hmsc_get_state", "hmsc_get_nf", "hmsc_sweep",
            "hmsc_update", "hmsc_set_noise_mode", "hmsc_run", "hmsc_run_verbose", "hmsc_sync", "hmsc_debug_get",
-           "hmsc_profile", "hmsc_profile_get", "hmsc_kernel_timing", "hmsc_kernel_timing_get", "hmsc_predict"]
+           "hmsc_profile", "hmsc_profile_get", "hmsc_kernel_timing", "hmsc_kernel_timing_get", "hmsc_predict",
+           "hmsc_prepare_graphs"]
 
 
 def lib():
@@ -112,6 +113,7 @@ def lib():
     L.hmsc_kernel_timing.argtypes = [C.c_void_p, C.c_int32]
     L.hmsc_kernel_timing_get.argtypes = [C.c_void_p, C.c_int32, dp, ip]
     L.hmsc_predict.argtypes = [C.POINTER(hmsc_predict_args), dp]
+    L.hmsc_prepare_graphs.argtypes = [C.c_void_p, C.c_int32, ip]
     _lib = L
     return L
 

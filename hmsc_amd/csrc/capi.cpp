@@ -3,8 +3,14 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <ucontext.h>
+
 #include <algorithm>
 #include <cmath>
+#include <csignal>
 #include <cstdio>
 #include <atomic>
 #include <cstring>
@@ -27,6 +33,56 @@ struct hmsc_state {
   hmsc::State s;
 };
 
+// ---------------------------- fault diagnostics ----------------------------
+// HMSC_SEGV_DIAG=1: on SIGSEGV / SIGBUS print the faulting address and PC, every frame with
+// the shared object (and symbol) it lies in, and the /proc/self/maps entries near the
+// faulting address, then re-raise.  Stripped runtimes print as "(unknown)" in glog's handler
+// (which rocprofv3 installs); this one names the library of each frame.  Diagnostic only.
+namespace {
+void fault_diag(int sig, siginfo_t* si, void* ctx) {
+  const ucontext_t* uc = static_cast<const ucontext_t*>(ctx);
+  void* pc = uc ? (void*)uc->uc_mcontext.gregs[REG_RIP] : nullptr;
+  std::fprintf(stderr, "[hmsc] signal %d: fault address %p, pc %p\n", sig, si ? si->si_addr : nullptr, pc);
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  for (int i = -1; i < n; ++i) {
+    void* a = i < 0 ? pc : fr[i];
+    Dl_info d{};
+    if (a && dladdr(a, &d) && d.dli_fname)
+      std::fprintf(stderr, "[hmsc]   #%d %p %s+0x%lx %s+0x%lx\n", i, a, d.dli_fname,
+                   (unsigned long)((char*)a - (char*)d.dli_fbase), d.dli_sname ? d.dli_sname : "?",
+                   d.dli_saddr ? (unsigned long)((char*)a - (char*)d.dli_saddr) : 0ul);
+    else
+      std::fprintf(stderr, "[hmsc]   #%d %p ?\n", i, a);
+  }
+  if (FILE* f = std::fopen("/proc/self/maps", "r")) {
+    const uintptr_t fa = si ? (uintptr_t)si->si_addr : 0;
+    char line[512];
+    while (std::fgets(line, sizeof(line), f)) {
+      unsigned long lo = 0, hi = 0;
+      if (std::sscanf(line, "%lx-%lx", &lo, &hi) == 2 && hi + (64ul << 20) >= fa && lo <= fa + (64ul << 20))
+        std::fprintf(stderr, "[hmsc]   map %s", line);
+    }
+    std::fclose(f);
+  }
+  std::fflush(stderr);
+  std::signal(sig, SIG_DFL);
+  std::raise(sig);
+}
+struct FaultDiagInstaller {
+  FaultDiagInstaller() {
+    const char* e = std::getenv("HMSC_SEGV_DIAG");
+    if (!e || e[0] != '1') return;
+    struct sigaction sa;
+    std::memset(&sa, 0, sizeof(sa));
+    sa.sa_sigaction = fault_diag;
+    sa.sa_flags = SA_SIGINFO;
+    sigaction(SIGSEGV, &sa, nullptr);
+    sigaction(SIGBUS, &sa, nullptr);
+  }
+} g_fault_diag;
+}  // namespace
+
 namespace hmsc {
 
 static thread_local std::string g_last_error;
@@ -36,6 +92,13 @@ static thread_local std::string g_last_error;
 // chain construction / destruction and every other allocation take this lock.
 static std::recursive_mutex g_dev_mu;
 static constexpr int RING_SLOTS = 32;  // recorded samples in flight between device and host
+// Kernel nodes per sweep graph.  rocprofv3 (rocprofiler-sdk, ROCm 7.2) faults inside its
+// queue interception -- reading past the end of a 1 MB host-mapped buffer, called from
+// hipGraphLaunch -> libhsa-runtime64 -> librocprofiler-sdk -- when a graph of thousands of
+// kernel nodes is launched (config 3: 8 sweeps x ~500 launches of the blocked
+// factorizations; gpurun_out/c3prof.err, s1_phy.err with HMSC_SEGV_DIAG=1).  Graphs are
+// kept to this many nodes; sweeps that need more run eagerly.
+static constexpr size_t GRAPH_MAX_NODES = 512;
 
 static int fail(int code, const std::string& msg) {
   g_last_error = msg;
@@ -354,6 +417,9 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
       L.alphapw = dupload(m->alphapw[r], 2 * G);
       if (m->spatialMethod[r] == 3 && !m->iWg[r]) {  // GPP in R's low-rank form
         const size_t nK = (size_t)m->nKnots[r];
+        // gpp_alpha_kernel / launch_eta_gpp stage one knot vector in a 1024-entry LDS array
+        // (spatial.hip); refuse larger knot sets here, before any updater can run
+        HMSC_REQUIRE(nK <= 1024, "GPP level: at most 1024 knots in this build");
         L.gpp = true;
         L.nK = (int)nK;
         L.idDg = dupload(m->idDg[r], (size_t)L.np * G);
@@ -991,7 +1057,7 @@ static void destroy_graph(State& s) {
 // Captures graph_sweeps sweeps (with or without the record pack after each).  Returns
 // nullptr when the sweep is not in a steady state, i.e. the host-side validity flags it
 // changes would differ on the next sweep.
-static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record) {
+static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, size_t* n_nodes = nullptr) {
   std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
   join_side(s);
   const bool xv = s.xeta_valid, zv = s.zt_valid, gv = s.g2prep_valid, gp = s.g_pending;
@@ -1021,16 +1087,31 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record) 
   HIP_OK(hipStreamEndCapture(s.stream, &g));
   const bool steady = xv == s.xeta_valid && zv == s.zt_valid && gv == s.g2prep_valid && gp == s.g_pending;
   s.xeta_valid = xv, s.zt_valid = zv, s.g2prep_valid = gv, s.g_pending = gp;  // nothing ran yet
+  size_t nodes = 0;
+  HIP_OK(hipGraphGetNodes(g, nullptr, &nodes));
+  if (n_nodes) *n_nodes = nodes;
   hipGraphExec_t ge = nullptr;
-  if (steady) HIP_OK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  if (steady && nodes <= GRAPH_MAX_NODES) HIP_OK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
   HIP_OK(hipGraphDestroy(g));
   return ge;
 }
 
 static bool build_sweep_graphs(State& s, uint32_t iter) {
   destroy_graph(s);
-  s.gexec = capture_sweeps(s, iter, false);
-  if (!s.gexec) return false;
+  size_t nodes = 0;
+  s.gexec = capture_sweeps(s, iter, false, &nodes);
+  if (!s.gexec && nodes > GRAPH_MAX_NODES && s.graph_sweeps > 1) {
+    // a sweep with many launches (dense phylogeny / spatial factorizations): fewer sweeps
+    // per graph, or none when one sweep alone exceeds the cap (its launch overhead is hidden
+    // behind milliseconds of device work anyway)
+    const size_t per_sweep = (nodes + s.graph_sweeps - 1) / s.graph_sweeps;
+    s.graph_sweeps = (int)std::max<size_t>(1, GRAPH_MAX_NODES / (per_sweep + 4));  // + the record pack
+    s.gexec = capture_sweeps(s, iter, false, &nodes);
+  }
+  if (!s.gexec) {
+    if (nodes > GRAPH_MAX_NODES) s.use_graph = false;  // eager from here on
+    return false;
+  }
   s.gexec_rec = capture_sweeps(s, iter, true);
   if (!s.gexec_rec) {
     destroy_graph(s);
@@ -1056,6 +1137,11 @@ static bool replay_sweeps(State& s, uint32_t iter, bool with_record) {
 }
 
 static void eager_sweep(State& s, uint32_t iter, bool adapt) {
+  if (s.graph_dirty) {  // state changed under the graphs: they are rebuilt after this sweep
+    destroy_graph(s);
+    s.graph_dirty = false;
+    s.eager_streak = 0;
+  }
   sweep(s, iter, adapt);
   s.eager_streak = adapt ? 0 : s.eager_streak + 1;
 }
@@ -1514,6 +1600,26 @@ int hmsc_run(hmsc_state* h, int32_t transient, int32_t samples, int32_t thin, co
 int hmsc_run_verbose(hmsc_state* h, int32_t transient, int32_t samples, int32_t thin, const int32_t* adaptNf,
                      int32_t iter0, int32_t verbose, int32_t chain, hmsc_record* rec) {
   return guarded([&] { run(h->s, transient, samples, thin, adaptNf, iter0, verbose, chain, rec); });
+}
+
+int hmsc_prepare_graphs(hmsc_state* h, int32_t iter, int32_t* built) {
+  return guarded([&] {
+    HMSC_REQUIRE(built != nullptr, "hmsc_prepare_graphs: built is NULL");
+    State& s = h->s;
+    DeviceGuard dg(s.device);
+    *built = 0;
+    if (!s.use_graph || s.nranks != 1 || s.prof) return;
+    if (s.gexec && (s.graph_dirty || s.graph_K != s.K || s.graph_NF != s.NF)) destroy_graph(s);
+    if (!s.gexec) {
+      if (s.graph_dirty) s.eager_streak = 0, s.graph_dirty = false;
+      if (s.eager_streak < 1 || !build_sweep_graphs(s, (uint32_t)iter)) return;
+    }
+    // make the executable graphs device-resident now, not at their first launch
+    HIP_OK(hipGraphUpload(s.gexec, s.stream));
+    HIP_OK(hipGraphUpload(s.gexec_rec, s.stream));
+    HIP_OK(hipStreamSynchronize(s.stream));
+    *built = 1;
+  });
 }
 
 int hmsc_sync(hmsc_state* h) {

@@ -610,6 +610,7 @@ void launch_alpha(State& s, uint32_t iter) {
     const SpArgs a = sp_args(s, r, iter);
     ProfScope ps(s, PROF_ALPHA);
     if (L.gpp) {
+      HMSC_REQUIRE(L.nK <= 1024, "GPP level: at most 1024 knots in this build");  // t2[1024] in LDS
       const GppLayout o = gpp_layout(L.np, std::max(1, std::min(L.nfmax, s.NFmax)), L.nK, L.nalpha);
       SpArgs b = a;
       b.work = L.spWork + o.alpha;

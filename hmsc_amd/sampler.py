@@ -274,6 +274,13 @@ class Chain:
     def sync(self):
         L.check(self.lib.hmsc_sync(self.h))
 
+    def prepare_graphs(self, it):
+        """Capture the steady-state sweep graphs now (hmsc_prepare_graphs), so a timed
+        run() starts replaying at once; True when they exist afterwards."""
+        built = np.zeros(1, dtype=np.int32)
+        L.check(self.lib.hmsc_prepare_graphs(self.h, int(it), L.iptr(built)))
+        return bool(built[0])
+
     PROF_IDS = dict(z=0, zl=1, betalambda=2, eta_unit=3, sweep=4, eta_spatial=5, chol=6, alpha=7, gamma_eta=8, rho=9)
 
     def profile(self, enable=True):
@@ -500,10 +507,14 @@ def sampleMcmc(hM, samples, transient=0, thin=1, initPar=None, verbose=None, ada
         if nChains > 1:
             print(f'[1] "Computing chain {c + 1}"')
         ch = Chain(hM, int(initSeed[c]), device=devices[c % len(devices)], updater=updater)
-        ch.init(nf0)
-        if initPar is not None:
-            ch.set_state(initPar)
-            ch.init_z()        # the reference draws Z last, from the initPar state (:229-254)
+        try:
+            ch.init(nf0)
+            if initPar is not None:
+                ch.set_state(initPar)
+                ch.init_z()        # the reference draws Z last, from the initPar state (:229-254)
+        except BaseException:
+            ch.close()
+            raise
         return ch
 
     def run_chain(c, ch):                                                  # :155-327
@@ -517,8 +528,10 @@ def sampleMcmc(hM, samples, transient=0, thin=1, initPar=None, verbose=None, ada
     # synchronisation), and only their sweep loops run concurrently, nParallel at a time.
     for start in range(0, nChains, max(1, nParallel)):
         idx = list(range(start, min(nChains, start + max(1, nParallel))))
-        chains = [make_chain(c) for c in idx]
+        chains = []
         try:
+            for c in idx:   # built one at a time: a failure still closes the ones already made
+                chains.append(make_chain(c))
             if len(idx) > 1:
                 th = [threading.Thread(target=run_chain, args=(c, ch)) for c, ch in zip(idx, chains)]
                 for t in th:

@@ -130,3 +130,45 @@ def vignette3_phylo(ns=300, ny=200, seed=SYNTHETIC_SEED):
         study = {"sample": units}
     return Hmsc(Y=Y, X=X, covNames=["(Intercept)", "habitatforest", "climate", "climate2"], XScale=True,
                 Tr=Tr, C=C, distr="normal", studyDesign=study, ranLevels={"sample": rl})
+
+
+def vignette2(model="linear", n=100, seed=SYNTHETIC_SEED):
+    """BASELINE.json config 2: the models of vignettes/vignette_2_multivariate_low.Rmd with its
+    generators (numpy's stream in place of R's set.seed):
+      "linear"     :55   Hmsc(Y, XData, XFormula=~x1+x2), 5 normal species, NO random level (nr = 0)
+      "latent"     :143  the same with a sample-level random level (units = 1..n)
+      "reduced"    :189  XFormula = ~x1 with the sample level (x2 left to the latent factors)
+      "ordination" :253  XFormula = ~1, sample level with nfMin = nfMax = 2
+      "mixed"      :299  4 species normal / probit / Poisson / lognormal Poisson, ~x1+x2, nr = 0
+    """
+    rng = np.random.default_rng(seed)
+    x1, x2 = rng.standard_normal(n), rng.standard_normal(n)
+    if model == "mixed":
+        b1, b2 = np.array([1.0, 1, -1, -1]), np.array([1.0, -1, 1, -1])       # :277-279
+        L = np.outer(x1, b1) + np.outer(x2, b2)
+        Y = np.empty((n, 4))
+        Y[:, 0] = L[:, 0] + rng.standard_normal(n)                             # :287-290
+        Y[:, 1] = ((L[:, 1] + rng.standard_normal(n)) > 0).astype(np.float64)
+        Y[:, 2] = rng.poisson(np.exp(L[:, 2]))
+        Y[:, 3] = rng.poisson(np.exp(L[:, 3] + rng.standard_normal(n)))
+        X = np.column_stack([np.ones(n), x1, x2])
+        return Hmsc(Y=Y, X=X, covNames=["(Intercept)", "x1", "x2"], XScale=True,
+                    distr=["normal", "probit", "poisson", "lognormal poisson"])
+    b1, b2 = np.array([1.0, 1, -1, -1, 0]), np.array([1.0, -1, 1, -1, 0])      # :36-38
+    Y = np.outer(x1, b1) + np.outer(x2, b2) + rng.standard_normal((n, 5))      # :41-44
+    cols = {"linear": [x1, x2], "latent": [x1, x2], "reduced": [x1], "ordination": []}[model]
+    X = np.column_stack([np.ones(n)] + cols)
+    covNames = ["(Intercept)"] + ["x1", "x2"][:len(cols)]
+    if model == "linear":
+        return Hmsc(Y=Y, X=X, covNames=covNames, XScale=True, distr="normal")
+    units = np.arange(1, n + 1)
+    rl = HmscRandomLevel(units=units)                                          # :142-143
+    if model == "ordination":
+        setPriors(rl, nfMin=2, nfMax=2)                                        # :250-251
+    try:
+        import pandas as pd
+        study = pd.DataFrame({"sample": units})
+    except Exception:  # pragma: no cover
+        study = {"sample": units}
+    return Hmsc(Y=Y, X=X, covNames=covNames, XScale=True, distr="normal", studyDesign=study,
+                ranLevels={"sample": rl})

@@ -254,6 +254,16 @@ int hmsc_kernel_timing_get(hmsc_state* s, int32_t id, double* total_us, int32_t*
 /* Wait for all device work of this chain. */
 int hmsc_sync(hmsc_state* s);
 
+/* Capture (without running) the steady-state sweep graphs that hmsc_run replays, so a
+ * caller that times hmsc_run (bench.py) does not pay for stream capture and
+ * hipGraphInstantiate inside its timed region.  `iter` is the next sweep index the caller
+ * will run (the Philox counters of a replay are set per launch, so any value works).
+ * *built = 1 when the graphs exist afterwards; 0 when the chain is not in a steady state
+ * yet (no eager sweep since the last init / set_state / updateNf repack), is sharded, or
+ * graphs are disabled (HMSC_NO_GRAPH, profiling) -- hmsc_run then captures on its own.
+ * No reference counterpart: the R loop has no launch overhead to amortise. */
+int hmsc_prepare_graphs(hmsc_state* s, int32_t iter, int32_t* built);
+
 /* The blocked device Cholesky (dense.hip) on one host matrix, for tests: A (n x n,
  * column-major, lower triangle read) is overwritten by L (A = L L^T; the strict upper
  * triangle is scratch), b (may be NULL) by A^-1 b through L^-T L^-1; *info = 1 if A is not

@@ -19,10 +19,15 @@ pytestmark = pytest.mark.gpu
 class HostAllReduce:
     """In-process sum over `n` ranks (threads): deposit, barrier, sum, barrier."""
 
-    def __init__(self, n):
+    def __init__(self, n, timeout=60.0):
         self.n = n
-        self.bar = threading.Barrier(n)
+        # a rank that fails before an all-reduce would leave its peers waiting: the barrier
+        # times out (BrokenBarrierError -> the callback returns -1 -> the library raises)
+        self.bar = threading.Barrier(n, timeout=timeout)
         self.parts = [None] * n
+
+    def abort(self):
+        self.bar.abort()
 
     def for_rank(self, r):
         def f(x):
@@ -34,7 +39,7 @@ class HostAllReduce:
         return f
 
 
-def _run_ranks(fns):
+def _run_ranks(fns, red=None):
     err = []
 
     def wrap(f):
@@ -42,11 +47,14 @@ def _run_ranks(fns):
             f()
         except Exception as e:
             err.append(e)
+            if red is not None:
+                red.abort()        # release the peers blocked in the all-reduce
     th = [threading.Thread(target=wrap, args=(f,)) for f in fns]
     for t in th:
         t.start()
     for t in th:
         t.join(timeout=120)
+    assert not any(t.is_alive() for t in th), "a rank is still inside a sweep"
     if err:
         raise err[0]
 
@@ -62,10 +70,10 @@ def test_sharded_chain_follows_unsharded(kw):
     red = HostAllReduce(nr)
     ranks = [H.Chain(hM, seed, device=0, updater=up, rank=r, nranks=nr, host_allreduce=red.for_rank(r))
              for r in range(nr)]
-    _run_ranks([ch.init for ch in ranks])
+    _run_ranks([ch.init for ch in ranks], red)
     for it in range(1, 6):
         full.sweep(it)
-        _run_ranks([lambda ch=ch, it=it: ch.sweep(it) for ch in ranks])
+        _run_ranks([lambda ch=ch, it=it: ch.sweep(it) for ch in ranks], red)
     g = full.get_state()
     parts = [ch.get_state() for ch in ranks]
     blocks = [shard_range(hM.ns, r, nr) for r in range(nr)]
