@@ -23,7 +23,8 @@ ip = C.POINTER(C.c_int32)
 
 
 class hmsc_model(C.Structure):
-    _fields_ = [("ny", C.c_int32), ("ns", C.c_int32), ("nc", C.c_int32), ("nt", C.c_int32), ("nr", C.c_int32),
+    _fields_ = [("struct_size", C.c_int32),
+                ("ny", C.c_int32), ("ns", C.c_int32), ("nc", C.c_int32), ("nt", C.c_int32), ("nr", C.c_int32),
                 ("Y", dp), ("Yraw", dp), ("X", dp), ("Tr", dp), ("Pi", ip), ("np", ip), ("distr", ip),
                 ("V0", dp), ("f0", C.c_double), ("mGamma", dp), ("UGamma", dp), ("aSigma", dp), ("bSigma", dp),
                 ("nu", dp), ("a1", dp), ("b1", dp), ("a2", dp), ("b2", dp), ("nfMin", ip), ("nfMax", ip),
@@ -33,7 +34,11 @@ class hmsc_model(C.Structure):
                 ("RiWg", dp * MAX_LEVELS), ("detWg", dp * MAX_LEVELS),
                 ("sCoord", dp * MAX_LEVELS), ("distMat", dp * MAX_LEVELS),
                 ("nKnots", ip), ("idDg", dp * MAX_LEVELS), ("idDW12g", dp * MAX_LEVELS), ("Fg", dp * MAX_LEVELS),
-                ("iFg", dp * MAX_LEVELS), ("detDg", dp * MAX_LEVELS)]
+                ("iFg", dp * MAX_LEVELS), ("detDg", dp * MAX_LEVELS), ("nNeighbours", ip)]
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        self.struct_size = C.sizeof(hmsc_model)   # hmsc_create checks it (include/hmsc_amd.h)
 
 
 class hmsc_params(C.Structure):

@@ -128,6 +128,33 @@ struct DeviceGuard {
   ~DeviceGuard() { (void)hipSetDevice(prev); }
 };
 
+// Owners for the scratch device buffers and streams of one-shot entry points
+// (hmsc_dense_chol_solve, hmsc_spatial_full_grid): freed on every exit, including an
+// HmscError thrown by HIP_OK half way (guarded() turns it into an error code).
+struct DevBufs {
+  std::vector<void*> p;
+  template <class T>
+  T* alloc(size_t n) {
+    void* q = nullptr;
+    HIP_OK(hipMalloc(&q, std::max<size_t>(1, n) * sizeof(T)));
+    p.push_back(q);
+    return static_cast<T*>(q);
+  }
+  ~DevBufs() {
+    for (void* q : p) (void)hipFree(q);
+  }
+};
+struct OwnedStream {
+  hipStream_t s = nullptr;
+  OwnedStream() { HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking)); }
+  ~OwnedStream() {
+    if (s) {
+      (void)hipStreamSynchronize(s);
+      (void)hipStreamDestroy(s);
+    }
+  }
+};
+
 // ---------------------------- host dense helpers ----------------------------
 using Mat = std::vector<double>;  // column-major
 
@@ -309,6 +336,9 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
                         void* host_ctx = nullptr) {
   std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
   HMSC_REQUIRE(m != nullptr, "model is NULL");
+  HMSC_REQUIRE(m->struct_size == (int32_t)sizeof(hmsc_model),
+               "hmsc_model.struct_size must be sizeof(hmsc_model) of include/hmsc_amd.h (rebuild the caller "
+               "against this header and zero-initialise the struct)");
   HMSC_REQUIRE(m->ny > 0 && m->ns > 0 && m->nc >= 0 && m->nt > 0, "bad dimensions");
   HMSC_REQUIRE(m->nr >= 0 && m->nr <= HMSC_MAX_LEVELS, "nr out of range");
   s.ny = m->ny;
@@ -356,7 +386,11 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
                    "spatial level: spatialMethod must be 1 (Full), 2 (NNGP) or 3 (GPP)");
       HMSC_REQUIRE(m->spatialMethod[r] == 1 || m->np[r] == ny,
                    "spatial level: NNGP / GPP levels need np == ny (R/updateEta.R:140,165)");
-      const bool geom = m->spatialMethod[r] == 1 && !m->iWg[r] && (m->sCoord[r] || m->distMat[r]);
+      HMSC_REQUIRE(m->spatialMethod[r] != 2 || (m->sCoord[r] && m->nNeighbours),
+                   "NNGP level: pass the unit coordinates (sCoord) and nNeighbours; nearest neighbours are not "
+                   "available for distance matrices (R/computeDataParameters.R:86-88)");
+      const bool geom = (m->spatialMethod[r] == 1 && !m->iWg[r] && (m->sCoord[r] || m->distMat[r])) ||
+                        m->spatialMethod[r] == 2;
       const bool gpp = m->spatialMethod[r] == 3 && !m->iWg[r] && m->nKnots && m->nKnots[r] > 0 && m->idDg[r] &&
                        m->idDW12g[r] && m->Fg[r] && m->iFg[r] && m->detDg[r];
       HMSC_REQUIRE(m->nalpha == nullptr || m->nalpha[r] <= HMSC_MAX_ALPHA,
@@ -415,7 +449,10 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
       const size_t G = m->nalpha[r], np2 = (size_t)L.np * L.np;
       L.nalpha = (int)G;
       L.alphapw = dupload(m->alphapw[r], 2 * G);
-      if (m->spatialMethod[r] == 3 && !m->iWg[r]) {  // GPP in R's low-rank form
+      if (m->spatialMethod[r] == 2) {  // NNGP in the sparse Vecchia form (spatial.hip)
+        std::vector<double> alphas(m->alphapw[r], m->alphapw[r] + G);
+        setup_nngp_level(s, r, m->sCoord[r], m->sDim[r], m->nNeighbours[r], alphas.data(), (int)G);
+      } else if (m->spatialMethod[r] == 3 && !m->iWg[r]) {  // GPP in R's low-rank form
         const size_t nK = (size_t)m->nKnots[r];
         // gpp_alpha_kernel / launch_eta_gpp stage one knot vector in a 1024-entry LDS array
         // (spatial.hip); refuse larger knot sets here, before any updater can run
@@ -496,6 +533,19 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.has_na = !na_cols.empty();
   ycode.resize((size_t)ny * (nsl + 32) + 64, 0);  // z kernel loads past the last species (z_kernel.h ZArgs)
   s.Ycode = dupload(ycode.data(), ycode.size());
+  {  // the z kernel's packed codes: word (species block b, site i) holds code + 1 of species
+     // 32 b + jj in bits 2 jj, 2 jj + 1 (padding: code 0)
+    const int nblk = (nsl + 31) / 32;
+    std::vector<uint64_t> yb((size_t)nblk * ny + 64, 0x5555555555555555ull);
+    for (int j = 0; j < nsl; ++j) {
+      const int sh = 2 * (j % 32);
+      for (int i = 0; i < ny; ++i) {
+        uint64_t& w = yb[(size_t)(j / 32) * ny + i];
+        w = (w & ~(3ull << sh)) | ((uint64_t)(ycode[i + (size_t)ny * j] + 1) << sh);
+      }
+    }
+    s.Ybits = dupload(yb.data(), yb.size());
+  }
   if (!s.all_probit) {
     s.Yval = dupload(yval.data(), yval.size());
     s.Yraw = dupload(yraw.data(), yraw.size());
@@ -655,7 +705,7 @@ static void free_state(State& s) {
   std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
   DeviceGuard dg(s.device);
   (void)hipDeviceSynchronize();
-  void* ptrs[] = {s.X, s.Tr, s.Yval, s.Yraw, s.Ycode, s.fam, s.varest, s.V0, s.iUGamma, s.mGamma, s.UGammaL,
+  void* ptrs[] = {s.X, s.Tr, s.Yval, s.Yraw, s.Ycode, s.Ybits, s.fam, s.varest, s.V0, s.iUGamma, s.mGamma, s.UGammaL,
                   s.aSigma, s.bSigma, s.XX, s.TT, s.V0g, s.V0gXXV0g, s.iV0, s.V0inv, s.iUmG, s.V0gXX, s.g2prep, s.scratch2, s.na_cols, s.na_index,
                   s.na_rows, s.row_na, s.row_slot, s.dev_flags, s.Z, s.XEta, s.BL, s.Psi, s.Delta, s.Gamma, s.iV,
                   s.iSigma, s.rho, s.XZ, s.G, s.ZTr, s.XZ_part, s.G_part, s.ZTr_part, s.Gna, s.ZL, s.ZL_part,
@@ -666,7 +716,7 @@ static void free_state(State& s) {
   for (int r = 0; r < s.nr; ++r) {
     Level& L = s.lev[r];
     void* lp[] = {L.Eta, L.Pi, L.unit_ptr, L.unit_rows, L.Alpha, L.AlphaD, L.alphapw, L.iWg, L.RiWg, L.detWg, L.spWork,
-                  L.idDg, L.idDW12g, L.Fg, L.iFg};
+                  L.idDg, L.idDW12g, L.Fg, L.iFg, L.nnIdx, L.nnA, L.nnD, L.nnPerm, L.nnPos, L.nnChPtr, L.nnCh};
     for (void* p : lp)
       if (p) (void)hipFree(p);
   }
@@ -676,7 +726,8 @@ static void free_state(State& s) {
   if (s.gv_part) (void)hipFree(s.gv_part);
   if (s.host_rec) (void)hipHostFree(s.host_rec);
   if (s.copied_host) (void)hipHostFree(s.copied_host);
-  if (s.gexec) (void)hipGraphExecDestroy(s.gexec);
+  for (hipGraphExec_t g : {s.gexec, s.gexec_rec, s.gexec1, s.gexec1_rec})
+    if (g) (void)hipGraphExecDestroy(g);
   if (s.d_iters) (void)hipFree(s.d_iters);
   if (s.d_kt) (void)hipFree(s.d_kt);
   if (s.comm) ncclCommDestroy((ncclComm_t)s.comm);
@@ -1049,15 +1100,18 @@ __global__ void set_desc_kernel(int32_t* d, int32_t iter0, int32_t transient, in
 }
 
 static void destroy_graph(State& s) {
-  if (s.gexec) (void)hipGraphExecDestroy(s.gexec);
-  if (s.gexec_rec) (void)hipGraphExecDestroy(s.gexec_rec);
-  s.gexec = s.gexec_rec = nullptr;
+  for (hipGraphExec_t* g : {&s.gexec, &s.gexec_rec, &s.gexec1, &s.gexec1_rec}) {
+    if (*g) (void)hipGraphExecDestroy(*g);
+    *g = nullptr;
+  }
 }
 
 // Captures graph_sweeps sweeps (with or without the record pack after each).  Returns
 // nullptr when the sweep is not in a steady state, i.e. the host-side validity flags it
 // changes would differ on the next sweep.
-static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, size_t* n_nodes = nullptr) {
+static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, size_t* n_nodes = nullptr,
+                                     int nsweeps = 0) {
+  if (nsweeps <= 0) nsweeps = s.graph_sweeps;
   std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
   join_side(s);
   const bool xv = s.xeta_valid, zv = s.zt_valid, gv = s.g2prep_valid, gp = s.g_pending;
@@ -1065,7 +1119,7 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
   HIP_OK(hipStreamBeginCapture(s.stream, hipStreamCaptureModeThreadLocal));
   s.capturing = true;
   try {
-    for (int i = 0; i < s.graph_sweeps; ++i) {
+    for (int i = 0; i < nsweeps; ++i) {
       s.d_iter = s.d_iters + i;
       s.pack_req = with_record;
       s.pack_done = false;
@@ -1090,6 +1144,10 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
   size_t nodes = 0;
   HIP_OK(hipGraphGetNodes(g, nullptr, &nodes));
   if (n_nodes) *n_nodes = nodes;
+  if (const char* e = std::getenv("HMSC_GRAPH_DEBUG"))
+    if (e[0] == '1')
+      std::fprintf(stderr, "[hmsc] captured %d sweeps%s: %zu nodes%s\n", nsweeps, with_record ? " + record" : "",
+                   nodes, steady ? "" : " (not steady)");
   hipGraphExec_t ge = nullptr;
   if (steady && nodes <= GRAPH_MAX_NODES) HIP_OK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
   HIP_OK(hipGraphDestroy(g));
@@ -1117,22 +1175,33 @@ static bool build_sweep_graphs(State& s, uint32_t iter) {
     destroy_graph(s);
     return false;
   }
+  if (s.graph_sweeps > 1) {  // remainders of a run (optional: eager sweeps otherwise)
+    s.gexec1 = capture_sweeps(s, iter, false, nullptr, 1);
+    s.gexec1_rec = s.gexec1 ? capture_sweeps(s, iter, true, nullptr, 1) : nullptr;
+  }
   s.graph_K = s.K;
   s.graph_NF = s.NF;
   s.graph_dirty = false;
   return true;
 }
 
-// Runs sweeps iter .. iter+n-1 (n == graph_sweeps) as one graph replay if the graphs exist
-// or can be built now; returns false (nothing launched) when the caller must run eagerly.
-static bool replay_sweeps(State& s, uint32_t iter, bool with_record) {
+// Runs sweeps iter .. iter+n-1 (n == graph_sweeps, or 1 for the remainder of a run) as one
+// graph replay if the graphs exist or can be built now; returns false (nothing launched) when
+// the caller must run eagerly.
+static bool replay_sweeps(State& s, uint32_t iter, bool with_record, int n) {
   if (!s.use_graph || s.nranks != 1 || s.prof) return false;
   if (s.gexec && (s.graph_dirty || s.graph_K != s.K || s.graph_NF != s.NF)) destroy_graph(s);
   if (s.graph_dirty) s.eager_streak = 0, s.graph_dirty = false;
   if (!s.gexec && (s.eager_streak < 1 || !build_sweep_graphs(s, iter))) return false;  // steady first
+  hipGraphExec_t ge = nullptr;
+  if (n == s.graph_sweeps)
+    ge = with_record ? s.gexec_rec : s.gexec;
+  else if (n == 1)
+    ge = with_record ? s.gexec1_rec : s.gexec1;
+  if (!ge) return false;
   join_side(s);
-  set_iters_kernel<<<1, 64, 0, s.stream>>>(s.d_iters, iter, s.graph_sweeps);
-  HIP_OK(hipGraphLaunch(with_record ? s.gexec_rec : s.gexec, s.stream));
+  set_iters_kernel<<<1, 64, 0, s.stream>>>(s.d_iters, iter, n);
+  HIP_OK(hipGraphLaunch(ge, s.stream));
   return true;
 }
 
@@ -1300,16 +1369,17 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
     int n = 1;
     bool replayed = false;
     int kfirst = -1, klast = -1;
-    if (it > max_adapt && it + G - 1 <= total) {
-      for (int j = it; j < it + G; ++j)
+    if (it > max_adapt) {
+      const int ng = it + G - 1 <= total ? G : 1;  // the run's remainder: one-sweep graphs
+      for (int j = it; j < it + ng; ++j)
         if (recorded(j)) {
           if (kfirst < 0) kfirst = sample_of(j);
           klast = sample_of(j);
         }
       if (klast >= 0) wait_slot(klast);
-      if (replay_sweeps(s, (uint32_t)(iter0 + it), klast >= 0)) {
+      if (replay_sweeps(s, (uint32_t)(iter0 + it), klast >= 0, ng)) {
         replayed = true;
-        n = G;
+        n = ng;
         if (klast >= 0) {
           HIP_OK(hipEventRecord(s.ev_graph, s.stream));
           HIP_OK(hipStreamWaitEvent(s.copy_stream, s.ev_graph, 0));
@@ -1397,15 +1467,14 @@ int hmsc_dense_chol_solve(int32_t device, double* A, int32_t n, double* b, int32
     HMSC_REQUIRE(A != nullptr && n > 0 && info != nullptr, "hmsc_dense_chol_solve: bad arguments");
     std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
     DeviceGuard dg(device);
-    hipStream_t st;
-    HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    DevBufs bufs;  // declared before the stream: the stream is synchronised before the frees
+    OwnedStream os;
+    const hipStream_t st = os.s;
     const size_t nn = (size_t)n * n;
-    double *dA = nullptr, *db = nullptr, *ws = nullptr;
-    int* dinfo = nullptr;
-    HIP_OK(hipMalloc(&dA, nn * sizeof(double)));
-    HIP_OK(hipMalloc(&db, (size_t)n * sizeof(double)));
-    HIP_OK(hipMalloc(&ws, dense_ws_doubles(n) * sizeof(double)));
-    HIP_OK(hipMalloc(&dinfo, sizeof(int)));
+    double* dA = bufs.alloc<double>(nn);
+    double* db = bufs.alloc<double>(n);
+    double* ws = bufs.alloc<double>(dense_ws_doubles(n));
+    int* dinfo = bufs.alloc<int>(1);
     HIP_OK(hipMemsetAsync(dinfo, 0, sizeof(int), st));
     HIP_OK(hipMemcpyAsync(dA, A, nn * sizeof(double), hipMemcpyHostToDevice, st));
     if (b) HIP_OK(hipMemcpyAsync(db, b, (size_t)n * sizeof(double), hipMemcpyHostToDevice, st));
@@ -1418,8 +1487,6 @@ int hmsc_dense_chol_solve(int32_t device, double* A, int32_t n, double* b, int32
     HIP_OK(hipMemcpyAsync(A, dA, nn * sizeof(double), hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(info, dinfo, sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
-    (void)hipFree(dA), (void)hipFree(db), (void)hipFree(ws), (void)hipFree(dinfo);
-    (void)hipStreamDestroy(st);
   });
 }
 
@@ -1430,23 +1497,26 @@ int hmsc_spatial_full_grid(int32_t device, int32_t np, int32_t sdim, const doubl
                  "hmsc_spatial_full_grid: bad arguments");
     std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
     DeviceGuard dg(device);
-    hipStream_t st;
-    HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    DevBufs bufs;
+    OwnedStream os;
+    const hipStream_t st = os.s;
     const size_t n2 = (size_t)np * np;
-    double* geo = coords ? dupload(coords, (size_t)np * sdim) : dupload(dist, n2);
-    double* dI = dalloc<double>(n2 * G);
-    double* dR = dalloc<double>(n2 * G);
-    double* dd = dalloc<double>(G);
-    int* flag = dalloc<int>(1);
+    double* geo = bufs.alloc<double>(coords ? (size_t)np * sdim : n2);
+    copy_sync(geo, coords ? coords : dist, (coords ? (size_t)np * sdim : n2) * sizeof(double), hipMemcpyHostToDevice, st);
+    double* dI = bufs.alloc<double>(n2 * G);
+    double* dR = bufs.alloc<double>(n2 * G);
+    double* dd = bufs.alloc<double>(G);
+    int* flag = bufs.alloc<int>(1);
+    HIP_OK(hipMemsetAsync(flag, 0, sizeof(int), st));
+    HIP_OK(hipMemsetAsync(dI, 0, n2 * G * sizeof(double), st));
+    HIP_OK(hipMemsetAsync(dR, 0, n2 * G * sizeof(double), st));
     spatial_full_grid(st, np, coords ? sdim : 0, coords ? geo : nullptr, coords ? nullptr : geo, alphas, G, dI, dR,
                       dd, flag);
-    int bad = 0;
-    copy_sync(&bad, flag, sizeof(int), hipMemcpyDeviceToHost);
-    copy_sync(iWg, dI, n2 * G * sizeof(double), hipMemcpyDeviceToHost);
-    copy_sync(RiWg, dR, n2 * G * sizeof(double), hipMemcpyDeviceToHost);
-    copy_sync(detWg, dd, G * sizeof(double), hipMemcpyDeviceToHost);
-    (void)hipFree(geo), (void)hipFree(dI), (void)hipFree(dR), (void)hipFree(dd), (void)hipFree(flag);
-    (void)hipStreamDestroy(st);
+    int bad = 0;  // every copy on the grid's own stream (ordered after its kernels)
+    copy_sync(&bad, flag, sizeof(int), hipMemcpyDeviceToHost, st);
+    copy_sync(iWg, dI, n2 * G * sizeof(double), hipMemcpyDeviceToHost, st);
+    copy_sync(RiWg, dR, n2 * G * sizeof(double), hipMemcpyDeviceToHost, st);
+    copy_sync(detWg, dd, G * sizeof(double), hipMemcpyDeviceToHost, st);
     HMSC_REQUIRE(bad == 0, "hmsc_spatial_full_grid: a grid matrix is not positive definite");
   });
 }
@@ -1615,8 +1685,8 @@ int hmsc_prepare_graphs(hmsc_state* h, int32_t iter, int32_t* built) {
       if (s.eager_streak < 1 || !build_sweep_graphs(s, (uint32_t)iter)) return;
     }
     // make the executable graphs device-resident now, not at their first launch
-    HIP_OK(hipGraphUpload(s.gexec, s.stream));
-    HIP_OK(hipGraphUpload(s.gexec_rec, s.stream));
+    for (hipGraphExec_t g : {s.gexec, s.gexec_rec, s.gexec1, s.gexec1_rec})
+      if (g) HIP_OK(hipGraphUpload(g, s.stream));
     HIP_OK(hipStreamSynchronize(s.stream));
     *built = 1;
   });
@@ -1650,6 +1720,21 @@ int hmsc_debug_get(hmsc_state* h, const char* name, double* out, int64_t n) {
     else if (nm == "ZL") src = s.ZL_part, avail = (int64_t)s.zl_split * s.ny * s.NF;
     else if (nm == "stamps") {
       read_stamps(out, (int)n);
+      return;
+    } else if (nm.rfind("nngp_perm", 0) == 0 || nm.rfind("nngp_bw", 0) == 0) {  // NNGP factorization order
+      const bool perm = nm.rfind("nngp_perm", 0) == 0;
+      const int r = std::atoi(nm.c_str() + (perm ? 9 : 7));
+      HMSC_REQUIRE(r >= 0 && r < s.nr && s.lev[r].nngp, "debug_get: not an NNGP level");
+      const Level& L = s.lev[r];
+      if (!perm) {
+        HMSC_REQUIRE(n >= 1, "nngp_bw needs 1 slot");
+        out[0] = L.nnBwUnits;
+        return;
+      }
+      HMSC_REQUIRE(n >= L.np, "nngp_perm needs np slots");
+      std::vector<int> pv(L.np);
+      copy_sync(pv.data(), L.nnPerm, sizeof(int) * L.np, hipMemcpyDeviceToHost, s.stream);
+      for (int i = 0; i < L.np; ++i) out[i] = pv[i];
       return;
     } else if (nm == "graph") {
       HMSC_REQUIRE(n >= 4, "graph needs 4 slots");

@@ -465,14 +465,14 @@ __global__ __launch_bounds__(256) void trsv_fwd_kernel(const double* L, int lda,
 // backward, block k: z = Linv_k^T x_k -> y_k; x[j] -= sum_c L[k0 + c, j] z_c for the
 // columns j < k0, 64 columns per workgroup read as a coalesced 64 x 64 tile
 __global__ __launch_bounds__(256) void trsv_bwd_kernel(const double* L, int lda, int n, int k0, const double* Linv,
-                                                       double* x, double* y) {
+                                                       double* x, double* y, int jb0) {
   __shared__ double T[DB * DLD];
   __shared__ double z[DB];
   __shared__ double part[4 * DB];
   const int nb = min(DB, n - k0), t = threadIdx.x, lane = t & 63, w = t >> 6;
   block_solve(Linv + (size_t)(k0 / DB) * DB * DB, x, k0, nb, 1, T, z, part);
   if (blockIdx.x == 0 && t < nb) y[k0 + t] = z[t];
-  const int j0 = blockIdx.x * DB, cols = min(DB, k0 - j0);
+  const int j0 = (jb0 + (int)blockIdx.x) * DB, cols = min(DB, k0 - j0);
   if (cols <= 0) return;
   stage_n(T, L, lda, k0, j0, nb, cols);
   __syncthreads();
@@ -758,11 +758,15 @@ void dense_lauum_lower(hipStream_t st, const double* M, int ldm, int n, double* 
 // than doubles the one-workgroup diagonal factorization, and the cross-stream joins add
 // ~10 us per panel.)
 
-void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, int* info) {
+// Banded (bw > 0): block column k0 has nonzeros in rows < k0 + DB + bw only, and the trailing
+// update of its panel adds exact zeros outside the band, so the panel and update launches stop
+// at the tiles covering rows k0 + DB .. k0 + DB + bw (the update's tile map depends on the
+// launch size only: a smaller grid is the band's triangle of tiles).
+void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, int* info, int bw) {
   for (int k0 = 0; k0 < n; k0 += DB) {
     double* Linv = ws + (size_t)(k0 / DB) * DB * DB;
     chol_diag_kernel<<<1, 256, 0, st>>>(A, lda, n, k0, Linv, info);
-    const int rem = n - (k0 + DB);
+    const int rem = bw > 0 ? std::min(n - (k0 + DB), bw) : n - (k0 + DB);
     if (rem > 0) {
       const int nt = (rem + DB - 1) / DB;
       chol_panel_kernel<<<nt, 256, 0, st>>>(A, lda, n, k0, Linv);
@@ -775,18 +779,22 @@ void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, in
 // x <- L^-1 x  (trans = 0)  or  x <- L^-T x  (trans = 1), L lower (n x n, ld lda) as left by
 // dense_potrf_lower together with its workspace `ws` (diagonal-block inverses, then n doubles
 // in which the solution is assembled before it is copied back to x)
-void dense_trsv_lower(hipStream_t st, const double* L, int n, int lda, double* x, int trans, double* ws) {
+void dense_trsv_lower(hipStream_t st, const double* L, int n, int lda, double* x, int trans, double* ws, int bw) {
   const int nbk = (n + DB - 1) / DB;
   double* y = ws + (size_t)nbk * DB * DB;
   if (!trans) {
     for (int b = 0; b < nbk; ++b) {
-      const int k0 = b * DB, rem = n - (k0 + DB);
+      const int k0 = b * DB;
+      const int rem = bw > 0 ? std::min(n - (k0 + DB), bw) : n - (k0 + DB);  // band: rows < k0 + DB + bw
       trsv_fwd_kernel<<<rem > 0 ? (rem + DB - 1) / DB : 1, 256, 0, st>>>(L, lda, n, k0, ws, x, y);
     }
   } else {
     for (int b = nbk - 1; b >= 0; --b) {
       const int k0 = b * DB;
-      trsv_bwd_kernel<<<k0 > 0 ? (k0 + DB - 1) / DB : 1, 256, 0, st>>>(L, lda, n, k0, ws, x, y);
+      // band: block k's rows reach back to column k0 - bw only
+      const int jb0 = bw > 0 ? std::max(0, (k0 - bw) / DB) : 0;
+      const int nblk = k0 > 0 ? (k0 + DB - 1) / DB - jb0 : 1;
+      trsv_bwd_kernel<<<std::max(1, nblk), 256, 0, st>>>(L, lda, n, k0, ws, x, y, jb0);
     }
   }
   copy_vec_kernel<<<(n + 255) / 256, 256, 0, st>>>(x, y, n);

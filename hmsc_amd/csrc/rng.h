@@ -234,6 +234,27 @@ __host__ __device__ __forceinline__ double log_fast_t(double x, const double* ls
 
 __host__ __device__ __forceinline__ double log_fast(double x) { return log_fast_t(x, kLogSeries); }
 
+// exp(x) for x <= 700 without the libm range handling (the truncated-normal draw evaluates it
+// on -a^2 + g(t) <= 0 only): x = n ln2 + r, |r| <= ln2 / 2, exp(r) by its degree-12 Taylor
+// polynomial (truncation 1.7e-16 relative), 2^n by ldexp (underflows to 0 below -745).
+HMSC_TABLE double kExpTaylor[13] = {1.0 / 479001600.0, 1.0 / 39916800.0, 1.0 / 3628800.0, 1.0 / 362880.0,
+                                    1.0 / 40320.0,     1.0 / 5040.0,     1.0 / 720.0,     1.0 / 120.0,
+                                    1.0 / 24.0,        1.0 / 6.0,        0.5,             1.0,
+                                    1.0};
+__host__ __device__ __forceinline__ double exp_small(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double n = __builtin_rint(x * 1.4426950408889634);
+  double r = fma(-n, 6.93147180369123816490e-01, x);  // ln2 = hi + lo (fdlibm split: n hi exact)
+  r = fma(-n, 1.90821492927058770002e-10, r);
+  double p = kExpTaylor[0];
+#pragma unroll
+  for (int k = 1; k < 13; ++k) p = fma_sc(p, r, kExpTaylor[k]);
+  return __builtin_ldexp(p, (int)n);
+#else
+  return exp(x);
+#endif
+}
+
 __host__ __device__ __forceinline__ double erfc_fast_t(double z, const double* ep) {
   const double a = fmin(fabs(z), 40.0);
   const double t = 2.0 * rcp_pos(2.0 + a);

@@ -21,6 +21,12 @@
 // Randomness (oracle/hmsc_oracle.py _eta_spatial_full / update_alpha): Eta normal(p, h,
 // S_ETA + LEVEL_STRIDE r) -- the same counters as the non-spatial branch --, Alpha the first
 // uniform of (h, 0, S_ALPHA + LEVEL_STRIDE r).
+#include <algorithm>
+#include <cmath>
+#include <thread>
+#include <utility>
+#include <vector>
+
 #include "common.h"
 #include "state.h"
 
@@ -554,6 +560,348 @@ static void launch_eta_gpp(State& s, int r, uint32_t iter) {
   HIP_OK(hipGetLastError());
 }
 
+static int* dupload_i32(const int* h, size_t n) {
+  int* p = nullptr;
+  HIP_OK(hipMalloc(&p, std::max<size_t>(1, n) * sizeof(int)));
+  if (n) HIP_OK(hipMemcpy(p, h, n * sizeof(int), hipMemcpyHostToDevice));
+  return p;
+}
+static double* dupload_f64(const double* h, size_t n) {
+  double* p = nullptr;
+  HIP_OK(hipMalloc(&p, std::max<size_t>(1, n) * sizeof(double)));
+  if (n) HIP_OK(hipMemcpy(p, h, n * sizeof(double), hipMemcpyHostToDevice));
+  return p;
+}
+
+// ---------------------------------------------------------------------------------------
+// 'NNGP' levels in the sparse Vecchia form (R/computeDataParameters.R:82-136, R/updateEta.R:
+// 137-147, R/updateAlpha.R:21-34).  Per grid point g the prior precision is
+// iW_g = B_g' D_g^-1 B_g, B_g = I - A_g unit lower triangular with A_g[i, nb(i, k)] on the nnK
+// nearest EARLIER units of unit i: nnK + 1 numbers per unit, no np^2 array anywhere.
+//  * updateAlpha: v_gh = sum_i (eta_ih - sum_k A_g[i, nb(i,k)] eta_nb(i,k),h)^2 / D_g[i], one
+//    thread per unit (nalpha x ceil(np / 256) workgroups, the same chunk-partial layout as the
+//    'Full' kernel, so alpha_draw_kernel draws the grid index).
+//  * updateEta: iUEta = bdiag_h(iW_alpha_h) + kron(Lam iSigma Lam', I) is sparse; in the reverse
+//    Cuthill-McKee order of the units (setup_nngp_level), factors interleaved per unit (index
+//    pos(q) nf + h), it is a band matrix of bandwidth bw = (bwUnits + 1) nf - 1 (bwUnits 301 at
+//    np = 5000, 10 neighbours, against 4968 in the data order).  It is assembled straight into
+//    that band (one wave per column: each entry is the sum over the rows i whose support holds
+//    both units, in ascending i), factored by the blocked Cholesky restricted to the band's
+//    tiles (dense.hip, n bw^2 instead of n^3 / 3 flops) and solved: eta = P' L^-T (L^-1 P vec(fS)
+//    + P xi) with L L' = P iUEta P' -- the conditional of R's code, the noise of (unit q,
+//    factor h) the normal of R's order (S_ETA counters); the oracle restates this order
+//    (oracle/hmsc_oracle.py nngp_rcm, _eta_spatial_full).
+// ---------------------------------------------------------------------------------------
+struct NnArgs {
+  int np, nf, N, K, bw;
+  const int* idx;      // K x np
+  const double* A;     // nalpha x K x np
+  const double* D;     // nalpha x np
+  const int* perm;
+  const int* pos;
+  const int* chptr;
+  const int* ch;
+  const int* unit_ptr;
+  const double* AlphaD;
+};
+
+static NnArgs nn_args(const State& s, int r) {
+  const Level& L = s.lev[r];
+  NnArgs n{};
+  n.np = L.np;
+  n.nf = L.nf;
+  n.N = L.np * L.nf;
+  n.K = L.nnK;
+  n.bw = (L.nnBwUnits + 1) * L.nf - 1;
+  n.idx = L.nnIdx;
+  n.A = L.nnA;
+  n.D = L.nnD;
+  n.perm = L.nnPerm;
+  n.pos = L.nnPos;
+  n.chptr = L.nnChPtr;
+  n.ch = L.nnCh;
+  n.unit_ptr = L.unit_ptr;
+  n.AlphaD = L.AlphaD;
+  return n;
+}
+
+__global__ __launch_bounds__(256) void nngp_alpha_kernel(SpArgs a, NnArgs n) {
+  const int g = blockIdx.x, chunk = blockIdx.y, nch = gridDim.y, np = n.np, K = n.K;
+  const int i = chunk * 256 + threadIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __shared__ double red[4];
+  for (int h = 0; h < n.nf; ++h) {
+    const double* eta = a.Eta + (size_t)np * h;
+    double v = 0.0;
+    if (i < np) {
+      double r = eta[i];
+      for (int k = 0; k < K; ++k) {
+        const int j = n.idx[(size_t)k * np + i];
+        if (j >= 0) r = fma(-n.A[((size_t)g * K + k) * np + i], eta[j], r);
+      }
+      v = r * r / n.D[(size_t)g * np + i];
+    }
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) a.work[((size_t)g * nch + chunk) * n.nf + h] = (red[0] + red[1]) + (red[2] + red[3]);
+    __syncthreads();
+  }
+}
+
+// B_g[i, u] for the support entry e = i (K + 1) + slot of unit u in row i
+__device__ __forceinline__ double nn_b(const NnArgs& n, int g, int e) {
+  const int i = e / (n.K + 1), slot = e - i * (n.K + 1);
+  return slot == 0 ? 1.0 : -n.A[((size_t)g * n.K + slot - 1) * n.np + i];
+}
+
+// column c of the band (rows c .. c + bw) of P iUEta P', one wave per column
+__global__ __launch_bounds__(64) void nngp_assemble_kernel(NnArgs n, const double* LDL, double* Q) {
+  constexpr int SB = 256;
+  __shared__ int sb[SB];
+  const int c = blockIdx.x, lane = threadIdx.x, nf = n.nf, N = n.N, K1 = n.K + 1;
+  const int pb = c / nf, h = c - pb * nf, b = n.perm[pb];
+  const int g = (int)n.AlphaD[h] - 1;
+  const int b0 = n.chptr[b], nb = n.chptr[b + 1] - b0;
+  for (int q = lane; q < min(nb, SB); q += 64) sb[q] = n.ch[b0 + q];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  auto sb_at = [&](int q) { return q < SB ? sb[q] : n.ch[b0 + q]; };
+  for (int t = lane; t <= n.bw && c + t < N; t += 64) {
+    const int row = c + t, pa = row / nf, h2 = row - pa * nf, a = n.perm[pa];
+    double v = 0.0;
+    if (h2 == h) {  // iW_g[a, b] = sum over rows i holding both: B[i, a] B[i, b] / D[i]
+      const int a0 = n.chptr[a], na = n.chptr[a + 1] - a0;
+      int p = 0, q = 0;
+      while (p < na && q < nb) {
+        const int ea = n.ch[a0 + p], eb = sb_at(q);
+        const int ia = ea / K1, ib = eb / K1;
+        if (ia < ib) {
+          ++p;
+        } else if (ib < ia) {
+          ++q;
+        } else {
+          v = fma(nn_b(n, g, ea) * nn_b(n, g, eb), 1.0 / n.D[(size_t)g * n.np + ia], v);
+          ++p, ++q;
+        }
+      }
+    }
+    if (a == b) v = fma(LDL[h2 + nf * h], (double)(n.unit_ptr[a + 1] - n.unit_ptr[a]), v);
+    Q[row + (size_t)N * c] = v;
+  }
+}
+
+// x[pos(q) nf + h] = rhs[q + np h]  (mode 0);  Eta[q + np h] = x[pos(q) nf + h]  (mode 2);
+// x[pos(q) nf + h] += normal(q, h, S_ETA + LEVEL_STRIDE r)  (mode 1, the noise of R's order)
+__global__ __launch_bounds__(256) void nngp_perm_kernel(SpArgs a, NnArgs n, const double* rhs, double* x, int mode) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n.N) return;
+  const int q = e % n.np, h = e / n.np, k = n.pos[q] * n.nf + h;
+  if (mode == 0)
+    x[k] = rhs[e];
+  else if (mode == 1) {
+    if (!a.noise_zero) x[k] += normal(a.key, (uint32_t)q, (uint32_t)h, S_ETA + LEVEL_STRIDE * a.r, SWEEP_ITER(a));
+  } else
+    a.Eta[e] = x[k];
+}
+
+struct NnLayout {
+  size_t Q, x, rhs, ws, LDL, tot;
+};
+static NnLayout nn_layout(int np, int nfc) {
+  NnLayout o{};
+  const size_t N = (size_t)np * nfc;
+  o.Q = 0;
+  o.x = o.Q + N * N;
+  o.rhs = o.x + N + 8;
+  o.ws = o.rhs + N + 8;
+  o.LDL = o.ws + dense_ws_doubles((int)N);
+  o.tot = o.LDL + (size_t)nfc * nfc + 64;
+  return o;
+}
+
+static void launch_eta_nngp(State& s, int r, uint32_t iter) {
+  Level& L = s.lev[r];
+  const SpArgs a = sp_args(s, r, iter);
+  const NnArgs n = nn_args(s, r);
+  const NnLayout o = nn_layout(L.np, std::max(1, std::min(L.nfmax, s.NFmax)));
+  double* w = L.spWork;
+  double *Q = w + o.Q, *x = w + o.x, *rhs = w + o.rhs, *ws = w + o.ws, *LDL = w + o.LDL;
+  const int N = n.N, g1 = (N + 255) / 256;
+  if (L.nnAssembledN != N) {  // a new system size (updateNf): entries outside its band must be 0
+    HIP_OK(hipMemsetAsync(Q, 0, (size_t)N * N * sizeof(double), s.stream));
+    L.nnAssembledN = N;
+  }
+  sp_rhs_kernel<<<g1, 256, 0, s.stream>>>(a, rhs, LDL);
+  nngp_assemble_kernel<<<N, 64, 0, s.stream>>>(n, LDL, Q);
+  nngp_perm_kernel<<<g1, 256, 0, s.stream>>>(a, n, rhs, x, 0);
+  HIP_OK(hipGetLastError());
+  {
+    ProfScope pc(s, PROF_CHOL);
+    dense_potrf_lower(s.stream, Q, N, N, ws, s.dev_flags, n.bw);
+  }
+  dense_trsv_lower(s.stream, Q, N, N, x, 0, ws, n.bw);   // backsolve(R, fS, transpose = TRUE)
+  nngp_perm_kernel<<<g1, 256, 0, s.stream>>>(a, n, rhs, x, 1);
+  dense_trsv_lower(s.stream, Q, N, N, x, 1, ws, n.bw);   // backsolve(R, tmp2)
+  nngp_perm_kernel<<<g1, 256, 0, s.stream>>>(a, n, rhs, x, 2);
+  HIP_OK(hipGetLastError());
+}
+
+// ---- host setup (chain creation) ----
+void setup_nngp_level(State& s, int r, const double* crd, int sdim, int k, const double* alphapw, int G) {
+  Level& L = s.lev[r];
+  const int n = L.np;
+  HMSC_REQUIRE(crd != nullptr && sdim > 0, "NNGP level: pass the unit coordinates (sCoord); nearest neighbours are "
+                                           "not available for distance matrices (R/computeDataParameters.R:86-88)");
+  HMSC_REQUIRE(k >= 1 && k < n, "NNGP level: nNeighbours must be in [1, np - 1]");
+  auto d2 = [&](int i, int j) {
+    double t = 0.0;
+    for (int c = 0; c < sdim; ++c) {
+      const double u = crd[i + (size_t)n * c] - crd[j + (size_t)n * c];
+      t += u * u;
+    }
+    return t;
+  };
+  const int nth = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+  auto par_for = [&](int count, auto&& body) {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nth; ++t)
+      th.emplace_back([&, t] {
+        for (int i = t; i < count; i += nth) body(i);
+      });
+    for (auto& x : th) x.join();
+  };
+  // FNN::get.knn(s, k): the k nearest other units (exact Euclidean; ties to the lower index),
+  // sorted ascending, only earlier units kept (:93-104)
+  std::vector<int> nb((size_t)k * n, -1), cnt(n, 0);
+  par_for(n, [&](int i) {
+    std::vector<std::pair<double, int>> dj;
+    dj.reserve(n - 1);
+    for (int j = 0; j < n; ++j)
+      if (j != i) dj.emplace_back(d2(i, j), j);
+    std::partial_sort(dj.begin(), dj.begin() + k, dj.end());
+    std::vector<int> near;
+    for (int q = 0; q < k; ++q)
+      if (dj[q].second < i) near.push_back(dj[q].second);
+    std::sort(near.begin(), near.end());
+    cnt[i] = (int)near.size();
+    for (int q = 0; q < (int)near.size(); ++q) nb[(size_t)q * n + i] = near[q];
+  });
+  // Vecchia factor per grid point: A[i, nb] = K11^-1 k12, D[i] = 1 - k21 K11^-1 k12 (:105-126)
+  std::vector<double> A((size_t)G * k * n, 0.0), D((size_t)G * n, 1.0), det(G, 0.0);
+  par_for(G, [&](int g) {
+    const double al = alphapw[g];
+    if (al == 0.0) return;  // iW = RiW = I, detW = 0
+    std::vector<double> Km((size_t)k * k), v(k);
+    double ld = 0.0;
+    for (int i = 0; i < n; ++i) {
+      const int m = cnt[i];
+      if (m == 0) continue;  // D[i] = 1
+      for (int p = 0; p < m; ++p) {
+        const int jp = nb[(size_t)p * n + i];
+        v[p] = std::exp(-std::sqrt(d2(jp, i)) / al);
+        for (int q = 0; q <= p; ++q) Km[p + (size_t)k * q] = std::exp(-std::sqrt(d2(jp, nb[(size_t)q * n + i])) / al);
+      }
+      for (int c = 0; c < m; ++c) {  // Cholesky of K11 (lower, in place)
+        double dd = Km[c + (size_t)k * c];
+        for (int q = 0; q < c; ++q) dd -= Km[c + (size_t)k * q] * Km[c + (size_t)k * q];
+        HMSC_REQUIRE(dd > 0.0, "NNGP level: a neighbour covariance is not positive definite (duplicated coordinates?)");
+        dd = std::sqrt(dd);
+        Km[c + (size_t)k * c] = dd;
+        for (int p = c + 1; p < m; ++p) {
+          double t = Km[p + (size_t)k * c];
+          for (int q = 0; q < c; ++q) t -= Km[p + (size_t)k * q] * Km[c + (size_t)k * q];
+          Km[p + (size_t)k * c] = t / dd;
+        }
+      }
+      std::vector<double> y(v.begin(), v.begin() + m);
+      for (int p = 0; p < m; ++p) {  // L y = k12
+        for (int q = 0; q < p; ++q) y[p] -= Km[p + (size_t)k * q] * y[q];
+        y[p] /= Km[p + (size_t)k * p];
+      }
+      double Di = 1.0;
+      for (int p = 0; p < m; ++p) Di -= y[p] * y[p];
+      for (int p = m - 1; p >= 0; --p) {  // L' a = y
+        for (int q = p + 1; q < m; ++q) y[p] -= Km[q + (size_t)k * p] * y[q];
+        y[p] /= Km[p + (size_t)k * p];
+      }
+      HMSC_REQUIRE(Di > 0.0, "NNGP level: a conditional variance is not positive");
+      for (int p = 0; p < m; ++p) A[((size_t)g * k + p) * n + i] = y[p];
+      D[(size_t)g * n + i] = Di;
+      ld += std::log(Di);
+    }
+    det[g] = ld;  // detW = sum(log(D))
+  });
+  // reverse Cuthill-McKee over the units that share a row support (oracle nngp_rcm)
+  std::vector<std::vector<int>> adj(n);
+  for (int i = 0; i < n; ++i) {
+    std::vector<int> sup{i};
+    for (int p = 0; p < cnt[i]; ++p) sup.push_back(nb[(size_t)p * n + i]);
+    for (int u : sup)
+      for (int w : sup)
+        if (u != w) adj[u].push_back(w);
+  }
+  std::vector<int> deg(n);
+  for (int u = 0; u < n; ++u) {
+    std::sort(adj[u].begin(), adj[u].end());
+    adj[u].erase(std::unique(adj[u].begin(), adj[u].end()), adj[u].end());
+    deg[u] = (int)adj[u].size();
+  }
+  std::vector<char> seen(n, 0);
+  std::vector<int> order;
+  order.reserve(n);
+  while ((int)order.size() < n) {
+    int start = -1;
+    for (int u = 0; u < n; ++u)
+      if (!seen[u] && (start < 0 || deg[u] < deg[start])) start = u;
+    seen[start] = 1;
+    size_t head = order.size();
+    order.push_back(start);
+    while (head < order.size()) {
+      const int v = order[head++];
+      std::vector<int> nx;
+      for (int u : adj[v])
+        if (!seen[u]) nx.push_back(u);
+      std::sort(nx.begin(), nx.end(), [&](int x, int y) { return deg[x] != deg[y] ? deg[x] < deg[y] : x < y; });
+      for (int u : nx) {
+        seen[u] = 1;
+        order.push_back(u);
+      }
+    }
+  }
+  std::reverse(order.begin(), order.end());
+  std::vector<int> pos(n);
+  for (int p = 0; p < n; ++p) pos[order[p]] = p;
+  int bwu = 0;
+  for (int u = 0; u < n; ++u)
+    for (int w : adj[u]) bwu = std::max(bwu, std::abs(pos[u] - pos[w]));
+  // rows whose support holds each unit, ascending row (children CSR)
+  std::vector<int> chptr(n + 1, 0), ch;
+  {
+    std::vector<std::vector<int>> lists(n);
+    for (int i = 0; i < n; ++i) {
+      lists[i].push_back(i * (k + 1));
+      for (int p = 0; p < cnt[i]; ++p) lists[nb[(size_t)p * n + i]].push_back(i * (k + 1) + p + 1);
+    }
+    for (int u = 0; u < n; ++u) {
+      std::sort(lists[u].begin(), lists[u].end());
+      chptr[u + 1] = chptr[u] + (int)lists[u].size();
+      ch.insert(ch.end(), lists[u].begin(), lists[u].end());
+    }
+  }
+  L.nngp = true;
+  L.nnK = k;
+  L.nnIdx = dupload_i32(nb.data(), nb.size());
+  L.nnA = dupload_f64(A.data(), A.size());
+  L.nnD = dupload_f64(D.data(), D.size());
+  L.detWg = dupload_f64(det.data(), det.size());
+  L.nnPerm = dupload_i32(order.data(), order.size());
+  L.nnPos = dupload_i32(pos.data(), pos.size());
+  L.nnChPtr = dupload_i32(chptr.data(), chptr.size());
+  L.nnCh = dupload_i32(ch.data(), ch.size());
+  L.nnBwUnits = bwu;
+}
+
 // np * nf above which updateEta's dense system goes to the multi-workgroup blocked path
 constexpr int SP_BLOCKED_N = 1024;
 
@@ -561,6 +909,9 @@ size_t spatial_work_doubles(const State& s, int r) {
   const Level& L = s.lev[r];
   const size_t nfc = std::max(1, std::min(L.nfmax, s.NFmax));
   if (L.gpp) return gpp_layout(L.np, (int)nfc, L.nK, L.nalpha).tot + 64;
+  if (L.nngp)
+    return std::max(nn_layout(L.np, (int)nfc).tot,
+                    (size_t)L.nalpha * ((L.np + 255) / 256) * nfc) + 64;
   const size_t N = (size_t)L.np * nfc;
   const size_t eta = N * N + N + dense_ws_doubles((int)N) + nfc * nfc + 64;
   const size_t alpha = (size_t)L.nalpha * ((L.np + 255) / 256) * std::max(1, std::min(L.nfmax, s.NFmax));
@@ -574,6 +925,10 @@ void launch_eta_spatial(State& s, int r, uint32_t iter) {
   ProfScope ps(s, PROF_ETA_SP);
   if (L.gpp) {
     launch_eta_gpp(s, r, iter);
+    return;
+  }
+  if (L.nngp) {
+    launch_eta_nngp(s, r, iter);
     return;
   }
   const SpArgs a = sp_args(s, r, iter);
@@ -620,7 +975,10 @@ void launch_alpha(State& s, uint32_t iter) {
       HIP_OK(hipGetLastError());
       continue;
     }
-    alpha_quad_kernel<<<dim3(L.nalpha, (L.np + 255) / 256), 256, 0, s.stream>>>(a);
+    if (L.nngp)
+      nngp_alpha_kernel<<<dim3(L.nalpha, (L.np + 255) / 256), 256, 0, s.stream>>>(a, nn_args(s, r));
+    else
+      alpha_quad_kernel<<<dim3(L.nalpha, (L.np + 255) / 256), 256, 0, s.stream>>>(a);
     HIP_OK(hipGetLastError());
     alpha_draw_kernel<<<1, 256, 0, s.stream>>>(a);
     HIP_OK(hipGetLastError());

@@ -48,6 +48,19 @@ struct Level {
   double* idDW12g = nullptr;    // np x nK x nalpha
   double* Fg = nullptr;         // nK x nK x nalpha
   double* iFg = nullptr;        // nK x nK x nalpha
+  // 'NNGP' level in the sparse Vecchia form (spatial.hip, R/computeDataParameters.R:82-136):
+  // RiW_g = D_g^-1/2 (I - A_g), A_g[i, nb(i, k)] over the nnK nearest earlier units
+  bool nngp = false;
+  int nnK = 0;                  // neighbours per unit (rL$nNeighbours)
+  int* nnIdx = nullptr;         // nnK x np: earlier neighbours of unit i (ascending), -1 padded
+  double* nnA = nullptr;        // nalpha x nnK x np: Vecchia coefficients A_g[i, nb(i, k)]
+  double* nnD = nullptr;        // nalpha x np: conditional variances D_g[i]
+  int* nnPerm = nullptr;        // np: unit at each position of the factorization order (RCM)
+  int* nnPos = nullptr;         // np: position of each unit
+  int* nnChPtr = nullptr;       // np + 1: CSR of the rows whose support {i} + nb(i) holds the unit
+  int* nnCh = nullptr;          // entries i (nnK + 1) + slot, slot 0 = the unit itself (B = 1), ascending i
+  int nnBwUnits = 0;            // bandwidth of the precision in units (RCM order)
+  int nnAssembledN = 0;         // size of the last assembled system (its band layout zeroed for it)
 };
 
 struct State {
@@ -86,6 +99,7 @@ struct State {
   // model (device)
   double *X = nullptr, *Tr = nullptr, *Yval = nullptr, *Yraw = nullptr;
   int8_t* Ycode = nullptr;
+  uint64_t* Ybits = nullptr;     // ceil(nsl / 32) x ny: the same codes + 1, 2 bits per species (z kernel)
   int* fam = nullptr;            // ns_loc family code
   int* varest = nullptr;         // ns_loc distr[,2]
   double *V0 = nullptr, *iUGamma = nullptr, *mGamma = nullptr, *UGammaL = nullptr, *UGamma = nullptr;
@@ -173,6 +187,8 @@ struct State {
   int graph_K = -1, graph_NF = -1;
   hipGraphExec_t gexec = nullptr;
   hipGraphExec_t gexec_rec = nullptr;  // the same sweeps, each followed by the record pack
+  hipGraphExec_t gexec1 = nullptr;     // one sweep (run lengths that are not a multiple of graph_sweeps)
+  hipGraphExec_t gexec1_rec = nullptr;
   bool single_stream = false;          // HMSC_SINGLE_STREAM: no side-stream overlap (diagnostic)
   int graph_sweeps = 4;                 // sweeps per replay (HMSC_GRAPH_SWEEPS)
   int32_t* d_rec_desc = nullptr;        // {iter0, transient, thin, samples} of the current run
@@ -276,8 +292,10 @@ void launch_rho(State& s, uint32_t iter, hipStream_t st);
 void launch_beta_lambda_phylo(State& s, uint32_t iter);
 void launch_side_fused(State& s, uint32_t iter);
 // blocked dense fp64 factorisation / solves (dense.hip)
-void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, int* info);
-void dense_trsv_lower(hipStream_t st, const double* L, int n, int lda, double* x, int trans, double* ws);
+// bw > 0: A is banded (A[i, j] = 0 for i - j > bw, entries outside the band zero on entry);
+// the factor keeps the band, and only the band's tiles are touched (n bw^2 work instead of n^3)
+void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, int* info, int bw = 0);
+void dense_trsv_lower(hipStream_t st, const double* L, int n, int lda, double* x, int trans, double* ws, int bw = 0);
 void dense_trtri_lower(hipStream_t st, const double* L, int ldl, int n, double* M, int ldm, double* dinv,
                        bool have_dinv);
 // workspace of dense_potrf_lower + dense_trsv_lower: the 64 x 64 diagonal-block inverses, then n
@@ -293,6 +311,9 @@ void spatial_full_grid(hipStream_t st, int np, int sdim, const double* coords, c
                        const double* alphas, int G, double* iWg, double* RiWg, double* detWg, int* info);
 // spatial "Full" levels (spatial.hip)
 size_t spatial_work_doubles(const State& s, int r);
+// NNGP level setup on the host: nearest earlier neighbours, Vecchia coefficients over the
+// alphapw grid, detWg, the RCM factorization order and its bandwidth (device arrays of Level)
+void setup_nngp_level(State& s, int r, const double* coords, int sdim, int k, const double* alphapw, int G);
 void launch_eta_spatial(State& s, int r, uint32_t iter);
 void launch_alpha(State& s, uint32_t iter);
 // updateGammaEta (gamma_eta.hip)

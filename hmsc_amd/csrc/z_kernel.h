@@ -28,13 +28,15 @@ namespace hmsc {
 // XEta and Ycode are allocated with padding (capi.cpp build_state) so the kernel loads them
 // unguarded: XEta holds ny * 16 ceil(Kmax / 16) + 64 doubles (finite; columns >= K and the
 // rows past ny of the last tile only ever meet zero BL rows / zeroed Z), Ycode ny (nsl + 32) + 64
-// bytes (zero past the last species).
+// bytes (zero past the last species), Ybits ceil(nsl / 32) ny + 64 words (code 0 past the last
+// species and site).
 struct ZArgs {
   const double* XEta;  // ny x K (ld ny)
   int ny, K, ns_loc, sp0, nt, tiles_per_chunk;
   const double* BL;
   const double* iSigma;
   const int8_t* Ycode;
+  const uint64_t* Ybits;  // [species block][site]: 2 bits per species (code + 1: 0 NA, 1 zero, 2 one)
   const double* Yval;
   const int* fam;
   const double* Tr;  // local species rows, ld ns_loc
@@ -131,7 +133,7 @@ __device__ __forceinline__ ZPair z_probit_pair(double e0, double e1, double sd0,
       g0 = fma_sc(g0, x0, kErfcPoly[k]);
       g1 = fma_sc(g1, x1, kErfcPoly[k]);
     }
-    const double r0 = t0 * exp(fma(-a0, a0, g0)), r1 = t1 * exp(fma(-a1, a1, g1));
+    const double r0 = t0 * exp_small(fma(-a0, a0, g0)), r1 = t1 * exp_small(fma(-a1, a1, g1));
     const double p0 = u0 * (0.5 * (h0 < 0.0 ? 2.0 - r0 : r0));
     const double p1 = u1 * (0.5 * (h1 < 0.0 ? 2.0 - r1 : r1));
     // w = -log_fast(4 p (1 - p)) for both cells, interleaved
@@ -160,19 +162,29 @@ __device__ __forceinline__ ZPair z_probit_pair(double e0, double e1, double sd0,
     const double d0 = (double)ex0, d1 = (double)ex1;
     const double w0 = -fma(d0, 0.6931471803691238, fma(d0, 1.9082149292705877e-10, l0));
     const double w1 = -fma(d1, 0.6931471803691238, fma(d1, 1.9082149292705877e-10, l1));
-    if (w0 < 6.25 && w1 < 6.25) {  // qnorm_fast's central branch for both cells
-      const double y0 = w0 - 3.125, y1 = w1 - 3.125;
-      double F0 = kQnormA[0], F1 = kQnormA[0];
+    // qnorm_fast's central branch (w < 6.25) for both cells, on every lane
+    const double y0 = w0 - 3.125, y1 = w1 - 3.125;
+    double F0 = kQnormA[0], F1 = kQnormA[0];
 #pragma unroll
-      for (int k = 1; k < 23; ++k) {
-        F0 = fma_sc(F0, y0, kQnormA[k]);
-        F1 = fma_sc(F1, y1, kQnormA[k]);
+    for (int k = 1; k < 23; ++k) {
+      F0 = fma_sc(F0, y0, kQnormA[k]);
+      F1 = fma_sc(F1, y1, kQnormA[k]);
+    }
+    q0 = (2.0 * p0 - 1.0) * F0;
+    q1 = (2.0 * p1 - 1.0) * F1;
+    if (w0 >= 6.25 || w1 >= 6.25) {
+      // a lane with a cell in qnorm_fast's outer branches (p within 4.8e-4 of 0 or 1: about
+      // a third of the wave iterations on a fitted probit model hold one): region B for both
+      // cells, reusing w -- not the whole quantile again -- and AS241's tail below p < 2.8e-8
+      const double sw0 = sqrt(fmax(w0, 6.25)) - 3.25, sw1 = sqrt(fmax(w1, 6.25)) - 3.25;
+      double B0 = kQnormB[0], B1 = kQnormB[0];
+#pragma unroll
+      for (int k = 1; k < 19; ++k) {
+        B0 = fma_sc(B0, sw0, kQnormB[k]);
+        B1 = fma_sc(B1, sw1, kQnormB[k]);
       }
-      q0 = (2.0 * p0 - 1.0) * F0;
-      q1 = (2.0 * p1 - 1.0) * F1;
-    } else {
-      q0 = qnorm_fast(p0);
-      q1 = qnorm_fast(p1);
+      if (w0 >= 6.25) q0 = w0 < 16.0 ? (2.0 * p0 - 1.0) * B0 : qnorm_as241_tail_t(p0, kLogSeries);
+      if (w1 >= 6.25) q1 = w1 < 16.0 ? (2.0 * p1 - 1.0) * B1 : qnorm_as241_tail_t(p1, kLogSeries);
     }
   }
   ZPair z;
@@ -251,7 +263,11 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
     g_reduce_body(a, smem);
     return;
   }
-  const int by = (int)blockIdx.y - a.gred_y0;  // species block
+  // grid (species blocks, site chunks): the workgroups of one site chunk are consecutive in
+  // dispatch order, so its XEta rows are fetched once per XCD (round-robin placement) while
+  // they are L2-resident, instead of once per species block
+  const int by = (int)blockIdx.x;                   // species block
+  const int chunk = (int)blockIdx.y - a.gred_y0;    // site chunk
   const unsigned long long kt0 = a.kt ? kt_now() : 0ull;
   constexpr int K16 = 16 * NKB;
   const int K = a.K, K4 = (K + 3) & ~3;
@@ -289,25 +305,18 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
   for (int q = 0; q < NKB; ++q) acc[q][0] = acc[q][1] = d4{0.0, 0.0, 0.0, 0.0};
 
   const int n_tiles = (ny + ZT_I - 1) / ZT_I;
-  const int tb = blockIdx.x * a.tiles_per_chunk;
+  const int tb = chunk * a.tiles_per_chunk;
   const int te = min(n_tiles, tb + a.tiles_per_chunk);
   for (int tile = tb; tile < te; ++tile) {
     const int i0 = tile * ZT_I + 16 * w;
     if (i0 >= ny) break;
     // ---- this lane's 8 Y codes (site i0 + lm, species j0 + 2(4c + lk) + b), loaded before
     //      the E contraction so their latency overlaps it; 4 bits each, code + 1
-    uint32_t ycodes = 0;
-    if (DRAW) {
-      const int i = i0 + lm;
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const int j = j0 + 2 * (4 * c + lk) + b;
-          const int code = a.Ycode[(size_t)i + (size_t)ny * j];  // padded buffer (ZArgs)
-          ycodes |= (uint32_t)(code + 1) << (8 * c + 4 * b);
-        }
-    }
+    //      (one 8-byte word per site and species block: 2 bits per species, code + 1)
+    uint64_t yw = 0;
+    if (DRAW) yw = a.Ybits[(size_t)by * ny + (i0 + lm)];  // padded buffer (ZArgs)
+    // code of species jj = 2 (4 c + lk) + b of this lane's site
+    auto ycode_of = [&](int c, int b) { return (int)((yw >> (16 * c + 4 * lk + 2 * b)) & 3u) - 1; };
     // ---- E = XEta BL for 16 sites x 32 species (R/updateZ.R:11-34); T[2m+b][lk+4r] <- E
     if (DRAW) {
       d4 e0 = {0.0, 0.0, 0.0, 0.0}, e1 = {0.0, 0.0, 0.0, 0.0};
@@ -349,7 +358,7 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
         if (DRAW && !POIS && (MODE & 2)) {
           // probit / NA pair (the whole chain is probit, or the pair's species are):
           // both draws inline with interleaved chains; normal species keep Z = Y
-          const int cd0 = (int)((ycodes >> (8 * c)) & 15u) - 1, cd1 = (int)((ycodes >> (8 * c + 4)) & 15u) - 1;
+          const int cd0 = ycode_of(c, 0), cd1 = ycode_of(c, 1);
           const int jj0 = 2 * m, jj1 = 2 * m + 1;
           const bool in0 = i < ny && ja < a.ns_loc, in1 = i < ny && ja + 1 < a.ns_loc;
           const double e0 = sT[jj0 * ZT_TLD + s], e1 = sT[jj1 * ZT_TLD + s];
@@ -372,7 +381,7 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
           if (i < ny && j < a.ns_loc) {
             const size_t cell = (size_t)i + (size_t)ny * j;
             if (DRAW) {
-              const int code = a.Ycode[cell];
+              const int code = ycode_of(c, b);
               const double e = sT[jj * ZT_TLD + s];
               if (sFam[jj] == 1 && code >= 0)
                 z = a.Yval[cell];  // normal: Z = Y   R/updateZ.R:40-41
@@ -427,10 +436,10 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
         const int ir = i0 + 4 * r + lk;
         double z0 = sT[(2 * lm) * ZT_TLD + lk + 4 * r];
         double z1 = sT[(2 * lm + 1) * ZT_TLD + lk + 4 * r];
-        if (HAS_NA && ir < ny) {
-          const int ja = j0 + 2 * lm;
-          if (ja < a.ns_loc && a.Ycode[(size_t)ir + (size_t)ny * ja] < 0) z0 = 0.0;
-          if (ja + 1 < a.ns_loc && a.Ycode[(size_t)ir + (size_t)ny * (ja + 1)] < 0) z1 = 0.0;
+        if (HAS_NA) {  // NA cells (code + 1 == 0) out of the contraction
+          const uint64_t w2 = a.Ybits[(size_t)by * ny + ir];  // padded buffer: ir < ny + 64
+          if (((w2 >> (4 * lm)) & 3u) == 0) z0 = 0.0;
+          if (((w2 >> (4 * lm + 2)) & 3u) == 0) z1 = 0.0;
         }
 #pragma unroll
         for (int q = 0; q < NKB; ++q) {  // rows >= K are discarded, sites >= ny have Z = 0
@@ -455,7 +464,7 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
   }
   __syncthreads();
   if (w == 0) {
-    double* dst = a.XZ_part + (size_t)blockIdx.x * K * a.ns_loc;
+    double* dst = a.XZ_part + (size_t)chunk * K * a.ns_loc;
 #pragma unroll
     for (int q = 0; q < NKB; ++q)
 #pragma unroll

@@ -78,6 +78,7 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   a.BL = s.BL;
   a.iSigma = s.iSigma;
   a.Ycode = s.Ycode;
+  a.Ybits = s.Ybits;
   a.Yval = use_raw_y ? s.Yraw : s.Yval;
   a.fam = s.fam;
   a.Tr = s.Tr;
@@ -90,7 +91,7 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   a.noise_zero = s.noise_mode;
   a.zprev_is_e = use_raw_y;  // only the init draw reads hM$Y (R/computeInitialParameters.R:254)
   a.kt = s.kt_on ? s.d_kt + (size_t)KT_Z * 2 * KT_SLOTS : nullptr;
-  dim3 grid(nchunk, s.ntile_j);
+  dim3 grid(s.ntile_j, nchunk);  // species blocks fastest (z_kernel.h)
   size_t smem = z_smem_bytes(s.K, s.nt);
   if (draw && s.g_pending) {  // G's Eta rows reduced on an extra first grid row
     a.gred_y0 = 1;

@@ -81,8 +81,13 @@ class ModelBuffers:
             # computeDataParameters' alphapw grid (R/computeDataParameters.R:53-81); the R shim
             # would pass dataParList$rLPar[[r]]$iWg / RiWg / detWg
             from .dataparams import _level_order, spatialDataParameters
-            on_device = [bool(lv.sDim) and spatial_grid == "device" and lv.spatialMethod == "Full" for lv in rl]
+            # 'Full' (spatial_grid="device") and 'NNGP' levels hand over their coordinates: the
+            # library builds the Full grid on the device and the NNGP Vecchia factor itself
+            on_device = [bool(lv.sDim) and ((spatial_grid == "device" and lv.spatialMethod == "Full")
+                                            or lv.spatialMethod == "NNGP") for lv in rl]
             rlp = spatialDataParameters(hM, skip=on_device, gpp_dense=False)
+            m.nNeighbours = L.colmajor_ptr([int(lv.nNeighbours or 10) if lv.sDim and lv.spatialMethod == "NNGP" else 0
+                                            for lv in rl], k, np.int32)
             m.nalpha = L.colmajor_ptr([r.alphapw.shape[0] if r.sDim else 0 for r in rl], k, np.int32)
             m.nKnots = L.colmajor_ptr([rlp[r]["Fg"].shape[0] if lv.sDim and lv.spatialMethod == "GPP" else 0
                                        for r, lv in enumerate(rl)], k, np.int32)
@@ -92,6 +97,8 @@ class ModelBuffers:
                 m.alphapw[r] = L.colmajor_ptr(np.asarray(lv.alphapw, dtype=np.float64), k)
                 if on_device[r]:
                     idx = _level_order(hM, r, lv)
+                    if lv.spatialMethod == "NNGP" and lv.distMat is not None:
+                        raise ValueError("computeDataParameters: Nearest neighbours not available for distance matrices")
                     if lv.distMat is None:
                         m.sCoord[r] = L.colmajor_ptr(np.asarray(lv.s, dtype=np.float64)[idx], k)
                     else:

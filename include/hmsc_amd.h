@@ -46,8 +46,12 @@ enum hmsc_updater {
 };
 
 /* The hM fields consumed by the sampler (R/Hmsc.R:118-167 after construction and
- * setPriors defaults R/setPriors.Hmsc.R:28-77, R/setPriors.HmscRandomLevel.R:31-108). */
+ * setPriors defaults R/setPriors.Hmsc.R:28-77, R/setPriors.HmscRandomLevel.R:31-108).
+ * Zero-initialise the struct and set struct_size = sizeof(hmsc_model) (HMSC_MODEL_SIZE):
+ * hmsc_create refuses any other value, so a caller built against an older header (a shorter
+ * struct) gets an error instead of having fields read past its end. */
 typedef struct hmsc_model {
+  int32_t struct_size;    /* sizeof(hmsc_model) of the header the caller was built with */
   int32_t ny, ns, nc, nt, nr;
   const double* Y;        /* ny*ns  hM$YScaled (NaN = NA)                      */
   const double* Yraw;     /* ny*ns  hM$Y (initial Z, R/computeInitialParameters.R:254); may equal Y */
@@ -88,7 +92,7 @@ typedef struct hmsc_model {
    * [np, np, alphaN] arrays) with RiWg' RiWg = iWg, detWg nalpha = log det W.  RiWg is
    * upper triangular, except for NNGP (R's lower-triangular factor) and GPP (lower).
    *   Full: computeDataParameters' iWg / RiWg / detWg as they are (:53-81).
-   *   NNGP: as.matrix(iWg[[g]]), as.matrix(RiWg[[g]]) (the Vecchia factor), detWg (:82-136).
+   *   NNGP: not through these arrays -- sCoord and nNeighbours below (sparse Vecchia form).
    *   GPP:  iWg = diag(idDg[,g]) - idDW12g[,,g] iFg[,,g] t(idDW12g[,,g]) = W^-1, passed as
    *         RiWg = solve(t(chol(W))) (lower) with W = D + W12 iW22 t(W12), iWg = t(RiWg) RiWg,
    *         detWg = detDg (:138-194; the precision R/updateEta.R:148-196 samples from).
@@ -96,7 +100,7 @@ typedef struct hmsc_model {
   const int32_t* spatialMethod;              /* nr: 0 none, 1 Full, 2 NNGP, 3 GPP        */
   const int32_t* nalpha;                     /* nr: nrow(rL$alphapw)                     */
   const double* alphapw[HMSC_MAX_LEVELS];    /* nalpha*2: grid value, prior weight      */
-  const double* iWg[HMSC_MAX_LEVELS];
+  const double* iWg[HMSC_MAX_LEVELS];      /* Full (host grid) only; NNGP: see sCoord */
   const double* RiWg[HMSC_MAX_LEVELS];
   const double* detWg[HMSC_MAX_LEVELS];
   /* 'Full' levels may leave iWg / RiWg / detWg NULL and hand over the level's geometry
@@ -119,7 +123,16 @@ typedef struct hmsc_model {
   const double* Fg[HMSC_MAX_LEVELS];
   const double* iFg[HMSC_MAX_LEVELS];
   const double* detDg[HMSC_MAX_LEVELS];
+  /* 'NNGP' levels (spatialMethod 2) hand over the coordinates of their units (sCoord[r], unit
+   * order) and rL$nNeighbours (nNeighbours[r]; R's default 10): the library finds the nearest
+   * earlier neighbours (FNN::get.knn restated), evaluates the Vecchia factor of every alphapw
+   * grid point (R/computeDataParameters.R:82-136) and samples in that sparse form (np nNeighbours
+   * numbers per grid point; updateEta factors the band of the precision in reverse Cuthill-McKee
+   * order).  NNGP levels never take iWg / RiWg. */
+  const int32_t* nNeighbours;                /* nr (entries of non-NNGP levels ignored) */
 } hmsc_model;
+
+#define HMSC_MODEL_SIZE ((int32_t)sizeof(hmsc_model))
 
 /* Sampler state = R's parList (R/computeInitialParameters.R:256-270) with iV in
  * place of V and iSigma in place of sigma, as sampleChain keeps them

@@ -132,7 +132,45 @@ def _nngp_data_parameters(rl):
                 RiW[i, :] /= np.sqrt(Di)
                 detWg[g] += np.log(Di)
         iWg[g], RiWg[g] = RiW.T @ RiW, RiW
-    return dict(iWg=iWg, RiWg=RiWg, detWg=detWg)
+    perm, bw = nngp_rcm(nb, n)
+    return dict(iWg=iWg, RiWg=RiWg, detWg=detWg, nb=nb, perm=perm, bw_units=bw)
+
+
+def nngp_rcm(nb, n):
+    """The unit order in which the device factors an NNGP level's precision (hmsc_amd/csrc/
+    nngp.hip, nngp_setup): reverse Cuthill-McKee on the graph whose edges join units that share a
+    row of the Vecchia factor (the support {i} + nb[i] of row i), BFS from the unvisited unit of
+    least degree (lowest index on ties), neighbours visited by increasing (degree, index), the
+    visit order reversed.  Returns perm (perm[k] = unit at position k) and the bandwidth in
+    units, max |pos[a] - pos[b]| over edges.  Not a reference function: R factors the sparse
+    precision with CHOLMOD in its own order; any order gives the same conditional."""
+    adj = [set() for _ in range(n)]
+    for i in range(n):
+        sup = [i] + list(nb[i])
+        for a in sup:
+            for b in sup:
+                if a != b:
+                    adj[a].add(b)
+    adj = [sorted(a) for a in adj]
+    deg = [len(a) for a in adj]
+    seen = [False] * n
+    order = []
+    while len(order) < n:
+        start = min((i for i in range(n) if not seen[i]), key=lambda i: (deg[i], i))
+        seen[start] = True
+        q, head = [start], 0
+        while head < len(q):
+            v = q[head]
+            head += 1
+            for u in sorted((u for u in adj[v] if not seen[u]), key=lambda u: (deg[u], u)):
+                seen[u] = True
+                q.append(u)
+        order.extend(q)
+    perm = np.array(order[::-1], dtype=np.int64)
+    pos = np.empty(n, dtype=np.int64)
+    pos[perm] = np.arange(n)
+    bw = max((abs(int(pos[a]) - int(pos[b])) for a in range(n) for b in adj[a]), default=0)
+    return perm, bw
 
 
 def _gpp_data_parameters(rl):
@@ -579,11 +617,25 @@ def _eta_spatial_full(st, model, r, S, dp, rng, it, zero_noise):
     for h in range(nf):
         iU[h * npr:(h + 1) * npr, h * npr:(h + 1) * npr] += iWg[alpha[h] - 1]
     fS = (P.T @ S) @ (lam * iS[None, :]).T
+    xi = None if zero_noise else \
+        rng.normal(np.arange(npr)[:, None], np.arange(nf)[None, :], R.S_ETA + R.LEVEL_STRIDE * r, it).ravel(order="F")
+    if model["rL"][r].get("spatialMethod", "Full") == "NNGP":
+        # the device factors the sparse NNGP precision in RCM order, factors interleaved per unit
+        # (index pos[q] nf + h, nngp.hip): eta = P' L^-T (L^-1 P vec(fS) + P xi), L L' = P iUEta P'
+        # -- the same conditional, the noise of (unit q, factor h) as in R's order
+        perm = dp["rLPar"][r]["perm"]
+        ix = (perm[:, None] + npr * np.arange(nf)[None, :]).ravel()   # position-major, factor fastest
+        Rm = chol_upper(iU[np.ix_(ix, ix)])
+        tmp2 = backsolve(Rm, fS.ravel(order="F")[ix], transpose=True)
+        if xi is not None:
+            tmp2 = tmp2 + xi[ix]
+        out = np.empty(npr * nf)
+        out[ix] = backsolve(Rm, tmp2)
+        return out.reshape((npr, nf), order="F")
     Rm = chol_upper(iU)
     tmp2 = backsolve(Rm, fS.ravel(order="F"), transpose=True)
-    if not zero_noise:
-        xi = rng.normal(np.arange(npr)[:, None], np.arange(nf)[None, :], R.S_ETA + R.LEVEL_STRIDE * r, it)
-        tmp2 = tmp2 + xi.ravel(order="F")
+    if xi is not None:
+        tmp2 = tmp2 + xi
     return backsolve(Rm, tmp2).reshape((npr, nf), order="F")
 
 

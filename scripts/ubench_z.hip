@@ -46,12 +46,24 @@ int main(int argc, char** argv) {
   int8_t* Y;
   int* F;
   const int ntile_j = (ns + 31) / 32, n_tiles = (ny + 63) / 64;
-  (void)hipMalloc(&X, hX.size() * 8);
+  // XEta padded as the product's (z_kernel.h ZArgs: 16 ceil(K / 16) columns + 64)
+  (void)hipMalloc(&X, ((size_t)ny * 16 * ((K + 15) / 16) + 64) * 8);
+  (void)hipMemset(X, 0, ((size_t)ny * 16 * ((K + 15) / 16) + 64) * 8);
+  std::vector<uint64_t> hYb((size_t)ntile_j * ny + 64, 0x5555555555555555ull);
+  for (int j = 0; j < ns; ++j)
+    for (int i = 0; i < ny; ++i) {
+      uint64_t& w = hYb[(size_t)(j / 32) * ny + i];
+      const int sh = 2 * (j % 32);
+      w = (w & ~(3ull << sh)) | ((uint64_t)(hY[i + (size_t)ny * j] + 1) << sh);
+    }
+  uint64_t* Yb;
+  (void)hipMalloc(&Yb, hYb.size() * 8);
+  (void)hipMemcpy(Yb, hYb.data(), hYb.size() * 8, hipMemcpyHostToDevice);
   (void)hipMalloc(&BL, hBL.size() * 8);
   (void)hipMalloc(&Tr, ns * 8);
   (void)hipMalloc(&Is, ns * 8);
   (void)hipMalloc(&Z, (size_t)ny * ns * 8);
-  (void)hipMalloc(&Y, (size_t)ny * ns);
+  (void)hipMalloc(&Y, (size_t)ny * (ns + 32) + 64);
   (void)hipMalloc(&F, ns * 4);
   (void)hipMalloc(&XZp, (size_t)n_tiles * K * ns * 8);
   (void)hipMalloc(&ZTrp, (size_t)ntile_j * ny * 8);
@@ -74,10 +86,10 @@ int main(int argc, char** argv) {
     a.XEta = X; a.ny = ny; a.K = K; a.ns_loc = ns; a.sp0 = 0; a.nt = nt;
     a.tiles_per_chunk = (n_tiles + nchunk_req - 1) / nchunk_req;
     const int nchunk = (n_tiles + a.tiles_per_chunk - 1) / a.tiles_per_chunk;
-    a.BL = BL; a.iSigma = Is; a.Ycode = Y; a.Yval = nullptr; a.fam = F; a.Tr = Tr; a.Z = Z;
+    a.BL = BL; a.iSigma = Is; a.Ycode = Y; a.Ybits = Yb; a.Yval = nullptr; a.fam = F; a.Tr = Tr; a.Z = Z;
     a.XZ_part = XZp; a.ZTr_part = ZTrp; a.key = Key{7u, 9u}; a.iter = 3; a.noise_zero = 0;
     a.iter_dev = dIter;  // as in the product's graph replays
-    dim3 grid(nchunk, ntile_j);
+    dim3 grid(ntile_j, nchunk);
     printf("grid %d x %d (tiles/chunk %d)\n", nchunk, ntile_j, a.tiles_per_chunk);
     if (prof_only) {
       printf("  all                 %7.1f us\n", run<15>(a, grid, smem, 20));

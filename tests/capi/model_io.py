@@ -39,10 +39,13 @@ def model_arrays(hM):
     out["nalpha"] = _i([r.alphapw.shape[0] if r.sDim else 0 for r in rl] or [0])
     for r, lv in enumerate(rl):
         if lv.sDim:
-            if lv.spatialMethod != "Full" or lv.distMat is not None:
-                raise NotImplementedError("the shim test marshals 'Full' levels given by coordinates")
+            if lv.spatialMethod == "GPP" or lv.distMat is not None:
+                raise NotImplementedError("the shim test marshals 'Full' / 'NNGP' levels given by coordinates")
             out[f"alphapw{r}"] = _f(lv.alphapw)
             out[f"sCoord{r}"] = _f(np.asarray(lv.s, dtype=np.float64)[_level_order(hM, r, lv)])
+    if any(lv.sDim and lv.spatialMethod == "NNGP" for lv in rl):
+        out["nNeighbours"] = _i([int(lv.nNeighbours or 10) if lv.sDim and lv.spatialMethod == "NNGP" else 0
+                                 for lv in rl])
     if hM.C is not None:
         Cm = np.asarray(hM.C, dtype=np.float64)
         d, U = np.linalg.eigh(Cm)  # R: e = eigen(hM$C, symmetric = TRUE)

@@ -74,6 +74,7 @@ int main(int argc, char** argv) {
   /* ---- the shim's marshalling (hmsc_run_chain_R) ---- */
   hmsc_model mod;
   memset(&mod, 0, sizeof mod);
+  mod.struct_size = HMSC_MODEL_SIZE;
   const int32_t* dims = INT("dims");
   mod.ny = dims[0], mod.ns = dims[1], mod.nc = dims[2], mod.nt = dims[3], mod.nr = dims[4];
   mod.Y = DBL("Y"), mod.Yraw = DBL("Yraw"), mod.X = DBL("X"), mod.Tr = DBL("Tr");
@@ -102,6 +103,7 @@ int main(int argc, char** argv) {
     snprintf(nm, sizeof nm, "sCoord%d", r);
     mod.sCoord[r] = DBL(nm);
   }
+  mod.nNeighbours = INT("nNeighbours"); /* NNGP levels (NULL when the model has none) */
 
   hmsc_state* st = NULL;
   if (hmsc_create(&mod, seed, 0, mask, &st)) {

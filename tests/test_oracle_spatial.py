@@ -201,8 +201,9 @@ def test_gpp_knot_on_a_site():
 
 def test_model_buffers_full_grid_routing():
     """'Full' levels hand their coordinates (unit order) to the device by default and
-    computeDataParameters' arrays with spatial_grid='host'; NNGP passes its dense arrays, GPP
-    R's low-rank arrays (nKnots, idDg, idDW12g, Fg, iFg, detDg) and no np^2 array."""
+    computeDataParameters' arrays with spatial_grid='host'; NNGP its coordinates and
+    nNeighbours (the library builds the sparse Vecchia factor), GPP R's low-rank arrays (nKnots,
+    idDg, idDW12g, Fg, iFg, detDg); neither passes an np^2 array."""
     from hmsc_amd.sampler import ModelBuffers
     hM = _model("Full")
     b = ModelBuffers(hM)
@@ -215,6 +216,8 @@ def test_model_buffers_full_grid_routing():
     assert not bool(g.iWg[0]) and not bool(g.RiWg[0]) and not bool(g.sCoord[0])
     assert g.nKnots[0] > 0 and all(bool(getattr(g, f)[0]) for f in ("idDg", "idDW12g", "Fg", "iFg", "detDg"))
     n = ModelBuffers(_model("NNGP")).struct
-    assert bool(n.iWg[0]) and bool(n.RiWg[0])
+    assert not bool(n.iWg[0]) and not bool(n.RiWg[0]) and bool(n.sCoord[0])
+    assert n.nNeighbours[0] == int(_model("NNGP").rL[0].nNeighbours or 10)
+    assert m.struct_size == n.struct_size > 0
     with pytest.raises(ValueError):
         ModelBuffers(hM, spatial_grid="cpu")
