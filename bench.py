@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--workload", choices=["synthetic", "spatial", "phylo"], default="synthetic",
                    help="synthetic: config 4 (the metric); spatial: config 5, vignette_4 'Full' at --ny; "
                         "phylo: config 3, vignette_3 (phylogeny, traits, GammaEta) at --ns species")
-    p.add_argument("--method", choices=["Full", "GPP"], default="Full",
+    p.add_argument("--method", choices=["Full", "NNGP", "GPP"], default="Full",
                    help="config 5's spatial method (vignettes/vignette_4_spatial.Rmd:95-245)")
     p.add_argument("--ny", type=int, default=10000)
     p.add_argument("--ns", type=int, default=1000)
@@ -299,6 +299,7 @@ def main_spatial(args):
         tot, n = ch.profile_get(name)
         kern[name] = dict(total_ms=tot, launches=n, avg_us=1e3 * tot / max(1, n))
     ch.profile(False)
+    nngp_bw = int(ch.debug_get("nngp_bw0", 1)[0]) if args.method == "NNGP" else None
     ch.close()
     tmax = t_run
     if dist is not None:
@@ -325,6 +326,18 @@ def main_spatial(args):
                 "timer": "HIP events on the chain stream around the updater (eager sweeps)"}
         workload = (f"vignette_4 spatial 'GPP' ny={ny} ns=5 nc=2 nf=1, {nK} knots (knotDist 0.2), "
                     f"101-point alphapw grid, R's low-rank updateEta, updater GammaEta=FALSE, record every sweep")
+    elif args.method == "NNGP":
+        # band Cholesky of the NNGP precision in RCM order: sum over columns of (band rows)^2
+        bw = nngp_bw  # nf = 1: the matrix bandwidth is the unit bandwidth
+        flops = float(N) * bw * bw
+        roof = {"kernel": "band Cholesky of the NNGP Eta precision in RCM order (chol_diag/panel/update on the band)",
+                "bound": "mfma", "achieved": round(flops / max(chol_s, 1e-12) / 1e12, 3), "peak": peak_tf,
+                "unit": "TFLOP/s", "frac": round(flops / max(chol_s, 1e-12) / 1e12 / peak_tf, 5), "traffic": None,
+                "algorithmic_flops_per_launch": flops, "bandwidth": bw, "avg_launch_us": round(kern["chol"]["avg_us"], 1),
+                "timer": "HIP events on the chain stream around each factorization (eager sweeps)",
+                "note": "latency bound: ceil(np / 64) dependent diagonal-block steps"}
+        workload = (f"vignette_4 spatial 'NNGP' ny={ny} ns=5 nc=2 nf=1, 10 nearest neighbours, sparse Vecchia "
+                    f"factor over the 101-point alphapw grid, updater GammaEta=FALSE, record every sweep")
     else:
         roof = {"kernel": "blocked Cholesky of the (np nf)^2 Eta precision (chol_diag/panel/update)",
                 "bound": "mfma", "achieved": round(achieved, 2), "peak": peak_tf, "unit": "TFLOP/s",

@@ -60,6 +60,13 @@ class hmsc_predict_args(C.Structure):
                 ("np", ip), ("nf", ip), ("Eta", dp * MAX_LEVELS), ("Lambda", dp * MAX_LEVELS)]
 
 
+class hmsc_vp_args(C.Structure):
+    _fields_ = [("device", C.c_int32), ("ny", C.c_int32), ("ns", C.c_int32), ("nc", C.c_int32), ("nt", C.c_int32),
+                ("S", C.c_int32), ("ngroups", C.c_int32), ("nr", C.c_int32), ("group", ip), ("X", dp), ("Tr", dp),
+                ("cM", dp), ("Beta", dp), ("Gamma", dp), ("nf", ip), ("nfmax", C.c_int32 * MAX_LEVELS),
+                ("Lambda", dp * MAX_LEVELS)]
+
+
 class HmscNativeError(RuntimeError):
     pass
 
@@ -75,7 +82,7 @@ EXPORTS = ["hmsc_last_error", "hmsc_device_count", "hmsc_create", "hmsc_create_s
            "hmsc_destroy", "hmsc_init_state", "hmsc_init_z", "hmsc_set_state", "hmsc_get_state", "hmsc_get_nf", "hmsc_sweep",
            "hmsc_update", "hmsc_set_noise_mode", "hmsc_run", "hmsc_run_verbose", "hmsc_sync", "hmsc_debug_get",
            "hmsc_profile", "hmsc_profile_get", "hmsc_kernel_timing", "hmsc_kernel_timing_get", "hmsc_predict",
-           "hmsc_prepare_graphs"]
+           "hmsc_prepare_graphs", "hmsc_post_omega", "hmsc_variance_partitioning", "hmsc_effective_size"]
 
 
 def lib():
@@ -119,6 +126,9 @@ def lib():
     L.hmsc_kernel_timing_get.argtypes = [C.c_void_p, C.c_int32, dp, ip]
     L.hmsc_predict.argtypes = [C.POINTER(hmsc_predict_args), dp]
     L.hmsc_prepare_graphs.argtypes = [C.c_void_p, C.c_int32, ip]
+    L.hmsc_post_omega.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32, ip, dp, dp, dp, dp, dp]
+    L.hmsc_variance_partitioning.argtypes = [C.POINTER(hmsc_vp_args), dp]
+    L.hmsc_effective_size.argtypes = [C.c_int32, C.c_int32, C.c_int32, dp, dp, ip]
     _lib = L
     return L
 

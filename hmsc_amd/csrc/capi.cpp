@@ -1438,6 +1438,10 @@ using namespace hmsc;
 
 namespace hmsc {
 void run_predict(const hmsc_predict_args* p, double* out);  // predict.hip
+void post_omega(int device, int S, int ns, int nfmax, const int* nf, const double* Lambda, double* mean_cor,
+                double* support, double* support_neg, double* mean_omega);  // post.hip
+void post_vp(const hmsc_vp_args* v, double* out);
+void post_ess(int device, int n, int p, const double* x, double* ess, int* order);
 }
 
 extern "C" {
@@ -1449,6 +1453,32 @@ int hmsc_predict(const hmsc_predict_args* args, double* out) {
     HMSC_REQUIRE(args != nullptr && out != nullptr, "hmsc_predict: NULL argument");
     std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);  // it allocates (predict.hip)
     run_predict(args, out);
+  });
+}
+
+int hmsc_post_omega(int32_t device, int32_t S, int32_t ns, int32_t nfmax, const int32_t* nf, const double* Lambda,
+                    double* mean_cor, double* support, double* support_neg, double* mean_omega) {
+  return guarded([&] {
+    std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);  // it allocates
+    DeviceGuard dg(device);
+    post_omega(device, S, ns, nfmax, nf, Lambda, mean_cor, support, support_neg, mean_omega);
+  });
+}
+
+int hmsc_variance_partitioning(const hmsc_vp_args* args, double* out) {
+  return guarded([&] {
+    HMSC_REQUIRE(args != nullptr, "hmsc_variance_partitioning: NULL argument");
+    std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
+    DeviceGuard dg(args->device);
+    post_vp(args, out);
+  });
+}
+
+int hmsc_effective_size(int32_t device, int32_t n, int32_t p, const double* x, double* ess, int32_t* order) {
+  return guarded([&] {
+    std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
+    DeviceGuard dg(device);
+    post_ess(device, n, p, x, ess, order);
   });
 }
 

@@ -1902,6 +1902,146 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
   }
 }
 
+// Eight waves per 16-site tile (512 threads): the Z stream of stage 1 is split over twice the
+// waves (5000 on the synthetic config instead of 2500, every one resident at once: <= 80 VGPRs
+// for NFB <= 12, three workgroups per CU) and each wave keeps two batches of four steps'
+// loads in flight (double-buffered registers: the next batch is issued before the current
+// one's MFMAs), so the stream no longer drains at every batch boundary.  Stages 2-4 as in the
+// four-wave kernel; the eight ZL partials are added in a fixed tree.
+template <int NFB>
+__global__ __launch_bounds__(512, NFB <= 12 ? 6 : 4) void eta_fused8_kernel(EtaFArgs a) {
+  __shared__ double sPart[8][16][EF_SITES + 1];  // [wave][factor][site] ZL partials
+  __shared__ double sW[NFB * NFB];            // W = L^-1, L the lower factor of Q (row m at m NFB)
+  __shared__ double sWs[NFB * (NFB + 1)];     // wv_inv_lower_rows scratch
+  __shared__ double sB[NFB][EF_SITES], sXi[NFB][EF_SITES], sU[NFB][EF_SITES];
+  __shared__ double sX[64][EF_SITES + 1];     // XEta tile [k][site] (K <= 64)
+  __shared__ double sCR[64 * NFB];            // CR[k][h], k < K
+  const unsigned long long kt0 = a.kt ? kt_now() : 0ull;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, lm = lane & 15, lk = lane >> 4;
+  const int ny = a.ny, nf = a.nf, K = a.K, nc = a.nc, ns = a.ns_loc;
+  const int i0 = blockIdx.x * EF_SITES;
+  if (blockIdx.x == 0) HMSC_STAMP(50);
+  // ---- stage 1: ZL = Z (Lambda diag(iSigma))^T on the matrix cores, the HBM stream of the
+  // launch, issued first: species j = 16 s + 4 w + lk, B = LS[j][lm] straight from L2 (128 KB,
+  // shared by every workgroup); eight steps' loads in flight before their MFMAs
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  const double* zc = a.Z + min(i0 + lm, ny - 1);  // sites past ny: any finite row, unused
+  const int nsteps = (ns + 31) >> 5;                // step = 32 species, wave w: 32 s + 4 w + lk
+  double zv0[4], lv0[4], zv1[4], lv1[4];
+  auto load = [&](double (&zv)[4], double (&lv)[4], int s0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = 32 * (s0 + u) + 4 * w + lk;
+      const bool in = s0 + u < nsteps && j < ns;
+      zv[u] = in ? zc[(size_t)ny * j] : 0.0;
+      lv[u] = in ? a.LS[(size_t)16 * j + lm] : 0.0;
+    }
+  };
+  load(zv0, lv0, 0);
+  for (int s = 0; s < nsteps; s += 8) {
+    load(zv1, lv1, s + 4);  // in flight while the MFMAs below wait for zv0 / lv0
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = mfma_f64(zv0[u], lv0[u], acc);
+    load(zv0, lv0, s + 8);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = mfma_f64(zv1[u], lv1[u], acc);
+  }
+  // acc[r] = partial ZL[site lk + 4 r][factor lm]
+#pragma unroll
+  for (int r = 0; r < 4; ++r) sPart[w][lm][lk + 4 * r] = acc[r];
+  // CR from its species-block partials, in block order (L2; every partial's load in flight
+  // before the adds)
+  for (int p = t; p < K * nf; p += 512) {
+    const int k = p % K, h = p / K;
+    const double* src = a.CR_part + k + (size_t)a.ldcr * h;
+    double v = 0.0;
+    int b = 0;
+    for (; b + 8 <= a.ncr; b += 8) {
+      double x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = src[(size_t)a.slab * (b + u)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v += x[u];
+    }
+    for (; b < a.ncr; ++b) v += src[(size_t)a.slab * b];
+    sCR[k * NFB + h] = v;
+    if (blockIdx.x == 0) a.CR[k + (size_t)a.ldcr * h] = v;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0) HMSC_STAMP(51);
+  if (w == 0) {  // Q = I + Lambda D Lambda^T factor, while waves 1-3 form the right-hand sides
+    double q[NFB], dinv;
+    const int r = lane < nf ? lane : 0;
+#pragma unroll
+    for (int c = 0; c < NFB; ++c) {
+      const double v = (r == c ? 1.0 : 0.0) + sCR[(nc + r) * NFB + (c < nf ? c : 0)];
+      q[c] = (lane < nf && c < nf) ? v : (lane == c ? 1.0 : 0.0);
+    }
+    wv_chol<NFB>(q, dinv);
+    double wr[NFB];
+    wv_inv_lower_rows<NFB>(q, dinv, wr, sWs);  // lane m: row m of L^-1
+    if (lane < NFB)
+#pragma unroll
+      for (int c = 0; c < NFB; ++c) sW[lane * NFB + c] = (lane < nf && c < nf && c <= lane) ? wr[c] : 0.0;
+  } else {
+    // ---- stage 2: b = ZL - X CR_x, and the noise, one (site, factor) per thread
+    for (int p = t - 64; p < EF_SITES * nf; p += 448) {
+      const int s2 = p % EF_SITES, h = p / EF_SITES, ii = i0 + s2;
+      const double zl = ((sPart[0][h][s2] + sPart[1][h][s2]) + (sPart[2][h][s2] + sPart[3][h][s2])) +
+                        ((sPart[4][h][s2] + sPart[5][h][s2]) + (sPart[6][h][s2] + sPart[7][h][s2]));
+      double corr = 0.0, xi = 0.0;
+      if (ii < ny) {
+        for (int k = 0; k < nc; ++k) corr = fma(a.XEta[ii + (size_t)ny * k], sCR[k * NFB + h], corr);
+        xi = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)a.Pi[ii], (uint32_t)h, S_ETA, SWEEP_ITER(a));
+      }
+      sB[h][s2] = zl - corr;
+      sXi[h][s2] = xi;
+    }
+    // X columns of the tile into the Gram tile
+    for (int p = t - 64; p < nc * EF_SITES; p += 448) {
+      const int s2 = p % EF_SITES, k = p / EF_SITES, ii = i0 + s2;
+      sX[k][s2] = ii < ny ? a.XEta[ii + (size_t)ny * k] : 0.0;
+    }
+  }
+  __syncthreads();
+  if (blockIdx.x == 0) HMSC_STAMP(53);
+  // ---- stage 3: eta = L^-T (L^-1 b + xi) = W^T (W b + xi), two matrix-vector phases over
+  // the (factor, site) pairs (no serial substitution chain)
+  for (int p = t; p < EF_SITES * nf; p += 512) {
+    const int s2 = p % EF_SITES, m = p / EF_SITES;
+    double u = sXi[m][s2];
+    for (int k = 0; k <= m; ++k) u = fma(sW[m * NFB + k], sB[k][s2], u);
+    sU[m][s2] = u;
+  }
+  __syncthreads();
+  for (int p = t; p < EF_SITES * nf; p += 512) {
+    const int s2 = p % EF_SITES, h = p / EF_SITES, ii = i0 + s2;
+    double e = 0.0;
+    for (int m = h; m < nf; ++m) e = fma(sW[m * NFB + h], sU[m][s2], e);
+    if (ii < ny) {
+      a.Eta[a.Pi[ii] + (size_t)a.np * h] = e;
+      a.XEta[ii + (size_t)ny * (nc + h)] = e;
+    }
+    sX[nc + h][s2] = ii < ny ? e : 0.0;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0) HMSC_STAMP(54);
+  // ---- stage 4: Gram partial of the tile's Eta rows, Eta^T XEta (nf x K, ld Kmax)
+  double* dst = a.G_part + (size_t)blockIdx.x * a.Kmax * nf;
+  for (int p = t; p < K * nf; p += 512) {
+    const int k = p % K, h = p / K;
+    double g = 0.0;
+#pragma unroll
+    for (int s2 = 0; s2 < EF_SITES; ++s2) g = fma(sX[nc + h][s2], sX[k][s2], g);
+    dst[k + a.Kmax * h] = g;
+  }
+  if (blockIdx.x == 0) HMSC_STAMP(55);
+  if (a.kt) {
+    __syncthreads();
+    if (t == 0) kt_record(a.kt, SWEEP_ITER(a), kt0);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Co-launched side updaters (one queue).  After BetaLambda a sweep has three independent
 // species-parallel passes -- CR for updateEta, the GammaV partials (R/updateGammaV.R:17-19)
@@ -2094,12 +2234,22 @@ static void launch_eta_fused(State& s, uint32_t iter, bool cr_done = false) {
   const int ntile = (s.ny + EF_SITES - 1) / EF_SITES;
   {
     ProfScope ps(s, PROF_ETA_UNIT);
-    if (L.nf <= 8)
-      eta_fused_kernel<8><<<ntile, 256, 0, s.stream>>>(a);
-    else if (L.nf <= 12)
-      eta_fused_kernel<12><<<ntile, 256, 0, s.stream>>>(a);
-    else
-      eta_fused_kernel<16><<<ntile, 256, 0, s.stream>>>(a);
+    static const bool four = getenv_flag("HMSC_ETA_FOUR_WAVES");  // A/B: the four-wave kernel
+    if (four) {
+      if (L.nf <= 8)
+        eta_fused_kernel<8><<<ntile, 256, 0, s.stream>>>(a);
+      else if (L.nf <= 12)
+        eta_fused_kernel<12><<<ntile, 256, 0, s.stream>>>(a);
+      else
+        eta_fused_kernel<16><<<ntile, 256, 0, s.stream>>>(a);
+    } else {
+      if (L.nf <= 8)
+        eta_fused8_kernel<8><<<ntile, 512, 0, s.stream>>>(a);
+      else if (L.nf <= 12)
+        eta_fused8_kernel<12><<<ntile, 512, 0, s.stream>>>(a);
+      else
+        eta_fused8_kernel<16><<<ntile, 512, 0, s.stream>>>(a);
+    }
     HIP_OK(hipGetLastError());
   }
   // G's Eta rows: reduced from G_part by the next updateZ launch (or flush_g)

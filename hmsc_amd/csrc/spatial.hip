@@ -909,9 +909,8 @@ size_t spatial_work_doubles(const State& s, int r) {
   const Level& L = s.lev[r];
   const size_t nfc = std::max(1, std::min(L.nfmax, s.NFmax));
   if (L.gpp) return gpp_layout(L.np, (int)nfc, L.nK, L.nalpha).tot + 64;
-  if (L.nngp)
-    return std::max(nn_layout(L.np, (int)nfc).tot,
-                    (size_t)L.nalpha * ((L.np + 255) / 256) * nfc) + 64;
+  if (L.nngp)  // updateAlpha's partial sums after the band matrix: its zeros outside the band persist
+    return nn_layout(L.np, (int)nfc).tot + (size_t)L.nalpha * ((L.np + 255) / 256) * nfc + 64;
   const size_t N = (size_t)L.np * nfc;
   const size_t eta = N * N + N + dense_ws_doubles((int)N) + nfc * nfc + 64;
   const size_t alpha = (size_t)L.nalpha * ((L.np + 255) / 256) * std::max(1, std::min(L.nfmax, s.NFmax));
@@ -975,10 +974,16 @@ void launch_alpha(State& s, uint32_t iter) {
       HIP_OK(hipGetLastError());
       continue;
     }
-    if (L.nngp)
-      nngp_alpha_kernel<<<dim3(L.nalpha, (L.np + 255) / 256), 256, 0, s.stream>>>(a, nn_args(s, r));
-    else
-      alpha_quad_kernel<<<dim3(L.nalpha, (L.np + 255) / 256), 256, 0, s.stream>>>(a);
+    if (L.nngp) {  // the band matrix at the start of spWork stays untouched (zeros outside the band)
+      SpArgs b = a;
+      b.work = L.spWork + nn_layout(L.np, std::max(1, std::min(L.nfmax, s.NFmax))).tot;
+      nngp_alpha_kernel<<<dim3(L.nalpha, (L.np + 255) / 256), 256, 0, s.stream>>>(b, nn_args(s, r));
+      HIP_OK(hipGetLastError());
+      alpha_draw_kernel<<<1, 256, 0, s.stream>>>(b);
+      HIP_OK(hipGetLastError());
+      continue;
+    }
+    alpha_quad_kernel<<<dim3(L.nalpha, (L.np + 255) / 256), 256, 0, s.stream>>>(a);
     HIP_OK(hipGetLastError());
     alpha_draw_kernel<<<1, 256, 0, s.stream>>>(a);
     HIP_OK(hipGetLastError());

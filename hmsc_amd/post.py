@@ -5,15 +5,20 @@
   Beta as.vector covariate-fastest, Lambda as.vector(t(.)) species-fastest,
   Omega = crossprod(Lambda)), returned as ``{name: [chain arrays (samples, p)]}``
   plus ``{name: column names}``.
-* ``effectiveSize`` / ``gelman_diag`` — restatements of coda::effectiveSize
-  (spectrum0.ar: AR order by AIC via Yule-Walker, R's ar.yw.default) and
-  coda::gelman.diag(multivariate=FALSE), used for the Beta ESS/sec metric.
+* ``effectiveSize`` — coda::effectiveSize (spectrum0.ar: AR order by AIC via Yule-Walker,
+  R's ar.yw.default) on the device (post.hip), used for the Beta ESS/sec metric;
+  ``gelman_diag`` — coda::gelman.diag(multivariate=FALSE) on the host (m x p numbers).
+* ``computeVariancePartitioning``, ``computeAssociations``, ``getPostEstimate(.., "Omega")``
+  — their loops over posterior samples on the device (post.hip); checkers in
+  oracle/post_oracle.py.
 * ``poolMcmcChains``, ``getPostEstimate``, ``computeWAIC`` — R/poolMcmcChains.R,
   R/getPostEstimate.R, R/computeWAIC.R:25-131 (normal and probit columns).
 """
 import numpy as np
 from scipy import stats
 from scipy.special import log_ndtr
+
+from . import _lib as L
 
 
 def poolMcmcChains(postList, start=1, thin=1):
@@ -119,58 +124,40 @@ def _pad_cols(a, n):
 
 
 # ---------------------------------------------------------------------------
-# coda::effectiveSize restated (spectrum0.ar with R's ar.yw.default)
+# coda::effectiveSize on the device (hmsc_effective_size, post.hip; the numpy restatement
+# of spectrum0.ar with R's ar.yw.default is the checker in oracle/post_oracle.py)
 # ---------------------------------------------------------------------------
-def spectrum0_ar(x):
-    """Spectral density at zero for every column of x (n, p) — coda::spectrum0.ar."""
+def _device():
+    """The device post-processing runs on: HMSC_POST_DEVICE, else 0."""
+    import os
+    return int(os.environ.get("HMSC_POST_DEVICE", "0"))
+
+
+def spectrum0_ar(x, device=None):
+    """coda::spectrum0.ar for every column of x (n, p): (spec, AR order), on the device.
+    spec follows from the ESS: spec = n var / ESS (0 for a constant column)."""
     x = np.asarray(x, dtype=np.float64)
     if x.ndim == 1:
         x = x[:, None]
-    n, p = x.shape
-    z = np.arange(1, n + 1, dtype=np.float64)
-    zc = z - z.mean()
-    xc = x - x.mean(axis=0)
-    beta = (zc @ xc) / (zc @ zc)
-    resid = xc - np.outer(zc, beta)
-    rsd = resid.std(axis=0, ddof=1)
-    scale = np.maximum(np.abs(x).max(axis=0), 1e-300)
-    const = rsd <= 1.5e-8 * scale                                          # all.equal(sd(resid), 0)
-    order_max = int(min(n - 1, np.floor(10 * np.log10(n))))
-    # autocovariances with denominator n (acf type="covariance", demean=TRUE)
-    r = np.empty((order_max + 1, p))
-    for k in range(order_max + 1):
-        r[k] = np.sum(xc[: n - k] * xc[k:], axis=0) / n
-    r0 = np.where(r[0] > 0, r[0], 1.0)
-    # Levinson-Durbin (R's eureka) for all orders
-    vars_ = np.empty((order_max + 1, p))
-    vars_[0] = r0
-    coefs = np.zeros((order_max + 1, order_max + 1, p))
-    a = np.zeros((order_max + 1, p))
-    v = r0.copy()
-    for m in range(1, order_max + 1):
-        acc = r[m] - np.sum(a[1:m] * r[m - 1:0:-1], axis=0) if m > 1 else r[m].copy()
-        k = acc / v
-        a_new = a.copy()
-        a_new[m] = k
-        if m > 1:
-            a_new[1:m] = a[1:m] - k * a[m - 1:0:-1]
-        a = a_new
-        v = v * (1 - k * k)
-        vars_[m] = v
-        coefs[m, 1:m + 1] = a[1:m + 1]
+    ess, order = _ess_device(x, device)
+    var = x.var(axis=0, ddof=1)
     with np.errstate(divide="ignore", invalid="ignore"):
-        xaic = n * np.log(vars_) + 2 * np.arange(order_max + 1)[:, None] + 2.0
-    order = np.argmin(xaic, axis=0)
-    cols = np.arange(p)
-    var_pred = vars_[order, cols] * n / (n - (order + 1))
-    ar_sum = np.array([coefs[order[j], 1:order[j] + 1, j].sum() for j in range(p)])
-    spec = var_pred / (1 - ar_sum) ** 2
-    spec[const] = 0.0
+        spec = np.where(ess == 0, 0.0, x.shape[0] * var / ess)
     return spec, order
 
 
-def effectiveSize(chains):
-    """coda::effectiveSize for an mcmc.list: per-chain n*var/spec0, summed over chains."""
+def _ess_device(x, device=None):
+    n, p = x.shape
+    xf = np.asfortranarray(x)
+    ess = np.zeros(p)
+    order = np.zeros(p, dtype=np.int32)
+    L.check(L.lib().hmsc_effective_size(_device() if device is None else int(device), n, p,
+                                        xf.ctypes.data_as(L.dp), L.fptr(ess), L.iptr(order)))
+    return ess, order
+
+
+def effectiveSize(chains, device=None):
+    """coda::effectiveSize for an mcmc.list: per-chain n var / spec0 (device), summed over chains."""
     if isinstance(chains, np.ndarray):
         chains = [chains]
     total = 0.0
@@ -178,11 +165,7 @@ def effectiveSize(chains):
         x = np.asarray(x, dtype=np.float64)
         if x.ndim == 1:
             x = x[:, None]
-        spec, _ = spectrum0_ar(x)
-        var = x.var(axis=0, ddof=1)
-        with np.errstate(divide="ignore", invalid="ignore"):
-            ess = np.where(spec == 0, 0.0, x.shape[0] * var / spec)
-        total = total + ess
+        total = total + _ess_device(x, device)[0]
     return total
 
 
@@ -216,6 +199,9 @@ def getPostEstimate(hM, parName, r=1, x=None, q=(), chainIndex=None, start=1):
     """R/getPostEstimate.R: posterior mean and support (P(>0)) of Beta/Gamma/V/Sigma/Omega."""
     postList = hM.postList if chainIndex is None else [hM.postList[i] for i in chainIndex]
     post = poolMcmcChains(postList, start=start)
+    if parName == "Omega" and not q:   # mean and supports summed on the device (hmsc_post_omega)
+        o = _omega_device(post, r - 1, hM.ns)
+        return dict(mean=o["mean_omega"], support=o["support"], supportNeg=o["support_neg"])
     if parName == "Omega":
         vals = np.stack([s["Lambda"][r - 1].T @ s["Lambda"][r - 1] for s in post])
     elif parName == "Sigma":
@@ -274,8 +260,9 @@ def computeWAIC(hM, ghN=11):
     return float(np.mean(Bl + Vv))
 
 
-def computeVariancePartitioning(hM, group=None, groupnames=None, start=1):
-    """R/computeVariancePartitioning.R:37-204 (X a matrix, na.ignore=FALSE).
+def computeVariancePartitioning(hM, group=None, groupnames=None, start=1, device=None):
+    """R/computeVariancePartitioning.R:37-204 (X a matrix, na.ignore=FALSE), the loop over
+    samples on the device (hmsc_variance_partitioning, post.hip).
 
     Reproduces the reference's loop ``for (i in 1:hM$samples)`` over the *pooled* list
     (:125), i.e. with nChains > 1 only the first chain's samples enter (SURVEY.md
@@ -292,52 +279,85 @@ def computeVariancePartitioning(hM, group=None, groupnames=None, start=1):
             groupnames = [hM.covNames[0]]
     group = np.asarray(group)
     ngroups = int(group.max())
-    X, Tr = hM.X, hM.Tr
+    X = np.asarray(hM.X, dtype=np.float64)
+    Tr = np.asarray(hM.Tr, dtype=np.float64)
     cM = np.cov(X, rowvar=False).reshape(nc, nc)                           # :66
-    post = poolMcmcChains(hM.postList, start=start)
-    S = hM.samples
-    fixed = np.zeros(ns)
-    fixedsplit = np.zeros((ns, ngroups))
-    random = np.zeros((ns, nr))
-    R2T_Y = 0.0
-    R2T_Beta = np.zeros(nc)
-    for i in range(S):                                                     # :125
-        s = post[i]
-        Beta = s["Beta"]
-        mu = (Tr @ s["Gamma"].T).T                                         # gemu :100-103
-        for k in range(nc):                                                # :126-128
-            R2T_Beta[k] += np.corrcoef(Beta[k], mu[k])[0, 1] ** 2
-        f = X @ Beta                                                       # getf :87-97
-        a = X @ mu                                                         # geta :75-84
-        a = a - a.mean(axis=1, keepdims=True)
-        f = f - f.mean(axis=1, keepdims=True)
-        res1 = np.sum((np.sum(a * f, axis=1) / (ns - 1)) ** 2)            # :139-141
-        res2 = np.sum((np.sum(a * a, axis=1) / (ns - 1)) * (np.sum(f * f, axis=1) / (ns - 1)))
-        R2T_Y += res1 / res2
-        fixed1 = np.einsum("kj,kl,lj->j", Beta, cM, Beta)                  # :142-146
-        fixedsplit1 = np.zeros((ns, ngroups))
-        for g in range(1, ngroups + 1):                                    # :147-151
-            sel = group == g
-            fixedsplit1[:, g - 1] = np.einsum("kj,kl,lj->j", Beta[sel], cM[np.ix_(sel, sel)], Beta[sel])
-        random1 = np.zeros((ns, nr))
-        for r in range(nr):                                                # :154-160
-            lam = s["Lambda"][r]
-            random1[:, r] = np.sum(lam * lam, axis=0)
-        if nr > 0:                                                         # :161-170
-            tot = fixed1 + random1.sum(axis=1)
-            fixed += fixed1 / tot
-            random += random1 / tot[:, None]
-        else:
-            fixed += 1.0
-        fixedsplit += fixedsplit1 / fixedsplit1.sum(axis=1, keepdims=True)  # :171-173
-    fixed /= S
-    random /= S
-    fixedsplit /= S
+    post = poolMcmcChains(hM.postList, start=start)[:hM.samples]            # :125 (quirk above)
+    S = len(post)
+    keep = []
+    a = L.hmsc_vp_args()
+    a.device = _default_device_of(device)
+    a.ny, a.ns, a.nc, a.nt, a.S, a.ngroups, a.nr = hM.ny, ns, nc, Tr.shape[1], S, ngroups, nr
+    a.group = L.colmajor_ptr(group.astype(np.int32), keep, np.int32)
+    a.X = L.colmajor_ptr(X, keep)
+    a.Tr = L.colmajor_ptr(Tr, keep)
+    a.cM = L.colmajor_ptr(cM, keep)
+    a.Beta = L.fptr(_flat(keep, [np.asarray(s_["Beta"], dtype=np.float64) for s_ in post]))
+    a.Gamma = L.fptr(_flat(keep, [np.asarray(s_["Gamma"], dtype=np.float64) for s_ in post]))
+    nfs = np.zeros((max(1, nr), S), dtype=np.int32)
+    for r in range(nr):
+        nfm = max(int(np.asarray(s_["Lambda"][r]).shape[0]) for s_ in post)
+        lam = np.zeros((S, nfm, ns))
+        for k, s_ in enumerate(post):
+            l_ = np.asarray(s_["Lambda"][r], dtype=np.float64)
+            nfs[r, k] = l_.shape[0]
+            lam[k, :l_.shape[0]] = l_
+        a.nfmax[r] = nfm
+        a.Lambda[r] = L.fptr(_flat(keep, list(lam)))
+    a.nf = L.iptr(_keep(keep, np.ascontiguousarray(nfs.ravel())))
+    slot = nc + 1 + ns * (1 + nr + ngroups)
+    out = np.zeros(slot)
+    L.check(L.lib().hmsc_variance_partitioning(L.C.byref(a), L.fptr(out)))
+    R2T_Beta, R2T_Y = out[:nc], float(out[nc])
+    fixed = out[nc + 1:nc + 1 + ns]
+    random = out[nc + 1 + ns:nc + 1 + ns * (1 + nr)].reshape(nr, ns).T
+    fixedsplit = out[nc + 1 + ns * (1 + nr):].reshape(ngroups, ns).T
     vals = np.zeros((ngroups + nr, ns))                                    # :180-187
     for g in range(ngroups):
         vals[g] = fixed * fixedsplit[:, g]
     for r in range(nr):
         vals[ngroups + r] = random[:, r]
     rl = list(getattr(hM, "rLNames", None) or [f"level{r + 1}" for r in range(nr)])
-    return dict(vals=vals, R2T=dict(Beta=R2T_Beta / S, Y=R2T_Y / S), group=group, groupnames=groupnames,
+    return dict(vals=vals, R2T=dict(Beta=R2T_Beta, Y=R2T_Y), group=group, groupnames=groupnames,
                 rownames=list(groupnames) + [f"Random: {n}" for n in rl])
+
+
+def _keep(keep, arr):
+    keep.append(arr)
+    return arr
+
+
+def _flat(keep, mats):
+    """Samples stacked as consecutive column-major matrices (the C side's S x (m x n))."""
+    return _keep(keep, np.ascontiguousarray(np.concatenate([np.asarray(m_).ravel(order="F") for m_ in mats])))
+
+
+def _default_device_of(device):
+    return _device() if device is None else int(device)
+
+
+def computeAssociations(hM, start=1, thin=1, device=None):
+    """R/computeAssociations.R: per random level, dict(mean, support) of
+    cov2cor(crossprod(Lambda)) over the pooled samples, on the device (hmsc_post_omega)."""
+    post = poolMcmcChains(hM.postList, start=start, thin=thin)
+    out = []
+    for r in range(hM.nr):
+        res = _omega_device(post, r, hM.ns, device)
+        out.append(dict(mean=res["mean_cor"], support=res["support"]))
+    return out
+
+
+def _omega_device(post, r, ns, device=None):
+    S = len(post)
+    nfm = max(int(np.asarray(s_["Lambda"][r]).shape[0]) for s_ in post)
+    lam = np.zeros((S, ns, nfm))   # C order (S, ns, nfm) = each sample nfm x ns column-major
+    nf = np.zeros(S, dtype=np.int32)
+    for k, s_ in enumerate(post):
+        l_ = np.asarray(s_["Lambda"][r], dtype=np.float64)
+        nf[k] = l_.shape[0]
+        lam[k, :, :l_.shape[0]] = l_.T
+    outs = {k: np.zeros((ns, ns), order="F") for k in ("mean_cor", "support", "support_neg", "mean_omega")}
+    L.check(L.lib().hmsc_post_omega(_default_device_of(device), S, ns, nfm, L.iptr(nf), L.fptr(lam),
+                                    *[outs[k].ctypes.data_as(L.dp) for k in ("mean_cor", "support", "support_neg",
+                                                                             "mean_omega")]))
+    return outs

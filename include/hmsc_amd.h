@@ -264,6 +264,44 @@ int hmsc_profile_get(hmsc_state* s, int32_t id, double* total_ms, int32_t* count
 int hmsc_kernel_timing(hmsc_state* s, int32_t enable);
 int hmsc_kernel_timing_get(hmsc_state* s, int32_t id, double* total_us, int32_t* count);
 
+/* ---- post-sampling statistics on the device ----
+ * Reductions over posterior samples that return only their summaries; every sum is in a
+ * fixed order, so results repeat bit for bit. */
+
+/* computeAssociations (R/computeAssociations.R) and getPostEstimate(hM, "Omega")
+ * (R/getPostEstimate.R) for one random level: Lambda holds S samples of nfmax x ns
+ * (column-major each; factors h >= nf[s] ignored).  Outputs ns x ns: the mean of
+ * cov2cor(Lambda_s' Lambda_s), its support mean(> 0), and for Omega_s = Lambda_s' Lambda_s the
+ * posterior mean and mean(Omega_s < 0). */
+int hmsc_post_omega(int32_t device, int32_t S, int32_t ns, int32_t nfmax, const int32_t* nf,
+                    const double* Lambda, double* mean_cor, double* support, double* support_neg,
+                    double* mean_omega);
+
+/* computeVariancePartitioning (R/computeVariancePartitioning.R:37-204; X a matrix): the
+ * caller passes the S samples the reference loops over (its quirk: `for (i in 1:hM$samples)`
+ * over the pooled list, i.e. the first chain when nChains > 1), cM = cov(hM$X), and the group
+ * of every covariate (1-based).  out (nc + 1 + ns (1 + nr + ngroups) doubles):
+ * R2T.Beta (nc) | R2T.Y | fixed (ns) | random (nr x ns) | fixedsplit (ngroups x ns),
+ * all already averaged over the samples; vals = fixed * fixedsplit and random follow on the host. */
+typedef struct hmsc_vp_args {
+  int32_t device, ny, ns, nc, nt, S, ngroups, nr;
+  const int32_t* group;     /* nc */
+  const double* X;          /* ny x nc  hM$X */
+  const double* Tr;         /* ns x nt  hM$Tr */
+  const double* cM;         /* nc x nc  cov(hM$X) */
+  const double* Beta;       /* S x (nc x ns) */
+  const double* Gamma;      /* S x (nc x nt) */
+  const int32_t* nf;        /* nr x S: factors of level r in sample s at [r S + s] */
+  int32_t nfmax[HMSC_MAX_LEVELS];
+  const double* Lambda[HMSC_MAX_LEVELS];  /* S x (nfmax_r x ns) */
+} hmsc_vp_args;
+int hmsc_variance_partitioning(const hmsc_vp_args* args, double* out);
+
+/* coda::effectiveSize of each column of x (n x p, column-major; one chain): n var / spec0
+ * with spectrum0.ar (AR order by AIC up to min(n - 1, 10 log10 n), Yule-Walker by
+ * Levinson-Durbin).  ess[p]; order[p] (may be NULL) the chosen AR orders. */
+int hmsc_effective_size(int32_t device, int32_t n, int32_t p, const double* x, double* ess, int32_t* order);
+
 /* Wait for all device work of this chain. */
 int hmsc_sync(hmsc_state* s);
 

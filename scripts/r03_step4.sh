@@ -7,7 +7,7 @@ TAG=${1:-s4}
 mkdir -p $R/gpurun_out
 cd $R
 export HMSC_GRAPH_DEBUG=1
-timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests/test_gpu_vignette2.py tests/test_gpu_spatial.py -k "not posterior" -x -q --timeout 200 --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/${TAG}_pytest.log; exit 1; }
+timeout -k 10 800 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests/test_gpu_vignette2.py tests/test_gpu_spatial.py tests/test_gpu_spatial_large.py tests/test_gpu_post.py tests/test_gpu_determinism.py tests/test_gpu_multigpu.py -k "not posterior" -x -q --timeout 200 --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/${TAG}_pytest.log; exit 1; }
 tail -2 gpurun_out/${TAG}_pytest.log
 timeout -k 10 120 ./scripts/ubench_z > gpurun_out/${TAG}_ubz.log 2>&1 || { echo "ubench failed"; tail gpurun_out/${TAG}_ubz.log; exit 1; }
 cat gpurun_out/${TAG}_ubz.log

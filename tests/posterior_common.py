@@ -5,6 +5,7 @@ partitioning)."""
 import numpy as np
 
 import hmsc_amd as H
+from oracle import post_oracle as P
 
 MODELS = {
     # probit with traits: Gamma2 acts (all iSigma == 1), GammaV, MGP priors, Eta
@@ -72,7 +73,7 @@ def variance_partitioning(hM, rec):
     post = H.combine_parameters(full, hM)
     hM.postList = [post]
     hM.samples = S
-    return H.computeVariancePartitioning(hM)["vals"]
+    return P.computeVariancePartitioning(hM)["vals"]
 
 
 def summarise(hM, chains):
@@ -82,6 +83,6 @@ def summarise(hM, chains):
         draws=np.stack([v[::THIN_STORE] for v in vecs]).astype(np.float32),
         mean=np.stack([v.mean(axis=0) for v in vecs]),
         sd=np.stack([v.std(axis=0, ddof=1) for v in vecs]),
-        ess=np.stack([H.effectiveSize(v) for v in vecs]),
+        ess=np.stack([P.effectiveSize(v) for v in vecs]),
         vp=np.stack([variance_partitioning(hM, r) for r in chains]),
     )

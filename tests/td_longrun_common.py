@@ -59,8 +59,8 @@ def param_rows(hM, Beta, Gamma, iV, rho_idx, Lambdas, Alphas):
 
 
 def chain_summary(rows):
-    import hmsc_amd as H
-    return dict(mean=rows.mean(0), var=rows.var(0, ddof=1), ess=H.effectiveSize(rows))
+    from oracle import post_oracle as P
+    return dict(mean=rows.mean(0), var=rows.var(0, ddof=1), ess=P.effectiveSize(rows))
 
 
 def pooled(means, variances, ess):

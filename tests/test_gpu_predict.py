@@ -76,8 +76,9 @@ def test_conditional_prediction(fitted):
     fc = H.evaluateModelFit(hM, cond)["AUC"][probit]
     # the units are the fitted ones, so the posterior Eta already conditions on this same Y:
     # conditioning again must not degrade the fit (and must change the predictions); a strict
-    # AUC gain is not guaranteed (GPU reductions are not bit-reproducible run to run, and the
-    # two means differed by < 0.01 either way over runs)
+    # AUC gain is not guaranteed on a 12-sample posterior (the two means differed by < 0.01
+    # either way across model seeds; for a given seed the result is bitwise repeatable,
+    # tests/test_gpu_determinism.py)
     assert np.all(np.isfinite(cond)) and np.mean(fc) > np.mean(fb) - 0.02, (fb, fc)
     assert not np.allclose(cond, base)
     same = np.stack(H.predict(hM, post=post, Yc=np.full((hM.ny, hM.ns), np.nan), expected=True, seed=11), axis=2)

@@ -12,6 +12,7 @@ and for a random level the upper triangle of Omega = Lambda' Lambda.
 import numpy as np
 
 import hmsc_amd as H
+from oracle import post_oracle as P
 
 MODELS = ("linear", "mixed", "latent")
 # updaters as the reference's defaults resolve them for each model (GammaEta off for nr == 0)
@@ -77,4 +78,4 @@ def summarise(hM, chains):
     return dict(draws=np.stack([v[::THIN_STORE] for v in vecs]).astype(np.float32),
                 mean=np.stack([v.mean(axis=0) for v in vecs]),
                 sd=np.stack([v.std(axis=0, ddof=1) for v in vecs]),
-                ess=np.stack([H.effectiveSize(v) for v in vecs]))
+                ess=np.stack([P.effectiveSize(v) for v in vecs]))
