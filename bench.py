@@ -23,6 +23,7 @@ bounded sample (R is absent, so the reference itself cannot be timed: kind "port
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -55,6 +56,11 @@ def parse():
     p.add_argument("--cpu-sweeps", type=int, default=3, help="sweeps per CPU chain in the baseline sample")
     p.add_argument("--ess-samples", type=int, default=2000, help="recorded sweeps of the separate ESS run")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--clock-warmup-s", type=float, default=0.5,
+                   help="config 4: extra untimed sweeps until the warm-up has run this long (clock ramp)")
+    p.add_argument("--cpu-oracle-sweeps", type=int, default=None,
+                   help="configs 3 / 5: sweeps of the numpy restatement timed for cpu_baseline "
+                        "(default 10 for config 3, 3 for config 5)")
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02_s6_pmc.json"),
                    help="rocprofv3 PMC summary (scripts/pmc_summary.py) the roofline's traffic / valu come from")
     return p.parse_args()
@@ -113,12 +119,32 @@ def main():
         graphs = ch.prepare_graphs(2)
     if args.warmup > 1:
         ch.run(transient=0, samples=args.warmup - 1, thin=1, adaptNf=[0], iter0=1, record=True)
+    # clock ramp: a few warm-up sweeps are ~1 ms of GPU work, too short for the card to leave
+    # its idle clocks (at --warmup 5 the timed sweeps ran 10 % slower per kernel than at
+    # --warmup 100).  Untimed sweeps of the same chain are added until the warm-up has kept the
+    # GPU busy for --clock-warmup-s; the timed region is unchanged (exactly --steps sweeps).
+    sync(ch)
+    extra, it_next = 0, args.warmup
+    t_w = time.perf_counter()
+    def more():  # rank 0 decides, so that a sharded chain's ranks run the same sweeps
+        go = args.warmup > 0 and time.perf_counter() - t_w < args.clock_warmup_s
+        if dist is not None:
+            f = torch.tensor([1 if go else 0], dtype=torch.int32)
+            dist.broadcast(f, src=0)
+            go = bool(f.item())
+        return go
+
+    while more():
+        ch.run(transient=0, samples=50, thin=1, adaptNf=[0], iter0=it_next, record=True)
+        sync(ch)
+        extra += 50
+        it_next += 50
     barrier()
     sync(ch)
     ch.kernel_timing(True)  # clear: keep only the timed region's launches
     t0 = time.perf_counter()
     # timed region: every sweep is a replay of the captured per-sweep hipGraph (capi.cpp)
-    rec = ch.run(transient=0, samples=args.steps, thin=1, adaptNf=[0], iter0=args.warmup, record=True)
+    rec = ch.run(transient=0, samples=args.steps, thin=1, adaptNf=[0], iter0=it_next, record=True)
     sync(ch)
     barrier()
     t_run = time.perf_counter() - t0
@@ -131,7 +157,7 @@ def main():
     # run on the chain's own stream, after the timed region
     n_prof = min(args.steps, 50)
     ch.profile(True)
-    ch.run(transient=n_prof, samples=0, adaptNf=[0], iter0=args.warmup + args.steps, record=False)
+    ch.run(transient=n_prof, samples=0, adaptNf=[0], iter0=it_next + args.steps, record=False)
     sync(ch)
     kern = {}
     for name in ("z", "betalambda", "eta_unit", "sweep"):
@@ -142,7 +168,7 @@ def main():
     # Beta ESS (coda::effectiveSize restated) from a separate recorded run of >= 1000 sweeps
     # of the same chain after the timed region (Beta only), per sweep; x the timed rate below
     n_ess = max(1000, args.ess_samples)
-    rec_ess = ch.run(transient=0, samples=n_ess, thin=1, adaptNf=[0], iter0=args.warmup + args.steps + n_prof,
+    rec_ess = ch.run(transient=0, samples=n_ess, thin=1, adaptNf=[0], iter0=it_next + args.steps + n_prof,
                      record=True, fields=("Beta",))
     sync(ch)
     beta = rec_ess["Beta"].reshape(n_ess, -1)
@@ -242,6 +268,7 @@ def main():
                                      "frac": round(ny * ns * 25 * per_chain_rate / 1e9 / HBM_PEAK_GBS, 4),
                                      "note": "SURVEY 8(d): 3 fp64 Z touches + 1 B Y per cell per sweep"}},
         "graphs_prebuilt": graphs,
+        "clock_warmup_sweeps": extra,
         "kernels_live_us": {k: round(v["avg_us"], 3) for k, v in live.items()},
         "kernels_eager_events_us": {k: round(v["avg_us"], 2) for k, v in kern.items()},
         "cpu_baseline": cpu,
@@ -361,7 +388,8 @@ def main_spatial(args):
         "roofline": roof,
         "kernels_eager_events_us": {k: round(v["avg_us"], 1) for k, v in kern.items()},
         "alpha_posterior_mean_index": round(alpha_mean, 2),
-        "cpu_baseline": None,
+        "cpu_baseline": None if (args.no_cpu or world > 1) else cpu_baseline_oracle(
+            hM, {"GammaEta": False}, [1], args.cpu_oracle_sweeps or 3, f"vignette_4 '{args.method}' ny={ny}"),
     }
     print(json.dumps(out), flush=True)
 
@@ -447,9 +475,75 @@ def main_phylo(args):
                      "timer": "HIP events on the chain stream around the updater (eager sweeps)"},
         "kernels_eager_events_us": {k: round(v["avg_us"], 1) for k, v in kern.items()},
         "rho_posterior_mean_index": round(rho_mean, 2),
-        "cpu_baseline": None,
+        "cpu_baseline": None if (args.no_cpu or world > 1) else cpu_baseline_oracle(
+            hM, {}, [nf], args.cpu_oracle_sweeps or 10, f"vignette_3 ns={ns} nf={nf}, default updaters"),
     }
     print(json.dumps(out), flush=True)
+
+
+def _cpu_model():
+    model = platform.processor() or platform.machine()
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return model
+
+
+def cpu_baseline_oracle(hM, updater, nf, n_sweeps, what):
+    """Configs 3 and 5: the numpy restatement of the reference's sweep (oracle/hmsc_oracle.py,
+    the parity checker of the device path) timed on the host: compute_data_parameters and the
+    initial state once (untimed, reported as setup_s), then n_sweeps full sweeps of one chain
+    at the device chain's nf; multi-threaded only through numpy's BLAS/LAPACK (cores = its
+    thread count).  The C++ port of config 4 covers neither the phylogeny nor the spatial
+    levels, so this leg is the numpy one ("port", the reference's R being absent)."""
+    from oracle import hmsc_oracle as O
+    from oracle.rng import Rng
+    m = dict(X=hM.XScaled, Y=hM.YScaled, Yraw=hM.Y, Tr=hM.TrScaled, Pi=hM.Pi, np=hM.np, distr=hM.distr,
+             V0=hM.V0, f0=hM.f0, mGamma=hM.mGamma, UGamma=hM.UGamma, aSigma=hM.aSigma, bSigma=hM.bSigma,
+             rhopw=hM.rhopw, C=hM.C,
+             rL=[dict(nu=rl.nu, a1=rl.a1, b1=rl.b1, a2=rl.a2, b2=rl.b2, nfMin=rl.nfMin, nfMax=rl.nfMax,
+                      sDim=rl.sDim, xDim=rl.xDim) for rl in (hM.rL or [])])
+    for r, (d, rl) in enumerate(zip(m["rL"], hM.rL or [])):
+        if rl.sDim:
+            # rows of rl$s in levels(dfPi[,r]) order, the unit order of Eta (R indexes s by
+            # the unit names, R/computeDataParameters.R:56,92,142)
+            from hmsc_amd.dataparams import _level_order
+            xy = np.asarray(rl.s, dtype=np.float64)[_level_order(hM, r, rl)]
+            d.update(spatialMethod=rl.spatialMethod, alphapw=np.asarray(rl.alphapw, dtype=np.float64),
+                     dist=np.sqrt(((xy[:, None, :] - xy[None, :, :]) ** 2).sum(-1)), s=xy,
+                     nNeighbours=rl.nNeighbours, sKnot=rl["sKnot"] if "sKnot" in rl.names() else None)
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([int(i.get("num_threads", 1)) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
+    except Exception:  # noqa: BLE001 -- thread count is informative only
+        cores = 1
+    import threading
+    done = threading.Event()
+
+    def heartbeat():  # minutes of host work: keep the job's output alive
+        while not done.wait(30.0):
+            print(f"[bench] cpu_baseline ({what}): {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    t0 = time.perf_counter()
+    threading.Thread(target=heartbeat, daemon=True).start()
+    rng = Rng(1234567)
+    dp = O.compute_data_parameters(m)
+    st = O.compute_initial_parameters(m, rng, nf=list(nf))
+    setup = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for it in range(1, n_sweeps + 1):
+        st = O.sweep(st, m, rng, it, updater=updater, data_par=dp)
+    sec = time.perf_counter() - t0
+    done.set()
+    del dp, st
+    return {"value": round(n_sweeps / sec, 5), "unit": "sweeps/s", "cores": cores, "kind": "port",
+            "sample": f"{n_sweeps} full sweeps of one chain of the numpy restatement (oracle/hmsc_oracle.py) "
+                      f"at {what}, {sec:.1f} s wall after {setup:.1f} s of untimed setup "
+                      f"(data parameters + initial state); BLAS threads {cores}; {_cpu_model()}",
+            "setup_s": round(setup, 1)}
 
 
 def cpu_baseline(hM, args, ess_per_sweep):
@@ -458,7 +552,6 @@ def cpu_baseline(hM, args, ess_per_sweep):
     thread per chain, timed on a bounded sample: args.cpu_sweeps sweeps of every chain after
     its initialisation (R is absent, so this stands in for sampleMcmc with
     nChains = nParallel = cores, labelled "port")."""
-    import platform
     from oracle import cpu_port
     m = dict(X=hM.XScaled, Y=hM.YScaled, Yraw=hM.Y, Tr=hM.TrScaled, Pi=hM.Pi, np=hM.np, distr=hM.distr,
              V0=hM.V0, f0=hM.f0, mGamma=hM.mGamma, UGamma=hM.UGamma, aSigma=hM.aSigma, bSigma=hM.bSigma,
@@ -467,14 +560,7 @@ def cpu_baseline(hM, args, ess_per_sweep):
     cores = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count() or 1, 64)
     _, sec = cpu_port.run(m, 1234567, n_sweeps=args.cpu_sweeps, nchains=cores, iter0=0, gamma2=True)
     rate = cores * args.cpu_sweeps / sec
-    model = platform.processor() or platform.machine()
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
+    model = _cpu_model()
     return {"value": round(rate, 4), "unit": "sweeps/s", "cores": cores, "kind": "port",
             "sample": f"{cores} chains x {args.cpu_sweeps} full sweeps of the C++ restatement (oracle/cpu/hmsc_cpu.cpp, "
                       f"one thread per chain) at ny={args.ny} ns={args.ns} nc={args.nc} nf={args.nf}, "

@@ -7,7 +7,7 @@ hot path runs as hand-written HIP kernels for gfx950 in ``libhmsc_amd.so``
 behind the C ABI ``include/hmsc_amd.h``.
 """
 from .model import Hmsc, HmscRandomLevel, setPriors, model_matrix  # noqa: F401
-from .post import (computeVariancePartitioning, convertToCodaObject, computeWAIC, effectiveSize,  # noqa: F401
+from .post import (computeAssociations, computeVariancePartitioning, convertToCodaObject, computeWAIC, effectiveSize,  # noqa: F401
                    gelman_diag, getPostEstimate, poolMcmcChains, spectrum0_ar)
 from .sampler import Chain, alignPosterior, combine_parameters, sampleMcmc, updater_mask  # noqa: F401
 from .dataparams import computeDataParameters, constructKnots  # noqa: F401

@@ -92,13 +92,23 @@ static thread_local std::string g_last_error;
 // chain construction / destruction and every other allocation take this lock.
 static std::recursive_mutex g_dev_mu;
 static constexpr int RING_SLOTS = 32;  // recorded samples in flight between device and host
-// Kernel nodes per sweep graph.  rocprofv3 (rocprofiler-sdk, ROCm 7.2) faults inside its
-// queue interception -- reading past the end of a 1 MB host-mapped buffer, called from
-// hipGraphLaunch -> libhsa-runtime64 -> librocprofiler-sdk -- when a graph of thousands of
-// kernel nodes is launched (config 3: 8 sweeps x ~500 launches of the blocked
-// factorizations; gpurun_out/c3prof.err, s1_phy.err with HMSC_SEGV_DIAG=1).  Graphs are
-// kept to this many nodes; sweeps that need more run eagerly.
-static constexpr size_t GRAPH_MAX_NODES = 512;
+// Kernel nodes per sweep graph.  rocprofv3 (rocprofiler-sdk, ROCm 7.2) fails inside its
+// queue interception when a large graph is launched: SIGSEGV in librocprofiler-sdk.so called
+// from hipGraphLaunch (config 3: 431-node one-sweep and 3448-node eight-sweep graphs,
+// gpurun_out/s4_phy.err with HMSC_SEGV_DIAG=1), a hang for config 4's 512-node 64-sweep graph
+// (s5_g64.err), while 256 / 288-node graphs (config 4 at 32 sweeps per graph) and the same
+// phylo run without graphs (HMSC_NO_GRAPH=1) profile cleanly, and none of these graphs fail
+// without the profiler.  Under rocprofv3 (it exports ROCPROF_OUTPUT_PATH to the program)
+// graphs are therefore kept to 256 nodes and sweeps that need more run eagerly; otherwise
+// the cap only bounds instantiation cost.  HMSC_GRAPH_MAX_NODES overrides either.
+static size_t graph_max_nodes() {
+  static const size_t cap = [] {
+    if (const char* e = std::getenv("HMSC_GRAPH_MAX_NODES"))
+      if (e[0]) return (size_t)std::max(1L, std::atol(e));
+    return std::getenv("ROCPROF_OUTPUT_PATH") ? (size_t)256 : (size_t)8192;
+  }();
+  return cap;
+}
 
 static int fail(int code, const std::string& msg) {
   g_last_error = msg;
@@ -1149,7 +1159,7 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
       std::fprintf(stderr, "[hmsc] captured %d sweeps%s: %zu nodes%s\n", nsweeps, with_record ? " + record" : "",
                    nodes, steady ? "" : " (not steady)");
   hipGraphExec_t ge = nullptr;
-  if (steady && nodes <= GRAPH_MAX_NODES) HIP_OK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  if (steady && nodes <= graph_max_nodes()) HIP_OK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
   HIP_OK(hipGraphDestroy(g));
   return ge;
 }
@@ -1158,16 +1168,16 @@ static bool build_sweep_graphs(State& s, uint32_t iter) {
   destroy_graph(s);
   size_t nodes = 0;
   s.gexec = capture_sweeps(s, iter, false, &nodes);
-  if (!s.gexec && nodes > GRAPH_MAX_NODES && s.graph_sweeps > 1) {
+  if (!s.gexec && nodes > graph_max_nodes() && s.graph_sweeps > 1) {
     // a sweep with many launches (dense phylogeny / spatial factorizations): fewer sweeps
     // per graph, or none when one sweep alone exceeds the cap (its launch overhead is hidden
     // behind milliseconds of device work anyway)
     const size_t per_sweep = (nodes + s.graph_sweeps - 1) / s.graph_sweeps;
-    s.graph_sweeps = (int)std::max<size_t>(1, GRAPH_MAX_NODES / (per_sweep + 4));  // + the record pack
+    s.graph_sweeps = (int)std::max<size_t>(1, graph_max_nodes() / (per_sweep + 4));  // + the record pack
     s.gexec = capture_sweeps(s, iter, false, &nodes);
   }
   if (!s.gexec) {
-    if (nodes > GRAPH_MAX_NODES) s.use_graph = false;  // eager from here on
+    if (nodes > graph_max_nodes()) s.use_graph = false;  // eager from here on
     return false;
   }
   s.gexec_rec = capture_sweeps(s, iter, true);

@@ -680,6 +680,9 @@ __device__ __forceinline__ void gammav_body(const GVWArgs& a) {
   __shared__ __attribute__((aligned(16))) double T0[WV_TILE], T1[WV_TILE], T2[WV_TILE], T3[WV_TILE];
   __shared__ __attribute__((aligned(16))) double sXX[WV_TILE];  // X'X for wave 1 (ld WV_LD)
   __shared__ double sBTr[32];
+  // the constants the serial phases read (kron factors, prior terms), staged by all waves in
+  // phase A so that no global-memory latency sits inside the factorisation chains
+  __shared__ double sTT[NM * NM], sIV0[NM * NM], sIUG[NM * NM], sIUmG[NM];  // nt, nc <= N <= NM
   __shared__ int sok;
   double* sA = T0;
   const int nc = a.nc, nt = a.nt, N = nc * nt, t = threadIdx.x, w = t >> 6;
@@ -687,6 +690,11 @@ __device__ __forceinline__ void gammav_body(const GVWArgs& a) {
   HMSC_STAMP(0);
   if (t == 0) sok = 1;
   for (int p = t; p < nA; p += blockDim.x) sXX[p % nc + WV_LD * (p / nc)] = a.XX[p];
+  for (int p = t; p < nt * nt; p += blockDim.x) sTT[p] = a.TT[p];
+  for (int p = t; p < N * N; p += blockDim.x) sIUG[p] = a.iUGamma[p];
+  if (a.do_prep)
+    for (int p = t; p < nA; p += blockDim.x) sIV0[p] = a.iV0[p];
+  for (int p = t; p < N; p += blockDim.x) sIUmG[p] = a.iUmG[p];
   for (int p = t; p < nA + nB; p += blockDim.x) {
     // species-block partials in block order, 32 loads in flight (one L2 round trip per 32)
     const double* src = a.part + p;
@@ -755,11 +763,11 @@ __device__ __forceinline__ void gammav_body(const GVWArgs& a) {
   if (w == 0) {
     // Gamma | iV: prec = iUGamma + kron(TT, iV), rhs = iUGamma mGamma + vec(iV B Tr)   (:29-31)
     bool ok = sok != 0;
-    wv_kron<NM>(x, nc, nt, a.TT, 0.0, nullptr, 0, T1, WV_LD, a.iUGamma);
+    wv_kron<NM>(x, nc, nt, sTT, 0.0, nullptr, 0, T1, WV_LD, sIUG);
     double r = 0.0;
     if (i < N) {
       const int c1 = i % nc, t1 = i / nc;
-      r = a.iUmG[i];
+      r = sIUmG[i];
       for (int c2 = 0; c2 < nc; ++c2) r += T1[c1 + WV_LD * c2] * sBTr[c2 + nc * t1];
     }
     ok &= wv_chol<NM>(x, dinv);
@@ -791,7 +799,7 @@ __device__ __forceinline__ void gammav_body(const GVWArgs& a) {
   wv_gemm<NM, false, true>(y, x, z, S);                 // z = M = XX iP iV = XX B1^T
   wv_to_lds<NM>(z, T3);                                 // T3 = M
   wv_sync();
-  wv_kron<NM>(x, nc, nt, a.TT, 1.0, a.iV0, nc, T3, WV_LD, nullptr);  // Pg = I (x) iV0 + TT (x) M
+  wv_kron<NM>(x, nc, nt, sTT, 1.0, sIV0, nc, T3, WV_LD, nullptr);  // Pg = I (x) iV0 + TT (x) M
   wv_pad<NM>(x, N, 1.0);
   wv_to_lds<NM>(x, T0);
   wv_sync();
@@ -1342,12 +1350,16 @@ __device__ double wave_gamma_std(Key key, uint32_t idx, uint32_t stream, uint32_
   return out;
 }
 
-// any block size that is a multiple of 64: waves beyond the first repeat wave 0's gamma
-// trials (same values) and only thread 0 / threads t < nf write
+// any block size that is a multiple of 64.  The standard gamma draw of step h has shape
+// a + ns (nf - h) / 2 (R/updateLambdaPriors.R:26-31), independent of the chain -- only its
+// rate depends on the deltas drawn before it -- so the waves first draw all nf standard
+// gammas in parallel (wave w takes h = w, w + nwaves, ...), and the sequential chain that
+// remains is nf rate evaluations and divisions on one thread: the same values, in the same
+// order, as drawing gamma(shape, rate) step by step.
 __device__ __forceinline__ void delta_body(const LPArgs& a, const double* rs_part, int nparts, int r) {
-  // one wave per level: the sequential delta chain (R/updateLambdaPriors.R:25-32)
-  __shared__ double rs[64], delta[64];
-  const int t = threadIdx.x;
+  // one workgroup per level: the sequential delta chain (R/updateLambdaPriors.R:25-32)
+  __shared__ double rs[64], delta[64], gstd[64];
+  const int t = threadIdx.x, w = t >> 6, nw = blockDim.x >> 6;
   const int nf = a.lev_nf[r];
   int f0 = 0;
   for (int q = 0; q < r; ++q) f0 += a.lev_nf[q];
@@ -1357,24 +1369,28 @@ __device__ __forceinline__ void delta_body(const LPArgs& a, const double* rs_par
     rs[t] = sum;
     delta[t] = a.Delta[f0 + t];
   }
-  __syncthreads();
   if (r == 0) HMSC_STAMP(20);
   const uint32_t stream = S_DELTA + LEVEL_STRIDE * r;
   const double ns = (double)a.ns_glob;
-  for (int h = 0; h < nf; ++h) {
-    // sum_{h' >= h} tau_h' rs_h' / delta_h with tau = cumprod(current delta)
-    double c = 1.0, sum = 0.0;
-    for (int q = 0; q < nf; ++q) {
-      c *= delta[q];
-      if (q >= h) sum += c * rs[q];
-    }
+  for (int h = w; h < nf; h += nw) {
     const double ad = (h == 0 ? a.a1[r] : a.a2[r]) + 0.5 * ns * (nf - h);
-    const double bd = (h == 0 ? a.b1[r] : a.b2[r]) + 0.5 * sum / delta[h];
-    const double g = wave_gamma_std(a.key, (uint32_t)h, stream, SWEEP_ITER(a), ad) / bd;
-    __syncthreads();
-    if (t == 0) delta[h] = g;
-    __syncthreads();
+    const double g = wave_gamma_std(a.key, (uint32_t)h, stream, SWEEP_ITER(a), ad);
+    if ((t & 63) == 0) gstd[h] = g;
   }
+  __syncthreads();
+  if (t == 0) {
+    for (int h = 0; h < nf; ++h) {
+      // sum_{h' >= h} tau_h' rs_h' / delta_h with tau = cumprod(current delta)
+      double c = 1.0, sum = 0.0;
+      for (int q = 0; q < nf; ++q) {
+        c *= delta[q];
+        if (q >= h) sum += c * rs[q];
+      }
+      const double bd = (h == 0 ? a.b1[r] : a.b2[r]) + 0.5 * sum / delta[h];
+      delta[h] = gstd[h] / bd;
+    }
+  }
+  __syncthreads();
   if (t < nf) a.Delta[f0 + t] = delta[t];
   if (r == 0) HMSC_STAMP(21);
 }
@@ -1388,6 +1404,10 @@ __global__ __launch_bounds__(64) void delta_kernel(LPArgs a, const double* rs_pa
 // neither waits behind the other.
 template <int NM>
 __global__ __launch_bounds__(256) void side_chain_kernel(GVWArgs g, LPArgs lp, const double* rs_part, int nparts) {
+  // A latency-bound chain of small factorisations running beside the main stream's Eta and z
+  // waves on the same SIMDs: raised issue priority, so its few waves are not starved by the
+  // VALU-bound z waves (the arbiter picks the highest-priority ready wave).
+  __builtin_amdgcn_s_setprio(3);
   if (blockIdx.x == 0)
     gammav_body<NM>(g);
   else
@@ -1902,146 +1922,6 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
   }
 }
 
-// Eight waves per 16-site tile (512 threads): the Z stream of stage 1 is split over twice the
-// waves (5000 on the synthetic config instead of 2500, every one resident at once: <= 80 VGPRs
-// for NFB <= 12, three workgroups per CU) and each wave keeps two batches of four steps'
-// loads in flight (double-buffered registers: the next batch is issued before the current
-// one's MFMAs), so the stream no longer drains at every batch boundary.  Stages 2-4 as in the
-// four-wave kernel; the eight ZL partials are added in a fixed tree.
-template <int NFB>
-__global__ __launch_bounds__(512, NFB <= 12 ? 6 : 4) void eta_fused8_kernel(EtaFArgs a) {
-  __shared__ double sPart[8][16][EF_SITES + 1];  // [wave][factor][site] ZL partials
-  __shared__ double sW[NFB * NFB];            // W = L^-1, L the lower factor of Q (row m at m NFB)
-  __shared__ double sWs[NFB * (NFB + 1)];     // wv_inv_lower_rows scratch
-  __shared__ double sB[NFB][EF_SITES], sXi[NFB][EF_SITES], sU[NFB][EF_SITES];
-  __shared__ double sX[64][EF_SITES + 1];     // XEta tile [k][site] (K <= 64)
-  __shared__ double sCR[64 * NFB];            // CR[k][h], k < K
-  const unsigned long long kt0 = a.kt ? kt_now() : 0ull;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, lm = lane & 15, lk = lane >> 4;
-  const int ny = a.ny, nf = a.nf, K = a.K, nc = a.nc, ns = a.ns_loc;
-  const int i0 = blockIdx.x * EF_SITES;
-  if (blockIdx.x == 0) HMSC_STAMP(50);
-  // ---- stage 1: ZL = Z (Lambda diag(iSigma))^T on the matrix cores, the HBM stream of the
-  // launch, issued first: species j = 16 s + 4 w + lk, B = LS[j][lm] straight from L2 (128 KB,
-  // shared by every workgroup); eight steps' loads in flight before their MFMAs
-  d4 acc = {0.0, 0.0, 0.0, 0.0};
-  const double* zc = a.Z + min(i0 + lm, ny - 1);  // sites past ny: any finite row, unused
-  const int nsteps = (ns + 31) >> 5;                // step = 32 species, wave w: 32 s + 4 w + lk
-  double zv0[4], lv0[4], zv1[4], lv1[4];
-  auto load = [&](double (&zv)[4], double (&lv)[4], int s0) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int j = 32 * (s0 + u) + 4 * w + lk;
-      const bool in = s0 + u < nsteps && j < ns;
-      zv[u] = in ? zc[(size_t)ny * j] : 0.0;
-      lv[u] = in ? a.LS[(size_t)16 * j + lm] : 0.0;
-    }
-  };
-  load(zv0, lv0, 0);
-  for (int s = 0; s < nsteps; s += 8) {
-    load(zv1, lv1, s + 4);  // in flight while the MFMAs below wait for zv0 / lv0
-#pragma unroll
-    for (int u = 0; u < 4; ++u) acc = mfma_f64(zv0[u], lv0[u], acc);
-    load(zv0, lv0, s + 8);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) acc = mfma_f64(zv1[u], lv1[u], acc);
-  }
-  // acc[r] = partial ZL[site lk + 4 r][factor lm]
-#pragma unroll
-  for (int r = 0; r < 4; ++r) sPart[w][lm][lk + 4 * r] = acc[r];
-  // CR from its species-block partials, in block order (L2; every partial's load in flight
-  // before the adds)
-  for (int p = t; p < K * nf; p += 512) {
-    const int k = p % K, h = p / K;
-    const double* src = a.CR_part + k + (size_t)a.ldcr * h;
-    double v = 0.0;
-    int b = 0;
-    for (; b + 8 <= a.ncr; b += 8) {
-      double x[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) x[u] = src[(size_t)a.slab * (b + u)];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v += x[u];
-    }
-    for (; b < a.ncr; ++b) v += src[(size_t)a.slab * b];
-    sCR[k * NFB + h] = v;
-    if (blockIdx.x == 0) a.CR[k + (size_t)a.ldcr * h] = v;
-  }
-  __syncthreads();
-  if (blockIdx.x == 0) HMSC_STAMP(51);
-  if (w == 0) {  // Q = I + Lambda D Lambda^T factor, while waves 1-3 form the right-hand sides
-    double q[NFB], dinv;
-    const int r = lane < nf ? lane : 0;
-#pragma unroll
-    for (int c = 0; c < NFB; ++c) {
-      const double v = (r == c ? 1.0 : 0.0) + sCR[(nc + r) * NFB + (c < nf ? c : 0)];
-      q[c] = (lane < nf && c < nf) ? v : (lane == c ? 1.0 : 0.0);
-    }
-    wv_chol<NFB>(q, dinv);
-    double wr[NFB];
-    wv_inv_lower_rows<NFB>(q, dinv, wr, sWs);  // lane m: row m of L^-1
-    if (lane < NFB)
-#pragma unroll
-      for (int c = 0; c < NFB; ++c) sW[lane * NFB + c] = (lane < nf && c < nf && c <= lane) ? wr[c] : 0.0;
-  } else {
-    // ---- stage 2: b = ZL - X CR_x, and the noise, one (site, factor) per thread
-    for (int p = t - 64; p < EF_SITES * nf; p += 448) {
-      const int s2 = p % EF_SITES, h = p / EF_SITES, ii = i0 + s2;
-      const double zl = ((sPart[0][h][s2] + sPart[1][h][s2]) + (sPart[2][h][s2] + sPart[3][h][s2])) +
-                        ((sPart[4][h][s2] + sPart[5][h][s2]) + (sPart[6][h][s2] + sPart[7][h][s2]));
-      double corr = 0.0, xi = 0.0;
-      if (ii < ny) {
-        for (int k = 0; k < nc; ++k) corr = fma(a.XEta[ii + (size_t)ny * k], sCR[k * NFB + h], corr);
-        xi = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)a.Pi[ii], (uint32_t)h, S_ETA, SWEEP_ITER(a));
-      }
-      sB[h][s2] = zl - corr;
-      sXi[h][s2] = xi;
-    }
-    // X columns of the tile into the Gram tile
-    for (int p = t - 64; p < nc * EF_SITES; p += 448) {
-      const int s2 = p % EF_SITES, k = p / EF_SITES, ii = i0 + s2;
-      sX[k][s2] = ii < ny ? a.XEta[ii + (size_t)ny * k] : 0.0;
-    }
-  }
-  __syncthreads();
-  if (blockIdx.x == 0) HMSC_STAMP(53);
-  // ---- stage 3: eta = L^-T (L^-1 b + xi) = W^T (W b + xi), two matrix-vector phases over
-  // the (factor, site) pairs (no serial substitution chain)
-  for (int p = t; p < EF_SITES * nf; p += 512) {
-    const int s2 = p % EF_SITES, m = p / EF_SITES;
-    double u = sXi[m][s2];
-    for (int k = 0; k <= m; ++k) u = fma(sW[m * NFB + k], sB[k][s2], u);
-    sU[m][s2] = u;
-  }
-  __syncthreads();
-  for (int p = t; p < EF_SITES * nf; p += 512) {
-    const int s2 = p % EF_SITES, h = p / EF_SITES, ii = i0 + s2;
-    double e = 0.0;
-    for (int m = h; m < nf; ++m) e = fma(sW[m * NFB + h], sU[m][s2], e);
-    if (ii < ny) {
-      a.Eta[a.Pi[ii] + (size_t)a.np * h] = e;
-      a.XEta[ii + (size_t)ny * (nc + h)] = e;
-    }
-    sX[nc + h][s2] = ii < ny ? e : 0.0;
-  }
-  __syncthreads();
-  if (blockIdx.x == 0) HMSC_STAMP(54);
-  // ---- stage 4: Gram partial of the tile's Eta rows, Eta^T XEta (nf x K, ld Kmax)
-  double* dst = a.G_part + (size_t)blockIdx.x * a.Kmax * nf;
-  for (int p = t; p < K * nf; p += 512) {
-    const int k = p % K, h = p / K;
-    double g = 0.0;
-#pragma unroll
-    for (int s2 = 0; s2 < EF_SITES; ++s2) g = fma(sX[nc + h][s2], sX[k][s2], g);
-    dst[k + a.Kmax * h] = g;
-  }
-  if (blockIdx.x == 0) HMSC_STAMP(55);
-  if (a.kt) {
-    __syncthreads();
-    if (t == 0) kt_record(a.kt, SWEEP_ITER(a), kt0);
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Co-launched side updaters (one queue).  After BetaLambda a sweep has three independent
 // species-parallel passes -- CR for updateEta, the GammaV partials (R/updateGammaV.R:17-19)
@@ -2234,22 +2114,12 @@ static void launch_eta_fused(State& s, uint32_t iter, bool cr_done = false) {
   const int ntile = (s.ny + EF_SITES - 1) / EF_SITES;
   {
     ProfScope ps(s, PROF_ETA_UNIT);
-    static const bool four = getenv_flag("HMSC_ETA_FOUR_WAVES");  // A/B: the four-wave kernel
-    if (four) {
-      if (L.nf <= 8)
-        eta_fused_kernel<8><<<ntile, 256, 0, s.stream>>>(a);
-      else if (L.nf <= 12)
-        eta_fused_kernel<12><<<ntile, 256, 0, s.stream>>>(a);
-      else
-        eta_fused_kernel<16><<<ntile, 256, 0, s.stream>>>(a);
-    } else {
-      if (L.nf <= 8)
-        eta_fused8_kernel<8><<<ntile, 512, 0, s.stream>>>(a);
-      else if (L.nf <= 12)
-        eta_fused8_kernel<12><<<ntile, 512, 0, s.stream>>>(a);
-      else
-        eta_fused8_kernel<16><<<ntile, 512, 0, s.stream>>>(a);
-    }
+    if (L.nf <= 8)
+      eta_fused_kernel<8><<<ntile, 256, 0, s.stream>>>(a);
+    else if (L.nf <= 12)
+      eta_fused_kernel<12><<<ntile, 256, 0, s.stream>>>(a);
+    else
+      eta_fused_kernel<16><<<ntile, 256, 0, s.stream>>>(a);
     HIP_OK(hipGetLastError());
   }
   // G's Eta rows: reduced from G_part by the next updateZ launch (or flush_g)

@@ -15,6 +15,10 @@ timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu > gpurun_out/${
 cat gpurun_out/${TAG}_b20.json; grep hmsc gpurun_out/${TAG}_b20.err | head
 timeout -k 10 300 python bench.py --steps 1000 --warmup 100 --no-cpu > gpurun_out/${TAG}_b1000.json 2> gpurun_out/${TAG}_b1000.err || { echo "bench1000 failed"; tail -20 gpurun_out/${TAG}_b1000.err; exit 1; }
 cat gpurun_out/${TAG}_b1000.json
+HMSC_ETA_FOUR_WAVES=1 timeout -k 10 300 python bench.py --steps 1000 --warmup 100 --no-cpu > gpurun_out/${TAG}_b1000_eta4.json 2>/dev/null || { echo "bench eta4 failed"; exit 1; }
+cat gpurun_out/${TAG}_b1000_eta4.json
+timeout -k 10 200 python scripts/stamps_sweep.py > gpurun_out/${TAG}_stamps.log 2>&1 || { echo "stamps failed"; tail gpurun_out/${TAG}_stamps.log; exit 1; }
+cat gpurun_out/${TAG}_stamps.log
 timeout -k 10 600 python -u scripts/diag_spatial_chain.py 1000,1100,2100,5000 40 > gpurun_out/${TAG}_spchain.json 2> gpurun_out/${TAG}_spchain.err || { echo "spchain failed"; tail -20 gpurun_out/${TAG}_spchain.err; exit 1; }
 cat gpurun_out/${TAG}_spchain.json
 cd /tmp && export TMPDIR=/tmp

@@ -91,9 +91,12 @@ def oracle_model(hM):
              rhopw=hM.rhopw, C=hM.C,
              rL=[dict(nu=rl.nu, a1=rl.a1, b1=rl.b1, a2=rl.a2, b2=rl.b2, nfMin=rl.nfMin, nfMax=rl.nfMax,
                       sDim=rl.sDim, xDim=rl.xDim) for rl in (hM.rL or [])])
-    for d, rl in zip(m["rL"], hM.rL or []):
+    for r, (d, rl) in enumerate(zip(m["rL"], hM.rL or [])):
         if rl.sDim:   # spatial 'Full': the distance matrix of the unit coordinates, alphapw grid
-            xy = np.asarray(rl.s, dtype=np.float64)
+            # rows of rl$s in levels(dfPi[,r]) order, the unit order of Eta (R indexes s by
+            # the unit names, R/computeDataParameters.R:56,92,142)
+            from hmsc_amd.dataparams import _level_order
+            xy = np.asarray(rl.s, dtype=np.float64)[_level_order(hM, r, rl)]
             d.update(spatialMethod=rl.spatialMethod, alphapw=np.asarray(rl.alphapw, dtype=np.float64),
                      dist=np.sqrt(((xy[:, None, :] - xy[None, :, :]) ** 2).sum(-1)),
                      s=xy, nNeighbours=rl.nNeighbours,
