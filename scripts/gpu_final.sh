@@ -15,9 +15,12 @@ bash scripts/pmc_z.sh ${TAG}_pmc "z_wave|eta_fused|beta_lambda|side_chain" || ex
 python scripts/pmc_summary.py gpurun_out/${TAG}_pmc > gpurun_out/${TAG}_pmc.json || exit 1
 timeout -k 10 600 python bench.py --steps 1000 --warmup 100 --pmc-json gpurun_out/${TAG}_pmc.json > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { echo "bench failed"; tail -20 gpurun_out/${TAG}_bench.err; exit 1; }
 cat gpurun_out/${TAG}_bench.json
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --pmc-json gpurun_out/${TAG}_pmc.json --no-cpu > gpurun_out/${TAG}_b20.json 2> gpurun_out/${TAG}_b20.err || { echo "bench20 failed"; tail -20 gpurun_out/${TAG}_b20.err; exit 1; }
+cat gpurun_out/${TAG}_b20.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_prof -o run -- python $R/bench.py --steps 1000 --warmup 100 --no-cpu --pmc-json $R/gpurun_out/${TAG}_pmc.json > $R/gpurun_out/${TAG}_prof_bench.json 2> $R/gpurun_out/${TAG}_prof.err || { echo "rocprof failed"; tail -20 $R/gpurun_out/${TAG}_prof.err; exit 1; }
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_chol -o run -- python $R/scripts/chol_bench.py 5000 3 > $R/gpurun_out/${TAG}_chol.log 2>&1 || { echo "chol profile failed"; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_phyprof -o run -- python3 $R/bench.py --workload phylo --steps 100 --warmup 100 --no-cpu > $R/gpurun_out/${TAG}_phyprof.json 2> $R/gpurun_out/${TAG}_phyprof.err || { echo "phylo rocprof failed"; tail -5 $R/gpurun_out/${TAG}_phyprof.err; exit 1; }
 cd $R
 timeout -k 10 300 python bench.py --workload phylo --steps 200 --warmup 200 > gpurun_out/${TAG}_config3.json 2>/dev/null || exit 1
 timeout -k 10 300 python bench.py --workload spatial --method GPP --steps 500 --warmup 50 > gpurun_out/${TAG}_config5_gpp.json 2>/dev/null || exit 1
