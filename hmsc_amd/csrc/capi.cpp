@@ -91,7 +91,10 @@ static thread_local std::string g_last_error;
 // (hipMalloc / hipFree / hipDeviceSynchronize): those would invalidate it.  Captures,
 // chain construction / destruction and every other allocation take this lock.
 static std::recursive_mutex g_dev_mu;
-static constexpr int RING_SLOTS = 32;  // recorded samples in flight between device and host
+// recorded samples in flight between device and host: two replays' worth (a replay's samples
+// are copied and unpacked while the next replay runs), at most ~256 MB of pinned host memory
+static constexpr int RING_SLOTS_MIN = 8;
+static constexpr size_t RING_BYTES_MAX = (size_t)256 << 20;
 // Kernel nodes per sweep graph.  rocprofv3 (rocprofiler-sdk, ROCm 7.2) fails inside its
 // queue interception when a large graph is launched: SIGSEGV in librocprofiler-sdk.so called
 // from hipGraphLaunch (config 3: 431-node one-sweep and 3448-node eight-sweep graphs,
@@ -108,6 +111,15 @@ static size_t graph_max_nodes() {
     return std::getenv("ROCPROF_OUTPUT_PATH") ? (size_t)256 : (size_t)8192;
   }();
   return cap;
+}
+
+int z_log_table_doubles();           // zdraw.hip
+void z_log_table_fill(double* t);
+
+static int graph_level(int n) {  // floor(log2 n)
+  int k = 0;
+  while ((1 << (k + 1)) <= n) ++k;
+  return k;
 }
 
 static int fail(int code, const std::string& msg) {
@@ -556,6 +568,11 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
     }
     s.Ybits = dupload(yb.data(), yb.size());
   }
+  {  // the z kernel's log table (z_kernel.h log_tab)
+    std::vector<double> lt(z_log_table_doubles());
+    z_log_table_fill(lt.data());
+    s.logtab = dupload(lt.data(), lt.size());
+  }
   if (!s.all_probit) {
     s.Yval = dupload(yval.data(), yval.size());
     s.Yraw = dupload(yraw.data(), yraw.size());
@@ -686,10 +703,20 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
     }
     s.geWork = dalloc<double>(gamma_eta_work_doubles(s));
   }
-  // recording ring: RING_SLOTS device slots, their pinned host mirror and the copied counter,
-  // allocated once here so no run pays for pinning
+  {
+    const char* g = getenv("HMSC_GRAPH_SWEEPS");
+    // a power of two (remainders replay graphs of the smaller powers); one replay launch per
+    // 32 sweeps at a steady state (8 was +1.8 % over 4)
+    s.graph_sweeps = 1 << graph_level(g ? std::max(1, std::min(64, atoi(g))) : 32);
+  }
+  // recording ring: device slots for two replays, their pinned host mirror and the copied
+  // counter, allocated once here so no run pays for pinning
   s.slot_doubles = record_slot_doubles(s);
-  s.ring_slots = RING_SLOTS;
+  {
+    const size_t fit = RING_BYTES_MAX / std::max<size_t>(1, sizeof(double) * s.slot_doubles);
+    s.ring_slots = (int)std::max<size_t>(RING_SLOTS_MIN, std::min<size_t>(2 * (size_t)s.graph_sweeps, fit));
+    while (s.graph_sweeps > 1 && 2 * s.graph_sweeps > s.ring_slots) s.graph_sweeps >>= 1;
+  }
   s.ring = dalloc<double>(s.slot_doubles * s.ring_slots);
   HIP_OK(hipHostMalloc(&s.host_rec, sizeof(double) * s.slot_doubles * s.ring_slots, hipHostMallocDefault));
   HIP_OK(hipHostMalloc(&s.copied_host, 64, hipHostMallocMapped | hipHostMallocCoherent));
@@ -698,10 +725,6 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.d_iter_side = dalloc<uint32_t>(1);
   s.gv_part = dalloc<double>((size_t)((nsl + 31) / 32) * (nc * nc + nc * nt));
   HIP_OK(hipEventCreateWithFlags(&s.ev_graph, hipEventDisableTiming));
-  {
-    const char* g = getenv("HMSC_GRAPH_SWEEPS");
-    s.graph_sweeps = g ? std::max(1, std::min(64, atoi(g))) : 8;  // 8: +1.8 % over 4 (one replay launch per 8 sweeps)
-  }
   {
     const char* g1 = getenv("HMSC_SINGLE_STREAM");
     s.single_stream = g1 && g1[0] == '1';
@@ -715,7 +738,7 @@ static void free_state(State& s) {
   std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
   DeviceGuard dg(s.device);
   (void)hipDeviceSynchronize();
-  void* ptrs[] = {s.X, s.Tr, s.Yval, s.Yraw, s.Ycode, s.Ybits, s.fam, s.varest, s.V0, s.iUGamma, s.mGamma, s.UGammaL,
+  void* ptrs[] = {s.X, s.Tr, s.Yval, s.Yraw, s.Ycode, s.Ybits, s.logtab, s.fam, s.varest, s.V0, s.iUGamma, s.mGamma, s.UGammaL,
                   s.aSigma, s.bSigma, s.XX, s.TT, s.V0g, s.V0gXXV0g, s.iV0, s.V0inv, s.iUmG, s.V0gXX, s.g2prep, s.scratch2, s.na_cols, s.na_index,
                   s.na_rows, s.row_na, s.row_slot, s.dev_flags, s.Z, s.XEta, s.BL, s.Psi, s.Delta, s.Gamma, s.iV,
                   s.iSigma, s.rho, s.XZ, s.G, s.ZTr, s.XZ_part, s.G_part, s.ZTr_part, s.Gna, s.ZL, s.ZL_part,
@@ -736,8 +759,9 @@ static void free_state(State& s) {
   if (s.gv_part) (void)hipFree(s.gv_part);
   if (s.host_rec) (void)hipHostFree(s.host_rec);
   if (s.copied_host) (void)hipHostFree(s.copied_host);
-  for (hipGraphExec_t g : {s.gexec, s.gexec_rec, s.gexec1, s.gexec1_rec})
-    if (g) (void)hipGraphExecDestroy(g);
+  for (auto& row : s.gx)
+    for (hipGraphExec_t g : row)
+      if (g) (void)hipGraphExecDestroy(g);
   if (s.d_iters) (void)hipFree(s.d_iters);
   if (s.d_kt) (void)hipFree(s.d_kt);
   if (s.comm) ncclCommDestroy((ncclComm_t)s.comm);
@@ -1085,9 +1109,9 @@ static void sweep(State& s, uint32_t iter, bool adapt) {
 // of ~20 kernel launches + event records per sweep, and the relaunch gap between replays is
 // paid once per replay.  Kernels captured with s.capturing read the Philox sweep counter
 // from s.d_iter, which for the i-th captured sweep is slot i of s.d_iters; one small kernel
-// writes iter .. iter + graph_sweeps - 1 into the slots before each replay.  gexec_rec is the same sequence
-// with the record pack after every sweep; the pack picks its ring slot (or returns, for a
-// sweep that is not recorded) from d_iter and the run descriptor d_rec_desc.
+// writes iter .. iter + n - 1 into the slots before each replay.  gx[1][k] is the same
+// sequence with the record pack after every sweep; the pack picks its ring slot (or returns,
+// for a sweep that is not recorded) from d_iter and the run descriptor d_rec_desc.
 // Pack the state after a sweep into a ring slot (nullptr: chosen on the device in a graph
 // replay).  With co-launched side updaters the side stream's outputs are packed on it, so
 // the main stream need not wait for the GammaV algebra.
@@ -1110,11 +1134,14 @@ __global__ void set_desc_kernel(int32_t* d, int32_t iter0, int32_t transient, in
 }
 
 static void destroy_graph(State& s) {
-  for (hipGraphExec_t* g : {&s.gexec, &s.gexec_rec, &s.gexec1, &s.gexec1_rec}) {
-    if (*g) (void)hipGraphExecDestroy(*g);
-    *g = nullptr;
-  }
+  for (auto& row : s.gx)
+    for (hipGraphExec_t& g : row) {
+      if (g) (void)hipGraphExecDestroy(g);
+      g = nullptr;
+    }
 }
+
+
 
 // Captures graph_sweeps sweeps (with or without the record pack after each).  Returns
 // nullptr when the sweep is not in a steady state, i.e. the host-side validity flags it
@@ -1164,30 +1191,38 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
   return ge;
 }
 
+// Graphs of graph_sweeps, graph_sweeps / 2, ..., 1 sweeps, with and without the record pack:
+// a run of n sweeps replays n's binary decomposition (at most log2(graph_sweeps) + 1 replays
+// for the remainder, instead of one replay per remaining sweep).
 static bool build_sweep_graphs(State& s, uint32_t iter) {
   destroy_graph(s);
   size_t nodes = 0;
-  s.gexec = capture_sweeps(s, iter, false, &nodes);
-  if (!s.gexec && nodes > graph_max_nodes() && s.graph_sweeps > 1) {
+  const int top = graph_level(s.graph_sweeps);
+  s.gx[0][top] = capture_sweeps(s, iter, false, &nodes);
+  if (!s.gx[0][top] && nodes > graph_max_nodes() && s.graph_sweeps > 1) {
     // a sweep with many launches (dense phylogeny / spatial factorizations): fewer sweeps
     // per graph, or none when one sweep alone exceeds the cap (its launch overhead is hidden
     // behind milliseconds of device work anyway)
     const size_t per_sweep = (nodes + s.graph_sweeps - 1) / s.graph_sweeps;
-    s.graph_sweeps = (int)std::max<size_t>(1, graph_max_nodes() / (per_sweep + 4));  // + the record pack
-    s.gexec = capture_sweeps(s, iter, false, &nodes);
+    const int fit = (int)std::max<size_t>(1, graph_max_nodes() / (per_sweep + 4));  // + the record pack
+    s.graph_sweeps = 1 << graph_level(fit);
+    s.gx[0][graph_level(s.graph_sweeps)] = capture_sweeps(s, iter, false, &nodes);
   }
-  if (!s.gexec) {
+  const int lv = graph_level(s.graph_sweeps);
+  if (!s.gx[0][lv]) {
     if (nodes > graph_max_nodes()) s.use_graph = false;  // eager from here on
     return false;
   }
-  s.gexec_rec = capture_sweeps(s, iter, true);
-  if (!s.gexec_rec) {
-    destroy_graph(s);
-    return false;
-  }
-  if (s.graph_sweeps > 1) {  // remainders of a run (optional: eager sweeps otherwise)
-    s.gexec1 = capture_sweeps(s, iter, false, nullptr, 1);
-    s.gexec1_rec = s.gexec1 ? capture_sweeps(s, iter, true, nullptr, 1) : nullptr;
+  for (int k = lv; k >= 0; --k) {
+    if (k < lv) s.gx[0][k] = capture_sweeps(s, iter, false, nullptr, 1 << k);
+    if (s.gx[0][k]) s.gx[1][k] = capture_sweeps(s, iter, true, nullptr, 1 << k);
+    if (!s.gx[0][k] || !s.gx[1][k]) {
+      if (k == lv) {
+        destroy_graph(s);
+        return false;
+      }
+      break;  // smaller remainders run eagerly
+    }
   }
   s.graph_K = s.K;
   s.graph_NF = s.NF;
@@ -1195,19 +1230,18 @@ static bool build_sweep_graphs(State& s, uint32_t iter) {
   return true;
 }
 
-// Runs sweeps iter .. iter+n-1 (n == graph_sweeps, or 1 for the remainder of a run) as one
+static bool graphs_built(const State& s) { return s.gx[0][graph_level(s.graph_sweeps)] != nullptr; }
+
+// Runs sweeps iter .. iter+n-1 (n a power of two <= graph_sweeps) as one
 // graph replay if the graphs exist or can be built now; returns false (nothing launched) when
 // the caller must run eagerly.
 static bool replay_sweeps(State& s, uint32_t iter, bool with_record, int n) {
   if (!s.use_graph || s.nranks != 1 || s.prof) return false;
-  if (s.gexec && (s.graph_dirty || s.graph_K != s.K || s.graph_NF != s.NF)) destroy_graph(s);
+  if (graphs_built(s) && (s.graph_dirty || s.graph_K != s.K || s.graph_NF != s.NF)) destroy_graph(s);
   if (s.graph_dirty) s.eager_streak = 0, s.graph_dirty = false;
-  if (!s.gexec && (s.eager_streak < 1 || !build_sweep_graphs(s, iter))) return false;  // steady first
-  hipGraphExec_t ge = nullptr;
-  if (n == s.graph_sweeps)
-    ge = with_record ? s.gexec_rec : s.gexec;
-  else if (n == 1)
-    ge = with_record ? s.gexec1_rec : s.gexec1;
+  if (!graphs_built(s) && (s.eager_streak < 1 || !build_sweep_graphs(s, iter))) return false;  // steady first
+  if (n < 1 || n > s.graph_sweeps || (n & (n - 1))) return false;
+  hipGraphExec_t ge = s.gx[with_record ? 1 : 0][graph_level(n)];
   if (!ge) return false;
   join_side(s);
   set_iters_kernel<<<1, 64, 0, s.stream>>>(s.d_iters, iter, n);
@@ -1276,6 +1310,36 @@ static void unpack_record(const State& s, const double* slot, int k, int samples
   }
 }
 
+// First write to each page of sample k's slice of the caller's record arrays (zeros: every
+// element of the slice is overwritten by unpack_record).  Fresh arrays (numpy zeros = untouched
+// anonymous memory) fault on their first write, and that -- not the copy -- was most of an
+// unpack (~100 us per 1.1 MB sample); an unpack worker does it for the sample it waits for,
+// while the GPU is still producing it.
+static void pretouch_record(const State& s, int k, const hmsc_record* rec) {
+  constexpr size_t PG = 4096;
+  auto touch = [&](void* base, size_t elem, size_t n) {
+    if (!base || n == 0) return;
+    char* p = (char*)base + (size_t)k * elem * n;
+    const size_t bytes = elem * n;
+    // first byte of the slice, then every page boundary inside it, then its last element
+    volatile char* vp = p;
+    vp[0] = 0;
+    for (size_t o = PG - ((uintptr_t)p & (PG - 1)); o < bytes; o += PG) vp[o] = 0;
+    vp[bytes - 1] = 0;
+  };
+  const size_t nc = s.nc, nsl = s.nsl;
+  touch(rec->Beta, sizeof(double), nc * nsl);
+  touch(rec->Gamma, sizeof(double), nc * s.nt);
+  touch(rec->iV, sizeof(double), nc * nc);
+  touch(rec->iSigma, sizeof(double), nsl);
+  for (int r = 0; r < s.nr; ++r) {
+    const size_t nfm = s.lev[r].nfmax;
+    touch(rec->Eta[r], sizeof(double), (size_t)s.lev[r].np * nfm);
+    touch(rec->Lambda[r], sizeof(double), nfm * nsl);
+    touch(rec->Psi[r], sizeof(double), nfm * nsl);
+  }
+}
+
 static void run(State& s, int transient, int samples, int thin, const int* adaptNf, int iter0, int verbose,
                 int chain, hmsc_record* rec) {
   DeviceGuard dg(s.device);
@@ -1302,7 +1366,7 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
   volatile uint64_t* copied = s.copied_host;
   if (recording) *copied = 0;           // no copy is in flight between runs
   const char* w_env = getenv("HMSC_UNPACK_THREADS");
-  const int W = recording ? std::max(1, std::min(w_env ? atoi(w_env) : 2,
+  const int W = recording ? std::max(1, std::min(w_env ? atoi(w_env) : 4,
                                                  std::max(1, (int)std::thread::hardware_concurrency() / 2)))
                           : 0;
   std::vector<std::thread> workers;
@@ -1319,6 +1383,7 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
     workers.emplace_back([&, w] {
       try {
         for (int k = w; k < samples; k += W) {
+          if (__atomic_load_n(copied, __ATOMIC_ACQUIRE) <= (uint64_t)k) pretouch_record(s, k, rec);
           for (int spin = 0; __atomic_load_n(copied, __ATOMIC_ACQUIRE) <= (uint64_t)k; ++spin) {
             if (stop.load(std::memory_order_relaxed)) return;
             if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
@@ -1380,7 +1445,8 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
     bool replayed = false;
     int kfirst = -1, klast = -1;
     if (it > max_adapt) {
-      const int ng = it + G - 1 <= total ? G : 1;  // the run's remainder: one-sweep graphs
+      int ng = G;  // the run's remainder: its binary decomposition, largest graph first
+      while (ng > 1 && it + ng - 1 > total) ng >>= 1;
       for (int j = it; j < it + ng; ++j)
         if (recorded(j)) {
           if (kfirst < 0) kfirst = sample_of(j);
@@ -1719,14 +1785,15 @@ int hmsc_prepare_graphs(hmsc_state* h, int32_t iter, int32_t* built) {
     DeviceGuard dg(s.device);
     *built = 0;
     if (!s.use_graph || s.nranks != 1 || s.prof) return;
-    if (s.gexec && (s.graph_dirty || s.graph_K != s.K || s.graph_NF != s.NF)) destroy_graph(s);
-    if (!s.gexec) {
+    if (graphs_built(s) && (s.graph_dirty || s.graph_K != s.K || s.graph_NF != s.NF)) destroy_graph(s);
+    if (!graphs_built(s)) {
       if (s.graph_dirty) s.eager_streak = 0, s.graph_dirty = false;
       if (s.eager_streak < 1 || !build_sweep_graphs(s, (uint32_t)iter)) return;
     }
     // make the executable graphs device-resident now, not at their first launch
-    for (hipGraphExec_t g : {s.gexec, s.gexec_rec, s.gexec1, s.gexec1_rec})
-      if (g) HIP_OK(hipGraphUpload(g, s.stream));
+    for (auto& row : s.gx)
+      for (hipGraphExec_t g : row)
+        if (g) HIP_OK(hipGraphUpload(g, s.stream));
     HIP_OK(hipStreamSynchronize(s.stream));
     *built = 1;
   });
@@ -1778,7 +1845,8 @@ int hmsc_debug_get(hmsc_state* h, const char* name, double* out, int64_t n) {
       return;
     } else if (nm == "graph") {
       HMSC_REQUIRE(n >= 4, "graph needs 4 slots");
-      const double d[4] = {(double)(s.gexec != nullptr), (double)(s.gexec_rec != nullptr), (double)s.graph_sweeps,
+      const int top = graph_level(s.graph_sweeps);
+      const double d[4] = {(double)(s.gx[0][top] != nullptr), (double)(s.gx[1][top] != nullptr), (double)s.graph_sweeps,
                            (double)s.eager_streak};
       std::memcpy(out, d, sizeof(d));
       return;

@@ -93,6 +93,34 @@ __host__ __device__ __forceinline__ Uniform2 uniforms(Key key, uint32_t idx, uin
   return Uniform2{u53(r.x, r.y), u53(r.z, r.w)};
 }
 
+// The same Philox4x32-10 for a wave-uniform key (a kernel argument: the key words stay in
+// SGPRs and the round keys are scalar adds): each round's two three-way XORs are single
+// gfx950 v_bitop3_b32 instructions (truth table 0x96 = a ^ b ^ c) taking the round key as
+// their SGPR operand (the compiler emits two v_xor_b32 each).  Same values as philox4x32_10.
+__device__ __forceinline__ U4 philox4x32_10_wave_key(U4 c, Key key) {
+  uint32_t k0 = key.k0, k1 = key.k1;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t x, z;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(x) : "v"(hi1), "v"(c.y), "s"(k0));
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(z) : "v"(hi0), "v"(c.w), "s"(k1));
+    c = U4{x, lo1, z, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+__device__ __forceinline__ Uniform2 uniforms_wave_key(Key key, uint32_t idx, uint32_t sub, uint32_t stream,
+                                                      uint32_t iter) {
+  const U4 r = philox4x32_10_wave_key(U4{idx, sub, stream, iter}, key);
+  return Uniform2{u53(r.x, r.y), u53(r.z, r.w)};
+}
+
 // Phi^-1(p), Wichura (1988) AS241 PPND16 (the algorithm behind R's qnorm), |rel err| ~1e-16.
 __host__ __device__ __forceinline__ double qnorm_as241(double p) {
   const double q = p - 0.5;

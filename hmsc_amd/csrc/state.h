@@ -100,6 +100,7 @@ struct State {
   double *X = nullptr, *Tr = nullptr, *Yval = nullptr, *Yraw = nullptr;
   int8_t* Ycode = nullptr;
   uint64_t* Ybits = nullptr;     // ceil(nsl / 32) x ny: the same codes + 1, 2 bits per species (z kernel)
+  double* logtab = nullptr;      // z_log_table: the z kernel's table log (ZLOG_N x 4)
   int* fam = nullptr;            // ns_loc family code
   int* varest = nullptr;         // ns_loc distr[,2]
   double *V0 = nullptr, *iUGamma = nullptr, *mGamma = nullptr, *UGammaL = nullptr, *UGamma = nullptr;
@@ -180,17 +181,19 @@ struct State {
   // per-sweep hipGraph (single rank, no updateNf): captured once, replayed every sweep; the
   // kernels read the Philox sweep counter from d_iter, which the graph's first node advances
   uint32_t* d_iter = nullptr;          // the Philox sweep counter captured kernels read (a slot of d_iters)
-  uint32_t* d_iters = nullptr;         // one counter per captured sweep, set once per replay
+  uint32_t* d_iters = nullptr;         // one counter per captured sweep; a replay's last kernel advances them
   bool capturing = false;
   bool use_graph = true;
   bool graph_dirty = true;
   int graph_K = -1, graph_NF = -1;
-  hipGraphExec_t gexec = nullptr;
-  hipGraphExec_t gexec_rec = nullptr;  // the same sweeps, each followed by the record pack
-  hipGraphExec_t gexec1 = nullptr;     // one sweep (run lengths that are not a multiple of graph_sweeps)
-  hipGraphExec_t gexec1_rec = nullptr;
+  // gx[rec][k]: 2^k consecutive sweeps (rec: each followed by the record pack), k = 0 ..
+  // log2(graph_sweeps); a run of n sweeps replays its binary decomposition, largest first
+  static constexpr int GRAPH_LEVELS = 7;  // up to 64 sweeps per replay
+  hipGraphExec_t gx[2][GRAPH_LEVELS] = {};
   bool single_stream = false;          // HMSC_SINGLE_STREAM: no side-stream overlap (diagnostic)
-  int graph_sweeps = 4;                 // sweeps per replay (HMSC_GRAPH_SWEEPS)
+  int graph_sweeps = 4;                 // sweeps per replay, a power of two (HMSC_GRAPH_SWEEPS)
+  uint32_t dev_iter_next = 0;           // the sweep the device's d_iters slots already hold (valid_iters)
+  bool valid_iters = false;
   int32_t* d_rec_desc = nullptr;        // {iter0, transient, thin, samples} of the current run
   hipEvent_t ev_graph = nullptr;        // after a recording replay: the copy stream waits on it
   int eager_streak = 0;          // eager steady sweeps since the graph was invalidated

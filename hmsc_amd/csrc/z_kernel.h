@@ -55,6 +55,7 @@ struct ZArgs {
   const double* gred_part;
   const double* gred_XX;
   double* gred_G;
+  const double* logtab;  // z_log_table (ZLOG_N x 4 doubles), staged in LDS by every workgroup
 };
 
 constexpr int ZT_I = 64;   // sites per workgroup tile (4 waves x 16)
@@ -109,11 +110,50 @@ __device__ __noinline__ double z_probit_draw(double e, double sd, double isd, in
 // same arithmetic as trunc_normal_lower (rng.h) on each cell, two independent dependency
 // chains per lane.  Tails (alpha > 25, or a quantile outside qnorm_fast's central branch,
 // w >= 6.25) take the scalar path.
+// log x for positive normal x by Tang's table method: x = m 2^e with m in [1, 2), c_j the
+// midpoint of the 1/64-wide interval holding m (its top six mantissa bits), r = (m - c_j) / c_j
+// with |r| <= 1/129, log x = e ln2 + log c_j + log1p(r), log1p by its degree-8 series (|r^9/9|
+// < 1e-20).  The table row j = {1 / c_j, log c_j = hi + lo, 0} lives in LDS (z_log_table fills
+// it on the host in extended precision); ~19 VALU instructions, against ~33 for log_fast's
+// reciprocal and degree-10 atanh series.
+constexpr int ZLOG_N = 64;
+inline void z_log_table(double* t) {
+  for (int j = 0; j < ZLOG_N; ++j) {
+    const long double c = 1.0L + (2 * j + 1) / 128.0L;
+    const long double l = logl(c);
+    t[4 * j] = (double)(1.0L / c);
+    t[4 * j + 1] = (double)l;
+    t[4 * j + 2] = (double)(l - (long double)t[4 * j + 1]);
+    t[4 * j + 3] = 0.0;
+  }
+}
+HMSC_TABLE double kLog1pSeries[8] = {-1.0 / 8.0, 1.0 / 7.0, -1.0 / 6.0, 1.0 / 5.0,
+                                     -1.0 / 4.0, 1.0 / 3.0, -1.0 / 2.0, 1.0};
+__device__ __forceinline__ double log_tab(double x, const double* tab) {
+  const int e = __builtin_amdgcn_frexp_exp(x) - 1;        // x = m2 2^e, m2 in [1, 2)
+  const double m2 = 2.0 * __builtin_amdgcn_frexp_mant(x);
+  uint64_t b;
+  __builtin_memcpy(&b, &m2, 8);
+  const uint32_t hi = (uint32_t)(b >> 32);
+  const int j = (int)((hi >> 14) & 63u);
+  const uint64_t cb = (uint64_t)((hi & 0xFFFFC000u) | 0x2000u) << 32;  // c_j = 1 + j / 64 + 1 / 128
+  double c;
+  __builtin_memcpy(&c, &cb, 8);
+  const double* tj = tab + 4 * j;
+  const double r = (m2 - c) * tj[0];                      // m2 - c_j exact
+  double P = kLog1pSeries[0];
+#pragma unroll
+  for (int k = 1; k < 8; ++k) P = fma_sc(P, r, kLog1pSeries[k]);
+  const double de = (double)e;
+  return fma(de, 0.6931471803691238, tj[1]) + fma(r, P, fma(de, 1.9082149292705877e-10, tj[2]));
+}
+
 struct ZPair {
   double z0, z1;
 };
 __device__ __forceinline__ ZPair z_probit_pair(double e0, double e1, double sd0, double sd1, double isd0, double isd1,
-                                            int c0, int c1, double u0, double u1, int noise_zero) {
+                                            int c0, int c1, double u0, double u1, int noise_zero,
+                                            const double* ltab) {
   const double sg0 = c0 == 0 ? -1.0 : 1.0, sg1 = c1 == 0 ? -1.0 : 1.0;
   const double al0 = c0 < 0 ? -INFINITY : -sg0 * e0 * isd0;
   const double al1 = c1 < 0 ? -INFINITY : -sg1 * e1 * isd1;
@@ -136,32 +176,8 @@ __device__ __forceinline__ ZPair z_probit_pair(double e0, double e1, double sd0,
     const double r0 = t0 * exp_small(fma(-a0, a0, g0)), r1 = t1 * exp_small(fma(-a1, a1, g1));
     const double p0 = u0 * (0.5 * (h0 < 0.0 ? 2.0 - r0 : r0));
     const double p1 = u1 * (0.5 * (h1 < 0.0 ? 2.0 - r1 : r1));
-    // w = -log_fast(4 p (1 - p)) for both cells, interleaved
-    const double m0 = 4.0 * p0 * (1.0 - p0), m1 = 4.0 * p1 * (1.0 - p1);
-    uint64_t b0, b1;
-    __builtin_memcpy(&b0, &m0, 8);
-    __builtin_memcpy(&b1, &m1, 8);
-    int ex0 = (int)(b0 >> 52) - 1023, ex1 = (int)(b1 >> 52) - 1023;
-    const uint64_t mb0 = (b0 & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull;
-    const uint64_t mb1 = (b1 & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull;
-    double mm0, mm1;
-    __builtin_memcpy(&mm0, &mb0, 8);
-    __builtin_memcpy(&mm1, &mb1, 8);
-    if (mm0 > 1.4142135623730951) mm0 *= 0.5, ex0 += 1;
-    if (mm1 > 1.4142135623730951) mm1 *= 0.5, ex1 += 1;
-    const double f0 = mm0 - 1.0, f1 = mm1 - 1.0;
-    const double s0 = f0 * rcp_pos(2.0 + f0), s1 = f1 * rcp_pos(2.0 + f1);
-    const double v0 = s0 * s0, v1 = s1 * s1;
-    double P0 = kLogSeries[0], P1 = kLogSeries[0];
-#pragma unroll
-    for (int k = 1; k < 10; ++k) {
-      P0 = fma_sc(P0, v0, kLogSeries[k]);
-      P1 = fma_sc(P1, v1, kLogSeries[k]);
-    }
-    const double l0 = fma(s0 * v0, P0, 2.0 * s0), l1 = fma(s1 * v1, P1, 2.0 * s1);
-    const double d0 = (double)ex0, d1 = (double)ex1;
-    const double w0 = -fma(d0, 0.6931471803691238, fma(d0, 1.9082149292705877e-10, l0));
-    const double w1 = -fma(d1, 0.6931471803691238, fma(d1, 1.9082149292705877e-10, l1));
+    // w = -log(4 p (1 - p)) for both cells (table log, ltab in LDS)
+    const double w0 = -log_tab(4.0 * p0 * (1.0 - p0), ltab), w1 = -log_tab(4.0 * p1 * (1.0 - p1), ltab);
     // qnorm_fast's central branch (w < 6.25) for both cells, on every lane
     const double y0 = w0 - 3.125, y1 = w1 - 3.125;
     double F0 = kQnormA[0], F1 = kQnormA[0];
@@ -249,6 +265,7 @@ __device__ inline void g_reduce_body(const ZArgs& a, double* red) {
 // MODE bits (all set in the product; the microbenchmark clears them to cost each part):
 //   1 = E on the matrix cores, 2 = draws, 4 = XZ contraction, 8 = ZTr contraction
 constexpr int Z_ALL = 15;
+constexpr int Z_NOSTORE = 16;  // microbenchmark only: skip the Z stores
 constexpr int ZT_TLD = 17;  // leading dimension of the wave's 16-site x 32-species tile T[jj][site]
 
 // POIS: instantiated only for chains with Poisson species, so the probit kernel carries no
@@ -277,11 +294,12 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
   double* sSd = sTr + ZT_J * a.nt;                  // [32] iSigma^-1/2
   double* sIsd = sSd + ZT_J;                        // [32] iSigma^1/2
   int* sFam = (int*)(sIsd + ZT_J);                  // [32]
+  double* sLog = (double*)(sFam + ZT_J);            // [ZLOG_N][4] log table (log_tab)
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, lm = lane & 15, lk = lane >> 4;
   // the Philox sweep counter, read once (a load inside the site loop would wait, vmcnt(0),
   // behind every Z store in flight)
   const uint32_t iter = SWEEP_ITER(a);
-  double* sT = (double*)(sFam + ZT_J) + w * (ZT_J * ZT_TLD);  // this wave's tile: E, then Z
+  double* sT = sLog + 4 * ZLOG_N + w * (ZT_J * ZT_TLD);  // this wave's tile: E, then Z
   const int j0 = by * ZT_J;
   for (int p = t; p < K16 * ZT_J; p += 256) {
     const int k = p >> 5, jj = p & 31, j = j0 + jj;
@@ -298,6 +316,8 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
     sIsd[t] = sqrt(is);
     sFam[t] = (j < a.ns_loc) ? a.fam[j] : 0;
   }
+  if (DRAW && (MODE & 2))
+    for (int p = t; p < 4 * ZLOG_N; p += 256) sLog[p] = a.logtab[p];
   __syncthreads();
 
   d4 acc[NKB][2];
@@ -354,7 +374,7 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
       for (int c = 0; c < 4; ++c) {
         const int m = 4 * c + lk, ja = j0 + 2 * m;
         Uniform2 u{0.0, 0.0};
-        if (DRAW) u = uniforms(a.key, (uint32_t)((size_t)i + (size_t)ny * (uint32_t)((a.sp0 + ja) >> 1)), 0, S_Z, iter);
+        if (DRAW) u = uniforms_wave_key(a.key, (uint32_t)((size_t)i + (size_t)ny * (uint32_t)((a.sp0 + ja) >> 1)), 0, S_Z, iter);
         if (DRAW && !POIS && (MODE & 2)) {
           // probit / NA pair (the whole chain is probit, or the pair's species are):
           // both draws inline with interleaved chains; normal species keep Z = Y
@@ -362,14 +382,16 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
           const int jj0 = 2 * m, jj1 = 2 * m + 1;
           const bool in0 = i < ny && ja < a.ns_loc, in1 = i < ny && ja + 1 < a.ns_loc;
           const double e0 = sT[jj0 * ZT_TLD + s], e1 = sT[jj1 * ZT_TLD + s];
-          const ZPair zp = z_probit_pair(e0, e1, sSd[jj0], sSd[jj1], sIsd[jj0], sIsd[jj1], cd0, cd1, u.a, u.b, a.noise_zero);
+          const ZPair zp = z_probit_pair(e0, e1, sSd[jj0], sSd[jj1], sIsd[jj0], sIsd[jj1], cd0, cd1, u.a, u.b, a.noise_zero, sLog);
           double z0 = zp.z0, z1 = zp.z1;
           if (NORMAL) {  // R/updateZ.R:40-41
             if (sFam[jj0] == 1 && cd0 >= 0 && in0) z0 = a.Yval[(size_t)i + (size_t)ny * ja];
             if (sFam[jj1] == 1 && cd1 >= 0 && in1) z1 = a.Yval[(size_t)i + (size_t)ny * (ja + 1)];
           }
-          if (in0) a.Z[(size_t)i + (size_t)ny * ja] = z0;
-          if (in1) a.Z[(size_t)i + (size_t)ny * (ja + 1)] = z1;
+          if (!(MODE & Z_NOSTORE)) {
+            if (in0) a.Z[(size_t)i + (size_t)ny * ja] = z0;
+            if (in1) a.Z[(size_t)i + (size_t)ny * (ja + 1)] = z1;
+          }
           sT[jj0 * ZT_TLD + s] = in0 ? z0 : 0.0;
           sT[jj1 * ZT_TLD + s] = in1 ? z1 : 0.0;
           continue;
@@ -394,7 +416,7 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
                 z = z_probit_draw(e, sSd[jj], sIsd[jj], code, b ? u.b : u.a, a.noise_zero);
               else
                 z = e + (b ? u.b : u.a);
-              a.Z[cell] = z;
+              if (!(MODE & Z_NOSTORE)) a.Z[cell] = z;
             } else {
               z = a.Z[cell];
             }
@@ -485,7 +507,8 @@ inline int z_nkb(int K) { return (K + 15) / 16; }
 
 inline size_t z_smem_bytes(int K, int nt) {
   const size_t K16 = 16 * (size_t)z_nkb(K);
-  const size_t body = K16 * ZT_J + (size_t)ZT_J * nt + 2 * ZT_J + ZT_J / 2 + 4 * (size_t)ZT_J * ZT_TLD;  // doubles
+  const size_t body = K16 * ZT_J + (size_t)ZT_J * nt + 2 * ZT_J + ZT_J / 2 + 4 * (size_t)ZLOG_N +
+                      4 * (size_t)ZT_J * ZT_TLD;  // doubles
   const size_t red = 3 * K16 * ZT_J;                                                                   // wave combine
   return (body > red ? body : red) * sizeof(double);
 }

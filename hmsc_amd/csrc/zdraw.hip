@@ -79,6 +79,7 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   a.iSigma = s.iSigma;
   a.Ycode = s.Ycode;
   a.Ybits = s.Ybits;
+  a.logtab = s.logtab;
   a.Yval = use_raw_y ? s.Yraw : s.Yval;
   a.fam = s.fam;
   a.Tr = s.Tr;
@@ -136,6 +137,9 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
     launch_slab_sum2(s.XZ_part, s.XZ, nXZ, nchunk, s.ZTr_part, s.ZTr, nZT, s.ntile_j, s.stream);
   }
 }
+
+int z_log_table_doubles() { return 4 * ZLOG_N; }
+void z_log_table_fill(double* t) { z_log_table(t); }
 
 void launch_update_z(State& s, uint32_t iter, bool use_raw_y) {
   run_z_fused(s, true, iter, use_raw_y);

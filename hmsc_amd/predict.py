@@ -270,8 +270,6 @@ def computePredictedValues(hM, partition=None, start=1, thin=1, Yc=None, mcmcSte
         post = poolMcmcChains(hM.postList, start=start, thin=thin)
         pred = predict(hM, post=post, Yc=Yc, mcmcStep=mcmcStep, expected=expected, seed=seed)
         return np.stack(pred, axis=2)
-    from .model import Hmsc
-    from .sampler import sampleMcmc
     partition = np.asarray(partition)
     nfolds = len(np.unique(partition))
     nChains = len(hM.postList) if nChains is None else nChains
@@ -279,24 +277,7 @@ def computePredictedValues(hM, partition=None, start=1, thin=1, Yc=None, mcmcSte
     out = np.full((hM.ny, hM.ns, postN), np.nan)
     for k in np.unique(partition):
         train, val = partition != k, partition == k
-        sd = None if hM.studyDesign is None else hM.studyDesign.loc[train].reset_index(drop=True)
-        rl = {name: hM.ranLevels[name] for name in hM.rLNames} if hM.nr else None
-        hM1 = Hmsc(Y=hM.Y[train], X=hM.X[train], Tr=hM.Tr, distr=hM.distr, C=hM.C,               # :92
-                   studyDesign=sd, ranLevels=rl, covNames=list(hM.covNames), spNames=list(hM.spNames))
-        # :93-94 calls setPriors(hM1, V0 = hM$V0, ...) without assigning its result, so the
-        # refit keeps Hmsc()'s default priors (the random levels' priors travel with ranLevels);
-        # the scalings are the full model's (:95-116)
-        hM1.YScalePar = hM.YScalePar
-        hM1.YScaled = (hM1.Y - hM1.YScalePar[0][None, :]) / hM1.YScalePar[1][None, :]
-        hM1.XInterceptInd = hM.XInterceptInd
-        hM1.XScalePar = hM.XScalePar
-        hM1.XScaled = (np.asarray(hM1.X, dtype=np.float64) - hM1.XScalePar[0][None, :]) / hM1.XScalePar[1][None, :]
-        hM1.TrInterceptInd = hM.TrInterceptInd
-        hM1.TrScalePar = hM.TrScalePar
-        hM1.TrScaled = (np.asarray(hM1.Tr, dtype=np.float64) - hM1.TrScalePar[0][None, :]) / hM1.TrScalePar[1][None, :]
-        hM1 = sampleMcmc(hM1, samples=hM.samples, thin=hM.thin, transient=hM.transient, nChains=nChains,      # :117
-                         adaptNf=getattr(hM, "adaptNf", None), updater=updater, initPar=initPar, verbose=0,
-                         nParallel=nParallel)
+        hM1 = _cv_refit(hM, train, k, seed, nChains, updater, initPar, nParallel)
         post = poolMcmcChains(hM1.postList, start=start)
         sdv = None if hM.studyDesign is None else hM.studyDesign.loc[val].reset_index(drop=True)
         pred = predict(hM1, post=post, X=hM.X[val], studyDesign=sdv, Yc=None if Yc is None else np.asarray(Yc)[val],
@@ -304,6 +285,43 @@ def computePredictedValues(hM, partition=None, start=1, thin=1, Yc=None, mcmcSte
         out[val] = np.stack(pred, axis=2)
     del nfolds
     return out
+
+
+def _cv_fold_model(hM, train):
+    """R/computePredictedValues.R:92-116: the model on the training rows, with the full
+    model's scalings."""
+    from .model import Hmsc
+    sd = None if hM.studyDesign is None else hM.studyDesign.loc[train].reset_index(drop=True)
+    rl = {name: hM.ranLevels[name] for name in hM.rLNames} if hM.nr else None
+    hM1 = Hmsc(Y=hM.Y[train], X=hM.X[train], Tr=hM.Tr, distr=hM.distr, C=hM.C,                   # :92
+               studyDesign=sd, ranLevels=rl, covNames=list(hM.covNames), spNames=list(hM.spNames))
+    # :93-94 calls setPriors(hM1, V0 = hM$V0, ...) without assigning its result, so the refit
+    # keeps Hmsc()'s default priors (the random levels' priors travel with ranLevels); the
+    # scalings are the full model's (:95-116)
+    hM1.YScalePar = hM.YScalePar
+    hM1.YScaled = (hM1.Y - hM1.YScalePar[0][None, :]) / hM1.YScalePar[1][None, :]
+    hM1.XInterceptInd = hM.XInterceptInd
+    hM1.XScalePar = hM.XScalePar
+    hM1.XScaled = (np.asarray(hM1.X, dtype=np.float64) - hM1.XScalePar[0][None, :]) / hM1.XScalePar[1][None, :]
+    hM1.TrInterceptInd = hM.TrInterceptInd
+    hM1.TrScalePar = hM.TrScalePar
+    hM1.TrScaled = (np.asarray(hM1.Tr, dtype=np.float64) - hM1.TrScalePar[0][None, :]) / hM1.TrScalePar[1][None, :]
+    return hM1
+
+
+def cv_fold_seed(seed, k):
+    """Seed of fold k's refit: R draws the refit's chain seeds from its global RNG; here a given
+    predict seed fixes them per fold (None: fresh seeds)."""
+    return None if seed is None else int(np.random.default_rng([int(seed), int(k)]).integers(1, 2 ** 62))
+
+
+def _cv_refit(hM, train, k, seed, nChains, updater, initPar, nParallel):
+    """R/computePredictedValues.R:117: sampleMcmc of the fold model with the fitted run's
+    samples / transient / thin / adaptNf."""
+    from .sampler import sampleMcmc
+    return sampleMcmc(_cv_fold_model(hM, train), samples=hM.samples, thin=hM.thin, transient=hM.transient,
+                      nChains=nChains, adaptNf=getattr(hM, "adaptNf", None), updater=updater, initPar=initPar,
+                      verbose=0, nParallel=nParallel, seed=cv_fold_seed(seed, k))
 
 
 def _auc(y, p):

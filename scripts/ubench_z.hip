@@ -13,10 +13,11 @@ float run(const ZArgs& a, dim3 grid, size_t smem, int reps) {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
-  z_wave_kernel<true, false, 2, MODE, false, false><<<grid, 256, smem>>>(a);
+  auto k = z_wave_kernel<true, false, 2, MODE, false, false>;
+  k<<<grid, 256, smem>>>(a);
   (void)hipDeviceSynchronize();
   (void)hipEventRecord(e0);
-  for (int i = 0; i < reps; ++i) z_wave_kernel<true, false, 2, MODE, false, false><<<grid, 256, smem>>>(a);
+  for (int i = 0; i < reps; ++i) k<<<grid, 256, smem>>>(a);
   (void)hipEventRecord(e1);
   (void)hipEventSynchronize(e1);
   float ms;
@@ -25,7 +26,7 @@ float run(const ZArgs& a, dim3 grid, size_t smem, int reps) {
 }
 
 int main(int argc, char** argv) {
-  const bool prof_only = argc > 1;
+  const bool prof_only = argc > 1 && argv[1][0] == 'p';
   const int ny = 10000, ns = 1000, K = 30, nt = 1;
   std::vector<double> hX((size_t)ny * K), hBL((size_t)K * ns), hTr(ns, 1.0), hIs(ns, 1.0);
   std::vector<int8_t> hY((size_t)ny * ns);
@@ -73,6 +74,13 @@ int main(int argc, char** argv) {
   (void)hipMemcpy(Is, hIs.data(), ns * 8, hipMemcpyHostToDevice);
   (void)hipMemcpy(Y, hY.data(), hY.size(), hipMemcpyHostToDevice);
   (void)hipMemcpy(F, hF.data(), ns * 4, hipMemcpyHostToDevice);
+  double* LT;
+  {
+    std::vector<double> lt(4 * ZLOG_N);
+    z_log_table(lt.data());
+    (void)hipMalloc(&LT, lt.size() * 8);
+    (void)hipMemcpy(LT, lt.data(), lt.size() * 8, hipMemcpyHostToDevice);
+  }
   uint32_t* dIter;
   (void)hipMalloc(&dIter, 4);
   { const uint32_t three = 3; (void)hipMemcpy(dIter, &three, 4, hipMemcpyHostToDevice); }
@@ -81,7 +89,7 @@ int main(int argc, char** argv) {
   (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, false, 2, Z_ALL, false, false>, 256, smem);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
   printf("occupancy %d blocks/CU, %d CUs, smem %zu B\n", nb, ncu, smem);
-  for (int nchunk_req : {nb * ncu / ntile_j, 2 * nb * ncu / ntile_j, n_tiles}) {
+  for (int nchunk_req : {nb * ncu / ntile_j, 3 * nb * ncu / ntile_j}) {
     ZArgs a{};
     a.XEta = X; a.ny = ny; a.K = K; a.ns_loc = ns; a.sp0 = 0; a.nt = nt;
     a.tiles_per_chunk = (n_tiles + nchunk_req - 1) / nchunk_req;
@@ -89,25 +97,31 @@ int main(int argc, char** argv) {
     a.BL = BL; a.iSigma = Is; a.Ycode = Y; a.Ybits = Yb; a.Yval = nullptr; a.fam = F; a.Tr = Tr; a.Z = Z;
     a.XZ_part = XZp; a.ZTr_part = ZTrp; a.key = Key{7u, 9u}; a.iter = 3; a.noise_zero = 0;
     a.iter_dev = dIter;  // as in the product's graph replays
+    a.logtab = LT;
     dim3 grid(ntile_j, nchunk);
     printf("grid %d x %d (tiles/chunk %d)\n", nchunk, ntile_j, a.tiles_per_chunk);
     if (prof_only) {
-      printf("  all                 %7.1f us\n", run<15>(a, grid, smem, 20));
+      printf("  product (MODE 7)    %7.1f us\n", run<7>(a, grid, smem, 20));
       return 0;
     }
-    printf("  all                 %7.1f us\n", run<15>(a, grid, smem, 20));
-    printf("  no E mfma           %7.1f us\n", run<14>(a, grid, smem, 20));
-    printf("  no draw             %7.1f us\n", run<13>(a, grid, smem, 20));
-    printf("  no XZ               %7.1f us\n", run<11>(a, grid, smem, 20));
-    printf("  no ZTr              %7.1f us\n", run<7>(a, grid, smem, 20));
+    printf("  product (MODE 7)    %7.1f us\n", run<7>(a, grid, smem, 20));
+    printf("  product, no stores  %7.1f us\n", run<7 | 16>(a, grid, smem, 20));
+    printf("  no XZ               %7.1f us\n", run<3>(a, grid, smem, 20));
+    printf("  no draw             %7.1f us\n", run<5>(a, grid, smem, 20));
     printf("  draw only (E VALU)  %7.1f us\n", run<2>(a, grid, smem, 20));
     printf("  nothing             %7.1f us\n", run<0>(a, grid, smem, 20));
-    run<15>(a, grid, smem, 1);
+    printf("  nothing, no stores  %7.1f us\n", run<16>(a, grid, smem, 20));
+    run<7>(a, grid, smem, 1);
     std::vector<double> hz((size_t)ny * ns);
     (void)hipMemcpy(hz.data(), Z, hz.size() * 8, hipMemcpyDeviceToHost);
     double cs = 0, ca = 0;
     for (size_t q = 0; q < hz.size(); ++q) cs += hz[q], ca += std::fabs(hz[q]) * (1 + (q % 7));
     printf("  checksum Z %.15e %.15e  z[12345] %.17g\n", cs, ca, hz[12345]);
+    std::vector<double> hp((size_t)nchunk * K * ns);
+    (void)hipMemcpy(hp.data(), XZp, hp.size() * 8, hipMemcpyDeviceToHost);
+    double px = 0;
+    for (size_t q = 0; q < hp.size(); ++q) px += hp[q] * (1 + (q % 5));
+    printf("  checksum XZ partials %.15e\n", px);
   }
   return 0;
 }

@@ -208,10 +208,11 @@ def test_graph_replay_matches_eager(monkeypatch, thin):
     """hmsc_run replays captured graphs of several sweeps (the record pack inside, its ring
     slot chosen on the device); the recorded chain must equal the eager launch sequence bit
     for bit (same kernels, same order, same Philox counters), also when the run length is
-    not a multiple of the sweeps per replay."""
+    not a multiple of the sweeps per replay (remainders replay the graphs of the smaller
+    powers of two: 46 = 32 + 8 + 4 + 2 at the default 32 sweeps per replay)."""
     hM = synthetic_model(ny=200, ns=30, nc=4, nf=3, nt=2, seed=12)
     out = []
-    for no_graph, per in (("1", "4"), ("0", "4"), ("0", "3"), ("0", "1")):
+    for no_graph, per in (("1", "4"), ("0", "4"), ("0", "3"), ("0", "1"), ("0", "32")):
         monkeypatch.setenv("HMSC_NO_GRAPH", no_graph)
         monkeypatch.setenv("HMSC_GRAPH_SWEEPS", per)
         ch = H.Chain(hM, 77, device=0, updater={"GammaEta": False})

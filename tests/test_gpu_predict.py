@@ -83,3 +83,102 @@ def test_conditional_prediction(fitted):
     assert not np.allclose(cond, base)
     same = np.stack(H.predict(hM, post=post, Yc=np.full((hM.ny, hM.ns), np.nan), expected=True, seed=11), axis=2)
     assert np.array_equal(same, base)
+
+
+def test_conditional_prediction_matches_oracle(fitted):
+    """predict(Yc) step by step (R/predict.R:181-202): per posterior sample, Z = L, updateZ
+    given Yc, then mcmcStep x (updateEta, updateZ) with the sample's Beta, sigma and Lambda
+    fixed.  The device path (_conditional_etas: a chain built on (Yc, X), hmsc_update) against
+    the oracle's updateZ / updateEta on the same Philox key and sweep counters: the conditioned
+    Eta of every sample to 1e-8 (fp64 rounding through mcmcStep Gaussian conditionals)."""
+    from helpers import oracle_model
+    from hmsc_amd.model import Hmsc
+    from hmsc_amd.predict import _conditional_etas, _levels, predictLatentFactor
+    hM = fitted
+    post = H.poolMcmcChains(hM.postList)[:3]
+    probit = np.nonzero(hM.distr[:, 0] == 2)[0]
+    pois = np.nonzero(hM.distr[:, 0] == 3)[0]
+    Yc = np.full((hM.ny, hM.ns), np.nan)
+    Yc[:, probit] = hM.Y[:, probit]
+    Yc[::3, pois[0]] = hM.Y[::3, pois[0]]          # a partly observed Poisson column too
+    X = np.asarray(hM.X, dtype=np.float64)
+    mcmc_step = 2
+    dev = _conditional_etas(hM, post, X, hM.studyDesign, Yc, mcmc_step, np.random.default_rng(77), 0)
+
+    rng = np.random.default_rng(77)               # the same draws _conditional_etas makes
+    seed = int(rng.integers(1, 2 ** 62))
+    sd = hM.studyDesign.reset_index(drop=True)
+    rl = {name: hM.rL[r] for r, name in enumerate(hM.rLNames)}
+    hMc = Hmsc(Y=Yc, X=X, XScale=False, YScale=False, distr=hM.distr, studyDesign=sd, ranLevels=rl,
+               covNames=list(hM.covNames), spNames=list(hM.spNames))
+    m = oracle_model(hMc)
+    orng = Rng(seed)
+    units = [_levels(hM.dfPi[name]) for name in hM.rLNames]
+    for k, sam in enumerate(post):
+        etas = [predictLatentFactor(_levels(sd[name]), units[r], [sam["Eta"][r]], hM.rL[r], rng=rng)[0]
+                for r, name in enumerate(hM.rLNames)]
+        st = dict(Beta=np.asarray(sam["Beta"]), iSigma=1.0 / np.asarray(sam["sigma"], dtype=np.float64),
+                  Eta=etas, Lambda=[np.asarray(lm) for lm in sam["Lambda"]])
+        st["Z"] = O.linear_predictor(st, m)
+        it = 1 + k * (2 * mcmc_step + 1)
+        st["Z"] = O.update_z(st, m, orng, it)
+        for s in range(mcmc_step):
+            st["Eta"] = O.update_eta(st, m, orng, it + 1 + 2 * s)
+            st["Z"] = O.update_z(st, m, orng, it + 2 + 2 * s)
+        for r in range(hM.nr):
+            e = np.max(np.abs(dev[k][r] - st["Eta"][r])) / np.max(np.abs(st["Eta"][r]))
+            assert e < 1e-8, (k, r, e)
+
+
+def test_cv_refit_matches_oracle():
+    """A K-fold refit (R/computePredictedValues.R:92-118) step by step: the fold model on the
+    training rows with the full model's scalings (_cv_fold_model), sampled by sampleMcmc with
+    the fold's chain seed, against the oracle's chain on the same fold model and Philox key --
+    computeInitialParameters, then transient + samples x thin sweeps, recorded as R records
+    them -- compared after combineParameters' un-scaling (Beta, Gamma, V, sigma to 1e-6: fp64
+    rounding through 8 sweeps of a Poisson / normal / probit chain); then the fold's
+    predictions of the held-out rows are predict() on that refit."""
+    from helpers import oracle_model
+    from hmsc_amd.predict import _cv_fold_model, _cv_refit, cv_fold_seed
+    from hmsc_amd.sampler import combine_parameters
+    hM = synthetic_model(ny=60, ns=7, nc=3, nf=2, nr=1, n_normal=2, n_poisson=2, seed=71, yscale=True)
+    hM = H.sampleMcmc(hM, samples=4, transient=4, thin=1, nChains=1, updater={"GammaEta": False}, seed=8,
+                      verbose=0)
+    part = np.arange(hM.ny) % 2 + 1
+    seed, k, upd = 13, 1, {"GammaEta": False}
+    train, val = part != k, part == k
+    dev = _cv_refit(hM, train, k, seed, 1, upd, None, 1)
+
+    hM1 = _cv_fold_model(hM, train)
+    m = oracle_model(hM1)
+    init_seed = int(np.random.default_rng(cv_fold_seed(seed, k)).integers(1, 2 ** 31 - 1, size=1)[0])
+    rng = Rng(init_seed)
+    st = O.compute_initial_parameters(m, rng, nf=[int(rl.nfMin) for rl in hM1.rL])
+    recs = []
+    for it in range(1, hM.transient + hM.samples * hM.thin + 1):
+        st = O.sweep(st, m, rng, it, updater=upd, adapt_nf=list(hM.adaptNf))
+        if it > hM.transient and (it - hM.transient) % hM.thin == 0:
+            recs.append(st)
+    S, nfm = len(recs), int(hM1.rL[0].nfMax)
+    pad = lambda a, n, ax: np.pad(a, [(0, n - a.shape[ax]) if d == ax else (0, 0) for d in range(a.ndim)])  # noqa: E731
+    rec = dict(Beta=np.stack([s["Beta"] for s in recs]), Gamma=np.stack([s["Gamma"] for s in recs]),
+               iV=np.stack([s["iV"] for s in recs]), iSigma=np.stack([s["iSigma"] for s in recs]),
+               rho=np.ones(S, dtype=np.int64), nf=np.array([[s["Lambda"][0].shape[0] for s in recs]]),
+               Eta0=np.stack([pad(s["Eta"][0], nfm, 1) for s in recs]),
+               Lambda0=np.stack([pad(s["Lambda"][0], nfm, 0) for s in recs]),
+               Psi0=np.stack([pad(s["Psi"][0], nfm, 0) for s in recs]),
+               Delta0=np.stack([pad(np.asarray(s["Delta"][0]), nfm, 0) for s in recs]),
+               Alpha0=np.stack([pad(np.asarray(s["Alpha"][0]), nfm, 0) for s in recs]))
+    opost = combine_parameters(rec, hM1)
+    dpost = dev.postList[0]
+    assert len(dpost) == len(opost) == hM.samples
+    for d, o in zip(dpost, opost):
+        for key in ("Beta", "Gamma", "V", "sigma"):
+            e = np.max(np.abs(np.asarray(d[key]) - o[key])) / max(1e-300, np.max(np.abs(o[key])))
+            assert e < 1e-6, (key, e)
+    # the fold's held-out predictions are predict() on this refit (same posterior, same seed)
+    full = H.computePredictedValues(hM, partition=part, expected=True, seed=seed, nChains=1, updater=upd)
+    sdv = hM.studyDesign.loc[val].reset_index(drop=True)
+    pv = np.stack(H.predict(dev, post=H.poolMcmcChains(dev.postList), X=hM.X[val], studyDesign=sdv,
+                            expected=True, seed=seed), axis=2)
+    np.testing.assert_array_equal(full[val], pv)
