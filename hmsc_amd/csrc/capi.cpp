@@ -690,6 +690,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.ABpart = dalloc<double>((size_t)((nsl + 31) / 32) * (nc * nc + 2 * N + nfm * nt + 8));
   s.allreduce_buf = dalloc<double>((size_t)nc * nc + 2 * N + nfm * nt + nfm + 64);
   s.dev_flags = dalloc<int>(16);
+  s.gbl_sync = dalloc<int>(4);  // dalloc zero-fills
   s.d_iters = dalloc<uint32_t>(64);  // graph_sweeps <= 64
   s.d_iter = s.d_iters;
   if (s.mask & HMSC_UP_GAMMAETA) {  // updateGammaEta: dense (nc ns)^2 systems, one workgroup per level
@@ -740,7 +741,7 @@ static void free_state(State& s) {
   (void)hipDeviceSynchronize();
   void* ptrs[] = {s.X, s.Tr, s.Yval, s.Yraw, s.Ycode, s.Ybits, s.logtab, s.fam, s.varest, s.V0, s.iUGamma, s.mGamma, s.UGammaL,
                   s.aSigma, s.bSigma, s.XX, s.TT, s.V0g, s.V0gXXV0g, s.iV0, s.V0inv, s.iUmG, s.V0gXX, s.g2prep, s.scratch2, s.na_cols, s.na_index,
-                  s.na_rows, s.row_na, s.row_slot, s.dev_flags, s.Z, s.XEta, s.BL, s.Psi, s.Delta, s.Gamma, s.iV,
+                  s.na_rows, s.row_na, s.row_slot, s.dev_flags, s.gbl_sync, s.Z, s.XEta, s.BL, s.Psi, s.Delta, s.Gamma, s.iV,
                   s.iSigma, s.rho, s.XZ, s.G, s.ZTr, s.XZ_part, s.G_part, s.ZTr_part, s.Gna, s.ZL, s.ZL_part,
                   s.CR, s.CR_part, s.LS, s.Msmall, s.scratch, s.psi_rs, s.ABpart, s.dbg_prec, s.ring, s.allreduce_buf,
                   s.phU, s.phWinv, s.phRbase, s.phTt, s.phBt, s.phEt, s.phTTw, s.phWork, s.UGamma, s.geWork};
@@ -1070,10 +1071,14 @@ static void sweep(State& s, uint32_t iter, bool adapt) {
   // may still run on the side stream; Gamma2 joins it before its final stage
   const bool fused = s.nranks == 1 && side_fusion_ok(s);
   if (!fused) join_side(s);
-  if (s.mask & HMSC_UP_GAMMA2) run_updater(s, HMSC_UP_GAMMA2, iter);
-  if (s.mask & HMSC_UP_GAMMAETA) run_updater(s, HMSC_UP_GAMMAETA, iter);
-  join_side(s);  // BetaLambda reads Gamma and iV
-  if (s.mask & HMSC_UP_BETALAMBDA) run_updater(s, HMSC_UP_BETALAMBDA, iter);
+  if (gamma2_bl_fusion_ok(s)) {
+    launch_gamma2_bl(s, iter);  // both updaters in one launch (BetaLambda's factorization overlaps Gamma2)
+  } else {
+    if (s.mask & HMSC_UP_GAMMA2) run_updater(s, HMSC_UP_GAMMA2, iter);
+    if (s.mask & HMSC_UP_GAMMAETA) run_updater(s, HMSC_UP_GAMMAETA, iter);
+    join_side(s);  // BetaLambda reads Gamma and iV
+    if (s.mask & HMSC_UP_BETALAMBDA) run_updater(s, HMSC_UP_BETALAMBDA, iter);
+  }
   s.side_fused = fused;
   if (fused) {
     launch_side_fused(s, iter);
@@ -1342,6 +1347,7 @@ static void pretouch_record(const State& s, int k, const hmsc_record* rec) {
 
 static void run(State& s, int transient, int samples, int thin, const int* adaptNf, int iter0, int verbose,
                 int chain, hmsc_record* rec) {
+  const auto t_entry = std::chrono::steady_clock::now();
   DeviceGuard dg(s.device);
   HMSC_REQUIRE(thin >= 1 && samples >= 0 && transient >= 0, "bad transient/samples/thin");
   for (int r = 0; r < s.nr; ++r)
@@ -1384,9 +1390,11 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
       try {
         for (int k = w; k < samples; k += W) {
           if (__atomic_load_n(copied, __ATOMIC_ACQUIRE) <= (uint64_t)k) pretouch_record(s, k, rec);
+          // spin (yielding) rather than sleep: a timed sleep oversleeps by the kernel's timer
+          // slack (~50 us), which at the end of a short run is most of the unpack tail
           for (int spin = 0; __atomic_load_n(copied, __ATOMIC_ACQUIRE) <= (uint64_t)k; ++spin) {
             if (stop.load(std::memory_order_relaxed)) return;
-            if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+            if (spin > (1 << 20)) std::this_thread::sleep_for(std::chrono::microseconds(20));
             else std::this_thread::yield();
           }
           const auto tu0 = std::chrono::steady_clock::now();
@@ -1459,8 +1467,12 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
         if (klast >= 0) {
           HIP_OK(hipEventRecord(s.ev_graph, s.stream));
           HIP_OK(hipStreamWaitEvent(s.copy_stream, s.ev_graph, 0));
-          for (int k = kfirst; k <= klast; ++k) copy_out(k);
-          launch_copied_flag(s, (uint64_t)klast + 1);
+          // a flag after every sample's copy: the unpack of sample k starts as soon as its
+          // copy lands, not after the whole replay's copies
+          for (int k = kfirst; k <= klast; ++k) {
+            copy_out(k);
+            launch_copied_flag(s, (uint64_t)k + 1);
+          }
         }
       }
     }
@@ -1491,20 +1503,26 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
   const auto t_enq = std::chrono::steady_clock::now();
   HIP_OK(hipStreamSynchronize(s.stream));
   HIP_OK(hipStreamSynchronize(s.copy_stream));
-  if (getenv("HMSC_DIAG_TIMING")) {  // host run-ahead diagnostic: enqueue time vs total
-    const auto t_end = std::chrono::steady_clock::now();
-    std::fprintf(stderr, "[hmsc] run %d sweeps: enqueued in %.3f ms, done in %.3f ms; unpack %.3f ms, slot waits %.3f ms\n",
-                 total, std::chrono::duration<double, std::milli>(t_enq - t_start).count(),
-                 std::chrono::duration<double, std::milli>(t_end - t_start).count(), 1e-6 * diag_unpack_ns.load(),
-                 1e-6 * diag_wait_ns);
-  }
+  const auto t_done = std::chrono::steady_clock::now();
   int flag[2] = {0, 0};
   copy_sync(flag, s.dev_flags, sizeof(flag), hipMemcpyDeviceToHost, s.stream);
   HMSC_REQUIRE(flag[0] == 0 && flag[1] == 0, "a Cholesky factorisation failed (matrix not positive definite)");
+  int gsync[4] = {0, 0, 0, 0};
+  copy_sync(gsync, s.gbl_sync, sizeof(gsync), hipMemcpyDeviceToHost, s.stream);
+  HMSC_REQUIRE(gsync[3] == 0, "internal: the Gamma2 / BetaLambda in-launch handshake timed out");
   if (recording) {
     for (auto& th : workers) th.join();
     std::lock_guard<std::mutex> lk(mu);
     HMSC_REQUIRE(!worker_failed.load(), "record unpack: " + worker_err);
+  }
+  if (getenv("HMSC_DIAG_TIMING")) {  // host run-ahead diagnostic: enqueue time vs total
+    const auto t_end = std::chrono::steady_clock::now();
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    std::fprintf(stderr,
+                 "[hmsc] run %d sweeps: setup %.3f ms, enqueued in %.3f ms, done in %.3f ms, unpacked + joined %.3f "
+                 "ms later; unpack %.3f ms, slot waits %.3f ms\n",
+                 total, ms(t_entry, t_start), ms(t_start, t_enq), ms(t_start, t_done), ms(t_done, t_end),
+                 1e-6 * diag_unpack_ns.load(), 1e-6 * diag_wait_ns);
   }
 }
 

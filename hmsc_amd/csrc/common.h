@@ -73,7 +73,19 @@ extern __device__ unsigned long long g_stamps[256];
     __builtin_amdgcn_sched_barrier(0);                                             \
     if ((threadIdx.x & 63) == 0) g_stamps[(i)] = t_;                               \
   } while (0)
+// wall clock (s_memrealtime, 100 MHz: comparable across workgroups and XCDs)
+#define HMSC_STAMP_RT(i)                                                           \
+  do {                                                                             \
+    unsigned long long t_;                                                         \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    if ((threadIdx.x & 63) == 0) g_stamps[(i)] = t_;                               \
+  } while (0)
 #else
+#define HMSC_STAMP_RT(i) \
+  do {                   \
+  } while (0)
 #define HMSC_STAMP(i) \
   do {                \
   } while (0)

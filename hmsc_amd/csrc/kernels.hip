@@ -300,14 +300,23 @@ __global__ __launch_bounds__(64) void beta_lambda_kernel(BLArgs a) {
 // inputs every species shares (G = XEta^T XEta, iV, Gamma, tau = cumprod(Delta)) are staged
 // into LDS once per workgroup by all 256 threads, so each wave's prologue is LDS reads plus
 // its own species' column loads, all issued before the first use.
-template <int NM>
-__global__ __launch_bounds__(256) void beta_lambda_wave_kernel(BLArgs a) {
-  __shared__ __attribute__((aligned(16))) double tiles[4 * WV_TILE];
-  __shared__ double sG[32 * 33], sIV[32 * 32], sGam[32 * 8], sTau[64];
+// LDS of the body (doubles): the four waves' tiles, G, iV, Gamma, tau
+constexpr int BLW_LDS = 4 * WV_TILE + 32 * 33 + 32 * 32 + 32 * 8 + 64;
+
+// WAIT_GAMMA (the fused Gamma2 + BetaLambda launch, gamma2_bl_kernel): the new Gamma is
+// published by another workgroup of the same launch (gsync[1]); everything that does not
+// depend on it -- the prologue, iU and its Cholesky factor -- runs first.
+template <int NM, bool WAIT_GAMMA>
+__device__ __forceinline__ void beta_lambda_wave_body(const BLArgs& a, double* lds0, int blk, int* gsync) {
+  double* tiles = lds0;
+  double* sG = tiles + 4 * WV_TILE;
+  double* sIV = sG + 32 * 33;
+  double* sGam = sIV + 32 * 32;
+  double* sTau = sGam + 32 * 8;
   const unsigned long long kt0 = a.kt ? kt_now() : 0ull;
   const int K = a.K, nc = a.nc, nt = a.nt, i = lane_id(), w = threadIdx.x >> 6, t = threadIdx.x;
-  const int j = blockIdx.x * 4 + w;
-  if (blockIdx.x == 0) HMSC_STAMP(60);
+  const int j = blk * 4 + w;
+  if (blk == 0) HMSC_STAMP(60);
   // every global load of the prologue is issued before the first LDS store (a staging loop
   // with a store per iteration waits out one memory latency per iteration)
   double gv[4], ivv[4];
@@ -317,7 +326,7 @@ __global__ __launch_bounds__(256) void beta_lambda_wave_kernel(BLArgs a) {
     gv[u] = a.G[pc % K + (size_t)a.Kmax * (pc / K)];
     ivv[u] = a.iV[p < nc * nc ? p : 0];
   }
-  const double gam = a.Gamma[t < nc * nt ? t : 0];
+  const double gam = WAIT_GAMMA ? 0.0 : a.Gamma[t < nc * nt ? t : 0];
   const double del = a.NF > 0 ? a.Delta[t < a.NF ? t : 0] : 1.0;
   // this species' own inputs, loaded before the barrier so their latency overlaps it
   const int jj = j < a.ns_loc ? j : a.ns_loc - 1;
@@ -334,7 +343,7 @@ __global__ __launch_bounds__(256) void beta_lambda_wave_kernel(BLArgs a) {
     if (p < K * K) sG[p % K + 33 * (p / K)] = gv[u];
     if (p < nc * nc) sIV[p] = ivv[u];
   }
-  if (t < nc * nt && t < 32 * 8) sGam[t] = gam;
+  if (!WAIT_GAMMA && t < nc * nt && t < 32 * 8) sGam[t] = gam;
   if (t < a.NF) sTau[t] = del;  // Delta here; each lane forms its own cumprod below
   __syncthreads();
   if (j >= a.ns_loc) return;
@@ -348,11 +357,6 @@ __global__ __launch_bounds__(256) void beta_lambda_wave_kernel(BLArgs a) {
   }
   // prior precision diagonal of Lambda rows: Psi_hj * tau_h
   const double pd = (i >= nc && i < K) ? psi * tau : 0.0;
-  double mu = 0.0;  // Mu_j = Gamma Tr_j^T   (:62)
-  if (i < nc)
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-      if (q < nt) mu += sGam[i + nc * q] * trj[q];
   // iU = P + XEtaTXEta * iSigma[j]   (:83-92)
   double x[NM];
   const int ir = i < K ? i : 0;
@@ -376,6 +380,47 @@ __global__ __launch_bounds__(256) void beta_lambda_wave_kernel(BLArgs a) {
       x[k] = (i < K && k < K) ? v : (i == k ? 1.0 : 0.0);
     }
   }
+  if (a.dbg_prec && i < K)
+#pragma unroll
+    for (int k = 0; k < NM; ++k)
+      if (k < K) a.dbg_prec[(size_t)j * K * K + i + (size_t)K * k] = x[k];
+  double dinv;
+  if (blk == 0) HMSC_STAMP(61);
+  wv_chol<NM>(x, dinv);                    // RiU = chol(iU)  (:98)
+  if (blk == 0) HMSC_STAMP(62);
+  if (WAIT_GAMMA && blk == 0 && w == 0) HMSC_STAMP_RT(74);
+  double mu = 0.0;  // Mu_j = Gamma Tr_j^T   (:62)
+  if (WAIT_GAMMA) {
+    // the new Gamma of this sweep (updateGamma2, published by the launch's Gamma2 workgroup)
+    // relaxed polling (an acquire load per poll would invalidate the XCD's L2 every time,
+    // under every other wave of the device), then one acquire fence; bounded: a broken
+    // handshake raises the error flag (hmsc_run reports it) instead of hanging
+    for (int spin = 0; __hip_atomic_load(&gsync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0; ++spin) {
+      if (spin > (1 << 20)) {
+        if (i == 0) __hip_atomic_store(&gsync[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (blk == 0 && w == 0) HMSC_STAMP_RT(75);
+    if (i == 0) {  // the last wave through resets the handshake for the next launch
+      const int done = __hip_atomic_fetch_add(&gsync[2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (done == a.ns_loc - 1) {
+        __hip_atomic_store(&gsync[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&gsync[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&gsync[2], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (i < nc)
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (q < nt) mu += a.Gamma[i + nc * q] * trj[q];
+  } else if (i < nc) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (q < nt) mu += sGam[i + nc * q] * trj[q];
+  }
   // rhs = P Mu + isXTS   (:66, :100)
   double r = isig * xz;
   if (i < nc) {
@@ -383,24 +428,25 @@ __global__ __launch_bounds__(256) void beta_lambda_wave_kernel(BLArgs a) {
     for (int c = 0; c < nc; ++c) pm += sIV[i + nc * c] * bcast(mu, c);
     r += pm;
   }
-  if (a.dbg_prec && i < K)
-#pragma unroll
-    for (int k = 0; k < NM; ++k)
-      if (k < K) a.dbg_prec[(size_t)j * K * K + i + (size_t)K * k] = x[k];
-  double dinv;
-  if (blockIdx.x == 0) HMSC_STAMP(61);
-  wv_chol<NM>(x, dinv);                    // RiU = chol(iU)  (:98)
-  if (blockIdx.x == 0) HMSC_STAMP(62);
   wv_forward<NM>(x, dinv, r);              // y = L^-1 rhs
   if (i < K && !a.noise_zero) r += normal(a.key, (uint32_t)(a.sp0 + j), (uint32_t)i, S_BETALAMBDA, SWEEP_ITER(a));
-  if (blockIdx.x == 0) HMSC_STAMP(63);
+  if (blk == 0) HMSC_STAMP(63);
   double lt[NM];
   wv_transpose<NM, true>(x, lt, lds);
   wv_backward_t<NM>(lt, dinv, r);          // m + backsolve(RiU, xi)  (:101)
   if (i < K) a.BL[i + (size_t)K * j] = r;
-  if (blockIdx.x == 0) HMSC_STAMP(64);
+  if (blk == 0) HMSC_STAMP(64);
+  if (WAIT_GAMMA && blk == 0 && w == 0) HMSC_STAMP_RT(76);
   if (a.kt && i == 0) kt_record(a.kt, SWEEP_ITER(a), kt0);
 }
+
+template <int NM>
+__global__ __launch_bounds__(256) void beta_lambda_wave_kernel(BLArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  beta_lambda_wave_body<NM, false>(a, smem, blockIdx.x, nullptr);
+}
+
+static BLArgs make_bl_args(State& s, uint32_t iter);
 
 void launch_beta_lambda(State& s, uint32_t iter) {
   if (!s.xeta_valid) launch_xeta(s);
@@ -415,6 +461,25 @@ void launch_beta_lambda(State& s, uint32_t iter) {
     EtaView ev = make_view(s);
     gram_na_kernel<<<s.n_na_cols, 256, 0, s.stream>>>(ev, s.XEta, s.K, s.Kmax, s.na_cols, s.Ycode, s.Gna);
   }
+  const BLArgs a = make_bl_args(s, iter);
+  ProfScope ps(s, PROF_BL);
+  if (s.K <= 32 && s.nt <= 8 && s.nc * s.nt <= 256 && s.NF <= 64) {
+    const int nb = (s.nsl + 3) / 4;
+    switch (wv_bucket(s.K)) {
+      case 8: beta_lambda_wave_kernel<8><<<nb, 256, BLW_LDS * sizeof(double), s.stream>>>(a); break;
+      case 16: beta_lambda_wave_kernel<16><<<nb, 256, BLW_LDS * sizeof(double), s.stream>>>(a); break;
+      case 24: beta_lambda_wave_kernel<24><<<nb, 256, BLW_LDS * sizeof(double), s.stream>>>(a); break;
+      default: beta_lambda_wave_kernel<32><<<nb, 256, BLW_LDS * sizeof(double), s.stream>>>(a); break;
+    }
+    HIP_OK(hipGetLastError());
+    return;
+  }
+  const size_t smem = ((size_t)s.K * s.K + s.K + s.NF + 1 + s.nc + 1) * sizeof(double) + 16;
+  beta_lambda_kernel<<<s.nsl, 64, smem, s.stream>>>(a);
+  HIP_OK(hipGetLastError());
+}
+
+static BLArgs make_bl_args(State& s, uint32_t iter) {
   BLArgs a{};
   a.K = s.K;
   a.Kmax = s.Kmax;
@@ -443,21 +508,7 @@ void launch_beta_lambda(State& s, uint32_t iter) {
   a.iter_dev = s.capturing ? s.d_iter : nullptr;
   a.noise_zero = s.noise_mode;
   a.kt = s.kt_on ? s.d_kt + (size_t)KT_BL * 2 * KT_SLOTS : nullptr;
-  ProfScope ps(s, PROF_BL);
-  if (s.K <= 32 && s.nt <= 8 && s.nc * s.nt <= 256 && s.NF <= 64) {
-    const int nb = (s.nsl + 3) / 4;
-    switch (wv_bucket(s.K)) {
-      case 8: beta_lambda_wave_kernel<8><<<nb, 256, 0, s.stream>>>(a); break;
-      case 16: beta_lambda_wave_kernel<16><<<nb, 256, 0, s.stream>>>(a); break;
-      case 24: beta_lambda_wave_kernel<24><<<nb, 256, 0, s.stream>>>(a); break;
-      default: beta_lambda_wave_kernel<32><<<nb, 256, 0, s.stream>>>(a); break;
-    }
-    HIP_OK(hipGetLastError());
-    return;
-  }
-  const size_t smem = ((size_t)s.K * s.K + s.K + s.NF + 1 + s.nc + 1) * sizeof(double) + 16;
-  beta_lambda_kernel<<<s.nsl, 64, smem, s.stream>>>(a);
-  HIP_OK(hipGetLastError());
+  return a;
 }
 
 // ---------------------------------------------------------------------------
@@ -921,14 +972,12 @@ void launch_gamma_v(State& s, uint32_t iter, hipStream_t st) {
 //   X^T Z Tr = XZ[0:nc,:] Tr (no NA)  and  X^T Eta_r[Pi] (Lambda_r Tr)  from G.
 // Stage 2: single-workgroup dense algebra.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void gamma2_partial_kernel(const double* XZ, const double* BL, int K, int nc,
-                                                             int NF, int nt, int ns_loc, const double* Tr,
-                                                             double* part) {
+__device__ __forceinline__ void gamma2_partial_body(const double* XZ, const double* BL, int K, int nc, int NF, int nt,
+                                                    int ns_loc, const double* Tr, double* part, double* smem, int bid) {
   // part[b] = [ XZ[0:nc, block] Tr (nc*nt) | Lambda_all[:, block] Tr (NF*nt) ]
-  extern __shared__ __attribute__((aligned(16))) double smem[];
   double* sX = smem;             // K x SB: rows < nc from XZ, rows >= nc from BL (Lambda)
   double* sTr = sX + K * SB;     // SB x nt
-  const int t = threadIdx.x, j0 = blockIdx.x * SB, nj = min(SB, ns_loc - j0);
+  const int t = threadIdx.x, j0 = bid * SB, nj = min(SB, ns_loc - j0);
   for (int p = t; p < K * nj; p += 256) {
     const int k = p % K, jj = p / K;
     const size_t g = k + (size_t)K * (j0 + jj);
@@ -940,7 +989,7 @@ __global__ __launch_bounds__(256) void gamma2_partial_kernel(const double* XZ, c
   }
   __syncthreads();
   const int n1 = nc * nt, n2 = NF * nt;
-  double* out = part + (size_t)blockIdx.x * (n1 + n2);
+  double* out = part + (size_t)bid * (n1 + n2);
   for (int p = t; p < n1 + n2; p += 256) {
     int k, q;
     if (p < n1) {
@@ -954,6 +1003,13 @@ __global__ __launch_bounds__(256) void gamma2_partial_kernel(const double* XZ, c
     for (int jj = 0; jj < nj; ++jj) acc = fma(sX[k + K * jj], sTr[jj + SB * q], acc);
     out[p] = acc;
   }
+}
+
+__global__ __launch_bounds__(256) void gamma2_partial_kernel(const double* XZ, const double* BL, int K, int nc,
+                                                             int NF, int nt, int ns_loc, const double* Tr,
+                                                             double* part) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  gamma2_partial_body(XZ, BL, K, nc, NF, nt, ns_loc, Tr, part, smem, blockIdx.x);
 }
 
 // X^T ZTr (nc x nt) for models with NA (where XZ is masked): reduction over sites
@@ -1063,12 +1119,21 @@ __device__ __forceinline__ void batched_for(int n, Load load, Store store) {
   }
 }
 
-__global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
+// LDS of the final stage (doubles), before the staged B1 | LS (n2 + N^2 more when a.stage)
+constexpr int G2F_LDS = 512 + 512 + 3 * 256 + 8 * 64 + 2048;
+
+__device__ __forceinline__ void gamma2_final_body(const G2Args& a, double* lds) {
   // Every input is staged into LDS by all 256 threads first (coalesced, in parallel); the
   // small products then run from LDS instead of as per-thread loops of dependent global loads.
   __shared__ int all_one;
-  __shared__ double S0[512], LTr[512], v1[256], v2[256], xi[256], red[8][64], sGL[2048];
-  extern __shared__ __attribute__((aligned(16))) double dyn[];  // B1 | LS  when a.stage
+  double* S0 = lds;
+  double* LTr = S0 + 512;
+  double* v1 = LTr + 512;
+  double* v2 = v1 + 256;
+  double* xi = v2 + 256;
+  double (*red)[64] = (double (*)[64])(xi + 256);
+  double* sGL = xi + 256 + 8 * 64;
+  double* dyn = sGL + 2048;  // B1 | LS  when a.stage
   HMSC_STAMP(30);
   const int nc = a.nc, nt = a.nt, N = nc * nt, t = threadIdx.x, n2 = nc * nc;
   if (t == 0) all_one = 1;
@@ -1167,6 +1232,59 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
   HMSC_STAMP(32);
 }
 
+__global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  gamma2_final_body(a, smem);
+}
+
+// ---------------------------------------------------------------------------
+// updateGamma2 + updateBetaLambda in one launch (R/sampleMcmc.R:221-229 runs them back to
+// back; BetaLambda's precision iU and its Cholesky factor do not depend on the Gamma that
+// Gamma2 draws, only its mean does).  Workgroups 0 .. nparts-1 form Gamma2's species-block
+// partials; the last of them to finish (a ticket) reduces them in block order, runs the final
+// stage and publishes Gamma (sync[1]); workgroups nparts.. run the wave BetaLambda body, which
+// factors iU while Gamma2 runs and waits for Gamma only for the mean and the solves.  Every
+// workgroup of the launch is resident at once (nparts + ns / 4 <= 3 per CU at 52 KB of LDS),
+// so the wait cannot block the workgroup it waits for.  The last BetaLambda wave through resets
+// the handshake (ticket, flag, count) for the next launch.
+// ---------------------------------------------------------------------------
+struct G2BLArgs {
+  G2Args g2;
+  BLArgs bl;
+  const double* XZ;
+  const double* BLold;  // Lambda rows of the partials (read before any BetaLambda write: the
+                        // writes follow the Gamma flag, which follows every partial's ticket)
+  const double* Tr;
+  double* part;
+  int K, nc, NF, nt, nsl;
+  int* sync;            // [ticket, Gamma published, BetaLambda waves through]
+};
+
+template <int NM>
+__global__ __launch_bounds__(256) void gamma2_bl_kernel(G2BLArgs f) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int s_last;
+  const int nparts = f.g2.nparts;
+  if ((int)blockIdx.x < nparts) {
+    if (blockIdx.x == 0 && threadIdx.x < 64) HMSC_STAMP_RT(70);
+    gamma2_partial_body(f.XZ, f.BLold, f.K, f.nc, f.NF, f.nt, f.nsl, f.Tr, f.part, smem, blockIdx.x);
+    __syncthreads();  // the workgroup's partial stores complete; thread 0's release publishes them
+    if (threadIdx.x == 0)
+      s_last = __hip_atomic_fetch_add(&f.sync[0], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nparts - 1;
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x < 64) HMSC_STAMP_RT(71);
+    if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every block's partials
+    if (threadIdx.x < 64) HMSC_STAMP_RT(72);
+    gamma2_final_body(f.g2, smem);
+    __syncthreads();
+    if (threadIdx.x < 64) HMSC_STAMP_RT(73);
+    if (threadIdx.x == 0) __hip_atomic_store(&f.sync[1], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  beta_lambda_wave_body<NM, true>(f.bl, smem, blockIdx.x - nparts, f.sync);
+}
+
 static void launch_gamma2_prep(State& s, hipStream_t st) {
   G2PrepArgs a{};
   a.nc = s.nc;
@@ -1249,9 +1367,70 @@ void launch_gamma2(State& s, uint32_t iter) {
   a.iter_dev = s.capturing ? s.d_iter : nullptr;
   a.noise_zero = s.noise_mode;
   const size_t N = (size_t)s.nc * s.nt, stage_bytes = ((size_t)s.nc * s.nc + N * N) * sizeof(double);
-  a.stage = stage_bytes <= 28 * 1024;  // + 35 KB static: within 64 KB per workgroup
+  a.stage = stage_bytes <= 28 * 1024;  // + 35 KB of the final stage's own: within 64 KB per workgroup
   join_side(s);  // iV and the prep matrices come from the previous sweep's GammaV (side stream)
-  gamma2_final_kernel<<<1, 256, a.stage ? stage_bytes : 0, s.stream>>>(a);
+  gamma2_final_kernel<<<1, 256, G2F_LDS * sizeof(double) + (a.stage ? stage_bytes : 0), s.stream>>>(a);
+  HIP_OK(hipGetLastError());
+}
+
+bool gamma2_bl_fusion_ok(const State& s) {
+  const uint32_t need = HMSC_UP_GAMMA2 | HMSC_UP_BETALAMBDA;
+  const size_t N = (size_t)s.nc * s.nt;
+  return (s.mask & need) == need && !(s.mask & HMSC_UP_GAMMAETA) && s.nranks == 1 && !s.has_na && !s.phylo &&
+         s.K <= 32 && s.nt <= 8 && N <= 256 && s.NF <= 64 && s.NF * s.nt + N <= 64 && s.gbl_sync != nullptr &&
+         (G2F_LDS + (size_t)s.nc * s.nc + N * N) <= (size_t)BLW_LDS && !getenv_flag("HMSC_NO_G2BL_FUSION");
+}
+
+// updateGamma2 then updateBetaLambda as one launch (gamma2_bl_kernel)
+void launch_gamma2_bl(State& s, uint32_t iter) {
+  if (!s.xeta_valid) launch_xeta(s);
+  flush_g(s);
+  if (!s.zt_valid) launch_zt_refresh(s);
+  join_side(s);  // iV, Gamma2's prep, Psi and Delta come from the previous sweep's side updaters
+  if (!s.g2prep_valid) launch_gamma2_prep(s, s.stream);
+  G2BLArgs f{};
+  const int nparts = (s.nsl + SB - 1) / SB;
+  G2Args& a = f.g2;
+  a.nc = s.nc;
+  a.nt = s.nt;
+  a.Kmax = s.Kmax;
+  a.NF = s.NF;
+  a.nparts = nparts;
+  a.ns_loc = s.nsl;
+  a.use_xtztr = 0;
+  a.check_isigma = 1;
+  a.isig_count = nullptr;
+  a.part = s.ABpart;
+  a.xtztr = nullptr;
+  a.G = s.G;
+  a.prep = s.g2prep;
+  a.iSigma = s.iSigma;
+  a.Gamma = s.Gamma;
+  a.key = s.key;
+  a.iter = iter;
+  a.iter_dev = s.capturing ? s.d_iter : nullptr;
+  a.noise_zero = s.noise_mode;
+  a.stage = 1;
+  f.bl = make_bl_args(s, iter);
+  f.XZ = s.XZ;
+  f.BLold = s.BL;
+  f.Tr = s.Tr;
+  f.part = s.ABpart;
+  f.K = s.K;
+  f.nc = s.nc;
+  f.NF = s.NF;
+  f.nt = s.nt;
+  f.nsl = s.nsl;
+  f.sync = s.gbl_sync;
+  const int nb = nparts + (s.nsl + 3) / 4;
+  const size_t smem = BLW_LDS * sizeof(double);
+  ProfScope ps(s, PROF_BL);
+  switch (wv_bucket(s.K)) {
+    case 8: gamma2_bl_kernel<8><<<nb, 256, smem, s.stream>>>(f); break;
+    case 16: gamma2_bl_kernel<16><<<nb, 256, smem, s.stream>>>(f); break;
+    case 24: gamma2_bl_kernel<24><<<nb, 256, smem, s.stream>>>(f); break;
+    default: gamma2_bl_kernel<32><<<nb, 256, smem, s.stream>>>(f); break;
+  }
   HIP_OK(hipGetLastError());
 }
 
@@ -1785,15 +1964,26 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
   __shared__ double sB[NFB][EF_SITES], sXi[NFB][EF_SITES], sU[NFB][EF_SITES];
   __shared__ double sX[64][EF_SITES + 1];     // XEta tile [k][site] (K <= 64)
   __shared__ double sCR[64 * NFB];            // CR[k][h], k < K
+  __shared__ int sPi[EF_SITES];               // the tile's units
   const unsigned long long kt0 = a.kt ? kt_now() : 0ull;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, lm = lane & 15, lk = lane >> 4;
   const int ny = a.ny, nf = a.nf, K = a.K, nc = a.nc, ns = a.ns_loc;
   const int i0 = blockIdx.x * EF_SITES;
   if (blockIdx.x == 0) HMSC_STAMP(50);
+  const uint32_t iter = SWEEP_ITER(a);       // read once, ahead of the stream
+  if (t < EF_SITES) sPi[t] = i0 + t < ny ? a.Pi[i0 + t] : 0;
   // ---- stage 1: ZL = Z (Lambda diag(iSigma))^T on the matrix cores, the HBM stream of the
   // launch, issued first: species j = 16 s + 4 w + lk, B = LS[j][lm] straight from L2 (128 KB,
   // shared by every workgroup); eight steps' loads in flight before their MFMAs
   d4 acc = {0.0, 0.0, 0.0, 0.0};
+  // the tile's X columns (the residual's fixed part and the Gram tile), loaded before the
+  // stream so they arrive during it: nc x 16 values, at most 4 per thread (nc < 64)
+  double xr[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int p = t + 256 * u, s2 = p % EF_SITES, k = p / EF_SITES, ii = i0 + s2;
+    xr[u] = (k < nc && ii < ny) ? a.XEta[ii + (size_t)ny * k] : 0.0;
+  }
   const double* zc = a.Z + min(i0 + lm, ny - 1);  // sites past ny: any finite row, unused
   const int nsteps = (ns + 15) >> 4;
   int s = 0;
@@ -1823,6 +2013,11 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
   // acc[r] = partial ZL[site lk + 4 r][factor lm]
 #pragma unroll
   for (int r = 0; r < 4; ++r) sPart[w][lm][lk + 4 * r] = acc[r];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int p = t + 256 * u, s2 = p % EF_SITES, k = p / EF_SITES;
+    if (k < nc) sX[k][s2] = xr[u];
+  }
   // CR from its species-block partials, in block order (L2; every partial's load in flight
   // before the adds)
   for (int p = t; p < K * nf; p += 256) {
@@ -1871,16 +2066,13 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
       const double zl = (sPart[0][h][s2] + sPart[1][h][s2]) + (sPart[2][h][s2] + sPart[3][h][s2]);
       double corr = 0.0, xi = 0.0;
       if (ii < ny) {
-        for (int k = 0; k < nc; ++k) corr = fma(a.XEta[ii + (size_t)ny * k], sCR[k * NFB + h], corr);
-        xi = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)a.Pi[ii], (uint32_t)h, S_ETA, SWEEP_ITER(a));
+        // X from the tile staged in LDS (a global load per term here waited out one L2
+        // round trip per covariate: ~6 us of the kernel's serial tail)
+        for (int k = 0; k < nc; ++k) corr = fma(sX[k][s2], sCR[k * NFB + h], corr);
+        xi = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)sPi[s2], (uint32_t)h, S_ETA, iter);
       }
       sB[h][s2] = zl - corr;
       sXi[h][s2] = xi;
-    }
-    // X columns of the tile into the Gram tile
-    for (int p = t - 64; p < nc * EF_SITES; p += 192) {
-      const int s2 = p % EF_SITES, k = p / EF_SITES, ii = i0 + s2;
-      sX[k][s2] = ii < ny ? a.XEta[ii + (size_t)ny * k] : 0.0;
     }
   }
   __syncthreads();
@@ -1899,7 +2091,7 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
     double e = 0.0;
     for (int m = h; m < nf; ++m) e = fma(sW[m * NFB + h], sU[m][s2], e);
     if (ii < ny) {
-      a.Eta[a.Pi[ii] + (size_t)a.np * h] = e;
+      a.Eta[sPi[s2] + (size_t)a.np * h] = e;
       a.XEta[ii + (size_t)ny * (nc + h)] = e;
     }
     sX[nc + h][s2] = ii < ny ? e : 0.0;
@@ -1918,7 +2110,7 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
   if (blockIdx.x == 0) HMSC_STAMP(55);
   if (a.kt) {
     __syncthreads();
-    if (t == 0) kt_record(a.kt, SWEEP_ITER(a), kt0);
+    if (t == 0) kt_record(a.kt, iter, kt0);
   }
 }
 

@@ -121,6 +121,7 @@ struct State {
   int* row_slot = nullptr;       // ny: index into na_rows, or -1
   int n_na_rows = 0;
   int* dev_flags = nullptr;      // device error flags (Cholesky failures)
+  int* gbl_sync = nullptr;       // gamma2_bl_kernel's in-launch handshake (zero between launches)
   std::vector<int> h_na_cols;
 
   // chain state (device)
@@ -281,6 +282,8 @@ void launch_slab_sum2_pack(State& s, const double* p0, double* o0, int64_t n0, i
 void launch_beta_lambda(State& s, uint32_t iter);
 void launch_gamma_v(State& s, uint32_t iter, hipStream_t st);
 void launch_gamma2(State& s, uint32_t iter);
+bool gamma2_bl_fusion_ok(const State& s);
+void launch_gamma2_bl(State& s, uint32_t iter);  // updateGamma2 + updateBetaLambda in one launch
 void launch_lambda_priors(State& s, uint32_t iter, hipStream_t st);
 void launch_eta(State& s, uint32_t iter);
 void launch_inv_sigma(State& s, uint32_t iter);

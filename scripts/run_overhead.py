@@ -26,12 +26,14 @@ for rec in (True, False):
         t0 = time.perf_counter()
         if rec:
             ch.run(transient=0, samples=S, thin=1, adaptNf=[0], iter0=it, record=True)
+            t1 = time.perf_counter()
         else:
             ch.run(transient=S, samples=0, thin=1, adaptNf=[0], iter0=it, record=False)
         ch.sync()
         dt = time.perf_counter() - t0
         it += S
-        print(f"record={rec} S={S}: {1e3 * dt:.3f} ms, {1e3 * dt / S:.4f} ms/sweep", flush=True)
+        extra = f" (run() returned at {1e3 * (t1 - t0):.3f} ms)" if rec else ""
+        print(f"record={rec} S={S}: {1e3 * dt:.3f} ms, {1e3 * dt / S:.4f} ms/sweep{extra}", flush=True)
 t0 = time.perf_counter()
 a = np.zeros((20, 10, 10000))
 a[:] = 1.0

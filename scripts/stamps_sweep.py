@@ -20,6 +20,10 @@ ch.sync()
 st = ch.debug_get("stamps", 128)
 groups = {"gammav_wave": range(0, 10), "delta": range(20, 22), "gamma2_final": range(30, 33), "eta_shared(block0)": range(40, 45), "eta_fused(block0)": range(50, 56),
           "beta_lambda(block0)": range(60, 65), "gammav_wave1": range(10, 15)}
+v = np.array([st[i] for i in range(70, 77)])
+print("gamma2_bl (10 ns ticks from the first partial block's start): partial0 done", v[1] - v[0],
+      "final start", v[2] - v[0], "final done", v[3] - v[0], "BL0 chol done", v[4] - v[0],
+      "BL0 wait done", v[5] - v[0], "BL0 end", v[6] - v[0])
 for name, idx in groups.items():
     v = np.array([st[i] for i in idx])
     d = np.diff(v)
