@@ -896,7 +896,10 @@ static void set_state(State& s, const hmsc_params* p) {
   h2d(s.Delta, Delta.data(), s.NF, s.stream);
   if (p->Gamma) h2d(s.Gamma, p->Gamma, (size_t)nc * s.nt, s.stream);
   if (p->iV) h2d(s.iV, p->iV, (size_t)nc * nc, s.stream);
-  if (p->iSigma) h2d(s.iSigma, p->iSigma, nsl, s.stream);
+  if (p->iSigma) {
+    h2d(s.iSigma, p->iSigma, nsl, s.stream);
+    s.isigma_fixed_one = false;  // an initPar sigma: updateGamma2 checks iSigma == 1 again
+  }
   if (p->Z) h2d(s.Z, p->Z, (size_t)s.ny * nsl, s.stream);
   if (p->rho > 0) {  // initPar$rho as a grid index (R/computeInitialParameters.R:223-224)
     HMSC_REQUIRE(!s.phylo || p->rho <= s.nrho, "set_state: rho index out of range");

@@ -392,9 +392,11 @@ __device__ __forceinline__ void beta_lambda_wave_body(const BLArgs& a, double* l
   double mu = 0.0;  // Mu_j = Gamma Tr_j^T   (:62)
   if (WAIT_GAMMA) {
     // the new Gamma of this sweep (updateGamma2, published by the launch's Gamma2 workgroup)
-    // relaxed polling (an acquire load per poll would invalidate the XCD's L2 every time,
-    // under every other wave of the device), then one acquire fence; bounded: a broken
-    // handshake raises the error flag (hmsc_run reports it) instead of hanging
+    // relaxed polling, and Gamma (the only datum published inside the launch) read with
+    // device-coherent loads below: an acquire -- per poll, or one fence per wave after it --
+    // invalidates the XCD's L2, and a thousand of them under every other wave of the device
+    // took the solves after the wait from 5 to 16 us; bounded: a broken handshake raises the
+    // error flag (hmsc_run reports it) instead of hanging
     for (int spin = 0; __hip_atomic_load(&gsync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0; ++spin) {
       if (spin > (1 << 20)) {
         if (i == 0) __hip_atomic_store(&gsync[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -402,7 +404,6 @@ __device__ __forceinline__ void beta_lambda_wave_body(const BLArgs& a, double* l
       }
       __builtin_amdgcn_s_sleep(8);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     if (blk == 0 && w == 0) HMSC_STAMP_RT(75);
     if (i == 0) {  // the last wave through resets the handshake for the next launch
       const int done = __hip_atomic_fetch_add(&gsync[2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -415,7 +416,11 @@ __device__ __forceinline__ void beta_lambda_wave_body(const BLArgs& a, double* l
     if (i < nc)
 #pragma unroll
       for (int q = 0; q < 8; ++q)
-        if (q < nt) mu += a.Gamma[i + nc * q] * trj[q];
+        if (q < nt) {
+          const unsigned long long gb = __hip_atomic_load((const unsigned long long*)(a.Gamma + i + nc * q),
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          mu += __longlong_as_double((long long)gb) * trj[q];
+        }
   } else if (i < nc) {
 #pragma unroll
     for (int q = 0; q < 8; ++q)
@@ -1398,7 +1403,8 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
   a.nparts = nparts;
   a.ns_loc = s.nsl;
   a.use_xtztr = 0;
-  a.check_isigma = 1;
+  // probit iSigma is 1 by construction (updateInvSigma leaves it) unless set from outside
+  a.check_isigma = (s.all_probit && s.isigma_fixed_one) ? 0 : 1;
   a.isig_count = nullptr;
   a.part = s.ABpart;
   a.xtztr = nullptr;

@@ -77,6 +77,7 @@ struct State {
   bool any_var = false;          // any species with estimated variance (distr[,2]==1)
   bool any_poisson = false;
   bool all_probit = true;
+  bool isigma_fixed_one = true;  // all probit and iSigma never set from outside: iSigma == 1
   int K = 0, NF = 0, Kmax = 0, NFmax = 0;
   double f0 = 0;
   Level lev[HMSC_MAX_LEVELS];

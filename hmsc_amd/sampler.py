@@ -329,10 +329,14 @@ class Chain:
         arrays = None
         if record and samples > 0:
             S = samples
-            arrays = dict(Beta=np.zeros((S, ns, hM.nc)), Gamma=np.zeros((S, hM.nt, hM.nc)),
-                          iV=np.zeros((S, hM.nc, hM.nc)), iSigma=np.zeros((S, ns)),
-                          rho=np.zeros(S, dtype=np.int32), rec_nf=np.zeros((max(1, nr), S), dtype=np.int32))
             want = (lambda k: True) if fields is None else (lambda k: k in fields)  # noqa: E731
+            # the library writes every element of a recorded field (and first touches its pages
+            # in its unpack threads), so recorded fields need no zero fill: np.zeros of a large
+            # array reused from the heap is a full memset on this thread (~2 ms per 16 MB)
+            new = lambda k, shape, dt=np.float64: (np.empty if want(k) else np.zeros)(shape, dtype=dt)  # noqa: E731
+            arrays = dict(Beta=new("Beta", (S, ns, hM.nc)), Gamma=new("Gamma", (S, hM.nt, hM.nc)),
+                          iV=new("iV", (S, hM.nc, hM.nc)), iSigma=new("iSigma", (S, ns)),
+                          rho=new("rho", S, np.int32), rec_nf=np.zeros((max(1, nr), S), dtype=np.int32))
             rec = L.hmsc_record()
             for k, fp in (("Beta", L.fptr), ("Gamma", L.fptr), ("iV", L.fptr), ("iSigma", L.fptr), ("rho", L.iptr)):
                 if want(k):
@@ -344,7 +348,7 @@ class Chain:
                                      ("Psi", (S, ns, nfm), np.float64), ("Delta", (S, nfm), np.float64),
                                      ("Alpha", (S, nfm), np.int32)):
                     if want(k):
-                        arrays[f"{k}{r}"] = np.zeros(shape, dtype=dt)
+                        arrays[f"{k}{r}"] = np.empty(shape, dtype=dt)
                         getattr(rec, k)[r] = (L.iptr if dt == np.int32 else L.fptr)(arrays[f"{k}{r}"])
         L.check(self.lib.hmsc_run_verbose(self.h, int(transient), int(samples), int(thin), L.iptr(adapt),
                                           int(iter0), int(verbose), int(chain),
