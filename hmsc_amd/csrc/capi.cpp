@@ -20,6 +20,7 @@
 #include <memory>
 #include <chrono>
 #include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -739,6 +740,7 @@ static void free_state(State& s) {
   std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
   DeviceGuard dg(s.device);
   (void)hipDeviceSynchronize();
+  s.unpack_pool.reset();  // idle between runs; joined before the host ring goes
   void* ptrs[] = {s.X, s.Tr, s.Yval, s.Yraw, s.Ycode, s.Ybits, s.logtab, s.fam, s.varest, s.V0, s.iUGamma, s.mGamma, s.UGammaL,
                   s.aSigma, s.bSigma, s.XX, s.TT, s.V0g, s.V0gXXV0g, s.iV0, s.V0inv, s.iUmG, s.V0gXX, s.g2prep, s.scratch2, s.na_cols, s.na_index,
                   s.na_rows, s.row_na, s.row_slot, s.dev_flags, s.gbl_sync, s.Z, s.XEta, s.BL, s.Psi, s.Delta, s.Gamma, s.iV,
@@ -1348,6 +1350,58 @@ static void pretouch_record(const State& s, int k, const hmsc_record* rec) {
   }
 }
 
+// Record-unpack workers kept for the life of a chain: starting W threads in every run() cost
+// ~0.1 ms, a few percent of a 20-sweep run.  Between runs they sleep on a condition variable;
+// a run hands them one job (worker w unpacks samples w, w + W, ...) and waits for all of them.
+struct UnpackPool {
+  std::vector<std::thread> th;
+  std::mutex m;
+  std::condition_variable cv_job, cv_idle;
+  std::function<void(int)> job;
+  uint64_t gen = 0;
+  int busy = 0;
+  bool quit = false;
+  explicit UnpackPool(int W) {
+    for (int w = 0; w < W; ++w) th.emplace_back([this, w] { loop(w); });
+  }
+  void loop(int w) {
+    uint64_t seen = 0;
+    for (;;) {
+      std::function<void(int)> f;
+      {
+        std::unique_lock<std::mutex> lk(m);
+        cv_job.wait(lk, [&] { return quit || gen != seen; });
+        if (quit) return;
+        seen = gen;
+        f = job;
+      }
+      f(w);  // never throws: the job records its own failure
+      std::lock_guard<std::mutex> lk(m);
+      if (--busy == 0) cv_idle.notify_all();
+    }
+  }
+  void start(std::function<void(int)> f) {
+    std::lock_guard<std::mutex> lk(m);
+    job = std::move(f);
+    busy = (int)th.size();
+    ++gen;
+    cv_job.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> lk(m);
+    cv_idle.wait(lk, [&] { return busy == 0; });
+    job = nullptr;  // drop the finished run's references
+  }
+  ~UnpackPool() {
+    {
+      std::lock_guard<std::mutex> lk(m);
+      quit = true;
+    }
+    cv_job.notify_all();
+    for (auto& t : th) t.join();
+  }
+};
+
 static void run(State& s, int transient, int samples, int thin, const int* adaptNf, int iter0, int verbose,
                 int chain, hmsc_record* rec) {
   const auto t_entry = std::chrono::steady_clock::now();
@@ -1378,18 +1432,19 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
   const int W = recording ? std::max(1, std::min(w_env ? atoi(w_env) : 4,
                                                  std::max(1, (int)std::thread::hardware_concurrency() / 2)))
                           : 0;
-  std::vector<std::thread> workers;
-  struct Joiner {
-    std::vector<std::thread>& t;
+  if (recording && (!s.unpack_pool || (int)s.unpack_pool->th.size() != W))
+    s.unpack_pool = std::make_shared<UnpackPool>(W);
+  UnpackPool* pool = recording ? s.unpack_pool.get() : nullptr;
+  struct Joiner {  // an exception in the launch loop stops the workers before its locals go
+    UnpackPool* p;
     std::atomic<bool>& stop;
     ~Joiner() {
       stop.store(true);
-      for (auto& th : t)
-        if (th.joinable()) th.join();
+      if (p) p->wait();
     }
-  } joiner{workers, stop};
-  for (int w = 0; w < W; ++w)
-    workers.emplace_back([&, w] {
+  } joiner{nullptr, stop};
+  if (pool) {
+    pool->start([&](int w) {
       try {
         for (int k = w; k < samples; k += W) {
           if (__atomic_load_n(copied, __ATOMIC_ACQUIRE) <= (uint64_t)k) pretouch_record(s, k, rec);
@@ -1416,6 +1471,8 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
         cv_done.notify_all();
       }
     });
+    joiner.p = pool;
+  }
   const int total = transient + samples * thin;
   auto recorded = [&](int it) { return recording && it > transient && (it - transient) % thin == 0; };
   auto sample_of = [&](int it) { return (it - transient) / thin - 1; };
@@ -1458,6 +1515,9 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
     if (it > max_adapt) {
       int ng = G;  // the run's remainder: its binary decomposition, largest graph first
       while (ng > 1 && it + ng - 1 > total) ng >>= 1;
+      // a recorded run ends on single-sweep replays (..., 2, 1, 1): the samples of the last
+      // replay are copied out only after it, so a small last replay shortens the copy tail
+      if (recording && ng > 1 && it + ng - 1 == total) ng >>= 1;
       for (int j = it; j < it + ng; ++j)
         if (recorded(j)) {
           if (kfirst < 0) kfirst = sample_of(j);
@@ -1514,7 +1574,7 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
   copy_sync(gsync, s.gbl_sync, sizeof(gsync), hipMemcpyDeviceToHost, s.stream);
   HMSC_REQUIRE(gsync[3] == 0, "internal: the Gamma2 / BetaLambda in-launch handshake timed out");
   if (recording) {
-    for (auto& th : workers) th.join();
+    pool->wait();
     std::lock_guard<std::mutex> lk(mu);
     HMSC_REQUIRE(!worker_failed.load(), "record unpack: " + worker_err);
   }

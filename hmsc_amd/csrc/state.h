@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <memory>
 #include <vector>
 
 #include "../../include/hmsc_amd.h"
@@ -179,6 +180,7 @@ struct State {
   double* host_rec = nullptr;    // pinned host ring (ring_slots slots)
   uint64_t* copied_host = nullptr;  // fine-grained pinned counter: samples whose D2H copy landed
   uint64_t* copied_dev = nullptr;   // its device address
+  std::shared_ptr<struct UnpackPool> unpack_pool;  // record-unpack workers (capi.cpp), kept across runs
 
   // per-sweep hipGraph (single rank, no updateNf): captured once, replayed every sweep; the
   // kernels read the Philox sweep counter from d_iter, which the graph's first node advances
