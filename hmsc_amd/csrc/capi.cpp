@@ -694,14 +694,14 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.gbl_sync = dalloc<int>(4);  // dalloc zero-fills
   s.d_iters = dalloc<uint32_t>(64);  // graph_sweeps <= 64
   s.d_iter = s.d_iters;
-  if (s.mask & HMSC_UP_GAMMAETA) {  // updateGammaEta: dense (nc ns)^2 systems, one workgroup per level
+  if (s.mask & HMSC_UP_GAMMAETA) {  // updateGammaEta: dense (nc ns)^2 / joint spatial systems
     HMSC_REQUIRE(s.nranks == 1, "updateGammaEta cannot run on a species-sharded chain: pass updater GammaEta=FALSE");
     HMSC_REQUIRE((size_t)nc * s.ns <= 32768, "updateGammaEta: nc * ns must be <= 32768 (dense (nc ns)^2 systems, 4 x 8.6 GB)");
     for (int r = 0; r < s.nr; ++r)
     {
       HMSC_REQUIRE(s.lev[r].nfmax <= 16, "updateGammaEta: nfMax must be <= 16 in this build");
-      HMSC_REQUIRE(!s.lev[r].spatial || (size_t)nc * s.nt + (size_t)s.lev[r].np * s.lev[r].nfmax <= 8192,
-                   "updateGammaEta, spatial level: nc nt + np nfMax must be <= 8192 (dense joint system)");
+      HMSC_REQUIRE(!s.lev[r].spatial || (size_t)nc * s.nt + (size_t)s.lev[r].np * s.lev[r].nfmax <= 32768,
+                   "updateGammaEta, spatial level: nc nt + np nfMax must be <= 32768 (dense joint system, 8.6 GB)");
     }
     s.geWork = dalloc<double>(gamma_eta_work_doubles(s));
   }

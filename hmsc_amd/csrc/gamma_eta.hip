@@ -869,24 +869,38 @@ struct GESArgs {
   const double* AlphaD;   // nf, 1-based grid index
 };
 
-__global__ __launch_bounds__(1024) void gamma_eta_spatial_kernel(GESArgs sa) {
-  const GEArgs& a = sa.g;
-  __shared__ int flag;
-  const int t = threadIdx.x, nthr = blockDim.x;
-  const int ny = a.ny, ns = a.ns, nc = a.nc, nt = a.nt, nf = a.nf, np = a.np, K = a.K;
-  const int N = nc * ns, G = nc * nt, D2 = G + np * nf;
-  const GESLayout o = ges_layout(ny, ns, nc, nt, nf, np);
-  double* w = a.work;
-  double *S = w + o.S, *XtX = w + o.XtX, *XtS = w + o.XtS, *LamiD = w + o.LamiD, *LDL = w + o.LDL;
-  double *iQm = w + o.iQm, *PtX = w + o.PtX, *PtS = w + o.PtS, *cnt = w + o.cnt, *TdT = w + o.TdT;
-  double *TdL = w + o.TdL, *H = w + o.H, *C = w + o.C, *y = w + o.y, *iG = w + o.iG, *b = w + o.b;
-  const uint32_t it = SWEEP_ITER(a);
-  const uint32_t str = LEVEL_STRIDE * (uint32_t)a.r;
-  const double* lam = a.BL + a.loff;  // Lambda_r[h, j] = lam[h + K j]
-  const double* id = a.iSigma;
-  const int* pi = a.lev_pi[a.r];
+// The stages below are written over a flat index range [t0, n) with stride nthr, so the
+// same code runs inside one workgroup (gamma_eta_spatial_kernel: threads of the block,
+// __syncthreads between stages) and over a grid (the blocked path above GES_WG_MAX: one
+// launch per stage, the two factorizations on dense.hip's MFMA Cholesky).
+struct GESView {
+  int ny, ns, nc, nt, nf, np, K, N, G, D2;
+  double *S, *XtX, *XtS, *LamiD, *LDL, *iQm, *PtX, *PtS, *cnt, *TdT, *TdL, *H, *C, *y, *iG, *b;
+  const double *lam, *id;
+  const int* pi;
+};
 
-  // ---- stage 1: S (:37-42), X'X, Lam iD, Lam iD Lam', iQ, P'X, unit counts, Tr'iD Tr, Tr'iD Lam'
+__device__ inline GESView ges_view(const GESArgs& sa) {
+  const GEArgs& a = sa.g;
+  GESView v;
+  v.ny = a.ny, v.ns = a.ns, v.nc = a.nc, v.nt = a.nt, v.nf = a.nf, v.np = a.np, v.K = a.K;
+  v.N = v.nc * v.ns, v.G = v.nc * v.nt, v.D2 = v.G + v.np * v.nf;
+  const GESLayout o = ges_layout(v.ny, v.ns, v.nc, v.nt, v.nf, v.np);
+  double* w = a.work;
+  v.S = w + o.S, v.XtX = w + o.XtX, v.XtS = w + o.XtS, v.LamiD = w + o.LamiD, v.LDL = w + o.LDL;
+  v.iQm = w + o.iQm, v.PtX = w + o.PtX, v.PtS = w + o.PtS, v.cnt = w + o.cnt, v.TdT = w + o.TdT;
+  v.TdL = w + o.TdL, v.H = w + o.H, v.C = w + o.C, v.y = w + o.y, v.iG = w + o.iG, v.b = w + o.b;
+  v.lam = a.BL + a.loff;  // Lambda_r[h, j] = lam[h + K j]
+  v.id = a.iSigma;
+  v.pi = a.lev_pi[a.r];
+  return v;
+}
+
+// stage 1: S (:37-42), X'X, Lam iD, Lam iD Lam', iQ, P'X, unit counts, Tr'iD Tr, Tr'iD Lam'
+__device__ void ges_stage1(const GESArgs& sa, const GESView& v, size_t t, size_t nthr) {
+  const GEArgs& a = sa.g;
+  const int ny = v.ny, ns = v.ns, nc = v.nc, nt = v.nt, nf = v.nf, np = v.np, K = v.K;
+  const double *lam = v.lam, *id = v.id;
   for (size_t p = t; p < (size_t)ny * ns; p += nthr) {
     const int i = (int)(p % ny), j = (int)(p / ny);
     double sv = a.Z[p];
@@ -897,145 +911,244 @@ __global__ __launch_bounds__(1024) void gamma_eta_spatial_kernel(GESArgs sa) {
       const double* lq = a.BL + a.lev_loff[q] + (size_t)K * j;
       for (int h = 0; h < a.lev_nf[q]; ++h) sv -= eq[u + (size_t)npq * h] * lq[h];
     }
-    S[p] = sv;
+    v.S[p] = sv;
   }
-  for (int p = t; p < nc * nc; p += nthr) {
-    const int c1 = p % nc, c2 = p / nc;
+  for (size_t p = t; p < (size_t)nc * nc; p += nthr) {
+    const int c1 = (int)(p % nc), c2 = (int)(p / nc);
     double s = 0.0;
     for (int i = 0; i < ny; ++i) s = fma(a.X[i + (size_t)ny * c1], a.X[i + (size_t)ny * c2], s);
-    XtX[p] = s;
+    v.XtX[p] = s;
   }
-  for (int p = t; p < nf * ns; p += nthr) {
-    const int h = p % nf, j = p / nf;
-    LamiD[p] = lam[h + (size_t)K * j] * id[j];
+  for (size_t p = t; p < (size_t)nf * ns; p += nthr) {
+    const int h = (int)(p % nf), j = (int)(p / nf);
+    v.LamiD[p] = lam[h + (size_t)K * j] * id[j];
   }
-  for (int p = t; p < nf * nf; p += nthr) {
-    const int h1 = p % nf, h2 = p / nf;
+  for (size_t p = t; p < (size_t)nf * nf; p += nthr) {
+    const int h1 = (int)(p % nf), h2 = (int)(p / nf);
     double s = 0.0;
     for (int j = 0; j < ns; ++j) s = fma(lam[h1 + (size_t)K * j] * id[j], lam[h2 + (size_t)K * j], s);
-    LDL[p] = s;
+    v.LDL[p] = s;
   }
   if (a.phU) {
     const double* wq = a.phWinv + (size_t)ns * ((int)(*a.rho) - 1);
-    for (int p = t; p < ns * ns; p += nthr) {
-      const int j1 = p % ns, j2 = p / ns;
+    for (size_t p = t; p < (size_t)ns * ns; p += nthr) {
+      const int j1 = (int)(p % ns), j2 = (int)(p / ns);
       double si = 0.0;
       for (int i = 0; i < ns; ++i) si = fma(a.phU[j1 + (size_t)ns * i] * a.phU[j2 + (size_t)ns * i], wq[i], si);
-      iQm[p] = si;
+      v.iQm[p] = si;
     }
   } else {
-    for (int p = t; p < ns * ns; p += nthr) iQm[p] = (p % ns == p / ns) ? 1.0 : 0.0;
+    for (size_t p = t; p < (size_t)ns * ns; p += nthr) v.iQm[p] = (p % ns == p / ns) ? 1.0 : 0.0;
   }
-  for (int p = t; p < np * (nc + 1); p += nthr) {
-    const int u = p % np, c = p / np;
+  // P'X and the unit counts from the level's unit -> rows lists
+  for (size_t p = t; p < (size_t)np * (nc + 1); p += nthr) {
+    const int u = (int)(p % np), c = (int)(p / np);
     double s = 0.0;
-    for (int i = 0; i < ny; ++i)
-      if (pi[i] == u) s += (c < nc) ? a.X[i + (size_t)ny * c] : 1.0;
-    if (c < nc) PtX[p] = s; else cnt[u] = s;
+    for (int q = a.unit_ptr[u]; q < a.unit_ptr[u + 1]; ++q) s += (c < nc) ? a.X[a.unit_rows[q] + (size_t)ny * c] : 1.0;
+    if (c < nc) v.PtX[p] = s; else v.cnt[u] = s;
   }
-  for (int p = t; p < nt * (nt + nf); p += nthr) {
-    const int t1 = p % nt, k = p / nt;
+  for (size_t p = t; p < (size_t)nt * (nt + nf); p += nthr) {
+    const int t1 = (int)(p % nt), k = (int)(p / nt);
     double s = 0.0;
     for (int j = 0; j < ns; ++j)
       s = fma(id[j] * a.Tr[j + (size_t)ns * t1], k < nt ? a.Tr[j + (size_t)ns * k] : lam[(k - nt) + (size_t)K * j], s);
-    if (k < nt) TdT[t1 + nt * k] = s; else TdL[t1 + nt * (k - nt)] = s;
+    if (k < nt) v.TdT[t1 + nt * k] = s; else v.TdL[t1 + nt * (k - nt)] = s;
   }
-  __syncthreads();
-  // ---- stage 2: X'S, P'S, H = kron(iQ, iV) + kron(iD, X'X)  (:183)
-  for (int p = t; p < N; p += nthr) {
-    const int c = p % nc, j = p / nc;
+}
+
+// stage 2: X'S, P'S, H = kron(iQ, iV) + kron(iD, X'X)  (:183)
+__device__ void ges_stage2(const GESArgs& sa, const GESView& v, size_t t, size_t nthr) {
+  const GEArgs& a = sa.g;
+  const int ny = v.ny, ns = v.ns, nc = v.nc, np = v.np, N = v.N;
+  for (size_t p = t; p < (size_t)N; p += nthr) {
+    const int c = (int)(p % nc), j = (int)(p / nc);
     double s = 0.0;
-    for (int i = 0; i < ny; ++i) s = fma(a.X[i + (size_t)ny * c], S[i + (size_t)ny * j], s);
-    XtS[p] = s;
+    for (int i = 0; i < ny; ++i) s = fma(a.X[i + (size_t)ny * c], v.S[i + (size_t)ny * j], s);
+    v.XtS[p] = s;
   }
-  for (int p = t; p < np * ns; p += nthr) {
-    const int u = p % np, j = p / np;
+  for (size_t p = t; p < (size_t)np * ns; p += nthr) {
+    const int u = (int)(p % np), j = (int)(p / np);
     double s = 0.0;
-    for (int i = 0; i < ny; ++i)
-      if (pi[i] == u) s += S[i + (size_t)ny * j];
-    PtS[p] = s;
+    for (int q = a.unit_ptr[u]; q < a.unit_ptr[u + 1]; ++q) s += v.S[a.unit_rows[q] + (size_t)ny * j];
+    v.PtS[p] = s;
   }
   for (size_t p = t; p < (size_t)N * N; p += nthr) {
     const int r1 = (int)(p % N), r2 = (int)(p / N);
     const int c1 = r1 % nc, j1 = r1 / nc, c2 = r2 % nc, j2 = r2 / nc;
-    H[p] = iQm[j1 + (size_t)ns * j2] * a.iV[c1 + nc * c2] + (j1 == j2 ? id[j1] * XtX[c1 + nc * c2] : 0.0);
+    v.H[p] = v.iQm[j1 + (size_t)ns * j2] * a.iV[c1 + nc * c2] + (j1 == j2 ? v.id[j1] * v.XtX[c1 + nc * c2] : 0.0);
   }
-  __syncthreads();
-  // ---- stage 3: C, then L_H and tmp = L_H^-1 C (one column per thread), y = L_H^-1 vec(X'S iD)
-  for (size_t p = t; p < (size_t)N * D2; p += nthr) {
+}
+
+// stage 3: C = [kron(iD Tr, X'X), t(kron(Lam iD, P'X))] and y = vec(X'S iD)
+__device__ void ges_stage3(const GESArgs& sa, const GESView& v, size_t t, size_t nthr) {
+  const GEArgs& a = sa.g;
+  const int ns = v.ns, nc = v.nc, nf = v.nf, np = v.np, N = v.N, G = v.G;
+  for (size_t p = t; p < (size_t)N * v.D2; p += nthr) {
     const int r1 = (int)(p % N), col = (int)(p / N);
     const int c1 = r1 % nc, j = r1 / nc;
-    double v;
+    double val;
     if (col < G) {
       const int c2 = col % nc, q = col / nc;
-      v = id[j] * a.Tr[j + (size_t)ns * q] * XtX[c1 + nc * c2];
+      val = v.id[j] * a.Tr[j + (size_t)ns * q] * v.XtX[c1 + nc * c2];
     } else {
       const int e = col - G, u = e % np, h = e / np;
-      v = LamiD[h + nf * j] * PtX[u + (size_t)np * c1];
+      val = v.LamiD[h + nf * j] * v.PtX[u + (size_t)np * c1];
     }
-    C[p] = v;
+    v.C[p] = val;
   }
-  for (int p = t; p < N; p += nthr) y[p] = XtS[p] * id[p / nc];
-  __syncthreads();
-  if (!wg_chol(H, N, N, &flag) && t == 0) a.fail[0] = 1;
-  for (int col = t; col < D2 + 1; col += nthr) {
-    double* x = col < D2 ? C + (size_t)N * col : y;
+  for (size_t p = t; p < (size_t)N; p += nthr) v.y[p] = v.XtS[p] * v.id[p / nc];
+}
+
+// tmp = L_H^-1 [C | y], one column per index (L_H lower, in H)
+__device__ void ges_forward_cols(const GESView& v, size_t t, size_t nthr) {
+  const int N = v.N;
+  for (size_t col = t; col < (size_t)v.D2 + 1; col += nthr) {
+    double* x = col < (size_t)v.D2 ? v.C + (size_t)N * col : v.y;
     for (int i = 0; i < N; ++i) {
       double s = x[i];
-      for (int k = 0; k < i; ++k) s -= H[i + (size_t)N * k] * x[k];
-      x[i] = s / H[i + (size_t)N * i];
+      for (int k = 0; k < i; ++k) s -= v.H[i + (size_t)N * k] * x[k];
+      x[i] = s / v.H[i + (size_t)N * i];
     }
   }
-  __syncthreads();
-  // ---- stage 4: iG = bdiag(iU, iK) + Gm'Gm - tmp'tmp (:184-191), b = c0 - tmp'y
+}
+
+// stage 4: iG = bdiag(iU, iK) + Gm'Gm - tmp'tmp (:184-191), b = c0 - tmp'y; lower_only:
+// entries p1 >= p2 of iG (all the blocked Cholesky reads)
+__device__ void ges_stage4(const GESArgs& sa, const GESView& v, size_t t, size_t nthr, bool lower_only) {
+  const GEArgs& a = sa.g;
+  const int ns = v.ns, nc = v.nc, nt = v.nt, nf = v.nf, np = v.np, N = v.N, G = v.G, D2 = v.D2;
   for (size_t p = t; p < (size_t)D2 * D2; p += nthr) {
     const int p1 = (int)(p % D2), p2 = (int)(p / D2);
-    double v;
+    if (lower_only && p1 < p2) continue;
+    double val;
     if (p1 < G && p2 < G) {
       const int c1 = p1 % nc, t1 = p1 / nc, c2 = p2 % nc, t2 = p2 / nc;
-      v = TdT[t1 + nt * t2] * XtX[c1 + nc * c2] + a.iUGamma[p1 + (size_t)G * p2];
+      val = v.TdT[t1 + nt * t2] * v.XtX[c1 + nc * c2] + a.iUGamma[p1 + (size_t)G * p2];
     } else if (p1 >= G && p2 >= G) {
       const int e1 = p1 - G, e2 = p2 - G, u1 = e1 % np, h1 = e1 / np, u2 = e2 % np, h2 = e2 / np;
-      v = (u1 == u2) ? cnt[u1] * LDL[h1 + nf * h2] : 0.0;
+      val = (u1 == u2) ? v.cnt[u1] * v.LDL[h1 + nf * h2] : 0.0;
       if (h1 == h2) {
         const int g = (int)sa.AlphaD[h1] - 1;
-        v += sa.iWg[(size_t)np * np * g + u1 + (size_t)np * u2];
+        val += sa.iWg[(size_t)np * np * g + u1 + (size_t)np * u2];
       }
     } else {
       const int pg = p1 < G ? p1 : p2, pe = (p1 < G ? p2 : p1) - G;
       const int c = pg % nc, q = pg / nc, u = pe % np, h = pe / np;
-      v = TdL[q + nt * h] * PtX[u + (size_t)np * c];
+      val = v.TdL[q + nt * h] * v.PtX[u + (size_t)np * c];
     }
-    const double* c1 = C + (size_t)N * p1;
-    const double* c2 = C + (size_t)N * p2;
+    const double* c1 = v.C + (size_t)N * p1;
+    const double* c2 = v.C + (size_t)N * p2;
     double s = 0.0;
     for (int k = 0; k < N; ++k) s = fma(c1[k], c2[k], s);
-    iG[p] = v - s;
+    v.iG[p] = val - s;
   }
-  for (int p = t; p < D2; p += nthr) {
+  for (size_t p = t; p < (size_t)D2; p += nthr) {
     double c0 = 0.0;
-    if (p < G) {
-      const int c = p % nc, q = p / nc;
-      for (int j = 0; j < ns; ++j) c0 = fma(XtS[c + nc * j] * id[j], a.Tr[j + (size_t)ns * q], c0);
+    if ((int)p < G) {
+      const int c = (int)p % nc, q = (int)p / nc;
+      for (int j = 0; j < ns; ++j) c0 = fma(v.XtS[c + nc * j] * v.id[j], a.Tr[j + (size_t)ns * q], c0);
     } else {
-      const int e = p - G, u = e % np, h = e / np;
-      for (int j = 0; j < ns; ++j) c0 = fma(PtS[u + (size_t)np * j], LamiD[h + nf * j], c0);
+      const int e = (int)p - G, u = e % np, h = e / np;
+      for (int j = 0; j < ns; ++j) c0 = fma(v.PtS[u + (size_t)np * j], v.LamiD[h + nf * j], c0);
     }
-    const double* cp = C + (size_t)N * p;
+    const double* cp = v.C + (size_t)N * p;
     double s = 0.0;
-    for (int k = 0; k < N; ++k) s = fma(cp[k], y[k], s);
-    b[p] = c0 - s;
+    for (int k = 0; k < N; ++k) s = fma(cp[k], v.y[k], s);
+    v.b[p] = c0 - s;
   }
+}
+
+__device__ inline void ges_add_noise(const GESArgs& sa, const GESView& v, size_t t, size_t nthr) {
+  const GEArgs& a = sa.g;
+  const uint32_t it = SWEEP_ITER(a);
+  const uint32_t str = LEVEL_STRIDE * (uint32_t)a.r;
+  for (size_t p = t; p < (size_t)v.D2; p += nthr)
+    if (!a.noise_zero) v.b[p] += normal(a.key, (uint32_t)p, 0, S_GE_GAMMA + str, it);
+}
+
+__device__ inline void ges_store(const GESArgs& sa, const GESView& v, size_t t, size_t nthr) {
+  const GEArgs& a = sa.g;
+  for (size_t p = t; p < (size_t)v.G; p += nthr) a.Gamma[p] = v.b[p];
+  for (size_t p = t; p < (size_t)v.np * v.nf; p += nthr) a.Eta[p] = v.b[v.G + p];
+}
+
+__global__ __launch_bounds__(1024) void gamma_eta_spatial_kernel(GESArgs sa) {
+  __shared__ int flag;
+  const GESView v = ges_view(sa);
+  const size_t t = threadIdx.x, nthr = blockDim.x;
+  ges_stage1(sa, v, t, nthr);
   __syncthreads();
-  // ---- stage 5: m + chol(iG)^-1 xi = L^-T (L^-1 b + xi)   (:193-194)
-  if (!wg_chol(iG, D2, D2, &flag) && t == 0) a.fail[0] = 1;
-  wg_forward(iG, D2, D2, b);
-  for (int p = t; p < D2; p += nthr)
-    if (!a.noise_zero) b[p] += normal(a.key, (uint32_t)p, 0, S_GE_GAMMA + str, it);
+  ges_stage2(sa, v, t, nthr);
   __syncthreads();
-  wg_backward_t(iG, D2, D2, b);
-  for (int p = t; p < G; p += nthr) a.Gamma[p] = b[p];
-  for (int p = t; p < np * nf; p += nthr) a.Eta[p] = b[G + p];
+  ges_stage3(sa, v, t, nthr);
+  __syncthreads();
+  if (!wg_chol(v.H, v.N, v.N, &flag) && t == 0) sa.g.fail[0] = 1;
+  ges_forward_cols(v, t, nthr);
+  __syncthreads();
+  ges_stage4(sa, v, t, nthr, false);
+  __syncthreads();
+  // stage 5: m + chol(iG)^-1 xi = L^-T (L^-1 b + xi)   (:193-194)
+  if (!wg_chol(v.iG, v.D2, v.D2, &flag) && t == 0) sa.g.fail[0] = 1;
+  wg_forward(v.iG, v.D2, v.D2, v.b);
+  ges_add_noise(sa, v, t, nthr);
+  __syncthreads();
+  wg_backward_t(v.iG, v.D2, v.D2, v.b);
+  ges_store(sa, v, t, nthr);
+}
+
+// blocked path: each stage one grid launch
+template <int STAGE>
+__global__ __launch_bounds__(256) void ges_grid_kernel(GESArgs sa) {
+  const GESView v = ges_view(sa);
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nthr = (size_t)gridDim.x * blockDim.x;
+  if (STAGE == 1) ges_stage1(sa, v, t, nthr);
+  if (STAGE == 2) ges_stage2(sa, v, t, nthr);
+  if (STAGE == 3) ges_stage3(sa, v, t, nthr);
+  if (STAGE == 4) ges_forward_cols(v, t, nthr);
+  if (STAGE == 5) ges_stage4(sa, v, t, nthr, true);
+  if (STAGE == 6) ges_add_noise(sa, v, t, nthr);
+  if (STAGE == 7) ges_store(sa, v, t, nthr);
+}
+
+// one workgroup up to this joint size; above it the blocked path
+constexpr int GES_WG_MAX = 1024;
+
+static bool ges_blocked(int N, int D2) {
+  const char* env = getenv("HMSC_GES_BLOCKED");  // 1 / 0: force the blocked / one-workgroup path
+  const int force = env ? atoi(env) : -1;
+  if (force >= 0) return force > 0;
+  return D2 > GES_WG_MAX || N > GES_WG_MAX;
+}
+
+// the blocked path's workspace past ges_layout: dense_potrf_lower workspaces for H and iG
+static size_t ges_blocked_extra(int N, int D2) { return dense_ws_doubles(N) + dense_ws_doubles(D2) + 16; }
+
+static void launch_gamma_eta_spatial(State& s, const GESArgs& sa, hipStream_t st) {
+  const GEArgs& a = sa.g;
+  const int N = a.nc * a.ns, D2 = a.nc * a.nt + a.np * a.nf;
+  if (!ges_blocked(N, D2)) {
+    gamma_eta_spatial_kernel<<<1, 1024, 0, st>>>(sa);
+    HIP_OK(hipGetLastError());
+    return;
+  }
+  const GESLayout o = ges_layout(a.ny, a.ns, a.nc, a.nt, a.nf, a.np);
+  double* w = a.work;
+  double* ws1 = w + o.tot;
+  double* ws2 = ws1 + dense_ws_doubles(N);
+  auto grid = [](size_t n) { return (int)std::max<size_t>(1, std::min<size_t>(8192, (n + 255) / 256)); };
+  const size_t big1 = std::max({(size_t)a.ny * a.ns, (size_t)a.np * (a.nc + 1), (size_t)a.ns * a.ns});
+  ges_grid_kernel<1><<<grid(big1), 256, 0, st>>>(sa);
+  ges_grid_kernel<2><<<grid(std::max((size_t)N * N, (size_t)a.np * a.ns)), 256, 0, st>>>(sa);
+  ges_grid_kernel<3><<<grid((size_t)N * D2), 256, 0, st>>>(sa);
+  dense_potrf_lower(st, w + o.H, N, N, ws1, a.fail);
+  ges_grid_kernel<4><<<grid((size_t)D2 + 1), 256, 0, st>>>(sa);
+  ges_grid_kernel<5><<<grid((size_t)D2 * D2), 256, 0, st>>>(sa);
+  dense_potrf_lower(st, w + o.iG, D2, D2, ws2, a.fail);
+  dense_trsv_lower(st, w + o.iG, D2, D2, w + o.b, 0, ws2);
+  ges_grid_kernel<6><<<grid(D2), 256, 0, st>>>(sa);
+  dense_trsv_lower(st, w + o.iG, D2, D2, w + o.b, 1, ws2);
+  ges_grid_kernel<7><<<grid(D2), 256, 0, st>>>(sa);
+  HIP_OK(hipGetLastError());
 }
 
 size_t gamma_eta_work_doubles(const State& s) {
@@ -1044,7 +1157,11 @@ size_t gamma_eta_work_doubles(const State& s) {
     const int nf = std::max(1, s.lev[r].nfmax);
     const int np = s.lev[r].np == s.ny ? 0 : s.lev[r].np;
     m = std::max(m, ge_layout(s.ny, s.ns, s.nc, s.nt, nf, np).tot + ge_blocked_extra(s.nc * s.ns));
-    if (s.lev[r].spatial) m = std::max(m, ges_layout(s.ny, s.ns, s.nc, s.nt, nf, s.lev[r].np).tot);
+    if (s.lev[r].spatial) {
+      const int N = s.nc * s.ns, D2 = s.nc * s.nt + s.lev[r].np * nf;
+      m = std::max(m, ges_layout(s.ny, s.ns, s.nc, s.nt, nf, s.lev[r].np).tot +
+                          (ges_blocked(N, D2) ? ges_blocked_extra(N, D2) : 0));
+    }
   }
   return m + 64;
 }
@@ -1099,7 +1216,7 @@ void launch_gamma_eta(State& s, uint32_t iter) {
       sa.g = a;
       sa.iWg = s.lev[r].iWg;
       sa.AlphaD = s.lev[r].AlphaD;
-      gamma_eta_spatial_kernel<<<1, 1024, 0, s.stream>>>(sa);
+      launch_gamma_eta_spatial(s, sa, s.stream);
     } else if (a.nc * a.ns > GE_WG_MAX) {
       launch_gamma_eta_blocked(s, a, s.stream);
     } else {

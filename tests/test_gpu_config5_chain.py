@@ -56,6 +56,32 @@ def test_full_ny1000_trajectory_matches_oracle():
     assert rel_err(g["Lambda"][0], o["Lambda"][0]) < 1e-6
 
 
+def test_full_ny1000_default_updaters_with_gamma_eta_matches_oracle(monkeypatch):
+    """R's default updater set on the vignette's model (GammaEta on, which the vignette itself
+    turns off at :124): updateGammaEta's spatial branch draws (Gamma, Eta) jointly from the
+    (nc nt + np)^2 = 1002^2 precision on the blocked grid path (dense.hip Cholesky)."""
+    monkeypatch.setenv("HMSC_GES_BLOCKED", "1")
+    hM = spatial_vignette4(ny=1000, method="Full")
+    m = oracle_model(hM)
+    dp = O.compute_data_parameters(m)
+    seed = 4243
+    rng = Rng(seed)
+    st = O.compute_initial_parameters(m, rng, nf=[1])
+    ch = H.Chain(hM, seed, device=0, updater={})
+    ch.init([1])
+    ch.set_state(st)
+    o = dict(st)
+    for it in range(1, 9):
+        ch.sweep(it)
+        o = O.sweep(o, m, rng, it, data_par=dp)
+    g = ch.get_state()
+    ch.close()
+    for k in ("Beta", "Gamma", "iV"):
+        assert rel_err(g[k], o[k]) < 1e-6, (k, rel_err(g[k], o[k]))
+    assert rel_err(g["Eta"][0], o["Eta"][0]) < 1e-6
+    assert np.array_equal(g["Alpha"][0], o["Alpha"][0])
+
+
 def test_full_ny5000_from_init_stays_where_the_conditional_says():
     from hmsc_amd.dataparams import _level_order
     hM = spatial_vignette4(ny=5000, method="Full")

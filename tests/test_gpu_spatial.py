@@ -4,7 +4,7 @@ alphapw grid matrices iWg[,,alpha_h]) and updateAlpha (R/updateAlpha.R:20-79: gr
 posterior from |RiWg eta_h|^2 and detWg).  The grids are computeDataParameters' (host,
 R/computeDataParameters.R:53-81; the oracle recomputes them itself from the distances).
 Both sides share the Philox counters: moments to 1e-10, draws to fp64 rounding, the drawn
-grid indices exactly, and full sweeps (GammaEta off: its spatial branch is not built)."""
+grid indices exactly, and full sweeps; updateGammaEta's spatial branch further down."""
 import numpy as np
 import pytest
 
@@ -173,8 +173,16 @@ def _ge_chain(hM, seed, st):
     return ch
 
 
-def test_spatial_gamma_eta_moments(ge_setup):
+# "auto": one workgroup up to nc nt + np nf = 1024 (large_full is above it: the blocked grid
+# path); "blocked": every model forced onto the blocked path (grid stages, dense.hip Cholesky)
+GE_PATHS = ["auto", "blocked"]
+
+
+@pytest.mark.parametrize("path", GE_PATHS)
+def test_spatial_gamma_eta_moments(ge_setup, path, monkeypatch):
     name, hM, m, dp, seed, st = ge_setup
+    if path == "blocked":
+        monkeypatch.setenv("HMSC_GES_BLOCKED", "1")
     ch = _ge_chain(hM, seed, st)
     ch.set_noise_mode(1)
     ch.update("GammaEta", 5)
@@ -186,8 +194,11 @@ def test_spatial_gamma_eta_moments(ge_setup):
     ch.close()
 
 
-def test_spatial_gamma_eta_draws(ge_setup):
+@pytest.mark.parametrize("path", GE_PATHS)
+def test_spatial_gamma_eta_draws(ge_setup, path, monkeypatch):
     name, hM, m, dp, seed, st = ge_setup
+    if path == "blocked":
+        monkeypatch.setenv("HMSC_GES_BLOCKED", "1")
     ch = _ge_chain(hM, seed, st)
     ch.update("GammaEta", 6)
     g = ch.get_state()
