@@ -1506,6 +1506,9 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
   if (adaptNf)
     for (int r = 0; r < s.nr; ++r) max_adapt = std::max(max_adapt, adaptNf[r]);
   if (recording) set_desc_kernel<<<1, 1, 0, s.stream>>>(s.d_rec_desc, iter0, transient, thin, samples);
+  // the fused Gamma2 + BetaLambda flag holds the epoch of the last sweep that published: a
+  // run's sweeps are distinct, but an earlier run may have ended on one of them
+  if (s.gbl_sync) HIP_OK(hipMemsetAsync(s.gbl_sync + 1, 0, sizeof(int), s.stream));
   const auto t_start = std::chrono::steady_clock::now();
   for (int it = 1; it <= total;) {
     const int G = s.graph_sweeps;

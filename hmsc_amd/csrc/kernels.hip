@@ -303,6 +303,10 @@ __global__ __launch_bounds__(64) void beta_lambda_kernel(BLArgs a) {
 // LDS of the body (doubles): the four waves' tiles, G, iV, Gamma, tau
 constexpr int BLW_LDS = 4 * WV_TILE + 32 * 33 + 32 * 32 + 32 * 8 + 64;
 
+// the fused Gamma2 + BetaLambda launch's publish value for sweep `iter`: never 0 (the reset
+// value hmsc_run / the eager launcher write), distinct for distinct sweeps of a run
+__device__ __host__ inline int g2bl_epoch(uint32_t iter) { return (int)(iter | 0x80000000u); }
+
 // WAIT_GAMMA (the fused Gamma2 + BetaLambda launch, gamma2_bl_kernel): the new Gamma is
 // published by another workgroup of the same launch (gsync[1]); everything that does not
 // depend on it -- the prologue, iU and its Cholesky factor -- runs first.
@@ -391,13 +395,16 @@ __device__ __forceinline__ void beta_lambda_wave_body(const BLArgs& a, double* l
   if (WAIT_GAMMA && blk == 0 && w == 0) HMSC_STAMP_RT(74);
   double mu = 0.0;  // Mu_j = Gamma Tr_j^T   (:62)
   if (WAIT_GAMMA) {
-    // the new Gamma of this sweep (updateGamma2, published by the launch's Gamma2 workgroup)
+    // the new Gamma of this sweep (updateGamma2, published by the launch's Gamma2 workgroup
+    // as this sweep's epoch, so nothing has to reset the flag: a per-wave "done" count for
+    // that reset was 1000 same-address device-scope atomics, ~10 us of serialised tail)
     // relaxed polling, and Gamma (the only datum published inside the launch) read with
     // device-coherent loads below: an acquire -- per poll, or one fence per wave after it --
     // invalidates the XCD's L2, and a thousand of them under every other wave of the device
     // took the solves after the wait from 5 to 16 us; bounded: a broken handshake raises the
     // error flag (hmsc_run reports it) instead of hanging
-    for (int spin = 0; __hip_atomic_load(&gsync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0; ++spin) {
+    const int epoch = g2bl_epoch(SWEEP_ITER(a));
+    for (int spin = 0; __hip_atomic_load(&gsync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch; ++spin) {
       if (spin > (1 << 20)) {
         if (i == 0) __hip_atomic_store(&gsync[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
@@ -405,14 +412,6 @@ __device__ __forceinline__ void beta_lambda_wave_body(const BLArgs& a, double* l
       __builtin_amdgcn_s_sleep(8);
     }
     if (blk == 0 && w == 0) HMSC_STAMP_RT(75);
-    if (i == 0) {  // the last wave through resets the handshake for the next launch
-      const int done = __hip_atomic_fetch_add(&gsync[2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (done == a.ns_loc - 1) {
-        __hip_atomic_store(&gsync[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&gsync[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&gsync[2], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
     if (i < nc)
 #pragma unroll
       for (int q = 0; q < 8; ++q)
@@ -1250,8 +1249,10 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
 // stage and publishes Gamma (sync[1]); workgroups nparts.. run the wave BetaLambda body, which
 // factors iU while Gamma2 runs and waits for Gamma only for the mean and the solves.  Every
 // workgroup of the launch is resident at once (nparts + ns / 4 <= 3 per CU at 52 KB of LDS),
-// so the wait cannot block the workgroup it waits for.  The last BetaLambda wave through resets
-// the handshake (ticket, flag, count) for the next launch.
+// so the wait cannot block the workgroup it waits for.  The ticket is reset by the workgroup
+// that takes the last one; the flag holds the sweep's epoch (g2bl_epoch), reset to 0 by the
+// host at the start of every run and before every eager launch, so it never needs a reset
+// inside the launch.
 // ---------------------------------------------------------------------------
 struct G2BLArgs {
   G2Args g2;
@@ -1262,7 +1263,7 @@ struct G2BLArgs {
   const double* Tr;
   double* part;
   int K, nc, NF, nt, nsl;
-  int* sync;            // [ticket, Gamma published, BetaLambda waves through]
+  int* sync;            // [ticket, epoch of the published Gamma, -, handshake timed out]
 };
 
 template <int NM>
@@ -1284,7 +1285,10 @@ __global__ __launch_bounds__(256) void gamma2_bl_kernel(G2BLArgs f) {
     gamma2_final_body(f.g2, smem);
     __syncthreads();
     if (threadIdx.x < 64) HMSC_STAMP_RT(73);
-    if (threadIdx.x == 0) __hip_atomic_store(&f.sync[1], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(&f.sync[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every ticket is in
+      __hip_atomic_store(&f.sync[1], g2bl_epoch(SWEEP_ITER(f.g2)), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
     return;
   }
   beta_lambda_wave_body<NM, true>(f.bl, smem, blockIdx.x - nparts, f.sync);
@@ -1428,6 +1432,7 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
   f.nt = s.nt;
   f.nsl = s.nsl;
   f.sync = s.gbl_sync;
+  if (!s.capturing) HIP_OK(hipMemsetAsync(s.gbl_sync + 1, 0, sizeof(int), s.stream));  // an eager sweep may repeat an iter
   const int nb = nparts + (s.nsl + 3) / 4;
   const size_t smem = BLW_LDS * sizeof(double);
   ProfScope ps(s, PROF_BL);
