@@ -1,12 +1,15 @@
 #!/bin/bash
-# A/B on one box: bench.py with and without the per-sweep hipGraph, twice each, interleaved.
+# same-box A/B of two builds of the library: alternating 1000-step bench runs
+# usage: ab_bench.sh TAG LIB_A LIB_B [ROUNDS]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=$1; A=$2; B=$3; N=${4:-3}
 mkdir -p $R/gpurun_out
 cd $R
-for rep in 1 2; do
-  for ng in 0 1; do
-    HMSC_NO_GRAPH=$ng timeout -k 10 300 python bench.py --steps ${STEPS:-300} --warmup 30 --no-cpu > gpurun_out/ab_${ng}_${rep}.json 2>gpurun_out/ab.err || { tail -5 gpurun_out/ab.err; exit 1; }
-    python -c "import json; d=json.load(open('gpurun_out/ab_${ng}_${rep}.json')); print('no_graph=$ng', d['value'], d['ms_per_step'], d['kernels_us'])"
-  done
+for i in $(seq 1 $N); do
+for L in A B; do
+  LIB=$A; [ $L = B ] && LIB=$B
+  HMSC_AMD_LIB=$R/$LIB timeout -k 10 300 python bench.py --steps 1000 --warmup 100 --no-cpu > gpurun_out/${TAG}_${L}_$i.json 2> gpurun_out/${TAG}_${L}_$i.err || { echo "bench $L failed"; tail -20 gpurun_out/${TAG}_${L}_$i.err; exit 1; }
+  python -c "import json;d=json.load(open('gpurun_out/${TAG}_${L}_$i.json'));print('$L', d['value'], d.get('kernels_live_us'))"
+done
 done
