@@ -744,14 +744,22 @@ __device__ __forceinline__ void gammav_body(const GVWArgs& a) {
   const int nA = nc * nc, nB = nc * nt;
   HMSC_STAMP(0);
   if (t == 0) sok = 1;
-  for (int p = t; p < nA; p += blockDim.x) sXX[p % nc + WV_LD * (p / nc)] = a.XX[p];
-  for (int p = t; p < nt * nt; p += blockDim.x) sTT[p] = a.TT[p];
-  for (int p = t; p < N * N; p += blockDim.x) sIUG[p] = a.iUGamma[p];
-  if (a.do_prep)
-    for (int p = t; p < nA; p += blockDim.x) sIV0[p] = a.iV0[p];
-  for (int p = t; p < N; p += blockDim.x) sIUmG[p] = a.iUmG[p];
+  // the constants' loads all issued first and stored after the partial sums' loads below (a
+  // staging loop with a store per iteration waits out one memory latency per iteration:
+  // five arrays were ~8 round trips before the first partial load).  nc^2, N^2 <= 1024.
+  double cXX[4], cIUG[4], cIV0[4], cTT, cIUmG;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int p = t + 256 * u;
+    cXX[u] = p < nA ? a.XX[p] : 0.0;
+    cIUG[u] = p < N * N ? a.iUGamma[p] : 0.0;
+    cIV0[u] = (a.do_prep && p < nA) ? a.iV0[p] : 0.0;
+  }
+  cTT = t < nt * nt ? a.TT[t] : 0.0;
+  cIUmG = t < N ? a.iUmG[t] : 0.0;
   for (int p = t; p < nA + nB; p += blockDim.x) {
     // species-block partials in block order, 32 loads in flight (one L2 round trip per 32)
+    const double v0 = p < nA ? a.V0[p] : 0.0;
     const double* src = a.part + p;
     const size_t st = (size_t)(nA + nB);
     double sum = 0.0;
@@ -772,10 +780,19 @@ __device__ __forceinline__ void gammav_body(const GVWArgs& a) {
     }
     for (; b < a.nparts; ++b) sum += src[st * b];
     if (p < nA)
-      sA[p] = sum + a.V0[p];  // E E^T + V0   (R/updateGammaV.R:18-19)
+      sA[p] = sum + v0;       // E E^T + V0   (R/updateGammaV.R:18-19)
     else
       sBTr[p - nA] = sum;     // B Tr
   }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int p = t + 256 * u;
+    if (p < nA) sXX[p % nc + WV_LD * (p / nc)] = cXX[u];
+    if (p < N * N) sIUG[p] = cIUG[u];
+    if (a.do_prep && p < nA) sIV0[p] = cIV0[u];
+  }
+  if (t < nt * nt) sTT[t] = cTT;
+  if (t < N) sIUmG[t] = cIUmG;
   // Bartlett factor Zb of rwish (MCMCpack: diag sqrt(chisq(v - i)), upper N(0,1)), drawn by
   // all 256 threads at once: T3 = Zb padded with I to 32 x 32
   {
@@ -907,9 +924,10 @@ static GVWArgs make_gvw_args(State& s, uint32_t iter, const double* part, int np
 static void launch_gammav_wave(State& s, uint32_t iter, hipStream_t st, const double* part, int np,
                                const uint32_t* iter_dev) {
   const GVWArgs w = make_gvw_args(s, iter, part, np, iter_dev);
-  switch (wv_bucket(s.nc * s.nt)) {
+  switch (wv_bucket_gv(s.nc * s.nt)) {
     case 8: gammav_wave_kernel<8><<<1, 256, 0, st>>>(w); break;
     case 16: gammav_wave_kernel<16><<<1, 256, 0, st>>>(w); break;
+    case 20: gammav_wave_kernel<20><<<1, 256, 0, st>>>(w); break;
     case 24: gammav_wave_kernel<24><<<1, 256, 0, st>>>(w); break;
     default: gammav_wave_kernel<32><<<1, 256, 0, st>>>(w); break;
   }
@@ -2218,9 +2236,10 @@ void launch_side_fused(State& s, uint32_t iter) {
   const GVWArgs gw = make_gvw_args(s, iter, s.gv_part, ngv, itd);
   LPArgs lps = a.lp;
   lps.iter_dev = itd;
-  switch (wv_bucket(s.nc * s.nt)) {
+  switch (wv_bucket_gv(s.nc * s.nt)) {
     case 8: side_chain_kernel<8><<<1 + s.nr, 256, 0, s.side>>>(gw, lps, s.psi_rs, npsi); break;
     case 16: side_chain_kernel<16><<<1 + s.nr, 256, 0, s.side>>>(gw, lps, s.psi_rs, npsi); break;
+    case 20: side_chain_kernel<20><<<1 + s.nr, 256, 0, s.side>>>(gw, lps, s.psi_rs, npsi); break;
     case 24: side_chain_kernel<24><<<1 + s.nr, 256, 0, s.side>>>(gw, lps, s.psi_rs, npsi); break;
     default: side_chain_kernel<32><<<1 + s.nr, 256, 0, s.side>>>(gw, lps, s.psi_rs, npsi); break;
   }

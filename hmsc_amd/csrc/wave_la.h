@@ -26,6 +26,10 @@ __device__ __forceinline__ double bcast(double v, int l) {
 
 // dimension bucket for a runtime size (callers dispatch on it)
 __host__ __device__ constexpr int wv_bucket(int n) { return n <= 8 ? 8 : n <= 16 ? 16 : n <= 24 ? 24 : 32; }
+// the GammaV / Gamma2-prep chain (nc nt): also a 20 bucket -- its factorisations and
+// inverses run every step to NM, so 20 x 20 systems (nc = 20, nt = 1) padded to 24 did
+// (24/20)^3 = 1.7x the work of the cubic steps
+__host__ __device__ constexpr int wv_bucket_gv(int n) { return n <= 8 ? 8 : n <= 16 ? 16 : n <= 20 ? 20 : n <= 24 ? 24 : 32; }
 
 // rows/cols >= n (and lanes >= n) set to d * I
 template <int NM>
