@@ -692,6 +692,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.allreduce_buf = dalloc<double>((size_t)nc * nc + 2 * N + nfm * nt + nfm + 64);
   s.dev_flags = dalloc<int>(16);
   s.gbl_sync = dalloc<int>(4);  // dalloc zero-fills
+  s.trsv_sync = dalloc<int>(2 + 4096);
   s.d_iters = dalloc<uint32_t>(64);  // graph_sweeps <= 64
   s.d_iter = s.d_iters;
   if (s.mask & HMSC_UP_GAMMAETA) {  // updateGammaEta: dense (nc ns)^2 / joint spatial systems
@@ -743,7 +744,7 @@ static void free_state(State& s) {
   s.unpack_pool.reset();  // idle between runs; joined before the host ring goes
   void* ptrs[] = {s.X, s.Tr, s.Yval, s.Yraw, s.Ycode, s.Ybits, s.logtab, s.fam, s.varest, s.V0, s.iUGamma, s.mGamma, s.UGammaL,
                   s.aSigma, s.bSigma, s.XX, s.TT, s.V0g, s.V0gXXV0g, s.iV0, s.V0inv, s.iUmG, s.V0gXX, s.g2prep, s.scratch2, s.na_cols, s.na_index,
-                  s.na_rows, s.row_na, s.row_slot, s.dev_flags, s.gbl_sync, s.Z, s.XEta, s.BL, s.Psi, s.Delta, s.Gamma, s.iV,
+                  s.na_rows, s.row_na, s.row_slot, s.dev_flags, s.gbl_sync, s.trsv_sync, s.Z, s.XEta, s.BL, s.Psi, s.Delta, s.Gamma, s.iV,
                   s.iSigma, s.rho, s.XZ, s.G, s.ZTr, s.XZ_part, s.G_part, s.ZTr_part, s.Gna, s.ZL, s.ZL_part,
                   s.CR, s.CR_part, s.LS, s.Msmall, s.scratch, s.psi_rs, s.ABpart, s.dbg_prec, s.ring, s.allreduce_buf,
                   s.phU, s.phWinv, s.phRbase, s.phTt, s.phBt, s.phEt, s.phTTw, s.phWork, s.UGamma, s.geWork};
@@ -1665,13 +1666,15 @@ int hmsc_dense_chol_solve(int32_t device, double* A, int32_t n, double* b, int32
     double* db = bufs.alloc<double>(n);
     double* ws = bufs.alloc<double>(dense_ws_doubles(n));
     int* dinfo = bufs.alloc<int>(1);
+    int* dsync = bufs.alloc<int>(2 + 4096);  // the sync-free solves' handshake, zeroed
     HIP_OK(hipMemsetAsync(dinfo, 0, sizeof(int), st));
+    HIP_OK(hipMemsetAsync(dsync, 0, (2 + 4096) * sizeof(int), st));
     HIP_OK(hipMemcpyAsync(dA, A, nn * sizeof(double), hipMemcpyHostToDevice, st));
     if (b) HIP_OK(hipMemcpyAsync(db, b, (size_t)n * sizeof(double), hipMemcpyHostToDevice, st));
     dense_potrf_lower(st, dA, n, n, ws, dinfo);
     if (b) {
-      dense_trsv_lower(st, dA, n, n, db, 0, ws);
-      dense_trsv_lower(st, dA, n, n, db, 1, ws);
+      dense_trsv_lower(st, dA, n, n, db, 0, ws, 0, dsync);
+      dense_trsv_lower(st, dA, n, n, db, 1, ws, 0, dsync);
       HIP_OK(hipMemcpyAsync(b, db, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, st));
     }
     HIP_OK(hipMemcpyAsync(A, dA, nn * sizeof(double), hipMemcpyDeviceToHost, st));

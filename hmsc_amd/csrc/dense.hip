@@ -21,6 +21,8 @@
 // a one-workgroup solve of the diagonal block, then a multi-workgroup GEMV of the panel.
 // Only the lower triangle of A is read; its upper triangle is left untouched except inside
 // diagonal tiles (scratch).
+#include <cstdlib>
+
 #include "common.h"
 #include "state.h"
 #include "z_kernel.h"  // d4, mfma_f64
@@ -484,6 +486,135 @@ __global__ __launch_bounds__(256) void trsv_bwd_kernel(const double* L, int lda,
 }
 
 // ---------------------------------------------------------------------------------------
+// Sync-free triangular solve (dense, unbanded): one launch, one workgroup per 64-row block,
+// blocks taken in dependency order through a ticket (so every block a workgroup waits on
+// belongs to a workgroup that is already running: no residency assumption).  Block k
+// accumulates its update from each finished block j as soon as that block's flag is up
+// (forward: sum_j L_kj y_j, j < k; transposed: sum_j L_jk^T x_j, j > k), with the next
+// block's L tile already in flight, then solves its diagonal block with the factorization's
+// Linv_k (a 64 x 64 matrix-vector product) in place in x and raises its flag.  The chain of
+// blocks costs one flag round trip + one block solve per block instead of one kernel launch
+// per block.  Flags are read with relaxed polling and the solved values with device-coherent
+// loads (an acquire per poll would invalidate the XCD's L2); the last workgroup to finish
+// resets the ticket, the done count and the flags for the next call.
+// sync (device, zeroed once): [0] ticket, [1] done count, [2 + b] flag of block b.
+constexpr int TRSV_SF_MAXB = 4096;
+
+__device__ __forceinline__ double load_coherent(const double* p) {
+  return __longlong_as_double(
+      (long long)__hip_atomic_load((const unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+__device__ __forceinline__ void wait_flag(const int* f) {
+  for (int spin = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 && spin < (1 << 24); ++spin)
+    __builtin_amdgcn_s_sleep(1);
+}
+
+template <bool TR>
+__global__ __launch_bounds__(256) void trsv_sf_kernel(const double* L, int lda, int n, const double* Linv, double* x,
+                                                      int* sync) {
+  __shared__ int s_ord;
+  __shared__ double red[DB * (DB + 1)];  // [row][part] partial sums (ld DB + 1)
+  __shared__ double z[DB];
+  const int nbk = (n + DB - 1) / DB, t = threadIdx.x, lane = t & 63, g = t >> 6;
+  if (t == 0) s_ord = __hip_atomic_fetch_add(&sync[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int ord = s_ord;
+  const int k = TR ? nbk - 1 - ord : ord, R0 = k * DB, nb = min(DB, n - R0);
+  int* flag = sync + 2;
+  // this block's own operands -- Linv_k (lane = output row, wave g = terms 16 g ..) and x_k --
+  // loaded before the dependency chain, so the solve after the last flag waits on no memory
+  const double* Li = Linv + (size_t)k * DB * DB;
+  double li[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int c = 16 * g + u;
+    li[u] = TR ? Li[c + DB * lane] : Li[lane + DB * c];
+  }
+  const double xk = t < nb ? x[R0 + t] : 0.0;
+  double acc[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) acc[u] = 0.0;
+  if (!TR) {
+    // lane = row r of block k, wave g = columns 16 g .. 16 g + 15 of each block j < k (full blocks)
+    const size_t row = (size_t)(R0 + min(lane, nb - 1));
+    double lc[16], ln[16];
+    if (k > 0)
+#pragma unroll
+      for (int u = 0; u < 16; ++u) lc[u] = L[row + (size_t)lda * (16 * g + u)];
+    for (int j = 0; j < k; ++j) {
+      if (j + 1 < k)
+#pragma unroll
+        for (int u = 0; u < 16; ++u) ln[u] = L[row + (size_t)lda * (DB * (j + 1) + 16 * g + u)];
+      if (t == 0) wait_flag(flag + j);
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < 16; ++u) acc[u] = fma(lc[u], load_coherent(x + DB * j + 16 * g + u), acc[u]);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) lc[u] = ln[u];
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) s += acc[u];
+    red[lane * (DB + 1) + g] = s;
+  } else {
+    // lane = row c of block j > k (coalesced column runs), wave g = outputs r = 16 g .. 16 g + 15
+    double lc[16], ln[16];
+    auto ldt = [&](double (&v)[16], int j) {
+      const int rows = min(DB, n - DB * j);
+      const size_t row = (size_t)(DB * j + min(lane, rows - 1));
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = lane < rows ? L[row + (size_t)lda * (R0 + min(16 * g + u, nb - 1))] : 0.0;
+    };
+    if (k < nbk - 1) ldt(lc, nbk - 1);
+    for (int j = nbk - 1; j > k; --j) {
+      if (j - 1 > k) ldt(ln, j - 1);
+      if (t == 0) wait_flag(flag + j);
+      __syncthreads();
+      const int rows = min(DB, n - DB * j);
+      const double xv = lane < rows ? load_coherent(x + DB * j + lane) : 0.0;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) acc[u] = fma(lc[u], xv, acc[u]);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) lc[u] = ln[u];
+    }
+    // acc[u]: partial over this lane's row c for output 16 g + u -> red[output][c]
+#pragma unroll
+    for (int u = 0; u < 16; ++u) red[(16 * g + u) * (DB + 1) + lane] = acc[u];
+  }
+  __syncthreads();
+  // b = x_k - update
+  if (t < DB) {
+    double s = 0.0;
+    if (!TR) {
+      s = (red[t * (DB + 1)] + red[t * (DB + 1) + 1]) + (red[t * (DB + 1) + 2] + red[t * (DB + 1) + 3]);
+    } else {
+      for (int c = 0; c < DB; ++c) s += red[t * (DB + 1) + c];
+    }
+    z[t] = t < nb ? xk - s : 0.0;
+  }
+  __syncthreads();
+  // x_k = Linv_k b (or Linv_k^T b): lane = output row, wave g = 16 of the 64 terms
+  double s = 0.0;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) s = fma(li[u], z[16 * g + u], s);
+  red[lane * (DB + 1) + g] = s;
+  __syncthreads();
+  if (t < nb) x[R0 + t] = (red[t * (DB + 1)] + red[t * (DB + 1) + 1]) + (red[t * (DB + 1) + 2] + red[t * (DB + 1) + 3]);
+  __syncthreads();  // every store of the block done before the flag
+  if (t == 0) {
+    __hip_atomic_store(flag + k, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    // the last workgroup through resets the call's handshake (every other one has finished
+    // its reads: it counted itself done after them)
+    if (__hip_atomic_fetch_add(&sync[1], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nbk - 1) {
+      for (int b = 0; b < nbk; ++b) __hip_atomic_store(flag + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&sync[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&sync[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // inverse of a lower factor (trtri) and M^T M (lauum): the spatial grid precompute
 // (R/computeDataParameters.R:53-81 evaluates iW = chol2inv(chol(W)) for every grid point)
 // ---------------------------------------------------------------------------------------
@@ -779,8 +910,21 @@ void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, in
 // x <- L^-1 x  (trans = 0)  or  x <- L^-T x  (trans = 1), L lower (n x n, ld lda) as left by
 // dense_potrf_lower together with its workspace `ws` (diagonal-block inverses, then n doubles
 // in which the solution is assembled before it is copied back to x)
-void dense_trsv_lower(hipStream_t st, const double* L, int n, int lda, double* x, int trans, double* ws, int bw) {
+void dense_trsv_lower(hipStream_t st, const double* L, int n, int lda, double* x, int trans, double* ws, int bw,
+                      int* sync) {
   const int nbk = (n + DB - 1) / DB;
+  static const bool sf_off = [] {  // HMSC_NO_TRSV_SF=1: one launch per block (A/B diagnostics)
+    const char* e = std::getenv("HMSC_NO_TRSV_SF");
+    return e && e[0] && e[0] != '0';
+  }();
+  if (sync && bw <= 0 && nbk >= 2 && nbk <= TRSV_SF_MAXB && !sf_off) {
+    if (trans)
+      trsv_sf_kernel<true><<<nbk, 256, 0, st>>>(L, lda, n, ws, x, sync);
+    else
+      trsv_sf_kernel<false><<<nbk, 256, 0, st>>>(L, lda, n, ws, x, sync);
+    HIP_OK(hipGetLastError());
+    return;
+  }
   double* y = ws + (size_t)nbk * DB * DB;
   if (!trans) {
     for (int b = 0; b < nbk; ++b) {

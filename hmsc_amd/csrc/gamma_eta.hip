@@ -809,11 +809,11 @@ static void launch_gamma_eta_blocked(State& s, const GEArgs& a, hipStream_t st) 
   ge_b_m_kernel<<<ge_blocks(NN), 256, 0, st>>>(a);
   // RM = chol(M); v = M^-1 (mb10 - mb20)
   dense_potrf_lower(st, M, N, N, ws2, a.fail);
-  dense_trsv_lower(st, M, N, N, v, 0, ws2);
-  dense_trsv_lower(st, M, N, N, v, 1, ws2);
+  dense_trsv_lower(st, M, N, N, v, 0, ws2, 0, s.trsv_sync);
+  dense_trsv_lower(st, M, N, N, v, 1, ws2, 0, s.trsv_sync);
   ge_b_wv_kernel<<<ge_blocks(64 * (size_t)N), 256, 0, st>>>(a);  // one wave per output
   ge_b_mb_kernel<<<ge_blocks(64 * (size_t)N), 256, 0, st>>>(a);
-  dense_trsv_lower(st, M, N, N, xi, 1, ws2);  // backsolve(RM, rnorm(nc ns))  (:66)
+  dense_trsv_lower(st, M, N, N, xi, 1, ws2, 0, s.trsv_sync);  // backsolve(RM, rnorm(nc ns))  (:66)
   ge_b_gamma_kernel<<<1, 1024, 0, st>>>(a);
   ge_b_eta_kernel<<<ge_blocks(64 * (size_t)(obs ? a.ny : a.np)), 256, 0, st>>>(a);
   HIP_OK(hipGetLastError());
@@ -1144,9 +1144,9 @@ static void launch_gamma_eta_spatial(State& s, const GESArgs& sa, hipStream_t st
   ges_grid_kernel<4><<<grid((size_t)D2 + 1), 256, 0, st>>>(sa);
   ges_grid_kernel<5><<<grid((size_t)D2 * D2), 256, 0, st>>>(sa);
   dense_potrf_lower(st, w + o.iG, D2, D2, ws2, a.fail);
-  dense_trsv_lower(st, w + o.iG, D2, D2, w + o.b, 0, ws2);
+  dense_trsv_lower(st, w + o.iG, D2, D2, w + o.b, 0, ws2, 0, s.trsv_sync);
   ges_grid_kernel<6><<<grid(D2), 256, 0, st>>>(sa);
-  dense_trsv_lower(st, w + o.iG, D2, D2, w + o.b, 1, ws2);
+  dense_trsv_lower(st, w + o.iG, D2, D2, w + o.b, 1, ws2, 0, s.trsv_sync);
   ges_grid_kernel<7><<<grid(D2), 256, 0, st>>>(sa);
   HIP_OK(hipGetLastError());
 }

@@ -740,9 +740,9 @@ static void launch_eta_nngp(State& s, int r, uint32_t iter) {
     ProfScope pc(s, PROF_CHOL);
     dense_potrf_lower(s.stream, Q, N, N, ws, s.dev_flags, n.bw);
   }
-  dense_trsv_lower(s.stream, Q, N, N, x, 0, ws, n.bw);   // backsolve(R, fS, transpose = TRUE)
+  dense_trsv_lower(s.stream, Q, N, N, x, 0, ws, n.bw, s.trsv_sync);   // backsolve(R, fS, transpose = TRUE)
   nngp_perm_kernel<<<g1, 256, 0, s.stream>>>(a, n, rhs, x, 1);
-  dense_trsv_lower(s.stream, Q, N, N, x, 1, ws, n.bw);   // backsolve(R, tmp2)
+  dense_trsv_lower(s.stream, Q, N, N, x, 1, ws, n.bw, s.trsv_sync);   // backsolve(R, tmp2)
   nngp_perm_kernel<<<g1, 256, 0, s.stream>>>(a, n, rhs, x, 2);
   HIP_OK(hipGetLastError());
 }
@@ -950,9 +950,9 @@ void launch_eta_spatial(State& s, int r, uint32_t iter) {
     ProfScope pc(s, PROF_CHOL);
     dense_potrf_lower(s.stream, U, N, N, ws, s.dev_flags);
   }
-  dense_trsv_lower(s.stream, U, N, N, rhs, 0, ws);   // backsolve(R, fS, transpose = TRUE)
+  dense_trsv_lower(s.stream, U, N, N, rhs, 0, ws, 0, s.trsv_sync);   // backsolve(R, fS, transpose = TRUE)
   sp_noise_kernel<<<g1, 256, 0, s.stream>>>(a, rhs);
-  dense_trsv_lower(s.stream, U, N, N, rhs, 1, ws);   // backsolve(R, tmp2)
+  dense_trsv_lower(s.stream, U, N, N, rhs, 1, ws, 0, s.trsv_sync);   // backsolve(R, tmp2)
   sp_store_kernel<<<g1, 256, 0, s.stream>>>(a, rhs);
   HIP_OK(hipGetLastError());
 }

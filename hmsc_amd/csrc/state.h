@@ -180,7 +180,8 @@ struct State {
   double* host_rec = nullptr;    // pinned host ring (ring_slots slots)
   uint64_t* copied_host = nullptr;  // fine-grained pinned counter: samples whose D2H copy landed
   uint64_t* copied_dev = nullptr;   // its device address
-  std::shared_ptr<struct UnpackPool> unpack_pool;  // record-unpack workers (capi.cpp), kept across runs
+  std::shared_ptr<struct UnpackPool> unpack_pool;
+  int* trsv_sync = nullptr;  // dense_trsv_lower's sync-free handshake (2 + 4096 ints)  // record-unpack workers (capi.cpp), kept across runs
 
   // per-sweep hipGraph (single rank, no updateNf): captured once, replayed every sweep; the
   // kernels read the Philox sweep counter from d_iter, which the graph's first node advances
@@ -304,7 +305,10 @@ void launch_side_fused(State& s, uint32_t iter);
 // bw > 0: A is banded (A[i, j] = 0 for i - j > bw, entries outside the band zero on entry);
 // the factor keeps the band, and only the band's tiles are touched (n bw^2 work instead of n^3)
 void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, int* info, int bw = 0);
-void dense_trsv_lower(hipStream_t st, const double* L, int n, int lda, double* x, int trans, double* ws, int bw = 0);
+// sync: the State's trsv_sync (2 + 4096 ints, zeroed) for the one-launch sync-free solve, or
+// null for one launch per 64-block
+void dense_trsv_lower(hipStream_t st, const double* L, int n, int lda, double* x, int trans, double* ws, int bw = 0,
+                      int* sync = nullptr);
 void dense_trtri_lower(hipStream_t st, const double* L, int ldl, int n, double* M, int ldm, double* dinv,
                        bool have_dinv);
 // workspace of dense_potrf_lower + dense_trsv_lower: the 64 x 64 diagonal-block inverses, then n
