@@ -331,7 +331,13 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(double* A, int lda, int
 // ---------------------------------------------------------------------------------------
 // 3. trailing update of the lower tiles: A_IJ -= P_I P_J^T  (P = the just-finished panel)
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void chol_update_kernel(double* A, int lda, int n, int k0) {
+// DIAG: workgroup 0 -- the next diagonal block's tile, (0, 0) -- then factors that block
+// (diag_body on its LDS, the panels' buffers reused) while the other workgroups finish the
+// trailing update, instead of a separate one-workgroup launch on the critical path per
+// panel.  Two workgroups per CU either way (LDS), so the diagonal code may take 256 VGPRs.
+template <bool DIAG>
+__global__ __launch_bounds__(256, 2) void chol_update_kernel(double* A, int lda, int n, int k0, double* Linv_next,
+                                                             int* info) {
   __shared__ double PI[DB * DLD];
   __shared__ double PJ[DB * DLD];
   const int nb = min(DB, n - k0), base = k0 + nb;
@@ -365,31 +371,64 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* A, int lda, in
         cv[a][b][q] = live ? A[(size_t)(I0 + r) + (size_t)lda * (J0 + c)] : 0.0;
       }
   __syncthreads();
-  if (!live) return;
+  const bool diag_next = DIAG && blockIdx.x == 0;  // tile (0, 0): the next diagonal block
+  if (!live && !diag_next) return;
   d4 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+  if (live) {
 #pragma unroll 4
-  for (int s = 0; s < DB / 4; ++s) {
-    const int k = 4 * s + lk;
-    const double bI0 = PI[qr + lm + DLD * k], bI1 = PI[qr + 16 + lm + DLD * k];
-    const double aJ0 = PJ[qc + lm + DLD * k], aJ1 = PJ[qc + 16 + lm + DLD * k];
-    acc[0][0] = mfma_f64(aJ0, bI0, acc[0][0]);
-    acc[0][1] = mfma_f64(aJ0, bI1, acc[0][1]);
-    acc[1][0] = mfma_f64(aJ1, bI0, acc[1][0]);
-    acc[1][1] = mfma_f64(aJ1, bI1, acc[1][1]);
+    for (int s = 0; s < DB / 4; ++s) {
+      const int k = 4 * s + lk;
+      const double bI0 = PI[qr + lm + DLD * k], bI1 = PI[qr + 16 + lm + DLD * k];
+      const double aJ0 = PJ[qc + lm + DLD * k], aJ1 = PJ[qc + 16 + lm + DLD * k];
+      acc[0][0] = mfma_f64(aJ0, bI0, acc[0][0]);
+      acc[0][1] = mfma_f64(aJ0, bI1, acc[0][1]);
+      acc[1][0] = mfma_f64(aJ1, bI0, acc[1][0]);
+      acc[1][1] = mfma_f64(aJ1, bI1, acc[1][1]);
+    }
   }
+  if (!diag_next) {
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < 2; ++b)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int c = qc + 16 * a + lk + 4 * q, r = qr + 16 * b + lm;
-        if (r < rowsI && c < rowsJ) A[(size_t)(I0 + r) + (size_t)lda * (J0 + c)] = cv[a][b][q] - acc[a][b][q];
-      }
+        for (int q = 0; q < 4; ++q) {
+          const int c = qc + 16 * a + lk + 4 * q, r = qr + 16 * b + lm;
+          if (r < rowsI && c < rowsJ) A[(size_t)(I0 + r) + (size_t)lda * (J0 + c)] = cv[a][b][q] - acc[a][b][q];
+        }
+    return;
+  }
+  if constexpr (DIAG) {
+    // the updated block into T (= PI: lower triangle, zeros above, identity past nb), I (= PJ)
+    // zeroed, then the diagonal factorization of block base (writes L into A, Linv_next)
+    __shared__ double S[4][16 * 17];
+    __syncthreads();  // every wave's panel reads done
+    double* T = PI;
+    double* I = PJ;
+#pragma unroll
+    for (int u = 0; u < DB * DB / 256; ++u) {
+      const int p = t + 256 * u, r = p & 63, c = p >> 6;
+      T[r + DLD * c] = (r == c && r >= rowsI) ? 1.0 : 0.0;
+      I[r + DLD * c] = 0.0;
+    }
+    __syncthreads();
+    if (live)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int c = qc + 16 * a + lk + 4 * q, r = qr + 16 * b + lm;
+            if (r < rowsI && c < rowsJ && r >= c) T[r + DLD * c] = cv[a][b][q] - acc[a][b][q];
+          }
+    __syncthreads();
+    diag_body(T, I, S, A, lda, n, base, Linv_next, info);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -894,14 +933,25 @@ void dense_lauum_lower(hipStream_t st, const double* M, int ldm, int n, double* 
 // at the tiles covering rows k0 + DB .. k0 + DB + bw (the update's tile map depends on the
 // launch size only: a smaller grid is the band's triangle of tiles).
 void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, int* info, int bw) {
+  static const bool fuse_diag = [] {  // HMSC_NO_CHOL_DIAG_FUSION=1: the diagonal block as its own launch
+    const char* e = std::getenv("HMSC_NO_CHOL_DIAG_FUSION");
+    return !(e && e[0] && e[0] != '0');
+  }();
+  bool diag_done = false;  // block k0 already factored by the previous trailing update
   for (int k0 = 0; k0 < n; k0 += DB) {
     double* Linv = ws + (size_t)(k0 / DB) * DB * DB;
-    chol_diag_kernel<<<1, 256, 0, st>>>(A, lda, n, k0, Linv, info);
+    if (!diag_done) chol_diag_kernel<<<1, 256, 0, st>>>(A, lda, n, k0, Linv, info);
+    diag_done = false;
     const int rem = bw > 0 ? std::min(n - (k0 + DB), bw) : n - (k0 + DB);
     if (rem > 0) {
       const int nt = (rem + DB - 1) / DB;
       chol_panel_kernel<<<nt, 256, 0, st>>>(A, lda, n, k0, Linv);
-      chol_update_kernel<<<nt * (nt + 1) / 2, 256, 0, st>>>(A, lda, n, k0);
+      if (fuse_diag) {
+        chol_update_kernel<true><<<nt * (nt + 1) / 2, 256, 0, st>>>(A, lda, n, k0, Linv + DB * DB, info);
+        diag_done = true;
+      } else {
+        chol_update_kernel<false><<<nt * (nt + 1) / 2, 256, 0, st>>>(A, lda, n, k0, nullptr, nullptr);
+      }
     }
   }
   HIP_OK(hipGetLastError());
