@@ -102,14 +102,17 @@ static constexpr size_t RING_BYTES_MAX = (size_t)256 << 20;
 // gpurun_out/s4_phy.err with HMSC_SEGV_DIAG=1), a hang for config 4's 512-node 64-sweep graph
 // (s5_g64.err), while 256 / 288-node graphs (config 4 at 32 sweeps per graph) and the same
 // phylo run without graphs (HMSC_NO_GRAPH=1) profile cleanly, and none of these graphs fail
-// without the profiler.  Under rocprofv3 (it exports ROCPROF_OUTPUT_PATH to the program)
-// graphs are therefore kept to 256 nodes and sweeps that need more run eagerly; otherwise
-// the cap only bounds instantiation cost.  HMSC_GRAPH_MAX_NODES overrides either.
+// without the profiler.  Node count is not the whole story: after round 3's one-launch
+// triangular solves config 3's one-sweep graph has 235 nodes and still faults under the
+// profiler (gpurun_out/r03_s28_phyprof.err), while config 4's 256-node graphs do not.  Under
+// rocprofv3 (it exports ROCPROF_OUTPUT_PATH to the program) graphs are therefore kept to 128
+// nodes and sweeps that need more run eagerly (config 3 then profiles cleanly); otherwise the
+// cap only bounds instantiation cost.  HMSC_GRAPH_MAX_NODES overrides either.
 static size_t graph_max_nodes() {
   static const size_t cap = [] {
     if (const char* e = std::getenv("HMSC_GRAPH_MAX_NODES"))
       if (e[0]) return (size_t)std::max(1L, std::atol(e));
-    return std::getenv("ROCPROF_OUTPUT_PATH") ? (size_t)256 : (size_t)8192;
+    return std::getenv("ROCPROF_OUTPUT_PATH") ? (size_t)128 : (size_t)8192;
   }();
   return cap;
 }
