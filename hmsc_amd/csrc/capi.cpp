@@ -1450,8 +1450,16 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
   if (pool) {
     pool->start([&](int w) {
       try {
+        // first touch of this worker's next samples' pages ahead of their data: a replay's
+        // samples arrive together (one copy + flag per replay), so touching only the sample
+        // being waited for left the later ones to fault inside their unpack
+        constexpr int LOOKAHEAD = 4;
+        int touched = w - W;
         for (int k = w; k < samples; k += W) {
-          if (__atomic_load_n(copied, __ATOMIC_ACQUIRE) <= (uint64_t)k) pretouch_record(s, k, rec);
+          while (touched + W < samples && touched + W <= k + W * LOOKAHEAD) {
+            touched += W;
+            pretouch_record(s, touched, rec);
+          }
           // spin (yielding) rather than sleep: a timed sleep oversleeps by the kernel's timer
           // slack (~50 us), which at the end of a short run is most of the unpack tail
           for (int spin = 0; __atomic_load_n(copied, __ATOMIC_ACQUIRE) <= (uint64_t)k; ++spin) {
@@ -1537,12 +1545,17 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
         if (klast >= 0) {
           HIP_OK(hipEventRecord(s.ev_graph, s.stream));
           HIP_OK(hipStreamWaitEvent(s.copy_stream, s.ev_graph, 0));
-          // a flag after every sample's copy: the unpack of sample k starts as soon as its
-          // copy lands, not after the whole replay's copies
-          for (int k = kfirst; k <= klast; ++k) {
-            copy_out(k);
-            launch_copied_flag(s, (uint64_t)k + 1);
+          // the replay's samples in one copy per contiguous run of ring slots (at most two),
+          // then one flag: a copy + flag per sample cost ~48 us of copy-engine and dispatch
+          // time each (26 us of transfer), so a 32-sweep replay's copies backed up behind the
+          // next replays and trailed the run's last sweep (rocprofv3 --memory-copy-trace)
+          for (int k = kfirst; k <= klast;) {
+            const int slot = k % s.ring_slots, nk = std::min(klast - k + 1, s.ring_slots - slot);
+            HIP_OK(hipMemcpyAsync(s.host_rec + s.slot_doubles * slot, s.ring + s.slot_doubles * slot,
+                                  sizeof(double) * s.slot_doubles * nk, hipMemcpyDeviceToHost, s.copy_stream));
+            k += nk;
           }
+          launch_copied_flag(s, (uint64_t)klast + 1);
         }
       }
     }
