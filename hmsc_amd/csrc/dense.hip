@@ -267,7 +267,9 @@ __device__ inline void diag_body(double* T, double* I, double (*S)[16 * 17], dou
   DENSE_STAMP(111);
 }
 
-__global__ __launch_bounds__(256) void chol_diag_kernel(double* A, int lda, int n, int k0, double* Linv, int* info) {
+__global__ __launch_bounds__(256) void chol_diag_kernel(double* A, int lda, int n, int k0, double* Linv, int* info,
+                                                        int* pflag_reset = nullptr) {
+  if (pflag_reset && threadIdx.x == 0) *pflag_reset = 0;  // a factorization's first launch: its steps start at 1
   __shared__ double T[DB * DLD];  // the block; its lower triangle becomes L
   __shared__ double I[DB * DLD];  // L^-1 (lower)
   __shared__ double S[4][16 * 17];  // per-wave 16 x 16 scratch (ld 17)
@@ -335,9 +337,13 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(double* A, int lda, int
 // (diag_body on its LDS, the panels' buffers reused) while the other workgroups finish the
 // trailing update, instead of a separate one-workgroup launch on the critical path per
 // panel.  Two workgroups per CU either way (LDS), so the diagonal code may take 256 VGPRs.
+// With pflag (dense, unbanded: the next panel is exactly the tiles (i, 0), i >= 1, of this
+// update) those workgroups also apply the next panel step to their tile -- tile Linv_next^T,
+// once workgroup 0 has raised pflag = step + 1 with Linv_next written -- so the next step
+// needs no panel launch either.
 template <bool DIAG>
 __global__ __launch_bounds__(256, 2) void chol_update_kernel(double* A, int lda, int n, int k0, double* Linv_next,
-                                                             int* info) {
+                                                             int* info, int* pflag) {
   __shared__ double PI[DB * DLD];
   __shared__ double PJ[DB * DLD];
   const int nb = min(DB, n - k0), base = k0 + nb;
@@ -372,6 +378,7 @@ __global__ __launch_bounds__(256, 2) void chol_update_kernel(double* A, int lda,
       }
   __syncthreads();
   const bool diag_next = DIAG && blockIdx.x == 0;  // tile (0, 0): the next diagonal block
+  const bool panel_next = DIAG && pflag && tj == 0 && ti >= 1;  // a tile of the next panel
   if (!live && !diag_next) return;
   d4 acc[2][2];
 #pragma unroll
@@ -390,7 +397,7 @@ __global__ __launch_bounds__(256, 2) void chol_update_kernel(double* A, int lda,
       acc[1][1] = mfma_f64(aJ1, bI1, acc[1][1]);
     }
   }
-  if (!diag_next) {
+  if (!diag_next && !panel_next) {
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -403,6 +410,62 @@ __global__ __launch_bounds__(256, 2) void chol_update_kernel(double* A, int lda,
     return;
   }
   if constexpr (DIAG) {
+    if (panel_next) {
+      // the updated tile into P (= PI, P[r][k] at r + DLD k), then -- once the next diagonal
+      // block's inverse is published -- Linv_next (coherent loads: written by workgroup 0,
+      // possibly on another XCD) into Li (= PJ) and out = P Linv_next^T as in chol_panel_kernel
+      __syncthreads();  // every wave's reads of the staged panels done
+      double* P = PI;
+      double* Li = PJ;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int c = qc + 16 * a + lk + 4 * q, r = qr + 16 * b + lm;
+            P[r + DLD * c] = (r < rowsI && c < rowsJ) ? cv[a][b][q] - acc[a][b][q] : 0.0;
+          }
+      const int step = k0 / DB + 1;
+      if (t == 0)
+        for (int spin = 0; __hip_atomic_load(pflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != step; ++spin) {
+          if (spin > (1 << 24)) {  // a broken handshake reports, never hangs
+            atomicExch(info, 1);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      __syncthreads();
+      {
+        double li[DB * DB / 256];
+#pragma unroll
+        for (int u = 0; u < DB * DB / 256; ++u)
+          li[u] = __longlong_as_double((long long)__hip_atomic_load(
+              (const unsigned long long*)(Linv_next + t + 256 * u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+#pragma unroll
+        for (int u = 0; u < DB * DB / 256; ++u) Li[((t + 256 * u) & 63) + DLD * ((t + 256 * u) >> 6)] = li[u];
+      }
+      __syncthreads();
+      d4 pacc[4];
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) pacc[ct] = d4{0.0, 0.0, 0.0, 0.0};
+      const int r = 16 * w + lm;
+#pragma unroll 4
+      for (int s = 0; s < DB / 4; ++s) {
+        const int k = 4 * s + lk;
+        const double bv = P[r + DLD * k];
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) pacc[ct] = mfma_f64(Li[16 * ct + lm + DLD * k], bv, pacc[ct]);
+      }
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = 16 * ct + lk + 4 * q;
+          if (r < rowsI && c < rowsJ) A[(size_t)(I0 + r) + (size_t)lda * (base + c)] = pacc[ct][q];
+        }
+      return;
+    }
     // the updated block into T (= PI: lower triangle, zeros above, identity past nb), I (= PJ)
     // zeroed, then the diagonal factorization of block base (writes L into A, Linv_next)
     __shared__ double S[4][16 * 17];
@@ -428,6 +491,10 @@ __global__ __launch_bounds__(256, 2) void chol_update_kernel(double* A, int lda,
           }
     __syncthreads();
     diag_body(T, I, S, A, lda, n, base, Linv_next, info);
+    if (pflag) {  // Linv_next written (diag_body's stores precede the barrier): publish it
+      __syncthreads();
+      if (t == 0) __hip_atomic_store(pflag, k0 / DB + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -937,21 +1004,32 @@ void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, in
     const char* e = std::getenv("HMSC_NO_CHOL_DIAG_FUSION");
     return !(e && e[0] && e[0] != '0');
   }();
-  bool diag_done = false;  // block k0 already factored by the previous trailing update
+  static const bool fuse_panel = [] {  // HMSC_CHOL_PANEL_FUSION=1: the next panel inside the update (opt-in)
+    const char* e = std::getenv("HMSC_CHOL_PANEL_FUSION");
+    return e && e[0] && e[0] != '0';
+  }();
+  // the panel handshake flag: past the workspace's diagonal-block inverses and solve vector
+  // (dense_ws_doubles' slack), reset by the factorization's first launch
+  const int nbk = (n + DB - 1) / DB;
+  int* pflag = (fuse_diag && fuse_panel && bw <= 0) ? (int*)(ws + (size_t)nbk * DB * DB + n + 8) : nullptr;
+  bool diag_done = false, panel_done = false;  // block k0 / panel k0 done by the previous trailing update
   for (int k0 = 0; k0 < n; k0 += DB) {
     double* Linv = ws + (size_t)(k0 / DB) * DB * DB;
-    if (!diag_done) chol_diag_kernel<<<1, 256, 0, st>>>(A, lda, n, k0, Linv, info);
-    diag_done = false;
+    if (!diag_done) chol_diag_kernel<<<1, 256, 0, st>>>(A, lda, n, k0, Linv, info, k0 == 0 ? pflag : nullptr);
     const int rem = bw > 0 ? std::min(n - (k0 + DB), bw) : n - (k0 + DB);
     if (rem > 0) {
       const int nt = (rem + DB - 1) / DB;
-      chol_panel_kernel<<<nt, 256, 0, st>>>(A, lda, n, k0, Linv);
+      if (!panel_done) chol_panel_kernel<<<nt, 256, 0, st>>>(A, lda, n, k0, Linv);
       if (fuse_diag) {
-        chol_update_kernel<true><<<nt * (nt + 1) / 2, 256, 0, st>>>(A, lda, n, k0, Linv + DB * DB, info);
+        chol_update_kernel<true><<<nt * (nt + 1) / 2, 256, 0, st>>>(A, lda, n, k0, Linv + DB * DB, info, pflag);
         diag_done = true;
+        panel_done = pflag != nullptr;
       } else {
-        chol_update_kernel<false><<<nt * (nt + 1) / 2, 256, 0, st>>>(A, lda, n, k0, nullptr, nullptr);
+        chol_update_kernel<false><<<nt * (nt + 1) / 2, 256, 0, st>>>(A, lda, n, k0, nullptr, nullptr, nullptr);
+        diag_done = panel_done = false;
       }
+    } else {
+      diag_done = panel_done = false;
     }
   }
   HIP_OK(hipGetLastError());
