@@ -1004,9 +1004,9 @@ void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, in
     const char* e = std::getenv("HMSC_NO_CHOL_DIAG_FUSION");
     return !(e && e[0] && e[0] != '0');
   }();
-  static const bool fuse_panel = [] {  // HMSC_CHOL_PANEL_FUSION=1: the next panel inside the update (opt-in)
-    const char* e = std::getenv("HMSC_CHOL_PANEL_FUSION");
-    return e && e[0] && e[0] != '0';
+  static const bool fuse_panel = [] {  // HMSC_NO_CHOL_PANEL_FUSION=1: the panel as its own launch
+    const char* e = std::getenv("HMSC_NO_CHOL_PANEL_FUSION");
+    return !(e && e[0] && e[0] != '0');
   }();
   // the panel handshake flag: past the workspace's diagonal-block inverses and solve vector
   // (dense_ws_doubles' slack), reset by the factorization's first launch
