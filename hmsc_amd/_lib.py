@@ -79,8 +79,10 @@ ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int64, C.c_void_p
 
 EXPORTS = ["hmsc_last_error", "hmsc_device_count", "hmsc_create", "hmsc_create_sharded", "hmsc_comm_unique_id",
            "hmsc_shard_range", "hmsc_create_sharded_host", "hmsc_dense_chol_solve", "hmsc_spatial_full_grid",
-           "hmsc_destroy", "hmsc_init_state", "hmsc_init_z", "hmsc_set_state", "hmsc_get_state", "hmsc_get_nf", "hmsc_sweep",
+           "hmsc_destroy", "hmsc_init_state", "hmsc_init_z", "hmsc_set_state", "hmsc_get_state", "hmsc_get_nf", "hmsc_get_nf_cap",
+           "hmsc_sweep",
            "hmsc_update", "hmsc_set_noise_mode", "hmsc_run", "hmsc_run_verbose", "hmsc_sync", "hmsc_debug_get",
+           "hmsc_debug_poison",
            "hmsc_profile", "hmsc_profile_get", "hmsc_kernel_timing", "hmsc_kernel_timing_get", "hmsc_predict",
            "hmsc_prepare_graphs", "hmsc_post_omega", "hmsc_variance_partitioning", "hmsc_effective_size"]
 
@@ -112,6 +114,7 @@ def lib():
     L.hmsc_set_state.argtypes = [C.c_void_p, C.POINTER(hmsc_params)]
     L.hmsc_get_state.argtypes = [C.c_void_p, C.POINTER(hmsc_params)]
     L.hmsc_get_nf.argtypes = [C.c_void_p, ip]
+    L.hmsc_get_nf_cap.argtypes = [C.c_void_p, ip]
     L.hmsc_sweep.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
     L.hmsc_update.argtypes = [C.c_void_p, C.c_uint32, C.c_int32]
     L.hmsc_set_noise_mode.argtypes = [C.c_void_p, C.c_int32]
@@ -120,6 +123,7 @@ def lib():
                                    C.c_int32, C.POINTER(hmsc_record)]
     L.hmsc_sync.argtypes = [C.c_void_p]
     L.hmsc_debug_get.argtypes = [C.c_void_p, C.c_char_p, dp, C.c_int64]
+    L.hmsc_debug_poison.argtypes = [C.c_void_p, C.c_char_p]
     L.hmsc_profile.argtypes = [C.c_void_p, C.c_int32]
     L.hmsc_profile_get.argtypes = [C.c_void_p, C.c_int32, dp, ip]
     L.hmsc_kernel_timing.argtypes = [C.c_void_p, C.c_int32]

@@ -261,6 +261,14 @@ static T* dalloc(size_t n) {
   return p;
 }
 
+double* device_realloc_doubles(State& s, double* old, size_t n) {
+  std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
+  DeviceGuard dg(s.device);
+  HIP_OK(hipStreamSynchronize(s.stream));
+  if (old) HIP_OK(hipFree(old));
+  return dalloc<double>(n);
+}
+
 template <class T>
 static T* dupload(const T* h, size_t n) {
   T* p = dalloc<T>(n);
@@ -306,7 +314,9 @@ static void setup_phylo(State& s, const hmsc_model* m) {
                "phylogeny: pass the eigendecomposition of C (C_vectors, C_values)");
   HMSC_REQUIRE(m->nrho > 0 && m->rhopw != nullptr, "phylogeny: rhopw grid missing");
   HMSC_REQUIRE(s.nranks == 1, "phylogeny couples all species: species-sharded chains are not supported");
-  HMSC_REQUIRE(!s.has_na, "phylogeny with NA in Y is not supported in this build");
+  // NA in Y: R's phylogeny branch factors kronecker(XEtaTXEta, diag(iSigma)) + P over the
+  // imputed Z with no per-species masking (R/updateBetaLambda.R:124-146), so the device's
+  // phylogeny system takes the full Gram and an unmasked XZ (zdraw.hip mask_na = 0)
   s.phylo = true;
   s.nrho = m->nrho;
   std::vector<double> winv((size_t)s.nrho * ns), rbase(s.nrho);
@@ -442,13 +452,26 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
     L.b2 = m->b2[r];
     sum_nfmax += L.nfmax;
   }
+  // K = nc + sum(nf) <= 64 is this build's kernel limit (one wave per species row set in
+  // updateBetaLambda, 16-row MFMA blocks of updateZ).  R's default nfMax = Inf becomes ns
+  // (R/Hmsc.R:554), so a default model with many species asks for more factors than the
+  // device holds: every level's buffers and record slots then hold nfcap = min(nfMax, 64 - nc
+  // - the other levels' nfMin) factors (hmsc_get_nf_cap; the Python wrapper warns), and the
+  // chain stops with an explicit error only if updateNf actually has to grow a level past it
+  // (MGP shrinkage keeps the adapted nf far below that in practice).
+  HMSC_REQUIRE(nc + [&] { int v = 0; for (int r = 0; r < s.nr; ++r) v += s.lev[r].nfmin; return v; }() <= 64,
+               "nc + sum(nfMin) exceeds 64: this build's limit is K = nc + sum(nf) <= 64");
   s.Kmax = std::min(nc + sum_nfmax, 64);
   s.NFmax = s.Kmax - nc;
   s.refresh_dims();
-  HMSC_REQUIRE(s.K <= s.Kmax, "nc + sum(nfMin) exceeds 64: not supported in this build");
   for (int r = 0; r < s.nr; ++r) {
     Level& L = s.lev[r];
-    const int nfcap = std::min(L.nfmax, s.NFmax);
+    int others = 0;
+    for (int q = 0; q < s.nr; ++q)
+      if (q != r) others += s.lev[q].nfmin;
+    L.nfcap = std::max(L.nfmin, std::min(L.nfmax, s.NFmax - others));
+    L.nf_alloc = std::max(1, L.nf);
+    const int nfcap = L.nfcap;
     L.Eta = dalloc<double>((size_t)L.np * nfcap);
     std::vector<int> pi(ny), cnt(L.np + 1, 0), rows(ny);
     for (int i = 0; i < ny; ++i) {
@@ -467,7 +490,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
     L.Pi = dupload(pi.data(), ny);
     L.unit_ptr = dupload(cnt.data(), L.np + 1);
     L.unit_rows = dupload(rows.data(), ny);
-    std::vector<int> alpha(std::max(1, L.nfmax > 0 ? std::min(L.nfmax, s.NFmax) : 1), 1);
+    std::vector<int> alpha(std::max(1, L.nfcap), 1);
     L.Alpha = dupload(alpha.data(), alpha.size());
     std::vector<double> alphad(alpha.size(), 1.0);  // Alpha = rep(1, nf) (R/computeInitialParameters.R:216-221)
     L.AlphaD = dupload(alphad.data(), alphad.size());
@@ -695,19 +718,18 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.allreduce_buf = dalloc<double>((size_t)nc * nc + 2 * N + nfm * nt + nfm + 64);
   s.dev_flags = dalloc<int>(16);
   s.gbl_sync = dalloc<int>(4);  // dalloc zero-fills
-  s.trsv_sync = dalloc<int>(2 + 4096);
+  s.trsv_sync = dalloc<int>(DENSE_SYNC_INTS);
   s.d_iters = dalloc<uint32_t>(64);  // graph_sweeps <= 64
   s.d_iter = s.d_iters;
   if (s.mask & HMSC_UP_GAMMAETA) {  // updateGammaEta: dense (nc ns)^2 / joint spatial systems
     HMSC_REQUIRE(s.nranks == 1, "updateGammaEta cannot run on a species-sharded chain: pass updater GammaEta=FALSE");
     HMSC_REQUIRE((size_t)nc * s.ns <= 32768, "updateGammaEta: nc * ns must be <= 32768 (dense (nc ns)^2 systems, 4 x 8.6 GB)");
+    // sized for the levels' nf now (nfMin); launch_gamma_eta grows it if updateNf adds factors
     for (int r = 0; r < s.nr; ++r)
-    {
-      HMSC_REQUIRE(s.lev[r].nfmax <= 16, "updateGammaEta: nfMax must be <= 16 in this build");
-      HMSC_REQUIRE(!s.lev[r].spatial || (size_t)nc * s.nt + (size_t)s.lev[r].np * s.lev[r].nfmax <= 32768,
-                   "updateGammaEta, spatial level: nc nt + np nfMax must be <= 32768 (dense joint system, 8.6 GB)");
-    }
-    s.geWork = dalloc<double>(gamma_eta_work_doubles(s));
+      HMSC_REQUIRE(!s.lev[r].spatial || (size_t)nc * s.nt + (size_t)s.lev[r].np * s.lev[r].nf <= 32768,
+                   "updateGammaEta, spatial level: nc nt + np nf must be <= 32768 (dense joint system, 8.6 GB)");
+    s.geWork_doubles = gamma_eta_work_doubles(s);
+    s.geWork = dalloc<double>(s.geWork_doubles);
   }
   {
     const char* g = getenv("HMSC_GRAPH_SWEEPS");
@@ -796,11 +818,43 @@ void join_side(State& s) {
   s.side_pending = 0;
 }
 
+// ---------------------------- device error flags ----------------------------
+// Every failure a kernel can detect is a device word the host reads once the work is done
+// (nothing throws inside a launch): a Cholesky factor that is not positive definite
+// (dev_flags[0] the per-species / per-unit / GammaEta / spatial systems, [1] updateGamma2,
+// [2] the phylogeny BetaLambda system), and every bounded in-launch handshake that timed out
+// (the Gamma2 / BetaLambda launch's gbl_sync[3]; the dense solver's error word, whose bits
+// name the wait, state.h HsErr).  A timed-out wait lets its launch drain on stale data, so a
+// run that saw one must fail, never return its samples.  Called with the streams idle.
+static void check_device_flags(State& s) {
+  int flag[16] = {0};
+  copy_sync(flag, s.dev_flags, sizeof(flag), hipMemcpyDeviceToHost, s.stream);
+  int gsync[4] = {0, 0, 0, 0};
+  copy_sync(gsync, s.gbl_sync, sizeof(gsync), hipMemcpyDeviceToHost, s.stream);
+  int hs = 0;
+  copy_sync(&hs, s.trsv_sync + DENSE_SYNC_ERR, sizeof(int), hipMemcpyDeviceToHost, s.stream);
+  if (hs != 0) {
+    std::string what;
+    if (hs & HS_ERR_TRSV_FLAG) what += " [sync-free triangular solve: a block flag never came up]";
+    if (hs & HS_ERR_TRSV_TICKET) what += " [sync-free triangular solve: corrupt block ticket]";
+    if (hs & HS_ERR_CHOL_PANEL) what += " [blocked Cholesky: the fused panel step's diagonal-inverse flag never came up]";
+    throw HmscError(-5, "internal: an in-launch handshake of the blocked dense solver timed out; the sweep used a "
+                        "half-solved system and its draws are invalid" + what);
+  }
+  if (gsync[3] != 0)
+    throw HmscError(-5, "internal: the Gamma2 / BetaLambda in-launch handshake timed out; the sweep's draws are invalid");
+  if (flag[2] != 0)
+    throw HmscError(-1, "a Cholesky factorisation failed in the phylogeny BetaLambda system (matrix not positive definite)");
+  if (flag[1] != 0) throw HmscError(-1, "a Cholesky factorisation failed in updateGamma2 (matrix not positive definite)");
+  if (flag[0] != 0) throw HmscError(-1, "a Cholesky factorisation failed (matrix not positive definite)");
+}
+
 // ---------------------------- state get / set ----------------------------
 static void get_state(State& s, hmsc_params* p) {
   DeviceGuard dg(s.device);
   join_side(s);
   HIP_OK(hipStreamSynchronize(s.stream));
+  check_device_flags(s);
   const int K = s.K, nsl = s.nsl, nc = s.nc;
   std::vector<double> BL((size_t)K * nsl), Psi((size_t)s.NF * nsl), Delta(std::max(1, s.NF));
   d2h(BL.data(), s.BL, BL.size(), s.stream);
@@ -854,12 +908,12 @@ static void set_state(State& s, const hmsc_params* p) {
   HIP_OK(hipStreamSynchronize(s.stream));
   for (int r = 0; r < s.nr; ++r) {
     if (p->nf[r] > 0) {
-      HMSC_REQUIRE(p->nf[r] <= std::min(s.lev[r].nfmax, s.NFmax), "set_state: nf exceeds allocation");
+      HMSC_REQUIRE(p->nf[r] <= s.lev[r].nfcap, "set_state: nf exceeds the level's factor capacity (hmsc_get_nf_cap)");
       s.lev[r].nf = p->nf[r];
     }
   }
   s.refresh_dims();
-  HMSC_REQUIRE(s.K <= s.Kmax, "set_state: K exceeds 64");
+  HMSC_REQUIRE(s.K <= s.Kmax, "set_state: K = nc + sum(nf) exceeds this build's limit of 64");
   const int K = s.K;
   std::vector<double> BL((size_t)K * nsl, 0.0), Psi((size_t)std::max(1, s.NF) * nsl, 1.0), Delta(std::max(1, s.NF), 1.0);
   for (int j = 0; j < nsl; ++j)
@@ -949,14 +1003,18 @@ static void update_nf(State& s, int r, uint32_t iter) {
     if (prop >= 1.0) ++num_red;
     if (!(prop < 0.995)) all_lt = false;
   }
-  const int nfcap = std::min(L.nfmax, s.NFmax);
+  const int nfcap = L.nfcap;
   std::vector<double> Psi((size_t)s.NF * nsl), Delta(s.NF), Eta((size_t)L.np * nf);
   d2h(Psi.data(), s.Psi, Psi.size(), s.stream);
   d2h(Delta.data(), s.Delta, s.NF, s.stream);
   d2h(Eta.data(), L.Eta, Eta.size(), s.stream);
   HIP_OK(hipStreamSynchronize(s.stream));
   if (nf < L.nfmax && iter > 20 && num_red == 0 && all_lt) {
-    HMSC_REQUIRE(nf + 1 <= nfcap && s.K + 1 <= 64, "updateNf: nf would exceed this build's limit (K <= 64)");
+    if (nf + 1 > nfcap || s.K + 1 > s.Kmax)
+      throw HmscError(-6, "updateNf: level " + std::to_string(r + 1) + " needs " + std::to_string(nf + 1) +
+                              " latent factors at iteration " + std::to_string(iter) + ", but this build holds at most " +
+                              std::to_string(nfcap) + " for it (K = nc + sum(nf) <= 64); set nfMax <= " +
+                              std::to_string(nfcap) + " with setPriors (or fewer covariates) to run this model");
     const int K2 = K + 1, NF2 = s.NF + 1;
     std::vector<double> BL2((size_t)K2 * nsl), Psi2((size_t)NF2 * nsl), Delta2(NF2);
     for (int j = 0; j < nsl; ++j) {
@@ -1290,7 +1348,7 @@ static void unpack_record(const State& s, const double* slot, int k, int samples
   if (rec->iSigma) std::memcpy(rec->iSigma + (size_t)k * nsl, iS, sizeof(double) * nsl);
   for (int r = 0; r < s.nr; ++r) {
     const Level& L = s.lev[r];
-    const int nf = L.nf, nfm = L.nfmax, lo = s.loff(r), fo = s.foff(r);
+    const int nf = L.nf, nfm = L.nfcap, lo = s.loff(r), fo = s.foff(r);
     if (rec->rec_nf) rec->rec_nf[r * samples + k] = nf;
     if (rec->Lambda[r] || rec->Psi[r])
       for (int j = 0; j < nsl; ++j)
@@ -1318,8 +1376,8 @@ static void unpack_record(const State& s, const double* slot, int k, int samples
   for (int r = 0; r < s.nr; ++r) {
     const Level& L = s.lev[r];
     if (!L.spatial) continue;
-    for (int h = 0; h < L.nfmax; ++h)
-      if (rec->Alpha[r]) rec->Alpha[r][(size_t)k * L.nfmax + h] = h < L.nf ? (int32_t)al[h] : 1;
+    for (int h = 0; h < L.nfcap; ++h)
+      if (rec->Alpha[r]) rec->Alpha[r][(size_t)k * L.nfcap + h] = h < L.nf ? (int32_t)al[h] : 1;
     al += L.nf;
   }
 }
@@ -1347,7 +1405,7 @@ static void pretouch_record(const State& s, int k, const hmsc_record* rec) {
   touch(rec->iV, sizeof(double), nc * nc);
   touch(rec->iSigma, sizeof(double), nsl);
   for (int r = 0; r < s.nr; ++r) {
-    const size_t nfm = s.lev[r].nfmax;
+    const size_t nfm = s.lev[r].nfcap;
     touch(rec->Eta[r], sizeof(double), (size_t)s.lev[r].np * nfm);
     touch(rec->Lambda[r], sizeof(double), nfm * nsl);
     touch(rec->Psi[r], sizeof(double), nfm * nsl);
@@ -1587,12 +1645,7 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
   HIP_OK(hipStreamSynchronize(s.stream));
   HIP_OK(hipStreamSynchronize(s.copy_stream));
   const auto t_done = std::chrono::steady_clock::now();
-  int flag[2] = {0, 0};
-  copy_sync(flag, s.dev_flags, sizeof(flag), hipMemcpyDeviceToHost, s.stream);
-  HMSC_REQUIRE(flag[0] == 0 && flag[1] == 0, "a Cholesky factorisation failed (matrix not positive definite)");
-  int gsync[4] = {0, 0, 0, 0};
-  copy_sync(gsync, s.gbl_sync, sizeof(gsync), hipMemcpyDeviceToHost, s.stream);
-  HMSC_REQUIRE(gsync[3] == 0, "internal: the Gamma2 / BetaLambda in-launch handshake timed out");
+  check_device_flags(s);
   if (recording) {
     pool->wait();
     std::lock_guard<std::mutex> lk(mu);
@@ -1682,12 +1735,12 @@ int hmsc_dense_chol_solve(int32_t device, double* A, int32_t n, double* b, int32
     double* db = bufs.alloc<double>(n);
     double* ws = bufs.alloc<double>(dense_ws_doubles(n));
     int* dinfo = bufs.alloc<int>(1);
-    int* dsync = bufs.alloc<int>(2 + 4096);  // the sync-free solves' handshake, zeroed
+    int* dsync = bufs.alloc<int>(DENSE_SYNC_INTS);  // the dense handshake block, zeroed
     HIP_OK(hipMemsetAsync(dinfo, 0, sizeof(int), st));
-    HIP_OK(hipMemsetAsync(dsync, 0, (2 + 4096) * sizeof(int), st));
+    HIP_OK(hipMemsetAsync(dsync, 0, DENSE_SYNC_INTS * sizeof(int), st));
     HIP_OK(hipMemcpyAsync(dA, A, nn * sizeof(double), hipMemcpyHostToDevice, st));
     if (b) HIP_OK(hipMemcpyAsync(db, b, (size_t)n * sizeof(double), hipMemcpyHostToDevice, st));
-    dense_potrf_lower(st, dA, n, n, ws, dinfo);
+    dense_potrf_lower(st, dA, n, n, ws, dinfo, 0, dsync);
     if (b) {
       dense_trsv_lower(st, dA, n, n, db, 0, ws, 0, dsync);
       dense_trsv_lower(st, dA, n, n, db, 1, ws, 0, dsync);
@@ -1695,7 +1748,12 @@ int hmsc_dense_chol_solve(int32_t device, double* A, int32_t n, double* b, int32
     }
     HIP_OK(hipMemcpyAsync(A, dA, nn * sizeof(double), hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(info, dinfo, sizeof(int), hipMemcpyDeviceToHost, st));
+    int hs = 0;
+    HIP_OK(hipMemcpyAsync(&hs, dsync + DENSE_SYNC_ERR, sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
+    if (hs != 0)
+      throw HmscError(-5, "internal: an in-launch handshake of the blocked dense solver timed out (error bits " +
+                              std::to_string(hs) + "); the result is invalid");
   });
 }
 
@@ -1801,11 +1859,11 @@ int hmsc_init_state(hmsc_state* h, const int32_t* nf0) {
     DeviceGuard dg(s.device);
     if (nf0)
       for (int r = 0; r < s.nr; ++r) {
-        HMSC_REQUIRE(nf0[r] >= 1 && nf0[r] <= std::min(s.lev[r].nfmax, s.NFmax), "init: bad nf0");
+        HMSC_REQUIRE(nf0[r] >= 1 && nf0[r] <= s.lev[r].nfcap, "init: nf0 exceeds the level's factor capacity");
         s.lev[r].nf = nf0[r];
       }
     s.refresh_dims();
-    HMSC_REQUIRE(s.K <= s.Kmax, "init: K exceeds 64");
+    HMSC_REQUIRE(s.K <= s.Kmax, "init: K = nc + sum(nf) exceeds this build's limit of 64");
     launch_init(s);
     const double one = 1.0;  // rho = 1 (R/computeInitialParameters.R:226)
     HIP_OK(hipMemcpyAsync(s.rho, &one, sizeof(double), hipMemcpyHostToDevice, s.stream));
@@ -1838,6 +1896,12 @@ int hmsc_get_state(hmsc_state* h, hmsc_params* p) {
 int hmsc_get_nf(hmsc_state* h, int32_t* nf) {
   return guarded([&] {
     for (int r = 0; r < h->s.nr; ++r) nf[r] = h->s.lev[r].nf;
+  });
+}
+
+int hmsc_get_nf_cap(hmsc_state* h, int32_t* nfcap) {
+  return guarded([&] {
+    for (int r = 0; r < h->s.nr; ++r) nfcap[r] = h->s.lev[r].nfcap;
   });
 }
 
@@ -1908,6 +1972,27 @@ int hmsc_sync(hmsc_state* h) {
     join_side(h->s);
     HIP_OK(hipStreamSynchronize(h->s.stream));
     HIP_OK(hipStreamSynchronize(h->s.copy_stream));
+    check_device_flags(h->s);
+  });
+}
+
+// Test hook: corrupt one of the chain's in-launch handshakes so the next launch that uses it
+// must time out and report ("trsv_ticket": the sync-free solve's ticket starts at 1, so block 0
+// is never solved; "chol_publish": the next fused panel step of the blocked Cholesky withholds
+// its flag).
+int hmsc_debug_poison(hmsc_state* h, const char* what) {
+  return guarded([&] {
+    State& s = h->s;
+    DeviceGuard dg(s.device);
+    HMSC_REQUIRE(what != nullptr, "hmsc_debug_poison: what is NULL");
+    join_side(s);
+    HIP_OK(hipStreamSynchronize(s.stream));
+    const std::string w(what);
+    int v = 1, at = 0;
+    if (w == "trsv_ticket") at = 0;
+    else if (w == "chol_publish") at = DENSE_SYNC_TEST, v = HS_TEST_SKIP_PUBLISH;
+    else throw HmscError(-1, "hmsc_debug_poison: unknown handshake " + w);
+    copy_sync(s.trsv_sync + at, &v, sizeof(int), hipMemcpyHostToDevice, s.stream);
   });
 }
 

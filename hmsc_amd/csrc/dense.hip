@@ -43,6 +43,33 @@ namespace hmsc {
 constexpr int DB = 64;       // panel / tile size
 constexpr int DLD = DB + 1;  // padded LDS leading dimension
 
+// Every in-launch handshake of this file (the sync-free solve's block flags, the fused
+// panel's diagonal-inverse flag) is bounded in time: a wait that outlasts HS_TIMEOUT_TICKS of
+// the 100 MHz wall clock (1 s; a legitimate wait is microseconds) raises its bit in the sync
+// block's error word (DENSE_SYNC_ERR, state.h) and the workgroup carries on, so the launch
+// drains; the host reads that word after the sweep (capi.cpp check_device_flags) and fails
+// the call instead of returning a half-solved system.
+constexpr unsigned long long HS_TIMEOUT_TICKS = 100000000ull;
+
+__device__ __forceinline__ void hs_raise(int* sync, int bit) {
+  __hip_atomic_fetch_or(sync + DENSE_SYNC_ERR, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// poll *f (relaxed, device scope) until pred(value); false (and bit raised) on timeout
+template <class P>
+__device__ __forceinline__ bool hs_wait(const int* f, P pred, int* sync, int bit) {
+  if (pred(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) return true;
+  const unsigned long long t0 = kt_now();
+  for (int spin = 1;; ++spin) {
+    __builtin_amdgcn_s_sleep(1);
+    if (pred(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) return true;
+    if ((spin & 255) == 0 && kt_now() - t0 > HS_TIMEOUT_TICKS) {
+      hs_raise(sync, bit);
+      return false;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // 1. diagonal block: L_kk (in place) and Linv_k = L_kk^-1 (64 x 64, ld 64, zero above)
 // ---------------------------------------------------------------------------------------
@@ -343,7 +370,7 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(double* A, int lda, int
 // needs no panel launch either.
 template <bool DIAG>
 __global__ __launch_bounds__(256, 2) void chol_update_kernel(double* A, int lda, int n, int k0, double* Linv_next,
-                                                             int* info, int* pflag) {
+                                                             int* info, int* pflag, int* sync) {
   __shared__ double PI[DB * DLD];
   __shared__ double PJ[DB * DLD];
   const int nb = min(DB, n - k0), base = k0 + nb;
@@ -427,14 +454,7 @@ __global__ __launch_bounds__(256, 2) void chol_update_kernel(double* A, int lda,
             P[r + DLD * c] = (r < rowsI && c < rowsJ) ? cv[a][b][q] - acc[a][b][q] : 0.0;
           }
       const int step = k0 / DB + 1;
-      if (t == 0)
-        for (int spin = 0; __hip_atomic_load(pflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != step; ++spin) {
-          if (spin > (1 << 24)) {  // a broken handshake reports, never hangs
-            atomicExch(info, 1);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
+      if (t == 0) hs_wait(pflag, [&](int v) { return v == step; }, sync, HS_ERR_CHOL_PANEL);
       __syncthreads();
       {
         double li[DB * DB / 256];
@@ -491,9 +511,18 @@ __global__ __launch_bounds__(256, 2) void chol_update_kernel(double* A, int lda,
           }
     __syncthreads();
     diag_body(T, I, S, A, lda, n, base, Linv_next, info);
-    if (pflag) {  // Linv_next written (diag_body's stores precede the barrier): publish it
+    if (pflag) {
+      // Linv_next written: every thread's stores complete at device scope (each wave's own
+      // fence -- the barrier alone orders them only within the workgroup), then publish.
+      // A test (hmsc_debug_poison "chol_publish") can withhold one publish: the waiting
+      // tiles must then time out and report.
+      __threadfence();
       __syncthreads();
-      if (t == 0) __hip_atomic_store(pflag, k0 / DB + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == 0) {
+        const bool skip = __hip_atomic_exchange(sync + DENSE_SYNC_TEST, 0, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT) == HS_TEST_SKIP_PUBLISH;
+        if (!skip) __hip_atomic_store(pflag, k0 / DB + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
 }
@@ -603,17 +632,26 @@ __global__ __launch_bounds__(256) void trsv_bwd_kernel(const double* L, int lda,
 // per block.  Flags are read with relaxed polling and the solved values with device-coherent
 // loads (an acquire per poll would invalidate the XCD's L2); the last workgroup to finish
 // resets the ticket, the done count and the flags for the next call.
-// sync (device, zeroed once): [0] ticket, [1] done count, [2 + b] flag of block b.
-constexpr int TRSV_SF_MAXB = 4096;
+// sync (the DENSE_SYNC_INTS block of state.h, zeroed once): [0] ticket, [1] done count, [2 + b]
+// flag of block b, [DENSE_SYNC_ERR] the handshake error word.
 
 __device__ __forceinline__ double load_coherent(const double* p) {
   return __longlong_as_double(
       (long long)__hip_atomic_load((const unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
-__device__ __forceinline__ void wait_flag(const int* f) {
-  for (int spin = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 && spin < (1 << 24); ++spin)
-    __builtin_amdgcn_s_sleep(1);
+__device__ __forceinline__ void wait_flag(const int* f, int* sync) {
+  hs_wait(f, [](int v) { return v != 0; }, sync, HS_ERR_TRSV_FLAG);
+}
+
+// a workgroup done with the call: the last one through resets the ticket, the done count and
+// the flags (every other one has finished its reads: it counted itself done after them)
+__device__ __forceinline__ void trsv_sf_done(int* sync, int nbk) {
+  if (__hip_atomic_fetch_add(&sync[1], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nbk - 1) {
+    for (int b = 0; b < nbk; ++b) __hip_atomic_store(sync + 2 + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&sync[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&sync[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 template <bool TR>
@@ -626,6 +664,13 @@ __global__ __launch_bounds__(256) void trsv_sf_kernel(const double* L, int lda, 
   if (t == 0) s_ord = __hip_atomic_fetch_add(&sync[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   const int ord = s_ord;
+  if (ord >= nbk) {  // a corrupt ticket (the call's handshake was not reset): report, drain
+    if (t == 0) {
+      hs_raise(sync, HS_ERR_TRSV_TICKET);
+      trsv_sf_done(sync, nbk);
+    }
+    return;
+  }
   const int k = TR ? nbk - 1 - ord : ord, R0 = k * DB, nb = min(DB, n - R0);
   int* flag = sync + 2;
   // this block's own operands -- Linv_k (lane = output row, wave g = terms 16 g ..) and x_k --
@@ -652,7 +697,7 @@ __global__ __launch_bounds__(256) void trsv_sf_kernel(const double* L, int lda, 
       if (j + 1 < k)
 #pragma unroll
         for (int u = 0; u < 16; ++u) ln[u] = L[row + (size_t)lda * (DB * (j + 1) + 16 * g + u)];
-      if (t == 0) wait_flag(flag + j);
+      if (t == 0) wait_flag(flag + j, sync);
       __syncthreads();
 #pragma unroll
       for (int u = 0; u < 16; ++u) acc[u] = fma(lc[u], load_coherent(x + DB * j + 16 * g + u), acc[u]);
@@ -675,7 +720,7 @@ __global__ __launch_bounds__(256) void trsv_sf_kernel(const double* L, int lda, 
     if (k < nbk - 1) ldt(lc, nbk - 1);
     for (int j = nbk - 1; j > k; --j) {
       if (j - 1 > k) ldt(ln, j - 1);
-      if (t == 0) wait_flag(flag + j);
+      if (t == 0) wait_flag(flag + j, sync);
       __syncthreads();
       const int rows = min(DB, n - DB * j);
       const double xv = lane < rows ? load_coherent(x + DB * j + lane) : 0.0;
@@ -707,16 +752,11 @@ __global__ __launch_bounds__(256) void trsv_sf_kernel(const double* L, int lda, 
   red[lane * (DB + 1) + g] = s;
   __syncthreads();
   if (t < nb) x[R0 + t] = (red[t * (DB + 1)] + red[t * (DB + 1) + 1]) + (red[t * (DB + 1) + 2] + red[t * (DB + 1) + 3]);
-  __syncthreads();  // every store of the block done before the flag
+  __threadfence();  // each wave's stores of the block complete at device scope ...
+  __syncthreads();  // ... before the flag
   if (t == 0) {
     __hip_atomic_store(flag + k, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    // the last workgroup through resets the call's handshake (every other one has finished
-    // its reads: it counted itself done after them)
-    if (__hip_atomic_fetch_add(&sync[1], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nbk - 1) {
-      for (int b = 0; b < nbk; ++b) __hip_atomic_store(flag + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&sync[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&sync[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    trsv_sf_done(sync, nbk);
   }
 }
 
@@ -999,7 +1039,7 @@ void dense_lauum_lower(hipStream_t st, const double* M, int ldm, int n, double* 
 // update of its panel adds exact zeros outside the band, so the panel and update launches stop
 // at the tiles covering rows k0 + DB .. k0 + DB + bw (the update's tile map depends on the
 // launch size only: a smaller grid is the band's triangle of tiles).
-void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, int* info, int bw) {
+void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, int* info, int bw, int* sync) {
   static const bool fuse_diag = [] {  // HMSC_NO_CHOL_DIAG_FUSION=1: the diagonal block as its own launch
     const char* e = std::getenv("HMSC_NO_CHOL_DIAG_FUSION");
     return !(e && e[0] && e[0] != '0');
@@ -1011,7 +1051,8 @@ void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, in
   // the panel handshake flag: past the workspace's diagonal-block inverses and solve vector
   // (dense_ws_doubles' slack), reset by the factorization's first launch
   const int nbk = (n + DB - 1) / DB;
-  int* pflag = (fuse_diag && fuse_panel && bw <= 0) ? (int*)(ws + (size_t)nbk * DB * DB + n + 8) : nullptr;
+  // (the fused panel needs the sync block for its timeout report)
+  int* pflag = (fuse_diag && fuse_panel && bw <= 0 && sync) ? (int*)(ws + (size_t)nbk * DB * DB + n + 8) : nullptr;
   bool diag_done = false, panel_done = false;  // block k0 / panel k0 done by the previous trailing update
   for (int k0 = 0; k0 < n; k0 += DB) {
     double* Linv = ws + (size_t)(k0 / DB) * DB * DB;
@@ -1021,11 +1062,13 @@ void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, in
       const int nt = (rem + DB - 1) / DB;
       if (!panel_done) chol_panel_kernel<<<nt, 256, 0, st>>>(A, lda, n, k0, Linv);
       if (fuse_diag) {
-        chol_update_kernel<true><<<nt * (nt + 1) / 2, 256, 0, st>>>(A, lda, n, k0, Linv + DB * DB, info, pflag);
+        chol_update_kernel<true><<<nt * (nt + 1) / 2, 256, 0, st>>>(A, lda, n, k0, Linv + DB * DB, info, pflag,
+                                                                      sync);
         diag_done = true;
         panel_done = pflag != nullptr;
       } else {
-        chol_update_kernel<false><<<nt * (nt + 1) / 2, 256, 0, st>>>(A, lda, n, k0, nullptr, nullptr, nullptr);
+        chol_update_kernel<false><<<nt * (nt + 1) / 2, 256, 0, st>>>(A, lda, n, k0, nullptr, nullptr, nullptr,
+                                                                       nullptr);
         diag_done = panel_done = false;
       }
     } else {

@@ -24,7 +24,13 @@
 
 namespace hmsc {
 
-constexpr int GE_NF_MAX = 16;
+// Per-thread arrays over the level's factors (tv, x1) are sized by a compile-time capacity:
+// the launcher picks the 16-factor instantiation while nf <= 16 (registers) and the 64-factor
+// one above it (K = nc + sum nf <= 64 bounds nf), so the updater follows the nf in use --
+// R's default nfMax = ns (R/Hmsc.R:554, truncated to the allocation) adapts upward from
+// nfMin = 2 (R/updateNf.R) -- instead of refusing a large nfMax at chain creation.
+constexpr int GE_NF_SMALL = 16;
+constexpr int GE_NF_LARGE = 64;
 
 struct GEArgs {
   int ny, ns, nc, nt, K, r, nr, nf, np, loff;
@@ -251,6 +257,7 @@ __device__ inline void ge_seg_tmp1(const GEArgs& a, const GEPtrs& P, int g0, int
 }
 
 // np = ny: M = iA + kron(tmp1, X'X) (:58), mb20 = vec((X'S LamiD') iW0 LamiD) (:62)
+template <int NFC>
 __device__ inline void ge_seg_m_obs(const GEArgs& a, const GEPtrs& P, int g0, int gs) {
   const int ns = a.ns, nc = a.nc, nf = a.nf, N = P.N;
   for (size_t p = g0; p < (size_t)N * N; p += gs) {
@@ -259,7 +266,7 @@ __device__ inline void ge_seg_m_obs(const GEArgs& a, const GEPtrs& P, int g0, in
   }
   for (int p = g0; p < N; p += gs) {
     const int c = p % nc, j = p / nc;
-    double x1[GE_NF_MAX];  // (X'S LamiD')[c, h1]: the same for every j, formed once
+    double x1[NFC];  // (X'S LamiD')[c, h1]: the same for every j, formed once
     for (int h1 = 0; h1 < nf; ++h1) {
       double x = 0.0;
       for (int j2 = 0; j2 < ns; ++j2) x = fma(P.XtS[c + nc * j2], P.LamiD[h1 + nf * j2], x);
@@ -430,12 +437,13 @@ __device__ inline void ge_wg_gamma(const GEArgs& a, const GEPtrs& P, int* flag, 
 }
 
 // Eta | Beta, S   (:71-74 / :136-146); S1 = S - X Beta, per row (np = ny) or per unit
+template <int NFC>
 __device__ inline void ge_seg_eta(const GEArgs& a, const GEPtrs& P, int g0, int gs, uint32_t it) {
   const int ny = a.ny, ns = a.ns, nc = a.nc, nf = a.nf, np = a.np;
   const uint32_t str = LEVEL_STRIDE * (uint32_t)a.r;
   if (P.obs) {
     for (int i = g0; i < ny; i += gs) {
-      double tv[GE_NF_MAX];
+      double tv[NFC];
       for (int h = 0; h < nf; ++h) tv[h] = 0.0;
       for (int j = 0; j < ns; ++j) {
         double s1 = P.S[i + (size_t)ny * j];
@@ -454,7 +462,7 @@ __device__ inline void ge_seg_eta(const GEArgs& a, const GEPtrs& P, int g0, int 
     }
   } else {
     for (int q = g0; q < np; q += gs) {
-      double tv[GE_NF_MAX];
+      double tv[NFC];
       for (int h = 0; h < nf; ++h) tv[h] = 0.0;
       for (int j = 0; j < ns; ++j) {
         double s1 = P.PtS[q + (size_t)np * j];
@@ -477,6 +485,7 @@ __device__ inline void ge_seg_eta(const GEArgs& a, const GEPtrs& P, int g0, int 
 
 // One workgroup per level (small nc ns): the segments between barriers, the factorizations
 // by wg_chol / wg_chol2inv on the L2-resident workspace.
+template <int NFC>
 __global__ __launch_bounds__(1024) void gamma_eta_kernel(GEArgs a) {
   __shared__ int flag;
   const int t = threadIdx.x, nthr = blockDim.x;
@@ -499,7 +508,7 @@ __global__ __launch_bounds__(1024) void gamma_eta_kernel(GEArgs a) {
     __syncthreads();
     ge_seg_tmp1(a, P, t, nthr);
     __syncthreads();
-    ge_seg_m_obs(a, P, t, nthr);
+    ge_seg_m_obs<NFC>(a, P, t, nthr);
   } else {
     if (!ge_seg_units(a, P, t, nthr)) a.fail[0] = 1;
     __syncthreads();
@@ -518,7 +527,7 @@ __global__ __launch_bounds__(1024) void gamma_eta_kernel(GEArgs a) {
   wg_backward_t(P.M, N, N, P.xi);  // backsolve(RM, rnorm(nc ns))  (:66)
   ge_wg_gamma(a, P, &flag, it);
   __syncthreads();
-  ge_seg_eta(a, P, t, nthr, it);
+  ge_seg_eta<NFC>(a, P, t, nthr, it);
 }
 
 // ---- the blocked path (nc ns > GE_WG_MAX): one launch per segment, the three (nc ns)^2
@@ -617,6 +626,7 @@ __global__ __launch_bounds__(256) void ge_b_a_kernel(GEArgs a) {
   ge_seg_a(a, P, g0, gs);
   if (P.obs) ge_seg_tmp1(a, P, g0, gs);
 }
+template <int NFC>
 __global__ __launch_bounds__(256) void ge_b_m_kernel(GEArgs a) {
   GE_GRID_IDX
   if (!P.obs) {
@@ -633,7 +643,7 @@ __global__ __launch_bounds__(256) void ge_b_m_kernel(GEArgs a) {
   const int lane = threadIdx.x & 63, w0 = g0 >> 6, ws = gs >> 6;
   for (int p = w0; p < N; p += ws) {
     const int c = p % nc, j = p / nc;
-    double x1[GE_NF_MAX];
+    double x1[NFC];
     for (int h1 = 0; h1 < nf; ++h1)
       x1[h1] = wave_sum<8>(ns, [&](int j2) { return P.XtS[c + nc * j2] * P.LamiD[h1 + nf * j2]; });
     if (lane == 0) {
@@ -733,13 +743,14 @@ __global__ __launch_bounds__(1024) void ge_b_gamma_kernel(GEArgs a) {
   for (int p = t; p < G; p += nthr) a.Gamma[p] = P.rg[p];
 }
 // Eta | Beta, S (:71-74 / :136-146): one wave per row (np = ny) or unit, lanes over species
+template <int NFC>
 __global__ __launch_bounds__(256) void ge_b_eta_kernel(GEArgs a) {
   GE_WAVE_IDX
   const int ny = a.ny, ns = a.ns, nc = a.nc, nf = a.nf, np = a.np;
   const uint32_t str = LEVEL_STRIDE * (uint32_t)a.r, it = SWEEP_ITER(a);
   const int nrow = P.obs ? ny : np;
   for (int i = w0; i < nrow; i += ws) {
-    double tv[GE_NF_MAX];
+    double tv[NFC];
     for (int h = 0; h < nf; ++h) tv[h] = 0.0;
     for (int j = lane; j < ns; j += 64) {
       double s1;
@@ -803,19 +814,26 @@ static void launch_gamma_eta_blocked(State& s, const GEArgs& a, hipStream_t st) 
   ge_b_xts_kernel<<<ge_blocks(std::max<size_t>(64 * ((size_t)N + a.ns * a.nt), obs ? 128 : a.np)), 256, 0, st>>>(a);
   ge_b_a_kernel<<<ge_blocks(NN), 256, 0, st>>>(a);
   // iA = chol2inv(chol(A)) = L^-T L^-1   (:33)
-  dense_potrf_lower(st, L, N, N, ws1, a.fail);
+  dense_potrf_lower(st, L, N, N, ws1, a.fail, 0, s.trsv_sync);
   dense_trtri_lower(st, L, N, N, T, N, ws1, true);
   dense_lauum_lower(st, T, N, N, M, N);
-  ge_b_m_kernel<<<ge_blocks(NN), 256, 0, st>>>(a);
+  if (a.nf <= GE_NF_SMALL)
+    ge_b_m_kernel<GE_NF_SMALL><<<ge_blocks(NN), 256, 0, st>>>(a);
+  else
+    ge_b_m_kernel<GE_NF_LARGE><<<ge_blocks(NN), 256, 0, st>>>(a);
   // RM = chol(M); v = M^-1 (mb10 - mb20)
-  dense_potrf_lower(st, M, N, N, ws2, a.fail);
+  dense_potrf_lower(st, M, N, N, ws2, a.fail, 0, s.trsv_sync);
   dense_trsv_lower(st, M, N, N, v, 0, ws2, 0, s.trsv_sync);
   dense_trsv_lower(st, M, N, N, v, 1, ws2, 0, s.trsv_sync);
   ge_b_wv_kernel<<<ge_blocks(64 * (size_t)N), 256, 0, st>>>(a);  // one wave per output
   ge_b_mb_kernel<<<ge_blocks(64 * (size_t)N), 256, 0, st>>>(a);
   dense_trsv_lower(st, M, N, N, xi, 1, ws2, 0, s.trsv_sync);  // backsolve(RM, rnorm(nc ns))  (:66)
   ge_b_gamma_kernel<<<1, 1024, 0, st>>>(a);
-  ge_b_eta_kernel<<<ge_blocks(64 * (size_t)(obs ? a.ny : a.np)), 256, 0, st>>>(a);
+  const int eta_grid = ge_blocks(64 * (size_t)(obs ? a.ny : a.np));
+  if (a.nf <= GE_NF_SMALL)
+    ge_b_eta_kernel<GE_NF_SMALL><<<eta_grid, 256, 0, st>>>(a);
+  else
+    ge_b_eta_kernel<GE_NF_LARGE><<<eta_grid, 256, 0, st>>>(a);
   HIP_OK(hipGetLastError());
 }
 
@@ -1140,10 +1158,10 @@ static void launch_gamma_eta_spatial(State& s, const GESArgs& sa, hipStream_t st
   ges_grid_kernel<1><<<grid(big1), 256, 0, st>>>(sa);
   ges_grid_kernel<2><<<grid(std::max((size_t)N * N, (size_t)a.np * a.ns)), 256, 0, st>>>(sa);
   ges_grid_kernel<3><<<grid((size_t)N * D2), 256, 0, st>>>(sa);
-  dense_potrf_lower(st, w + o.H, N, N, ws1, a.fail);
+  dense_potrf_lower(st, w + o.H, N, N, ws1, a.fail, 0, s.trsv_sync);
   ges_grid_kernel<4><<<grid((size_t)D2 + 1), 256, 0, st>>>(sa);
   ges_grid_kernel<5><<<grid((size_t)D2 * D2), 256, 0, st>>>(sa);
-  dense_potrf_lower(st, w + o.iG, D2, D2, ws2, a.fail);
+  dense_potrf_lower(st, w + o.iG, D2, D2, ws2, a.fail, 0, s.trsv_sync);
   dense_trsv_lower(st, w + o.iG, D2, D2, w + o.b, 0, ws2, 0, s.trsv_sync);
   ges_grid_kernel<6><<<grid(D2), 256, 0, st>>>(sa);
   dense_trsv_lower(st, w + o.iG, D2, D2, w + o.b, 1, ws2, 0, s.trsv_sync);
@@ -1151,10 +1169,12 @@ static void launch_gamma_eta_spatial(State& s, const GESArgs& sa, hipStream_t st
   HIP_OK(hipGetLastError());
 }
 
+// sized by the factors each level has now: a level's nf grows only in updateNf's adaptive
+// sweeps (eager, never inside a graph capture), and launch_gamma_eta grows the workspace then
 size_t gamma_eta_work_doubles(const State& s) {
   size_t m = 0;
   for (int r = 0; r < s.nr; ++r) {
-    const int nf = std::max(1, s.lev[r].nfmax);
+    const int nf = std::max(1, s.lev[r].nf);
     const int np = s.lev[r].np == s.ny ? 0 : s.lev[r].np;
     m = std::max(m, ge_layout(s.ny, s.ns, s.nc, s.nt, nf, np).tot + ge_blocked_extra(s.nc * s.ns));
     if (s.lev[r].spatial) {
@@ -1169,6 +1189,17 @@ size_t gamma_eta_work_doubles(const State& s) {
 void launch_gamma_eta(State& s, uint32_t iter) {
   HMSC_REQUIRE(s.nranks == 1, "updateGammaEta: species-sharded chains are not supported (dense (nc ns)^2 system)");
   HMSC_REQUIRE(s.geWork != nullptr, "updateGammaEta: workspace not allocated");
+  for (int r = 0; r < s.nr; ++r)
+    HMSC_REQUIRE(!s.lev[r].spatial || (size_t)s.nc * s.nt + (size_t)s.lev[r].np * s.lev[r].nf <= 32768,
+                 "updateGammaEta, spatial level: nc nt + np nf must be <= 32768 (dense joint system, 8.6 GB)");
+  {
+    const size_t need = gamma_eta_work_doubles(s);
+    if (need > s.geWork_doubles) {  // nf grew (updateNf): a larger workspace, outside any capture
+      HMSC_REQUIRE(!s.capturing, "internal: updateGammaEta workspace growth inside a graph capture");
+      s.geWork = device_realloc_doubles(s, s.geWork, need);
+      s.geWork_doubles = need;
+    }
+  }
   ProfScope ps(s, PROF_GE);
   for (int r = 0; r < s.nr; ++r) {
     GEArgs a{};
@@ -1182,7 +1213,7 @@ void launch_gamma_eta(State& s, uint32_t iter) {
     a.nf = s.lev[r].nf;
     a.np = s.lev[r].np;
     a.loff = s.loff(r);
-    HMSC_REQUIRE(a.nf <= GE_NF_MAX, "updateGammaEta: nf must be <= 16 in this build");
+    HMSC_REQUIRE(a.nf <= GE_NF_LARGE, "updateGammaEta: nf must be <= 64 (K = nc + sum nf <= 64)");
     for (int q = 0; q < s.nr; ++q) {
       a.lev_np[q] = s.lev[q].np;
       a.lev_nf[q] = s.lev[q].nf;
@@ -1220,7 +1251,10 @@ void launch_gamma_eta(State& s, uint32_t iter) {
     } else if (a.nc * a.ns > GE_WG_MAX) {
       launch_gamma_eta_blocked(s, a, s.stream);
     } else {
-      gamma_eta_kernel<<<1, 1024, 0, s.stream>>>(a);
+      if (a.nf <= GE_NF_SMALL)
+        gamma_eta_kernel<GE_NF_SMALL><<<1, 1024, 0, s.stream>>>(a);
+      else
+        gamma_eta_kernel<GE_NF_LARGE><<<1, 1024, 0, s.stream>>>(a);
     }
     HIP_OK(hipGetLastError());
   }

@@ -2732,7 +2732,7 @@ void launch_copied_flag(State& s, uint64_t value) {
 size_t record_slot_doubles(const State& s) {
   size_t n = (size_t)s.Kmax * s.nsl + (size_t)s.NFmax * s.nsl + s.NFmax + (size_t)s.nc * s.nt +
              (size_t)s.nc * s.nc + s.nsl + 2;
-  for (int r = 0; r < s.nr; ++r) n += (size_t)s.lev[r].np * s.lev[r].nfmax + (s.lev[r].spatial ? s.lev[r].nfmax : 0);
+  for (int r = 0; r < s.nr; ++r) n += (size_t)s.lev[r].np * s.lev[r].nfcap + (s.lev[r].spatial ? s.lev[r].nfcap : 0);
   return n;
 }
 

@@ -407,7 +407,7 @@ void launch_beta_lambda_phylo(State& s, uint32_t iter) {
   ph_assemble_kernel<<<dim3(g1, N), 256, 0, s.stream>>>(a);
   ph_rhs_kernel<<<(unsigned)std::min<size_t>(4096, ((size_t)N * 64 + 255) / 256), 256, 0, s.stream>>>(a);
   HIP_OK(hipGetLastError());
-  dense_potrf_lower(s.stream, M, N, N, ws, s.dev_flags + 2);
+  dense_potrf_lower(s.stream, M, N, N, ws, s.dev_flags + 2, 0, s.trsv_sync);
   dense_trsv_lower(s.stream, M, N, N, rhs, 0, ws, 0, s.trsv_sync);   // m1 = backsolve(RiU, ., transpose=TRUE)  (:145)
   ph_noise_kernel<<<g1, 256, 0, s.stream>>>(a);
   dense_trsv_lower(s.stream, M, N, N, rhs, 1, ws, 0, s.trsv_sync);   // backsolve(RiU, m1 + rnorm)  (:146)

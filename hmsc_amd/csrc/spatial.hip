@@ -32,6 +32,10 @@
 
 namespace hmsc {
 
+// factor capacity of a spatial level's workspace layout (sp_ensure_capacity)
+static inline int sp_nfc(const Level& L) { return L.nf_alloc > 1 ? L.nf_alloc : 1; }
+
+
 struct SpArgs {
   int ny, ns, K, nf, np, loff, nalpha, r;
   const double* Z;        // ny x ns
@@ -539,7 +543,7 @@ static void launch_eta_gpp(State& s, int r, uint32_t iter) {
   HMSC_REQUIRE(L.nK <= 1024, "GPP level: at most 1024 knots in this build");
   const SpArgs a = sp_args(s, r, iter);
   const int np = L.np, nf = L.nf, NP = np * nf, KF = L.nK * nf;
-  const GppLayout o = gpp_layout(np, std::max(1, std::min(L.nfmax, s.NFmax)), L.nK, L.nalpha);
+  const GppLayout o = gpp_layout(np, sp_nfc(L), L.nK, L.nalpha);
   double* w = L.spWork;
   double *rhs = w + o.rhs, *LDL = w + o.LDL, *B1 = w + o.B1, *LB1 = w + o.LB1, *iAW = w + o.iAW, *H = w + o.H;
   double *M = w + o.M, *ws = w + o.ws, *T = w + o.T, *v = w + o.v;
@@ -551,7 +555,7 @@ static void launch_eta_gpp(State& s, int r, uint32_t iter) {
   HIP_OK(hipGetLastError());
   {
     ProfScope pc(s, PROF_CHOL);
-    dense_potrf_lower(s.stream, H, KF, KF, ws, s.dev_flags);  // RH = chol(H) = L_H^T
+    dense_potrf_lower(s.stream, H, KF, KF, ws, s.dev_flags, 0, s.trsv_sync);  // RH = chol(H) = L_H^T
   }
   dense_trtri_lower(s.stream, H, KF, KF, M, KF, ws, true);     // M = L_H^-1, RH^-1 = M^T
   gpp_t_kernel<<<dim3(g1, KF), 256, 0, s.stream>>>(a, iAW, M, T);
@@ -724,7 +728,7 @@ static void launch_eta_nngp(State& s, int r, uint32_t iter) {
   Level& L = s.lev[r];
   const SpArgs a = sp_args(s, r, iter);
   const NnArgs n = nn_args(s, r);
-  const NnLayout o = nn_layout(L.np, std::max(1, std::min(L.nfmax, s.NFmax)));
+  const NnLayout o = nn_layout(L.np, sp_nfc(L));
   double* w = L.spWork;
   double *Q = w + o.Q, *x = w + o.x, *rhs = w + o.rhs, *ws = w + o.ws, *LDL = w + o.LDL;
   const int N = n.N, g1 = (N + 255) / 256;
@@ -738,7 +742,7 @@ static void launch_eta_nngp(State& s, int r, uint32_t iter) {
   HIP_OK(hipGetLastError());
   {
     ProfScope pc(s, PROF_CHOL);
-    dense_potrf_lower(s.stream, Q, N, N, ws, s.dev_flags, n.bw);
+    dense_potrf_lower(s.stream, Q, N, N, ws, s.dev_flags, n.bw, s.trsv_sync);
   }
   dense_trsv_lower(s.stream, Q, N, N, x, 0, ws, n.bw, s.trsv_sync);   // backsolve(R, fS, transpose = TRUE)
   nngp_perm_kernel<<<g1, 256, 0, s.stream>>>(a, n, rhs, x, 1);
@@ -907,17 +911,31 @@ constexpr int SP_BLOCKED_N = 1024;
 
 size_t spatial_work_doubles(const State& s, int r) {
   const Level& L = s.lev[r];
-  const size_t nfc = std::max(1, std::min(L.nfmax, s.NFmax));
+  const size_t nfc = sp_nfc(L);
   if (L.gpp) return gpp_layout(L.np, (int)nfc, L.nK, L.nalpha).tot + 64;
   if (L.nngp)  // updateAlpha's partial sums after the band matrix: its zeros outside the band persist
     return nn_layout(L.np, (int)nfc).tot + (size_t)L.nalpha * ((L.np + 255) / 256) * nfc + 64;
   const size_t N = (size_t)L.np * nfc;
   const size_t eta = N * N + N + dense_ws_doubles((int)N) + nfc * nfc + 64;
-  const size_t alpha = (size_t)L.nalpha * ((L.np + 255) / 256) * std::max(1, std::min(L.nfmax, s.NFmax));
+  const size_t alpha = (size_t)L.nalpha * ((L.np + 255) / 256) * sp_nfc(L);
   return std::max(eta, alpha) + 64;
 }
 
+// The level's workspace follows the factors in use: laid out for L.nf_alloc factors at chain
+// creation (nfMin), re-laid out for more when updateNf has added factors -- always outside a
+// graph capture (nf changes only in eager adaptive sweeps, or by set_state / init) -- so a
+// level with R's default nfMax = ns never holds an (np nfMax)^2 system it does not use.
+static void sp_ensure_capacity(State& s, int r) {
+  Level& L = s.lev[r];
+  if (L.nf <= L.nf_alloc) return;
+  HMSC_REQUIRE(!s.capturing, "internal: spatial workspace growth inside a graph capture");
+  L.nf_alloc = L.nf;
+  L.spWork = device_realloc_doubles(s, L.spWork, spatial_work_doubles(s, r));
+  L.nnAssembledN = 0;  // the band layout's zeros are gone with the old buffer
+}
+
 void launch_eta_spatial(State& s, int r, uint32_t iter) {
+  sp_ensure_capacity(s, r);
   const Level& L = s.lev[r];
   HMSC_REQUIRE(s.nranks == 1, "spatial levels: species-sharded chains are not supported");
   if (!s.xeta_valid) launch_xeta(s);
@@ -948,7 +966,7 @@ void launch_eta_spatial(State& s, int r, uint32_t iter) {
   HIP_OK(hipGetLastError());
   {
     ProfScope pc(s, PROF_CHOL);
-    dense_potrf_lower(s.stream, U, N, N, ws, s.dev_flags);
+    dense_potrf_lower(s.stream, U, N, N, ws, s.dev_flags, 0, s.trsv_sync);
   }
   dense_trsv_lower(s.stream, U, N, N, rhs, 0, ws, 0, s.trsv_sync);   // backsolve(R, fS, transpose = TRUE)
   sp_noise_kernel<<<g1, 256, 0, s.stream>>>(a, rhs);
@@ -959,13 +977,14 @@ void launch_eta_spatial(State& s, int r, uint32_t iter) {
 
 void launch_alpha(State& s, uint32_t iter) {
   for (int r = 0; r < s.nr; ++r) {
+    if (!s.lev[r].spatial || s.lev[r].nf == 0) continue;  // rep(1, nf) otherwise (R/updateAlpha.R:81-82)
+    sp_ensure_capacity(s, r);
     const Level& L = s.lev[r];
-    if (!L.spatial || L.nf == 0) continue;  // rep(1, nf) otherwise (R/updateAlpha.R:81-82)
     const SpArgs a = sp_args(s, r, iter);
     ProfScope ps(s, PROF_ALPHA);
     if (L.gpp) {
       HMSC_REQUIRE(L.nK <= 1024, "GPP level: at most 1024 knots in this build");  // t2[1024] in LDS
-      const GppLayout o = gpp_layout(L.np, std::max(1, std::min(L.nfmax, s.NFmax)), L.nK, L.nalpha);
+      const GppLayout o = gpp_layout(L.np, sp_nfc(L), L.nK, L.nalpha);
       SpArgs b = a;
       b.work = L.spWork + o.alpha;
       gpp_alpha_kernel<<<L.nalpha, 256, 0, s.stream>>>(b, b.work);
@@ -976,7 +995,7 @@ void launch_alpha(State& s, uint32_t iter) {
     }
     if (L.nngp) {  // the band matrix at the start of spWork stays untouched (zeros outside the band)
       SpArgs b = a;
-      b.work = L.spWork + nn_layout(L.np, std::max(1, std::min(L.nfmax, s.NFmax))).tot;
+      b.work = L.spWork + nn_layout(L.np, sp_nfc(L)).tot;
       nngp_alpha_kernel<<<dim3(L.nalpha, (L.np + 255) / 256), 256, 0, s.stream>>>(b, nn_args(s, r));
       HIP_OK(hipGetLastError());
       alpha_draw_kernel<<<1, 256, 0, s.stream>>>(b);
@@ -1037,8 +1056,11 @@ void spatial_full_grid(hipStream_t st, int np, int sdim, const double* coords, c
                        const double* alphas, int G, double* iWg, double* RiWg, double* detWg, int* info) {
   const size_t n2 = (size_t)np * np;
   double *W = nullptr, *dinv = nullptr;
+  int* sync = nullptr;  // the dense handshake block (the fused panel step's flag timeout)
   HIP_OK(hipMalloc(&W, n2 * sizeof(double)));
   HIP_OK(hipMalloc(&dinv, dense_ws_doubles(np) * sizeof(double)));
+  HIP_OK(hipMalloc(&sync, DENSE_SYNC_INTS * sizeof(int)));
+  HIP_OK(hipMemsetAsync(sync, 0, DENSE_SYNC_INTS * sizeof(int), st));
   for (int g = 0; g < G; ++g) {
     double* iW = iWg + n2 * g;
     double* RiW = RiWg + n2 * g;
@@ -1050,15 +1072,20 @@ void spatial_full_grid(hipStream_t st, int np, int sdim, const double* coords, c
       continue;
     }
     sp_w_kernel<<<dim3((np + 255) / 256, np), 256, 0, st>>>(W, np, sdim, coords, dist, alphas[g]);
-    dense_potrf_lower(st, W, np, np, dinv, info);
+    dense_potrf_lower(st, W, np, np, dinv, info, 0, sync);
     sp_logdet_kernel<<<1, 256, 0, st>>>(W, np, detWg + g);
     dense_trtri_lower(st, W, np, np, RiW, np, dinv, true);
     dense_lauum_lower(st, RiW, np, np, iW, np);
   }
   HIP_OK(hipGetLastError());
+  int err = 0;
+  HIP_OK(hipMemcpyAsync(&err, sync + DENSE_SYNC_ERR, sizeof(int), hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
   HIP_OK(hipFree(W));
   HIP_OK(hipFree(dinv));
+  HIP_OK(hipFree(sync));
+  HMSC_REQUIRE(err == 0, "spatial grid: an in-launch handshake of the blocked Cholesky timed out (error bits " +
+                             std::to_string(err) + ")");
 }
 
 }  // namespace hmsc

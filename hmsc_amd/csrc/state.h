@@ -25,6 +25,9 @@ namespace hmsc {
 
 struct Level {
   int np = 0, nf = 0, nfmax = 0, nfmin = 0;
+  // factors this level's buffers hold: min(nfMax, K cap - nc) -- Eta storage, record slots;
+  // and the factors its spatial workspace is laid out for now (grown with nf, spatial.hip)
+  int nfcap = 0, nf_alloc = 0;
   double nu = 3, a1 = 50, b1 = 1, a2 = 50, b2 = 1;
   double* Eta = nullptr;        // np x nfmax storage, live np x nf (ld = np)
   int* Pi = nullptr;            // ny, 0-based unit of each row
@@ -107,6 +110,7 @@ struct State {
   int* varest = nullptr;         // ns_loc distr[,2]
   double *V0 = nullptr, *iUGamma = nullptr, *mGamma = nullptr, *UGammaL = nullptr, *UGamma = nullptr;
   double* geWork = nullptr;      // updateGammaEta workspace (gamma_eta.hip), only if that updater is on
+  size_t geWork_doubles = 0;     // its size (grown with the levels' nf)
   double *aSigma = nullptr, *bSigma = nullptr;
   double *XX = nullptr, *TT = nullptr, *V0g = nullptr, *V0gXXV0g = nullptr, *iV0 = nullptr;
   double* V0inv = nullptr;       // V0^-1 (initial riwish draw)
@@ -181,7 +185,7 @@ struct State {
   uint64_t* copied_host = nullptr;  // fine-grained pinned counter: samples whose D2H copy landed
   uint64_t* copied_dev = nullptr;   // its device address
   std::shared_ptr<struct UnpackPool> unpack_pool;
-  int* trsv_sync = nullptr;  // dense_trsv_lower's sync-free handshake (2 + 4096 ints)  // record-unpack workers (capi.cpp), kept across runs
+  int* trsv_sync = nullptr;  // the dense handshake block (DENSE_SYNC_INTS ints, zeroed): sync-free solves, fused panel
 
   // per-sweep hipGraph (single rank, no updateNf): captured once, replayed every sweep; the
   // kernels read the Philox sweep counter from d_iter, which the graph's first node advances
@@ -302,11 +306,24 @@ void launch_rho(State& s, uint32_t iter, hipStream_t st);
 void launch_beta_lambda_phylo(State& s, uint32_t iter);
 void launch_side_fused(State& s, uint32_t iter);
 // blocked dense fp64 factorisation / solves (dense.hip)
+// The dense handshake block (one per chain, State::trsv_sync, zero-initialised): [0] ticket,
+// [1] done count, [2 + b] flag of 64-block b of a sync-free solve, [DENSE_SYNC_ERR] the error
+// word every bounded in-launch wait raises a bit of on timeout (HS_ERR_*; the host checks it
+// after a run, capi.cpp check_device_flags), [DENSE_SYNC_TEST] a test hook
+// (hmsc_debug_poison).
+constexpr int TRSV_SF_MAXB = 4096;
+constexpr int DENSE_SYNC_ERR = 2 + TRSV_SF_MAXB;
+constexpr int DENSE_SYNC_TEST = DENSE_SYNC_ERR + 1;
+constexpr int DENSE_SYNC_INTS = DENSE_SYNC_ERR + 2;
+enum HsErr { HS_ERR_TRSV_FLAG = 1, HS_ERR_TRSV_TICKET = 2, HS_ERR_CHOL_PANEL = 4 };
+constexpr int HS_TEST_SKIP_PUBLISH = 1;  // DENSE_SYNC_TEST: the next fused panel step withholds its flag
 // bw > 0: A is banded (A[i, j] = 0 for i - j > bw, entries outside the band zero on entry);
-// the factor keeps the band, and only the band's tiles are touched (n bw^2 work instead of n^3)
-void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, int* info, int bw = 0);
-// sync: the State's trsv_sync (2 + 4096 ints, zeroed) for the one-launch sync-free solve, or
-// null for one launch per 64-block
+// the factor keeps the band, and only the band's tiles are touched (n bw^2 work instead of n^3).
+// sync: the dense handshake block (enables the fused panel step), or null.
+void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, int* info, int bw = 0,
+                       int* sync = nullptr);
+// sync: the dense handshake block for the one-launch sync-free solve, or null for one launch
+// per 64-block
 void dense_trsv_lower(hipStream_t st, const double* L, int n, int lda, double* x, int trans, double* ws, int bw = 0,
                       int* sync = nullptr);
 void dense_trtri_lower(hipStream_t st, const double* L, int ldl, int n, double* M, int ldm, double* dinv,
@@ -333,6 +350,9 @@ void launch_alpha(State& s, uint32_t iter);
 size_t gamma_eta_work_doubles(const State& s);
 void launch_gamma_eta(State& s, uint32_t iter);  // GammaV + LambdaPriors + Eta, co-launched
 void join_side(State& s);
+// a fresh zeroed device buffer of n doubles replacing `old` (freed), under the allocation
+// lock every chain's captures respect (capi.cpp)
+double* device_realloc_doubles(State& s, double* old, size_t n);
 void launch_copied_flag(State& s, uint64_t value);
 size_t record_slot_doubles(const State& s);
 void read_stamps(double* out, int n);  // diagnostic build (HMSC_STAMPS)

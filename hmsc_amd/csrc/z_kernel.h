@@ -48,6 +48,10 @@ struct ZArgs {
   const uint32_t* iter_dev;  // graph replay: the sweep counter is read from the device
   int noise_zero;
   int zprev_is_e;            // chain init: ZPrev = LFix + LRan (R/computeInitialParameters.R:250-254)
+  // NA cells leave the XZ contraction (the C = NULL branch's per-species observed rows,
+  // R/updateBetaLambda.R:103-117); 0 with a phylogeny, whose dense system takes the full
+  // crossprod(XEta, S) over the imputed Z (:66, :124-146)
+  int mask_na;
   unsigned long long* kt;    // live launch timing (KT_Z block) or null
   // G = XEta^T XEta's Eta rows from the fused Eta pass' tile partials, reduced by the first
   // grid row's workgroups while the others draw (gred_y0 = 1; see g_reduce_body)
@@ -458,7 +462,7 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
         const int ir = i0 + 4 * r + lk;
         double z0 = sT[(2 * lm) * ZT_TLD + lk + 4 * r];
         double z1 = sT[(2 * lm + 1) * ZT_TLD + lk + 4 * r];
-        if (HAS_NA) {  // NA cells (code + 1 == 0) out of the contraction
+        if (HAS_NA && a.mask_na) {  // NA cells (code + 1 == 0) out of the contraction
           const uint64_t w2 = a.Ybits[(size_t)by * ny + ir];  // padded buffer: ir < ny + 64
           if (((w2 >> (4 * lm)) & 3u) == 0) z0 = 0.0;
           if (((w2 >> (4 * lm + 2)) & 3u) == 0) z1 = 0.0;

@@ -91,6 +91,7 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   a.iter_dev = s.capturing ? s.d_iter : nullptr;
   a.noise_zero = s.noise_mode;
   a.zprev_is_e = use_raw_y;  // only the init draw reads hM$Y (R/computeInitialParameters.R:254)
+  a.mask_na = s.phylo ? 0 : 1;
   a.kt = s.kt_on ? s.d_kt + (size_t)KT_Z * 2 * KT_SLOTS : nullptr;
   dim3 grid(s.ntile_j, nchunk);  // species blocks fastest (z_kernel.h)
   size_t smem = z_smem_bytes(s.K, s.nt);

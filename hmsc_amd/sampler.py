@@ -176,6 +176,16 @@ class Chain:
         self.h = h
         self.rank, self.nranks = rank, nranks
         self.sp0, self.nsl = shard_range(hM.ns, rank, nranks)
+        cap = np.zeros(L.MAX_LEVELS, dtype=np.int32)
+        L.check(self.lib.hmsc_get_nf_cap(self.h, L.iptr(cap)))
+        # factors each level's device buffers and record slots hold (K = nc + sum(nf) <= 64)
+        self.nf_cap = [int(c) for c in cap[: hM.nr]]
+        short = [(r, self.buf.nfMax[r], c) for r, c in enumerate(self.nf_cap) if c < self.buf.nfMax[r]]
+        if short and rank == 0:
+            import warnings
+            warnings.warn("nfMax " + ", ".join(f"{m} of level {r + 1} held as {c}" for r, m, c in short) +
+                          ": this build holds K = nc + sum(nf) <= 64 latent dimensions; the chain stops "
+                          "with an error only if updateNf must grow a level past that", stacklevel=2)
 
     def close(self):
         if self.h:
@@ -317,13 +327,18 @@ class Chain:
         L.check(self.lib.hmsc_debug_get(self.h, name.encode(), L.fptr(out), int(n)))
         return out
 
+    def debug_poison(self, what):
+        """Test hook (hmsc_debug_poison): corrupt one in-launch handshake ("trsv_ticket",
+        "chol_publish") so the next launch using it must time out and report."""
+        L.check(self.lib.hmsc_debug_poison(self.h, what.encode()))
+
     def run(self, transient, samples, thin=1, adaptNf=None, iter0=0, verbose=0, chain=1, record=True, fields=None):
         """hmsc_run: the device sweep loop with recording; returns the raw record arrays.
         fields: record only these (e.g. ("Beta",)); None records everything."""
         hM = self.hM
         nr = hM.nr
         ns = self.nsl
-        nfMax = self.buf.nfMax
+        nfMax = self.nf_cap   # record slots are strided by the device's per-level factor capacity
         adapt = L.i32(adaptNf if adaptNf is not None else [transient] * max(1, nr))
         rec = None
         arrays = None

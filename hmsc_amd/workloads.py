@@ -132,6 +132,30 @@ def vignette3_phylo(ns=300, ny=200, seed=SYNTHETIC_SEED):
                 Tr=Tr, C=C, distr="normal", studyDesign=study, ranLevels={"sample": rl})
 
 
+def vignette3_ma500(ns=50, ny=200, seed=SYNTHETIC_SEED, na_frac=0.0):
+    """vignette_3's ``ma500`` (vignettes/vignette_3_multivariate_high.Rmd:445-453): the data of
+    vignette3_phylo, XFormula.1 = ~poly(climate, degree = 2, raw = TRUE) (nc = 3), the same
+    traits and phylogeny, and a FRESH HmscRandomLevel with setPriors(a1 = 500, a2 = 500) only --
+    R's default nfMin = 2 and nfMax = Inf (= ns, R/Hmsc.R:554) and default updaters (GammaEta
+    and Rho on).  na_frac > 0 blanks that share of Y cells (NA), the phylogeny-with-NA case."""
+    base = vignette3_phylo(ns=ns, ny=ny, seed=seed)
+    rng = np.random.default_rng(seed + 1)
+    X = base.X[:, [0, 2, 3]]   # intercept, climate, climate^2 (no habitat)
+    Y = np.array(base.Y, dtype=np.float64)
+    if na_frac > 0:
+        Y[rng.random(Y.shape) < na_frac] = np.nan
+    units = np.array([f"sample_{i:03d}" for i in range(1, ny + 1)])
+    rl = HmscRandomLevel(units=units)
+    setPriors(rl, a1=500, a2=500)
+    try:
+        import pandas as pd
+        study = pd.DataFrame({"sample": units})
+    except Exception:  # pragma: no cover
+        study = {"sample": units}
+    return Hmsc(Y=Y, X=X, covNames=["(Intercept)", "climate", "climate2"], XScale=True, Tr=base.Tr,
+                C=base.C, distr="normal", studyDesign=study, ranLevels={"sample": rl})
+
+
 def vignette2(model="linear", n=100, seed=SYNTHETIC_SEED):
     """BASELINE.json config 2: the models of vignettes/vignette_2_multivariate_low.Rmd with its
     generators (numpy's stream in place of R's set.seed):

@@ -156,18 +156,19 @@ typedef struct hmsc_params {
 /* Recording buffers for hmsc_run: caller-allocated, `samples` slots each.  The
  * fields are the raw (scaled-X) state; the host applies combineParameters
  * (R/combineParameters.R:1-58) afterwards.  Eta/Lambda/Psi/Delta/Alpha slots are
- * padded to nfMax[r]; rec_nf[r*samples+k] gives the live nf of sample k. */
+ * padded to nfcap[r] (hmsc_get_nf_cap: min(nfMax[r], the K <= 64 limit)); rec_nf[r*samples+k]
+ * gives the live nf of sample k. */
 typedef struct hmsc_record {
   double* Beta;           /* samples*nc*ns */
   double* Gamma;          /* samples*nc*nt */
   double* iV;             /* samples*nc*nc */
   double* iSigma;         /* samples*ns    */
   int32_t* rho;           /* samples       */
-  double* Eta[HMSC_MAX_LEVELS];     /* samples*np[r]*nfMax[r]  */
-  double* Lambda[HMSC_MAX_LEVELS];  /* samples*nfMax[r]*ns     */
-  double* Psi[HMSC_MAX_LEVELS];     /* samples*nfMax[r]*ns     */
-  double* Delta[HMSC_MAX_LEVELS];   /* samples*nfMax[r]        */
-  int32_t* Alpha[HMSC_MAX_LEVELS];  /* samples*nfMax[r]        */
+  double* Eta[HMSC_MAX_LEVELS];     /* samples*np[r]*nfcap[r]  */
+  double* Lambda[HMSC_MAX_LEVELS];  /* samples*nfcap[r]*ns     */
+  double* Psi[HMSC_MAX_LEVELS];     /* samples*nfcap[r]*ns     */
+  double* Delta[HMSC_MAX_LEVELS];   /* samples*nfcap[r]        */
+  int32_t* Alpha[HMSC_MAX_LEVELS];  /* samples*nfcap[r]        */
   int32_t* rec_nf;                  /* nr*samples              */
 } hmsc_record;
 
@@ -180,7 +181,7 @@ const char* hmsc_last_error(void);
 int hmsc_device_count(int32_t* n);
 
 /* Create one chain's device state: copies the model, allocates HBM for the state
- * at nfMax, keys Philox by `seed` (R: set.seed(initSeed[chain]), R/sampleMcmc.R:158).
+ * at nfcap (hmsc_get_nf_cap; work buffers of the dense updaters follow the nf in use), keys Philox by `seed` (R: set.seed(initSeed[chain]), R/sampleMcmc.R:158).
  * Replaces the per-chain setup of sampleChain, R/sampleMcmc.R:155-216. */
 int hmsc_create(const hmsc_model* model, uint64_t seed, int32_t device, uint32_t updater_mask,
                 hmsc_state** out);
@@ -217,6 +218,11 @@ int hmsc_init_state(hmsc_state* s, const int32_t* nf0);
 int hmsc_set_state(hmsc_state* s, const hmsc_params* p);
 int hmsc_get_state(hmsc_state* s, hmsc_params* p);
 int hmsc_get_nf(hmsc_state* s, int32_t* nf);
+/* nfcap[r]: the factors level r's buffers and record slots hold, min(nfMax_r, 64 - nc - the
+ * other levels' nfMin) (K = nc + sum(nf) <= 64 in this build).  Below nfMax_r (R's default
+ * nfMax = ns for many species) the run fails with -6 only if updateNf must grow the level
+ * past it.  hmsc_record's per-level arrays are strided by nfcap, not nfMax. */
+int hmsc_get_nf_cap(hmsc_state* s, int32_t* nfcap);
 
 /* The closing step of computeInitialParameters: Z = updateZ(Y = hM$Y, Z = LFix + LRan, ...)
  * at the CURRENT state (R/computeInitialParameters.R:229-254) -- after hmsc_set_state has
@@ -302,7 +308,8 @@ int hmsc_variance_partitioning(const hmsc_vp_args* args, double* out);
  * Levinson-Durbin).  ess[p]; order[p] (may be NULL) the chosen AR orders. */
 int hmsc_effective_size(int32_t device, int32_t n, int32_t p, const double* x, double* ess, int32_t* order);
 
-/* Wait for all device work of this chain. */
+/* Wait for all device work of this chain; fails (-1 not positive definite, -5 a timed-out
+ * in-launch handshake) if any of it raised a device error flag. */
 int hmsc_sync(hmsc_state* s);
 
 /* Capture (without running) the steady-state sweep graphs that hmsc_run replays, so a
@@ -332,6 +339,13 @@ int hmsc_spatial_full_grid(int32_t device, int32_t np, int32_t sdim, const doubl
 /* Copy a named internal device buffer (fp64) for tests / profiling:
  * "Z", "E", "XEtaTZ", "Gram", "ZTr", "BL", "BL_prec" ... ; n = element count. */
 int hmsc_debug_get(hmsc_state* s, const char* name, double* out, int64_t n);
+
+/* Test hook: corrupt one in-launch handshake of this chain so the next launch that uses it
+ * times out (about 1 s) and reports: "trsv_ticket" (the sync-free triangular solve's block
+ * ticket) or "chol_publish" (the blocked Cholesky's fused panel flag, withheld once).  The next
+ * hmsc_run / hmsc_sync / hmsc_get_state then fails with code -5 ("... handshake timed out").
+ * Instrumentation of this port, no reference counterpart. */
+int hmsc_debug_poison(hmsc_state* s, const char* what);
 
 /* predict.Hmsc (R/predict.R:1-231) for a pooled posterior: every sample's
  * L = X Beta + sum_r Eta_r[Pi_r,] Lambda_r, then expected values (pnorm / exp(L + sigma/2) / L)

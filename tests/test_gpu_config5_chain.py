@@ -10,6 +10,8 @@
     (R/updateAlpha.R:20-80: log prior - log det(W)/2 - eta' W^-1 eta / 2) evaluated with
     numpy's Cholesky of W = exp(-d / alpha) itself -- not the device's grid -- puts all but
     e^-8 of its mass on grid point 1 (among the grid points evaluated).
+  * 'NNGP' at ny = 5000: the RCM order and band of the sparse factor, and 300 sweeps from the
+    GPP chain's state against the GPP chain (test_nngp_ny5000_chain_agrees_with_gpp).
   * 'Full' at ny = 5000 (BASELINE's size) started from the state a 'GPP' chain reaches (the
     predictive-process approximation of the same covariance): 300 recorded sweeps stay off grid
     point 1 and their mean alpha is within a factor 2 of the GPP chain's; from Alpha = 1 the
@@ -131,3 +133,52 @@ def test_full_ny5000_from_gpp_state_agrees_with_gpp():
     mf = grid[a_f[150:] - 1].mean()
     assert np.all(a_f > 1), a_f.min()
     assert 0.5 * mg < mf < 2.0 * mg, (mf, mg)
+
+
+def _nngp_order_host(hM, k=10):
+    """The unit order the device factors an NNGP level in, from the host: exact kNN of the
+    level's units (numpy; FNN::get.knn restated, R/computeDataParameters.R:86-104), earlier
+    neighbours only, then the oracle's reverse Cuthill-McKee (oracle.nngp_rcm)."""
+    from hmsc_amd.dataparams import _level_order
+    rl = hM.rL[0]
+    xy = np.asarray(rl.s, dtype=np.float64)[_level_order(hM, 0, rl)]
+    n = xy.shape[0]
+    nb = []
+    for i0 in range(0, n, 500):
+        d = ((xy[i0:i0 + 500, None, :] - xy[None, :, :]) ** 2).sum(-1)
+        for r in range(d.shape[0]):
+            d[r, i0 + r] = np.inf
+        near = np.argpartition(d, k, axis=1)[:, :k]
+        for r in range(d.shape[0]):
+            i = i0 + r
+            nb.append(sorted(int(j) for j in near[r] if j < i))
+    return O.nngp_rcm(nb, n)
+
+
+def test_nngp_ny5000_chain_agrees_with_gpp():
+    """Config 5 with 'NNGP' (R/updateEta.R:137-147, vignettes/vignette_4_spatial.Rmd:177-203) at
+    BASELINE's ny = 5000: the device's factorization order and the banded factor's bandwidth
+    are the reverse Cuthill-McKee order's, 300 recorded sweeps from the GPP chain's state are
+    finite, stay off grid point 1 and their mean alpha is within a factor 2 of the GPP chain's
+    (the two approximate the same exponential covariance)."""
+    a_g, grid, st = _run("GPP", 300)
+    keep = {k: st[k] for k in ("Beta", "Gamma", "iV", "iSigma", "Eta", "Lambda", "Psi", "Delta", "Alpha", "Z")}
+    hM = spatial_vignette4(ny=5000, method="NNGP")
+    ch = H.Chain(hM, 4245, device=0, updater=UPD)
+    ch.init([1])
+    perm = ch.debug_get("nngp_perm0", hM.np[0]).astype(np.int64)
+    bw = int(ch.debug_get("nngp_bw0", 1)[0])
+    perm_h, bw_h = _nngp_order_host(hM)
+    np.testing.assert_array_equal(perm, perm_h)
+    assert bw == bw_h and bw < 500, (bw, bw_h)
+    ch.set_state(keep)
+    rec = ch.run(transient=0, samples=300, thin=1, adaptNf=[0], iter0=0, record=True)
+    g = ch.get_state()
+    ch.close()
+    assert np.all(np.isfinite(rec["Beta"]))
+    assert np.all(np.isfinite(rec["Eta0"])) and np.all(np.isfinite(g["Eta"][0])) and np.all(np.isfinite(g["Z"]))
+    a_n = rec["Alpha0"][:, 0].astype(int)
+    assert np.all(a_n > 1), a_n.min()
+    mg = grid[a_g[150:] - 1].mean()
+    mn = grid[a_n[150:] - 1].mean()
+    assert 0.5 * mg < mn < 2.0 * mg, (mn, mg)
