@@ -710,6 +710,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.CR = dalloc<double>((size_t)s.Kmax * nfm);
   s.CR_part = dalloc<double>((size_t)((nsl + 31) / 32) * s.Kmax * nfm);
   s.LS = dalloc<double>((size_t)std::max(nfm, 16) * nsl);  // [species][16] (cr_body)
+  s.etaW = dalloc<double>(16 * 16);
   s.scratch_doubles = 1 << 20;
   s.scratch = dalloc<double>(s.scratch_doubles);
   s.scratch2 = dalloc<double>(s.scratch_doubles);
@@ -717,7 +718,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.ABpart = dalloc<double>((size_t)((nsl + 31) / 32) * (nc * nc + 2 * N + nfm * nt + 8));
   s.allreduce_buf = dalloc<double>((size_t)nc * nc + 2 * N + nfm * nt + nfm + 64);
   s.dev_flags = dalloc<int>(16);
-  s.gbl_sync = dalloc<int>(4);  // dalloc zero-fills
+  s.gbl_sync = dalloc<int>(8);  // dalloc zero-fills; [4] the CR ticket (cr_finalize)
   s.trsv_sync = dalloc<int>(DENSE_SYNC_INTS);
   s.d_iters = dalloc<uint32_t>(64);  // graph_sweeps <= 64
   s.d_iter = s.d_iters;
@@ -771,7 +772,7 @@ static void free_state(State& s) {
                   s.aSigma, s.bSigma, s.XX, s.TT, s.V0g, s.V0gXXV0g, s.iV0, s.V0inv, s.iUmG, s.V0gXX, s.g2prep, s.scratch2, s.na_cols, s.na_index,
                   s.na_rows, s.row_na, s.row_slot, s.dev_flags, s.gbl_sync, s.trsv_sync, s.Z, s.XEta, s.BL, s.Psi, s.Delta, s.Gamma, s.iV,
                   s.iSigma, s.rho, s.XZ, s.G, s.ZTr, s.XZ_part, s.G_part, s.ZTr_part, s.Gna, s.ZL, s.ZL_part,
-                  s.CR, s.CR_part, s.LS, s.Msmall, s.scratch, s.psi_rs, s.ABpart, s.dbg_prec, s.ring, s.allreduce_buf,
+                  s.CR, s.CR_part, s.LS, s.etaW, s.Msmall, s.scratch, s.psi_rs, s.ABpart, s.dbg_prec, s.ring, s.allreduce_buf,
                   s.phU, s.phWinv, s.phRbase, s.phTt, s.phBt, s.phEt, s.phTTw, s.phWork, s.UGamma, s.geWork};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);

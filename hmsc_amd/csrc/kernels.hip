@@ -1761,10 +1761,74 @@ __device__ __forceinline__ void cr_body(const double* BL, const double* iSigma, 
   }
 }
 
+// The fused Eta kernel's per-sweep constants, formed once instead of in each of its ~600
+// workgroups: the workgroup of the last CR species block to finish (a ticket) reduces the
+// partials in block order into CR (K x NF, ld ldcr) and factors Q = I + Lambda diag(iSigma)
+// Lambda^T (its rows nc.. of CR, one level, nf <= 16) in one wave's registers, writing W =
+// L^-1 (lower, row m at 16 m, zero padded) -- the same algebra and summation order each Eta
+// workgroup ran before.
+struct CRFin {
+  int* ticket;   // zero between launches; reset by the last workgroup
+  int n_cr;
+  double* CR;
+  double* W;     // 16 x 16
+  int nc, nf;
+};
+
+__device__ __forceinline__ void cr_finalize(const CRFin& f, const double* CR_part, int K, int ldcr, int slab) {
+  __shared__ int s_last;
+  __threadfence();  // every wave's partial stores complete at device scope before the ticket
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(f.ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == f.n_cr - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every block's partials
+  __shared__ double sQ[16 * 16];
+  const int t = threadIdx.x, nc = f.nc, nf = f.nf;
+  for (int p = t; p < K * nf; p += 256) {
+    const int kk = p % K, h = p / K;
+    const double* src = CR_part + kk + (size_t)ldcr * h;
+    double v = 0.0;
+    int b = 0;
+    for (; b + 8 <= f.n_cr; b += 8) {
+      double x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = src[(size_t)slab * (b + u)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v += x[u];
+    }
+    for (; b < f.n_cr; ++b) v += src[(size_t)slab * b];
+    f.CR[kk + (size_t)ldcr * h] = v;
+    if (kk >= nc) sQ[(kk - nc) * 16 + h] = v;
+  }
+  __syncthreads();
+  if (t < 64) {  // Q = I + Lambda D Lambda^T, its factor L and W = L^-1 by rows (wave_la.h)
+    __shared__ double sWs[16 * 17];
+    const int lane = t;
+    double q[16], dinv;
+    const int r = lane < nf ? lane : 0;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const double v = (r == c ? 1.0 : 0.0) + sQ[r * 16 + (c < nf ? c : 0)];
+      q[c] = (lane < nf && c < nf) ? v : (lane == c ? 1.0 : 0.0);
+    }
+    wv_chol<16>(q, dinv);
+    double wr[16];
+    wv_inv_lower_rows<16>(q, dinv, wr, sWs);
+    if (lane < 16)
+#pragma unroll
+      for (int c = 0; c < 16; ++c) f.W[lane * 16 + c] = (lane < nf && c < nf && c <= lane) ? wr[c] : 0.0;
+  }
+  if (t == 0) __hip_atomic_store(f.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ __launch_bounds__(256) void cr_kernel(const double* BL, const double* iSigma, int K, int nc, int NF,
-                                                 int ns_loc, double* CR_part, int ldcr, int slab, double* LS) {
+                                                 int ns_loc, double* CR_part, int ldcr, int slab, double* LS,
+                                                 CRFin fin) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   cr_body(BL, iSigma, K, nc, NF, ns_loc, CR_part, ldcr, slab, LS, smem, blockIdx.x);
+  if (fin.ticket) cr_finalize(fin, CR_part, K, ldcr, slab);
 }
 
 struct EtaArgs {
@@ -1965,9 +2029,8 @@ __global__ __launch_bounds__(64) void eta_na_row_kernel(EtaView ev, int r, int n
 struct EtaFArgs {
   const double* Z;
   const double* LS;   // ns_loc x 16: Lambda diag(iSigma), zero past nf (cr_body)
-  const double* CR_part;  // [ncr][slab] species-block partials of CR = BL diag(iSigma) Lambda^T
-  double* CR;         // Kmax x NF (ld ldcr): the reduced CR, written by workgroup 0 (debug / other paths)
-  int ncr, slab;
+  const double* CR;   // Kmax x NF (ld ldcr): CR = BL diag(iSigma) Lambda^T (cr_finalize)
+  const double* W;    // 16 x 16: L^-1 of Q = I + Lambda diag(iSigma) Lambda^T, row m at 16 m (cr_finalize)
   double* XEta;       // ny x K (ld ny)
   const int* Pi;      // ny: unit of each row (0-based)
   double* Eta;        // np x nf
@@ -1985,11 +2048,14 @@ constexpr int EF_SITES = 16;
 // __launch_bounds__(256, 3): <= 168 VGPRs, three waves per SIMD, so the 625 workgroups of the
 // synthetic config (2500 waves) are resident in one round (at 196 VGPRs they took two: 33 ->
 // 29 us).  A fifth wave doing the Z-independent work during the stream measured slower (49 us).
+// The stream's depth: EF_DEPTH 16-species steps' loads in flight per lane before their MFMAs.
+#ifndef EF_DEPTH
+#define EF_DEPTH 12
+#endif
 template <int NFB>
 __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
   __shared__ double sPart[4][16][EF_SITES + 1];  // [wave][factor][site] ZL partials
   __shared__ double sW[NFB * NFB];            // W = L^-1, L the lower factor of Q (row m at m NFB)
-  __shared__ double sWs[NFB * (NFB + 1)];     // wv_inv_lower_rows scratch
   __shared__ double sB[NFB][EF_SITES], sXi[NFB][EF_SITES], sU[NFB][EF_SITES];
   __shared__ double sX[64][EF_SITES + 1];     // XEta tile [k][site] (K <= 64)
   __shared__ double sCR[64 * NFB];            // CR[k][h], k < K
@@ -2013,21 +2079,34 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
     const int p = t + 256 * u, s2 = p % EF_SITES, k = p / EF_SITES, ii = i0 + s2;
     xr[u] = (k < nc && ii < ny) ? a.XEta[ii + (size_t)ny * k] : 0.0;
   }
+  // CR (K x nf) and W (nf x nf) of this sweep, formed once by cr_finalize: loads issued here,
+  // ahead of the stream, stored to LDS after it
+  double crv[4], wv[NFB * NFB / 256 + 1];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int p = t + 256 * u, k = p % K, h = p / K;
+    crv[u] = p < K * nf ? a.CR[k + (size_t)a.ldcr * h] : 0.0;
+  }
+#pragma unroll
+  for (int u = 0; u < NFB * NFB / 256 + 1; ++u) {
+    const int p = t + 256 * u, m = p / NFB, c = p % NFB;
+    wv[u] = p < NFB * NFB ? a.W[m * 16 + c] : 0.0;
+  }
   const double* zc = a.Z + min(i0 + lm, ny - 1);  // sites past ny: any finite row, unused
   const int nsteps = (ns + 15) >> 4;
   int s = 0;
-  for (; s + 8 <= nsteps; s += 8) {
-    double zv[8], lv[8];
+  for (; s + EF_DEPTH <= nsteps; s += EF_DEPTH) {
+    double zv[EF_DEPTH], lv[EF_DEPTH];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < EF_DEPTH; ++u) {
       const int j = 16 * (s + u) + 4 * w + lk;
       zv[u] = j < ns ? zc[(size_t)ny * j] : 0.0;
       lv[u] = j < ns ? a.LS[(size_t)16 * j + lm] : 0.0;
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) acc = mfma_f64(zv[u], lv[u], acc);
+    for (int u = 0; u < EF_DEPTH; ++u) acc = mfma_f64(zv[u], lv[u], acc);
   }
-  if (s < nsteps) {  // the tail: all its loads at once
+  for (; s < nsteps; s += 8) {  // the tail: eight steps' loads at once
     double zv[8], lv[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -2047,62 +2126,31 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
     const int p = t + 256 * u, s2 = p % EF_SITES, k = p / EF_SITES;
     if (k < nc) sX[k][s2] = xr[u];
   }
-  // CR from its species-block partials, in block order (L2; every partial's load in flight
-  // before the adds)
-  for (int p = t; p < K * nf; p += 256) {
-    const int k = p % K, h = p / K;
-    const double* src = a.CR_part + k + (size_t)a.ldcr * h;
-    double v = 0.0;
-    int b = 0;
-    for (; b + 32 <= a.ncr; b += 32) {
-      double x[32];
 #pragma unroll
-      for (int u = 0; u < 32; ++u) x[u] = src[(size_t)a.slab * (b + u)];
+  for (int u = 0; u < 4; ++u) {
+    const int p = t + 256 * u, k = p % K, h = p / K;
+    if (p < K * nf) sCR[k * NFB + h] = crv[u];
+  }
 #pragma unroll
-      for (int u = 0; u < 32; ++u) v += x[u];
-    }
-    for (; b + 8 <= a.ncr; b += 8) {
-      double x[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) x[u] = src[(size_t)a.slab * (b + u)];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v += x[u];
-    }
-    for (; b < a.ncr; ++b) v += src[(size_t)a.slab * b];
-    sCR[k * NFB + h] = v;
-    if (blockIdx.x == 0) a.CR[k + (size_t)a.ldcr * h] = v;
+  for (int u = 0; u < NFB * NFB / 256 + 1; ++u) {
+    const int p = t + 256 * u;
+    if (p < NFB * NFB) sW[p] = wv[u];
   }
   __syncthreads();
   if (blockIdx.x == 0) HMSC_STAMP(51);
-  if (w == 0) {  // Q = I + Lambda D Lambda^T factor, while waves 1-3 form the right-hand sides
-    double q[NFB], dinv;
-    const int r = lane < nf ? lane : 0;
-#pragma unroll
-    for (int c = 0; c < NFB; ++c) {
-      const double v = (r == c ? 1.0 : 0.0) + sCR[(nc + r) * NFB + (c < nf ? c : 0)];
-      q[c] = (lane < nf && c < nf) ? v : (lane == c ? 1.0 : 0.0);
+  // ---- stage 2: b = ZL - X CR_x, and the noise, one (site, factor) per thread
+  for (int p = t; p < EF_SITES * nf; p += 256) {
+    const int s2 = p % EF_SITES, h = p / EF_SITES, ii = i0 + s2;
+    const double zl = (sPart[0][h][s2] + sPart[1][h][s2]) + (sPart[2][h][s2] + sPart[3][h][s2]);
+    double corr = 0.0, xi = 0.0;
+    if (ii < ny) {
+      // X from the tile staged in LDS (a global load per term here waited out one L2
+      // round trip per covariate: ~6 us of the kernel's serial tail)
+      for (int k = 0; k < nc; ++k) corr = fma(sX[k][s2], sCR[k * NFB + h], corr);
+      xi = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)sPi[s2], (uint32_t)h, S_ETA, iter);
     }
-    wv_chol<NFB>(q, dinv);
-    double wr[NFB];
-    wv_inv_lower_rows<NFB>(q, dinv, wr, sWs);  // lane m: row m of L^-1
-    if (lane < NFB)
-#pragma unroll
-      for (int c = 0; c < NFB; ++c) sW[lane * NFB + c] = (lane < nf && c < nf && c <= lane) ? wr[c] : 0.0;
-  } else {
-    // ---- stage 2: b = ZL - X CR_x, and the noise, one (site, factor) per thread
-    for (int p = t - 64; p < EF_SITES * nf; p += 192) {
-      const int s2 = p % EF_SITES, h = p / EF_SITES, ii = i0 + s2;
-      const double zl = (sPart[0][h][s2] + sPart[1][h][s2]) + (sPart[2][h][s2] + sPart[3][h][s2]);
-      double corr = 0.0, xi = 0.0;
-      if (ii < ny) {
-        // X from the tile staged in LDS (a global load per term here waited out one L2
-        // round trip per covariate: ~6 us of the kernel's serial tail)
-        for (int k = 0; k < nc; ++k) corr = fma(sX[k][s2], sCR[k * NFB + h], corr);
-        xi = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)sPi[s2], (uint32_t)h, S_ETA, iter);
-      }
-      sB[h][s2] = zl - corr;
-      sXi[h][s2] = xi;
-    }
+    sB[h][s2] = zl - corr;
+    sXi[h][s2] = xi;
   }
   __syncthreads();
   if (blockIdx.x == 0) HMSC_STAMP(53);
@@ -2167,6 +2215,7 @@ struct PostBLArgs {
   int n_psi;
   const uint32_t* iter_src;  // graph replay: d_iter, snapshotted into iter_side for the side stream
   uint32_t* iter_side;
+  CRFin fin;                 // the fused Eta kernel's CR and W, by the last CR workgroup
 };
 
 __global__ __launch_bounds__(256) void post_bl_kernel(PostBLArgs a) {
@@ -2175,6 +2224,7 @@ __global__ __launch_bounds__(256) void post_bl_kernel(PostBLArgs a) {
   if (b == 0 && threadIdx.x == 0 && a.iter_src) *a.iter_side = *a.iter_src;
   if (b < a.n_cr) {
     cr_body(a.BL, a.iSigma, a.K, a.nc, a.NF, a.ns_loc, a.CR_part, a.ldcr, a.slab, a.LS, smem, b);
+    if (a.fin.ticket) cr_finalize(a.fin, a.CR_part, a.K, a.ldcr, a.slab);
     return;
   }
   b -= a.n_cr;
@@ -2187,6 +2237,7 @@ __global__ __launch_bounds__(256) void post_bl_kernel(PostBLArgs a) {
 
 static bool eta_fused_ok(const State& s);
 static void launch_eta_fused(State& s, uint32_t iter, bool cr_done);
+static CRFin make_cr_fin(const State& s);
 
 bool side_fusion_ok(const State& s) {
   const uint32_t need = HMSC_UP_GAMMAV | HMSC_UP_LAMBDAPRIORS | HMSC_UP_ETA;
@@ -2221,6 +2272,7 @@ void launch_side_fused(State& s, uint32_t iter) {
   a.n_psi = npsi;
   a.iter_src = s.capturing ? s.d_iter : nullptr;
   a.iter_side = s.d_iter_side;
+  a.fin = make_cr_fin(s);
   const size_t smem = std::max((size_t)s.K * SB, (size_t)(2 * s.nc * SB + SB * s.nt)) * sizeof(double);
   post_bl_kernel<<<ncr + ngv + npsi, 256, smem, s.stream>>>(a);
   HIP_OK(hipGetLastError());
@@ -2300,22 +2352,32 @@ static bool eta_fused_ok(const State& s) {
          s.lev[0].nf <= 16 && s.K <= 64 && s.LS != nullptr && !getenv_flag("HMSC_NO_ETA_FUSION");
 }
 
+static CRFin make_cr_fin(const State& s) {
+  CRFin f{};
+  f.ticket = s.gbl_sync + 4;
+  f.n_cr = (s.nsl + SB - 1) / SB;
+  f.CR = s.CR;
+  f.W = s.etaW;
+  f.nc = s.nc;
+  f.nf = s.lev[0].nf;
+  return f;
+}
+
 static void launch_eta_fused(State& s, uint32_t iter, bool cr_done = false) {
   const int ncr = (s.nsl + SB - 1) / SB;
   const int64_t slab = (int64_t)s.Kmax * s.NFmax;
-  if (!cr_done) {  // the CR partials (post_bl_kernel computes them in the co-launched path)
+  if (!cr_done) {  // the CR partials (post_bl_kernel computes them in the co-launched path), CR and W
     cr_kernel<<<ncr, 256, (size_t)s.K * SB * sizeof(double), s.stream>>>(s.BL, s.iSigma, s.K, s.nc, s.NF, s.nsl,
-                                                                           s.CR_part, s.Kmax, (int)slab, s.LS);
+                                                                           s.CR_part, s.Kmax, (int)slab, s.LS,
+                                                                           make_cr_fin(s));
     HIP_OK(hipGetLastError());
   }
   const Level& L = s.lev[0];
   EtaFArgs a{};
   a.Z = s.Z;
   a.LS = s.LS;
-  a.CR_part = s.CR_part;
   a.CR = s.CR;
-  a.ncr = ncr;
-  a.slab = (int)slab;
+  a.W = s.etaW;
   a.XEta = s.XEta;
   a.Pi = L.Pi;
   a.Eta = L.Eta;
@@ -2382,7 +2444,8 @@ void launch_eta(State& s, uint32_t iter) {
     const int ncr = (s.nsl + SB - 1) / SB;
     const int64_t slab = (int64_t)s.Kmax * s.NFmax;
     cr_kernel<<<ncr, 256, (size_t)s.K * SB * sizeof(double), s.stream>>>(s.BL, s.iSigma, s.K, s.nc, s.NF, s.nsl,
-                                                                           s.CR_part, s.Kmax, (int)slab, nullptr);
+                                                                           s.CR_part, s.Kmax, (int)slab, nullptr,
+                                                                           CRFin{});
     HIP_OK(hipGetLastError());
     slab_sum_kernel<<<grid_for(slab), 256, 0, s.stream>>>(s.CR_part, s.CR, slab, ncr, slab);
     HIP_OK(hipGetLastError());

@@ -105,7 +105,7 @@ struct State {
   double *X = nullptr, *Tr = nullptr, *Yval = nullptr, *Yraw = nullptr;
   int8_t* Ycode = nullptr;
   uint64_t* Ybits = nullptr;     // ceil(nsl / 32) x ny: the same codes + 1, 2 bits per species (z kernel)
-  double* logtab = nullptr;      // z_log_table: the z kernel's table log (ZLOG_N x 4)
+  double* logtab = nullptr;      // z_log_table: the z kernel's table log (ZLOG_N x ZLOG_W)
   int* fam = nullptr;            // ns_loc family code
   int* varest = nullptr;         // ns_loc distr[,2]
   double *V0 = nullptr, *iUGamma = nullptr, *mGamma = nullptr, *UGammaL = nullptr, *UGamma = nullptr;
@@ -168,6 +168,7 @@ struct State {
   double* CR = nullptr;          // Kmax x NFmax  BL diag(iSigma) Lambda_all^T
   double* CR_part = nullptr;     // species-block partials of CR
   double* LS = nullptr;          // NFmax x ns_loc  Lambda_all diag(iSigma) (fused Eta kernel)
+  double* etaW = nullptr;        // 16 x 16  L^-1 of Q = I + Lambda diag(iSigma) Lambda^T (fused Eta kernel)
   double* Msmall = nullptr;      // per-level masked row grams (NA rows)
   double* scratch = nullptr;     // single-workgroup updaters
   double* psi_rs = nullptr;      // psi-lambda^2 row-sum partials

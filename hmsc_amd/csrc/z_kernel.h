@@ -59,7 +59,7 @@ struct ZArgs {
   const double* gred_part;
   const double* gred_XX;
   double* gred_G;
-  const double* logtab;  // z_log_table (ZLOG_N x 4 doubles), staged in LDS by every workgroup
+  const double* logtab;  // z_log_table (ZLOG_N x ZLOG_W doubles), staged in LDS by every workgroup
 };
 
 constexpr int ZT_I = 64;   // sites per workgroup tile (4 waves x 16)
@@ -116,23 +116,19 @@ __device__ __noinline__ double z_probit_draw(double e, double sd, double isd, in
 // w >= 6.25) take the scalar path.
 // log x for positive normal x by Tang's table method: x = m 2^e with m in [1, 2), c_j the
 // midpoint of the 1/64-wide interval holding m (its top six mantissa bits), r = (m - c_j) / c_j
-// with |r| <= 1/129, log x = e ln2 + log c_j + log1p(r), log1p by its degree-8 series (|r^9/9|
-// < 1e-20).  The table row j = {1 / c_j, log c_j = hi + lo, 0} lives in LDS (z_log_table fills
-// it on the host in extended precision); ~19 VALU instructions, against ~33 for log_fast's
-// reciprocal and degree-10 atanh series.
+// with |r| <= 1/129, log x = e ln2 + log c_j + log1p(r), log1p by its degree-5 series (|r^6/6|
+// < 4e-14 absolute).  The table row j = {1 / c_j, log c_j} (16 bytes: one ds_read_b128) lives
+// in LDS (z_log_table fills it on the host in extended precision); ~14 VALU instructions.
 constexpr int ZLOG_N = 64;
+constexpr int ZLOG_W = 2;  // doubles per table row
 inline void z_log_table(double* t) {
   for (int j = 0; j < ZLOG_N; ++j) {
     const long double c = 1.0L + (2 * j + 1) / 128.0L;
-    const long double l = logl(c);
-    t[4 * j] = (double)(1.0L / c);
-    t[4 * j + 1] = (double)l;
-    t[4 * j + 2] = (double)(l - (long double)t[4 * j + 1]);
-    t[4 * j + 3] = 0.0;
+    t[ZLOG_W * j] = (double)(1.0L / c);
+    t[ZLOG_W * j + 1] = (double)logl(c);
   }
 }
-HMSC_TABLE double kLog1pSeries[8] = {-1.0 / 8.0, 1.0 / 7.0, -1.0 / 6.0, 1.0 / 5.0,
-                                     -1.0 / 4.0, 1.0 / 3.0, -1.0 / 2.0, 1.0};
+HMSC_TABLE double kLog1pSeries[5] = {1.0 / 5.0, -1.0 / 4.0, 1.0 / 3.0, -1.0 / 2.0, 1.0};
 __device__ __forceinline__ double log_tab(double x, const double* tab) {
   const int e = __builtin_amdgcn_frexp_exp(x) - 1;        // x = m2 2^e, m2 in [1, 2)
   const double m2 = 2.0 * __builtin_amdgcn_frexp_mant(x);
@@ -143,13 +139,13 @@ __device__ __forceinline__ double log_tab(double x, const double* tab) {
   const uint64_t cb = (uint64_t)((hi & 0xFFFFC000u) | 0x2000u) << 32;  // c_j = 1 + j / 64 + 1 / 128
   double c;
   __builtin_memcpy(&c, &cb, 8);
-  const double* tj = tab + 4 * j;
+  const double* tj = tab + ZLOG_W * j;
   const double r = (m2 - c) * tj[0];                      // m2 - c_j exact
   double P = kLog1pSeries[0];
 #pragma unroll
-  for (int k = 1; k < 8; ++k) P = fma_sc(P, r, kLog1pSeries[k]);
+  for (int k = 1; k < 5; ++k) P = fma_sc(P, r, kLog1pSeries[k]);
   const double de = (double)e;
-  return fma(de, 0.6931471803691238, tj[1]) + fma(r, P, fma(de, 1.9082149292705877e-10, tj[2]));
+  return fma(de, 0.6931471803691238, tj[1]) + fma(r, P, de * 1.9082149292705877e-10);
 }
 
 struct ZPair {
@@ -173,7 +169,7 @@ __device__ __forceinline__ ZPair z_probit_pair(double e0, double e1, double sd0,
     const double x0 = 2.0 * t0 - 1.0, x1 = 2.0 * t1 - 1.0;
     double g0 = kErfcPoly[0], g1 = kErfcPoly[0];
 #pragma unroll
-    for (int k = 1; k < 25; ++k) {
+    for (int k = 1; k < ERFC_NC; ++k) {
       g0 = fma_sc(g0, x0, kErfcPoly[k]);
       g1 = fma_sc(g1, x1, kErfcPoly[k]);
     }
@@ -186,7 +182,7 @@ __device__ __forceinline__ ZPair z_probit_pair(double e0, double e1, double sd0,
     const double y0 = w0 - 3.125, y1 = w1 - 3.125;
     double F0 = kQnormA[0], F1 = kQnormA[0];
 #pragma unroll
-    for (int k = 1; k < 23; ++k) {
+    for (int k = 1; k < QNA_NC; ++k) {
       F0 = fma_sc(F0, y0, kQnormA[k]);
       F1 = fma_sc(F1, y1, kQnormA[k]);
     }
@@ -199,7 +195,7 @@ __device__ __forceinline__ ZPair z_probit_pair(double e0, double e1, double sd0,
       const double sw0 = sqrt(fmax(w0, 6.25)) - 3.25, sw1 = sqrt(fmax(w1, 6.25)) - 3.25;
       double B0 = kQnormB[0], B1 = kQnormB[0];
 #pragma unroll
-      for (int k = 1; k < 19; ++k) {
+      for (int k = 1; k < QNB_NC; ++k) {
         B0 = fma_sc(B0, sw0, kQnormB[k]);
         B1 = fma_sc(B1, sw1, kQnormB[k]);
       }
@@ -298,12 +294,12 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
   double* sSd = sTr + ZT_J * a.nt;                  // [32] iSigma^-1/2
   double* sIsd = sSd + ZT_J;                        // [32] iSigma^1/2
   int* sFam = (int*)(sIsd + ZT_J);                  // [32]
-  double* sLog = (double*)(sFam + ZT_J);            // [ZLOG_N][4] log table (log_tab)
+  double* sLog = (double*)(sFam + ZT_J);            // [ZLOG_N][ZLOG_W] log table (log_tab)
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, lm = lane & 15, lk = lane >> 4;
   // the Philox sweep counter, read once (a load inside the site loop would wait, vmcnt(0),
   // behind every Z store in flight)
   const uint32_t iter = SWEEP_ITER(a);
-  double* sT = sLog + 4 * ZLOG_N + w * (ZT_J * ZT_TLD);  // this wave's tile: E, then Z
+  double* sT = sLog + ZLOG_W * ZLOG_N + w * (ZT_J * ZT_TLD);  // this wave's tile: E, then Z
   const int j0 = by * ZT_J;
   for (int p = t; p < K16 * ZT_J; p += 256) {
     const int k = p >> 5, jj = p & 31, j = j0 + jj;
@@ -321,7 +317,7 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
     sFam[t] = (j < a.ns_loc) ? a.fam[j] : 0;
   }
   if (DRAW && (MODE & 2))
-    for (int p = t; p < 4 * ZLOG_N; p += 256) sLog[p] = a.logtab[p];
+    for (int p = t; p < ZLOG_W * ZLOG_N; p += 256) sLog[p] = a.logtab[p];
   __syncthreads();
 
   d4 acc[NKB][2];
@@ -511,7 +507,7 @@ inline int z_nkb(int K) { return (K + 15) / 16; }
 
 inline size_t z_smem_bytes(int K, int nt) {
   const size_t K16 = 16 * (size_t)z_nkb(K);
-  const size_t body = K16 * ZT_J + (size_t)ZT_J * nt + 2 * ZT_J + ZT_J / 2 + 4 * (size_t)ZLOG_N +
+  const size_t body = K16 * ZT_J + (size_t)ZT_J * nt + 2 * ZT_J + ZT_J / 2 + ZLOG_W * (size_t)ZLOG_N +
                       4 * (size_t)ZT_J * ZT_TLD;  // doubles
   const size_t red = 3 * K16 * ZT_J;                                                                   // wave combine
   return (body > red ? body : red) * sizeof(double);

@@ -139,7 +139,7 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   }
 }
 
-int z_log_table_doubles() { return 4 * ZLOG_N; }
+int z_log_table_doubles() { return ZLOG_W * ZLOG_N; }
 void z_log_table_fill(double* t) { z_log_table(t); }
 
 void launch_update_z(State& s, uint32_t iter, bool use_raw_y) {

@@ -12,7 +12,7 @@ import mpmath as mp
 import numpy as np
 from numpy.polynomial import chebyshev as C
 
-DEG = 24
+DEG = 20
 mp.mp.dps = 40
 
 

@@ -77,7 +77,7 @@ def qnorm_fast(p, cA, cB):
 
 
 if __name__ == "__main__":
-    degA, degB = (int(a) for a in sys.argv[1:3]) if len(sys.argv) > 2 else (22, 18)
+    degA, degB = (int(a) for a in sys.argv[1:3]) if len(sys.argv) > 2 else (18, 14)
     cA = fit(lambda v: v, 0.0, 6.25, degA, center=3.125)
     cB = fit(lambda v: v * v, 2.5, 4.0, degB, center=3.25)
     rng = np.random.default_rng(0)

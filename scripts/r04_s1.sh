@@ -6,6 +6,8 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r04_s1}
 mkdir -p $R/gpurun_out
 cd $R
+timeout -k 10 60 ./scripts/ubench_rates > gpurun_out/${TAG}_rates.log 2>&1 && cat gpurun_out/${TAG}_rates.log
+timeout -k 10 120 ./scripts/ubench_parts > gpurun_out/${TAG}_parts.log 2>&1 && cat gpurun_out/${TAG}_parts.log
 timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1
 rc=$?
 tail -3 gpurun_out/${TAG}_pytest.log

@@ -19,9 +19,9 @@ __global__ __launch_bounds__(256, 4) void parts_kernel(const double* Etab, const
                                                        double* out, const double* LT) {
   __shared__ double sE[NTAB];
   __shared__ int sC[NTAB];
-  __shared__ double sLog[4 * ZLOG_N];
+  __shared__ double sLog[ZLOG_W * ZLOG_N];
   for (int p = threadIdx.x; p < NTAB; p += 256) sE[p] = Etab[p], sC[p] = Ctab[p];
-  for (int p = threadIdx.x; p < 4 * ZLOG_N; p += 256) sLog[p] = LT[p];
+  for (int p = threadIdx.x; p < ZLOG_W * ZLOG_N; p += 256) sLog[p] = LT[p];
   __syncthreads();
   double acc = 0.0;
   const int stride = gridDim.x * blockDim.x;
@@ -49,7 +49,7 @@ __global__ __launch_bounds__(256, 4) void parts_kernel(const double* Etab, const
       const double x0 = 2.0 * t0 - 1.0, x1 = 2.0 * t1 - 1.0;
       double g0 = kErfcPoly[0], g1 = kErfcPoly[0];
 #pragma unroll
-      for (int k = 1; k < 25; ++k) {
+      for (int k = 1; k < ERFC_NC; ++k) {
         g0 = fma_sc(g0, x0, kErfcPoly[k]);
         g1 = fma_sc(g1, x1, kErfcPoly[k]);
       }
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256, 4) void parts_kernel(const double* Etab, const
       const double y0 = u.a * 6.0 - 3.125, y1 = u.b * 6.0 - 3.125;
       double F0 = kQnormA[0], F1 = kQnormA[0];
 #pragma unroll
-      for (int k = 1; k < 23; ++k) {
+      for (int k = 1; k < QNA_NC; ++k) {
         F0 = fma_sc(F0, y0, kQnormA[k]);
         F1 = fma_sc(F1, y1, kQnormA[k]);
       }
@@ -74,8 +74,8 @@ __global__ __launch_bounds__(256, 4) void parts_kernel(const double* Etab, const
 // accuracy of log_tab against the device libm log over x = 2^(-k / 64) (k < 64 * 1000) and
 // x = 1 - j 2^-20 (j < 4096): max absolute and relative error
 __global__ void logacc_kernel(const double* LT, double* out) {
-  __shared__ double sLog[4 * ZLOG_N];
-  for (int p = threadIdx.x; p < 4 * ZLOG_N; p += blockDim.x) sLog[p] = LT[p];
+  __shared__ double sLog[ZLOG_W * ZLOG_N];
+  for (int p = threadIdx.x; p < ZLOG_W * ZLOG_N; p += blockDim.x) sLog[p] = LT[p];
   __syncthreads();
   double ea = 0.0, er = 0.0;
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < 64 * 1000 + 4096; k += gridDim.x * blockDim.x) {
@@ -126,7 +126,7 @@ int main() {
   (void)hipMemcpy(E, hE.data(), NTAB * 8, hipMemcpyHostToDevice);
   (void)hipMemcpy(C, hC.data(), NTAB * 4, hipMemcpyHostToDevice);
   {
-    std::vector<double> lt(4 * ZLOG_N);
+    std::vector<double> lt(ZLOG_W * ZLOG_N);
     z_log_table(lt.data());
     (void)hipMalloc(&g_lt, lt.size() * 8);
     (void)hipMemcpy(g_lt, lt.data(), lt.size() * 8, hipMemcpyHostToDevice);

@@ -38,7 +38,7 @@ def test_poisoned_handshake_is_reported(what):
     ch.sync()                                    # clean: no flag raised
     ch.debug_poison(what)
     ch.update("BetaLambda", 2)
-    with pytest.raises(HmscNativeError, match="handshake timed out") as ei:
+    with pytest.raises(HmscNativeError, match=r"handshake.*timed out") as ei:
         ch.sync()
     assert "error -5" in str(ei.value)
     assert "not positive definite" not in str(ei.value)
@@ -48,7 +48,7 @@ def test_poisoned_handshake_is_reported(what):
 def test_poisoned_handshake_fails_the_run():
     ch = _blocked_phylo_chain()
     ch.debug_poison("trsv_ticket")
-    with pytest.raises(HmscNativeError, match="handshake timed out"):
+    with pytest.raises(HmscNativeError, match=r"handshake.*timed out"):
         ch.run(transient=1, samples=1, thin=1)
     ch.close()
 

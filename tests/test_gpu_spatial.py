@@ -23,8 +23,9 @@ MODELS = {
     "td_like": dict(ny=50, ns=4, nc=3, nf=2, nr=2, units=[50, 10], spatial=[1], seed=51, alpha_n=30),
     # observation-level spatial factors (np = ny), the default 101-point grid
     "obs_level": dict(ny=40, ns=6, nc=2, nf=2, nr=1, spatial=[0], seed=52),
-    # NNGP (R/computeDataParameters.R:82-136) reaches the device as the dense prior precision
-    # of its grid, GPP (:138-194) as R's low-rank arrays, sampled in R's form on both sides
+    # NNGP (R/computeDataParameters.R:82-136) reaches the device as the unit coordinates: the
+    # library builds the sparse Vecchia factor and factors the banded precision in reverse
+    # Cuthill-McKee order (spatial.hip); GPP (:138-194) as R's low-rank arrays, sampled in R's form on both sides
     # (R/updateEta.R:148-196: oracle gpp_eta_literal, spatial.hip gpp_*); the oracle's GPP
     # updateAlpha is R's literal knot formula (R/updateAlpha.R:35-75)
     "nngp": dict(ny=40, ns=6, nc=2, nf=2, nr=1, spatial=[0], seed=53, spatial_method="NNGP", n_neighbours=6),
