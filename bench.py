@@ -49,6 +49,9 @@ def parse():
                         "phylo: config 3, vignette_3 (phylogeny, traits, GammaEta) at --ns species")
     p.add_argument("--method", choices=["Full", "NNGP", "GPP"], default="Full",
                    help="config 5's spatial method (vignettes/vignette_4_spatial.Rmd:95-245)")
+    p.add_argument("--spatial-start", choices=["gpp", "init"], default="gpp",
+                   help="config 5 Full / NNGP: start from the state of 300 GPP sweeps (mixing) or from "
+                        "computeInitialParameters (Alpha stuck at grid point 1 for hundreds of sweeps)")
     p.add_argument("--ny", type=int, default=10000)
     p.add_argument("--ns", type=int, default=1000)
     p.add_argument("--nc", type=int, default=20)
@@ -300,8 +303,25 @@ def main_spatial(args):
     ny = 5000 if args.ny == 10000 else args.ny
     hM = spatial_vignette4(ny=ny, method=args.method)
     t0 = time.perf_counter()
+    start_state = None
+    if args.method != "GPP" and args.spatial_start == "gpp":
+        # the timed chain starts where a chain mixes, not at Alpha = grid point 1: from
+        # Alpha = 1 the Full / NNGP chain's Eta is drawn under the independent prior and
+        # updateAlpha keeps it there for hundreds of sweeps at this ny (tests/
+        # test_gpu_config5_chain.py), so the state of 300 sweeps of the same model on GPP
+        # (R's predictive-process form, ~0.1 s) is handed over first, outside the timed region
+        hG = spatial_vignette4(ny=ny, method="GPP")
+        cg = H.Chain(hG, 4241 + 7919 * rank, device=local, updater={"GammaEta": False})
+        cg.init([1])
+        cg.run(transient=300, samples=0, thin=1, adaptNf=[0], record=False)
+        sg = cg.get_state()
+        cg.close()
+        start_state = {k: sg[k] for k in ("Beta", "Gamma", "iV", "iSigma", "Eta", "Lambda", "Psi", "Delta",
+                                          "Alpha", "Z")}
     ch = H.Chain(hM, 4242 + 7919 * rank, device=local, updater={"GammaEta": False})
     ch.init([1])
+    if start_state is not None:
+        ch.set_state(start_state)
     ch.sync()
     setup = time.perf_counter() - t0
     ch.run(transient=0, samples=args.warmup, thin=1, adaptNf=[0], record=True)
@@ -388,6 +408,9 @@ def main_spatial(args):
         "roofline": roof,
         "kernels_eager_events_us": {k: round(v["avg_us"], 1) for k, v in kern.items()},
         "alpha_posterior_mean_index": round(alpha_mean, 2),
+        "start": ("state of 300 GPP sweeps of the same model (Alpha index %s)" % (
+            start_state["Alpha"][0].tolist() if start_state is not None else None)) if start_state is not None
+                 else "computeInitialParameters (Alpha = grid point 1)",
         "cpu_baseline": None if (args.no_cpu or world > 1) else cpu_baseline_oracle(
             hM, {"GammaEta": False}, [1], args.cpu_oracle_sweeps or 3, f"vignette_4 '{args.method}' ny={ny}"),
     }

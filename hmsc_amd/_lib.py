@@ -114,7 +114,8 @@ def lib():
     L.hmsc_set_state.argtypes = [C.c_void_p, C.POINTER(hmsc_params)]
     L.hmsc_get_state.argtypes = [C.c_void_p, C.POINTER(hmsc_params)]
     L.hmsc_get_nf.argtypes = [C.c_void_p, ip]
-    L.hmsc_get_nf_cap.argtypes = [C.c_void_p, ip]
+    if hasattr(L, "hmsc_get_nf_cap"):  # (absent from a pre-round-4 library loaded for A/B timing)
+        L.hmsc_get_nf_cap.argtypes = [C.c_void_p, ip]
     L.hmsc_sweep.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
     L.hmsc_update.argtypes = [C.c_void_p, C.c_uint32, C.c_int32]
     L.hmsc_set_noise_mode.argtypes = [C.c_void_p, C.c_int32]
@@ -123,7 +124,8 @@ def lib():
                                    C.c_int32, C.POINTER(hmsc_record)]
     L.hmsc_sync.argtypes = [C.c_void_p]
     L.hmsc_debug_get.argtypes = [C.c_void_p, C.c_char_p, dp, C.c_int64]
-    L.hmsc_debug_poison.argtypes = [C.c_void_p, C.c_char_p]
+    if hasattr(L, "hmsc_debug_poison"):
+        L.hmsc_debug_poison.argtypes = [C.c_void_p, C.c_char_p]
     L.hmsc_profile.argtypes = [C.c_void_p, C.c_int32]
     L.hmsc_profile_get.argtypes = [C.c_void_p, C.c_int32, dp, ip]
     L.hmsc_kernel_timing.argtypes = [C.c_void_p, C.c_int32]

@@ -711,6 +711,16 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.CR_part = dalloc<double>((size_t)((nsl + 31) / 32) * s.Kmax * nfm);
   s.LS = dalloc<double>((size_t)std::max(nfm, 16) * nsl);  // [species][16] (cr_body)
   s.etaW = dalloc<double>(16 * 16);
+  {  // crw_kernel: 4 parts x 4 tiles x 16 x 16; crw_tail: (nbl + ngroups) tiles of 512
+    const size_t nbl = (size_t)(nsl + 3) / 4, ngr = (nbl + 15) / 16;
+    s.crw_part = dalloc<double>(std::max((size_t)4 * 4 * 256, (nbl + ngr) * 512));
+    s.crw_ticket = dalloc<int>(2 + ngr);  // dalloc zero-fills
+    s.gvt_ld = nc * nc + N + nfm;             // [A nc^2 | BTr nc nt | rs NF]
+    s.gvt = dalloc<double>((nbl + ngr) * (size_t)s.gvt_ld);
+  }
+  s.side_sync = dalloc<int>(2 + HMSC_MAX_LEVELS);
+  s.Gamma_side = dalloc<double>(N);
+  if (const char* e = std::getenv("HMSC_SIDE_EDGES")) s.edge_free = e[0] != '1';
   s.scratch_doubles = 1 << 20;
   s.scratch = dalloc<double>(s.scratch_doubles);
   s.scratch2 = dalloc<double>(s.scratch_doubles);
@@ -718,7 +728,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.ABpart = dalloc<double>((size_t)((nsl + 31) / 32) * (nc * nc + 2 * N + nfm * nt + 8));
   s.allreduce_buf = dalloc<double>((size_t)nc * nc + 2 * N + nfm * nt + nfm + 64);
   s.dev_flags = dalloc<int>(16);
-  s.gbl_sync = dalloc<int>(8);  // dalloc zero-fills; [4] the CR ticket (cr_finalize)
+  s.gbl_sync = dalloc<int>(4);  // dalloc zero-fills
   s.trsv_sync = dalloc<int>(DENSE_SYNC_INTS);
   s.d_iters = dalloc<uint32_t>(64);  // graph_sweeps <= 64
   s.d_iter = s.d_iters;
@@ -772,7 +782,7 @@ static void free_state(State& s) {
                   s.aSigma, s.bSigma, s.XX, s.TT, s.V0g, s.V0gXXV0g, s.iV0, s.V0inv, s.iUmG, s.V0gXX, s.g2prep, s.scratch2, s.na_cols, s.na_index,
                   s.na_rows, s.row_na, s.row_slot, s.dev_flags, s.gbl_sync, s.trsv_sync, s.Z, s.XEta, s.BL, s.Psi, s.Delta, s.Gamma, s.iV,
                   s.iSigma, s.rho, s.XZ, s.G, s.ZTr, s.XZ_part, s.G_part, s.ZTr_part, s.Gna, s.ZL, s.ZL_part,
-                  s.CR, s.CR_part, s.LS, s.etaW, s.Msmall, s.scratch, s.psi_rs, s.ABpart, s.dbg_prec, s.ring, s.allreduce_buf,
+                  s.CR, s.CR_part, s.LS, s.etaW, s.crw_part, s.crw_ticket, s.gvt, s.side_sync, s.Gamma_side, s.Msmall, s.scratch, s.psi_rs, s.ABpart, s.dbg_prec, s.ring, s.allreduce_buf,
                   s.phU, s.phWinv, s.phRbase, s.phTt, s.phBt, s.phEt, s.phTTw, s.phWork, s.UGamma, s.geWork};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -1231,14 +1241,17 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
   try {
     for (int i = 0; i < nsweeps; ++i) {
       s.d_iter = s.d_iters + i;
+      s.cap_sweep = i;
       s.pack_req = with_record;
       s.pack_done = false;
       sweep(s, iter, false);
       if (with_record) record_after_sweep(s, nullptr);
     }
     s.d_iter = s.d_iters;
+    s.cap_sweep = -1;
     join_side(s);
   } catch (...) {
+    s.cap_sweep = -1;
     s.d_iter = s.d_iters;
     s.pack_req = s.pack_done = false;
     s.capturing = false;
@@ -1579,7 +1592,10 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
   if (recording) set_desc_kernel<<<1, 1, 0, s.stream>>>(s.d_rec_desc, iter0, transient, thin, samples);
   // the fused Gamma2 + BetaLambda flag holds the epoch of the last sweep that published: a
   // run's sweeps are distinct, but an earlier run may have ended on one of them
-  if (s.gbl_sync) HIP_OK(hipMemsetAsync(s.gbl_sync + 1, 0, sizeof(int), s.stream));
+  // (the same for the tails epoch and the side chain's flags, graph sweeps' device-side joins)
+  join_side(s);
+  if (s.gbl_sync) HIP_OK(hipMemsetAsync(s.gbl_sync + 1, 0, 2 * sizeof(int), s.stream));
+  if (s.side_sync) HIP_OK(hipMemsetAsync(s.side_sync, 0, (2 + HMSC_MAX_LEVELS) * sizeof(int), s.stream));
   const auto t_start = std::chrono::steady_clock::now();
   for (int it = 1; it <= total;) {
     const int G = s.graph_sweeps;

@@ -50,6 +50,24 @@ __device__ inline void kt_record(unsigned long long* kt, uint32_t iter, unsigned
   __hip_atomic_fetch_max(kt + KT_SLOTS + slot, t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// A device-scope (L2-bypassing) load of a value another workgroup of the same launch, on
+// any XCD, published behind a flag: the reader polls the flag relaxed and then loads with
+// these, instead of an acquire fence that would invalidate its XCD's whole L2.
+__device__ __forceinline__ double load_coherent(const double* p) {
+  return __longlong_as_double(
+      (long long)__hip_atomic_load((const unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+// ... and its producer side: a device-scope (write-through) store.  A workgroup publishes a
+// tile of these with vm_stores_done() + __syncthreads() + a relaxed ticket, without the
+// release fence's write-back of the whole L2 (buffer_wbl2, ~0.1-1 us each under load, once
+// per wave) that __threadfence() would cost.
+__device__ __forceinline__ void store_coherent(double* p, double v) {
+  __hip_atomic_store((unsigned long long*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+// this wave's vector memory operations (the coherent stores above) have completed
+__device__ __forceinline__ void vm_stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // Diagnostic build only (python -m hmsc_amd.build --stamps -> libhmsc_amd_stamps.so):
 // HMSC_STAMP(i) records the shader clock (s_memtime) of lane 0 of the calling workgroup
 // into slot i of a device table read back with hmsc_debug_get(s, "stamps", ...).  The

@@ -635,11 +635,6 @@ __global__ __launch_bounds__(256) void trsv_bwd_kernel(const double* L, int lda,
 // sync (the DENSE_SYNC_INTS block of state.h, zeroed once): [0] ticket, [1] done count, [2 + b]
 // flag of block b, [DENSE_SYNC_ERR] the handshake error word.
 
-__device__ __forceinline__ double load_coherent(const double* p) {
-  return __longlong_as_double(
-      (long long)__hip_atomic_load((const unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-
 __device__ __forceinline__ void wait_flag(const int* f, int* sync) {
   hs_wait(f, [](int v) { return v != 0; }, sync, HS_ERR_TRSV_FLAG);
 }

@@ -310,8 +310,33 @@ __device__ __host__ inline int g2bl_epoch(uint32_t iter) { return (int)(iter | 0
 // WAIT_GAMMA (the fused Gamma2 + BetaLambda launch, gamma2_bl_kernel): the new Gamma is
 // published by another workgroup of the same launch (gsync[1]); everything that does not
 // depend on it -- the prologue, iU and its Cholesky factor -- runs first.
+// Bounded wait (every thread) until flags[0 .. n-1] all hold `epoch`; a wait that outlasts the
+// bound raises the launch's handshake error word (err[3], reported as error -5 by the host)
+// and goes on.  Relaxed polls: the data behind the flags is read with load_coherent.
+__device__ __forceinline__ void side_wait(const int* flags, int n, int epoch, int* err) {
+  for (int q = 0; q < n; ++q)
+    for (int spin = 0; __hip_atomic_load(&flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch; ++spin) {
+      if (spin > (1 << 20)) {
+        __hip_atomic_store(&err[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+}
+
+// What the fused launch's tail (bl_tail) needs of a species' update, lane k holding row k:
+// the new column BL[:, j], Mu_j = Gamma Tr_j^T (rows < nc) and tau = cumprod(Delta) (rows >= nc)
+struct BLCol {
+  double r, mu, tau;
+};
+
+// side_wait (the fused launch inside a sweep graph, sweeps after the first): iV and Delta come
+// from the previous sweep's side chain, which publishes them through side_sync instead of a
+// cross-queue graph edge; they are read with device-coherent loads after its flags.
 template <int NM, bool WAIT_GAMMA>
-__device__ __forceinline__ void beta_lambda_wave_body(const BLArgs& a, double* lds0, int blk, int* gsync) {
+__device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* lds0, int blk, int* gsync,
+                                                       const int* side_sync = nullptr, int side_epoch = 0,
+                                                       int side_n = 0) {
   double* tiles = lds0;
   double* sG = tiles + 4 * WV_TILE;
   double* sIV = sG + 32 * 33;
@@ -321,6 +346,7 @@ __device__ __forceinline__ void beta_lambda_wave_body(const BLArgs& a, double* l
   const int K = a.K, nc = a.nc, nt = a.nt, i = lane_id(), w = threadIdx.x >> 6, t = threadIdx.x;
   const int j = blk * 4 + w;
   if (blk == 0) HMSC_STAMP(60);
+  if (side_n > 0) side_wait(side_sync, side_n, side_epoch, gsync);
   // every global load of the prologue is issued before the first LDS store (a staging loop
   // with a store per iteration waits out one memory latency per iteration)
   double gv[4], ivv[4];
@@ -328,10 +354,11 @@ __device__ __forceinline__ void beta_lambda_wave_body(const BLArgs& a, double* l
   for (int u = 0; u < 4; ++u) {
     const int p = t + 256 * u, pc = p < K * K ? p : 0;
     gv[u] = a.G[pc % K + (size_t)a.Kmax * (pc / K)];
-    ivv[u] = a.iV[p < nc * nc ? p : 0];
+    ivv[u] = side_n > 0 ? load_coherent(a.iV + (p < nc * nc ? p : 0)) : a.iV[p < nc * nc ? p : 0];
   }
   const double gam = WAIT_GAMMA ? 0.0 : a.Gamma[t < nc * nt ? t : 0];
-  const double del = a.NF > 0 ? a.Delta[t < a.NF ? t : 0] : 1.0;
+  const double* dp = a.Delta + (t < a.NF ? t : 0);
+  const double del = a.NF > 0 ? (side_n > 0 ? load_coherent(dp) : *dp) : 1.0;
   // this species' own inputs, loaded before the barrier so their latency overlaps it
   const int jj = j < a.ns_loc ? j : a.ns_loc - 1;
   const double isig = a.iSigma[jj];
@@ -350,7 +377,7 @@ __device__ __forceinline__ void beta_lambda_wave_body(const BLArgs& a, double* l
   if (!WAIT_GAMMA && t < nc * nt && t < 32 * 8) sGam[t] = gam;
   if (t < a.NF) sTau[t] = del;  // Delta here; each lane forms its own cumprod below
   __syncthreads();
-  if (j >= a.ns_loc) return;
+  if (j >= a.ns_loc) return BLCol{0.0, 0.0, 1.0};
   double* lds = tiles + w * WV_TILE;
   // tau = cumprod(Delta) within the level of factor i - nc   (:51)
   double tau = 1.0;
@@ -442,6 +469,7 @@ __device__ __forceinline__ void beta_lambda_wave_body(const BLArgs& a, double* l
   if (blk == 0) HMSC_STAMP(64);
   if (WAIT_GAMMA && blk == 0 && w == 0) HMSC_STAMP_RT(76);
   if (a.kt && i == 0) kt_record(a.kt, SWEEP_ITER(a), kt0);
+  return BLCol{r, mu, tau};
 }
 
 template <int NM>
@@ -673,7 +701,11 @@ void allreduce_sum(State& s, double* buf, size_t n, hipStream_t st = nullptr);  
 // ---------------------------------------------------------------------------
 struct GVWArgs {
   int nc, nt, ns_glob, nparts, do_prep;
-  const double* part;
+  const double* part;  // nparts species partials [A nc^2 | BTr nc nt], ld part_ld (device-coherent loads)
+  int part_ld;
+  double* Gamma_side;  // copy of the new Gamma for the side stream's record pack, or null
+  int* flags;          // side_sync or null: wave 0 raises flags[0] (Gamma, iV), wave 1 flags[prep_flag]
+  int prep_flag;
   const double* V0;
   double f0;
   const double* iUGamma;
@@ -761,24 +793,26 @@ __device__ __forceinline__ void gammav_body(const GVWArgs& a) {
     // species-block partials in block order, 32 loads in flight (one L2 round trip per 32)
     const double v0 = p < nA ? a.V0[p] : 0.0;
     const double* src = a.part + p;
-    const size_t st = (size_t)(nA + nB);
+    const size_t st = (size_t)a.part_ld;
     double sum = 0.0;
     int b = 0;
+    // (device-coherent loads: the partials may come from another launch still running on
+    // another XCD -- the fused BetaLambda tail -- published by a flag, not a kernel boundary)
     for (; b + 32 <= a.nparts; b += 32) {
       double x[32];
 #pragma unroll
-      for (int u = 0; u < 32; ++u) x[u] = src[st * (b + u)];
+      for (int u = 0; u < 32; ++u) x[u] = load_coherent(src + st * (b + u));
 #pragma unroll
       for (int u = 0; u < 32; ++u) sum += x[u];
     }
     for (; b + 8 <= a.nparts; b += 8) {
       double x[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) x[u] = src[st * (b + u)];
+      for (int u = 0; u < 8; ++u) x[u] = load_coherent(src + st * (b + u));
 #pragma unroll
       for (int u = 0; u < 8; ++u) sum += x[u];
     }
-    for (; b < a.nparts; ++b) sum += src[st * b];
+    for (; b < a.nparts; ++b) sum += load_coherent(src + st * b);
     if (p < nA)
       sA[p] = sum + v0;       // E E^T + V0   (R/updateGammaV.R:18-19)
     else
@@ -848,8 +882,13 @@ __device__ __forceinline__ void gammav_body(const GVWArgs& a) {
     wv_transpose<NM, true>(x, y, SG);
     wv_backward_t<NM>(y, dinv, r);
     if (i < N) a.Gamma[i] = r;
+    if (i < N && a.Gamma_side) a.Gamma_side[i] = r;
     HMSC_STAMP(4);
     if (!ok && i == 0) a.fail[0] = 1;
+    if (a.flags) {  // Gamma and iV are out (the next sweep's fused launch waits on this)
+      __threadfence();
+      if (i == 0) __hip_atomic_store(&a.flags[0], g2bl_epoch(SWEEP_ITER(a)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     return;
   }
 
@@ -888,6 +927,10 @@ __device__ __forceinline__ void gammav_body(const GVWArgs& a) {
       if (k < N) LS[(N - 1 - k) + (size_t)N * (N - 1 - i)] = (k <= i) ? y[k] : 0.0;
   if (!ok2 && i == 0) a.fail[1] = 1;
   HMSC_STAMP_W(14);
+  if (a.flags) {  // Gamma2's prep is out
+    __threadfence();
+    if (i == 0) __hip_atomic_store(&a.flags[a.prep_flag], g2bl_epoch(SWEEP_ITER(a)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 template <int NM>
@@ -903,6 +946,10 @@ static GVWArgs make_gvw_args(State& s, uint32_t iter, const double* part, int np
   w.nparts = np;
   w.do_prep = (s.mask & HMSC_UP_GAMMA2) ? 1 : 0;
   w.part = part;
+  w.part_ld = s.nc * s.nc + s.nc * s.nt;
+  w.Gamma_side = s.Gamma_side;
+  w.flags = nullptr;
+  w.prep_flag = 1 + s.nr;
   w.V0 = s.V0;
   w.f0 = s.f0;
   w.iUGamma = s.iUGamma;
@@ -1272,6 +1319,197 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
 // host at the start of every run and before every eager launch, so it never needs a reset
 // inside the launch.
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// The fused Eta kernel's per-sweep constants (kernels.hip eta_fused_kernel, R/updateEta.R
+// :53-56 for one unstructured level):
+//   CR = BL diag(iSigma) Lambda^T   (K x nf; rows nc.. are Q - I, Q = I + Lambda diag(iSigma) Lambda^T)
+//   W  = L^-1, L L^T = Q            (16 x 16, row m at 16 m, zero padded)
+//   LS = Lambda diag(iSigma)        ([species][16], the Eta stream's MFMA B operand)
+// formed either in the tail of the fused Gamma2 + BetaLambda launch (crw_tail, where each
+// species' new column is still in registers) or, on the other paths, by crw_kernel.
+// ---------------------------------------------------------------------------
+constexpr int CRW_PARTS = 4;    // crw_kernel's workgroups
+constexpr int CRW_GROUP = 16;   // crw_tail: BetaLambda workgroups summed by one group reducer
+constexpr int CRW_TILE = 512;   // crw_tail partial tile: [h < 16][k < 32]
+struct CRWArgs {
+  const double* BL;
+  const double* iSigma;
+  int K, nc, nf, ns, ldcr;
+  double* CR;
+  double* W;
+  double* LS;
+  double* part;  // crw_kernel: CRW_PARTS x (4 x 256); crw_tail: (nbl + ngroups) x CRW_TILE
+  int* ticket;   // [crw_kernel, crw_tail's groups, crw_tail's group tickets ...]; zero between
+                 // launches, each reset by the workgroup that takes its last value
+};
+
+// Q = I + (rows nc.. of CR) -> its Cholesky factor and W = L^-1 by rows, on one wave;
+// sCR is CR in LDS as [row][16], scratch >= 16 x 17 doubles.
+template <int NFB>
+__device__ __forceinline__ void crw_finish(const CRWArgs& a, const double* sCR, double* scratch) {
+  const int lane = lane_id(), nc = a.nc, nf = a.nf;
+  double qv[NFB], dinv;
+  const int r = lane < nf ? lane : 0;
+#pragma unroll
+  for (int c = 0; c < NFB; ++c) {
+    const double v = (r == c ? 1.0 : 0.0) + sCR[(nc + r) * 16 + (c < nf ? c : 0)];
+    qv[c] = (lane < nf && c < nf) ? v : (lane == c ? 1.0 : 0.0);
+  }
+  wv_chol<NFB>(qv, dinv);
+  double wr[NFB];
+  wv_inv_lower_rows<NFB>(qv, dinv, wr, scratch);  // lane m: row m of L^-1
+  if (lane < 16)
+#pragma unroll
+    for (int c = 0; c < 16; ++c)
+      a.W[lane * 16 + c] = (lane < nf && c < NFB && c < nf && c <= lane) ? wr[c < NFB ? c : 0] : 0.0;
+}
+
+// The tail of a BetaLambda workgroup of the fused launch (K <= 32, nf <= 16), with the
+// species' new column still in registers:
+//   * the fused Eta kernel's constants: BL[k, j] iSigma_j Lambda[h, j] and LS (above);
+//   * gv_on: updateGammaV's species sums (R/updateGammaV.R:17-19) -- E E^T, E = Beta - Gamma
+//     Tr^T (Mu_j from the body) and Beta Tr -- and updateLambdaPriors' psi draws (:22-24),
+//     written to Psi, with their per-factor sums psi Lambda^2, as a second partial tile
+//     [A nc^2 | BTr nc nt | rs NF] (ld gvt_ld).  The side chain (GammaV algebra, delta chains)
+//     reads the group tiles of these.
+// The workgroups' four species are summed in LDS; the last workgroup of each group of
+// CRW_GROUP (a ticket) sums the group's tiles in workgroup order, the last group through sums
+// the CR group tiles in group order (deterministic), raises tails_flag (the side chain's
+// start, when it is not behind a graph edge) and factors Q.  No workgroup waits for another:
+// each level's work is done by whichever arrives last.  The tiles cross XCDs as device-scope
+// (write-through) stores and loads, published by relaxed tickets once every wave's stores
+// have completed: no release / acquire fence, whose whole-L2 write-back / invalidate per wave
+// of ~250 workgroups cost ~45 us here.
+struct BLTailArgs {
+  CRWArgs crw;
+  int gv_on;
+  int nt, NF, nr, sp0, gvt_ld;
+  int lev_nf[HMSC_MAX_LEVELS];
+  double nu[HMSC_MAX_LEVELS];
+  const double* Tr;
+  double* Psi;
+  double* gvt;      // (nbl + ngroups) x gvt_ld
+  int* tails_flag;  // epoch of the sweep whose tails are all in
+  Key key;
+};
+
+template <int NFB>
+__device__ void bl_tail(const BLTailArgs& ta, const BLCol col, int b, int nbl, uint32_t iter, double* smem) {
+  __shared__ int s_last;
+  const CRWArgs& a = ta.crw;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, K = a.K, nc = a.nc, nf = a.nf;
+  const int j = 4 * b + w;
+  const bool act = j < a.ns;
+  const double r = col.r;
+  const double isig = act ? a.iSigma[j] : 0.0;
+  const double lam = __shfl(r, nc + (lane & 15));  // lane h: Lambda[h, j]
+  if (act && lane < 16) a.LS[(size_t)16 * j + lane] = lane < nf ? isig * lam : 0.0;
+  const double rk = (act && lane < K) ? r * isig : 0.0;
+  double c[16];
+#pragma unroll
+  for (int h = 0; h < 16; ++h) {
+    const double l = __shfl(r, nc + h < 64 ? nc + h : 0);
+    c[h] = (h < nf) ? rk * l : 0.0;
+  }
+  // GammaV's E = Beta - Gamma Tr^T (lanes < nc) and the psi draw of factor lane - nc
+  const int nt = ta.nt, NF = ta.NF, nA = nc * nc, nB = nc * nt, ngv = nA + nB + NF;
+  const double e = (act && lane < nc) ? r - col.mu : 0.0;
+  double m2 = 0.0;
+  if (ta.gv_on && act && lane >= nc && lane < K) {  // (R/updateLambdaPriors.R:22-24)
+    const int f = lane - nc;
+    int f0 = 0, lv = 0;
+    while (lv < ta.nr - 1 && f >= f0 + ta.lev_nf[lv]) f0 += ta.lev_nf[lv++];
+    const int h = f - f0;
+    const double lam2 = r * r;
+    const double shape = ta.nu[lv] / 2 + 0.5;
+    const double rate = ta.nu[lv] / 2 + 0.5 * lam2 * col.tau;
+    const uint32_t idx = (uint32_t)(h + ta.lev_nf[lv] * (ta.sp0 + j));
+    const double psi = gamma_std(ta.key, idx, S_PSI + LEVEL_STRIDE * lv, iter, shape) / rate;
+    ta.Psi[f + (size_t)NF * j] = psi;
+    m2 = psi * lam2;
+  }
+  __syncthreads();  // every wave is past the body's LDS tiles
+  double* sC = smem;                  // [w][h][k]
+  double* sV = smem + 4 * CRW_TILE;   // [w][ngv]
+  if (lane < 32)
+#pragma unroll
+    for (int h = 0; h < 16; ++h)
+      if (h < nf) sC[w * CRW_TILE + h * 32 + lane] = c[h];
+  if (ta.gv_on) {
+    double* v = sV + w * ngv;
+#pragma unroll
+    for (int c2 = 0; c2 < 32; ++c2) {
+      const double e2 = __shfl(e, c2);
+      if (c2 < nc && lane < nc) v[lane + nc * c2] = e * e2;  // E E^T
+    }
+    if (lane < nc)
+      for (int q = 0; q < nt; ++q) v[nA + lane + nc * q] = act ? r * ta.Tr[j + (size_t)a.ns * q] : 0.0;  // Beta Tr
+    if (lane >= nc && lane < K) v[nA + nB + lane - nc] = m2;
+    else if (lane >= K && lane < nc + NF) v[nA + nB + lane - nc] = 0.0;
+  }
+  __syncthreads();
+  const int ne = nf * 32;
+  double* P = a.part;
+  double* V = ta.gvt;
+  const int ld = ta.gvt_ld;
+  for (int q = t; q < ne; q += 256)
+    store_coherent(P + (size_t)b * CRW_TILE + q,
+                   (sC[q] + sC[CRW_TILE + q]) + (sC[2 * CRW_TILE + q] + sC[3 * CRW_TILE + q]));
+  if (ta.gv_on)
+    for (int q = t; q < ngv; q += 256)
+      store_coherent(V + (size_t)b * ld + q, (sV[q] + sV[ngv + q]) + (sV[2 * ngv + q] + sV[3 * ngv + q]));
+  vm_stores_done();
+  __syncthreads();
+  const int g = b / CRW_GROUP, g0 = g * CRW_GROUP, gn = min(CRW_GROUP, nbl - g0);
+  const int ng = (nbl + CRW_GROUP - 1) / CRW_GROUP;
+  if (t == 0) s_last = __hip_atomic_fetch_add(&a.ticket[2 + g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gn - 1;
+  __syncthreads();
+  if (!s_last) return;
+  // group reducer: the group's tiles in workgroup order
+  const int ntot = ne + (ta.gv_on ? ngv : 0);
+  for (int q = t; q < ntot; q += 256) {
+    const bool cr = q < ne;
+    const double* src = cr ? P + q : V + (q - ne);
+    const size_t st = cr ? CRW_TILE : ld;
+    double x[CRW_GROUP];
+#pragma unroll
+    for (int u = 0; u < CRW_GROUP; ++u) x[u] = u < gn ? load_coherent(src + (size_t)(g0 + u) * st) : 0.0;
+    double v = 0.0;
+#pragma unroll
+    for (int u = 0; u < CRW_GROUP; ++u) v += x[u];
+    store_coherent((cr ? P + q : V + (q - ne)) + (size_t)(nbl + g) * st, v);
+  }
+  if (t == 0) __hip_atomic_store(&a.ticket[2 + g], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  vm_stores_done();
+  __syncthreads();
+  if (t == 0) s_last = __hip_atomic_fetch_add(&a.ticket[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+  __syncthreads();
+  if (!s_last) return;
+  // every group tile is in: the side chain may start (it sums the GammaV / psi group tiles)
+  if (t == 0) {
+    __hip_atomic_store(&a.ticket[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ta.gv_on) __hip_atomic_store(ta.tails_flag, g2bl_epoch(iter), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  double* sCR = smem + 4 * CRW_TILE;  // [row k][16]
+  for (int q = t; q < 512; q += 256) {
+    const int h = q >> 5, k = q & 31;
+    double v = 0.0;
+    if (h < nf)
+      for (int q0 = 0; q0 < ng; q0 += CRW_GROUP) {
+        double x[CRW_GROUP];
+#pragma unroll
+        for (int u = 0; u < CRW_GROUP; ++u)
+          x[u] = q0 + u < ng ? load_coherent(P + (size_t)(nbl + q0 + u) * CRW_TILE + q) : 0.0;
+#pragma unroll
+        for (int u = 0; u < CRW_GROUP; ++u) v += x[u];
+      }
+    sCR[k * 16 + h] = v;
+    if (h < nf && k < K) a.CR[k + (size_t)a.ldcr * h] = v;
+  }
+  __syncthreads();
+  if (w == 0) crw_finish<NFB>(a, sCR, smem);
+}
+
 struct G2BLArgs {
   G2Args g2;
   BLArgs bl;
@@ -1282,6 +1520,11 @@ struct G2BLArgs {
   double* part;
   int K, nc, NF, nt, nsl;
   int* sync;            // [ticket, epoch of the published Gamma, -, handshake timed out]
+  BLTailArgs tail;      // the BetaLambda workgroups' tail (crw_on): Eta constants [+ side partials]
+  int crw_on;
+  const int* side_sync; // side_wait: [GammaV, delta chain per level ..., Gamma2 prep] flags of
+  int side_wait;        // the previous sweep's side chain (graph sweeps after the first)
+  int side_prep;        // ... and its Gamma2 prep flag
 };
 
 template <int NM>
@@ -1298,6 +1541,11 @@ __global__ __launch_bounds__(256) void gamma2_bl_kernel(G2BLArgs f) {
     __syncthreads();
     if (blockIdx.x == 0 && threadIdx.x < 64) HMSC_STAMP_RT(71);
     if (!s_last) return;
+    if (f.side_wait) {  // the previous sweep's GammaV (Gamma, iV) and Gamma2 prep, behind the fence below
+      const int ep = g2bl_epoch(SWEEP_ITER(f.g2) - 1);
+      side_wait(f.side_sync, 1, ep, f.sync);
+      if (f.side_prep) side_wait(f.side_sync + 1 + f.bl.nr, 1, ep, f.sync);
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every block's partials
     if (threadIdx.x < 64) HMSC_STAMP_RT(72);
     gamma2_final_body(f.g2, smem);
@@ -1309,7 +1557,10 @@ __global__ __launch_bounds__(256) void gamma2_bl_kernel(G2BLArgs f) {
     }
     return;
   }
-  beta_lambda_wave_body<NM, true>(f.bl, smem, blockIdx.x - nparts, f.sync);
+  const uint32_t iter = SWEEP_ITER(f.g2);
+  const BLCol col = beta_lambda_wave_body<NM, true>(f.bl, smem, blockIdx.x - nparts, f.sync, f.side_sync,
+                                                    g2bl_epoch(iter - 1), f.side_wait ? 1 + f.bl.nr : 0);
+  if (f.crw_on) bl_tail<(NM < 16 ? NM : 16)>(f.tail, col, blockIdx.x - nparts, gridDim.x - nparts, iter, smem);
 }
 
 static void launch_gamma2_prep(State& s, hipStream_t st) {
@@ -1409,11 +1660,23 @@ bool gamma2_bl_fusion_ok(const State& s) {
 }
 
 // updateGamma2 then updateBetaLambda as one launch (gamma2_bl_kernel)
+static CRWArgs make_crw_args(const State& s);
+bool side_fusion_ok(const State& s);
+
 void launch_gamma2_bl(State& s, uint32_t iter) {
   if (!s.xeta_valid) launch_xeta(s);
   flush_g(s);
   if (!s.zt_valid) launch_zt_refresh(s);
-  join_side(s);  // iV, Gamma2's prep, Psi and Delta come from the previous sweep's side updaters
+  // the co-launched sweep (launch_side_fused) runs the fused Eta kernel next: its constants
+  // are formed in the BetaLambda workgroups' tail (K <= 32 on this path, nf <= 16), with
+  // GammaV's and LambdaPriors' species partials when their tile fits the tail's LDS
+  const bool crw_on = s.nranks == 1 && side_fusion_ok(s) && s.lev[0].nf <= 16 && s.K <= 32;
+  const bool tail_gv = crw_on && (s.mask & HMSC_UP_GAMMA2) && s.nt <= 8 && s.nc * s.nc + s.nc * s.nt + s.NF <= 1024 &&
+                       s.gvt != nullptr;
+  // graph sweeps after the first: the previous sweep's side chain is joined on the device
+  const bool dev_join = tail_gv && s.edge_free && s.capturing && s.cap_sweep > 0 && s.side_tail;
+  // iV, Gamma2's prep, Psi and Delta come from the previous sweep's side updaters
+  if (!dev_join) join_side(s);
   if (!s.g2prep_valid) launch_gamma2_prep(s, s.stream);
   G2BLArgs f{};
   const int nparts = (s.nsl + SB - 1) / SB;
@@ -1450,6 +1713,32 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
   f.nt = s.nt;
   f.nsl = s.nsl;
   f.sync = s.gbl_sync;
+  f.crw_on = crw_on;
+  if (crw_on) {
+    BLTailArgs& t = f.tail;
+    t.crw = make_crw_args(s);
+    t.gv_on = tail_gv;
+    t.nt = s.nt;
+    t.NF = s.NF;
+    t.nr = s.nr;
+    t.sp0 = s.sp0;
+    t.gvt_ld = s.gvt_ld;
+    for (int r = 0; r < s.nr; ++r) {
+      t.lev_nf[r] = s.lev[r].nf;
+      t.nu[r] = s.lev[r].nu;
+    }
+    t.Tr = s.Tr;
+    t.Psi = s.Psi;
+    t.gvt = s.gvt;
+    t.tails_flag = s.gbl_sync + 2;
+    t.key = s.key;
+  }
+  s.crw_fresh = crw_on;
+  s.tail_gv = tail_gv;
+  s.side_tail = false;  // (set again by this sweep's launch_side_fused)
+  f.side_sync = s.side_sync;
+  f.side_wait = dev_join;
+  f.side_prep = (s.mask & HMSC_UP_GAMMA2) ? 1 : 0;
   if (!s.capturing) HIP_OK(hipMemsetAsync(s.gbl_sync + 1, 0, sizeof(int), s.stream));  // an eager sweep may repeat an iter
   const int nb = nparts + (s.nsl + 3) / 4;
   const size_t smem = BLW_LDS * sizeof(double);
@@ -1564,7 +1853,9 @@ __device__ double wave_gamma_std(Key key, uint32_t idx, uint32_t stream, uint32_
 // gammas in parallel (wave w takes h = w, w + nwaves, ...), and the sequential chain that
 // remains is nf rate evaluations and divisions on one thread: the same values, in the same
 // order, as drawing gamma(shape, rate) step by step.
-__device__ __forceinline__ void delta_body(const LPArgs& a, const double* rs_part, int nparts, int r) {
+__device__ __forceinline__ void delta_body(const LPArgs& a, const double* rs_part, int nparts, int r,
+                                           int rs_ld = 0, int* flags = nullptr) {
+  if (rs_ld == 0) rs_ld = a.NF;
   // one workgroup per level: the sequential delta chain (R/updateLambdaPriors.R:25-32)
   __shared__ double rs[64], delta[64], gstd[64];
   const int t = threadIdx.x, w = t >> 6, nw = blockDim.x >> 6;
@@ -1573,7 +1864,7 @@ __device__ __forceinline__ void delta_body(const LPArgs& a, const double* rs_par
   for (int q = 0; q < r; ++q) f0 += a.lev_nf[q];
   if (t < nf) {
     double sum = 0.0;
-    for (int b = 0; b < nparts; ++b) sum += rs_part[(size_t)b * a.NF + f0 + t];
+    for (int b = 0; b < nparts; ++b) sum += load_coherent(rs_part + (size_t)b * rs_ld + f0 + t);
     rs[t] = sum;
     delta[t] = a.Delta[f0 + t];
   }
@@ -1601,6 +1892,11 @@ __device__ __forceinline__ void delta_body(const LPArgs& a, const double* rs_par
   __syncthreads();
   if (t < nf) a.Delta[f0 + t] = delta[t];
   if (r == 0) HMSC_STAMP(21);
+  if (flags) {  // this level's Delta is out (the next sweep's fused launch waits on this)
+    __threadfence();
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(&flags[1 + r], g2bl_epoch(SWEEP_ITER(a)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 __global__ __launch_bounds__(64) void delta_kernel(LPArgs a, const double* rs_part, int nparts) {
@@ -1610,16 +1906,20 @@ __global__ __launch_bounds__(64) void delta_kernel(LPArgs a, const double* rs_pa
 // The side stream's whole chain in one launch: workgroup 0 runs updateGammaV (+ Gamma2's
 // prep), workgroups 1..nr the delta chains of updateLambdaPriors -- independent updaters, so
 // neither waits behind the other.
+// tails_flag (graph sweeps after the first): the launch is not behind a graph edge from the
+// fused Gamma2 + BetaLambda launch it reads; it waits for that launch's tails to be in.
 template <int NM>
-__global__ __launch_bounds__(256) void side_chain_kernel(GVWArgs g, LPArgs lp, const double* rs_part, int nparts) {
+__global__ __launch_bounds__(256) void side_chain_kernel(GVWArgs g, LPArgs lp, const double* rs_part, int nparts,
+                                                         int rs_ld, const int* tails_flag, int* err) {
   // A latency-bound chain of small factorisations running beside the main stream's Eta and z
   // waves on the same SIMDs: raised issue priority, so its few waves are not starved by the
   // VALU-bound z waves (the arbiter picks the highest-priority ready wave).
   __builtin_amdgcn_s_setprio(3);
+  if (tails_flag) side_wait(tails_flag, 1, g2bl_epoch(SWEEP_ITER(g)), err);
   if (blockIdx.x == 0)
     gammav_body<NM>(g);
   else
-    delta_body(lp, rs_part, nparts, blockIdx.x - 1);
+    delta_body(lp, rs_part, nparts, blockIdx.x - 1, rs_ld, g.flags);
 }
 
 constexpr int LP_PARTS = 64;
@@ -1761,74 +2061,96 @@ __device__ __forceinline__ void cr_body(const double* BL, const double* iSigma, 
   }
 }
 
-// The fused Eta kernel's per-sweep constants, formed once instead of in each of its ~600
-// workgroups: the workgroup of the last CR species block to finish (a ticket) reduces the
-// partials in block order into CR (K x NF, ld ldcr) and factors Q = I + Lambda diag(iSigma)
-// Lambda^T (its rows nc.. of CR, one level, nf <= 16) in one wave's registers, writing W =
-// L^-1 (lower, row m at 16 m, zero padded) -- the same algebra and summation order each Eta
-// workgroup ran before.
-struct CRFin {
-  int* ticket;   // zero between launches; reset by the last workgroup
-  int n_cr;
-  double* CR;
-  double* W;     // 16 x 16
-  int nc, nf;
-};
+// The fused Eta kernel's per-sweep constants, formed once per sweep on the matrix cores by
+// CRW_PARTS workgroups (instead of in each of the Eta kernel's ~600 workgroups):
+//   CR = BL diag(iSigma) Lambda^T   (K x nf; rows nc.. are Q - I, Q = I + Lambda diag(iSigma) Lambda^T)
+//   W  = L^-1, L L^T = Q            (16 x 16, row m at 16 m, zero padded)
+//   LS = Lambda diag(iSigma)        ([species][16], the Eta stream's MFMA B operand)
+// v_mfma_f64_16x16x4 over groups of 4 species: A[i][k] = BL[16 q + i, j0 + k] (tile q of the K
+// rows), B[k][h] = iSigma_j Lambda[h, j] (= LS, written as it is formed).  Workgroup p, wave w
+// take every (4 CRW_PARTS)-th species group, eight groups' loads in flight per lane; the
+// waves' accumulators meet in LDS in wave order, the workgroups' partial tiles in global
+// memory; the last workgroup through (a ticket) adds them in part order (deterministic) and
+// factors Q in one wave's registers (wave_la.h).
 
-__device__ __forceinline__ void cr_finalize(const CRFin& f, const double* CR_part, int K, int ldcr, int slab) {
+template <int NFB>
+__device__ __forceinline__ void crw_body(const CRWArgs& a, int p, double* smem) {
   __shared__ int s_last;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, lm = lane & 15, lk = lane >> 4;
+  const int K = a.K, nc = a.nc, nf = a.nf, ns = a.ns, nq = (K + 15) >> 4;  // nq <= 4
+  d4 acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+  const int ng = (ns + 3) >> 2, gstride = 4 * CRW_PARTS;
+  constexpr int D = 8;  // species groups' loads in flight per lane
+  for (int g0 = 4 * p + w; g0 < ng; g0 += gstride * D) {
+    double av[D][4], bv[D];
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int g = g0 + gstride * u, j = 4 * g + lk;
+      const bool in = g < ng && j < ns;
+      const double* col = a.BL + (size_t)K * (in ? j : 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) av[u][q] = (in && q < nq && 16 * q + lm < K) ? col[16 * q + lm] : 0.0;
+      bv[u] = (in && lm < nf) ? col[nc + lm] * a.iSigma[j] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int g = g0 + gstride * u, j = 4 * g + lk;
+      if (g < ng && j < ns) a.LS[(size_t)16 * j + lm] = bv[u];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (q < nq) acc[q] = mfma_f64(av[u][q], bv[u], acc[q]);
+    }
+  }
+  // acc[q][r] = partial CR[16 q + lk + 4 r][lm]: the waves' sum in LDS, then to this part's slot
+  double* sAcc = smem;  // [wave][q][16 rows][16 cols]
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (q < nq)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sAcc[((w * 4 + q) * 16 + lk + 4 * r) * 16 + lm] = acc[q][r];
+  __syncthreads();
+  double* mine = a.part + (size_t)p * 4 * 256;
+  for (int e = t; e < nq * 256; e += 256) {
+    const int q = e >> 8, rc = e & 255;
+    mine[e] = (sAcc[(0 * 4 + q) * 256 + rc] + sAcc[(1 * 4 + q) * 256 + rc]) +
+              (sAcc[(2 * 4 + q) * 256 + rc] + sAcc[(3 * 4 + q) * 256 + rc]);
+  }
   __threadfence();  // every wave's partial stores complete at device scope before the ticket
   __syncthreads();
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(f.ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == f.n_cr - 1;
+  if (t == 0) s_last = __hip_atomic_fetch_add(a.ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == CRW_PARTS - 1;
   __syncthreads();
   if (!s_last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every block's partials
-  __shared__ double sQ[16 * 16];
-  const int t = threadIdx.x, nc = f.nc, nf = f.nf;
-  for (int p = t; p < K * nf; p += 256) {
-    const int kk = p % K, h = p / K;
-    const double* src = CR_part + kk + (size_t)ldcr * h;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every part's tiles
+  double* sCR = smem + 4 * 4 * 256;  // [row k][16]
+  for (int e = t; e < nq * 256; e += 256) {
     double v = 0.0;
-    int b = 0;
-    for (; b + 8 <= f.n_cr; b += 8) {
-      double x[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) x[u] = src[(size_t)slab * (b + u)];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v += x[u];
-    }
-    for (; b < f.n_cr; ++b) v += src[(size_t)slab * b];
-    f.CR[kk + (size_t)ldcr * h] = v;
-    if (kk >= nc) sQ[(kk - nc) * 16 + h] = v;
+    for (int q2 = 0; q2 < CRW_PARTS; ++q2) v += a.part[(size_t)q2 * 4 * 256 + e];
+    sCR[e] = v;
+    const int row = e >> 4, h = e & 15;
+    if (row < K && h < nf) a.CR[row + (size_t)a.ldcr * h] = v;
   }
   __syncthreads();
-  if (t < 64) {  // Q = I + Lambda D Lambda^T, its factor L and W = L^-1 by rows (wave_la.h)
-    __shared__ double sWs[16 * 17];
-    const int lane = t;
-    double q[16], dinv;
-    const int r = lane < nf ? lane : 0;
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      const double v = (r == c ? 1.0 : 0.0) + sQ[r * 16 + (c < nf ? c : 0)];
-      q[c] = (lane < nf && c < nf) ? v : (lane == c ? 1.0 : 0.0);
-    }
-    wv_chol<16>(q, dinv);
-    double wr[16];
-    wv_inv_lower_rows<16>(q, dinv, wr, sWs);
-    if (lane < 16)
-#pragma unroll
-      for (int c = 0; c < 16; ++c) f.W[lane * 16 + c] = (lane < nf && c < nf && c <= lane) ? wr[c] : 0.0;
+  if (w == 0) {
+    crw_finish<NFB>(a, sCR, sAcc);  // the wave partials are consumed: their LDS is the scratch
+    if (lane == 0) __hip_atomic_store(a.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (t == 0) __hip_atomic_store(f.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// LDS of crw_body (doubles): the waves' partial tiles, the reduced CR
+constexpr int CRW_LDS = 4 * 4 * 256 + 4 * 16 * 16;
+
+template <int NFB>
+__global__ __launch_bounds__(256) void crw_kernel(CRWArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  crw_body<NFB>(a, blockIdx.x, smem);
 }
 
 __global__ __launch_bounds__(256) void cr_kernel(const double* BL, const double* iSigma, int K, int nc, int NF,
-                                                 int ns_loc, double* CR_part, int ldcr, int slab, double* LS,
-                                                 CRFin fin) {
+                                                 int ns_loc, double* CR_part, int ldcr, int slab, double* LS) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   cr_body(BL, iSigma, K, nc, NF, ns_loc, CR_part, ldcr, slab, LS, smem, blockIdx.x);
-  if (fin.ticket) cr_finalize(fin, CR_part, K, ldcr, slab);
 }
 
 struct EtaArgs {
@@ -2029,8 +2351,8 @@ __global__ __launch_bounds__(64) void eta_na_row_kernel(EtaView ev, int r, int n
 struct EtaFArgs {
   const double* Z;
   const double* LS;   // ns_loc x 16: Lambda diag(iSigma), zero past nf (cr_body)
-  const double* CR;   // Kmax x NF (ld ldcr): CR = BL diag(iSigma) Lambda^T (cr_finalize)
-  const double* W;    // 16 x 16: L^-1 of Q = I + Lambda diag(iSigma) Lambda^T, row m at 16 m (cr_finalize)
+  const double* CR;   // Kmax x NF (ld ldcr): CR = BL diag(iSigma) Lambda^T (crw_body)
+  const double* W;    // 16 x 16: L^-1 of Q = I + Lambda diag(iSigma) Lambda^T, row m at 16 m (crw_body)
   double* XEta;       // ny x K (ld ny)
   const int* Pi;      // ny: unit of each row (0-based)
   double* Eta;        // np x nf
@@ -2079,7 +2401,7 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
     const int p = t + 256 * u, s2 = p % EF_SITES, k = p / EF_SITES, ii = i0 + s2;
     xr[u] = (k < nc && ii < ny) ? a.XEta[ii + (size_t)ny * k] : 0.0;
   }
-  // CR (K x nf) and W (nf x nf) of this sweep, formed once by cr_finalize: loads issued here,
+  // CR (K x nf) and W (nf x nf) of this sweep, formed once by crw_body: loads issued here,
   // ahead of the stream, stored to LDS after it
   double crv[4], wv[NFB * NFB / 256 + 1];
 #pragma unroll
@@ -2192,21 +2514,19 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Co-launched side updaters (one queue).  After BetaLambda a sweep has three independent
-// species-parallel passes -- CR for updateEta, the GammaV partials (R/updateGammaV.R:17-19)
-// and the psi draws of updateLambdaPriors (:22-24) -- and two small serial tails, the delta
-// chain (:25-32) and the GammaV algebra.  An event wait between queues leaves the GPU idle
-// for ~10-20 us on this stack, so instead of two side streams the three passes share one
-// launch (post_bl_kernel), and only the two serial tails -- the GammaV algebra and the
-// delta chain, one workgroup each -- run on the side stream, which is joined just before
-// the next sweep's Gamma2 final stage.
+// Co-launched side updaters.  After BetaLambda a sweep has the fused updateEta on the
+// critical path (its constants CR, W, LS already formed in the BetaLambda launch's tail,
+// crw_tail) and, off it, two species-parallel passes -- the GammaV partials
+// (R/updateGammaV.R:17-19) and the psi draws of updateLambdaPriors (:22-24) -- followed by
+// two small serial tails, the GammaV algebra and the delta chain (:25-32).  The passes share
+// one launch (post_bl_kernel) and the tails another (side_chain_kernel, one workgroup each),
+// both on the side stream behind one event after BetaLambda; the side stream is joined just
+// before the next sweep's Gamma2 + BetaLambda launch.
 // ---------------------------------------------------------------------------
 struct PostBLArgs {
   const double* BL;
   const double* iSigma;
-  int K, nc, NF, ns_loc, ldcr, slab, n_cr;
-  double* CR_part;
-  double* LS;
+  int K, nc, NF, ns_loc;
   int nt, n_gv;
   const double* Gamma;
   const double* Tr;
@@ -2215,19 +2535,13 @@ struct PostBLArgs {
   int n_psi;
   const uint32_t* iter_src;  // graph replay: d_iter, snapshotted into iter_side for the side stream
   uint32_t* iter_side;
-  CRFin fin;                 // the fused Eta kernel's CR and W, by the last CR workgroup
 };
 
+// workgroups 0 .. n_gv-1: the GammaV partial blocks; then the psi parts
 __global__ __launch_bounds__(256) void post_bl_kernel(PostBLArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  int b = blockIdx.x;
+  const int b = blockIdx.x;
   if (b == 0 && threadIdx.x == 0 && a.iter_src) *a.iter_side = *a.iter_src;
-  if (b < a.n_cr) {
-    cr_body(a.BL, a.iSigma, a.K, a.nc, a.NF, a.ns_loc, a.CR_part, a.ldcr, a.slab, a.LS, smem, b);
-    if (a.fin.ticket) cr_finalize(a.fin, a.CR_part, a.K, a.ldcr, a.slab);
-    return;
-  }
-  b -= a.n_cr;
   if (b < a.n_gv) {
     gammav_partial_body(a.BL, a.K, a.nc, a.nt, a.ns_loc, a.Gamma, a.Tr, a.gv_part, smem, b);
     return;
@@ -2237,7 +2551,23 @@ __global__ __launch_bounds__(256) void post_bl_kernel(PostBLArgs a) {
 
 static bool eta_fused_ok(const State& s);
 static void launch_eta_fused(State& s, uint32_t iter, bool cr_done);
-static CRFin make_cr_fin(const State& s);
+
+static CRWArgs make_crw_args(const State& s) {
+  CRWArgs c{};
+  c.BL = s.BL;
+  c.iSigma = s.iSigma;
+  c.K = s.K;
+  c.nc = s.nc;
+  c.nf = s.lev[0].nf;
+  c.ns = s.nsl;
+  c.ldcr = s.Kmax;
+  c.CR = s.CR;
+  c.W = s.etaW;
+  c.LS = s.LS;
+  c.part = s.crw_part;
+  c.ticket = s.crw_ticket;
+  return c;
+}
 
 bool side_fusion_ok(const State& s) {
   const uint32_t need = HMSC_UP_GAMMAV | HMSC_UP_LAMBDAPRIORS | HMSC_UP_ETA;
@@ -2246,54 +2576,81 @@ bool side_fusion_ok(const State& s) {
 }
 
 // GammaV + LambdaPriors + Eta of one sweep (BetaLambda done), main stream + one side launch
+template <int NM>
+static void launch_side_chain(State& s, const GVWArgs& gw, const LPArgs& lp, const double* rs, int nparts, int rs_ld,
+                              const int* tails_flag) {
+  side_chain_kernel<NM><<<1 + s.nr, 256, 0, s.side>>>(gw, lp, rs, nparts, rs_ld, tails_flag, s.gbl_sync);
+}
+
+// GammaV + LambdaPriors + Eta of one sweep (BetaLambda done), main stream + the side stream
 void launch_side_fused(State& s, uint32_t iter) {
   if (!s.xeta_valid) launch_xeta(s);
-  const int ncr = (s.nsl + SB - 1) / SB, ngv = (s.nsl + SB - 1) / SB;
-  const int npsi = std::min(LP_PARTS, std::max(1, s.nsl));
-  const int64_t slab = (int64_t)s.Kmax * s.NFmax;
-  PostBLArgs a{};
-  a.BL = s.BL;
-  a.iSigma = s.iSigma;
-  a.K = s.K;
-  a.nc = s.nc;
-  a.NF = s.NF;
-  a.ns_loc = s.nsl;
-  a.ldcr = s.Kmax;
-  a.slab = (int)slab;
-  a.n_cr = ncr;
-  a.CR_part = s.CR_part;
-  a.LS = s.LS;
-  a.nt = s.nt;
-  a.n_gv = ngv;
-  a.Gamma = s.Gamma;
-  a.Tr = s.Tr;
-  a.gv_part = s.gv_part;
-  a.lp = make_lp_args(s, iter);
-  a.n_psi = npsi;
-  a.iter_src = s.capturing ? s.d_iter : nullptr;
-  a.iter_side = s.d_iter_side;
-  a.fin = make_cr_fin(s);
-  const size_t smem = std::max((size_t)s.K * SB, (size_t)(2 * s.nc * SB + SB * s.nt)) * sizeof(double);
-  post_bl_kernel<<<ncr + ngv + npsi, 256, smem, s.stream>>>(a);
-  HIP_OK(hipGetLastError());
-  HIP_OK(hipEventRecord(s.ev_bl, s.stream));
   // the main continuation is captured before the side branch (the graph executor keeps the
   // first-created child of a node on its parent's queue, so the critical path stays on one
-  // queue); the CR partials are reduced inside the fused Eta kernel
-  launch_eta_fused(s, iter, true);
-  // GammaV algebra on the side stream (reads gv_part; writes Gamma, iV and Gamma2's prep)
-  HIP_OK(hipStreamWaitEvent(s.side, s.ev_bl, 0));
-  // with the delta chains (reading the psi partials) as extra workgroups of the same launch
-  const uint32_t* itd = s.capturing ? s.d_iter_side : nullptr;
-  const GVWArgs gw = make_gvw_args(s, iter, s.gv_part, ngv, itd);
-  LPArgs lps = a.lp;
-  lps.iter_dev = itd;
+  // queue); CR, W and LS come from the fused Gamma2 + BetaLambda launch's tail when it formed
+  // them, else from crw_kernel ahead of the Eta kernel
+  const bool cr_done = s.crw_fresh, tail = s.tail_gv;
+  s.crw_fresh = false;
+  s.tail_gv = false;
+  // graph sweeps after the first: the side chain is not forked by a graph edge; it waits on
+  // the device for the fused launch's tails (which it reads), see State::cap_sweep
+  const bool dev_fork = tail && s.edge_free && s.capturing && s.cap_sweep > 0;
+  if (!dev_fork) HIP_OK(hipEventRecord(s.ev_bl, s.stream));
+  launch_eta_fused(s, iter, cr_done);
+  if (!dev_fork) HIP_OK(hipStreamWaitEvent(s.side, s.ev_bl, 0));
+  LPArgs lp = make_lp_args(s, iter);
+  const double* rs;
+  int nparts, rs_ld;
+  GVWArgs gw;
+  if (tail) {
+    // the BetaLambda tail's group tiles: [A nc^2 | BTr nc nt | rs NF], ld gvt_ld
+    const int nbl = (s.nsl + 3) / 4, ngr = (nbl + CRW_GROUP - 1) / CRW_GROUP;
+    const double* gt = s.gvt + (size_t)nbl * s.gvt_ld;
+    gw = make_gvw_args(s, iter, gt, ngr, s.capturing ? s.d_iter : nullptr);
+    gw.part_ld = s.gvt_ld;
+    gw.flags = s.side_sync;
+    rs = gt + s.nc * s.nc + s.nc * s.nt;
+    nparts = ngr;
+    rs_ld = s.gvt_ld;
+    s.side_tail = true;
+  } else {
+    // the species partials of GammaV and LambdaPriors first (post_bl_kernel), on the side stream
+    const int ngv = (s.nsl + SB - 1) / SB;
+    const int npsi = std::min(LP_PARTS, std::max(1, s.nsl));
+    PostBLArgs a{};
+    a.BL = s.BL;
+    a.iSigma = s.iSigma;
+    a.K = s.K;
+    a.nc = s.nc;
+    a.NF = s.NF;
+    a.ns_loc = s.nsl;
+    a.nt = s.nt;
+    a.n_gv = ngv;
+    a.Gamma = s.Gamma;
+    a.Tr = s.Tr;
+    a.gv_part = s.gv_part;
+    a.lp = lp;
+    a.n_psi = npsi;
+    a.iter_src = s.capturing ? s.d_iter : nullptr;
+    a.iter_side = s.d_iter_side;
+    const size_t smem = (size_t)(2 * s.nc * SB + SB * s.nt) * sizeof(double);
+    post_bl_kernel<<<ngv + npsi, 256, smem, s.side>>>(a);
+    HIP_OK(hipGetLastError());
+    gw = make_gvw_args(s, iter, s.gv_part, ngv, s.capturing ? s.d_iter_side : nullptr);
+    rs = s.psi_rs;
+    nparts = npsi;
+    rs_ld = s.NF;
+  }
+  lp.iter_dev = gw.iter_dev;
+  // the GammaV algebra (writes Gamma, iV and Gamma2's prep) with the delta chains as extra
+  // workgroups of the same launch
+  const int* tf = dev_fork ? s.gbl_sync + 2 : nullptr;
   switch (wv_bucket_gv(s.nc * s.nt)) {
-    case 8: side_chain_kernel<8><<<1 + s.nr, 256, 0, s.side>>>(gw, lps, s.psi_rs, npsi); break;
-    case 16: side_chain_kernel<16><<<1 + s.nr, 256, 0, s.side>>>(gw, lps, s.psi_rs, npsi); break;
-    case 20: side_chain_kernel<20><<<1 + s.nr, 256, 0, s.side>>>(gw, lps, s.psi_rs, npsi); break;
-    case 24: side_chain_kernel<24><<<1 + s.nr, 256, 0, s.side>>>(gw, lps, s.psi_rs, npsi); break;
-    default: side_chain_kernel<32><<<1 + s.nr, 256, 0, s.side>>>(gw, lps, s.psi_rs, npsi); break;
+    case 8: launch_side_chain<8>(s, gw, lp, rs, nparts, rs_ld, tf); break;
+    case 16: launch_side_chain<16>(s, gw, lp, rs, nparts, rs_ld, tf); break;
+    case 20: launch_side_chain<20>(s, gw, lp, rs, nparts, rs_ld, tf); break;
+    case 24: launch_side_chain<24>(s, gw, lp, rs, nparts, rs_ld, tf); break;
+    default: launch_side_chain<32>(s, gw, lp, rs, nparts, rs_ld, tf); break;
   }
   HIP_OK(hipGetLastError());
   if (gw.do_prep) s.g2prep_valid = true;
@@ -2352,24 +2709,18 @@ static bool eta_fused_ok(const State& s) {
          s.lev[0].nf <= 16 && s.K <= 64 && s.LS != nullptr && !getenv_flag("HMSC_NO_ETA_FUSION");
 }
 
-static CRFin make_cr_fin(const State& s) {
-  CRFin f{};
-  f.ticket = s.gbl_sync + 4;
-  f.n_cr = (s.nsl + SB - 1) / SB;
-  f.CR = s.CR;
-  f.W = s.etaW;
-  f.nc = s.nc;
-  f.nf = s.lev[0].nf;
-  return f;
-}
-
 static void launch_eta_fused(State& s, uint32_t iter, bool cr_done = false) {
   const int ncr = (s.nsl + SB - 1) / SB;
   const int64_t slab = (int64_t)s.Kmax * s.NFmax;
-  if (!cr_done) {  // the CR partials (post_bl_kernel computes them in the co-launched path), CR and W
-    cr_kernel<<<ncr, 256, (size_t)s.K * SB * sizeof(double), s.stream>>>(s.BL, s.iSigma, s.K, s.nc, s.NF, s.nsl,
-                                                                           s.CR_part, s.Kmax, (int)slab, s.LS,
-                                                                           make_cr_fin(s));
+  if (!cr_done) {  // CR, W and LS (post_bl_kernel's workgroup 0 forms them in the co-launched path)
+    const size_t smem = (size_t)CRW_LDS * sizeof(double);
+    const CRWArgs c = make_crw_args(s);
+    if (c.nf <= 8)
+      crw_kernel<8><<<CRW_PARTS, 256, smem, s.stream>>>(c);
+    else if (c.nf <= 12)
+      crw_kernel<12><<<CRW_PARTS, 256, smem, s.stream>>>(c);
+    else
+      crw_kernel<16><<<CRW_PARTS, 256, smem, s.stream>>>(c);
     HIP_OK(hipGetLastError());
   }
   const Level& L = s.lev[0];
@@ -2415,6 +2766,7 @@ static void launch_eta_fused(State& s, uint32_t iter, bool cr_done = false) {
 }
 
 void launch_eta(State& s, uint32_t iter) {
+  s.crw_fresh = false;  // (the co-launched path consumes the tail's constants itself)
   if (s.nr == 0) return;
   if (!s.xeta_valid) launch_xeta(s);  // the Eta kernels read XEta of the current Eta
   if (eta_fused_ok(s)) {
@@ -2444,8 +2796,7 @@ void launch_eta(State& s, uint32_t iter) {
     const int ncr = (s.nsl + SB - 1) / SB;
     const int64_t slab = (int64_t)s.Kmax * s.NFmax;
     cr_kernel<<<ncr, 256, (size_t)s.K * SB * sizeof(double), s.stream>>>(s.BL, s.iSigma, s.K, s.nc, s.NF, s.nsl,
-                                                                           s.CR_part, s.Kmax, (int)slab, nullptr,
-                                                                           CRFin{});
+                                                                           s.CR_part, s.Kmax, (int)slab, nullptr);
     HIP_OK(hipGetLastError());
     slab_sum_kernel<<<grid_for(slab), 256, 0, s.stream>>>(s.CR_part, s.CR, slab, ncr, slab);
     HIP_OK(hipGetLastError());
@@ -2803,16 +3154,17 @@ static PackArgs make_pack_args(State& s, double* slot, int part) {
   PackArgs a{};
   int64_t off = 0;
   int k = 0;
-  // side pieces (Gamma, iV, Delta) are written by the GammaV algebra and the delta chain,
-  // which may still run on the side stream: part 2 packs them there, part 1 the rest
+  // side pieces (Gamma, iV, Delta; Psi unless the BetaLambda tail drew it) are written by the
+  // GammaV algebra, the delta chain and the species partials, which may still run on the side
+  // stream: part 2 packs them there, part 1 the rest
   auto add = [&](const double* src, int64_t n, bool side) {
     if (part == 0 || (part == 2) == side) a.p[k++] = PackPiece{src, n, off};
     off += n;
   };
   add(s.BL, (int64_t)s.K * s.nsl, false);
-  add(s.Psi, (int64_t)s.NF * s.nsl, false);
+  add(s.Psi, (int64_t)s.NF * s.nsl, !s.side_tail);  // the BetaLambda tail (main) or post_bl_kernel (side)
   add(s.Delta, s.NF, true);
-  add(s.Gamma, (int64_t)s.nc * s.nt, true);
+  add(part == 2 ? s.Gamma_side : s.Gamma, (int64_t)s.nc * s.nt, true);  // (the next sweep's Gamma2 rewrites Gamma)
   add(s.iV, (int64_t)s.nc * s.nc, true);
   add(s.iSigma, s.nsl, false);
   for (int r = 0; r < s.nr; ++r) add(s.lev[r].Eta, (int64_t)s.lev[r].np * s.lev[r].nf, false);
@@ -2823,7 +3175,7 @@ static PackArgs make_pack_args(State& s, double* slot, int part) {
   a.slot = slot;
   if (slot == nullptr) {  // captured into a graph replay: slot chosen on the device
     a.slot = s.ring;
-    a.iter_dev = part == 2 ? s.d_iter_side : s.d_iter;
+    a.iter_dev = (part == 2 && !s.side_tail) ? s.d_iter_side : s.d_iter;
     a.desc = s.d_rec_desc;
     a.slot_stride = (int64_t)s.slot_doubles;
     a.ring_slots = s.ring_slots;
@@ -2834,7 +3186,7 @@ static PackArgs make_pack_args(State& s, double* slot, int part) {
 void launch_record(State& s, double* slot, int part) {
   const PackArgs a = make_pack_args(s, slot, part);
   if (part == 2)
-    pack_kernel<<<1, 256, 0, s.side>>>(a);
+    pack_kernel<<<8, 256, 0, s.side>>>(a);
   else
     pack_kernel<<<512, 256, 0, s.stream>>>(a);
   HIP_OK(hipGetLastError());

@@ -98,6 +98,21 @@ struct State {
   // Philox sweep counter is snapshotted into d_iter_side by the launch that forks it, so the
   // main stream may advance d_iter for the next sweep while it runs
   bool side_fused = false;
+  bool crw_fresh = false;   // the last Gamma2 + BetaLambda launch formed the fused Eta constants
+  // ... and its BetaLambda tail also formed GammaV's and LambdaPriors' species partials (gvt),
+  // which the side chain reads instead of post_bl_kernel's
+  bool tail_gv = false;
+  // graph sweeps after the first of a capture (cap_sweep > 0): the side chain is not forked
+  // from the main stream nor joined into it by graph edges (each a ~5-6 us cross-queue gap on
+  // the critical path) but synchronised by device flags: it waits for the fused launch's tails
+  // (gbl_sync[2]), and the next fused launch waits for its side_sync flags
+  int cap_sweep = -1;
+  bool edge_free = true;    // (HMSC_SIDE_EDGES=1: graph edges everywhere)
+  bool side_tail = false;   // the last side chain read the BetaLambda tail's tiles and raises side_sync
+  int* side_sync = nullptr;      // [GammaV, delta chain per level ..., Gamma2 prep]: epoch of the sweep
+  double* gvt = nullptr;         // the BetaLambda tail's GammaV / psi partial tiles
+  int gvt_ld = 0;
+  double* Gamma_side = nullptr;  // GammaV's Gamma, for the side stream's record pack
   uint32_t* d_iter_side = nullptr;
   double* gv_part = nullptr;     // GammaV species partials (not shared with Gamma2's ABpart)
 
@@ -127,7 +142,7 @@ struct State {
   int* row_slot = nullptr;       // ny: index into na_rows, or -1
   int n_na_rows = 0;
   int* dev_flags = nullptr;      // device error flags (Cholesky failures)
-  int* gbl_sync = nullptr;       // gamma2_bl_kernel's in-launch handshake (zero between launches)
+  int* gbl_sync = nullptr;       // gamma2_bl_kernel's in-launch handshake [ticket, Gamma epoch, tails epoch, error]
   std::vector<int> h_na_cols;
 
   // chain state (device)
@@ -168,6 +183,8 @@ struct State {
   double* CR = nullptr;          // Kmax x NFmax  BL diag(iSigma) Lambda_all^T
   double* CR_part = nullptr;     // species-block partials of CR
   double* LS = nullptr;          // NFmax x ns_loc  Lambda_all diag(iSigma) (fused Eta kernel)
+  double* crw_part = nullptr;    // the fused Eta constants' partial tiles (kernels.hip crw_body / crw_tail)
+  int* crw_ticket = nullptr;     // [crw_kernel, crw_tail's groups, crw_tail's per-group tickets]
   double* etaW = nullptr;        // 16 x 16  L^-1 of Q = I + Lambda diag(iSigma) Lambda^T (fused Eta kernel)
   double* Msmall = nullptr;      // per-level masked row grams (NA rows)
   double* scratch = nullptr;     // single-workgroup updaters

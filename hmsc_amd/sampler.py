@@ -176,8 +176,9 @@ class Chain:
         self.h = h
         self.rank, self.nranks = rank, nranks
         self.sp0, self.nsl = shard_range(hM.ns, rank, nranks)
-        cap = np.zeros(L.MAX_LEVELS, dtype=np.int32)
-        L.check(self.lib.hmsc_get_nf_cap(self.h, L.iptr(cap)))
+        cap = np.array(self.buf.nfMax + [0] * (L.MAX_LEVELS - len(self.buf.nfMax)), dtype=np.int32)
+        if hasattr(self.lib, "hmsc_get_nf_cap"):  # (a pre-round-4 library strides records by nfMax)
+            L.check(self.lib.hmsc_get_nf_cap(self.h, L.iptr(cap)))
         # factors each level's device buffers and record slots hold (K = nc + sum(nf) <= 64)
         self.nf_cap = [int(c) for c in cap[: hM.nr]]
         short = [(r, self.buf.nfMax[r], c) for r, c in enumerate(self.nf_cap) if c < self.buf.nfMax[r]]

@@ -14,8 +14,11 @@ from hmsc_amd.workloads import synthetic_probit  # noqa: E402
 hM = synthetic_probit()
 ch = H.Chain(hM, 1234567, device=0, updater={"GammaEta": False})
 ch.init([10])
-for it in range(1, 6):
-    ch.sweep(it)
+if "--graph" in sys.argv:  # the last sweep of a run of captured-graph replays
+    ch.run(transient=300, samples=1, thin=1, record=False)
+else:
+    for it in range(1, 6):
+        ch.sweep(it)
 ch.sync()
 st = ch.debug_get("stamps", 128)
 groups = {"gammav_wave": range(0, 10), "delta": range(20, 22), "gamma2_final": range(30, 33), "eta_shared(block0)": range(40, 45), "eta_fused(block0)": range(50, 56),

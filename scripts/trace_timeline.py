@@ -1,40 +1,34 @@
-"""Per-sweep timeline from a rocprofv3 kernel-trace CSV: each kernel's start, duration and
-the idle gap before it on its queue, for the last sweep, plus the mean sweep period.
-
-    python scripts/trace_timeline.py gpurun_out/<tag>/run_kernel_trace.csv [anchor-kernel]
-
-The anchor kernel (default gamma2_partial) starts every sweep.
-"""
+"""Per-sweep timeline of a rocprofv3 kernel trace (run_kernel_trace.csv): for the steady
+sweeps, each kernel's start / end relative to the sweep's gamma2_bl start, with queues, and
+the median over sweeps.  usage: trace_timeline.py TRACE.csv [first_sweep] [n_sweeps]"""
 import csv
 import sys
+from collections import defaultdict
 
+import numpy as np
 
-def short(name):
-    return name.split("(")[0].replace("void ", "").replace("hmsc::", "")[:44]
-
-
-def main():
-    path = sys.argv[1]
-    anchor = sys.argv[2] if len(sys.argv) > 2 else "gamma2_partial"
-    rows = []
-    with open(path) as f:
-        for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), int(r["Queue_Id"])))
-    rows.sort()
-    starts = [i for i, r in enumerate(rows) if anchor in r[2]]
-    sweeps = list(zip(starts[:-1], starts[1:]))[-30:]
-    per = [(rows[b][0] - rows[a][0]) / 1e3 for a, b in sweeps]
-    print(f"sweep period: mean {sum(per) / len(per):.1f} us, min {min(per):.1f} over {len(per)} sweeps")
-    a, b = sweeps[-1]
-    t0 = rows[a][0]
-    last_end = {}
-    busy = 0.0
-    print(f"{'kernel':46s} {'q':>2s} {'start':>8s} {'dur':>7s} {'gap':>6s}")
-    for s, e, n, q in rows[a:b]:
-        g = (s - last_end[q]) / 1e3 if q in last_end else 0.0
-        last_end[q] = max(e, last_end.get(q, 0))
-        print(f"{n:46s} {q:2d} {(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f} {g:6.1f}")
-
-
-if __name__ == "__main__":
-    main()
+rows = list(csv.DictReader(open(sys.argv[1])))
+rows = [r for r in rows if r["Kind"] == "KERNEL_DISPATCH"]
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+first = int(sys.argv[2]) if len(sys.argv) > 2 else 200
+nsw = int(sys.argv[3]) if len(sys.argv) > 3 else 200
+short = lambda n: n.split("(")[0].replace("void ", "").replace("hmsc::", "")[:28]
+starts = [i for i, r in enumerate(rows) if "gamma2_bl_kernel" in r["Kernel_Name"]]
+rel = defaultdict(list)
+period = []
+for s_i in range(first, min(first + nsw, len(starts) - 1)):
+    a, b = starts[s_i], starts[s_i + 1]
+    t0 = int(rows[a]["Start_Timestamp"])
+    period.append(int(rows[b]["Start_Timestamp"]) - t0)
+    seen = defaultdict(int)
+    for r in rows[a:b]:
+        k = short(r["Kernel_Name"])
+        seen[k] += 1
+        key = f"{k}#{seen[k]}" if seen[k] > 1 else k
+        rel[key].append((int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0, r["Queue_Id"]))
+print(f"sweep period median {np.median(period)/1e3:.2f} us  (n={len(period)})")
+for k, v in sorted(rel.items(), key=lambda kv: np.median([x[0] for x in kv[1]])):
+    s = np.median([x[0] for x in v]) / 1e3
+    e = np.median([x[1] for x in v]) / 1e3
+    q = max(set(x[2] for x in v), key=[x[2] for x in v].count)
+    print(f"{k:32s} q{q:>3s} start {s:8.2f} end {e:8.2f} dur {e - s:7.2f}  (n={len(v)})")

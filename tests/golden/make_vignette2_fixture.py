@@ -5,6 +5,8 @@ of tests/test_gpu_vignette2.py.
 The oracle (oracle/hmsc_oracle.py) restates the reference R updaters (R is not installed
 here).  Oracle chains are keyed 1000+c, the GPU test's chains 1..8, so the two sides are
 independent samples of one posterior; both start from the same converged oracle state.
+The fixture is therefore oracle-relative (parity with the reference unpinned for these
+posteriors: no output of the reference covers them); the oracle is pinned by the TD fixtures.
 
     python tests/golden/make_vignette2_fixture.py      # ~7 minutes on 8 cores
 """

@@ -209,12 +209,16 @@ def test_graph_replay_matches_eager(monkeypatch, thin):
     slot chosen on the device); the recorded chain must equal the eager launch sequence bit
     for bit (same kernels, same order, same Philox counters), also when the run length is
     not a multiple of the sweeps per replay (remainders replay the graphs of the smaller
-    powers of two: 46 = 32 + 8 + 4 + 2 at the default 32 sweeps per replay)."""
+    powers of two: 46 = 32 + 8 + 4 + 2 at the default 32 sweeps per replay).  Inside a
+    replay the side chain is joined on the device (flags, no cross-queue graph edges) unless
+    HMSC_SIDE_EDGES=1; both equal the eager sequence."""
     hM = synthetic_model(ny=200, ns=30, nc=4, nf=3, nt=2, seed=12)
     out = []
-    for no_graph, per in (("1", "4"), ("0", "4"), ("0", "3"), ("0", "1"), ("0", "32")):
+    for no_graph, per, edges in (("1", "4", "0"), ("0", "4", "0"), ("0", "3", "0"), ("0", "1", "0"), ("0", "32", "0"),
+                                 ("0", "32", "1")):
         monkeypatch.setenv("HMSC_NO_GRAPH", no_graph)
         monkeypatch.setenv("HMSC_GRAPH_SWEEPS", per)
+        monkeypatch.setenv("HMSC_SIDE_EDGES", edges)
         ch = H.Chain(hM, 77, device=0, updater={"GammaEta": False})
         ch.init()
         rec = ch.run(transient=5, samples=41, thin=thin, adaptNf=[0])

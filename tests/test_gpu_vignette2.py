@@ -11,6 +11,11 @@ itself off, :150-152).  Checked against the oracle:
   * the posterior of 8 GPU chains against 4 oracle chains (tests/golden/vignette2_posterior.npz)
     for the two nr = 0 models and the vignette's sample-level model (:143, GammaEta on):
     means within Monte Carlo error, Gelman-Rubin over both sides, KS on thinned draws.
+The posterior fixture is produced by this repository's CPU oracle
+(tests/golden/make_vignette2_fixture.py), not by the reference: R is absent and
+/root/reference holds no vignette_2 posterior draws (its PDF shows only ESS / summary tables),
+so the posterior checks are oracle-relative -- the device chains against the oracle's chains.
+The oracle itself is pinned to the reference by the TD fixtures.
 """
 import os
 
