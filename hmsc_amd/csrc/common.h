@@ -73,7 +73,7 @@ __device__ __forceinline__ void vm_stores_done() { asm volatile("s_waitcnt vmcnt
 // into slot i of a device table read back with hmsc_debug_get(s, "stamps", ...).  The
 // product build compiles it away.
 #ifdef HMSC_STAMPS
-extern __device__ unsigned long long g_stamps[256];
+extern __device__ unsigned long long g_stamps[1024];  // [0, 256): named slots; [256, 1024): per-workgroup
 #define HMSC_STAMP(i)                                                              \
   do {                                                                             \
     unsigned long long t_;                                                         \

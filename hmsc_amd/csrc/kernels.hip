@@ -32,7 +32,7 @@
 namespace hmsc {
 
 #ifdef HMSC_STAMPS
-__device__ unsigned long long g_stamps[256];
+__device__ unsigned long long g_stamps[1024];
 #endif
 
 static bool getenv_flag(const char* name) {
@@ -42,8 +42,8 @@ static bool getenv_flag(const char* name) {
 
 void read_stamps(double* out, int n) {
 #ifdef HMSC_STAMPS
-  unsigned long long h[256];
-  HMSC_REQUIRE(n <= 256, "stamps: at most 256 slots");
+  unsigned long long h[1024];
+  HMSC_REQUIRE(n <= 1024, "stamps: at most 1024 slots");
   HIP_OK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_stamps), sizeof(h)));
   for (int i = 0; i < n; ++i) out[i] = (double)h[i];
 #else
@@ -327,7 +327,7 @@ __device__ __forceinline__ void side_wait(const int* flags, int n, int epoch, in
 // What the fused launch's tail (bl_tail) needs of a species' update, lane k holding row k:
 // the new column BL[:, j], Mu_j = Gamma Tr_j^T (rows < nc) and tau = cumprod(Delta) (rows >= nc)
 struct BLCol {
-  double r, mu, tau;
+  double r, mu, tau, isig;
 };
 
 // side_wait (the fused launch inside a sweep graph, sweeps after the first): iV and Delta come
@@ -347,6 +347,7 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
   const int j = blk * 4 + w;
   if (blk == 0) HMSC_STAMP(60);
   if (side_n > 0) side_wait(side_sync, side_n, side_epoch, gsync);
+  if (WAIT_GAMMA && blk == 0 && w == 0) HMSC_STAMP_RT(84);
   // every global load of the prologue is issued before the first LDS store (a staging loop
   // with a store per iteration waits out one memory latency per iteration)
   double gv[4], ivv[4];
@@ -377,7 +378,7 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
   if (!WAIT_GAMMA && t < nc * nt && t < 32 * 8) sGam[t] = gam;
   if (t < a.NF) sTau[t] = del;  // Delta here; each lane forms its own cumprod below
   __syncthreads();
-  if (j >= a.ns_loc) return BLCol{0.0, 0.0, 1.0};
+  if (j >= a.ns_loc) return BLCol{0.0, 0.0, 1.0, 0.0};
   double* lds = tiles + w * WV_TILE;
   // tau = cumprod(Delta) within the level of factor i - nc   (:51)
   double tau = 1.0;
@@ -469,7 +470,14 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
   if (blk == 0) HMSC_STAMP(64);
   if (WAIT_GAMMA && blk == 0 && w == 0) HMSC_STAMP_RT(76);
   if (a.kt && i == 0) kt_record(a.kt, SWEEP_ITER(a), kt0);
-  return BLCol{r, mu, tau};
+#ifdef HMSC_STAMPS
+  if (WAIT_GAMMA && w == 0 && blk < 384) {  // per-workgroup body start / end (wall clock)
+    unsigned long long t1;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+    if (i == 0) g_stamps[256 + blk] = t1;
+  }
+#endif
+  return BLCol{r, mu, tau, isig};
 }
 
 template <int NM>
@@ -886,6 +894,7 @@ __device__ __forceinline__ void gammav_body(const GVWArgs& a) {
     HMSC_STAMP(4);
     if (!ok && i == 0) a.fail[0] = 1;
     if (a.flags) {  // Gamma and iV are out (the next sweep's fused launch waits on this)
+      HMSC_STAMP_RT(83);
       __threadfence();
       if (i == 0) __hip_atomic_store(&a.flags[0], g2bl_epoch(SWEEP_ITER(a)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -1042,7 +1051,8 @@ void launch_gamma_v(State& s, uint32_t iter, hipStream_t st) {
 // Stage 2: single-workgroup dense algebra.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void gamma2_partial_body(const double* XZ, const double* BL, int K, int nc, int NF, int nt,
-                                                    int ns_loc, const double* Tr, double* part, double* smem, int bid) {
+                                                    int ns_loc, const double* Tr, double* part, double* smem, int bid,
+                                                    bool coherent = false) {
   // part[b] = [ XZ[0:nc, block] Tr (nc*nt) | Lambda_all[:, block] Tr (NF*nt) ]
   double* sX = smem;             // K x SB: rows < nc from XZ, rows >= nc from BL (Lambda)
   double* sTr = sX + K * SB;     // SB x nt
@@ -1070,7 +1080,10 @@ __device__ __forceinline__ void gamma2_partial_body(const double* XZ, const doub
     }
     double acc = 0.0;
     for (int jj = 0; jj < nj; ++jj) acc = fma(sX[k + K * jj], sTr[jj + SB * q], acc);
-    out[p] = acc;
+    if (coherent)
+      store_coherent(out + p, acc);
+    else
+      out[p] = acc;
   }
 }
 
@@ -1160,6 +1173,7 @@ __global__ __launch_bounds__(256) void gamma2_prep_kernel(G2PrepArgs a) {
 
 struct G2Args {
   int nc, nt, Kmax, NF, nparts, ns_loc, use_xtztr, check_isigma, stage;
+  int coherent;  // partials (and prep) written by other workgroups of the same launch / another queue
   const double* isig_count;  // sharded chain: all-reduced count of species with iSigma != 1
   const double* part;
   const double* xtztr;
@@ -1218,7 +1232,8 @@ __device__ __forceinline__ void gamma2_final_body(const G2Args& a, double* lds) 
   const double *B1 = a.prep, *LS = a.prep + n2;
   if (a.stage) {
     double* d = dyn;
-    batched_for<8>(n2 + N * N, [&](int p) { return a.prep[p]; }, [&](int p, double v) { d[p] = v; });
+    batched_for<8>(n2 + N * N, [&](int p) { return a.coherent ? load_coherent(a.prep + p) : a.prep[p]; },
+                   [&](int p, double v) { d[p] = v; });
     B1 = d;
     LS = d + n2;
   }
@@ -1233,11 +1248,14 @@ __device__ __forceinline__ void gamma2_final_body(const G2Args& a, double* lds) 
         for (; b + 56 < a.nparts; b += 64) {
           double x[8];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) x[u] = a.part[(size_t)(b + 8 * u) * P + p];
+          for (int u = 0; u < 8; ++u) {
+            const double* q = a.part + (size_t)(b + 8 * u) * P + p;
+            x[u] = a.coherent ? load_coherent(q) : *q;
+          }
 #pragma unroll
           for (int u = 0; u < 8; ++u) s += x[u];
         }
-        for (; b < a.nparts; b += 8) s += a.part[(size_t)b * P + p];
+        for (; b < a.nparts; b += 8) s += a.coherent ? load_coherent(a.part + (size_t)b * P + p) : a.part[(size_t)b * P + p];
       }
       red[g][l + (p0 ? 32 : 0)] = s;
     }
@@ -1256,7 +1274,7 @@ __device__ __forceinline__ void gamma2_final_body(const G2Args& a, double* lds) 
     for (int p = t; p < P; p += blockDim.x) {
       double s = 0.0;
 #pragma unroll 8
-      for (int b = 0; b < a.nparts; ++b) s += a.part[(size_t)b * P + p];
+      for (int b = 0; b < a.nparts; ++b) s += a.coherent ? load_coherent(a.part + (size_t)b * P + p) : a.part[(size_t)b * P + p];
       if (p < n1)
         S0[p] = a.use_xtztr ? a.xtztr[p] : s;
       else
@@ -1309,14 +1327,18 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
 // ---------------------------------------------------------------------------
 // updateGamma2 + updateBetaLambda in one launch (R/sampleMcmc.R:221-229 runs them back to
 // back; BetaLambda's precision iU and its Cholesky factor do not depend on the Gamma that
-// Gamma2 draws, only its mean does).  Workgroups 0 .. nparts-1 form Gamma2's species-block
-// partials; the last of them to finish (a ticket) reduces them in block order, runs the final
-// stage and publishes Gamma (sync[1]); workgroups nparts.. run the wave BetaLambda body, which
-// factors iU while Gamma2 runs and waits for Gamma only for the mean and the solves.  Every
-// workgroup of the launch is resident at once (nparts + ns / 4 <= 3 per CU at 52 KB of LDS),
-// so the wait cannot block the workgroup it waits for.  The ticket is reset by the workgroup
-// that takes the last one; the flag holds the sweep's epoch (g2bl_epoch), reset to 0 by the
-// host at the start of every run and before every eager launch, so it never needs a reset
+// Gamma2 draws, only its mean does).  Workgroups 1 .. nbl run the wave BetaLambda body (four
+// species each, one per wave), which factors iU while Gamma2 runs and waits for Gamma only
+// for the mean and the solves; the first nparts of them form one of Gamma2's species-block
+// partials first (device-coherent stores, a relaxed count in sync[0]).  Workgroup 0 waits for
+// the count, reduces the partials in block order, runs the final stage and publishes Gamma
+// (sync[1]).  One extra workgroup instead of nparts: the launch is nbl + 1 <= 256 workgroups
+// at the config-4 size, one per CU -- with nparts separate partial workgroups some CUs carried
+// two BetaLambda chains and the slowest species finished ~8 us after the rest.  Every
+// workgroup of the launch is resident at once (two per CU at 52 KB of LDS), and workgroup 0 is
+// dispatched before the ones it waits for, so no wait can block the workgroup it waits for.
+// Workgroup 0 resets the count; the flag holds the sweep's epoch (g2bl_epoch), reset to 0 by
+// the host at the start of every run and before every eager launch, so it never needs a reset
 // inside the launch.
 // ---------------------------------------------------------------------------
 // ---------------------------------------------------------------------------
@@ -1393,15 +1415,19 @@ struct BLTailArgs {
   Key key;
 };
 
-template <int NFB>
-__device__ void bl_tail(const BLTailArgs& ta, const BLCol col, int b, int nbl, uint32_t iter, double* smem) {
+__device__ __forceinline__ void bl_tail(const BLTailArgs& ta, const BLCol& col, int b, int nbl, uint32_t iter,
+                                        double* smem) {
   __shared__ int s_last;
   const CRWArgs& a = ta.crw;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, K = a.K, nc = a.nc, nf = a.nf;
   const int j = 4 * b + w;
   const bool act = j < a.ns;
   const double r = col.r;
-  const double isig = act ? a.iSigma[j] : 0.0;
+  if (b == 0 && w == 0) HMSC_STAMP_RT(77);
+  double trq[8];  // Tr[j, q] (loaded first: its latency overlaps the draws below)
+#pragma unroll
+  for (int q = 0; q < 8; ++q) trq[q] = (ta.gv_on && act && q < ta.nt) ? ta.Tr[j + (size_t)a.ns * q] : 0.0;
+  const double isig = act ? col.isig : 0.0;
   const double lam = __shfl(r, nc + (lane & 15));  // lane h: Lambda[h, j]
   if (act && lane < 16) a.LS[(size_t)16 * j + lane] = lane < nf ? isig * lam : 0.0;
   const double rk = (act && lane < K) ? r * isig : 0.0;
@@ -1428,6 +1454,7 @@ __device__ void bl_tail(const BLTailArgs& ta, const BLCol col, int b, int nbl, u
     ta.Psi[f + (size_t)NF * j] = psi;
     m2 = psi * lam2;
   }
+  if (b == 0 && w == 0) HMSC_STAMP_RT(85);
   __syncthreads();  // every wave is past the body's LDS tiles
   double* sC = smem;                  // [w][h][k]
   double* sV = smem + 4 * CRW_TILE;   // [w][ngv]
@@ -1443,7 +1470,9 @@ __device__ void bl_tail(const BLTailArgs& ta, const BLCol col, int b, int nbl, u
       if (c2 < nc && lane < nc) v[lane + nc * c2] = e * e2;  // E E^T
     }
     if (lane < nc)
-      for (int q = 0; q < nt; ++q) v[nA + lane + nc * q] = act ? r * ta.Tr[j + (size_t)a.ns * q] : 0.0;  // Beta Tr
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (q < nt) v[nA + lane + nc * q] = r * trq[q];  // Beta Tr
     if (lane >= nc && lane < K) v[nA + nB + lane - nc] = m2;
     else if (lane >= K && lane < nc + NF) v[nA + nB + lane - nc] = 0.0;
   }
@@ -1452,19 +1481,23 @@ __device__ void bl_tail(const BLTailArgs& ta, const BLCol col, int b, int nbl, u
   double* P = a.part;
   double* V = ta.gvt;
   const int ld = ta.gvt_ld;
+  // (plain stores + one L2 write-back per workgroup before the ticket measured 3 % slower per
+  // sweep than these write-through stores)
+  auto put = [&](double* p, double v) { store_coherent(p, v); };
   for (int q = t; q < ne; q += 256)
-    store_coherent(P + (size_t)b * CRW_TILE + q,
-                   (sC[q] + sC[CRW_TILE + q]) + (sC[2 * CRW_TILE + q] + sC[3 * CRW_TILE + q]));
+    put(P + (size_t)b * CRW_TILE + q, (sC[q] + sC[CRW_TILE + q]) + (sC[2 * CRW_TILE + q] + sC[3 * CRW_TILE + q]));
   if (ta.gv_on)
     for (int q = t; q < ngv; q += 256)
-      store_coherent(V + (size_t)b * ld + q, (sV[q] + sV[ngv + q]) + (sV[2 * ngv + q] + sV[3 * ngv + q]));
+      put(V + (size_t)b * ld + q, (sV[q] + sV[ngv + q]) + (sV[2 * ngv + q] + sV[3 * ngv + q]));
   vm_stores_done();
   __syncthreads();
+  if (b == 0 && t < 64) HMSC_STAMP_RT(86);
   const int g = b / CRW_GROUP, g0 = g * CRW_GROUP, gn = min(CRW_GROUP, nbl - g0);
   const int ng = (nbl + CRW_GROUP - 1) / CRW_GROUP;
   if (t == 0) s_last = __hip_atomic_fetch_add(&a.ticket[2 + g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gn - 1;
   __syncthreads();
   if (!s_last) return;
+  if (g == 0 && t < 64) HMSC_STAMP_RT(78);
   // group reducer: the group's tiles in workgroup order
   const int ntot = ne + (ta.gv_on ? ngv : 0);
   for (int q = t; q < ntot; q += 256) {
@@ -1477,15 +1510,17 @@ __device__ void bl_tail(const BLTailArgs& ta, const BLCol col, int b, int nbl, u
     double v = 0.0;
 #pragma unroll
     for (int u = 0; u < CRW_GROUP; ++u) v += x[u];
-    store_coherent((cr ? P + q : V + (q - ne)) + (size_t)(nbl + g) * st, v);
+    put((cr ? P + q : V + (q - ne)) + (size_t)(nbl + g) * st, v);
   }
   if (t == 0) __hip_atomic_store(&a.ticket[2 + g], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   vm_stores_done();
   __syncthreads();
+  if (g == 0 && t < 64) HMSC_STAMP_RT(87);
   if (t == 0) s_last = __hip_atomic_fetch_add(&a.ticket[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
   __syncthreads();
   if (!s_last) return;
   // every group tile is in: the side chain may start (it sums the GammaV / psi group tiles)
+  if (t < 64) HMSC_STAMP_RT(79);
   if (t == 0) {
     __hip_atomic_store(&a.ticket[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (ta.gv_on) __hip_atomic_store(ta.tails_flag, g2bl_epoch(iter), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1507,7 +1542,16 @@ __device__ void bl_tail(const BLTailArgs& ta, const BLCol col, int b, int nbl, u
     if (h < nf && k < K) a.CR[k + (size_t)a.ldcr * h] = v;
   }
   __syncthreads();
-  if (w == 0) crw_finish<NFB>(a, sCR, smem);
+  if (t < 64) HMSC_STAMP_RT(88);
+  if (w == 0) {
+    if (nf <= 8)
+      crw_finish<8>(a, sCR, smem);
+    else if (nf <= 12)
+      crw_finish<12>(a, sCR, smem);
+    else
+      crw_finish<16>(a, sCR, smem);
+  }
+  if (w == 0) HMSC_STAMP_RT(80);
 }
 
 struct G2BLArgs {
@@ -1530,37 +1574,48 @@ struct G2BLArgs {
 template <int NM>
 __global__ __launch_bounds__(256) void gamma2_bl_kernel(G2BLArgs f) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  __shared__ int s_last;
-  const int nparts = f.g2.nparts;
-  if ((int)blockIdx.x < nparts) {
-    if (blockIdx.x == 0 && threadIdx.x < 64) HMSC_STAMP_RT(70);
-    gamma2_partial_body(f.XZ, f.BLold, f.K, f.nc, f.NF, f.nt, f.nsl, f.Tr, f.part, smem, blockIdx.x);
-    __syncthreads();  // the workgroup's partial stores complete; thread 0's release publishes them
-    if (threadIdx.x == 0)
-      s_last = __hip_atomic_fetch_add(&f.sync[0], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nparts - 1;
-    __syncthreads();
-    if (blockIdx.x == 0 && threadIdx.x < 64) HMSC_STAMP_RT(71);
-    if (!s_last) return;
-    if (f.side_wait) {  // the previous sweep's GammaV (Gamma, iV) and Gamma2 prep, behind the fence below
+  const int nparts = f.g2.nparts, nbl = (int)gridDim.x - 1;
+  if (blockIdx.x == 0) {
+    if (threadIdx.x < 64) HMSC_STAMP_RT(70);
+    // every partial is in (relaxed count; the partials are device-coherent stores, read with
+    // device-coherent loads), bounded like every in-launch wait
+    if (threadIdx.x == 0) {
+      for (int spin = 0; __hip_atomic_load(&f.sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nparts; ++spin) {
+        if (spin > (1 << 20)) {
+          __hip_atomic_store(&f.sync[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    if (f.side_wait) {  // the previous sweep's GammaV (Gamma, iV) and Gamma2 prep (read coherently)
       const int ep = g2bl_epoch(SWEEP_ITER(f.g2) - 1);
       side_wait(f.side_sync, 1, ep, f.sync);
       if (f.side_prep) side_wait(f.side_sync + 1 + f.bl.nr, 1, ep, f.sync);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every block's partials
+    __syncthreads();
     if (threadIdx.x < 64) HMSC_STAMP_RT(72);
     gamma2_final_body(f.g2, smem);
     __syncthreads();
     if (threadIdx.x < 64) HMSC_STAMP_RT(73);
     if (threadIdx.x == 0) {
-      __hip_atomic_store(&f.sync[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every ticket is in
+      __hip_atomic_store(&f.sync[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every partial is in
       __hip_atomic_store(&f.sync[1], g2bl_epoch(SWEEP_ITER(f.g2)), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
     return;
   }
+  const int b = blockIdx.x - 1;
+  if (b < nparts) {
+    if (b == 0 && threadIdx.x < 64) HMSC_STAMP_RT(71);
+    gamma2_partial_body(f.XZ, f.BLold, f.K, f.nc, f.NF, f.nt, f.nsl, f.Tr, f.part, smem, b, true);
+    vm_stores_done();
+    __syncthreads();  // every wave's partial stores have completed (and the LDS is free again)
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(&f.sync[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   const uint32_t iter = SWEEP_ITER(f.g2);
-  const BLCol col = beta_lambda_wave_body<NM, true>(f.bl, smem, blockIdx.x - nparts, f.sync, f.side_sync,
-                                                    g2bl_epoch(iter - 1), f.side_wait ? 1 + f.bl.nr : 0);
-  if (f.crw_on) bl_tail<(NM < 16 ? NM : 16)>(f.tail, col, blockIdx.x - nparts, gridDim.x - nparts, iter, smem);
+  const BLCol col = beta_lambda_wave_body<NM, true>(f.bl, smem, b, f.sync, f.side_sync, g2bl_epoch(iter - 1),
+                                                    f.side_wait ? 1 + f.bl.nr : 0);
+  if (f.crw_on) bl_tail(f.tail, col, b, nbl, iter, smem);
 }
 
 static void launch_gamma2_prep(State& s, hipStream_t st) {
@@ -1702,6 +1757,7 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
   a.iter_dev = s.capturing ? s.d_iter : nullptr;
   a.noise_zero = s.noise_mode;
   a.stage = 1;
+  a.coherent = 1;
   f.bl = make_bl_args(s, iter);
   f.XZ = s.XZ;
   f.BLold = s.BL;
@@ -1740,7 +1796,8 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
   f.side_wait = dev_join;
   f.side_prep = (s.mask & HMSC_UP_GAMMA2) ? 1 : 0;
   if (!s.capturing) HIP_OK(hipMemsetAsync(s.gbl_sync + 1, 0, sizeof(int), s.stream));  // an eager sweep may repeat an iter
-  const int nb = nparts + (s.nsl + 3) / 4;
+  const int nb = 1 + (s.nsl + 3) / 4;
+  HMSC_REQUIRE(nparts <= nb - 1, "fused Gamma2 + BetaLambda: more Gamma2 partials than BetaLambda workgroups");
   const size_t smem = BLW_LDS * sizeof(double);
   ProfScope ps(s, PROF_BL);
   switch (wv_bucket(s.K)) {
@@ -1915,7 +1972,9 @@ __global__ __launch_bounds__(256) void side_chain_kernel(GVWArgs g, LPArgs lp, c
   // waves on the same SIMDs: raised issue priority, so its few waves are not starved by the
   // VALU-bound z waves (the arbiter picks the highest-priority ready wave).
   __builtin_amdgcn_s_setprio(3);
+  if (blockIdx.x == 0 && threadIdx.x < 64) HMSC_STAMP_RT(81);
   if (tails_flag) side_wait(tails_flag, 1, g2bl_epoch(SWEEP_ITER(g)), err);
+  if (blockIdx.x == 0 && threadIdx.x < 64) HMSC_STAMP_RT(82);
   if (blockIdx.x == 0)
     gammav_body<NM>(g);
   else

@@ -24,9 +24,22 @@ st = ch.debug_get("stamps", 128)
 groups = {"gammav_wave": range(0, 10), "delta": range(20, 22), "gamma2_final": range(30, 33), "eta_shared(block0)": range(40, 45), "eta_fused(block0)": range(50, 56),
           "beta_lambda(block0)": range(60, 65), "gammav_wave1": range(10, 15)}
 v = np.array([st[i] for i in range(70, 77)])
-print("gamma2_bl (10 ns ticks from the first partial block's start): partial0 done", v[1] - v[0],
+print("gamma2_bl (10 ns ticks from workgroup 0's start): partial0 start", v[1] - v[0],
       "final start", v[2] - v[0], "final done", v[3] - v[0], "BL0 chol done", v[4] - v[0],
       "BL0 wait done", v[5] - v[0], "BL0 end", v[6] - v[0])
+v = np.array([st[i] for i in range(70, 89)], dtype=np.float64)
+t0 = v[0]
+print("  tail (10 ns ticks from workgroup 0 start): BL0 side-wait done", v[14] - t0, "BL0 tail start", v[7] - t0,
+      "group0 reducer", v[8] - t0, "final reducer", v[9] - t0, "final done", v[10] - t0)
+print("  tail block0: draws done", v[15] - t0, "tile stored", v[16] - t0, "group0 tile stored", v[17] - t0,
+      "final sums in", v[18] - t0)
+print("  side chain: start", v[11] - t0, "tails seen", v[12] - t0, "GammaV out", v[13] - t0, "(of the last sweep)")
+if "--blocks" in sys.argv:  # per-BetaLambda-workgroup body end (wall clock), from workgroup 0's start
+    allst = ch.debug_get("stamps", 1024)
+    e = np.array(allst[256:256 + 250], dtype=np.float64) - t0
+    print("  BL body end per workgroup (10 ns): min %.0f median %.0f p90 %.0f max %.0f" % (e.min(), np.median(e), np.percentile(e, 90), e.max()))
+    order = np.argsort(e)[::-1][:12]
+    print("  latest workgroups:", [(int(b), int(e[b])) for b in order])
 for name, idx in groups.items():
     v = np.array([st[i] for i in idx])
     d = np.diff(v)
