@@ -711,9 +711,9 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.CR_part = dalloc<double>((size_t)((nsl + 31) / 32) * s.Kmax * nfm);
   s.LS = dalloc<double>((size_t)std::max(nfm, 16) * nsl);  // [species][16] (cr_body)
   s.etaW = dalloc<double>(16 * 16);
-  {  // crw_kernel: 4 parts x 4 tiles x 16 x 16; crw_tail: (nbl + ngroups) tiles of 512
+  {  // crw_kernel: 4 parts x 4 tiles x 16 x 16; bl_tail: (nbl + ngroups) tiles of CRW_TILE (520)
     const size_t nbl = (size_t)(nsl + 3) / 4, ngr = (nbl + 15) / 16;
-    s.crw_part = dalloc<double>(std::max((size_t)4 * 4 * 256, (nbl + ngr) * 512));
+    s.crw_part = dalloc<double>(std::max((size_t)4 * 4 * 256, (nbl + ngr) * 520));
     s.crw_ticket = dalloc<int>(2 + ngr);  // dalloc zero-fills
     s.gvt_ld = nc * nc + N + nfm;             // [A nc^2 | BTr nc nt | rs NF]
     s.gvt = dalloc<double>((nbl + ngr) * (size_t)s.gvt_ld);
@@ -2032,6 +2032,13 @@ int hmsc_debug_get(hmsc_state* h, const char* name, double* out, int64_t n) {
     else if (nm == "ZL") src = s.ZL_part, avail = (int64_t)s.zl_split * s.ny * s.NF;
     else if (nm == "stamps") {
       read_stamps(out, (int)n);
+      return;
+    } else if (nm == "kt") {  // raw live-timing words: per id, KT_SLOTS starts then KT_SLOTS ends (wall-clock ticks)
+      HMSC_REQUIRE(s.d_kt != nullptr, "debug_get kt: kernel timing is off");
+      const int64_t m = std::min<int64_t>(n, (int64_t)KT_N * 2 * KT_SLOTS);
+      std::vector<unsigned long long> v((size_t)m);
+      copy_sync(v.data(), s.d_kt, sizeof(unsigned long long) * m, hipMemcpyDeviceToHost, s.stream);
+      for (int64_t i = 0; i < m; ++i) out[i] = (double)v[i];
       return;
     } else if (nm.rfind("nngp_perm", 0) == 0 || nm.rfind("nngp_bw", 0) == 0) {  // NNGP factorization order
       const bool perm = nm.rfind("nngp_perm", 0) == 0;

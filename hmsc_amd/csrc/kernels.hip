@@ -232,6 +232,7 @@ struct BLArgs {
   uint32_t iter;
   const uint32_t* iter_dev;  // graph replay: the sweep counter is read from the device
   unsigned long long* kt;    // live launch timing (KT_BL block) or null
+  int kt_defer;              // the fused launch's tail records the BetaLambda timing (BLCol kt0 / kt1)
   int noise_zero;
 };
 
@@ -328,6 +329,7 @@ __device__ __forceinline__ void side_wait(const int* flags, int n, int epoch, in
 // the new column BL[:, j], Mu_j = Gamma Tr_j^T (rows < nc) and tau = cumprod(Delta) (rows >= nc)
 struct BLCol {
   double r, mu, tau, isig;
+  unsigned long long kt0, kt1;  // the wave's body start / end (wall clock) when the tail records them
 };
 
 // side_wait (the fused launch inside a sweep graph, sweeps after the first): iV and Delta come
@@ -378,7 +380,7 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
   if (!WAIT_GAMMA && t < nc * nt && t < 32 * 8) sGam[t] = gam;
   if (t < a.NF) sTau[t] = del;  // Delta here; each lane forms its own cumprod below
   __syncthreads();
-  if (j >= a.ns_loc) return BLCol{0.0, 0.0, 1.0, 0.0};
+  if (j >= a.ns_loc) return BLCol{0.0, 0.0, 1.0, 0.0, ~0ull, 0ull};
   double* lds = tiles + w * WV_TILE;
   // tau = cumprod(Delta) within the level of factor i - nc   (:51)
   double tau = 1.0;
@@ -469,7 +471,10 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
   if (i < K) a.BL[i + (size_t)K * j] = r;
   if (blk == 0) HMSC_STAMP(64);
   if (WAIT_GAMMA && blk == 0 && w == 0) HMSC_STAMP_RT(76);
-  if (a.kt && i == 0) kt_record(a.kt, SWEEP_ITER(a), kt0);
+  // (the fused launch's tail folds the waves' start / end into its reduction tree and records
+  // once: a thousand same-address device atomics at the end of the bodies cost ~10 us)
+  const unsigned long long kt1 = (a.kt && a.kt_defer) ? kt_now() : 0ull;
+  if (a.kt && !a.kt_defer && i == 0) kt_record(a.kt, SWEEP_ITER(a), kt0);
 #ifdef HMSC_STAMPS
   if (WAIT_GAMMA && w == 0 && blk < 384) {  // per-workgroup body start / end (wall clock)
     unsigned long long t1;
@@ -477,7 +482,7 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
     if (i == 0) g_stamps[256 + blk] = t1;
   }
 #endif
-  return BLCol{r, mu, tau, isig};
+  return BLCol{r, mu, tau, isig, kt0, kt1};
 }
 
 template <int NM>
@@ -1352,7 +1357,7 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
 // ---------------------------------------------------------------------------
 constexpr int CRW_PARTS = 4;    // crw_kernel's workgroups
 constexpr int CRW_GROUP = 16;   // crw_tail: BetaLambda workgroups summed by one group reducer
-constexpr int CRW_TILE = 512;   // crw_tail partial tile: [h < 16][k < 32]
+constexpr int CRW_TILE = 520;   // bl_tail partial tile: [h < 16][k < 32], then 2 timing words
 struct CRWArgs {
   const double* BL;
   const double* iSigma;
@@ -1413,6 +1418,8 @@ struct BLTailArgs {
   double* gvt;      // (nbl + ngroups) x gvt_ld
   int* tails_flag;  // epoch of the sweep whose tails are all in
   Key key;
+  unsigned long long* kt;     // live timing of the last reducer (KT_TAIL block) or null
+  unsigned long long* kt_bl;  // live timing of the BetaLambda bodies (KT_BL block), via the tiles
 };
 
 __device__ __forceinline__ void bl_tail(const BLTailArgs& ta, const BLCol& col, int b, int nbl, uint32_t iter,
@@ -1462,6 +1469,10 @@ __device__ __forceinline__ void bl_tail(const BLTailArgs& ta, const BLCol& col, 
 #pragma unroll
     for (int h = 0; h < 16; ++h)
       if (h < nf) sC[w * CRW_TILE + h * 32 + lane] = c[h];
+  if (ta.kt_bl && lane == 0) {
+    sC[w * CRW_TILE + 512] = (double)col.kt0;
+    sC[w * CRW_TILE + 513] = (double)col.kt1;
+  }
   if (ta.gv_on) {
     double* v = sV + w * ngv;
 #pragma unroll
@@ -1486,6 +1497,11 @@ __device__ __forceinline__ void bl_tail(const BLTailArgs& ta, const BLCol& col, 
   auto put = [&](double* p, double v) { store_coherent(p, v); };
   for (int q = t; q < ne; q += 256)
     put(P + (size_t)b * CRW_TILE + q, (sC[q] + sC[CRW_TILE + q]) + (sC[2 * CRW_TILE + q] + sC[3 * CRW_TILE + q]));
+  if (ta.kt_bl && t < 2) {  // the workgroup's first body start / last body end
+    const int q = 512 + t;
+    const double x0 = sC[q], x1 = sC[CRW_TILE + q], x2 = sC[2 * CRW_TILE + q], x3 = sC[3 * CRW_TILE + q];
+    put(P + (size_t)b * CRW_TILE + q, t == 0 ? fmin(fmin(x0, x1), fmin(x2, x3)) : fmax(fmax(x0, x1), fmax(x2, x3)));
+  }
   if (ta.gv_on)
     for (int q = t; q < ngv; q += 256)
       put(V + (size_t)b * ld + q, (sV[q] + sV[ngv + q]) + (sV[2 * ngv + q] + sV[3 * ngv + q]));
@@ -1512,6 +1528,14 @@ __device__ __forceinline__ void bl_tail(const BLTailArgs& ta, const BLCol& col, 
     for (int u = 0; u < CRW_GROUP; ++u) v += x[u];
     put((cr ? P + q : V + (q - ne)) + (size_t)(nbl + g) * st, v);
   }
+  if (ta.kt_bl && t < 2) {
+    double m = t == 0 ? 1e300 : 0.0;
+    for (int u = 0; u < gn; ++u) {
+      const double x = load_coherent(P + (size_t)(g0 + u) * CRW_TILE + 512 + t);
+      m = t == 0 ? fmin(m, x) : fmax(m, x);
+    }
+    put(P + (size_t)(nbl + g) * CRW_TILE + 512 + t, m);
+  }
   if (t == 0) __hip_atomic_store(&a.ticket[2 + g], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   vm_stores_done();
   __syncthreads();
@@ -1519,6 +1543,7 @@ __device__ __forceinline__ void bl_tail(const BLTailArgs& ta, const BLCol& col, 
   if (t == 0) s_last = __hip_atomic_fetch_add(&a.ticket[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
   __syncthreads();
   if (!s_last) return;
+  const unsigned long long kt0 = ta.kt ? kt_now() : 0ull;
   // every group tile is in: the side chain may start (it sums the GammaV / psi group tiles)
   if (t < 64) HMSC_STAMP_RT(79);
   if (t == 0) {
@@ -1552,6 +1577,17 @@ __device__ __forceinline__ void bl_tail(const BLTailArgs& ta, const BLCol& col, 
       crw_finish<16>(a, sCR, smem);
   }
   if (w == 0) HMSC_STAMP_RT(80);
+  if (ta.kt && t == 0) kt_record(ta.kt, iter, kt0);
+  if (ta.kt_bl && t == 0) {  // the BetaLambda bodies' first start / last end, once
+    double m0 = 1e300, m1 = 0.0;
+    for (int u = 0; u < ng; ++u) {
+      m0 = fmin(m0, load_coherent(P + (size_t)(nbl + u) * CRW_TILE + 512));
+      m1 = fmax(m1, load_coherent(P + (size_t)(nbl + u) * CRW_TILE + 513));
+    }
+    const uint32_t slot = iter & (KT_SLOTS - 1);
+    __hip_atomic_fetch_min(ta.kt_bl + slot, (unsigned long long)m0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_max(ta.kt_bl + KT_SLOTS + slot, (unsigned long long)m1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 struct G2BLArgs {
@@ -1569,6 +1605,7 @@ struct G2BLArgs {
   const int* side_sync; // side_wait: [GammaV, delta chain per level ..., Gamma2 prep] flags of
   int side_wait;        // the previous sweep's side chain (graph sweeps after the first)
   int side_prep;        // ... and its Gamma2 prep flag
+  unsigned long long* kt_g2;  // live timing of workgroup 0 (KT_G2 block) or null
 };
 
 template <int NM>
@@ -1576,6 +1613,7 @@ __global__ __launch_bounds__(256) void gamma2_bl_kernel(G2BLArgs f) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int nparts = f.g2.nparts, nbl = (int)gridDim.x - 1;
   if (blockIdx.x == 0) {
+    const unsigned long long kt0 = f.kt_g2 ? kt_now() : 0ull;
     if (threadIdx.x < 64) HMSC_STAMP_RT(70);
     // every partial is in (relaxed count; the partials are device-coherent stores, read with
     // device-coherent loads), bounded like every in-launch wait
@@ -1601,6 +1639,7 @@ __global__ __launch_bounds__(256) void gamma2_bl_kernel(G2BLArgs f) {
     if (threadIdx.x == 0) {
       __hip_atomic_store(&f.sync[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every partial is in
       __hip_atomic_store(&f.sync[1], g2bl_epoch(SWEEP_ITER(f.g2)), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      if (f.kt_g2) kt_record(f.kt_g2, SWEEP_ITER(f.g2), kt0);
     }
     return;
   }
@@ -1788,6 +1827,9 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
     t.gvt = s.gvt;
     t.tails_flag = s.gbl_sync + 2;
     t.key = s.key;
+    t.kt = s.kt_on ? s.d_kt + (size_t)KT_TAIL * 2 * KT_SLOTS : nullptr;
+    t.kt_bl = f.bl.kt;
+    f.bl.kt_defer = 1;
   }
   s.crw_fresh = crw_on;
   s.tail_gv = tail_gv;
@@ -1795,7 +1837,8 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
   f.side_sync = s.side_sync;
   f.side_wait = dev_join;
   f.side_prep = (s.mask & HMSC_UP_GAMMA2) ? 1 : 0;
-  if (!s.capturing) HIP_OK(hipMemsetAsync(s.gbl_sync + 1, 0, sizeof(int), s.stream));  // an eager sweep may repeat an iter
+  f.kt_g2 = s.kt_on ? s.d_kt + (size_t)KT_G2 * 2 * KT_SLOTS : nullptr;
+  if (!s.capturing) HIP_OK(hipMemsetAsync(s.gbl_sync + 1, 0, 2 * sizeof(int), s.stream));  // an eager sweep may repeat an iter
   const int nb = 1 + (s.nsl + 3) / 4;
   HMSC_REQUIRE(nparts <= nb - 1, "fused Gamma2 + BetaLambda: more Gamma2 partials than BetaLambda workgroups");
   const size_t smem = BLW_LDS * sizeof(double);
