@@ -64,7 +64,7 @@ def parse():
     p.add_argument("--cpu-oracle-sweeps", type=int, default=None,
                    help="configs 3 / 5: sweeps of the numpy restatement timed for cpu_baseline "
                         "(default 10 for config 3, 3 for config 5)")
-    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r03_s31_pmc.json"),
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r04_s3_pmc.json"),
                    help="rocprofv3 PMC summary (scripts/pmc_summary.py) the roofline's traffic / valu come from")
     return p.parse_args()
 
@@ -261,6 +261,8 @@ def main():
                                       f"effectiveSize restated); ESS/s = ESS per sweep x timed sweeps/s"},
         "roofline": {"kernel": roof_kernel, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_source": (os.path.relpath(args.pmc_json, ROOT) + " (rocprofv3 PMC passes, FETCH_SIZE x 2 "
+                                        "+ WRITE_SIZE per launch)") if traffic else None,
                      "algorithmic_bytes_per_launch": algo_bytes[roof_kernel],
                      "avg_launch_us": round(live[roof_kernel]["avg_us"], 3),
                      "timed_launches": live[roof_kernel]["launches"],

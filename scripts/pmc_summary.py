@@ -35,7 +35,14 @@ for k, cs in vals.items():
         # are 8-B or 1-B per lane may be over-corrected, so the raw figure is kept beside it
         d["hbm_bytes_per_launch_uncorrected"] = d["FETCH_SIZE"] * 1024 + d["hbm_write_bytes"]
     if "GRBM_GUI_ACTIVE" in d and d["avg_us_profiled"] > 0:
-        d["eff_clock_ghz"] = d["GRBM_GUI_ACTIVE"] / 8 / (d["avg_us_profiled"] * 1e3)
+        # GRBM_GUI_ACTIVE / 8 / wall time reads high on dispatches shorter than ~0.3 ms
+        # (MI355X_MICROARCH.md, DVFS give-back: the counter's window is wider than the kernel),
+        # so the quotient is an effective clock only for long dispatches
+        q = d["GRBM_GUI_ACTIVE"] / 8 / (d["avg_us_profiled"] * 1e3)
+        if d["avg_us_profiled"] >= 300:
+            d["eff_clock_ghz"] = q
+        else:
+            d["grbm_active_per_us_not_a_clock"] = q
     if "SQ_INSTS_VALU" in d and "SQ_WAVES" in d:
         d["valu_insts_per_wave"] = d["SQ_INSTS_VALU"] / max(1, d["SQ_WAVES"])
     if "SQ_WAVE_CYCLES" in d and "SQ_ACTIVE_INST_VALU" in d:
