@@ -727,9 +727,11 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.psi_rs = dalloc<double>((size_t)64 * nfm);
   s.ABpart = dalloc<double>((size_t)((nsl + 31) / 32) * (nc * nc + 2 * N + nfm * nt + 8));
   s.allreduce_buf = dalloc<double>((size_t)nc * nc + 2 * N + nfm * nt + nfm + 64);
-  s.dev_flags = dalloc<int>(16);
-  s.gbl_sync = dalloc<int>(4);  // dalloc zero-fills
-  s.trsv_sync = dalloc<int>(DENSE_SYNC_INTS);
+  // the device error / handshake words in one block (dalloc zero-fills), so the host reads
+  // every error word with one copy: [dev_flags 16 | gbl_sync 4 | trsv_sync DENSE_SYNC_INTS]
+  s.dev_flags = dalloc<int>(16 + 4 + DENSE_SYNC_INTS);
+  s.gbl_sync = s.dev_flags + 16;
+  s.trsv_sync = s.dev_flags + 20;
   s.d_iters = dalloc<uint32_t>(64);  // graph_sweeps <= 64
   s.d_iter = s.d_iters;
   if (s.mask & HMSC_UP_GAMMAETA) {  // updateGammaEta: dense (nc ns)^2 / joint spatial systems
@@ -780,7 +782,7 @@ static void free_state(State& s) {
   s.unpack_pool.reset();  // idle between runs; joined before the host ring goes
   void* ptrs[] = {s.X, s.Tr, s.Yval, s.Yraw, s.Ycode, s.Ybits, s.logtab, s.fam, s.varest, s.V0, s.iUGamma, s.mGamma, s.UGammaL,
                   s.aSigma, s.bSigma, s.XX, s.TT, s.V0g, s.V0gXXV0g, s.iV0, s.V0inv, s.iUmG, s.V0gXX, s.g2prep, s.scratch2, s.na_cols, s.na_index,
-                  s.na_rows, s.row_na, s.row_slot, s.dev_flags, s.gbl_sync, s.trsv_sync, s.Z, s.XEta, s.BL, s.Psi, s.Delta, s.Gamma, s.iV,
+                  s.na_rows, s.row_na, s.row_slot, s.dev_flags, s.Z, s.XEta, s.BL, s.Psi, s.Delta, s.Gamma, s.iV,
                   s.iSigma, s.rho, s.XZ, s.G, s.ZTr, s.XZ_part, s.G_part, s.ZTr_part, s.Gna, s.ZL, s.ZL_part,
                   s.CR, s.CR_part, s.LS, s.etaW, s.crw_part, s.crw_ticket, s.gvt, s.side_sync, s.Gamma_side, s.Msmall, s.scratch, s.psi_rs, s.ABpart, s.dbg_prec, s.ring, s.allreduce_buf,
                   s.phU, s.phWinv, s.phRbase, s.phTt, s.phBt, s.phEt, s.phTTw, s.phWork, s.UGamma, s.geWork};
@@ -838,12 +840,12 @@ void join_side(State& s) {
 // name the wait, state.h HsErr).  A timed-out wait lets its launch drain on stale data, so a
 // run that saw one must fail, never return its samples.  Called with the streams idle.
 static void check_device_flags(State& s) {
-  int flag[16] = {0};
-  copy_sync(flag, s.dev_flags, sizeof(flag), hipMemcpyDeviceToHost, s.stream);
-  int gsync[4] = {0, 0, 0, 0};
-  copy_sync(gsync, s.gbl_sync, sizeof(gsync), hipMemcpyDeviceToHost, s.stream);
-  int hs = 0;
-  copy_sync(&hs, s.trsv_sync + DENSE_SYNC_ERR, sizeof(int), hipMemcpyDeviceToHost, s.stream);
+  // one copy of the error block (build_state): dev_flags, gbl_sync, the dense handshake words
+  int blk[20 + DENSE_SYNC_ERR + 1] = {0};
+  copy_sync(blk, s.dev_flags, sizeof(blk), hipMemcpyDeviceToHost, s.stream);
+  const int* flag = blk;
+  const int* gsync = blk + 16;
+  const int hs = blk[20 + DENSE_SYNC_ERR];
   if (hs != 0) {
     std::string what;
     if (hs & HS_ERR_TRSV_FLAG) what += " [sync-free triangular solve: a block flag never came up]";

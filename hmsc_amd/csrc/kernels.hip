@@ -2518,6 +2518,12 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
   }
   const double* zc = a.Z + min(i0 + lm, ny - 1);  // sites past ny: any finite row, unused
   const int nsteps = (ns + 15) >> 4;
+  // the per-site noise of stage 2 (one (site, factor) pair per thread, t < EF_SITES nf <= 256):
+  // drawn while the stream's first loads are in flight instead of after the stream
+  double xi_pre = 0.0;
+  const int xs2 = t % EF_SITES, xh = t / EF_SITES;
+  const bool x_on = t < EF_SITES * nf && i0 + xs2 < ny && !a.noise_zero;
+  const int x_unit = x_on ? a.Pi[i0 + xs2] : 0;
   int s = 0;
   for (; s + EF_DEPTH <= nsteps; s += EF_DEPTH) {
     double zv[EF_DEPTH], lv[EF_DEPTH];
@@ -2527,9 +2533,11 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
       zv[u] = j < ns ? zc[(size_t)ny * j] : 0.0;
       lv[u] = j < ns ? a.LS[(size_t)16 * j + lm] : 0.0;
     }
+    if (s == 0 && x_on) xi_pre = normal(a.key, (uint32_t)x_unit, (uint32_t)xh, S_ETA, iter);
 #pragma unroll
     for (int u = 0; u < EF_DEPTH; ++u) acc = mfma_f64(zv[u], lv[u], acc);
   }
+  if (s == 0 && x_on) xi_pre = normal(a.key, (uint32_t)x_unit, (uint32_t)xh, S_ETA, iter);  // (a short stream)
   for (; s < nsteps; s += 8) {  // the tail: eight steps' loads at once
     double zv[8], lv[8];
 #pragma unroll
@@ -2571,7 +2579,7 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
       // X from the tile staged in LDS (a global load per term here waited out one L2
       // round trip per covariate: ~6 us of the kernel's serial tail)
       for (int k = 0; k < nc; ++k) corr = fma(sX[k][s2], sCR[k * NFB + h], corr);
-      xi = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)sPi[s2], (uint32_t)h, S_ETA, iter);
+      xi = p == t ? xi_pre : (a.noise_zero ? 0.0 : normal(a.key, (uint32_t)sPi[s2], (uint32_t)h, S_ETA, iter));
     }
     sB[h][s2] = zl - corr;
     sXi[h][s2] = xi;
