@@ -538,6 +538,17 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
         HMSC_REQUIRE(bad == 0, "spatial level: a grid matrix W_g = exp(-d / alpha_g) is not positive definite "
                                "(duplicated coordinates?)");
       }
+      {  // the spatial workspace (for NNGP the band is still held in a full (np nf)^2 array):
+         // a clear create-time error instead of an allocation failure mid-setup
+        const size_t need = spatial_work_doubles(s, r) * sizeof(double);
+        size_t free_b = 0, total_b = 0;
+        HIP_OK(hipMemGetInfo(&free_b, &total_b));
+        HMSC_REQUIRE(need < free_b, "spatial level " + std::to_string(r) + ": its workspace needs " +
+                                        std::to_string(need >> 20) + " MiB (the " +
+                                        (L.nngp ? std::string("NNGP band is stored as a full (np nf)^2 array") :
+                                                  std::string("(np nf)^2 dense system")) +
+                                        "), " + std::to_string(free_b >> 20) + " MiB free on the device");
+      }
       L.spWork = dalloc<double>(spatial_work_doubles(s, r));
     }
   }
@@ -720,6 +731,11 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   }
   s.side_sync = dalloc<int>(2 + HMSC_MAX_LEVELS);
   s.Gamma_side = dalloc<double>(N);
+  // under rocprofv3 (ROCPROF_OUTPUT_PATH, as for the graph node cap) the side chain keeps its
+  // graph edges: counter passes serialise dispatches, and a device-side join would wait on a
+  // launch queued behind it until its time bound (error -5); the kernel tracer delays the side
+  // queue's dispatches enough that the traced durations would not be the sweep's
+  if (std::getenv("ROCPROF_OUTPUT_PATH")) s.edge_free = false;
   if (const char* e = std::getenv("HMSC_SIDE_EDGES")) s.edge_free = e[0] != '1';
   s.scratch_doubles = 1 << 20;
   s.scratch = dalloc<double>(s.scratch_doubles);

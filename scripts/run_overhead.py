@@ -1,6 +1,6 @@
-"""Fixed cost of one hmsc_run call at the synthetic config 4 (GPU box): wall time of
-run(samples=S) for S = 1, 8, 20, 100, 1000, recorded and unrecorded, after warm-up; with
-HMSC_DIAG_TIMING=1 the library prints enqueue / completion / unpack / slot-wait times."""
+"""Where a short recorded run's time goes (the driver's 20-step line): the bench's chain
+prepared the same way (graphs prebuilt, clock warm-up), then repeated 20-sweep recorded
+runs timed piecewise on the host; HMSC_DIAG_TIMING adds the library's own breakdown."""
 import os
 import sys
 import time
@@ -12,30 +12,32 @@ sys.path.insert(0, ROOT)
 import hmsc_amd as H  # noqa: E402
 from hmsc_amd.workloads import synthetic_probit  # noqa: E402
 
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 hM = synthetic_probit()
 ch = H.Chain(hM, 1234567, device=0, updater={"GammaEta": False})
 ch.init([10])
+ch.kernel_timing(True)
 ch.run(transient=0, samples=1, thin=1, adaptNf=[0], record=True)
 ch.prepare_graphs(2)
 it = 1
-ch.run(transient=0, samples=400, thin=1, adaptNf=[0], iter0=it, record=True)
-it += 400
+t_w = time.perf_counter()
+while time.perf_counter() - t_w < 0.5:
+    ch.run(transient=0, samples=50, thin=1, adaptNf=[0], iter0=it, record=True)
+    it += 50
 ch.sync()
-for rec in (True, False):
-    for S in (1, 8, 20, 20, 100, 1000):
-        t0 = time.perf_counter()
-        if rec:
-            ch.run(transient=0, samples=S, thin=1, adaptNf=[0], iter0=it, record=True)
-            t1 = time.perf_counter()
-        else:
-            ch.run(transient=S, samples=0, thin=1, adaptNf=[0], iter0=it, record=False)
-        ch.sync()
-        dt = time.perf_counter() - t0
-        it += S
-        extra = f" (run() returned at {1e3 * (t1 - t0):.3f} ms)" if rec else ""
-        print(f"record={rec} S={S}: {1e3 * dt:.3f} ms, {1e3 * dt / S:.4f} ms/sweep{extra}", flush=True)
+rows = []
+for rep in range(8):
+    t0 = time.perf_counter()
+    rec = ch.run(transient=0, samples=n, thin=1, adaptNf=[0], iter0=it, record=True)
+    t1 = time.perf_counter()
+    ch.sync()
+    t2 = time.perf_counter()
+    it += n
+    rows.append((t1 - t0, t2 - t1))
+r = np.array(rows) * 1e3
+print(f"{n}-sweep recorded run: run() {np.median(r[:, 0]):.3f} ms, sync() {np.median(r[:, 1]):.3f} ms, "
+      f"per sweep {np.median(r.sum(1)) / n * 1e3:.1f} us")
 t0 = time.perf_counter()
-a = np.zeros((20, 10, 10000))
-a[:] = 1.0
-print(f"alloc+touch 16 MB: {1e3 * (time.perf_counter() - t0):.3f} ms")
-ch.close()
+ch.run(transient=0, samples=1000, thin=1, adaptNf=[0], iter0=it, record=True)
+ch.sync()
+print(f"1000-sweep recorded run: {(time.perf_counter() - t0) / 1000 * 1e6:.1f} us per sweep")
