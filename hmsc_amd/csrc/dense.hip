@@ -209,35 +209,71 @@ __device__ inline bool chol16_mfma(double* Tb, double* Ib) {
   return ok;
 }
 
+// Off-diagonal 16-block (ib, jb) of L^-1 by one wave: I_ib,jb = -I_ib,ib sum_{k = jb}^{ib - 1}
+// L_ib,k I_k,jb -- needs L's block row ib and the inverse blocks (k, jb), k < ib, and
+// (ib, ib).  Sw: this wave's 16 x 17 scratch.
+__device__ __forceinline__ void inv_block(const double* T, double* I, double* Sw, int ib, int jb) {
+  const int lane = threadIdx.x & 63, lm = lane & 15, lk = lane >> 4;
+  // S = sum_{k = jb}^{ib - 1} L_ib,k I_k,jb   (B operand B[k][j] = I[16 k' + k][16 jb + j])
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  for (int kk = 16 * jb; kk < 16 * ib; kk += 4)
+    acc = mfma_f64(T[(16 * ib + lm) + DLD * (kk + lk)], I[(kk + lk) + DLD * (16 * jb + lm)], acc);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) Sw[(lk + 4 * r) + 17 * lm] = acc[r];
+  wave_lds_sync();
+  // I_ib,jb = -I_ib,ib S
+  d4 acc2 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4)
+    acc2 = mfma_f64(I[(16 * ib + lm) + DLD * (16 * ib + 4 * s4 + lk)], Sw[(4 * s4 + lk) + 17 * lm], acc2);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) I[(16 * ib + lk + 4 * r) + DLD * (16 * jb + lm)] = -acc2[r];
+}
+
 // The factorization of the block staged in T (lower triangle, zeros above, identity past nb);
-// I zeroed; S: 4 x 16 x 17 doubles.  All 256 threads.
+// I zeroed; S: 4 x 16 x 17 doubles.  All 256 threads.  L^-1's off-diagonal blocks are formed
+// by the waves that would idle while wave 0 factors the next 16 x 16 pivot block (row kb - 1
+// of the inverse during step kb's pivot), the last block row after the loop.  Linv goes out
+// first (device-coherent stores); with pflag (the fused update's next panel waits on it) the
+// flag is raised before L itself is written back to A (no launch reads the block's L).
 __device__ inline void diag_body(double* T, double* I, double (*S)[16 * 17], double* A, int lda, int n, int k0,
-                          double* Linv, int* info) {
+                          double* Linv, int* info, int* pflag = nullptr, int pflag_value = 0, int* sync = nullptr) {
   __shared__ int bad;
   const int nb = min(DB, n - k0), t = threadIdx.x, lane = t & 63, w = t >> 6, lm = lane & 15, lk = lane >> 4;
   if (t == 0) bad = 0;
   __syncthreads();
-  for (int kb = 0; kb < 4; ++kb) {
+  // a. 16 x 16 Cholesky and inverse of pivot block 0 on the matrix cores (chol16_mfma)
+  if (w == 0 && !chol16_mfma(T, I) && lane == 0) bad = 1;
+  __syncthreads();
+  DENSE_STAMP(102);
+  for (int kb = 0; kb < 3; ++kb) {
     const int K0 = 16 * kb;
-    if (w == 0) {  // a. 16 x 16 Cholesky and inverse on the matrix cores (chol16_mfma)
-      if (!chol16_mfma(T + K0 + DLD * K0, I + K0 + DLD * K0) && lane == 0) bad = 1;
+    const int nrt = 3 - kb;  // 16-row tiles below this diagonal block
+    // b. P_I = A_I,kb L16^-T for tiles I = kb + 1 + w (w < nrt)
+    if (w < nrt) {
+      const int R = K0 + 16 + 16 * w;
+      d4 acc = {0.0, 0.0, 0.0, 0.0};
+      acc = mma16_nt(T, R, K0, I, K0, K0, acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) T[(R + lk + 4 * r) + DLD * (K0 + lm)] = acc[r];
     }
     __syncthreads();
-    DENSE_STAMP(102 + 2 * kb);
-    const int nrt = 3 - kb;  // 16-row tiles below this diagonal block
-    if (nrt > 0) {
-      // b. P_I = A_I,kb L16^-T for tiles I = kb + 1 + w (w < nrt)
-      if (w < nrt) {
-        const int R = K0 + 16 + 16 * w;
-        d4 acc = {0.0, 0.0, 0.0, 0.0};
-        acc = mma16_nt(T, R, K0, I, K0, K0, acc);
+    DENSE_STAMP(103 + 2 * kb);
+    // c. A_IJ -= P_I P_J^T for kb < J <= I.  Wave 0 takes the next pivot block (kb+1, kb+1)
+    // and goes straight on to factor it (a. of step kb + 1); waves 1-3 take the other tiles
+    // and then block row kb of L^-1 (its blocks are independent of each other): the pivot
+    // chain no longer waits for the whole trailing update, nor for the inverse.
+    const int ntile = nrt * (nrt + 1) / 2;
+    if (w == 0) {
+      const int R = K0 + 16;
+      d4 acc = {0.0, 0.0, 0.0, 0.0};
+      acc = mma16_nt(T, R, K0, T, R, K0, acc);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) T[(R + lk + 4 * r) + DLD * (K0 + lm)] = acc[r];
-      }
-      __syncthreads();
-      // c. A_IJ -= P_I P_J^T for kb < J <= I (nrt (nrt + 1) / 2 <= 6 tiles over the 4 waves)
-      const int ntile = nrt * (nrt + 1) / 2;
-      for (int q = w; q < ntile; q += 4) {
+      for (int r = 0; r < 4; ++r) T[(R + lk + 4 * r) + DLD * (R + lm)] -= acc[r];
+      wave_lds_sync();
+      if (!chol16_mfma(T + R + DLD * R, I + R + DLD * R) && lane == 0) bad = 1;
+    } else {
+      for (int q = w; q < ntile; q += 3) {  // tiles 1 .. ntile - 1 over waves 1-3
         int ti = 0;
         while ((ti + 1) * (ti + 2) / 2 <= q) ++ti;
         const int tj = q - ti * (ti + 1) / 2;
@@ -247,47 +283,49 @@ __device__ inline void diag_body(double* T, double* I, double (*S)[16 * 17], dou
 #pragma unroll
         for (int r = 0; r < 4; ++r) T[(R + lk + 4 * r) + DLD * (C + lm)] -= acc[r];
       }
-      __syncthreads();
-    }
-    DENSE_STAMP(103 + 2 * kb);
-  }
-  // off-diagonal 16-blocks of L^-1 by diagonal distance, one wave per block
-  for (int dd = 1; dd < 4; ++dd) {
-    const int nblk = 4 - dd;
-    if (w < nblk) {
-      const int jb = w, ib = jb + dd;
-      double* Sw = S[w];
-      // S = sum_{k = jb}^{ib - 1} L_ib,k I_k,jb   (B operand B[k][j] = I[16 k' + k][16 jb + j])
-      d4 acc = {0.0, 0.0, 0.0, 0.0};
-      for (int kk = 16 * jb; kk < 16 * ib; kk += 4)
-        acc = mfma_f64(T[(16 * ib + lm) + DLD * (kk + lk)], I[(kk + lk) + DLD * (16 * jb + lm)], acc);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Sw[(lk + 4 * r) + 17 * lm] = acc[r];
-      wave_lds_sync();
-      // I_ib,jb = -I_ib,ib S
-      d4 acc2 = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4)
-        acc2 = mfma_f64(I[(16 * ib + lm) + DLD * (16 * ib + 4 * s4 + lk)], Sw[(4 * s4 + lk) + 17 * lm], acc2);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) I[(16 * ib + lk + 4 * r) + DLD * (16 * jb + lm)] = -acc2[r];
+      if (w <= kb) inv_block(T, I, S[w], kb, w - 1);  // block row kb: jb = 0 .. kb - 1
     }
     __syncthreads();
+    DENSE_STAMP(104 + 2 * kb);
   }
+  DENSE_STAMP(109);
+  // the last block row of L^-1 (its three blocks are independent), one wave per block
+  if (w < 3) inv_block(T, I, S[w], 3, w);
+  __syncthreads();
   DENSE_STAMP(110);
   {
-    double tv[DB * DB / 256], iv[DB * DB / 256];  // every LDS read before the first store
+    double iv[DB * DB / 256];  // every LDS read before the first store
+#pragma unroll
+    for (int u = 0; u < DB * DB / 256; ++u) {
+      const int p = t + 256 * u, r = p & 63, c = p >> 6;
+      iv[u] = I[r + DLD * c];
+    }
+#pragma unroll
+    for (int u = 0; u < DB * DB / 256; ++u) store_coherent(Linv + t + 256 * u, iv[u]);
+  }
+  if (pflag) {
+    // Linv out at device scope (write-through stores, each wave waits for its own), then the
+    // publish.  A test (hmsc_debug_poison "chol_publish") can withhold one publish: the waiting
+    // tiles must then time out and report.
+    vm_stores_done();
+    __syncthreads();
+    if (t == 0) {
+      const bool skip = __hip_atomic_exchange(sync + DENSE_SYNC_TEST, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                        HS_TEST_SKIP_PUBLISH;
+      if (!skip) __hip_atomic_store(pflag, pflag_value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  {
+    double tv[DB * DB / 256];
 #pragma unroll
     for (int u = 0; u < DB * DB / 256; ++u) {
       const int p = t + 256 * u, r = p & 63, c = p >> 6;
       tv[u] = T[r + DLD * c];
-      iv[u] = I[r + DLD * c];
     }
 #pragma unroll
     for (int u = 0; u < DB * DB / 256; ++u) {
       const int p = t + 256 * u, r = p & 63, c = p >> 6;
       if (r < nb && c < nb && r >= c) A[(size_t)(k0 + r) + (size_t)lda * (k0 + c)] = tv[u];
-      Linv[p] = iv[u];
     }
   }
   if (t == 0 && bad) atomicExch(info, 1);
@@ -510,20 +548,8 @@ __global__ __launch_bounds__(256, 2) void chol_update_kernel(double* A, int lda,
             if (r < rowsI && c < rowsJ && r >= c) T[r + DLD * c] = cv[a][b][q] - acc[a][b][q];
           }
     __syncthreads();
-    diag_body(T, I, S, A, lda, n, base, Linv_next, info);
-    if (pflag) {
-      // Linv_next written: every thread's stores complete at device scope (each wave's own
-      // fence -- the barrier alone orders them only within the workgroup), then publish.
-      // A test (hmsc_debug_poison "chol_publish") can withhold one publish: the waiting
-      // tiles must then time out and report.
-      __threadfence();
-      __syncthreads();
-      if (t == 0) {
-        const bool skip = __hip_atomic_exchange(sync + DENSE_SYNC_TEST, 0, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT) == HS_TEST_SKIP_PUBLISH;
-        if (!skip) __hip_atomic_store(pflag, k0 / DB + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
+    // (Linv_next out with device-coherent stores and pflag raised inside, before L's write-back)
+    diag_body(T, I, S, A, lda, n, base, Linv_next, info, pflag, k0 / DB + 1, sync);
   }
 }
 

@@ -22,8 +22,9 @@ int main() {
   (void)hipMalloc(&dA, sizeof(double) * n * n);
   (void)hipMalloc(&dL, sizeof(double) * 64 * 64);
   (void)hipMalloc(&info, sizeof(int));
-  const char* names[] = {"load+stage", "kb0 chol16", "kb0 panel+update", "kb1 chol16", "kb1 panel+update",
-                         "kb2 chol16", "kb2 panel+update", "kb3 chol16", "kb3 (none)", "inverse blocks", "store"};
+  const char* names[] = {"load+stage", "pivot 0", "kb0 panel", "kb0 update | pivot 1 | inverse row 0",
+                         "kb1 panel", "kb1 update | pivot 2 | inverse row 1", "kb2 panel",
+                         "kb2 update | pivot 3 | inverse row 2", "-", "inverse row 3", "store"};
   for (int rep = 0; rep < 5; ++rep) {
     (void)hipMemcpy(dA, A.data(), sizeof(double) * n * n, hipMemcpyHostToDevice);
     hipEvent_t e0, e1;
