@@ -64,7 +64,7 @@ def parse():
     p.add_argument("--cpu-oracle-sweeps", type=int, default=None,
                    help="configs 3 / 5: sweeps of the numpy restatement timed for cpu_baseline "
                         "(default 10 for config 3, 3 for config 5)")
-    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r04_s3_pmc.json"),
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r04_s4_pmc.json"),
                    help="rocprofv3 PMC summary (scripts/pmc_summary.py) the roofline's traffic / valu come from")
     return p.parse_args()
 
