@@ -1578,7 +1578,7 @@ __device__ __forceinline__ void bl_tail(const BLTailArgs& ta, const BLCol& col, 
   }
   if (w == 0) HMSC_STAMP_RT(80);
   if (ta.kt && t == 0) kt_record(ta.kt, iter, kt0);
-  if (ta.kt_bl && t == 0) {  // the BetaLambda bodies' first start / last end, once
+  if (ta.kt_bl && t == 64) {  // the BetaLambda bodies' first start / last end, once (wave 1, beside wave 0's factor)
     double m0 = 1e300, m1 = 0.0;
     for (int u = 0; u < ng; ++u) {
       m0 = fmin(m0, load_coherent(P + (size_t)(nbl + u) * CRW_TILE + 512));
