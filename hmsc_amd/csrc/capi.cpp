@@ -737,6 +737,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   // queue's dispatches enough that the traced durations would not be the sweep's
   if (std::getenv("ROCPROF_OUTPUT_PATH")) s.edge_free = false;
   if (const char* e = std::getenv("HMSC_SIDE_EDGES")) s.edge_free = e[0] != '1';
+  if (const char* e = std::getenv("HMSC_SIDE_PARTIALS")) s.side_partials = e[0] == '1';
   s.scratch_doubles = 1 << 20;
   s.scratch = dalloc<double>(s.scratch_doubles);
   s.scratch2 = dalloc<double>(s.scratch_doubles);

@@ -366,7 +366,8 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
   const int jj = j < a.ns_loc ? j : a.ns_loc - 1;
   const double isig = a.iSigma[jj];
   const double xz = i < K ? a.XZ[(i < K ? i : 0) + (size_t)K * jj] : 0.0;
-  const double psi = (i >= nc && i < K) ? a.Psi[(i - nc) + (size_t)a.NF * jj] : 0.0;
+  const double* pp = a.Psi + ((i >= nc && i < K) ? (i - nc) + (size_t)a.NF * jj : 0);
+  const double psi = (i >= nc && i < K) ? (side_n > 0 ? load_coherent(pp) : *pp) : 0.0;  // (post_bl_kernel's, side)
   double trj[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) trj[q] = q < nt ? a.Tr[jj + (size_t)a.ns_loc * q] : 0.0;
@@ -468,7 +469,14 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
   double lt[NM];
   wv_transpose<NM, true>(x, lt, lds);
   wv_backward_t<NM>(lt, dinv, r);          // m + backsolve(RiU, xi)  (:101)
-  if (i < K) a.BL[i + (size_t)K * j] = r;
+  // the fused launch: write-through, so the side work forked on the device at the tails flag
+  // (post_bl_kernel, still inside this launch's lifetime) reads the new column coherently
+  if (i < K) {
+    if (WAIT_GAMMA)
+      store_coherent(a.BL + i + (size_t)K * j, r);
+    else
+      a.BL[i + (size_t)K * j] = r;
+  }
   if (blk == 0) HMSC_STAMP(64);
   if (WAIT_GAMMA && blk == 0 && w == 0) HMSC_STAMP_RT(76);
   // (the fused launch's tail folds the waves' start / end into its reduction tree and records
@@ -564,16 +572,19 @@ constexpr int SB = 32;  // species per block of the species-sum reductions
 
 // Species-block partial sums for updateGammaV (R/updateGammaV.R:16-18,30):
 //   A = E E^T (E = Beta - Gamma Tr^T) and BTr = Beta Tr, staged through LDS.
+// coh: BL and Gamma read with device-coherent loads (post_bl_kernel forked on the device while
+// the fused Gamma2 + BetaLambda launch that wrote them is still running, post_bl_kernel)
 __device__ __forceinline__ void gammav_partial_body(const double* BL, int K, int nc, int nt, int ns_loc,
                                                     const double* Gamma, const double* Tr, double* part,
-                                                    double* smem, int bid) {
+                                                    double* smem, int bid, bool coh = false) {
   double* sB = smem;             // nc x SB
   double* sE = sB + nc * SB;     // nc x SB
   double* sTr = sE + nc * SB;    // SB x nt
   const int t = threadIdx.x, j0 = bid * SB, nj = min(SB, ns_loc - j0);
   for (int p = t; p < nc * nj; p += 256) {
     const int c = p % nc, jj = p / nc;
-    sB[p] = BL[c + (size_t)K * (j0 + jj)];
+    const double* q = BL + c + (size_t)K * (j0 + jj);
+    sB[p] = coh ? load_coherent(q) : *q;
   }
   for (int p = t; p < SB * nt; p += 256) {
     const int jj = p % SB, q = p / SB;
@@ -583,7 +594,7 @@ __device__ __forceinline__ void gammav_partial_body(const double* BL, int K, int
   for (int p = t; p < nc * nj; p += 256) {
     const int c = p % nc, jj = p / nc;
     double e = sB[p];
-    for (int q = 0; q < nt; ++q) e -= Gamma[c + nc * q] * sTr[jj + SB * q];
+    for (int q = 0; q < nt; ++q) e -= (coh ? load_coherent(Gamma + c + nc * q) : Gamma[c + nc * q]) * sTr[jj + SB * q];
     sE[p] = e;
   }
   __syncthreads();
@@ -1514,27 +1525,44 @@ __device__ __forceinline__ void bl_tail(const BLTailArgs& ta, const BLCol& col, 
   __syncthreads();
   if (!s_last) return;
   if (g == 0 && t < 64) HMSC_STAMP_RT(78);
-  // group reducer: the group's tiles in workgroup order
+  // group reducer: the group's tiles in workgroup order.  Every load of a thread (two elements
+  // x the group's tiles, and the timing words on threads 254 / 255) is issued before the first
+  // sum, so a pass costs one memory latency (a load-use loop pays one per tile)
   const int ntot = ne + (ta.gv_on ? ngv : 0);
-  for (int q = t; q < ntot; q += 256) {
-    const bool cr = q < ne;
-    const double* src = cr ? P + q : V + (q - ne);
-    const size_t st = cr ? CRW_TILE : ld;
-    double x[CRW_GROUP];
+  const bool kt_thr = ta.kt_bl && t >= 254;  // timing words 512 (min) / 513 (max)
+  double ktx[CRW_GROUP];
+  if (kt_thr)
 #pragma unroll
-    for (int u = 0; u < CRW_GROUP; ++u) x[u] = u < gn ? load_coherent(src + (size_t)(g0 + u) * st) : 0.0;
-    double v = 0.0;
+    for (int u = 0; u < CRW_GROUP; ++u)
+      ktx[u] = u < gn ? load_coherent(P + (size_t)(g0 + u) * CRW_TILE + 512 + (t - 254)) : (t == 254 ? 1e300 : 0.0);
+  for (int q0 = 0; q0 < ntot; q0 += 512) {
+    double x[2][CRW_GROUP];
 #pragma unroll
-    for (int u = 0; u < CRW_GROUP; ++u) v += x[u];
-    put((cr ? P + q : V + (q - ne)) + (size_t)(nbl + g) * st, v);
-  }
-  if (ta.kt_bl && t < 2) {
-    double m = t == 0 ? 1e300 : 0.0;
-    for (int u = 0; u < gn; ++u) {
-      const double x = load_coherent(P + (size_t)(g0 + u) * CRW_TILE + 512 + t);
-      m = t == 0 ? fmin(m, x) : fmax(m, x);
+    for (int e = 0; e < 2; ++e) {
+      const int q = q0 + t + 256 * e;
+      const bool cr = q < ne;
+      const double* src = cr ? P + q : V + (q - ne);
+      const size_t st = cr ? CRW_TILE : ld;
+#pragma unroll
+      for (int u = 0; u < CRW_GROUP; ++u)
+        x[e][u] = (q < ntot && u < gn) ? load_coherent(src + (size_t)(g0 + u) * st) : 0.0;
     }
-    put(P + (size_t)(nbl + g) * CRW_TILE + 512 + t, m);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int q = q0 + t + 256 * e;
+      if (q >= ntot) continue;
+      const bool cr = q < ne;
+      double v = 0.0;
+#pragma unroll
+      for (int u = 0; u < CRW_GROUP; ++u) v += x[e][u];
+      put((cr ? P + q : V + (q - ne)) + (size_t)(nbl + g) * (cr ? CRW_TILE : ld), v);
+    }
+  }
+  if (kt_thr) {
+    double m = ktx[0];
+#pragma unroll
+    for (int u = 1; u < CRW_GROUP; ++u) m = t == 254 ? fmin(m, ktx[u]) : fmax(m, ktx[u]);
+    put(P + (size_t)(nbl + g) * CRW_TILE + 512 + (t - 254), m);
   }
   if (t == 0) __hip_atomic_store(&a.ticket[2 + g], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   vm_stores_done();
@@ -1548,23 +1576,35 @@ __device__ __forceinline__ void bl_tail(const BLTailArgs& ta, const BLCol& col, 
   if (t < 64) HMSC_STAMP_RT(79);
   if (t == 0) {
     __hip_atomic_store(&a.ticket[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (ta.gv_on) __hip_atomic_store(ta.tails_flag, g2bl_epoch(iter), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // every BetaLambda column and tile is out: the side work (post_bl_kernel, or the side
+    // chain reading the tail's GammaV / psi group tiles) may start
+    if (ta.tails_flag) __hip_atomic_store(ta.tails_flag, g2bl_epoch(iter), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   double* sCR = smem + 4 * CRW_TILE;  // [row k][16]
-  for (int q = t; q < 512; q += 256) {
-    const int h = q >> 5, k = q & 31;
-    double v = 0.0;
-    if (h < nf)
-      for (int q0 = 0; q0 < ng; q0 += CRW_GROUP) {
-        double x[CRW_GROUP];
+  {
+    // CR = the group tiles summed in group order; each thread's two elements' loads of a
+    // chunk of groups issued together
+    double v[2] = {0.0, 0.0};
+    for (int q0 = 0; q0 < ng; q0 += CRW_GROUP) {
+      double x[2][CRW_GROUP];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int q = t + 256 * e, h = q >> 5;
 #pragma unroll
         for (int u = 0; u < CRW_GROUP; ++u)
-          x[u] = q0 + u < ng ? load_coherent(P + (size_t)(nbl + q0 + u) * CRW_TILE + q) : 0.0;
-#pragma unroll
-        for (int u = 0; u < CRW_GROUP; ++u) v += x[u];
+          x[e][u] = (h < nf && q0 + u < ng) ? load_coherent(P + (size_t)(nbl + q0 + u) * CRW_TILE + q) : 0.0;
       }
-    sCR[k * 16 + h] = v;
-    if (h < nf && k < K) a.CR[k + (size_t)a.ldcr * h] = v;
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int u = 0; u < CRW_GROUP; ++u) v[e] += x[e][u];
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int q = t + 256 * e, h = q >> 5, k = q & 31;
+      sCR[k * 16 + h] = v[e];
+      if (h < nf && k < K) a.CR[k + (size_t)a.ldcr * h] = v[e];
+    }
   }
   __syncthreads();
   if (t < 64) HMSC_STAMP_RT(88);
@@ -1580,9 +1620,19 @@ __device__ __forceinline__ void bl_tail(const BLTailArgs& ta, const BLCol& col, 
   if (ta.kt && t == 0) kt_record(ta.kt, iter, kt0);
   if (ta.kt_bl && t == 64) {  // the BetaLambda bodies' first start / last end, once (wave 1, beside wave 0's factor)
     double m0 = 1e300, m1 = 0.0;
-    for (int u = 0; u < ng; ++u) {
-      m0 = fmin(m0, load_coherent(P + (size_t)(nbl + u) * CRW_TILE + 512));
-      m1 = fmax(m1, load_coherent(P + (size_t)(nbl + u) * CRW_TILE + 513));
+    for (int q0 = 0; q0 < ng; q0 += CRW_GROUP) {
+      double x0[CRW_GROUP], x1[CRW_GROUP];
+#pragma unroll
+      for (int u = 0; u < CRW_GROUP; ++u) {
+        const double* p = P + (size_t)(nbl + (q0 + u < ng ? q0 + u : q0)) * CRW_TILE + 512;
+        x0[u] = load_coherent(p);
+        x1[u] = load_coherent(p + 1);
+      }
+#pragma unroll
+      for (int u = 0; u < CRW_GROUP; ++u) {
+        m0 = fmin(m0, x0[u]);
+        m1 = fmax(m1, x1[u]);
+      }
     }
     const uint32_t slot = iter & (KT_SLOTS - 1);
     __hip_atomic_fetch_min(ta.kt_bl + slot, (unsigned long long)m0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1765,10 +1815,10 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
   // are formed in the BetaLambda workgroups' tail (K <= 32 on this path, nf <= 16), with
   // GammaV's and LambdaPriors' species partials when their tile fits the tail's LDS
   const bool crw_on = s.nranks == 1 && side_fusion_ok(s) && s.lev[0].nf <= 16 && s.K <= 32;
-  const bool tail_gv = crw_on && (s.mask & HMSC_UP_GAMMA2) && s.nt <= 8 && s.nc * s.nc + s.nc * s.nt + s.NF <= 1024 &&
-                       s.gvt != nullptr;
+  const bool tail_gv = !s.side_partials && crw_on && (s.mask & HMSC_UP_GAMMA2) && s.nt <= 8 &&
+                       s.nc * s.nc + s.nc * s.nt + s.NF <= 1024 && s.gvt != nullptr;
   // graph sweeps after the first: the previous sweep's side chain is joined on the device
-  const bool dev_join = tail_gv && s.edge_free && s.capturing && s.cap_sweep > 0 && s.side_tail;
+  const bool dev_join = crw_on && s.edge_free && s.capturing && s.cap_sweep > 0 && s.side_tail;
   // iV, Gamma2's prep, Psi and Delta come from the previous sweep's side updaters
   if (!dev_join) join_side(s);
   if (!s.g2prep_valid) launch_gamma2_prep(s, s.stream);
@@ -1833,7 +1883,8 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
   }
   s.crw_fresh = crw_on;
   s.tail_gv = tail_gv;
-  s.side_tail = false;  // (set again by this sweep's launch_side_fused)
+  s.side_tail = false;  // (both set again by this sweep's launch_side_fused)
+  s.psi_side = true;
   f.side_sync = s.side_sync;
   f.side_wait = dev_join;
   f.side_prep = (s.mask & HMSC_UP_GAMMA2) ? 1 : 0;
@@ -1870,7 +1921,7 @@ struct LPArgs {
   const uint32_t* iter_dev;  // graph replay: the sweep counter is read from the device
 };
 
-__device__ __forceinline__ void psi_body(const LPArgs& a, int bid, int nb) {
+__device__ __forceinline__ void psi_body(const LPArgs& a, int bid, int nb, bool coh = false) {
   // grid over species columns; each block handles a contiguous species range
   __shared__ double sM[256];
   __shared__ double sTau[64];
@@ -1901,7 +1952,8 @@ __device__ __forceinline__ void psi_body(const LPArgs& a, int bid, int nb) {
     if (p < nelem) {
       const int f = p % NF, j = ja + p / NF;
       const int r = sLev[f], h = sH[f];
-      const double lam = a.BL[a.nc + f + (size_t)a.K * j];
+      const double* lp = a.BL + a.nc + f + (size_t)a.K * j;
+      const double lam = coh ? load_coherent(lp) : *lp;
       const double lam2 = lam * lam;
       const double shape = a.nu[r] / 2 + 0.5;
       const double rate = a.nu[r] / 2 + 0.5 * lam2 * sTau[f];            // (:22)
@@ -2630,8 +2682,10 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
 // (R/updateGammaV.R:17-19) and the psi draws of updateLambdaPriors (:22-24) -- followed by
 // two small serial tails, the GammaV algebra and the delta chain (:25-32).  The passes share
 // one launch (post_bl_kernel) and the tails another (side_chain_kernel, one workgroup each),
-// both on the side stream behind one event after BetaLambda; the side stream is joined just
-// before the next sweep's Gamma2 + BetaLambda launch.
+// both on the side stream.  Eager sweeps and a capture's first sweep fork them behind one
+// event after BetaLambda and join the side stream before the next sweep's Gamma2 +
+// BetaLambda launch; later graph sweeps do both on the device (post_bl_kernel waits for the
+// fused launch's tails flag, the next fused launch for the side chain's side_sync flags).
 // ---------------------------------------------------------------------------
 struct PostBLArgs {
   const double* BL;
@@ -2645,18 +2699,33 @@ struct PostBLArgs {
   int n_psi;
   const uint32_t* iter_src;  // graph replay: d_iter, snapshotted into iter_side for the side stream
   uint32_t* iter_side;
+  // graph sweeps after the first (edge-free): not behind a graph edge from the fused Gamma2 +
+  // BetaLambda launch; every workgroup waits for that launch's tails flag (its last reducer,
+  // after every BetaLambda workgroup's write-through column stores) and reads BL and Gamma
+  // with device-coherent loads
+  const int* tails_flag;
+  int* err;
 };
 
-// workgroups 0 .. n_gv-1: the GammaV partial blocks; then the psi parts
+// workgroup b < n_gv: GammaV partial block b; b < n_psi: psi part b
 __global__ __launch_bounds__(256) void post_bl_kernel(PostBLArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x;
-  if (b == 0 && threadIdx.x == 0 && a.iter_src) *a.iter_side = *a.iter_src;
-  if (b < a.n_gv) {
-    gammav_partial_body(a.BL, a.K, a.nc, a.nt, a.ns_loc, a.Gamma, a.Tr, a.gv_part, smem, b);
-    return;
+  const bool coh = a.tails_flag != nullptr;
+  if (b == 0 && threadIdx.x < 64) HMSC_STAMP_RT(89);
+  if (coh) {
+    if (threadIdx.x == 0) side_wait(a.tails_flag, 1, g2bl_epoch(SWEEP_ITER(a.lp)), a.err);
+    __syncthreads();
   }
-  psi_body(a.lp, b - a.n_gv, a.n_psi);
+  if (b == 0 && threadIdx.x < 64) HMSC_STAMP_RT(90);
+  if (b == 0 && threadIdx.x == 0 && a.iter_src) *a.iter_side = *a.iter_src;
+  // workgroup b: the GammaV partial of species block b, then the psi draws of its own species
+  // range (one launch of ceil(ns / SB) workgroups beside Eta and z, not one per pass)
+  if (b < a.n_gv) gammav_partial_body(a.BL, a.K, a.nc, a.nt, a.ns_loc, a.Gamma, a.Tr, a.gv_part, smem, b, coh);
+  if (b < a.n_psi) {
+    if (b < a.n_gv) __syncthreads();
+    psi_body(a.lp, b, a.n_psi, coh);
+  }
 }
 
 static bool eta_fused_ok(const State& s);
@@ -2702,9 +2771,10 @@ void launch_side_fused(State& s, uint32_t iter) {
   const bool cr_done = s.crw_fresh, tail = s.tail_gv;
   s.crw_fresh = false;
   s.tail_gv = false;
-  // graph sweeps after the first: the side chain is not forked by a graph edge; it waits on
-  // the device for the fused launch's tails (which it reads), see State::cap_sweep
-  const bool dev_fork = tail && s.edge_free && s.capturing && s.cap_sweep > 0;
+  // graph sweeps after the first: the side work is not forked by a graph edge; its first
+  // launch waits on the device for the fused launch's tails flag (raised by the last reducer
+  // of the tail, after every BetaLambda workgroup's stores), see State::cap_sweep
+  const bool dev_fork = cr_done && s.edge_free && s.capturing && s.cap_sweep > 0;
   if (!dev_fork) HIP_OK(hipEventRecord(s.ev_bl, s.stream));
   launch_eta_fused(s, iter, cr_done);
   if (!dev_fork) HIP_OK(hipStreamWaitEvent(s.side, s.ev_bl, 0));
@@ -2722,11 +2792,10 @@ void launch_side_fused(State& s, uint32_t iter) {
     rs = gt + s.nc * s.nc + s.nc * s.nt;
     nparts = ngr;
     rs_ld = s.gvt_ld;
-    s.side_tail = true;
   } else {
     // the species partials of GammaV and LambdaPriors first (post_bl_kernel), on the side stream
     const int ngv = (s.nsl + SB - 1) / SB;
-    const int npsi = std::min(LP_PARTS, std::max(1, s.nsl));
+    const int npsi = std::max(1, std::min({ngv, LP_PARTS, s.nsl}));  // psi_rs holds LP_PARTS rows
     PostBLArgs a{};
     a.BL = s.BL;
     a.iSigma = s.iSigma;
@@ -2743,18 +2812,25 @@ void launch_side_fused(State& s, uint32_t iter) {
     a.n_psi = npsi;
     a.iter_src = s.capturing ? s.d_iter : nullptr;
     a.iter_side = s.d_iter_side;
+    a.tails_flag = dev_fork ? s.gbl_sync + 2 : nullptr;
+    a.err = s.gbl_sync;
     const size_t smem = (size_t)(2 * s.nc * SB + SB * s.nt) * sizeof(double);
-    post_bl_kernel<<<ngv + npsi, 256, smem, s.side>>>(a);
+    post_bl_kernel<<<std::max(ngv, npsi), 256, smem, s.side>>>(a);
     HIP_OK(hipGetLastError());
     gw = make_gvw_args(s, iter, s.gv_part, ngv, s.capturing ? s.d_iter_side : nullptr);
     rs = s.psi_rs;
     nparts = npsi;
     rs_ld = s.NF;
   }
+  // the side chain publishes Gamma / iV, its Gamma2 prep and each level's Delta through
+  // side_sync, so the next graph sweep's fused launch can join it on the device
+  if (cr_done) gw.flags = s.side_sync;
+  s.side_tail = cr_done;
+  s.psi_side = !tail;
   lp.iter_dev = gw.iter_dev;
   // the GammaV algebra (writes Gamma, iV and Gamma2's prep) with the delta chains as extra
   // workgroups of the same launch
-  const int* tf = dev_fork ? s.gbl_sync + 2 : nullptr;
+  const int* tf = (dev_fork && tail) ? s.gbl_sync + 2 : nullptr;  // (else post_bl_kernel waited)
   switch (wv_bucket_gv(s.nc * s.nt)) {
     case 8: launch_side_chain<8>(s, gw, lp, rs, nparts, rs_ld, tf); break;
     case 16: launch_side_chain<16>(s, gw, lp, rs, nparts, rs_ld, tf); break;
@@ -3272,7 +3348,7 @@ static PackArgs make_pack_args(State& s, double* slot, int part) {
     off += n;
   };
   add(s.BL, (int64_t)s.K * s.nsl, false);
-  add(s.Psi, (int64_t)s.NF * s.nsl, !s.side_tail);  // the BetaLambda tail (main) or post_bl_kernel (side)
+  add(s.Psi, (int64_t)s.NF * s.nsl, s.psi_side);  // post_bl_kernel (side) or the BetaLambda tail (main)
   add(s.Delta, s.NF, true);
   add(part == 2 ? s.Gamma_side : s.Gamma, (int64_t)s.nc * s.nt, true);  // (the next sweep's Gamma2 rewrites Gamma)
   add(s.iV, (int64_t)s.nc * s.nc, true);
@@ -3285,7 +3361,7 @@ static PackArgs make_pack_args(State& s, double* slot, int part) {
   a.slot = slot;
   if (slot == nullptr) {  // captured into a graph replay: slot chosen on the device
     a.slot = s.ring;
-    a.iter_dev = (part == 2 && !s.side_tail) ? s.d_iter_side : s.d_iter;
+    a.iter_dev = (part == 2 && s.psi_side) ? s.d_iter_side : s.d_iter;
     a.desc = s.d_rec_desc;
     a.slot_stride = (int64_t)s.slot_doubles;
     a.ring_slots = s.ring_slots;

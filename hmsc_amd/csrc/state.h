@@ -102,13 +102,19 @@ struct State {
   // ... and its BetaLambda tail also formed GammaV's and LambdaPriors' species partials (gvt),
   // which the side chain reads instead of post_bl_kernel's
   bool tail_gv = false;
-  // graph sweeps after the first of a capture (cap_sweep > 0): the side chain is not forked
+  // HMSC_SIDE_PARTIALS=1 (read at create): the species partials always from post_bl_kernel on
+  // the side stream, forked on the device at the tails flag -- the fused launch ends ~5 us
+  // sooner, but the side work beside Eta and z costs them about as much (same 1000-step rate)
+  // and a replay's first sweeps wait longer for it (20-step line ~2 % lower)
+  bool side_partials = false;
+  // graph sweeps after the first of a capture (cap_sweep > 0): the side work is not forked
   // from the main stream nor joined into it by graph edges (each a ~5-6 us cross-queue gap on
-  // the critical path) but synchronised by device flags: it waits for the fused launch's tails
-  // (gbl_sync[2]), and the next fused launch waits for its side_sync flags
+  // the critical path) but synchronised by device flags: its first launch waits for the fused
+  // launch's tails (gbl_sync[2]), and the next fused launch waits for its side_sync flags
   int cap_sweep = -1;
   bool edge_free = true;    // (HMSC_SIDE_EDGES=1: graph edges everywhere)
-  bool side_tail = false;   // the last side chain read the BetaLambda tail's tiles and raises side_sync
+  bool side_tail = false;   // the last side chain raises side_sync (the next fused launch may join it on the device)
+  bool psi_side = true;     // the last sweep's psi draws ran on the side stream (post_bl_kernel), not in the tail
   int* side_sync = nullptr;      // [GammaV, delta chain per level ..., Gamma2 prep]: epoch of the sweep
   double* gvt = nullptr;         // the BetaLambda tail's GammaV / psi partial tiles
   int gvt_ld = 0;

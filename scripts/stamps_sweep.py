@@ -27,12 +27,13 @@ v = np.array([st[i] for i in range(70, 77)])
 print("gamma2_bl (10 ns ticks from workgroup 0's start): partial0 start", v[1] - v[0],
       "final start", v[2] - v[0], "final done", v[3] - v[0], "BL0 chol done", v[4] - v[0],
       "BL0 wait done", v[5] - v[0], "BL0 end", v[6] - v[0])
-v = np.array([st[i] for i in range(70, 89)], dtype=np.float64)
+v = np.array([st[i] for i in range(70, 91)], dtype=np.float64)
 t0 = v[0]
 print("  tail (10 ns ticks from workgroup 0 start): BL0 side-wait done", v[14] - t0, "BL0 tail start", v[7] - t0,
       "group0 reducer", v[8] - t0, "final reducer", v[9] - t0, "final done", v[10] - t0)
 print("  tail block0: draws done", v[15] - t0, "tile stored", v[16] - t0, "group0 tile stored", v[17] - t0,
       "final sums in", v[18] - t0)
+print("  post_bl (side partials): start", v[19] - t0, "tails seen", v[20] - t0)
 print("  side chain: start", v[11] - t0, "tails seen", v[12] - t0, "GammaV out", v[13] - t0, "(of the last sweep)")
 if "--blocks" in sys.argv:  # per-BetaLambda-workgroup body end (wall clock), from workgroup 0's start
     allst = ch.debug_get("stamps", 1024)

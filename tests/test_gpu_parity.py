@@ -213,22 +213,31 @@ def test_graph_replay_matches_eager(monkeypatch, thin):
     replay the side chain is joined on the device (flags, no cross-queue graph edges) unless
     HMSC_SIDE_EDGES=1; both equal the eager sequence."""
     hM = synthetic_model(ny=200, ns=30, nc=4, nf=3, nt=2, seed=12)
-    out = []
-    for no_graph, per, edges in (("1", "4", "0"), ("0", "4", "0"), ("0", "3", "0"), ("0", "1", "0"), ("0", "32", "0"),
-                                 ("0", "32", "1")):
+    # HMSC_SIDE_PARTIALS=1: GammaV's / psi's species partials from post_bl_kernel, forked on the
+    # device inside a replay (its own summation order: compared among themselves)
+    cases = (("1", "4", "0", "0"), ("0", "4", "0", "0"), ("0", "3", "0", "0"), ("0", "1", "0", "0"),
+             ("0", "32", "0", "0"), ("0", "32", "1", "0"), ("1", "4", "0", "1"), ("0", "4", "0", "1"),
+             ("0", "32", "0", "1"), ("0", "32", "1", "1"))
+    out = {}
+    for no_graph, per, edges, sidep in cases:
         monkeypatch.setenv("HMSC_NO_GRAPH", no_graph)
         monkeypatch.setenv("HMSC_GRAPH_SWEEPS", per)
         monkeypatch.setenv("HMSC_SIDE_EDGES", edges)
+        monkeypatch.setenv("HMSC_SIDE_PARTIALS", sidep)
         ch = H.Chain(hM, 77, device=0, updater={"GammaEta": False})
         ch.init()
         rec = ch.run(transient=5, samples=41, thin=thin, adaptNf=[0])
         rec2 = ch.run(transient=2, samples=7, thin=thin, adaptNf=[0], iter0=5 + 41 * thin)
-        out.append((rec, rec2))
+        out.setdefault(sidep, []).append((rec, rec2))
         ch.close()
-    for o in out[1:]:
-        for i in range(2):
-            for k in ("Beta", "Gamma", "iV", "iSigma", "Lambda0", "Eta0", "Delta0", "Psi0"):
-                np.testing.assert_array_equal(out[0][i][k], o[i][k], err_msg=k)
+    for runs in out.values():
+        for o in runs[1:]:
+            for i in range(2):
+                for k in ("Beta", "Gamma", "iV", "iSigma", "Lambda0", "Eta0", "Delta0", "Psi0"):
+                    np.testing.assert_array_equal(runs[0][i][k], o[i][k], err_msg=k)
+    for i in range(2):  # the two partial paths differ by summation order only
+        for k in ("Beta", "Gamma", "iV", "Lambda0", "Eta0", "Psi0"):
+            np.testing.assert_allclose(out["1"][0][i][k], out["0"][0][i][k], rtol=1e-6, atol=1e-9, err_msg=k)
 
 
 def test_init_par_fixed_effects_chain_start():
