@@ -738,6 +738,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   if (std::getenv("ROCPROF_OUTPUT_PATH")) s.edge_free = false;
   if (const char* e = std::getenv("HMSC_SIDE_EDGES")) s.edge_free = e[0] != '1';
   if (const char* e = std::getenv("HMSC_SIDE_PARTIALS")) s.side_partials = e[0] == '1';
+  if (const char* e = std::getenv("HMSC_LONG_TAIL")) s.long_tail = e[0] == '1';
   s.scratch_doubles = 1 << 20;
   s.scratch = dalloc<double>(s.scratch_doubles);
   s.scratch2 = dalloc<double>(s.scratch_doubles);
@@ -1257,7 +1258,18 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
   hipGraph_t g = nullptr;
   HIP_OK(hipStreamBeginCapture(s.stream, hipStreamCaptureModeThreadLocal));
   s.capturing = true;
+  s.side_root = false;
   try {
+    const char* no_root = std::getenv("HMSC_NO_SIDE_ROOT");
+    if (s.side_fused && s.edge_free && !(no_root && no_root[0] == '1')) {
+      // the side stream forked at the graph's root: the first sweep's side work then waits for
+      // the fused launch's tails flag on the device like the later sweeps', instead of behind a
+      // graph edge from that launch (whose first replay sweep's side chain ended ~100 us late)
+      HIP_OK(hipEventRecord(s.ev_bl, s.stream));
+      HIP_OK(hipStreamWaitEvent(s.side, s.ev_bl, 0));
+      s.side_pending |= 1;
+      s.side_root = true;
+    }
     for (int i = 0; i < nsweeps; ++i) {
       s.d_iter = s.d_iters + i;
       s.cap_sweep = i;
@@ -1268,9 +1280,11 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
     }
     s.d_iter = s.d_iters;
     s.cap_sweep = -1;
+    s.side_root = false;
     join_side(s);
   } catch (...) {
     s.cap_sweep = -1;
+    s.side_root = false;
     s.d_iter = s.d_iters;
     s.pack_req = s.pack_done = false;
     s.capturing = false;
@@ -1626,7 +1640,7 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
       while (ng > 1 && it + ng - 1 > total) ng >>= 1;
       // a recorded run ends on single-sweep replays (..., 2, 1, 1): the samples of the last
       // replay are copied out only after it, so a small last replay shortens the copy tail
-      if (recording && ng > 1 && it + ng - 1 == total) ng >>= 1;
+      if (recording && ng > 1 && it + ng - 1 == total && !s.long_tail) ng >>= 1;
       for (int j = it; j < it + ng; ++j)
         if (recorded(j)) {
           if (kfirst < 0) kfirst = sample_of(j);

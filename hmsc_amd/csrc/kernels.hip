@@ -2062,7 +2062,9 @@ __global__ __launch_bounds__(64) void delta_kernel(LPArgs a, const double* rs_pa
 // fused Gamma2 + BetaLambda launch it reads; it waits for that launch's tails to be in.
 template <int NM>
 __global__ __launch_bounds__(256) void side_chain_kernel(GVWArgs g, LPArgs lp, const double* rs_part, int nparts,
-                                                         int rs_ld, const int* tails_flag, int* err) {
+                                                         int rs_ld, const int* tails_flag, int* err,
+                                                         unsigned long long* kt) {
+  const unsigned long long kt0 = kt ? kt_now() : 0ull;
   // A latency-bound chain of small factorisations running beside the main stream's Eta and z
   // waves on the same SIMDs: raised issue priority, so its few waves are not starved by the
   // VALU-bound z waves (the arbiter picks the highest-priority ready wave).
@@ -2074,6 +2076,7 @@ __global__ __launch_bounds__(256) void side_chain_kernel(GVWArgs g, LPArgs lp, c
     gammav_body<NM>(g);
   else
     delta_body(lp, rs_part, nparts, blockIdx.x - 1, rs_ld, g.flags);
+  if (kt && threadIdx.x == 0) kt_record(kt, SWEEP_ITER(g), kt0);
 }
 
 constexpr int LP_PARTS = 64;
@@ -2758,7 +2761,8 @@ bool side_fusion_ok(const State& s) {
 template <int NM>
 static void launch_side_chain(State& s, const GVWArgs& gw, const LPArgs& lp, const double* rs, int nparts, int rs_ld,
                               const int* tails_flag) {
-  side_chain_kernel<NM><<<1 + s.nr, 256, 0, s.side>>>(gw, lp, rs, nparts, rs_ld, tails_flag, s.gbl_sync);
+  side_chain_kernel<NM><<<1 + s.nr, 256, 0, s.side>>>(gw, lp, rs, nparts, rs_ld, tails_flag, s.gbl_sync,
+                                                      s.kt_on ? s.d_kt + (size_t)KT_SIDE * 2 * KT_SLOTS : nullptr);
 }
 
 // GammaV + LambdaPriors + Eta of one sweep (BetaLambda done), main stream + the side stream
@@ -2774,7 +2778,7 @@ void launch_side_fused(State& s, uint32_t iter) {
   // graph sweeps after the first: the side work is not forked by a graph edge; its first
   // launch waits on the device for the fused launch's tails flag (raised by the last reducer
   // of the tail, after every BetaLambda workgroup's stores), see State::cap_sweep
-  const bool dev_fork = cr_done && s.edge_free && s.capturing && s.cap_sweep > 0;
+  const bool dev_fork = cr_done && s.edge_free && s.capturing && (s.cap_sweep > 0 || s.side_root);
   if (!dev_fork) HIP_OK(hipEventRecord(s.ev_bl, s.stream));
   launch_eta_fused(s, iter, cr_done);
   if (!dev_fork) HIP_OK(hipStreamWaitEvent(s.side, s.ev_bl, 0));

@@ -107,6 +107,7 @@ struct State {
   // sooner, but the side work beside Eta and z costs them about as much (same 1000-step rate)
   // and a replay's first sweeps wait longer for it (20-step line ~2 % lower)
   bool side_partials = false;
+  bool long_tail = false;   // HMSC_LONG_TAIL=1: a recorded run's last replay not split into single sweeps
   // graph sweeps after the first of a capture (cap_sweep > 0): the side work is not forked
   // from the main stream nor joined into it by graph edges (each a ~5-6 us cross-queue gap on
   // the critical path) but synchronised by device flags: its first launch waits for the fused
@@ -114,6 +115,9 @@ struct State {
   int cap_sweep = -1;
   bool edge_free = true;    // (HMSC_SIDE_EDGES=1: graph edges everywhere)
   bool side_tail = false;   // the last side chain raises side_sync (the next fused launch may join it on the device)
+  // the capture in progress forked the side stream at the graph's root, so its first sweep's
+  // side work waits for the tails flag on the device too (no edge from the fused launch)
+  bool side_root = false;
   bool psi_side = true;     // the last sweep's psi draws ran on the side stream (post_bl_kernel), not in the tail
   int* side_sync = nullptr;      // [GammaV, delta chain per level ..., Gamma2 prep]: epoch of the sweep
   double* gvt = nullptr;         // the BetaLambda tail's GammaV / psi partial tiles

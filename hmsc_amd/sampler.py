@@ -310,7 +310,7 @@ class Chain:
         L.check(self.lib.hmsc_profile_get(self.h, self.PROF_IDS[name], L.fptr(t), L.iptr(n)))
         return float(t[0]), int(n[0])
 
-    KT_IDS = dict(z=0, eta=1, betalambda=2, bl_tail=3)
+    KT_IDS = dict(z=0, eta=1, betalambda=2, bl_tail=3, gamma2=4, side_chain=5)
 
     def kernel_timing(self, enable=True):
         """Clear and enable (or disable) the in-kernel launch timer (hmsc_kernel_timing)."""

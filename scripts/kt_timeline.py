@@ -11,7 +11,7 @@ sys.path.insert(0, ROOT)
 import hmsc_amd as H  # noqa: E402
 from hmsc_amd.workloads import synthetic_probit  # noqa: E402
 
-KT_SLOTS, KT_N = 8192, 5
+KT_SLOTS, KT_N = 8192, 6
 hM = synthetic_probit()
 ch = H.Chain(hM, 1234567, device=0, updater={"GammaEta": False})
 ch.init([10])

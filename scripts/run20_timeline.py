@@ -12,7 +12,7 @@ sys.path.insert(0, ROOT)
 import hmsc_amd as H  # noqa: E402
 from hmsc_amd.workloads import synthetic_probit  # noqa: E402
 
-KT_SLOTS, KT_N = 8192, 5
+KT_SLOTS, KT_N = 8192, 6
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 hM = synthetic_probit()
 ch = H.Chain(hM, 1234567, device=0, updater={"GammaEta": False})
@@ -37,7 +37,7 @@ for rep in range(3):
     kt = ch.debug_get("kt", KT_N * 2 * KT_SLOTS).reshape(KT_N, 2, KT_SLOTS).astype(np.float64)
     its = (np.arange(it + 1, it + n + 1)) % KT_SLOTS
     it += n
-    names = ("z", "eta", "bl", "tail", "g2")
+    names = ("z", "eta", "bl", "tail", "g2", "side")
     st = {k: kt[i, 0, its] for i, k in enumerate(names)}
     en = {k: kt[i, 1, its] for i, k in enumerate(names)}
     base = st["g2"][0]
@@ -46,4 +46,5 @@ for rep in range(3):
           f"{us(en['z'][-1]):.1f} us")
     for k in range(n):
         print(f"  sweep {k:2d}: g2 {us(st['g2'][k]):8.1f}  bl_end {us(en['bl'][k]):8.1f}  tail_end {us(en['tail'][k]):8.1f}"
-              f"  eta {us(st['eta'][k]):8.1f}-{us(en['eta'][k]):8.1f}  z {us(st['z'][k]):8.1f}-{us(en['z'][k]):8.1f}")
+              f"  eta {us(st['eta'][k]):8.1f}-{us(en['eta'][k]):8.1f}  z {us(st['z'][k]):8.1f}-{us(en['z'][k]):8.1f}"
+              f"  side {us(st['side'][k]):8.1f}-{us(en['side'][k]):8.1f}")
