@@ -739,6 +739,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   if (const char* e = std::getenv("HMSC_SIDE_EDGES")) s.edge_free = e[0] != '1';
   if (const char* e = std::getenv("HMSC_SIDE_PARTIALS")) s.side_partials = e[0] == '1';
   if (const char* e = std::getenv("HMSC_LONG_TAIL")) s.long_tail = e[0] == '1';
+  if (const char* e = std::getenv("HMSC_FIRST_REPLAY")) s.first_replay = std::max(0, atoi(e));
   s.scratch_doubles = 1 << 20;
   s.scratch = dalloc<double>(s.scratch_doubles);
   s.scratch2 = dalloc<double>(s.scratch_doubles);
@@ -1630,6 +1631,7 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
   if (s.gbl_sync) HIP_OK(hipMemsetAsync(s.gbl_sync + 1, 0, 2 * sizeof(int), s.stream));
   if (s.side_sync) HIP_OK(hipMemsetAsync(s.side_sync, 0, (2 + HMSC_MAX_LEVELS) * sizeof(int), s.stream));
   const auto t_start = std::chrono::steady_clock::now();
+  int n_replays = 0;
   for (int it = 1; it <= total;) {
     const int G = s.graph_sweeps;
     int n = 1;
@@ -1641,6 +1643,12 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
       // a recorded run ends on single-sweep replays (..., 2, 1, 1): the samples of the last
       // replay are copied out only after it, so a small last replay shortens the copy tail
       if (recording && ng > 1 && it + ng - 1 == total && !s.long_tail) ng >>= 1;
+      // (optional) a short first replay: the graph launch submits the side stream's nodes only
+      // after the main stream's, ~16 us of host time per sweep, so the side chain of a big
+      // first replay's first sweep starts late (~0.35 ms at 32 sweeps) and the second sweep
+      // waits for it; later replays are submitted while the previous one runs
+      if (n_replays == 0 && s.first_replay > 0)
+        while (ng > s.first_replay) ng >>= 1;
       for (int j = it; j < it + ng; ++j)
         if (recorded(j)) {
           if (kfirst < 0) kfirst = sample_of(j);
@@ -1649,6 +1657,7 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
       if (klast >= 0) wait_slot(klast);
       if (replay_sweeps(s, (uint32_t)(iter0 + it), klast >= 0, ng)) {
         replayed = true;
+        ++n_replays;
         n = ng;
         if (klast >= 0) {
           HIP_OK(hipEventRecord(s.ev_graph, s.stream));

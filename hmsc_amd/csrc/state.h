@@ -108,6 +108,11 @@ struct State {
   // and a replay's first sweeps wait longer for it (20-step line ~2 % lower)
   bool side_partials = false;
   bool long_tail = false;   // HMSC_LONG_TAIL=1: a recorded run's last replay not split into single sweeps
+  // HMSC_FIRST_REPLAY=k: a run's first replay at most k sweeps (0, the default: no limit).  It
+  // takes the side-node dispatch delay of a big first replay away (device span of a 20-sweep
+  // run -25 us), but the 16-sample copy of the following replay then trails the run (its
+  // 20-step line 5,260 -> 5,110 sweeps/s same box)
+  int first_replay = 0;
   // graph sweeps after the first of a capture (cap_sweep > 0): the side work is not forked
   // from the main stream nor joined into it by graph edges (each a ~5-6 us cross-queue gap on
   // the critical path) but synchronised by device flags: its first launch waits for the fused
