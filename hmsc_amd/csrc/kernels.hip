@@ -1611,6 +1611,8 @@ __device__ __forceinline__ void bl_tail(const BLTailArgs& ta, const BLCol& col, 
   if (w == 0) {
     if (nf <= 8)
       crw_finish<8>(a, sCR, smem);
+    else if (nf <= 10)
+      crw_finish<10>(a, sCR, smem);
     else if (nf <= 12)
       crw_finish<12>(a, sCR, smem);
     else
