@@ -28,9 +28,11 @@ def _finite_int(v, cap):
     return int(min(cap, v)) if not (isinstance(v, float) and math.isinf(v)) else int(cap)
 
 
-# include/hmsc_amd.h spatialMethod codes; Full and NNGP reach the device as the dense prior
-# precision of their alphapw grid (Full built on the device from the coordinates), GPP as
-# R's low-rank predictive-process arrays (hmsc_amd/dataparams.py)
+# include/hmsc_amd.h spatialMethod codes.  'Full' levels reach the device as their
+# coordinates (or distances), from which the library builds the alphapw grid of dense prior
+# precisions; 'NNGP' as coordinates + nNeighbours, kept in the sparse Vecchia form (per grid
+# point the k neighbour weights and conditional variances, spatial.hip setup_nngp_level);
+# 'GPP' as R's low-rank predictive-process arrays (hmsc_amd/dataparams.py)
 SPATIAL_CODE = {"Full": 1, "NNGP": 2, "GPP": 3}
 
 
