@@ -286,22 +286,39 @@ static void d2h(T* h, const T* d, size_t n, hipStream_t st) {
   if (n) HIP_OK(hipMemcpyAsync(h, d, n * sizeof(T), hipMemcpyDeviceToHost, st));
 }
 
-void allreduce_sum(State& s, double* buf, size_t n, hipStream_t st = nullptr);
-void allreduce_sum(State& s, double* buf, size_t n, hipStream_t st) {
-  if (s.nranks <= 1) return;
-  hipStream_t q = st ? st : s.stream;
-  if (s.host_allreduce) {  // host transport: device -> host, caller's sum over ranks, back
-    s.host_ar_buf.resize(n);
-    HIP_OK(hipMemcpyAsync(s.host_ar_buf.data(), buf, n * sizeof(double), hipMemcpyDeviceToHost, q));
-    HIP_OK(hipStreamSynchronize(q));
-    HMSC_REQUIRE(s.host_allreduce(s.host_ar_buf.data(), (int64_t)n, s.host_allreduce_ctx) == 0,
-                 "host all-reduce callback failed");
-    HIP_OK(hipMemcpyAsync(buf, s.host_ar_buf.data(), n * sizeof(double), hipMemcpyHostToDevice, q));
-    HIP_OK(hipStreamSynchronize(q));
+// The all-reduce of a sharded chain (state.h "species-sharded chain"): buf[0 .. n) summed over
+// the ranks in place, on the chain's stream.  RCCL: one ncclAllReduce (captured into the sweep
+// graphs like any kernel).  Host transport: the sum goes through pinned host memory and the
+// caller's callback; inside a graph capture the capture is split here into segments, which
+// hmsc_run replays with the callback between them.  Every call is counted (hmsc_debug_get
+// "ar_calls"): a steady sweep issues two (kernels.hip sweep_sharded).
+void ar_point(State& s, double* buf, size_t n) {
+  if (n == 0) return;
+  HMSC_REQUIRE(s.sharded, "internal: all-reduce on an unsharded chain");
+  ++s.ar_calls;
+  s.ar_doubles += n;
+  if (s.capturing) ++s.ar_in_capture;
+  if (s.comm) {
+    const ncclResult_t r = ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, (ncclComm_t)s.comm, s.stream);
+    HMSC_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
     return;
   }
-  const ncclResult_t r = ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, (ncclComm_t)s.comm, q);
-  HMSC_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  HMSC_REQUIRE(n <= s.ar_host_doubles, "internal: all-reduce larger than its host staging buffer");
+  // a segment boundary may not leave the side stream forked; outside a capture the join keeps
+  // the two transports' stream order alike
+  join_side(s);
+  HIP_OK(hipMemcpyAsync(s.ar_host, buf, n * sizeof(double), hipMemcpyDeviceToHost, s.stream));
+  if (s.capturing && s.cap_segs) {
+    hipGraph_t g = nullptr;
+    HIP_OK(hipStreamEndCapture(s.stream, &g));
+    s.cap_segs->emplace_back(g, n);
+    HIP_OK(hipStreamBeginCapture(s.stream, hipStreamCaptureModeThreadLocal));
+  } else {
+    HMSC_REQUIRE(!s.capturing, "internal: host-transport all-reduce inside a capture without segments");
+    HIP_OK(hipStreamSynchronize(s.stream));
+    HMSC_REQUIRE(s.host_allreduce(s.ar_host, (int64_t)n, s.host_allreduce_ctx) == 0, "host all-reduce callback failed");
+  }
+  HIP_OK(hipMemcpyAsync(buf, s.ar_host, n * sizeof(double), hipMemcpyHostToDevice, s.stream));
 }
 
 // ---------------------------- phylogeny ----------------------------
@@ -313,7 +330,7 @@ static void setup_phylo(State& s, const hmsc_model* m) {
   HMSC_REQUIRE(m->C_vectors != nullptr && m->C_values != nullptr,
                "phylogeny: pass the eigendecomposition of C (C_vectors, C_values)");
   HMSC_REQUIRE(m->nrho > 0 && m->rhopw != nullptr, "phylogeny: rhopw grid missing");
-  HMSC_REQUIRE(s.nranks == 1, "phylogeny couples all species: species-sharded chains are not supported");
+  HMSC_REQUIRE(!s.sharded, "phylogeny couples all species: species-sharded chains are not supported");
   // NA in Y: R's phylogeny branch factors kronecker(XEtaTXEta, diag(iSigma)) + P over the
   // imputed Z with no per-species masking (R/updateBetaLambda.R:124-146), so the device's
   // phylogeny system takes the full Gram and an unmasked XZ (zdraw.hip mask_na = 0)
@@ -402,7 +419,10 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   HIP_OK(hipEventCreateWithFlags(&s.ev_side2, hipEventDisableTiming));
   s.host_allreduce = host_fn;
   s.host_allreduce_ctx = host_ctx;
-  if (nranks > 1 && host_fn == nullptr) {
+  // sharded: more than one rank, or one rank given a communicator / host transport (the sharded
+  // kernels and collectives on a single GPU: tests/test_gpu_sharded.py)
+  s.sharded = nranks > 1 || comm_id != nullptr || host_fn != nullptr;
+  if (s.sharded && host_fn == nullptr) {
     HMSC_REQUIRE(comm_id != nullptr, "sharded chain needs an RCCL unique id");
     ncclUniqueId id;
     std::memcpy(&id, comm_id, sizeof(id));
@@ -441,6 +461,8 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
     }
     HMSC_REQUIRE(m->xDim == nullptr || m->xDim[r] == 0,
                  "covariate-dependent random levels are a 'next' row: not in this build");
+    HMSC_REQUIRE(!(s.sharded && L.spatial), "spatial levels couple the units of every species' factors densely: "
+                                            "species-sharded chains are not supported (run one chain per GPU)");
     L.np = m->np[r];
     L.nfmin = m->nfMin[r];
     L.nfmax = m->nfMax[r];
@@ -558,7 +580,12 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   std::vector<int> fam(nsl), var(nsl);
   std::vector<double> as(nsl), bs(nsl);
   std::vector<int> na_cols, na_index(nsl, -1);
+  // rows with any NA in the WHOLE Y (every rank of a sharded chain must agree on them: updateEta's
+  // NA rows, R/updateEta.R:59-70); NA in this rank's own species: has_na
   std::vector<int8_t> row_na(ny, 0);
+  for (int jg = 0; jg < m->ns; ++jg)
+    for (int i = 0; i < ny; ++i)
+      if (std::isnan(m->Y[i + (size_t)ny * jg])) row_na[i] = 1, s.any_na_global = true;
   for (int j = 0; j < nsl; ++j) {
     const int jg = sp0 + j;
     fam[j] = m->distr[jg];
@@ -580,7 +607,6 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
       if (std::isnan(y)) {
         ycode[c] = -1;
         col_na = true;
-        row_na[i] = 1;
       } else {
         ycode[c] = (fam[j] == 2 && y != 0.0) ? 1 : 0;
       }
@@ -626,6 +652,9 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   if (s.has_na) {
     s.na_cols = dupload(na_cols.data(), na_cols.size());
     s.na_index = dupload(na_index.data(), nsl);
+    s.Gna = dalloc<double>((size_t)s.n_na_cols * s.Kmax * s.Kmax);
+  }
+  if (s.any_na_global) {
     std::vector<int> na_rows, slot(ny, -1);
     for (int i = 0; i < ny; ++i)
       if (row_na[i]) {
@@ -636,7 +665,6 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
     s.na_rows = dupload(na_rows.data(), na_rows.size());
     s.row_na = dupload(row_na.data(), ny);
     s.row_slot = dupload(slot.data(), ny);
-    s.Gna = dalloc<double>((size_t)s.n_na_cols * s.Kmax * s.Kmax);
     s.Msmall = dalloc<double>((size_t)s.n_na_rows * (s.NFmax * s.NFmax + s.NFmax));
   }
   // priors and constants (host precompute)
@@ -746,6 +774,16 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.psi_rs = dalloc<double>((size_t)64 * nfm);
   s.ABpart = dalloc<double>((size_t)((nsl + 31) / 32) * (nc * nc + 2 * N + nfm * nt + 8));
   s.allreduce_buf = dalloc<double>((size_t)nc * nc + 2 * N + nfm * nt + nfm + 64);
+  if (s.sharded) {  // the two all-reduce buffers (state.h) and the host transport's staging
+    const size_t na = (size_t)N + (size_t)nfm * nt + 8, nb = arb_capacity(s);
+    s.ar_a = dalloc<double>(na);
+    s.ar_b = dalloc<double>(nb);
+    s.shard_ticket = dalloc<int>(4);
+    if (s.host_allreduce) {
+      s.ar_host_doubles = std::max(na, nb);
+      HIP_OK(hipHostMalloc(&s.ar_host, sizeof(double) * s.ar_host_doubles, hipHostMallocDefault));
+    }
+  }
   // the device error / handshake words in one block (dalloc zero-fills), so the host reads
   // every error word with one copy: [dev_flags 16 | gbl_sync 4 | trsv_sync DENSE_SYNC_INTS]
   s.dev_flags = dalloc<int>(16 + 4 + DENSE_SYNC_INTS);
@@ -754,7 +792,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.d_iters = dalloc<uint32_t>(64);  // graph_sweeps <= 64
   s.d_iter = s.d_iters;
   if (s.mask & HMSC_UP_GAMMAETA) {  // updateGammaEta: dense (nc ns)^2 / joint spatial systems
-    HMSC_REQUIRE(s.nranks == 1, "updateGammaEta cannot run on a species-sharded chain: pass updater GammaEta=FALSE");
+    HMSC_REQUIRE(!s.sharded, "updateGammaEta cannot run on a species-sharded chain: pass updater GammaEta=FALSE");
     HMSC_REQUIRE((size_t)nc * s.ns <= 32768, "updateGammaEta: nc * ns must be <= 32768 (dense (nc ns)^2 systems, 4 x 8.6 GB)");
     // sized for the levels' nf now (nfMin); launch_gamma_eta grows it if updateNf adds factors
     for (int r = 0; r < s.nr; ++r)
@@ -768,6 +806,9 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
     // a power of two (remainders replay graphs of the smaller powers); one replay launch per
     // 32 sweeps at a steady state (8 was +1.8 % over 4)
     s.graph_sweeps = 1 << graph_level(g ? std::max(1, std::min(64, atoi(g))) : 32);
+    // a host-transport sharded chain replays one sweep at a time (its all-reduces run on the
+    // host between the segments of the sweep graph)
+    if (s.sharded && s.comm == nullptr) s.graph_sweeps = 1;
   }
   // recording ring: device slots for two replays, their pinned host mirror and the copied
   // counter, allocated once here so no run pays for pinning
@@ -820,6 +861,12 @@ static void free_state(State& s) {
   if (s.gv_part) (void)hipFree(s.gv_part);
   if (s.host_rec) (void)hipHostFree(s.host_rec);
   if (s.copied_host) (void)hipHostFree(s.copied_host);
+  if (s.ar_host) (void)hipHostFree(s.ar_host);
+  for (void* p : {(void*)s.ar_a, (void*)s.ar_b, (void*)s.shard_ticket})
+    if (p) (void)hipFree(p);
+  for (auto& v : s.gseg)
+    for (auto& g : v)
+      if (g.g) (void)hipGraphExecDestroy(g.g);
   for (auto& row : s.gx)
     for (hipGraphExec_t g : row)
       if (g) (void)hipGraphExecDestroy(g);
@@ -1002,6 +1049,7 @@ static void set_state(State& s, const hmsc_params* p) {
   s.zt_valid = false;
   s.xeta_valid = false;
   s.g2prep_valid = false;
+  s.g2s_valid = false;
   s.graph_dirty = true;
 }
 
@@ -1022,9 +1070,9 @@ static void update_nf(State& s, int r, uint32_t iter) {
   std::vector<double> small(nf, 0.0);
   for (int j = 0; j < nsl; ++j)
     for (int h = 0; h < nf; ++h) small[h] += std::fabs(BL[lo + h + (size_t)K * j]) < 1e-3 ? 1.0 : 0.0;
-  if (s.nranks > 1) {
+  if (s.sharded) {  // the counts over every rank's species (an adaptation sweep's extra all-reduce)
     h2d(s.allreduce_buf, small.data(), nf, s.stream);
-    allreduce_sum(s, s.allreduce_buf, nf);
+    ar_point(s, s.allreduce_buf, nf);
     d2h(small.data(), s.allreduce_buf, nf, s.stream);
     HIP_OK(hipStreamSynchronize(s.stream));
   }
@@ -1119,11 +1167,16 @@ static void update_nf(State& s, int r, uint32_t iter) {
   s.refresh_dims();
   s.zt_valid = false;
   s.xeta_valid = false;
+  s.g2s_valid = false;
   s.graph_dirty = true;
 }
 
 // ---------------------------- sweep ----------------------------
 static void run_updater(State& s, uint32_t which, uint32_t iter) {
+  if (s.sharded) {
+    run_updater_sharded(s, which, iter);
+    return;
+  }
   switch (which) {
     case HMSC_UP_GAMMA2:
       launch_gamma2(s, iter);
@@ -1165,6 +1218,14 @@ static void run_updater(State& s, uint32_t which, uint32_t iter) {
 // updateLambdaPriors of sweep t only feed sweep t+1 (Gamma2 / BetaLambda and the record),
 // so they run on the side stream after BetaLambda, overlapped with Eta / InvSigma / Z.
 static void sweep(State& s, uint32_t iter, bool adapt) {
+  if (s.sharded) {
+    sweep_sharded(s, iter);  // kernels.hip: two all-reduces per sweep
+    if (adapt) {
+      join_side(s);
+      for (int r = 0; r < s.nr; ++r) update_nf(s, r, iter);
+    }
+    return;
+  }
   ProfScope ps(s, PROF_SWEEP);
   // co-launched side updaters (launch_side_fused): the GammaV algebra of the previous sweep
   // may still run on the side stream; Gamma2 joins it before its final stage
@@ -1243,26 +1304,42 @@ static void destroy_graph(State& s) {
       if (g) (void)hipGraphExecDestroy(g);
       g = nullptr;
     }
+  for (auto& v : s.gseg) {
+    for (auto& g : v)
+      if (g.g) (void)hipGraphExecDestroy(g.g);
+    v.clear();
+  }
 }
 
-
+// a sharded chain on a host transport: its sweep graphs are segments split at the all-reduces
+static bool host_segments(const State& s) { return s.sharded && s.comm == nullptr; }
 
 // Captures graph_sweeps sweeps (with or without the record pack after each).  Returns
 // nullptr when the sweep is not in a steady state, i.e. the host-side validity flags it
-// changes would differ on the next sweep.
+// changes would differ on the next sweep.  segs (a host-transport sharded chain): the sweep is
+// captured as segments split at its all-reduces (ar_point), instantiated into *segs; the
+// return value is then null.
 static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, size_t* n_nodes = nullptr,
-                                     int nsweeps = 0) {
+                                     int nsweeps = 0, std::vector<State::Seg>* segs = nullptr) {
   if (nsweeps <= 0) nsweeps = s.graph_sweeps;
   std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
   join_side(s);
-  const bool xv = s.xeta_valid, zv = s.zt_valid, gv = s.g2prep_valid, gp = s.g_pending;
+  const bool xv = s.xeta_valid, zv = s.zt_valid, gv = s.g2prep_valid, gp = s.g_pending, g2v = s.g2s_valid;
   hipGraph_t g = nullptr;
+  std::vector<std::pair<hipGraph_t, size_t>> parts;  // (host transport) the segments so far
+  auto drop_parts = [&] {
+    for (auto& pr : parts)
+      if (pr.first) (void)hipGraphDestroy(pr.first);
+    parts.clear();
+  };
   HIP_OK(hipStreamBeginCapture(s.stream, hipStreamCaptureModeThreadLocal));
   s.capturing = true;
   s.side_root = false;
+  s.ar_in_capture = 0;
+  s.cap_segs = segs ? &parts : nullptr;
   try {
     const char* no_root = std::getenv("HMSC_NO_SIDE_ROOT");
-    if (s.side_fused && s.edge_free && !(no_root && no_root[0] == '1')) {
+    if (s.side_fused && s.edge_free && !s.sharded && !(no_root && no_root[0] == '1')) {
       // the side stream forked at the graph's root: the first sweep's side work then waits for
       // the fused launch's tails flag on the device like the later sweeps', instead of behind a
       // graph edge from that launch (whose first replay sweep's side chain ended ~100 us late)
@@ -1289,23 +1366,56 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
     s.d_iter = s.d_iters;
     s.pack_req = s.pack_done = false;
     s.capturing = false;
+    s.cap_segs = nullptr;
     (void)hipStreamEndCapture(s.stream, &g);
     if (g) (void)hipGraphDestroy(g);
-    s.xeta_valid = xv, s.zt_valid = zv, s.g2prep_valid = gv, s.g_pending = gp;
+    drop_parts();
+    s.xeta_valid = xv, s.zt_valid = zv, s.g2prep_valid = gv, s.g_pending = gp, s.g2s_valid = g2v;
     throw;
   }
   s.capturing = false;
+  s.cap_segs = nullptr;
   HIP_OK(hipStreamEndCapture(s.stream, &g));
-  const bool steady = xv == s.xeta_valid && zv == s.zt_valid && gv == s.g2prep_valid && gp == s.g_pending;
-  s.xeta_valid = xv, s.zt_valid = zv, s.g2prep_valid = gv, s.g_pending = gp;  // nothing ran yet
+  const bool steady = xv == s.xeta_valid && zv == s.zt_valid && gv == s.g2prep_valid && gp == s.g_pending &&
+                      g2v == s.g2s_valid;
+  s.xeta_valid = xv, s.zt_valid = zv, s.g2prep_valid = gv, s.g_pending = gp, s.g2s_valid = g2v;  // nothing ran yet
+  if (s.sharded && !with_record) s.ar_per_graph_sweep = s.ar_in_capture / std::max(1, nsweeps);
   size_t nodes = 0;
   HIP_OK(hipGraphGetNodes(g, nullptr, &nodes));
+  for (auto& pr : parts) {
+    size_t k = 0;
+    HIP_OK(hipGraphGetNodes(pr.first, nullptr, &k));
+    nodes += k;
+  }
   if (n_nodes) *n_nodes = nodes;
   if (const char* e = std::getenv("HMSC_GRAPH_DEBUG"))
     if (e[0] == '1')
-      std::fprintf(stderr, "[hmsc] captured %d sweeps%s: %zu nodes%s\n", nsweeps, with_record ? " + record" : "",
-                   nodes, steady ? "" : " (not steady)");
+      std::fprintf(stderr, "[hmsc] captured %d sweeps%s: %zu nodes in %zu segment(s)%s\n", nsweeps,
+                   with_record ? " + record" : "", nodes, parts.size() + 1, steady ? "" : " (not steady)");
   hipGraphExec_t ge = nullptr;
+  if (segs) {
+    parts.emplace_back(g, 0);  // the last segment: no all-reduce after it
+    g = nullptr;
+    segs->clear();
+    if (steady && nodes <= graph_max_nodes()) {
+      try {
+        for (size_t k = 0; k < parts.size(); ++k) {
+          State::Seg sg;
+          HIP_OK(hipGraphInstantiate(&sg.g, parts[k].first, nullptr, nullptr, 0));
+          sg.ar_n = parts[k].second;
+          segs->push_back(sg);
+        }
+      } catch (...) {
+        for (auto& sg : *segs)
+          if (sg.g) (void)hipGraphExecDestroy(sg.g);
+        segs->clear();
+        drop_parts();
+        throw;
+      }
+    }
+    drop_parts();
+    return nullptr;
+  }
   if (steady && nodes <= graph_max_nodes()) HIP_OK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
   HIP_OK(hipGraphDestroy(g));
   return ge;
@@ -1317,6 +1427,20 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
 static bool build_sweep_graphs(State& s, uint32_t iter) {
   destroy_graph(s);
   size_t nodes = 0;
+  if (host_segments(s)) {  // one sweep per replay, as segments (the host sums between them)
+    s.graph_sweeps = 1;
+    capture_sweeps(s, iter, false, &nodes, 1, &s.gseg[0]);
+    if (!s.gseg[0].empty()) capture_sweeps(s, iter, true, nullptr, 1, &s.gseg[1]);
+    if (s.gseg[0].empty() || s.gseg[1].empty()) {
+      if (nodes > graph_max_nodes()) s.use_graph = false;
+      destroy_graph(s);
+      return false;
+    }
+    s.graph_K = s.K;
+    s.graph_NF = s.NF;
+    s.graph_dirty = false;
+    return true;
+  }
   const int top = graph_level(s.graph_sweeps);
   s.gx[0][top] = capture_sweeps(s, iter, false, &nodes);
   if (!s.gx[0][top] && nodes > graph_max_nodes() && s.graph_sweeps > 1) {
@@ -1350,22 +1474,42 @@ static bool build_sweep_graphs(State& s, uint32_t iter) {
   return true;
 }
 
-static bool graphs_built(const State& s) { return s.gx[0][graph_level(s.graph_sweeps)] != nullptr; }
+static bool graphs_built(const State& s) {
+  return host_segments(s) ? !s.gseg[0].empty() : s.gx[0][graph_level(s.graph_sweeps)] != nullptr;
+}
 
 // Runs sweeps iter .. iter+n-1 (n a power of two <= graph_sweeps) as one
 // graph replay if the graphs exist or can be built now; returns false (nothing launched) when
 // the caller must run eagerly.
 static bool replay_sweeps(State& s, uint32_t iter, bool with_record, int n) {
-  if (!s.use_graph || s.nranks != 1 || s.prof) return false;
+  if (!s.use_graph || s.prof) return false;
   if (graphs_built(s) && (s.graph_dirty || s.graph_K != s.K || s.graph_NF != s.NF)) destroy_graph(s);
   if (s.graph_dirty) s.eager_streak = 0, s.graph_dirty = false;
   if (!graphs_built(s) && (s.eager_streak < 1 || !build_sweep_graphs(s, iter))) return false;  // steady first
   if (n < 1 || n > s.graph_sweeps || (n & (n - 1))) return false;
+  if (host_segments(s)) {
+    const auto& segs = s.gseg[with_record ? 1 : 0];
+    if (segs.empty() || n != 1) return false;
+    join_side(s);
+    set_iters_kernel<<<1, 64, 0, s.stream>>>(s.d_iters, iter, n);
+    for (const auto& sg : segs) {
+      HIP_OK(hipGraphLaunch(sg.g, s.stream));
+      if (sg.ar_n) {  // the segment ended with the D2H copy of the all-reduce buffer; the next one starts with its H2D
+        HIP_OK(hipStreamSynchronize(s.stream));
+        ++s.ar_calls;
+        s.ar_doubles += sg.ar_n;
+        HMSC_REQUIRE(s.host_allreduce(s.ar_host, (int64_t)sg.ar_n, s.host_allreduce_ctx) == 0,
+                     "host all-reduce callback failed");
+      }
+    }
+    return true;
+  }
   hipGraphExec_t ge = s.gx[with_record ? 1 : 0][graph_level(n)];
   if (!ge) return false;
   join_side(s);
   set_iters_kernel<<<1, 64, 0, s.stream>>>(s.d_iters, iter, n);
   HIP_OK(hipGraphLaunch(ge, s.stream));
+  if (s.sharded && s.ar_per_graph_sweep > 0) s.ar_calls += (uint64_t)s.ar_per_graph_sweep * n;
   return true;
 }
 
@@ -1928,6 +2072,7 @@ int hmsc_init_state(hmsc_state* h, const int32_t* nf0) {
     HIP_OK(hipMemcpyAsync(s.rho, &one, sizeof(double), hipMemcpyHostToDevice, s.stream));
     s.graph_dirty = true;
     s.xeta_valid = false;
+    s.g2s_valid = false;
     launch_update_z(s, 0, true);  // Z = updateZ(Y=hM$Y, ...) (R/computeInitialParameters.R:254)
     HIP_OK(hipStreamSynchronize(s.stream));
   });
@@ -1939,6 +2084,7 @@ int hmsc_init_z(hmsc_state* h) {
     DeviceGuard dg(s.device);
     join_side(s);
     s.graph_dirty = true;
+    s.g2s_valid = false;
     launch_update_z(s, 0, true);  // R/computeInitialParameters.R:254 (iter 0: the init stream)
     HIP_OK(hipStreamSynchronize(s.stream));
   });
@@ -2010,7 +2156,7 @@ int hmsc_prepare_graphs(hmsc_state* h, int32_t iter, int32_t* built) {
     State& s = h->s;
     DeviceGuard dg(s.device);
     *built = 0;
-    if (!s.use_graph || s.nranks != 1 || s.prof) return;
+    if (!s.use_graph || s.prof) return;
     if (graphs_built(s) && (s.graph_dirty || s.graph_K != s.K || s.graph_NF != s.NF)) destroy_graph(s);
     if (!graphs_built(s)) {
       if (s.graph_dirty) s.eager_streak = 0, s.graph_dirty = false;
@@ -2020,6 +2166,8 @@ int hmsc_prepare_graphs(hmsc_state* h, int32_t iter, int32_t* built) {
     for (auto& row : s.gx)
       for (hipGraphExec_t g : row)
         if (g) HIP_OK(hipGraphUpload(g, s.stream));
+    for (auto& v : s.gseg)
+      for (auto& sg : v) HIP_OK(hipGraphUpload(sg.g, s.stream));
     HIP_OK(hipStreamSynchronize(s.stream));
     *built = 1;
   });
@@ -2097,10 +2245,17 @@ int hmsc_debug_get(hmsc_state* h, const char* name, double* out, int64_t n) {
       copy_sync(pv.data(), L.nnPerm, sizeof(int) * L.np, hipMemcpyDeviceToHost, s.stream);
       for (int i = 0; i < L.np; ++i) out[i] = pv[i];
       return;
+    } else if (nm == "ar_calls") {  // sharded chain: [all-reduces so far, their doubles, per captured sweep, sharded]
+      HMSC_REQUIRE(n >= 4, "ar_calls needs 4 slots");
+      const double d[4] = {(double)s.ar_calls, (double)s.ar_doubles, (double)s.ar_per_graph_sweep, (double)s.sharded};
+      std::memcpy(out, d, sizeof(d));
+      return;
     } else if (nm == "graph") {
       HMSC_REQUIRE(n >= 4, "graph needs 4 slots");
       const int top = graph_level(s.graph_sweeps);
-      const double d[4] = {(double)(s.gx[0][top] != nullptr), (double)(s.gx[1][top] != nullptr), (double)s.graph_sweeps,
+      const bool segs = host_segments(s);
+      const double d[4] = {(double)(segs ? !s.gseg[0].empty() : s.gx[0][top] != nullptr),
+                           (double)(segs ? !s.gseg[1].empty() : s.gx[1][top] != nullptr), (double)s.graph_sweeps,
                            (double)s.eager_streak};
       std::memcpy(out, d, sizeof(d));
       return;

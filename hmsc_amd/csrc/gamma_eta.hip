@@ -1187,7 +1187,7 @@ size_t gamma_eta_work_doubles(const State& s) {
 }
 
 void launch_gamma_eta(State& s, uint32_t iter) {
-  HMSC_REQUIRE(s.nranks == 1, "updateGammaEta: species-sharded chains are not supported (dense (nc ns)^2 system)");
+  HMSC_REQUIRE(!s.sharded, "updateGammaEta: species-sharded chains are not supported (dense (nc ns)^2 system)");
   HMSC_REQUIRE(s.geWork != nullptr, "updateGammaEta: workspace not allocated");
   for (int r = 0; r < s.nr; ++r)
     HMSC_REQUIRE(!s.lev[r].spatial || (size_t)s.nc * s.nt + (size_t)s.lev[r].np * s.lev[r].nf <= 32768,

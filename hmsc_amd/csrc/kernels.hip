@@ -715,7 +715,6 @@ __global__ __launch_bounds__(256) void gammav_final_kernel(GVArgs a) {
   for (int r = t; r < N; r += blockDim.x) a.Gamma[r] = rhs[r];
 }
 
-void allreduce_sum(State& s, double* buf, size_t n, hipStream_t st = nullptr);  // capi.cpp
 
 // ---------------------------------------------------------------------------
 // Wave-resident GammaV + Gamma2-prep for N = nc*nt <= 32 (the common case): one workgroup,
@@ -1019,13 +1018,6 @@ void launch_gamma_v(State& s, uint32_t iter, hipStream_t st) {
     gammav_partial_kernel<<<nparts, 256, (size_t)(2 * s.nc * SB + SB * s.nt) * sizeof(double), st>>>(
         s.BL, s.K, s.nc, s.nt, s.nsl, s.Gamma, s.Tr, part);
     HIP_OK(hipGetLastError());
-  }
-  if (s.nranks > 1) {
-    const int64_t n = (int64_t)s.nc * s.nc + (int64_t)s.nc * s.nt;
-    slab_sum_kernel<<<grid_for(n), 256, 0, st>>>(part, s.allreduce_buf, n, nparts, n);
-    allreduce_sum(s, s.allreduce_buf, n, st);
-    part = s.allreduce_buf;
-    np = 1;
   }
   const int Ng = s.nc * s.nt;
   if (Ng <= 32) {
@@ -1383,23 +1375,45 @@ struct CRWArgs {
 
 // Q = I + (rows nc.. of CR) -> its Cholesky factor and W = L^-1 by rows, on one wave;
 // sCR is CR in LDS as [row][16], scratch >= 16 x 17 doubles.
+// qm[r * ld + c] = (Q - I)[r][c] (r, c < nf): W[m * wld + c] = row m of L^-1, L L^T = Q, for
+// m, c < wn (zero past nf and above the diagonal); one wave, scratch >= NFB (NFB + 1) doubles
 template <int NFB>
-__device__ __forceinline__ void crw_finish(const CRWArgs& a, const double* sCR, double* scratch) {
-  const int lane = lane_id(), nc = a.nc, nf = a.nf;
+__device__ __forceinline__ void q_inv_factor(const double* qm, int ld, int nf, double* W, int wld, int wn,
+                                             double* scratch) {
+  const int lane = lane_id();
   double qv[NFB], dinv;
   const int r = lane < nf ? lane : 0;
 #pragma unroll
   for (int c = 0; c < NFB; ++c) {
-    const double v = (r == c ? 1.0 : 0.0) + sCR[(nc + r) * 16 + (c < nf ? c : 0)];
+    const double v = (r == c ? 1.0 : 0.0) + qm[r * ld + (c < nf ? c : 0)];
     qv[c] = (lane < nf && c < nf) ? v : (lane == c ? 1.0 : 0.0);
   }
   wv_chol<NFB>(qv, dinv);
   double wr[NFB];
   wv_inv_lower_rows<NFB>(qv, dinv, wr, scratch);  // lane m: row m of L^-1
-  if (lane < 16)
+  if (lane < wn)
 #pragma unroll
-    for (int c = 0; c < 16; ++c)
-      a.W[lane * 16 + c] = (lane < nf && c < NFB && c < nf && c <= lane) ? wr[c < NFB ? c : 0] : 0.0;
+    for (int c = 0; c < 16; ++c)  // (compile-time trip: wr stays in registers)
+      if (c < wn) W[lane * wld + c] = (lane < nf && c < NFB && c < nf && c <= lane) ? wr[c < NFB ? c : 0] : 0.0;
+}
+
+// the same factorization bucketed by nf exactly as the BetaLambda tail does it (8 / 10 / 12 / 16),
+// so a sharded chain's Eta solve forms the unsharded chain's W bit for bit
+__device__ __forceinline__ void q_inv_factor_nf(const double* qm, int ld, int nf, double* W, int wld, int wn,
+                                                double* scratch) {
+  if (nf <= 8)
+    q_inv_factor<8>(qm, ld, nf, W, wld, wn, scratch);
+  else if (nf <= 10)
+    q_inv_factor<10>(qm, ld, nf, W, wld, wn, scratch);
+  else if (nf <= 12)
+    q_inv_factor<12>(qm, ld, nf, W, wld, wn, scratch);
+  else
+    q_inv_factor<16>(qm, ld, nf, W, wld, wn, scratch);
+}
+
+template <int NFB>
+__device__ __forceinline__ void crw_finish(const CRWArgs& a, const double* sCR, double* scratch) {
+  q_inv_factor<NFB>(sCR + a.nc * 16, 16, a.nf, a.W, 16, 16, scratch);
 }
 
 // The tail of a BetaLambda workgroup of the fused launch (K <= 32, nf <= 16), with the
@@ -1431,6 +1445,10 @@ struct BLTailArgs {
   Key key;
   unsigned long long* kt;     // live timing of the last reducer (KT_TAIL block) or null
   unsigned long long* kt_bl;  // live timing of the BetaLambda bodies (KT_BL block), via the tiles
+  // sharded chain: the last reducer also sums the GammaV / psi group tiles in group order into
+  // ar_gv (ar_b's [GV | RS] sections, the all-reduce's input) and leaves W to the Eta solve
+  // (Q = I + Lambda diag(iSigma) Lambda^T is a sum over every rank's species)
+  double* ar_gv;
 };
 
 __device__ __forceinline__ void bl_tail(const BLTailArgs& ta, const BLCol& col, int b, int nbl, uint32_t iter,
@@ -1606,9 +1624,21 @@ __device__ __forceinline__ void bl_tail(const BLTailArgs& ta, const BLCol& col, 
       if (h < nf && k < K) a.CR[k + (size_t)a.ldcr * h] = v[e];
     }
   }
+  if (ta.ar_gv && ta.gv_on)  // (sharded) the GammaV / psi sums of this rank's species, group order
+    for (int q = t; q < ngv; q += 256) {
+      double v = 0.0;
+      for (int q0 = 0; q0 < ng; q0 += CRW_GROUP) {
+        double x[CRW_GROUP];
+#pragma unroll
+        for (int u = 0; u < CRW_GROUP; ++u) x[u] = q0 + u < ng ? load_coherent(V + (size_t)(nbl + q0 + u) * ld + q) : 0.0;
+#pragma unroll
+        for (int u = 0; u < CRW_GROUP; ++u) v += x[u];
+      }
+      ta.ar_gv[q] = v;
+    }
   __syncthreads();
   if (t < 64) HMSC_STAMP_RT(88);
-  if (w == 0) {
+  if (w == 0 && !ta.ar_gv) {
     if (nf <= 8)
       crw_finish<8>(a, sCR, smem);
     else if (nf <= 10)
@@ -1651,6 +1681,10 @@ struct G2BLArgs {
   const double* Tr;
   double* part;
   int K, nc, NF, nt, nsl;
+  // BetaLambda workgroups that first form one of Gamma2's species-block partials (and the count
+  // workgroup 0 waits for): g2.nparts on one rank; 0 on a sharded chain, whose Gamma2 sums
+  // arrive all-reduced (g2.part = ar_a, g2.nparts = 1)
+  int part_wg;
   int* sync;            // [ticket, epoch of the published Gamma, -, handshake timed out]
   BLTailArgs tail;      // the BetaLambda workgroups' tail (crw_on): Eta constants [+ side partials]
   int crw_on;
@@ -1663,7 +1697,7 @@ struct G2BLArgs {
 template <int NM>
 __global__ __launch_bounds__(256) void gamma2_bl_kernel(G2BLArgs f) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int nparts = f.g2.nparts, nbl = (int)gridDim.x - 1;
+  const int nparts = f.part_wg, nbl = (int)gridDim.x - 1;
   if (blockIdx.x == 0) {
     const unsigned long long kt0 = f.kt_g2 ? kt_now() : 0ull;
     if (threadIdx.x < 64) HMSC_STAMP_RT(70);
@@ -1728,19 +1762,6 @@ static void launch_gamma2_prep(State& s, hipStream_t st) {
   s.g2prep_valid = true;
 }
 
-// number of local species with iSigma != 1 (updateGamma2 acts only if there is none in the
-// whole chain, R/updateGamma2.R:35-36): one slot of a sharded chain's all-reduce
-__global__ __launch_bounds__(256) void isigma_ne1_count_kernel(const double* iSigma, int n, double* out) {
-  __shared__ int c;
-  if (threadIdx.x == 0) c = 0;
-  __syncthreads();
-  int k = 0;
-  for (int j = threadIdx.x; j < n; j += blockDim.x) k += iSigma[j] != 1.0;
-  if (k) atomicAdd(&c, k);
-  __syncthreads();
-  if (threadIdx.x == 0) *out = (double)c;
-}
-
 void launch_gamma2(State& s, uint32_t iter) {
   HMSC_REQUIRE((size_t)s.nc * s.nt <= 256 && s.NF * s.nt + s.nc * s.nt <= 1024,
                "updateGamma2: nc*nt must be <= 256 in this build");
@@ -1761,15 +1782,6 @@ void launch_gamma2(State& s, uint32_t iter) {
   double* xtztr = s.allreduce_buf + (n1 + n2);
   if (s.has_na) xt_ztr_kernel<<<n1, 256, 0, s.stream>>>(s.X, s.ZTr, s.ny, s.nc, s.nt, xtztr);
   double* isig_count = nullptr;
-  if (s.nranks > 1) {
-    slab_sum_kernel<<<grid_for(n1 + n2), 256, 0, s.stream>>>(part, s.allreduce_buf, n1 + n2, nparts, n1 + n2);
-    isig_count = s.allreduce_buf + 2 * n1 + n2;  // after the X'ZTr slot (used with NA only)
-    if (!s.has_na) HIP_OK(hipMemsetAsync(xtztr, 0, sizeof(double) * n1, s.stream));
-    isigma_ne1_count_kernel<<<1, 256, 0, s.stream>>>(s.iSigma, s.nsl, isig_count);
-    allreduce_sum(s, s.allreduce_buf, 2 * n1 + n2 + 1);
-    part = s.allreduce_buf;
-    np = 1;
-  }
   G2Args a{};
   a.nc = s.nc;
   a.nt = s.nt;
@@ -1800,13 +1812,14 @@ void launch_gamma2(State& s, uint32_t iter) {
 bool gamma2_bl_fusion_ok(const State& s) {
   const uint32_t need = HMSC_UP_GAMMA2 | HMSC_UP_BETALAMBDA;
   const size_t N = (size_t)s.nc * s.nt;
-  return (s.mask & need) == need && !(s.mask & HMSC_UP_GAMMAETA) && s.nranks == 1 && !s.has_na && !s.phylo &&
+  return (s.mask & need) == need && !(s.mask & HMSC_UP_GAMMAETA) && !s.sharded && !s.has_na && !s.phylo &&
          s.K <= 32 && s.nt <= 8 && N <= 256 && s.NF <= 64 && s.NF * s.nt + N <= 64 && s.gbl_sync != nullptr &&
          (G2F_LDS + (size_t)s.nc * s.nc + N * N) <= (size_t)BLW_LDS && !getenv_flag("HMSC_NO_G2BL_FUSION");
 }
 
 // updateGamma2 then updateBetaLambda as one launch (gamma2_bl_kernel)
 static CRWArgs make_crw_args(const State& s);
+static void shard_g2_stats(State& s);
 bool side_fusion_ok(const State& s);
 
 void launch_gamma2_bl(State& s, uint32_t iter) {
@@ -1816,28 +1829,34 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
   // the co-launched sweep (launch_side_fused) runs the fused Eta kernel next: its constants
   // are formed in the BetaLambda workgroups' tail (K <= 32 on this path, nf <= 16), with
   // GammaV's and LambdaPriors' species partials when their tile fits the tail's LDS
-  const bool crw_on = s.nranks == 1 && side_fusion_ok(s) && s.lev[0].nf <= 16 && s.K <= 32;
-  const bool tail_gv = !s.side_partials && crw_on && (s.mask & HMSC_UP_GAMMA2) && s.nt <= 8 &&
-                       s.nc * s.nc + s.nc * s.nt + s.NF <= 1024 && s.gvt != nullptr;
+  // a sharded chain (sharded_fused_ok): Gamma2's sums arrive all-reduced in ar_a, and the tail
+  // leaves this rank's CR and GammaV / psi sums in ar_b for the all-reduce B
+  const bool sh = s.sharded;
+  const bool crw_on = sh || (side_fusion_ok(s) && s.lev[0].nf <= 16 && s.K <= 32);
+  const bool tail_gv = sh || (!s.side_partials && crw_on && (s.mask & HMSC_UP_GAMMA2) && s.nt <= 8 &&
+                              s.nc * s.nc + s.nc * s.nt + s.NF <= 1024 && s.gvt != nullptr);
   // graph sweeps after the first: the previous sweep's side chain is joined on the device
-  const bool dev_join = crw_on && s.edge_free && s.capturing && s.cap_sweep > 0 && s.side_tail;
+  const bool dev_join = !sh && crw_on && s.edge_free && s.capturing && s.cap_sweep > 0 && s.side_tail;
   // iV, Gamma2's prep, Psi and Delta come from the previous sweep's side updaters
   if (!dev_join) join_side(s);
+  if (sh && !s.g2s_valid) shard_g2_stats(s);
   if (!s.g2prep_valid) launch_gamma2_prep(s, s.stream);
   G2BLArgs f{};
   const int nparts = (s.nsl + SB - 1) / SB;
+  const int n12 = s.nc * s.nt + s.NF * s.nt;
   G2Args& a = f.g2;
   a.nc = s.nc;
   a.nt = s.nt;
   a.Kmax = s.Kmax;
   a.NF = s.NF;
-  a.nparts = nparts;
+  a.nparts = sh ? 1 : nparts;
   a.ns_loc = s.nsl;
   a.use_xtztr = 0;
-  // probit iSigma is 1 by construction (updateInvSigma leaves it) unless set from outside
-  a.check_isigma = (s.all_probit && s.isigma_fixed_one) ? 0 : 1;
-  a.isig_count = nullptr;
-  a.part = s.ABpart;
+  // probit iSigma is 1 by construction (updateInvSigma leaves it) unless set from outside; a
+  // sharded chain counts iSigma != 1 over every rank's species (ar_a)
+  a.check_isigma = (sh || (s.all_probit && s.isigma_fixed_one)) ? 0 : 1;
+  a.isig_count = sh ? s.ar_a + n12 : nullptr;
+  a.part = sh ? s.ar_a : s.ABpart;
   a.xtztr = nullptr;
   a.G = s.G;
   a.prep = s.g2prep;
@@ -1859,6 +1878,7 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
   f.NF = s.NF;
   f.nt = s.nt;
   f.nsl = s.nsl;
+  f.part_wg = sh ? 0 : nparts;
   f.sync = s.gbl_sync;
   f.crw_on = crw_on;
   if (crw_on) {
@@ -1882,18 +1902,25 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
     t.kt = s.kt_on ? s.d_kt + (size_t)KT_TAIL * 2 * KT_SLOTS : nullptr;
     t.kt_bl = f.bl.kt;
     f.bl.kt_defer = 1;
+    t.ar_gv = nullptr;
+    if (sh) {
+      const ArbLayout L = arb_layout(s);
+      t.crw.CR = s.ar_b + L.cr;
+      t.crw.ldcr = L.ldcr;
+      t.ar_gv = s.ar_b + L.gv;  // [GV | RS], the tile layout
+    }
   }
-  s.crw_fresh = crw_on;
-  s.tail_gv = tail_gv;
+  s.crw_fresh = crw_on && !sh;
+  s.tail_gv = tail_gv && !sh;
   s.side_tail = false;  // (both set again by this sweep's launch_side_fused)
-  s.psi_side = true;
+  s.psi_side = !sh;     // (a sharded chain's tail draws psi: its record pack reads Psi on the main stream)
   f.side_sync = s.side_sync;
   f.side_wait = dev_join;
   f.side_prep = (s.mask & HMSC_UP_GAMMA2) ? 1 : 0;
   f.kt_g2 = s.kt_on ? s.d_kt + (size_t)KT_G2 * 2 * KT_SLOTS : nullptr;
   if (!s.capturing) HIP_OK(hipMemsetAsync(s.gbl_sync + 1, 0, 2 * sizeof(int), s.stream));  // an eager sweep may repeat an iter
   const int nb = 1 + (s.nsl + 3) / 4;
-  HMSC_REQUIRE(nparts <= nb - 1, "fused Gamma2 + BetaLambda: more Gamma2 partials than BetaLambda workgroups");
+  HMSC_REQUIRE(f.part_wg <= nb - 1, "fused Gamma2 + BetaLambda: more Gamma2 partials than BetaLambda workgroups");
   const size_t smem = BLW_LDS * sizeof(double);
   ProfScope ps(s, PROF_BL);
   switch (wv_bucket(s.K)) {
@@ -2117,15 +2144,7 @@ void launch_lambda_priors(State& s, uint32_t iter, hipStream_t st) {
   const int nparts = std::min(LP_PARTS, std::max(1, s.nsl));
   psi_kernel<<<nparts, 256, 0, st>>>(a);
   HIP_OK(hipGetLastError());
-  const double* rs = s.psi_rs;
-  int np = nparts;
-  if (s.nranks > 1) {
-    slab_sum_kernel<<<1, 256, 0, st>>>(s.psi_rs, s.allreduce_buf, s.NF, nparts, s.NF);
-    allreduce_sum(s, s.allreduce_buf, s.NF, st);
-    rs = s.allreduce_buf;
-    np = 1;
-  }
-  delta_kernel<<<s.nr, 64, 0, st>>>(a, rs, np);
+  delta_kernel<<<s.nr, 64, 0, st>>>(a, s.psi_rs, nparts);
   HIP_OK(hipGetLastError());
 }
 
@@ -2140,8 +2159,9 @@ void launch_lambda_priors(State& s, uint32_t iter, hipStream_t st) {
 // ---------------------------------------------------------------------------
 template <int NFB>
 __global__ __launch_bounds__(256) void zl_kernel(const double* __restrict__ Z, const double* __restrict__ BL,
-                                                 const double* __restrict__ iSigma, int ny, int ns_loc, int K,
-                                                 int nc, int NF, int split, double* __restrict__ ZL_part) {
+                                                 const double* __restrict__ iSigma, const int8_t* __restrict__ mask,
+                                                 int ny, int ns_loc, int K, int nc, int NF, int split,
+                                                 double* __restrict__ ZL_part) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int i = blockIdx.x * 64 + lane;
@@ -2157,13 +2177,18 @@ __global__ __launch_bounds__(256) void zl_kernel(const double* __restrict__ Z, c
   double acc[NFB];
 #pragma unroll
   for (int f = 0; f < NFB; ++f) acc[f] = 0.0;
+  // mask (a sharded chain's NA cells, R/updateEta.R:59-70): Y codes; NA cells add nothing
+  auto zv = [&](int j) {
+    const double z = Z[i + (size_t)ny * j];
+    return (mask && mask[i + (size_t)ny * j] < 0) ? 0.0 : z;
+  };
   if (i < ny) {
     int jj = w;
     for (; jj + 12 < nj; jj += 16) {
-      const double z0 = Z[i + (size_t)ny * (ja + jj)];
-      const double z1 = Z[i + (size_t)ny * (ja + jj + 4)];
-      const double z2 = Z[i + (size_t)ny * (ja + jj + 8)];
-      const double z3 = Z[i + (size_t)ny * (ja + jj + 12)];
+      const double z0 = zv(ja + jj);
+      const double z1 = zv(ja + jj + 4);
+      const double z2 = zv(ja + jj + 8);
+      const double z3 = zv(ja + jj + 12);
       const double* l0 = sL + jj * NF;
       const double* l1 = l0 + 4 * NF;
       const double* l2 = l0 + 8 * NF;
@@ -2173,7 +2198,7 @@ __global__ __launch_bounds__(256) void zl_kernel(const double* __restrict__ Z, c
         if (f < NF) acc[f] = fma(z3, l3[f], fma(z2, l2[f], fma(z1, l1[f], fma(z0, l0[f], acc[f]))));
     }
     for (; jj < nj; jj += 4) {
-      const double z0 = Z[i + (size_t)ny * (ja + jj)];
+      const double z0 = zv(ja + jj);
       const double* l0 = sL + jj * NF;
 #pragma unroll
       for (int f = 0; f < NFB; ++f)
@@ -2516,6 +2541,7 @@ struct EtaFArgs {
   const int* Pi;      // ny: unit of each row (0-based)
   double* Eta;        // np x nf
   double* G_part;     // [tile][K x nf]  (Eta^T XEta partial, ld Kmax)
+  double* ZL;         // sharded chain: ZL [site][nf] -- written by the stream (EF_STREAM), read by the solve (EF_SOLVE)
   int ny, ns_loc, K, Kmax, nc, nf, np, ldcr;
   Key key;
   uint32_t iter;
@@ -2525,6 +2551,13 @@ struct EtaFArgs {
 };
 
 constexpr int EF_SITES = 16;
+// EF_FUSED: the one-pass kernel above.  A species-sharded chain splits it at the all-reduce
+// of ZL (a sum over every rank's species): EF_STREAM is stage 1 alone over this rank's species,
+// its 4 waves' partials added in the fused kernel's order and stored as ZL [site][nf];
+// EF_SOLVE is stages 2-4 on the all-reduced ZL and CR, each workgroup forming W = L^-1 itself
+// (one wave, the BetaLambda tail's factorization) -- on one rank the pair reproduces the
+// fused kernel bit for bit.
+enum EtaMode { EF_FUSED = 0, EF_STREAM = 1, EF_SOLVE = 2 };
 
 // __launch_bounds__(256, 3): <= 168 VGPRs, three waves per SIMD, so the 625 workgroups of the
 // synthetic config (2500 waves) are resident in one round (at 196 VGPRs they took two: 33 ->
@@ -2533,9 +2566,9 @@ constexpr int EF_SITES = 16;
 #ifndef EF_DEPTH
 #define EF_DEPTH 12
 #endif
-template <int NFB>
+template <int NFB, int MODE>
 __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
-  __shared__ double sPart[4][16][EF_SITES + 1];  // [wave][factor][site] ZL partials
+  __shared__ double sPart[4][16][EF_SITES + 1];  // [wave][factor][site] ZL partials (EF_SOLVE: W's scratch)
   __shared__ double sW[NFB * NFB];            // W = L^-1, L the lower factor of Q (row m at m NFB)
   __shared__ double sB[NFB][EF_SITES], sXi[NFB][EF_SITES], sU[NFB][EF_SITES];
   __shared__ double sX[64][EF_SITES + 1];     // XEta tile [k][site] (K <= 64)
@@ -2547,39 +2580,47 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
   const int i0 = blockIdx.x * EF_SITES;
   if (blockIdx.x == 0) HMSC_STAMP(50);
   const uint32_t iter = SWEEP_ITER(a);       // read once, ahead of the stream
-  if (t < EF_SITES) sPi[t] = i0 + t < ny ? a.Pi[i0 + t] : 0;
+  if (MODE != EF_STREAM && t < EF_SITES) sPi[t] = i0 + t < ny ? a.Pi[i0 + t] : 0;
   // ---- stage 1: ZL = Z (Lambda diag(iSigma))^T on the matrix cores, the HBM stream of the
   // launch, issued first: species j = 16 s + 4 w + lk, B = LS[j][lm] straight from L2 (128 KB,
   // shared by every workgroup); eight steps' loads in flight before their MFMAs
   d4 acc = {0.0, 0.0, 0.0, 0.0};
   // the tile's X columns (the residual's fixed part and the Gram tile), loaded before the
   // stream so they arrive during it: nc x 16 values, at most 4 per thread (nc < 64)
-  double xr[4];
+  double xr[4] = {0.0, 0.0, 0.0, 0.0};
+  if (MODE != EF_STREAM)
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int p = t + 256 * u, s2 = p % EF_SITES, k = p / EF_SITES, ii = i0 + s2;
-    xr[u] = (k < nc && ii < ny) ? a.XEta[ii + (size_t)ny * k] : 0.0;
-  }
+    for (int u = 0; u < 4; ++u) {
+      const int p = t + 256 * u, s2 = p % EF_SITES, k = p / EF_SITES, ii = i0 + s2;
+      xr[u] = (k < nc && ii < ny) ? a.XEta[ii + (size_t)ny * k] : 0.0;
+    }
   // CR (K x nf) and W (nf x nf) of this sweep, formed once by crw_body: loads issued here,
   // ahead of the stream, stored to LDS after it
-  double crv[4], wv[NFB * NFB / 256 + 1];
+  double crv[4] = {0.0, 0.0, 0.0, 0.0}, wv[NFB * NFB / 256 + 1];
+  if (MODE != EF_STREAM)
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int p = t + 256 * u, k = p % K, h = p / K;
-    crv[u] = p < K * nf ? a.CR[k + (size_t)a.ldcr * h] : 0.0;
-  }
+    for (int u = 0; u < 4; ++u) {
+      const int p = t + 256 * u, k = p % K, h = p / K;
+      crv[u] = p < K * nf ? a.CR[k + (size_t)a.ldcr * h] : 0.0;
+    }
 #pragma unroll
   for (int u = 0; u < NFB * NFB / 256 + 1; ++u) {
     const int p = t + 256 * u, m = p / NFB, c = p % NFB;
-    wv[u] = p < NFB * NFB ? a.W[m * 16 + c] : 0.0;
+    wv[u] = (MODE == EF_FUSED && p < NFB * NFB) ? a.W[m * 16 + c] : 0.0;
+  }
+  // EF_SOLVE: the tile's all-reduced ZL (16 sites x nf, contiguous), one element per thread
+  double zlv = 0.0;
+  if (MODE == EF_SOLVE && t < EF_SITES * nf) {
+    const int s2 = t % EF_SITES, h = t / EF_SITES;
+    zlv = i0 + s2 < ny ? a.ZL[(size_t)(i0 + s2) * nf + h] : 0.0;
   }
   const double* zc = a.Z + min(i0 + lm, ny - 1);  // sites past ny: any finite row, unused
-  const int nsteps = (ns + 15) >> 4;
+  const int nsteps = MODE == EF_SOLVE ? 0 : (ns + 15) >> 4;
   // the per-site noise of stage 2 (one (site, factor) pair per thread, t < EF_SITES nf <= 256):
   // drawn while the stream's first loads are in flight instead of after the stream
   double xi_pre = 0.0;
   const int xs2 = t % EF_SITES, xh = t / EF_SITES;
-  const bool x_on = t < EF_SITES * nf && i0 + xs2 < ny && !a.noise_zero;
+  const bool x_on = MODE != EF_STREAM && t < EF_SITES * nf && i0 + xs2 < ny && !a.noise_zero;
   const int x_unit = x_on ? a.Pi[i0 + xs2] : 0;
   int s = 0;
   for (; s + EF_DEPTH <= nsteps; s += EF_DEPTH) {
@@ -2608,8 +2649,22 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
     for (int u = 0; u < 8; ++u) acc = mfma_f64(zv[u], lv[u], acc);
   }
   // acc[r] = partial ZL[site lk + 4 r][factor lm]
+  if (MODE != EF_SOLVE)
 #pragma unroll
-  for (int r = 0; r < 4; ++r) sPart[w][lm][lk + 4 * r] = acc[r];
+    for (int r = 0; r < 4; ++r) sPart[w][lm][lk + 4 * r] = acc[r];
+  if (MODE == EF_STREAM) {  // this rank's ZL, the 4 waves' partials added as stage 2 adds them
+    __syncthreads();
+    for (int p = t; p < EF_SITES * nf; p += 256) {
+      const int s2 = p % EF_SITES, h = p / EF_SITES, ii = i0 + s2;
+      const double zl = (sPart[0][h][s2] + sPart[1][h][s2]) + (sPart[2][h][s2] + sPart[3][h][s2]);
+      if (ii < ny) a.ZL[(size_t)ii * nf + h] = zl;
+    }
+    if (a.kt) {
+      __syncthreads();
+      if (t == 0) kt_record(a.kt, iter, kt0);
+    }
+    return;
+  }
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int p = t + 256 * u, s2 = p % EF_SITES, k = p / EF_SITES;
@@ -2620,17 +2675,22 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
     const int p = t + 256 * u, k = p % K, h = p / K;
     if (p < K * nf) sCR[k * NFB + h] = crv[u];
   }
+  if (MODE == EF_FUSED)
 #pragma unroll
-  for (int u = 0; u < NFB * NFB / 256 + 1; ++u) {
-    const int p = t + 256 * u;
-    if (p < NFB * NFB) sW[p] = wv[u];
-  }
+    for (int u = 0; u < NFB * NFB / 256 + 1; ++u) {
+      const int p = t + 256 * u;
+      if (p < NFB * NFB) sW[p] = wv[u];
+    }
   __syncthreads();
+  if (MODE == EF_SOLVE) {  // W = L^-1 of Q = I + (rows nc.. of CR), one wave, into sW (rows m < NFB)
+    if (w == 0) q_inv_factor_nf(sCR + nc * NFB, NFB, nf, sW, NFB, NFB, &sPart[0][0][0]);
+    __syncthreads();
+  }
   if (blockIdx.x == 0) HMSC_STAMP(51);
   // ---- stage 2: b = ZL - X CR_x, and the noise, one (site, factor) per thread
   for (int p = t; p < EF_SITES * nf; p += 256) {
     const int s2 = p % EF_SITES, h = p / EF_SITES, ii = i0 + s2;
-    const double zl = (sPart[0][h][s2] + sPart[1][h][s2]) + (sPart[2][h][s2] + sPart[3][h][s2]);
+    const double zl = MODE == EF_SOLVE ? zlv : (sPart[0][h][s2] + sPart[1][h][s2]) + (sPart[2][h][s2] + sPart[3][h][s2]);
     double corr = 0.0, xi = 0.0;
     if (ii < ny) {
       // X from the tile staged in LDS (a global load per term here waited out one L2
@@ -2897,24 +2957,11 @@ void flush_g(State& s) {
 }
 
 static bool eta_fused_ok(const State& s) {
-  return s.nranks == 1 && s.nr == 1 && !s.lev[0].spatial && s.n_na_rows == 0 && s.lev[0].np == s.ny && s.lev[0].uniform_n == 1 &&
+  return !s.sharded && s.nr == 1 && !s.lev[0].spatial && s.n_na_rows == 0 && s.lev[0].np == s.ny && s.lev[0].uniform_n == 1 &&
          s.lev[0].nf <= 16 && s.K <= 64 && s.LS != nullptr && !getenv_flag("HMSC_NO_ETA_FUSION");
 }
 
-static void launch_eta_fused(State& s, uint32_t iter, bool cr_done = false) {
-  const int ncr = (s.nsl + SB - 1) / SB;
-  const int64_t slab = (int64_t)s.Kmax * s.NFmax;
-  if (!cr_done) {  // CR, W and LS (post_bl_kernel's workgroup 0 forms them in the co-launched path)
-    const size_t smem = (size_t)CRW_LDS * sizeof(double);
-    const CRWArgs c = make_crw_args(s);
-    if (c.nf <= 8)
-      crw_kernel<8><<<CRW_PARTS, 256, smem, s.stream>>>(c);
-    else if (c.nf <= 12)
-      crw_kernel<12><<<CRW_PARTS, 256, smem, s.stream>>>(c);
-    else
-      crw_kernel<16><<<CRW_PARTS, 256, smem, s.stream>>>(c);
-    HIP_OK(hipGetLastError());
-  }
+static EtaFArgs make_etaf_args(State& s, uint32_t iter) {
   const Level& L = s.lev[0];
   EtaFArgs a{};
   a.Z = s.Z;
@@ -2925,6 +2972,7 @@ static void launch_eta_fused(State& s, uint32_t iter, bool cr_done = false) {
   a.Pi = L.Pi;
   a.Eta = L.Eta;
   a.G_part = s.G_part;
+  a.ZL = nullptr;
   a.ny = s.ny;
   a.ns_loc = s.nsl;
   a.K = s.K;
@@ -2938,74 +2986,82 @@ static void launch_eta_fused(State& s, uint32_t iter, bool cr_done = false) {
   a.iter_dev = s.capturing ? s.d_iter : nullptr;
   a.noise_zero = s.noise_mode;
   a.kt = s.kt_on ? s.d_kt + (size_t)KT_ETA * 2 * KT_SLOTS : nullptr;
-  const int ntile = (s.ny + EF_SITES - 1) / EF_SITES;
-  {
-    ProfScope ps(s, PROF_ETA_UNIT);
-    if (L.nf <= 8)
-      eta_fused_kernel<8><<<ntile, 256, 0, s.stream>>>(a);
-    else if (L.nf <= 12)
-      eta_fused_kernel<12><<<ntile, 256, 0, s.stream>>>(a);
-    else
-      eta_fused_kernel<16><<<ntile, 256, 0, s.stream>>>(a);
-    HIP_OK(hipGetLastError());
-  }
-  // G's Eta rows: reduced from G_part by the next updateZ launch (or flush_g)
-  s.g_pending = true;
-  s.g_ntile = ntile;
-  s.g_nf = L.nf;
-  s.zt_valid = false;   // Eta changed: XZ is stale until the next updateZ
-  s.xeta_valid = true;  // XEta rows rewritten above, G pending
+  return a;
 }
 
-void launch_eta(State& s, uint32_t iter) {
-  s.crw_fresh = false;  // (the co-launched path consumes the tail's constants itself)
-  if (s.nr == 0) return;
-  if (!s.xeta_valid) launch_xeta(s);  // the Eta kernels read XEta of the current Eta
-  if (eta_fused_ok(s)) {
-    launch_eta_fused(s, iter);
-    return;
+template <int MODE>
+static void launch_eta_fused_mode(State& s, const EtaFArgs& a) {
+  const int ntile = (s.ny + EF_SITES - 1) / EF_SITES;
+  const int nf = s.lev[0].nf;
+  if (nf <= 8)
+    eta_fused_kernel<8, MODE><<<ntile, 256, 0, s.stream>>>(a);
+  else if (nf <= 12)
+    eta_fused_kernel<12, MODE><<<ntile, 256, 0, s.stream>>>(a);
+  else
+    eta_fused_kernel<16, MODE><<<ntile, 256, 0, s.stream>>>(a);
+  HIP_OK(hipGetLastError());
+  if (MODE != EF_STREAM) {
+    // G's Eta rows: reduced from G_part by the next updateZ launch (or flush_g)
+    s.g_pending = true;
+    s.g_ntile = ntile;
+    s.g_nf = nf;
+    s.zt_valid = false;   // Eta changed: XZ is stale until the next updateZ
+    s.xeta_valid = true;  // XEta rows rewritten, G pending
   }
-  HMSC_REQUIRE(s.NF <= 64, "updateEta: sum(nf) must be <= 64 in this build");
-  for (int r = 0; r < s.nr; ++r)
-    HMSC_REQUIRE(s.lev[r].nf >= 1, "updateEta: a level has zero factors");
-  // ZL over all levels in one pass over Z
-  {
-    dim3 grid((s.ny + 63) / 64, s.zl_split);
-    const int per = (s.nsl + s.zl_split - 1) / s.zl_split;
-    const size_t smem = std::max((size_t)per * s.NF, (size_t)4 * s.NF * 64) * sizeof(double);
-    ProfScope ps(s, PROF_ZL);
-    if (s.NF <= 8)
-      zl_kernel<8><<<grid, 256, smem, s.stream>>>(s.Z, s.BL, s.iSigma, s.ny, s.nsl, s.K, s.nc, s.NF, s.zl_split, s.ZL_part);
-    else if (s.NF <= 16)
-      zl_kernel<16><<<grid, 256, smem, s.stream>>>(s.Z, s.BL, s.iSigma, s.ny, s.nsl, s.K, s.nc, s.NF, s.zl_split, s.ZL_part);
-    else if (s.NF <= 32)
-      zl_kernel<32><<<grid, 256, smem, s.stream>>>(s.Z, s.BL, s.iSigma, s.ny, s.nsl, s.K, s.nc, s.NF, s.zl_split, s.ZL_part);
+}
+
+static void launch_eta_fused(State& s, uint32_t iter, bool cr_done = false) {
+  if (!cr_done) {  // CR, W and LS (post_bl_kernel's workgroup 0 forms them in the co-launched path)
+    const size_t smem = (size_t)CRW_LDS * sizeof(double);
+    const CRWArgs c = make_crw_args(s);
+    if (c.nf <= 8)
+      crw_kernel<8><<<CRW_PARTS, 256, smem, s.stream>>>(c);
+    else if (c.nf <= 12)
+      crw_kernel<12><<<CRW_PARTS, 256, smem, s.stream>>>(c);
     else
-      zl_kernel<64><<<grid, 256, smem, s.stream>>>(s.Z, s.BL, s.iSigma, s.ny, s.nsl, s.K, s.nc, s.NF, s.zl_split, s.ZL_part);
+      crw_kernel<16><<<CRW_PARTS, 256, smem, s.stream>>>(c);
     HIP_OK(hipGetLastError());
   }
-  {
-    const int ncr = (s.nsl + SB - 1) / SB;
-    const int64_t slab = (int64_t)s.Kmax * s.NFmax;
-    cr_kernel<<<ncr, 256, (size_t)s.K * SB * sizeof(double), s.stream>>>(s.BL, s.iSigma, s.K, s.nc, s.NF, s.nsl,
-                                                                           s.CR_part, s.Kmax, (int)slab, nullptr);
-    HIP_OK(hipGetLastError());
-    slab_sum_kernel<<<grid_for(slab), 256, 0, s.stream>>>(s.CR_part, s.CR, slab, ncr, slab);
-    HIP_OK(hipGetLastError());
+  const EtaFArgs a = make_etaf_args(s, iter);
+  ProfScope ps(s, PROF_ETA_UNIT);
+  launch_eta_fused_mode<EF_FUSED>(s, a);
+}
+
+// NA rows of a sharded chain, level r (R/updateEta.R:59-70): the masked per-row precision and
+// numerator of eta_na_row_kernel from the all-reduced row-masked CR (na_crrow_kernel) and the
+// masked ZL, so no per-row sum over species is left after the all-reduce:
+//   Mrow = CRrow[loff + h1, foff + h2],  brow_h = ZL_i[foff + h] - sum_{k not in r} XEta_ik CRrow[k, foff + h]
+__global__ __launch_bounds__(64) void na_row_finish_kernel(EtaView ev, int r, int nf, int K, int NF, int loff, int foff,
+                                                           const int* na_rows, const double* ZL, const double* CRrow,
+                                                           double* Mrow, double* brow) {
+  extern __shared__ __attribute__((aligned(16))) double sx[];  // XEta row (K)
+  const int slot = blockIdx.x, i = na_rows[slot], t = threadIdx.x;
+  const double* C = CRrow + (size_t)slot * K * NF;  // [k + K f]
+  for (int k = t; k < K; k += 64) sx[k] = xeta_at(ev, i, k);
+  __syncthreads();
+  for (int p = t; p < nf * nf + nf; p += 64) {
+    if (p < nf * nf) {
+      const int h1 = p % nf, h2 = p / nf;
+      Mrow[(size_t)slot * nf * nf + p] = C[loff + h1 + (size_t)K * (foff + h2)];
+    } else {
+      const int h = p - nf * nf;
+      double v = ZL[(size_t)i * NF + foff + h];
+      for (int k = 0; k < K; ++k)
+        if (k < loff || k >= loff + nf) v -= sx[k] * C[k + (size_t)K * (foff + h)];
+      brow[(size_t)slot * nf + h] = v;
+    }
   }
-  const double* zl = s.ZL_part;
-  int nzl = s.zl_split;
-  if (s.nranks > 1) {
-    const int64_t nzle = (int64_t)s.ny * s.NF;
-    slab_sum_kernel<<<grid_for(nzle), 256, 0, s.stream>>>(s.ZL_part, s.ZL, nzle, s.zl_split, nzle);
-    allreduce_sum(s, s.ZL, nzle);
-    allreduce_sum(s, s.CR, (size_t)s.Kmax * s.NFmax);
-    zl = s.ZL;
-    nzl = 1;
-  }
+}
+
+// The per-level Eta draws of the general path (R/updateEta.R:42-92, levels in order, each
+// seeing the new Eta of the previous ones): ZL (nzl partials, [site][NF]) and CR (ld ldcr)
+// are the sums over species -- this chain's own, or a sharded chain's all-reduced ones, whose
+// NA rows then come from the all-reduced row-masked CR (na_crrow) instead of eta_na_row_kernel.
+static void eta_levels(State& s, uint32_t iter, const double* zl, int nzl, const double* cr, int ldcr,
+                       const double* na_crrow) {
   for (int r = 0; r < s.nr; ++r) {
     const Level& L = s.lev[r];
-    if (r > 0) launch_xeta(s);  // levels r' < r were just redrawn (R/updateEta.R:31-37 uses them)
+    if (r > 0) launch_xeta(s);  // levels r' < r were just redrawn (R/updateEta.R:218-226 rebuilds LRan[[r']])
     if (L.spatial) {            // R/updateEta.R:111-140 (spatial.hip)
       launch_eta_spatial(s, r, iter);
       continue;
@@ -3021,10 +3077,10 @@ void launch_eta(State& s, uint32_t iter) {
     a.NF = s.NF;
     a.foff = s.foff(r);
     a.loff = s.loff(r);
-    a.ldcr = s.Kmax;
+    a.ldcr = ldcr;
     a.nzl = nzl;
     a.ZL = zl;
-    a.CR = s.CR;
+    a.CR = cr;
     a.unit_ptr = L.unit_ptr;
     a.unit_rows = L.unit_rows;
     a.Eta = L.Eta;
@@ -3033,11 +3089,15 @@ void launch_eta(State& s, uint32_t iter) {
     a.iter_dev = s.capturing ? s.d_iter : nullptr;
     a.noise_zero = s.noise_mode;
     if (s.n_na_rows > 0) {
-      HMSC_REQUIRE(s.nranks == 1, "updateEta: NA rows with species sharding not supported");
       double* Mrow = s.Msmall;
       double* brow = Mrow + (size_t)s.n_na_rows * L.nf * L.nf;
-      eta_na_row_kernel<<<s.n_na_rows, 64, s.K * sizeof(double), s.stream>>>(
-          a.ev, r, L.nf, s.K, s.nc, a.loff, s.na_rows, s.Z, s.BL, s.iSigma, s.Ycode, s.nsl, Mrow, brow);
+      if (na_crrow) {
+        na_row_finish_kernel<<<s.n_na_rows, 64, s.K * sizeof(double), s.stream>>>(
+            a.ev, r, L.nf, s.K, s.NF, a.loff, a.foff, s.na_rows, zl, na_crrow, Mrow, brow);
+      } else {
+        eta_na_row_kernel<<<s.n_na_rows, 64, s.K * sizeof(double), s.stream>>>(
+            a.ev, r, L.nf, s.K, s.nc, a.loff, s.na_rows, s.Z, s.BL, s.iSigma, s.Ycode, s.nsl, Mrow, brow);
+      }
       HIP_OK(hipGetLastError());
       a.row_na = s.row_na;
       a.row_slot = s.row_slot;
@@ -3062,6 +3122,46 @@ void launch_eta(State& s, uint32_t iter) {
   }
   s.zt_valid = false;  // Eta changed: XZ is stale until the next updateZ
   launch_xeta(s);      // XEta and G for the new Eta
+}
+
+static void launch_zl(State& s, const int8_t* mask) {
+  dim3 grid((s.ny + 63) / 64, s.zl_split);
+  const int per = (s.nsl + s.zl_split - 1) / s.zl_split;
+  const size_t smem = std::max((size_t)per * s.NF, (size_t)4 * s.NF * 64) * sizeof(double);
+  ProfScope ps(s, PROF_ZL);
+  if (s.NF <= 8)
+    zl_kernel<8><<<grid, 256, smem, s.stream>>>(s.Z, s.BL, s.iSigma, mask, s.ny, s.nsl, s.K, s.nc, s.NF, s.zl_split, s.ZL_part);
+  else if (s.NF <= 16)
+    zl_kernel<16><<<grid, 256, smem, s.stream>>>(s.Z, s.BL, s.iSigma, mask, s.ny, s.nsl, s.K, s.nc, s.NF, s.zl_split, s.ZL_part);
+  else if (s.NF <= 32)
+    zl_kernel<32><<<grid, 256, smem, s.stream>>>(s.Z, s.BL, s.iSigma, mask, s.ny, s.nsl, s.K, s.nc, s.NF, s.zl_split, s.ZL_part);
+  else
+    zl_kernel<64><<<grid, 256, smem, s.stream>>>(s.Z, s.BL, s.iSigma, mask, s.ny, s.nsl, s.K, s.nc, s.NF, s.zl_split, s.ZL_part);
+  HIP_OK(hipGetLastError());
+}
+
+void launch_eta(State& s, uint32_t iter) {
+  s.crw_fresh = false;  // (the co-launched path consumes the tail's constants itself)
+  if (s.nr == 0) return;
+  if (!s.xeta_valid) launch_xeta(s);  // the Eta kernels read XEta of the current Eta
+  if (eta_fused_ok(s)) {
+    launch_eta_fused(s, iter);
+    return;
+  }
+  HMSC_REQUIRE(s.NF <= 64, "updateEta: sum(nf) must be <= 64 in this build");
+  for (int r = 0; r < s.nr; ++r)
+    HMSC_REQUIRE(s.lev[r].nf >= 1, "updateEta: a level has zero factors");
+  launch_zl(s, nullptr);  // ZL over all levels in one pass over Z
+  {
+    const int ncr = (s.nsl + SB - 1) / SB;
+    const int64_t slab = (int64_t)s.Kmax * s.NFmax;
+    cr_kernel<<<ncr, 256, (size_t)s.K * SB * sizeof(double), s.stream>>>(s.BL, s.iSigma, s.K, s.nc, s.NF, s.nsl,
+                                                                           s.CR_part, s.Kmax, (int)slab, nullptr);
+    HIP_OK(hipGetLastError());
+    slab_sum_kernel<<<grid_for(slab), 256, 0, s.stream>>>(s.CR_part, s.CR, slab, ncr, slab);
+    HIP_OK(hipGetLastError());
+  }
+  eta_levels(s, iter, s.ZL_part, s.zl_split, s.CR, s.Kmax, nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -3392,6 +3492,475 @@ void launch_slab_sum2_pack(State& s, const double* p0, double* o0, int64_t n0, i
   constexpr int NPACK = 256;
   slab_pack_kernel<<<j0.nb + j1.nb + NPACK, 256, 0, s.stream>>>(j0, j1, pk, NPACK);
   HIP_OK(hipGetLastError());
+}
+
+// ===========================================================================
+// Species-sharded sweep (the data layout in state.h "species-sharded chain").
+// Every rank owns a block of species; each updater's sums over species become one section of
+// the all-reduce buffers, and the sweep issues exactly two all-reduces (ar_point, capi.cpp):
+//   A  after updateZ:          ar_a, the next updateGamma2's species sums
+//   B  after updateBetaLambda: ar_b, updateEta's ZL / CR (+ NA rows), updateGammaV's and
+//                              updateLambdaPriors' species sums
+// With every updater of the synthetic config on, the same fused launches as one rank run:
+// the Gamma2 + BetaLambda launch (Gamma2 from ar_a; its tail leaves CR and the GammaV / psi
+// sums in ar_b), the Eta stream (ZL into ar_b), the all-reduce, the side chain (GammaV algebra,
+// delta chains) on the side stream, and the Eta solve.  On one rank that reproduces the
+// unsharded chain bit for bit (tests/test_gpu_sharded.py).
+// ===========================================================================
+ArbLayout arb_layout(const State& s) {
+  ArbLayout L;
+  const bool eta = (s.mask & HMSC_UP_ETA) && s.nr > 0;
+  const bool gv = (s.mask & HMSC_UP_GAMMAV) != 0;
+  const bool lp = (s.mask & HMSC_UP_LAMBDAPRIORS) && s.nr > 0;
+  size_t o = 0;
+  L.zl = o;
+  o += eta ? (size_t)s.ny * s.NF : 0;
+  L.cr = o;
+  o += eta ? (size_t)s.K * s.NF : 0;
+  L.ldcr = s.K;
+  L.gv = o;
+  o += gv ? (size_t)s.nc * s.nc + (size_t)s.nc * s.nt : 0;
+  L.rs = o;
+  o += lp ? (size_t)s.NF : 0;
+  L.na = o;
+  o += (eta && s.n_na_rows > 0) ? (size_t)s.n_na_rows * s.K * s.NF : 0;
+  L.n = o;
+  return L;
+}
+
+size_t arb_capacity(const State& s) {
+  const size_t NF = std::max(1, s.NFmax), K = s.Kmax;
+  return (size_t)s.ny * NF + K * NF + (size_t)s.nc * s.nc + (size_t)s.nc * s.nt + NF + (size_t)s.n_na_rows * K * NF + 64;
+}
+
+bool sharded_fused_ok(const State& s) {
+  const uint32_t need = HMSC_UP_GAMMA2 | HMSC_UP_BETALAMBDA | HMSC_UP_GAMMAV | HMSC_UP_LAMBDAPRIORS | HMSC_UP_ETA;
+  const size_t N = (size_t)s.nc * s.nt;
+  return s.sharded && (s.mask & need) == need && !(s.mask & HMSC_UP_GAMMAETA) && !s.any_na_global && !s.phylo &&
+         s.nr == 1 && !s.lev[0].spatial && s.n_na_rows == 0 && s.lev[0].np == s.ny && s.lev[0].uniform_n == 1 &&
+         s.lev[0].nf <= 16 && s.K <= 32 && s.nt <= 8 && N <= 32 && s.NF * s.nt + N <= 64 &&
+         (G2F_LDS + (size_t)s.nc * s.nc + N * N) <= (size_t)BLW_LDS &&
+         (size_t)s.nc * s.nc + N + s.NF <= 1024 && s.LS != nullptr && s.gvt != nullptr && s.gbl_sync != nullptr &&
+         !getenv_flag("HMSC_NO_G2BL_FUSION") && !getenv_flag("HMSC_NO_ETA_FUSION") && !getenv_flag("HMSC_NO_SHARD_FUSION");
+}
+
+// out[p] = sum_b part[b * ld + p] in b order from 0 (the order gammav_body / delta_body sum
+// a single rank's partials), eight partials' loads in flight per thread
+__global__ __launch_bounds__(256) void seq_sum_kernel(const double* __restrict__ part, int nparts, int64_t ld,
+                                                      int64_t n, double* __restrict__ out) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    double v = 0.0;
+    int b = 0;
+    for (; b + 8 <= nparts; b += 8) {
+      double x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = part[(int64_t)(b + u) * ld + p];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v += x[u];
+    }
+    for (; b < nparts; ++b) v += part[(int64_t)b * ld + p];
+    out[p] = v;
+  }
+}
+
+static void seq_sum(const double* part, int nparts, int64_t ld, int64_t n, double* out, hipStream_t st) {
+  if (n <= 0) return;
+  seq_sum_kernel<<<grid_for(n, 256, 1024), 256, 0, st>>>(part, nparts, ld, n, out);
+  HIP_OK(hipGetLastError());
+}
+
+// ---- all-reduce A: updateGamma2's sums over this rank's species (R/updateGamma2.R:36,46)
+//   ar_a = [X^T Z Tr (nc nt) | Lambda_all Tr (NF nt) | #(iSigma != 1)]
+// Workgroup b forms the partial of species block b (gamma2_partial_body, as the BetaLambda
+// workgroups of the fused launch do); the last one through (a ticket) adds them in the order
+// gamma2_final_body adds a single rank's partials, so Gamma2 of a 1-rank sharded chain is the
+// unsharded chain's bit for bit.  With NA in this rank's Y, XZ is masked and X^T Z Tr comes
+// from ZTr (xtztr) instead.
+struct G2SArgs {
+  const double* XZ;
+  const double* BL;
+  const double* Tr;
+  const double* iSigma;
+  const double* xtztr;
+  double* part;
+  int* ticket;
+  double* out;
+  int K, nc, NF, nt, nsl, nparts;
+};
+
+__global__ __launch_bounds__(256) void g2_stats_kernel(G2SArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int s_last, s_cnt;
+  const int t = threadIdx.x;
+  gamma2_partial_body(a.XZ, a.BL, a.K, a.nc, a.NF, a.nt, a.nsl, a.Tr, a.part, smem, blockIdx.x, true);
+  vm_stores_done();
+  __syncthreads();
+  if (t == 0) s_last = __hip_atomic_fetch_add(a.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.nparts - 1;
+  __syncthreads();
+  if (!s_last) return;
+  if (t == 0) {
+    s_cnt = 0;
+    __hip_atomic_store(a.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const int n1 = a.nc * a.nt, P = n1 + a.NF * a.nt;
+  for (int p = t; p < P; p += 256) {
+    double v = 0.0;
+    if (P <= 64 && a.nparts > 1) {  // gamma2_final_body: 8 groups of every 8th part, then the groups
+      for (int g = 0; g < 8; ++g) {
+        double sg = 0.0;
+        for (int b = g; b < a.nparts; b += 8) sg += load_coherent(a.part + (size_t)b * P + p);
+        v += sg;
+      }
+    } else {
+      for (int b = 0; b < a.nparts; ++b) v += load_coherent(a.part + (size_t)b * P + p);
+    }
+    a.out[p] = (p < n1 && a.xtztr) ? a.xtztr[p] : v;
+  }
+  __syncthreads();
+  int c = 0;
+  for (int j = t; j < a.nsl; j += 256) c += a.iSigma[j] != 1.0;
+  if (c) atomicAdd(&s_cnt, c);
+  __syncthreads();
+  if (t == 0) a.out[P] = (double)s_cnt;
+}
+
+static void shard_g2_stats(State& s) {
+  if (!(s.mask & HMSC_UP_GAMMA2)) return;
+  HMSC_REQUIRE((size_t)s.nc * s.nt <= 256 && s.NF * s.nt + s.nc * s.nt <= 1024,
+               "updateGamma2: nc*nt must be <= 256 in this build");
+  if (!s.xeta_valid) launch_xeta(s);
+  if (!s.zt_valid) launch_zt_refresh(s);  // XZ (and ZTr) of the current Z and Eta
+  const int n1 = s.nc * s.nt, n12 = n1 + s.NF * s.nt;
+  const double* xt = nullptr;
+  if (s.has_na) {  // this rank's XZ is masked: X^T (Z Tr) from ZTr
+    xt_ztr_kernel<<<n1, 256, 0, s.stream>>>(s.X, s.ZTr, s.ny, s.nc, s.nt, s.allreduce_buf);
+    HIP_OK(hipGetLastError());
+    xt = s.allreduce_buf;
+  }
+  G2SArgs a{};
+  a.XZ = s.XZ;
+  a.BL = s.BL;
+  a.Tr = s.Tr;
+  a.iSigma = s.iSigma;
+  a.xtztr = xt;
+  a.part = s.ABpart;
+  a.ticket = s.shard_ticket;
+  a.out = s.ar_a;
+  a.K = s.K;
+  a.nc = s.nc;
+  a.NF = s.NF;
+  a.nt = s.nt;
+  a.nsl = s.nsl;
+  a.nparts = (s.nsl + SB - 1) / SB;
+  g2_stats_kernel<<<a.nparts, 256, (size_t)(s.K * SB + SB * s.nt) * sizeof(double), s.stream>>>(a);
+  HIP_OK(hipGetLastError());
+  ar_point(s, s.ar_a, (size_t)n12 + 1);  // all-reduce A
+  s.g2s_valid = true;
+}
+
+// updateGamma2 of a sharded chain on the general path: the final stage on the all-reduced sums
+static void launch_gamma2_sharded(State& s, uint32_t iter) {
+  HMSC_REQUIRE((size_t)s.nc * s.nt <= 256 && s.NF * s.nt + s.nc * s.nt <= 1024,
+               "updateGamma2: nc*nt must be <= 256 in this build");
+  if (!s.g2s_valid) shard_g2_stats(s);
+  if (!s.xeta_valid) launch_xeta(s);
+  flush_g(s);  // the final stage reads G's X^T Eta block
+  if (!s.g2prep_valid) {
+    join_side(s);
+    launch_gamma2_prep(s, s.stream);
+  }
+  const int n12 = s.nc * s.nt + s.NF * s.nt;
+  G2Args a{};
+  a.nc = s.nc;
+  a.nt = s.nt;
+  a.Kmax = s.Kmax;
+  a.NF = s.NF;
+  a.nparts = 1;
+  a.ns_loc = s.nsl;
+  a.use_xtztr = 0;
+  a.check_isigma = 0;
+  a.isig_count = s.ar_a + n12;
+  a.part = s.ar_a;
+  a.xtztr = nullptr;
+  a.G = s.G;
+  a.prep = s.g2prep;
+  a.iSigma = s.iSigma;
+  a.Gamma = s.Gamma;
+  a.key = s.key;
+  a.iter = iter;
+  a.iter_dev = s.capturing ? s.d_iter : nullptr;
+  a.noise_zero = s.noise_mode;
+  const size_t N = (size_t)s.nc * s.nt, stage_bytes = ((size_t)s.nc * s.nc + N * N) * sizeof(double);
+  a.stage = stage_bytes <= 28 * 1024;
+  join_side(s);  // iV and the prep matrices come from the previous sweep's GammaV (side stream)
+  gamma2_final_kernel<<<1, 256, G2F_LDS * sizeof(double) + (a.stage ? stage_bytes : 0), s.stream>>>(a);
+  HIP_OK(hipGetLastError());
+}
+
+// ---- all-reduce B producers of the general path (this rank's species -> ar_b sections)
+// updateGammaV: E E^T and B Tr (R/updateGammaV.R:16-18)
+static void shard_gv_stats(State& s, hipStream_t st) {
+  const ArbLayout L = arb_layout(s);
+  const int nparts = (s.nsl + SB - 1) / SB;
+  gammav_partial_kernel<<<nparts, 256, (size_t)(2 * s.nc * SB + SB * s.nt) * sizeof(double), st>>>(
+      s.BL, s.K, s.nc, s.nt, s.nsl, s.Gamma, s.Tr, s.gv_part);
+  HIP_OK(hipGetLastError());
+  const int64_t n = (int64_t)s.nc * s.nc + (int64_t)s.nc * s.nt;
+  seq_sum(s.gv_part, nparts, n, n, s.ar_b + L.gv, st);
+}
+
+// updateLambdaPriors: the psi draws of this rank's species and sum_j psi lambda^2 (:22-24)
+static void shard_psi(State& s, uint32_t iter, hipStream_t st) {
+  const ArbLayout L = arb_layout(s);
+  HMSC_REQUIRE(s.NF <= 64, "updateLambdaPriors: sum(nf) must be <= 64 in this build");
+  const LPArgs a = make_lp_args(s, iter);
+  const int nparts = std::min(LP_PARTS, std::max(1, s.nsl));
+  psi_kernel<<<nparts, 256, 0, st>>>(a);
+  HIP_OK(hipGetLastError());
+  seq_sum(s.psi_rs, nparts, s.NF, s.NF, s.ar_b + L.rs, st);
+}
+
+// the row-masked CR of every NA row (all ranks agree on the rows: any NA in the whole Y), this
+// rank's part: CR - sum over its species NA in row i of BL_j iSigma_j Lambda_j^T, species in
+// ascending order (deterministic); the codes of the row's species from the packed Ybits words
+struct NACRArgs {
+  const double* CR;  // this rank's CR (K x NF, ld K), before the all-reduce
+  const int* na_rows;
+  const uint64_t* Ybits;
+  const double* BL;
+  const double* iSigma;
+  double* out;       // n_na_rows x (K x NF)
+  int ny, nsl, K, NF, nc;
+};
+
+__global__ __launch_bounds__(256) void na_crrow_kernel(NACRArgs a) {
+  extern __shared__ uint64_t sw[];  // the row's code words, one per 32-species block
+  const int slot = blockIdx.x, i = a.na_rows[slot], t = threadIdx.x, nblk = (a.nsl + 31) / 32;
+  for (int b = t; b < nblk; b += 256) sw[b] = a.Ybits[(size_t)b * a.ny + i];
+  __syncthreads();
+  double* dst = a.out + (size_t)slot * a.K * a.NF;
+  for (int p = t; p < a.K * a.NF; p += 256) {
+    const int k = p % a.K, f = p / a.K;
+    double v = a.CR[p];
+    for (int b = 0; b < nblk; ++b) {
+      const uint64_t wd = sw[b];
+      uint64_t na = ~(wd | (wd >> 1)) & 0x5555555555555555ull;  // 2-bit fields equal to 0: code -1 (NA)
+      while (na) {
+        const int q = __ffsll((long long)na) - 1;
+        na &= na - 1;
+        const int j = 32 * b + (q >> 1);
+        if (j < a.nsl) v -= a.BL[k + (size_t)a.K * j] * a.iSigma[j] * a.BL[a.nc + f + (size_t)a.K * j];
+      }
+    }
+    dst[p] = v;
+  }
+}
+
+// updateEta: ZL = Z (Lambda diag(iSigma))^T over this rank's observed cells and CR (+ the NA rows)
+static void shard_eta_stats(State& s) {
+  const ArbLayout L = arb_layout(s);
+  HMSC_REQUIRE(s.NF <= 64, "updateEta: sum(nf) must be <= 64 in this build");
+  launch_zl(s, s.has_na ? s.Ycode : nullptr);
+  const int64_t nzl = (int64_t)s.ny * s.NF;
+  slab_sum_kernel<<<grid_for(nzl), 256, 0, s.stream>>>(s.ZL_part, s.ar_b + L.zl, nzl, s.zl_split, nzl);
+  HIP_OK(hipGetLastError());
+  const int ncr = (s.nsl + SB - 1) / SB;
+  const int64_t slab = (int64_t)s.K * s.NF;
+  cr_kernel<<<ncr, 256, (size_t)s.K * SB * sizeof(double), s.stream>>>(s.BL, s.iSigma, s.K, s.nc, s.NF, s.nsl, s.CR_part,
+                                                                         L.ldcr, (int)slab, nullptr);
+  HIP_OK(hipGetLastError());
+  slab_sum_kernel<<<grid_for(slab), 256, 0, s.stream>>>(s.CR_part, s.ar_b + L.cr, slab, ncr, slab);
+  HIP_OK(hipGetLastError());
+  if (s.n_na_rows > 0) {
+    NACRArgs a{};
+    a.CR = s.ar_b + L.cr;
+    a.na_rows = s.na_rows;
+    a.Ybits = s.Ybits;
+    a.BL = s.BL;
+    a.iSigma = s.iSigma;
+    a.out = s.ar_b + L.na;
+    a.ny = s.ny;
+    a.nsl = s.nsl;
+    a.K = s.K;
+    a.NF = s.NF;
+    a.nc = s.nc;
+    na_crrow_kernel<<<s.n_na_rows, 256, (size_t)((s.nsl + 31) / 32) * sizeof(uint64_t), s.stream>>>(a);
+    HIP_OK(hipGetLastError());
+  }
+}
+
+// ---- consumers of all-reduce B
+static void shard_gammav_final(State& s, uint32_t iter, hipStream_t st) {
+  const ArbLayout L = arb_layout(s);
+  const double* part = s.ar_b + L.gv;
+  if (s.nc * s.nt <= 32) {
+    launch_gammav_wave(s, iter, st, part, 1, s.capturing ? s.d_iter : nullptr);  // (+ Gamma2's prep)
+    return;
+  }
+  GVArgs a{};
+  a.nc = s.nc;
+  a.nt = s.nt;
+  a.ns_glob = s.ns;
+  a.nparts = 1;
+  a.part = part;
+  a.V0 = s.V0;
+  a.f0 = s.f0;
+  a.iUGamma = s.iUGamma;
+  a.mGamma = s.mGamma;
+  a.iUmG = s.iUmG;
+  a.TT = s.TT;
+  a.iV = s.iV;
+  a.Gamma = s.Gamma;
+  a.scratch = s.scratch;
+  a.key = s.key;
+  a.iter = iter;
+  a.iter_dev = s.capturing ? s.d_iter : nullptr;
+  a.noise_zero = s.noise_mode;
+  a.fail = s.dev_flags;
+  const size_t need = (6 * (size_t)s.nc * s.nc + (size_t)s.nc * s.nt + (size_t)s.nc * s.nt * s.nc * s.nt +
+                       (size_t)s.nc * s.nt) * sizeof(double);
+  a.use_lds = need <= 64 * 1024;
+  gammav_final_kernel<<<1, 64, a.use_lds ? need : 0, st>>>(a);
+  HIP_OK(hipGetLastError());
+  if (s.mask & HMSC_UP_GAMMA2) launch_gamma2_prep(s, st);
+}
+
+static void shard_delta(State& s, uint32_t iter, hipStream_t st) {
+  const ArbLayout L = arb_layout(s);
+  LPArgs a = make_lp_args(s, iter);
+  delta_kernel<<<s.nr, 64, 0, st>>>(a, s.ar_b + L.rs, 1);
+  HIP_OK(hipGetLastError());
+}
+
+static void shard_eta_solve(State& s, uint32_t iter, bool fused) {
+  const ArbLayout L = arb_layout(s);
+  if (fused) {
+    EtaFArgs a = make_etaf_args(s, iter);
+    a.ZL = s.ar_b + L.zl;
+    a.CR = s.ar_b + L.cr;
+    a.ldcr = L.ldcr;
+    a.kt = nullptr;  // (the live Eta timer times the stream)
+    launch_eta_fused_mode<EF_SOLVE>(s, a);
+    return;
+  }
+  for (int r = 0; r < s.nr; ++r) HMSC_REQUIRE(s.lev[r].nf >= 1, "updateEta: a level has zero factors");
+  eta_levels(s, iter, s.ar_b + L.zl, 1, s.ar_b + L.cr, L.ldcr, s.n_na_rows > 0 ? s.ar_b + L.na : nullptr);
+}
+
+// One sweep of a sharded chain in the reference order (R/sampleMcmc.R:219-306); see the
+// section comment above.  GammaV's algebra and the delta chains (they feed only the next
+// sweep) run on the side stream after all-reduce B, joined before the next sweep's Gamma2.
+void sweep_sharded(State& s, uint32_t iter) {
+  ProfScope ps(s, PROF_SWEEP);
+  HMSC_REQUIRE(!(s.mask & HMSC_UP_GAMMAETA), "updateGammaEta cannot run on a species-sharded chain");
+  const bool fused = sharded_fused_ok(s);
+  s.side_fused = false;
+  join_side(s);
+  if (s.nr > 0 && !s.xeta_valid) launch_xeta(s);
+  if (fused) {
+    launch_gamma2_bl(s, iter);  // Gamma2 from ar_a; BetaLambda; the tail's CR, LS, psi, GammaV / psi sums
+    EtaFArgs a = make_etaf_args(s, iter);
+    a.ZL = s.ar_b + arb_layout(s).zl;
+    ProfScope pe(s, PROF_ETA_UNIT);
+    launch_eta_fused_mode<EF_STREAM>(s, a);  // this rank's ZL
+  } else {
+    if (s.mask & HMSC_UP_GAMMA2) launch_gamma2_sharded(s, iter);
+    if (s.mask & HMSC_UP_BETALAMBDA) launch_beta_lambda(s, iter);
+    if (s.mask & HMSC_UP_GAMMAV) shard_gv_stats(s, s.stream);
+    if ((s.mask & HMSC_UP_LAMBDAPRIORS) && s.nr > 0) shard_psi(s, iter, s.stream);
+    if ((s.mask & HMSC_UP_ETA) && s.nr > 0) {
+      if (!s.xeta_valid) launch_xeta(s);
+      shard_eta_stats(s);
+    }
+  }
+  const ArbLayout L = arb_layout(s);
+  ar_point(s, s.ar_b, L.n);  // all-reduce B
+  // GammaV (+ Gamma2's prep) and the delta chains, beside Eta and updateZ
+  const bool side_gv = (s.mask & HMSC_UP_GAMMAV) != 0, side_lp = (s.mask & HMSC_UP_LAMBDAPRIORS) && s.nr > 0;
+  if (side_gv || side_lp) {
+    HIP_OK(hipEventRecord(s.ev_bl, s.stream));
+    HIP_OK(hipStreamWaitEvent(s.side, s.ev_bl, 0));
+    if (fused) {
+      GVWArgs gw = make_gvw_args(s, iter, s.ar_b + L.gv, 1, s.capturing ? s.d_iter : nullptr);
+      LPArgs lp = make_lp_args(s, iter);
+      lp.iter_dev = gw.iter_dev;
+      switch (wv_bucket_gv(s.nc * s.nt)) {
+        case 8: launch_side_chain<8>(s, gw, lp, s.ar_b + L.rs, 1, s.NF, nullptr); break;
+        case 16: launch_side_chain<16>(s, gw, lp, s.ar_b + L.rs, 1, s.NF, nullptr); break;
+        case 20: launch_side_chain<20>(s, gw, lp, s.ar_b + L.rs, 1, s.NF, nullptr); break;
+        case 24: launch_side_chain<24>(s, gw, lp, s.ar_b + L.rs, 1, s.NF, nullptr); break;
+        default: launch_side_chain<32>(s, gw, lp, s.ar_b + L.rs, 1, s.NF, nullptr); break;
+      }
+      HIP_OK(hipGetLastError());
+      if (gw.do_prep) s.g2prep_valid = true;
+    } else {
+      if (side_gv) shard_gammav_final(s, iter, s.side);
+      if (side_lp) shard_delta(s, iter, s.side);
+    }
+    s.side_pending |= 1;
+  }
+  if ((s.mask & HMSC_UP_ETA) && s.nr > 0) shard_eta_solve(s, iter, fused);
+  if (s.mask & HMSC_UP_ALPHA) launch_alpha(s, iter);
+  if (s.mask & HMSC_UP_INVSIGMA) launch_inv_sigma(s, iter);
+  if (s.mask & HMSC_UP_Z) launch_update_z(s, iter, false);
+  s.g2s_valid = false;
+  shard_g2_stats(s);  // all-reduce A, for the next sweep's updateGamma2
+}
+
+// hmsc_update(which) on a sharded chain: the updater with its own all-reduce (the sweep merges
+// them into A and B)
+void run_updater_sharded(State& s, uint32_t which, uint32_t iter) {
+  const ArbLayout L = arb_layout(s);
+  switch (which) {
+    case HMSC_UP_GAMMA2:
+      launch_gamma2_sharded(s, iter);
+      break;
+    case HMSC_UP_GAMMAETA:
+      throw HmscError(-1, "updateGammaEta cannot run on a species-sharded chain");
+    case HMSC_UP_BETALAMBDA:
+      join_side(s);
+      launch_beta_lambda(s, iter);
+      s.g2s_valid = false;
+      break;
+    case HMSC_UP_GAMMAV:
+      join_side(s);
+      shard_gv_stats(s, s.stream);
+      ar_point(s, s.ar_b + L.gv, (size_t)s.nc * s.nc + (size_t)s.nc * s.nt);
+      shard_gammav_final(s, iter, s.stream);
+      break;
+    case HMSC_UP_RHO:
+      break;  // no phylogeny on a sharded chain
+    case HMSC_UP_LAMBDAPRIORS:
+      if (s.nr == 0) break;
+      join_side(s);
+      shard_psi(s, iter, s.stream);
+      ar_point(s, s.ar_b + L.rs, s.NF);
+      shard_delta(s, iter, s.stream);
+      break;
+    case HMSC_UP_ETA:
+      if (s.nr == 0) break;
+      join_side(s);
+      if (!s.xeta_valid) launch_xeta(s);
+      shard_eta_stats(s);
+      ar_point(s, s.ar_b + L.zl, L.gv - L.zl);  // ZL | CR
+      if (s.n_na_rows > 0) ar_point(s, s.ar_b + L.na, L.n - L.na);
+      shard_eta_solve(s, iter, false);
+      s.g2s_valid = false;
+      break;
+    case HMSC_UP_ALPHA:
+      launch_alpha(s, iter);
+      break;
+    case HMSC_UP_INVSIGMA:
+      launch_inv_sigma(s, iter);
+      s.g2s_valid = false;
+      break;
+    case HMSC_UP_Z:
+      launch_update_z(s, iter, false);
+      s.g2s_valid = false;
+      break;
+    default:
+      throw HmscError(-1, "unknown or out-of-scope updater bit");
+  }
 }
 
 }  // namespace hmsc

@@ -937,7 +937,7 @@ static void sp_ensure_capacity(State& s, int r) {
 void launch_eta_spatial(State& s, int r, uint32_t iter) {
   sp_ensure_capacity(s, r);
   const Level& L = s.lev[r];
-  HMSC_REQUIRE(s.nranks == 1, "spatial levels: species-sharded chains are not supported");
+  HMSC_REQUIRE(!s.sharded, "spatial levels: species-sharded chains are not supported");
   if (!s.xeta_valid) launch_xeta(s);
   ProfScope ps(s, PROF_ETA_SP);
   if (L.gpp) {

@@ -152,7 +152,7 @@ struct State {
   int* na_cols = nullptr;        // local species with any NA
   int* na_index = nullptr;       // nsl: row of species j in Gna, or -1
   int n_na_cols = 0;
-  int* na_rows = nullptr;        // rows with any NA (local)
+  int* na_rows = nullptr;        // rows with any NA in the whole Y (every rank of a sharded chain: the same rows)
   int8_t* row_na = nullptr;      // ny: 1 if the row has an NA
   int* row_slot = nullptr;       // ny: index into na_rows, or -1
   int n_na_rows = 0;
@@ -255,6 +255,40 @@ struct State {
   hmsc_allreduce_fn host_allreduce = nullptr;
   void* host_allreduce_ctx = nullptr;
   std::vector<double> host_ar_buf;
+
+  // ---- species-sharded chain (kernels.hip "species-sharded sweep", capi.cpp sweep_sharded).
+  // A sharded chain (nranks > 1, or a 1-rank chain created with a communicator or a host
+  // transport) reduces its cross-species sums in exactly two all-reduces per sweep:
+  //   A (after updateZ, for the next sweep's updateGamma2): ar_a = [X^T Z Tr (nc nt) |
+  //     Lambda_all Tr (NF nt) | #(iSigma != 1)]   (R/updateGamma2.R:36,46)
+  //   B (after updateBetaLambda): ar_b = [ZL = Z (Lambda diag(iSigma))^T (ny NF, site-major) |
+  //     CR = BL diag(iSigma) Lambda^T (K x NF, ld K) | GammaV's E E^T, B Tr (nc^2 + nc nt) |
+  //     sum_j psi lambda^2 (NF) | NA rows: CR masked to the row's observed species
+  //     (n_na_rows x K x NF)]   (R/updateEta.R:45-55,59-70, R/updateGammaV.R:16-18,
+  //     R/updateLambdaPriors.R:22-32)
+  // Everything downstream of a sum (Gamma, iV, Delta, Eta) is drawn redundantly on every
+  // rank from the same Philox counters, so the ranks' copies stay bit-identical.
+  bool sharded = false;
+  bool any_na_global = false;    // any NA in the whole Y (the fusion decisions of every rank agree)
+  double* ar_a = nullptr;
+  double* ar_b = nullptr;
+  double* ar_host = nullptr;     // pinned host staging of the host transport (max of A, B)
+  size_t ar_host_doubles = 0;
+  int* shard_ticket = nullptr;   // [g2 stats ticket, spare]: zero between launches
+  bool g2s_valid = false;        // ar_a holds the reduced Gamma2 sums of the current Z, BL, iSigma
+  // debug counters (hmsc_debug_get "ar_calls"): collectives issued / executed and their doubles;
+  // the all-reduces a captured sweep contains (graph replays add ar_per_graph_sweep per sweep)
+  uint64_t ar_calls = 0, ar_doubles = 0;
+  int ar_in_capture = 0, ar_per_graph_sweep = -1;
+  // host transport inside graph capture: a sweep is captured as segments split at its
+  // all-reduces (the host sums between them); cap_segs collects them during the capture
+  struct Seg {
+    hipGraphExec_t g = nullptr;
+    size_t ar_n = 0;             // doubles of ar_host to all-reduce after this segment (0: none)
+    double* ar_dev = nullptr;    // (the device buffer the next segment copies the sum back into)
+  };
+  std::vector<std::pair<hipGraph_t, size_t>>* cap_segs = nullptr;
+  std::vector<Seg> gseg[2];      // [with record]: one sweep of a host-transport sharded chain
 
   std::vector<int> h_nf() const {
     std::vector<int> v(nr);
@@ -388,6 +422,17 @@ void join_side(State& s);
 double* device_realloc_doubles(State& s, double* old, size_t n);
 void launch_copied_flag(State& s, uint64_t value);
 size_t record_slot_doubles(const State& s);
+// ---- species-sharded sweep (kernels.hip); ar_point is the transport (capi.cpp)
+struct ArbLayout {
+  size_t zl = 0, cr = 0, gv = 0, rs = 0, na = 0, n = 0;  // offsets into ar_b, n = doubles in use
+  int ldcr = 0;
+};
+ArbLayout arb_layout(const State& s);
+size_t arb_capacity(const State& s);
+void ar_point(State& s, double* buf, size_t n);
+void sweep_sharded(State& s, uint32_t iter);
+void run_updater_sharded(State& s, uint32_t which, uint32_t iter);
+bool sharded_fused_ok(const State& s);
 void read_stamps(double* out, int n);  // diagnostic build (HMSC_STAMPS)
 
 }  // namespace hmsc

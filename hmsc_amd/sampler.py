@@ -145,20 +145,33 @@ def shard_range(ns, rank, nranks):
     return int(a[0]), int(b[0])
 
 
+def comm_unique_id():
+    """A fresh RCCL unique id (hmsc_comm_unique_id, 128 bytes): one rank creates it and every
+    rank of a species-sharded chain passes it to Chain(..., comm_id=...)."""
+    buf = np.zeros(128, dtype=np.uint8)
+    L.check(L.lib().hmsc_comm_unique_id(buf.ctypes.data))
+    return bytes(buf)
+
+
 class Chain:
     """One chain's device-resident state (hmsc_create ... hmsc_destroy)."""
 
     def __init__(self, hM, seed, device=0, updater=None, rank=0, nranks=1, comm_id=None, mask=None,
                  host_allreduce=None, spatial_grid="device"):
-        """host_allreduce: for a species-sharded chain without RCCL, a callable f(x) that
-        replaces the float64 array x by its sum over all ranks, in place (hmsc_create_sharded_host).
+        """A species-sharded chain (rank of nranks, two all-reduces per sweep) is created when
+        comm_id (an RCCL unique id, hmsc_comm_unique_id) or host_allreduce is given -- also at
+        nranks = 1, where it runs the sharded kernels and collectives on one GPU.
+        host_allreduce: a callable f(x) that replaces the float64 array x by its sum over all
+        ranks, in place (hmsc_create_sharded_host; RCCL is not used).
         spatial_grid: where a 'Full' level's alphapw grid is evaluated (ModelBuffers)."""
         self.hM = hM
         self.lib = L.lib()
         self.buf = ModelBuffers(hM, spatial_grid=spatial_grid)
         self.mask = updater_mask(updater) if mask is None else mask
         h = C.c_void_p()
-        if nranks > 1 and host_allreduce is not None:
+        if nranks > 1 and host_allreduce is None and comm_id is None:
+            raise ValueError("a species-sharded chain needs comm_id (RCCL) or host_allreduce")
+        if host_allreduce is not None:
             def _cb(ptr, n, ctx):
                 try:
                     host_allreduce(np.ctypeslib.as_array(ptr, shape=(int(n),)))
@@ -168,7 +181,7 @@ class Chain:
             self._ar_cb = L.ALLREDUCE_FN(_cb)
             L.check(self.lib.hmsc_create_sharded_host(C.byref(self.buf.struct), C.c_uint64(int(seed)), device,
                                                       self.mask, rank, nranks, self._ar_cb, None, C.byref(h)))
-        elif nranks > 1:
+        elif comm_id is not None:
             cid = C.create_string_buffer(bytes(comm_id), 128)
             L.check(self.lib.hmsc_create_sharded(C.byref(self.buf.struct), C.c_uint64(int(seed)), device,
                                                  self.mask, rank, nranks, cid, C.byref(h)))
