@@ -25,6 +25,7 @@ import json
 import os
 import platform
 import sys
+import threading
 import time
 
 import numpy as np
@@ -64,6 +65,9 @@ def parse():
     p.add_argument("--cpu-oracle-sweeps", type=int, default=None,
                    help="configs 3 / 5: sweeps of the numpy restatement timed for cpu_baseline "
                         "(default 10 for config 3, 3 for config 5)")
+    p.add_argument("--no-sharded-leg", action="store_true",
+                   help="chains mode: skip the short species-sharded run reported beside the main line")
+    p.add_argument("--sharded-leg-timeout", type=float, default=180.0)
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r04_s4_pmc.json"),
                    help="rocprofv3 PMC summary (scripts/pmc_summary.py) the roofline's traffic / valu come from")
     return p.parse_args()
@@ -97,15 +101,8 @@ def main():
 
     hM = synthetic_probit(ny=args.ny, ns=args.ns, nc=args.nc, nf=args.nf)
     upd = {"GammaEta": False}
-    if args.mode == "sharded" and world > 1:
-        cid = None
-        if rank == 0:
-            buf = np.zeros(128, dtype=np.uint8)
-            H._lib.check(H._lib.lib().hmsc_comm_unique_id(buf.ctypes.data))
-            cid = bytes(buf)
-        obj = [cid]
-        dist.broadcast_object_list(obj, src=0)
-        ch = H.Chain(hM, 1234567, device=local, updater=upd, rank=rank, nranks=world, comm_id=obj[0])
+    if args.mode == "sharded":
+        ch = H.Chain(hM, 1234567, device=local, updater=upd, rank=rank, nranks=world, comm_id=_shared_comm_id(rank, dist))
     else:
         ch = H.Chain(hM, 1234567 + 7919 * rank, device=local, updater=upd)
     ch.init([args.nf])
@@ -190,8 +187,39 @@ def main():
             ess_all = np.sum(np.stack(gathered), axis=0)  # chains: per-sweep ESS adds over chains
     else:
         ess_all = ess_local
-    if rank != 0:
-        return
+    ch.close()
+    # the species-sharded form of config 4 over the same GPUs (chains runs only), guarded: if
+    # its collectives do not finish within --sharded-leg-timeout, rank 0 still prints the main
+    # line (with the leg marked timed out) and every rank exits
+    lock, printed = threading.Lock(), [False]
+
+    def finish(sharded):
+        with lock:
+            if printed[0]:
+                return
+            printed[0] = True
+        if rank == 0:
+            _finish_main(args, world, tmax, ess_all, ess_local, n_ess, live, kern, graphs, extra, hM, sharded)
+
+    sharded = None
+    if args.mode == "chains" and not args.no_sharded_leg:
+        def fire():
+            try:
+                finish({"error": f"timed out after {args.sharded_leg_timeout:.0f} s"})
+            finally:
+                os._exit(0)
+        timer = threading.Timer(args.sharded_leg_timeout, fire)
+        timer.daemon = True
+        timer.start()
+        try:
+            sharded = sharded_leg(hM, args, rank, world, local, dist)
+        except Exception as e:  # noqa: BLE001 -- reported beside the main line, not fatal to it
+            sharded = {"error": str(e)[:400]}
+        timer.cancel()
+    finish(sharded)
+
+
+def _finish_main(args, world, tmax, ess_all, ess_local, n_ess, live, kern, graphs, extra, hM, sharded):
     ny, ns = args.ny, args.ns
     sweeps = args.steps * (world if args.mode == "chains" else 1)
     value = sweeps / tmax
@@ -277,8 +305,55 @@ def main():
         "kernels_live_us": {k: round(v["avg_us"], 3) for k, v in live.items()},
         "kernels_eager_events_us": {k: round(v["avg_us"], 2) for k, v in kern.items()},
         "cpu_baseline": cpu,
+        "sharded_chain": sharded,
     }
     print(json.dumps(out), flush=True)
+
+
+def _shared_comm_id(rank, dist):
+    """An RCCL unique id made by rank 0 and broadcast over gloo (hmsc_comm_unique_id)."""
+    from hmsc_amd.sampler import comm_unique_id
+    obj = [comm_unique_id() if rank == 0 else None]
+    if dist is not None:
+        dist.broadcast_object_list(obj, src=0)
+    return obj[0]
+
+
+def sharded_leg(hM, args, rank, world, local, dist, steps=200, warmup=40):
+    """Config 4's other form on the same GPUs: ONE chain species-sharded over the `world` ranks
+    (RCCL; at world = 1 a 1-rank communicator), two all-reduces per sweep captured in the sweep
+    graphs (kernels.hip "species-sharded sweep").  A short timed run after the main measurement,
+    reported beside it (strong scaling: the same ns = 1000 species over more GPUs)."""
+    import torch
+    cid = _shared_comm_id(rank, dist)
+    ch = H.Chain(hM, 1234567, device=local, updater={"GammaEta": False}, rank=rank, nranks=world, comm_id=cid)
+    ch.init([args.nf])
+    ch.run(transient=0, samples=1, thin=1, adaptNf=[0], record=True)
+    ch.prepare_graphs(2)
+    ch.run(transient=0, samples=warmup, thin=1, adaptNf=[0], iter0=1, record=True)
+    ch.sync()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    ch.run(transient=0, samples=steps, thin=1, adaptNf=[0], iter0=1 + warmup, record=True)
+    ch.sync()
+    if dist is not None:
+        dist.barrier()
+    t = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([t], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+    ar = ch.debug_get("ar_calls", 4)
+    graph = ch.debug_get("graph", 4)
+    nsl = ch.nsl
+    ch.close()
+    return {"value": round(steps / t, 3), "unit": "sweeps/s", "ms_per_step": round(1e3 * t / steps, 4),
+            "steps": steps, "warmup": warmup, "ranks": world, "species_per_rank": nsl, "scaling": "strong",
+            "allreduces_per_sweep": int(ar[2]), "graphs": bool(graph[0]),
+            "transport": f"RCCL ({world}-rank communicator)",
+            "note": "one chain, species-sharded over the GPUs, recording every sweep (beside the main line, "
+                    "which is the chains form)"}
 
 
 def main_spatial(args):

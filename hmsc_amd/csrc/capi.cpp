@@ -295,9 +295,12 @@ static void d2h(T* h, const T* d, size_t n, hipStream_t st) {
 void ar_point(State& s, double* buf, size_t n) {
   if (n == 0) return;
   HMSC_REQUIRE(s.sharded, "internal: all-reduce on an unsharded chain");
-  ++s.ar_calls;
-  s.ar_doubles += n;
-  if (s.capturing) ++s.ar_in_capture;
+  if (s.capturing) {
+    ++s.ar_in_capture;  // (executed, and counted, by the replays)
+  } else {
+    ++s.ar_calls;
+    s.ar_doubles += n;
+  }
   if (s.comm) {
     const ncclResult_t r = ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, (ncclComm_t)s.comm, s.stream);
     HMSC_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
@@ -1509,7 +1512,7 @@ static bool replay_sweeps(State& s, uint32_t iter, bool with_record, int n) {
   join_side(s);
   set_iters_kernel<<<1, 64, 0, s.stream>>>(s.d_iters, iter, n);
   HIP_OK(hipGraphLaunch(ge, s.stream));
-  if (s.sharded && s.ar_per_graph_sweep > 0) s.ar_calls += (uint64_t)s.ar_per_graph_sweep * n;
+  if (s.sharded && s.ar_per_graph_sweep > 0) s.ar_calls += (uint64_t)s.ar_per_graph_sweep * n;  // (RCCL: captured)
   return true;
 }
 
