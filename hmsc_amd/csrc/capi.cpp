@@ -87,6 +87,8 @@ struct FaultDiagInstaller {
 namespace hmsc {
 
 static thread_local std::string g_last_error;
+// live chains per device in this process (build_state / free_state, under g_dev_mu)
+static std::map<int, int> g_live_chains;
 // Chains may live on concurrent host threads (sampleMcmc nParallel, one stream each).  A
 // stream capture must not overlap another thread's device-wide synchronising calls
 // (hipMalloc / hipFree / hipDeviceSynchronize): those would invalidate it.  Captures,
@@ -387,10 +389,18 @@ static int shard_range(int ns, int rank, int nranks, int* sp0, int* nsl) {
   return *nsl > 0 ? 0 : -1;
 }
 
+static int live_chains(int device) {
+  std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
+  auto it = g_live_chains.find(device);
+  return it == g_live_chains.end() ? 0 : it->second;
+}
+
 static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device, uint32_t mask, int rank,
                         int nranks, const void* comm_id, hmsc_allreduce_fn host_fn = nullptr,
                         void* host_ctx = nullptr) {
   std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
+  ++g_live_chains[device];
+  s.counted_live = true;
   HMSC_REQUIRE(m != nullptr, "model is NULL");
   HMSC_REQUIRE(m->struct_size == (int32_t)sizeof(hmsc_model),
                "hmsc_model.struct_size must be sizeof(hmsc_model) of include/hmsc_amd.h (rebuild the caller "
@@ -840,6 +850,8 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
 
 static void free_state(State& s) {
   std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
+  if (s.counted_live) --g_live_chains[s.device];
+  s.counted_live = false;
   DeviceGuard dg(s.device);
   (void)hipDeviceSynchronize();
   s.unpack_pool.reset();  // idle between runs; joined before the host ring goes
@@ -908,6 +920,15 @@ void join_side(State& s) {
 // (the Gamma2 / BetaLambda launch's gbl_sync[3]; the dense solver's error word, whose bits
 // name the wait, state.h HsErr).  A timed-out wait lets its launch drain on stale data, so a
 // run that saw one must fail, never return its samples.  Called with the streams idle.
+// zero the error words (not the handshake state): an error is reported by the one call that
+// saw it, and the chain can be read, reset with set_state / init_state and run again
+static void clear_device_errors(State& s) {
+  HIP_OK(hipMemsetAsync(s.dev_flags, 0, 3 * sizeof(int), s.stream));
+  HIP_OK(hipMemsetAsync(s.gbl_sync + 3, 0, sizeof(int), s.stream));
+  HIP_OK(hipMemsetAsync(s.trsv_sync + DENSE_SYNC_ERR, 0, sizeof(int), s.stream));
+  HIP_OK(hipStreamSynchronize(s.stream));
+}
+
 static void check_device_flags(State& s) {
   // one copy of the error block (build_state): dev_flags, gbl_sync, the dense handshake words
   int blk[20 + DENSE_SYNC_ERR + 1] = {0};
@@ -915,6 +936,7 @@ static void check_device_flags(State& s) {
   const int* flag = blk;
   const int* gsync = blk + 16;
   const int hs = blk[20 + DENSE_SYNC_ERR];
+  if (flag[0] || flag[1] || flag[2] || gsync[3] || hs) clear_device_errors(s);  // reported once
   if (hs != 0) {
     std::string what;
     if (hs & HS_ERR_TRSV_FLAG) what += " [sync-free triangular solve: a block flag never came up]";
@@ -977,6 +999,7 @@ static void set_state(State& s, const hmsc_params* p) {
   DeviceGuard dg(s.device);
   join_side(s);
   HIP_OK(hipStreamSynchronize(s.stream));
+  clear_device_errors(s);  // a new state: earlier failures are not its own
   // the device holds BL / Psi / Delta in the current layout (K, NF and the per-level row
   // offsets); read them in that layout, then remap every level's rows to the new nf (rows a
   // level gains: Lambda 0, Psi 1, Delta 1) before the supplied fields are applied
@@ -1342,7 +1365,8 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
   s.cap_segs = segs ? &parts : nullptr;
   try {
     const char* no_root = std::getenv("HMSC_NO_SIDE_ROOT");
-    if (s.side_fused && s.edge_free && !s.sharded && !(no_root && no_root[0] == '1')) {
+    s.edge_free_now = s.edge_free && live_chains(s.device) == 1;
+    if (s.side_fused && s.edge_free_now && !s.sharded && !(no_root && no_root[0] == '1')) {
       // the side stream forked at the graph's root: the first sweep's side work then waits for
       // the fused launch's tails flag on the device like the later sweeps', instead of behind a
       // graph edge from that launch (whose first replay sweep's side chain ended ~100 us late)
@@ -1370,6 +1394,7 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
     s.pack_req = s.pack_done = false;
     s.capturing = false;
     s.cap_segs = nullptr;
+    s.edge_free_now = false;
     (void)hipStreamEndCapture(s.stream, &g);
     if (g) (void)hipGraphDestroy(g);
     drop_parts();
@@ -1378,6 +1403,8 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
   }
   s.capturing = false;
   s.cap_segs = nullptr;
+  s.graph_edge_free = s.edge_free_now;
+  s.edge_free_now = false;
   HIP_OK(hipStreamEndCapture(s.stream, &g));
   const bool steady = xv == s.xeta_valid && zv == s.zt_valid && gv == s.g2prep_valid && gp == s.g_pending &&
                       g2v == s.g2s_valid;
@@ -1486,6 +1513,7 @@ static bool graphs_built(const State& s) {
 // the caller must run eagerly.
 static bool replay_sweeps(State& s, uint32_t iter, bool with_record, int n) {
   if (!s.use_graph || s.prof) return false;
+  if (graphs_built(s) && s.graph_edge_free && live_chains(s.device) > 1) s.graph_dirty = true;  // recapture with edges
   if (graphs_built(s) && (s.graph_dirty || s.graph_K != s.K || s.graph_NF != s.NF)) destroy_graph(s);
   if (s.graph_dirty) s.eager_streak = 0, s.graph_dirty = false;
   if (!graphs_built(s) && (s.eager_streak < 1 || !build_sweep_graphs(s, iter))) return false;  // steady first
@@ -2070,6 +2098,8 @@ int hmsc_init_state(hmsc_state* h, const int32_t* nf0) {
       }
     s.refresh_dims();
     HMSC_REQUIRE(s.K <= s.Kmax, "init: K = nc + sum(nf) exceeds this build's limit of 64");
+    join_side(s);
+    clear_device_errors(s);
     launch_init(s);
     const double one = 1.0;  // rho = 1 (R/computeInitialParameters.R:226)
     HIP_OK(hipMemcpyAsync(s.rho, &one, sizeof(double), hipMemcpyHostToDevice, s.stream));
@@ -2160,6 +2190,7 @@ int hmsc_prepare_graphs(hmsc_state* h, int32_t iter, int32_t* built) {
     DeviceGuard dg(s.device);
     *built = 0;
     if (!s.use_graph || s.prof) return;
+    if (graphs_built(s) && s.graph_edge_free && live_chains(s.device) > 1) s.graph_dirty = true;
     if (graphs_built(s) && (s.graph_dirty || s.graph_K != s.K || s.graph_NF != s.NF)) destroy_graph(s);
     if (!graphs_built(s)) {
       if (s.graph_dirty) s.eager_streak = 0, s.graph_dirty = false;

@@ -52,6 +52,25 @@ __device__ inline void kt_record(unsigned long long* kt, uint32_t iter, unsigned
   __hip_atomic_fetch_max(kt + KT_SLOTS + slot, t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Every bounded in-launch / cross-stream wait is bounded in wall-clock time: a wait that
+// outlasts HS_TIMEOUT_TICKS of the 100 MHz wall clock (1 s; a legitimate wait is microseconds)
+// gives up, the caller raises its error bit and carries on so the launch drains, and the host
+// fails the call after the sweep (capi.cpp check_device_flags).  A bound by spin count would
+// vary with load latency and clocks.
+constexpr unsigned long long HS_TIMEOUT_TICKS = 100000000ull;
+
+// poll done() with s_sleep(SLEEP) between tries until it holds (true) or the bound passes (false)
+template <int SLEEP, class F>
+__device__ __forceinline__ bool spin_until(F done) {
+  if (done()) return true;
+  const unsigned long long t0 = kt_now();
+  for (int spin = 1;; ++spin) {
+    __builtin_amdgcn_s_sleep(SLEEP);
+    if (done()) return true;
+    if ((spin & 63) == 0 && kt_now() - t0 > HS_TIMEOUT_TICKS) return false;
+  }
+}
+
 // A device-scope (L2-bypassing) load of a value another workgroup of the same launch, on
 // any XCD, published behind a flag: the reader polls the flag relaxed and then loads with
 // these, instead of an acquire fence that would invalidate its XCD's whole L2.

@@ -45,11 +45,10 @@ constexpr int DLD = DB + 1;  // padded LDS leading dimension
 
 // Every in-launch handshake of this file (the sync-free solve's block flags, the fused
 // panel's diagonal-inverse flag) is bounded in time: a wait that outlasts HS_TIMEOUT_TICKS of
-// the 100 MHz wall clock (1 s; a legitimate wait is microseconds) raises its bit in the sync
-// block's error word (DENSE_SYNC_ERR, state.h) and the workgroup carries on, so the launch
-// drains; the host reads that word after the sweep (capi.cpp check_device_flags) and fails
-// the call instead of returning a half-solved system.
-constexpr unsigned long long HS_TIMEOUT_TICKS = 100000000ull;
+// the 100 MHz wall clock (common.h) raises its bit in the sync block's error word
+// (DENSE_SYNC_ERR, state.h) and the workgroup carries on, so the launch drains; the host reads
+// that word after the sweep (capi.cpp check_device_flags) and fails the call instead of
+// returning a half-solved system.
 
 __device__ __forceinline__ void hs_raise(int* sync, int bit) {
   __hip_atomic_fetch_or(sync + DENSE_SYNC_ERR, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -316,13 +316,8 @@ __device__ __host__ inline int g2bl_epoch(uint32_t iter) { return (int)(iter | 0
 // and goes on.  Relaxed polls: the data behind the flags is read with load_coherent.
 __device__ __forceinline__ void side_wait(const int* flags, int n, int epoch, int* err) {
   for (int q = 0; q < n; ++q)
-    for (int spin = 0; __hip_atomic_load(&flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch; ++spin) {
-      if (spin > (1 << 20)) {
-        __hip_atomic_store(&err[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(8);
-    }
+    if (!spin_until<8>([&] { return __hip_atomic_load(&flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch; }))
+      __hip_atomic_store(&err[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // What the fused launch's tail (bl_tail) needs of a species' update, lane k holding row k:
@@ -435,13 +430,9 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
     // took the solves after the wait from 5 to 16 us; bounded: a broken handshake raises the
     // error flag (hmsc_run reports it) instead of hanging
     const int epoch = g2bl_epoch(SWEEP_ITER(a));
-    for (int spin = 0; __hip_atomic_load(&gsync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch; ++spin) {
-      if (spin > (1 << 20)) {
-        if (i == 0) __hip_atomic_store(&gsync[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(8);
-    }
+    if (!spin_until<8>([&] { return __hip_atomic_load(&gsync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch; }) &&
+        i == 0)
+      __hip_atomic_store(&gsync[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (blk == 0 && w == 0) HMSC_STAMP_RT(75);
     if (i < nc)
 #pragma unroll
@@ -1703,15 +1694,9 @@ __global__ __launch_bounds__(256) void gamma2_bl_kernel(G2BLArgs f) {
     if (threadIdx.x < 64) HMSC_STAMP_RT(70);
     // every partial is in (relaxed count; the partials are device-coherent stores, read with
     // device-coherent loads), bounded like every in-launch wait
-    if (threadIdx.x == 0) {
-      for (int spin = 0; __hip_atomic_load(&f.sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nparts; ++spin) {
-        if (spin > (1 << 20)) {
-          __hip_atomic_store(&f.sync[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-    }
+    if (threadIdx.x == 0 &&
+        !spin_until<2>([&] { return __hip_atomic_load(&f.sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nparts; }))
+      __hip_atomic_store(&f.sync[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (f.side_wait) {  // the previous sweep's GammaV (Gamma, iV) and Gamma2 prep (read coherently)
       const int ep = g2bl_epoch(SWEEP_ITER(f.g2) - 1);
       side_wait(f.side_sync, 1, ep, f.sync);
@@ -1836,7 +1821,7 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
   const bool tail_gv = sh || (!s.side_partials && crw_on && (s.mask & HMSC_UP_GAMMA2) && s.nt <= 8 &&
                               s.nc * s.nc + s.nc * s.nt + s.NF <= 1024 && s.gvt != nullptr);
   // graph sweeps after the first: the previous sweep's side chain is joined on the device
-  const bool dev_join = !sh && crw_on && s.edge_free && s.capturing && s.cap_sweep > 0 && s.side_tail;
+  const bool dev_join = !sh && crw_on && s.edge_free_now && s.capturing && s.cap_sweep > 0 && s.side_tail;
   // iV, Gamma2's prep, Psi and Delta come from the previous sweep's side updaters
   if (!dev_join) join_side(s);
   if (sh && !s.g2s_valid) shard_g2_stats(s);
@@ -2840,7 +2825,7 @@ void launch_side_fused(State& s, uint32_t iter) {
   // graph sweeps after the first: the side work is not forked by a graph edge; its first
   // launch waits on the device for the fused launch's tails flag (raised by the last reducer
   // of the tail, after every BetaLambda workgroup's stores), see State::cap_sweep
-  const bool dev_fork = cr_done && s.edge_free && s.capturing && (s.cap_sweep > 0 || s.side_root);
+  const bool dev_fork = cr_done && s.edge_free_now && s.capturing && (s.cap_sweep > 0 || s.side_root);
   if (!dev_fork) HIP_OK(hipEventRecord(s.ev_bl, s.stream));
   launch_eta_fused(s, iter, cr_done);
   if (!dev_fork) HIP_OK(hipStreamWaitEvent(s.side, s.ev_bl, 0));

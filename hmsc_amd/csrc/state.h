@@ -119,6 +119,13 @@ struct State {
   // launch's tails (gbl_sync[2]), and the next fused launch waits for its side_sync flags
   int cap_sweep = -1;
   bool edge_free = true;    // (HMSC_SIDE_EDGES=1: graph edges everywhere)
+  // edge_free for the capture in progress / the graphs held: only while this chain is the one
+  // live chain on its device in the process.  Device-side joins need the main and side streams
+  // on separate hardware queues; the streams of several chains (nParallel > 1 on one GPU) can
+  // share the few queues and wait on each other in a cycle, so their graphs keep
+  // graph edges, and graphs captured edge-free are rebuilt once a second chain appears.
+  bool edge_free_now = false, graph_edge_free = false;
+  bool counted_live = false;  // counted in capi.cpp's live chains of its device
   bool side_tail = false;   // the last side chain raises side_sync (the next fused launch may join it on the device)
   // the capture in progress forked the side stream at the graph's root, so its first sweep's
   // side work waits for the tails flag on the device too (no edge from the fused launch)

@@ -57,3 +57,20 @@ def test_conditional_prediction_repeatable(fits):
     p1 = np.stack(H.predict(hM, post=post, Yc=Yc, mcmcStep=3, expected=True, seed=11), axis=2)
     p2 = np.stack(H.predict(hM, post=post, Yc=Yc, mcmcStep=3, expected=True, seed=11), axis=2)
     np.testing.assert_array_equal(p1, p2)
+
+
+def test_two_chains_one_device_fused_path_with_graphs():
+    """with nParallel = 2 on one device the two chains' streams may share hardware
+    queues, so the device-side joins of edge-free sweep graphs could wait on each other in a
+    cycle.  A second live chain on the device makes every chain capture with graph edges
+    (capi.cpp live_chains): at a size where the fused BetaLambda launch fills the CUs (ns =
+    1000: 251 workgroups) and long enough for graph replays, both chains finish, and each equals
+    the same chain run alone."""
+    from hmsc_amd.workloads import synthetic_probit
+    hM = synthetic_probit(ny=2000, ns=1000, nc=6, nf=4)
+    fit2 = H.sampleMcmc(hM, samples=60, transient=10, thin=1, nChains=2, nParallel=2,
+                        updater={"GammaEta": False}, seed=9, verbose=0, alignPost=False)
+    hM1 = synthetic_probit(ny=2000, ns=1000, nc=6, nf=4)
+    fit1 = H.sampleMcmc(hM1, samples=60, transient=10, thin=1, nChains=2, nParallel=1,
+                        updater={"GammaEta": False}, seed=9, verbose=0, alignPost=False)
+    _same_post(fit2, fit1)

@@ -42,6 +42,9 @@ def test_poisoned_handshake_is_reported(what):
         ch.sync()
     assert "error -5" in str(ei.value)
     assert "not positive definite" not in str(ei.value)
+    # reported once: the error words are cleared, so the state can be read to diagnose it
+    st = ch.get_state(with_z=False)
+    assert np.all(np.isfinite(st["Gamma"]))
     ch.close()
 
 
