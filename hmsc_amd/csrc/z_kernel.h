@@ -6,6 +6,7 @@
 
 #include "common.h"
 #include "rng.h"
+#include "z_tables.h"
 
 namespace hmsc {
 
@@ -60,6 +61,7 @@ struct ZArgs {
   const double* gred_XX;
   double* gred_G;
   const double* logtab;  // z_log_table (ZLOG_N x ZLOG_W doubles), staged in LDS by every workgroup
+  const double* ztab;    // z_draw_tables (ZT_DOUBLES: erfcx | F(w) | 2^(k/64)), staged in LDS likewise
 };
 
 constexpr int ZT_I = 64;   // sites per workgroup tile (4 waves x 16)
@@ -151,6 +153,118 @@ __device__ __forceinline__ double log_tab(double x, const double* tab) {
 struct ZPair {
   double z0, z1;
 };
+
+// ---------------------------------------------------------------------------------------------
+// The LDS-table draw (round 5).  The same inversion, z = e - sd sg Phi^-1(u Phic(alpha)), with
+// every special function a table lookup plus a low-degree polynomial (scripts/fit_tables.py,
+// z_tables.h; coefficients staged in LDS, read as 16-byte pairs):
+//   Phic(alpha)  = erfc(a) / 2 (alpha >= 0) or 1 - erfc(a) / 2, a = |alpha| / sqrt 2, with
+//                  erfc(a) = exp(-a^2) erfcx(a): erfcx on 72 segments of width 1/4 (degree 9,
+//                  1.1e-14 relative), exp(-a^2) with a^2 split exactly (hi + lo) and exp by the
+//                  2^(k/64) table and a degree-5 polynomial (|r| <= ln2 / 128: 4e-17)
+//   w            = -log(4 p (1 - p))  (log_tab, as before)
+//   Phi^-1(p)    = (2p - 1) F(w), F on 64 segments of width 1/4 over w in [0, 16) (degree 7,
+//                  3.3e-15) -- one branch for all p in (2.8e-8, 1 - 2.8e-8), where the previous
+//                  global fits switched to a second polynomial (and a sqrt) at w = 6.25 in a
+//                  third of the wave iterations; AS241's tail beyond, as before
+// replacing the degree-20 erfc polynomial with its reciprocal and exp, and the degree-18 / 14
+// quantile polynomials (~45 fewer VALU instructions per cell, no region-B divergence).
+// Row strides (doubles): rows start 16-byte aligned and their LDS banks (4-dword quads,
+// bank = dword mod 64) differ for rows j, j' unless j = j' (mod 16) -- a stride of 20 dwords; an
+// 8-coefficient row at its natural 16 dwords put rows j, j + 4, j + 8, ... of the quantile
+// table on the same quad, a 4-way conflict among the lanes of a 16-lane group
+#ifndef ZT_Q_LD_DEF
+#define ZT_Q_LD_DEF 10
+#endif
+constexpr int ZT_E_LD = 10, ZT_Q_LD = ZT_Q_LD_DEF;
+constexpr int ZT_E_SEG = ZT_E_MAX * ZT_E_PER_UNIT, ZT_Q_SEG = ZT_Q_MAX * ZT_Q_PER_UNIT;
+constexpr int ZT_OFF_E = 0, ZT_OFF_Q = ZT_E_SEG * ZT_E_LD, ZT_OFF_X = ZT_OFF_Q + ZT_Q_SEG * ZT_Q_LD;
+constexpr int ZT_DOUBLES = ZT_OFF_X + 64;
+static_assert(ZT_E_NC % 2 == 0 && ZT_Q_NC % 2 == 0 && ZT_E_LD % 2 == 0 && ZT_Q_LD % 2 == 0 && ZT_E_LD >= ZT_E_NC &&
+                  ZT_Q_LD >= ZT_Q_NC,
+              "16-byte rows");
+inline void z_draw_tables(double* t) {
+  for (int i = 0; i < ZT_DOUBLES; ++i) t[i] = 0.0;
+  for (int j = 0; j < ZT_E_SEG; ++j)
+    for (int k = 0; k < ZT_E_NC; ++k) t[ZT_OFF_E + ZT_E_LD * j + k] = kZtErfcx[ZT_E_NC * j + k];
+  for (int j = 0; j < ZT_Q_SEG; ++j)
+    for (int k = 0; k < ZT_Q_NC; ++k) t[ZT_OFF_Q + ZT_Q_LD * j + k] = kZtQnormF[ZT_Q_NC * j + k];
+  for (int i = 0; i < 64; ++i) t[ZT_OFF_X + i] = kZtExp2[i];
+}
+typedef double zt_d2 __attribute__((ext_vector_type(2)));
+
+// polynomial of table row `row` (NC coefficients, highest first, 16-byte aligned) at d
+template <int NC>
+__device__ __forceinline__ double zt_poly(const double* row, double d) {
+  const zt_d2* r2 = (const zt_d2*)row;
+  zt_d2 c[NC / 2];
+#pragma unroll
+  for (int k = 0; k < NC / 2; ++k) c[k] = r2[k];  // ds_read_b128, all issued before the chain
+  double v = c[0][0];
+  v = fma(v, d, c[0][1]);
+#pragma unroll
+  for (int k = 1; k < NC / 2; ++k) {
+    v = fma(v, d, c[k][0]);
+    v = fma(v, d, c[k][1]);
+  }
+  return v;
+}
+
+HMSC_TABLE double kZtExpPoly[6] = {1.0 / 120.0, 1.0 / 24.0, 1.0 / 6.0, 0.5, 1.0, 1.0};
+// erfc(a) for 0 <= a < ZT_E_MAX (the caller clamps a)
+__device__ __forceinline__ double zt_erfc(double a, const double* zt) {
+  const int j = min((int)(a * (double)ZT_E_PER_UNIT), ZT_E_SEG - 1);
+  const double d = a - ((double)j + 0.5) * (1.0 / ZT_E_PER_UNIT);
+  const double cx = zt_poly<ZT_E_NC>(zt + ZT_OFF_E + ZT_E_LD * j, d);
+  // exp(-(hi + lo)), a^2 = hi + lo exactly: k = rint(-hi 64 / ln2), r = -hi - k ln2 / 64 - lo
+  const double hi = a * a, lo = fma(a, a, -hi);
+  const double kf = __builtin_rint(hi * -92.33248261689366);  // 64 / ln2
+  double r = fma(kf, -0.01083042469326756, -hi);              // ln2 / 64 = hi (fdlibm's ln2_hi / 64: k hi exact)
+  r = fma(kf, -2.9815858269852933e-12, r) - lo;               //            + lo
+  double p = kZtExpPoly[0];
+#pragma unroll
+  for (int k = 1; k < 6; ++k) p = fma_sc(p, r, kZtExpPoly[k]);
+  const int ki = (int)kf;
+  return __builtin_ldexp(p * zt[ZT_OFF_X + (ki & 63)], ki >> 6) * cx;
+}
+
+// (2p - 1) F(w) = Phi^-1(p) for w = -log(4 p (1 - p)) < ZT_Q_MAX
+__device__ __forceinline__ double zt_qnorm_w(double p, double w, const double* zt) {
+  const int j = max(0, min((int)(w * (double)ZT_Q_PER_UNIT), ZT_Q_SEG - 1));
+  const double d = w - ((double)j + 0.5) * (1.0 / ZT_Q_PER_UNIT);
+  return (2.0 * p - 1.0) * zt_poly<ZT_Q_NC>(zt + ZT_OFF_Q + ZT_Q_LD * j, d);
+}
+
+__device__ __forceinline__ ZPair z_probit_pair_tab(double e0, double e1, double sd0, double sd1, double isd0,
+                                                double isd1, int c0, int c1, double u0, double u1, int noise_zero,
+                                                const double* ltab, const double* zt) {
+  const double sg0 = c0 == 0 ? -1.0 : 1.0, sg1 = c1 == 0 ? -1.0 : 1.0;
+  const double al0 = c0 < 0 ? -INFINITY : -sg0 * e0 * isd0;
+  const double al1 = c1 < 0 ? -INFINITY : -sg1 * e1 * isd1;
+  double q0, q1;  // -Phic^-1 (u Phic(alpha)) = qnorm(p), z = e - sd sg q
+  if (al0 > 25.0 || al1 > 25.0) {  // deep tail of either cell: each cell by the scalar inversion
+    q0 = -trunc_normal_lower(al0, u0);
+    q1 = -trunc_normal_lower(al1, u1);
+  } else {
+    // a >= 17.99 only for alpha < -25.4, where Phic(alpha) = 1 - erfc(a) / 2 rounds to 1
+    const double a0 = fmin(fabs(al0) * 0.7071067811865476, 17.99);
+    const double a1 = fmin(fabs(al1) * 0.7071067811865476, 17.99);
+    const double r0 = 0.5 * zt_erfc(a0, zt), r1 = 0.5 * zt_erfc(a1, zt);
+    const double p0 = u0 * (al0 < 0.0 ? 1.0 - r0 : r0);
+    const double p1 = u1 * (al1 < 0.0 ? 1.0 - r1 : r1);
+    const double w0 = -log_tab(4.0 * p0 * (1.0 - p0), ltab), w1 = -log_tab(4.0 * p1 * (1.0 - p1), ltab);
+    q0 = zt_qnorm_w(p0, w0, zt);
+    q1 = zt_qnorm_w(p1, w1, zt);
+    if (w0 >= (double)ZT_Q_MAX || w1 >= (double)ZT_Q_MAX) {  // p < 2.8e-8 or > 1 - 2.8e-8: AS241's tail
+      if (w0 >= (double)ZT_Q_MAX) q0 = qnorm_as241_tail_t(p0, kLogSeries);
+      if (w1 >= (double)ZT_Q_MAX) q1 = qnorm_as241_tail_t(p1, kLogSeries);
+    }
+  }
+  ZPair z;
+  z.z0 = (c0 < 0 && noise_zero) ? e0 : e0 - sd0 * sg0 * q0;
+  z.z1 = (c1 < 0 && noise_zero) ? e1 : e1 - sd1 * sg1 * q1;
+  return z;
+}
 __device__ __forceinline__ ZPair z_probit_pair(double e0, double e1, double sd0, double sd1, double isd0, double isd1,
                                             int c0, int c1, double u0, double u1, int noise_zero,
                                             const double* ltab) {
@@ -295,11 +409,12 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
   double* sIsd = sSd + ZT_J;                        // [32] iSigma^1/2
   int* sFam = (int*)(sIsd + ZT_J);                  // [32]
   double* sLog = (double*)(sFam + ZT_J);            // [ZLOG_N][ZLOG_W] log table (log_tab)
+  double* sZT = sLog + ZLOG_W * ZLOG_N;              // z_draw_tables (16-byte aligned rows)
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, lm = lane & 15, lk = lane >> 4;
   // the Philox sweep counter, read once (a load inside the site loop would wait, vmcnt(0),
   // behind every Z store in flight)
   const uint32_t iter = SWEEP_ITER(a);
-  double* sT = sLog + ZLOG_W * ZLOG_N + w * (ZT_J * ZT_TLD);  // this wave's tile: E, then Z
+  double* sT = sZT + ZT_DOUBLES + w * (ZT_J * ZT_TLD);  // this wave's tile: E, then Z
   const int j0 = by * ZT_J;
   for (int p = t; p < K16 * ZT_J; p += 256) {
     const int k = p >> 5, jj = p & 31, j = j0 + jj;
@@ -316,8 +431,10 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
     sIsd[t] = sqrt(is);
     sFam[t] = (j < a.ns_loc) ? a.fam[j] : 0;
   }
-  if (DRAW && (MODE & 2))
+  if (DRAW && (MODE & 2)) {
     for (int p = t; p < ZLOG_W * ZLOG_N; p += 256) sLog[p] = a.logtab[p];
+    for (int p = t; p < ZT_DOUBLES; p += 256) sZT[p] = a.ztab[p];
+  }
   __syncthreads();
 
   d4 acc[NKB][2];
@@ -367,10 +484,7 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
     //      one Philox call per (site, pair); Z stores are 128-B site runs
     {
       const int s = lm, i = i0 + s;
-#ifndef Z_CUNROLL
-#define Z_CUNROLL 1
-#endif
-#pragma unroll Z_CUNROLL
+#pragma unroll 1
       for (int c = 0; c < 4; ++c) {
         const int m = 4 * c + lk, ja = j0 + 2 * m;
         Uniform2 u{0.0, 0.0};
@@ -382,7 +496,8 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
           const int jj0 = 2 * m, jj1 = 2 * m + 1;
           const bool in0 = i < ny && ja < a.ns_loc, in1 = i < ny && ja + 1 < a.ns_loc;
           const double e0 = sT[jj0 * ZT_TLD + s], e1 = sT[jj1 * ZT_TLD + s];
-          const ZPair zp = z_probit_pair(e0, e1, sSd[jj0], sSd[jj1], sIsd[jj0], sIsd[jj1], cd0, cd1, u.a, u.b, a.noise_zero, sLog);
+          const ZPair zp = z_probit_pair_tab(e0, e1, sSd[jj0], sSd[jj1], sIsd[jj0], sIsd[jj1], cd0, cd1, u.a, u.b,
+                                             a.noise_zero, sLog, sZT);
           double z0 = zp.z0, z1 = zp.z1;
           if (NORMAL) {  // R/updateZ.R:40-41
             if (sFam[jj0] == 1 && cd0 >= 0 && in0) z0 = a.Yval[(size_t)i + (size_t)ny * ja];
@@ -507,7 +622,7 @@ inline int z_nkb(int K) { return (K + 15) / 16; }
 
 inline size_t z_smem_bytes(int K, int nt) {
   const size_t K16 = 16 * (size_t)z_nkb(K);
-  const size_t body = K16 * ZT_J + (size_t)ZT_J * nt + 2 * ZT_J + ZT_J / 2 + ZLOG_W * (size_t)ZLOG_N +
+  const size_t body = K16 * ZT_J + (size_t)ZT_J * nt + 2 * ZT_J + ZT_J / 2 + ZLOG_W * (size_t)ZLOG_N + ZT_DOUBLES +
                       4 * (size_t)ZT_J * ZT_TLD;  // doubles
   const size_t red = 3 * K16 * ZT_J;                                                                   // wave combine
   return (body > red ? body : red) * sizeof(double);

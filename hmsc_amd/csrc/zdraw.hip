@@ -80,6 +80,7 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   a.Ycode = s.Ycode;
   a.Ybits = s.Ybits;
   a.logtab = s.logtab;
+  a.ztab = s.logtab + ZLOG_W * ZLOG_N;
   a.Yval = use_raw_y ? s.Yraw : s.Yval;
   a.fam = s.fam;
   a.Tr = s.Tr;
@@ -139,8 +140,12 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   }
 }
 
-int z_log_table_doubles() { return ZLOG_W * ZLOG_N; }
-void z_log_table_fill(double* t) { z_log_table(t); }
+// the z kernel's tables in one device buffer: the log table, then z_draw_tables
+int z_log_table_doubles() { return ZLOG_W * ZLOG_N + ZT_DOUBLES; }
+void z_log_table_fill(double* t) {
+  z_log_table(t);
+  z_draw_tables(t + ZLOG_W * ZLOG_N);
+}
 
 void launch_update_z(State& s, uint32_t iter, bool use_raw_y) {
   run_z_fused(s, true, iter, use_raw_y);
