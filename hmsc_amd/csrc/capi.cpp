@@ -487,16 +487,18 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
     L.b2 = m->b2[r];
     sum_nfmax += L.nfmax;
   }
-  // K = nc + sum(nf) <= 64 is this build's kernel limit (one wave per species row set in
-  // updateBetaLambda, 16-row MFMA blocks of updateZ).  R's default nfMax = Inf becomes ns
-  // (R/Hmsc.R:554), so a default model with many species asks for more factors than the
-  // device holds: every level's buffers and record slots then hold nfcap = min(nfMax, 64 - nc
-  // - the other levels' nfMin) factors (hmsc_get_nf_cap; the Python wrapper warns), and the
-  // chain stops with an explicit error only if updateNf actually has to grow a level past it
-  // (MGP shrinkage keeps the adapted nf far below that in practice).
-  HMSC_REQUIRE(nc + [&] { int v = 0; for (int r = 0; r < s.nr; ++r) v += s.lev[r].nfmin; return v; }() <= 64,
-               "nc + sum(nfMin) exceeds 64: this build's limit is K = nc + sum(nf) <= 64");
-  s.Kmax = std::min(nc + sum_nfmax, 64);
+  // K = nc + sum(nf) <= HMSC_KCAP (128) is this build's kernel limit (16-row MFMA blocks of
+  // updateZ, NKB <= 8; K x K factors in LDS).  R's default nfMax = Inf becomes ns
+  // (R/Hmsc.R:554), so a default model with many species may ask for more factors than the
+  // device holds: every level's buffers and record slots then hold nfcap = min(nfMax, 128 - nc
+  // - the other levels' nfMin) factors (hmsc_get_nf_cap; the Python wrapper warns, or refuses
+  // with nf_capacity="error"), and the chain stops with an explicit error only if updateNf
+  // actually has to grow a level past it (MGP shrinkage keeps the adapted nf far below that in
+  // practice).  The capacity beyond every level's nfMin is shared: a level may be refused below
+  // its nfcap when the other levels have already grown into it (K would pass Kmax).
+  HMSC_REQUIRE(nc + [&] { int v = 0; for (int r = 0; r < s.nr; ++r) v += s.lev[r].nfmin; return v; }() <= HMSC_KCAP,
+               "nc + sum(nfMin) exceeds 128: this build's limit is K = nc + sum(nf) <= 128");
+  s.Kmax = std::min(nc + sum_nfmax, HMSC_KCAP);
   s.NFmax = s.Kmax - nc;
   s.refresh_dims();
   for (int r = 0; r < s.nr; ++r) {
@@ -749,7 +751,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   const int n_sblk = (ny + 63) / 64;
   s.zl_split = std::max(1, std::min(std::min(16, (nsl + 3) / 4), (640 + n_sblk - 1) / n_sblk));
   s.XZ = dalloc<double>((size_t)s.Kmax * nsl);
-  s.XEta = dalloc<double>((size_t)ny * 16 * ((s.Kmax + 15) / 16) + 64);  // padded (z_kernel.h ZArgs)
+  s.XEta = dalloc<double>((size_t)ny * z_xeta_cols_for(s.Kmax) + 64);  // padded (z_kernel.h ZArgs)
   s.G = dalloc<double>((size_t)s.Kmax * s.Kmax);
   s.ZTr = dalloc<double>((size_t)ny * nt);
   s.XZ_part = dalloc<double>((size_t)s.nchunk * s.Kmax * nsl);
@@ -1018,7 +1020,7 @@ static void set_state(State& s, const hmsc_params* p) {
     }
   }
   s.refresh_dims();
-  HMSC_REQUIRE(s.K <= s.Kmax, "set_state: K = nc + sum(nf) exceeds this build's limit of 64");
+  HMSC_REQUIRE(s.K <= s.Kmax, "set_state: K = nc + sum(nf) exceeds the chain's capacity (<= 128)");
   const int K = s.K;
   std::vector<double> BL((size_t)K * nsl, 0.0), Psi((size_t)std::max(1, s.NF) * nsl, 1.0), Delta(std::max(1, s.NF), 1.0);
   for (int j = 0; j < nsl; ++j)
@@ -1119,7 +1121,7 @@ static void update_nf(State& s, int r, uint32_t iter) {
     if (nf + 1 > nfcap || s.K + 1 > s.Kmax)
       throw HmscError(-6, "updateNf: level " + std::to_string(r + 1) + " needs " + std::to_string(nf + 1) +
                               " latent factors at iteration " + std::to_string(iter) + ", but this build holds at most " +
-                              std::to_string(nfcap) + " for it (K = nc + sum(nf) <= 64); set nfMax <= " +
+                              std::to_string(nfcap) + " for it (K = nc + sum(nf) <= 128); set nfMax <= " +
                               std::to_string(nfcap) + " with setPriors (or fewer covariates) to run this model");
     const int K2 = K + 1, NF2 = s.NF + 1;
     std::vector<double> BL2((size_t)K2 * nsl), Psi2((size_t)NF2 * nsl), Delta2(NF2);
@@ -2097,7 +2099,7 @@ int hmsc_init_state(hmsc_state* h, const int32_t* nf0) {
         s.lev[r].nf = nf0[r];
       }
     s.refresh_dims();
-    HMSC_REQUIRE(s.K <= s.Kmax, "init: K = nc + sum(nf) exceeds this build's limit of 64");
+    HMSC_REQUIRE(s.K <= s.Kmax, "init: K = nc + sum(nf) exceeds the chain's capacity (<= 128)");
     join_side(s);
     clear_device_errors(s);
     launch_init(s);

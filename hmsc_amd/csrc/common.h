@@ -10,6 +10,8 @@ namespace hmsc {
 
 // largest alphapw grid (nrow(rL$alphapw); R's default has 101 points) the device takes
 constexpr int HMSC_MAX_ALPHA = 2048;
+// K = nc + sum(nf): the latent dimensions a chain may hold (z kernel NKB <= 8, LDS factors)
+constexpr int HMSC_KCAP = 128;
 
 struct HmscError : std::runtime_error {
   int code;

@@ -1213,7 +1213,7 @@ void launch_gamma_eta(State& s, uint32_t iter) {
     a.nf = s.lev[r].nf;
     a.np = s.lev[r].np;
     a.loff = s.loff(r);
-    HMSC_REQUIRE(a.nf <= GE_NF_LARGE, "updateGammaEta: nf must be <= 64 (K = nc + sum nf <= 64)");
+    HMSC_REQUIRE(a.nf <= GE_NF_LARGE, "updateGammaEta: a level's nf must be <= 64 in this build");
     for (int q = 0; q < s.nr; ++q) {
       a.lev_np[q] = s.lev[q].np;
       a.lev_nf[q] = s.lev[q].nf;

@@ -1403,8 +1403,8 @@ __device__ __forceinline__ void q_inv_factor_nf(const double* qm, int ld, int nf
 }
 
 template <int NFB>
-__device__ __forceinline__ void crw_finish(const CRWArgs& a, const double* sCR, double* scratch) {
-  q_inv_factor<NFB>(sCR + a.nc * 16, 16, a.nf, a.W, 16, 16, scratch);
+__device__ __forceinline__ void crw_finish(const CRWArgs& a, const double* sCR, double* W, double* scratch) {
+  q_inv_factor<NFB>(sCR + a.nc * 16, 16, a.nf, W, 16, 16, scratch);
 }
 
 // The tail of a BetaLambda workgroup of the fused launch (K <= 32, nf <= 16), with the
@@ -1440,7 +1440,189 @@ struct BLTailArgs {
   // ar_gv (ar_b's [GV | RS] sections, the all-reduce's input) and leaves W to the Eta solve
   // (Q = I + Lambda diag(iSigma) Lambda^T is a sum over every rank's species)
   double* ar_gv;
+  // sweep graphs after the first, edge-free: the fused Eta launch runs the last reduction level
+  // (defer 1: this launch ends after the group reducers) or both (defer 2: it ends after the
+  // workgroups' tiles) in its leading workgroups
+  int defer;
 };
+
+// Level 1 of the tail's reduction: group g's tiles (workgroups g0 .. g0 + gn - 1) summed in
+// workgroup order into group tile nbl + g (write-through), with the bodies' timing words.
+// src_coh / dst_coh: the workgroup tiles / the group tile cross workgroups of one launch
+// (device-scope loads / write-through stores), else a launch boundary (plain).
+__device__ __forceinline__ void tail_group_sum(const BLTailArgs& ta, int g, int nbl, bool src_coh, bool dst_coh) {
+  const CRWArgs& a = ta.crw;
+  const int t = threadIdx.x, nc = a.nc, nf = a.nf;
+  const int g0 = g * CRW_GROUP, gn = min(CRW_GROUP, nbl - g0);
+  const int ngv = nc * nc + nc * ta.nt + ta.NF, ne = nf * 32;
+  double* P = a.part;
+  double* V = ta.gvt;
+  const int ld = ta.gvt_ld;
+  auto put = [&](double* p, double v) {
+    if (dst_coh)
+      store_coherent(p, v);
+    else
+      *p = v;
+  };
+  auto get = [&](const double* p) { return src_coh ? load_coherent(p) : *p; };
+  if (g == 0 && t < 64) HMSC_STAMP_RT(78);
+  // group reducer: the group's tiles in workgroup order.  Every load of a thread (two elements
+  // x the group's tiles, and the timing words on threads 254 / 255) is issued before the first
+  // sum, so a pass costs one memory latency (a load-use loop pays one per tile)
+  const int ntot = ne + (ta.gv_on ? ngv : 0);
+  const bool kt_thr = ta.kt_bl && t >= 254;  // timing words 512 (min) / 513 (max)
+  double ktx[CRW_GROUP];
+  if (kt_thr)
+#pragma unroll
+    for (int u = 0; u < CRW_GROUP; ++u)
+      ktx[u] = u < gn ? get(P + (size_t)(g0 + u) * CRW_TILE + 512 + (t - 254)) : (t == 254 ? 1e300 : 0.0);
+  for (int q0 = 0; q0 < ntot; q0 += 512) {
+    double x[2][CRW_GROUP];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int q = q0 + t + 256 * e;
+      const bool cr = q < ne;
+      const double* src = cr ? P + q : V + (q - ne);
+      const size_t st = cr ? CRW_TILE : ld;
+#pragma unroll
+      for (int u = 0; u < CRW_GROUP; ++u)
+        x[e][u] = (q < ntot && u < gn) ? get(src + (size_t)(g0 + u) * st) : 0.0;
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int q = q0 + t + 256 * e;
+      if (q >= ntot) continue;
+      const bool cr = q < ne;
+      double v = 0.0;
+#pragma unroll
+      for (int u = 0; u < CRW_GROUP; ++u) v += x[e][u];
+      put((cr ? P + q : V + (q - ne)) + (size_t)(nbl + g) * (cr ? CRW_TILE : ld), v);
+    }
+  }
+  if (kt_thr) {
+    double m = ktx[0];
+#pragma unroll
+    for (int u = 1; u < CRW_GROUP; ++u) m = t == 254 ? fmin(m, ktx[u]) : fmax(m, ktx[u]);
+    put(P + (size_t)(nbl + g) * CRW_TILE + 512 + (t - 254), m);
+  }
+}
+
+// Level 2 (the last group through): CR = the group tiles in group order, W = L^-1 of Q, the
+// sharded chain's GammaV / psi sums.  tails_flag is raised once every group tile is in, or
+// (defer, in the Eta launch) once CR and W are out, since the Eta launch's tile workgroups
+// read them behind it.
+// grp_coh: the group tiles were written in this launch (device-scope loads), else in the
+// previous one.
+__device__ __forceinline__ void tail_final(const BLTailArgs& ta, int nbl, uint32_t iter, double* smem, bool defer,
+                                           bool grp_coh) {
+  const CRWArgs& a = ta.crw;
+  const int t = threadIdx.x, w = t >> 6, K = a.K, nc = a.nc, nf = a.nf;
+  const int ng = (nbl + CRW_GROUP - 1) / CRW_GROUP;
+  const int ngv = nc * nc + nc * ta.nt + ta.NF;
+  double* P = a.part;
+  double* V = ta.gvt;
+  const int ld = ta.gvt_ld;
+  auto get = [&](const double* p) { return grp_coh ? load_coherent(p) : *p; };
+  const unsigned long long kt0 = ta.kt ? kt_now() : 0ull;
+  // every group tile is in: the side chain may start (it sums the GammaV / psi group tiles)
+  if (t < 64) HMSC_STAMP_RT(79);
+  if (t == 0) {
+    __hip_atomic_store(&a.ticket[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // every BetaLambda column and tile is out: the side work (post_bl_kernel, or the side
+    // chain reading the tail's GammaV / psi group tiles) may start
+    if (ta.tails_flag && !defer)
+      __hip_atomic_store(ta.tails_flag, g2bl_epoch(iter), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  double* sCR = smem + 4 * CRW_TILE;  // [row k][16]
+  {
+    // CR = the group tiles summed in group order; each thread's two elements' loads of a
+    // chunk of groups issued together
+    double v[2] = {0.0, 0.0};
+    for (int q0 = 0; q0 < ng; q0 += CRW_GROUP) {
+      double x[2][CRW_GROUP];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int q = t + 256 * e, h = q >> 5;
+#pragma unroll
+        for (int u = 0; u < CRW_GROUP; ++u)
+          x[e][u] = (h < nf && q0 + u < ng) ? get(P + (size_t)(nbl + q0 + u) * CRW_TILE + q) : 0.0;
+      }
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int u = 0; u < CRW_GROUP; ++u) v[e] += x[e][u];
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int q = t + 256 * e, h = q >> 5, k = q & 31;
+      sCR[k * 16 + h] = v[e];
+      if (h < nf && k < K) {
+        double* d = a.CR + k + (size_t)a.ldcr * h;
+        if (defer)
+          store_coherent(d, v[e]);
+        else
+          *d = v[e];
+      }
+    }
+  }
+  if (ta.ar_gv && ta.gv_on)  // (sharded) the GammaV / psi sums of this rank's species, group order
+    for (int q = t; q < ngv; q += 256) {
+      double v = 0.0;
+      for (int q0 = 0; q0 < ng; q0 += CRW_GROUP) {
+        double x[CRW_GROUP];
+#pragma unroll
+        for (int u = 0; u < CRW_GROUP; ++u) x[u] = q0 + u < ng ? get(V + (size_t)(nbl + q0 + u) * ld + q) : 0.0;
+#pragma unroll
+        for (int u = 0; u < CRW_GROUP; ++u) v += x[u];
+      }
+      ta.ar_gv[q] = v;
+    }
+  __syncthreads();
+  if (t < 64) HMSC_STAMP_RT(88);
+  // (deferred: W is formed in LDS and published write-through with CR behind tails_flag, which
+  // the Eta launch's tile workgroups wait on before their solves)
+  double* wdst = defer ? sCR + 32 * 16 : a.W;
+  if (w == 0 && !ta.ar_gv) {
+    if (nf <= 8)
+      crw_finish<8>(a, sCR, wdst, smem);
+    else if (nf <= 10)
+      crw_finish<10>(a, sCR, wdst, smem);
+    else if (nf <= 12)
+      crw_finish<12>(a, sCR, wdst, smem);
+    else
+      crw_finish<16>(a, sCR, wdst, smem);
+  }
+  if (defer) {
+    __syncthreads();
+    store_coherent(a.W + t, wdst[t]);  // 16 x 16, one element per thread
+    vm_stores_done();
+    __syncthreads();
+    if (t == 0 && ta.tails_flag)
+      __hip_atomic_store(ta.tails_flag, g2bl_epoch(iter), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (w == 0) HMSC_STAMP_RT(80);
+  if (ta.kt && t == 0) kt_record(ta.kt, iter, kt0);
+  if (ta.kt_bl && t == 64) {  // the BetaLambda bodies' first start / last end, once (wave 1, beside wave 0's factor)
+    double m0 = 1e300, m1 = 0.0;
+    for (int q0 = 0; q0 < ng; q0 += CRW_GROUP) {
+      double x0[CRW_GROUP], x1[CRW_GROUP];
+#pragma unroll
+      for (int u = 0; u < CRW_GROUP; ++u) {
+        const double* p = P + (size_t)(nbl + (q0 + u < ng ? q0 + u : q0)) * CRW_TILE + 512;
+        x0[u] = get(p);
+        x1[u] = get(p + 1);
+      }
+#pragma unroll
+      for (int u = 0; u < CRW_GROUP; ++u) {
+        m0 = fmin(m0, x0[u]);
+        m1 = fmax(m1, x1[u]);
+      }
+    }
+    const uint32_t slot = iter & (KT_SLOTS - 1);
+    __hip_atomic_fetch_min(ta.kt_bl + slot, (unsigned long long)m0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_max(ta.kt_bl + KT_SLOTS + slot, (unsigned long long)m1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 
 __device__ __forceinline__ void bl_tail(const BLTailArgs& ta, const BLCol& col, int b, int nbl, uint32_t iter,
                                         double* smem) {
@@ -1513,8 +1695,14 @@ __device__ __forceinline__ void bl_tail(const BLTailArgs& ta, const BLCol& col, 
   double* V = ta.gvt;
   const int ld = ta.gvt_ld;
   // (plain stores + one L2 write-back per workgroup before the ticket measured 3 % slower per
-  // sweep than these write-through stores)
-  auto put = [&](double* p, double v) { store_coherent(p, v); };
+  // sweep than these write-through stores; defer 2: the tiles are read in the next launch)
+  const int defer = ta.defer;
+  auto put = [&](double* p, double v) {
+    if (defer == 2)
+      *p = v;
+    else
+      store_coherent(p, v);
+  };
   for (int q = t; q < ne; q += 256)
     put(P + (size_t)b * CRW_TILE + q, (sC[q] + sC[CRW_TILE + q]) + (sC[2 * CRW_TILE + q] + sC[3 * CRW_TILE + q]));
   if (ta.kt_bl && t < 2) {  // the workgroup's first body start / last body end
@@ -1525,142 +1713,25 @@ __device__ __forceinline__ void bl_tail(const BLTailArgs& ta, const BLCol& col, 
   if (ta.gv_on)
     for (int q = t; q < ngv; q += 256)
       put(V + (size_t)b * ld + q, (sV[q] + sV[ngv + q]) + (sV[2 * ngv + q] + sV[3 * ngv + q]));
+  if (defer == 2) return;  // both reduction levels run in the Eta launch's leading workgroups
   vm_stores_done();
   __syncthreads();
   if (b == 0 && t < 64) HMSC_STAMP_RT(86);
-  const int g = b / CRW_GROUP, g0 = g * CRW_GROUP, gn = min(CRW_GROUP, nbl - g0);
+  const int g = b / CRW_GROUP, gn = min(CRW_GROUP, nbl - g * CRW_GROUP);
   const int ng = (nbl + CRW_GROUP - 1) / CRW_GROUP;
   if (t == 0) s_last = __hip_atomic_fetch_add(&a.ticket[2 + g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gn - 1;
   __syncthreads();
   if (!s_last) return;
-  if (g == 0 && t < 64) HMSC_STAMP_RT(78);
-  // group reducer: the group's tiles in workgroup order.  Every load of a thread (two elements
-  // x the group's tiles, and the timing words on threads 254 / 255) is issued before the first
-  // sum, so a pass costs one memory latency (a load-use loop pays one per tile)
-  const int ntot = ne + (ta.gv_on ? ngv : 0);
-  const bool kt_thr = ta.kt_bl && t >= 254;  // timing words 512 (min) / 513 (max)
-  double ktx[CRW_GROUP];
-  if (kt_thr)
-#pragma unroll
-    for (int u = 0; u < CRW_GROUP; ++u)
-      ktx[u] = u < gn ? load_coherent(P + (size_t)(g0 + u) * CRW_TILE + 512 + (t - 254)) : (t == 254 ? 1e300 : 0.0);
-  for (int q0 = 0; q0 < ntot; q0 += 512) {
-    double x[2][CRW_GROUP];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int q = q0 + t + 256 * e;
-      const bool cr = q < ne;
-      const double* src = cr ? P + q : V + (q - ne);
-      const size_t st = cr ? CRW_TILE : ld;
-#pragma unroll
-      for (int u = 0; u < CRW_GROUP; ++u)
-        x[e][u] = (q < ntot && u < gn) ? load_coherent(src + (size_t)(g0 + u) * st) : 0.0;
-    }
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int q = q0 + t + 256 * e;
-      if (q >= ntot) continue;
-      const bool cr = q < ne;
-      double v = 0.0;
-#pragma unroll
-      for (int u = 0; u < CRW_GROUP; ++u) v += x[e][u];
-      put((cr ? P + q : V + (q - ne)) + (size_t)(nbl + g) * (cr ? CRW_TILE : ld), v);
-    }
-  }
-  if (kt_thr) {
-    double m = ktx[0];
-#pragma unroll
-    for (int u = 1; u < CRW_GROUP; ++u) m = t == 254 ? fmin(m, ktx[u]) : fmax(m, ktx[u]);
-    put(P + (size_t)(nbl + g) * CRW_TILE + 512 + (t - 254), m);
-  }
+  tail_group_sum(ta, g, nbl, true, defer == 0);
   if (t == 0) __hip_atomic_store(&a.ticket[2 + g], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (defer == 1) return;  // the last level runs in the Eta launch's leading workgroup
   vm_stores_done();
   __syncthreads();
   if (g == 0 && t < 64) HMSC_STAMP_RT(87);
   if (t == 0) s_last = __hip_atomic_fetch_add(&a.ticket[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
   __syncthreads();
   if (!s_last) return;
-  const unsigned long long kt0 = ta.kt ? kt_now() : 0ull;
-  // every group tile is in: the side chain may start (it sums the GammaV / psi group tiles)
-  if (t < 64) HMSC_STAMP_RT(79);
-  if (t == 0) {
-    __hip_atomic_store(&a.ticket[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // every BetaLambda column and tile is out: the side work (post_bl_kernel, or the side
-    // chain reading the tail's GammaV / psi group tiles) may start
-    if (ta.tails_flag) __hip_atomic_store(ta.tails_flag, g2bl_epoch(iter), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  double* sCR = smem + 4 * CRW_TILE;  // [row k][16]
-  {
-    // CR = the group tiles summed in group order; each thread's two elements' loads of a
-    // chunk of groups issued together
-    double v[2] = {0.0, 0.0};
-    for (int q0 = 0; q0 < ng; q0 += CRW_GROUP) {
-      double x[2][CRW_GROUP];
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int q = t + 256 * e, h = q >> 5;
-#pragma unroll
-        for (int u = 0; u < CRW_GROUP; ++u)
-          x[e][u] = (h < nf && q0 + u < ng) ? load_coherent(P + (size_t)(nbl + q0 + u) * CRW_TILE + q) : 0.0;
-      }
-#pragma unroll
-      for (int e = 0; e < 2; ++e)
-#pragma unroll
-        for (int u = 0; u < CRW_GROUP; ++u) v[e] += x[e][u];
-    }
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int q = t + 256 * e, h = q >> 5, k = q & 31;
-      sCR[k * 16 + h] = v[e];
-      if (h < nf && k < K) a.CR[k + (size_t)a.ldcr * h] = v[e];
-    }
-  }
-  if (ta.ar_gv && ta.gv_on)  // (sharded) the GammaV / psi sums of this rank's species, group order
-    for (int q = t; q < ngv; q += 256) {
-      double v = 0.0;
-      for (int q0 = 0; q0 < ng; q0 += CRW_GROUP) {
-        double x[CRW_GROUP];
-#pragma unroll
-        for (int u = 0; u < CRW_GROUP; ++u) x[u] = q0 + u < ng ? load_coherent(V + (size_t)(nbl + q0 + u) * ld + q) : 0.0;
-#pragma unroll
-        for (int u = 0; u < CRW_GROUP; ++u) v += x[u];
-      }
-      ta.ar_gv[q] = v;
-    }
-  __syncthreads();
-  if (t < 64) HMSC_STAMP_RT(88);
-  if (w == 0 && !ta.ar_gv) {
-    if (nf <= 8)
-      crw_finish<8>(a, sCR, smem);
-    else if (nf <= 10)
-      crw_finish<10>(a, sCR, smem);
-    else if (nf <= 12)
-      crw_finish<12>(a, sCR, smem);
-    else
-      crw_finish<16>(a, sCR, smem);
-  }
-  if (w == 0) HMSC_STAMP_RT(80);
-  if (ta.kt && t == 0) kt_record(ta.kt, iter, kt0);
-  if (ta.kt_bl && t == 64) {  // the BetaLambda bodies' first start / last end, once (wave 1, beside wave 0's factor)
-    double m0 = 1e300, m1 = 0.0;
-    for (int q0 = 0; q0 < ng; q0 += CRW_GROUP) {
-      double x0[CRW_GROUP], x1[CRW_GROUP];
-#pragma unroll
-      for (int u = 0; u < CRW_GROUP; ++u) {
-        const double* p = P + (size_t)(nbl + (q0 + u < ng ? q0 + u : q0)) * CRW_TILE + 512;
-        x0[u] = load_coherent(p);
-        x1[u] = load_coherent(p + 1);
-      }
-#pragma unroll
-      for (int u = 0; u < CRW_GROUP; ++u) {
-        m0 = fmin(m0, x0[u]);
-        m1 = fmax(m1, x1[u]);
-      }
-    }
-    const uint32_t slot = iter & (KT_SLOTS - 1);
-    __hip_atomic_fetch_min(ta.kt_bl + slot, (unsigned long long)m0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_max(ta.kt_bl + KT_SLOTS + slot, (unsigned long long)m1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  tail_final(ta, nbl, iter, smem, false, true);
 }
 
 struct G2BLArgs {
@@ -1807,6 +1878,47 @@ static CRWArgs make_crw_args(const State& s);
 static void shard_g2_stats(State& s);
 bool side_fusion_ok(const State& s);
 
+
+// how many of the tail's reduction levels a deferred tail leaves to the Eta launch
+static int tail_defer_levels() {
+  static const int v = [] {
+    const char* e = getenv("HMSC_TAIL_DEFER_LEVELS");
+    return (e && atoi(e) == 2) ? 2 : 1;
+  }();
+  return v;
+}
+
+// the BetaLambda workgroups' tail (crw_on), also the Eta launch's reducers under EF_DEFER
+static BLTailArgs make_tail_args(State& s, bool tail_gv, bool sh) {
+  BLTailArgs t{};
+  t.crw = make_crw_args(s);
+  t.gv_on = tail_gv;
+  t.nt = s.nt;
+  t.NF = s.NF;
+  t.nr = s.nr;
+  t.sp0 = s.sp0;
+  t.gvt_ld = s.gvt_ld;
+  for (int r = 0; r < s.nr; ++r) {
+    t.lev_nf[r] = s.lev[r].nf;
+    t.nu[r] = s.lev[r].nu;
+  }
+  t.Tr = s.Tr;
+  t.Psi = s.Psi;
+  t.gvt = s.gvt;
+  t.tails_flag = s.gbl_sync + 2;
+  t.key = s.key;
+  t.kt = s.kt_on ? s.d_kt + (size_t)KT_TAIL * 2 * KT_SLOTS : nullptr;
+  t.kt_bl = s.kt_on ? s.d_kt + (size_t)KT_BL * 2 * KT_SLOTS : nullptr;
+  t.ar_gv = nullptr;
+  t.defer = 0;
+  if (sh) {
+    const ArbLayout L = arb_layout(s);
+    t.crw.CR = s.ar_b + L.cr;
+    t.crw.ldcr = L.ldcr;
+    t.ar_gv = s.ar_b + L.gv;  // [GV | RS], the tile layout
+  }
+  return t;
+}
 void launch_gamma2_bl(State& s, uint32_t iter) {
   if (!s.xeta_valid) launch_xeta(s);
   flush_g(s);
@@ -1866,35 +1978,16 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
   f.part_wg = sh ? 0 : nparts;
   f.sync = s.gbl_sync;
   f.crw_on = crw_on;
+  // sweep graphs after the first, edge-free (the side work forked on the device, see
+  // launch_side_fused): the tail's reductions move into the Eta launch (EF_DEFER)
+  const bool defer = crw_on && !sh && s.edge_free_now && s.capturing && (s.cap_sweep > 0 || s.side_root) &&
+                     !getenv_flag("HMSC_NO_TAIL_DEFER");
   if (crw_on) {
-    BLTailArgs& t = f.tail;
-    t.crw = make_crw_args(s);
-    t.gv_on = tail_gv;
-    t.nt = s.nt;
-    t.NF = s.NF;
-    t.nr = s.nr;
-    t.sp0 = s.sp0;
-    t.gvt_ld = s.gvt_ld;
-    for (int r = 0; r < s.nr; ++r) {
-      t.lev_nf[r] = s.lev[r].nf;
-      t.nu[r] = s.lev[r].nu;
-    }
-    t.Tr = s.Tr;
-    t.Psi = s.Psi;
-    t.gvt = s.gvt;
-    t.tails_flag = s.gbl_sync + 2;
-    t.key = s.key;
-    t.kt = s.kt_on ? s.d_kt + (size_t)KT_TAIL * 2 * KT_SLOTS : nullptr;
-    t.kt_bl = f.bl.kt;
+    f.tail = make_tail_args(s, tail_gv, sh);
+    f.tail.defer = defer ? tail_defer_levels() : 0;
     f.bl.kt_defer = 1;
-    t.ar_gv = nullptr;
-    if (sh) {
-      const ArbLayout L = arb_layout(s);
-      t.crw.CR = s.ar_b + L.cr;
-      t.crw.ldcr = L.ldcr;
-      t.ar_gv = s.ar_b + L.gv;  // [GV | RS], the tile layout
-    }
   }
+  s.tail_defer = defer;
   s.crw_fresh = crw_on && !sh;
   s.tail_gv = tail_gv && !sh;
   s.side_tail = false;  // (both set again by this sweep's launch_side_fused)
@@ -1938,8 +2031,8 @@ struct LPArgs {
 __device__ __forceinline__ void psi_body(const LPArgs& a, int bid, int nb, bool coh = false) {
   // grid over species columns; each block handles a contiguous species range
   __shared__ double sM[256];
-  __shared__ double sTau[64];
-  __shared__ int sLev[64], sH[64];
+  __shared__ double sTau[HMSC_KCAP];
+  __shared__ int sLev[HMSC_KCAP], sH[HMSC_KCAP];
   const int t = threadIdx.x;
   if (t == 0) {
     int f = 0;
@@ -2023,16 +2116,16 @@ __device__ __forceinline__ void delta_body(const LPArgs& a, const double* rs_par
                                            int rs_ld = 0, int* flags = nullptr) {
   if (rs_ld == 0) rs_ld = a.NF;
   // one workgroup per level: the sequential delta chain (R/updateLambdaPriors.R:25-32)
-  __shared__ double rs[64], delta[64], gstd[64];
+  __shared__ double rs[HMSC_KCAP], delta[HMSC_KCAP], gstd[HMSC_KCAP];
   const int t = threadIdx.x, w = t >> 6, nw = blockDim.x >> 6;
   const int nf = a.lev_nf[r];
   int f0 = 0;
   for (int q = 0; q < r; ++q) f0 += a.lev_nf[q];
-  if (t < nf) {
+  for (int h = t; h < nf; h += blockDim.x) {
     double sum = 0.0;
-    for (int b = 0; b < nparts; ++b) sum += load_coherent(rs_part + (size_t)b * rs_ld + f0 + t);
-    rs[t] = sum;
-    delta[t] = a.Delta[f0 + t];
+    for (int b = 0; b < nparts; ++b) sum += load_coherent(rs_part + (size_t)b * rs_ld + f0 + h);
+    rs[h] = sum;
+    delta[h] = a.Delta[f0 + h];
   }
   if (r == 0) HMSC_STAMP(20);
   const uint32_t stream = S_DELTA + LEVEL_STRIDE * r;
@@ -2056,7 +2149,7 @@ __device__ __forceinline__ void delta_body(const LPArgs& a, const double* rs_par
     }
   }
   __syncthreads();
-  if (t < nf) a.Delta[f0 + t] = delta[t];
+  for (int h = t; h < nf; h += blockDim.x) a.Delta[f0 + h] = delta[h];
   if (r == 0) HMSC_STAMP(21);
   if (flags) {  // this level's Delta is out (the next sweep's fused launch waits on this)
     __threadfence();
@@ -2124,7 +2217,7 @@ static LPArgs make_lp_args(State& s, uint32_t iter) {
 
 void launch_lambda_priors(State& s, uint32_t iter, hipStream_t st) {
   if (s.nr == 0) return;
-  HMSC_REQUIRE(s.NF <= 64, "updateLambdaPriors: sum(nf) must be <= 64 in this build");
+  HMSC_REQUIRE(s.NF <= HMSC_KCAP, "updateLambdaPriors: sum(nf) must be <= 128 in this build");
   const LPArgs a = make_lp_args(s, iter);
   const int nparts = std::min(LP_PARTS, std::max(1, s.nsl));
   psi_kernel<<<nparts, 256, 0, st>>>(a);
@@ -2145,8 +2238,9 @@ void launch_lambda_priors(State& s, uint32_t iter, hipStream_t st) {
 template <int NFB>
 __global__ __launch_bounds__(256) void zl_kernel(const double* __restrict__ Z, const double* __restrict__ BL,
                                                  const double* __restrict__ iSigma, const int8_t* __restrict__ mask,
-                                                 int ny, int ns_loc, int K, int nc, int NF, int split,
-                                                 double* __restrict__ ZL_part) {
+                                                 int ny, int ns_loc, int K, int nc, int NFtot, int split,
+                                                 double* __restrict__ ZL_part, int fo, int NF) {
+  // factors fo .. fo + NF - 1 of the NFtot (NF <= NFB <= 64 per launch)
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int i = blockIdx.x * 64 + lane;
@@ -2156,7 +2250,7 @@ __global__ __launch_bounds__(256) void zl_kernel(const double* __restrict__ Z, c
   double* sL = smem;  // [jj][NF]
   for (int p = t; p < nj * NF; p += 256) {
     const int jj = p / NF, f = p % NF, j = ja + jj;
-    sL[p] = BL[nc + f + (size_t)K * j] * iSigma[j];
+    sL[p] = BL[nc + fo + f + (size_t)K * j] * iSigma[j];
   }
   __syncthreads();
   double acc[NFB];
@@ -2200,7 +2294,7 @@ __global__ __launch_bounds__(256) void zl_kernel(const double* __restrict__ Z, c
     const int f = p / 64, l = p % 64, ii = blockIdx.x * 64 + l;
     const double v = sR[(0 * NF + f) * 64 + l] + sR[(1 * NF + f) * 64 + l] + sR[(2 * NF + f) * 64 + l] +
                      sR[(3 * NF + f) * 64 + l];
-    if (ii < ny) ZL_part[(size_t)blockIdx.y * ny * NF + (size_t)ii * NF + f] = v;
+    if (ii < ny) ZL_part[(size_t)blockIdx.y * ny * NFtot + (size_t)ii * NFtot + fo + f] = v;
   }
 }
 
@@ -2303,7 +2397,7 @@ __device__ __forceinline__ void crw_body(const CRWArgs& a, int p, double* smem) 
   }
   __syncthreads();
   if (w == 0) {
-    crw_finish<NFB>(a, sCR, sAcc);  // the wave partials are consumed: their LDS is the scratch
+    crw_finish<NFB>(a, sCR, a.W, sAcc);  // the wave partials are consumed: their LDS is the scratch
     if (lane == 0) __hip_atomic_store(a.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -2533,6 +2627,12 @@ struct EtaFArgs {
   const uint32_t* iter_dev;  // graph replay: the sweep counter is read from the device
   int noise_zero;
   unsigned long long* kt;    // live launch timing (KT_ETA block) or null
+  // EF_DEFER: the BetaLambda tail's two reduction levels run in workgroups 0 .. nred - 1 (one
+  // per group of CRW_GROUP BetaLambda workgroups, nbl of them); the tile workgroups after them
+  // stream Z meanwhile and wait for tail.tails_flag before reading CR and W
+  BLTailArgs tail;
+  int nred, nbl;
+  int* err;
 };
 
 constexpr int EF_SITES = 16;
@@ -2542,7 +2642,15 @@ constexpr int EF_SITES = 16;
 // EF_SOLVE is stages 2-4 on the all-reduced ZL and CR, each workgroup forming W = L^-1 itself
 // (one wave, the BetaLambda tail's factorization) -- on one rank the pair reproduces the
 // fused kernel bit for bit.
-enum EtaMode { EF_FUSED = 0, EF_STREAM = 1, EF_SOLVE = 2 };
+// EF_DEFER: EF_FUSED with the BetaLambda tail's reductions folded in (EtaFArgs::nred), so the
+// Gamma2 + BetaLambda launch ends with its bodies and this launch's Z stream overlaps the
+// reductions and Q's factorization instead of following them.
+enum EtaMode { EF_FUSED = 0, EF_STREAM = 1, EF_SOLVE = 2, EF_DEFER = 3 };
+template <int NFB>
+constexpr int ef_lds_doubles() {
+  return 4 * 16 * (EF_SITES + 1) + NFB * NFB + 3 * NFB * EF_SITES + 64 * (EF_SITES + 1) + 64 * NFB;
+}
+static_assert(ef_lds_doubles<8>() >= 4 * CRW_TILE + 32 * 16 + 256, "EF_DEFER reducers: LDS scratch");
 
 // __launch_bounds__(256, 3): <= 168 VGPRs, three waves per SIMD, so the 625 workgroups of the
 // synthetic config (2500 waves) are resident in one round (at 196 VGPRs they took two: 33 ->
@@ -2553,17 +2661,37 @@ enum EtaMode { EF_FUSED = 0, EF_STREAM = 1, EF_SOLVE = 2 };
 #endif
 template <int NFB, int MODE>
 __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
-  __shared__ double sPart[4][16][EF_SITES + 1];  // [wave][factor][site] ZL partials (EF_SOLVE: W's scratch)
-  __shared__ double sW[NFB * NFB];            // W = L^-1, L the lower factor of Q (row m at m NFB)
-  __shared__ double sB[NFB][EF_SITES], sXi[NFB][EF_SITES], sU[NFB][EF_SITES];
-  __shared__ double sX[64][EF_SITES + 1];     // XEta tile [k][site] (K <= 64)
-  __shared__ double sCR[64 * NFB];            // CR[k][h], k < K
-  __shared__ int sPi[EF_SITES];               // the tile's units
-  const unsigned long long kt0 = a.kt ? kt_now() : 0ull;
+  // one block carved into the stages' arrays (EF_DEFER's reducer workgroups: their scratch)
+  __shared__ __attribute__((aligned(16))) double sAll[ef_lds_doubles<NFB>()];
+  double(*sPart)[16][EF_SITES + 1] = reinterpret_cast<double(*)[16][EF_SITES + 1]>(sAll);  // [wave][factor][site] ZL partials (EF_SOLVE: W's scratch)
+  double* sW = sAll + 4 * 16 * (EF_SITES + 1);  // W = L^-1, L the lower factor of Q (row m at m NFB)
+  double(*sB)[EF_SITES] = reinterpret_cast<double(*)[EF_SITES]>(sW + NFB * NFB);
+  double(*sXi)[EF_SITES] = sB + NFB;
+  double(*sU)[EF_SITES] = sXi + NFB;
+  double(*sX)[EF_SITES + 1] = reinterpret_cast<double(*)[EF_SITES + 1]>(&sU[NFB][0]);  // XEta tile [k][site] (K <= 64)
+  double* sCR = &sX[64][0];  // CR[k][h], k < K
+  __shared__ int sPi[EF_SITES];  // the tile's units
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, lm = lane & 15, lk = lane >> 4;
+  if (MODE == EF_DEFER && blockIdx.x < a.nred) {  // the BetaLambda tail's reductions
+    const bool two = a.tail.defer == 2;
+    if (two) {  // group blockIdx.x's tiles, then the last group through sums the group tiles
+      __shared__ int s_last;
+      tail_group_sum(a.tail, blockIdx.x, a.nbl, false, true);
+      vm_stores_done();
+      __syncthreads();
+      if (t == 0)
+        s_last = __hip_atomic_fetch_add(&a.tail.crw.ticket[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.nred - 1;
+      __syncthreads();
+      if (!s_last) return;
+    }
+    tail_final(a.tail, a.nbl, SWEEP_ITER(a), sAll, true, two);
+    return;
+  }
+  const int tile = MODE == EF_DEFER ? blockIdx.x - a.nred : blockIdx.x;
+  const unsigned long long kt0 = a.kt ? kt_now() : 0ull;
   const int ny = a.ny, nf = a.nf, K = a.K, nc = a.nc, ns = a.ns_loc;
-  const int i0 = blockIdx.x * EF_SITES;
-  if (blockIdx.x == 0) HMSC_STAMP(50);
+  const int i0 = tile * EF_SITES;
+  if (tile == 0) HMSC_STAMP(50);
   const uint32_t iter = SWEEP_ITER(a);       // read once, ahead of the stream
   if (MODE != EF_STREAM && t < EF_SITES) sPi[t] = i0 + t < ny ? a.Pi[i0 + t] : 0;
   // ---- stage 1: ZL = Z (Lambda diag(iSigma))^T on the matrix cores, the HBM stream of the
@@ -2582,7 +2710,7 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
   // CR (K x nf) and W (nf x nf) of this sweep, formed once by crw_body: loads issued here,
   // ahead of the stream, stored to LDS after it
   double crv[4] = {0.0, 0.0, 0.0, 0.0}, wv[NFB * NFB / 256 + 1];
-  if (MODE != EF_STREAM)
+  if (MODE == EF_FUSED || MODE == EF_SOLVE)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int p = t + 256 * u, k = p % K, h = p / K;
@@ -2650,6 +2778,23 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
     }
     return;
   }
+  if (MODE == EF_DEFER) {  // CR and W of this sweep: out once the tail's last reducer raises the flag
+    if (t == 0 && !spin_until<2>([&] {
+          return __hip_atomic_load(a.tail.tails_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g2bl_epoch(iter);
+        }))
+      __hip_atomic_store(&a.err[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = t + 256 * u, k = p % K, h = p / K;
+      crv[u] = p < K * nf ? load_coherent(a.CR + k + (size_t)a.ldcr * h) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < NFB * NFB / 256 + 1; ++u) {
+      const int p = t + 256 * u, m = p / NFB, c = p % NFB;
+      wv[u] = p < NFB * NFB ? load_coherent(a.W + m * 16 + c) : 0.0;
+    }
+  }
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int p = t + 256 * u, s2 = p % EF_SITES, k = p / EF_SITES;
@@ -2660,7 +2805,7 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
     const int p = t + 256 * u, k = p % K, h = p / K;
     if (p < K * nf) sCR[k * NFB + h] = crv[u];
   }
-  if (MODE == EF_FUSED)
+  if (MODE == EF_FUSED || MODE == EF_DEFER)
 #pragma unroll
     for (int u = 0; u < NFB * NFB / 256 + 1; ++u) {
       const int p = t + 256 * u;
@@ -2668,10 +2813,10 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
     }
   __syncthreads();
   if (MODE == EF_SOLVE) {  // W = L^-1 of Q = I + (rows nc.. of CR), one wave, into sW (rows m < NFB)
-    if (w == 0) q_inv_factor_nf(sCR + nc * NFB, NFB, nf, sW, NFB, NFB, &sPart[0][0][0]);
+    if (w == 0) q_inv_factor_nf(sCR + nc * NFB, NFB, nf, sW, NFB, NFB, sAll);
     __syncthreads();
   }
-  if (blockIdx.x == 0) HMSC_STAMP(51);
+  if (tile == 0) HMSC_STAMP(51);
   // ---- stage 2: b = ZL - X CR_x, and the noise, one (site, factor) per thread
   for (int p = t; p < EF_SITES * nf; p += 256) {
     const int s2 = p % EF_SITES, h = p / EF_SITES, ii = i0 + s2;
@@ -2687,7 +2832,7 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
     sXi[h][s2] = xi;
   }
   __syncthreads();
-  if (blockIdx.x == 0) HMSC_STAMP(53);
+  if (tile == 0) HMSC_STAMP(53);
   // ---- stage 3: eta = L^-T (L^-1 b + xi) = W^T (W b + xi), two matrix-vector phases over
   // the (factor, site) pairs (no serial substitution chain)
   for (int p = t; p < EF_SITES * nf; p += 256) {
@@ -2708,9 +2853,9 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
     sX[nc + h][s2] = ii < ny ? e : 0.0;
   }
   __syncthreads();
-  if (blockIdx.x == 0) HMSC_STAMP(54);
+  if (tile == 0) HMSC_STAMP(54);
   // ---- stage 4: Gram partial of the tile's Eta rows, Eta^T XEta (nf x K, ld Kmax)
-  double* dst = a.G_part + (size_t)blockIdx.x * a.Kmax * nf;
+  double* dst = a.G_part + (size_t)tile * a.Kmax * nf;
   for (int p = t; p < K * nf; p += 256) {
     const int k = p % K, h = p / K;
     double g = 0.0;
@@ -2718,7 +2863,7 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
     for (int s2 = 0; s2 < EF_SITES; ++s2) g = fma(sX[nc + h][s2], sX[k][s2], g);
     dst[k + a.Kmax * h] = g;
   }
-  if (blockIdx.x == 0) HMSC_STAMP(55);
+  if (tile == 0) HMSC_STAMP(55);
   if (a.kt) {
     __syncthreads();
     if (t == 0) kt_record(a.kt, iter, kt0);
@@ -2779,7 +2924,7 @@ __global__ __launch_bounds__(256) void post_bl_kernel(PostBLArgs a) {
 }
 
 static bool eta_fused_ok(const State& s);
-static void launch_eta_fused(State& s, uint32_t iter, bool cr_done);
+static void launch_eta_fused(State& s, uint32_t iter, bool cr_done, bool defer, bool tail_gv);
 
 static CRWArgs make_crw_args(const State& s) {
   CRWArgs c{};
@@ -2826,8 +2971,11 @@ void launch_side_fused(State& s, uint32_t iter) {
   // launch waits on the device for the fused launch's tails flag (raised by the last reducer
   // of the tail, after every BetaLambda workgroup's stores), see State::cap_sweep
   const bool dev_fork = cr_done && s.edge_free_now && s.capturing && (s.cap_sweep > 0 || s.side_root);
+  const bool defer = cr_done && s.tail_defer;
+  s.tail_defer = false;
+  HMSC_REQUIRE(!defer || dev_fork, "fused Eta: the tail's reductions deferred to a launch the side work is not forked from");
   if (!dev_fork) HIP_OK(hipEventRecord(s.ev_bl, s.stream));
-  launch_eta_fused(s, iter, cr_done);
+  launch_eta_fused(s, iter, cr_done, defer, tail);
   if (!dev_fork) HIP_OK(hipStreamWaitEvent(s.side, s.ev_bl, 0));
   LPArgs lp = make_lp_args(s, iter);
   const double* rs;
@@ -2971,19 +3119,20 @@ static EtaFArgs make_etaf_args(State& s, uint32_t iter) {
   a.iter_dev = s.capturing ? s.d_iter : nullptr;
   a.noise_zero = s.noise_mode;
   a.kt = s.kt_on ? s.d_kt + (size_t)KT_ETA * 2 * KT_SLOTS : nullptr;
+  a.err = s.gbl_sync;
   return a;
 }
 
 template <int MODE>
 static void launch_eta_fused_mode(State& s, const EtaFArgs& a) {
   const int ntile = (s.ny + EF_SITES - 1) / EF_SITES;
-  const int nf = s.lev[0].nf;
+  const int nf = s.lev[0].nf, nb = ntile + (MODE == EF_DEFER ? a.nred : 0);
   if (nf <= 8)
-    eta_fused_kernel<8, MODE><<<ntile, 256, 0, s.stream>>>(a);
+    eta_fused_kernel<8, MODE><<<nb, 256, 0, s.stream>>>(a);
   else if (nf <= 12)
-    eta_fused_kernel<12, MODE><<<ntile, 256, 0, s.stream>>>(a);
+    eta_fused_kernel<12, MODE><<<nb, 256, 0, s.stream>>>(a);
   else
-    eta_fused_kernel<16, MODE><<<ntile, 256, 0, s.stream>>>(a);
+    eta_fused_kernel<16, MODE><<<nb, 256, 0, s.stream>>>(a);
   HIP_OK(hipGetLastError());
   if (MODE != EF_STREAM) {
     // G's Eta rows: reduced from G_part by the next updateZ launch (or flush_g)
@@ -2995,7 +3144,7 @@ static void launch_eta_fused_mode(State& s, const EtaFArgs& a) {
   }
 }
 
-static void launch_eta_fused(State& s, uint32_t iter, bool cr_done = false) {
+static void launch_eta_fused(State& s, uint32_t iter, bool cr_done = false, bool defer = false, bool tail_gv = false) {
   if (!cr_done) {  // CR, W and LS (post_bl_kernel's workgroup 0 forms them in the co-launched path)
     const size_t smem = (size_t)CRW_LDS * sizeof(double);
     const CRWArgs c = make_crw_args(s);
@@ -3007,9 +3156,17 @@ static void launch_eta_fused(State& s, uint32_t iter, bool cr_done = false) {
       crw_kernel<16><<<CRW_PARTS, 256, smem, s.stream>>>(c);
     HIP_OK(hipGetLastError());
   }
-  const EtaFArgs a = make_etaf_args(s, iter);
+  EtaFArgs a = make_etaf_args(s, iter);
   ProfScope ps(s, PROF_ETA_UNIT);
-  launch_eta_fused_mode<EF_FUSED>(s, a);
+  if (defer) {
+    a.nbl = (s.nsl + 3) / 4;
+    a.tail = make_tail_args(s, tail_gv, false);
+    a.tail.defer = tail_defer_levels();
+    a.nred = a.tail.defer == 2 ? (a.nbl + CRW_GROUP - 1) / CRW_GROUP : 1;
+    launch_eta_fused_mode<EF_DEFER>(s, a);
+  } else {
+    launch_eta_fused_mode<EF_FUSED>(s, a);
+  }
 }
 
 // NA rows of a sharded chain, level r (R/updateEta.R:59-70): the masked per-row precision and
@@ -3112,17 +3269,23 @@ static void eta_levels(State& s, uint32_t iter, const double* zl, int nzl, const
 static void launch_zl(State& s, const int8_t* mask) {
   dim3 grid((s.ny + 63) / 64, s.zl_split);
   const int per = (s.nsl + s.zl_split - 1) / s.zl_split;
-  const size_t smem = std::max((size_t)per * s.NF, (size_t)4 * s.NF * 64) * sizeof(double);
   ProfScope ps(s, PROF_ZL);
-  if (s.NF <= 8)
-    zl_kernel<8><<<grid, 256, smem, s.stream>>>(s.Z, s.BL, s.iSigma, mask, s.ny, s.nsl, s.K, s.nc, s.NF, s.zl_split, s.ZL_part);
-  else if (s.NF <= 16)
-    zl_kernel<16><<<grid, 256, smem, s.stream>>>(s.Z, s.BL, s.iSigma, mask, s.ny, s.nsl, s.K, s.nc, s.NF, s.zl_split, s.ZL_part);
-  else if (s.NF <= 32)
-    zl_kernel<32><<<grid, 256, smem, s.stream>>>(s.Z, s.BL, s.iSigma, mask, s.ny, s.nsl, s.K, s.nc, s.NF, s.zl_split, s.ZL_part);
-  else
-    zl_kernel<64><<<grid, 256, smem, s.stream>>>(s.Z, s.BL, s.iSigma, mask, s.ny, s.nsl, s.K, s.nc, s.NF, s.zl_split, s.ZL_part);
-  HIP_OK(hipGetLastError());
+  // at most 64 factors per pass over Z (NF > 64: two passes)
+  for (int fo = 0; fo < s.NF; fo += 64) {
+    const int nf = std::min(64, s.NF - fo);
+    const size_t smem = std::max((size_t)per * nf, (size_t)4 * nf * 64) * sizeof(double);
+#define ZL_ARGS s.Z, s.BL, s.iSigma, mask, s.ny, s.nsl, s.K, s.nc, s.NF, s.zl_split, s.ZL_part, fo, nf
+    if (nf <= 8)
+      zl_kernel<8><<<grid, 256, smem, s.stream>>>(ZL_ARGS);
+    else if (nf <= 16)
+      zl_kernel<16><<<grid, 256, smem, s.stream>>>(ZL_ARGS);
+    else if (nf <= 32)
+      zl_kernel<32><<<grid, 256, smem, s.stream>>>(ZL_ARGS);
+    else
+      zl_kernel<64><<<grid, 256, smem, s.stream>>>(ZL_ARGS);
+#undef ZL_ARGS
+    HIP_OK(hipGetLastError());
+  }
 }
 
 void launch_eta(State& s, uint32_t iter) {
@@ -3133,7 +3296,7 @@ void launch_eta(State& s, uint32_t iter) {
     launch_eta_fused(s, iter);
     return;
   }
-  HMSC_REQUIRE(s.NF <= 64, "updateEta: sum(nf) must be <= 64 in this build");
+  HMSC_REQUIRE(s.NF <= HMSC_KCAP, "updateEta: sum(nf) must be <= 128 in this build");
   for (int r = 0; r < s.nr; ++r)
     HMSC_REQUIRE(s.lev[r].nf >= 1, "updateEta: a level has zero factors");
   launch_zl(s, nullptr);  // ZL over all levels in one pass over Z
@@ -3697,7 +3860,7 @@ static void shard_gv_stats(State& s, hipStream_t st) {
 // updateLambdaPriors: the psi draws of this rank's species and sum_j psi lambda^2 (:22-24)
 static void shard_psi(State& s, uint32_t iter, hipStream_t st) {
   const ArbLayout L = arb_layout(s);
-  HMSC_REQUIRE(s.NF <= 64, "updateLambdaPriors: sum(nf) must be <= 64 in this build");
+  HMSC_REQUIRE(s.NF <= HMSC_KCAP, "updateLambdaPriors: sum(nf) must be <= 128 in this build");
   const LPArgs a = make_lp_args(s, iter);
   const int nparts = std::min(LP_PARTS, std::max(1, s.nsl));
   psi_kernel<<<nparts, 256, 0, st>>>(a);
@@ -3744,7 +3907,7 @@ __global__ __launch_bounds__(256) void na_crrow_kernel(NACRArgs a) {
 // updateEta: ZL = Z (Lambda diag(iSigma))^T over this rank's observed cells and CR (+ the NA rows)
 static void shard_eta_stats(State& s) {
   const ArbLayout L = arb_layout(s);
-  HMSC_REQUIRE(s.NF <= 64, "updateEta: sum(nf) must be <= 64 in this build");
+  HMSC_REQUIRE(s.NF <= HMSC_KCAP, "updateEta: sum(nf) must be <= 128 in this build");
   launch_zl(s, s.has_na ? s.Ycode : nullptr);
   const int64_t nzl = (int64_t)s.ny * s.NF;
   slab_sum_kernel<<<grid_for(nzl), 256, 0, s.stream>>>(s.ZL_part, s.ar_b + L.zl, nzl, s.zl_split, nzl);

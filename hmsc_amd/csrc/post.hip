@@ -21,12 +21,14 @@ namespace hmsc {
 // "Omega").  A 64 x 64 output tile per workgroup (16 x 16 threads, 4 x 4 outputs each); per
 // sample the tile's two 64-species blocks of Lambda_s are staged in LDS.
 // ---------------------------------------------------------------------------------------
-constexpr int OT = 64, OF_MAX = 64;
+constexpr int OT = 64, OF_MAX = HMSC_KCAP;
 
 __global__ __launch_bounds__(256) void omega_assoc_kernel(int S, int ns, int nfmax, const int* nf, const double* Lam,
                                                            double* mean_cor, double* support, double* support_neg,
                                                            double* mean_omega) {
-  __shared__ double LI[OF_MAX * OT], LJ[OF_MAX * OT];  // [h][species in block]
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* LI = smem;                // [h][species in block], h < nfmax
+  double* LJ = smem + nfmax * OT;
   const int ntile = (ns + OT - 1) / OT;
   const int bi = blockIdx.x % ntile, bj = blockIdx.x / ntile;
   const int i0 = bi * OT, j0 = bj * OT, t = threadIdx.x, ti = t & 15, tj = t >> 4;
@@ -106,7 +108,8 @@ __global__ __launch_bounds__(256) void omega_assoc_kernel(int S, int ns, int nfm
 //   random1[j, r] = sum_h Lambda_r[h, j]^2, then the per-sample normalisations   (:142-173)
 // The sample's terms go to a per-sample slot; vp_reduce_kernel adds them in sample order.
 // ---------------------------------------------------------------------------------------
-constexpr int VP_NC = 64;
+constexpr int VP_NC = HMSC_KCAP;
+constexpr size_t VP_LDS_MAX = 150 * 1024;  // the three Gram matrices in LDS up to here, else global
 
 struct VpArgs {
   int ny, ns, nc, nt, S, ngroups, nr;
@@ -121,12 +124,16 @@ struct VpArgs {
   const double* Lambda[HMSC_MAX_LEVELS];  // S x nfmax_r x ns
   double* work;          // S x slot
   size_t slot;           // doubles per sample: nc + 1 + ns (1 + nr + ngroups)
+  double* gram;          // S x 3 nc^2 when they do not fit LDS (nc > 80), else null
 };
 
 __global__ __launch_bounds__(256) void vp_sample_kernel(VpArgs a) {
-  __shared__ double C[3][VP_NC * VP_NC];  // Mc Bc', Mc Mc', Bc Bc'
+  extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ double mB[VP_NC], mM[VP_NC], red[8];
   const int s = blockIdx.x, t = threadIdx.x, nc = a.nc, ns = a.ns, nt = a.nt;
+  double* Cb = a.gram ? a.gram + (size_t)s * 3 * nc * nc : smem;
+  double* C[3] = {Cb, Cb + (size_t)nc * nc, Cb + (size_t)2 * nc * nc};  // Mc Bc', Mc Mc', Bc Bc'
+
   const double* B = a.Beta + (size_t)s * nc * ns;
   const double* G = a.Gamma + (size_t)s * nc * nt;
   double* out = a.work + (size_t)s * a.slot;
@@ -357,7 +364,7 @@ void post_omega(int device, int S, int ns, int nfmax, const int* nf, const doubl
                 double* support, double* support_neg, double* mean_omega) {
   HMSC_REQUIRE(S > 0 && ns > 0 && nfmax > 0 && nfmax <= OF_MAX && nf && Lambda && mean_cor && support && support_neg &&
                    mean_omega,
-               "hmsc_post_omega: bad arguments (nfmax <= 64)");
+               "hmsc_post_omega: bad arguments (nfmax <= 128)");
   for (int s = 0; s < S; ++s) HMSC_REQUIRE(nf[s] >= 1 && nf[s] <= nfmax, "hmsc_post_omega: nf out of range");
   HIP_OK(hipSetDevice(device));
   PostBufs b;  // before the stream: the stream drains before the buffers are freed
@@ -367,7 +374,8 @@ void post_omega(int device, int S, int ns, int nfmax, const int* nf, const doubl
   const double* dL = b.up(Lambda, (size_t)S * nfmax * ns, ps.s);
   double *mc = b.alloc<double>(n2), *sp = b.alloc<double>(n2), *sn = b.alloc<double>(n2), *mo = b.alloc<double>(n2);
   const int nt = (ns + OT - 1) / OT;
-  omega_assoc_kernel<<<nt * nt, 256, 0, ps.s>>>(S, ns, nfmax, dnf, dL, mc, sp, sn, mo);
+  omega_assoc_kernel<<<nt * nt, 256, (size_t)2 * nfmax * OT * sizeof(double), ps.s>>>(S, ns, nfmax, dnf, dL, mc, sp, sn,
+                                                                                     mo);
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(mean_cor, mc, n2 * sizeof(double), hipMemcpyDeviceToHost, ps.s));
   HIP_OK(hipMemcpyAsync(support, sp, n2 * sizeof(double), hipMemcpyDeviceToHost, ps.s));
@@ -379,7 +387,7 @@ void post_omega(int device, int S, int ns, int nfmax, const int* nf, const doubl
 void post_vp(const hmsc_vp_args* v, double* out) {
   HMSC_REQUIRE(v && out && v->ny > 1 && v->ns > 1 && v->nc >= 1 && v->nc <= VP_NC && v->nt >= 1 && v->S >= 1 &&
                    v->ngroups >= 1 && v->ngroups <= VP_NC && v->nr >= 0 && v->nr <= HMSC_MAX_LEVELS,
-               "hmsc_variance_partitioning: bad dimensions (nc, ngroups <= 64)");
+               "hmsc_variance_partitioning: bad dimensions (nc, ngroups <= 128)");
   for (int k = 0; k < v->nc; ++k)
     HMSC_REQUIRE(v->group[k] >= 1 && v->group[k] <= v->ngroups, "hmsc_variance_partitioning: group out of range");
   HIP_OK(hipSetDevice(v->device));
@@ -400,7 +408,9 @@ void post_vp(const hmsc_vp_args* v, double* out) {
   }
   a.slot = (size_t)a.nc + 1 + (size_t)a.ns * (1 + a.nr + a.ngroups);
   a.work = b.alloc<double>(a.slot * a.S);
-  vp_sample_kernel<<<a.S, 256, 0, ps.s>>>(a);
+  const size_t gram_bytes = (size_t)3 * a.nc * a.nc * sizeof(double);
+  a.gram = gram_bytes > VP_LDS_MAX ? b.alloc<double>((size_t)a.S * 3 * a.nc * a.nc) : nullptr;
+  vp_sample_kernel<<<a.S, 256, a.gram ? 0 : gram_bytes, ps.s>>>(a);
   double* dout = b.alloc<double>(a.slot);
   vp_reduce_kernel<<<(unsigned)((a.slot + 255) / 256), 256, 0, ps.s>>>(a.work, a.slot, a.S, dout);
   HIP_OK(hipGetLastError());

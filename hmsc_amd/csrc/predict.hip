@@ -22,7 +22,7 @@
 namespace hmsc {
 
 constexpr uint32_t S_PREDICT = 30;
-constexpr int PT_I = 64, PT_J = 32, PK_MAX = 64;
+constexpr int PT_I = 64, PT_J = 32, PK_MAX = HMSC_KCAP;
 
 struct PredArgs {
   int ny, ns, nc, nr, nsamples, K, expected;
@@ -70,11 +70,12 @@ __device__ double rpois_dev(double lam, Key key, uint32_t cell, uint32_t s) {
 }
 
 __global__ __launch_bounds__(256) void predict_kernel(PredArgs a) {
-  __shared__ double sA[PT_I * (PK_MAX + 1)];  // [site][k], padded
-  __shared__ double sB[PK_MAX * PT_J];        // [k][species]
+  extern __shared__ __attribute__((aligned(16))) double smem[];
   const int t = threadIdx.x, i0 = blockIdx.x * PT_I, j0 = blockIdx.y * PT_J, s = blockIdx.z;
   const int ny = a.ny, ns = a.ns, nc = a.nc, K = a.K;
-  const int LD = PK_MAX + 1;
+  const int LD = K | 1;                 // odd: conflict-free column reads
+  double* sA = smem;                    // [site][k], padded
+  double* sB = smem + PT_I * LD;        // [k][species]
   for (int p = t; p < PT_I * K; p += 256) {
     const int ii = p % PT_I, k = p / PT_I, i = i0 + ii;
     double v = 0.0;
@@ -144,7 +145,7 @@ void run_predict(const hmsc_predict_args* p, double* out) {
   HMSC_REQUIRE(p->nr >= 0 && p->nr <= HMSC_MAX_LEVELS, "predict: bad nr");
   int K = p->nc;
   for (int r = 0; r < p->nr; ++r) K += p->nf[r];
-  HMSC_REQUIRE(K <= PK_MAX, "predict: nc + sum(nf) must be <= 64");
+  HMSC_REQUIRE(K <= PK_MAX, "predict: nc + sum(nf) must be <= 128");
   HMSC_REQUIRE((size_t)p->ny * p->ns < ((size_t)1 << 32), "predict: ny * ns must fit 32-bit cell counters");
   HIP_OK(hipSetDevice(p->device));
   const size_t S = p->nsamples, ny = p->ny, ns = p->ns, nc = p->nc;
@@ -186,7 +187,8 @@ void run_predict(const hmsc_predict_args* p, double* out) {
   a.key = Key{(uint32_t)p->seed, (uint32_t)(p->seed >> 32)};
   if (S > 0) {
     dim3 grid((p->ny + PT_I - 1) / PT_I, (p->ns + PT_J - 1) / PT_J, p->nsamples);
-    predict_kernel<<<grid, 256>>>(a);
+    const size_t smem = ((size_t)PT_I * (K | 1) + (size_t)K * PT_J) * sizeof(double);
+    predict_kernel<<<grid, 256, smem>>>(a);
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpy(out, a.out, S * ny * ns * 8, hipMemcpyDeviceToHost));
   }

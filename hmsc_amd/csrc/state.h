@@ -99,6 +99,7 @@ struct State {
   // main stream may advance d_iter for the next sweep while it runs
   bool side_fused = false;
   bool crw_fresh = false;   // the last Gamma2 + BetaLambda launch formed the fused Eta constants
+  bool tail_defer = false;  // ... with its reductions left to the Eta launch (EF_DEFER)
   // ... and its BetaLambda tail also formed GammaV's and LambdaPriors' species partials (gvt),
   // which the side chain reads instead of post_bl_kernel's
   bool tail_gv = false;
@@ -354,6 +355,7 @@ void launch_init(State& s);
 void launch_update_z(State& s, uint32_t iter, bool use_raw_y);
 void launch_zt_refresh(State& s);
 int z_resident_slots(const State& s);
+int z_xeta_cols_for(int Kmax);  // XEta columns the z kernel reads (zdraw.hip)
 void launch_xeta(State& s);
 void flush_g(State& s);
 void launch_slab_sum2(const double* p0, double* o0, int64_t n0, int np0, const double* p1, double* o1, int64_t n1,

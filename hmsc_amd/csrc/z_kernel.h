@@ -66,7 +66,7 @@ struct ZArgs {
 
 constexpr int ZT_I = 64;   // sites per workgroup tile (4 waves x 16)
 constexpr int ZT_J = 32;   // species per workgroup (16 pairs)
-constexpr int KMAX_Z = 64;
+constexpr int KMAX_Z = 128;
 constexpr int ZT_LD = 65;  // padded LDS leading dimension of the 64-site XEta tile (xeta_gram_kernel)
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -387,8 +387,11 @@ constexpr int ZT_TLD = 17;  // leading dimension of the wave's 16-site x 32-spec
 // NORMAL: the chain has normal species (their cells copy Yval, R/updateZ.R:40-41); a probit-
 // only chain's kernel then issues no load inside the draw loop (a load there would make each
 // use wait, vmcnt being in order, behind every Z store still in flight).
+// NKB > 4 (64 < K <= 128, one instantiation NKB = 8): the XZ accumulators (128 registers, the
+// matrix cores' accumulation registers) at two waves per SIMD; the E and XZ operands are
+// loaded 64 rows at a time and the waves' XZ combined 64 rows at a time (LDS).
 template <bool DRAW, bool HAS_NA, int NKB, int MODE = Z_ALL, bool POIS = false, bool NORMAL = true>
-__global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
+__global__ __launch_bounds__(256, NKB > 4 ? 2 : 4) void z_wave_kernel(ZArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   if (a.gred_y0 && blockIdx.y == 0) {  // the co-launched G reduction row
     g_reduce_body(a, smem);
@@ -460,17 +463,21 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
       // all K16 operand rows, loaded before the first MFMA (padded buffer, ZArgs: rows k >= K
       // meet zero BL rows), so their latency is paid once per tile
       const double* xp = a.XEta + (i0 + lm) + (size_t)ny * lk;
-      double xa[K16 / 4];
+      constexpr int EC = NKB > 4 ? 16 : K16 / 4;  // operand steps loaded at once
 #pragma unroll
-      for (int s4 = 0; s4 < K16 / 4; ++s4) xa[s4] = xp[(size_t)ny * 4 * s4];
+      for (int c0 = 0; c0 < K16 / 4; c0 += EC) {
+        double xa[EC];
 #pragma unroll
-      for (int s4 = 0; s4 < K16 / 4; ++s4) {
-        const int k = 4 * s4 + lk;
-        if (MODE & 1) {
-          e0 = mfma_f64(xa[s4], sBL[k * ZT_J + 2 * lm], e0);
-          e1 = mfma_f64(xa[s4], sBL[k * ZT_J + 2 * lm + 1], e1);
-        } else {
-          e0[s4 & 3] += xa[s4];
+        for (int s4 = 0; s4 < EC; ++s4) xa[s4] = xp[(size_t)ny * 4 * (c0 + s4)];
+#pragma unroll
+        for (int s4 = 0; s4 < EC; ++s4) {
+          const int k = 4 * (c0 + s4) + lk;
+          if (MODE & 1) {
+            e0 = mfma_f64(xa[s4], sBL[k * ZT_J + 2 * lm], e0);
+            e1 = mfma_f64(xa[s4], sBL[k * ZT_J + 2 * lm + 1], e1);
+          } else {
+            e0[s4 & 3] += xa[s4];
+          }
         }
       }
 #pragma unroll
@@ -560,7 +567,36 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
     wave_lds_sync();
     // ---- XZ += XEta^T (Yx o Z) over the 16 sites (R/updateBetaLambda.R:66 of the next sweep);
     //      B operand = Z[site lk+4r][species 2lm+b] from the tile
-    if (MODE & 4) {
+    if ((MODE & 4) && NKB > 4) {  // 64 rows of A operands at a time
+      double zz[4][2];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ir = i0 + 4 * r + lk;
+        zz[r][0] = sT[(2 * lm) * ZT_TLD + lk + 4 * r];
+        zz[r][1] = sT[(2 * lm + 1) * ZT_TLD + lk + 4 * r];
+        if (HAS_NA && a.mask_na) {
+          const uint64_t w2 = a.Ybits[(size_t)by * ny + ir];
+          if (((w2 >> (4 * lm)) & 3u) == 0) zz[r][0] = 0.0;
+          if (((w2 >> (4 * lm + 2)) & 3u) == 0) zz[r][1] = 0.0;
+        }
+      }
+      const double* xq = a.XEta + (i0 + lk) + (size_t)ny * lm;
+#pragma unroll
+      for (int q0 = 0; q0 < NKB; q0 += 4) {
+        double xt[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) xt[r][q] = xq[4 * r + (size_t)ny * 16 * (q0 + q)];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            acc[q0 + q][0] = mfma_f64(xt[r][q], zz[r][0], acc[q0 + q][0]);
+            acc[q0 + q][1] = mfma_f64(xt[r][q], zz[r][1], acc[q0 + q][1]);
+          }
+      }
+    } else if (MODE & 4) {
       // A operands (XEta^T rows) of all 4 x NKB MFMAs loaded first: one latency per tile
       double xt[4][NKB];
       const double* xq = a.XEta + (i0 + lk) + (size_t)ny * lm;
@@ -587,44 +623,54 @@ __global__ __launch_bounds__(256, 4) void z_wave_kernel(ZArgs a) {
     }
     wave_lds_sync();
   }
-  // combine the 4 waves' XZ and write this chunk's partial
-  __syncthreads();
-  double* sR = smem;  // [w-1][K16][32] (reuses the whole workgroup's LDS)
-  if (w > 0) {
+  // combine the 4 waves' XZ and write this chunk's partial, 64 rows (4 blocks) at a time
+  constexpr int QC = NKB > 4 ? 4 : NKB, KC = 16 * QC;
+  double* sR = smem;  // [w-1][KC][32] (reuses the whole workgroup's LDS)
 #pragma unroll
-    for (int q = 0; q < NKB; ++q)
+  for (int q0 = 0; q0 < NKB; q0 += QC) {
+    __syncthreads();
+    if (w > 0) {
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+      for (int q = 0; q < QC; ++q)
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
-          sR[((w - 1) * K16 + 16 * q + lk + 4 * rr) * ZT_J + 2 * lm + b] = acc[q][b][rr];
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr)
+            sR[((w - 1) * KC + 16 * q + lk + 4 * rr) * ZT_J + 2 * lm + b] = acc[q0 + q][b][rr];
+    }
+    __syncthreads();
+    if (w == 0) {
+      double* dst = a.XZ_part + (size_t)chunk * K * a.ns_loc;
+#pragma unroll
+      for (int q = 0; q < QC; ++q)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const int kl = 16 * q + lk + 4 * rr, k = 16 * q0 + kl, jj = 2 * lm + b, j = j0 + jj;
+            const double v = acc[q0 + q][b][rr] + sR[(0 * KC + kl) * ZT_J + jj] + sR[(1 * KC + kl) * ZT_J + jj] +
+                             sR[(2 * KC + kl) * ZT_J + jj];
+            if (k < K && j < a.ns_loc) dst[k + (size_t)K * j] = v;
+          }
+    }
   }
-  __syncthreads();
-  if (w == 0) {
-    double* dst = a.XZ_part + (size_t)chunk * K * a.ns_loc;
-#pragma unroll
-    for (int q = 0; q < NKB; ++q)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int k = 16 * q + lk + 4 * rr, jj = 2 * lm + b, j = j0 + jj;
-          const double v = acc[q][b][rr] + sR[(0 * K16 + k) * ZT_J + jj] + sR[(1 * K16 + k) * ZT_J + jj] +
-                           sR[(2 * K16 + k) * ZT_J + jj];
-          if (k < K && j < a.ns_loc) dst[k + (size_t)K * j] = v;
-        }
-    if (a.kt && t == 0) kt_record(a.kt, iter, kt0);
-  }
+  if (w == 0 && a.kt && t == 0) kt_record(a.kt, iter, kt0);
 }
 
 // launch geometry shared by the launcher and the microbenchmark
-inline int z_nkb(int K) { return (K + 15) / 16; }
+// 16-row blocks of the instantiation serving K: 1 .. 4, or 8 for 64 < K <= 128
+inline int z_nkb(int K) {
+  const int n = (K + 15) / 16;
+  return n > 4 ? 8 : n;
+}
+// XEta columns the z kernel reads (rows past K meet zero BL rows / are discarded)
+inline int z_xeta_cols(int Kmax) { return 16 * z_nkb(Kmax); }
 
 inline size_t z_smem_bytes(int K, int nt) {
   const size_t K16 = 16 * (size_t)z_nkb(K);
   const size_t body = K16 * ZT_J + (size_t)ZT_J * nt + 2 * ZT_J + ZT_J / 2 + ZLOG_W * (size_t)ZLOG_N + ZT_DOUBLES +
                       4 * (size_t)ZT_J * ZT_TLD;  // doubles
-  const size_t red = 3 * K16 * ZT_J;                                                                   // wave combine
+  const size_t red = 3 * (K16 > 64 ? 64 : K16) * ZT_J;                                                   // wave combine
   return (body > red ? body : red) * sizeof(double);
 }
 

@@ -26,7 +26,8 @@ static void z_dispatch_k(const State& s, dim3 grid, size_t smem, const ZArgs& a)
     case 1: z_wave_kernel<DRAW, HAS_NA, 1, M, POIS, NORMAL><<<grid, 256, smem, s.stream>>>(a); break;
     case 2: z_wave_kernel<DRAW, HAS_NA, 2, M, POIS, NORMAL><<<grid, 256, smem, s.stream>>>(a); break;
     case 3: z_wave_kernel<DRAW, HAS_NA, 3, M, POIS, NORMAL><<<grid, 256, smem, s.stream>>>(a); break;
-    default: z_wave_kernel<DRAW, HAS_NA, 4, M, POIS, NORMAL><<<grid, 256, smem, s.stream>>>(a); break;
+    case 4: z_wave_kernel<DRAW, HAS_NA, 4, M, POIS, NORMAL><<<grid, 256, smem, s.stream>>>(a); break;
+    default: z_wave_kernel<DRAW, HAS_NA, 8, M, POIS, NORMAL><<<grid, 256, smem, s.stream>>>(a); break;
   }
 }
 
@@ -45,10 +46,13 @@ static int z_occupancy(int nkb, size_t smem) {
     case 1: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 1, z_mode<HAS_NA>()>, 256, smem)); break;
     case 2: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 2, z_mode<HAS_NA>()>, 256, smem)); break;
     case 3: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 3, z_mode<HAS_NA>()>, 256, smem)); break;
-    default: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 4, z_mode<HAS_NA>()>, 256, smem)); break;
+    case 4: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 4, z_mode<HAS_NA>()>, 256, smem)); break;
+    default: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, z_wave_kernel<true, HAS_NA, 8, z_mode<HAS_NA>()>, 256, smem)); break;
   }
   return nb;
 }
+
+int z_xeta_cols_for(int Kmax) { return z_xeta_cols(Kmax); }
 
 // Workgroups of the drawing z kernel resident on the whole device at once (occupancy x CUs):
 // the site-chunk count is sized so the (chunk x species-block) grid fills exactly one round.
@@ -62,7 +66,7 @@ int z_resident_slots(const State& s) {
 }
 
 static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
-  HMSC_REQUIRE(s.K <= KMAX_Z, "updateZ: K = nc + sum(nf) must be <= 64 in this build");
+  HMSC_REQUIRE(s.K <= KMAX_Z, "updateZ: K = nc + sum(nf) must be <= 128 in this build");
   HMSC_REQUIRE((s.sp0 & 1) == 0, "updateZ: species shards must start at an even species (Philox pairs)");
   if (!s.xeta_valid) launch_xeta(s);
   ZArgs a{};

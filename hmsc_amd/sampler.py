@@ -157,13 +157,19 @@ class Chain:
     """One chain's device-resident state (hmsc_create ... hmsc_destroy)."""
 
     def __init__(self, hM, seed, device=0, updater=None, rank=0, nranks=1, comm_id=None, mask=None,
-                 host_allreduce=None, spatial_grid="device"):
+                 host_allreduce=None, spatial_grid="device", nf_capacity="warn"):
         """A species-sharded chain (rank of nranks, two all-reduces per sweep) is created when
         comm_id (an RCCL unique id, hmsc_comm_unique_id) or host_allreduce is given -- also at
         nranks = 1, where it runs the sharded kernels and collectives on one GPU.
         host_allreduce: a callable f(x) that replaces the float64 array x by its sum over all
         ranks, in place (hmsc_create_sharded_host; RCCL is not used).
-        spatial_grid: where a 'Full' level's alphapw grid is evaluated (ModelBuffers)."""
+        spatial_grid: where a 'Full' level's alphapw grid is evaluated (ModelBuffers).
+        nf_capacity: what to do when a level's nfMax exceeds what the device holds (K = nc +
+        sum(nf) <= 128, hmsc_get_nf_cap): "warn" (hold nfMax at the capacity; the chain stops
+        with an error only if updateNf must grow a level past it), "error" (refuse the model
+        here) or "ignore" (hold it at the capacity silently)."""
+        if nf_capacity not in ("warn", "error", "ignore"):
+            raise ValueError("nf_capacity must be 'warn', 'error' or 'ignore'")
         self.hM = hM
         self.lib = L.lib()
         self.buf = ModelBuffers(hM, spatial_grid=spatial_grid)
@@ -194,14 +200,20 @@ class Chain:
         cap = np.array(self.buf.nfMax + [0] * (L.MAX_LEVELS - len(self.buf.nfMax)), dtype=np.int32)
         if hasattr(self.lib, "hmsc_get_nf_cap"):  # (a pre-round-4 library strides records by nfMax)
             L.check(self.lib.hmsc_get_nf_cap(self.h, L.iptr(cap)))
-        # factors each level's device buffers and record slots hold (K = nc + sum(nf) <= 64)
+        # factors each level's device buffers and record slots hold (K = nc + sum(nf) <= 128; the
+        # capacity past every level's nfMin is shared between the levels)
         self.nf_cap = [int(c) for c in cap[: hM.nr]]
         short = [(r, self.buf.nfMax[r], c) for r, c in enumerate(self.nf_cap) if c < self.buf.nfMax[r]]
-        if short and rank == 0:
-            import warnings
-            warnings.warn("nfMax " + ", ".join(f"{m} of level {r + 1} held as {c}" for r, m, c in short) +
-                          ": this build holds K = nc + sum(nf) <= 64 latent dimensions; the chain stops "
-                          "with an error only if updateNf must grow a level past that", stacklevel=2)
+        if short:
+            msg = ("nfMax " + ", ".join(f"{m} of level {r + 1} held as {c}" for r, m, c in short) +
+                   ": this build holds K = nc + sum(nf) <= 128 latent dimensions")
+            if nf_capacity == "error":
+                self.close()
+                raise ValueError(msg + "; set nfMax with setPriors (or pass nf_capacity='warn')")
+            if nf_capacity == "warn" and rank == 0:
+                import warnings
+                warnings.warn(msg + "; the chain stops with an error only if updateNf must grow a level past "
+                              "that", stacklevel=2)
 
     def close(self):
         if self.h:
@@ -489,7 +501,7 @@ def alignPosterior(hM):
 # ---------------------------------------------------------------------------
 def sampleMcmc(hM, samples, transient=0, thin=1, initPar=None, verbose=None, adaptNf=None, nChains=1,
                nParallel=1, dataParList=None, updater=None, fromPrior=False, alignPost=True, seed=None,
-               devices=None):
+               devices=None, nf_capacity="warn"):
     if not isinstance(hM, Hmsc):
         raise TypeError("sampleMcmc: hM must be an Hmsc object")
     if verbose is None:
@@ -548,7 +560,8 @@ def sampleMcmc(hM, samples, transient=0, thin=1, initPar=None, verbose=None, ada
     def make_chain(c):
         if nChains > 1:
             print(f'[1] "Computing chain {c + 1}"')
-        ch = Chain(hM, int(initSeed[c]), device=devices[c % len(devices)], updater=updater)
+        ch = Chain(hM, int(initSeed[c]), device=devices[c % len(devices)], updater=updater,
+                   nf_capacity=nf_capacity if c == 0 else "ignore")
         try:
             ch.init(nf0)
             if initPar is not None:

@@ -1,15 +1,21 @@
 #!/bin/bash
-# A/B on one box: bench.py under two environment settings, interleaved, twice each.
-#   bash scripts/ab_env.sh "HMSC_GRAPH_EXECS=1" "HMSC_GRAPH_EXECS=2"
+# Same-box A/B of environment settings: bench.py (config 4, STEPS steps) alternately under each
+# setting given on the command line ("-" = none, else VAR=value[,VAR=value]), ROUNDS rounds.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-mkdir -p $R/gpurun_out
-cd $R
-for rep in 1 2; do
+ROUNDS=${ROUNDS:-2}
+STEPS=${STEPS:-1000}
+mkdir -p $R/gpurun_out/ab
+for r in $(seq 1 $ROUNDS); do
   i=0
-  for e in "$@"; do
+  for setting in "$@"; do
     i=$((i+1))
-    env $e timeout -k 10 300 python bench.py --steps ${STEPS:-1000} --warmup 30 --no-cpu > gpurun_out/abe_${i}_${rep}.json 2>gpurun_out/abe.err || { tail -5 gpurun_out/abe.err; exit 1; }
-    python -c "import json; d=json.load(open('gpurun_out/abe_${i}_${rep}.json')); print('$e', d['value'], d['ms_per_step'])"
+    envs=()
+    [ "$setting" != "-" ] && IFS=, read -ra envs <<< "$setting"
+    env "${envs[@]}" timeout -k 10 200 python -u $R/bench.py --steps $STEPS --warmup 100 --no-cpu --no-sharded-leg \
+      > $R/gpurun_out/ab/env$i.$r.json 2> $R/gpurun_out/ab/env$i.$r.err || { echo "bench failed: $setting"; exit 1; }
+    python3 -c "
+import json; d=json.loads(open('$R/gpurun_out/ab/env$i.$r.json').read().strip().splitlines()[-1])
+print('$setting', $r, d['value'], d['kernels_live_us'])"
   done
 done

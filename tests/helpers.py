@@ -14,7 +14,7 @@ from oracle import hmsc_oracle as O  # noqa: E402
 
 def synthetic_model(ny=200, ns=30, nc=4, nf=3, seed=1, na_frac=0.0, n_normal=0, units=None, nr=1,
                     nf_fit=None, nt=1, yscale=False, C=None, n_poisson=0, n_lognormal=0, spatial=None,
-                    alpha_n=None, spatial_method="Full", n_neighbours=None, n_knots=None):
+                    alpha_n=None, spatial_method="Full", n_neighbours=None, n_knots=None, nf_default=False):
     """Probit JSDM generated like BASELINE.md's synthetic config; optionally the first
     n_normal species normal, the next n_poisson Poisson and n_lognormal lognormal Poisson
     (counts ~ Poisson(exp(L / 2)), vignette_2's mixed-distribution model)."""
@@ -53,7 +53,8 @@ def synthetic_model(ny=200, ns=30, nc=4, nf=3, seed=1, na_frac=0.0, n_normal=0, 
             sd[name] = np.array([f"u{k}" for k in pi])
             rl = H.HmscRandomLevel(units=sd[name])
         nff = nf if nf_fit is None else nf_fit
-        H.setPriors(rl, nfMin=nff, nfMax=nff)
+        if not nf_default:  # (nf_default: the reference's priors, nfMin 2 and nfMax Inf = ns)
+            H.setPriors(rl, nfMin=nff, nfMax=nff)
         ranLevels[name] = rl
         levels[name] = pi
     Ylat = L + rng.standard_normal((ny, ns))
