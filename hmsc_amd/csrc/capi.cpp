@@ -768,7 +768,8 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   {  // crw_kernel: 4 parts x 4 tiles x 16 x 16; bl_tail: (nbl + ngroups) tiles of CRW_TILE (520)
     const size_t nbl = (size_t)(nsl + 3) / 4, ngr = (nbl + 15) / 16;
     s.crw_part = dalloc<double>(std::max((size_t)4 * 4 * 256, (nbl + ngr) * 520));
-    s.crw_ticket = dalloc<int>(2 + ngr);  // dalloc zero-fills
+    s.crw_ticket = dalloc<int>(3 + ngr);  // dalloc zero-fills
+    s.crw_flag = s.crw_ticket + 2 + ngr;
     s.gvt_ld = nc * nc + N + nfm;             // [A nc^2 | BTr nc nt | rs NF]
     s.gvt = dalloc<double>((nbl + ngr) * (size_t)s.gvt_ld);
   }
@@ -1075,6 +1076,7 @@ static void set_state(State& s, const hmsc_params* p) {
   }
   HIP_OK(hipStreamSynchronize(s.stream));
   s.zt_valid = false;
+  s.xz_parts = 0;
   s.xeta_valid = false;
   s.g2prep_valid = false;
   s.g2s_valid = false;
@@ -1194,6 +1196,7 @@ static void update_nf(State& s, int r, uint32_t iter) {
   }
   s.refresh_dims();
   s.zt_valid = false;
+  s.xz_parts = 0;
   s.xeta_valid = false;
   s.g2s_valid = false;
   s.graph_dirty = true;
@@ -1353,6 +1356,7 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
   std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
   join_side(s);
   const bool xv = s.xeta_valid, zv = s.zt_valid, gv = s.g2prep_valid, gp = s.g_pending, g2v = s.g2s_valid;
+  const int xzp = s.xz_parts;
   hipGraph_t g = nullptr;
   std::vector<std::pair<hipGraph_t, size_t>> parts;  // (host transport) the segments so far
   auto drop_parts = [&] {
@@ -1401,6 +1405,7 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
     if (g) (void)hipGraphDestroy(g);
     drop_parts();
     s.xeta_valid = xv, s.zt_valid = zv, s.g2prep_valid = gv, s.g_pending = gp, s.g2s_valid = g2v;
+    s.xz_parts = xzp;
     throw;
   }
   s.capturing = false;
@@ -1409,8 +1414,9 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
   s.edge_free_now = false;
   HIP_OK(hipStreamEndCapture(s.stream, &g));
   const bool steady = xv == s.xeta_valid && zv == s.zt_valid && gv == s.g2prep_valid && gp == s.g_pending &&
-                      g2v == s.g2s_valid;
+                      g2v == s.g2s_valid && xzp == s.xz_parts;
   s.xeta_valid = xv, s.zt_valid = zv, s.g2prep_valid = gv, s.g_pending = gp, s.g2s_valid = g2v;  // nothing ran yet
+  s.xz_parts = xzp;
   if (s.sharded && !with_record) s.ar_per_graph_sweep = s.ar_in_capture / std::max(1, nsweeps);
   size_t nodes = 0;
   HIP_OK(hipGraphGetNodes(g, nullptr, &nodes));
@@ -1806,6 +1812,7 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
   // (the same for the tails epoch and the side chain's flags, graph sweeps' device-side joins)
   join_side(s);
   if (s.gbl_sync) HIP_OK(hipMemsetAsync(s.gbl_sync + 1, 0, 2 * sizeof(int), s.stream));
+  if (s.crw_flag) HIP_OK(hipMemsetAsync(s.crw_flag, 0, sizeof(int), s.stream));
   if (s.side_sync) HIP_OK(hipMemsetAsync(s.side_sync, 0, (2 + HMSC_MAX_LEVELS) * sizeof(int), s.stream));
   const auto t_start = std::chrono::steady_clock::now();
   int n_replays = 0;
@@ -2249,7 +2256,7 @@ int hmsc_debug_get(hmsc_state* h, const char* name, double* out, int64_t n) {
     const double* src = nullptr;
     int64_t avail = 0;
     if (nm == "Z") src = s.Z, avail = (int64_t)s.ny * s.nsl;
-    else if (nm == "XZ") src = s.XZ, avail = (int64_t)s.K * s.nsl;
+    else if (nm == "XZ") flush_xz(s), src = s.XZ, avail = (int64_t)s.K * s.nsl;
     else if (nm == "G") flush_g(s), src = s.G, avail = (int64_t)s.Kmax * s.Kmax;
     else if (nm == "ZTr") src = s.ZTr, avail = (int64_t)s.ny * s.nt;
     else if (nm == "BL") src = s.BL, avail = (int64_t)s.K * s.nsl;

