@@ -22,7 +22,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libhmsc_amd.so")
 SOURCES = ["kernels.hip", "zdraw.hip", "dense.hip", "phylo.hip", "gamma_eta.hip", "spatial.hip", "predict.hip", "post.hip",
            "capi.cpp"]
-HEADERS = ["common.h", "rng.h", "state.h", "wave_la.h", "z_kernel.h", "z_tables.h", os.path.join("..", "..", "include", "hmsc_amd.h")]
+HEADERS = ["common.h", "rng.h", "state.h", "wave_la.h", "z_kernel.h", "z_tables.h", "record.h", os.path.join("..", "..", "include", "hmsc_amd.h")]
 ARCH = os.environ.get("HMSC_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-fPIC", "-std=c++17", "-pthread", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",

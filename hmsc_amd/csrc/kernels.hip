@@ -2724,7 +2724,9 @@ static_assert(ef_lds_doubles<8>() >= 4 * CRW_TILE + 32 * 16 + 256, "EF_DEFER red
 // __launch_bounds__(256, 3): <= 168 VGPRs, three waves per SIMD, so the 625 workgroups of the
 // synthetic config (2500 waves) are resident in one round (at 196 VGPRs they took two: 33 ->
 // 29 us).  A fifth wave doing the Z-independent work during the stream measured slower (49 us).
-// The stream's depth: EF_DEPTH 16-species steps' loads in flight per lane before their MFMAs.
+// The stream's depth: EF_DEPTH 16-species steps' loads in flight per lane before their MFMAs
+// (16, and a software-pipelined stream of two 6- or 8-step batches, measured the same within
+// 1 %: the stream is not bound by the loads a wave has in flight, profiles/r05_eta_ab.txt).
 #ifndef EF_DEPTH
 #define EF_DEPTH 12
 #endif
