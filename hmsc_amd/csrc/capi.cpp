@@ -842,6 +842,9 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.d_iter_side = dalloc<uint32_t>(1);
   s.gv_part = dalloc<double>((size_t)((nsl + 31) / 32) * (nc * nc + nc * nt));
   HIP_OK(hipEventCreateWithFlags(&s.ev_graph, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&s.ev_ext, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&s.ev_ext_go, hipEventDisableTiming));
+  s.d_ext_iter = dalloc<uint32_t>(64);
   {
     const char* g1 = getenv("HMSC_SINGLE_STREAM");
     s.single_stream = g1 && g1[0] == '1';
@@ -894,6 +897,8 @@ static void free_state(State& s) {
   if (s.ev_bl) (void)hipEventDestroy(s.ev_bl);
   if (s.ev_side) (void)hipEventDestroy(s.ev_side);
   if (s.ev_side2) (void)hipEventDestroy(s.ev_side2);
+  if (s.ev_ext) (void)hipEventDestroy(s.ev_ext);
+  if (s.ev_ext_go) (void)hipEventDestroy(s.ev_ext_go);
   if (s.side) (void)hipStreamDestroy(s.side);
   if (s.side2) (void)hipStreamDestroy(s.side2);
   if (s.stream) (void)hipStreamDestroy(s.stream);
@@ -1312,7 +1317,10 @@ static void sweep(State& s, uint32_t iter, bool adapt) {
 // replay).  With co-launched side updaters the side stream's outputs are packed on it, so
 // the main stream need not wait for the GammaV algebra.
 static void record_after_sweep(State& s, double* slot) {
-  if (s.side_fused && (s.side_pending & 1)) {
+  if (s.ext_pending && s.capturing && s.cap_sweep == 0) {  // the first sweep's side work is external
+    if (!s.pack_done) launch_record(s, slot, 1);
+    ext_add_record(s);
+  } else if (s.side_fused && (s.side_pending & 1)) {
     if (!s.pack_done) launch_record(s, slot, 1);  // else updateZ's slab-sum launch packed it
     launch_record(s, slot, 2);
   } else {
@@ -1335,6 +1343,8 @@ static void destroy_graph(State& s) {
       if (g) (void)hipGraphExecDestroy(g);
       g = nullptr;
     }
+  for (auto& row : s.ext_side)
+    for (auto& f : row) f = nullptr;
   for (auto& v : s.gseg) {
     for (auto& g : v)
       if (g.g) (void)hipGraphExecDestroy(g.g);
@@ -1396,6 +1406,7 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
   } catch (...) {
     s.cap_sweep = -1;
     s.side_root = false;
+    s.ext_pending = nullptr;
     s.d_iter = s.d_iters;
     s.pack_req = s.pack_done = false;
     s.capturing = false;
@@ -1456,6 +1467,9 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
   }
   if (steady && nodes <= graph_max_nodes()) HIP_OK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
   HIP_OK(hipGraphDestroy(g));
+  // the first sweep's side work, if it was left out of the graph, goes with it
+  s.ext_side[with_record ? 1 : 0][graph_level(nsweeps)] = ge ? std::move(s.ext_pending) : nullptr;
+  s.ext_pending = nullptr;
   return ge;
 }
 
@@ -1547,6 +1561,19 @@ static bool replay_sweeps(State& s, uint32_t iter, bool with_record, int n) {
   if (!ge) return false;
   join_side(s);
   set_iters_kernel<<<1, 64, 0, s.stream>>>(s.d_iters, iter, n);
+  if (const auto& ext = s.ext_side[with_record ? 1 : 0][graph_level(n)]) {
+    // the replay's first side chain, on the side stream ahead of the graph (State::ext_side):
+    // it waits on the device for that sweep's tails flag like the graph's own side chains
+    // (behind the replay's start on the main stream: enqueued early, it would otherwise hold
+    // its CU slots spinning through the previous replay)
+    HIP_OK(hipEventRecord(s.ev_ext_go, s.stream));
+    HIP_OK(hipStreamWaitEvent(s.side, s.ev_ext_go, 0));
+    set_iters_kernel<<<1, 64, 0, s.side>>>(s.d_ext_iter, iter, 1);
+    ext();
+    HIP_OK(hipEventRecord(s.ev_ext, s.side));
+    s.side_pending |= 1;
+    s.ext_launched = true;
+  }
   HIP_OK(hipGraphLaunch(ge, s.stream));
   if (s.sharded && s.ar_per_graph_sweep > 0) s.ar_calls += (uint64_t)s.ar_per_graph_sweep * n;  // (RCCL: captured)
   return true;
@@ -1846,6 +1873,8 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
         if (klast >= 0) {
           HIP_OK(hipEventRecord(s.ev_graph, s.stream));
           HIP_OK(hipStreamWaitEvent(s.copy_stream, s.ev_graph, 0));
+          if (s.ext_launched) HIP_OK(hipStreamWaitEvent(s.copy_stream, s.ev_ext, 0));  // its record pack
+          s.ext_launched = false;
           // the replay's samples in one copy per contiguous run of ring slots (at most two),
           // then one flag: a copy + flag per sample cost ~48 us of copy-engine and dispatch
           // time each (26 us of transfer), so a 32-sweep replay's copies backed up behind the

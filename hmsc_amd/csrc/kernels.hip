@@ -3101,15 +3101,29 @@ void launch_side_fused(State& s, uint32_t iter) {
   // the GammaV algebra (writes Gamma, iV and Gamma2's prep) with the delta chains as extra
   // workgroups of the same launch
   const int* tf = (dev_fork && tail) ? s.gbl_sync + 2 : nullptr;  // (else post_bl_kernel waited)
-  switch (wv_bucket_gv(s.nc * s.nt)) {
-    case 8: launch_side_chain<8>(s, gw, lp, rs, nparts, rs_ld, tf); break;
-    case 16: launch_side_chain<16>(s, gw, lp, rs, nparts, rs_ld, tf); break;
-    case 20: launch_side_chain<20>(s, gw, lp, rs, nparts, rs_ld, tf); break;
-    case 24: launch_side_chain<24>(s, gw, lp, rs, nparts, rs_ld, tf); break;
-    default: launch_side_chain<32>(s, gw, lp, rs, nparts, rs_ld, tf); break;
-  }
-  HIP_OK(hipGetLastError());
+  auto launch = [&s](GVWArgs g, LPArgs l, const double* r, int np, int ld, const int* f) {
+    switch (wv_bucket_gv(s.nc * s.nt)) {
+      case 8: launch_side_chain<8>(s, g, l, r, np, ld, f); break;
+      case 16: launch_side_chain<16>(s, g, l, r, np, ld, f); break;
+      case 20: launch_side_chain<20>(s, g, l, r, np, ld, f); break;
+      case 24: launch_side_chain<24>(s, g, l, r, np, ld, f); break;
+      default: launch_side_chain<32>(s, g, l, r, np, ld, f); break;
+    }
+    HIP_OK(hipGetLastError());
+  };
   if (gw.do_prep) s.g2prep_valid = true;
+  // a capture's first sweep, side stream forked at the root: the side chain is left out of the
+  // graph and launched ahead of each replay (State::ext_side), reading the sweep counter the
+  // replay writes to d_ext_iter
+  if (s.capturing && s.cap_sweep == 0 && s.side_root && dev_fork && tail && !getenv_flag("HMSC_NO_EXT_SIDE")) {
+    GVWArgs g2 = gw;
+    LPArgs l2 = lp;
+    g2.iter_dev = s.d_ext_iter;
+    l2.iter_dev = s.d_ext_iter;
+    s.ext_pending = [launch, g2, l2, rs, nparts, rs_ld, tf] { launch(g2, l2, rs, nparts, rs_ld, tf); };
+    return;
+  }
+  launch(gw, lp, rs, nparts, rs_ld, tf);
   s.side_pending |= 1;  // joined (ev_side recorded) by the next join_side
 }
 
@@ -3660,6 +3674,18 @@ static PackArgs make_pack_args(State& s, double* slot, int part) {
 }
 
 PackArgs record_pack_args(State& s, int part) { return make_pack_args(s, nullptr, part); }
+
+// the external first-sweep side work (State::ext_side) also packs the record's side pieces
+void ext_add_record(State& s) {
+  PackArgs a = make_pack_args(s, nullptr, 2);
+  a.iter_dev = s.d_ext_iter;
+  auto prev = std::move(s.ext_pending);
+  s.ext_pending = [prev, a, &s] {
+    prev();
+    pack_kernel<<<8, 256, 0, s.side>>>(a);
+    HIP_OK(hipGetLastError());
+  };
+}
 
 void launch_record(State& s, double* slot, int part) {
   const PackArgs a = make_pack_args(s, slot, part);

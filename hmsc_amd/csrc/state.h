@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <functional>
 #include <memory>
 #include <vector>
 
@@ -244,6 +245,17 @@ struct State {
   // log2(graph_sweeps); a run of n sweeps replays its binary decomposition, largest first
   static constexpr int GRAPH_LEVELS = 7;  // up to 64 sweeps per replay
   hipGraphExec_t gx[2][GRAPH_LEVELS] = {};
+  // The first sweep of a replay's side work (side chain [+ record pack part 2]) runs outside
+  // the graph: a graph launch submits its side-stream nodes only after all its main-stream
+  // nodes (~16 us of host time per sweep), so that sweep's side chain started late and the
+  // next sweep's fused launch waited for it.  capture_sweeps keeps it as a closure per graph
+  // (ext_side, launched on the side stream ahead of the graph by replay_sweeps) instead.
+  std::function<void()> ext_pending;                // built while capturing sweep 0
+  std::function<void()> ext_side[2][GRAPH_LEVELS];  // per graph in gx
+  uint32_t* d_ext_iter = nullptr;                   // the external side work's sweep counter
+  hipEvent_t ev_ext = nullptr;                      // after it: the record copy waits on it
+  hipEvent_t ev_ext_go = nullptr;                   // the replay's start, which it waits behind
+  bool ext_launched = false;
   bool single_stream = false;          // HMSC_SINGLE_STREAM: no side-stream overlap (diagnostic)
   int graph_sweeps = 4;                 // sweeps per replay, a power of two (HMSC_GRAPH_SWEEPS)
   uint32_t dev_iter_next = 0;           // the sweep the device's d_iters slots already hold (valid_iters)
@@ -361,6 +373,7 @@ void launch_zt_refresh(State& s);
 int z_resident_slots(const State& s);
 int z_xeta_cols_for(int Kmax);  // XEta columns the z kernel reads (zdraw.hip)
 void flush_xz(State& s);        // reduce XZ from its chunk partials if they are pending (kernels.hip)
+void ext_add_record(State& s);  // add record pack part 2 to the external first-sweep side work (kernels.hip)
 void launch_xeta(State& s);
 void flush_g(State& s);
 void launch_slab_sum2(const double* p0, double* o0, int64_t n0, int np0, const double* p1, double* o1, int64_t n1,
