@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 config 3 / config 5 bench lines with their CPU baselines (numpy restatement).
+# Config 3 / config 5 bench lines with their CPU baselines (numpy restatement), into gpurun_out/cfg.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/gpurun_out/cfg
