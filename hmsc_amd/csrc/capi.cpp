@@ -575,14 +575,14 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
         HMSC_REQUIRE(bad == 0, "spatial level: a grid matrix W_g = exp(-d / alpha_g) is not positive definite "
                                "(duplicated coordinates?)");
       }
-      {  // the spatial workspace (for NNGP the band is still held in a full (np nf)^2 array):
+      {  // the spatial workspace (NNGP: the band in its tile-band layout, np nf x (bw + 128)):
          // a clear create-time error instead of an allocation failure mid-setup
         const size_t need = spatial_work_doubles(s, r) * sizeof(double);
         size_t free_b = 0, total_b = 0;
         HIP_OK(hipMemGetInfo(&free_b, &total_b));
         HMSC_REQUIRE(need < free_b, "spatial level " + std::to_string(r) + ": its workspace needs " +
                                         std::to_string(need >> 20) + " MiB (the " +
-                                        (L.nngp ? std::string("NNGP band is stored as a full (np nf)^2 array") :
+                                        (L.nngp ? std::string("NNGP band matrix, np nf x (bw + 128)") :
                                                   std::string("(np nf)^2 dense system")) +
                                         "), " + std::to_string(free_b >> 20) + " MiB free on the device");
       }
@@ -2301,6 +2301,11 @@ int hmsc_debug_get(hmsc_state* h, const char* name, double* out, int64_t n) {
       std::vector<unsigned long long> v((size_t)m);
       copy_sync(v.data(), s.d_kt, sizeof(unsigned long long) * m, hipMemcpyDeviceToHost, s.stream);
       for (int64_t i = 0; i < m; ++i) out[i] = (double)v[i];
+      return;
+    } else if (nm.rfind("spwork_doubles", 0) == 0) {  // a spatial level's workspace size (doubles)
+      const int r = std::atoi(nm.c_str() + 14);
+      HMSC_REQUIRE(r >= 0 && r < s.nr && s.lev[r].spatial && n >= 1, "debug_get: not a spatial level");
+      out[0] = (double)spatial_work_doubles(s, r);
       return;
     } else if (nm.rfind("nngp_perm", 0) == 0 || nm.rfind("nngp_bw", 0) == 0) {  // NNGP factorization order
       const bool perm = nm.rfind("nngp_perm", 0) == 0;

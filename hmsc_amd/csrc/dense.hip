@@ -43,6 +43,15 @@ namespace hmsc {
 constexpr int DB = 64;       // panel / tile size
 constexpr int DLD = DB + 1;  // padded LDS leading dimension
 
+// Element (r, c) of a matrix argument.  ld > 0: column-major with leading dimension ld.  ld < 0:
+// the tile-band layout of a band matrix (dense_band_ld, state.h): each 64-column panel J is a
+// (-ld) x 64 column-major block holding rows 64 J .. 64 J - ld - 1, i.e. element (r, c) at
+// (r - 64 J) + (-ld) c -- N (bw + 128) doubles instead of N^2.  The factorization and the
+// solves touch only tiles inside the band (their bw restriction), which that block holds whole.
+__device__ __forceinline__ size_t aix(int ld, int r, int c) {
+  return ld > 0 ? (size_t)r + (size_t)ld * c : (size_t)(r - (c & ~(DB - 1))) + (size_t)(-ld) * c;
+}
+
 // Every in-launch handshake of this file (the sync-free solve's block flags, the fused
 // panel's diagonal-inverse flag) is bounded in time: a wait that outlasts HS_TIMEOUT_TICKS of
 // the 100 MHz wall clock (common.h) raises its bit in the sync block's error word
@@ -94,7 +103,7 @@ __device__ __forceinline__ void panel_load(const double* A, int lda, int R0, int
 #pragma unroll
   for (int u = 0; u < ROWS * DB / 256; ++u) {
     const int p = threadIdx.x + 256 * u, r = p % ROWS, c = p / ROWS;
-    v[u] = A[(size_t)(R0 + min(r, rows - 1)) + (size_t)lda * (k0 + min(c, nb - 1))];
+    v[u] = A[aix(lda, R0 + min(r, rows - 1), k0 + min(c, nb - 1))];
   }
 }
 
@@ -324,7 +333,7 @@ __device__ inline void diag_body(double* T, double* I, double (*S)[16 * 17], dou
 #pragma unroll
     for (int u = 0; u < DB * DB / 256; ++u) {
       const int p = t + 256 * u, r = p & 63, c = p >> 6;
-      if (r < nb && c < nb && r >= c) A[(size_t)(k0 + r) + (size_t)lda * (k0 + c)] = tv[u];
+      if (r < nb && c < nb && r >= c) A[aix(lda, k0 + r, k0 + c)] = tv[u];
     }
   }
   if (t == 0 && bad) atomicExch(info, 1);
@@ -390,7 +399,7 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(double* A, int lda, int
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int c = 16 * ct + lk + 4 * q;
-      if (r < rows && c < nb) A[(size_t)(i0 + r) + (size_t)lda * (k0 + c)] = acc[ct][q];
+      if (r < rows && c < nb) A[aix(lda, i0 + r, k0 + c)] = acc[ct][q];
     }
 }
 
@@ -438,7 +447,7 @@ __global__ __launch_bounds__(256, 2) void chol_update_kernel(double* A, int lda,
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int c = min(qc + 16 * a + lk + 4 * q, rowsJ - 1), r = min(qr + 16 * b + lm, rowsI - 1);
-        cv[a][b][q] = live ? A[(size_t)(I0 + r) + (size_t)lda * (J0 + c)] : 0.0;
+        cv[a][b][q] = live ? A[aix(lda, I0 + r, J0 + c)] : 0.0;
       }
   __syncthreads();
   const bool diag_next = DIAG && blockIdx.x == 0;  // tile (0, 0): the next diagonal block
@@ -469,7 +478,7 @@ __global__ __launch_bounds__(256, 2) void chol_update_kernel(double* A, int lda,
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int c = qc + 16 * a + lk + 4 * q, r = qr + 16 * b + lm;
-          if (r < rowsI && c < rowsJ) A[(size_t)(I0 + r) + (size_t)lda * (J0 + c)] = cv[a][b][q] - acc[a][b][q];
+          if (r < rowsI && c < rowsJ) A[aix(lda, I0 + r, J0 + c)] = cv[a][b][q] - acc[a][b][q];
         }
     return;
   }
@@ -519,7 +528,7 @@ __global__ __launch_bounds__(256, 2) void chol_update_kernel(double* A, int lda,
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int c = 16 * ct + lk + 4 * q;
-          if (r < rowsI && c < rowsJ) A[(size_t)(I0 + r) + (size_t)lda * (base + c)] = pacc[ct][q];
+          if (r < rowsI && c < rowsJ) A[aix(lda, I0 + r, base + c)] = pacc[ct][q];
         }
       return;
     }
@@ -566,7 +575,7 @@ __device__ inline void stage(double* S, const double* M, int ld, int R0, int C0,
 #pragma unroll
   for (int u = 0; u < DB * DB / 256; ++u) {
     const int p = threadIdx.x + 256 * u, a = p & 63, b = p >> 6;
-    v[u] = M[(size_t)(R0 + min(a, rows - 1)) + (size_t)ld * (C0 + min(b, cols - 1))];
+    v[u] = M[aix(ld, R0 + min(a, rows - 1), C0 + min(b, cols - 1))];
   }
 #pragma unroll
   for (int u = 0; u < DB * DB / 256; ++u) {
@@ -615,7 +624,7 @@ __global__ __launch_bounds__(256) void trsv_fwd_kernel(const double* L, int lda,
   const int i = k0 + nb + blockIdx.x * DB + lane;
   double lv[16];
 #pragma unroll
-  for (int u = 0; u < 16; ++u) lv[u] = L[(size_t)min(i, n - 1) + (size_t)lda * (k0 + min(16 * w + u, nb - 1))];
+  for (int u = 0; u < 16; ++u) lv[u] = L[aix(lda, min(i, n - 1), k0 + min(16 * w + u, nb - 1))];
   double s = 0.0;
 #pragma unroll
   for (int u = 0; u < 16; ++u) s = fma(16 * w + u < nb ? lv[u] : 0.0, z[16 * w + u], s);
@@ -1072,7 +1081,9 @@ void dense_potrf_lower(hipStream_t st, double* A, int n, int lda, double* ws, in
   // (dense_ws_doubles' slack), reset by the factorization's first launch
   const int nbk = (n + DB - 1) / DB;
   // (the fused panel needs the sync block for its timeout report)
-  int* pflag = (fuse_diag && fuse_panel && bw <= 0 && sync) ? (int*)(ws + (size_t)nbk * DB * DB + n + 8) : nullptr;
+  int* pflag = (fuse_diag && fuse_panel && bw <= 0 && lda > 0 && sync) ? (int*)(ws + (size_t)nbk * DB * DB + n + 8)
+                                                                      : nullptr;
+  HMSC_REQUIRE(lda > 0 || (bw > 0 && -lda >= dense_band_ld(bw)), "dense_potrf_lower: band layout narrower than the band");
   bool diag_done = false, panel_done = false;  // block k0 / panel k0 done by the previous trailing update
   for (int k0 = 0; k0 < n; k0 += DB) {
     double* Linv = ws + (size_t)(k0 / DB) * DB * DB;
@@ -1108,7 +1119,7 @@ void dense_trsv_lower(hipStream_t st, const double* L, int n, int lda, double* x
     const char* e = std::getenv("HMSC_NO_TRSV_SF");
     return e && e[0] && e[0] != '0';
   }();
-  if (sync && bw <= 0 && nbk >= 2 && nbk <= TRSV_SF_MAXB && !sf_off) {
+  if (sync && bw <= 0 && lda > 0 && nbk >= 2 && nbk <= TRSV_SF_MAXB && !sf_off) {
     if (trans)
       trsv_sf_kernel<true><<<nbk, 256, 0, st>>>(L, lda, n, ws, x, sync);
     else

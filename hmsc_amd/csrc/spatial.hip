@@ -597,7 +597,7 @@ static double* dupload_f64(const double* h, size_t n) {
 //    (oracle/hmsc_oracle.py nngp_rcm, _eta_spatial_full).
 // ---------------------------------------------------------------------------------------
 struct NnArgs {
-  int np, nf, N, K, bw;
+  int np, nf, N, K, bw, ldq;  // ldq: rows per panel of the tile-band layout of the band matrix
   const int* idx;      // K x np
   const double* A;     // nalpha x K x np
   const double* D;     // nalpha x np
@@ -617,6 +617,7 @@ static NnArgs nn_args(const State& s, int r) {
   n.N = L.np * L.nf;
   n.K = L.nnK;
   n.bw = (L.nnBwUnits + 1) * L.nf - 1;
+  n.ldq = dense_band_ld(n.bw);
   n.idx = L.nnIdx;
   n.A = L.nnA;
   n.D = L.nnD;
@@ -691,7 +692,7 @@ __global__ __launch_bounds__(64) void nngp_assemble_kernel(NnArgs n, const doubl
       }
     }
     if (a == b) v = fma(LDL[h2 + nf * h], (double)(n.unit_ptr[a + 1] - n.unit_ptr[a]), v);
-    Q[row + (size_t)N * c] = v;
+    Q[(size_t)(row - (c & ~63)) + (size_t)n.ldq * c] = v;  // tile-band layout (dense.hip aix)
   }
 }
 
@@ -712,11 +713,13 @@ __global__ __launch_bounds__(256) void nngp_perm_kernel(SpArgs a, NnArgs n, cons
 struct NnLayout {
   size_t Q, x, rhs, ws, LDL, tot;
 };
-static NnLayout nn_layout(int np, int nfc) {
+// the band matrix in the tile-band layout (N x dense_band_ld(bw) doubles, O(N bw)), at the
+// level's factor capacity nfc
+static NnLayout nn_layout(int np, int nfc, int bw_units) {
   NnLayout o{};
   const size_t N = (size_t)np * nfc;
   o.Q = 0;
-  o.x = o.Q + N * N;
+  o.x = o.Q + N * (size_t)dense_band_ld((bw_units + 1) * nfc - 1);
   o.rhs = o.x + N + 8;
   o.ws = o.rhs + N + 8;
   o.LDL = o.ws + dense_ws_doubles((int)N);
@@ -728,12 +731,12 @@ static void launch_eta_nngp(State& s, int r, uint32_t iter) {
   Level& L = s.lev[r];
   const SpArgs a = sp_args(s, r, iter);
   const NnArgs n = nn_args(s, r);
-  const NnLayout o = nn_layout(L.np, sp_nfc(L));
+  const NnLayout o = nn_layout(L.np, sp_nfc(L), L.nnBwUnits);
   double* w = L.spWork;
   double *Q = w + o.Q, *x = w + o.x, *rhs = w + o.rhs, *ws = w + o.ws, *LDL = w + o.LDL;
   const int N = n.N, g1 = (N + 255) / 256;
   if (L.nnAssembledN != N) {  // a new system size (updateNf): entries outside its band must be 0
-    HIP_OK(hipMemsetAsync(Q, 0, (size_t)N * N * sizeof(double), s.stream));
+    HIP_OK(hipMemsetAsync(Q, 0, (size_t)N * n.ldq * sizeof(double), s.stream));
     L.nnAssembledN = N;
   }
   sp_rhs_kernel<<<g1, 256, 0, s.stream>>>(a, rhs, LDL);
@@ -742,11 +745,11 @@ static void launch_eta_nngp(State& s, int r, uint32_t iter) {
   HIP_OK(hipGetLastError());
   {
     ProfScope pc(s, PROF_CHOL);
-    dense_potrf_lower(s.stream, Q, N, N, ws, s.dev_flags, n.bw, s.trsv_sync);
+    dense_potrf_lower(s.stream, Q, N, -n.ldq, ws, s.dev_flags, n.bw, s.trsv_sync);
   }
-  dense_trsv_lower(s.stream, Q, N, N, x, 0, ws, n.bw, s.trsv_sync);   // backsolve(R, fS, transpose = TRUE)
+  dense_trsv_lower(s.stream, Q, N, -n.ldq, x, 0, ws, n.bw, s.trsv_sync);   // backsolve(R, fS, transpose = TRUE)
   nngp_perm_kernel<<<g1, 256, 0, s.stream>>>(a, n, rhs, x, 1);
-  dense_trsv_lower(s.stream, Q, N, N, x, 1, ws, n.bw, s.trsv_sync);   // backsolve(R, tmp2)
+  dense_trsv_lower(s.stream, Q, N, -n.ldq, x, 1, ws, n.bw, s.trsv_sync);   // backsolve(R, tmp2)
   nngp_perm_kernel<<<g1, 256, 0, s.stream>>>(a, n, rhs, x, 2);
   HIP_OK(hipGetLastError());
 }
@@ -914,7 +917,7 @@ size_t spatial_work_doubles(const State& s, int r) {
   const size_t nfc = sp_nfc(L);
   if (L.gpp) return gpp_layout(L.np, (int)nfc, L.nK, L.nalpha).tot + 64;
   if (L.nngp)  // updateAlpha's partial sums after the band matrix: its zeros outside the band persist
-    return nn_layout(L.np, (int)nfc).tot + (size_t)L.nalpha * ((L.np + 255) / 256) * nfc + 64;
+    return nn_layout(L.np, (int)nfc, L.nnBwUnits).tot + (size_t)L.nalpha * ((L.np + 255) / 256) * nfc + 64;
   const size_t N = (size_t)L.np * nfc;
   const size_t eta = N * N + N + dense_ws_doubles((int)N) + nfc * nfc + 64;
   const size_t alpha = (size_t)L.nalpha * ((L.np + 255) / 256) * sp_nfc(L);
@@ -995,7 +998,7 @@ void launch_alpha(State& s, uint32_t iter) {
     }
     if (L.nngp) {  // the band matrix at the start of spWork stays untouched (zeros outside the band)
       SpArgs b = a;
-      b.work = L.spWork + nn_layout(L.np, sp_nfc(L)).tot;
+      b.work = L.spWork + nn_layout(L.np, sp_nfc(L), L.nnBwUnits).tot;
       nngp_alpha_kernel<<<dim3(L.nalpha, (L.np + 255) / 256), 256, 0, s.stream>>>(b, nn_args(s, r));
       HIP_OK(hipGetLastError());
       alpha_draw_kernel<<<1, 256, 0, s.stream>>>(b);

@@ -424,6 +424,11 @@ void dense_trtri_lower(hipStream_t st, const double* L, int ldl, int n, double* 
                        bool have_dinv);
 // workspace of dense_potrf_lower + dense_trsv_lower: the 64 x 64 diagonal-block inverses, then n
 inline size_t dense_ws_doubles(int n) { return (size_t)((n + 63) / 64) * 64 * 64 + (size_t)n + 64; }
+// rows per 64-column panel of the tile-band layout of a band matrix of bandwidth bw (pass
+// lda = -dense_band_ld(bw) to dense_potrf_lower / dense_trsv_lower; dense.hip aix): the panel's
+// diagonal tile, the tiles below it in the band, and one more for the transposed solve's
+// tile-aligned reach
+inline int dense_band_ld(int bw) { return 64 * (2 + (bw + 63) / 64); }
 void dense_lauum_lower(hipStream_t st, const double* M, int ldm, int n, double* out, int ldo);
 // out = U diag(d) U^T (full symmetric), d = dbase + n (*rho - 1) or its reciprocal
 void dense_gram_diag(hipStream_t st, const double* U, int ldu, int n, const double* dbase, const double* rho,

@@ -132,3 +132,24 @@ def test_full_large_eta_and_alpha(full_large):
         a = O.update_alpha(st, m, Rng(seed), it, dp)
         assert np.array_equal(ch.get_state()["Alpha"][0], a[0]), it
     ch.close()
+
+
+def test_nngp_band_storage_is_linear():
+    """np = 12000, nf = 2: the NNGP level's band matrix is held in the tile-band layout
+    (dense.hip aix), O(N bw) doubles -- a dense (np nf)^2 array would be 4.6 GB -- and
+    default-updater sweeps run on it with finite states (R factors the same matrix as a sparse
+    one, R/updateEta.R:137-147)."""
+    hM = synthetic_model(ny=12000, ns=3, nc=2, nf=2, nr=1, spatial=[0], seed=74, alpha_n=10,
+                         spatial_method="NNGP", n_neighbours=10)
+    ch = H.Chain(hM, 5, device=0, updater=UPD)
+    ch.init()
+    units = int(ch.debug_get("nngp_bw0", 1)[0])
+    N, bw = 12000 * 2, (units + 1) * 2 - 1
+    work = float(ch.debug_get("spwork_doubles0", 1)[0])
+    assert work < N * (bw + 200) + 64 * N + 4e6, (work, N, bw)
+    assert work < 0.05 * N * N
+    for it in range(1, 4):
+        ch.sweep(it)
+    g = ch.get_state()
+    assert np.isfinite(g["Eta"][0]).all() and np.isfinite(g["Beta"]).all()
+    ch.close()
