@@ -1300,19 +1300,20 @@ __device__ __forceinline__ void gamma2_final_body(const G2Args& a, double* lds) 
     for (int p0 = 0; p0 < P; p0 += 32) {
       const int p = p0 + l;
       double s = 0.0;
-      if (p < P) {  // every 8th part, eight loads in flight per step, summed in order
-        int b = g;
-        for (; b + 56 < a.nparts; b += 64) {
+      if (p < P) {  // every 8th part, eight loads in flight per step (the remainder's too: a
+                    // load-use loop over it paid one device-coherent round trip per part), summed in order
+        for (int b = g; b < a.nparts; b += 64) {
           double x[8];
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
-            const double* q = a.part + (size_t)(b + 8 * u) * P + p;
+            const int bb = min(b + 8 * u, a.nparts - 1);
+            const double* q = a.part + (size_t)bb * P + p;
             x[u] = a.coherent ? load_coherent(q) : *q;
           }
 #pragma unroll
-          for (int u = 0; u < 8; ++u) s += x[u];
+          for (int u = 0; u < 8; ++u)
+            if (b + 8 * u < a.nparts) s += x[u];
         }
-        for (; b < a.nparts; b += 8) s += a.coherent ? load_coherent(a.part + (size_t)b * P + p) : a.part[(size_t)b * P + p];
       }
       red[g][l + (p0 ? 32 : 0)] = s;
     }
@@ -3817,15 +3818,30 @@ __global__ __launch_bounds__(256) void g2_stats_kernel(G2SArgs a) {
   }
   const int n1 = a.nc * a.nt, P = n1 + a.NF * a.nt;
   for (int p = t; p < P; p += 256) {
+    // (every part's load of a chunk issued before the first sum: a load-use loop paid one
+    // device-coherent round trip per part, ~14 us at 32 parts)
     double v = 0.0;
     if (P <= 64 && a.nparts > 1) {  // gamma2_final_body: 8 groups of every 8th part, then the groups
-      for (int g = 0; g < 8; ++g) {
-        double sg = 0.0;
-        for (int b = g; b < a.nparts; b += 8) sg += load_coherent(a.part + (size_t)b * P + p);
-        v += sg;
+      double sg[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+      for (int b0 = 0; b0 < a.nparts; b0 += 32) {
+        double x[32];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) x[u] = load_coherent(a.part + (size_t)min(b0 + u, a.nparts - 1) * P + p);
+#pragma unroll
+        for (int u = 0; u < 32; ++u)
+          if (b0 + u < a.nparts) sg[u & 7] += x[u];  // part b0 + u is in group u mod 8 (b0 mod 8 == 0)
       }
+#pragma unroll
+      for (int g = 0; g < 8; ++g) v += sg[g];
     } else {
-      for (int b = 0; b < a.nparts; ++b) v += load_coherent(a.part + (size_t)b * P + p);
+      for (int b0 = 0; b0 < a.nparts; b0 += 32) {
+        double x[32];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) x[u] = load_coherent(a.part + (size_t)min(b0 + u, a.nparts - 1) * P + p);
+#pragma unroll
+        for (int u = 0; u < 32; ++u)
+          if (b0 + u < a.nparts) v += x[u];
+      }
     }
     a.out[p] = (p < n1 && a.xtztr) ? a.xtztr[p] : v;
   }
