@@ -149,12 +149,17 @@ struct SlabJob {
   int nparts, nb;
 };
 
-// two independent slab reductions in one launch: blocks [0, j0.nb) reduce j0, the rest j1
-__global__ __launch_bounds__(256) void slab_sum2_kernel(SlabJob j0, SlabJob j1) {
+__device__ void side_gate_body(const SideGate& g);
+
+// two independent slab reductions in one launch: blocks [0, j0.nb) reduce j0, the next j1.nb
+// j1, and a last block the side gate when there is one
+__global__ __launch_bounds__(256) void slab_sum2_kernel(SlabJob j0, SlabJob j1, SideGate g) {
   if ((int)blockIdx.x < j0.nb)
     slab_sum_body(j0.part, j0.out, j0.n, j0.nparts, j0.stride, blockIdx.x, j0.nb);
-  else
+  else if ((int)blockIdx.x < j0.nb + j1.nb)
     slab_sum_body(j1.part, j1.out, j1.n, j1.nparts, j1.stride, blockIdx.x - j0.nb, j1.nb);
+  else
+    side_gate_body(g);
 }
 
 static int grid_for(int64_t n, int block = 64, int cap = 2048) {
@@ -196,10 +201,10 @@ __global__ __launch_bounds__(256) void gram_na_kernel(EtaView ev, const double* 
 
 // the two slab reductions that follow the z kernel (XZ, ZTr), one launch (zdraw.hip)
 void launch_slab_sum2(const double* p0, double* o0, int64_t n0, int np0, const double* p1, double* o1, int64_t n1,
-                      int np1, hipStream_t st) {
+                      int np1, hipStream_t st, SideGate gate) {
   const SlabJob j0{p0, o0, n0, n0, np0, grid_for(n0)};
   const SlabJob j1{p1, o1, n1, n1, np1, grid_for(n1)};
-  slab_sum2_kernel<<<j0.nb + j1.nb, 256, 0, st>>>(j0, j1);
+  slab_sum2_kernel<<<j0.nb + j1.nb + (gate.n > 0 ? 1 : 0), 256, 0, st>>>(j0, j1, gate);
   HIP_OK(hipGetLastError());
 }
 
@@ -330,6 +335,42 @@ __device__ __forceinline__ void side_wait(const int* flags, int n, int epoch, in
       __hip_atomic_store(&err[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// side_wait over n <= 64 flags by a whole wave, lane q polling flag q: the flags' round trips
+// overlap instead of following one another (two flags in sequence were ~3 us of the BetaLambda
+// prologue); every lane of the wave must be active
+__device__ __forceinline__ void side_wait_lanes(const int* flags, int n, int epoch, int* err) {
+  const int q = threadIdx.x & 63;
+  auto seen = [&] {
+    return q >= n || __hip_atomic_load(&flags[q < n ? q : 0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+  };
+  if (!spin_until<8>([&] { return __all(seen()) != 0; }) && q == 0)
+    __hip_atomic_store(&err[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The gate: wave 0 of the slab launch's extra workgroup polls the side chain's flags of sweep
+// `iter` (GammaV, the delta chains, Gamma2's prep), so that launch ends only once they are up and
+// the next fused launch -- after a launch boundary -- reads iV, Delta, Psi and the prep with plain
+// loads and no poll at its start (on its critical path the polls and the device-coherent loads
+// behind them were ~4 us of the BetaLambda prologue).  Bounded like every in-launch wait.
+__device__ void side_gate_body(const SideGate& g) {
+  if (g.n > 0 && threadIdx.x < 64) side_wait_lanes(g.flags, g.n, g2bl_epoch(SWEEP_ITER(g)), g.err);
+}
+
+SideGate side_gate_next(State& s, uint32_t iter) {
+  SideGate g{};
+  s.side_gated = false;
+  if (s.sharded || !s.capturing || !s.edge_free_now || !s.side_tail || !gamma2_bl_fusion_ok(s) ||
+      getenv_flag("HMSC_NO_SIDE_GATE"))
+    return g;
+  g.flags = s.side_sync;
+  g.n = 1 + s.nr + ((s.mask & HMSC_UP_GAMMA2) ? 1 : 0);
+  g.iter = iter;
+  g.iter_dev = s.d_iter;
+  g.err = s.gbl_sync;
+  s.side_gated = true;
+  return g;
+}
+
 // What the fused launch's tail (bl_tail) needs of a species' update, lane k holding row k:
 // the new column BL[:, j], Mu_j = Gamma Tr_j^T (rows < nc) and tau = cumprod(Delta) (rows >= nc)
 struct BLCol {
@@ -353,30 +394,38 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
   const int K = a.K, nc = a.nc, nt = a.nt, i = lane_id(), w = threadIdx.x >> 6, t = threadIdx.x;
   const int j = blk * 4 + w;
   if (blk == 0) HMSC_STAMP(60);
-  if (side_n > 0) side_wait(side_sync, side_n, side_epoch, gsync);
-  if (WAIT_GAMMA && blk == 0 && w == 0) HMSC_STAMP_RT(84);
+  if (WAIT_GAMMA && blk == 40 && w == 0) HMSC_STAMP_RT(91);
   // every global load of the prologue is issued before the first LDS store (a staging loop
-  // with a store per iteration waits out one memory latency per iteration)
+  // with a store per iteration waits out one memory latency per iteration); the loads no side
+  // flag guards go out first, so their latency overlaps the flags' polls
   double gv[4], ivv[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int p = t + 256 * u, pc = p < K * K ? p : 0;
     gv[u] = a.G[pc % K + (size_t)a.Kmax * (pc / K)];
-    ivv[u] = side_n > 0 ? load_coherent(a.iV + (p < nc * nc ? p : 0)) : a.iV[p < nc * nc ? p : 0];
   }
   const double gam = WAIT_GAMMA ? 0.0 : a.Gamma[t < nc * nt ? t : 0];
-  const double* dp = a.Delta + (t < a.NF ? t : 0);
-  const double del = a.NF > 0 ? (side_n > 0 ? load_coherent(dp) : *dp) : 1.0;
   // this species' own inputs, loaded before the barrier so their latency overlaps it
   const int jj = j < a.ns_loc ? j : a.ns_loc - 1;
   const double isig = a.iSigma[jj];
   const double xz = i < K ? xz_get(a.xz, (i < K ? i : 0) + (size_t)K * jj) : 0.0;
-  const double* pp = a.Psi + ((i >= nc && i < K) ? (i - nc) + (size_t)a.NF * jj : 0);
-  const double psi = (i >= nc && i < K) ? (side_n > 0 ? load_coherent(pp) : *pp) : 0.0;  // (post_bl_kernel's, side)
   double trj[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) trj[q] = q < nt ? a.Tr[jj + (size_t)a.ns_loc * q] : 0.0;
   const int nai = a.na_index ? a.na_index[jj] : -1;
+  if (side_n > 0) side_wait_lanes(side_sync, side_n, side_epoch, gsync);
+  if (WAIT_GAMMA && blk == 0 && w == 0) HMSC_STAMP_RT(84);
+  // what the previous sweep's side chain published (device-coherent after its flags)
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int p = t + 256 * u;
+    ivv[u] = side_n > 0 ? load_coherent(a.iV + (p < nc * nc ? p : 0)) : a.iV[p < nc * nc ? p : 0];
+  }
+  const double* dp = a.Delta + (t < a.NF ? t : 0);
+  const double del = a.NF > 0 ? (side_n > 0 ? load_coherent(dp) : *dp) : 1.0;
+  const double* pp = a.Psi + ((i >= nc && i < K) ? (i - nc) + (size_t)a.NF * jj : 0);
+  const double psi = (i >= nc && i < K) ? (side_n > 0 ? load_coherent(pp) : *pp) : 0.0;  // (post_bl_kernel's, side)
+  if (WAIT_GAMMA && blk == 40 && w == 0) HMSC_STAMP_RT(92);
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int p = t + 256 * u;
@@ -386,6 +435,7 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
   if (!WAIT_GAMMA && t < nc * nt && t < 32 * 8) sGam[t] = gam;
   if (t < a.NF) sTau[t] = del;  // Delta here; each lane forms its own cumprod below
   __syncthreads();
+  if (WAIT_GAMMA && blk == 40 && w == 0) HMSC_STAMP_RT(93);
   if (j >= a.ns_loc) return BLCol{0.0, 0.0, 1.0, 0.0, ~0ull, 0ull};
   double* lds = tiles + w * WV_TILE;
   // tau = cumprod(Delta) within the level of factor i - nc   (:51)
@@ -429,6 +479,7 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
   wv_chol<NM>(x, dinv);                    // RiU = chol(iU)  (:98)
   if (blk == 0) HMSC_STAMP(62);
   if (WAIT_GAMMA && blk == 0 && w == 0) HMSC_STAMP_RT(74);
+  if (WAIT_GAMMA && blk == 40 && w == 0) HMSC_STAMP_RT(94);
   double mu = 0.0;  // Mu_j = Gamma Tr_j^T   (:62)
   if (WAIT_GAMMA) {
     // the new Gamma of this sweep (updateGamma2, published by the launch's Gamma2 workgroup
@@ -444,6 +495,7 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
         i == 0)
       __hip_atomic_store(&gsync[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (blk == 0 && w == 0) HMSC_STAMP_RT(75);
+    if (blk == 40 && w == 0) HMSC_STAMP_RT(95);
     if (i < nc)
 #pragma unroll
       for (int q = 0; q < 8; ++q)
@@ -480,6 +532,7 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
   }
   if (blk == 0) HMSC_STAMP(64);
   if (WAIT_GAMMA && blk == 0 && w == 0) HMSC_STAMP_RT(76);
+  if (WAIT_GAMMA && blk == 40 && w == 0) HMSC_STAMP_RT(96);
   // (the fused launch's tail folds the waves' start / end into its reduction tree and records
   // once: a thousand same-address device atomics at the end of the bodies cost ~10 us)
   const unsigned long long kt1 = (a.kt && a.kt_defer) ? kt_now() : 0ull;
@@ -1136,6 +1189,7 @@ __device__ __forceinline__ void gamma2_partial_body(const XZSrc& XZ, const doubl
       q = (p - n1) / NF;
     }
     double acc = 0.0;
+#pragma unroll 8
     for (int jj = 0; jj < nj; ++jj) acc = fma(sX[k + K * jj], sTr[jj + SB * q], acc);
     if (coherent)
       store_coherent(out + p, acc);
@@ -1230,7 +1284,8 @@ __global__ __launch_bounds__(256) void gamma2_prep_kernel(G2PrepArgs a) {
 
 struct G2Args {
   int nc, nt, Kmax, NF, nparts, ns_loc, use_xtztr, check_isigma, stage;
-  int coherent;  // partials (and prep) written by other workgroups of the same launch / another queue
+  int coherent;       // partials written by other workgroups of the same launch
+  int prep_coherent;  // the prep written by another queue's launch, behind a flag polled in this one
   const double* isig_count;  // sharded chain: all-reduced count of species with iSigma != 1
   const double* part;
   const double* xtztr;
@@ -1262,71 +1317,100 @@ __device__ __forceinline__ void batched_for(int n, Load load, Store store) {
 // LDS of the final stage (doubles), before the staged B1 | LS (n2 + N^2 more when a.stage)
 constexpr int G2F_LDS = 512 + 512 + 3 * 256 + 8 * 64 + 2048;
 
-__device__ __forceinline__ void gamma2_final_body(const G2Args& a, double* lds) {
-  // Every input is staged into LDS by all 256 threads first (coalesced, in parallel); the
-  // small products then run from LDS instead of as per-thread loops of dependent global loads.
-  __shared__ int all_one;
-  double* S0 = lds;
-  double* LTr = S0 + 512;
-  double* v1 = LTr + 512;
-  double* v2 = v1 + 256;
-  double* xi = v2 + 256;
-  double (*red)[64] = (double (*)[64])(xi + 256);
-  double* sGL = xi + 256 + 8 * 64;
-  double* dyn = sGL + 2048;  // B1 | LS  when a.stage
+struct G2FLds {
+  double *S0, *LTr, *v1, *v2, *xi, *sGL, *dyn;
+  double (*red)[64];
+  __device__ explicit G2FLds(double* lds)
+      : S0(lds), LTr(lds + 512), v1(lds + 1024), v2(lds + 1280), xi(lds + 1536), sGL(lds + 1792 + 8 * 64),
+        dyn(lds + 1792 + 8 * 64 + 2048), red((double (*)[64])(lds + 1792)) {}
+};
+
+// The final stage in two phases.  gamma2_final_pre: what no flag guards -- iSigma's all-ones
+// test (:36), G's X^T Eta block, the noise -- so that the fused launch's workgroup 0 issues it
+// while it waits for the partials and the side chain's flags; returns this thread's vote of the
+// all-ones test (the caller's barrier ANDs them).  Everything is staged into LDS by all 256
+// threads (coalesced, every load of a thread issued before its first use).
+__device__ __forceinline__ int gamma2_final_pre(const G2Args& a, double* lds) {
+  const G2FLds L(lds);
+  const int nc = a.nc, N = nc * a.nt, t = threadIdx.x;
+  int ok = 1;
+  if (a.check_isigma)
+    batched_for<8>(a.ns_loc, [&](int j) { return a.iSigma[j]; }, [&](int, double v) {
+      if (v != 1.0) ok = 0;
+    });
+  if (t == 0 && a.isig_count && *a.isig_count != 0.0) ok = 0;  // ... over every rank's species
+  if (nc * a.NF <= 2048)  // X^T Eta block of G, read by the XZT products
+    batched_for<8>(nc * a.NF, [&](int p) { return a.G[p % nc + (size_t)a.Kmax * (nc + p / nc)]; },
+                   [&](int p, double v) { L.sGL[p] = v; });
+  for (int r = t; r < N; r += blockDim.x) L.xi[r] = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)r, 0, S_GAMMA2, SWEEP_ITER(a));
+  return ok;
+}
+
+// gamma2_final_main: after the barrier that follows the pre phase (and the flags): the prep
+// matrices and the species-block partials (their loads issued together), then the products.
+__device__ __forceinline__ void gamma2_final_main(const G2Args& a, double* lds) {
+  const G2FLds L(lds);
   HMSC_STAMP(30);
   const int nc = a.nc, nt = a.nt, N = nc * nt, t = threadIdx.x, n2 = nc * nc;
-  if (t == 0) all_one = 1;
-  __syncthreads();
-  if (a.check_isigma)  // acts only if all(iSigma == 1)  (:36)
-    batched_for<8>(a.ns_loc, [&](int j) { return a.iSigma[j]; }, [&](int, double v) {
-      if (v != 1.0) all_one = 0;
-    });
-  if (t == 0 && a.isig_count && *a.isig_count != 0.0) all_one = 0;  // ... over every rank's species
-  __syncthreads();
-  if (!all_one) return;
   const int n1 = nc * nt, nL = a.NF * nt, P = n1 + nL;
   const double *B1 = a.prep, *LS = a.prep + n2;
+  const bool grouped = P <= 64 && a.nparts > 1;
+  // species-block partials: 8 groups of 32 threads, each summing every 8th part in order; up to
+  // 64 parts every load of a thread is issued before the prep staging's (one latency for both)
+  const int g = t >> 5, l = t & 31;
+  double x[2][8];
+  const bool direct = grouped && a.nparts <= 64;
+  if (direct)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int p = min(32 * h + l, P - 1);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const double* q = a.part + (size_t)min(g + 8 * u, a.nparts - 1) * P + p;
+        x[h][u] = a.coherent ? load_coherent(q) : *q;
+      }
+    }
   if (a.stage) {
-    double* d = dyn;
-    batched_for<8>(n2 + N * N, [&](int p) { return a.coherent ? load_coherent(a.prep + p) : a.prep[p]; },
+    double* d = L.dyn;
+    batched_for<8>(n2 + N * N, [&](int p) { return a.prep_coherent ? load_coherent(a.prep + p) : a.prep[p]; },
                    [&](int p, double v) { d[p] = v; });
     B1 = d;
     LS = d + n2;
   }
-  // species-block partials: 8 groups of 32 threads, each summing every 8th part
-  if (P <= 64 && a.nparts > 1) {
-    const int g = t >> 5, l = t & 31;
+  if (grouped) {
     for (int p0 = 0; p0 < P; p0 += 32) {
       const int p = p0 + l;
       double s = 0.0;
-      if (p < P) {  // every 8th part, eight loads in flight per step (the remainder's too: a
-                    // load-use loop over it paid one device-coherent round trip per part), summed in order
-        for (int b = g; b < a.nparts; b += 64) {
-          double x[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const int bb = min(b + 8 * u, a.nparts - 1);
-            const double* q = a.part + (size_t)bb * P + p;
-            x[u] = a.coherent ? load_coherent(q) : *q;
-          }
+      if (p < P) {
+        if (direct) {
 #pragma unroll
           for (int u = 0; u < 8; ++u)
-            if (b + 8 * u < a.nparts) s += x[u];
+            if (g + 8 * u < a.nparts) s += x[p0 ? 1 : 0][u];
+        } else {
+          for (int b = g; b < a.nparts; b += 64) {  // eight loads in flight per step, summed in order
+            double y[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const double* q = a.part + (size_t)min(b + 8 * u, a.nparts - 1) * P + p;
+              y[u] = a.coherent ? load_coherent(q) : *q;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+              if (b + 8 * u < a.nparts) s += y[u];
+          }
         }
       }
-      red[g][l + (p0 ? 32 : 0)] = s;
+      L.red[g][l + (p0 ? 32 : 0)] = s;
     }
     __syncthreads();
     for (int p = t; p < P; p += blockDim.x) {
-      const int slot = p < 32 ? p : 32 + (p - 32);
       double s = 0.0;
 #pragma unroll
-      for (int g2 = 0; g2 < 8; ++g2) s += red[g2][slot];
+      for (int g2 = 0; g2 < 8; ++g2) s += L.red[g2][p];
       if (p < n1)
-        S0[p] = a.use_xtztr ? a.xtztr[p] : s;
+        L.S0[p] = a.use_xtztr ? a.xtztr[p] : s;
       else
-        LTr[p - n1] = s;
+        L.LTr[p - n1] = s;
     }
   } else {
     for (int p = t; p < P; p += blockDim.x) {
@@ -1334,52 +1418,56 @@ __device__ __forceinline__ void gamma2_final_body(const G2Args& a, double* lds) 
 #pragma unroll 8
       for (int b = 0; b < a.nparts; ++b) s += a.coherent ? load_coherent(a.part + (size_t)b * P + p) : a.part[(size_t)b * P + p];
       if (p < n1)
-        S0[p] = a.use_xtztr ? a.xtztr[p] : s;
+        L.S0[p] = a.use_xtztr ? a.xtztr[p] : s;
       else
-        LTr[p - n1] = s;
+        L.LTr[p - n1] = s;
     }
   }
   const bool stage_g = nc * a.NF <= 2048;
-  if (stage_g)  // X^T Eta block of G, read by the XZT products below
-    batched_for<8>(nc * a.NF, [&](int p) { return a.G[p % nc + (size_t)a.Kmax * (nc + p / nc)]; },
-                   [&](int p, double v) { sGL[p] = v; });
-  for (int r = t; r < N; r += blockDim.x) xi[r] = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)r, 0, S_GAMMA2, SWEEP_ITER(a));
   __syncthreads();
   HMSC_STAMP(31);
+  // (the products' LDS operands unrolled eight deep, so their loads issue ahead of the
+  // accumulation chain; the accumulation order is unchanged)
   // XZT = X^T Z Tr - sum_r (X^T Eta_r[Pi]) (Lambda_r Tr)   (:46 with S = Z - sum LRan)
   for (int p = t; p < n1; p += blockDim.x) {
     const int c = p % nc, q = p / nc;
     double s = 0.0;
+#pragma unroll 8
     for (int f = 0; f < a.NF; ++f)
-      s += (stage_g ? sGL[c + nc * f] : a.G[c + a.Kmax * (nc + f)]) * LTr[f + a.NF * q];
-    S0[p] -= s;
+      s += (stage_g ? L.sGL[c + nc * f] : a.G[c + a.Kmax * (nc + f)]) * L.LTr[f + a.NF * q];
+    L.S0[p] -= s;
   }
   __syncthreads();
   // r = vec(B1 XZT); u = LS^T r + xi; Gamma = LS u = muG + LS xi   (:49, :53-54)
   for (int p = t; p < N; p += blockDim.x) {
     const int c = p % nc, q = p / nc;
     double s2 = 0.0;
-    for (int k = 0; k < nc; ++k) s2 += B1[c + nc * k] * S0[k + nc * q];
-    v2[p] = s2;
+#pragma unroll 8
+    for (int k = 0; k < nc; ++k) s2 += B1[c + nc * k] * L.S0[k + nc * q];
+    L.v2[p] = s2;
   }
   __syncthreads();
   for (int r = t; r < N; r += blockDim.x) {
-    double u = xi[r];
-    for (int c = r; c < N; ++c) u = fma(LS[c + N * r], v2[c], u);
-    v1[r] = u;
+    double u = L.xi[r];
+#pragma unroll 8
+    for (int c = r; c < N; ++c) u = fma(LS[c + N * r], L.v2[c], u);
+    L.v1[r] = u;
   }
   __syncthreads();
   for (int r = t; r < N; r += blockDim.x) {
-    double g = 0.0;
-    for (int c = 0; c <= r; ++c) g = fma(LS[r + N * c], v1[c], g);
-    a.Gamma[r] = g;
+    double gm = 0.0;
+#pragma unroll 8
+    for (int c = 0; c <= r; ++c) gm = fma(LS[r + N * c], L.v1[c], gm);
+    a.Gamma[r] = gm;
   }
   HMSC_STAMP(32);
 }
 
 __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  gamma2_final_body(a, smem);
+  const int ok = gamma2_final_pre(a, smem);
+  if (!__syncthreads_and(ok)) return;  // acts only if all(iSigma == 1)  (:36)
+  gamma2_final_main(a, smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -1828,19 +1916,27 @@ __global__ __launch_bounds__(256) void gamma2_bl_kernel(G2BLArgs f) {
   if (blockIdx.x == 0) {
     const unsigned long long kt0 = f.kt_g2 ? kt_now() : 0ull;
     if (threadIdx.x < 64) HMSC_STAMP_RT(70);
-    // every partial is in (relaxed count; the partials are device-coherent stores, read with
-    // device-coherent loads), bounded like every in-launch wait
-    if (threadIdx.x == 0 &&
-        !spin_until<2>([&] { return __hip_atomic_load(&f.sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nparts; }))
-      __hip_atomic_store(&f.sync[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (f.side_wait) {  // the previous sweep's GammaV (Gamma, iV) and Gamma2 prep (read coherently)
-      const int ep = g2bl_epoch(SWEEP_ITER(f.g2) - 1);
-      side_wait(f.side_sync, 1, ep, f.sync);
-      if (f.side_prep) side_wait(f.side_sync + 1 + f.bl.nr, 1, ep, f.sync);
+    // wave 0's lanes poll together: lane 0 the partials' count (relaxed; the partials are
+    // device-coherent stores, read with device-coherent loads), lanes 1 and 2 the previous
+    // sweep's GammaV (Gamma, iV) and Gamma2 prep flags.  Their first loads are issued before
+    // the pre phase's, whose latency they share; every wait bounded like every in-launch wait.
+    const int lane = threadIdx.x & 63;
+    const int ep = g2bl_epoch(SWEEP_ITER(f.g2) - 1);
+    const int* pf = nullptr;
+    if (threadIdx.x < 64) {
+      if (lane == 0) pf = &f.sync[0];
+      else if (lane == 1 && f.side_wait) pf = f.side_sync;
+      else if (lane == 2 && f.side_wait && f.side_prep) pf = f.side_sync + 1 + f.bl.nr;
     }
-    __syncthreads();
+    auto seen = [&](int v) { return !pf || (lane == 0 ? v >= nparts : v == ep); };
+    auto poll = [&] { return pf ? __hip_atomic_load(pf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0; };
+    const int v0 = poll();
+    const int ok = gamma2_final_pre(f.g2, smem);
+    if (threadIdx.x < 64 && !__all(seen(v0)) && !spin_until<2>([&] { return __all(seen(poll())) != 0; }) && lane == 0)
+      __hip_atomic_store(&f.sync[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int all_one = __syncthreads_and(ok);
     if (threadIdx.x < 64) HMSC_STAMP_RT(72);
-    gamma2_final_body(f.g2, smem);
+    if (all_one) gamma2_final_main(f.g2, smem);
     __syncthreads();
     if (threadIdx.x < 64) HMSC_STAMP_RT(73);
     if (threadIdx.x == 0) {
@@ -1851,6 +1947,7 @@ __global__ __launch_bounds__(256) void gamma2_bl_kernel(G2BLArgs f) {
     return;
   }
   const int b = blockIdx.x - 1;
+  if (b == 40 && threadIdx.x < 64) HMSC_STAMP_RT(97);
   if (b < nparts) {
     if (b == 0 && threadIdx.x < 64) HMSC_STAMP_RT(71);
     gamma2_partial_body(f.xz, f.BLold, f.K, f.nc, f.NF, f.nt, f.nsl, f.Tr, f.part, smem, b, true);
@@ -2003,6 +2100,10 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
   const bool dev_join = !sh && crw_on && s.edge_free_now && s.capturing && s.cap_sweep > 0 && s.side_tail;
   // iV, Gamma2's prep, Psi and Delta come from the previous sweep's side updaters
   if (!dev_join) join_side(s);
+  // ... and when the slab launch after the last updateZ has waited for them (SideGate), this
+  // launch reads them with plain loads
+  const bool gated = dev_join && s.side_gated;
+  s.side_gated = false;
   if (sh && !s.g2s_valid) shard_g2_stats(s);
   if (!s.g2prep_valid) launch_gamma2_prep(s, s.stream);
   G2BLArgs f{};
@@ -2060,7 +2161,8 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
   s.side_tail = false;  // (both set again by this sweep's launch_side_fused)
   s.psi_side = !sh;     // (a sharded chain's tail draws psi: its record pack reads Psi on the main stream)
   f.side_sync = s.side_sync;
-  f.side_wait = dev_join;
+  f.side_wait = dev_join && !gated;
+  a.prep_coherent = f.side_wait;
   f.side_prep = (s.mask & HMSC_UP_GAMMA2) ? 1 : 0;
   f.kt_g2 = s.kt_on ? s.d_kt + (size_t)KT_G2 * 2 * KT_SLOTS : nullptr;
   if (!s.capturing) {  // an eager sweep may repeat an iter
@@ -3611,14 +3713,16 @@ __global__ __launch_bounds__(256) void pack_kernel(PackArgs a) { pack_body(a, bl
 // updateZ's two slab reductions and the record pack of the sweep's main-stream outputs in one
 // launch (graph replays of recorded sweeps): the pack reads none of what the slab sums or
 // updateZ write (Z is not recorded), so it need not wait for them
-__global__ __launch_bounds__(256) void slab_pack_kernel(SlabJob j0, SlabJob j1, PackArgs pk, int npack) {
+__global__ __launch_bounds__(256) void slab_pack_kernel(SlabJob j0, SlabJob j1, PackArgs pk, int npack, SideGate g) {
   const int b = blockIdx.x;
   if (b < j0.nb)
     slab_sum_body(j0.part, j0.out, j0.n, j0.nparts, j0.stride, b, j0.nb);
   else if (b < j0.nb + j1.nb)
     slab_sum_body(j1.part, j1.out, j1.n, j1.nparts, j1.stride, b - j0.nb, j1.nb);
-  else
+  else if (b < j0.nb + j1.nb + npack)
     pack_body(pk, b - j0.nb - j1.nb, npack);
+  else
+    side_gate_body(g);
 }
 
 // Publishes "samples < value have landed in the host ring" to the host with a system-scope
@@ -3698,12 +3802,12 @@ void launch_record(State& s, double* slot, int part) {
 }
 
 void launch_slab_sum2_pack(State& s, const double* p0, double* o0, int64_t n0, int np0, const double* p1, double* o1,
-                           int64_t n1, int np1) {
+                           int64_t n1, int np1, SideGate gate) {
   const SlabJob j0{p0, o0, n0, n0, np0, grid_for(n0)};
   const SlabJob j1{p1, o1, n1, n1, np1, grid_for(n1)};
   const PackArgs pk = make_pack_args(s, nullptr, 1);
   constexpr int NPACK = 256;
-  slab_pack_kernel<<<j0.nb + j1.nb + NPACK, 256, 0, s.stream>>>(j0, j1, pk, NPACK);
+  slab_pack_kernel<<<j0.nb + j1.nb + NPACK + (gate.n > 0 ? 1 : 0), 256, 0, s.stream>>>(j0, j1, pk, NPACK, gate);
   HIP_OK(hipGetLastError());
 }
 

@@ -128,6 +128,7 @@ struct State {
   // graph edges, and graphs captured edge-free are rebuilt once a second chain appears.
   bool edge_free_now = false, graph_edge_free = false;
   bool counted_live = false;  // counted in capi.cpp's live chains of its device
+  bool side_gated = false;  // the last slab launch waited for the side chain's flags (SideGate)
   bool side_tail = false;   // the last side chain raises side_sync (the next fused launch may join it on the device)
   // the capture in progress forked the side stream at the graph's root, so its first sweep's
   // side work waits for the tails flag on the device too (no edge from the fused launch)
@@ -376,11 +377,22 @@ void flush_xz(State& s);        // reduce XZ from its chunk partials if they are
 void ext_add_record(State& s);  // add record pack part 2 to the external first-sweep side work (kernels.hip)
 void launch_xeta(State& s);
 void flush_g(State& s);
+// SideGate: the slab launch after updateZ waits (one extra workgroup) for the flags of this
+// sweep's side chain that the next sweep's fused Gamma2 + BetaLambda launch would otherwise
+// poll at its start (kernels.hip side_gate_next); n = 0: no gate
+struct SideGate {
+  const int* flags = nullptr;
+  int n = 0;
+  uint32_t iter = 0;
+  const uint32_t* iter_dev = nullptr;
+  int* err = nullptr;
+};
+SideGate side_gate_next(State& s, uint32_t iter);
 void launch_slab_sum2(const double* p0, double* o0, int64_t n0, int np0, const double* p1, double* o1, int64_t n1,
-                      int np1, hipStream_t st);
+                      int np1, hipStream_t st, SideGate gate = SideGate{});
 // the same with the main-stream record pack (part 1) of a captured recorded sweep appended
 void launch_slab_sum2_pack(State& s, const double* p0, double* o0, int64_t n0, int np0, const double* p1, double* o1,
-                           int64_t n1, int np1);
+                           int64_t n1, int np1, SideGate gate = SideGate{});
 void launch_beta_lambda(State& s, uint32_t iter);
 void launch_gamma_v(State& s, uint32_t iter, hipStream_t st);
 void launch_gamma2(State& s, uint32_t iter);

@@ -35,6 +35,9 @@ print("  tail block0: draws done", v[15] - t0, "tile stored", v[16] - t0, "group
       "final sums in", v[18] - t0)
 print("  post_bl (side partials): start", v[19] - t0, "tails seen", v[20] - t0)
 print("  side chain: start", v[11] - t0, "tails seen", v[12] - t0, "GammaV out", v[13] - t0, "(of the last sweep)")
+v = np.array([st[i] for i in range(91, 98)], dtype=np.float64) - t0
+print("  BL workgroup 40 (10 ns from workgroup 0 start): kernel entry %.0f body entry %.0f loads issued %.0f staged %.0f"
+      " chol done %.0f Gamma seen %.0f end %.0f" % (v[6], v[0], v[1], v[2], v[3], v[4], v[5]))
 if "--blocks" in sys.argv:  # per-BetaLambda-workgroup body end (wall clock), from workgroup 0's start
     allst = ch.debug_get("stamps", 1024)
     e = np.array(allst[256:256 + 250], dtype=np.float64) - t0
