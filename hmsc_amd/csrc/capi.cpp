@@ -788,7 +788,8 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.scratch = dalloc<double>(s.scratch_doubles);
   s.scratch2 = dalloc<double>(s.scratch_doubles);
   s.psi_rs = dalloc<double>((size_t)64 * nfm);
-  s.ABpart = dalloc<double>((size_t)((nsl + 31) / 32) * (nc * nc + 2 * N + nfm * nt + 8));
+  // (the species-block partials of GammaV (32 species a block) and Gamma2 (G2SB = 8))
+  s.ABpart = dalloc<double>((size_t)((nsl + 7) / 8) * (nc * nc + 2 * N + nfm * nt + 8));
   s.allreduce_buf = dalloc<double>((size_t)nc * nc + 2 * N + nfm * nt + nfm + 64);
   if (s.sharded) {  // the two all-reduce buffers (state.h) and the host transport's staging
     const size_t na = (size_t)N + (size_t)nfm * nt + 8, nb = arb_capacity(s);

@@ -68,6 +68,22 @@ __device__ inline void kt_record(unsigned long long* kt, uint32_t iter, unsigned
 // vary with load latency and clocks.
 constexpr unsigned long long HS_TIMEOUT_TICKS = 100000000ull;
 
+// Kernel arguments are read through the scalar cache, and the compiler waits for each argument
+// load before the value's first use, so a large argument block read field by field as the code
+// reaches them pays one cache round trip per 64-byte line, in sequence, at the start of every
+// workgroup (the fused Gamma2 + BetaLambda launch's 0.8 KB block: ~a dozen dependent misses in
+// its prologue).  kernarg_warm<bytes>() issues one scalar load per line first, all in flight
+// together, so the later reads hit the scalar cache.  (Loads only.)
+template <int BYTES>
+__device__ __forceinline__ void kernarg_warm() {
+  typedef const __attribute__((address_space(4))) uint32_t* kptr;
+  const kptr p = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
+  uint32_t acc = 0;
+#pragma unroll
+  for (int o = 0; o < (BYTES + 3) / 4; o += 16) acc ^= p[o];
+  asm volatile("" ::"s"(acc));
+}
+
 // poll done() with s_sleep(SLEEP) between tries until it holds (true) or the bound passes (false)
 template <int SLEEP, class F>
 __device__ __forceinline__ bool spin_until(F done) {
@@ -330,12 +346,12 @@ struct XZSrc {
 __device__ __forceinline__ double xz_get(const XZSrc& x, size_t g) {
   if (!x.part) return x.XZ[g];
   double s[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int cb = 0; cb < x.nparts; cb += 16) {  // 16 partials' loads in flight, then their sums
-    double v[16];
+  for (int cb = 0; cb < x.nparts; cb += 48) {  // 48 partials' loads in flight (one round at the
+    double v[48];                                // z launch's 48 chunks), then their sums
 #pragma unroll
-    for (int u = 0; u < 16; ++u) v[u] = cb + u < x.nparts ? x.part[(int64_t)(cb + u) * x.stride + g] : 0.0;
+    for (int u = 0; u < 48; ++u) v[u] = x.part[(int64_t)min(cb + u, x.nparts - 1) * x.stride + g];  // (clamped)
 #pragma unroll
-    for (int u = 0; u < 16; ++u)
+    for (int u = 0; u < 48; ++u)
       if (cb + u < x.nparts) s[u & 3] += v[u];  // stripe u mod 4 in chunk order
   }
   return (s[0] + s[1]) + (s[2] + s[3]);

@@ -126,9 +126,15 @@ __device__ __forceinline__ void slab_sum_body(const double* __restrict__ part, d
   for (int64_t base = (int64_t)bid * 64; base < n; base += (int64_t)nb * 64) {
     const int64_t e = base + lane;
     double s = 0.0;
-    if (e < n) {
-#pragma unroll 4
-      for (int c = w; c < nparts; c += 4) s += part[(int64_t)c * stride + e];
+    if (e < n) {  // up to 16 partials of a wave's loads in flight, summed in the same order
+      for (int c0 = w; c0 < nparts; c0 += 64) {
+        double x[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) x[u] = part[(int64_t)min(c0 + 4 * u, nparts - 1) * stride + e];
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (c0 + 4 * u < nparts) s += x[u];
+      }
     }
     red[w][lane] = s;
     __syncthreads();
@@ -317,7 +323,11 @@ __global__ __launch_bounds__(64) void beta_lambda_kernel(BLArgs a) {
 // LDS of the body (doubles): the four waves' tiles, G, iV, Gamma, tau
 constexpr int BLW_LDS = 4 * WV_TILE + 32 * 33 + 32 * 32 + 32 * 8 + 64;
 // (gamma2_partial_body from XZ's chunk partials in the fused launch: K x SB, SB x nt, 4 nc SB)
-static_assert(32 * 32 + 32 * 8 + 4 * 32 * 32 <= BLW_LDS, "fused Gamma2 partial: LDS");
+// species per block of updateGamma2's species sums (gamma2_partial_body): small blocks, so that
+// a block's partial is quick when it sums XZ from updateZ's chunk partials itself (the fused
+// launch with xz_parts > 0)
+constexpr int G2SB = 8;
+static_assert(32 * G2SB + G2SB * 8 + 4 * 32 * G2SB <= BLW_LDS, "fused Gamma2 partial: LDS");
 
 // the fused Gamma2 + BetaLambda launch's publish value for sweep `iter`: never 0 (the reset
 // value hmsc_run / the eager launcher write), distinct for distinct sweeps of a run
@@ -413,6 +423,9 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
 #pragma unroll
   for (int q = 0; q < 8; ++q) trj[q] = q < nt ? a.Tr[jj + (size_t)a.ns_loc * q] : 0.0;
   const int nai = a.na_index ? a.na_index[jj] : -1;
+  // the draw's noise (R/updateBetaLambda.R:101) needs none of it: drawn while the loads fly
+  const double xi_bl = (i < K && !a.noise_zero && j < a.ns_loc)
+                           ? normal(a.key, (uint32_t)(a.sp0 + j), (uint32_t)i, S_BETALAMBDA, SWEEP_ITER(a)) : 0.0;
   if (side_n > 0) side_wait_lanes(side_sync, side_n, side_epoch, gsync);
   if (WAIT_GAMMA && blk == 0 && w == 0) HMSC_STAMP_RT(84);
   // what the previous sweep's side chain published (device-coherent after its flags)
@@ -445,6 +458,7 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
     while (r < a.nr && f0 + a.lev_nf[r] <= i - nc) f0 += a.lev_nf[r++];
     for (int h = f0; h <= i - nc; ++h) tau *= sTau[h];
   }
+  if (WAIT_GAMMA && blk == 40 && w == 0) HMSC_STAMP_RT(100);
   // prior precision diagonal of Lambda rows: Psi_hj * tau_h
   const double pd = (i >= nc && i < K) ? psi * tau : 0.0;
   // iU = P + XEtaTXEta * iSigma[j]   (:83-92)
@@ -461,13 +475,26 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
       x[k] = (i < K && k < K) ? v : (i == k ? 1.0 : 0.0);
     }
   } else {
+    // every LDS read of the row first, at clamped addresses, then the sums (a read per column
+    // with its use right behind it waited out two LDS round trips per column: ~8 k cycles at K =
+    // 32); the same operations as one column at a time, uncontracted
+    double gk[NM], vk[NM];
+    const int ivr = i < nc ? ir : 0;
 #pragma unroll
     for (int k = 0; k < NM; ++k) {
       const int kc = k < K ? k : 0;
-      double v = isig * sG[ir + 33 * kc];
-      if (i < nc && k < nc) v += sIV[ir + nc * kc];
-      if (i == k) v += pd;
-      x[k] = (i < K && k < K) ? v : (i == k ? 1.0 : 0.0);
+      gk[k] = sG[ir + 33 * kc];
+      vk[k] = sIV[ivr + nc * (k < nc ? k : 0)];
+    }
+    {
+#pragma clang fp contract(off)
+#pragma unroll
+      for (int k = 0; k < NM; ++k) {
+        double v = isig * gk[k];
+        if (i < nc && k < nc) v += vk[k];
+        if (i == k) v += pd;
+        x[k] = (i < K && k < K) ? v : (i == k ? 1.0 : 0.0);
+      }
     }
   }
   if (a.dbg_prec && i < K)
@@ -476,6 +503,10 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
       if (k < K) a.dbg_prec[(size_t)j * K * K + i + (size_t)K * k] = x[k];
   double dinv;
   if (blk == 0) HMSC_STAMP(61);
+  if (WAIT_GAMMA && blk == 40 && w == 0) HMSC_STAMP_RT(101);
+  // the Gamma flag's first poll goes out ahead of the factorization, its latency under it
+  const int g_epoch = WAIT_GAMMA ? g2bl_epoch(SWEEP_ITER(a)) : 0;
+  const int g_seen = WAIT_GAMMA ? __hip_atomic_load(&gsync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
   wv_chol<NM>(x, dinv);                    // RiU = chol(iU)  (:98)
   if (blk == 0) HMSC_STAMP(62);
   if (WAIT_GAMMA && blk == 0 && w == 0) HMSC_STAMP_RT(74);
@@ -490,8 +521,8 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
     // invalidates the XCD's L2, and a thousand of them under every other wave of the device
     // took the solves after the wait from 5 to 16 us; bounded: a broken handshake raises the
     // error flag (hmsc_run reports it) instead of hanging
-    const int epoch = g2bl_epoch(SWEEP_ITER(a));
-    if (!spin_until<8>([&] { return __hip_atomic_load(&gsync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch; }) &&
+    if (g_seen != g_epoch &&
+        !spin_until<8>([&] { return __hip_atomic_load(&gsync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g_epoch; }) &&
         i == 0)
       __hip_atomic_store(&gsync[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (blk == 0 && w == 0) HMSC_STAMP_RT(75);
@@ -511,17 +542,29 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
   }
   // rhs = P Mu + isXTS   (:66, :100)
   double r = isig * xz;
-  if (i < nc) {
-    double pm = 0.0;
-    for (int c = 0; c < nc; ++c) pm += sIV[i + nc * c] * bcast(mu, c);
-    r += pm;
+  {
+    double ivc[NM];  // (the row's LDS reads together, then the chain)
+    const int ivr = i < nc ? i : 0;
+#pragma unroll
+    for (int c = 0; c < NM; ++c) ivc[c] = sIV[ivr + nc * (c < nc ? c : 0)];
+    if (i < nc) {
+      double pm = 0.0;
+#pragma unroll
+      for (int c = 0; c < NM; ++c)
+        if (c < nc) pm += ivc[c] * bcast(mu, c);
+      r += pm;
+    }
   }
+  if (WAIT_GAMMA && blk == 40 && w == 0) HMSC_STAMP_RT(102);
   wv_forward<NM>(x, dinv, r);              // y = L^-1 rhs
-  if (i < K && !a.noise_zero) r += normal(a.key, (uint32_t)(a.sp0 + j), (uint32_t)i, S_BETALAMBDA, SWEEP_ITER(a));
+  if (WAIT_GAMMA && blk == 40 && w == 0) HMSC_STAMP_RT(103);
+  if (i < K && !a.noise_zero) r += xi_bl;
   if (blk == 0) HMSC_STAMP(63);
   double lt[NM];
   wv_transpose<NM, true>(x, lt, lds);
+  if (WAIT_GAMMA && blk == 40 && w == 0) HMSC_STAMP_RT(104);
   wv_backward_t<NM>(lt, dinv, r);          // m + backsolve(RiU, xi)  (:101)
+  if (WAIT_GAMMA && blk == 40 && w == 0) HMSC_STAMP_RT(105);
   // the fused launch: write-through, so the side work forked on the device at the tails flag
   // (post_bl_kernel, still inside this launch's lifetime) reads the new column coherently
   if (i < K) {
@@ -1116,37 +1159,37 @@ __device__ __forceinline__ void gamma2_partial_body(const XZSrc& XZ, const doubl
                                                     int ns_loc, const double* Tr, double* part, double* smem, int bid,
                                                     bool coherent = false) {
   // part[b] = [ XZ[0:nc, block] Tr (nc*nt) | Lambda_all[:, block] Tr (NF*nt) ]
-  double* sX = smem;             // K x SB: rows < nc from XZ, rows >= nc from BL (Lambda)
-  double* sTr = sX + K * SB;     // SB x nt
-  const int t = threadIdx.x, j0 = bid * SB, nj = min(SB, ns_loc - j0);
+  double* sX = smem;             // K x G2SB: rows < nc from XZ, rows >= nc from BL (Lambda)
+  double* sTr = sX + K * G2SB;     // G2SB x nt
+  const int t = threadIdx.x, j0 = bid * G2SB, nj = min(G2SB, ns_loc - j0);
   if (XZ.part) {
     // rows < nc from updateZ's chunk partials (the fused launch; LDS for the stripe sums):
     // task (element e of the nc x nj block, stripe w) sums partials w, w + 4, ... in order
     // (slab_sum_body's), four tasks' loads in flight per thread; the stripes then meet as
     // (s0 + s1) + (s2 + s3), the reduced buffer's bits
-    double* sS = sTr + SB * nt;  // [stripe][e] (task w ne + e: neighbouring threads, neighbouring rows)
+    double* sS = sTr + G2SB * nt;  // [stripe][e] (task w ne + e: neighbouring threads, neighbouring rows)
     const int ne = nc * nj, ntask = 4 * ne, n = XZ.nparts;
     for (int q0 = 0; q0 < ntask; q0 += 256 * 4) {
       double acc[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[u] = 0.0;
-      for (int cb = 0; cb < n; cb += 32) {
-        double x[4][8];
+      for (int cb = 0; cb < n; cb += 48) {  // (one round at the z launch's 48 chunks)
+        double x[4][12];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int task = q0 + t + 256 * u, e = task % ne, w = task / ne, k = e % nc, jj = e / nc;
           const double* src = XZ.part + k + (size_t)K * (j0 + jj);
 #pragma unroll
-          for (int v = 0; v < 8; ++v) {
+          for (int v = 0; v < 12; ++v) {
             const int c = cb + w + 4 * v;
-            x[u][v] = (task < ntask && c < n) ? src[(int64_t)c * XZ.stride] : 0.0;
+            x[u][v] = task < ntask ? src[(int64_t)min(c, n - 1) * XZ.stride] : 0.0;
           }
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int w = (q0 + t + 256 * u) / ne;
 #pragma unroll
-          for (int v = 0; v < 8; ++v)
+          for (int v = 0; v < 12; ++v)
             if (cb + w + 4 * v < n) acc[u] += x[u][v];
         }
       }
@@ -1172,8 +1215,8 @@ __device__ __forceinline__ void gamma2_partial_body(const XZSrc& XZ, const doubl
       sX[p] = k < nc ? XZ.XZ[g] : BL[g];
     }
   }
-  for (int p = t; p < SB * nt; p += 256) {
-    const int jj = p % SB, q = p / SB;
+  for (int p = t; p < G2SB * nt; p += 256) {
+    const int jj = p % G2SB, q = p / G2SB;
     sTr[p] = jj < nj ? Tr[j0 + jj + (size_t)ns_loc * q] : 0.0;
   }
   __syncthreads();
@@ -1190,7 +1233,7 @@ __device__ __forceinline__ void gamma2_partial_body(const XZSrc& XZ, const doubl
     }
     double acc = 0.0;
 #pragma unroll 8
-    for (int jj = 0; jj < nj; ++jj) acc = fma(sX[k + K * jj], sTr[jj + SB * q], acc);
+    for (int jj = 0; jj < nj; ++jj) acc = fma(sX[k + K * jj], sTr[jj + G2SB * q], acc);
     if (coherent)
       store_coherent(out + p, acc);
     else
@@ -1307,7 +1350,7 @@ __device__ __forceinline__ void batched_for(int n, Load load, Store store) {
   for (int p0 = threadIdx.x; p0 < n; p0 += U * nt) {
     double v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = p0 + u * nt < n ? load(p0 + u * nt) : 0.0;
+    for (int u = 0; u < U; ++u) v[u] = load(min(p0 + u * nt, n - 1));  // (clamped, unconditional)
 #pragma unroll
     for (int u = 0; u < U; ++u)
       if (p0 + u * nt < n) store(p0 + u * nt, v[u]);
@@ -1358,16 +1401,16 @@ __device__ __forceinline__ void gamma2_final_main(const G2Args& a, double* lds) 
   // species-block partials: 8 groups of 32 threads, each summing every 8th part in order; up to
   // 64 parts every load of a thread is issued before the prep staging's (one latency for both)
   const int g = t >> 5, l = t & 31;
-  double x[2][8];
-  const bool direct = grouped && a.nparts <= 64;
+  double x[2][16];
+  const bool direct = grouped && a.nparts <= 128;
   if (direct)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int p = min(32 * h + l, P - 1);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 16; ++u) {
         const double* q = a.part + (size_t)min(g + 8 * u, a.nparts - 1) * P + p;
-        x[h][u] = a.coherent ? load_coherent(q) : *q;
+        x[h][u] = a.coherent ? load_coherent(q) : *q;  // (clamped address, unconditional)
       }
     }
   if (a.stage) {
@@ -1384,7 +1427,7 @@ __device__ __forceinline__ void gamma2_final_main(const G2Args& a, double* lds) 
       if (p < P) {
         if (direct) {
 #pragma unroll
-          for (int u = 0; u < 8; ++u)
+          for (int u = 0; u < 16; ++u)
             if (g + 8 * u < a.nparts) s += x[p0 ? 1 : 0][u];
         } else {
           for (int b = g; b < a.nparts; b += 64) {  // eight loads in flight per step, summed in order
@@ -1432,9 +1475,12 @@ __device__ __forceinline__ void gamma2_final_main(const G2Args& a, double* lds) 
   for (int p = t; p < n1; p += blockDim.x) {
     const int c = p % nc, q = p / nc;
     double s = 0.0;
+    if (stage_g) {
 #pragma unroll 8
-    for (int f = 0; f < a.NF; ++f)
-      s += (stage_g ? L.sGL[c + nc * f] : a.G[c + a.Kmax * (nc + f)]) * L.LTr[f + a.NF * q];
+      for (int f = 0; f < a.NF; ++f) s += L.sGL[c + nc * f] * L.LTr[f + a.NF * q];
+    } else {
+      for (int f = 0; f < a.NF; ++f) s += a.G[c + a.Kmax * (nc + f)] * L.LTr[f + a.NF * q];
+    }
     L.S0[p] -= s;
   }
   __syncthreads();
@@ -1900,6 +1946,7 @@ struct G2BLArgs {
   // workgroup 0 waits for): g2.nparts on one rank; 0 on a sharded chain, whose Gamma2 sums
   // arrive all-reduced (g2.part = ar_a, g2.nparts = 1)
   int part_wg;
+  int part_tail;        // the partial workgroups follow the BetaLambda ones (else: the first of them)
   int* sync;            // [ticket, epoch of the published Gamma, -, handshake timed out]
   BLTailArgs tail;      // the BetaLambda workgroups' tail (crw_on): Eta constants [+ side partials]
   int crw_on;
@@ -1911,8 +1958,9 @@ struct G2BLArgs {
 
 template <int NM>
 __global__ __launch_bounds__(256) void gamma2_bl_kernel(G2BLArgs f) {
+  kernarg_warm<sizeof(G2BLArgs)>();
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int nparts = f.part_wg, nbl = (int)gridDim.x - 1;
+  const int nparts = f.part_wg, nbl = (int)gridDim.x - 1 - (f.part_tail ? nparts : 0);
   if (blockIdx.x == 0) {
     const unsigned long long kt0 = f.kt_g2 ? kt_now() : 0ull;
     if (threadIdx.x < 64) HMSC_STAMP_RT(70);
@@ -1948,12 +1996,22 @@ __global__ __launch_bounds__(256) void gamma2_bl_kernel(G2BLArgs f) {
   }
   const int b = blockIdx.x - 1;
   if (b == 40 && threadIdx.x < 64) HMSC_STAMP_RT(97);
-  if (b < nparts) {
-    if (b == 0 && threadIdx.x < 64) HMSC_STAMP_RT(71);
-    gamma2_partial_body(f.xz, f.BLold, f.K, f.nc, f.NF, f.nt, f.nsl, f.Tr, f.part, smem, b, true);
+  // Gamma2's partials: part_tail, on workgroups of their own after the BetaLambda ones (default);
+  // else on the first nparts BetaLambda workgroups ahead of their bodies
+  const int pb = f.part_tail ? b - nbl : b;
+  if (pb >= 0 && pb < nparts) {
+    if (pb == 0 && threadIdx.x < 64) HMSC_STAMP_RT(71);
+#ifdef HMSC_STAMPS
+    if (pb < 160 && threadIdx.x == 0) g_stamps[700 + pb] = __builtin_amdgcn_s_memrealtime();
+#endif
+    gamma2_partial_body(f.xz, f.BLold, f.K, f.nc, f.NF, f.nt, f.nsl, f.Tr, f.part, smem, pb, true);
     vm_stores_done();
     __syncthreads();  // every wave's partial stores have completed (and the LDS is free again)
     if (threadIdx.x == 0) __hip_atomic_fetch_add(&f.sync[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef HMSC_STAMPS
+    if (pb < 160 && threadIdx.x == 0) g_stamps[860 + pb] = __builtin_amdgcn_s_memrealtime();
+#endif
+    if (f.part_tail) return;
   }
   const uint32_t iter = SWEEP_ITER(f.g2);
   const BLCol col = beta_lambda_wave_body<NM, true>(f.bl, smem, b, f.sync, f.side_sync, g2bl_epoch(iter - 1),
@@ -1990,9 +2048,9 @@ void launch_gamma2(State& s, uint32_t iter) {
     join_side(s);
     launch_gamma2_prep(s, s.stream);
   }
-  const int nparts = (s.nsl + SB - 1) / SB;
+  const int nparts = (s.nsl + G2SB - 1) / G2SB;
   flush_xz(s);  // (the stripe sums of a partial-reading gamma2_partial_body need the fused launch's LDS)
-  gamma2_partial_kernel<<<nparts, 256, (size_t)(s.K * SB + SB * s.nt) * sizeof(double), s.stream>>>(
+  gamma2_partial_kernel<<<nparts, 256, (size_t)(s.K * G2SB + G2SB * s.nt) * sizeof(double), s.stream>>>(
       xz_src(s), s.BL, s.K, s.nc, s.NF, s.nt, s.nsl, s.Tr, s.ABpart);
   HIP_OK(hipGetLastError());
   const int n1 = s.nc * s.nt, n2 = s.NF * s.nt;
@@ -2107,7 +2165,7 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
   if (sh && !s.g2s_valid) shard_g2_stats(s);
   if (!s.g2prep_valid) launch_gamma2_prep(s, s.stream);
   G2BLArgs f{};
-  const int nparts = (s.nsl + SB - 1) / SB;
+  const int nparts = (s.nsl + G2SB - 1) / G2SB;
   const int n12 = s.nc * s.nt + s.NF * s.nt;
   G2Args& a = f.g2;
   a.nc = s.nc;
@@ -2169,8 +2227,12 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
     HIP_OK(hipMemsetAsync(s.gbl_sync + 1, 0, 2 * sizeof(int), s.stream));
     HIP_OK(hipMemsetAsync(s.crw_flag, 0, sizeof(int), s.stream));
   }
-  const int nb = 1 + (s.nsl + 3) / 4;
-  HMSC_REQUIRE(f.part_wg <= nb - 1, "fused Gamma2 + BetaLambda: more Gamma2 partials than BetaLambda workgroups");
+  // the partials on workgroups of their own after the BetaLambda ones (the launch's 52 KB of
+  // LDS and <= 256 VGPRs keep two workgroups per CU resident); HMSC_G2_PART_INLINE: ahead of
+  // the first BetaLambda bodies instead
+  f.part_tail = getenv_flag("HMSC_G2_PART_INLINE") ? 0 : 1;
+  const int nb = 1 + (s.nsl + 3) / 4 + (f.part_tail ? f.part_wg : 0);
+  HMSC_REQUIRE(f.part_tail || f.part_wg <= nb - 1, "fused Gamma2 + BetaLambda: more Gamma2 partials than BetaLambda workgroups");
   const size_t smem = BLW_LDS * sizeof(double);
   ProfScope ps(s, PROF_BL);
   switch (wv_bucket(s.K)) {
@@ -2343,6 +2405,7 @@ template <int NM>
 __global__ __launch_bounds__(256) void side_chain_kernel(GVWArgs g, LPArgs lp, const double* rs_part, int nparts,
                                                          int rs_ld, const int* tails_flag, int* err,
                                                          unsigned long long* kt) {
+  kernarg_warm<sizeof(GVWArgs) + sizeof(LPArgs) + 64>();
   const unsigned long long kt0 = kt ? kt_now() : 0ull;
   // A latency-bound chain of small factorisations running beside the main stream's Eta and z
   // waves on the same SIMDs: raised issue priority, so its few waves are not starved by the
@@ -2835,6 +2898,7 @@ static_assert(ef_lds_doubles<8>() >= 4 * CRW_TILE + 32 * 16 + 256, "EF_DEFER red
 #endif
 template <int NFB, int MODE>
 __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
+  kernarg_warm<sizeof(EtaFArgs)>();
   // one block carved into the stages' arrays (EF_DEFER's reducer workgroups: their scratch)
   __shared__ __attribute__((aligned(16))) double sAll[ef_lds_doubles<NFB>()];
   double(*sPart)[16][EF_SITES + 1] = reinterpret_cast<double(*)[16][EF_SITES + 1]>(sAll);  // [wave][factor][site] ZL partials (EF_SOLVE: W's scratch)
@@ -3078,6 +3142,7 @@ struct PostBLArgs {
 
 // workgroup b < n_gv: GammaV partial block b; b < n_psi: psi part b
 __global__ __launch_bounds__(256) void post_bl_kernel(PostBLArgs a) {
+  kernarg_warm<sizeof(PostBLArgs)>();
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x;
   const bool coh = a.tails_flag != nullptr;
@@ -3984,8 +4049,8 @@ static void shard_g2_stats(State& s) {
   a.NF = s.NF;
   a.nt = s.nt;
   a.nsl = s.nsl;
-  a.nparts = (s.nsl + SB - 1) / SB;
-  g2_stats_kernel<<<a.nparts, 256, (size_t)(s.K * SB + SB * s.nt) * sizeof(double), s.stream>>>(a);
+  a.nparts = (s.nsl + G2SB - 1) / G2SB;
+  g2_stats_kernel<<<a.nparts, 256, (size_t)(s.K * G2SB + G2SB * s.nt) * sizeof(double), s.stream>>>(a);
   HIP_OK(hipGetLastError());
   ar_point(s, s.ar_a, (size_t)n12 + 1);  // all-reduce A
   s.g2s_valid = true;

@@ -397,6 +397,7 @@ constexpr int ZT_TLD = 17;  // leading dimension of the wave's 16-site x 32-spec
 // loaded 64 rows at a time and the waves' XZ combined 64 rows at a time (LDS).
 template <bool DRAW, bool HAS_NA, int NKB, int MODE = Z_ALL, bool POIS = false, bool NORMAL = true>
 __global__ __launch_bounds__(256, NKB > 4 ? 2 : 4) void z_wave_kernel(ZArgs a) {
+  kernarg_warm<sizeof(ZArgs)>();
   extern __shared__ __attribute__((aligned(16))) double smem[];
   if (a.gred_y0 && blockIdx.y == 0) {  // the co-launched G reduction row
     g_reduce_body(a, smem);

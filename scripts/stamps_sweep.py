@@ -38,6 +38,14 @@ print("  side chain: start", v[11] - t0, "tails seen", v[12] - t0, "GammaV out",
 v = np.array([st[i] for i in range(91, 98)], dtype=np.float64) - t0
 print("  BL workgroup 40 (10 ns from workgroup 0 start): kernel entry %.0f body entry %.0f loads issued %.0f staged %.0f"
       " chol done %.0f Gamma seen %.0f end %.0f" % (v[6], v[0], v[1], v[2], v[3], v[4], v[5]))
+v = np.array([st[i] for i in range(100, 106)], dtype=np.float64) - t0
+print("  BL workgroup 40: tau done %.0f precision built %.0f rhs formed %.0f forward done %.0f transposed %.0f backward done %.0f" % tuple(v))
+if "--parts" in sys.argv:  # Gamma2 partial workgroups: start / end (wall clock) from workgroup 0's start
+    allst = np.array(ch.debug_get("stamps", 1024), dtype=np.float64)
+    n = int(sys.argv[sys.argv.index("--parts") + 1])
+    ps, pe = allst[700:700 + n] - t0, allst[860:860 + n] - t0
+    print("  Gamma2 partials (10 ns): start min %.0f max %.0f  end min %.0f median %.0f max %.0f  longest %.0f" %
+          (ps.min(), ps.max(), pe.min(), np.median(pe), pe.max(), (pe - ps).max()))
 if "--blocks" in sys.argv:  # per-BetaLambda-workgroup body end (wall clock), from workgroup 0's start
     allst = ch.debug_get("stamps", 1024)
     e = np.array(allst[256:256 + 250], dtype=np.float64) - t0
