@@ -742,10 +742,11 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   // workspaces
   const int n_tiles = (ny + 63) / 64;
   s.ntile_j = (nsl + 31) / 32;
-  // three rounds of the resident z workgroups: a grid of exactly one round leaves every
+  // four rounds of the resident z workgroups: a grid of exactly one round leaves every
   // workgroup displaced by a concurrent side-stream kernel to run after the round (measured
-  // 142 us vs 104 us per launch at the config-4 size, scripts/z_chunk_sweep.sh)
-  s.nchunk = std::max(1, std::min(n_tiles, 3 * z_resident_slots(s) / std::max(1, s.ntile_j)));
+  // 142 us vs 104 us per launch at the config-4 size, scripts/z_chunk_sweep.sh); 16 / 24 / 32 /
+  // 48 / 64 / 96 chunks at config 4: z 90 / 91 / 82 / 83 / 79 / 80 us (round 5, HMSC_Z_CHUNKS)
+  s.nchunk = std::max(1, std::min(n_tiles, 4 * z_resident_slots(s) / std::max(1, s.ntile_j)));
   if (const char* e = std::getenv("HMSC_Z_CHUNKS"))  // tuning knob: site chunks of the z grid
     if (std::atoi(e) > 0) s.nchunk = std::max(1, std::min(n_tiles, std::atoi(e)));
   const int n_sblk = (ny + 63) / 64;

@@ -346,12 +346,12 @@ struct XZSrc {
 __device__ __forceinline__ double xz_get(const XZSrc& x, size_t g) {
   if (!x.part) return x.XZ[g];
   double s[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int cb = 0; cb < x.nparts; cb += 48) {  // 48 partials' loads in flight (one round at the
-    double v[48];                                // z launch's 48 chunks), then their sums
+  for (int cb = 0; cb < x.nparts; cb += 64) {  // 64 partials' loads in flight (one round up to
+    double v[64];                                // the z launch's 64 chunks), then their sums
 #pragma unroll
-    for (int u = 0; u < 48; ++u) v[u] = x.part[(int64_t)min(cb + u, x.nparts - 1) * x.stride + g];  // (clamped)
+    for (int u = 0; u < 64; ++u) v[u] = x.part[(int64_t)min(cb + u, x.nparts - 1) * x.stride + g];  // (clamped)
 #pragma unroll
-    for (int u = 0; u < 48; ++u)
+    for (int u = 0; u < 64; ++u)
       if (cb + u < x.nparts) s[u & 3] += v[u];  // stripe u mod 4 in chunk order
   }
   return (s[0] + s[1]) + (s[2] + s[3]);

@@ -1956,8 +1956,10 @@ struct G2BLArgs {
   unsigned long long* kt_g2;  // live timing of workgroup 0 (KT_G2 block) or null
 };
 
+// (two workgroups per CU: with Gamma2's partial workgroups after the BetaLambda ones the launch
+// exceeds one per CU, and its workgroups wait on each other, so all must be resident together)
 template <int NM>
-__global__ __launch_bounds__(256) void gamma2_bl_kernel(G2BLArgs f) {
+__global__ __launch_bounds__(256, 2) void gamma2_bl_kernel(G2BLArgs f) {
   kernarg_warm<sizeof(G2BLArgs)>();
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int nparts = f.part_wg, nbl = (int)gridDim.x - 1 - (f.part_tail ? nparts : 0);

@@ -102,14 +102,16 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   a.kt = s.kt_on ? s.d_kt + (size_t)KT_Z * 2 * KT_SLOTS : nullptr;
   dim3 grid(s.ntile_j, nchunk);  // species blocks fastest (z_kernel.h)
   size_t smem = z_smem_bytes(s.K, s.nt);
-  // XZ left as chunk partials, summed by the fused Gamma2 + BetaLambda launch where it reads
-  // them (xz_src: the BetaLambda bodies' 48-partial loads, Gamma2's species-block partials of
-  // G2SB species), so no reduction launch sits between this launch and that one, and the record
-  // pack rides along as this launch's last grid row (with NA the ZTr reduction runs anyway, and
-  // a sharded chain all-reduces XZ sums).  1000-step same box: 6,524 -> 6,574-6,582 sweeps/s
-  // (profiles/r05_fold_ab.txt); HMSC_NO_XZ_FOLD restores the reduction launch
+  // HMSC_XZ_FOLD: XZ left as chunk partials, summed by the fused Gamma2 + BetaLambda launch
+  // where it reads them (xz_src: the BetaLambda bodies' partial loads, Gamma2's species-block
+  // partials of G2SB species), so no reduction launch sits between this launch and that one,
+  // and the record pack rides along as this launch's last grid row (with NA the ZTr reduction
+  // runs anyway, and a sharded chain all-reduces XZ sums).  Off by default: at four rounds of
+  // z workgroups (capi.cpp) the reduction launch measured 6,677-6,713 sweeps/s against the
+  // fold's 6,601-6,688 (its ~15 MB of partial loads land on the BetaLambda prologue), and at
+  // three rounds the fold led by ~1 % (profiles/r05_fold_ab2.txt)
   const bool fold = draw && !s.has_na && !s.sharded && !s.phylo && gamma2_bl_fusion_ok(s) &&
-                    !getenv_flag("HMSC_NO_XZ_FOLD");
+                    getenv_flag("HMSC_XZ_FOLD");
   a.pack_row = 0;
   if (fold && s.pack_req && s.side_fused && s.capturing) {  // ... and the record pack rides along
     a.pack_row = 1;

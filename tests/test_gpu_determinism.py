@@ -76,14 +76,14 @@ def test_two_chains_one_device_fused_path_with_graphs():
     _same_post(fit2, fit1)
 
 
-@pytest.mark.parametrize("env", ["HMSC_NO_XZ_FOLD", "HMSC_NO_TAIL_DEFER", "HMSC_NO_SIDE_GATE", "HMSC_G2_PART_INLINE"])
+@pytest.mark.parametrize("env", ["HMSC_XZ_FOLD", "HMSC_NO_TAIL_DEFER", "HMSC_NO_SIDE_GATE", "HMSC_G2_PART_INLINE"])
 def test_launch_variants_bitwise(env, monkeypatch):
     """Launch-structure variants give the same bits: XZ read from updateZ's chunk partials by the
-    fused Gamma2 + BetaLambda launch (default, with the record pack in the z launch) or reduced
-    first (HMSC_NO_XZ_FOLD), Gamma2's species-block partials on workgroups of their own (default)
+    fused Gamma2 + BetaLambda launch (HMSC_XZ_FOLD, with the record pack in the z launch) or
+    reduced first (default), Gamma2's species-block partials on workgroups of their own (default)
     or ahead of the first BetaLambda bodies (HMSC_G2_PART_INLINE), the BetaLambda tail's last
-    level deferred to the Eta launch (default) or not, and -- behind the reduction launch -- the
-    previous sweep's side chain awaited by that launch or polled by the fused launch itself
+    level deferred to the Eta launch (default) or not, and the previous sweep's side chain awaited
+    by the reduction launch after updateZ (default) or polled by the fused launch itself
     (HMSC_NO_SIDE_GATE).  A probit-only model (the fused paths), recorded graph sweeps."""
     def fit():
         hM = synthetic_model(ny=300, ns=60, nc=4, nf=3, seed=17)
