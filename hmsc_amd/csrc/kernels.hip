@@ -3988,23 +3988,35 @@ __global__ __launch_bounds__(256) void g2_stats_kernel(G2SArgs a) {
     __hip_atomic_store(a.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const int n1 = a.nc * a.nt, P = n1 + a.NF * a.nt;
-  for (int p = t; p < P; p += 256) {
-    // (every part's load of a chunk issued before the first sum: a load-use loop paid one
-    // device-coherent round trip per part, ~14 us at 32 parts)
-    double v = 0.0;
-    if (P <= 64 && a.nparts > 1) {  // gamma2_final_body: 8 groups of every 8th part, then the groups
-      double sg[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-      for (int b0 = 0; b0 < a.nparts; b0 += 32) {
-        double x[32];
+  if (P <= 64 && a.nparts > 1) {
+    // gamma2_final_main's order: 8 groups of 32 threads, group g summing parts g, g + 8, ... (16
+    // loads of a thread in flight), then the groups in order -- the 256 threads together
+    // instead of one thread per output walking every part
+    __shared__ double red[8][64];
+    const int g = t >> 5, l = t & 31;
+    for (int p0 = 0; p0 < P; p0 += 32) {
+      const int p = min(p0 + l, P - 1);
+      double sg = 0.0;
+      for (int b0 = g; b0 < a.nparts; b0 += 128) {
+        double x[16];
 #pragma unroll
-        for (int u = 0; u < 32; ++u) x[u] = load_coherent(a.part + (size_t)min(b0 + u, a.nparts - 1) * P + p);
+        for (int u = 0; u < 16; ++u) x[u] = load_coherent(a.part + (size_t)min(b0 + 8 * u, a.nparts - 1) * P + p);
 #pragma unroll
-        for (int u = 0; u < 32; ++u)
-          if (b0 + u < a.nparts) sg[u & 7] += x[u];  // part b0 + u is in group u mod 8 (b0 mod 8 == 0)
+        for (int u = 0; u < 16; ++u)
+          if (b0 + 8 * u < a.nparts) sg += x[u];
       }
+      red[g][p0 + l] = sg;
+    }
+    __syncthreads();
+    for (int p = t; p < P; p += 256) {
+      double v = 0.0;
 #pragma unroll
-      for (int g = 0; g < 8; ++g) v += sg[g];
-    } else {
+      for (int g2 = 0; g2 < 8; ++g2) v += red[g2][p];
+      a.out[p] = (p < n1 && a.xtztr) ? a.xtztr[p] : v;
+    }
+  } else {
+    for (int p = t; p < P; p += 256) {
+      double v = 0.0;
       for (int b0 = 0; b0 < a.nparts; b0 += 32) {
         double x[32];
 #pragma unroll
@@ -4013,8 +4025,8 @@ __global__ __launch_bounds__(256) void g2_stats_kernel(G2SArgs a) {
         for (int u = 0; u < 32; ++u)
           if (b0 + u < a.nparts) v += x[u];
       }
+      a.out[p] = (p < n1 && a.xtztr) ? a.xtztr[p] : v;
     }
-    a.out[p] = (p < n1 && a.xtztr) ? a.xtztr[p] : v;
   }
   __syncthreads();
   int c = 0;
