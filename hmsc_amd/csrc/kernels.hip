@@ -1521,14 +1521,14 @@ __global__ __launch_bounds__(256) void gamma2_final_kernel(G2Args a) {
 // back; BetaLambda's precision iU and its Cholesky factor do not depend on the Gamma that
 // Gamma2 draws, only its mean does).  Workgroups 1 .. nbl run the wave BetaLambda body (four
 // species each, one per wave), which factors iU while Gamma2 runs and waits for Gamma only
-// for the mean and the solves; the first nparts of them form one of Gamma2's species-block
-// partials first (device-coherent stores, a relaxed count in sync[0]).  Workgroup 0 waits for
-// the count, reduces the partials in block order, runs the final stage and publishes Gamma
-// (sync[1]).  One extra workgroup instead of nparts: the launch is nbl + 1 <= 256 workgroups
-// at the config-4 size, one per CU -- with nparts separate partial workgroups some CUs carried
-// two BetaLambda chains and the slowest species finished ~8 us after the rest.  Every
-// workgroup of the launch is resident at once (two per CU at 52 KB of LDS), and workgroup 0 is
-// dispatched before the ones it waits for, so no wait can block the workgroup it waits for.
+// for the mean and the solves; nparts further workgroups after them (G2SB species each) form
+// Gamma2's species-block partials (device-coherent stores, a relaxed count in sync[0]).
+// Workgroup 0 waits for the count, reduces the partials in block order, runs the final stage
+// and publishes Gamma (sync[1]).  (Round 4 put the partials ahead of the first BetaLambda
+// bodies to keep the launch at one workgroup per CU; those bodies then ended ~3 us after the
+// rest, and the trailing partial workgroups measured faster, HMSC_G2_PART_INLINE restores
+// it.)  Every workgroup of the launch is resident at once (two per CU: 52 KB of LDS and
+// __launch_bounds__(256, 2)), and workgroup 0 is dispatched before the ones it waits for.
 // Workgroup 0 resets the count; the flag holds the sweep's epoch (g2bl_epoch), reset to 0 by
 // the host at the start of every run and before every eager launch, so it never needs a reset
 // inside the launch.
