@@ -386,15 +386,21 @@ SideGate side_gate_next(State& s, uint32_t iter) {
 struct BLCol {
   double r, mu, tau, isig;
   unsigned long long kt0, kt1;  // the wave's body start / end (wall clock) when the tail records them
+  double gpre;                  // the tail's psi draw before its rate (BLPre), when pre-drawn
+};
+
+// Work the body runs for the tail while its prologue's loads fly: none by default
+struct BLNoPre {
+  __device__ double operator()(int, int) const { return 0.0; }
 };
 
 // side_wait (the fused launch inside a sweep graph, sweeps after the first): iV and Delta come
 // from the previous sweep's side chain, which publishes them through side_sync instead of a
 // cross-queue graph edge; they are read with device-coherent loads after its flags.
-template <int NM, bool WAIT_GAMMA>
+template <int NM, bool WAIT_GAMMA, class Pre = BLNoPre>
 __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* lds0, int blk, int* gsync,
                                                        const int* side_sync = nullptr, int side_epoch = 0,
-                                                       int side_n = 0) {
+                                                       int side_n = 0, Pre pre = Pre{}) {
   double* tiles = lds0;
   double* sG = tiles + 4 * WV_TILE;
   double* sIV = sG + 32 * 33;
@@ -426,6 +432,7 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
   // the draw's noise (R/updateBetaLambda.R:101) needs none of it: drawn while the loads fly
   const double xi_bl = (i < K && !a.noise_zero && j < a.ns_loc)
                            ? normal(a.key, (uint32_t)(a.sp0 + j), (uint32_t)i, S_BETALAMBDA, SWEEP_ITER(a)) : 0.0;
+  const double gpre = j < a.ns_loc ? pre(j, i) : 0.0;
   if (side_n > 0) side_wait_lanes(side_sync, side_n, side_epoch, gsync);
   if (WAIT_GAMMA && blk == 0 && w == 0) HMSC_STAMP_RT(84);
   // what the previous sweep's side chain published (device-coherent after its flags)
@@ -449,7 +456,7 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
   if (t < a.NF) sTau[t] = del;  // Delta here; each lane forms its own cumprod below
   __syncthreads();
   if (WAIT_GAMMA && blk == 40 && w == 0) HMSC_STAMP_RT(93);
-  if (j >= a.ns_loc) return BLCol{0.0, 0.0, 1.0, 0.0, ~0ull, 0ull};
+  if (j >= a.ns_loc) return BLCol{0.0, 0.0, 1.0, 0.0, ~0ull, 0ull, 0.0};
   double* lds = tiles + w * WV_TILE;
   // tau = cumprod(Delta) within the level of factor i - nc   (:51)
   double tau = 1.0;
@@ -587,7 +594,7 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
     if (i == 0) g_stamps[256 + blk] = t1;
   }
 #endif
-  return BLCol{r, mu, tau, isig, kt0, kt1};
+  return BLCol{r, mu, tau, isig, kt0, kt1, gpre};
 }
 
 template <int NM>
@@ -1619,6 +1626,7 @@ __device__ __forceinline__ void crw_finish(const CRWArgs& a, const double* sCR, 
 struct BLTailArgs {
   CRWArgs crw;
   int gv_on;
+  int psi_pre;      // the body pre-drew the psi gamma variates (BLPsiPre, BLCol::gpre)
   int nt, NF, nr, sp0, gvt_ld;
   int lev_nf[HMSC_MAX_LEVELS];
   double nu[HMSC_MAX_LEVELS];
@@ -1852,7 +1860,10 @@ __device__ __forceinline__ void bl_tail(const BLTailArgs& ta, const BLCol& col, 
     const double shape = ta.nu[lv] / 2 + 0.5;
     const double rate = ta.nu[lv] / 2 + 0.5 * lam2 * col.tau;
     const uint32_t idx = (uint32_t)(h + ta.lev_nf[lv] * (ta.sp0 + j));
-    const double psi = gamma_std(ta.key, idx, S_PSI + LEVEL_STRIDE * lv, iter, shape) / rate;
+    // (the standard gamma draw needs only the shape: drawn ahead by the body, BLPsiPre; drawn
+    // by Gamma2's partial workgroups instead it delayed Gamma: 6,549-6,577 vs 6,676-6,704)
+    const double gs = ta.psi_pre ? col.gpre : gamma_std(ta.key, idx, S_PSI + LEVEL_STRIDE * lv, iter, shape);
+    const double psi = gs / rate;
     ta.Psi[f + (size_t)NF * j] = psi;
     m2 = psi * lam2;
   }
@@ -1958,6 +1969,29 @@ struct G2BLArgs {
 
 // (two workgroups per CU: with Gamma2's partial workgroups after the BetaLambda ones the launch
 // exceeds one per CU, and its workgroups wait on each other, so all must be resident together)
+// The tail's psi draw (R/updateLambdaPriors.R:22-24) is psi = g / rate with g a standard
+// gamma variate of shape nu / 2 + 1 / 2 -- independent of the new Lambda, so the body draws g
+// while its prologue's loads fly and the tail only divides (the rejection sampler was ~2.5 us
+// of the tail's chain); the same (key, index, stream, sweep), so the same bits
+__device__ __forceinline__ double psi_gamma_std(const BLTailArgs& ta, uint32_t iter, int j, int fct) {
+  int f0 = 0, lv = 0;
+  while (lv < ta.nr - 1 && fct >= f0 + ta.lev_nf[lv]) f0 += ta.lev_nf[lv++];
+  const int h = fct - f0;
+  const double shape = ta.nu[lv] / 2 + 0.5;
+  const uint32_t idx = (uint32_t)(h + ta.lev_nf[lv] * (ta.sp0 + j));
+  return gamma_std(ta.key, idx, S_PSI + LEVEL_STRIDE * lv, iter, shape);
+}
+struct BLPsiPre {
+  const BLTailArgs& ta;
+  uint32_t iter;
+  bool on;
+  int nc, K;
+  __device__ double operator()(int j, int lane) const {
+    if (!on || !ta.gv_on || lane < nc || lane >= K) return 0.0;
+    return psi_gamma_std(ta, iter, j, lane - nc);
+  }
+};
+
 template <int NM>
 __global__ __launch_bounds__(256, 2) void gamma2_bl_kernel(G2BLArgs f) {
   kernarg_warm<sizeof(G2BLArgs)>();
@@ -2017,7 +2051,8 @@ __global__ __launch_bounds__(256, 2) void gamma2_bl_kernel(G2BLArgs f) {
   }
   const uint32_t iter = SWEEP_ITER(f.g2);
   const BLCol col = beta_lambda_wave_body<NM, true>(f.bl, smem, b, f.sync, f.side_sync, g2bl_epoch(iter - 1),
-                                                    f.side_wait ? 1 + f.bl.nr : 0);
+                                                    f.side_wait ? 1 + f.bl.nr : 0,
+                                                    BLPsiPre{f.tail, iter, f.crw_on && f.tail.psi_pre, f.nc, f.K});
   if (f.crw_on) bl_tail(f.tail, col, b, nbl, iter, smem);
 }
 
@@ -2213,6 +2248,7 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
   if (crw_on) {
     f.tail = make_tail_args(s, tail_gv, sh);
     f.tail.defer = defer ? tail_defer_levels() : 0;
+    f.tail.psi_pre = getenv_flag("HMSC_NO_PSI_PRE") ? 0 : 1;
     f.bl.kt_defer = 1;
   }
   s.tail_defer = defer;

@@ -76,7 +76,8 @@ def test_two_chains_one_device_fused_path_with_graphs():
     _same_post(fit2, fit1)
 
 
-@pytest.mark.parametrize("env", ["HMSC_XZ_FOLD", "HMSC_NO_TAIL_DEFER", "HMSC_NO_SIDE_GATE", "HMSC_G2_PART_INLINE"])
+@pytest.mark.parametrize("env", ["HMSC_XZ_FOLD", "HMSC_NO_TAIL_DEFER", "HMSC_NO_SIDE_GATE", "HMSC_G2_PART_INLINE",
+                                 "HMSC_NO_PSI_PRE"])
 def test_launch_variants_bitwise(env, monkeypatch):
     """Launch-structure variants give the same bits: XZ read from updateZ's chunk partials by the
     fused Gamma2 + BetaLambda launch (HMSC_XZ_FOLD, with the record pack in the z launch) or
@@ -84,7 +85,9 @@ def test_launch_variants_bitwise(env, monkeypatch):
     or ahead of the first BetaLambda bodies (HMSC_G2_PART_INLINE), the BetaLambda tail's last
     level deferred to the Eta launch (default) or not, and the previous sweep's side chain awaited
     by the reduction launch after updateZ (default) or polled by the fused launch itself
-    (HMSC_NO_SIDE_GATE).  A probit-only model (the fused paths), recorded graph sweeps."""
+    (HMSC_NO_SIDE_GATE), and the BetaLambda tail's psi gamma variates drawn ahead by the bodies
+    (default) or in the tail (HMSC_NO_PSI_PRE).  A probit-only model (the fused paths), recorded
+    graph sweeps."""
     def fit():
         hM = synthetic_model(ny=300, ns=60, nc=4, nf=3, seed=17)
         return H.sampleMcmc(hM, samples=30, transient=40, thin=1, nChains=1, updater={"GammaEta": False},
