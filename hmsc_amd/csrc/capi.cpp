@@ -1335,8 +1335,17 @@ static void record_after_sweep(State& s, double* slot) {
 __global__ void set_iters_kernel(uint32_t* p, uint32_t v, int n) {
   if ((int)threadIdx.x < n) p[threadIdx.x] = v + threadIdx.x;
 }
-__global__ void set_desc_kernel(int32_t* d, int32_t iter0, int32_t transient, int32_t thin, int32_t samples) {
-  d[0] = iter0, d[1] = transient, d[2] = thin, d[3] = samples;
+// A run's start in one launch instead of a descriptor kernel and three fills (~25 us of the
+// 20-sweep line): the record descriptor, and the device flags a run resets -- the fused
+// Gamma2 + BetaLambda launch's epoch words, the tails' CR / W flag and the side chain's flags
+// (a run's sweeps are distinct, but an earlier run may have ended on one of them)
+__global__ void run_start_kernel(int32_t* desc, int32_t iter0, int32_t transient, int32_t thin, int32_t samples,
+                                 int* gbl, int* crw, int* side, int nside) {
+  const int t = threadIdx.x;
+  if (desc && t < 4) desc[t] = t == 0 ? iter0 : t == 1 ? transient : t == 2 ? thin : samples;
+  if (gbl && (t == 4 || t == 5)) gbl[t - 3] = 0;
+  if (crw && t == 6) crw[0] = 0;
+  if (side && t >= 8 && t < 8 + nside) side[t - 8] = 0;
 }
 
 static void destroy_graph(State& s) {
@@ -1835,14 +1844,14 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
   int max_adapt = 0;
   if (adaptNf)
     for (int r = 0; r < s.nr; ++r) max_adapt = std::max(max_adapt, adaptNf[r]);
-  if (recording) set_desc_kernel<<<1, 1, 0, s.stream>>>(s.d_rec_desc, iter0, transient, thin, samples);
   // the fused Gamma2 + BetaLambda flag holds the epoch of the last sweep that published: a
   // run's sweeps are distinct, but an earlier run may have ended on one of them
   // (the same for the tails epoch and the side chain's flags, graph sweeps' device-side joins)
   join_side(s);
-  if (s.gbl_sync) HIP_OK(hipMemsetAsync(s.gbl_sync + 1, 0, 2 * sizeof(int), s.stream));
-  if (s.crw_flag) HIP_OK(hipMemsetAsync(s.crw_flag, 0, sizeof(int), s.stream));
-  if (s.side_sync) HIP_OK(hipMemsetAsync(s.side_sync, 0, (2 + HMSC_MAX_LEVELS) * sizeof(int), s.stream));
+  static_assert(2 + HMSC_MAX_LEVELS <= 56, "run_start_kernel: side flags");
+  run_start_kernel<<<1, 64, 0, s.stream>>>(recording ? s.d_rec_desc : nullptr, iter0, transient, thin, samples,
+                                           s.gbl_sync, s.crw_flag, s.side_sync, 2 + HMSC_MAX_LEVELS);
+  HIP_OK(hipGetLastError());
   const auto t_start = std::chrono::steady_clock::now();
   int n_replays = 0;
   for (int it = 1; it <= total;) {
