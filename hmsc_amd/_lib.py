@@ -87,6 +87,24 @@ EXPORTS = ["hmsc_last_error", "hmsc_device_count", "hmsc_create", "hmsc_create_s
            "hmsc_prepare_graphs", "hmsc_post_omega", "hmsc_variance_partitioning", "hmsc_effective_size"]
 
 
+def _check_fresh():
+    """Refuse a library built from other sources than the ones beside it: build.py stamps the
+    source digest next to the library (``libhmsc_amd.so.src``).  Only the in-tree library is
+    checked; ``HMSC_AMD_LIB`` selects another build (A/B timing) without the check, and
+    ``HMSC_AMD_ALLOW_STALE=1`` skips it."""
+    if "HMSC_AMD_LIB" in os.environ or os.environ.get("HMSC_AMD_ALLOW_STALE") == "1":
+        return
+    from . import build as B
+    stamp = LIB_PATH + ".src"
+    have = open(stamp).read().strip() if os.path.exists(stamp) else None
+    want = B.source_digest()
+    if have != want:
+        raise HmscNativeError(
+            f"{LIB_PATH} is stale: " + ("no source stamp " + stamp if have is None else
+                                        "built from other sources than hmsc_amd/csrc") +
+            " -- rebuild it (python -m hmsc_amd.build)")
+
+
 def lib():
     """Load the HIP library (raises if it has not been built: no CPU fallback)."""
     global _lib
@@ -95,6 +113,7 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise HmscNativeError(
             f"{LIB_PATH} not found: build the gfx950 HIP library first (python -m hmsc_amd.build)")
+    _check_fresh()
     L = C.CDLL(LIB_PATH)
     L.hmsc_last_error.restype = C.c_char_p
     L.hmsc_device_count.argtypes = [ip]

@@ -48,6 +48,18 @@ def _digest(paths, extra):
     return h.hexdigest()
 
 
+def source_digest():
+    """Hash of the library's sources and headers (content only).  The link step writes it next
+    to the library (``libhmsc_amd.so.src``) and ``_lib.lib()`` refuses a library whose stamp
+    does not match the sources beside it (a stale library pushed with newer sources)."""
+    paths = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    h = hashlib.sha256()
+    for p in paths:
+        with open(p, "rb") as f:
+            h.update(os.path.basename(p).encode() + b"\0" + f.read())
+    return h.hexdigest()
+
+
 def _fresh(target, digest):
     stamp = target + ".sha"
     if not (os.path.exists(target) and os.path.exists(stamp)):
@@ -96,6 +108,8 @@ def build(force=False, verbose=True, stamps=False, jobs=None):
             print(" ".join(link), flush=True)
         subprocess.check_call(link)
         _stamp(lib, ldg)
+    with open(lib + ".src", "w") as f:
+        f.write(source_digest() + "\n")
     if not stamps:
         build_shim(force=force, verbose=verbose)
     return lib

@@ -394,12 +394,21 @@ static int live_chains(int device) {
   auto it = g_live_chains.find(device);
   return it == g_live_chains.end() ? 0 : it->second;
 }
+int live_chains_on(int device) { return live_chains(device); }
 
 static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device, uint32_t mask, int rank,
                         int nranks, const void* comm_id, hmsc_allreduce_fn host_fn = nullptr,
                         void* host_ctx = nullptr) {
   std::lock_guard<std::recursive_mutex> dev_lock(g_dev_mu);
-  ++g_live_chains[device];
+  // the device first: free_state decrements the count of s.device, whichever check below throws
+  s.device = device;
+  if (++g_live_chains[device] == 2) {
+    // edge-free graphs (device-side joins) are only safe with one chain on a device: replays
+    // launch under g_dev_mu after rechecking the count (replay_sweeps), and the ones already
+    // queued by the chain that was alone drain here before this chain can launch anything
+    DeviceGuard dg0(device);
+    HIP_OK(hipDeviceSynchronize());
+  }
   s.counted_live = true;
   HMSC_REQUIRE(m != nullptr, "model is NULL");
   HMSC_REQUIRE(m->struct_size == (int32_t)sizeof(hmsc_model),
@@ -1432,7 +1441,9 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
   }
   s.capturing = false;
   s.cap_segs = nullptr;
-  s.graph_edge_free = s.edge_free_now;
+  // (also a graph captured while the chain was alone on its device: its fused launch may have
+  // taken the resident-slot layout that two overlapping launches cannot share, kernels.hip)
+  s.graph_edge_free = s.edge_free_now || live_chains(s.device) == 1;
   s.edge_free_now = false;
   HIP_OK(hipStreamEndCapture(s.stream, &g));
   const bool steady = xv == s.xeta_valid && zv == s.zt_valid && gv == s.g2prep_valid && gp == s.g_pending &&
@@ -1570,6 +1581,17 @@ static bool replay_sweeps(State& s, uint32_t iter, bool with_record, int n) {
   }
   hipGraphExec_t ge = s.gx[with_record ? 1 : 0][graph_level(n)];
   if (!ge) return false;
+  // the live-chain recheck and the launch under one lock: a chain created since the check above
+  // would run next to an edge-free graph's device-side joins (build_state drains the device
+  // when a device's count reaches 2, so the replays queued before that have finished)
+  std::unique_lock<std::recursive_mutex> dev_lock(g_dev_mu);
+  if (s.graph_edge_free && live_chains(s.device) > 1) {
+    dev_lock.unlock();
+    destroy_graph(s);  // this sweep runs eagerly; the graphs are recaptured with edges after it
+    s.graph_dirty = false;
+    s.eager_streak = 0;
+    return false;
+  }
   join_side(s);
   set_iters_kernel<<<1, 64, 0, s.stream>>>(s.d_iters, iter, n);
   if (const auto& ext = s.ext_side[with_record ? 1 : 0][graph_level(n)]) {
@@ -2346,6 +2368,11 @@ int hmsc_debug_get(hmsc_state* h, const char* name, double* out, int64_t n) {
                            (double)(segs ? !s.gseg[1].empty() : s.gx[1][top] != nullptr), (double)s.graph_sweeps,
                            (double)s.eager_streak};
       std::memcpy(out, d, sizeof(d));
+      return;
+    } else if (nm == "g2bl") {  // the last fused Gamma2 + BetaLambda launch: [partials trailing, grid size]
+      HMSC_REQUIRE(n >= 2, "g2bl needs 2 slots");
+      out[0] = (double)s.g2bl_last_tail;
+      out[1] = (double)s.g2bl_last_nb;
       return;
     } else if (nm == "dims") {
       HMSC_REQUIRE(n >= 8, "dims needs 8 slots");

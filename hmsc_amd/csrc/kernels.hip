@@ -22,6 +22,8 @@
 #include <algorithm>
 #include <cstdlib>
 #include <vector>
+#include <map>
+#include <mutex>
 
 #include "common.h"
 #include "rng.h"
@@ -2178,6 +2180,30 @@ static BLTailArgs make_tail_args(State& s, bool tail_gv, bool sh) {
   }
   return t;
 }
+// workgroup slots the side stream may hold while the fused launch runs (side chain, record pack)
+constexpr int G2BL_SLOT_MARGIN = 64;
+
+// workgroups of the fused Gamma2 + BetaLambda launch resident on the whole device at once
+static int g2bl_resident_slots(const State& s, size_t smem) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, int> cache;  // (device, K bucket) -> slots
+  const int kb = wv_bucket(s.K);
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find({s.device, kb});
+  if (it != cache.end()) return it->second;
+  int nb = 0, ncu = 0;
+  switch (kb) {
+    case 8: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gamma2_bl_kernel<8>, 256, smem)); break;
+    case 16: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gamma2_bl_kernel<16>, 256, smem)); break;
+    case 24: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gamma2_bl_kernel<24>, 256, smem)); break;
+    default: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gamma2_bl_kernel<32>, 256, smem)); break;
+  }
+  HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, s.device));
+  const int slots = std::max(0, nb) * std::max(0, ncu);
+  cache[{s.device, kb}] = slots;
+  return slots;
+}
+
 void launch_gamma2_bl(State& s, uint32_t iter) {
   if (!s.xeta_valid) launch_xeta(s);
   flush_g(s);
@@ -2268,10 +2294,20 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
   // the partials on workgroups of their own after the BetaLambda ones (the launch's 52 KB of
   // LDS and <= 256 VGPRs keep two workgroups per CU resident); HMSC_G2_PART_INLINE: ahead of
   // the first BetaLambda bodies instead
-  f.part_tail = getenv_flag("HMSC_G2_PART_INLINE") ? 0 : 1;
+  // Trailing partial workgroups are waited on by workgroup 0, which every BetaLambda
+  // workgroup waits on: they must all be resident at once, so the trailing layout is taken
+  // only when the whole grid fits the device's resident slots with room to spare for the side
+  // stream's kernels, and only with one chain on the device (two overlapping fused launches
+  // share the slots).  Otherwise the partials run ahead of the first BetaLambda bodies, whose
+  // workgroups are dispatched before any workgroup that waits.
+  const size_t smem = BLW_LDS * sizeof(double);
+  const int nb_tail = 1 + (s.nsl + 3) / 4 + f.part_wg;
+  f.part_tail = !getenv_flag("HMSC_G2_PART_INLINE") && live_chains_on(s.device) == 1 &&
+                nb_tail + G2BL_SLOT_MARGIN <= g2bl_resident_slots(s, smem);
   const int nb = 1 + (s.nsl + 3) / 4 + (f.part_tail ? f.part_wg : 0);
   HMSC_REQUIRE(f.part_tail || f.part_wg <= nb - 1, "fused Gamma2 + BetaLambda: more Gamma2 partials than BetaLambda workgroups");
-  const size_t smem = BLW_LDS * sizeof(double);
+  s.g2bl_last_tail = f.part_tail;
+  s.g2bl_last_nb = nb;
   ProfScope ps(s, PROF_BL);
   switch (wv_bucket(s.K)) {
     case 8: gamma2_bl_kernel<8><<<nb, 256, smem, s.stream>>>(f); break;

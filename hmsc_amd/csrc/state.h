@@ -128,6 +128,7 @@ struct State {
   // graph edges, and graphs captured edge-free are rebuilt once a second chain appears.
   bool edge_free_now = false, graph_edge_free = false;
   bool counted_live = false;  // counted in capi.cpp's live chains of its device
+  int g2bl_last_tail = -1, g2bl_last_nb = 0;  // the last fused Gamma2 + BetaLambda launch's layout (debug_get "g2bl")
   bool side_gated = false;  // the last slab launch waited for the side chain's flags (SideGate)
   bool side_tail = false;   // the last side chain raises side_sync (the next fused launch may join it on the device)
   // the capture in progress forked the side stream at the graph's root, so its first sweep's
@@ -398,6 +399,7 @@ void launch_gamma_v(State& s, uint32_t iter, hipStream_t st);
 void launch_gamma2(State& s, uint32_t iter);
 bool gamma2_bl_fusion_ok(const State& s);
 void launch_gamma2_bl(State& s, uint32_t iter);  // updateGamma2 + updateBetaLambda in one launch
+int live_chains_on(int device);                  // chains created and not destroyed on a device (capi.cpp)
 void launch_lambda_priors(State& s, uint32_t iter, hipStream_t st);
 void launch_eta(State& s, uint32_t iter);
 void launch_inv_sigma(State& s, uint32_t iter);

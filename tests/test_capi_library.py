@@ -56,3 +56,18 @@ def test_struct_layouts_match_header():
             fields.extend(names)
         ct = [f[0] for f in getattr(_lib, struct)._fields_]
         assert ct == fields, (struct, ct, fields)
+
+
+def test_stale_library_is_refused(monkeypatch):
+    """A library whose source stamp does not match the sources beside it is refused with a clear
+    error instead of running silently (build.py writes libhmsc_amd.so.src at link time)."""
+    import pytest
+    from hmsc_amd import _lib, build
+    build.build(verbose=False)
+    monkeypatch.delenv("HMSC_AMD_LIB", raising=False)
+    monkeypatch.delenv("HMSC_AMD_ALLOW_STALE", raising=False)
+    _lib._check_fresh()  # the freshly built library passes
+    monkeypatch.setattr(build, "source_digest", lambda: "0" * 64)
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(_lib.HmscNativeError, match="stale"):
+        _lib.lib()
