@@ -335,7 +335,17 @@ class Hmsc(_RList):
         if C is not None and phyloTree is not None:
             raise ValueError("Hmsc.setData: at maximum one of phyloTree and C arguments can be specified")
         if phyloTree is not None:
-            raise NotImplementedError("phyloTree needs ape::vcv.phylo; pass the correlation matrix C instead")
+            # corM = vcv.phylo(phyloTree, model="Brownian", corr=TRUE)[spNames, spNames] (:504-508)
+            from .phylo import read_tree, vcv_phylo
+            tree = read_tree(phyloTree) if isinstance(phyloTree, str) else phyloTree
+            corM, tips = vcv_phylo(tree, corr=True)
+            where = {t: k for k, t in enumerate(tips)}
+            missing = [s for s in self.spNames if s not in where]
+            if missing:
+                raise ValueError(f"Hmsc.setData: species {missing[:5]} are not tips of phyloTree")
+            ix = np.array([where[s] for s in self.spNames])
+            self.phyloTree = tree
+            C = corM[np.ix_(ix, ix)]
         if C is not None:
             C = np.asarray(C, dtype=np.float64)
             if C.shape != (ns, ns):

@@ -54,6 +54,10 @@ def main():
     out["aSigma"] = arr(m["aSigma"])
     out["bSigma"] = arr(m["bSigma"])
     out["rhopw"] = arr(m["rhopw"])
+    # TD$m was built with phyloTree = TD$phy (R/Hmsc.R:504-509 makes TD$m$C from it)
+    phy = m["phyloTree"]
+    out["phy_edge"] = arr(phy["edge"]).astype(np.int64)
+    out["phy_edge_length"] = arr(phy["edge.length"])
     out["xycoords"] = arr(TD["xycoords"])
     out["x1"] = arr(TD["X"]["x1"])
     rl = m["rL"]
@@ -103,6 +107,7 @@ def main():
         "samples": int(m["samples"].value[0]), "transient": int(m["transient"].value[0]),
         "thin": int(m["thin"].value[0]),
         "rL": rl_meta,
+        "phy_tip_label": list(phy["tip.label"].value), "phy_Nnode": int(phy["Nnode"].value[0]),
         # known answers from the reference's own tests
         "known": {
             "sum_detQg_round": -68, "sum_Qg_round": 575, "sum_iQg_round": 293, "sum_RQg_round": 461,
