@@ -2125,12 +2125,39 @@ void launch_gamma2(State& s, uint32_t iter) {
   HIP_OK(hipGetLastError());
 }
 
+// workgroup slots the side stream may hold while the fused launch runs (side chain, record pack)
+constexpr int G2BL_SLOT_MARGIN = 64;
+
+// workgroups of the fused Gamma2 + BetaLambda launch resident on the whole device at once
+static int g2bl_resident_slots(const State& s, size_t smem) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, int> cache;  // (device, K bucket) -> slots
+  const int kb = wv_bucket(s.K);
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find({s.device, kb});
+  if (it != cache.end()) return it->second;
+  int nb = 0, ncu = 0;
+  switch (kb) {
+    case 8: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gamma2_bl_kernel<8>, 256, smem)); break;
+    case 16: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gamma2_bl_kernel<16>, 256, smem)); break;
+    case 24: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gamma2_bl_kernel<24>, 256, smem)); break;
+    default: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gamma2_bl_kernel<32>, 256, smem)); break;
+  }
+  HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, s.device));
+  const int slots = std::max(0, nb) * std::max(0, ncu);
+  cache[{s.device, kb}] = slots;
+  return slots;
+}
+
 bool gamma2_bl_fusion_ok(const State& s) {
   const uint32_t need = HMSC_UP_GAMMA2 | HMSC_UP_BETALAMBDA;
   const size_t N = (size_t)s.nc * s.nt;
   return (s.mask & need) == need && !(s.mask & HMSC_UP_GAMMAETA) && !s.sharded && !s.has_na && !s.phylo &&
          s.K <= 32 && s.nt <= 8 && N <= 256 && s.NF <= 64 && s.NF * s.nt + N <= 64 && s.gbl_sync != nullptr &&
-         (G2F_LDS + (size_t)s.nc * s.nc + N * N) <= (size_t)BLW_LDS && !getenv_flag("HMSC_NO_G2BL_FUSION");
+         (G2F_LDS + (size_t)s.nc * s.nc + N * N) <= (size_t)BLW_LDS && !getenv_flag("HMSC_NO_G2BL_FUSION") &&
+         // workgroup 0 waits for the partials' workgroups, so they (dispatched first when not
+         // trailing) and workgroup 0 must be resident together, beside the side stream's kernels
+         1 + (s.nsl + G2SB - 1) / G2SB + G2BL_SLOT_MARGIN <= g2bl_resident_slots(s, BLW_LDS * sizeof(double));
 }
 
 // updateGamma2 then updateBetaLambda as one launch (gamma2_bl_kernel)
@@ -2180,30 +2207,6 @@ static BLTailArgs make_tail_args(State& s, bool tail_gv, bool sh) {
   }
   return t;
 }
-// workgroup slots the side stream may hold while the fused launch runs (side chain, record pack)
-constexpr int G2BL_SLOT_MARGIN = 64;
-
-// workgroups of the fused Gamma2 + BetaLambda launch resident on the whole device at once
-static int g2bl_resident_slots(const State& s, size_t smem) {
-  static std::mutex mu;
-  static std::map<std::pair<int, int>, int> cache;  // (device, K bucket) -> slots
-  const int kb = wv_bucket(s.K);
-  std::lock_guard<std::mutex> lk(mu);
-  auto it = cache.find({s.device, kb});
-  if (it != cache.end()) return it->second;
-  int nb = 0, ncu = 0;
-  switch (kb) {
-    case 8: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gamma2_bl_kernel<8>, 256, smem)); break;
-    case 16: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gamma2_bl_kernel<16>, 256, smem)); break;
-    case 24: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gamma2_bl_kernel<24>, 256, smem)); break;
-    default: HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gamma2_bl_kernel<32>, 256, smem)); break;
-  }
-  HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, s.device));
-  const int slots = std::max(0, nb) * std::max(0, ncu);
-  cache[{s.device, kb}] = slots;
-  return slots;
-}
-
 void launch_gamma2_bl(State& s, uint32_t iter) {
   if (!s.xeta_valid) launch_xeta(s);
   flush_g(s);

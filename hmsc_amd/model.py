@@ -89,6 +89,8 @@ class HmscRandomLevel(_RList):
             self["sKnot"] = sKnot
         if distMat is not None:
             self.distMat = np.asarray(distMat, dtype=np.float64)
+            # rownames(distMat): R indexes rL$distMat by unit name (predictLatentFactor)
+            self["distNames"] = [str(i) for i in distMat.index] if hasattr(distMat, "index") else None
             self.N = self.distMat.shape[0]
             self.spatialMethod = sMethod
             self.sDim = math.inf

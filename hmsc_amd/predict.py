@@ -36,6 +36,23 @@ def _coords(rL, names, units):
     return s[[pos[str(n)] for n in names]]
 
 
+def _dist_rows(rL, names, units):
+    """Row / column indices of rL$distMat for the given unit names (R indexes it by
+    rownames, R/predictLatentFactor.R:69-70,100)."""
+    dn = rL["distNames"] if "distNames" in rL.names() else None
+    if dn is None:            # unnamed: row k is the k-th level of the fitted units
+        pos = {u: k for k, u in enumerate(units)}
+        if any(n not in pos for n in names) or rL.distMat.shape[0] != len(units):
+            raise ValueError("predictLatentFactor: distances to new spatial units are needed: give distMat "
+                             "as a DataFrame whose index names every unit (rownames of rL$distMat)")
+    else:
+        pos = {str(u): k for k, u in enumerate(dn)}
+        missing = [n for n in names if str(n) not in pos]
+        if missing:
+            raise ValueError(f"predictLatentFactor: units {missing[:5]} are not rows of rL$distMat")
+    return np.array([pos[str(n)] for n in names], dtype=np.int64)
+
+
 def _pdist(a, b):
     return np.sqrt(((a[:, None, :] - b[None, :, :]) ** 2).sum(-1))
 
@@ -62,10 +79,18 @@ def predictLatentFactor(unitsPred, units, postEta, rL, predictMean=False, rng=No
     if spatial:
         if postAlpha is None:
             raise ValueError("predictLatentFactor: postAlpha is needed for new units of a spatial level")
+        newu = [u for u, o in zip(unitsPred, old) if not o]
         if rL.distMat is not None:
-            raise NotImplementedError("predictLatentFactor: spatial levels given by distMat")
-        s1 = _coords(rL, units, units)
-        s2 = _coords(rL, [u for u, o in zip(unitsPred, old) if not o], units)
+            # a level given by distances (R/predictLatentFactor.R:69-70,100): D from rL$distMat;
+            # 'NNGP' and 'GPP' need coordinates in R too (rL$s, :120,163)
+            if not (predictMean or predictMeanField) and rL.spatialMethod != "Full":
+                raise ValueError(f"predictLatentFactor: spatialMethod '{rL.spatialMethod}' needs coordinates "
+                                 f"(sData); a distMat level predicts with 'Full'")
+            s1 = _dist_rows(rL, units, units)
+            s2 = _dist_rows(rL, newu, units)
+        else:
+            s1 = _coords(rL, units, units)
+            s2 = _coords(rL, newu, units)
         alphapw = np.asarray(rL.alphapw, dtype=np.float64)
     out = []
     for k, eta in enumerate(postEta):
@@ -84,8 +109,14 @@ def predictLatentFactor(unitsPred, units, postEta, rL, predictMean=False, rng=No
 def _krige(rL, eta, alpha, alphapw, s1, s2, predictMean, predictMeanField, rng):
     npo, nf, nn = s1.shape[0], eta.shape[1], s2.shape[0]
     res = np.empty((nn, nf))
+    dm = rL.distMat
     if predictMean or predictMeanField:                                       # :62-92
-        D11, D12 = _pdist(s1, s1), _pdist(s1, s2)
+        # (with distMat R's :69-70 index rL$distMat by s1 / s2, which that branch never sets --
+        # an error in R; the fitted and new units' rows are what it evidently means)
+        if dm is not None:
+            D11, D12 = dm[np.ix_(s1, s1)], dm[np.ix_(s1, s2)]
+        else:
+            D11, D12 = _pdist(s1, s1), _pdist(s1, s2)
         for h in range(nf):
             a = alphapw[alpha[h] - 1, 0]
             if a > 0:
@@ -101,7 +132,11 @@ def _krige(rL, eta, alpha, alphapw, s1, s2, predictMean, predictMeanField, rng):
         return res
     method = rL.spatialMethod
     if method == "Full":                                                      # :95-117
-        D = _pdist(np.vstack([s1, s2]), np.vstack([s1, s2]))
+        if dm is not None:
+            ua = np.concatenate([s1, s2])
+            D = dm[np.ix_(ua, ua)]
+        else:
+            D = _pdist(np.vstack([s1, s2]), np.vstack([s1, s2]))
         for h in range(nf):
             a = alphapw[alpha[h] - 1, 0]
             if a > 0:

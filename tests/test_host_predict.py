@@ -96,3 +96,33 @@ def test_predict_latent_factor_spatial(method):
     assert np.allclose(mf[[0, 2, 3]], eta[:3], atol=1e-2)
     with pytest.raises(ValueError):
         predictLatentFactor(unitsPred, names, [eta], rl, predictMean=True, predictMeanField=True, postAlpha=[alpha])
+
+
+def test_predict_latent_factor_distmat_equals_coordinates():
+    """A spatial level given by distances (R/predictLatentFactor.R:69-70,100): rL$distMat rows by
+    unit name replace dist(rL$s); with the distances of the same coordinates the kriged Eta of
+    new units is the sData level's draw for draw ('Full', predictMean, predictMeanField)."""
+    import pandas as pd
+    rng = np.random.default_rng(4)
+    xy = rng.random((25, 2))
+    names = [f"p{k:02d}" for k in range(25)]
+    xy_all = np.vstack([xy, xy[:2] + 0.03])
+    all_names = names + ["n0", "n1"]
+    D = np.sqrt(((xy_all[:, None, :] - xy_all[None, :, :]) ** 2).sum(-1))
+    rl_s = _spatial_rl("Full", pd.DataFrame(xy_all, index=all_names))
+    order = np.random.default_rng(5).permutation(len(all_names))   # distMat rows in another order
+    dm = pd.DataFrame(D[np.ix_(order, order)], index=[all_names[k] for k in order])
+    rl_d = H.HmscRandomLevel(distMat=dm)
+    H.setPriors(rl_d, nfMin=2, nfMax=2)
+    H.setPriors(rl_d, alphapw=rl_s.alphapw)
+    eta = np.column_stack([np.sin(3 * xy[:, 0]), xy[:, 1]])
+    alpha = np.array([30, 50])
+    up = ["n0", "p03", "n1"]
+    for kw in (dict(predictMean=True), dict(predictMeanField=True), {}):
+        a = predictLatentFactor(up, names, [eta], rl_s, postAlpha=[alpha], rng=np.random.default_rng(6), **kw)[0]
+        b = predictLatentFactor(up, names, [eta], rl_d, postAlpha=[alpha], rng=np.random.default_rng(6), **kw)[0]
+        np.testing.assert_allclose(b, a, rtol=1e-12, atol=1e-12)
+    rl_n = H.HmscRandomLevel(distMat=dm, sMethod="NNGP")
+    H.setPriors(rl_n, nfMin=2, nfMax=2)
+    with pytest.raises(ValueError, match="needs coordinates"):
+        predictLatentFactor(up, names, [eta], rl_n, postAlpha=[alpha])
