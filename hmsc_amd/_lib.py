@@ -34,7 +34,8 @@ class hmsc_model(C.Structure):
                 ("RiWg", dp * MAX_LEVELS), ("detWg", dp * MAX_LEVELS),
                 ("sCoord", dp * MAX_LEVELS), ("distMat", dp * MAX_LEVELS),
                 ("nKnots", ip), ("idDg", dp * MAX_LEVELS), ("idDW12g", dp * MAX_LEVELS), ("Fg", dp * MAX_LEVELS),
-                ("iFg", dp * MAX_LEVELS), ("detDg", dp * MAX_LEVELS), ("nNeighbours", ip)]
+                ("iFg", dp * MAX_LEVELS), ("detDg", dp * MAX_LEVELS), ("nNeighbours", ip),
+                ("etaShare", ip), ("xScale", dp * MAX_LEVELS)]
 
     def __init__(self, *a, **kw):
         super().__init__(*a, **kw)

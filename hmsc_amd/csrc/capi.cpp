@@ -482,7 +482,30 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
                    "(R/updateGammaEta.R:153-158): pass updater GammaEta=FALSE");
     }
     HMSC_REQUIRE(m->xDim == nullptr || m->xDim[r] == 0,
-                 "covariate-dependent random levels are a 'next' row: not in this build");
+                 "a covariate-dependent level is passed as xDim consecutive levels sharing Eta "
+                 "(hmsc_model etaShare / xScale), with xDim = 0 for each");
+    {  // covariate-dependent level groups (etaShare / xScale, include/hmsc_amd.h)
+      const int owner = (m->etaShare && m->etaShare[r] >= 0) ? m->etaShare[r] : r;
+      HMSC_REQUIRE(owner <= r, "etaShare[r] must name r itself or an earlier level");
+      if (owner < r) {
+        HMSC_REQUIRE(s.lev[owner].eta_owner < 0 && owner + s.lev[owner].xgroup == r,
+                     "etaShare: the levels sharing one Eta must be consecutive, after the level named");
+        HMSC_REQUIRE(m->np[r] == m->np[owner] && m->nfMin[r] == m->nfMin[owner] && m->nfMax[r] == m->nfMax[owner],
+                     "etaShare: levels sharing Eta need the same units and nfMin / nfMax");
+        for (int i = 0; i < ny; ++i)
+          HMSC_REQUIRE(m->Pi[i + (size_t)ny * r] == m->Pi[i + (size_t)ny * owner], "etaShare: levels sharing Eta need the same Pi");
+        L.eta_owner = owner;
+        s.lev[owner].xgroup++;
+      }
+      if (m->xScale[r] || owner < r) {
+        HMSC_REQUIRE(m->xScale[r] != nullptr, "etaShare: every level of a shared-Eta group needs its xScale column");
+        s.any_xs = true;
+      }
+    }
+    HMSC_REQUIRE(!((m->xScale[r] != nullptr) && (L.spatial || s.sharded || (mask & HMSC_UP_GAMMAETA))),
+                 "covariate-dependent levels: not with spatial levels, species sharding or updateGammaEta "
+                 "(R/updateGammaEta.R and the spatial branches of R/updateEta.R take Lambda as a matrix): "
+                 "pass updater GammaEta=FALSE");
     HMSC_REQUIRE(!(s.sharded && L.spatial), "spatial levels couple the units of every species' factors densely: "
                                             "species-sharded chains are not supported (run one chain per GPU)");
     L.np = m->np[r];
@@ -518,7 +541,8 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
     L.nfcap = std::max(L.nfmin, std::min(L.nfmax, s.NFmax - others));
     L.nf_alloc = std::max(1, L.nf);
     const int nfcap = L.nfcap;
-    L.Eta = dalloc<double>((size_t)L.np * nfcap);
+    L.Eta = L.eta_alias() ? s.lev[L.eta_owner].Eta : dalloc<double>((size_t)L.np * nfcap);
+    if (m->xScale[r]) L.xs = dupload(m->xScale[r], (size_t)L.np);
     std::vector<int> pi(ny), cnt(L.np + 1, 0), rows(ny);
     for (int i = 0; i < ny; ++i) {
       const int u = m->Pi[i + (size_t)ny * r] - 1;
@@ -882,7 +906,7 @@ static void free_state(State& s) {
     if (p) (void)hipFree(p);
   for (int r = 0; r < s.nr; ++r) {
     Level& L = s.lev[r];
-    void* lp[] = {L.Eta, L.Pi, L.unit_ptr, L.unit_rows, L.Alpha, L.AlphaD, L.alphapw, L.iWg, L.RiWg, L.detWg, L.spWork,
+    void* lp[] = {L.eta_alias() ? nullptr : L.Eta, L.xs, L.Pi, L.unit_ptr, L.unit_rows, L.Alpha, L.AlphaD, L.alphapw, L.iWg, L.RiWg, L.detWg, L.spWork,
                   L.idDg, L.idDW12g, L.Fg, L.iFg, L.nnIdx, L.nnA, L.nnD, L.nnPerm, L.nnPos, L.nnChPtr, L.nnCh};
     for (void* p : lp)
       if (p) (void)hipFree(p);
@@ -1101,21 +1125,30 @@ static void set_state(State& s, const hmsc_params* p) {
 
 // ---------------------------- updateNf (host decision) ----------------------------
 // R/updateNf.R:3-70: with probability exp(-(1 + 0.0005 iter)) add a factor (if none is
-// redundant) or drop (reference quirk: setdiff(1:nf, logical) drops factor 1).
+// redundant) or drop (reference quirk: setdiff(1:nf, logical) drops factor 1).  A
+// covariate-dependent level's group (Level::xgroup levels from r sharing Eta, Lambda[,,k] in
+// level r + k) adapts together: the redundancy counts run over every k (rowMeans of the nf x ns
+// x ncr array), a new factor adds a row to every Lambda[,,k] / Psi[,,k] / Delta[,k] (:41-47)
+// and one Eta column, a dropped factor leaves all of them (:62-66).
 static void update_nf(State& s, int r, uint32_t iter) {
   Level& L = s.lev[r];
+  if (L.eta_alias()) return;  // (adapted with its group's first level)
+  const int m = L.xgroup;
   const uint32_t st = LEVEL_STRIDE * r;
   const double u = uniforms(s.key, 0, 0, S_NF + st, iter).a;
   const double prob = 1.0 / std::exp(1.0 + 0.0005 * iter);
   if (!(u < prob)) return;
   HIP_OK(hipStreamSynchronize(s.stream));
-  const int K = s.K, nsl = s.nsl, nf = L.nf, lo = s.loff(r), fo = s.foff(r);
+  const int K = s.K, NF = s.NF, nsl = s.nsl, nf = L.nf;
+  std::vector<int> lo0(s.nr), fo0(s.nr);
+  for (int q = 0; q < s.nr; ++q) lo0[q] = s.loff(q), fo0[q] = s.foff(q);
   std::vector<double> BL((size_t)K * nsl);
   d2h(BL.data(), s.BL, BL.size(), s.stream);
   HIP_OK(hipStreamSynchronize(s.stream));
   std::vector<double> small(nf, 0.0);
-  for (int j = 0; j < nsl; ++j)
-    for (int h = 0; h < nf; ++h) small[h] += std::fabs(BL[lo + h + (size_t)K * j]) < 1e-3 ? 1.0 : 0.0;
+  for (int k = 0; k < m; ++k)
+    for (int j = 0; j < nsl; ++j)
+      for (int h = 0; h < nf; ++h) small[h] += std::fabs(BL[lo0[r + k] + h + (size_t)K * j]) < 1e-3 ? 1.0 : 0.0;
   if (s.sharded) {  // the counts over every rank's species (an adaptation sweep's extra all-reduce)
     h2d(s.allreduce_buf, small.data(), nf, s.stream);
     ar_point(s, s.allreduce_buf, nf);
@@ -1125,92 +1158,71 @@ static void update_nf(State& s, int r, uint32_t iter) {
   int num_red = 0;
   bool all_lt = true;
   for (int h = 0; h < nf; ++h) {
-    const double prop = small[h] / s.ns;
+    const double prop = small[h] / ((double)s.ns * m);
     if (prop >= 1.0) ++num_red;
     if (!(prop < 0.995)) all_lt = false;
   }
-  const int nfcap = L.nfcap;
-  std::vector<double> Psi((size_t)s.NF * nsl), Delta(s.NF), Eta((size_t)L.np * nf);
-  d2h(Psi.data(), s.Psi, Psi.size(), s.stream);
-  d2h(Delta.data(), s.Delta, s.NF, s.stream);
-  d2h(Eta.data(), L.Eta, Eta.size(), s.stream);
-  HIP_OK(hipStreamSynchronize(s.stream));
+  int grow = 0;  // +1 add a factor, -1 drop factor 1
   if (nf < L.nfmax && iter > 20 && num_red == 0 && all_lt) {
-    if (nf + 1 > nfcap || s.K + 1 > s.Kmax)
+    if (nf + 1 > L.nfcap || s.K + m > s.Kmax)
       throw HmscError(-6, "updateNf: level " + std::to_string(r + 1) + " needs " + std::to_string(nf + 1) +
                               " latent factors at iteration " + std::to_string(iter) + ", but this build holds at most " +
-                              std::to_string(nfcap) + " for it (K = nc + sum(nf) <= 128); set nfMax <= " +
-                              std::to_string(nfcap) + " with setPriors (or fewer covariates) to run this model");
-    const int K2 = K + 1, NF2 = s.NF + 1;
-    std::vector<double> BL2((size_t)K2 * nsl), Psi2((size_t)NF2 * nsl), Delta2(NF2);
-    for (int j = 0; j < nsl; ++j) {
-      for (int k = 0, k2 = 0; k2 < K2; ++k2) {
-        if (k2 == lo + nf) {
-          BL2[k2 + (size_t)K2 * j] = 0.0;  // lambdaNew = rbind(lambda, 0)  (:33)
-        } else {
-          BL2[k2 + (size_t)K2 * j] = BL[k + (size_t)K * j];
-          ++k;
-        }
-      }
-      for (int f = 0, f2 = 0; f2 < NF2; ++f2) {
-        if (f2 == fo + nf) {
-          Psi2[f2 + (size_t)NF2 * j] =
-              gamma_std(s.key, (uint32_t)(s.sp0 + j), S_NF_PSI + st, iter, L.nu / 2) / (L.nu / 2);  // (:36)
-        } else {
-          Psi2[f2 + (size_t)NF2 * j] = Psi[f + (size_t)s.NF * j];
-          ++f;
-        }
-      }
-    }
-    for (int f = 0, f2 = 0; f2 < NF2; ++f2) {
-      if (f2 == fo + nf)
-        Delta2[f2] = gamma_std(s.key, 0, S_NF_DELTA + st, iter, L.a2) / L.b2;  // (:39)
-      else
-        Delta2[f2] = Delta[f++];
-    }
-    std::vector<double> col(L.np);
-    for (int q = 0; q < L.np; ++q) col[q] = normal(s.key, (uint32_t)q, 0, S_NF_ETA + st, iter);  // (:30)
-    h2d(s.BL, BL2.data(), BL2.size(), s.stream);
-    h2d(s.Psi, Psi2.data(), Psi2.size(), s.stream);
-    h2d(s.Delta, Delta2.data(), NF2, s.stream);
-    h2d(L.Eta + (size_t)L.np * nf, col.data(), L.np, s.stream);
-    const double one = 1.0;  // alphaNew = c(alpha, 1)  (:31)
-    h2d(L.AlphaD + nf, &one, 1, s.stream);
-    HIP_OK(hipStreamSynchronize(s.stream));
-    L.nf = nf + 1;
+                              std::to_string(L.nfcap) + " for it (K = nc + sum(nf) <= 128); set nfMax <= " +
+                              std::to_string(L.nfcap) + " with setPriors (or fewer covariates) to run this model");
+    grow = 1;
   } else if (num_red > 0 && nf > L.nfmin) {
-    // indNotRed = setdiff(1:nf, indRedundant): drops factor 1 (index 0)   (:56)
-    const int drop = 0;
-    const int K2 = K - 1, NF2 = s.NF - 1;
-    std::vector<double> BL2((size_t)K2 * nsl), Psi2((size_t)std::max(1, NF2) * nsl), Delta2(std::max(1, NF2));
-    for (int j = 0; j < nsl; ++j) {
-      for (int k = 0, k2 = 0; k < K; ++k)
-        if (k != lo + drop) BL2[k2++ + (size_t)K2 * j] = BL[k + (size_t)K * j];
-      for (int f = 0, f2 = 0; f < s.NF; ++f)
-        if (f != fo + drop) Psi2[f2++ + (size_t)NF2 * j] = Psi[f + (size_t)s.NF * j];
-    }
-    for (int f = 0, f2 = 0; f < s.NF; ++f)
-      if (f != fo + drop) Delta2[f2++] = Delta[f];
-    std::vector<double> Eta2((size_t)L.np * (nf - 1));
-    for (int h = 0, h2 = 0; h < nf; ++h)
-      if (h != drop) {
-        std::memcpy(&Eta2[(size_t)L.np * h2], &Eta[(size_t)L.np * h], L.np * sizeof(double));
-        ++h2;
-      }
-    h2d(s.BL, BL2.data(), BL2.size(), s.stream);
-    h2d(s.Psi, Psi2.data(), (size_t)NF2 * nsl, s.stream);
-    h2d(s.Delta, Delta2.data(), NF2, s.stream);
-    h2d(L.Eta, Eta2.data(), Eta2.size(), s.stream);
-    std::vector<double> ad(nf);  // alpha = alpha[indNotRed]  (:59)
-    d2h(ad.data(), L.AlphaD, nf, s.stream);
-    HIP_OK(hipStreamSynchronize(s.stream));
-    if (nf > 1) h2d(L.AlphaD, ad.data() + 1, nf - 1, s.stream);
-    HIP_OK(hipStreamSynchronize(s.stream));
-    L.nf = nf - 1;
+    grow = -1;
   } else {
     return;
   }
+  std::vector<double> Psi((size_t)NF * nsl), Delta(std::max(1, NF)), Eta((size_t)L.np * nf);
+  d2h(Psi.data(), s.Psi, Psi.size(), s.stream);
+  d2h(Delta.data(), s.Delta, NF, s.stream);
+  d2h(Eta.data(), L.Eta, Eta.size(), s.stream);
+  HIP_OK(hipStreamSynchronize(s.stream));
+  for (int k = 0; k < m; ++k) s.lev[r + k].nf = nf + grow;
   s.refresh_dims();
+  const int K2 = s.K, NF2 = s.NF;
+  std::vector<double> BL2((size_t)K2 * nsl), Psi2((size_t)std::max(1, NF2) * nsl), Delta2(std::max(1, NF2));
+  for (int j = 0; j < nsl; ++j)
+    for (int c = 0; c < s.nc; ++c) BL2[c + (size_t)K2 * j] = BL[c + (size_t)K * j];
+  for (int q = 0; q < s.nr; ++q) {
+    const bool in = q >= r && q < r + m;
+    const Level& Lq = s.lev[q];
+    const int lo2 = s.loff(q), fo2 = s.foff(q);
+    for (int h = 0; h < Lq.nf; ++h) {
+      // the old row of new row h: the same (other levels; kept factors), the next one (the
+      // dropped factor 1, :56), or none (the added factor)
+      const int ho = !in ? h : grow > 0 ? (h < nf ? h : -1) : h + 1;
+      for (int j = 0; j < nsl; ++j) {
+        BL2[lo2 + h + (size_t)K2 * j] = ho >= 0 ? BL[lo0[q] + ho + (size_t)K * j] : 0.0;  // rbind(lambda, 0) (:33)
+        Psi2[fo2 + h + (size_t)NF2 * j] =
+            ho >= 0 ? Psi[fo0[q] + ho + (size_t)NF * j]
+                    : gamma_std(s.key, (uint32_t)(s.sp0 + j), S_NF_PSI + LEVEL_STRIDE * q, iter, Lq.nu / 2) / (Lq.nu / 2);  // (:36,44)
+      }
+      Delta2[fo2 + h] = ho >= 0 ? Delta[fo0[q] + ho]
+                                : gamma_std(s.key, 0, S_NF_DELTA + LEVEL_STRIDE * q, iter, Lq.a2) / Lq.b2;  // (:39,47)
+    }
+  }
+  h2d(s.BL, BL2.data(), BL2.size(), s.stream);
+  h2d(s.Psi, Psi2.data(), (size_t)NF2 * nsl, s.stream);
+  h2d(s.Delta, Delta2.data(), NF2, s.stream);
+  if (grow > 0) {
+    std::vector<double> col(L.np);
+    for (int q = 0; q < L.np; ++q) col[q] = normal(s.key, (uint32_t)q, 0, S_NF_ETA + st, iter);  // (:30)
+    h2d(L.Eta + (size_t)L.np * nf, col.data(), L.np, s.stream);
+    const double one = 1.0;  // alphaNew = c(alpha, 1)  (:31)
+    for (int k = 0; k < m; ++k) h2d(s.lev[r + k].AlphaD + nf, &one, 1, s.stream);
+  } else {
+    h2d(L.Eta, Eta.data() + L.np, (size_t)L.np * (nf - 1), s.stream);  // eta[, indNotRed] (:57)
+    for (int k = 0; k < m; ++k) {  // alpha = alpha[indNotRed]  (:59)
+      std::vector<double> ad(nf);
+      d2h(ad.data(), s.lev[r + k].AlphaD, nf, s.stream);
+      HIP_OK(hipStreamSynchronize(s.stream));
+      if (nf > 1) h2d(s.lev[r + k].AlphaD, ad.data() + 1, nf - 1, s.stream);
+    }
+  }
+  HIP_OK(hipStreamSynchronize(s.stream));
   s.zt_valid = false;
   s.xz_parts = 0;
   s.xeta_valid = false;

@@ -60,13 +60,19 @@ struct EtaView {
   const int* Pi[HMSC_MAX_LEVELS];
   int np[HMSC_MAX_LEVELS];
   int nf[HMSC_MAX_LEVELS];
+  // covariate-dependent level r: its columns are Eta[Pi, h] * x[Pi, k] (R/updateBetaLambda.R:25-27)
+  const double* xs[HMSC_MAX_LEVELS];
 };
 
 __device__ __forceinline__ double xeta_at(const EtaView& v, int i, int k) {
   if (k < v.nc) return v.X[i + (size_t)v.ny * k];
   int h = k - v.nc;
   for (int r = 0; r < v.nr; ++r) {
-    if (h < v.nf[r]) return v.Eta[r][v.Pi[r][i] + (size_t)v.np[r] * h];
+    if (h < v.nf[r]) {
+      const int q = v.Pi[r][i];
+      const double e = v.Eta[r][q + (size_t)v.np[r] * h];
+      return v.xs[r] ? e * v.xs[r][q] : e;
+    }
     h -= v.nf[r];
   }
   return 0.0;
@@ -85,6 +91,7 @@ static EtaView make_view(const State& s) {
     v.Pi[r] = s.lev[r].Pi;
     v.np[r] = s.lev[r].np;
     v.nf[r] = s.lev[r].nf;
+    v.xs[r] = s.lev[r].xs;
   }
   return v;
 }
@@ -2152,7 +2159,7 @@ static int g2bl_resident_slots(const State& s, size_t smem) {
 bool gamma2_bl_fusion_ok(const State& s) {
   const uint32_t need = HMSC_UP_GAMMA2 | HMSC_UP_BETALAMBDA;
   const size_t N = (size_t)s.nc * s.nt;
-  return (s.mask & need) == need && !(s.mask & HMSC_UP_GAMMAETA) && !s.sharded && !s.has_na && !s.phylo &&
+  return (s.mask & need) == need && !(s.mask & HMSC_UP_GAMMAETA) && !s.sharded && !s.has_na && !s.phylo && !s.any_xs &&
          s.K <= 32 && s.nt <= 8 && N <= 256 && s.NF <= 64 && s.NF * s.nt + N <= 64 && s.gbl_sync != nullptr &&
          (G2F_LDS + (size_t)s.nc * s.nc + N * N) <= (size_t)BLW_LDS && !getenv_flag("HMSC_NO_G2BL_FUSION") &&
          // workgroup 0 waits for the partials' workgroups, so they (dispatched first when not
@@ -2908,6 +2915,115 @@ __global__ __launch_bounds__(64) void eta_na_row_kernel(EtaView ev, int r, int n
 }
 
 // ---------------------------------------------------------------------------
+// Covariate-dependent level (R/updateEta.R:93-108).  The m levels r0 .. r0+m-1 of a group share
+// Eta (np x nf, owned by r0); level r0+k scales its XEta columns by x[:, k] (EtaView::xs), so
+// its BL rows are R's Lambda[,,k].  Per unit q, with lambdaLocal = sum_k x_qk Lambda_k:
+//   Q_q = I + sum_{rows i of q} lambdaLocal diag(iSigma Yx_i) lambdaLocal^T
+//   b_q = sum_{rows i of q} S_i diag(iSigma Yx_i) lambdaLocal^T,   S = Z - XEta_(-group) BL
+//   eta_q = Q_q^-1 b_q + chol(Q_q)^-1 xi    (xi: normal(q, h, S_ETA + LEVEL_STRIDE r0))
+// A row with every cell observed adds the CR blocks (the group's K rows are loff0 + k nf + f,
+// its factor columns foff0 + k nf + f):
+//   Q += sum_{k,k'} x_qk x_qk' CR[loff0 + k nf + f1, foff0 + k' nf + f2]
+//   b += sum_k x_qk (ZL_i[foff0 + k nf + f] - sum_{c outside the group} XEta_ic CR[c, foff0 + k nf + f])
+// and an NA row its masked terms from eta_na_row_x_kernel.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void eta_na_row_x_kernel(EtaView ev, int r0, int m, int nf, int K, int loff0,
+                                                          const int* na_rows, const double* Z, const double* BL,
+                                                          const double* iSigma, const int8_t* Ycode, int ns_loc,
+                                                          double* Mrow, double* brow) {
+  const int slot = blockIdx.x, i = na_rows[slot], t = threadIdx.x, ny = ev.ny;
+  extern __shared__ __attribute__((aligned(16))) double sx[];  // XEta row (K), then x_q (m)
+  double* xq = sx + K;
+  const int q = ev.Pi[r0][i], gend = loff0 + m * nf;
+  for (int k = t; k < K; k += 64) sx[k] = xeta_at(ev, i, k);
+  for (int k = t; k < m; k += 64) xq[k] = ev.xs[r0 + k][q];
+  __syncthreads();
+  auto lam_local = [&](int h, int j) {
+    double v = 0.0;
+    for (int k = 0; k < m; ++k) v += xq[k] * BL[loff0 + k * nf + h + (size_t)K * j];
+    return v;
+  };
+  for (int p = t; p < nf * nf + nf; p += 64) {
+    double acc = 0.0;
+    if (p < nf * nf) {
+      const int h1 = p % nf, h2 = p / nf;
+      for (int j = 0; j < ns_loc; ++j)
+        if (Ycode[(size_t)i + (size_t)ny * j] >= 0) acc += lam_local(h1, j) * iSigma[j] * lam_local(h2, j);
+      Mrow[(size_t)slot * nf * nf + p] = acc;
+    } else {
+      const int h = p - nf * nf;
+      for (int j = 0; j < ns_loc; ++j) {
+        if (Ycode[(size_t)i + (size_t)ny * j] < 0) continue;
+        double l = 0.0;  // the linear predictor without the group's columns
+        for (int c = 0; c < K; ++c)
+          if (c < loff0 || c >= gend) l += sx[c] * BL[c + (size_t)K * j];
+        acc += (Z[(size_t)i + (size_t)ny * j] - l) * iSigma[j] * lam_local(h, j);
+      }
+      brow[(size_t)slot * nf + h] = acc;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void eta_unit_x_kernel(EtaArgs a, int m) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int nf = a.nf, t = threadIdx.x, q = blockIdx.x, gend = a.loff + m * nf;
+  double* Q = smem;         // nf x nf
+  double* b = Q + nf * nf;  // nf
+  double* xq = b + nf;      // m
+  int* flag = (int*)(xq + m + 1);
+  for (int k = t; k < m; k += 64) xq[k] = a.ev.xs[a.r + k][q];
+  __syncthreads();
+  const int rb = a.unit_ptr[q], re = a.unit_ptr[q + 1];
+  int n_full = 0;
+  for (int p = rb; p < re; ++p) n_full += (a.row_na && a.row_na[a.unit_rows[p]]) ? 0 : 1;
+  for (int p = t; p < nf * nf; p += 64) {
+    const int r1 = p % nf, c1 = p / nf;
+    double g = 0.0;
+    for (int k = 0; k < m; ++k)
+      for (int k2 = 0; k2 < m; ++k2)
+        g += xq[k] * xq[k2] * a.CR[a.loff + k * nf + r1 + (size_t)a.ldcr * (a.foff + k2 * nf + c1)];
+    double v = (r1 == c1 ? 1.0 : 0.0) + n_full * g;
+    if (a.row_na)
+      for (int pp = rb; pp < re; ++pp) {
+        const int slot = a.row_slot[a.unit_rows[pp]];
+        if (slot >= 0) v += a.Mrow[(size_t)slot * nf * nf + p];
+      }
+    Q[p] = v;
+  }
+  for (int h = t; h < nf; h += 64) {
+    double v = 0.0;
+    for (int pp = rb; pp < re; ++pp) {
+      const int i = a.unit_rows[pp];
+      const int slot = a.row_na ? a.row_slot[i] : -1;
+      if (slot >= 0) {
+        v += a.brow[(size_t)slot * nf + h];
+        continue;
+      }
+      for (int k = 0; k < m; ++k) {
+        const int col = a.foff + k * nf + h;
+        double zl = 0.0;
+        for (int c = 0; c < a.nzl; ++c) zl += a.ZL[(size_t)c * a.ev.ny * a.NF + (size_t)i * a.NF + col];
+        double corr = 0.0;
+        for (int kk = 0; kk < a.K; ++kk) {
+          if (kk >= a.loff && kk < gend) continue;
+          corr += xeta_at(a.ev, i, kk) * a.CR[kk + (size_t)a.ldcr * col];
+        }
+        v += xq[k] * (zl - corr);
+      }
+    }
+    b[h] = v;
+  }
+  __syncthreads();
+  wg_chol(Q, nf, nf, flag);                         // RiV = chol(iV)   (:103)
+  wg_forward(Q, nf, nf, b);
+  for (int h = t; h < nf; h += 64)
+    b[h] += a.noise_zero ? 0.0 : normal(a.key, (uint32_t)q, (uint32_t)h, S_ETA + LEVEL_STRIDE * a.r, SWEEP_ITER(a));
+  __syncthreads();
+  wg_backward_t(Q, nf, nf, b);                      // mu + t(backsolve(RiV, rnorm))   (:106-107)
+  for (int h = t; h < nf; h += 64) a.Eta[q + (size_t)a.np * h] = b[h];
+}
+
+// ---------------------------------------------------------------------------
 // Fused updateEta for the common case -- one random level with np == ny (one row per
 // unit), no NA, one rank (R/updateEta.R:42-57).  One 256-thread workgroup per 16-site tile:
 //   1. ZL_i = sum_j Z_ij LS_j, LS = Lambda diag(iSigma)  (:55), on the matrix cores: wave w
@@ -3420,7 +3536,7 @@ void flush_g(State& s) {
 }
 
 static bool eta_fused_ok(const State& s) {
-  return !s.sharded && s.nr == 1 && !s.lev[0].spatial && s.n_na_rows == 0 && s.lev[0].np == s.ny && s.lev[0].uniform_n == 1 &&
+  return !s.sharded && !s.any_xs && s.nr == 1 && !s.lev[0].spatial && s.n_na_rows == 0 && s.lev[0].np == s.ny && s.lev[0].uniform_n == 1 &&
          s.lev[0].nf <= 16 && s.K <= 64 && s.LS != nullptr && !getenv_flag("HMSC_NO_ETA_FUSION");
 }
 
@@ -3533,6 +3649,7 @@ static void eta_levels(State& s, uint32_t iter, const double* zl, int nzl, const
                        const double* na_crrow) {
   for (int r = 0; r < s.nr; ++r) {
     const Level& L = s.lev[r];
+    if (L.eta_alias()) continue;  // a covariate-dependent level's Eta is drawn once, by its group's first level
     if (r > 0) launch_xeta(s);  // levels r' < r were just redrawn (R/updateEta.R:218-226 rebuilds LRan[[r']])
     if (L.spatial) {            // R/updateEta.R:111-140 (spatial.hip)
       launch_eta_spatial(s, r, iter);
@@ -3563,7 +3680,11 @@ static void eta_levels(State& s, uint32_t iter, const double* zl, int nzl, const
     if (s.n_na_rows > 0) {
       double* Mrow = s.Msmall;
       double* brow = Mrow + (size_t)s.n_na_rows * L.nf * L.nf;
-      if (na_crrow) {
+      if (L.xs) {
+        HMSC_REQUIRE(!na_crrow, "covariate-dependent levels: not on a species-sharded chain");
+        eta_na_row_x_kernel<<<s.n_na_rows, 64, (s.K + L.xgroup) * sizeof(double), s.stream>>>(
+            a.ev, r, L.xgroup, L.nf, s.K, a.loff, s.na_rows, s.Z, s.BL, s.iSigma, s.Ycode, s.nsl, Mrow, brow);
+      } else if (na_crrow) {
         na_row_finish_kernel<<<s.n_na_rows, 64, s.K * sizeof(double), s.stream>>>(
             a.ev, r, L.nf, s.K, s.NF, a.loff, a.foff, s.na_rows, zl, na_crrow, Mrow, brow);
       } else {
@@ -3577,7 +3698,10 @@ static void eta_levels(State& s, uint32_t iter, const double* zl, int nzl, const
       a.brow = brow;
     }
     ProfScope ps(s, PROF_ETA_UNIT);
-    if (s.n_na_rows == 0 && L.uniform_n > 0 && L.nf <= 32) {
+    if (L.xs) {
+      const size_t smem = ((size_t)L.nf * L.nf + L.nf + L.xgroup + 2) * sizeof(double);
+      eta_unit_x_kernel<<<L.np, 64, smem, s.stream>>>(a, L.xgroup);
+    } else if (s.n_na_rows == 0 && L.uniform_n > 0 && L.nf <= 32) {
       const size_t smem = ((size_t)L.nf * L.nf + (size_t)s.K * L.nf + 2) * sizeof(double);
       const int grid = (L.np + 63) / 64;
       if (L.nf <= 8)
@@ -3795,6 +3919,7 @@ __global__ __launch_bounds__(256) void init_big_kernel(InitArgs a) {
   }
   // Eta ~ N(0,1)   (:207)
   for (int r = 0; r < a.nr; ++r) {
+    if (!a.Eta[r]) continue;  // (a level sharing another level's Eta: drawn once, by its owner)
     const int64_t n = (int64_t)a.lev_np[r] * a.lev_nf[r];
     for (int64_t p = t0; p < n; p += stride) {
       const int q = (int)(p % a.lev_np[r]), h = (int)(p / a.lev_np[r]);
@@ -3820,7 +3945,7 @@ void launch_init(State& s) {
     a.b1[r] = s.lev[r].b1;
     a.a2[r] = s.lev[r].a2;
     a.b2[r] = s.lev[r].b2;
-    a.Eta[r] = s.lev[r].Eta;
+    a.Eta[r] = s.lev[r].eta_alias() ? nullptr : s.lev[r].Eta;
   }
   a.UGammaL = s.UGammaL;
   a.mGamma = s.mGamma;

@@ -66,6 +66,14 @@ struct Level {
   int* nnCh = nullptr;          // entries i (nnK + 1) + slot, slot 0 = the unit itself (B = 1), ascending i
   int nnBwUnits = 0;            // bandwidth of the precision in units (RCM order)
   int nnAssembledN = 0;         // size of the last assembled system (its band layout zeroed for it)
+  // covariate-dependent level (hmsc_model etaShare / xScale): the level whose units and Eta
+  // this one shares (eta_owner < this index: Eta aliases the owner's buffer), the covariate
+  // column scaling its XEta columns (np, unit order), and -- on the owner -- the levels of
+  // its group (xgroup consecutive levels from it)
+  int eta_owner = -1;
+  double* xs = nullptr;
+  int xgroup = 1;
+  bool eta_alias() const { return eta_owner >= 0; }
 };
 
 struct State {
@@ -81,6 +89,7 @@ struct State {
   bool any_normal = false;       // any family==1 species (local)
   bool any_var = false;          // any species with estimated variance (distr[,2]==1)
   bool any_poisson = false;
+  bool any_xs = false;           // a covariate-dependent level (Level::xs): general updateEta path
   bool all_probit = true;
   bool isigma_fixed_one = true;  // all probit and iSigma never set from outside: iSigma == 1
   int K = 0, NF = 0, Kmax = 0, NFmax = 0;

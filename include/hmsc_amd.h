@@ -76,7 +76,8 @@ typedef struct hmsc_model {
   const int32_t* nfMax;
   const int32_t* sDim;    /* > 0: spatial level (see spatialMethod below); the number of
                            * coordinate columns when sCoord[r] is given             */
-  const int32_t* xDim;    /* covariate-dependent levels: must be 0       */
+  const int32_t* xDim;    /* 0 for every level passed: a covariate-dependent level is passed
+                           * expanded, see etaShare / xScale at the end */
   /* Phylogeny (hM$C; NULL = none).  The grid of R/computeDataParameters.R:19-39
    * (iQg/RQg/detQg over hM$rhopw) is taken in spectral form: the caller passes the
    * eigendecomposition of C (R: e <- eigen(hM$C, symmetric=TRUE); numpy: eigh), from which
@@ -130,6 +131,19 @@ typedef struct hmsc_model {
    * numbers per grid point; updateEta factors the band of the precision in reverse Cuthill-McKee
    * order).  NNGP levels never take iWg / RiWg. */
   const int32_t* nNeighbours;                /* nr (entries of non-NNGP levels ignored) */
+  /* Covariate-dependent levels (HmscRandomLevel(xData=...), rL$xDim = ncr > 0): R's
+   * LRan = sum_k (Eta[Pi,] * x[dfPi, k]) %*% Lambda[,,k] (R/updateZ.R:24-29) is passed as ncr
+   * consecutive levels r0 .. r0+ncr-1 that share the units (same np, Pi), nf and Eta:
+   * etaShare[r] = r0 for each of them (the level whose Eta they use; r itself, or a negative
+   * value, for an ordinary level; NULL: none shared) and xScale[r] = column k of rL$x in unit
+   * order (np doubles), so level r0+k's XEta columns are Eta[Pi,] * x[Pi, k] and its Lambda,
+   * Psi and Delta are R's Lambda[,,k], Psi[,,k] and Delta[,k] with priors nu[k], a1[k], b1[k],
+   * a2[k], b2[k] (R/updateBetaLambda.R:22-53, R/updateLambdaPriors.R:34-48).  updateEta draws
+   * the shared Eta once per unit from lambdaLocal = sum_k x[q, k] Lambda[,,k]
+   * (R/updateEta.R:93-108) and updateNf adds or drops a factor of all ncr levels together
+   * (R/updateNf.R).  Not with spatial levels, updateGammaEta or species sharding. */
+  const int32_t* etaShare;                   /* nr, or NULL                              */
+  const double* xScale[HMSC_MAX_LEVELS];     /* np[r] each, or NULL                      */
 } hmsc_model;
 
 #define HMSC_MODEL_SIZE ((int32_t)sizeof(hmsc_model))
