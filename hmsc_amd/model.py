@@ -487,12 +487,21 @@ def _set_priors_hmsc(hM, V0=None, f0=None, mGamma=None, UGamma=None, aSigma=None
 
 def _set_priors_rl(rL, nu=None, a1=None, b1=None, a2=None, b2=None, alphapw=None, nfMax=None, nfMin=None,
                    setDefault=False, **_):
-    """R/setPriors.HmscRandomLevel.R:18-110 (xDim = 0 levels carry scalar priors)."""
+    """R/setPriors.HmscRandomLevel.R:18-110.  The shrinkage priors are one value per column of
+    rL$x for a covariate-dependent level (xDim = max(rL$xDim, 1), :21-80: a scalar is repeated,
+    a vector must have length xDim), a scalar otherwise."""
+    xDim = max(int(rL.xDim or 0), 1)
     for name, val, dflt in (("nu", nu, 3.0), ("a1", a1, 50.0), ("b1", b1, 1.0), ("a2", a2, 50.0), ("b2", b2, 1.0)):
         if val is not None:
-            rL[name] = float(val)
+            v = np.atleast_1d(np.asarray(val, dtype=np.float64))
+            if v.size == 1:
+                rL[name] = float(v[0]) if not rL.xDim else np.full(xDim, float(v[0]))
+            elif v.size == xDim:
+                rL[name] = v.copy()
+            else:
+                raise ValueError(f"HmscRandomLevel.setPriors: length of {name} argument must be either 1 or rL$xDim")
         elif setDefault:
-            rL[name] = dflt
+            rL[name] = dflt if not rL.xDim else np.full(xDim, dflt)
     if alphapw is not None:
         if not rL.sDim:
             raise ValueError("HmscRandomLevel.setPriors: prior for spatial scale was given, but not spatial coordinates were specified")

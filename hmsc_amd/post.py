@@ -230,10 +230,12 @@ def computeWAIC(hM, ghN=11):
         Yrec = Y.ravel(order="F")[(ii + hM.ny * cc + hM.ny * cN * gg) % Y.size]
     na = np.isnan(Y)
     vals = []
+    from .sampler import level_lran, x_unit_order
+    xs = [x_unit_order(hM, r, rl) if rl.xDim else None for r, rl in enumerate(hM.rL or [])]
     for s in post:
         E = X @ s["Beta"]
         for r in range(hM.nr):
-            E = E + s["Eta"][r][Pi[:, r] - 1] @ s["Lambda"][r]
+            E = E + level_lran(s["Eta"][r], s["Lambda"][r], Pi[:, r] - 1, xs[r])
         std = np.asarray(s["sigma"]) ** -0.5
         Lr = np.zeros(hM.ny)
         if normal.any():

@@ -216,8 +216,15 @@ def predict(hM, post=None, X=None, studyDesign=None, Yc=None, mcmcStep=1, expect
     a.family = L.colmajor_ptr(hM.distr[:, 0], keep, np.int32)
     a.YScalePar = L.colmajor_ptr(hM.YScalePar, keep)
     if hM.nr:
-        PiNew = np.zeros((nyN, hM.nr), dtype=np.int32)
+        # a covariate-dependent level goes to the kernel as one level per column of rL$x with
+        # Eta[q, ] * x[q, k] of the prediction units (R/predict.R:171-176: LRan = sum_k
+        # (Eta[dfPiNew,] * x[dfPiNew, k]) %*% Lambda[,,k])
+        ndev = sum(max(int(rl.xDim or 0), 1) for rl in hM.rL)
+        if ndev > L.MAX_LEVELS:
+            raise ValueError(f"predict: at most {L.MAX_LEVELS} device levels")
+        PiNew = np.zeros((nyN, ndev), dtype=np.int32)
         nps, nfs = [], []
+        d = 0
         for r, name in enumerate(hM.rLNames):
             raw = studyDesign[name]
             col = np.asarray(raw).astype(str)
@@ -234,13 +241,20 @@ def predict(hM, post=None, X=None, studyDesign=None, Yc=None, mcmcStep=1, expect
             nf = max(e.shape[1] for e in etas)
             lams = [np.asarray(s["Lambda"][r]) for s in post]
             etas = [np.pad(e, ((0, 0), (0, nf - e.shape[1]))) for e in etas]      # nf may vary (updateNf)
-            lams = [np.pad(lm, ((0, nf - lm.shape[0]), (0, 0))) for lm in lams]
+            lams = [np.pad(lm, ((0, nf - lm.shape[0]),) + ((0, 0),) * (lm.ndim - 1)) for lm in lams]
             idx = {u: k for k, u in enumerate(unitsPred)}
-            PiNew[:, r] = [idx[v] + 1 for v in col]
-            a.Eta[r] = L.fptr(_stack(keep, [e.reshape(-1, order="F") for e in etas]))
-            a.Lambda[r] = L.fptr(_stack(keep, [lm.reshape(-1, order="F") for lm in lams]))
-            nps.append(len(unitsPred))
-            nfs.append(nf)
+            xd = int(hM.rL[r].xDim or 0)
+            xp = _x_rows(hM, r, unitsPred) if xd else None
+            for k in range(max(xd, 1)):
+                PiNew[:, d] = [idx[v] + 1 for v in col]
+                ek = etas if not xd else [e * xp[:, k:k + 1] for e in etas]
+                lk = lams if not xd else [lm[:, :, k] for lm in lams]
+                a.Eta[d] = L.fptr(_stack(keep, [e.reshape(-1, order="F") for e in ek]))
+                a.Lambda[d] = L.fptr(_stack(keep, [lm.reshape(-1, order="F") for lm in lk]))
+                nps.append(len(unitsPred))
+                nfs.append(nf)
+                d += 1
+        a.nr = ndev
         a.Pi = L.colmajor_ptr(PiNew, keep, np.int32)
         a.np = L.colmajor_ptr(nps, keep, np.int32)
         a.nf = L.colmajor_ptr(nfs, keep, np.int32)
@@ -250,12 +264,32 @@ def predict(hM, post=None, X=None, studyDesign=None, Yc=None, mcmcStep=1, expect
     return [out[k] for k in range(S)]
 
 
+def _x_rows(hM, r, units):
+    """rL$x rows of the given unit names (R indexes rL$x by unit name, R/predict.R:174); unnamed
+    rows are the fitted units in order."""
+    rl = hM.rL[r]
+    x = np.asarray(rl.x, dtype=np.float64)
+    names = [str(i) for i in rl.x.index] if hasattr(rl.x, "index") else None
+    if names is None:
+        fitted = _levels(hM.dfPi[hM.rLNames[r]])
+        pos = {u: k for k, u in enumerate(fitted)}
+        if any(u not in pos for u in units) or x.shape[0] != len(fitted):
+            raise ValueError(f"predict: covariates of new units of level {hM.rLNames[r]} are needed: give xData "
+                             f"as a DataFrame whose index names every unit")
+    else:
+        pos = {n: k for k, n in enumerate(names)}
+        missing = [u for u in units if str(u) not in pos]
+        if missing:
+            raise ValueError(f"predict: no xData rows for units {missing[:5]} of level {hM.rLNames[r]}")
+    return x[[pos[str(u)] for u in units]]
+
+
 def _conditional_etas(hM, post, X, studyDesign, Yc, mcmcStep, rng, device):
     """R/predict.R:191-202: per sample, Z = L; Z = updateZ(Yc); then mcmcStep x (updateEta,
     updateZ), all with the sample's Beta, sigma, Lambda fixed -- the device updaters of a chain
     built on (Yc, X) in R's unscaled space (X and Beta as `post` holds them)."""
     from .model import Hmsc
-    from .sampler import Chain
+    from .sampler import Chain, level_lran
     rl = {name: hM.rL[r] for r, name in enumerate(hM.rLNames)}
     sd = studyDesign.reset_index(drop=True) if hasattr(studyDesign, "reset_index") else studyDesign
     hMc = Hmsc(Y=Yc, X=X, XScale=False, YScale=False, distr=hM.distr, studyDesign=sd, ranLevels=rl,
@@ -272,7 +306,8 @@ def _conditional_etas(hM, post, X, studyDesign, Yc, mcmcStep, rng, device):
                                                 postAlpha=[sam["Alpha"][r]] if hM.rL[r].sDim else None)[0])
             L = X @ sam["Beta"]
             for r in range(hM.nr):
-                L = L + etas[r][hMc.Pi[:, r] - 1] @ sam["Lambda"][r]
+                xr = _x_rows(hM, r, _levels(sd[hM.rLNames[r]])) if hM.rL[r].xDim else None
+                L = L + level_lran(etas[r], sam["Lambda"][r], hMc.Pi[:, r] - 1, xr)
             # the sample's spatial scales condition the spatial levels' updateEta prior
             # (R/predict.R:185 passes Alpha = sam$Alpha)
             ch.set_state(dict(Beta=sam["Beta"], sigma=np.asarray(sam["sigma"]), Eta=etas,

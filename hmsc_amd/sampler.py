@@ -36,6 +36,67 @@ def _finite_int(v, cap):
 SPATIAL_CODE = {"Full": 1, "NNGP": 2, "GPP": 3}
 
 
+def x_unit_order(hM, r, rl):
+    """rL$x in the unit order of Eta (levels(dfPi[,r])): R indexes it by unit name,
+    rL$x[as.character(dfPi[,r]), k] (R/updateZ.R:27); unnamed rows are taken in that order."""
+    x = np.asarray(rl.x, dtype=np.float64)
+    names = [str(i) for i in rl.x.index] if hasattr(rl.x, "index") else None
+    from .model import _factor_levels
+    levels = _factor_levels(hM.dfPi[hM.rLNames[r]])
+    if names is None:
+        if x.shape[0] != len(levels):
+            raise ValueError(f"level {hM.rLNames[r]}: xData has {x.shape[0]} rows for {len(levels)} units; "
+                             f"give it as a DataFrame whose index names the units")
+        return x
+    pos = {n: k for k, n in enumerate(names)}
+    missing = [lv for lv in levels if str(lv) not in pos]
+    if missing:
+        raise ValueError(f"level {hM.rLNames[r]}: no xData rows for units {missing[:5]}")
+    return x[[pos[str(lv)] for lv in levels]]
+
+
+def level_lran(eta, lam, rows, x=None):
+    """LRan of one level for the rows' units (0-based): Eta[Pi,] %*% Lambda, or for a
+    covariate-dependent level sum_k (Eta[Pi,] * x[Pi, k]) %*% Lambda[,,k] (R/updateZ.R:24-29,
+    R/computeWAIC.R:66-70, R/predict.R:171-176); x in the units' order of eta."""
+    lam = np.asarray(lam)
+    if lam.ndim == 2:
+        return eta[rows] @ lam
+    return sum((eta[rows] * x[rows, k:k + 1]) @ lam[:, :, k] for k in range(lam.shape[2]))
+
+
+class LevelMap:
+    """R's random levels -> the device levels of the C ABI.  A covariate-dependent level
+    (rL$xDim = ncr > 0) is ncr consecutive device levels sharing its units and Eta, device level
+    k scaling its XEta columns by rL$x[, k] and holding Lambda[,,k], Psi[,,k], Delta[,k]
+    (include/hmsc_amd.h etaShare / xScale); every other level is one device level."""
+
+    def __init__(self, hM):
+        self.groups, self.xdim = [], []
+        d = 0
+        for rl in hM.rL or []:
+            xd = int(rl.xDim or 0)
+            n = max(xd, 1)
+            self.groups.append(list(range(d, d + n)))
+            self.xdim.append(xd)
+            d += n
+        self.ndev = d
+        if d > L.MAX_LEVELS:
+            raise ValueError(f"this build holds at most {L.MAX_LEVELS} device levels (a covariate-dependent level "
+                             f"counts one per column of xData); the model needs {d}")
+        self.owner = [r for r, g in enumerate(self.groups) for _ in g]     # device level -> R level
+        self.col = [k for g in self.groups for k in range(len(g))]         # device level -> column of rL$x
+
+    def expand(self, per_level):
+        """A per-R-level list -> per device level."""
+        return [per_level[self.owner[d]] for d in range(self.ndev)]
+
+
+def _prior_k(rl, name, k):
+    v = np.atleast_1d(np.asarray(rl[name], dtype=np.float64))
+    return float(v[k] if v.size > 1 else v[0])
+
+
 class ModelBuffers:
     """Column-major copies of the hM fields the sampler consumes (the marshalling the
     R ``.Call`` shim would do), kept alive for the lifetime of the C struct."""
@@ -49,18 +110,20 @@ class ModelBuffers:
         for rl in hM.rL or []:
             if rl.sDim and rl.spatialMethod not in SPATIAL_CODE:
                 raise ValueError(f"unknown spatialMethod {rl.spatialMethod!r}")
-            if rl.xDim:
-                raise NotImplementedError("covariate-dependent random levels are a 'next' row")
+            if rl.xDim and rl.sDim:
+                raise ValueError("a covariate-dependent level cannot also be spatial here (the spatial branches "
+                                 "of R/updateEta.R take Lambda as a matrix)")
+        self.lm = lm = LevelMap(hM)
         self.keep = []
         k = self.keep
         m = L.hmsc_model()
-        m.ny, m.ns, m.nc, m.nt, m.nr = hM.ny, hM.ns, hM.nc, hM.nt, hM.nr
+        m.ny, m.ns, m.nc, m.nt, m.nr = hM.ny, hM.ns, hM.nc, hM.nt, lm.ndev
         m.Y = L.colmajor_ptr(hM.YScaled, k)
         m.Yraw = L.colmajor_ptr(hM.Y, k)
         m.X = L.colmajor_ptr(hM.XScaled, k)
         m.Tr = L.colmajor_ptr(hM.TrScaled, k)
-        m.Pi = L.colmajor_ptr(hM.Pi if hM.nr else np.zeros((hM.ny, 1)), k, np.int32)
-        m.np = L.colmajor_ptr(hM.np if hM.nr else [0], k, np.int32)
+        m.Pi = L.colmajor_ptr(hM.Pi[:, lm.owner] if hM.nr else np.zeros((hM.ny, 1)), k, np.int32)
+        m.np = L.colmajor_ptr([int(hM.np[r]) for r in lm.owner] if hM.nr else [0], k, np.int32)
         m.distr = L.colmajor_ptr(hM.distr, k, np.int32)
         m.V0 = L.colmajor_ptr(hM.V0, k)
         m.f0 = float(hM.f0)
@@ -69,16 +132,27 @@ class ModelBuffers:
         m.aSigma = L.colmajor_ptr(hM.aSigma, k)
         m.bSigma = L.colmajor_ptr(hM.bSigma, k)
         rl = hM.rL or []
-        vec = lambda name: L.colmajor_ptr([float(r[name]) for r in rl] or [0.0], k)  # noqa: E731
+        # priors per device level: column k of a covariate-dependent level takes entry k of
+        # rL$nu / a1 / b1 / a2 / b2 (R/setPriors.HmscRandomLevel.R:21-80)
+        vec = lambda name: L.colmajor_ptr([_prior_k(rl[lm.owner[d]], name, lm.col[d])  # noqa: E731
+                                           for d in range(lm.ndev)] or [0.0], k)
         m.nu, m.a1, m.b1, m.a2, m.b2 = vec("nu"), vec("a1"), vec("b1"), vec("a2"), vec("b2")
         self.nfMax = [_finite_int(r.nfMax, hM.ns) for r in rl]
         self.nfMin = [int(r.nfMin) for r in rl]
-        m.nfMin = L.colmajor_ptr(self.nfMin or [0], k, np.int32)
-        m.nfMax = L.colmajor_ptr(self.nfMax or [0], k, np.int32)
+        m.nfMin = L.colmajor_ptr(lm.expand(self.nfMin) or [0], k, np.int32)
+        m.nfMax = L.colmajor_ptr(lm.expand(self.nfMax) or [0], k, np.int32)
+        if any(lm.xdim):
+            m.etaShare = L.colmajor_ptr([lm.groups[lm.owner[d]][0] for d in range(lm.ndev)], k, np.int32)
+            for r, g in enumerate(lm.groups):
+                if lm.xdim[r]:
+                    x = x_unit_order(hM, r, rl[r])
+                    for kk, d in enumerate(g):
+                        m.xScale[d] = L.colmajor_ptr(np.ascontiguousarray(x[:, kk]), k)
         sdim = [(r.s.shape[1] if r.s is not None else 1) if r.sDim else 0 for r in rl]
-        m.sDim = L.colmajor_ptr(sdim or [0], k, np.int32)
-        m.spatialMethod = L.colmajor_ptr([SPATIAL_CODE[r.spatialMethod] if r.sDim else 0 for r in rl] or [0],
+        m.sDim = L.colmajor_ptr(lm.expand(sdim) or [0], k, np.int32)
+        m.spatialMethod = L.colmajor_ptr(lm.expand([SPATIAL_CODE[r.spatialMethod] if r.sDim else 0 for r in rl]) or [0],
                                          k, np.int32)
+        dev = lambda r: lm.groups[r][0]  # noqa: E731  (the device level of a spatial R level)
         if any(sdim):
             # computeDataParameters' alphapw grid (R/computeDataParameters.R:53-81); the R shim
             # would pass dataParList$rLPar[[r]]$iWg / RiWg / detWg
@@ -88,31 +162,31 @@ class ModelBuffers:
             on_device = [bool(lv.sDim) and ((spatial_grid == "device" and lv.spatialMethod == "Full")
                                             or lv.spatialMethod == "NNGP") for lv in rl]
             rlp = spatialDataParameters(hM, skip=on_device, gpp_dense=False)
-            m.nNeighbours = L.colmajor_ptr([int(lv.nNeighbours or 10) if lv.sDim and lv.spatialMethod == "NNGP" else 0
-                                            for lv in rl], k, np.int32)
-            m.nalpha = L.colmajor_ptr([r.alphapw.shape[0] if r.sDim else 0 for r in rl], k, np.int32)
-            m.nKnots = L.colmajor_ptr([rlp[r]["Fg"].shape[0] if lv.sDim and lv.spatialMethod == "GPP" else 0
-                                       for r, lv in enumerate(rl)], k, np.int32)
+            m.nNeighbours = L.colmajor_ptr(lm.expand([int(lv.nNeighbours or 10) if lv.sDim and lv.spatialMethod == "NNGP"
+                                                      else 0 for lv in rl]), k, np.int32)
+            m.nalpha = L.colmajor_ptr(lm.expand([r.alphapw.shape[0] if r.sDim else 0 for r in rl]), k, np.int32)
+            m.nKnots = L.colmajor_ptr(lm.expand([rlp[r]["Fg"].shape[0] if lv.sDim and lv.spatialMethod == "GPP" else 0
+                                                 for r, lv in enumerate(rl)]), k, np.int32)
             for r, lv in enumerate(rl):
                 if not lv.sDim:
                     continue
-                m.alphapw[r] = L.colmajor_ptr(np.asarray(lv.alphapw, dtype=np.float64), k)
+                m.alphapw[dev(r)] = L.colmajor_ptr(np.asarray(lv.alphapw, dtype=np.float64), k)
                 if on_device[r]:
                     idx = _level_order(hM, r, lv)
                     if lv.spatialMethod == "NNGP" and lv.distMat is not None:
                         raise ValueError("computeDataParameters: Nearest neighbours not available for distance matrices")
                     if lv.distMat is None:
-                        m.sCoord[r] = L.colmajor_ptr(np.asarray(lv.s, dtype=np.float64)[idx], k)
+                        m.sCoord[dev(r)] = L.colmajor_ptr(np.asarray(lv.s, dtype=np.float64)[idx], k)
                     else:
-                        m.distMat[r] = L.colmajor_ptr(lv.distMat[np.ix_(idx, idx)], k)
+                        m.distMat[dev(r)] = L.colmajor_ptr(lv.distMat[np.ix_(idx, idx)], k)
                 elif lv.spatialMethod == "GPP":  # R's low-rank arrays (include/hmsc_amd.h)
                     for f in ("idDg", "idDW12g", "Fg", "iFg", "detDg"):
-                        getattr(m, f)[r] = L.colmajor_ptr(rlp[r][f], k)
+                        getattr(m, f)[dev(r)] = L.colmajor_ptr(rlp[r][f], k)
                 else:
-                    m.iWg[r] = L.colmajor_ptr(rlp[r]["iWg"], k)
-                    m.RiWg[r] = L.colmajor_ptr(rlp[r]["RiWg"], k)
-                    m.detWg[r] = L.colmajor_ptr(rlp[r]["detWg"], k)
-        m.xDim = L.colmajor_ptr([0] * max(1, hM.nr), k, np.int32)
+                    m.iWg[dev(r)] = L.colmajor_ptr(rlp[r]["iWg"], k)
+                    m.RiWg[dev(r)] = L.colmajor_ptr(rlp[r]["RiWg"], k)
+                    m.detWg[dev(r)] = L.colmajor_ptr(rlp[r]["detWg"], k)
+        m.xDim = L.colmajor_ptr([0] * max(1, lm.ndev), k, np.int32)
         m.C = None
         if hM.C is not None:
             # computeDataParameters' rho grid in spectral form (include/hmsc_amd.h): the
@@ -195,14 +269,17 @@ class Chain:
             L.check(self.lib.hmsc_create(C.byref(self.buf.struct), C.c_uint64(int(seed)), device, self.mask,
                                          C.byref(h)))
         self.h = h
+        self.lm = lm = self.buf.lm
         self.rank, self.nranks = rank, nranks
         self.sp0, self.nsl = shard_range(hM.ns, rank, nranks)
-        cap = np.array(self.buf.nfMax + [0] * (L.MAX_LEVELS - len(self.buf.nfMax)), dtype=np.int32)
+        dmax = lm.expand(self.buf.nfMax)
+        cap = np.array(dmax + [0] * (L.MAX_LEVELS - len(dmax)), dtype=np.int32)
         if hasattr(self.lib, "hmsc_get_nf_cap"):  # (a pre-round-4 library strides records by nfMax)
             L.check(self.lib.hmsc_get_nf_cap(self.h, L.iptr(cap)))
         # factors each level's device buffers and record slots hold (K = nc + sum(nf) <= 128; the
         # capacity past every level's nfMin is shared between the levels)
-        self.nf_cap = [int(c) for c in cap[: hM.nr]]
+        self.nf_cap_dev = [int(c) for c in cap[: lm.ndev]]
+        self.nf_cap = [self.nf_cap_dev[g[0]] for g in lm.groups]
         short = [(r, self.buf.nfMax[r], c) for r, c in enumerate(self.nf_cap) if c < self.buf.nfMax[r]]
         if short:
             msg = ("nfMax " + ", ".join(f"{m} of level {r + 1} held as {c}" for r, m, c in short) +
@@ -228,7 +305,7 @@ class Chain:
 
     # ---- state
     def init(self, nf0=None):
-        arr = None if nf0 is None else L.i32(nf0)
+        arr = None if nf0 is None else L.i32(self.lm.expand(list(nf0)))
         L.check(self.lib.hmsc_init_state(self.h, L.iptr(arr)))
 
     def init_z(self):
@@ -238,7 +315,7 @@ class Chain:
     def nf(self):
         out = np.zeros(L.MAX_LEVELS, dtype=np.int32)
         L.check(self.lib.hmsc_get_nf(self.h, L.iptr(out)))
-        return out[: self.hM.nr].copy()
+        return np.array([out[g[0]] for g in self.lm.groups], dtype=np.int32)
 
     def get_state(self, with_z=True):
         hM = self.hM
@@ -251,29 +328,35 @@ class Chain:
         p = L.hmsc_params()
         for key in st:
             setattr(p, key, L.fptr(st[key]))
+        lm = self.lm
         lv = {f: [] for f in ("Eta", "Lambda", "Psi", "Delta", "Alpha")}
-        for r in range(hM.nr):
+        for d in range(lm.ndev):
+            r = lm.owner[d]
             lv["Eta"].append(np.zeros(int(hM.np[r]) * nf[r]))
             lv["Lambda"].append(np.zeros(nf[r] * ns))
             lv["Psi"].append(np.zeros(nf[r] * ns))
             lv["Delta"].append(np.zeros(nf[r]))
             lv["Alpha"].append(np.zeros(nf[r], dtype=np.int32))
-            p.Eta[r] = L.fptr(lv["Eta"][r])
-            p.Lambda[r] = L.fptr(lv["Lambda"][r])
-            p.Psi[r] = L.fptr(lv["Psi"][r])
-            p.Delta[r] = L.fptr(lv["Delta"][r])
-            p.Alpha[r] = L.iptr(lv["Alpha"][r])
+            p.Eta[d] = L.fptr(lv["Eta"][d])
+            p.Lambda[d] = L.fptr(lv["Lambda"][d])
+            p.Psi[d] = L.fptr(lv["Psi"][d])
+            p.Delta[d] = L.fptr(lv["Delta"][d])
+            p.Alpha[d] = L.iptr(lv["Alpha"][d])
         L.check(self.lib.hmsc_get_state(self.h, C.byref(p)))
         out = dict(Gamma=st["Gamma"].reshape(hM.nc, hM.nt, order="F"),
                    iV=st["iV"].reshape(hM.nc, hM.nc, order="F"),
                    Beta=st["Beta"].reshape(hM.nc, ns, order="F"), iSigma=st["iSigma"], rho=int(p.rho))
         if with_z:
             out["Z"] = st["Z"].reshape(hM.ny, ns, order="F")
-        out["Eta"] = [lv["Eta"][r].reshape(int(hM.np[r]), nf[r], order="F") for r in range(hM.nr)]
-        out["Lambda"] = [lv["Lambda"][r].reshape(nf[r], ns, order="F") for r in range(hM.nr)]
-        out["Psi"] = [lv["Psi"][r].reshape(nf[r], ns, order="F") for r in range(hM.nr)]
-        out["Delta"] = [lv["Delta"][r] for r in range(hM.nr)]
-        out["Alpha"] = [lv["Alpha"][r].astype(np.int64) for r in range(hM.nr)]
+        def grp(f, r, shape):  # R's matrix, or for a covariate-dependent level the nf x ns x ncr array
+            parts = [lv[f][d].reshape(shape, order="F") for d in lm.groups[r]]
+            return np.stack(parts, axis=-1) if lm.xdim[r] else parts[0]
+        g0 = [g[0] for g in lm.groups]
+        out["Eta"] = [lv["Eta"][g0[r]].reshape(int(hM.np[r]), nf[r], order="F") for r in range(hM.nr)]
+        out["Lambda"] = [grp("Lambda", r, (nf[r], ns)) for r in range(hM.nr)]
+        out["Psi"] = [grp("Psi", r, (nf[r], ns)) for r in range(hM.nr)]
+        out["Delta"] = [grp("Delta", r, (nf[r],)) for r in range(hM.nr)]
+        out["Alpha"] = [lv["Alpha"][g0[r]].astype(np.int64) for r in range(hM.nr)]
         return out
 
     def set_state(self, st):
@@ -292,6 +375,7 @@ class Chain:
                 setattr(p, key, L.colmajor_ptr(st[key], keep))
         if st.get("rho") is not None:
             p.rho = int(st["rho"])   # 1-based grid index, as parList$rho
+        lm = self.lm
         for r in range(hM.nr):
             nf = 0
             for key in ("Eta", "Lambda", "Psi", "Delta"):
@@ -299,11 +383,17 @@ class Chain:
                 if v is not None and v[r] is not None:
                     a = np.asarray(v[r], dtype=np.float64)
                     nf = a.shape[1] if key == "Eta" else a.shape[0]
-                    getattr(p, key)[r] = L.colmajor_ptr(a, keep)
-            p.nf[r] = nf
+                    for kk, d in enumerate(lm.groups[r]):
+                        # a covariate-dependent level: slice k of Lambda / Psi (nf x ns x ncr) and
+                        # column k of Delta (nf x ncr) to device level k of its group; Eta shared
+                        part = a if (key == "Eta" or not lm.xdim[r]) else a[..., kk]
+                        getattr(p, key)[d] = L.colmajor_ptr(part, keep)
+            for d in lm.groups[r]:
+                p.nf[d] = nf
             al = st.get("Alpha")
             if al is not None and al[r] is not None:   # initPar$Alpha: 1-based grid indices
-                p.Alpha[r] = L.colmajor_ptr(np.asarray(al[r]), keep, np.int32)
+                for d in lm.groups[r]:
+                    p.Alpha[d] = L.colmajor_ptr(np.asarray(al[r]), keep, np.int32)
         L.check(self.lib.hmsc_set_state(self.h, C.byref(p)))
 
     # ---- sweeps
@@ -364,10 +454,17 @@ class Chain:
         """hmsc_run: the device sweep loop with recording; returns the raw record arrays.
         fields: record only these (e.g. ("Beta",)); None records everything."""
         hM = self.hM
+        lm = self.lm
         nr = hM.nr
+        nd = lm.ndev
         ns = self.nsl
-        nfMax = self.nf_cap   # record slots are strided by the device's per-level factor capacity
-        adapt = L.i32(adaptNf if adaptNf is not None else [transient] * max(1, nr))
+        nfMax = self.nf_cap_dev   # record slots are strided by the device's per-level factor capacity
+        if adaptNf is not None and nr:
+            a = list(adaptNf)
+            a = a + [a[-1]] * (nr - len(a))
+            adapt = L.i32(lm.expand(a))
+        else:
+            adapt = L.i32([transient] * max(1, nd))
         rec = None
         arrays = None
         if record and samples > 0:
@@ -379,20 +476,22 @@ class Chain:
             new = lambda k, shape, dt=np.float64: (np.empty if want(k) else np.zeros)(shape, dtype=dt)  # noqa: E731
             arrays = dict(Beta=new("Beta", (S, ns, hM.nc)), Gamma=new("Gamma", (S, hM.nt, hM.nc)),
                           iV=new("iV", (S, hM.nc, hM.nc)), iSigma=new("iSigma", (S, ns)),
-                          rho=new("rho", S, np.int32), rec_nf=np.zeros((max(1, nr), S), dtype=np.int32))
+                          rho=new("rho", S, np.int32), rec_nf=np.zeros((max(1, nd), S), dtype=np.int32))
             rec = L.hmsc_record()
             for k, fp in (("Beta", L.fptr), ("Gamma", L.fptr), ("iV", L.fptr), ("iSigma", L.fptr), ("rho", L.iptr)):
                 if want(k):
                     setattr(rec, k, fp(arrays[k]))
             rec.rec_nf = L.iptr(arrays["rec_nf"])
-            for r in range(nr):
-                nfm = nfMax[r]
+            for d in range(nd):
+                nfm, r = nfMax[d], lm.owner[d]
                 for k, shape, dt in (("Eta", (S, nfm, int(hM.np[r])), np.float64), ("Lambda", (S, ns, nfm), np.float64),
                                      ("Psi", (S, ns, nfm), np.float64), ("Delta", (S, nfm), np.float64),
                                      ("Alpha", (S, nfm), np.int32)):
+                    if k in ("Eta", "Alpha") and d != lm.groups[r][0]:
+                        continue  # (shared by a covariate-dependent level's device levels)
                     if want(k):
-                        arrays[f"{k}{r}"] = np.empty(shape, dtype=dt)
-                        getattr(rec, k)[r] = (L.iptr if dt == np.int32 else L.fptr)(arrays[f"{k}{r}"])
+                        arrays[f"{k}{d}"] = np.empty(shape, dtype=dt)
+                        getattr(rec, k)[d] = (L.iptr if dt == np.int32 else L.fptr)(arrays[f"{k}{d}"])
         L.check(self.lib.hmsc_run_verbose(self.h, int(transient), int(samples), int(thin), L.iptr(adapt),
                                           int(iter0), int(verbose), int(chain),
                                           C.byref(rec) if rec is not None else None))
@@ -401,15 +500,21 @@ class Chain:
         # C buffers were written column-major per sample: view them in R orientation
         out = dict(Beta=arrays["Beta"].transpose(0, 2, 1), Gamma=arrays["Gamma"].transpose(0, 2, 1),
                    iV=arrays["iV"].transpose(0, 2, 1), iSigma=arrays["iSigma"], rho=arrays["rho"],
-                   nf=arrays["rec_nf"][:nr])
+                   nf=arrays["rec_nf"][[g[0] for g in lm.groups]] if nr else arrays["rec_nf"][:0])
         for r in range(nr):
-            for k in ("Eta", "Lambda", "Psi"):
-                if f"{k}{r}" in arrays:
-                    out[f"{k}{r}"] = arrays[f"{k}{r}"].transpose(0, 2, 1)
-            if f"Delta{r}" in arrays:
-                out[f"Delta{r}"] = arrays[f"Delta{r}"]
-            if f"Alpha{r}" in arrays:
-                out[f"Alpha{r}"] = arrays[f"Alpha{r}"].astype(np.int64)
+            g = lm.groups[r]
+            # a covariate-dependent level: Lambda / Psi as (S, nf, ns, ncr), Delta as (S, nf, ncr)
+            for k in ("Lambda", "Psi"):
+                if f"{k}{g[0]}" in arrays:
+                    parts = [arrays[f"{k}{d}"].transpose(0, 2, 1) for d in g]
+                    out[f"{k}{r}"] = np.stack(parts, axis=-1) if lm.xdim[r] else parts[0]
+            if f"Delta{g[0]}" in arrays:
+                parts = [arrays[f"Delta{d}"] for d in g]
+                out[f"Delta{r}"] = np.stack(parts, axis=-1) if lm.xdim[r] else parts[0]
+            if f"Eta{g[0]}" in arrays:
+                out[f"Eta{r}"] = arrays[f"Eta{g[0]}"].transpose(0, 2, 1)
+            if f"Alpha{g[0]}" in arrays:
+                out[f"Alpha{r}"] = arrays[f"Alpha{g[0]}"].astype(np.int64)
         return out
 
 
@@ -451,7 +556,7 @@ def combine_parameters(rec, hM):
             Eta.append(rec[f"Eta{r}"][k, :, :nf])
             Lambda.append(rec[f"Lambda{r}"][k, :nf, :])
             Psi.append(rec[f"Psi{r}"][k, :nf, :])
-            Delta.append(rec[f"Delta{r}"][k, :nf].reshape(nf, 1))
+            Delta.append(rec[f"Delta{r}"][k, :nf].reshape(nf, -1))   # nf x 1, or nf x ncr
             Alpha.append(rec[f"Alpha{r}"][k, :nf])
         post.append(dict(Beta=Beta[k], wRRR=None, Gamma=Gamma[k], V=V[k], rho=float(rho[k]), sigma=sigma[k],
                          Eta=Eta, Lambda=Lambda, Alpha=Alpha, Psi=Psi, Delta=Delta, PsiRRR=None, DeltaRRR=None))
@@ -462,15 +567,21 @@ def combine_parameters(rec, hM):
 # alignPosterior — R/alignPosterior.R:18-100 (sign alignment + nfMax padding)
 # ---------------------------------------------------------------------------
 def alignPosterior(hM):
+    """(For a covariate-dependent level, Lambda nf x ns x ncr, R's Lambda[k,] indexing fails on
+    the array; factor k's values over all species and columns, a[k,,], are what its
+    ns > 1 || xDim > 1 branch evidently compares and flips.)"""
     for r in range(hM.nr):
         nfVec = [pc[0]["Lambda"][r].shape[0] for pc in hM.postList]
         nfMax = max(nfVec)
         tmpl = hM.postList[int(np.argmax(nfVec))]
         LamMean = np.mean(np.stack([s["Lambda"][r] for s in tmpl]), axis=0)          # :31-33
+        xd = int(hM.rL[r].xDim or 0)
+        LamMean = LamMean.reshape(LamMean.shape[0], -1)
         for cInd, cpL in enumerate(hM.postList):
-            lam = np.stack([s["Lambda"][r] for s in cpL])                           # (S, nf, ns)
+            lam = np.stack([s["Lambda"][r] for s in cpL])                           # (S, nf, ns[, ncr])
+            lam = lam.reshape(lam.shape[0], lam.shape[1], -1)
             nf = lam.shape[1]
-            if hM.ns > 1:
+            if hM.ns > 1 or xd > 1:
                 a = lam - lam.mean(axis=2, keepdims=True)
                 b = LamMean[:nf] - LamMean[:nf].mean(axis=1, keepdims=True)
                 num = np.einsum("skj,kj->sk", a, b)
@@ -483,13 +594,15 @@ def alignPosterior(hM):
             for j, s in enumerate(cpL):
                 flip = sgn[j] < 0
                 if flip.any():                                                      # :50-56
-                    s["Lambda"][r] = np.where(flip[:, None], -s["Lambda"][r], s["Lambda"][r])
+                    fl = flip.reshape((-1,) + (1,) * (s["Lambda"][r].ndim - 1))
+                    s["Lambda"][r] = np.where(fl, -s["Lambda"][r], s["Lambda"][r])
                     s["Eta"][r] = np.where(flip[None, :], -s["Eta"][r], s["Eta"][r])
                 if nf < nfMax:                                                      # :57-68
                     pad = nfMax - nf
-                    s["Lambda"][r] = np.vstack([s["Lambda"][r], np.zeros((pad, hM.ns))])
-                    s["Psi"][r] = np.vstack([s["Psi"][r], np.zeros((pad, hM.ns))])
-                    s["Delta"][r] = np.vstack([s["Delta"][r], np.ones((pad, 1))])
+                    lsh = (pad,) + s["Lambda"][r].shape[1:]
+                    s["Lambda"][r] = np.concatenate([s["Lambda"][r], np.zeros(lsh)], axis=0)
+                    s["Psi"][r] = np.concatenate([s["Psi"][r], np.zeros(lsh)], axis=0)
+                    s["Delta"][r] = np.vstack([s["Delta"][r], np.ones((pad, s["Delta"][r].shape[1]))])
                     s["Eta"][r] = np.hstack([s["Eta"][r], np.zeros((s["Eta"][r].shape[0], pad))])
                     if hM.rL[r].sDim:
                         s["Alpha"][r] = np.r_[s["Alpha"][r], np.ones(pad, dtype=np.int64)]

@@ -250,12 +250,45 @@ def gpp_eta_literal(st, model, r, S, dp, xi1=None, xi2=None):
 # ---------------------------------------------------------------------------
 # linear predictor — R/updateZ.R:11-34 (repeated in updateEta/InvSigma/Gamma2)
 # ---------------------------------------------------------------------------
+def _xdim(model, r):
+    return int(model["rL"][r].get("xDim", 0) or 0) if r < len(model.get("rL", [])) else 0
+
+
+def _vlev(model, r):
+    """The device level index of level r's first column block: a covariate-dependent level
+    (xDim = ncr > 0) is ncr device levels sharing Eta (include/hmsc_amd.h etaShare / xScale),
+    so the Philox level streams of level r start at sum_{r' < r} max(xDim_r', 1); = r without
+    covariate-dependent levels."""
+    return sum(max(_xdim(model, q), 1) for q in range(r))
+
+
+def _prior(rl, name, k):
+    """rL$nu / a1 / b1 / a2 / b2: scalars, or one per column of rL$x
+    (R/setPriors.HmscRandomLevel.R:21-80)."""
+    v = np.atleast_1d(np.asarray(rl[name], dtype=np.float64))
+    return float(v[k] if v.size > 1 else v[0])
+
+
 def eta_full(st, model, r):
-    return st["Eta"][r][model["Pi"][:, r] - 1, :]
+    """Eta[Pi,] or, for a covariate-dependent level, [Eta[Pi,] * x[dfPi, k] for k] (the
+    EtaFull / EtaSt columns of R/updateBetaLambda.R:21-36; x rows in unit order)."""
+    E = st["Eta"][r][model["Pi"][:, r] - 1, :]
+    xd = _xdim(model, r)
+    if not xd:
+        return E
+    x = np.asarray(model["rL"][r]["x"], dtype=np.float64)[model["Pi"][:, r] - 1]
+    return np.concatenate([E * x[:, k:k + 1] for k in range(xd)], axis=1)
+
+
+def lambda_rows(lam):
+    """Lambda[[r]] as BetaLambda rows: the matrix itself, or for an nf x ns x ncr array the
+    ncr slices stacked (row f + nf k, R/updateBetaLambda.R:42-53,150-154)."""
+    lam = np.asarray(lam)
+    return lam if lam.ndim == 2 else np.concatenate([lam[:, :, k] for k in range(lam.shape[2])], axis=0)
 
 
 def l_ran(st, model, r):
-    return eta_full(st, model, r) @ st["Lambda"][r]
+    return eta_full(st, model, r) @ lambda_rows(st["Lambda"][r])
 
 
 def linear_predictor(st, model):
@@ -357,6 +390,10 @@ def _xeta_and_prior(st, model):
     ns = model["Y"].shape[1]
     pl = []
     for r in range(nr):                                               # :42-53
+        if _xdim(model, r):   # tau = apply(delta, 2, cumprod) per column k, psiSt rows f + nf k
+            tau = np.cumprod(st["Delta"][r], axis=0)
+            pl.append(lambda_rows(st["Psi"][r] * tau[:, None, :]))
+            continue
         tau = np.cumprod(st["Delta"][r])
         pl.append(st["Psi"][r] * tau[:, None])
     priorLambda = np.concatenate(pl, axis=0) if pl else np.zeros((0, ns))
@@ -412,6 +449,11 @@ def update_beta_lambda(st, model, rng, it, data_par=None, zero_noise=False):
     off = nc
     for r in range(nr):                                                # :149-155
         nf = st["Lambda"][r].shape[0]
+        xd = _xdim(model, r)
+        if xd:  # aperm(array(rows, c(nf, ncr, ns)), c(1, 3, 2))
+            Lambda.append(BL[off:off + nf * xd].reshape(xd, nf, ns).transpose(1, 2, 0).copy())
+            off += nf * xd
+            continue
         Lambda.append(BL[off:off + nf].copy())
         off += nf
     return Beta, Lambda
@@ -539,7 +581,13 @@ def update_lambda_priors(st, model, rng, it):
     Psi, Delta = [], []
     ns = model["Y"].shape[1]
     for r, rl in enumerate(model["rL"]):
+        if _xdim(model, r):
+            p, d = _lambda_priors_x(st, model, rng, it, r)
+            Psi.append(p)
+            Delta.append(d)
+            continue
         nu, a1, b1, a2, b2 = rl["nu"], rl["a1"], rl["b1"], rl["a2"], rl["b2"]
+        v = _vlev(model, r)
         delta = st["Delta"][r].astype(np.float64).copy()
         lam = st["Lambda"][r]
         nf = lam.shape[0]
@@ -548,20 +596,51 @@ def update_lambda_priors(st, model, rng, it):
         aPsi = nu / 2 + 0.5
         bPsi = nu / 2 + 0.5 * lam2 * tau[:, None]                      # :22
         hh, jj = np.meshgrid(np.arange(nf), np.arange(ns), indexing="ij")
-        psi = rng.gamma(hh + nf * jj, R.S_PSI + R.LEVEL_STRIDE * r, it, aPsi, bPsi)   # :23
+        psi = rng.gamma(hh + nf * jj, R.S_PSI + R.LEVEL_STRIDE * v, it, aPsi, bPsi)   # :23
         M = psi * lam2
         rs = M.sum(axis=1)
         ad = a1 + 0.5 * ns * nf                                        # :25
         bd = b1 + 0.5 * np.sum(tau * rs) / delta[0]                    # :26
-        delta[0] = rng.gamma(0, R.S_DELTA + R.LEVEL_STRIDE * r, it, ad, bd)
+        delta[0] = rng.gamma(0, R.S_DELTA + R.LEVEL_STRIDE * v, it, ad, bd)
         for h in range(1, nf):                                         # :28-32
             tau = np.cumprod(delta)
             ad = a2 + 0.5 * ns * (nf - h)
             bd = b2 + 0.5 * np.sum(tau[h:] * rs[h:]) / delta[h]
-            delta[h] = rng.gamma(h, R.S_DELTA + R.LEVEL_STRIDE * r, it, ad, bd)
+            delta[h] = rng.gamma(h, R.S_DELTA + R.LEVEL_STRIDE * v, it, ad, bd)
         Psi.append(psi)
         Delta.append(delta)
     return Psi, Delta
+
+
+def _lambda_priors_x(st, model, rng, it, r):
+    """The array branch (R/updateLambdaPriors.R:34-48) for Lambda nf x ns x ncr: psi and the
+    delta chain of column k are the matrix branch's on Lambda[,,k] with the priors' k-th entries
+    (device level _vlev(r) + k).  R draws psi as rgamma(nf*ns*ncr, aPsi, bPsi) with the length-ncr
+    nu recycled over the array's cells; with one nu for every column (the default, rep(3, xDim))
+    that is nu[k]."""
+    rl = model["rL"][r]
+    lam = st["Lambda"][r]
+    nf, ns, ncr = lam.shape
+    psi = np.empty_like(lam)
+    delta = np.asarray(st["Delta"][r], dtype=np.float64).reshape(nf, ncr).copy()
+    for k in range(ncr):
+        v = _vlev(model, r) + k
+        nu = _prior(rl, "nu", k)
+        d = delta[:, k]
+        tau = np.cumprod(d)
+        lam2 = lam[:, :, k] ** 2
+        hh, jj = np.meshgrid(np.arange(nf), np.arange(ns), indexing="ij")
+        psi[:, :, k] = rng.gamma(hh + nf * jj, R.S_PSI + R.LEVEL_STRIDE * v, it, nu / 2 + 0.5,
+                                 nu / 2 + 0.5 * lam2 * tau[:, None])
+        rs = (psi[:, :, k] * lam2).sum(axis=1)
+        bd = _prior(rl, "b1", k) + 0.5 * np.sum(tau * rs) / d[0]
+        d[0] = rng.gamma(0, R.S_DELTA + R.LEVEL_STRIDE * v, it, _prior(rl, "a1", k) + 0.5 * ns * nf, bd)
+        for h in range(1, nf):
+            tau = np.cumprod(d)
+            bd = _prior(rl, "b2", k) + 0.5 * np.sum(tau[h:] * rs[h:]) / d[h]
+            d[h] = rng.gamma(h, R.S_DELTA + R.LEVEL_STRIDE * v, it, _prior(rl, "a2", k) + 0.5 * ns * (nf - h), bd)
+        delta[:, k] = d
+    return psi, delta
 
 
 # ---------------------------------------------------------------------------
@@ -599,6 +678,33 @@ def eta_unit_moments(st, model, r, S):
     return precs, means
 
 
+def eta_unit_moments_x(st, model, r, S):
+    """Covariate-dependent level (R/updateEta.R:93-108): per unit q, lambdaLocal =
+    sum_k x[q, k] Lambda[,,k]; Q_q = I + sum_{rows p of q} lambdaLocal diag(iSigma Yx_p)
+    lambdaLocal^T, mu_q = Q_q^-1 sum_p lambdaLocal diag(iSigma Yx_p) S_p."""
+    Y = model["Y"]
+    lam = st["Lambda"][r]
+    nf = lam.shape[0]
+    iS = st["iSigma"]
+    Pi_r = model["Pi"][:, r] - 1
+    npr = st["Eta"][r].shape[0]
+    x = np.asarray(model["rL"][r]["x"], dtype=np.float64)
+    Yx = ~np.isnan(Y)
+    precs = np.empty((npr, nf, nf))
+    means = np.empty((npr, nf))
+    for q in range(npr):
+        lL = np.tensordot(lam, x[q], axes=([2], [0]))                    # rowSums(lambda * x[q,], dims=2)
+        Q = np.eye(nf)
+        b = np.zeros(nf)
+        for p in np.nonzero(Pi_r == q)[0]:
+            w = iS * Yx[p]
+            Q = Q + (lL * w[None, :]) @ lL.T
+            b = b + (np.where(Yx[p], S[p], 0.0) * iS) @ lL.T
+        precs[q] = Q
+        means[q] = np.linalg.solve(Q, b)
+    return precs, means
+
+
 def _eta_spatial_full(st, model, r, S, dp, rng, it, zero_noise):
     """Spatial level, R/updateEta.R:115-147 ('Full'; 'NNGP' is the same code on a sparse
     iWg; 'GPP' goes to _eta_spatial_gpp, R's low-rank form): one dense (np nf)^2 system
@@ -618,7 +724,7 @@ def _eta_spatial_full(st, model, r, S, dp, rng, it, zero_noise):
         iU[h * npr:(h + 1) * npr, h * npr:(h + 1) * npr] += iWg[alpha[h] - 1]
     fS = (P.T @ S) @ (lam * iS[None, :]).T
     xi = None if zero_noise else \
-        rng.normal(np.arange(npr)[:, None], np.arange(nf)[None, :], R.S_ETA + R.LEVEL_STRIDE * r, it).ravel(order="F")
+        rng.normal(np.arange(npr)[:, None], np.arange(nf)[None, :], R.S_ETA + R.LEVEL_STRIDE * _vlev(model, r), it).ravel(order="F")
     if model["rL"][r].get("spatialMethod", "Full") == "NNGP":
         # the device factors the sparse NNGP precision in RCM order, factors interleaved per unit
         # (index pos[q] nf + h, nngp.hip): eta = P' L^-T (L^-1 P vec(fS) + P xi), L L' = P iUEta P'
@@ -652,7 +758,7 @@ def _eta_spatial_gpp(st, model, r, S, dp, rng, it, zero_noise):
     nK = dp["rLPar"][r]["Fg"].shape[1]
     if zero_noise:
         return gpp_eta_literal(st, model, r, S, dp)[0]
-    stream = R.S_ETA + R.LEVEL_STRIDE * r
+    stream = R.S_ETA + R.LEVEL_STRIDE * _vlev(model, r)
     xi1 = rng.normal(np.arange(n)[:, None], np.arange(nf)[None, :], stream, it).ravel(order="F")
     xi2 = rng.normal(np.arange(nK)[:, None], GPP_XI2_SUB + np.arange(nf)[None, :], stream, it).ravel(order="F")
     return gpp_eta_literal(st, model, r, S, dp, xi1, xi2)[0]
@@ -690,7 +796,7 @@ def update_alpha(st, model, rng, it, data_par=None):
         for h in range(nf):
             like = np.log(alphapw[:, 1]) - 0.5 * det - 0.5 * v[:, h]
             like = np.exp(like - like.max())
-            u = rng.uniforms(h, 0, R.S_ALPHA + R.LEVEL_STRIDE * r, it)[0]
+            u = rng.uniforms(h, 0, R.S_ALPHA + R.LEVEL_STRIDE * _vlev(model, r), it)[0]
             a[h] = int(np.searchsorted(np.cumsum(like), u * like.sum(), side="right")) + 1
         out.append(a)
     return out
@@ -703,10 +809,12 @@ def update_eta(st, model, rng, it, zero_noise=False, data_par=None):
     LFix = model["X"] @ st["Beta"]                                     # :11-20
     for r in range(nr):
         S = st["Z"] - LFix                                             # :31-37
+        st["Eta"] = Eta
         for r2 in range(nr):
             if r2 != r:
-                S = S - Eta[r2][model["Pi"][:, r2] - 1] @ st["Lambda"][r2]
-        st["Eta"] = Eta
+                # (R's in-loop LRan refresh of a covariate-dependent level, :205, indexes x and
+                # Lambda by the level number r instead of k; this is the form of :23-29)
+                S = S - l_ran(st, model, r2)
         if model["rL"][r].get("sDim", 0) > 0:                          # :111-197
             dp = data_par if data_par is not None else compute_data_parameters(model)
             if model["rL"][r].get("spatialMethod", "Full") == "GPP":
@@ -714,13 +822,13 @@ def update_eta(st, model, rng, it, zero_noise=False, data_par=None):
             else:
                 Eta[r] = _eta_spatial_full(st, model, r, S, dp, rng, it, zero_noise)
             continue
-        precs, means = eta_unit_moments(st, model, r, S)
+        precs, means = eta_unit_moments_x(st, model, r, S) if _xdim(model, r) else eta_unit_moments(st, model, r, S)
         npr, nf = means.shape
         RiV = np.swapaxes(np.linalg.cholesky(precs), 1, 2)              # chol(): upper R, R'R = Q
         if zero_noise:
             xi = np.zeros((npr, nf))
         else:
-            xi = rng.normal(np.arange(npr)[:, None], np.arange(nf)[None, :], R.S_ETA + R.LEVEL_STRIDE * r, it)
+            xi = rng.normal(np.arange(npr)[:, None], np.arange(nf)[None, :], R.S_ETA + R.LEVEL_STRIDE * _vlev(model, r), it)
         Eta[r] = means + np.linalg.solve(RiV, xi[:, :, None])[:, :, 0]  # backsolve(RiV, xi)  :56,69,90
     return Eta
 
@@ -752,24 +860,35 @@ def update_nf(st, model, r, rng, it):
                                    st["Delta"][r], st["Alpha"][r])
     c0, c1, epsilon, prop = 1.0, 0.0005, 1e-3, 1.0                      # :10-13
     prob = 1 / np.exp(c0 + c1 * it)
-    stream = R.LEVEL_STRIDE * r
+    v0 = _vlev(model, r)
+    stream = R.LEVEL_STRIDE * v0
     u = rng.uniforms(0, 0, R.S_NF + stream, it)[0]
+    xd = _xdim(model, r)
     if u < prob:                                                       # :16
         ns = lam.shape[1]
         nf = lam.shape[0]
         npr = eta.shape[0]
         small = np.abs(lam) < epsilon
-        smallProp = small.mean(axis=1)
+        smallProp = small.reshape(nf, -1).mean(axis=1)                 # rowMeans (over ns, and ncr)
         indRedundant = smallProp >= prop
         numRedundant = int(indRedundant.sum())
         if nf < rl["nfMax"] and it > 20 and numRedundant == 0 and np.all(smallProp < 0.995):
             nf += 1                                                    # :26-54
             eta = np.concatenate([eta, rng.normal(np.arange(npr), 0, R.S_NF_ETA + stream, it)[:, None]], axis=1)
             alpha = np.concatenate([alpha, [1]])
-            lam = np.concatenate([lam, np.zeros((1, ns))], axis=0)
-            newpsi = rng.gamma(np.arange(ns), R.S_NF_PSI + stream, it, rl["nu"] / 2, rl["nu"] / 2)
-            psi = np.concatenate([psi, newpsi[None, :]], axis=0)
-            delta = np.concatenate([delta, [rng.gamma(0, R.S_NF_DELTA + stream, it, rl["a2"], rl["b2"])]])
+            if not xd:
+                lam = np.concatenate([lam, np.zeros((1, ns))], axis=0)
+                newpsi = rng.gamma(np.arange(ns), R.S_NF_PSI + stream, it, rl["nu"] / 2, rl["nu"] / 2)
+                psi = np.concatenate([psi, newpsi[None, :]], axis=0)
+                delta = np.concatenate([delta, [rng.gamma(0, R.S_NF_DELTA + stream, it, rl["a2"], rl["b2"])]])
+            else:                                                      # :41-47, column k on level v0 + k
+                lam = np.concatenate([lam, np.zeros((1, ns, xd))], axis=0)
+                newpsi = np.stack([rng.gamma(np.arange(ns), R.S_NF_PSI + R.LEVEL_STRIDE * (v0 + k), it,
+                                             _prior(rl, "nu", k) / 2, _prior(rl, "nu", k) / 2) for k in range(xd)], axis=1)
+                psi = np.concatenate([psi, newpsi[None]], axis=0)
+                newd = [rng.gamma(0, R.S_NF_DELTA + R.LEVEL_STRIDE * (v0 + k), it, _prior(rl, "a2", k),
+                                  _prior(rl, "b2", k)) for k in range(xd)]
+                delta = np.concatenate([delta, np.asarray(newd)[None, :]], axis=0)
         elif numRedundant > 0 and nf > rl["nfMin"]:                    # :55-68
             # setdiff(1:nf, indRedundant) with a logical vector: TRUE->1, FALSE->0,
             # so factor 1 is dropped whenever any factor is redundant (quirk kept).
@@ -803,15 +922,28 @@ def compute_initial_parameters(model, rng, nf=None):
     Eta, Lambda, Psi, Delta, Alpha = [], [], [], [], []
     for r, rl in enumerate(model["rL"]):
         nfr = int(rl["nfMin"]) if nf is None else int(nf[r])
-        s = R.LEVEL_STRIDE * r
-        d = np.empty(nfr)
-        d[0] = rng.gamma(0, R.S_INIT_DELTA + s, it, rl["a1"], rl["b1"])   # :175
-        if nfr > 1:
-            d[1:] = rng.gamma(np.arange(1, nfr), R.S_INIT_DELTA + s, it, rl["a2"], rl["b2"])
+        v0 = _vlev(model, r)
+        s = R.LEVEL_STRIDE * v0
         hh, jj2 = np.meshgrid(np.arange(nfr), np.arange(ns), indexing="ij")
-        psi = rng.gamma(hh + nfr * jj2, R.S_INIT_PSI + s, it, rl["nu"] / 2, rl["nu"] / 2)  # :183
-        tau = np.cumprod(d)
-        lam = rng.normal(hh + nfr * jj2, 0, R.S_INIT_LAMBDA + s, it) * np.sqrt(psi * tau[:, None]) ** -1  # :189-193
+        xd = _xdim(model, r)
+        blocks = []
+        for k in range(max(xd, 1)):  # covariate-dependent levels: column k of Delta / Psi / Lambda on device level v0 + k
+            sk = R.LEVEL_STRIDE * (v0 + k)
+            d = np.empty(nfr)
+            d[0] = rng.gamma(0, R.S_INIT_DELTA + sk, it, _prior(rl, "a1", k), _prior(rl, "b1", k))   # :175,177
+            if nfr > 1:
+                d[1:] = rng.gamma(np.arange(1, nfr), R.S_INIT_DELTA + sk, it, _prior(rl, "a2", k), _prior(rl, "b2", k))
+            nu = _prior(rl, "nu", k)
+            psi = rng.gamma(hh + nfr * jj2, R.S_INIT_PSI + sk, it, nu / 2, nu / 2)  # :183,185
+            tau = np.cumprod(d)
+            lam = rng.normal(hh + nfr * jj2, 0, R.S_INIT_LAMBDA + sk, it) * np.sqrt(psi * tau[:, None]) ** -1  # :189-198
+            blocks.append((d, psi, lam))
+        if xd:
+            d = np.stack([b[0] for b in blocks], axis=1)
+            psi = np.stack([b[1] for b in blocks], axis=2)
+            lam = np.stack([b[2] for b in blocks], axis=2)
+        else:
+            d, psi, lam = blocks[0]
         npr = int(model["np"][r])
         qq, kk2 = np.meshgrid(np.arange(npr), np.arange(nfr), indexing="ij")
         eta = rng.normal(qq, kk2, R.S_INIT_ETA + s, it)                # :207

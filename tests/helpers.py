@@ -14,10 +14,13 @@ from oracle import hmsc_oracle as O  # noqa: E402
 
 def synthetic_model(ny=200, ns=30, nc=4, nf=3, seed=1, na_frac=0.0, n_normal=0, units=None, nr=1,
                     nf_fit=None, nt=1, yscale=False, C=None, n_poisson=0, n_lognormal=0, spatial=None,
-                    alpha_n=None, spatial_method="Full", n_neighbours=None, n_knots=None, nf_default=False):
+                    alpha_n=None, spatial_method="Full", n_neighbours=None, n_knots=None, nf_default=False,
+                    x_dim=0):
     """Probit JSDM generated like BASELINE.md's synthetic config; optionally the first
     n_normal species normal, the next n_poisson Poisson and n_lognormal lognormal Poisson
-    (counts ~ Poisson(exp(L / 2)), vignette_2's mixed-distribution model)."""
+    (counts ~ Poisson(exp(L / 2)), vignette_2's mixed-distribution model).  x_dim > 0: level 0
+    is covariate-dependent (HmscRandomLevel(xData=...) with an intercept column and x_dim - 1
+    normal covariates per unit, R's LRan = sum_k (Eta[Pi,] * x[, k]) Lambda[,,k])."""
     rng = np.random.default_rng(seed)
     X = np.column_stack([np.ones(ny), rng.standard_normal((ny, nc - 1))])
     Tr = np.column_stack([np.ones(ns)] + [rng.standard_normal(ns) for _ in range(nt - 1)]) if nt > 1 else None
@@ -33,7 +36,13 @@ def synthetic_model(ny=200, ns=30, nc=4, nf=3, seed=1, na_frac=0.0, n_normal=0, 
         rng.shuffle(pi) if npr < ny else None
         eta = rng.standard_normal((npr, nf))
         lam = rng.standard_normal((nf, ns)) / (np.arange(1, nf + 1)[:, None])
-        L = L + eta[pi] @ lam
+        xr = None
+        if x_dim and r == 0:
+            xr = np.column_stack([np.ones(npr)] + [rng.standard_normal(npr) for _ in range(x_dim - 1)])
+            for k in range(x_dim):
+                L = L + (eta[pi] * xr[pi, k:k + 1]) @ (lam / (k + 1))
+        else:
+            L = L + eta[pi] @ lam
         name = f"lev{r}"
         if spatial is not None and r in spatial:
             # spatial 'Full' level: unit coordinates on the unit square, zero-padded unit
@@ -49,6 +58,11 @@ def synthetic_model(ny=200, ns=30, nc=4, nf=3, seed=1, na_frac=0.0, n_normal=0, 
                 diag = np.sqrt(2.0)
                 H.setPriors(rl, alphapw=np.column_stack([diag * np.arange(alpha_n + 1) / alpha_n,
                                                           np.r_[0.5, np.full(alpha_n, 0.5 / alpha_n)]]))
+        elif xr is not None:
+            import pandas as pd
+            sd[name] = np.array([f"u{k:05d}" for k in pi])
+            xdf = pd.DataFrame(xr, columns=[f"x{k}" for k in range(x_dim)], index=[f"u{k:05d}" for k in range(npr)])
+            rl = H.HmscRandomLevel(xData=xdf)
         else:
             sd[name] = np.array([f"u{k}" for k in pi])
             rl = H.HmscRandomLevel(units=sd[name])
@@ -93,6 +107,9 @@ def oracle_model(hM):
              rL=[dict(nu=rl.nu, a1=rl.a1, b1=rl.b1, a2=rl.a2, b2=rl.b2, nfMin=rl.nfMin, nfMax=rl.nfMax,
                       sDim=rl.sDim, xDim=rl.xDim) for rl in (hM.rL or [])])
     for r, (d, rl) in enumerate(zip(m["rL"], hM.rL or [])):
+        if rl.xDim:   # covariate-dependent level: rL$x in the unit order of Eta
+            from hmsc_amd.sampler import x_unit_order
+            d["x"] = x_unit_order(hM, r, rl)
         if rl.sDim:   # spatial 'Full': the distance matrix of the unit coordinates, alphapw grid
             # rows of rl$s in levels(dfPi[,r]) order, the unit order of Eta (R indexes s by
             # the unit names, R/computeDataParameters.R:56,92,142)
