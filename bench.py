@@ -180,7 +180,9 @@ def main():
     hM = synthetic_probit(ny=args.ny, ns=args.ns, nc=args.nc, nf=args.nf)
     upd = {"GammaEta": False}
     if args.mode == "sharded":
-        ch = H.Chain(hM, 1234567, device=local, updater=upd, rank=rank, nranks=world, comm_id=_shared_comm_id(rank, dist))
+        cid = _shared_comm_id(rank, dist)
+        with _stdout_to_stderr():
+            ch = H.Chain(hM, 1234567, device=local, updater=upd, rank=rank, nranks=world, comm_id=cid)
     else:
         ch = H.Chain(hM, 1234567 + 7919 * rank, device=local, updater=upd)
     ch.init([args.nf])
@@ -415,10 +417,28 @@ def traced_launch(csv_path, kernel):
     return None
 
 
+class _stdout_to_stderr:
+    """RCCL prints its version banner on stdout when the first communicator is made; the
+    driver reads bench.py's stdout as ONE JSON line, so the RCCL setup writes to stderr."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
 def _shared_comm_id(rank, dist):
     """An RCCL unique id made by rank 0 and broadcast over gloo (hmsc_comm_unique_id)."""
     from hmsc_amd.sampler import comm_unique_id
-    obj = [comm_unique_id() if rank == 0 else None]
+    with _stdout_to_stderr():
+        cid = comm_unique_id() if rank == 0 else None
+    obj = [cid]
     if dist is not None:
         dist.broadcast_object_list(obj, src=0)
     return obj[0]
@@ -431,16 +451,30 @@ def sharded_leg(hM, args, rank, world, local, dist, steps=200, warmup=40):
     reported beside it (strong scaling: the same ns = 1000 species over more GPUs)."""
     import torch
     cid = _shared_comm_id(rank, dist)
-    ch = H.Chain(hM, 1234567, device=local, updater={"GammaEta": False}, rank=rank, nranks=world, comm_id=cid)
+    with _stdout_to_stderr():
+        ch = H.Chain(hM, 1234567, device=local, updater={"GammaEta": False}, rank=rank, nranks=world, comm_id=cid)
     ch.init([args.nf])
     ch.run(transient=0, samples=1, thin=1, adaptNf=[0], record=True)
     ch.prepare_graphs(2)
-    ch.run(transient=0, samples=warmup, thin=1, adaptNf=[0], iter0=1, record=True)
-    ch.sync()
+    # warm-up: at least `warmup` recorded sweeps, and at least 0.5 s of them (a new sharded
+    # chain's first ~150 replayed sweeps ran ~40 % slower than its steady state, r06 traces);
+    # rank 0 decides so every rank runs the same sweeps
+    it, t_w = 1, time.perf_counter()
+    while True:
+        ch.run(transient=0, samples=warmup, thin=1, adaptNf=[0], iter0=it, record=True)
+        ch.sync()
+        it += warmup
+        go = time.perf_counter() - t_w < 0.5
+        if dist is not None:
+            f = torch.tensor([1 if go else 0], dtype=torch.int32)
+            dist.broadcast(f, src=0)
+            go = bool(f.item())
+        if not go:
+            break
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
-    ch.run(transient=0, samples=steps, thin=1, adaptNf=[0], iter0=1 + warmup, record=True)
+    ch.run(transient=0, samples=steps, thin=1, adaptNf=[0], iter0=it, record=True)
     ch.sync()
     if dist is not None:
         dist.barrier()
@@ -454,7 +488,7 @@ def sharded_leg(hM, args, rank, world, local, dist, steps=200, warmup=40):
     nsl = ch.nsl
     ch.close()
     return {"value": round(steps / t, 3), "unit": "sweeps/s", "ms_per_step": round(1e3 * t / steps, 4),
-            "steps": steps, "warmup": warmup, "ranks": world, "species_per_rank": nsl, "scaling": "strong",
+            "steps": steps, "warmup": it - 1, "ranks": world, "species_per_rank": nsl, "scaling": "strong",
             "allreduces_per_sweep": int(ar[2]), "graphs": bool(graph[0]),
             "transport": f"RCCL ({world}-rank communicator)",
             "note": "one chain, species-sharded over the GPUs, recording every sweep (beside the main line, "

@@ -1343,7 +1343,7 @@ static void record_after_sweep(State& s, double* slot) {
   if (s.ext_pending && s.capturing && s.cap_sweep == 0) {  // the first sweep's side work is external
     if (!s.pack_done) launch_record(s, slot, 1);
     ext_add_record(s);
-  } else if (s.side_fused && (s.side_pending & 1)) {
+  } else if ((s.side_fused || sharded_pack_split(s)) && (s.side_pending & 1)) {
     if (!s.pack_done) launch_record(s, slot, 1);  // else updateZ's slab-sum launch packed it
     launch_record(s, slot, 2);
   } else {

@@ -409,6 +409,10 @@ void launch_gamma2(State& s, uint32_t iter);
 bool gamma2_bl_fusion_ok(const State& s);
 void launch_gamma2_bl(State& s, uint32_t iter);  // updateGamma2 + updateBetaLambda in one launch
 int live_chains_on(int device);                  // chains created and not destroyed on a device (capi.cpp)
+// a species-sharded chain on RCCL: a recorded graph sweep packs its main-stream quantities in
+// updateZ's slab launch and the side chain's (Gamma, iV, Delta) on the side stream after it,
+// so no pack launch waits behind all-reduce A on the main stream (capi.cpp record_after_sweep)
+inline bool sharded_pack_split(const State& s) { return s.sharded && s.comm != nullptr && !s.single_stream; }
 void launch_lambda_priors(State& s, uint32_t iter, hipStream_t st);
 void launch_eta(State& s, uint32_t iter);
 void launch_inv_sigma(State& s, uint32_t iter);

@@ -161,7 +161,7 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   // XZ and ZTr from their partials, one launch
   const int64_t nXZ = (int64_t)s.K * s.nsl, nZT = s.has_na ? (int64_t)s.ny * s.nt : 0;
   const SideGate gate = draw ? side_gate_next(s, iter) : SideGate{};
-  if (draw && s.pack_req && s.side_fused && s.capturing) {
+  if (draw && s.pack_req && (s.side_fused || sharded_pack_split(s)) && s.capturing) {
     launch_slab_sum2_pack(s, s.XZ_part, s.XZ, nXZ, nchunk, s.ZTr_part, s.ZTr, nZT, s.ntile_j, gate);
     s.pack_req = false;
     s.pack_done = true;
