@@ -304,6 +304,11 @@ void ar_point(State& s, double* buf, size_t n) {
     s.ar_doubles += n;
   }
   if (s.comm) {
+    // one rank: the in-place sum is the identity.  RCCL's one-rank path still issued a copy on
+    // the copy engine the record ring's D2H copies use, so the first sweep of each replay
+    // waited behind the previous replay's record copy (~130 us per replay boundary in the r06
+    // traces); it is not issued (still counted: the sweep's all-reduce points are unchanged)
+    if (s.nranks == 1) return;
     const ncclResult_t r = ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, (ncclComm_t)s.comm, s.stream);
     HMSC_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
     return;
