@@ -25,12 +25,14 @@
 namespace hmsc {
 
 // Per-thread arrays over the level's factors (tv, x1) are sized by a compile-time capacity:
-// the launcher picks the 16-factor instantiation while nf <= 16 (registers) and the 64-factor
-// one above it (K = nc + sum nf <= 64 bounds nf), so the updater follows the nf in use --
-// R's default nfMax = ns (R/Hmsc.R:554, truncated to the allocation) adapts upward from
-// nfMin = 2 (R/updateNf.R) -- instead of refusing a large nfMax at chain creation.
+// the launcher picks the 16-factor instantiation while nf <= 16 (registers), the 64-factor one
+// up to 64 and the 128-factor one above it (K = nc + sum nf <= 128 bounds nf; its arrays live
+// in scratch memory, slower but with no factor limit below the chain's), so the updater follows
+// the nf in use -- R's default nfMax = ns (R/Hmsc.R:554, truncated to the allocation) adapts
+// upward from nfMin = 2 (R/updateNf.R) -- instead of refusing a large nfMax at chain creation.
 constexpr int GE_NF_SMALL = 16;
 constexpr int GE_NF_LARGE = 64;
+constexpr int GE_NF_XL = HMSC_KCAP;
 
 struct GEArgs {
   int ny, ns, nc, nt, K, r, nr, nf, np, loff;
@@ -765,8 +767,7 @@ __global__ __launch_bounds__(256) void ge_b_eta_kernel(GEArgs a) {
     }
     for (int h = 0; h < nf; ++h)
       for (int o = 32; o > 0; o >>= 1) tv[h] += __shfl_xor(tv[h], o);
-    const int h = lane;
-    if (h < nf) {
+    for (int h = lane; h < nf; h += 64) {  // (nf > 64: two factors a lane)
       double me = 0.0, nz = 0.0;
       if (P.obs) {
         for (int h2 = 0; h2 < nf; ++h2) me = fma(tv[h2], P.iW0[h2 + nf * h], me);
@@ -819,8 +820,10 @@ static void launch_gamma_eta_blocked(State& s, const GEArgs& a, hipStream_t st) 
   dense_lauum_lower(st, T, N, N, M, N);
   if (a.nf <= GE_NF_SMALL)
     ge_b_m_kernel<GE_NF_SMALL><<<ge_blocks(NN), 256, 0, st>>>(a);
-  else
+  else if (a.nf <= GE_NF_LARGE)
     ge_b_m_kernel<GE_NF_LARGE><<<ge_blocks(NN), 256, 0, st>>>(a);
+  else
+    ge_b_m_kernel<GE_NF_XL><<<ge_blocks(NN), 256, 0, st>>>(a);
   // RM = chol(M); v = M^-1 (mb10 - mb20)
   dense_potrf_lower(st, M, N, N, ws2, a.fail, 0, s.trsv_sync);
   dense_trsv_lower(st, M, N, N, v, 0, ws2, 0, s.trsv_sync);
@@ -832,8 +835,10 @@ static void launch_gamma_eta_blocked(State& s, const GEArgs& a, hipStream_t st) 
   const int eta_grid = ge_blocks(64 * (size_t)(obs ? a.ny : a.np));
   if (a.nf <= GE_NF_SMALL)
     ge_b_eta_kernel<GE_NF_SMALL><<<eta_grid, 256, 0, st>>>(a);
-  else
+  else if (a.nf <= GE_NF_LARGE)
     ge_b_eta_kernel<GE_NF_LARGE><<<eta_grid, 256, 0, st>>>(a);
+  else
+    ge_b_eta_kernel<GE_NF_XL><<<eta_grid, 256, 0, st>>>(a);
   HIP_OK(hipGetLastError());
 }
 
@@ -1213,7 +1218,7 @@ void launch_gamma_eta(State& s, uint32_t iter) {
     a.nf = s.lev[r].nf;
     a.np = s.lev[r].np;
     a.loff = s.loff(r);
-    HMSC_REQUIRE(a.nf <= GE_NF_LARGE, "updateGammaEta: a level's nf must be <= 64 in this build");
+    HMSC_REQUIRE(a.nf <= GE_NF_XL, "updateGammaEta: a level's nf must be <= 128 in this build");
     for (int q = 0; q < s.nr; ++q) {
       a.lev_np[q] = s.lev[q].np;
       a.lev_nf[q] = s.lev[q].nf;
@@ -1253,8 +1258,10 @@ void launch_gamma_eta(State& s, uint32_t iter) {
     } else {
       if (a.nf <= GE_NF_SMALL)
         gamma_eta_kernel<GE_NF_SMALL><<<1, 1024, 0, s.stream>>>(a);
-      else
+      else if (a.nf <= GE_NF_LARGE)
         gamma_eta_kernel<GE_NF_LARGE><<<1, 1024, 0, s.stream>>>(a);
+      else
+        gamma_eta_kernel<GE_NF_XL><<<1, 1024, 0, s.stream>>>(a);
     }
     HIP_OK(hipGetLastError());
   }

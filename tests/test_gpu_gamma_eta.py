@@ -28,6 +28,9 @@ MODELS = {
     "blocked_grouped": dict(ny=90, ns=180, nc=3, nf=2, units=[15], seed=47),
     # config 3 (vignette_3: nc = 4, two traits + intercept, phylogeny) at 300 species
     "blocked_cfg3": dict(ny=200, ns=300, nc=4, nt=3, nf=5, seed=48, phylo=True),
+    # nf > 64: the 128-factor instantiations, one workgroup and blocked
+    "wide_nf80": dict(ny=60, ns=10, nc=3, nf=80, seed=49),
+    "wide_nf72_blocked": dict(ny=80, ns=200, nc=3, nf=72, units=[20], seed=50),
 }
 
 
