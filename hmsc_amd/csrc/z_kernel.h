@@ -183,8 +183,19 @@ struct ZPair {
 #endif
 constexpr int ZT_E_LD = 10, ZT_Q_LD = ZT_Q_LD_DEF;
 constexpr int ZT_E_SEG = ZT_E_MAX * ZT_E_PER_UNIT, ZT_Q_SEG = ZT_Q_MAX * ZT_Q_PER_UNIT;
+// The exp and log tables are read at data-dependent rows by every lane.  ZT_COMPACT (round 6):
+// 32-entry tables of 8-byte words, each 64 dwords -- one LDS bank row, so a ds_read_b64 half-wave
+// (banks (a/4) mod 64) never meets two rows on one bank -- instead of the 64-entry 2^(k/64)
+// table (rows k and k + 32 shared banks: 2-way) and the 64 x 16-byte log rows read by
+// ds_read_b128 (rows j, j + 16, j + 32, j + 48 on one bank quad: up to 4-way among 16 lanes).
+// The exp polynomial goes one degree up (|r| <= ln2 / 64) and the log1p series two (|r| <= 1 / 65).
+#ifndef ZT_COMPACT
+#define ZT_COMPACT 1
+#endif
+constexpr int ZT_X_N = ZT_COMPACT ? 32 : 64;
 constexpr int ZT_OFF_E = 0, ZT_OFF_Q = ZT_E_SEG * ZT_E_LD, ZT_OFF_X = ZT_OFF_Q + ZT_Q_SEG * ZT_Q_LD;
-constexpr int ZT_DOUBLES = ZT_OFF_X + 64;
+constexpr int ZT_OFF_LI = ZT_OFF_X + ZT_X_N, ZT_OFF_LL = ZT_OFF_LI + 32;  // (ZT_COMPACT) 1 / c_j, log c_j
+constexpr int ZT_DOUBLES = ZT_OFF_LL + 32;
 static_assert(ZT_E_NC % 2 == 0 && ZT_Q_NC % 2 == 0 && ZT_E_LD % 2 == 0 && ZT_Q_LD % 2 == 0 && ZT_E_LD >= ZT_E_NC &&
                   ZT_Q_LD >= ZT_Q_NC,
               "16-byte rows");
@@ -194,7 +205,12 @@ inline void z_draw_tables(double* t) {
     for (int k = 0; k < ZT_E_NC; ++k) t[ZT_OFF_E + ZT_E_LD * j + k] = kZtErfcx[ZT_E_NC * j + k];
   for (int j = 0; j < ZT_Q_SEG; ++j)
     for (int k = 0; k < ZT_Q_NC; ++k) t[ZT_OFF_Q + ZT_Q_LD * j + k] = kZtQnormF[ZT_Q_NC * j + k];
-  for (int i = 0; i < 64; ++i) t[ZT_OFF_X + i] = kZtExp2[i];
+  for (int i = 0; i < ZT_X_N; ++i) t[ZT_OFF_X + i] = kZtExp2[(64 / ZT_X_N) * i];  // 2^(i / ZT_X_N)
+  for (int j = 0; j < 32; ++j) {  // log table on 32 intervals of [1, 2): c_j = 1 + j / 32 + 1 / 64
+    const long double c = 1.0L + (2 * j + 1) / 64.0L;
+    t[ZT_OFF_LI + j] = (double)(1.0L / c);
+    t[ZT_OFF_LL + j] = (double)logl(c);
+  }
 }
 typedef double zt_d2 __attribute__((ext_vector_type(2)));
 
@@ -216,13 +232,44 @@ __device__ __forceinline__ double zt_poly(const double* row, double d) {
 }
 
 HMSC_TABLE double kZtExpPoly[6] = {1.0 / 120.0, 1.0 / 24.0, 1.0 / 6.0, 0.5, 1.0, 1.0};
+HMSC_TABLE double kZtExpPoly7[7] = {1.0 / 720.0, 1.0 / 120.0, 1.0 / 24.0, 1.0 / 6.0, 0.5, 1.0, 1.0};
+HMSC_TABLE double kLog1pSeries7[7] = {1.0 / 7.0, -1.0 / 6.0, 1.0 / 5.0, -1.0 / 4.0, 1.0 / 3.0, -1.0 / 2.0, 1.0};
+// log x for positive normal x (log_tab on the compact tables): m2 in [1, 2) on 32 intervals,
+// |r| <= 1 / 65, log1p(r) by its degree-7 series (|r^8 / 8| < 4e-16 absolute)
+__device__ __forceinline__ double log_tab32(double x, const double* zt) {
+  const int e = __builtin_amdgcn_frexp_exp(x) - 1;
+  const double m2 = 2.0 * __builtin_amdgcn_frexp_mant(x);
+  uint64_t b;
+  __builtin_memcpy(&b, &m2, 8);
+  const uint32_t hi = (uint32_t)(b >> 32);
+  const int j = (int)((hi >> 15) & 31u);
+  const uint64_t cb = (uint64_t)((hi & 0xFFFF8000u) | 0x4000u) << 32;  // c_j = 1 + j / 32 + 1 / 64
+  double c;
+  __builtin_memcpy(&c, &cb, 8);
+  const double r = (m2 - c) * zt[ZT_OFF_LI + j];
+  double P = kLog1pSeries7[0];
+#pragma unroll
+  for (int k = 1; k < 7; ++k) P = fma_sc(P, r, kLog1pSeries7[k]);
+  const double de = (double)e;
+  return fma(de, 0.6931471803691238, zt[ZT_OFF_LL + j]) + fma(r, P, de * 1.9082149292705877e-10);
+}
 // erfc(a) for 0 <= a < ZT_E_MAX (the caller clamps a)
 __device__ __forceinline__ double zt_erfc(double a, const double* zt) {
   const int j = min((int)(a * (double)ZT_E_PER_UNIT), ZT_E_SEG - 1);
   const double d = a - ((double)j + 0.5) * (1.0 / ZT_E_PER_UNIT);
   const double cx = zt_poly<ZT_E_NC>(zt + ZT_OFF_E + ZT_E_LD * j, d);
-  // exp(-(hi + lo)), a^2 = hi + lo exactly: k = rint(-hi 64 / ln2), r = -hi - k ln2 / 64 - lo
+  // exp(-(hi + lo)), a^2 = hi + lo exactly: k = rint(-hi N / ln2), r = -hi - k ln2 / N - lo
   const double hi = a * a, lo = fma(a, a, -hi);
+#if ZT_COMPACT
+  const double kf = __builtin_rint(hi * -46.16624130844683);  // 32 / ln2
+  double r = fma(kf, -0.02166084938653512, -hi);              // ln2 / 32 = hi (fdlibm's ln2_hi / 32: k hi exact)
+  r = fma(kf, -5.9631716539705866e-12, r) - lo;               //            + lo
+  double p = kZtExpPoly7[0];
+#pragma unroll
+  for (int k = 1; k < 7; ++k) p = fma_sc(p, r, kZtExpPoly7[k]);
+  const int ki = (int)kf;
+  return __builtin_ldexp(p * zt[ZT_OFF_X + (ki & 31)], ki >> 5) * cx;
+#else
   const double kf = __builtin_rint(hi * -92.33248261689366);  // 64 / ln2
   double r = fma(kf, -0.01083042469326756, -hi);              // ln2 / 64 = hi (fdlibm's ln2_hi / 64: k hi exact)
   r = fma(kf, -2.9815858269852933e-12, r) - lo;               //            + lo
@@ -231,6 +278,7 @@ __device__ __forceinline__ double zt_erfc(double a, const double* zt) {
   for (int k = 1; k < 6; ++k) p = fma_sc(p, r, kZtExpPoly[k]);
   const int ki = (int)kf;
   return __builtin_ldexp(p * zt[ZT_OFF_X + (ki & 63)], ki >> 6) * cx;
+#endif
 }
 
 // (2p - 1) F(w) = Phi^-1(p) for w = -log(4 p (1 - p)) < ZT_Q_MAX
@@ -257,7 +305,11 @@ __device__ __forceinline__ ZPair z_probit_pair_tab(double e0, double e1, double 
     const double r0 = 0.5 * zt_erfc(a0, zt), r1 = 0.5 * zt_erfc(a1, zt);
     const double p0 = u0 * (al0 < 0.0 ? 1.0 - r0 : r0);
     const double p1 = u1 * (al1 < 0.0 ? 1.0 - r1 : r1);
+#if ZT_COMPACT
+    const double w0 = -log_tab32(4.0 * p0 * (1.0 - p0), zt), w1 = -log_tab32(4.0 * p1 * (1.0 - p1), zt);
+#else
     const double w0 = -log_tab(4.0 * p0 * (1.0 - p0), ltab), w1 = -log_tab(4.0 * p1 * (1.0 - p1), ltab);
+#endif
     q0 = zt_qnorm_w(p0, w0, zt);
     q1 = zt_qnorm_w(p1, w1, zt);
     if (w0 >= (double)ZT_Q_MAX || w1 >= (double)ZT_Q_MAX) {  // p < 2.8e-8 or > 1 - 2.8e-8: AS241's tail
