@@ -474,11 +474,15 @@ def sharded_leg(hM, args, rank, world, local, dist, steps=200, warmup=40):
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
-    ch.run(transient=0, samples=steps, thin=1, adaptNf=[0], iter0=it, record=True)
+    # (the record is kept past the timed region, as the main line's is: dropping ~0.2 GB of
+    # arrays inside it unmapped their pages within the bracket -- ~60 us a sweep at 200 steps,
+    # scripts/sharded_diag.py)
+    rec = ch.run(transient=0, samples=steps, thin=1, adaptNf=[0], iter0=it, record=True)
     ch.sync()
     if dist is not None:
         dist.barrier()
     t = time.perf_counter() - t0
+    del rec
     if dist is not None:
         tt = torch.tensor([t], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)

@@ -382,15 +382,15 @@ static void setup_phylo(State& s, const hmsc_model* m) {
 }
 
 // ---------------------------- create ----------------------------
-// Species shard of `rank`: whole species pairs (updateZ draws species 2m, 2m+1 from one Philox
-// block), the ceil(ns / 2) pairs spread as evenly as possible over the ranks: rank r owns pairs
-// [floor(r P / n), floor((r + 1) P / n)).  Every rank gets a pair when P >= n; returns -1 if
-// this rank's shard is empty.
+// Species shard of `rank`: whole species quads (updateZ draws species 4q .. 4q + 3 from one
+// Philox block), the ceil(ns / 4) quads spread as evenly as possible over the ranks: rank r owns
+// quads [floor(r Q / n), floor((r + 1) Q / n)).  Every rank gets a quad when Q >= n; returns -1
+// if this rank's shard is empty.
 static int shard_range(int ns, int rank, int nranks, int* sp0, int* nsl) {
-  const long pairs = (ns + 1) / 2;
-  const long p0 = pairs * rank / nranks, p1 = pairs * (rank + 1) / nranks;
-  *sp0 = (int)std::min<long>(ns, 2 * p0);
-  *nsl = (int)std::min<long>(ns, 2 * p1) - *sp0;
+  const long quads = (ns + 3) / 4;
+  const long q0 = quads * rank / nranks, q1 = quads * (rank + 1) / nranks;
+  *sp0 = (int)std::min<long>(ns, 4 * q0);
+  *nsl = (int)std::min<long>(ns, 4 * q1) - *sp0;
   return *nsl > 0 ? 0 : -1;
 }
 
@@ -812,7 +812,7 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
     s.gvt_ld = nc * nc + N + nfm;             // [A nc^2 | BTr nc nt | rs NF]
     s.gvt = dalloc<double>((nbl + ngr) * (size_t)s.gvt_ld);
   }
-  s.side_sync = dalloc<int>(2 + HMSC_MAX_LEVELS);
+  s.side_sync = dalloc<int>(SIDE_SYNC_INTS);
   s.Gamma_side = dalloc<double>(N);
   // under rocprofv3 (ROCPROF_OUTPUT_PATH, as for the graph node cap) the side chain keeps its
   // graph edges: counter passes serialise dispatches, and a device-side join would wait on a
@@ -823,9 +823,13 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   if (const char* e = std::getenv("HMSC_SIDE_PARTIALS")) s.side_partials = e[0] == '1';
   if (const char* e = std::getenv("HMSC_LONG_TAIL")) s.long_tail = e[0] == '1';
   if (const char* e = std::getenv("HMSC_FIRST_REPLAY")) s.first_replay = std::max(0, atoi(e));
-  s.scratch_doubles = 1 << 20;
+  // (GammaV's final stage and Gamma2's prep / final stage keep their N = nc nt systems here when
+  // they do not fit a workgroup's LDS: 3 N^2 + 7 nc^2 doubles and the final stage's arrays)
+  s.scratch_doubles = std::max<size_t>(1 << 20, 6 * (size_t)nc * nc + 2 * (size_t)N + (size_t)N * N);
   s.scratch = dalloc<double>(s.scratch_doubles);
-  s.scratch2 = dalloc<double>(s.scratch_doubles);
+  s.scratch2_doubles = std::max<size_t>(1 << 20, 7 * (size_t)nc * nc + 3 * (size_t)N * N + 16 + 8 * (size_t)N +
+                                                     (size_t)nfm * nt + 2 * 1024 + 8 * 64 + 16);
+  s.scratch2 = dalloc<double>(s.scratch2_doubles);
   s.psi_rs = dalloc<double>((size_t)64 * nfm);
   // (the species-block partials of GammaV (32 species a block) and Gamma2 (G2SB = 8))
   s.ABpart = dalloc<double>((size_t)((nsl + 7) / 8) * (nc * nc + 2 * N + nfm * nt + 8));
@@ -1419,7 +1423,10 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
   try {
     const char* no_root = std::getenv("HMSC_NO_SIDE_ROOT");
     s.edge_free_now = s.edge_free && live_chains(s.device) == 1;
-    if (s.side_fused && s.edge_free_now && !s.sharded && !(no_root && no_root[0] == '1')) {
+    // (a sharded RCCL chain: sweep_sharded's edge-free sweeps fork and join on the device too)
+    const bool shard_root = s.sharded && s.comm != nullptr && !s.single_stream && sharded_fused_ok(s) &&
+                            !getenv_flag("HMSC_NO_SHARD_DEV");
+    if (((s.side_fused && !s.sharded) || shard_root) && s.edge_free_now && !(no_root && no_root[0] == '1')) {
       // the side stream forked at the graph's root: the first sweep's side work then waits for
       // the fused launch's tails flag on the device like the later sweeps', instead of behind a
       // graph edge from that launch (whose first replay sweep's side chain ended ~100 us late)
@@ -1889,7 +1896,7 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
   join_side(s);
   static_assert(2 + HMSC_MAX_LEVELS <= 56, "run_start_kernel: side flags");
   run_start_kernel<<<1, 64, 0, s.stream>>>(recording ? s.d_rec_desc : nullptr, iter0, transient, thin, samples,
-                                           s.gbl_sync, s.crw_flag, s.side_sync, 2 + HMSC_MAX_LEVELS);
+                                           s.gbl_sync, s.crw_flag, s.side_sync, SIDE_SYNC_INTS);
   HIP_OK(hipGetLastError());
   const auto t_start = std::chrono::steady_clock::now();
   int n_replays = 0;
@@ -2038,7 +2045,7 @@ int hmsc_shard_range(int32_t ns, int32_t rank, int32_t nranks, int32_t* sp0, int
   return guarded([&] {
     HMSC_REQUIRE(ns > 0 && nranks >= 1 && rank >= 0 && rank < nranks, "bad ns / rank / nranks");
     int a = 0, b = 0;
-    HMSC_REQUIRE(shard_range(ns, rank, nranks, &a, &b) == 0, "species shard is empty: fewer than 2 species per rank");
+    HMSC_REQUIRE(shard_range(ns, rank, nranks, &a, &b) == 0, "species shard is empty: fewer than 4 species per rank");
     *sp0 = a;
     *nsl = b;
   });

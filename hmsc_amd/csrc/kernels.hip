@@ -1160,6 +1160,7 @@ void launch_gamma_v(State& s, uint32_t iter, hipStream_t st) {
   const size_t need = (6 * (size_t)s.nc * s.nc + (size_t)s.nc * s.nt + (size_t)s.nc * s.nt * s.nc * s.nt +
                        (size_t)s.nc * s.nt) * sizeof(double);
   a.use_lds = need <= 64 * 1024;
+  HMSC_REQUIRE(a.use_lds || need <= s.scratch_doubles * sizeof(double), "internal: GammaV scratch too small");
   gammav_final_kernel<<<1, 64, a.use_lds ? need : 0, st>>>(a);
   HIP_OK(hipGetLastError());
   if (s.mask & HMSC_UP_GAMMA2) launch_gamma2_prep(s, st);  // Gamma2's iV-only algebra for the next sweep
@@ -1356,6 +1357,11 @@ struct G2Args {
   uint32_t iter;
   const uint32_t* iter_dev;  // graph replay: the sweep counter is read from the device
   int noise_zero;
+  // the final stage's working arrays (G2FLds): lay_dyn == 0 is the fixed layout below (the fused
+  // launches, N + NF nt <= 64); otherwise offsets sized for this nc, nt, NF (g2f_layout), in LDS
+  // or, when they do not fit a workgroup's LDS, at gbase in global memory
+  int lay_ltr, lay_v1, lay_v2, lay_xi, lay_red, lay_sgl, lay_dyn;
+  double* gbase;
 };
 
 // for (p = threadIdx.x; p < n; p += blockDim.x) store(p, load(p)) with U loads of a thread in
@@ -1373,15 +1379,25 @@ __device__ __forceinline__ void batched_for(int n, Load load, Store store) {
   }
 }
 
-// LDS of the final stage (doubles), before the staged B1 | LS (n2 + N^2 more when a.stage)
+// LDS of the final stage (doubles) in the fixed layout, before the staged B1 | LS (n2 + N^2 more
+// when a.stage)
 constexpr int G2F_LDS = 512 + 512 + 3 * 256 + 8 * 64 + 2048;
 
 struct G2FLds {
   double *S0, *LTr, *v1, *v2, *xi, *sGL, *dyn;
   double (*red)[64];
-  __device__ explicit G2FLds(double* lds)
-      : S0(lds), LTr(lds + 512), v1(lds + 1024), v2(lds + 1280), xi(lds + 1536), sGL(lds + 1792 + 8 * 64),
-        dyn(lds + 1792 + 8 * 64 + 2048), red((double (*)[64])(lds + 1792)) {}
+  __device__ G2FLds(double* lds, const G2Args& a) {
+    if (a.gbase) lds = a.gbase;
+    const bool fixed = a.lay_dyn == 0;
+    S0 = lds;
+    LTr = lds + (fixed ? 512 : a.lay_ltr);
+    v1 = lds + (fixed ? 1024 : a.lay_v1);
+    v2 = lds + (fixed ? 1280 : a.lay_v2);
+    xi = lds + (fixed ? 1536 : a.lay_xi);
+    red = (double (*)[64])(lds + (fixed ? 1792 : a.lay_red));
+    sGL = lds + (fixed ? 1792 + 8 * 64 : a.lay_sgl);
+    dyn = lds + (fixed ? 1792 + 8 * 64 + 2048 : a.lay_dyn);
+  }
 };
 
 // The final stage in two phases.  gamma2_final_pre: what no flag guards -- iSigma's all-ones
@@ -1390,7 +1406,7 @@ struct G2FLds {
 // all-ones test (the caller's barrier ANDs them).  Everything is staged into LDS by all 256
 // threads (coalesced, every load of a thread issued before its first use).
 __device__ __forceinline__ int gamma2_final_pre(const G2Args& a, double* lds) {
-  const G2FLds L(lds);
+  const G2FLds L(lds, a);
   const int nc = a.nc, N = nc * a.nt, t = threadIdx.x;
   int ok = 1;
   if (a.check_isigma)
@@ -1408,7 +1424,7 @@ __device__ __forceinline__ int gamma2_final_pre(const G2Args& a, double* lds) {
 // gamma2_final_main: after the barrier that follows the pre phase (and the flags): the prep
 // matrices and the species-block partials (their loads issued together), then the products.
 __device__ __forceinline__ void gamma2_final_main(const G2Args& a, double* lds) {
-  const G2FLds L(lds);
+  const G2FLds L(lds, a);
   HMSC_STAMP(30);
   const int nc = a.nc, nt = a.nt, N = nc * nt, t = threadIdx.x, n2 = nc * nc;
   const int n1 = nc * nt, nL = a.NF * nt, P = n1 + nL;
@@ -2065,6 +2081,12 @@ __global__ __launch_bounds__(256, 2) void gamma2_bl_kernel(G2BLArgs f) {
   if (f.crw_on) bl_tail(f.tail, col, b, nbl, iter, smem);
 }
 
+// doubles of gamma2_prep_kernel's working set (in s.scratch2 when past 64 KB)
+static size_t g2_prep_doubles(const State& s) {
+  const size_t N = (size_t)s.nc * s.nt;
+  return 7 * (size_t)s.nc * s.nc + 3 * N * N;
+}
+
 static void launch_gamma2_prep(State& s, hipStream_t st) {
   G2PrepArgs a{};
   a.nc = s.nc;
@@ -2076,17 +2098,50 @@ static void launch_gamma2_prep(State& s, hipStream_t st) {
   a.prep = s.g2prep;
   a.scratch = s.scratch2;
   a.fail = s.dev_flags + 1;
-  const size_t N = (size_t)s.nc * s.nt;
-  const size_t need = (7 * (size_t)s.nc * s.nc + 3 * N * N) * sizeof(double);
+  const size_t need = g2_prep_doubles(s) * sizeof(double);
   a.use_lds = need <= 64 * 1024;
+  HMSC_REQUIRE(a.use_lds || g2_prep_doubles(s) <= s.scratch2_doubles, "internal: Gamma2 prep scratch too small");
   gamma2_prep_kernel<<<1, 256, a.use_lds ? need : 0, st>>>(a);
   HIP_OK(hipGetLastError());
   s.g2prep_valid = true;
 }
 
+constexpr size_t G2F_LDS_CAP = 64 * 1024;  // bytes of LDS the unfused final stage takes at most
+
+// the unfused final stage's layout for this chain's nc, nt, NF (G2FLds): S0 | LTr | v1 | v2 | xi |
+// red | sGL | B1 LS; staged B1 | LS when everything fits 64 KB, in LDS without them when the rest
+// does, else every array in global memory after the prep's working set (s.scratch2).  Returns
+// the launch's dynamic LDS bytes.
+static size_t g2f_layout(const State& s, G2Args& a) {
+  const int N = s.nc * s.nt, nL = s.NF * s.nt, ngl = s.nc * s.NF <= 2048 ? s.nc * s.NF : 0;
+  auto up2 = [](int v) { return (v + 1) & ~1; };  // 16-byte aligned arrays
+  int o = up2(N);
+  a.lay_ltr = o;
+  o += up2(nL);
+  a.lay_v1 = o;
+  o += up2(N);
+  a.lay_v2 = o;
+  o += up2(N);
+  a.lay_xi = o;
+  o += up2(N);
+  a.lay_red = o;
+  o += 8 * 64;
+  a.lay_sgl = o;
+  o += up2(ngl);
+  a.lay_dyn = o;
+  const size_t core = (size_t)o * sizeof(double);
+  const size_t stage_bytes = ((size_t)s.nc * s.nc + (size_t)N * N) * sizeof(double);
+  a.gbase = nullptr;
+  const bool force_global = getenv_flag("HMSC_G2F_GLOBAL");  // (tests: the global-memory layout at small N)
+  a.stage = !force_global && core + stage_bytes <= G2F_LDS_CAP;
+  if (a.stage) return core + stage_bytes;
+  if (!force_global && core <= G2F_LDS_CAP) return core;
+  a.gbase = s.scratch2 + ((g2_prep_doubles(s) + 15) & ~(size_t)15);
+  HMSC_REQUIRE((size_t)(a.gbase - s.scratch2) + o <= s.scratch2_doubles, "internal: Gamma2 scratch too small");
+  return 0;
+}
+
 void launch_gamma2(State& s, uint32_t iter) {
-  HMSC_REQUIRE((size_t)s.nc * s.nt <= 256 && s.NF * s.nt + s.nc * s.nt <= 1024,
-               "updateGamma2: nc*nt must be <= 256 in this build");
   if (!s.xeta_valid) launch_xeta(s);
   flush_g(s);
   if (!s.zt_valid) launch_zt_refresh(s);
@@ -2125,10 +2180,9 @@ void launch_gamma2(State& s, uint32_t iter) {
   a.iter = iter;
   a.iter_dev = s.capturing ? s.d_iter : nullptr;
   a.noise_zero = s.noise_mode;
-  const size_t N = (size_t)s.nc * s.nt, stage_bytes = ((size_t)s.nc * s.nc + N * N) * sizeof(double);
-  a.stage = stage_bytes <= 28 * 1024;  // + 35 KB of the final stage's own: within 64 KB per workgroup
+  const size_t lds = g2f_layout(s, a);
   join_side(s);  // iV and the prep matrices come from the previous sweep's GammaV (side stream)
-  gamma2_final_kernel<<<1, 256, G2F_LDS * sizeof(double) + (a.stage ? stage_bytes : 0), s.stream>>>(a);
+  gamma2_final_kernel<<<1, 256, lds, s.stream>>>(a);
   HIP_OK(hipGetLastError());
 }
 
@@ -2228,7 +2282,7 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
   const bool tail_gv = sh || (!s.side_partials && crw_on && (s.mask & HMSC_UP_GAMMA2) && s.nt <= 8 &&
                               s.nc * s.nc + s.nc * s.nt + s.NF <= 1024 && s.gvt != nullptr);
   // graph sweeps after the first: the previous sweep's side chain is joined on the device
-  const bool dev_join = !sh && crw_on && s.edge_free_now && s.capturing && s.cap_sweep > 0 && s.side_tail;
+  const bool dev_join = (!sh || s.shard_dev) && crw_on && s.edge_free_now && s.capturing && s.cap_sweep > 0 && s.side_tail;
   // iV, Gamma2's prep, Psi and Delta come from the previous sweep's side updaters
   if (!dev_join) join_side(s);
   // ... and when the slab launch after the last updateZ has waited for them (SideGate), this
@@ -3061,6 +3115,9 @@ struct EtaFArgs {
   BLTailArgs tail;
   int nred, nbl;
   int* err;
+  // EF_SOLVE of an edge-free sharded sweep graph: raised (this sweep's epoch) at the launch's
+  // start, i.e. after all-reduce B, for the side chain that reads ar_b (sweep_sharded)
+  int* arb_flag;
 };
 
 constexpr int EF_SITES = 16;
@@ -3124,6 +3181,8 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
   const int i0 = tile * EF_SITES;
   if (tile == 0) HMSC_STAMP(50);
   const uint32_t iter = SWEEP_ITER(a);       // read once, ahead of the stream
+  if (MODE == EF_SOLVE && a.arb_flag && tile == 0 && t == 0)  // all-reduce B is in (stream order)
+    __hip_atomic_store(a.arb_flag, g2bl_epoch(iter), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   if (MODE != EF_STREAM && t < EF_SITES) sPi[t] = i0 + t < ny ? a.Pi[i0 + t] : 0;
   // ---- stage 1: ZL = Z (Lambda diag(iSigma))^T on the matrix cores, the HBM stream of the
   // launch, issued first: species j = 16 s + 4 w + lk, B = LS[j][lm] straight from L2 (128 KB,
@@ -4238,8 +4297,6 @@ __global__ __launch_bounds__(256) void g2_stats_kernel(G2SArgs a) {
 
 static void shard_g2_stats(State& s) {
   if (!(s.mask & HMSC_UP_GAMMA2)) return;
-  HMSC_REQUIRE((size_t)s.nc * s.nt <= 256 && s.NF * s.nt + s.nc * s.nt <= 1024,
-               "updateGamma2: nc*nt must be <= 256 in this build");
   if (!s.xeta_valid) launch_xeta(s);
   if (!s.zt_valid) launch_zt_refresh(s);  // XZ (and ZTr) of the current Z and Eta
   const int n1 = s.nc * s.nt, n12 = n1 + s.NF * s.nt;
@@ -4272,8 +4329,6 @@ static void shard_g2_stats(State& s) {
 
 // updateGamma2 of a sharded chain on the general path: the final stage on the all-reduced sums
 static void launch_gamma2_sharded(State& s, uint32_t iter) {
-  HMSC_REQUIRE((size_t)s.nc * s.nt <= 256 && s.NF * s.nt + s.nc * s.nt <= 1024,
-               "updateGamma2: nc*nt must be <= 256 in this build");
   if (!s.g2s_valid) shard_g2_stats(s);
   if (!s.xeta_valid) launch_xeta(s);
   flush_g(s);  // the final stage reads G's X^T Eta block
@@ -4302,10 +4357,9 @@ static void launch_gamma2_sharded(State& s, uint32_t iter) {
   a.iter = iter;
   a.iter_dev = s.capturing ? s.d_iter : nullptr;
   a.noise_zero = s.noise_mode;
-  const size_t N = (size_t)s.nc * s.nt, stage_bytes = ((size_t)s.nc * s.nc + N * N) * sizeof(double);
-  a.stage = stage_bytes <= 28 * 1024;
+  const size_t lds = g2f_layout(s, a);
   join_side(s);  // iV and the prep matrices come from the previous sweep's GammaV (side stream)
-  gamma2_final_kernel<<<1, 256, G2F_LDS * sizeof(double) + (a.stage ? stage_bytes : 0), s.stream>>>(a);
+  gamma2_final_kernel<<<1, 256, lds, s.stream>>>(a);
   HIP_OK(hipGetLastError());
 }
 
@@ -4432,6 +4486,7 @@ static void shard_gammav_final(State& s, uint32_t iter, hipStream_t st) {
   const size_t need = (6 * (size_t)s.nc * s.nc + (size_t)s.nc * s.nt + (size_t)s.nc * s.nt * s.nc * s.nt +
                        (size_t)s.nc * s.nt) * sizeof(double);
   a.use_lds = need <= 64 * 1024;
+  HMSC_REQUIRE(a.use_lds || need <= s.scratch_doubles * sizeof(double), "internal: GammaV scratch too small");
   gammav_final_kernel<<<1, 64, a.use_lds ? need : 0, st>>>(a);
   HIP_OK(hipGetLastError());
   if (s.mask & HMSC_UP_GAMMA2) launch_gamma2_prep(s, st);
@@ -4452,6 +4507,7 @@ static void shard_eta_solve(State& s, uint32_t iter, bool fused) {
     a.CR = s.ar_b + L.cr;
     a.ldcr = L.ldcr;
     a.kt = nullptr;  // (the live Eta timer times the stream)
+    a.arb_flag = s.shard_dev ? arb_flag_ptr(s) : nullptr;
     launch_eta_fused_mode<EF_SOLVE>(s, a);
     return;
   }
@@ -4467,7 +4523,13 @@ void sweep_sharded(State& s, uint32_t iter) {
   HMSC_REQUIRE(!(s.mask & HMSC_UP_GAMMAETA), "updateGammaEta cannot run on a species-sharded chain");
   const bool fused = sharded_fused_ok(s);
   s.side_fused = false;
-  join_side(s);
+  // edge-free graph sweeps (an RCCL chain alone on its device, the side stream forked at the
+  // capture's root): as on one chain's unsharded sweep, the side chain is neither forked nor
+  // joined by graph edges -- it waits on the device for arb_flag, raised by the Eta solve after
+  // all-reduce B, and the next fused launch waits for its side_sync flags -- so the sweep's main
+  // kernels stay on one queue (each cross-queue edge cost ~10 us per sweep)
+  s.shard_dev = fused && s.comm != nullptr && s.capturing && s.edge_free_now && s.side_root;
+  if (!(s.shard_dev && s.cap_sweep > 0 && s.side_tail)) join_side(s);
   if (s.nr > 0 && !s.xeta_valid) launch_xeta(s);
   if (fused) {
     launch_gamma2_bl(s, iter);  // Gamma2 from ar_a; BetaLambda; the tail's CR, LS, psi, GammaV / psi sums
@@ -4489,7 +4551,28 @@ void sweep_sharded(State& s, uint32_t iter) {
   ar_point(s, s.ar_b, L.n);  // all-reduce B
   // GammaV (+ Gamma2's prep) and the delta chains, beside Eta and updateZ
   const bool side_gv = (s.mask & HMSC_UP_GAMMAV) != 0, side_lp = (s.mask & HMSC_UP_LAMBDAPRIORS) && s.nr > 0;
-  if (side_gv || side_lp) {
+  s.side_tail = false;
+  if (s.shard_dev && (s.mask & HMSC_UP_ETA) && s.nr > 0) {
+    // the main continuation first (the Eta solve raises arb_flag), then the side chain on the
+    // side stream, in the capture since the root fork, behind no edge
+    shard_eta_solve(s, iter, fused);
+    GVWArgs gw = make_gvw_args(s, iter, s.ar_b + L.gv, 1, s.d_iter);
+    LPArgs lp = make_lp_args(s, iter);
+    lp.iter_dev = gw.iter_dev;
+    gw.flags = s.side_sync;  // published for the next fused launch (side_wait)
+    const int* af = arb_flag_ptr(s);
+    switch (wv_bucket_gv(s.nc * s.nt)) {
+      case 8: launch_side_chain<8>(s, gw, lp, s.ar_b + L.rs, 1, s.NF, af); break;
+      case 16: launch_side_chain<16>(s, gw, lp, s.ar_b + L.rs, 1, s.NF, af); break;
+      case 20: launch_side_chain<20>(s, gw, lp, s.ar_b + L.rs, 1, s.NF, af); break;
+      case 24: launch_side_chain<24>(s, gw, lp, s.ar_b + L.rs, 1, s.NF, af); break;
+      default: launch_side_chain<32>(s, gw, lp, s.ar_b + L.rs, 1, s.NF, af); break;
+    }
+    HIP_OK(hipGetLastError());
+    if (gw.do_prep) s.g2prep_valid = true;
+    s.side_tail = true;
+    s.side_pending |= 1;
+  } else if (side_gv || side_lp) {
     HIP_OK(hipEventRecord(s.ev_bl, s.stream));
     HIP_OK(hipStreamWaitEvent(s.side, s.ev_bl, 0));
     if (fused) {
@@ -4511,12 +4594,13 @@ void sweep_sharded(State& s, uint32_t iter) {
     }
     s.side_pending |= 1;
   }
-  if ((s.mask & HMSC_UP_ETA) && s.nr > 0) shard_eta_solve(s, iter, fused);
+  if ((s.mask & HMSC_UP_ETA) && s.nr > 0 && !s.shard_dev) shard_eta_solve(s, iter, fused);
   if (s.mask & HMSC_UP_ALPHA) launch_alpha(s, iter);
   if (s.mask & HMSC_UP_INVSIGMA) launch_inv_sigma(s, iter);
   if (s.mask & HMSC_UP_Z) launch_update_z(s, iter, false);
   s.g2s_valid = false;
   shard_g2_stats(s);  // all-reduce A, for the next sweep's updateGamma2
+  s.shard_dev = false;
 }
 
 // hmsc_update(which) on a sharded chain: the updater with its own all-reduce (the sweep merges

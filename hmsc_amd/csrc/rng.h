@@ -83,6 +83,10 @@ __host__ __device__ __forceinline__ double u53(uint32_t hi, uint32_t lo) {
   return ((double)(hi >> 5) * 67108864.0 + (double)(lo >> 6) + 0.5) * (1.0 / 9007199254740992.0);
 }
 
+// open-interval uniform from one 32-bit word, (w + 1/2) 2^-32 (exact in double): updateZ's
+// uniforms, one Philox block feeding four cells, at the resolution of R's unif_rand
+__host__ __device__ __forceinline__ double u32o(uint32_t w) { return ((double)w + 0.5) * (1.0 / 4294967296.0); }
+
 struct Uniform2 {
   double a, b;
 };

@@ -144,7 +144,9 @@ struct State {
   // side work waits for the tails flag on the device too (no edge from the fused launch)
   bool side_root = false;
   bool psi_side = true;     // the last sweep's psi draws ran on the side stream (post_bl_kernel), not in the tail
-  int* side_sync = nullptr;      // [GammaV, delta chain per level ..., Gamma2 prep]: epoch of the sweep
+  int* side_sync = nullptr;      // [GammaV, delta chain per level ..., Gamma2 prep, (slot SIDE_ARB_SLOT) the
+                                 // sharded Eta solve's all-reduce-B flag]: epoch of the sweep
+  bool shard_dev = false;        // this sharded sweep joins and forks its side chain on the device (sweep_sharded)
   double* gvt = nullptr;         // the BetaLambda tail's GammaV / psi partial tiles
   int gvt_ld = 0;
   double* Gamma_side = nullptr;  // GammaV's Gamma, for the side stream's record pack
@@ -233,6 +235,7 @@ struct State {
   bool zt_valid = false;         // XZ/G/ZTr computed for the current Z and Eta
   int nchunk = 0, ntile_j = 0, zl_split = 0, NFP = 0;
   size_t scratch_doubles = 0;
+  size_t scratch2_doubles = 0;  // Gamma2's prep working set, then its final stage's arrays past 64 KB
 
   // recording ring
   double* ring = nullptr;
@@ -413,6 +416,10 @@ int live_chains_on(int device);                  // chains created and not destr
 // updateZ's slab launch and the side chain's (Gamma, iV, Delta) on the side stream after it,
 // so no pack launch waits behind all-reduce A on the main stream (capi.cpp record_after_sweep)
 inline bool sharded_pack_split(const State& s) { return s.sharded && s.comm != nullptr && !s.single_stream; }
+// side_sync words: GammaV, the delta chains, Gamma2's prep (1 + nr), then the sharded Eta solve's
+// all-reduce-B flag (sweep_sharded's edge-free sweeps)
+constexpr int SIDE_ARB_SLOT = 2 + HMSC_MAX_LEVELS, SIDE_SYNC_INTS = SIDE_ARB_SLOT + 1;
+inline int* arb_flag_ptr(State& s) { return s.side_sync + SIDE_ARB_SLOT; }
 void launch_lambda_priors(State& s, uint32_t iter, hipStream_t st);
 void launch_eta(State& s, uint32_t iter);
 void launch_inv_sigma(State& s, uint32_t iter);

@@ -20,7 +20,8 @@ namespace hmsc {
 //   E    = XEta BL          v_mfma_f64_16x16x4 (A = XEta rows, B = BL columns); the
 //                           accumulator leaves lane l holding sites lk+4r (r=0..3) of
 //                           species pair m = l&15, i.e. species j0+2m and j0+2m+1
-//   Z    truncated-normal draws (VALU); one Philox call feeds the species pair
+//   Z    truncated-normal draws (VALU); one Philox call feeds a species quad (two of the
+//                           lane's pairs, one 32-bit uniform a cell)
 //   XZ  += XEta^T (Yx o Z)  the drawn Z already sits in the B-operand layout of this
 //                           MFMA (sites = reduction index), A = XEta^T from a wave-
 //                           private LDS copy of the site tile
@@ -189,8 +190,10 @@ constexpr int ZT_E_SEG = ZT_E_MAX * ZT_E_PER_UNIT, ZT_Q_SEG = ZT_Q_MAX * ZT_Q_PE
 // table (rows k and k + 32 shared banks: 2-way) and the 64 x 16-byte log rows read by
 // ds_read_b128 (rows j, j + 16, j + 32, j + 48 on one bank quad: up to 4-way among 16 lanes).
 // The exp polynomial goes one degree up (|r| <= ln2 / 64) and the log1p series two (|r| <= 1 / 65).
+// Measured (profiles/r06_zab.txt): conflicts 34 -> 26 % of LDS-active cycles, but +0.5 M VALU per
+// launch and z 79.2 -> 80.0 us in the full sweep, so off by default.
 #ifndef ZT_COMPACT
-#define ZT_COMPACT 1
+#define ZT_COMPACT 0
 #endif
 constexpr int ZT_X_N = ZT_COMPACT ? 32 : 64;
 constexpr int ZT_OFF_E = 0, ZT_OFF_Q = ZT_E_SEG * ZT_E_LD, ZT_OFF_X = ZT_OFF_Q + ZT_Q_SEG * ZT_Q_LD;
@@ -447,8 +450,11 @@ constexpr int ZT_TLD = 17;  // leading dimension of the wave's 16-site x 32-spec
 // NKB > 4 (64 < K <= 128, one instantiation NKB = 8): the XZ accumulators (128 registers, the
 // matrix cores' accumulation registers) at two waves per SIMD; the E and XZ operands are
 // loaded 64 rows at a time and the waves' XZ combined 64 rows at a time (LDS).
+#ifndef Z_MIN_BLOCKS
+#define Z_MIN_BLOCKS 4  // workgroups per CU the K <= 64 instantiations are compiled for (128 registers)
+#endif
 template <bool DRAW, bool HAS_NA, int NKB, int MODE = Z_ALL, bool POIS = false, bool NORMAL = true>
-__global__ __launch_bounds__(256, NKB > 4 ? 2 : 4) void z_wave_kernel(ZArgs a) {
+__global__ __launch_bounds__(256, NKB > 4 ? 2 : Z_MIN_BLOCKS) void z_wave_kernel(ZArgs a) {
   kernarg_warm<sizeof(ZArgs)>();
   extern __shared__ __attribute__((aligned(16))) double smem[];
   if (a.gred_y0 && blockIdx.y == 0) {  // the co-launched G reduction row
@@ -517,8 +523,8 @@ __global__ __launch_bounds__(256, NKB > 4 ? 2 : 4) void z_wave_kernel(ZArgs a) {
     //      (one 8-byte word per site and species block: 2 bits per species, code + 1)
     uint64_t yw = 0;
     if (DRAW) yw = a.Ybits[(size_t)by * ny + (i0 + lm)];  // padded buffer (ZArgs)
-    // code of species jj = 2 (4 c + lk) + b of this lane's site
-    auto ycode_of = [&](int c, int b) { return (int)((yw >> (16 * c + 4 * lk + 2 * b)) & 3u) - 1; };
+    // code of species jj = 2 m + b of this lane's site
+    auto ycode_of = [&](int m, int b) { return (int)((yw >> (4 * m + 2 * b)) & 3u) - 1; };
     // ---- E = XEta BL for 16 sites x 32 species (R/updateZ.R:11-34); T[2m+b][lk+4r] <- E
     if (DRAW) {
       d4 e0 = {0.0, 0.0, 0.0, 0.0}, e1 = {0.0, 0.0, 0.0, 0.0};
@@ -549,19 +555,26 @@ __global__ __launch_bounds__(256, NKB > 4 ? 2 : 4) void z_wave_kernel(ZArgs a) {
       }
       wave_lds_sync();
     }
-    // ---- draws in coalesced order: lane = site s (16 consecutive) x species pair m = 4c + lk;
-    //      one Philox call per (site, pair); Z stores are 128-B site runs
+    // ---- draws in coalesced order: lane = site s (16 consecutive) x species pair m; the lane's
+    //      four pairs are two species quads, m = 8 (c >> 1) + 2 lk + (c & 1); one Philox call per
+    //      (site, quad), its words x, y for pair m (c even) and z, w for pair m + 1 (c odd), one
+    //      32-bit uniform a cell (rng.h u32o); Z stores are 128-B site runs
     {
       const int s = lm, i = i0 + s;
+      U4 qw{0u, 0u, 0u, 0u};
 #pragma unroll 1
       for (int c = 0; c < 4; ++c) {
-        const int m = 4 * c + lk, ja = j0 + 2 * m;
+        const int m = 8 * (c >> 1) + 2 * lk + (c & 1), ja = j0 + 2 * m;
         Uniform2 u{0.0, 0.0};
-        if (DRAW) u = uniforms_wave_key(a.key, (uint32_t)((size_t)i + (size_t)ny * (uint32_t)((a.sp0 + ja) >> 1)), 0, S_Z, iter);
+        if (DRAW) {
+          if (!(c & 1))  // (the species block and the shard start are multiples of 4)
+            qw = philox4x32_10_wave_key(U4{(uint32_t)((size_t)i + (size_t)ny * (uint32_t)((a.sp0 + ja) >> 2)), 0u, (uint32_t)S_Z, iter}, a.key);
+          u = (c & 1) ? Uniform2{u32o(qw.z), u32o(qw.w)} : Uniform2{u32o(qw.x), u32o(qw.y)};
+        }
         if (DRAW && !POIS && (MODE & 2)) {
           // probit / NA pair (the whole chain is probit, or the pair's species are):
           // both draws inline with interleaved chains; normal species keep Z = Y
-          const int cd0 = ycode_of(c, 0), cd1 = ycode_of(c, 1);
+          const int cd0 = ycode_of(m, 0), cd1 = ycode_of(m, 1);
           const int jj0 = 2 * m, jj1 = 2 * m + 1;
           const bool in0 = i < ny && ja < a.ns_loc, in1 = i < ny && ja + 1 < a.ns_loc;
           const double e0 = sT[jj0 * ZT_TLD + s], e1 = sT[jj1 * ZT_TLD + s];
@@ -587,7 +600,7 @@ __global__ __launch_bounds__(256, NKB > 4 ? 2 : 4) void z_wave_kernel(ZArgs a) {
           if (i < ny && j < a.ns_loc) {
             const size_t cell = (size_t)i + (size_t)ny * j;
             if (DRAW) {
-              const int code = ycode_of(c, b);
+              const int code = ycode_of(m, b);
               const double e = sT[jj * ZT_TLD + s];
               if (sFam[jj] == 1 && code >= 0)
                 z = a.Yval[cell];  // normal: Z = Y   R/updateZ.R:40-41

@@ -217,9 +217,9 @@ int hmsc_create_sharded_host(const hmsc_model* model, uint64_t seed, int32_t dev
                              uint32_t updater_mask, int32_t rank, int32_t nranks,
                              hmsc_allreduce_fn fn, void* ctx, hmsc_state** out);
 /* The species block [sp0, sp0 + nsl) rank `rank` of `nranks` owns in hmsc_create_sharded:
- * whole species pairs (updateZ's Philox species pairs), the ceil(ns/2) pairs spread evenly,
- * rank r owning pairs [floor(r P/nranks), floor((r+1) P/nranks)); an error if that block is
- * empty (fewer pairs than ranks).  No reference counterpart (species sharding is new). */
+ * whole species quads (updateZ's Philox species quads), the ceil(ns/4) quads spread evenly,
+ * rank r owning quads [floor(r Q/nranks), floor((r+1) Q/nranks)); an error if that block is
+ * empty (fewer quads than ranks).  No reference counterpart (species sharding is new). */
 int hmsc_shard_range(int32_t ns, int32_t rank, int32_t nranks, int32_t* sp0, int32_t* nsl);
 
 void hmsc_destroy(hmsc_state* s);

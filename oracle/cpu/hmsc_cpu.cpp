@@ -38,7 +38,7 @@ constexpr int GAMMA_MAX_TRIALS = 64;
 struct Rng {
   uint32_t k0, k1;
   explicit Rng(uint64_t seed) : k0((uint32_t)(seed & 0xFFFFFFFFu)), k1((uint32_t)(seed >> 32)) {}
-  void block(uint32_t idx, uint32_t sub, uint32_t stream, uint32_t it, double* a, double* b) const {
+  void words(uint32_t idx, uint32_t sub, uint32_t stream, uint32_t it, uint32_t w[4]) const {
     uint32_t c0 = idx, c1 = sub, c2 = stream, c3 = it, q0 = k0, q1 = k1;
     for (int r = 0; r < 10; ++r) {
       const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
@@ -48,8 +48,13 @@ struct Rng {
       q0 += 0x9E3779B9u;
       q1 += 0xBB67AE85u;
     }
-    *a = ((double)(c0 >> 5) * 67108864.0 + (double)(c1 >> 6) + 0.5) * (1.0 / 9007199254740992.0);
-    *b = ((double)(c2 >> 5) * 67108864.0 + (double)(c3 >> 6) + 0.5) * (1.0 / 9007199254740992.0);
+    w[0] = c0, w[1] = c1, w[2] = c2, w[3] = c3;
+  }
+  void block(uint32_t idx, uint32_t sub, uint32_t stream, uint32_t it, double* a, double* b) const {
+    uint32_t w[4];
+    words(idx, sub, stream, it, w);
+    *a = ((double)(w[0] >> 5) * 67108864.0 + (double)(w[1] >> 6) + 0.5) * (1.0 / 9007199254740992.0);
+    *b = ((double)(w[2] >> 5) * 67108864.0 + (double)(w[3] >> 6) + 0.5) * (1.0 / 9007199254740992.0);
   }
   double uniform(uint32_t idx, uint32_t sub, uint32_t stream, uint32_t it) const {
     double a, b;
@@ -267,10 +272,10 @@ struct Chain {
         for (int i = 0; i < ny; ++i) e[i] += x[i] * l;
       }
       const double sd = 1.0 / std::sqrt(iSigma[j]);
-      for (int i = 0; i < ny; ++i) {
-        double a, b;
-        rng.block(i + (uint32_t)ny * (uint32_t)(j >> 1), 0, S_Z, it, &a, &b);
-        const double u = (j & 1) ? b : a;
+      for (int i = 0; i < ny; ++i) {  // one Philox block per (site, species quad), word j & 3
+        uint32_t q[4];
+        rng.words(i + (uint32_t)ny * (uint32_t)(j >> 2), 0, S_Z, it, q);
+        const double u = ((double)q[j & 3] + 0.5) * (1.0 / 4294967296.0);
         const double s = yc[i] == 1.0 ? 1.0 : -1.0;
         const double w = trunc_normal_lower(-s * e[i] / sd, u);
         zc[i] = e[i] + sd * s * w;

@@ -348,17 +348,17 @@ def update_z(st, model, rng, it, Y=None, zero_noise=False):
     ny, ns = Y.shape
     E = linear_predictor(st, model)
     sd = st["iSigma"] ** -0.5
-    # one Philox block per (site, species pair (2m, 2m+1)); species 2m takes the first
-    # uniform, 2m+1 the second (rng.h contract, z_wave_kernel)
+    # one Philox block per (site, species quad 4q .. 4q + 3); species 4q + k takes word k as the
+    # uniform (w + 1/2) 2^-32 (rng.h contract, z_wave_kernel)
     j = np.arange(ns)
-    idx = (np.arange(ny)[:, None] + ny * (j[None, :] >> 1)).astype(np.uint64)
+    idx = (np.arange(ny)[:, None] + ny * (j[None, :] >> 2)).astype(np.uint64)
     fam = model["distr"][:, 0]
     na = np.isnan(Y)
     Z = np.empty((ny, ns))
     normal_cols = fam == 1
     Z[:, normal_cols] = Y[:, normal_cols]
-    ua, ub = rng.uniforms(idx, 0, R.S_Z, it)
-    u = np.where((j & 1)[None, :] == 1, ub, ua)
+    w4 = rng.words(idx, 0, R.S_Z, it)
+    u = R.u32o(np.choose(np.broadcast_to((j & 3)[None, :], idx.shape), w4))
     s = np.where(Y == 1, 1.0, -1.0)
     alpha = -s * E / sd[None, :]
     w = R.trunc_normal_lower(alpha, u)

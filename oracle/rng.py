@@ -75,6 +75,12 @@ def u53(hi, lo):
             + (lo >> np.uint64(6)).astype(np.float64) + 0.5) * (1.0 / 9007199254740992.0)
 
 
+def u32o(w):
+    """Open-interval uniform from one 32-bit word, (w + 1/2) 2^-32 (rng.h u32o, exact in
+    double): updateZ's uniforms, at the resolution of R's own unif_rand (Mersenne-Twister)."""
+    return (np.asarray(w, dtype=np.uint64).astype(np.float64) + 0.5) * (1.0 / 4294967296.0)
+
+
 class Rng:
     """Key = one chain's 64-bit seed; ``iter`` = sweep number (0 for initialisation)."""
 
@@ -86,6 +92,10 @@ class Rng:
     def uniforms(self, idx, sub, stream, it):
         x, y, z, w = philox4x32_10(idx, sub, stream, it, self.k0, self.k1)
         return u53(x, y), u53(z, w)
+
+    def words(self, idx, sub, stream, it):
+        """The block's four 32-bit words (uint64 arrays)."""
+        return philox4x32_10(idx, sub, stream, it, self.k0, self.k1)
 
     def normal(self, idx, sub, stream, it):
         """Standard normal by inversion of the first uniform of the (idx, sub) block

@@ -5,7 +5,7 @@ splits species into contiguous blocks and all-reduces, once per updater, the
 species-sums that couple the shards.  Here each rank computes its block's share of
 those sums with the oracle's formulas and a gloo all_reduce must reproduce the
 unsharded values — the same decomposition and block arithmetic the C library uses
-(capi.cpp shard_range: whole species pairs spread evenly over the ranks).  Chains mode needs no exchange;
+(capi.cpp shard_range: whole species quads spread evenly over the ranks).  Chains mode needs no exchange;
 its timing reduction (max over ranks) is checked too.
 """
 import os
@@ -30,9 +30,10 @@ def _free_port():
 
 
 def species_block(ns, rank, nranks):
-    """capi.cpp shard_range (hmsc_shard_range): whole species pairs, spread evenly."""
-    pairs = (ns + 1) // 2
-    return min(ns, 2 * (pairs * rank // nranks)), min(ns, 2 * (pairs * (rank + 1) // nranks))
+    """capi.cpp shard_range (hmsc_shard_range): whole species quads (updateZ draws a quad from
+    one Philox block), spread evenly."""
+    quads = (ns + 3) // 4
+    return min(ns, 4 * (quads * rank // nranks)), min(ns, 4 * (quads * (rank + 1) // nranks))
 
 
 def sufficient_stats(st, m, sl):
@@ -98,7 +99,7 @@ def test_species_sharded_statistics_allreduce_gloo():
 def test_species_blocks_partition():
     for ns in (1, 7, 1000, 1003):
         for n in (1, 2, 4, 8):
-            if 2 * n > ns + 1:
+            if 4 * n > ns + 3:
                 continue
             blocks = [species_block(ns, r, n) for r in range(n)]
             assert all(b > a for a, b in blocks)

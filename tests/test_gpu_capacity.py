@@ -92,6 +92,9 @@ WIDE = {
     "nf70": dict(ny=240, ns=30, nc=4, nf=70, seed=24),
     # two levels, K = 100, NA cells (masked XZ rows of the 128-row kernel)
     "k100_na": dict(ny=220, ns=36, nc=60, nf=20, nr=2, units=[220, 40], na_frac=0.03, seed=25),
+    # N = nc nt = 300 > 256: Gamma2's final stage in its sized LDS layout, the prep's and GammaV's
+    # 300 x 300 systems in global scratch
+    "n300": dict(ny=200, ns=80, nc=6, nf=2, nt=50, seed=27),
 }
 
 
@@ -195,3 +198,22 @@ def test_wide_sample_predict_post():
     o = P.computeAssociations(hA)
     assert rel_err(d[0]["mean"], o[0]["mean"]) < 1e-12
     np.testing.assert_array_equal(d[0]["support"], o[0]["support"])
+
+
+@pytest.mark.parametrize("force_global", [False, True])
+def test_gamma2_large_n(monkeypatch, force_global):
+    """updateGamma2 past the old nc nt <= 256 (R/updateGamma2.R has no limit): N = 6 x 50 = 300
+    and N = 12 x 30 = 360 against the oracle, with the final stage's arrays in LDS and, forced,
+    in global memory (the layout a workgroup's LDS cannot hold, N >~ 1800)."""
+    if force_global:
+        monkeypatch.setenv("HMSC_G2F_GLOBAL", "1")
+    for kw in (dict(ny=200, ns=80, nc=6, nf=2, nt=50, seed=28), dict(ny=180, ns=64, nc=12, nf=3, nt=30, seed=29)):
+        hM = synthetic_model(**kw)
+        m = oracle_model(hM)
+        seed = 4242
+        st = _oracle_state(m, seed)
+        ch = _chain(hM, seed, st)
+        ch.update("Gamma2", 9)
+        g = ch.get_state()
+        assert rel_err(g["Gamma"], O.update_gamma2(st, m, Rng(seed), 9)) < TOL_WIDE_GAMMA, kw
+        ch.close()

@@ -245,9 +245,9 @@ def test_single_updaters_on_shards():
 def test_shard_range_blocks():
     for ns in (2, 7, 41, 1000, 1003):
         for n in (1, 2, 4, 8):
-            if n > (ns + 1) // 2:
+            if n > (ns + 3) // 4:
                 continue
             bl = [shard_range(ns, r, n) for r in range(n)]
             assert bl[0][0] == 0 and sum(b for _, b in bl) == ns
-            assert all(a % 2 == 0 for a, _ in bl)
+            assert all(a % 4 == 0 for a, _ in bl)
             assert all(bl[i][0] + bl[i][1] == bl[i + 1][0] for i in range(n - 1))
