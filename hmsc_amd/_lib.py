@@ -180,6 +180,16 @@ def iptr(a):
     return None if a is None else a.ctypes.data_as(ip)
 
 
+def fptr_held(a):
+    """fptr for an array the caller keeps alive across the C call (the pointer does not hold
+    it): half data_as's cost, for the record buffers of every run."""
+    return C.cast(a.__array_interface__["data"][0], dp)
+
+
+def iptr_held(a):
+    return C.cast(a.__array_interface__["data"][0], ip)
+
+
 def fortran(a, dtype=np.float64):
     """Column-major contiguous copy (R storage order)."""
     return np.asfortranarray(np.asarray(a, dtype=dtype))

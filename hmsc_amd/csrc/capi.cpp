@@ -1646,8 +1646,13 @@ static void eager_sweep(State& s, uint32_t iter, bool adapt) {
   s.eager_streak = adapt ? 0 : s.eager_streak + 1;
 }
 
-static void unpack_record(const State& s, const double* slot, int k, int samples, hmsc_record* rec) {
+// part / nparts: this call's share of the sample -- Eta's factor columns h = part - 1 (mod
+// nparts), everything else in part 0 (a run's last sample is unpacked by every worker, after the device
+// is done: one worker took ~80 us of the 20-step run's tail)
+static void unpack_record(const State& s, const double* slot, int k, int samples, hmsc_record* rec, int part = 0,
+                          int nparts = 1) {
   const int K = s.K, nsl = s.nsl, nc = s.nc, nt = s.nt, NF = s.NF;
+  const bool p0 = part == 0;
   const double* BL = slot;
   const double* Psi = BL + (size_t)K * nsl;
   const double* Delta = Psi + (size_t)NF * nsl;
@@ -1655,29 +1660,29 @@ static void unpack_record(const State& s, const double* slot, int k, int samples
   const double* iV = Gamma + (size_t)nc * nt;
   const double* iS = iV + (size_t)nc * nc;
   const double* eta = iS + nsl;
-  if (rec->Beta)
+  if (rec->Beta && p0)
     for (int j = 0; j < nsl; ++j)
       for (int c = 0; c < nc; ++c) rec->Beta[(size_t)k * nc * nsl + c + (size_t)nc * j] = BL[c + (size_t)K * j];
-  if (rec->Gamma) std::memcpy(rec->Gamma + (size_t)k * nc * nt, Gamma, sizeof(double) * nc * nt);
-  if (rec->iV) std::memcpy(rec->iV + (size_t)k * nc * nc, iV, sizeof(double) * nc * nc);
-  if (rec->iSigma) std::memcpy(rec->iSigma + (size_t)k * nsl, iS, sizeof(double) * nsl);
+  if (rec->Gamma && p0) std::memcpy(rec->Gamma + (size_t)k * nc * nt, Gamma, sizeof(double) * nc * nt);
+  if (rec->iV && p0) std::memcpy(rec->iV + (size_t)k * nc * nc, iV, sizeof(double) * nc * nc);
+  if (rec->iSigma && p0) std::memcpy(rec->iSigma + (size_t)k * nsl, iS, sizeof(double) * nsl);
   for (int r = 0; r < s.nr; ++r) {
     const Level& L = s.lev[r];
     const int nf = L.nf, nfm = L.nfcap, lo = s.loff(r), fo = s.foff(r);
-    if (rec->rec_nf) rec->rec_nf[r * samples + k] = nf;
-    if (rec->Lambda[r] || rec->Psi[r])
+    if (rec->rec_nf && p0) rec->rec_nf[r * samples + k] = nf;
+    if ((rec->Lambda[r] || rec->Psi[r]) && p0)
       for (int j = 0; j < nsl; ++j)
         for (int h = 0; h < nfm; ++h) {
           const size_t o = (size_t)k * nfm * nsl + h + (size_t)nfm * j;
           if (rec->Lambda[r]) rec->Lambda[r][o] = h < nf ? BL[lo + h + (size_t)K * j] : 0.0;
           if (rec->Psi[r]) rec->Psi[r][o] = h < nf ? Psi[fo + h + (size_t)NF * j] : 0.0;
         }
-    for (int h = 0; h < nfm; ++h) {
+    for (int h = 0; h < nfm && p0; ++h) {
       if (rec->Delta[r]) rec->Delta[r][(size_t)k * nfm + h] = h < nf ? Delta[fo + h] : 1.0;
       if (rec->Alpha[r] && !L.spatial) rec->Alpha[r][(size_t)k * nfm + h] = 1;
     }
     if (rec->Eta[r])
-      for (int h = 0; h < nfm; ++h) {
+      for (int h = (part + nparts - 1) % nparts; h < nfm; h += nparts) {  // (part 0 also has the rest)
         double* dst = rec->Eta[r] + (size_t)k * L.np * nfm + (size_t)L.np * h;
         if (h < nf)
           std::memcpy(dst, eta + (size_t)L.np * h, sizeof(double) * L.np);
@@ -1686,6 +1691,7 @@ static void unpack_record(const State& s, const double* slot, int k, int samples
       }
     eta += (size_t)L.np * nf;
   }
+  if (!p0) return;
   if (rec->rho) rec->rho[k] = (int32_t)eta[0];  // packed after the Eta blocks (launch_record)
   const double* al = eta + 1;                   // then AlphaD of every spatial level
   for (int r = 0; r < s.nr; ++r) {
@@ -1802,6 +1808,8 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
   for (int k = 0; k < samples; ++k) done[k].store(0);
   int low = 0;  // every sample < low is unpacked (main thread only)
   std::atomic<int64_t> diag_unpack_ns{0};  // HMSC_DIAG_TIMING: time in unpack (all workers)
+  std::atomic<int> last_parts{0};           // workers through their share of the last sample
+  std::atomic<bool> last_touched{false};    // ... whose pages the launcher thread has touched
   int64_t diag_wait_ns = 0;                 // and the launcher's waits for a free ring slot
   volatile uint64_t* copied = s.copied_host;
   if (recording) *copied = 0;           // no copy is in flight between runs
@@ -1828,8 +1836,10 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
         // being waited for left the later ones to fault inside their unpack
         constexpr int LOOKAHEAD = 4;
         int touched = w - W;
-        for (int k = w; k < samples; k += W) {
-          while (touched + W < samples && touched + W <= k + W * LOOKAHEAD) {
+        // the run's last sample (W >= 2): every worker unpacks its share once it lands
+        const int split = (W >= 2 && samples >= 1) ? samples - 1 : samples;
+        for (int k = w; k < split; k += W) {
+          while (touched + W < split && touched + W <= k + W * LOOKAHEAD) {
             touched += W;
             pretouch_record(s, touched, rec);
           }
@@ -1848,6 +1858,28 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
             std::lock_guard<std::mutex> lk(mu);
           }
           cv_done.notify_one();
+        }
+        if (split < samples) {
+          const int k = split;
+          // (its pages are first touched by the launcher thread once the run is enqueued: a
+          // worker's zero-write of a page could land after another worker's share)
+          for (int spin = 0; __atomic_load_n(copied, __ATOMIC_ACQUIRE) <= (uint64_t)k ||
+                             !last_touched.load(std::memory_order_acquire);
+               ++spin) {
+            if (stop.load(std::memory_order_relaxed)) return;
+            if (spin > (1 << 20)) std::this_thread::sleep_for(std::chrono::microseconds(20));
+            else std::this_thread::yield();
+          }
+          const auto tu0 = std::chrono::steady_clock::now();
+          unpack_record(s, s.host_rec + s.slot_doubles * (k % s.ring_slots), k, samples, rec, w, W);
+          diag_unpack_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tu0).count();
+          if (last_parts.fetch_add(1, std::memory_order_acq_rel) == W - 1) {
+            done[k].store(1, std::memory_order_release);
+            {
+              std::lock_guard<std::mutex> lk(mu);
+            }
+            cv_done.notify_one();
+          }
         }
       } catch (const std::exception& e) {
         std::lock_guard<std::mutex> lk(mu);
@@ -1971,6 +2003,10 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
   }
   join_side(s);
   const auto t_enq = std::chrono::steady_clock::now();
+  if (pool && W >= 2 && samples >= 1) {  // the last sample's pages, while the device runs
+    pretouch_record(s, samples - 1, rec);
+    last_touched.store(true, std::memory_order_release);
+  }
   HIP_OK(hipStreamSynchronize(s.stream));
   HIP_OK(hipStreamSynchronize(s.copy_stream));
   const auto t_done = std::chrono::steady_clock::now();

@@ -164,15 +164,42 @@ struct SlabJob {
   int nparts, nb;
 };
 
+// all-reduce A's species sums of a sharded chain (g2_stats_body, below)
+struct G2SArgs {
+  const double* XZ;
+  const double* XZpart;  // updateZ's chunk partials (the slab launch's co-launched stats), else null
+  int64_t xz_stride;
+  int xz_nparts;
+  const double* BL;
+  const double* Tr;
+  const double* iSigma;
+  const double* xtztr;
+  double* part;
+  int* ticket;
+  double* out;
+  int K, nc, NF, nt, nsl, nparts;
+};
+__device__ void g2_stats_body(const G2SArgs& a, int bid, double* smem);
+struct G2SJob {
+  G2SArgs a;
+  size_t smem;
+};
+G2SJob shard_g2_job(State& s, const double* xz_part, int xz_nparts);
+
 __device__ void side_gate_body(const SideGate& g);
 
 // two independent slab reductions in one launch: blocks [0, j0.nb) reduce j0, the next j1.nb
-// j1, and a last block the side gate when there is one
-__global__ __launch_bounds__(256) void slab_sum2_kernel(SlabJob j0, SlabJob j1, SideGate g) {
-  if ((int)blockIdx.x < j0.nb)
-    slab_sum_body(j0.part, j0.out, j0.n, j0.nparts, j0.stride, blockIdx.x, j0.nb);
-  else if ((int)blockIdx.x < j0.nb + j1.nb)
-    slab_sum_body(j1.part, j1.out, j1.n, j1.nparts, j1.stride, blockIdx.x - j0.nb, j1.nb);
+// j1, then (a sharded chain's sweep) ng2 blocks of all-reduce A's species sums from updateZ's
+// chunk partials, and a last block the side gate when there is one
+__global__ __launch_bounds__(256) void slab_sum2_kernel(SlabJob j0, SlabJob j1, SideGate g, G2SArgs g2, int ng2) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int b = blockIdx.x;
+  if (b < j0.nb)
+    slab_sum_body(j0.part, j0.out, j0.n, j0.nparts, j0.stride, b, j0.nb);
+  else if (b < j0.nb + j1.nb)
+    slab_sum_body(j1.part, j1.out, j1.n, j1.nparts, j1.stride, b - j0.nb, j1.nb);
+  else if (b < j0.nb + j1.nb + ng2)
+    g2_stats_body(g2, b - j0.nb - j1.nb, smem);
   else
     side_gate_body(g);
 }
@@ -216,10 +243,15 @@ __global__ __launch_bounds__(256) void gram_na_kernel(EtaView ev, const double* 
 
 // the two slab reductions that follow the z kernel (XZ, ZTr), one launch (zdraw.hip)
 void launch_slab_sum2(const double* p0, double* o0, int64_t n0, int np0, const double* p1, double* o1, int64_t n1,
-                      int np1, hipStream_t st, SideGate gate) {
+                      int np1, hipStream_t st, SideGate gate, State* g2s) {
   const SlabJob j0{p0, o0, n0, n0, np0, grid_for(n0)};
   const SlabJob j1{p1, o1, n1, n1, np1, grid_for(n1)};
-  slab_sum2_kernel<<<j0.nb + j1.nb + (gate.n > 0 ? 1 : 0), 256, 0, st>>>(j0, j1, gate);
+  G2SJob job{};
+  if (g2s) job = shard_g2_job(*g2s, p0, np0);  // (p0: updateZ's XZ chunk partials)
+  const G2SJob* g2 = g2s ? &job : nullptr;
+  const int ng2 = g2 ? g2->a.nparts : 0;
+  slab_sum2_kernel<<<j0.nb + j1.nb + ng2 + (gate.n > 0 ? 1 : 0), 256, g2 ? g2->smem : 0, st>>>(
+      j0, j1, gate, g2 ? g2->a : G2SArgs{}, ng2);
   HIP_OK(hipGetLastError());
 }
 
@@ -4039,14 +4071,18 @@ __global__ __launch_bounds__(256) void pack_kernel(PackArgs a) { pack_body(a, bl
 // updateZ's two slab reductions and the record pack of the sweep's main-stream outputs in one
 // launch (graph replays of recorded sweeps): the pack reads none of what the slab sums or
 // updateZ write (Z is not recorded), so it need not wait for them
-__global__ __launch_bounds__(256) void slab_pack_kernel(SlabJob j0, SlabJob j1, PackArgs pk, int npack, SideGate g) {
+__global__ __launch_bounds__(256) void slab_pack_kernel(SlabJob j0, SlabJob j1, PackArgs pk, int npack, SideGate g,
+                                                        G2SArgs g2, int ng2) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x;
   if (b < j0.nb)
     slab_sum_body(j0.part, j0.out, j0.n, j0.nparts, j0.stride, b, j0.nb);
   else if (b < j0.nb + j1.nb)
     slab_sum_body(j1.part, j1.out, j1.n, j1.nparts, j1.stride, b - j0.nb, j1.nb);
-  else if (b < j0.nb + j1.nb + npack)
-    pack_body(pk, b - j0.nb - j1.nb, npack);
+  else if (b < j0.nb + j1.nb + ng2)
+    g2_stats_body(g2, b - j0.nb - j1.nb, smem);
+  else if (b < j0.nb + j1.nb + ng2 + npack)
+    pack_body(pk, b - j0.nb - j1.nb - ng2, npack);
   else
     side_gate_body(g);
 }
@@ -4128,12 +4164,17 @@ void launch_record(State& s, double* slot, int part) {
 }
 
 void launch_slab_sum2_pack(State& s, const double* p0, double* o0, int64_t n0, int np0, const double* p1, double* o1,
-                           int64_t n1, int np1, SideGate gate) {
+                           int64_t n1, int np1, SideGate gate, State* g2s) {
   const SlabJob j0{p0, o0, n0, n0, np0, grid_for(n0)};
   const SlabJob j1{p1, o1, n1, n1, np1, grid_for(n1)};
   const PackArgs pk = make_pack_args(s, nullptr, 1);
   constexpr int NPACK = 256;
-  slab_pack_kernel<<<j0.nb + j1.nb + NPACK + (gate.n > 0 ? 1 : 0), 256, 0, s.stream>>>(j0, j1, pk, NPACK, gate);
+  G2SJob job{};
+  if (g2s) job = shard_g2_job(*g2s, p0, np0);
+  const G2SJob* g2 = g2s ? &job : nullptr;
+  const int ng2 = g2 ? g2->a.nparts : 0;
+  slab_pack_kernel<<<j0.nb + j1.nb + ng2 + NPACK + (gate.n > 0 ? 1 : 0), 256, g2 ? g2->smem : 0, s.stream>>>(
+      j0, j1, pk, NPACK, gate, g2 ? g2->a : G2SArgs{}, ng2);
   HIP_OK(hipGetLastError());
 }
 
@@ -4219,24 +4260,14 @@ static void seq_sum(const double* part, int nparts, int64_t ld, int64_t n, doubl
 // gamma2_final_body adds a single rank's partials, so Gamma2 of a 1-rank sharded chain is the
 // unsharded chain's bit for bit.  With NA in this rank's Y, XZ is masked and X^T Z Tr comes
 // from ZTr (xtztr) instead.
-struct G2SArgs {
-  const double* XZ;
-  const double* BL;
-  const double* Tr;
-  const double* iSigma;
-  const double* xtztr;
-  double* part;
-  int* ticket;
-  double* out;
-  int K, nc, NF, nt, nsl, nparts;
-};
-
-__global__ __launch_bounds__(256) void g2_stats_kernel(G2SArgs a) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
+// (G2SArgs: declared with the slab kernels.)  With XZpart the rows < nc come from updateZ's
+// chunk partials, summed in the slab reduction's order (gamma2_partial_body): the same bits as
+// from the reduced XZ, so the stats can ride in the slab launch instead of following it.
+__device__ void g2_stats_body(const G2SArgs& a, int bid, double* smem) {
   __shared__ int s_last, s_cnt;
   const int t = threadIdx.x;
-  gamma2_partial_body(XZSrc{a.XZ, nullptr, 0, 0}, a.BL, a.K, a.nc, a.NF, a.nt, a.nsl, a.Tr, a.part, smem, blockIdx.x,
-                      true);
+  gamma2_partial_body(XZSrc{a.XZ, a.XZpart, a.xz_nparts, a.xz_stride}, a.BL, a.K, a.nc, a.NF, a.nt, a.nsl, a.Tr,
+                      a.part, smem, bid, true);
   vm_stores_done();
   __syncthreads();
   if (t == 0) s_last = __hip_atomic_fetch_add(a.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.nparts - 1;
@@ -4295,23 +4326,23 @@ __global__ __launch_bounds__(256) void g2_stats_kernel(G2SArgs a) {
   if (t == 0) a.out[P] = (double)s_cnt;
 }
 
-static void shard_g2_stats(State& s) {
-  if (!(s.mask & HMSC_UP_GAMMA2)) return;
-  if (!s.xeta_valid) launch_xeta(s);
-  if (!s.zt_valid) launch_zt_refresh(s);  // XZ (and ZTr) of the current Z and Eta
-  const int n1 = s.nc * s.nt, n12 = n1 + s.NF * s.nt;
-  const double* xt = nullptr;
-  if (s.has_na) {  // this rank's XZ is masked: X^T (Z Tr) from ZTr
-    xt_ztr_kernel<<<n1, 256, 0, s.stream>>>(s.X, s.ZTr, s.ny, s.nc, s.nt, s.allreduce_buf);
-    HIP_OK(hipGetLastError());
-    xt = s.allreduce_buf;
-  }
-  G2SArgs a{};
+__global__ __launch_bounds__(256) void g2_stats_kernel(G2SArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  g2_stats_body(a, blockIdx.x, smem);
+}
+
+// all-reduce A's stats job for this chain (with parts: from updateZ's chunk partials)
+G2SJob shard_g2_job(State& s, const double* xz_part, int xz_nparts) {
+  G2SJob j{};
+  G2SArgs& a = j.a;
   a.XZ = s.XZ;
+  a.XZpart = xz_part;
+  a.xz_nparts = xz_part ? xz_nparts : 0;
+  a.xz_stride = xz_part ? (int64_t)s.K * s.nsl : 0;
   a.BL = s.BL;
   a.Tr = s.Tr;
   a.iSigma = s.iSigma;
-  a.xtztr = xt;
+  a.xtztr = nullptr;
   a.part = s.ABpart;
   a.ticket = s.shard_ticket;
   a.out = s.ar_a;
@@ -4321,7 +4352,30 @@ static void shard_g2_stats(State& s) {
   a.nt = s.nt;
   a.nsl = s.nsl;
   a.nparts = (s.nsl + G2SB - 1) / G2SB;
-  g2_stats_kernel<<<a.nparts, 256, (size_t)(s.K * G2SB + G2SB * s.nt) * sizeof(double), s.stream>>>(a);
+  j.smem = (size_t)(s.K * G2SB + G2SB * s.nt + (xz_part ? 4 * s.nc * G2SB : 0)) * sizeof(double);
+  return j;
+}
+
+static void shard_g2_stats(State& s) {
+  if (!(s.mask & HMSC_UP_GAMMA2)) return;
+  const int n1 = s.nc * s.nt, n12 = n1 + s.NF * s.nt;
+  if (s.g2s_slab) {  // formed by updateZ's slab launch of this sweep (zdraw.hip)
+    s.g2s_slab = false;
+    ar_point(s, s.ar_a, (size_t)n12 + 1);  // all-reduce A
+    s.g2s_valid = true;
+    return;
+  }
+  if (!s.xeta_valid) launch_xeta(s);
+  if (!s.zt_valid) launch_zt_refresh(s);  // XZ (and ZTr) of the current Z and Eta
+  const double* xt = nullptr;
+  if (s.has_na) {  // this rank's XZ is masked: X^T (Z Tr) from ZTr
+    xt_ztr_kernel<<<n1, 256, 0, s.stream>>>(s.X, s.ZTr, s.ny, s.nc, s.nt, s.allreduce_buf);
+    HIP_OK(hipGetLastError());
+    xt = s.allreduce_buf;
+  }
+  G2SJob j = shard_g2_job(s, nullptr, 0);
+  j.a.xtztr = xt;
+  g2_stats_kernel<<<j.a.nparts, 256, j.smem, s.stream>>>(j.a);
   HIP_OK(hipGetLastError());
   ar_point(s, s.ar_a, (size_t)n12 + 1);  // all-reduce A
   s.g2s_valid = true;
@@ -4597,9 +4651,16 @@ void sweep_sharded(State& s, uint32_t iter) {
   if ((s.mask & HMSC_UP_ETA) && s.nr > 0 && !s.shard_dev) shard_eta_solve(s, iter, fused);
   if (s.mask & HMSC_UP_ALPHA) launch_alpha(s, iter);
   if (s.mask & HMSC_UP_INVSIGMA) launch_inv_sigma(s, iter);
-  if (s.mask & HMSC_UP_Z) launch_update_z(s, iter, false);
   s.g2s_valid = false;
+  // HMSC_G2S_SLAB: all-reduce A's sums formed in updateZ's slab launch from the chunk partials
+  // instead of a launch after it -- measured slower (ns = 1000: Z end -> next Gamma2 16.3 ->
+  // 18.7 us; ns = 125: 18.7 -> 25.4 us; the stats' 64-deep partial sums lengthen the slab
+  // launch more than the launch they replace), so off by default
+  s.g2s_slab_req = fused && !s.has_na && getenv_flag("HMSC_G2S_SLAB");  // (with NA: X^T Z Tr from ZTr)
+  if (s.mask & HMSC_UP_Z) launch_update_z(s, iter, false);
+  s.g2s_slab_req = false;
   shard_g2_stats(s);  // all-reduce A, for the next sweep's updateGamma2
+  s.g2s_slab = false;
   s.shard_dev = false;
 }
 

@@ -147,6 +147,8 @@ struct State {
   int* side_sync = nullptr;      // [GammaV, delta chain per level ..., Gamma2 prep, (slot SIDE_ARB_SLOT) the
                                  // sharded Eta solve's all-reduce-B flag]: epoch of the sweep
   bool shard_dev = false;        // this sharded sweep joins and forks its side chain on the device (sweep_sharded)
+  bool g2s_slab_req = false;     // sweep_sharded: updateZ's slab launch may form all-reduce A's sums ...
+  bool g2s_slab = false;         // ... and did (shard_g2_stats then only all-reduces)
   double* gvt = nullptr;         // the BetaLambda tail's GammaV / psi partial tiles
   int gvt_ld = 0;
   double* Gamma_side = nullptr;  // GammaV's Gamma, for the side stream's record pack
@@ -401,11 +403,13 @@ struct SideGate {
   int* err = nullptr;
 };
 SideGate side_gate_next(State& s, uint32_t iter);
+// g2s (a sharded chain's sweep, p0 = updateZ's XZ chunk partials): all-reduce A's species sums
+// formed in the same launch (g2_stats_body)
 void launch_slab_sum2(const double* p0, double* o0, int64_t n0, int np0, const double* p1, double* o1, int64_t n1,
-                      int np1, hipStream_t st, SideGate gate = SideGate{});
+                      int np1, hipStream_t st, SideGate gate = SideGate{}, State* g2s = nullptr);
 // the same with the main-stream record pack (part 1) of a captured recorded sweep appended
 void launch_slab_sum2_pack(State& s, const double* p0, double* o0, int64_t n0, int np0, const double* p1, double* o1,
-                           int64_t n1, int np1, SideGate gate = SideGate{});
+                           int64_t n1, int np1, SideGate gate = SideGate{}, State* g2s = nullptr);
 void launch_beta_lambda(State& s, uint32_t iter);
 void launch_gamma_v(State& s, uint32_t iter, hipStream_t st);
 void launch_gamma2(State& s, uint32_t iter);

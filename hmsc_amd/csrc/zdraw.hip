@@ -161,13 +161,16 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   // XZ and ZTr from their partials, one launch
   const int64_t nXZ = (int64_t)s.K * s.nsl, nZT = s.has_na ? (int64_t)s.ny * s.nt : 0;
   const SideGate gate = draw ? side_gate_next(s, iter) : SideGate{};
+  // a sharded sweep: all-reduce A's species sums ride in this launch (sweep_sharded)
+  State* g2s = (draw && s.g2s_slab_req && !s.has_na && (s.mask & HMSC_UP_GAMMA2)) ? &s : nullptr;
   if (draw && s.pack_req && (s.side_fused || sharded_pack_split(s)) && s.capturing) {
-    launch_slab_sum2_pack(s, s.XZ_part, s.XZ, nXZ, nchunk, s.ZTr_part, s.ZTr, nZT, s.ntile_j, gate);
+    launch_slab_sum2_pack(s, s.XZ_part, s.XZ, nXZ, nchunk, s.ZTr_part, s.ZTr, nZT, s.ntile_j, gate, g2s);
     s.pack_req = false;
     s.pack_done = true;
   } else {
-    launch_slab_sum2(s.XZ_part, s.XZ, nXZ, nchunk, s.ZTr_part, s.ZTr, nZT, s.ntile_j, s.stream, gate);
+    launch_slab_sum2(s.XZ_part, s.XZ, nXZ, nchunk, s.ZTr_part, s.ZTr, nZT, s.ntile_j, s.stream, gate, g2s);
   }
+  s.g2s_slab = g2s != nullptr;
 }
 
 // the z kernel's tables in one device buffer: the log table, then z_draw_tables

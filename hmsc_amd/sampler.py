@@ -478,10 +478,12 @@ class Chain:
                           iV=new("iV", (S, hM.nc, hM.nc)), iSigma=new("iSigma", (S, ns)),
                           rho=new("rho", S, np.int32), rec_nf=np.zeros((max(1, nd), S), dtype=np.int32))
             rec = L.hmsc_record()
-            for k, fp in (("Beta", L.fptr), ("Gamma", L.fptr), ("iV", L.fptr), ("iSigma", L.fptr), ("rho", L.iptr)):
+            # (the arrays are held in `arrays` across the call: pointers that do not hold them)
+            for k, fp in (("Beta", L.fptr_held), ("Gamma", L.fptr_held), ("iV", L.fptr_held), ("iSigma", L.fptr_held),
+                          ("rho", L.iptr_held)):
                 if want(k):
                     setattr(rec, k, fp(arrays[k]))
-            rec.rec_nf = L.iptr(arrays["rec_nf"])
+            rec.rec_nf = L.iptr_held(arrays["rec_nf"])
             for d in range(nd):
                 nfm, r = nfMax[d], lm.owner[d]
                 for k, shape, dt in (("Eta", (S, nfm, int(hM.np[r])), np.float64), ("Lambda", (S, ns, nfm), np.float64),
@@ -491,7 +493,7 @@ class Chain:
                         continue  # (shared by a covariate-dependent level's device levels)
                     if want(k):
                         arrays[f"{k}{d}"] = np.empty(shape, dtype=dt)
-                        getattr(rec, k)[d] = (L.iptr if dt == np.int32 else L.fptr)(arrays[f"{k}{d}"])
+                        getattr(rec, k)[d] = (L.iptr_held if dt == np.int32 else L.fptr_held)(arrays[f"{k}{d}"])
         L.check(self.lib.hmsc_run_verbose(self.h, int(transient), int(samples), int(thin), L.iptr(adapt),
                                           int(iter0), int(verbose), int(chain),
                                           C.byref(rec) if rec is not None else None))

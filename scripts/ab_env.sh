@@ -12,7 +12,7 @@ for r in $(seq 1 $ROUNDS); do
     i=$((i+1))
     envs=()
     [ "$setting" != "-" ] && IFS=, read -ra envs <<< "$setting"
-    env "${envs[@]}" timeout -k 10 200 python -u $R/bench.py --steps $STEPS --warmup 100 --no-cpu --no-sharded-leg \
+    env "${envs[@]}" timeout -k 10 200 python -u $R/bench.py --steps $STEPS --warmup ${WARMUP:-100} --no-cpu --no-sharded-leg \
       > $R/gpurun_out/ab/env$i.$r.json 2> $R/gpurun_out/ab/env$i.$r.err || { echo "bench failed: $setting"; exit 1; }
     python3 -c "
 import json; d=json.loads(open('$R/gpurun_out/ab/env$i.$r.json').read().strip().splitlines()[-1])
