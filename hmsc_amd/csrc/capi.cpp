@@ -882,7 +882,23 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   HIP_OK(hipHostMalloc(&s.host_rec, sizeof(double) * s.slot_doubles * s.ring_slots, hipHostMallocDefault));
   HIP_OK(hipHostMalloc(&s.copied_host, 64, hipHostMallocMapped | hipHostMallocCoherent));
   HIP_OK(hipHostGetDevicePointer((void**)&s.copied_dev, s.copied_host, 0));
-  s.d_rec_desc = dalloc<int32_t>(4);
+  s.d_rec_desc = dalloc<int32_t>(8);  // {iter0, transient, thin, samples, run nonce}
+  // kernel copies for the recorded graphs of at most kcopy_max sweeps: a run's last replays (the
+  // record tail), while long replays keep one host-issued copy each (HMSC_KERNEL_COPY=0: never,
+  // HMSC_KERNEL_COPY_MAX: the size bound; a 32-sweep graph with kernel copies measured 2.9 %
+  // slower over 1000 sweeps, the 20-step line 5 % faster, profiles/r06_kcopy_ab.txt)
+  {
+    const char* e = std::getenv("HMSC_KERNEL_COPY");
+    s.kcopy = !(e && e[0] == '0');
+    const char* m = std::getenv("HMSC_KERNEL_COPY_MAX");
+    s.kcopy_max = m ? std::max(0, atoi(m)) : 8;
+  }
+  if (s.kcopy && hipHostGetDevicePointer((void**)&s.host_rec_dev, s.host_rec, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    s.kcopy = false;  // (the host ring is not mapped for the device: host-issued copies)
+  }
+  s.pack_flags = dalloc<uint64_t>((size_t)3 * s.ring_slots);
+  s.pack_ticket = dalloc<int>(4);
   s.d_iter_side = dalloc<uint32_t>(1);
   s.gv_part = dalloc<double>((size_t)((nsl + 31) / 32) * (nc * nc + nc * nt));
   HIP_OK(hipEventCreateWithFlags(&s.ev_graph, hipEventDisableTiming));
@@ -905,7 +921,7 @@ static void free_state(State& s) {
   DeviceGuard dg(s.device);
   (void)hipDeviceSynchronize();
   s.unpack_pool.reset();  // idle between runs; joined before the host ring goes
-  void* ptrs[] = {s.X, s.Tr, s.Yval, s.Yraw, s.Ycode, s.Ybits, s.logtab, s.fam, s.varest, s.V0, s.iUGamma, s.mGamma, s.UGammaL,
+  void* ptrs[] = {s.pack_flags, s.pack_ticket, s.X, s.Tr, s.Yval, s.Yraw, s.Ycode, s.Ybits, s.logtab, s.fam, s.varest, s.V0, s.iUGamma, s.mGamma, s.UGammaL,
                   s.aSigma, s.bSigma, s.XX, s.TT, s.V0g, s.V0gXXV0g, s.iV0, s.V0inv, s.iUmG, s.V0gXX, s.g2prep, s.scratch2, s.na_cols, s.na_index,
                   s.na_rows, s.row_na, s.row_slot, s.dev_flags, s.Z, s.XEta, s.BL, s.Psi, s.Delta, s.Gamma, s.iV,
                   s.iSigma, s.rho, s.XZ, s.G, s.ZTr, s.XZ_part, s.G_part, s.ZTr_part, s.Gna, s.ZL, s.ZL_part,
@@ -1370,9 +1386,9 @@ __global__ void set_iters_kernel(uint32_t* p, uint32_t v, int n) {
 // Gamma2 + BetaLambda launch's epoch words, the tails' CR / W flag and the side chain's flags
 // (a run's sweeps are distinct, but an earlier run may have ended on one of them)
 __global__ void run_start_kernel(int32_t* desc, int32_t iter0, int32_t transient, int32_t thin, int32_t samples,
-                                 int* gbl, int* crw, int* side, int nside) {
+                                 int* gbl, int* crw, int* side, int nside, int32_t nonce) {
   const int t = threadIdx.x;
-  if (desc && t < 4) desc[t] = t == 0 ? iter0 : t == 1 ? transient : t == 2 ? thin : samples;
+  if (desc && t < 5) desc[t] = t == 0 ? iter0 : t == 1 ? transient : t == 2 ? thin : t == 3 ? samples : nonce;
   if (gbl && (t == 4 || t == 5)) gbl[t - 3] = 0;
   if (crw && t == 6) crw[0] = 0;
   if (side && t >= 8 && t < 8 + nside) side[t - 8] = 0;
@@ -1435,14 +1451,20 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
       s.side_pending |= 1;
       s.side_root = true;
     }
+    int pmask = 0;
+    s.cap_kcopy = s.kcopy && with_record && nsweeps <= s.kcopy_max;
     for (int i = 0; i < nsweeps; ++i) {
       s.d_iter = s.d_iters + i;
       s.cap_sweep = i;
       s.pack_req = with_record;
       s.pack_done = false;
+      s.cap_pack_mask = 0;
       sweep(s, iter, false);
       if (with_record) record_after_sweep(s, nullptr);
+      pmask = i == 0 ? s.cap_pack_mask : (pmask == s.cap_pack_mask ? pmask : -1);
     }
+    s.gx_pack_mask[with_record ? 1 : 0][graph_level(nsweeps)] = s.cap_kcopy ? pmask : 0;
+    s.cap_kcopy = false;
     s.d_iter = s.d_iters;
     s.cap_sweep = -1;
     s.side_root = false;
@@ -1450,6 +1472,7 @@ static hipGraphExec_t capture_sweeps(State& s, uint32_t iter, bool with_record, 
   } catch (...) {
     s.cap_sweep = -1;
     s.side_root = false;
+    s.cap_kcopy = false;
     s.ext_pending = nullptr;
     s.d_iter = s.d_iters;
     s.pack_req = s.pack_done = false;
@@ -1927,8 +1950,9 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
   // (the same for the tails epoch and the side chain's flags, graph sweeps' device-side joins)
   join_side(s);
   static_assert(2 + HMSC_MAX_LEVELS <= 56, "run_start_kernel: side flags");
+  ++s.run_nonce;  // (kcopy: pack flags of an earlier run never match this run's)
   run_start_kernel<<<1, 64, 0, s.stream>>>(recording ? s.d_rec_desc : nullptr, iter0, transient, thin, samples,
-                                           s.gbl_sync, s.crw_flag, s.side_sync, SIDE_SYNC_INTS);
+                                           s.gbl_sync, s.crw_flag, s.side_sync, SIDE_SYNC_INTS, (int32_t)s.run_nonce);
   HIP_OK(hipGetLastError());
   const auto t_start = std::chrono::steady_clock::now();
   int n_replays = 0;
@@ -1942,7 +1966,8 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
       while (ng > 1 && it + ng - 1 > total) ng >>= 1;
       // a recorded run ends on single-sweep replays (..., 2, 1, 1): the samples of the last
       // replay are copied out only after it, so a small last replay shortens the copy tail
-      if (recording && ng > 1 && it + ng - 1 == total && !s.long_tail) ng >>= 1;
+      // (not when that replay's graph copies each sample itself, kernel copies)
+      if (recording && ng > 1 && it + ng - 1 == total && !s.long_tail && !(s.kcopy && ng <= s.kcopy_max)) ng >>= 1;
       // (optional) a short first replay: the graph launch submits the side stream's nodes only
       // after the main stream's, ~16 us of host time per sweep, so the side chain of a big
       // first replay's first sweep starts late (~0.35 ms at 32 sweeps) and the second sweep
@@ -1959,7 +1984,12 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
         replayed = true;
         ++n_replays;
         n = ng;
-        if (klast >= 0) {
+        const int pm = klast >= 0 ? s.gx_pack_mask[1][graph_level(ng)] : 0;
+        if (klast >= 0 && pm > 0) {
+          // kernel copies: each sample to the host ring as soon as its pack parts are in
+          for (int k = kfirst; k <= klast; ++k) launch_rec_copy(s, k, pm);
+          s.ext_launched = false;
+        } else if (klast >= 0) {
           HIP_OK(hipEventRecord(s.ev_graph, s.stream));
           HIP_OK(hipStreamWaitEvent(s.copy_stream, s.ev_graph, 0));
           if (s.ext_launched) HIP_OK(hipStreamWaitEvent(s.copy_stream, s.ev_ext, 0));  // its record pack

@@ -4136,8 +4136,73 @@ static PackArgs make_pack_args(State& s, double* slot, int part) {
     a.desc = s.d_rec_desc;
     a.slot_stride = (int64_t)s.slot_doubles;
     a.ring_slots = s.ring_slots;
+    if (s.cap_kcopy) {  // this part's completion flag for the copy kernels
+      a.flags = s.pack_flags + (size_t)part * s.ring_slots;
+      a.ticket = s.pack_ticket + part;
+      s.cap_pack_mask |= 1 << part;
+    }
   }
   return a;
+}
+
+// ---------------------------------------------------------------------------
+// Kernel record copies (State::kcopy): sample k's ring slot to the pinned host ring by a small
+// kernel on the copy stream, launched with the replay that packs it and waiting on the device
+// for the pack parts' flags -- each sample lands on the host as soon as it is packed, instead
+// of every sample of a replay behind one copy after the replay (so a recorded run needs no
+// single-sweep replays at its end to keep the copy tail short).  Write-through (system scope)
+// stores, then the last workgroup publishes *copied = k + 1 for the unpack threads.
+// ---------------------------------------------------------------------------
+struct RecCopyArgs {
+  const double* ring;
+  double* host;
+  int64_t slot_doubles;
+  int ring_slots, k, parts;
+  const uint64_t* flags;  // [3][ring_slots]
+  uint64_t want;
+  int* ticket;
+  uint64_t* copied;
+  int* err;
+};
+
+constexpr int REC_COPY_WG = 16;
+
+__global__ __launch_bounds__(256) void rec_copy_kernel(RecCopyArgs a) {
+  const int slot = a.k % a.ring_slots, t = threadIdx.x;
+  if (t < 3 && ((a.parts >> t) & 1)) {
+    const uint64_t* f = a.flags + (size_t)t * a.ring_slots + slot;
+    if (!spin_until<8>([&] { return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.want; }))
+      __hip_atomic_store(&a.err[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const double* src = a.ring + (int64_t)slot * a.slot_doubles;
+  double* dst = a.host + (int64_t)slot * a.slot_doubles;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + t; e < a.slot_doubles; e += (int64_t)gridDim.x * blockDim.x)
+    __hip_atomic_store((unsigned long long*)(dst + e), (unsigned long long)__double_as_longlong(load_coherent(src + e)),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0 && __hip_atomic_fetch_add(a.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+    __hip_atomic_store(a.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.copied, (uint64_t)a.k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+void launch_rec_copy(State& s, int k, int parts) {
+  RecCopyArgs a{};
+  a.ring = s.ring;
+  a.host = s.host_rec_dev;
+  a.slot_doubles = (int64_t)s.slot_doubles;
+  a.ring_slots = s.ring_slots;
+  a.k = k;
+  a.parts = parts;
+  a.flags = s.pack_flags;
+  a.want = ((uint64_t)s.run_nonce << 32) | (uint32_t)(k + 1);
+  a.ticket = s.pack_ticket + 3;
+  a.copied = s.copied_dev;
+  a.err = s.gbl_sync;
+  rec_copy_kernel<<<REC_COPY_WG, 256, 0, s.copy_stream>>>(a);
+  HIP_OK(hipGetLastError());
 }
 
 PackArgs record_pack_args(State& s, int part) { return make_pack_args(s, nullptr, part); }

@@ -118,6 +118,16 @@ struct State {
   // sooner, but the side work beside Eta and z costs them about as much (same 1000-step rate)
   // and a replay's first sweeps wait longer for it (20-step line ~2 % lower)
   bool side_partials = false;
+  // kernel record copies (HMSC_KERNEL_COPY, kernels.hip rec_copy_kernel): graph replays' packs
+  // raise pack_flags and a copy kernel per sample moves it to the host ring
+  bool kcopy = false;
+  int kcopy_max = 8;               // ... for the recorded graphs of at most this many sweeps
+  bool cap_kcopy = false;          // the capture in progress packs with flags
+  uint64_t* pack_flags = nullptr;  // [3 parts][ring_slots]
+  int* pack_ticket = nullptr;      // [3 parts, copy kernel]
+  uint32_t run_nonce = 0;          // desc[4]: flags of an earlier run never match
+  double* host_rec_dev = nullptr;  // the pinned host ring's device address
+  int cap_pack_mask = 0;           // pack parts captured since the last reset (capture_sweeps)
   bool long_tail = false;   // HMSC_LONG_TAIL=1: a recorded run's last replay not split into single sweeps
   // HMSC_FIRST_REPLAY=k: a run's first replay at most k sweeps (0, the default: no limit).  It
   // takes the side-node dispatch delay of a big first replay away (device span of a 20-sweep
@@ -261,6 +271,7 @@ struct State {
   // log2(graph_sweeps); a run of n sweeps replays its binary decomposition, largest first
   static constexpr int GRAPH_LEVELS = 7;  // up to 64 sweeps per replay
   hipGraphExec_t gx[2][GRAPH_LEVELS] = {};
+  int gx_pack_mask[2][GRAPH_LEVELS] = {};  // kcopy: the pack parts every recorded sweep of the graph raises (-1: mixed)
   // The first sweep of a replay's side work (side chain [+ record pack part 2]) runs outside
   // the graph: a graph launch submits its side-stream nodes only after all its main-stream
   // nodes (~16 us of host time per sweep), so that sweep's side chain started late and the
@@ -430,6 +441,7 @@ void launch_inv_sigma(State& s, uint32_t iter);
 // record pack; slot == nullptr: device-chosen (graph replay).  part: 0 all, 1 the main-stream
 // quantities (BL, Psi, iSigma, Eta), 2 the side-stream ones (Gamma, iV, Delta) on `side`
 void launch_record(State& s, double* slot, int part = 0);
+void launch_rec_copy(State& s, int k, int parts);
 bool side_fusion_ok(const State& s);
 // phylogeny branch (phylo.hip)
 size_t phylo_work_doubles(int ns, int Kmax, int nc, int nrho);
