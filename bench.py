@@ -292,7 +292,8 @@ def main():
         timer.daemon = True
         timer.start()
         try:
-            sharded = sharded_leg(hM, args, rank, world, local, dist)
+            # (as many recorded sweeps as the main line, at least 200 and at most 1000)
+            sharded = sharded_leg(hM, args, rank, world, local, dist, steps=max(200, min(args.steps, 1000)))
         except Exception as e:  # noqa: BLE001 -- reported beside the main line, not fatal to it
             sharded = {"error": str(e)[:400]}
         timer.cancel()
