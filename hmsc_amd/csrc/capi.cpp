@@ -889,7 +889,9 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   // slower over 1000 sweeps, the 20-step line 5 % faster, profiles/r06_kcopy_ab.txt)
   {
     const char* e = std::getenv("HMSC_KERNEL_COPY");
-    s.kcopy = !(e && e[0] == '0');
+    // (HMSC_SIDE_EDGES=1, the counter-collection profiler's serialised dispatches: a copy kernel
+    // waiting on the device for a pack queued behind it would time out -- host copies then)
+    s.kcopy = !(e && e[0] == '0') && s.edge_free;
     const char* m = std::getenv("HMSC_KERNEL_COPY_MAX");
     s.kcopy_max = m ? std::max(0, atoi(m)) : 8;
   }
