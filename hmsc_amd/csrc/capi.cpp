@@ -1768,6 +1768,7 @@ struct UnpackPool {
   std::function<void(int)> job;
   uint64_t gen = 0;
   int busy = 0;
+  std::atomic<int> busy_a{0};  // busy, readable without the lock (wait_spin)
   bool quit = false;
   explicit UnpackPool(int W) {
     for (int w = 0; w < W; ++w) th.emplace_back([this, w] { loop(w); });
@@ -1785,6 +1786,7 @@ struct UnpackPool {
       }
       f(w);  // never throws: the job records its own failure
       std::lock_guard<std::mutex> lk(m);
+      busy_a.fetch_sub(1, std::memory_order_release);
       if (--busy == 0) cv_idle.notify_all();
     }
   }
@@ -1792,8 +1794,12 @@ struct UnpackPool {
     std::lock_guard<std::mutex> lk(m);
     job = std::move(f);
     busy = (int)th.size();
+    busy_a.store(busy, std::memory_order_relaxed);
     ++gen;
     cv_job.notify_all();
+  }
+  void wait_spin() {  // poll until every worker is through (then wait() returns at once)
+    while (busy_a.load(std::memory_order_acquire) != 0) std::this_thread::yield();
   }
   void wait() {
     std::unique_lock<std::mutex> lk(m);
@@ -2039,11 +2045,24 @@ static void run(State& s, int transient, int samples, int thin, const int* adapt
     pretouch_record(s, samples - 1, rec);
     last_touched.store(true, std::memory_order_release);
   }
-  HIP_OK(hipStreamSynchronize(s.stream));
-  HIP_OK(hipStreamSynchronize(s.copy_stream));
+  // HMSC_SPIN_WAIT=1: the run's end waited for by polling (the streams, the unpack workers)
+  // instead of blocking waits, whose wake-up latency lands on every run's tail
+  static const bool spin_wait = getenv_flag("HMSC_SPIN_WAIT");
+  if (spin_wait) {
+    for (hipStream_t q : {s.stream, s.copy_stream}) {
+      hipError_t e;
+      while ((e = hipStreamQuery(q)) == hipErrorNotReady) {
+      }
+      HIP_OK(e);
+    }
+  } else {
+    HIP_OK(hipStreamSynchronize(s.stream));
+    HIP_OK(hipStreamSynchronize(s.copy_stream));
+  }
   const auto t_done = std::chrono::steady_clock::now();
   check_device_flags(s);
   if (recording) {
+    if (spin_wait) pool->wait_spin();
     pool->wait();
     std::lock_guard<std::mutex> lk(mu);
     HMSC_REQUIRE(!worker_failed.load(), "record unpack: " + worker_err);
