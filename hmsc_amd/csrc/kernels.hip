@@ -3346,8 +3346,21 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
     double corr = 0.0, xi = 0.0;
     if (ii < ny) {
       // X from the tile staged in LDS (a global load per term here waited out one L2
-      // round trip per covariate: ~6 us of the kernel's serial tail)
-      for (int k = 0; k < nc; ++k) corr = fma(sX[k][s2], sCR[k * NFB + h], corr);
+      // round trip per covariate: ~6 us of the kernel's serial tail); eight terms' LDS reads
+      // issued before their FMAs (a read-FMA chain waited one LDS latency per covariate:
+      // stage 2 took ~3.9 k cycles of tile 0's ~39 k, scripts/stamps_sweep.py), same order
+      int k = 0;
+      for (; k + 8 <= nc; k += 8) {
+        double xv[8], cv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          xv[u] = sX[k + u][s2];
+          cv[u] = sCR[(k + u) * NFB + h];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) corr = fma(xv[u], cv[u], corr);
+      }
+      for (; k < nc; ++k) corr = fma(sX[k][s2], sCR[k * NFB + h], corr);
       xi = p == t ? xi_pre : (a.noise_zero ? 0.0 : normal(a.key, (uint32_t)sPi[s2], (uint32_t)h, S_ETA, iter));
     }
     sB[h][s2] = zl - corr;
@@ -3357,17 +3370,32 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
   if (tile == 0) HMSC_STAMP(53);
   // ---- stage 3: eta = L^-T (L^-1 b + xi) = W^T (W b + xi), two matrix-vector phases over
   // the (factor, site) pairs (no serial substitution chain)
+  // (every LDS operand of a thread's chain read before the chain, as in stage 2; same order)
   for (int p = t; p < EF_SITES * nf; p += 256) {
     const int s2 = p % EF_SITES, m = p / EF_SITES;
-    double u = sXi[m][s2];
-    for (int k = 0; k <= m; ++k) u = fma(sW[m * NFB + k], sB[k][s2], u);
+    double u = sXi[m][s2], wv[NFB], bv[NFB];
+#pragma unroll
+    for (int k = 0; k < NFB; ++k) {
+      wv[k] = k <= m ? sW[m * NFB + k] : 0.0;
+      bv[k] = k <= m ? sB[k][s2] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < NFB; ++k)
+      if (k <= m) u = fma(wv[k], bv[k], u);
     sU[m][s2] = u;
   }
   __syncthreads();
   for (int p = t; p < EF_SITES * nf; p += 256) {
     const int s2 = p % EF_SITES, h = p / EF_SITES, ii = i0 + s2;
-    double e = 0.0;
-    for (int m = h; m < nf; ++m) e = fma(sW[m * NFB + h], sU[m][s2], e);
+    double e = 0.0, wv[NFB], uv[NFB];
+#pragma unroll
+    for (int m = 0; m < NFB; ++m) {
+      wv[m] = (m >= h && m < nf) ? sW[m * NFB + h] : 0.0;
+      uv[m] = (m >= h && m < nf) ? sU[m][s2] : 0.0;
+    }
+#pragma unroll
+    for (int m = 0; m < NFB; ++m)
+      if (m >= h && m < nf) e = fma(wv[m], uv[m], e);
     if (ii < ny) {
       a.Eta[sPi[s2] + (size_t)a.np * h] = e;
       a.XEta[ii + (size_t)ny * (nc + h)] = e;
