@@ -113,7 +113,15 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
   const bool fold = draw && !s.has_na && !s.sharded && !s.phylo && gamma2_bl_fusion_ok(s) &&
                     getenv_flag("HMSC_XZ_FOLD");
   a.pack_row = 0;
-  if (fold && s.pack_req && s.side_fused && s.capturing) {  // ... and the record pack rides along
+  // The record pack is z's last grid row without the fold as well, so the slab launch after z
+  // sums XZ only: its ntile_j pack workgroups dispatch last and overlap z's final round
+  // (1000-step config 4: 6,852 sweeps/s against 6,761 with the pack in the slab launch,
+  // three same-box rounds, profiles/r06_packrow_ab.txt; HMSC_Z_PACK_ROW=0 restores the latter)
+  static const bool pack_row_env = []() {
+    const char* v = getenv("HMSC_Z_PACK_ROW");
+    return !(v && v[0] == '0');
+  }();
+  if ((fold || (pack_row_env && draw && !s.sharded)) && s.pack_req && s.side_fused && s.capturing) {
     a.pack_row = 1;
     a.pack = record_pack_args(s, 1);
     grid.y += 1;
