@@ -1725,7 +1725,7 @@ __device__ __forceinline__ void tail_group_sum(const BLTailArgs& ta, int g, int 
   };
   auto get = [&](const double* p) { return src_coh ? load_coherent(p) : *p; };
   if (g == 0 && t < 64) HMSC_STAMP_RT(78);
-  // group reducer: the group's tiles in workgroup order.  Every load of a thread (two elements
+  // group reducer: the group's tiles in workgroup order.  Every load of a thread (TG_E elements
   // x the group's tiles, and the timing words on threads 254 / 255) is issued before the first
   // sum, so a pass costs one memory latency (a load-use loop pays one per tile)
   const int ntot = ne + (ta.gv_on ? ngv : 0);
@@ -1735,10 +1735,16 @@ __device__ __forceinline__ void tail_group_sum(const BLTailArgs& ta, int g, int 
 #pragma unroll
     for (int u = 0; u < CRW_GROUP; ++u)
       ktx[u] = u < gn ? get(P + (size_t)(g0 + u) * CRW_TILE + 512 + (t - 254)) : (t == 254 ? 1e300 : 0.0);
-  for (int q0 = 0; q0 < ntot; q0 += 512) {
-    double x[2][CRW_GROUP];
+  // (TG_E elements per thread and pass: config 4's 750 elements (CR 320, GammaV 430) in one
+  // pass instead of two, one memory latency less on the way to the Eta launch)
+#ifndef HMSC_TG_E
+#define HMSC_TG_E 3
+#endif
+  constexpr int TG_E = HMSC_TG_E;
+  for (int q0 = 0; q0 < ntot; q0 += 256 * TG_E) {
+    double x[TG_E][CRW_GROUP];
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
+    for (int e = 0; e < TG_E; ++e) {
       const int q = q0 + t + 256 * e;
       const bool cr = q < ne;
       const double* src = cr ? P + q : V + (q - ne);
@@ -1748,7 +1754,7 @@ __device__ __forceinline__ void tail_group_sum(const BLTailArgs& ta, int g, int 
         x[e][u] = (q < ntot && u < gn) ? get(src + (size_t)(g0 + u) * st) : 0.0;
     }
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
+    for (int e = 0; e < TG_E; ++e) {
       const int q = q0 + t + 256 * e;
       if (q >= ntot) continue;
       const bool cr = q < ne;
