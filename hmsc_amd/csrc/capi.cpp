@@ -1380,8 +1380,12 @@ static void record_after_sweep(State& s, double* slot) {
   s.pack_req = s.pack_done = false;
 }
 
-__global__ void set_iters_kernel(uint32_t* p, uint32_t v, int n) {
+__global__ void set_iters_kernel(uint32_t* p, uint32_t v, int n, unsigned long long* kt = nullptr) {
   if ((int)threadIdx.x < n) p[threadIdx.x] = v + threadIdx.x;
+  if (kt && threadIdx.x == 0) kt_record(kt, v, kt_now());  // the replay's start (KT_IT)
+}
+static unsigned long long* kt_iters(const State& s) {
+  return s.kt_on ? s.d_kt + (size_t)KT_IT * 2 * KT_SLOTS : nullptr;
 }
 // A run's start in one launch instead of a descriptor kernel and three fills (~25 us of the
 // 20-sweep line): the record descriptor, and the device flags a run resets -- the fused
@@ -1615,7 +1619,7 @@ static bool replay_sweeps(State& s, uint32_t iter, bool with_record, int n) {
     const auto& segs = s.gseg[with_record ? 1 : 0];
     if (segs.empty() || n != 1) return false;
     join_side(s);
-    set_iters_kernel<<<1, 64, 0, s.stream>>>(s.d_iters, iter, n);
+    set_iters_kernel<<<1, 64, 0, s.stream>>>(s.d_iters, iter, n, kt_iters(s));
     for (const auto& sg : segs) {
       HIP_OK(hipGraphLaunch(sg.g, s.stream));
       if (sg.ar_n) {  // the segment ended with the D2H copy of the all-reduce buffer; the next one starts with its H2D
@@ -1642,7 +1646,7 @@ static bool replay_sweeps(State& s, uint32_t iter, bool with_record, int n) {
     return false;
   }
   join_side(s);
-  set_iters_kernel<<<1, 64, 0, s.stream>>>(s.d_iters, iter, n);
+  set_iters_kernel<<<1, 64, 0, s.stream>>>(s.d_iters, iter, n, kt_iters(s));
   if (const auto& ext = s.ext_side[with_record ? 1 : 0][graph_level(n)]) {
     // the replay's first side chain, on the side stream ahead of the graph (State::ext_side):
     // it waits on the device for that sweep's tails flag like the graph's own side chains

@@ -52,7 +52,8 @@ constexpr int WAVE = 64;
 constexpr int KT_SLOTS = 8192;
 // KT_TAIL: the fused Gamma2 + BetaLambda launch's last reducer; KT_G2: its Gamma2 workgroup
 // KT_SIDE: the side chain launch (GammaV algebra + delta chains), on the side stream
-enum KtId { KT_Z = 0, KT_ETA = 1, KT_BL = 2, KT_TAIL = 3, KT_G2 = 4, KT_SIDE = 5, KT_N = 6 };
+// KT_IT: a graph replay's sweep-counter launch (set_iters_kernel), slot of the replay's first sweep
+enum KtId { KT_Z = 0, KT_ETA = 1, KT_BL = 2, KT_TAIL = 3, KT_G2 = 4, KT_SIDE = 5, KT_IT = 6, KT_N = 7 };
 __device__ inline unsigned long long kt_now() { return __builtin_amdgcn_s_memrealtime(); }
 __device__ inline void kt_record(unsigned long long* kt, uint32_t iter, unsigned long long t0) {
   const unsigned long long t1 = kt_now();

@@ -64,8 +64,9 @@ struct ZArgs {
   double* gred_G;
   const double* logtab;  // z_log_table (ZLOG_N x ZLOG_W doubles), staged in LDS by every workgroup
   const double* ztab;    // z_draw_tables (ZT_DOUBLES: erfcx | F(w) | 2^(k/64)), staged in LDS likewise
-  // pack_row: the grid's last row packs the sweep's main-stream record pieces (BL, Psi,
-  // iSigma, Eta: final before this launch, not written by it) instead of a launch after it
+  // pack_row: a grid row packs the sweep's main-stream record pieces (BL, Psi, iSigma, Eta:
+  // final before this launch, not written by it) instead of a launch after it -- the last
+  // row (1) or the first after the G row (2)
   int pack_row;
   PackArgs pack;
 };
@@ -461,7 +462,9 @@ __global__ __launch_bounds__(256, NKB > 4 ? 2 : Z_MIN_BLOCKS) void z_wave_kernel
     g_reduce_body(a, smem);
     return;
   }
-  if (a.pack_row && blockIdx.y == gridDim.y - 1) {  // the record pack row (last in dispatch order)
+  // the record pack row: last in dispatch order (pack_row 1), or first after the G row (2)
+  const int pack_y = a.pack_row == 2 ? a.gred_y0 : (int)gridDim.y - 1;
+  if (a.pack_row && (int)blockIdx.y == pack_y) {
     pack_body(a.pack, blockIdx.x, gridDim.x);
     return;
   }
@@ -469,7 +472,7 @@ __global__ __launch_bounds__(256, NKB > 4 ? 2 : Z_MIN_BLOCKS) void z_wave_kernel
   // dispatch order, so its XEta rows are fetched once per XCD (round-robin placement) while
   // they are L2-resident, instead of once per species block
   const int by = (int)blockIdx.x;                   // species block
-  const int chunk = (int)blockIdx.y - a.gred_y0;    // site chunk
+  const int chunk = (int)blockIdx.y - a.gred_y0 - (a.pack_row == 2 ? 1 : 0);  // site chunk
   const unsigned long long kt0 = a.kt ? kt_now() : 0ull;
   constexpr int K16 = 16 * NKB;
   const int K = a.K, K4 = (K + 3) & ~3;

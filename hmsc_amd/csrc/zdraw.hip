@@ -121,8 +121,9 @@ static void run_z_fused(State& s, bool draw, uint32_t iter, bool use_raw_y) {
     const char* v = getenv("HMSC_Z_PACK_ROW");
     return !(v && v[0] == '0');
   }();
+  static const bool pack_first = getenv_flag("HMSC_Z_PACK_FIRST");
   if ((fold || (pack_row_env && draw && !s.sharded)) && s.pack_req && s.side_fused && s.capturing) {
-    a.pack_row = 1;
+    a.pack_row = pack_first ? 2 : 1;
     a.pack = record_pack_args(s, 1);
     grid.y += 1;
     s.pack_req = false;

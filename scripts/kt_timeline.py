@@ -11,7 +11,7 @@ sys.path.insert(0, ROOT)
 import hmsc_amd as H  # noqa: E402
 from hmsc_amd.workloads import synthetic_probit  # noqa: E402
 
-KT_SLOTS, KT_N = 8192, 6
+KT_SLOTS, KT_N = 8192, 7
 def _arg(name, default):
     return type(default)(sys.argv[sys.argv.index(name) + 1]) if name in sys.argv else default
 
