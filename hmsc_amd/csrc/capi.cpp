@@ -794,6 +794,9 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   s.G = dalloc<double>((size_t)s.Kmax * s.Kmax);
   s.ZTr = dalloc<double>((size_t)ny * nt);
   s.XZ_part = dalloc<double>((size_t)s.nchunk * s.Kmax * nsl);
+  s.bl_pre = dalloc<double>((size_t)64 * nsl);
+  s.bl_pre_tag = dalloc<int>(2);
+  HIP_OK(hipMemset(s.bl_pre_tag, 0xff, 2 * sizeof(int)));  // (sweep -1, K -1): nothing drawn yet
   s.G_part = dalloc<double>(std::max((size_t)std::max(std::max(s.nchunk, 64), (ny + 31) / 32) * s.Kmax * s.Kmax,
                                       (size_t)((ny + 15) / 16) * s.Kmax * std::max(1, s.NFmax)));
   s.ZTr_part = dalloc<double>((size_t)s.ntile_j * ny * nt);
@@ -926,7 +929,7 @@ static void free_state(State& s) {
   void* ptrs[] = {s.pack_flags, s.pack_ticket, s.X, s.Tr, s.Yval, s.Yraw, s.Ycode, s.Ybits, s.logtab, s.fam, s.varest, s.V0, s.iUGamma, s.mGamma, s.UGammaL,
                   s.aSigma, s.bSigma, s.XX, s.TT, s.V0g, s.V0gXXV0g, s.iV0, s.V0inv, s.iUmG, s.V0gXX, s.g2prep, s.scratch2, s.na_cols, s.na_index,
                   s.na_rows, s.row_na, s.row_slot, s.dev_flags, s.Z, s.XEta, s.BL, s.Psi, s.Delta, s.Gamma, s.iV,
-                  s.iSigma, s.rho, s.XZ, s.G, s.ZTr, s.XZ_part, s.G_part, s.ZTr_part, s.Gna, s.ZL, s.ZL_part,
+                  s.iSigma, s.rho, s.XZ, s.G, s.ZTr, s.XZ_part, s.bl_pre, s.bl_pre_tag, s.G_part, s.ZTr_part, s.Gna, s.ZL, s.ZL_part,
                   s.CR, s.CR_part, s.LS, s.etaW, s.crw_part, s.crw_ticket, s.gvt, s.side_sync, s.Gamma_side, s.Msmall, s.scratch, s.psi_rs, s.ABpart, s.dbg_prec, s.ring, s.allreduce_buf,
                   s.phU, s.phWinv, s.phRbase, s.phTt, s.phBt, s.phEt, s.phTTw, s.phWork, s.UGamma, s.geWork};
   for (void* p : ptrs)

@@ -294,6 +294,10 @@ struct BLArgs {
   unsigned long long* kt;    // live launch timing (KT_BL block) or null
   int kt_defer;              // the fused launch's tail records the BetaLambda timing (BLCol kt0 / kt1)
   int noise_zero;
+  // the draws of this sweep made ahead by the previous sweep's Eta launch (bl_predraw_body),
+  // used when pre_tag holds (this sweep, K); else drawn here -- the same bits either way
+  const double* pre_buf;
+  const int* pre_tag;
 };
 
 __global__ __launch_bounds__(64) void beta_lambda_kernel(BLArgs a) {
@@ -433,6 +437,7 @@ struct BLCol {
 // Work the body runs for the tail while its prologue's loads fly: none by default
 struct BLNoPre {
   __device__ double operator()(int, int) const { return 0.0; }
+  __device__ double from(const double*, int) const { return 0.0; }
 };
 
 // side_wait (the fused launch inside a sweep graph, sweeps after the first): iV and Delta come
@@ -471,9 +476,12 @@ __device__ __forceinline__ BLCol beta_lambda_wave_body(const BLArgs& a, double* 
   for (int q = 0; q < 8; ++q) trj[q] = q < nt ? a.Tr[jj + (size_t)a.ns_loc * q] : 0.0;
   const int nai = a.na_index ? a.na_index[jj] : -1;
   // the draw's noise (R/updateBetaLambda.R:101) needs none of it: drawn while the loads fly
+  const bool have_pre = a.pre_buf && a.pre_tag[0] == (int)SWEEP_ITER(a) && a.pre_tag[1] == K;
+  const double* prow = have_pre ? a.pre_buf + (size_t)jj * 64 : nullptr;
   const double xi_bl = (i < K && !a.noise_zero && j < a.ns_loc)
-                           ? normal(a.key, (uint32_t)(a.sp0 + j), (uint32_t)i, S_BETALAMBDA, SWEEP_ITER(a)) : 0.0;
-  const double gpre = j < a.ns_loc ? pre(j, i) : 0.0;
+                           ? (have_pre ? prow[i] : normal(a.key, (uint32_t)(a.sp0 + j), (uint32_t)i, S_BETALAMBDA, SWEEP_ITER(a)))
+                           : 0.0;
+  const double gpre = j < a.ns_loc ? (have_pre ? pre.from(prow, i) : pre(j, i)) : 0.0;
   if (side_n > 0) side_wait_lanes(side_sync, side_n, side_epoch, gsync);
   if (WAIT_GAMMA && blk == 0 && w == 0) HMSC_STAMP_RT(84);
   // what the previous sweep's side chain published (device-coherent after its flags)
@@ -2053,6 +2061,11 @@ struct BLPsiPre {
     if (!on || !ta.gv_on || lane < nc || lane >= K) return 0.0;
     return psi_gamma_std(ta, iter, j, lane - nc);
   }
+  // the same variate from the species' pre-drawn row (bl_predraw_body)
+  __device__ double from(const double* row, int lane) const {
+    if (!on || !ta.gv_on || lane < nc || lane >= K) return 0.0;
+    return row[32 + lane - nc];
+  }
 };
 
 template <int NM>
@@ -2265,6 +2278,12 @@ static void shard_g2_stats(State& s);
 bool side_fusion_ok(const State& s);
 
 
+// HMSC_BL_PREDRAW=1: the Eta launch of a captured one-rank sweep draws the next sweep's
+// BetaLambda noise and psi variates ahead (bl_predraw_body; the wave body's K <= 32)
+static bool bl_predraw_on(const State& s) {
+  return getenv_flag("HMSC_BL_PREDRAW") && !s.sharded && s.capturing && s.K <= 32 && s.bl_pre != nullptr;
+}
+
 // how many of the tail's reduction levels a deferred tail leaves to the Eta launch
 static int tail_defer_levels() {
   static const int v = [] {
@@ -2378,6 +2397,10 @@ void launch_gamma2_bl(State& s, uint32_t iter) {
     f.tail.defer = defer ? tail_defer_levels() : 0;
     f.tail.psi_pre = getenv_flag("HMSC_NO_PSI_PRE") ? 0 : 1;
     f.bl.kt_defer = 1;
+  }
+  if (bl_predraw_on(s)) {  // (used only when the tag names this sweep)
+    f.bl.pre_buf = s.bl_pre;
+    f.bl.pre_tag = s.bl_pre_tag;
   }
   s.tail_defer = defer;
   s.crw_fresh = crw_on && !sh;
@@ -3156,7 +3179,47 @@ struct EtaFArgs {
   // EF_SOLVE of an edge-free sharded sweep graph: raised (this sweep's epoch) at the launch's
   // start, i.e. after all-reduce B, for the side chain that reads ar_b (sweep_sharded)
   int* arb_flag;
+  // EF_DEFER: npre workgroups between the reducers and the tile workgroups draw the next
+  // sweep's BetaLambda noise and psi gamma variates (bl_predraw_body) into pre_buf (last in
+  // dispatch order they outlasted the tiles: Eta end -> z start 3.4 -> 6.8 us)
+  double* pre_buf;
+  int* pre_tag;
+  int npre, ntile;
 };
+
+// The next sweep's BetaLambda draws, made while this launch streams Z, into [species][64]:
+// slot k < K the noise xi_k of R/updateBetaLambda.R:101, slot 32 + f factor f's standard
+// gamma variate of R/updateLambdaPriors.R:22-24 (psi = variate / rate, in the tail).  Same
+// (key, index, stream, sweep) as the in-kernel draws, so the same bits; the BetaLambda
+// prologue (on the sweep's critical path) then loads them instead of drawing (~2 us of its
+// chain at config 4).  The ns K normals first, then the ns (K - nc) gamma variates, spread
+// over every thread of the npre workgroups, so a wave draws one kind (no divergence between
+// the two samplers).
+__device__ void bl_predraw_body(const EtaFArgs& a, int bid) {
+  const uint32_t it = SWEEP_ITER(a) + 1;
+  const BLTailArgs& ta = a.tail;
+  const int K = a.K, nc = a.nc, nl = K - nc;
+  const int nN = a.ns_loc * K, nG = a.ns_loc * nl;
+  for (int q = bid * 256 + (int)threadIdx.x; q < nN + nG; q += a.npre * 256) {
+    double v;
+    int j, slot;
+    if (q < nN) {
+      j = q / K;
+      slot = q - j * K;
+      v = a.noise_zero ? 0.0 : normal(a.key, (uint32_t)(ta.sp0 + j), (uint32_t)slot, S_BETALAMBDA, it);
+    } else {
+      j = (q - nN) / nl;
+      const int f = q - nN - j * nl;
+      slot = 32 + f;
+      v = psi_gamma_std(ta, it, j, f);
+    }
+    a.pre_buf[(size_t)j * 64 + slot] = v;
+  }
+  if (bid == 0 && threadIdx.x == 0) {  // read after this launch's boundary
+    a.pre_tag[0] = (int)it;
+    a.pre_tag[1] = K;
+  }
+}
 
 constexpr int EF_SITES = 16;
 // EF_FUSED: the one-pass kernel above.  A species-sharded chain splits it at the all-reduce
@@ -3213,7 +3276,11 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
     tail_final(a.tail, a.nbl, SWEEP_ITER(a), sAll, true, two, two);
     return;
   }
-  const int tile = MODE == EF_DEFER ? blockIdx.x - a.nred : blockIdx.x;
+  if (MODE == EF_DEFER && (int)blockIdx.x < a.nred + a.npre) {  // (after the reducers, ahead of the tiles)
+    bl_predraw_body(a, (int)blockIdx.x - a.nred);
+    return;
+  }
+  const int tile = MODE == EF_DEFER ? blockIdx.x - a.nred - a.npre : blockIdx.x;
   const unsigned long long kt0 = a.kt ? kt_now() : 0ull;
   const int ny = a.ny, nf = a.nf, K = a.K, nc = a.nc, ns = a.ns_loc;
   const int i0 = tile * EF_SITES;
@@ -3697,7 +3764,7 @@ static EtaFArgs make_etaf_args(State& s, uint32_t iter) {
 template <int MODE>
 static void launch_eta_fused_mode(State& s, const EtaFArgs& a) {
   const int ntile = (s.ny + EF_SITES - 1) / EF_SITES;
-  const int nf = s.lev[0].nf, nb = ntile + (MODE == EF_DEFER ? a.nred : 0);
+  const int nf = s.lev[0].nf, nb = ntile + (MODE == EF_DEFER ? a.nred + a.npre : 0);
   if (nf <= 8)
     eta_fused_kernel<8, MODE><<<nb, 256, 0, s.stream>>>(a);
   else if (nf <= 12)
@@ -3734,6 +3801,12 @@ static void launch_eta_fused(State& s, uint32_t iter, bool cr_done = false, bool
     a.tail = make_tail_args(s, tail_gv, false);
     a.tail.defer = tail_defer_levels();
     a.nred = a.tail.defer == 2 ? (a.nbl + CRW_GROUP - 1) / CRW_GROUP : 1;
+    if (bl_predraw_on(s)) {
+      a.npre = 64;  // ~40 k draws at config 4: 2-3 per thread
+      a.ntile = (s.ny + EF_SITES - 1) / EF_SITES;
+      a.pre_buf = s.bl_pre;
+      a.pre_tag = s.bl_pre_tag;
+    }
     launch_eta_fused_mode<EF_DEFER>(s, a);
   } else {
     launch_eta_fused_mode<EF_FUSED>(s, a);

@@ -224,6 +224,11 @@ struct State {
   double* G = nullptr;           // Kmax x Kmax  XEta^T XEta
   double* ZTr = nullptr;         // ny x nt      Z Tr (local species)
   double* XZ_part = nullptr;     // nchunk x K x ns_loc
+  // the next sweep's BetaLambda noise and psi gamma variates, drawn ahead by the Eta launch
+  // (kernels.hip bl_predraw_body): [species][64] (lane k < K: xi; 32 + f: psi's gamma), and
+  // the (sweep, K) they were drawn for
+  double* bl_pre = nullptr;
+  int* bl_pre_tag = nullptr;
   double* G_part = nullptr;      // nchunk x Kmax^2
   double* ZTr_part = nullptr;    // ntile_j x ny x nt
   double* Gna = nullptr;         // n_na_cols x Kmax^2 masked grams

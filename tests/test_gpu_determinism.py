@@ -77,7 +77,7 @@ def test_two_chains_one_device_fused_path_with_graphs():
 
 
 @pytest.mark.parametrize("env", ["HMSC_XZ_FOLD", "HMSC_NO_TAIL_DEFER", "HMSC_NO_SIDE_GATE", "HMSC_G2_PART_INLINE",
-                                 "HMSC_NO_PSI_PRE"])
+                                 "HMSC_NO_PSI_PRE", "HMSC_BL_PREDRAW"])
 def test_launch_variants_bitwise(env, monkeypatch):
     """Launch-structure variants give the same bits: XZ read from updateZ's chunk partials by the
     fused Gamma2 + BetaLambda launch (HMSC_XZ_FOLD, with the record pack in the z launch) or
