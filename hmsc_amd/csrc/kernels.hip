@@ -2278,19 +2278,21 @@ static void shard_g2_stats(State& s);
 bool side_fusion_ok(const State& s);
 
 
-// HMSC_BL_PREDRAW=1: the Eta launch of a captured one-rank sweep draws the next sweep's
-// BetaLambda noise and psi variates ahead (bl_predraw_body; the wave body's K <= 32)
+// The Eta launch of a captured one-rank sweep draws the next sweep's BetaLambda noise and psi
+// variates ahead (bl_predraw_body; the wave body's K <= 32).  With both tail levels in the Eta
+// launch: 1000-step 6,842 -> 6,947 sweeps/s, 3 of 3 same-box rounds; either alone within noise
+// (profiles/r06_predraw_ab.txt).  HMSC_NO_BL_PREDRAW=1: drawn in the BetaLambda prologue.
 static bool bl_predraw_on(const State& s) {
-  return getenv_flag("HMSC_BL_PREDRAW") && !s.sharded && s.capturing && s.K <= 32 && s.bl_pre != nullptr;
+  return !getenv_flag("HMSC_NO_BL_PREDRAW") && !s.sharded && s.capturing && s.K <= 32 && s.bl_pre != nullptr;
 }
 
-// how many of the tail's reduction levels a deferred tail leaves to the Eta launch
+// how many of the tail's reduction levels a deferred tail leaves to the Eta launch: both
+// (default since the BetaLambda draws are made ahead: the fused launch then ends with its
+// bodies and the Eta launch starts ~8 us sooner), or the last (HMSC_TAIL_DEFER_LEVELS=1;
+// round 5's default, when the bodies were draw-bound and two levels measured 0.5 % slower)
 static int tail_defer_levels() {
-  static const int v = [] {
-    const char* e = getenv("HMSC_TAIL_DEFER_LEVELS");
-    return (e && atoi(e) == 2) ? 2 : 1;
-  }();
-  return v;
+  const char* e = getenv("HMSC_TAIL_DEFER_LEVELS");
+  return (e && atoi(e) == 1) ? 1 : 2;
 }
 
 // the BetaLambda workgroups' tail (crw_on), also the Eta launch's reducers under EF_DEFER

@@ -77,13 +77,15 @@ def test_two_chains_one_device_fused_path_with_graphs():
 
 
 @pytest.mark.parametrize("env", ["HMSC_XZ_FOLD", "HMSC_NO_TAIL_DEFER", "HMSC_NO_SIDE_GATE", "HMSC_G2_PART_INLINE",
-                                 "HMSC_NO_PSI_PRE", "HMSC_BL_PREDRAW"])
+                                 "HMSC_NO_PSI_PRE", "HMSC_NO_BL_PREDRAW", "HMSC_TAIL_DEFER_LEVELS"])
 def test_launch_variants_bitwise(env, monkeypatch):
     """Launch-structure variants give the same bits: XZ read from updateZ's chunk partials by the
     fused Gamma2 + BetaLambda launch (HMSC_XZ_FOLD, with the record pack in the z launch) or
     reduced first (default), Gamma2's species-block partials on workgroups of their own (default)
-    or ahead of the first BetaLambda bodies (HMSC_G2_PART_INLINE), the BetaLambda tail's last
-    level deferred to the Eta launch (default) or not, and the previous sweep's side chain awaited
+    or ahead of the first BetaLambda bodies (HMSC_G2_PART_INLINE), the BetaLambda tail's two
+    reduction levels deferred to the Eta launch (default), only the last (HMSC_TAIL_DEFER_LEVELS=1)
+    or neither, the next sweep's BetaLambda draws made by the Eta launch (default) or in the
+    BetaLambda prologue (HMSC_NO_BL_PREDRAW), and the previous sweep's side chain awaited
     by the reduction launch after updateZ (default) or polled by the fused launch itself
     (HMSC_NO_SIDE_GATE), and the BetaLambda tail's psi gamma variates drawn ahead by the bodies
     (default) or in the tail (HMSC_NO_PSI_PRE).  A probit-only model (the fused paths), recorded
