@@ -886,17 +886,23 @@ static void build_state(State& s, const hmsc_model* m, uint64_t seed, int device
   HIP_OK(hipHostMalloc(&s.copied_host, 64, hipHostMallocMapped | hipHostMallocCoherent));
   HIP_OK(hipHostGetDevicePointer((void**)&s.copied_dev, s.copied_host, 0));
   s.d_rec_desc = dalloc<int32_t>(8);  // {iter0, transient, thin, samples, run nonce}
-  // kernel copies for the recorded graphs of at most kcopy_max sweeps: a run's last replays (the
-  // record tail), while long replays keep one host-issued copy each (HMSC_KERNEL_COPY=0: never,
+  // kernel copies for the recorded graphs of at most kcopy_max sweeps: a run's first and last
+  // replays, while long replays keep one host-issued copy each (HMSC_KERNEL_COPY=0: never,
   // HMSC_KERNEL_COPY_MAX: the size bound; a 32-sweep graph with kernel copies measured 2.9 %
-  // slower over 1000 sweeps, the 20-step line 5 % faster, profiles/r06_kcopy_ab.txt)
+  // slower over 1000 sweeps, the 20-step line 5 % faster, profiles/r06_kcopy_ab.txt).  With
+  // them a run starts on a replay of at most 4 sweeps (HMSC_FIRST_REPLAY overrides): the device
+  // starts after a short graph's submission instead of a 16- or 32-sweep one's, and a 20-sweep
+  // run is 4 + 16 replays with kernel copies throughout (bound 16): the 20-step line ahead in
+  // 10 of 12 same-box rounds (5,958 -> 6,210 over 7), 1000 steps unchanged
+  // (profiles/r06_first_replay_ab.txt)
   {
     const char* e = std::getenv("HMSC_KERNEL_COPY");
     // (HMSC_SIDE_EDGES=1, the counter-collection profiler's serialised dispatches: a copy kernel
     // waiting on the device for a pack queued behind it would time out -- host copies then)
     s.kcopy = !(e && e[0] == '0') && s.edge_free;
     const char* m = std::getenv("HMSC_KERNEL_COPY_MAX");
-    s.kcopy_max = m ? std::max(0, atoi(m)) : 8;
+    s.kcopy_max = m ? std::max(0, atoi(m)) : 16;
+    if (!std::getenv("HMSC_FIRST_REPLAY")) s.first_replay = s.kcopy ? 4 : 0;
   }
   if (s.kcopy && hipHostGetDevicePointer((void**)&s.host_rec_dev, s.host_rec, 0) != hipSuccess) {
     (void)hipGetLastError();
