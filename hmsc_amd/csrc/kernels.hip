@@ -3187,6 +3187,7 @@ struct EtaFArgs {
   double* pre_buf;
   int* pre_tag;
   int npre, ntile;
+  int red_prio;
 };
 
 // The next sweep's BetaLambda draws, made while this launch streams Z, into [species][64]:
@@ -3264,6 +3265,7 @@ __global__ __launch_bounds__(256, 3) void eta_fused_kernel(EtaFArgs a) {
   __shared__ int sPi[EF_SITES];  // the tile's units
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, lm = lane & 15, lk = lane >> 4;
   if (MODE == EF_DEFER && blockIdx.x < a.nred) {  // the BetaLambda tail's reductions
+    if (a.red_prio) __builtin_amdgcn_s_setprio(3);  // (HMSC_RED_PRIO=1: issue ahead of the streams)
     const bool two = a.tail.defer == 2;
     if (two) {  // group blockIdx.x's tiles, then the last group through sums the group tiles
       __shared__ int s_last;
@@ -3803,6 +3805,7 @@ static void launch_eta_fused(State& s, uint32_t iter, bool cr_done = false, bool
     a.tail = make_tail_args(s, tail_gv, false);
     a.tail.defer = tail_defer_levels();
     a.nred = a.tail.defer == 2 ? (a.nbl + CRW_GROUP - 1) / CRW_GROUP : 1;
+    a.red_prio = getenv_flag("HMSC_RED_PRIO") ? 1 : 0;
     if (bl_predraw_on(s)) {
       a.npre = 64;  // ~40 k draws at config 4: 2-3 per thread
       a.ntile = (s.ny + EF_SITES - 1) / EF_SITES;
